@@ -1,0 +1,231 @@
+// bindings.cpp — pybind11 module `_nfdp`: the Python control plane's handle on the native data
+// plane.  Buffers cross the boundary as raw addresses (torch HBM tensors or numpy host arrays),
+// so no copies and no torch headers are involved; the HIP stream is passed as an integer
+// (torch.cuda.current_stream().cuda_stream).
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "host.h"
+
+namespace py = pybind11;
+using namespace nfdp;
+
+namespace {
+
+template <typename T>
+T* ptr(const py::dict& d, const char* k) {
+  if (!d.contains(k)) return nullptr;
+  py::object o = d[k];
+  if (o.is_none()) return nullptr;
+  return reinterpret_cast<T*>(o.cast<uintptr_t>());
+}
+template <typename T>
+T val(const py::dict& d, const char* k, T def) {
+  if (!d.contains(k)) return def;
+  return d[k].cast<T>();
+}
+
+TablesView tables_from(const py::dict& d) {
+  TablesView t{};
+  t.ports = ptr<const PortEntry>(d, "ports");
+  t.chains = ptr<const ChainEntry>(d, "chains");
+  t.n_chains = val<uint32_t>(d, "n_chains", 0);
+  t.tags = ptr<const uint16_t>(d, "tags");
+  t.keys = ptr<const FlowKey>(d, "keys");
+  t.vals = ptr<const FlowAction>(d, "vals");
+  t.bucket_mask = val<uint32_t>(d, "bucket_mask", 0);
+  t.macs = ptr<const MacEntry>(d, "macs");
+  t.mac_mask = val<uint32_t>(d, "mac_mask", 0);
+  t.rss_key = ptr<const uint8_t>(d, "rss_key");
+  t.acl_value = ptr<const uint32_t>(d, "acl_value");
+  t.acl_mask = ptr<const uint32_t>(d, "acl_mask");
+  t.acl_permit = ptr<const uint8_t>(d, "acl_permit");
+  t.n_acl = val<uint32_t>(d, "n_acl", 0);
+  t.acl_default_permit = val<uint32_t>(d, "acl_default_permit", 1);
+  if (!t.ports || !t.chains || !t.tags || !t.keys || !t.vals || !t.rss_key)
+    throw std::invalid_argument("tables dict is missing a required buffer");
+  if (t.n_acl && (!t.acl_value || !t.acl_mask || !t.acl_permit))
+    throw std::invalid_argument("n_acl > 0 but ACL buffers missing");
+  return t;
+}
+
+void check(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+using U32Arr = py::array_t<uint32_t, py::array::c_style | py::array::forcecast>;
+
+}  // namespace
+
+PYBIND11_MODULE(_nfdp, m) {
+  m.doc() = "MI355X network-function data plane (HIP/CDNA4 kernels + host control structures)";
+  m.attr("SLOT_BYTES") = kSlotBytes;
+  m.attr("MAX_PORTS") = kMaxPorts;
+  m.attr("BUCKET_SLOTS") = kBucketSlots;
+  m.attr("PORT_NONE") = kPortNone;
+  m.attr("PORT_PUNT") = kPortPunt;
+  m.attr("NUM_REASONS") = (int)kNumReasons;
+
+  py::class_<FlowTableHost>(m, "FlowTable")
+      .def(py::init([](uint32_t nb, py::bytes rss) {
+             std::string s = rss;
+             return new FlowTableHost(nb, std::vector<uint8_t>(s.begin(), s.end()));
+           }),
+           py::arg("nbuckets"), py::arg("rss_key"))
+      .def_property_readonly("nbuckets", &FlowTableHost::nbuckets)
+      .def_property_readonly("mask", &FlowTableHost::mask)
+      .def("__len__", &FlowTableHost::size)
+      .def("hash", [](const FlowTableHost& t, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+        return t.hash(FlowKey{a, b, c, d});
+      })
+      .def("insert", [](FlowTableHost& t, py::tuple k, py::tuple v) {
+        FlowKey key{k[0].cast<uint32_t>(), k[1].cast<uint32_t>(), k[2].cast<uint32_t>(), k[3].cast<uint32_t>()};
+        const uint32_t w0 = v[0].cast<uint32_t>(), w1 = v[1].cast<uint32_t>(), w2 = v[2].cast<uint32_t>(), w3 = v[3].cast<uint32_t>();
+        FlowAction a;
+        a.chain_id = w0 & 0xFFFF; a.out_port = w0 >> 16; a.nat_ip = w1;
+        a.nat_port = w2 & 0xFFFF; a.vlan = w2 >> 16; a.flow_id = w3;
+        return t.insert(key, a);
+      })
+      .def("insert_many", [](FlowTableHost& t, U32Arr keys, U32Arr vals) {
+        if (keys.ndim() != 2 || keys.shape(1) != 4 || vals.ndim() != 2 || vals.shape(1) != 4 ||
+            keys.shape(0) != vals.shape(0))
+          throw std::invalid_argument("insert_many expects [n,4] uint32 keys and values");
+        const size_t n = keys.shape(0);
+        py::array_t<int64_t> slots(n);
+        auto k = keys.unchecked<2>();
+        auto v = vals.unchecked<2>();
+        auto o = slots.mutable_unchecked<1>();
+        for (size_t i = 0; i < n; ++i) {
+          FlowKey key{k(i, 0), k(i, 1), k(i, 2), k(i, 3)};
+          FlowAction a;
+          a.chain_id = v(i, 0) & 0xFFFF; a.out_port = v(i, 0) >> 16; a.nat_ip = v(i, 1);
+          a.nat_port = v(i, 2) & 0xFFFF; a.vlan = v(i, 2) >> 16; a.flow_id = v(i, 3);
+          o(i) = t.insert(key, a);
+        }
+        return slots;
+      })
+      .def("erase", [](FlowTableHost& t, py::tuple k) {
+        return t.erase(FlowKey{k[0].cast<uint32_t>(), k[1].cast<uint32_t>(), k[2].cast<uint32_t>(), k[3].cast<uint32_t>()});
+      })
+      .def("find", [](const FlowTableHost& t, py::tuple k) {
+        return t.find(FlowKey{k[0].cast<uint32_t>(), k[1].cast<uint32_t>(), k[2].cast<uint32_t>(), k[3].cast<uint32_t>()});
+      })
+      .def("tags", [](const FlowTableHost& t) {
+        auto& v = t.tags();
+        return py::array_t<uint16_t>(v.size(), v.data());
+      })
+      .def("keys", [](const FlowTableHost& t) {
+        auto& v = t.keys();
+        return py::array_t<uint32_t>({(py::ssize_t)v.size(), (py::ssize_t)4}, reinterpret_cast<const uint32_t*>(v.data()));
+      })
+      .def("vals", [](const FlowTableHost& t) {
+        auto& v = t.vals();
+        return py::array_t<uint32_t>({(py::ssize_t)v.size(), (py::ssize_t)4}, reinterpret_cast<const uint32_t*>(v.data()));
+      })
+      .def("take_dirty", [](FlowTableHost& t) {
+        auto v = t.take_dirty();
+        return py::array_t<uint32_t>(v.size(), v.data());
+      })
+      .def("take_moves", &FlowTableHost::take_moves)
+      .def("clear_dirty", &FlowTableHost::clear_dirty);
+
+  m.def("toeplitz", [](U32Arr keys, py::bytes rss) {
+    std::string s = rss;
+    if (s.size() < 20) throw std::invalid_argument("rss key must be >= 20 bytes");
+    if (keys.ndim() != 2 || keys.shape(1) != 4) throw std::invalid_argument("keys must be [n,4]");
+    const size_t n = keys.shape(0);
+    py::array_t<uint32_t> out(n);
+    auto k = keys.unchecked<2>();
+    auto o = out.mutable_unchecked<1>();
+    for (size_t i = 0; i < n; ++i)
+      o(i) = toeplitz_scalar(FlowKey{k(i, 0), k(i, 1), k(i, 2), k(i, 3)}, reinterpret_cast<const uint8_t*>(s.data()));
+    return out;
+  });
+  m.def("table_hash", [](uint32_t h, uint32_t mask) {
+    TableHash t = table_hash(h, mask);
+    return py::make_tuple(t.b1, t.b2, t.tag);
+  });
+  m.def("owner_of", &owner_of);
+  m.def("build_acl_frags", [](U32Arr value, U32Arr mask) {
+    if (value.ndim() != 2 || value.shape(1) != 4 || mask.ndim() != 2 || mask.shape(1) != 4 ||
+        value.shape(0) != mask.shape(0))
+      throw std::invalid_argument("ACL value/mask must be [n,4] uint32");
+    AclFrags f = build_acl_frags(value.data(), mask.data(), (uint32_t)value.shape(0));
+    return py::make_tuple(py::array_t<int8_t>(f.wfrag.size(), f.wfrag.data()),
+                          py::array_t<int32_t>(f.cinit.size(), f.cinit.data()), f.tiles);
+  });
+  m.def("build_toeplitz_frags", [](py::bytes rss) {
+    std::string s = rss;
+    if (s.size() < 20) throw std::invalid_argument("rss key must be >= 20 bytes");
+    auto v = build_toeplitz_frags(reinterpret_cast<const uint8_t*>(s.data()));
+    return py::array_t<int8_t>(v.size(), v.data());
+  });
+  m.def("build_toeplitz_table", [](py::bytes rss) {
+    std::string s = rss;
+    if (s.size() < 20) throw std::invalid_argument("rss key too short");
+    auto v = build_toeplitz_table(reinterpret_cast<const uint8_t*>(s.data()));
+    return py::array_t<uint32_t>(v.size(), v.data());
+  });
+
+  m.def("oracle_run", [](py::dict tables, uintptr_t pkts, uintptr_t inmeta, uint32_t n, uintptr_t out,
+                         uintptr_t out_meta, uintptr_t flow_ctr, uintptr_t port_ctr, uintptr_t drop_ctr,
+                         uintptr_t hashes, uintptr_t acl) {
+    TablesView t = tables_from(tables);
+    py::gil_scoped_release nogil;
+    oracle_run(t, reinterpret_cast<const uint32_t*>(pkts), reinterpret_cast<const uint32_t*>(inmeta), n,
+               reinterpret_cast<uint32_t*>(out), reinterpret_cast<uint32_t*>(out_meta),
+               reinterpret_cast<uint64_t*>(flow_ctr), reinterpret_cast<uint64_t*>(port_ctr),
+               reinterpret_cast<uint64_t*>(drop_ctr), reinterpret_cast<uint32_t*>(hashes),
+               reinterpret_cast<int32_t*>(acl));
+  });
+
+  m.def("fused_lds_bytes", &fused_lds_bytes);
+  m.def("launch_fused", [](py::dict tables, uintptr_t pkts, uintptr_t inmeta, uintptr_t out, uintptr_t out_meta,
+                           uint32_t n, uintptr_t flow_ctr, uintptr_t port_ctr, uintptr_t drop_ctr, uintptr_t t0,
+                           uintptr_t lat, uintptr_t acl_wfrag, uintptr_t acl_cinit, uint32_t acl_tiles,
+                           uintptr_t toep_frag, uintptr_t toep_tab, int hash_mode, int acl_mode, int num_cus,
+                           uintptr_t stream) {
+    FusedLaunch f{};
+    f.t = tables_from(tables);
+    f.pkts = reinterpret_cast<const void*>(pkts);
+    f.inmeta = reinterpret_cast<const uint32_t*>(inmeta);
+    f.out = reinterpret_cast<void*>(out);
+    f.out_meta = reinterpret_cast<uint32_t*>(out_meta);
+    f.n = n;
+    f.flow_ctr = reinterpret_cast<unsigned long long*>(flow_ctr);
+    f.port_ctr = reinterpret_cast<unsigned long long*>(port_ctr);
+    f.drop_ctr = reinterpret_cast<unsigned long long*>(drop_ctr);
+    f.t0 = reinterpret_cast<const unsigned long long*>(t0);
+    f.lat = reinterpret_cast<uint32_t*>(lat);
+    f.acl_wfrag = reinterpret_cast<const void*>(acl_wfrag);
+    f.acl_cinit = reinterpret_cast<const void*>(acl_cinit);
+    f.acl_tiles = acl_tiles;
+    f.toep_frag = reinterpret_cast<const void*>(toep_frag);
+    f.toep_tab = reinterpret_cast<const uint32_t*>(toep_tab);
+    if (!f.pkts || !f.inmeta || !f.out || !f.out_meta || !f.port_ctr || !f.drop_ctr)
+      throw std::invalid_argument("launch_fused: null buffer");
+    if (hash_mode == 2 && !f.toep_frag) throw std::invalid_argument("MFMA hash needs toeplitz frags");
+    if (hash_mode == 1 && !f.toep_tab) throw std::invalid_argument("LDS hash needs toeplitz table");
+    if (acl_mode == 1 && (!f.acl_wfrag || !f.acl_cinit)) throw std::invalid_argument("MFMA ACL needs frags");
+    LaunchCfg cfg;
+    cfg.hash_mode = hash_mode; cfg.acl_mode = acl_mode; cfg.num_cus = num_cus;
+    check(launch_fused(f, cfg, reinterpret_cast<hipStream_t>(stream)), "launch_fused");
+  });
+  m.def("launch_stamp", [](uintptr_t dst, uintptr_t stream) {
+    check(launch_stamp(reinterpret_cast<unsigned long long*>(dst), reinterpret_cast<hipStream_t>(stream)), "stamp");
+  });
+  m.def("launch_bucket_update", [](uintptr_t idx, uint32_t nb, uintptr_t tag_rows, uintptr_t key_rows,
+                                   uintptr_t val_rows, uintptr_t tags, uintptr_t keys, uintptr_t vals,
+                                   uint32_t bucket_mask, uintptr_t stream) {
+    check(launch_bucket_update(reinterpret_cast<const uint32_t*>(idx), nb, reinterpret_cast<const void*>(tag_rows),
+                               reinterpret_cast<const void*>(key_rows), reinterpret_cast<const void*>(val_rows),
+                               reinterpret_cast<void*>(tags), reinterpret_cast<void*>(keys),
+                               reinterpret_cast<void*>(vals), bucket_mask, reinterpret_cast<hipStream_t>(stream)),
+          "bucket_update");
+  });
+  m.def("launch_harvest", [](uintptr_t ctr, uintptr_t out, uint32_t n, uintptr_t stream) {
+    check(launch_harvest(reinterpret_cast<unsigned long long*>(ctr), reinterpret_cast<unsigned long long*>(out), n,
+                         reinterpret_cast<hipStream_t>(stream)), "harvest");
+  });
+}

@@ -1,0 +1,228 @@
+// host.cpp — authoritative flow table (cuckoo), classification-table builders, CPU oracle.
+#include "host.h"
+
+#include <algorithm>
+
+namespace nfdp {
+
+// ------------------------------------------------------------------------------------------
+// FlowTableHost
+// ------------------------------------------------------------------------------------------
+FlowTableHost::FlowTableHost(uint32_t nbuckets_pow2, const std::vector<uint8_t>& rss_key)
+    : nb_(nbuckets_pow2), rss_(rss_key) {
+  if (nb_ < 2 || (nb_ & (nb_ - 1))) throw std::invalid_argument("nbuckets must be a power of two >= 2");
+  if (rss_.size() < 20) throw std::invalid_argument("rss key must be >= 20 bytes");
+  tags_.assign((size_t)nb_ * kBucketSlots, 0);
+  keys_.assign((size_t)nb_ * kBucketSlots, FlowKey{0, 0, 0, 0});
+  vals_.assign((size_t)nb_ * kBucketSlots, FlowAction{});
+}
+
+int FlowTableHost::find_in_bucket(uint32_t b, uint16_t tag, const FlowKey& k) const {
+  for (int s = 0; s < kBucketSlots; ++s) {
+    const size_t i = (size_t)b * kBucketSlots + s;
+    if (tags_[i] != tag) continue;
+    const FlowKey& e = keys_[i];
+    if (e.src_ip == k.src_ip && e.dst_ip == k.dst_ip && e.ports == k.ports && e.meta == k.meta) return s;
+  }
+  return -1;
+}
+
+int64_t FlowTableHost::find(const FlowKey& k) const {
+  const TableHash th = table_hash(hash(k), mask());
+  int s = find_in_bucket(th.b1, th.tag, k);
+  if (s >= 0) return (int64_t)th.b1 * kBucketSlots + s;
+  s = find_in_bucket(th.b2, th.tag, k);
+  if (s >= 0) return (int64_t)th.b2 * kBucketSlots + s;
+  return -1;
+}
+
+int64_t FlowTableHost::insert(const FlowKey& key, const FlowAction& act) {
+  if (key.meta & 0xFF00u) throw std::invalid_argument("FlowKey.meta byte 1 must be zero");
+  const int64_t existing = find(key);
+  if (existing >= 0) {
+    vals_[existing] = act;
+    dirty_.insert((uint32_t)(existing / kBucketSlots));
+    return existing;
+  }
+  FlowKey k = key;
+  FlowAction a = act;
+  int64_t first_slot = -1;   // where the NEW key ends up
+  int64_t pending_from = -1; // slot the entry currently being placed was evicted from
+  uint32_t avoid = 0xFFFFFFFFu;  // bucket the current entry was just evicted from
+  // track the path so a failed insert can be rolled back
+  std::vector<std::tuple<size_t, uint16_t, FlowKey, FlowAction>> undo;
+  std::vector<std::pair<int64_t, int64_t>> new_moves;
+  for (int kick = 0; kick < 512; ++kick) {
+    const TableHash cur = table_hash(hash(k), mask());
+    const uint32_t cand[2] = {cur.b1, cur.b2};
+    for (int c = 0; c < 2; ++c) {
+      for (int s = 0; s < kBucketSlots; ++s) {
+        const size_t i = (size_t)cand[c] * kBucketSlots + s;
+        if (tags_[i] == 0) {
+          tags_[i] = cur.tag; keys_[i] = k; vals_[i] = a;
+          dirty_.insert(cand[c]);
+          ++count_;
+          if (first_slot < 0) first_slot = (int64_t)i;
+          if (pending_from >= 0) new_moves.emplace_back(pending_from, (int64_t)i);
+          moves_.insert(moves_.end(), new_moves.begin(), new_moves.end());
+          return first_slot;
+        }
+      }
+    }
+    // evict a random victim, preferring the bucket the current entry did not come from
+    uint32_t vb = cand[rng_() & 1u];
+    if (vb == avoid) vb = (vb == cand[0]) ? cand[1] : cand[0];
+    const int vs = (int)(rng_() % kBucketSlots);
+    const size_t vi = (size_t)vb * kBucketSlots + vs;
+    undo.emplace_back(vi, tags_[vi], keys_[vi], vals_[vi]);
+    const FlowKey vk = keys_[vi];
+    const FlowAction va = vals_[vi];
+    tags_[vi] = cur.tag; keys_[vi] = k; vals_[vi] = a;
+    dirty_.insert(vb);
+    if (first_slot < 0) first_slot = (int64_t)vi;
+    if (pending_from >= 0) new_moves.emplace_back(pending_from, (int64_t)vi);
+    pending_from = (int64_t)vi;
+    avoid = vb;
+    k = vk; a = va;
+  }
+  // roll back
+  for (auto it = undo.rbegin(); it != undo.rend(); ++it) {
+    const size_t i = std::get<0>(*it);
+    tags_[i] = std::get<1>(*it); keys_[i] = std::get<2>(*it); vals_[i] = std::get<3>(*it);
+  }
+  throw std::runtime_error("flow table full (cuckoo insert failed after 512 kicks)");
+}
+
+bool FlowTableHost::erase(const FlowKey& k) {
+  const int64_t i = find(k);
+  if (i < 0) return false;
+  tags_[i] = 0; keys_[i] = FlowKey{0, 0, 0, 0}; vals_[i] = FlowAction{};
+  dirty_.insert((uint32_t)(i / kBucketSlots));
+  --count_;
+  return true;
+}
+
+std::vector<uint32_t> FlowTableHost::take_dirty() {
+  std::vector<uint32_t> v(dirty_.begin(), dirty_.end());
+  std::sort(v.begin(), v.end());
+  dirty_.clear();
+  return v;
+}
+
+std::vector<std::pair<int64_t, int64_t>> FlowTableHost::take_moves() {
+  auto m = std::move(moves_);
+  moves_.clear();
+  return m;
+}
+
+// ------------------------------------------------------------------------------------------
+// Classification tables in MFMA fragment layout.
+// A operand of v_mfma_i32_16x16x64_i8: lane l holds row (l & 15), k = 16*(l >> 4) + j, j<16.
+// k-step s covers key bits [64 s, 64 s + 64); key bit b = LSB-first over the 4 LE dwords.
+// ------------------------------------------------------------------------------------------
+static inline int key_bit(const uint32_t* w, int b) { return (w[b >> 5] >> (b & 31)) & 1; }
+
+AclFrags build_acl_frags(const uint32_t* value, const uint32_t* mask, uint32_t n) {
+  if (n > 1024) throw std::invalid_argument("ACL supports at most 1024 rules (10-bit rule index)");
+  AclFrags f;
+  f.tiles = (n + 15) / 16;
+  if (f.tiles == 0) f.tiles = 1;
+  const uint32_t npad = f.tiles * 16;
+  f.wfrag.assign((size_t)f.tiles * 2 * 64 * 16, 0);
+  f.cinit.assign((size_t)f.tiles * 16, 0);
+  std::vector<int32_t> bias(npad, 1);  // padded rules never match (mismatch >= 1)
+  for (uint32_t r = 0; r < n; ++r) {
+    int32_t bb = 0;
+    for (int b = 0; b < 128; ++b)
+      if (key_bit(mask + 4 * r, b) && key_bit(value + 4 * r, b)) ++bb;
+    bias[r] = bb;
+  }
+  for (uint32_t nt = 0; nt < f.tiles; ++nt)
+    for (int s = 0; s < 2; ++s)
+      for (int l = 0; l < 64; ++l)
+        for (int j = 0; j < 16; ++j) {
+          const uint32_t r = nt * 16 + (l & 15);
+          const int b = 64 * s + 16 * (l >> 4) + j;
+          int8_t w = 0;
+          if (r < n && key_bit(mask + 4 * r, b)) w = key_bit(value + 4 * r, b) ? -1 : 1;
+          f.wfrag[(((size_t)nt * 2 + s) * 64 + l) * 16 + j] = w;
+        }
+  for (uint32_t nt = 0; nt < f.tiles; ++nt)
+    for (int g = 0; g < 4; ++g)
+      for (int r = 0; r < 4; ++r) f.cinit[((size_t)nt * 4 + g) * 4 + r] = bias[nt * 16 + 4 * g + r];
+  return f;
+}
+
+static inline int rss_bit(const uint8_t* key, int x) { return (key[x >> 3] >> (7 - (x & 7))) & 1; }
+
+std::vector<int8_t> build_toeplitz_frags(const uint8_t* rss_key) {
+  std::vector<int8_t> f(2 * 2 * 64 * 16, 0);
+  for (int m = 0; m < 2; ++m)
+    for (int s = 0; s < 2; ++s)
+      for (int l = 0; l < 64; ++l)
+        for (int j = 0; j < 16; ++j) {
+          const int ncol = 16 * m + (l & 15);              // window offset
+          const int b = 64 * s + 16 * (l >> 4) + j;        // key bit (LSB-first LE)
+          const int i = 8 * (b >> 3) + (7 - (b & 7));      // Toeplitz input bit (MSB-first)
+          f[(((size_t)m * 2 + s) * 64 + l) * 16 + j] = (int8_t)rss_bit(rss_key, i + ncol);
+        }
+  return f;
+}
+
+std::vector<uint32_t> build_toeplitz_table(const uint8_t* rss_key) {
+  std::vector<uint32_t> t(16 * 256, 0);
+  for (int pos = 0; pos < 16; ++pos)
+    for (int v = 0; v < 256; ++v) {
+      uint32_t h = 0;
+      for (int bit = 7; bit >= 0; --bit) {
+        if (!(v & (1 << bit))) continue;
+        const int i = 8 * pos + (7 - bit);
+        uint32_t win = 0;
+        for (int q = 0; q < 32; ++q) win = (win << 1) | (uint32_t)rss_bit(rss_key, i + q);
+        h ^= win;
+      }
+      t[pos * 256 + v] = h;
+    }
+  return t;
+}
+
+// ------------------------------------------------------------------------------------------
+// CPU oracle
+// ------------------------------------------------------------------------------------------
+void oracle_run(const TablesView& t, const uint32_t* pkts, const uint32_t* inmeta, uint32_t n,
+                uint32_t* out, uint32_t* out_meta, uint64_t* flow_ctr, uint64_t* port_ctr,
+                uint64_t* drop_ctr, uint32_t* hashes, int32_t* acl_rules) {
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t* d = pkts + (size_t)i * kSlotDwords;
+    Parsed p;
+    IngressState st;
+    ingress_stage(t, d, inmeta[i], p, st);
+    const uint32_t h = toeplitz_scalar(st.key, t.rss_key);
+    const int acl = acl_first_match(t, st.key);
+    if (hashes) hashes[i] = h;
+    if (acl_rules) acl_rules[i] = acl;
+    bool hit = false;
+    FlowAction act = {};
+    if (!st.reason && p.ipv4) {
+      const int64_t slot = flow_lookup(t, st.key, h);
+      if (slot >= 0) {
+        hit = true;
+        act = t.vals[slot];
+        if (flow_ctr) flow_ctr[slot] += ctr_inc(st.wire_len);
+      }
+    }
+    const EgressDecision e = chain_stage(t, p, st, hit, act, acl);
+    uint32_t o[kSlotDwords];
+    emit(p, e.tci, e.push != 0, o);
+    const uint32_t olen = e.reason ? 0u : p.len + (e.push ? 4u : 0u);
+    std::memcpy(out + (size_t)i * kSlotDwords, o, sizeof(o));
+    out_meta[i] = make_meta(e.out_port, olen, e.reason);
+    if (port_ctr) {
+      if (st.in_port < (uint32_t)kMaxPorts) port_ctr[2 * st.in_port] += ctr_inc(st.wire_len);
+      if (!e.reason) port_ctr[2 * e.out_port + 1] += ctr_inc(olen);
+    }
+    if (drop_ctr && e.reason) drop_ctr[e.reason & (kNumReasons - 1)] += 1;
+  }
+}
+
+}  // namespace nfdp

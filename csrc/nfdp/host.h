@@ -1,0 +1,94 @@
+// host.h — host-side control structures for the data plane (authoritative flow table,
+// classification-table builders, CPU oracle, kernel launchers).
+#pragma once
+#include <cstring>
+#include <random>
+#include <stdexcept>
+#include <unordered_set>
+#include <vector>
+
+#include "pipeline.h"
+
+namespace nfdp {
+
+// Authoritative host copy of the exact-match flow table.  Bucketized (8 slots) 2-choice cuckoo
+// with eviction; every mutation records the touched bucket so the device copy is kept in sync by
+// re-sending whole buckets (bucket_update_kernel), ordered on the data-plane stream between
+// batches.  Replaces the reference's per-rule `p4rt-ctl add-entry` round trips
+// (vendor/.../p4rtclient/p4rtclient.go:74-101) with batched HBM row writes.
+class FlowTableHost {
+ public:
+  FlowTableHost(uint32_t nbuckets_pow2, const std::vector<uint8_t>& rss_key);
+  uint32_t nbuckets() const { return nb_; }
+  uint32_t mask() const { return nb_ - 1; }
+  size_t size() const { return count_; }
+  // returns slot index; throws when the table is full (after max kicks)
+  int64_t insert(const FlowKey& k, const FlowAction& a);
+  bool erase(const FlowKey& k);
+  int64_t find(const FlowKey& k) const;
+  uint32_t hash(const FlowKey& k) const { return toeplitz_scalar(k, rss_.data()); }
+  const std::vector<uint16_t>& tags() const { return tags_; }
+  const std::vector<FlowKey>& keys() const { return keys_; }
+  const std::vector<FlowAction>& vals() const { return vals_; }
+  // dirty tracking
+  std::vector<uint32_t> take_dirty();
+  // slot moves performed by evictions since the last take (from, to), for counter migration
+  std::vector<std::pair<int64_t, int64_t>> take_moves();
+  void clear_dirty() { dirty_.clear(); moves_.clear(); }
+  const std::vector<uint8_t>& rss_key() const { return rss_; }
+
+ private:
+  int find_in_bucket(uint32_t b, uint16_t tag, const FlowKey& k) const;
+  uint32_t nb_;
+  size_t count_ = 0;
+  std::vector<uint8_t> rss_;
+  std::vector<uint16_t> tags_;
+  std::vector<FlowKey> keys_;
+  std::vector<FlowAction> vals_;
+  std::unordered_set<uint32_t> dirty_;
+  std::vector<std::pair<int64_t, int64_t>> moves_;
+  std::mt19937 rng_{12345};
+};
+
+// Device-layout classification tables.
+struct AclFrags {
+  std::vector<int8_t> wfrag;   // [tiles][2][64][16]
+  std::vector<int32_t> cinit;  // [tiles][4][4]
+  uint32_t tiles = 0;
+};
+AclFrags build_acl_frags(const uint32_t* value, const uint32_t* mask, uint32_t n);
+std::vector<int8_t> build_toeplitz_frags(const uint8_t* rss_key);   // [2][2][64][16]
+std::vector<uint32_t> build_toeplitz_table(const uint8_t* rss_key); // [16][256]
+
+// CPU oracle of the fused pipeline (bit-exact reference for the GPU kernels).
+struct OracleOut {
+  std::vector<uint64_t> port_ctr;  // kMaxPorts * 2
+  std::vector<uint64_t> drop_ctr;  // kNumReasons
+};
+void oracle_run(const TablesView& t, const uint32_t* pkts, const uint32_t* inmeta, uint32_t n,
+                uint32_t* out, uint32_t* out_meta, uint64_t* flow_ctr, uint64_t* port_ctr,
+                uint64_t* drop_ctr, uint32_t* hashes, int32_t* acl_rules);
+
+// ---- GPU launchers (kernels.hip) ----
+struct LaunchCfg {
+  int hash_mode = 2;
+  int acl_mode = 1;
+  int num_cus = 256;
+};
+struct FusedLaunch {
+  TablesView t;
+  const void* pkts; const uint32_t* inmeta; void* out; uint32_t* out_meta; uint32_t n;
+  unsigned long long* flow_ctr; unsigned long long* port_ctr; unsigned long long* drop_ctr;
+  const unsigned long long* t0; uint32_t* lat;
+  const void* acl_wfrag; const void* acl_cinit; uint32_t acl_tiles;
+  const void* toep_frag; const uint32_t* toep_tab;
+};
+hipError_t launch_fused(const FusedLaunch& f, const LaunchCfg& cfg, hipStream_t s);
+size_t fused_lds_bytes(int hash_mode, int acl_mode, uint32_t acl_tiles);
+hipError_t launch_stamp(unsigned long long* dst, hipStream_t s);
+hipError_t launch_bucket_update(const uint32_t* idx, uint32_t nb, const void* tag_rows,
+                                const void* key_rows, const void* val_rows, void* tags, void* keys,
+                                void* vals, uint32_t bucket_mask, hipStream_t s);
+hipError_t launch_harvest(unsigned long long* ctr, unsigned long long* out, uint32_t n, hipStream_t s);
+
+}  // namespace nfdp

@@ -1,0 +1,399 @@
+// kernels.hip — CDNA4 (gfx950) data-plane kernels.
+//
+// Design (MI355X-first, see docs/DATAPLANE.md):
+//  * one packet per lane, 64-B slots loaded as 4 x dwordx4, 8 waves per workgroup, grid sized
+//    to the CU count x the LDS-admitted blocks per CU, grid-stride over the batch;
+//  * classification is ONE int8 MFMA GEMM over the bit-expanded 128-bit FlowKey:
+//      - Toeplitz RSS hash = GF(2) product  key_bits[16 pkts x 128] x T[128 x 32], parity (&1)
+//      - TCAM / priority ACL = key_bits x W[128 x R] + bias, W in {-1,0,+1}; a rule matches
+//        iff its mismatch count is 0; first match by min((mismatch << 10) | rule)
+//    (v_mfma_i32_16x16x64_i8; rules/hash bits are the M rows, 16 packets the N columns), with
+//    the rule fragments staged once per workgroup in LDS;
+//  * exact-match flow lookup: 16-B tag row per bucket (8 x u16), 2 choices, then one 16-B key
+//    compare and one 16-B action load (tables sized for HBM: 1M flows = 68 MB, 288 GB ok);
+//  * per-port counters aggregated in LDS, flushed once per workgroup; per-flow counters are one
+//    packed 64-bit atomic per packet.
+#include "host.h"
+
+namespace nfdp {
+
+typedef int v4i __attribute__((ext_vector_type(4)));
+
+constexpr int kBlock = 512;
+constexpr int kWaves = kBlock / 64;
+constexpr int kLdsPorts = 256;
+
+enum HashMode { kHashScalar = 0, kHashLds = 1, kHashMfma = 2 };
+enum AclMode { kAclScalar = 0, kAclMfma = 1, kAclOff = 2 };
+
+struct FusedArgs {
+  TablesView t;
+  const uint4* pkts;              // n slots of 64 B
+  const uint32_t* inmeta;         // in_port | len << 16
+  uint4* out;                     // n slots
+  uint32_t* out_meta;             // out_port | len << 16 | reason << 24
+  uint32_t n;
+  unsigned long long* flow_ctr;   // nbuckets * 8 packed counters (nullable)
+  unsigned long long* port_ctr;   // kMaxPorts * 2 packed (rx, tx)
+  unsigned long long* drop_ctr;   // kNumReasons
+  const unsigned long long* t0;   // batch-release stamp (s_memrealtime ticks, 100 MHz)
+  uint32_t* lat;                  // n/16 latency samples (ticks) (nullable)
+  const v4i* acl_wfrag;           // [tiles][2][64] A fragments (int8 x16)
+  const v4i* acl_cinit;           // [tiles][4] C init (bias) for rows 4g..4g+3
+  const v4i* toep_frag;           // [2][2][64] A fragments of the Toeplitz matrix
+  const uint32_t* toep_tab;       // [16][256] byte tables (LDS hash variant)
+  uint32_t acl_tiles;             // ceil(n_acl / 16)
+};
+
+// 16 bits -> 16 bytes of {0,1}: byte j = bit j.  (nibble * 0x00204081) spreads 4 bits to 4
+// bytes without carries.
+__device__ __forceinline__ v4i expand16(uint32_t x) {
+  v4i r;
+  r[0] = (int)((((x) & 0xFu) * 0x00204081u) & 0x01010101u);
+  r[1] = (int)((((x >> 4) & 0xFu) * 0x00204081u) & 0x01010101u);
+  r[2] = (int)((((x >> 8) & 0xFu) * 0x00204081u) & 0x01010101u);
+  r[3] = (int)((((x >> 12) & 0xFu) * 0x00204081u) & 0x01010101u);
+  return r;
+}
+
+__device__ __forceinline__ uint32_t pick4(uint32_t g, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+  return g == 0 ? a : g == 1 ? b : g == 2 ? c : d;
+}
+
+// Wave-level classification over the wave's 64 packets (one per lane).  EXEC must be full.
+template <int HASH, int ACL>
+__device__ __forceinline__ void classify_wave(const FlowKey& key, uint4* kx, const v4i* lw,
+                                              const v4i* lc, uint32_t acl_tiles, const v4i* lt,
+                                              const uint32_t* ltab, const TablesView& t,
+                                              uint32_t& hash, int& acl_rule) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t g = lane >> 4, col = lane & 15u;
+  v4i bf[4][2];
+  if constexpr (HASH == kHashMfma || ACL == kAclMfma) {
+    kx[lane] = make_uint4(key.src_ip, key.dst_ip, key.ports, key.meta);
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+#pragma unroll
+    for (int tt = 0; tt < 4; ++tt) {
+      const uint32_t* src = reinterpret_cast<const uint32_t*>(kx + 16 * tt + col);
+      const uint32_t wlo = src[g >> 1], whi = src[2 + (g >> 1)];
+      const uint32_t sh = 16u * (g & 1u);
+      bf[tt][0] = expand16((wlo >> sh) & 0xFFFFu);
+      bf[tt][1] = expand16((whi >> sh) & 0xFFFFu);
+    }
+  }
+  // ---- hash ----
+  if constexpr (HASH == kHashMfma) {
+    uint32_t hv[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      const v4i a0 = lt[(m * 2 + 0) * 64 + lane], a1 = lt[(m * 2 + 1) * 64 + lane];
+#pragma unroll
+      for (int tt = 0; tt < 4; ++tt) {
+        v4i acc = {0, 0, 0, 0};
+        acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a0, bf[tt][0], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a1, bf[tt][1], acc, 0, 0, 0);
+        uint32_t bits = ((uint32_t)acc[0] & 1u) | (((uint32_t)acc[1] & 1u) << 1) |
+                        (((uint32_t)acc[2] & 1u) << 2) | (((uint32_t)acc[3] & 1u) << 3);
+        hv[tt] |= bits << (4u * g + 16u * m);
+      }
+    }
+#pragma unroll
+    for (int tt = 0; tt < 4; ++tt) {
+      hv[tt] |= __shfl_xor(hv[tt], 16);
+      hv[tt] |= __shfl_xor(hv[tt], 32);
+    }
+    hash = __builtin_bitreverse32(pick4(g, hv[0], hv[1], hv[2], hv[3]));
+  } else if constexpr (HASH == kHashLds) {
+    const uint32_t w[4] = {key.src_ip, key.dst_ip, key.ports, key.meta};
+    uint32_t h = 0;
+#pragma unroll
+    for (int b = 0; b < 16; ++b) h ^= ltab[b * 256 + ((w[b >> 2] >> (8 * (b & 3))) & 0xFFu)];
+    hash = h;
+  } else {
+    hash = toeplitz_scalar(key, t.rss_key);
+  }
+  // ---- ACL (TCAM) ----
+  if constexpr (ACL == kAclMfma) {
+    uint32_t best[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+    for (uint32_t nt = 0; nt < acl_tiles; ++nt) {
+      const v4i a0 = lw[(nt * 2 + 0) * 64 + lane], a1 = lw[(nt * 2 + 1) * 64 + lane];
+      const v4i c = lc[nt * 4 + g];
+      const uint32_t rb = nt * 16u + 4u * g;
+#pragma unroll
+      for (int tt = 0; tt < 4; ++tt) {
+        v4i acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a0, bf[tt][0], c, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a1, bf[tt][1], acc, 0, 0, 0);
+        const uint32_t e0 = ((uint32_t)acc[0] << 10) | (rb + 0);
+        const uint32_t e1 = ((uint32_t)acc[1] << 10) | (rb + 1);
+        const uint32_t e2 = ((uint32_t)acc[2] << 10) | (rb + 2);
+        const uint32_t e3 = ((uint32_t)acc[3] << 10) | (rb + 3);
+        best[tt] = min(best[tt], min(min(e0, e1), min(e2, e3)));
+      }
+    }
+#pragma unroll
+    for (int tt = 0; tt < 4; ++tt) {
+      best[tt] = min(best[tt], (uint32_t)__shfl_xor(best[tt], 16));
+      best[tt] = min(best[tt], (uint32_t)__shfl_xor(best[tt], 32));
+    }
+    const uint32_t b = pick4(g, best[0], best[1], best[2], best[3]);
+    acl_rule = (b >> 10) == 0 ? (int)(b & 1023u) : -1;
+    if (acl_rule >= (int)t.n_acl) acl_rule = -1;
+  } else if constexpr (ACL == kAclScalar) {
+    acl_rule = acl_first_match(t, key);
+  } else {
+    acl_rule = -1;
+  }
+}
+
+// Vectorized 2-choice bucket probe: one 16-B tag row per bucket, 16-B key compare on a tag hit.
+__device__ __forceinline__ int64_t flow_lookup_vec(const TablesView& t, const FlowKey& k, uint32_t h) {
+  const TableHash th = table_hash(h, t.bucket_mask);
+  const uint4* tags = reinterpret_cast<const uint4*>(t.tags);
+  const uint4* keys = reinterpret_cast<const uint4*>(t.keys);
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    const uint32_t b = c ? th.b2 : th.b1;
+    const uint4 tg = tags[b];
+    const uint32_t tw[4] = {tg.x, tg.y, tg.z, tg.w};
+    uint32_t m = 0;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      m |= ((tw[s] & 0xFFFFu) == th.tag ? 1u : 0u) << (2 * s);
+      m |= ((tw[s] >> 16) == th.tag ? 1u : 0u) << (2 * s + 1);
+    }
+    while (m) {
+      const uint32_t s = __builtin_ctz(m);
+      m &= m - 1;
+      const uint4 e = keys[(size_t)b * kBucketSlots + s];
+      if (e.x == k.src_ip && e.y == k.dst_ip && e.z == k.ports && e.w == k.meta)
+        return (int64_t)b * kBucketSlots + s;
+    }
+  }
+  return -1;
+}
+
+__device__ __forceinline__ size_t lds_align16(size_t x) { return (x + 15) & ~(size_t)15; }
+
+struct LdsLayout {
+  size_t acl_w, acl_c, toep_f, toep_t, kx, pc, drops, total;
+};
+__host__ __device__ inline LdsLayout lds_layout(int hash_mode, int acl_mode, uint32_t acl_tiles) {
+  LdsLayout L;
+  size_t o = 0;
+  L.acl_w = o; if (acl_mode == kAclMfma) o += (size_t)acl_tiles * 2 * 64 * 16;
+  L.acl_c = o; if (acl_mode == kAclMfma) o += (size_t)acl_tiles * 4 * 16;
+  L.toep_f = o; if (hash_mode == kHashMfma) o += 2 * 2 * 64 * 16;
+  L.toep_t = o; if (hash_mode == kHashLds) o += 16 * 256 * 4;
+  L.kx = o; o += kWaves * 64 * 16;
+  L.pc = o; o += kLdsPorts * 4 * 4;
+  L.drops = o; o += kNumReasons * 4;
+  L.total = (o + 15) & ~(size_t)15;
+  return L;
+}
+
+template <int HASH, int ACL>
+__global__ __launch_bounds__(kBlock) void fused_kernel(FusedArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const LdsLayout L = lds_layout(HASH, ACL, a.acl_tiles);
+  v4i* lw = reinterpret_cast<v4i*>(smem + L.acl_w);
+  v4i* lc = reinterpret_cast<v4i*>(smem + L.acl_c);
+  v4i* lt = reinterpret_cast<v4i*>(smem + L.toep_f);
+  uint32_t* ltab = reinterpret_cast<uint32_t*>(smem + L.toep_t);
+  uint4* kx = reinterpret_cast<uint4*>(smem + L.kx) + (threadIdx.x >> 6) * 64;
+  uint32_t* pc = reinterpret_cast<uint32_t*>(smem + L.pc);   // [4][256]: rx_pk rx_by tx_pk tx_by
+  uint32_t* drops = reinterpret_cast<uint32_t*>(smem + L.drops);
+
+  // ---- stage classification tables + zero counters ----
+  if constexpr (ACL == kAclMfma) {
+    const uint32_t nw = a.acl_tiles * 2 * 64, nc = a.acl_tiles * 4;
+    for (uint32_t i = threadIdx.x; i < nw; i += kBlock) lw[i] = a.acl_wfrag[i];
+    for (uint32_t i = threadIdx.x; i < nc; i += kBlock) lc[i] = a.acl_cinit[i];
+  }
+  if constexpr (HASH == kHashMfma)
+    for (uint32_t i = threadIdx.x; i < 256; i += kBlock) lt[i] = a.toep_frag[i];
+  if constexpr (HASH == kHashLds)
+    for (uint32_t i = threadIdx.x; i < 4096; i += kBlock) ltab[i] = a.toep_tab[i];
+  for (uint32_t i = threadIdx.x; i < kLdsPorts * 4; i += kBlock) pc[i] = 0;
+  if (threadIdx.x < kNumReasons) drops[threadIdx.x] = 0;
+  __syncthreads();
+
+  const unsigned long long t0 = a.t0 ? *a.t0 : 0ull;
+  const uint4* pk4 = a.pkts;
+  for (uint32_t base = blockIdx.x * kBlock; base < a.n; base += gridDim.x * kBlock) {
+    const uint32_t i = base + threadIdx.x;
+    const bool valid = i < a.n;
+    uint32_t d[kSlotDwords];
+    uint32_t im = 0;
+    if (valid) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint4 v = pk4[(size_t)i * 4 + q];
+        d[4 * q] = v.x; d[4 * q + 1] = v.y; d[4 * q + 2] = v.z; d[4 * q + 3] = v.w;
+      }
+      im = a.inmeta[i];
+    } else {
+#pragma unroll
+      for (int q = 0; q < kSlotDwords; ++q) d[q] = 0;
+    }
+    Parsed p;
+    IngressState st;
+    ingress_stage(a.t, d, im, p, st);
+    if (!valid) st.reason = kMalformed;
+
+    uint32_t hash = 0;
+    int acl_rule = -1;
+    classify_wave<HASH, ACL>(st.key, kx, lw, lc, a.acl_tiles, lt, ltab, a.t, hash, acl_rule);
+
+    bool hit = false;
+    FlowAction act = {};
+    if (!st.reason && p.ipv4) {
+      const int64_t slot = flow_lookup_vec(a.t, st.key, hash);
+      if (slot >= 0) {
+        hit = true;
+        const uint4 v = reinterpret_cast<const uint4*>(a.t.vals)[slot];
+        act.chain_id = v.x & 0xFFFFu; act.out_port = v.x >> 16; act.nat_ip = v.y;
+        act.nat_port = v.z & 0xFFFFu; act.vlan = v.z >> 16; act.flow_id = v.w;
+        if (a.flow_ctr) atomicAdd(a.flow_ctr + slot, ctr_inc(st.wire_len));
+      }
+    }
+    const EgressDecision e = chain_stage(a.t, p, st, hit, act, acl_rule);
+    if (valid) {
+      uint32_t o[kSlotDwords];
+      emit(p, e.tci, e.push != 0, o);
+      const uint32_t olen = e.reason ? 0u : p.len + (e.push ? 4u : 0u);
+      uint4* dst = a.out + (size_t)i * 4;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) dst[q] = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
+      a.out_meta[i] = make_meta(e.out_port, olen, e.reason);
+      // counters
+      if (st.in_port < kLdsPorts) {
+        atomicAdd(&pc[st.in_port], 1u); atomicAdd(&pc[kLdsPorts + st.in_port], st.wire_len);
+      } else if (st.in_port < (uint32_t)kMaxPorts) {
+        atomicAdd(a.port_ctr + 2 * st.in_port, ctr_inc(st.wire_len));
+      }
+      if (e.reason) {
+        atomicAdd(&drops[e.reason & (kNumReasons - 1)], 1u);
+      } else if (e.out_port < kLdsPorts) {
+        atomicAdd(&pc[2 * kLdsPorts + e.out_port], 1u); atomicAdd(&pc[3 * kLdsPorts + e.out_port], olen);
+      } else {
+        atomicAdd(a.port_ctr + 2 * e.out_port + 1, ctr_inc(olen));
+      }
+      if (a.lat && (i & 15u) == 0) {
+        const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+        a.lat[i >> 4] = (uint32_t)(now - t0);
+      }
+    }
+  }
+  __syncthreads();
+  for (uint32_t q = threadIdx.x; q < kLdsPorts; q += kBlock) {
+    if (pc[q]) atomicAdd(a.port_ctr + 2 * q, ((unsigned long long)pc[q] << 40) | pc[kLdsPorts + q]);
+    if (pc[2 * kLdsPorts + q])
+      atomicAdd(a.port_ctr + 2 * q + 1, ((unsigned long long)pc[2 * kLdsPorts + q] << 40) | pc[3 * kLdsPorts + q]);
+  }
+  if (threadIdx.x < kNumReasons && drops[threadIdx.x])
+    atomicAdd(a.drop_ctr + threadIdx.x, (unsigned long long)drops[threadIdx.x]);
+}
+
+__global__ void stamp_kernel(unsigned long long* dst) {
+  if (threadIdx.x == 0) *dst = __builtin_amdgcn_s_memrealtime();
+}
+
+// Scatter whole bucket rows (control-plane updates: a modified bucket is re-sent entire).
+__global__ void bucket_update_kernel(const uint32_t* idx, uint32_t nb, const uint4* tag_rows,
+                                     const uint4* key_rows, const uint4* val_rows, uint4* tags,
+                                     uint4* keys, uint4* vals, uint32_t bucket_mask) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;  // one thread per (bucket, slot)
+  const uint32_t bi = j / kBucketSlots, s = j % kBucketSlots;
+  if (bi >= nb) return;
+  const uint32_t b = idx[bi];
+  if (b > bucket_mask) return;
+  keys[(size_t)b * kBucketSlots + s] = key_rows[(size_t)bi * kBucketSlots + s];
+  vals[(size_t)b * kBucketSlots + s] = val_rows[(size_t)bi * kBucketSlots + s];
+  if (s == 0) tags[b] = tag_rows[bi];
+}
+
+// Read-and-reset packed counters (harvest); host accumulates into 64-bit totals.
+__global__ void harvest_kernel(unsigned long long* ctr, unsigned long long* out, uint32_t n) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j < n) out[j] = atomicExch(ctr + j, 0ull);
+}
+
+
+// ------------------------------------------------------------------------------------------
+// Launchers
+// ------------------------------------------------------------------------------------------
+size_t fused_lds_bytes(int hash_mode, int acl_mode, uint32_t acl_tiles) {
+  return lds_layout(hash_mode, acl_mode, acl_tiles).total;
+}
+
+template <int H, int A>
+static hipError_t launch_fused_t(const FusedArgs& a, int num_cus, hipStream_t s) {
+  const size_t lds = lds_layout(H, A, a.acl_tiles).total;
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&fused_kernel<H, A>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  int per_cu = (int)((160 * 1024) / (lds ? lds : 1));
+  per_cu = per_cu < 1 ? 1 : (per_cu > 4 ? 4 : per_cu);
+  const uint32_t need = (a.n + kBlock - 1) / kBlock;
+  uint32_t grid = (uint32_t)(per_cu * num_cus);
+  if (need < grid) grid = need;
+  if (grid == 0) return hipSuccess;
+  hipLaunchKernelGGL((fused_kernel<H, A>), dim3(grid), dim3(kBlock), lds, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_fused(const FusedLaunch& f, const LaunchCfg& cfg, hipStream_t s) {
+  FusedArgs a;
+  a.t = f.t;
+  a.pkts = reinterpret_cast<const uint4*>(f.pkts);
+  a.inmeta = f.inmeta;
+  a.out = reinterpret_cast<uint4*>(f.out);
+  a.out_meta = f.out_meta;
+  a.n = f.n;
+  a.flow_ctr = f.flow_ctr; a.port_ctr = f.port_ctr; a.drop_ctr = f.drop_ctr;
+  a.t0 = f.t0; a.lat = f.lat;
+  a.acl_wfrag = reinterpret_cast<const v4i*>(f.acl_wfrag);
+  a.acl_cinit = reinterpret_cast<const v4i*>(f.acl_cinit);
+  a.acl_tiles = f.acl_tiles;
+  a.toep_frag = reinterpret_cast<const v4i*>(f.toep_frag);
+  a.toep_tab = f.toep_tab;
+  if (cfg.acl_mode == kAclMfma && (f.acl_tiles == 0 || f.acl_tiles > 64)) return hipErrorInvalidValue;
+  const int h = cfg.hash_mode, ac = cfg.acl_mode, cu = cfg.num_cus;
+#define NFDP_CASE(HH, AA) if (h == HH && ac == AA) return launch_fused_t<HH, AA>(a, cu, s);
+  NFDP_CASE(0, 0) NFDP_CASE(0, 1) NFDP_CASE(0, 2)
+  NFDP_CASE(1, 0) NFDP_CASE(1, 1) NFDP_CASE(1, 2)
+  NFDP_CASE(2, 0) NFDP_CASE(2, 1) NFDP_CASE(2, 2)
+#undef NFDP_CASE
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_stamp(unsigned long long* dst, hipStream_t s) {
+  hipLaunchKernelGGL(stamp_kernel, dim3(1), dim3(64), 0, s, dst);
+  return hipGetLastError();
+}
+
+hipError_t launch_bucket_update(const uint32_t* idx, uint32_t nb, const void* tag_rows,
+                                const void* key_rows, const void* val_rows, void* tags, void* keys,
+                                void* vals, uint32_t bucket_mask, hipStream_t s) {
+  if (nb == 0) return hipSuccess;
+  const uint32_t threads = nb * kBucketSlots;
+  hipLaunchKernelGGL(bucket_update_kernel, dim3((threads + 255) / 256), dim3(256), 0, s, idx, nb,
+                     reinterpret_cast<const uint4*>(tag_rows), reinterpret_cast<const uint4*>(key_rows),
+                     reinterpret_cast<const uint4*>(val_rows), reinterpret_cast<uint4*>(tags),
+                     reinterpret_cast<uint4*>(keys), reinterpret_cast<uint4*>(vals), bucket_mask);
+  return hipGetLastError();
+}
+
+hipError_t launch_harvest(unsigned long long* ctr, unsigned long long* out, uint32_t n, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(harvest_kernel, dim3((n + 255) / 256), dim3(256), 0, s, ctr, out, n);
+  return hipGetLastError();
+}
+
+}  // namespace nfdp

@@ -1,0 +1,392 @@
+// nfdp.h — MI355X network-function data plane: shared types + scalar per-packet logic.
+//
+// This header is compiled only by hipcc (one toolchain, gfx950 only).  Everything here is
+// `__host__ __device__` so the same per-packet semantics run inside the GPU kernels
+// (kernels.hip) and inside the scalar CPU oracle (oracle.cpp) that the tests use to check the
+// GPU bit-exactly.
+//
+// What it replaces in the reference (Ximinhan/dpu-operator): the per-packet behaviour the
+// reference *configures* in DPU silicon / OvS but never executes itself:
+//   * VF VLAN isolation / spoof-check (intel-netsec/main.go:432-503, vspnetutils.go:249-258)
+//   * source-port / bridge-id classification (p4rtclient.go:242-256, 674-691)
+//   * (bridge, dst-MAC) L2 forwarding (p4rtclient.go:565-571; p4info.txt:600-692)
+//   * VLAN push/pop on the way to/from a host VF (p4rtclient.go:553-564)
+//   * OvS steering / hairpin used for SFC hops (ovsdp.go:113-142, marvell/main.go:490-563)
+// plus exact-match 5-tuple flow state (1M+ flows, sharded across GPUs) and built-in NFs.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define NFDP_HD __host__ __device__ __forceinline__
+
+namespace nfdp {
+
+// ----------------------------------------------------------------------------------------
+// Constants
+// ----------------------------------------------------------------------------------------
+constexpr int kSlotBytes = 64;         // one packet slot in HBM (60 B frame + room for one tag)
+constexpr int kSlotDwords = kSlotBytes / 4;
+constexpr int kMaxPorts = 4096;        // vport table size (VF / NF / wire / PR ports)
+constexpr int kBucketSlots = 8;        // flow-table bucket = 8 slots, 16-B tag row
+constexpr uint16_t kPortNone = 0xFFFF; // dropped
+constexpr uint16_t kPortPunt = 0xFFFE; // to slow path (control plane upcall)
+constexpr int kMaxHops = 7;
+constexpr int kAclKeyBits = 128;       // ACL / hash key = the 16-byte FlowKey
+
+// drop / disposition reasons (meta bits 24..31)
+enum Reason : uint32_t {
+  kOk = 0,
+  kBadPort = 1,
+  kVlanDrop = 2,
+  kSpoof = 3,
+  kAclDeny = 4,
+  kNoRoute = 5,  // punted to slow path (flow miss + MAC miss)
+  kTooBig = 6,
+  kChainDrop = 7,
+  kTtlExpired = 8,
+  kMalformed = 9,
+  kNumReasons = 16,
+};
+
+// port flags
+enum PortFlags : uint32_t {
+  kPortValid = 1u << 0,
+  kPortSpoofChk = 1u << 1,      // src MAC must equal port MAC (sriov spoofchk)
+  kPortVlanIsolate = 1u << 2,   // tagged ingress must carry port.vlan (K10)
+  kPortTagEgress = 1u << 3,     // push port.vlan on egress (K6 vlan_push to host VF)
+  kPortVlanBridge = 1u << 4,    // ingress vid selects bridge id (K7)
+  kPortTrust = 1u << 5,
+};
+
+// chain hop opcodes (built-in GPU network functions)
+enum Hop : uint8_t {
+  kHopNone = 0,
+  kHopAcl = 1,      // stateless firewall: TCAM (priority/ternary) on the ingress FlowKey
+  kHopNat = 2,      // SNAT: rewrite src ip/port from the flow entry, incremental checksums
+  kHopL2Fwd = 3,    // steer to flow.out_port, rewrite MACs to the egress port's (mac, peer_mac)
+  kHopTtl = 4,      // router hop: TTL-1, checksum
+  kHopHairpin = 5,  // bounce back out of the ingress port, swap MACs (OvS in_port action)
+  kHopVlan = 6,     // push (1..4094) / pop (0xFFFF) flow.vlan
+  kHopDrop = 7,
+  kHopPunt = 8,
+};
+
+// ----------------------------------------------------------------------------------------
+// Tables (all POD, 16-B aligned so the kernels use dwordx4 accesses)
+// ----------------------------------------------------------------------------------------
+struct alignas(16) PortEntry {   // 32 B
+  uint32_t flags;
+  uint16_t vlan;                 // VF vlan (vf+2 in the reference's convention)
+  uint16_t bridge_id;
+  uint32_t mac_lo;               // this port's MAC (raw network-order bytes 0..3)
+  uint16_t mac_hi;               //                  bytes 4..5
+  uint16_t gpu;                  // owning GPU rank (egress side)
+  uint32_t peer_mac_lo;          // MAC of whatever is attached (pod / NF / next hop)
+  uint16_t peer_mac_hi;
+  uint16_t pad0;
+  uint32_t pad1, pad2;
+};
+static_assert(sizeof(PortEntry) == 32, "PortEntry");
+
+struct alignas(16) FlowKey {     // 16 B; also the ACL / Toeplitz input (128 bits)
+  uint32_t src_ip;               // raw network-order bytes (little-endian load of the header)
+  uint32_t dst_ip;
+  uint32_t ports;                // sport (raw) | dport (raw) << 16
+  uint32_t meta;                 // proto | (zone << 16); byte 1 must be 0 in the key
+};
+static_assert(sizeof(FlowKey) == 16, "FlowKey");
+
+struct alignas(16) FlowAction {  // 16 B value of an exact-match flow entry
+  uint16_t chain_id;             // index into the chain table
+  uint16_t out_port;             // egress vport
+  uint32_t nat_ip;               // raw network order (used by kHopNat)
+  uint16_t nat_port;             // raw network order
+  uint16_t vlan;                 // used by kHopVlan: 0 none, 1..4094 push, 0xFFFF pop
+  uint32_t flow_id;              // stable id (control plane bookkeeping)
+};
+static_assert(sizeof(FlowAction) == 16, "FlowAction");
+
+struct alignas(16) ChainEntry {  // 16 B
+  uint8_t nhops;
+  uint8_t hop[kMaxHops];
+  uint16_t acl_id;
+  uint16_t flags;
+  uint32_t pad;
+};
+static_assert(sizeof(ChainEntry) == 16, "ChainEntry");
+
+struct alignas(16) MacEntry {    // 16 B, (bridge, dst-mac) -> port  (K5)
+  uint32_t mac_lo;
+  uint16_t mac_hi;
+  uint16_t bridge_id;
+  uint16_t out_port;
+  uint16_t valid;
+  uint32_t pad;
+};
+static_assert(sizeof(MacEntry) == 16, "MacEntry");
+
+// Verdict returned by the flow owner to the ingress GPU (multi-GPU path).
+struct alignas(16) Verdict {     // 16 B
+  uint16_t chain_id;
+  uint16_t out_port;
+  uint32_t nat_ip;
+  uint16_t nat_port;
+  uint16_t vlan;
+  uint32_t status;               // 1 = hit, 0 = miss
+};
+static_assert(sizeof(Verdict) == 16, "Verdict");
+
+// ----------------------------------------------------------------------------------------
+// Hashing
+// ----------------------------------------------------------------------------------------
+NFDP_HD uint32_t fmix32(uint32_t h) {
+  h ^= h >> 16; h *= 0x85ebca6bu; h ^= h >> 13; h *= 0xc2b2ae35u; h ^= h >> 16;
+  return h;
+}
+
+// Standard (Microsoft RSS) Toeplitz over the 16 key bytes in memory order, MSB-first bits.
+// `rss_key` is >= 20 bytes.  Its first 12 input bytes (src ip, dst ip, sport, dport) give the
+// standard RSS 4-tuple hash contribution; proto/zone extend it.
+NFDP_HD uint32_t toeplitz_scalar(const FlowKey& k, const uint8_t* rss_key) {
+  const uint32_t w[4] = {k.src_ip, k.dst_ip, k.ports, k.meta};
+  uint32_t v = ((uint32_t)rss_key[0] << 24) | ((uint32_t)rss_key[1] << 16) |
+               ((uint32_t)rss_key[2] << 8) | rss_key[3];
+  uint32_t h = 0;
+  for (int byte = 0; byte < 16; ++byte) {
+    const uint32_t b = (w[byte >> 2] >> (8 * (byte & 3))) & 0xFFu;
+    const uint32_t next = rss_key[byte + 4];
+    for (int bit = 7; bit >= 0; --bit) {
+      if (b & (1u << bit)) h ^= v;
+      v = (v << 1) | ((next >> bit) & 1u);
+    }
+  }
+  return h;
+}
+
+// Flow-table geometry derived from the Toeplitz hash.
+struct TableHash { uint32_t b1, b2; uint16_t tag; };
+NFDP_HD TableHash table_hash(uint32_t h, uint32_t bucket_mask) {
+  TableHash t;
+  const uint32_t m = fmix32(h ^ 0x9e3779b9u);
+  t.b1 = h & bucket_mask;
+  t.b2 = (m ^ (m >> 7)) & bucket_mask;
+  if (t.b2 == t.b1) t.b2 = (t.b1 + 1) & bucket_mask;  // two distinct choices
+  uint16_t tag = (uint16_t)(m >> 16);
+  t.tag = tag ? tag : 1;                                // 0 = empty slot
+  return t;
+}
+// Shard (owner GPU) from the top bits of the hash: independent of the bucket (low) bits.
+NFDP_HD uint32_t owner_of(uint32_t h, uint32_t nshards) {
+  return (uint32_t)(((uint64_t)h * nshards) >> 32);
+}
+
+// ----------------------------------------------------------------------------------------
+// Parsing.  A packet is 16 little-endian dwords.  `s` is the *normalized* (untagged) view:
+// an 802.1Q tag (4 B at offset 12) is removed by a one-dword shift, since 4 B = 1 dword.
+// ----------------------------------------------------------------------------------------
+struct Parsed {
+  uint32_t s[kSlotDwords];  // normalized frame (untagged layout), bytes beyond len are junk
+  uint32_t len;             // normalized length in bytes (tag removed)
+  uint32_t tci;             // 802.1Q TCI (0 if untagged)
+  bool tagged;
+  bool ipv4;                // IPv4 with IHL=5, first fragment, fully inside the slot
+  bool l4;                  // TCP or UDP ports present
+};
+
+NFDP_HD uint32_t be16_at(const uint32_t* s, int byte) {  // byte offset must be even
+  const uint32_t w = s[byte >> 2] >> (8 * (byte & 2));
+  return ((w & 0xFFu) << 8) | ((w >> 8) & 0xFFu);
+}
+NFDP_HD uint32_t raw16_at(const uint32_t* s, int byte) {  // raw LE 16 (even offset)
+  return (s[byte >> 2] >> (8 * (byte & 2))) & 0xFFFFu;
+}
+NFDP_HD void set_raw16(uint32_t* s, int byte, uint32_t v) {
+  const int sh = 8 * (byte & 2);
+  s[byte >> 2] = (s[byte >> 2] & ~(0xFFFFu << sh)) | ((v & 0xFFFFu) << sh);
+}
+NFDP_HD uint32_t raw32_at2(const uint32_t* s, int byte) {  // byte ≡ 2 (mod 4)
+  return (s[byte >> 2] >> 16) | (s[(byte >> 2) + 1] << 16);
+}
+NFDP_HD void set_raw32_at2(uint32_t* s, int byte, uint32_t v) {
+  s[byte >> 2] = (s[byte >> 2] & 0xFFFFu) | (v << 16);
+  s[(byte >> 2) + 1] = (s[(byte >> 2) + 1] & 0xFFFF0000u) | (v >> 16);
+}
+
+NFDP_HD void parse(const uint32_t* d, uint32_t len, Parsed& p) {
+  const uint32_t et = be16_at(d, 12);
+  p.tagged = (et == 0x8100u) && len >= 18;
+  p.tci = p.tagged ? be16_at(d, 14) : 0u;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) p.s[i] = d[i];
+#pragma unroll
+  for (int i = 3; i < kSlotDwords - 1; ++i) p.s[i] = p.tagged ? d[i + 1] : d[i];
+  p.s[kSlotDwords - 1] = p.tagged ? 0u : d[kSlotDwords - 1];
+  p.len = p.tagged ? len - 4 : len;
+  const uint32_t et2 = be16_at(p.s, 12);
+  const uint32_t verihl = p.s[3] >> 16 & 0xFFu;
+  const uint32_t frag = be16_at(p.s, 20);
+  p.ipv4 = et2 == 0x0800u && verihl == 0x45u && p.len >= 34 && (frag & 0x1FFFu) == 0;
+  const uint32_t proto = p.s[5] >> 24;
+  p.l4 = p.ipv4 && (proto == 6 || proto == 17) && p.len >= 38;
+}
+
+NFDP_HD uint32_t dmac_lo(const uint32_t* s) { return s[0]; }
+NFDP_HD uint32_t dmac_hi(const uint32_t* s) { return s[1] & 0xFFFFu; }
+NFDP_HD uint32_t smac_lo(const uint32_t* s) { return (s[1] >> 16) | (s[2] << 16); }
+NFDP_HD uint32_t smac_hi(const uint32_t* s) { return s[2] >> 16; }
+NFDP_HD void set_dmac(uint32_t* s, uint32_t lo, uint32_t hi) {
+  s[0] = lo; s[1] = (s[1] & 0xFFFF0000u) | (hi & 0xFFFFu);
+}
+NFDP_HD void set_smac(uint32_t* s, uint32_t lo, uint32_t hi) {
+  s[1] = (s[1] & 0xFFFFu) | (lo << 16);
+  s[2] = (lo >> 16) | (hi << 16);
+}
+
+NFDP_HD FlowKey make_key(const Parsed& p, uint32_t zone) {
+  FlowKey k;
+  k.src_ip = raw32_at2(p.s, 26);
+  k.dst_ip = raw32_at2(p.s, 30);
+  k.ports = p.l4 ? raw32_at2(p.s, 34) : 0u;
+  k.meta = (p.s[5] >> 24) | (zone << 16);
+  return k;
+}
+
+// ----------------------------------------------------------------------------------------
+// Checksums (RFC 1624 incremental update).  Works in the raw (byte-swapped) 16-bit domain:
+// the one's-complement sum is byte-order independent as long as field and csum agree.
+// ----------------------------------------------------------------------------------------
+NFDP_HD uint32_t csum_fold(uint32_t x) {
+  x = (x & 0xFFFFu) + (x >> 16);
+  x = (x & 0xFFFFu) + (x >> 16);
+  return x;
+}
+NFDP_HD uint32_t csum_update16(uint32_t csum, uint32_t old16, uint32_t new16) {
+  // HC' = ~(~HC + ~m + m')
+  uint32_t x = (~csum & 0xFFFFu) + (~old16 & 0xFFFFu) + (new16 & 0xFFFFu);
+  return ~csum_fold(x) & 0xFFFFu;
+}
+NFDP_HD uint32_t csum_update32(uint32_t csum, uint32_t old32, uint32_t new32) {
+  uint32_t x = (~csum & 0xFFFFu) + (~old32 & 0xFFFFu) + (~(old32 >> 16) & 0xFFFFu) +
+               (new32 & 0xFFFFu) + (new32 >> 16);
+  return ~csum_fold(x) & 0xFFFFu;
+}
+// full IPv4 header checksum over 20 bytes at offset 14 of the normalized view (raw domain)
+NFDP_HD uint32_t ipv4_csum_full(const uint32_t* s) {
+  uint32_t x = 0;
+  for (int b = 14; b < 34; b += 2)
+    if (b != 24) x += raw16_at(s, b);
+  return ~csum_fold(x) & 0xFFFFu;
+}
+
+// ----------------------------------------------------------------------------------------
+// Actions on the normalized view
+// ----------------------------------------------------------------------------------------
+NFDP_HD void act_snat(Parsed& p, uint32_t new_ip, uint32_t new_port) {
+  const uint32_t old_ip = raw32_at2(p.s, 26);
+  uint32_t ipc = raw16_at(p.s, 24);
+  ipc = csum_update32(ipc, old_ip, new_ip);
+  set_raw16(p.s, 24, ipc);
+  set_raw32_at2(p.s, 26, new_ip);
+  if (p.l4) {
+    const uint32_t proto = p.s[5] >> 24;
+    const int coff = proto == 6 ? 50 : 40;  // TCP csum at L4+16, UDP at L4+6
+    const uint32_t old_port = raw16_at(p.s, 34);
+    if (coff + 2 <= (int)p.len) {
+      uint32_t c = raw16_at(p.s, coff);
+      if (proto == 6 || c != 0) {           // UDP csum 0 = disabled
+        c = csum_update32(c, old_ip, new_ip);
+        c = csum_update16(c, old_port, new_port);
+        if (proto == 17 && c == 0) c = 0xFFFFu;
+        set_raw16(p.s, coff, c);
+      }
+    }
+    set_raw16(p.s, 34, new_port);
+  }
+}
+
+NFDP_HD bool act_ttl(Parsed& p) {  // returns false when the TTL expires
+  const uint32_t w = raw16_at(p.s, 22);  // raw: low byte = ttl, high byte = proto
+  const uint32_t ttl = w & 0xFFu;
+  if (ttl <= 1) return false;
+  const uint32_t nw = (w & 0xFF00u) | (ttl - 1);
+  set_raw16(p.s, 24, csum_update16(raw16_at(p.s, 24), w, nw));
+  set_raw16(p.s, 22, nw);
+  return true;
+}
+
+// Serialize the normalized view back to a slot, optionally inserting an 802.1Q tag.
+NFDP_HD void emit(const Parsed& p, uint32_t push_tci, bool push, uint32_t* out) {
+#pragma unroll
+  for (int i = 0; i < 3; ++i) out[i] = p.s[i];
+  const uint32_t tagw = 0x0081u | (((push_tci >> 8) & 0xFFu) << 16) | ((push_tci & 0xFFu) << 24);
+  out[3] = push ? tagw : p.s[3];
+#pragma unroll
+  for (int i = 4; i < kSlotDwords; ++i) out[i] = push ? p.s[i - 1] : p.s[i];
+}
+
+NFDP_HD uint32_t make_meta(uint32_t out_port, uint32_t len, uint32_t reason) {
+  return (out_port & 0xFFFFu) | ((len & 0xFFu) << 16) | (reason << 24);
+}
+
+// ----------------------------------------------------------------------------------------
+// Pipeline parameters (kernarg / oracle argument).  Raw pointers into HBM (or host memory
+// for the oracle).  Everything is sized by the control plane; the kernels never allocate.
+// ----------------------------------------------------------------------------------------
+struct TablesView {
+  const PortEntry* ports;        // kMaxPorts
+  const ChainEntry* chains;      // n_chains
+  uint32_t n_chains;
+  const uint16_t* tags;          // nbuckets * 8
+  const FlowKey* keys;           // nbuckets * 8
+  const FlowAction* vals;        // nbuckets * 8
+  uint32_t bucket_mask;          // nbuckets - 1 (power of two)
+  const MacEntry* macs;          // n_mac (power of two)
+  uint32_t mac_mask;
+  const uint8_t* rss_key;        // 52 B
+  // ACL (TCAM): rules in priority order; value/mask over the 128-bit FlowKey.
+  const uint32_t* acl_value;     // n_acl * 4
+  const uint32_t* acl_mask;      // n_acl * 4
+  const uint8_t* acl_permit;     // n_acl (1 permit, 0 deny)
+  uint32_t n_acl;
+  uint32_t acl_default_permit;   // verdict when no rule matches
+};
+
+// Flow-table lookup (scalar).  Returns slot index or -1.
+NFDP_HD int64_t flow_lookup(const TablesView& t, const FlowKey& k, uint32_t h) {
+  const TableHash th = table_hash(h, t.bucket_mask);
+  uint32_t bk[2] = {th.b1, th.b2};
+  for (int c = 0; c < 2; ++c) {
+    const uint16_t* tg = t.tags + (size_t)bk[c] * kBucketSlots;
+    for (int s = 0; s < kBucketSlots; ++s) {
+      if (tg[s] != th.tag) continue;
+      const FlowKey& e = t.keys[(size_t)bk[c] * kBucketSlots + s];
+      if (e.src_ip == k.src_ip && e.dst_ip == k.dst_ip && e.ports == k.ports && e.meta == k.meta)
+        return (int64_t)bk[c] * kBucketSlots + s;
+    }
+  }
+  return -1;
+}
+
+NFDP_HD int mac_lookup(const TablesView& t, uint32_t bridge, uint32_t lo, uint32_t hi) {
+  if (!t.macs) return -1;
+  uint32_t h = fmix32(lo ^ (hi << 16) ^ (bridge * 0x9E3779B1u)) & t.mac_mask;
+  for (int probe = 0; probe < 16; ++probe) {
+    const MacEntry& e = t.macs[(h + probe) & t.mac_mask];
+    if (!e.valid) return -1;
+    if (e.mac_lo == lo && e.mac_hi == (hi & 0xFFFFu) && e.bridge_id == bridge) return e.out_port;
+  }
+  return -1;
+}
+
+// Scalar ACL (priority order, first match).  Returns rule index or -1.
+NFDP_HD int acl_first_match(const TablesView& t, const FlowKey& k) {
+  const uint32_t w[4] = {k.src_ip, k.dst_ip, k.ports, k.meta};
+  for (uint32_t r = 0; r < t.n_acl; ++r) {
+    bool m = true;
+    for (int i = 0; i < 4; ++i) m = m && ((w[i] ^ t.acl_value[4 * r + i]) & t.acl_mask[4 * r + i]) == 0;
+    if (m) return (int)r;
+  }
+  return -1;
+}
+
+}  // namespace nfdp

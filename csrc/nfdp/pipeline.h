@@ -1,0 +1,116 @@
+// pipeline.h — scalar per-packet stages shared by the GPU kernels and the CPU oracle.
+//
+// Stage order (one packet):
+//   ingress_stage : port lookup, VLAN isolation (K10), spoof-check, bridge-id (K7), FlowKey
+//   [hash + ACL   : done by the caller — MFMA on the GPU, scalar in the oracle]
+//   flow lookup   : exact match, 2-choice bucketized cuckoo (1M+ flows)
+//   chain_stage   : built-in NF hops (ACL verdict, SNAT, TTL, L2 steer, VLAN, hairpin) or the
+//                   (bridge, dst-MAC) L2 table on a flow miss (K5); egress port tagging (K6)
+#pragma once
+#include "nfdp.h"
+
+namespace nfdp {
+
+struct IngressState {
+  uint32_t in_port;
+  uint32_t bridge;
+  uint32_t reason;    // != 0: already dropped
+  uint32_t wire_len;  // ingress length (bytes counted on rx)
+  FlowKey key;
+};
+
+NFDP_HD void ingress_stage(const TablesView& t, const uint32_t* d, uint32_t inmeta, Parsed& p,
+                           IngressState& st) {
+  st.in_port = inmeta & 0xFFFFu;
+  uint32_t len = (inmeta >> 16) & 0xFFu;
+  st.wire_len = len;
+  st.reason = kOk;
+  if (len < 14 || len > kSlotBytes) { st.reason = kMalformed; len = len < 14 ? 14 : kSlotBytes; }
+  parse(d, len, p);
+  st.bridge = 0;
+  if (st.in_port >= (uint32_t)kMaxPorts) {
+    st.reason = kBadPort;
+  } else {
+    const PortEntry pe = t.ports[st.in_port];
+    if (!(pe.flags & kPortValid)) st.reason = st.reason ? st.reason : kBadPort;
+    const uint32_t vid = p.tci & 0xFFFu;
+    if ((pe.flags & kPortVlanIsolate) && p.tagged && vid != pe.vlan)
+      st.reason = st.reason ? st.reason : kVlanDrop;
+    if ((pe.flags & kPortSpoofChk) &&
+        (smac_lo(p.s) != pe.mac_lo || smac_hi(p.s) != pe.mac_hi))
+      st.reason = st.reason ? st.reason : kSpoof;
+    st.bridge = ((pe.flags & kPortVlanBridge) && p.tagged) ? vid : pe.bridge_id;
+  }
+  st.key = make_key(p, st.bridge);
+}
+
+struct EgressDecision {
+  uint32_t out_port;
+  uint32_t reason;
+  uint32_t push;      // 1 -> insert an 802.1Q tag with `tci`
+  uint32_t tci;
+};
+
+// `hit`: flow entry found; `act`: its action; `acl_rule`: first matching ACL rule or -1.
+NFDP_HD EgressDecision chain_stage(const TablesView& t, Parsed& p, const IngressState& st,
+                                   bool hit, const FlowAction& act, int acl_rule) {
+  EgressDecision e;
+  e.out_port = kPortNone; e.reason = st.reason; e.push = 0; e.tci = 0;
+  if (e.reason) return e;
+  bool vlan_done = false;
+  if (!hit) {
+    const int op = mac_lookup(t, st.bridge, dmac_lo(p.s), dmac_hi(p.s));
+    if (op < 0) { e.out_port = kPortPunt; e.reason = kNoRoute; return e; }
+    e.out_port = (uint32_t)op;
+  } else {
+    e.out_port = act.out_port;
+    ChainEntry ch;
+    ch.nhops = 0;
+    if (act.chain_id < t.n_chains) ch = t.chains[act.chain_id];
+    const int nh = ch.nhops < kMaxHops ? ch.nhops : kMaxHops;
+    for (int i = 0; i < nh; ++i) {
+      const uint8_t op = ch.hop[i];
+      if (op == kHopAcl) {
+        const bool permit = acl_rule >= 0 ? t.acl_permit[acl_rule] != 0 : t.acl_default_permit != 0;
+        if (!permit) { e.reason = kAclDeny; e.out_port = kPortNone; return e; }
+      } else if (op == kHopNat) {
+        if (p.ipv4) act_snat(p, act.nat_ip, act.nat_port);
+      } else if (op == kHopL2Fwd) {
+        e.out_port = act.out_port;
+        if (e.out_port < (uint32_t)kMaxPorts) {
+          const PortEntry& pe = t.ports[e.out_port];
+          set_dmac(p.s, pe.peer_mac_lo, pe.peer_mac_hi);
+          set_smac(p.s, pe.mac_lo, pe.mac_hi);
+        }
+      } else if (op == kHopTtl) {
+        if (p.ipv4 && !act_ttl(p)) { e.reason = kTtlExpired; e.out_port = kPortNone; return e; }
+      } else if (op == kHopHairpin) {
+        e.out_port = st.in_port;
+        const uint32_t dl = dmac_lo(p.s), dh = dmac_hi(p.s);
+        set_dmac(p.s, smac_lo(p.s), smac_hi(p.s));
+        set_smac(p.s, dl, dh);
+      } else if (op == kHopVlan) {
+        if (act.vlan == 0xFFFFu) { e.push = 0; vlan_done = true; }
+        else if (act.vlan) { e.push = 1; e.tci = act.vlan & 0xFFFu; vlan_done = true; }
+      } else if (op == kHopDrop) {
+        e.reason = kChainDrop; e.out_port = kPortNone; return e;
+      } else if (op == kHopPunt) {
+        e.reason = kNoRoute; e.out_port = kPortPunt; return e;
+      }
+    }
+  }
+  if (e.out_port >= (uint32_t)kMaxPorts) { e.reason = kBadPort; e.out_port = kPortNone; return e; }
+  const PortEntry& pe = t.ports[e.out_port];
+  if (!(pe.flags & kPortValid)) { e.reason = kBadPort; e.out_port = kPortNone; return e; }
+  if (!vlan_done && (pe.flags & kPortTagEgress) && pe.vlan) { e.push = 1; e.tci = pe.vlan & 0xFFFu; }
+  if (p.len + (e.push ? 4u : 0u) > (uint32_t)kSlotBytes) {
+    e.reason = kTooBig; e.out_port = kPortNone; return e;
+  }
+  return e;
+}
+
+// Counter record helpers: packed (pkts << 40) | bytes in one 64-bit word so a packet costs a
+// single atomic.  The control plane harvests (read + reset) well before 2^24 packets.
+NFDP_HD uint64_t ctr_inc(uint32_t bytes) { return (1ull << 40) | (uint64_t)bytes; }
+
+}  // namespace nfdp

@@ -1,0 +1,285 @@
+"""Single-device data-plane runtime.
+
+``DataPlane`` owns the host table models, mirrors them into device memory (HBM tensors on a
+GPU, numpy arrays for the CPU oracle) and runs packet batches through the fused HIP kernel
+(`fused_kernel<HASH, ACL>` in csrc/nfdp/kernels.hip) or the bit-exact C++ oracle.
+
+Table updates are applied between batches on the same HIP stream, so a batch always sees one
+consistent table version (the reference serialises the same updates through `p4rt-ctl` calls;
+here they are batched bucket-row writes).  Per-flow counters are packed (pkts << 40 | bytes)
+and harvested (read + reset) before any update batch that moves entries.
+"""
+from __future__ import annotations
+
+import os
+import time
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from ..native import nfdp as _nfdp_mod
+from . import tables as T
+
+HASH_MODES = {"scalar": 0, "lds": 1, "mfma": 2}
+ACL_MODES = {"scalar": 0, "mfma": 1, "off": 2}
+
+
+def _torch():
+    import torch
+
+    return torch
+
+
+def unpack_ctr(x: np.ndarray) -> tuple[np.ndarray, np.ndarray]:
+    x = np.asarray(x).astype(np.uint64)
+    return x >> np.uint64(40), x & np.uint64((1 << 40) - 1)
+
+
+@dataclass
+class BatchResult:
+    out: object          # [n,64] uint8 (torch or numpy)
+    meta: object         # [n] uint32 (torch int32 view or numpy)
+    n: int
+    extra: dict = field(default_factory=dict)
+
+
+class DataPlane:
+    def __init__(
+        self,
+        device: str = "cuda",
+        flow_buckets: int = 1 << 16,
+        mac_slots: int = 1 << 14,
+        chains: int = 4096,
+        hash_mode: str = "mfma",
+        acl_mode: str = "mfma",
+        num_cus: int | None = None,
+        rss_key: bytes = T.RSS_KEY,
+    ):
+        self.nf = _nfdp_mod()
+        self.device = device
+        self.gpu = device != "cpu"
+        self.ports = T.PortTable()
+        self.chains = T.ChainTable(chains)
+        self.macs = T.MacTable(mac_slots)
+        self.acl = T.AclTable()
+        self.flows = T.FlowTable(flow_buckets, rss_key)
+        self.rss_key = rss_key
+        self.hash_mode = HASH_MODES[hash_mode]
+        self.acl_mode = ACL_MODES[acl_mode]
+        self._dev: dict[str, object] = {}
+        self._versions: dict[str, int] = {}
+        self._acl_tiles = 1
+        self.flow_totals = np.zeros((self.flows.nbuckets * 8, 2), np.uint64)
+        if self.gpu:
+            torch = _torch()
+            if not torch.cuda.is_available():
+                raise RuntimeError("DataPlane(device='cuda') but no GPU is visible")
+            self.tdev = torch.device(device)
+            props = torch.cuda.get_device_properties(self.tdev)
+            self.num_cus = num_cus or props.multi_processor_count
+            arch = getattr(props, "gcnArchName", "")
+            if arch and not arch.startswith("gfx950"):
+                raise RuntimeError(f"this data plane is built for gfx950 only (device is {arch})")
+        else:
+            self.num_cus = num_cus or 256
+        self._alloc_counters()
+
+    # ------------------------------------------------------------------ buffers
+    def _buf(self, name: str, arr: np.ndarray):
+        """Upload/replace a host array as a device buffer (torch uint8 view on GPU)."""
+        arr = np.ascontiguousarray(arr)
+        if self.gpu:
+            torch = _torch()
+            t = torch.from_numpy(arr.view(np.uint8).reshape(-1).copy()).to(self.tdev, non_blocking=False)
+            self._dev[name] = t
+        else:
+            self._dev[name] = arr.copy()
+        return self._dev[name]
+
+    def _zeros(self, name: str, n: int, dtype=np.uint64):
+        if self.gpu:
+            torch = _torch()
+            tdt = {np.uint64: torch.int64, np.uint32: torch.int32, np.uint8: torch.uint8}[dtype]
+            self._dev[name] = torch.zeros(n, dtype=tdt, device=self.tdev)
+        else:
+            self._dev[name] = np.zeros(n, dtype)
+        return self._dev[name]
+
+    def _ptr(self, name: str) -> int:
+        b = self._dev.get(name)
+        if b is None:
+            return 0
+        return int(b.data_ptr()) if self.gpu else int(b.ctypes.data)
+
+    def _alloc_counters(self) -> None:
+        self._zeros("flow_ctr", self.flows.nbuckets * 8)
+        self._zeros("port_ctr", T.MAX_PORTS * 2)
+        self._zeros("drop_ctr", 16)
+        self._zeros("t0", 1)
+
+    # ------------------------------------------------------------------ commit
+    def commit(self, full: bool = False) -> dict:
+        """Push host table changes to the device.  Returns what was sent."""
+        sent = {}
+        for name, model in (("ports", self.ports), ("chains", self.chains), ("macs", self.macs)):
+            if full or self._versions.get(name) != model.version or name not in self._dev:
+                self._buf(name, model.a)
+                self._versions[name] = model.version
+                sent[name] = model.a.nbytes
+        if full or "rss_key" not in self._dev:
+            key = np.frombuffer(self.rss_key, np.uint8)
+            self._buf("rss_key", key)
+            self._buf("toep_frag", self.nf.build_toeplitz_frags(self.rss_key))
+            self._buf("toep_tab", self.nf.build_toeplitz_table(self.rss_key))
+        if full or self._versions.get("acl") != self.acl.version or "acl_value" not in self._dev:
+            val, msk, per, n = self.acl.arrays()
+            self._buf("acl_value", val)
+            self._buf("acl_mask", msk)
+            self._buf("acl_permit", per)
+            w, c, tiles = self.nf.build_acl_frags(val[: max(n, 1)] if n else np.zeros((0, 4), np.uint32),
+                                                  msk[: max(n, 1)] if n else np.zeros((0, 4), np.uint32))
+            self._buf("acl_wfrag", w)
+            self._buf("acl_cinit", c)
+            self._acl_tiles = int(tiles)
+            self._n_acl = n
+            self._versions["acl"] = self.acl.version
+            sent["acl"] = n
+        ft = self.flows.t
+        if full or "tags" not in self._dev:
+            self.harvest()
+            self._buf("tags", ft.tags())
+            self._buf("keys", ft.keys())
+            self._buf("vals", ft.vals())
+            ft.clear_dirty()
+            sent["flows_full"] = len(self.flows)
+        else:
+            dirty = ft.take_dirty()
+            moves = ft.take_moves()
+            if len(dirty):
+                if moves:
+                    self.harvest()  # counters of moved slots are attributed before the move
+                sent["flow_buckets"] = int(len(dirty))
+                self._push_buckets(dirty)
+        return sent
+
+    def _push_buckets(self, dirty: np.ndarray) -> None:
+        ft = self.flows.t
+        tags = ft.tags().reshape(-1, 8)[dirty]
+        keys = ft.keys().reshape(-1, 8, 4)[dirty]
+        vals = ft.vals().reshape(-1, 8, 4)[dirty]
+        if self.gpu:
+            torch = _torch()
+            up = {k: torch.from_numpy(np.ascontiguousarray(v).view(np.uint8).reshape(-1).copy()).to(self.tdev)
+                  for k, v in (("idx", dirty.astype(np.uint32)), ("tag", tags), ("key", keys), ("val", vals))}
+            s = torch.cuda.current_stream(self.tdev).cuda_stream
+            self.nf.launch_bucket_update(up["idx"].data_ptr(), len(dirty), up["tag"].data_ptr(), up["key"].data_ptr(),
+                                         up["val"].data_ptr(), self._ptr("tags"), self._ptr("keys"), self._ptr("vals"),
+                                         ft.mask, s)
+            self._keepalive = up
+        else:
+            self._dev["tags"].view(np.uint16).reshape(-1, 8)[dirty] = tags
+            self._dev["keys"].view(np.uint32).reshape(-1, 8, 4)[dirty] = keys
+            self._dev["vals"].view(np.uint32).reshape(-1, 8, 4)[dirty] = vals
+
+    def tables_ptrs(self) -> dict:
+        return {
+            "ports": self._ptr("ports"), "chains": self._ptr("chains"), "n_chains": int(self.chains.n),
+            "tags": self._ptr("tags"), "keys": self._ptr("keys"), "vals": self._ptr("vals"),
+            "bucket_mask": int(self.flows.t.mask), "macs": self._ptr("macs"), "mac_mask": int(self.macs.mask),
+            "rss_key": self._ptr("rss_key"), "acl_value": self._ptr("acl_value"), "acl_mask": self._ptr("acl_mask"),
+            "acl_permit": self._ptr("acl_permit"), "n_acl": int(getattr(self, "_n_acl", 0)),
+            "acl_default_permit": 1 if self.acl.default_permit else 0,
+        }
+
+    # ------------------------------------------------------------------ run
+    def alloc_batch(self, n: int):
+        """Output buffers for a batch of n packets."""
+        if self.gpu:
+            torch = _torch()
+            out = torch.empty((n, 64), dtype=torch.uint8, device=self.tdev)
+            meta = torch.empty(n, dtype=torch.int32, device=self.tdev)
+            lat = torch.zeros((n + 15) // 16, dtype=torch.int32, device=self.tdev)
+        else:
+            out = np.zeros((n, 64), np.uint8)
+            meta = np.zeros(n, np.uint32)
+            lat = None
+        return out, meta, lat
+
+    def run(self, pkts, inmeta, out=None, meta=None, lat=None, stamp: bool = True, stream=None) -> BatchResult:
+        """Process one batch.  GPU: pkts/inmeta torch tensors on the device ([n,64] uint8 / [n]
+        int32); CPU: numpy arrays (runs the C++ oracle)."""
+        n = int(pkts.shape[0])
+        if out is None:
+            out, meta, lat = self.alloc_batch(n)
+        tp = self.tables_ptrs()
+        if self.gpu:
+            torch = _torch()
+            if pkts.device != self.tdev or inmeta.device != self.tdev:
+                raise ValueError("batch must live on the data-plane device")
+            if pkts.dtype != torch.uint8 or pkts.dim() != 2 or pkts.shape[1] != 64 or not pkts.is_contiguous():
+                raise ValueError("pkts must be contiguous [n,64] uint8")
+            if inmeta.numel() != n or out.shape[0] < n or meta.numel() < n:
+                raise ValueError("batch buffer size mismatch")
+            s = stream if stream is not None else torch.cuda.current_stream(self.tdev).cuda_stream
+            if stamp:
+                self.nf.launch_stamp(self._ptr("t0"), s)
+            self.nf.launch_fused(
+                tp, pkts.data_ptr(), inmeta.data_ptr(), out.data_ptr(), meta.data_ptr(), n,
+                self._ptr("flow_ctr"), self._ptr("port_ctr"), self._ptr("drop_ctr"), self._ptr("t0"),
+                lat.data_ptr() if lat is not None else 0,
+                self._ptr("acl_wfrag"), self._ptr("acl_cinit"), self._acl_tiles,
+                self._ptr("toep_frag"), self._ptr("toep_tab"),
+                self.hash_mode, self.acl_mode, self.num_cus, s,
+            )
+            return BatchResult(out, meta, n, {"lat": lat})
+        pk = np.ascontiguousarray(pkts, np.uint8)
+        im = np.ascontiguousarray(inmeta, np.uint32)
+        hashes = np.zeros(n, np.uint32)
+        acl = np.zeros(n, np.int32)
+        self.nf.oracle_run(tp, pk.ctypes.data, im.ctypes.data, n, out.ctypes.data, meta.ctypes.data,
+                           self._ptr("flow_ctr"), self._ptr("port_ctr"), self._ptr("drop_ctr"),
+                           hashes.ctypes.data, acl.ctypes.data)
+        return BatchResult(out, meta, n, {"hash": hashes, "acl": acl})
+
+    # ------------------------------------------------------------------ counters
+    def harvest(self) -> None:
+        """Read-and-reset the packed per-flow counters into 64-bit host totals."""
+        if "flow_ctr" not in self._dev:
+            return
+        n = self.flows.nbuckets * 8
+        if self.gpu:
+            torch = _torch()
+            tmp = torch.empty(n, dtype=torch.int64, device=self.tdev)
+            s = torch.cuda.current_stream(self.tdev).cuda_stream
+            self.nf.launch_harvest(self._ptr("flow_ctr"), tmp.data_ptr(), n, s)
+            raw = tmp.cpu().numpy().view(np.uint64)
+        else:
+            raw = self._dev["flow_ctr"].copy()
+            self._dev["flow_ctr"][:] = 0
+        pk, by = unpack_ctr(raw)
+        self.flow_totals[:, 0] += pk
+        self.flow_totals[:, 1] += by
+
+    def flow_counters(self, key) -> tuple[int, int]:
+        self.harvest()
+        s = self.flows.find(key)
+        if s < 0:
+            return 0, 0
+        return int(self.flow_totals[s, 0]), int(self.flow_totals[s, 1])
+
+    def port_counters(self) -> np.ndarray:
+        """[MAX_PORTS, 4] = rx_pkts, rx_bytes, tx_pkts, tx_bytes."""
+        raw = self._dev["port_ctr"]
+        raw = raw.cpu().numpy().view(np.uint64) if self.gpu else raw
+        rx_p, rx_b = unpack_ctr(raw[0::2])
+        tx_p, tx_b = unpack_ctr(raw[1::2])
+        return np.stack([rx_p, rx_b, tx_p, tx_b], axis=1)
+
+    def drop_counters(self) -> dict:
+        raw = self._dev["drop_ctr"]
+        raw = raw.cpu().numpy().view(np.uint64) if self.gpu else raw
+        return {T.REASONS.get(i, str(i)): int(v) for i, v in enumerate(raw) if v}
+
+    def reset_counters(self) -> None:
+        self._alloc_counters()
+        self.flow_totals[:] = 0

@@ -1,0 +1,325 @@
+"""Host-side models of the data-plane tables (numpy, byte-identical to csrc/nfdp/nfdp.h).
+
+Tables (what they replace in the reference):
+
+* ``PortTable``  — vports (VF / NF / wire / representor).  Replaces SR-IOV VF config
+  (vlan / spoofchk / trust, ``dpu-cni/pkgs/sriov/sriov.go:200-282``) and the P4
+  ``tx_source_port`` / ``source_port_to_pr_map`` tables (``p4rtclient.go:674-718``).
+* ``ChainTable`` — service-function chains of built-in GPU NFs (``api/v1/servicefunctionchain_types.go``).
+* ``MacTable``   — (bridge, dst MAC) -> port, the ``l2_fwd_*`` tables (``p4info.txt:600-692``) and
+  OvS dl_dst steering (``ovsdp.go:125-131``).
+* ``AclTable``   — priority/ternary rules over the 128-bit FlowKey (TCAM; MFMA-evaluated).
+* ``FlowTable``  — 1M+ exact-match 5-tuple flows (native cuckoo, ``_nfdp.FlowTable``).
+"""
+from __future__ import annotations
+
+import ipaddress
+from dataclasses import dataclass
+
+import numpy as np
+
+from ..native import nfdp as _nfdp_mod
+from ..ops.packets import ip_raw, mac_raw, port_raw
+
+MAX_PORTS = 4096
+PORT_NONE = 0xFFFF
+PORT_PUNT = 0xFFFE
+
+# port flags (nfdp.h PortFlags)
+PORT_VALID = 1 << 0
+PORT_SPOOFCHK = 1 << 1
+PORT_VLAN_ISOLATE = 1 << 2
+PORT_TAG_EGRESS = 1 << 3
+PORT_VLAN_BRIDGE = 1 << 4
+PORT_TRUST = 1 << 5
+
+# hop opcodes (nfdp.h Hop)
+HOP_NONE, HOP_ACL, HOP_NAT, HOP_L2FWD, HOP_TTL, HOP_HAIRPIN, HOP_VLAN, HOP_DROP, HOP_PUNT = range(9)
+HOP_NAMES = {
+    "acl": HOP_ACL, "nat": HOP_NAT, "l2fwd": HOP_L2FWD, "ttl": HOP_TTL, "hairpin": HOP_HAIRPIN,
+    "vlan": HOP_VLAN, "drop": HOP_DROP, "punt": HOP_PUNT,
+}
+
+# reasons (nfdp.h Reason)
+REASONS = {
+    0: "ok", 1: "bad_port", 2: "vlan_drop", 3: "spoof", 4: "acl_deny", 5: "no_route",
+    6: "too_big", 7: "chain_drop", 8: "ttl_expired", 9: "malformed",
+}
+
+PORT_DTYPE = np.dtype(
+    [
+        ("flags", "<u4"), ("vlan", "<u2"), ("bridge_id", "<u2"),
+        ("mac_lo", "<u4"), ("mac_hi", "<u2"), ("gpu", "<u2"),
+        ("peer_mac_lo", "<u4"), ("peer_mac_hi", "<u2"), ("pad0", "<u2"),
+        ("pad1", "<u4"), ("pad2", "<u4"),
+    ]
+)
+CHAIN_DTYPE = np.dtype([("nhops", "u1"), ("hop", "u1", (7,)), ("acl_id", "<u2"), ("flags", "<u2"), ("pad", "<u4")])
+MAC_DTYPE = np.dtype(
+    [("mac_lo", "<u4"), ("mac_hi", "<u2"), ("bridge_id", "<u2"), ("out_port", "<u2"), ("valid", "<u2"), ("pad", "<u4")]
+)
+assert PORT_DTYPE.itemsize == 32 and CHAIN_DTYPE.itemsize == 16 and MAC_DTYPE.itemsize == 16
+
+# Microsoft RSS verification key (40 B) — standard Toeplitz key.
+RSS_KEY = bytes(
+    [
+        0x6D, 0x5A, 0x56, 0xDA, 0x25, 0x5B, 0x0E, 0xC2, 0x41, 0x67, 0x25, 0x3D, 0x43, 0xA3, 0x8F, 0xB0,
+        0xD0, 0xCA, 0x2B, 0xCB, 0xAE, 0x7B, 0x30, 0xB4, 0x77, 0xCB, 0x2D, 0xA3, 0x80, 0x30, 0xF2, 0x0C,
+        0x6A, 0x42, 0xB7, 0x3B, 0xBE, 0xAC, 0x01, 0xFA,
+    ]
+)
+
+
+def fmix32(h):
+    h = np.asarray(h, dtype=np.uint32).copy()
+    with np.errstate(over="ignore"):
+        h ^= h >> np.uint32(16)
+        h *= np.uint32(0x85EBCA6B)
+        h ^= h >> np.uint32(13)
+        h *= np.uint32(0xC2B2AE35)
+        h ^= h >> np.uint32(16)
+    return h
+
+
+def ip_to_int(ip) -> int:
+    if isinstance(ip, (int, np.integer)):
+        return int(ip)
+    return int(ipaddress.IPv4Address(ip))
+
+
+def flow_key(src_ip, dst_ip, sport=0, dport=0, proto=17, zone=0) -> np.ndarray:
+    """Vectorized FlowKey construction (host-order ints in) -> uint32[n,4] raw words."""
+    src = ip_raw(np.asarray(src_ip, np.uint32))
+    dst = ip_raw(np.asarray(dst_ip, np.uint32))
+    ports = port_raw(sport) | (port_raw(dport) << np.uint32(16))
+    meta = (np.asarray(proto, np.uint32) & 0xFF) | ((np.asarray(zone, np.uint32) & 0xFFFF) << np.uint32(16))
+    n = max(np.size(src), np.size(dst), np.size(ports), np.size(meta))
+    k = np.zeros((n, 4), np.uint32)
+    k[:, 0], k[:, 1], k[:, 2], k[:, 3] = src, dst, ports, meta
+    return k
+
+
+def flow_action(chain_id=0, out_port=0, nat_ip=0, nat_port=0, vlan=0, flow_id=0) -> np.ndarray:
+    """Vectorized FlowAction -> uint32[n,4] (nat ip/port host order in)."""
+    w0 = (np.asarray(chain_id, np.uint32) & 0xFFFF) | ((np.asarray(out_port, np.uint32) & 0xFFFF) << np.uint32(16))
+    w1 = ip_raw(np.asarray(nat_ip, np.uint32))
+    w2 = port_raw(nat_port) | ((np.asarray(vlan, np.uint32) & 0xFFFF) << np.uint32(16))
+    w3 = np.asarray(flow_id, np.uint32)
+    n = max(np.size(w0), np.size(w1), np.size(w2), np.size(w3))
+    a = np.zeros((n, 4), np.uint32)
+    a[:, 0], a[:, 1], a[:, 2], a[:, 3] = w0, w1, w2, w3
+    return a
+
+
+class PortTable:
+    def __init__(self):
+        self.a = np.zeros(MAX_PORTS, PORT_DTYPE)
+        self.version = 0
+
+    def set(self, idx: int, *, flags=PORT_VALID, vlan=0, bridge_id=0, mac="00:00:00:00:00:00",
+            peer_mac="00:00:00:00:00:00", gpu=0) -> None:
+        if not 0 <= idx < MAX_PORTS:
+            raise ValueError(f"port index {idx} out of range")
+        lo, hi = mac_raw(mac)
+        plo, phi = mac_raw(peer_mac)
+        self.a[idx] = (flags | PORT_VALID, vlan, bridge_id, lo, hi, gpu, plo, phi, 0, 0, 0)
+        self.version += 1
+
+    def clear(self, idx: int) -> None:
+        self.a[idx] = np.zeros((), PORT_DTYPE)
+        self.version += 1
+
+    def valid(self, idx: int) -> bool:
+        return bool(self.a[idx]["flags"] & PORT_VALID)
+
+
+class ChainTable:
+    def __init__(self, capacity: int = 4096):
+        self.a = np.zeros(capacity, CHAIN_DTYPE)
+        self.n = 1  # chain 0 = empty chain (plain forward to flow.out_port)
+        self.version = 0
+
+    def add(self, hops, acl_id: int = 0) -> int:
+        if self.n >= len(self.a):
+            raise RuntimeError("chain table full")
+        cid = self.n
+        self.set(cid, hops, acl_id)
+        self.n += 1
+        return cid
+
+    def set(self, cid: int, hops, acl_id: int = 0) -> None:
+        codes = [HOP_NAMES[h] if isinstance(h, str) else int(h) for h in hops]
+        if len(codes) > 7:
+            raise ValueError("at most 7 hops per chain")
+        hop = np.zeros(7, np.uint8)
+        hop[: len(codes)] = codes
+        self.a[cid]["nhops"] = len(codes)
+        self.a[cid]["hop"] = hop
+        self.a[cid]["acl_id"] = acl_id
+        self.n = max(self.n, cid + 1)
+        self.version += 1
+
+
+class MacTable:
+    """(bridge, dst MAC) -> port; open addressing, hash identical to nfdp.h mac_lookup."""
+
+    def __init__(self, slots: int = 1 << 16):
+        if slots & (slots - 1):
+            raise ValueError("MAC table size must be a power of two")
+        self.a = np.zeros(slots, MAC_DTYPE)
+        self.mask = slots - 1
+        self.version = 0
+
+    def _h(self, bridge, lo, hi) -> int:
+        with np.errstate(over="ignore"):
+            x = np.uint32(lo) ^ (np.uint32(hi) << np.uint32(16)) ^ (np.uint32(bridge) * np.uint32(0x9E3779B1))
+        return int(fmix32(x)) & self.mask
+
+    def insert(self, bridge: int, mac, out_port: int) -> None:
+        lo, hi = mac_raw(mac)
+        h = self._h(bridge, lo, hi)
+        for p in range(16):
+            e = self.a[(h + p) & self.mask]
+            if not e["valid"] or (e["mac_lo"] == lo and e["mac_hi"] == hi and e["bridge_id"] == bridge):
+                self.a[(h + p) & self.mask] = (lo, hi, bridge, out_port, 1, 0)
+                self.version += 1
+                return
+        raise RuntimeError("MAC table probe limit reached")
+
+    def lookup(self, bridge: int, mac) -> int:
+        lo, hi = mac_raw(mac)
+        h = self._h(bridge, lo, hi)
+        for p in range(16):
+            e = self.a[(h + p) & self.mask]
+            if not e["valid"]:
+                return -1
+            if e["mac_lo"] == lo and e["mac_hi"] == hi and e["bridge_id"] == bridge:
+                return int(e["out_port"])
+        return -1
+
+    def remove(self, bridge: int, mac) -> bool:
+        # rebuild the cluster to keep linear probing correct
+        entries = [(int(e["bridge_id"]), int(e["mac_lo"]), int(e["mac_hi"]), int(e["out_port"]))
+                   for e in self.a if e["valid"]]
+        lo, hi = mac_raw(mac)
+        keep = [e for e in entries if not (e[0] == bridge and e[1] == lo and e[2] == hi)]
+        if len(keep) == len(entries):
+            return False
+        self.a[:] = np.zeros((), MAC_DTYPE)
+        for b, l, h, p in keep:
+            mac_b = bytes([l & 0xFF, (l >> 8) & 0xFF, (l >> 16) & 0xFF, (l >> 24) & 0xFF, h & 0xFF, (h >> 8) & 0xFF])
+            self.insert(b, mac_b, p)
+        return True
+
+
+@dataclass
+class AclRule:
+    value: np.ndarray  # uint32[4] over the FlowKey words
+    mask: np.ndarray
+    permit: bool
+
+
+def _prefix_mask(bits: int) -> int:
+    return 0 if bits == 0 else ((0xFFFFFFFF << (32 - bits)) & 0xFFFFFFFF)
+
+
+def range_to_prefixes(lo: int, hi: int, width: int = 16) -> list[tuple[int, int]]:
+    """[lo, hi] -> list of (value, mask) ternary prefixes (TCAM range expansion)."""
+    out = []
+    full = (1 << width) - 1
+    while lo <= hi:
+        size = lo & -lo if lo else 1 << width
+        while size > hi - lo + 1:
+            size >>= 1
+        out.append((lo, full & ~(size - 1)))
+        lo += size
+    return out
+
+
+class AclTable:
+    """Priority-ordered ternary rules (index = priority, first match wins), <= 1024 rules."""
+
+    MAX_RULES = 1024
+
+    def __init__(self, default_permit: bool = True):
+        self.rules: list[AclRule] = []
+        self.default_permit = default_permit
+        self.version = 0
+
+    def add_raw(self, value, mask, permit: bool) -> int:
+        if len(self.rules) >= self.MAX_RULES:
+            raise RuntimeError("ACL full (1024 rules = P4 table capacity)")
+        v = np.asarray(value, np.uint32) & np.asarray(mask, np.uint32)
+        self.rules.append(AclRule(v, np.asarray(mask, np.uint32), bool(permit)))
+        self.version += 1
+        return len(self.rules) - 1
+
+    def add(self, *, permit: bool, src=None, dst=None, sport=None, dport=None, proto=None, zone=None) -> list[int]:
+        """Add a rule from fields; CIDRs for src/dst, int or (lo, hi) ranges for ports.
+        Port ranges expand to several ternary entries (returned indices)."""
+        base_v = np.zeros(4, np.uint32)
+        base_m = np.zeros(4, np.uint32)
+        for word, cidr in ((0, src), (1, dst)):
+            if cidr is None:
+                continue
+            net = ipaddress.IPv4Network(cidr, strict=False)
+            base_v[word] = ip_raw(np.uint32(int(net.network_address)))
+            base_m[word] = ip_raw(np.uint32(_prefix_mask(net.prefixlen)))
+        if proto is not None:
+            base_v[3] |= np.uint32(proto & 0xFF)
+            base_m[3] |= np.uint32(0xFF)
+        if zone is not None:
+            base_v[3] |= np.uint32((zone & 0xFFFF) << 16)
+            base_m[3] |= np.uint32(0xFFFF0000)
+
+        def prefixes(p):
+            if p is None:
+                return [(0, 0)]
+            if isinstance(p, tuple):
+                return range_to_prefixes(p[0], p[1])
+            return [(int(p), 0xFFFF)]
+
+        idx = []
+        for sv, sm in prefixes(sport):
+            for dv, dm in prefixes(dport):
+                v, m = base_v.copy(), base_m.copy()
+                v[2] = port_raw(np.uint32(sv)) | (port_raw(np.uint32(dv)) << np.uint32(16))
+                m[2] = port_raw(np.uint32(sm)) | (port_raw(np.uint32(dm)) << np.uint32(16))
+                idx.append(self.add_raw(v, m, permit))
+        return idx
+
+    def arrays(self):
+        n = len(self.rules)
+        val = np.zeros((max(n, 1), 4), np.uint32)
+        msk = np.zeros((max(n, 1), 4), np.uint32)
+        per = np.zeros(max(n, 1), np.uint8)
+        for i, r in enumerate(self.rules):
+            val[i], msk[i], per[i] = r.value, r.mask, 1 if r.permit else 0
+        return val, msk, per, n
+
+
+class FlowTable:
+    """Thin wrapper over the native authoritative cuckoo table."""
+
+    def __init__(self, nbuckets: int, rss_key: bytes = RSS_KEY):
+        self.t = _nfdp_mod().FlowTable(nbuckets, rss_key)
+        self.rss_key = rss_key
+
+    def __len__(self) -> int:
+        return len(self.t)
+
+    @property
+    def nbuckets(self) -> int:
+        return self.t.nbuckets
+
+    def insert(self, key, action) -> int:
+        return self.t.insert(tuple(int(x) for x in key), tuple(int(x) for x in action))
+
+    def insert_many(self, keys: np.ndarray, actions: np.ndarray) -> np.ndarray:
+        return self.t.insert_many(np.ascontiguousarray(keys, np.uint32), np.ascontiguousarray(actions, np.uint32))
+
+    def erase(self, key) -> bool:
+        return self.t.erase(tuple(int(x) for x in key))
+
+    def find(self, key) -> int:
+        return self.t.find(tuple(int(x) for x in key))

@@ -1,0 +1,128 @@
+"""In-tree build of the native extensions (gfx950 only).
+
+Two modules, both built with the ROCm toolchain and placed next to this file so they travel with
+the repository snapshot to the GPU box:
+
+* ``_nfdp``  — HIP/CDNA4 data-plane kernels + host control structures (hipcc, ``-x hip``,
+  ``--offload-arch=gfx950``).
+* ``_agent`` — C++ host<->device control mailbox and control-plane agent (g++/hipcc host code).
+
+Incremental: an object is rebuilt when its source or any header in its directory is newer.
+Usage: ``python -m dpu_operator_amd.native.build [-v] [--force]``.
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import os
+import shutil
+import subprocess
+import sys
+import sysconfig
+from pathlib import Path
+
+HERE = Path(__file__).resolve().parent
+REPO = HERE.parent.parent
+CSRC = REPO / "csrc"
+BUILD = REPO / "build" / "native"
+ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
+HIPCC = str(ROCM / "bin" / "hipcc")
+ARCH = "gfx950"
+EXT = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+
+
+def _includes() -> list[str]:
+    import pybind11
+
+    return ["-I", pybind11.get_include(), "-I", sysconfig.get_paths()["include"]]
+
+
+MODULES = {
+    "_nfdp": {
+        "dir": CSRC / "nfdp",
+        "sources": ["kernels.hip", "host.cpp", "bindings.cpp"],
+        "hip": True,
+    },
+    "_agent": {
+        "dir": CSRC / "agent",
+        "sources": ["mbox.cpp", "ctrl_net.cpp", "agent.cpp", "bindings.cpp"],
+        "hip": False,
+    },
+}
+
+
+def _newest_header(d: Path) -> float:
+    ts = [p.stat().st_mtime for p in d.glob("*.h")]
+    return max(ts) if ts else 0.0
+
+
+def _compile(src: Path, obj: Path, hip: bool, verbose: bool) -> None:
+    obj.parent.mkdir(parents=True, exist_ok=True)
+    common = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function", *_includes(), "-I", str(src.parent)]
+    if hip:
+        cmd = [HIPCC, "-x", "hip", f"--offload-arch={ARCH}", "-munsafe-fp-atomics", *common, "-c", str(src), "-o", str(obj)]
+    else:
+        cxx = shutil.which("g++") or "g++"
+        cmd = [cxx, *common, "-pthread", "-c", str(src), "-o", str(obj)]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"compile failed: {src}\n{r.stdout}\n{r.stderr}")
+    if verbose and r.stderr.strip():
+        print(r.stderr, file=sys.stderr)
+
+
+def build_module(name: str, force: bool = False, verbose: bool = False) -> Path:
+    spec = MODULES[name]
+    d: Path = spec["dir"]
+    out = HERE / f"{name}{EXT}"
+    hdr = _newest_header(d)
+    objs = []
+    jobs = []
+    for s in spec["sources"]:
+        src = d / s
+        obj = BUILD / name / (s + ".o")
+        objs.append(obj)
+        stale = force or not obj.exists() or obj.stat().st_mtime < max(src.stat().st_mtime, hdr)
+        if stale:
+            jobs.append((src, obj))
+    if jobs:
+        with cf.ThreadPoolExecutor(max_workers=min(len(jobs), 4)) as ex:
+            list(ex.map(lambda j: _compile(j[0], j[1], spec["hip"], verbose), jobs))
+    newest_obj = max(o.stat().st_mtime for o in objs)
+    if force or jobs or not out.exists() or out.stat().st_mtime < newest_obj:
+        if spec["hip"]:
+            cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", str(out)]
+        else:
+            cmd = [shutil.which("g++") or "g++", "-shared", "-fPIC", "-pthread", *map(str, objs), "-o", str(out)]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed: {name}\n{r.stdout}\n{r.stderr}")
+    return out
+
+
+def build_all(force: bool = False, verbose: bool = False) -> list[Path]:
+    outs = []
+    for name, spec in MODULES.items():
+        if not (spec["dir"]).exists():
+            continue
+        if not all((spec["dir"] / s).exists() for s in spec["sources"]):
+            continue
+        outs.append(build_module(name, force=force, verbose=verbose))
+    return outs
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("-v", "--verbose", action="store_true")
+    ap.add_argument("--force", action="store_true")
+    a = ap.parse_args()
+    for p in build_all(force=a.force, verbose=a.verbose):
+        print(p)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,232 @@
+"""Vectorized synthetic packet crafting / checking (numpy), 64-byte slots.
+
+Used by tests, the benchmark and the traffic generator.  Frames are written into fixed 64-B
+slots (the data-plane slot size, ``_nfdp.SLOT_BYTES``); a "64-byte packet" on the wire is a
+60-byte frame plus 4-byte FCS, so an untagged 64-B packet occupies 60 B of its slot and a
+VLAN-tagged one the full 64 B.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+SLOT = 64
+ETH_IPV4 = 0x0800
+ETH_VLAN = 0x8100
+
+
+def mac_bytes(mac) -> np.ndarray:
+    """'aa:bb:..' | int | bytes -> uint8[6]."""
+    if isinstance(mac, str):
+        return np.array([int(x, 16) for x in mac.split(":")], dtype=np.uint8)
+    if isinstance(mac, (bytes, bytearray)):
+        return np.frombuffer(bytes(mac), dtype=np.uint8).copy()
+    if isinstance(mac, (int, np.integer)):
+        return np.array([(int(mac) >> (8 * (5 - i))) & 0xFF for i in range(6)], dtype=np.uint8)
+    return np.asarray(mac, dtype=np.uint8)
+
+
+def mac_raw(mac) -> tuple[int, int]:
+    """MAC -> (lo32, hi16) as the kernels hold it (little-endian load of the network bytes)."""
+    b = mac_bytes(mac)
+    return int(b[0]) | int(b[1]) << 8 | int(b[2]) << 16 | int(b[3]) << 24, int(b[4]) | int(b[5]) << 8
+
+
+def mac_str(b) -> str:
+    return ":".join(f"{int(x):02x}" for x in mac_bytes(b))
+
+
+def ip_raw(ip_host_order) -> np.ndarray:
+    """IPv4 as host-order int (e.g. 0x0A000001 = 10.0.0.1) -> raw LE-loaded network bytes."""
+    x = np.asarray(ip_host_order, dtype=np.uint32)
+    return ((x >> 24) & 0xFF) | ((x >> 8) & 0xFF00) | ((x << 8) & 0xFF0000) | ((x << 24) & 0xFF000000)
+
+
+def port_raw(p) -> np.ndarray:
+    p = np.asarray(p, dtype=np.uint32)
+    return ((p >> 8) & 0xFF) | ((p & 0xFF) << 8)
+
+
+def _put16(buf: np.ndarray, off, val) -> None:
+    val = np.asarray(val, dtype=np.uint32)
+    buf[:, off] = (val >> 8) & 0xFF
+    buf[:, off + 1] = val & 0xFF
+
+
+def _put32(buf: np.ndarray, off, val) -> None:
+    val = np.asarray(val, dtype=np.uint32)
+    for i in range(4):
+        buf[:, off + i] = (val >> (8 * (3 - i))) & 0xFF
+
+
+def _csum16(words: np.ndarray) -> np.ndarray:
+    """One's complement of the one's-complement sum over axis 1 of big-endian 16-bit words."""
+    s = words.astype(np.uint64).sum(axis=1)
+    while True:
+        hi = s >> 16
+        if not np.any(hi):
+            break
+        s = (s & 0xFFFF) + hi
+    return (~s.astype(np.uint32)) & 0xFFFF
+
+
+def _be16_words(buf: np.ndarray, start: int, end: int) -> np.ndarray:
+    seg = buf[:, start:end].astype(np.uint32)
+    if (end - start) % 2:
+        seg = np.concatenate([seg, np.zeros((seg.shape[0], 1), np.uint32)], axis=1)
+    return (seg[:, 0::2] << 8) | seg[:, 1::2]
+
+
+def craft(
+    n: int,
+    *,
+    dmac,
+    smac,
+    src_ip,
+    dst_ip,
+    sport,
+    dport,
+    proto: int = 17,
+    ttl: int = 64,
+    vlan=None,
+    frame_len: int = 60,
+    payload_seed: int = 0,
+) -> tuple[np.ndarray, np.ndarray]:
+    """Craft n IPv4 UDP/TCP frames into 64-B slots.
+
+    Per-packet arrays (length n) or scalars for every field.  ``dmac``/``smac`` are [n,6] or [6]
+    uint8.  ``vlan``: None (untagged) or per-packet VID array (-1 = untagged).  ``frame_len`` is
+    the untagged L2 length (<= 60 so a tag still fits the slot).  Returns (slots uint8[n,64],
+    lens uint32[n]) with valid IPv4 and L4 checksums.
+    """
+    if frame_len < 42 or frame_len > 60:
+        raise ValueError("frame_len must be in [42, 60] (untagged, without FCS)")
+    l3 = np.zeros((n, frame_len), np.uint8)
+    dm = np.broadcast_to(mac_bytes(dmac) if np.ndim(dmac) <= 1 else np.asarray(dmac, np.uint8), (n, 6))
+    sm = np.broadcast_to(mac_bytes(smac) if np.ndim(smac) <= 1 else np.asarray(smac, np.uint8), (n, 6))
+    l3[:, 0:6] = dm
+    l3[:, 6:12] = sm
+    _put16(l3, 12, np.full(n, ETH_IPV4))
+    l3[:, 14] = 0x45
+    tot = frame_len - 14
+    _put16(l3, 16, np.full(n, tot))
+    _put16(l3, 18, np.arange(n, dtype=np.uint32) & 0xFFFF)
+    _put16(l3, 20, np.full(n, 0x4000))
+    l3[:, 22] = ttl
+    l3[:, 23] = proto
+    _put32(l3, 26, np.broadcast_to(np.asarray(src_ip, np.uint32), (n,)))
+    _put32(l3, 30, np.broadcast_to(np.asarray(dst_ip, np.uint32), (n,)))
+    _put16(l3, 34, np.broadcast_to(np.asarray(sport, np.uint32), (n,)))
+    _put16(l3, 36, np.broadcast_to(np.asarray(dport, np.uint32), (n,)))
+    rng = np.random.default_rng(payload_seed)
+    if proto == 17:
+        _put16(l3, 38, np.full(n, tot - 20))
+        l3[:, 42:] = rng.integers(0, 256, (n, frame_len - 42), dtype=np.uint8)
+    elif proto == 6:
+        if frame_len < 54:
+            raise ValueError("TCP needs frame_len >= 54")
+        _put32(l3, 38, rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32))
+        l3[:, 46] = 0x50
+        l3[:, 47] = 0x18
+        _put16(l3, 48, np.full(n, 8192))
+        l3[:, 54:] = rng.integers(0, 256, (n, frame_len - 54), dtype=np.uint8)
+    else:
+        l3[:, 34:] = rng.integers(0, 256, (n, frame_len - 34), dtype=np.uint8)
+    # IPv4 header checksum
+    _put16(l3, 24, _csum16(_be16_words(l3, 14, 34)))
+    if proto in (6, 17):
+        set_l4_csum(l3, proto)
+    slots = np.zeros((n, SLOT), np.uint8)
+    lens = np.full(n, frame_len, np.uint32)
+    if vlan is None:
+        slots[:, :frame_len] = l3
+    else:
+        vid = np.broadcast_to(np.asarray(vlan, np.int64), (n,))
+        tagged = vid >= 0
+        slots[~tagged, :frame_len] = l3[~tagged]
+        t = np.where(tagged)[0]
+        if len(t):
+            slots[t, 0:12] = l3[t, 0:12]
+            slots[t, 12] = 0x81
+            slots[t, 13] = 0x00
+            slots[t, 14] = (vid[t] >> 8) & 0x0F
+            slots[t, 15] = vid[t] & 0xFF
+            slots[t, 16 : frame_len + 4] = l3[t, 12:frame_len]
+            lens[t] = frame_len + 4
+    return slots, lens
+
+
+def set_l4_csum(l3: np.ndarray, proto: int) -> None:
+    """(Re)compute the UDP/TCP checksum of untagged frames in place."""
+    tot = ((l3[:, 16].astype(np.uint32) << 8) | l3[:, 17]).astype(np.int64)
+    L = int(tot[0]) - 20
+    if not np.all(tot == tot[0]):
+        raise ValueError("set_l4_csum expects a uniform IP total length")
+    coff = 34 + (16 if proto == 6 else 6)
+    l3[:, coff] = 0
+    l3[:, coff + 1] = 0
+    pseudo = np.concatenate(
+        [
+            _be16_words(l3, 26, 34),
+            np.full((l3.shape[0], 1), proto, np.uint32),
+            np.full((l3.shape[0], 1), L, np.uint32),
+        ],
+        axis=1,
+    )
+    words = np.concatenate([pseudo, _be16_words(l3, 34, 34 + L)], axis=1)
+    c = _csum16(words)
+    if proto == 17:
+        c = np.where(c == 0, 0xFFFF, c)
+    _put16(l3, coff, c)
+
+
+def strip(slots: np.ndarray, lens: np.ndarray) -> tuple[np.ndarray, np.ndarray, np.ndarray]:
+    """Return (untagged frames [n,64], untagged lens, vid or -1)."""
+    et = (slots[:, 12].astype(np.uint32) << 8) | slots[:, 13]
+    tagged = et == ETH_VLAN
+    out = slots.copy()
+    vid = np.full(len(slots), -1, np.int64)
+    t = np.where(tagged)[0]
+    out[t, 12:60] = slots[t, 16:64]
+    out[t, 60:] = 0
+    vid[t] = ((slots[t, 14].astype(np.int64) & 0x0F) << 8) | slots[t, 15]
+    nl = lens.astype(np.int64) - np.where(tagged, 4, 0)
+    return out, nl, vid
+
+
+def check_csums(frames: np.ndarray, lens: np.ndarray) -> np.ndarray:
+    """Per-packet bool: IPv4 header + (UDP|TCP) checksum valid, for untagged frames."""
+    ok = _csum16(_be16_words(frames, 14, 34)) == 0
+    proto = frames[:, 23]
+    tot = (frames[:, 16].astype(np.int64) << 8) | frames[:, 17]
+    res = ok.copy()
+    for p in (6, 17):
+        idx = np.where(proto == p)[0]
+        for L in np.unique(tot[idx]):
+            sub = idx[tot[idx] == L]
+            l4 = int(L) - 20
+            pseudo = np.concatenate(
+                [
+                    _be16_words(frames[sub], 26, 34),
+                    np.full((len(sub), 1), p, np.uint32),
+                    np.full((len(sub), 1), l4, np.uint32),
+                ],
+                axis=1,
+            )
+            words = np.concatenate([pseudo, _be16_words(frames[sub], 34, 34 + l4)], axis=1)
+            if p == 17:
+                zero = (frames[sub, 40] == 0) & (frames[sub, 41] == 0)
+                res[sub] &= zero | (_csum16(words) == 0)
+            else:
+                res[sub] &= _csum16(words) == 0
+    return res
+
+
+def inmeta(in_port, lens) -> np.ndarray:
+    """Per-packet ingress metadata word: in_port | len << 16."""
+    return (np.asarray(in_port, np.uint32) & 0xFFFF) | (np.asarray(lens, np.uint32) << 16)
+
+
+def meta_fields(meta: np.ndarray) -> tuple[np.ndarray, np.ndarray, np.ndarray]:
+    """Egress metadata -> (out_port, len, reason)."""
+    m = np.asarray(meta, np.uint32)
+    return m & 0xFFFF, (m >> 16) & 0xFF, m >> 24
