@@ -1,0 +1,204 @@
+#!/usr/bin/env python3
+"""Headline benchmark: Mpps (+ p50 pod-to-pod latency) of a 1M-flow service-function chain.
+
+Metric / config from BASELINE.json: "Mpps + p50 pod-to-pod µs latency, 1M-flow SFC at 1/2/4/8
+MI355X".  One step = one batch of B 64-byte packets PER GPU (weak scaling) pushed through the
+whole chain:
+
+    pod VF ingress (VLAN-isolated, spoof-checked)  ->  ACL (TCAM, 256 ternary rules, MFMA)  ->
+    SNAT (per-flow state, 1M-flow exact-match table)  ->  L2 steer + egress VLAN tag  ->  pod VF
+
+N = 1: one fused HIP kernel.  N > 1 (one process per GPU, torchrun): the flow table is sharded
+across the GPUs; each step does ingress/classify -> all-to-all(16-B descriptors) -> owner lookup
+-> all-to-all(16-B verdicts) -> apply chain -> all-to-all(64-B packets to the destination pod's
+GPU) -> egress, all on RCCL over xGMI.  Traffic is random pod->pod over 8 pods per GPU, so
+(N-1)/N of the packets cross GPUs.
+
+Data: synthetic (random-init 1M-flow table, random 5-tuples); inputs rotate over 4 pre-generated
+batches so no step re-reads a cached one.  Latency: per-packet time from the batch release stamp
+(s_memrealtime at the start of the step) to the packet's egress, sampled 1/16, p50 over the timed
+steps' last batch.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+BASELINE_METRIC = "Mpps + p50 pod-to-pod µs latency, 1M-flow SFC at 1/2/4/8 MI355X"
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=1 << 22, help="packets per GPU per step")
+    ap.add_argument("--flows", type=int, default=1 << 20)
+    ap.add_argument("--acl", type=int, default=256, help="ACL (TCAM) rules evaluated per packet")
+    ap.add_argument("--pods-per-gpu", type=int, default=8)
+    ap.add_argument("--hash", default="lds", choices=["lds", "mfma"])
+    ap.add_argument("--acl-mode", default="mfma", choices=["mfma", "scalar"])
+    ap.add_argument("--rotate", type=int, default=4)
+    ap.add_argument("--no-lowlat", action="store_true", help="skip the small-batch latency probe")
+    return ap.parse_args()
+
+
+def main() -> None:
+    a = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        if world == 1 and a.gpus > 1:
+            raise SystemExit("--gpus > 1 must be launched with torch.distributed.run (one process per GPU)")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from dpu_operator_amd.dataplane import scenario as S
+    from dpu_operator_amd.dataplane.engine import DataPlane
+    from dpu_operator_amd.ops import packets as P
+    from dpu_operator_amd.parallel.sharded import ShardedDataPlane, shard_filter
+
+    t_setup = time.time()
+    flows_here = a.flows / world
+    buckets = 1 << max(10, int(math.ceil(math.log2(flows_here / 4))))  # <= 50% load, 8 slots
+    dp = DataPlane(device=str(dev), flow_buckets=buckets, hash_mode=a.hash, acl_mode=a.acl_mode)
+    n_pods = a.pods_per_gpu * world
+    pod_gpu = np.arange(n_pods) // a.pods_per_gpu
+    sc = S.build_sfc(dp, n_pods=n_pods, n_flows=a.flows, n_acl=a.acl, seed=0, pod_gpu=pod_gpu,
+                     flow_filter=shard_filter(rank, world) if world > 1 else None)
+    dp.commit(full=True)
+    my_pods = np.where(pod_gpu == rank)[0]
+    batches = []
+    for r in range(a.rotate):
+        pk, im = S.traffic(sc, a.batch, seed=1000 * rank + r + 1, src_pods=my_pods)
+        batches.append((torch.from_numpy(pk).to(dev), torch.from_numpy(im.view(np.int32)).to(dev)))
+        del pk, im
+    if world == 1:
+        out, meta, lat = dp.alloc_batch(a.batch)
+
+        def step(k):
+            pk, im = batches[k % a.rotate]
+            dp.run(pk, im, out, meta, lat)
+
+        def results():
+            return meta.cpu().numpy().view(np.uint32), lat.cpu().numpy().view(np.uint32).astype(np.float64) * 0.01
+    else:
+        eng = ShardedDataPlane(dp, rank, world, a.batch)
+
+        def step(k):
+            pk, im = batches[k % a.rotate]
+            eng.step(pk, im)
+
+        def results():
+            return eng.out_meta.cpu().numpy().view(np.uint32), eng.latency_samples_us()
+
+    setup_s = time.time() - t_setup
+    for k in range(a.warmup):
+        step(k)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(a.steps):
+        step(a.warmup + k)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    meta_np, lat_us = results()
+    _, _, reasons = P.meta_fields(meta_np)
+    fwd_local = float(np.mean((reasons == 0) | (reasons == 10)))
+    p50 = float(np.median(lat_us)) if len(lat_us) else float("nan")
+    p99 = float(np.percentile(lat_us, 99)) if len(lat_us) else float("nan")
+    if world > 1:
+        st = torch.tensor([p50, p99, fwd_local], dtype=torch.float64, device=dev)
+        g = [torch.zeros_like(st) for _ in range(world)]
+        dist.all_gather(g, st)
+        arr = torch.stack(g).cpu().numpy()
+        p50, p99, fwd_local = float(np.median(arr[:, 0])), float(np.max(arr[:, 1])), float(np.mean(arr[:, 2]))
+
+    # small-batch latency probe (outside the timed region): 64K packets per step, fused/sharded alike
+    p50_small = None
+    if not a.no_lowlat:
+        nsm = 1 << 16
+        pk, im = batches[0][0][:nsm].contiguous(), batches[0][1][:nsm].contiguous()
+        if world == 1:
+            o2, m2, l2 = dp.alloc_batch(nsm)
+            for _ in range(20):
+                dp.run(pk, im, o2, m2, l2)
+            torch.cuda.synchronize()
+            ls = l2.cpu().numpy().view(np.uint32).astype(np.float64) * 0.01
+        else:
+            eng_s = ShardedDataPlane(dp, rank, world, nsm)
+            for _ in range(20):
+                eng_s.step(pk, im)
+            torch.cuda.synchronize()
+            ls = eng_s.latency_samples_us()
+        p50_small = float(np.median(ls)) if len(ls) else None
+        if world > 1:
+            t = torch.tensor([p50_small or 0.0], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            p50_small = float(t.item())
+
+    total_pkts = world * a.batch * a.steps
+    mpps = total_pkts / elapsed / 1e6
+    if rank == 0:
+        line = {
+            "metric": BASELINE_METRIC,
+            "value": round(mpps, 2),
+            "unit": "Mpps",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(elapsed / a.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "uint8 packets / int8 MFMA classify",
+            "data": "synthetic (random 1M-flow table, random pod->pod 5-tuples, 64B frames)",
+            "config": {
+                "model": f"1M-flow SFC: acl({a.acl} TCAM rules)->snat->l2fwd, 64B frames, {a.pods_per_gpu} pods/GPU",
+                "global_batch": world * a.batch,
+                "seq_len": 64,
+                "parallelism": "fused-1gpu" if world == 1 else f"flow-shard x{world} + 3x all-to-all (RCCL/xGMI)",
+            },
+            "p50_latency_us": round(p50, 2),
+            "p99_latency_us": round(p99, 2),
+            "p50_latency_us_64k_batch": None if p50_small is None else round(p50_small, 2),
+            "forwarded_fraction": round(fwd_local, 6),
+            "flows": a.flows,
+            "batch_per_gpu": a.batch,
+            "hash": a.hash,
+            "acl_mode": a.acl_mode,
+            "setup_s": round(setup_s, 1),
+            "baseline_note": "reference publishes no numbers (BASELINE.md); 200GbE line rate at 64B = 297.6 Mpps",
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -7,6 +7,7 @@
 #include <pybind11/stl.h>
 
 #include "host.h"
+#include "shard.h"
 
 namespace py = pybind11;
 using namespace nfdp;
@@ -224,6 +225,74 @@ PYBIND11_MODULE(_nfdp, m) {
                                reinterpret_cast<void*>(vals), bucket_mask, reinterpret_cast<hipStream_t>(stream)),
           "bucket_update");
   });
+  // ---------------- sharded (multi-GPU) stages: device=True -> HIP kernels, False -> CPU twins
+  auto geom = [](const py::dict& d) {
+    ShardGeom g;
+    g.nranks = val<uint32_t>(d, "nranks", 1); g.rank = val<uint32_t>(d, "rank", 0);
+    g.cap_desc = val<uint32_t>(d, "cap_desc", 0); g.cap_pkt = val<uint32_t>(d, "cap_pkt", 0);
+    if (g.rank >= g.nranks || g.nranks > 127 || g.cap_desc >= (1u << 24)) throw std::invalid_argument("bad shard geometry");
+    return g;
+  };
+  m.def("desc_seg_bytes", [](uint32_t cap) { return desc_seg_bytes(cap); });
+  m.def("pkt_seg_bytes", [](uint32_t cap) { return pkt_seg_bytes(cap); });
+  m.def("pkt_meta_off", [](uint32_t cap) { return pkt_meta_off(cap); });
+  m.def("shard_ingress", [geom](py::dict tables, py::dict d, bool device, int hash_mode, int acl_mode, int num_cus,
+                                uintptr_t stream) {
+    IngressArgs a{};
+    a.t = tables_from(tables);
+    a.pkts = ptr<const uint4>(d, "pkts"); a.inmeta = ptr<const uint32_t>(d, "inmeta");
+    a.n = val<uint32_t>(d, "n", 0); a.g = geom(d);
+    a.send_desc = ptr<uint8_t>(d, "send_desc"); a.cnt = ptr<uint32_t>(d, "cnt");
+    a.ref = ptr<uint32_t>(d, "ref"); a.aux = ptr<uint32_t>(d, "aux");
+    a.acl_wfrag = ptr<const void>(d, "acl_wfrag"); a.acl_cinit = ptr<const void>(d, "acl_cinit");
+    a.acl_tiles = val<uint32_t>(d, "acl_tiles", 1);
+    a.toep_frag = ptr<const void>(d, "toep_frag"); a.toep_tab = ptr<const uint32_t>(d, "toep_tab");
+    if (!a.pkts || !a.inmeta || !a.send_desc || !a.cnt || !a.ref || !a.aux) throw std::invalid_argument("ingress: null buffer");
+    if (!device) { py::gil_scoped_release nogil; ingress_cpu(a); return; }
+    if (hash_mode == 2 && !a.toep_frag) throw std::invalid_argument("MFMA hash needs toeplitz frags");
+    if (!a.toep_tab) throw std::invalid_argument("ingress needs the toeplitz table");
+    if (acl_mode == 1 && (!a.acl_wfrag || !a.acl_cinit)) throw std::invalid_argument("MFMA ACL needs frags");
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    check(launch_ingress(a, hash_mode, acl_mode, num_cus, s), "shard_ingress");
+    check(launch_seg_headers(a.cnt, a.send_desc, a.g.nranks, desc_seg_bytes(a.g.cap_desc), a.g.cap_desc, s), "seg_headers");
+  });
+  m.def("shard_owner", [geom](py::dict tables, py::dict d, bool device, int num_cus, uintptr_t stream) {
+    OwnerArgs a{};
+    a.t = tables_from(tables); a.g = geom(d);
+    a.recv_desc = ptr<const uint8_t>(d, "recv_desc"); a.send_verdict = ptr<uint8_t>(d, "send_verdict");
+    a.flow_ctr = ptr<unsigned long long>(d, "flow_ctr"); a.toep_tab = ptr<const uint32_t>(d, "toep_tab");
+    if (!a.recv_desc || !a.send_verdict) throw std::invalid_argument("owner: null buffer");
+    if (!device) { py::gil_scoped_release nogil; owner_cpu(a); return; }
+    if (!a.toep_tab) throw std::invalid_argument("owner needs the toeplitz table");
+    check(launch_owner(a, num_cus, reinterpret_cast<hipStream_t>(stream)), "shard_owner");
+  });
+  m.def("shard_apply", [geom](py::dict tables, py::dict d, bool device, int num_cus, uintptr_t stream) {
+    ApplyArgs a{};
+    a.t = tables_from(tables); a.g = geom(d);
+    a.pkts = ptr<const uint4>(d, "pkts"); a.inmeta = ptr<const uint32_t>(d, "inmeta"); a.n = val<uint32_t>(d, "n", 0);
+    a.ref = ptr<const uint32_t>(d, "ref"); a.aux = ptr<const uint32_t>(d, "aux");
+    a.recv_verdict = ptr<const uint8_t>(d, "recv_verdict"); a.out = ptr<uint4>(d, "out");
+    a.out_meta = ptr<uint32_t>(d, "out_meta"); a.send_pkt = ptr<uint8_t>(d, "send_pkt"); a.pcnt = ptr<uint32_t>(d, "pcnt");
+    a.port_ctr = ptr<unsigned long long>(d, "port_ctr"); a.drop_ctr = ptr<unsigned long long>(d, "drop_ctr");
+    a.t0 = ptr<const unsigned long long>(d, "t0"); a.lat = ptr<uint32_t>(d, "lat");
+    if (!a.pkts || !a.inmeta || !a.ref || !a.aux || !a.recv_verdict || !a.out || !a.out_meta || !a.send_pkt || !a.pcnt ||
+        !a.port_ctr || !a.drop_ctr)
+      throw std::invalid_argument("apply: null buffer");
+    if (!device) { py::gil_scoped_release nogil; apply_cpu(a); return; }
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    check(launch_apply(a, num_cus, s), "shard_apply");
+    check(launch_seg_headers(a.pcnt, a.send_pkt, a.g.nranks, pkt_seg_bytes(a.g.cap_pkt), a.g.cap_pkt, s), "seg_headers");
+  });
+  m.def("shard_egress", [geom](py::dict d, bool device, int num_cus, uintptr_t stream) {
+    EgressArgs a{};
+    a.g = geom(d);
+    a.recv_pkt = ptr<const uint8_t>(d, "recv_pkt"); a.port_ctr = ptr<unsigned long long>(d, "port_ctr");
+    a.t0 = ptr<const unsigned long long>(d, "t0"); a.lat = ptr<uint32_t>(d, "lat");
+    if (!a.recv_pkt || !a.port_ctr) throw std::invalid_argument("egress: null buffer");
+    if (!device) { py::gil_scoped_release nogil; egress_cpu(a); return; }
+    check(launch_egress(a, num_cus, reinterpret_cast<hipStream_t>(stream)), "shard_egress");
+  });
+
   m.def("launch_harvest", [](uintptr_t ctr, uintptr_t out, uint32_t n, uintptr_t stream) {
     check(launch_harvest(reinterpret_cast<unsigned long long*>(ctr), reinterpret_cast<unsigned long long*>(out), n,
                          reinterpret_cast<hipStream_t>(stream)), "harvest");

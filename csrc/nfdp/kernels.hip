@@ -13,18 +13,9 @@
 //    compare and one 16-B action load (tables sized for HBM: 1M flows = 68 MB, 288 GB ok);
 //  * per-port counters aggregated in LDS, flushed once per workgroup; per-flow counters are one
 //    packed 64-bit atomic per packet.
-#include "host.h"
+#include "device.h"
 
 namespace nfdp {
-
-typedef int v4i __attribute__((ext_vector_type(4)));
-
-constexpr int kBlock = 512;
-constexpr int kWaves = kBlock / 64;
-constexpr int kLdsPorts = 256;
-
-enum HashMode { kHashScalar = 0, kHashLds = 1, kHashMfma = 2 };
-enum AclMode { kAclScalar = 0, kAclMfma = 1, kAclOff = 2 };
 
 struct FusedArgs {
   TablesView t;
@@ -44,134 +35,6 @@ struct FusedArgs {
   const uint32_t* toep_tab;       // [16][256] byte tables (LDS hash variant)
   uint32_t acl_tiles;             // ceil(n_acl / 16)
 };
-
-// 16 bits -> 16 bytes of {0,1}: byte j = bit j.  (nibble * 0x00204081) spreads 4 bits to 4
-// bytes without carries.
-__device__ __forceinline__ v4i expand16(uint32_t x) {
-  v4i r;
-  r[0] = (int)((((x) & 0xFu) * 0x00204081u) & 0x01010101u);
-  r[1] = (int)((((x >> 4) & 0xFu) * 0x00204081u) & 0x01010101u);
-  r[2] = (int)((((x >> 8) & 0xFu) * 0x00204081u) & 0x01010101u);
-  r[3] = (int)((((x >> 12) & 0xFu) * 0x00204081u) & 0x01010101u);
-  return r;
-}
-
-__device__ __forceinline__ uint32_t pick4(uint32_t g, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
-  return g == 0 ? a : g == 1 ? b : g == 2 ? c : d;
-}
-
-// Wave-level classification over the wave's 64 packets (one per lane).  EXEC must be full.
-template <int HASH, int ACL>
-__device__ __forceinline__ void classify_wave(const FlowKey& key, uint4* kx, const v4i* lw,
-                                              const v4i* lc, uint32_t acl_tiles, const v4i* lt,
-                                              const uint32_t* ltab, const TablesView& t,
-                                              uint32_t& hash, int& acl_rule) {
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t g = lane >> 4, col = lane & 15u;
-  v4i bf[4][2];
-  if constexpr (HASH == kHashMfma || ACL == kAclMfma) {
-    kx[lane] = make_uint4(key.src_ip, key.dst_ip, key.ports, key.meta);
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-#pragma unroll
-    for (int tt = 0; tt < 4; ++tt) {
-      const uint32_t* src = reinterpret_cast<const uint32_t*>(kx + 16 * tt + col);
-      const uint32_t wlo = src[g >> 1], whi = src[2 + (g >> 1)];
-      const uint32_t sh = 16u * (g & 1u);
-      bf[tt][0] = expand16((wlo >> sh) & 0xFFFFu);
-      bf[tt][1] = expand16((whi >> sh) & 0xFFFFu);
-    }
-  }
-  // ---- hash ----
-  if constexpr (HASH == kHashMfma) {
-    uint32_t hv[4] = {0, 0, 0, 0};
-#pragma unroll
-    for (int m = 0; m < 2; ++m) {
-      const v4i a0 = lt[(m * 2 + 0) * 64 + lane], a1 = lt[(m * 2 + 1) * 64 + lane];
-#pragma unroll
-      for (int tt = 0; tt < 4; ++tt) {
-        v4i acc = {0, 0, 0, 0};
-        acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a0, bf[tt][0], acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a1, bf[tt][1], acc, 0, 0, 0);
-        uint32_t bits = ((uint32_t)acc[0] & 1u) | (((uint32_t)acc[1] & 1u) << 1) |
-                        (((uint32_t)acc[2] & 1u) << 2) | (((uint32_t)acc[3] & 1u) << 3);
-        hv[tt] |= bits << (4u * g + 16u * m);
-      }
-    }
-#pragma unroll
-    for (int tt = 0; tt < 4; ++tt) {
-      hv[tt] |= __shfl_xor(hv[tt], 16);
-      hv[tt] |= __shfl_xor(hv[tt], 32);
-    }
-    hash = __builtin_bitreverse32(pick4(g, hv[0], hv[1], hv[2], hv[3]));
-  } else if constexpr (HASH == kHashLds) {
-    const uint32_t w[4] = {key.src_ip, key.dst_ip, key.ports, key.meta};
-    uint32_t h = 0;
-#pragma unroll
-    for (int b = 0; b < 16; ++b) h ^= ltab[b * 256 + ((w[b >> 2] >> (8 * (b & 3))) & 0xFFu)];
-    hash = h;
-  } else {
-    hash = toeplitz_scalar(key, t.rss_key);
-  }
-  // ---- ACL (TCAM) ----
-  if constexpr (ACL == kAclMfma) {
-    uint32_t best[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
-    for (uint32_t nt = 0; nt < acl_tiles; ++nt) {
-      const v4i a0 = lw[(nt * 2 + 0) * 64 + lane], a1 = lw[(nt * 2 + 1) * 64 + lane];
-      const v4i c = lc[nt * 4 + g];
-      const uint32_t rb = nt * 16u + 4u * g;
-#pragma unroll
-      for (int tt = 0; tt < 4; ++tt) {
-        v4i acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a0, bf[tt][0], c, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a1, bf[tt][1], acc, 0, 0, 0);
-        const uint32_t e0 = ((uint32_t)acc[0] << 10) | (rb + 0);
-        const uint32_t e1 = ((uint32_t)acc[1] << 10) | (rb + 1);
-        const uint32_t e2 = ((uint32_t)acc[2] << 10) | (rb + 2);
-        const uint32_t e3 = ((uint32_t)acc[3] << 10) | (rb + 3);
-        best[tt] = min(best[tt], min(min(e0, e1), min(e2, e3)));
-      }
-    }
-#pragma unroll
-    for (int tt = 0; tt < 4; ++tt) {
-      best[tt] = min(best[tt], (uint32_t)__shfl_xor(best[tt], 16));
-      best[tt] = min(best[tt], (uint32_t)__shfl_xor(best[tt], 32));
-    }
-    const uint32_t b = pick4(g, best[0], best[1], best[2], best[3]);
-    acl_rule = (b >> 10) == 0 ? (int)(b & 1023u) : -1;
-    if (acl_rule >= (int)t.n_acl) acl_rule = -1;
-  } else if constexpr (ACL == kAclScalar) {
-    acl_rule = acl_first_match(t, key);
-  } else {
-    acl_rule = -1;
-  }
-}
-
-// Vectorized 2-choice bucket probe: one 16-B tag row per bucket, 16-B key compare on a tag hit.
-__device__ __forceinline__ int64_t flow_lookup_vec(const TablesView& t, const FlowKey& k, uint32_t h) {
-  const TableHash th = table_hash(h, t.bucket_mask);
-  const uint4* tags = reinterpret_cast<const uint4*>(t.tags);
-  const uint4* keys = reinterpret_cast<const uint4*>(t.keys);
-#pragma unroll
-  for (int c = 0; c < 2; ++c) {
-    const uint32_t b = c ? th.b2 : th.b1;
-    const uint4 tg = tags[b];
-    const uint32_t tw[4] = {tg.x, tg.y, tg.z, tg.w};
-    uint32_t m = 0;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      m |= ((tw[s] & 0xFFFFu) == th.tag ? 1u : 0u) << (2 * s);
-      m |= ((tw[s] >> 16) == th.tag ? 1u : 0u) << (2 * s + 1);
-    }
-    while (m) {
-      const uint32_t s = __builtin_ctz(m);
-      m &= m - 1;
-      const uint4 e = keys[(size_t)b * kBucketSlots + s];
-      if (e.x == k.src_ip && e.y == k.dst_ip && e.z == k.ports && e.w == k.meta)
-        return (int64_t)b * kBucketSlots + s;
-    }
-  }
-  return -1;
-}
 
 __device__ __forceinline__ size_t lds_align16(size_t x) { return (x + 15) & ~(size_t)15; }
 

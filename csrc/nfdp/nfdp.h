@@ -45,6 +45,8 @@ enum Reason : uint32_t {
   kChainDrop = 7,
   kTtlExpired = 8,
   kMalformed = 9,
+  kRemote = 10,    // not a drop: handed to the egress GPU over xGMI (multi-GPU path)
+  kOverflow = 11,  // exchange segment full (multi-GPU path)
   kNumReasons = 16,
 };
 

@@ -75,6 +75,8 @@ class DataPlane:
             if not torch.cuda.is_available():
                 raise RuntimeError("DataPlane(device='cuda') but no GPU is visible")
             self.tdev = torch.device(device)
+            if self.tdev.index is None:
+                self.tdev = torch.device("cuda", torch.cuda.current_device())
             props = torch.cuda.get_device_properties(self.tdev)
             self.num_cus = num_cus or props.multi_processor_count
             arch = getattr(props, "gcnArchName", "")

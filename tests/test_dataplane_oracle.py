@@ -1,0 +1,246 @@
+"""CPU tests of the data-plane semantics (C++ oracle = the same per-packet code the kernels run).
+
+Independent references: the Microsoft RSS verification vector, full (non-incremental) checksum
+recomputation in numpy, and hand-built expectations per NF hop.
+"""
+import numpy as np
+import pytest
+
+from dpu_operator_amd.dataplane import scenario as S
+from dpu_operator_amd.dataplane import tables as T
+from dpu_operator_amd.dataplane.engine import DataPlane
+from dpu_operator_amd.ops import packets as P
+
+
+def test_toeplitz_ms_vector(nf):
+    # MS RSS verification suite: 66.9.149.187:2794 -> 161.142.100.80:1766  => 0x51ccc178 (IPv4+TCP)
+    k = T.flow_key(T.ip_to_int("66.9.149.187"), T.ip_to_int("161.142.100.80"), 2794, 1766, proto=0, zone=0)
+    assert int(nf.toeplitz(k, T.RSS_KEY)[0]) == 0x51CCC178
+    # 2-tuple (ports zero, proto zero) vector: 0x323e8fc2
+    k2 = T.flow_key(T.ip_to_int("66.9.149.187"), T.ip_to_int("161.142.100.80"), 0, 0, proto=0, zone=0)
+    assert int(nf.toeplitz(k2, T.RSS_KEY)[0]) == 0x323E8FC2
+
+
+def test_toeplitz_byte_table_matches_scalar(nf):
+    rng = np.random.default_rng(0)
+    keys = rng.integers(0, 2**32, (500, 4), dtype=np.uint64).astype(np.uint32)
+    keys[:, 3] &= np.uint32(0xFFFF00FF)
+    tab = nf.build_toeplitz_table(T.RSS_KEY).reshape(16, 256)
+    b = keys.view(np.uint8).reshape(-1, 16)
+    h = np.zeros(len(keys), np.uint32)
+    for pos in range(16):
+        h ^= tab[pos][b[:, pos]]
+    assert np.array_equal(h, nf.toeplitz(keys, T.RSS_KEY))
+
+
+def test_toeplitz_mfma_fragments_emulated(nf):
+    """Emulate the int8 MFMA GF(2) product on the host from the device fragments."""
+    fr = nf.build_toeplitz_frags(T.RSS_KEY).reshape(2, 2, 64, 16).astype(np.int64)
+    rng = np.random.default_rng(1)
+    keys = rng.integers(0, 2**32, (64, 4), dtype=np.uint64).astype(np.uint32)
+    bits = ((keys[:, :, None] >> np.arange(32, dtype=np.uint32)) & 1).reshape(64, 128).astype(np.int64)
+    # Matrix M[k][n] from fragment layout: lane l, byte j of (m, s) -> n = 16m + (l & 15), k = 64s + 16(l>>4) + j
+    M = np.zeros((128, 32), np.int64)
+    for m in range(2):
+        for s in range(2):
+            for l in range(64):
+                for j in range(16):
+                    M[64 * s + 16 * (l >> 4) + j, 16 * m + (l & 15)] = fr[m, s, l, j]
+    par = (bits @ M) & 1
+    hm = (par << np.arange(32)).sum(axis=1).astype(np.uint64)
+    h = np.array([int(f"{int(x):032b}"[::-1], 2) for x in hm], np.uint32)  # bit reverse
+    assert np.array_equal(h, nf.toeplitz(keys, T.RSS_KEY))
+
+
+def test_acl_fragments_emulated(nf):
+    """TCAM-as-GEMM: mismatch = bias + bits @ W must be 0 exactly on ternary matches."""
+    rng = np.random.default_rng(2)
+    n = 40
+    val = rng.integers(0, 2**32, (n, 4), dtype=np.uint64).astype(np.uint32)
+    msk = (rng.integers(0, 2**32, (n, 4), dtype=np.uint64) & rng.integers(0, 2**32, (n, 4), dtype=np.uint64)).astype(np.uint32)
+    w, c, tiles = nf.build_acl_frags(val, msk)
+    w = w.reshape(tiles, 2, 64, 16).astype(np.int64)
+    c = c.reshape(tiles, 4, 4)
+    W = np.zeros((128, tiles * 16), np.int64)
+    bias = np.zeros(tiles * 16, np.int64)
+    for nt in range(tiles):
+        for s in range(2):
+            for l in range(64):
+                for j in range(16):
+                    W[64 * s + 16 * (l >> 4) + j, nt * 16 + (l & 15)] = w[nt, s, l, j]
+        for g in range(4):
+            for r in range(4):
+                bias[nt * 16 + 4 * g + r] = c[nt, g, r]
+    keys = np.concatenate([val & msk, rng.integers(0, 2**32, (200, 4), dtype=np.uint64).astype(np.uint32)])
+    bits = ((keys[:, :, None] >> np.arange(32, dtype=np.uint32)) & 1).reshape(len(keys), 128).astype(np.int64)
+    mism = bits @ W + bias
+    assert (mism >= 0).all()
+    ref = np.all(((keys[:, None, :] ^ val[None]) & msk[None]) == 0, axis=2)
+    assert np.array_equal(mism[:, :n] == 0, ref)
+    assert (mism[:, n:] > 0).all()  # padding rules never match
+
+
+def test_flow_table_cuckoo_high_load(nf):
+    ft = T.FlowTable(1 << 10)  # 8192 slots
+    rng = np.random.default_rng(3)
+    n = 7000  # 85% load: forces evictions
+    keys = rng.integers(0, 2**32, (n, 4), dtype=np.uint64).astype(np.uint32)
+    keys[:, 3] &= np.uint32(0xFFFF00FF)
+    keys = np.unique(keys, axis=0)
+    acts = T.flow_action(chain_id=1, out_port=np.arange(len(keys)) % 4096, flow_id=np.arange(len(keys)))
+    ft.insert_many(keys, acts)
+    assert len(ft) == len(keys)
+    vals = ft.t.vals()
+    for i in rng.choice(len(keys), 300, replace=False):
+        s = ft.find(keys[i])
+        assert s >= 0 and vals[s][3] == i
+    # erase half, the rest still found
+    for i in range(0, len(keys), 2):
+        assert ft.erase(keys[i])
+    for i in range(1, len(keys), 2)[:500]:
+        assert ft.find(keys[i]) >= 0
+    assert ft.find(keys[0]) == -1
+    assert len(ft.t.take_dirty()) > 0
+
+
+def test_flow_key_meta_byte_rejected(nf):
+    ft = T.FlowTable(1 << 4)
+    with pytest.raises(ValueError):
+        ft.insert((1, 2, 3, 0x0100), (0, 0, 0, 0))
+
+
+def test_range_to_prefixes():
+    for lo, hi in ((0, 65535), (1024, 65535), (80, 80), (1000, 1999), (1, 6)):
+        pre = T.range_to_prefixes(lo, hi)
+        cover = set()
+        for v, m in pre:
+            free = (~m) & 0xFFFF
+            cover |= {v | x for x in range(free + 1) if (x & ~free) == 0}
+        assert cover == set(range(lo, hi + 1))
+
+
+def test_packet_craft_checksums():
+    pk, ln = P.craft(100, dmac="02:00:00:00:00:01", smac="02:00:00:00:00:02", src_ip=0x0A000001,
+                     dst_ip=0x0A000002, sport=np.arange(100) + 1000, dport=53, proto=17)
+    assert P.check_csums(pk, ln).all()
+    pk2, ln2 = P.craft(10, dmac=1, smac=2, src_ip=1, dst_ip=2, sport=1, dport=2, proto=6, vlan=7)
+    fr, fl, vid = P.strip(pk2, ln2)
+    assert (vid == 7).all() and (fl == 60).all()
+    assert P.check_csums(fr, fl).all()
+
+
+@pytest.fixture(scope="module")
+def sfc():
+    dp = DataPlane("cpu", flow_buckets=1 << 12)
+    sc = S.build_sfc(dp, n_pods=8, n_flows=20000, n_acl=64, seed=0)
+    dp.commit()
+    return dp, sc
+
+
+def test_sfc_forward_nat_l2_vlan(sfc):
+    dp, sc = sfc
+    pk, im = S.traffic(sc, 3000, seed=5)
+    r = dp.run(pk, im)
+    op, ln, rs = P.meta_fields(r.meta)
+    assert (rs == 0).all()
+    fr, fl, vid = P.strip(r.out, ln)
+    assert P.check_csums(fr, fl).all()          # incremental NAT checksum == full recompute
+    # expected per flow
+    keys = np.ascontiguousarray(pk[:, [30, 31, 32, 33]])  # tagged: src ip at 26+4
+    f_src = ((pk[:, 30].astype(np.uint32) << 24) | (pk[:, 31].astype(np.uint32) << 16) |
+             (pk[:, 32].astype(np.uint32) << 8) | pk[:, 33]) - S.POD_NET
+    out_src = (fr[:, 26].astype(np.uint32) << 24) | (fr[:, 27].astype(np.uint32) << 16) | (fr[:, 28].astype(np.uint32) << 8) | fr[:, 29]
+    assert ((out_src >> 8) == (S.NAT_NET >> 8)).all()   # SNAT'd into the pool
+    dst_pod = op - sc.pod_port[0]
+    assert (vid == dst_pod + 2).all()               # egress tag = destination VF vlan
+    dmac = fr[:, 0:6]
+    exp = np.stack([np.frombuffer(S.pod_mac(int(p)), np.uint8) for p in dst_pod])
+    assert np.array_equal(dmac, exp)                # L2 steer rewrote dst MAC
+    assert (f_src < sc.n_pods).all()
+    pc = dp.port_counters()
+    assert pc[:, 0].sum() >= 3000
+
+
+def _one(sc, flow=0, **kw):
+    slots, inm = S.traffic(sc, 1, seed=9, flows=np.array([flow]))
+    for k, v in kw.items():
+        if k == "inmeta":
+            inm[:] = v
+        elif k == "byte":
+            off, val = v
+            slots[0, off] = val
+    return slots, inm
+
+
+def test_drops_and_miss_paths(sfc):
+    dp, sc = sfc
+    # spoofed src mac
+    s, i = _one(sc, byte=(11, 0x77))
+    assert P.meta_fields(dp.run(s, i).meta)[2][0] == 3
+    # wrong vlan on a vlan-isolated port
+    s, i = _one(sc, byte=(15, 0xEE))
+    assert P.meta_fields(dp.run(s, i).meta)[2][0] == 2
+    # malformed length
+    s, i = _one(sc)
+    i[:] = (i & 0xFFFF) | (8 << 16)
+    assert P.meta_fields(dp.run(s, i).meta)[2][0] == 9
+    # invalid port
+    s, i = _one(sc)
+    i[:] = (i & 0xFFFF0000) | 4000
+    assert P.meta_fields(dp.run(s, i).meta)[2][0] == 1
+    # flow miss -> L2 path to the pod owning the dst MAC
+    src = 0
+    dst_pod = 3
+    slots, ln = P.craft(1, dmac=S.pod_mac(dst_pod), smac=S.pod_mac(src), src_ip=0x01010101, dst_ip=0x02020202,
+                        sport=1, dport=2, vlan=src + 2)
+    r = dp.run(slots, P.inmeta(sc.pod_port[src], ln))
+    op, _, rs = P.meta_fields(r.meta)
+    assert rs[0] == 0 and op[0] == sc.pod_port[dst_pod]
+    # unknown dst MAC on a flow miss -> punt
+    slots, ln = P.craft(1, dmac="02:99:99:99:99:99", smac=S.pod_mac(src), src_ip=1, dst_ip=2, sport=1, dport=2, vlan=2)
+    r = dp.run(slots, P.inmeta(sc.pod_port[src], ln))
+    op, _, rs = P.meta_fields(r.meta)
+    assert rs[0] == 5 and op[0] == T.PORT_PUNT
+
+
+def test_acl_deny_priority():
+    dp = DataPlane("cpu", flow_buckets=1 << 8)
+    sc = S.build_sfc(dp, n_pods=4, n_flows=100, n_acl=0, seed=1)
+    f = 5
+    dport = int(sc.flow_dport[f])
+    dp.acl.add(permit=True, dport=dport, src="10.128.0.0/16")     # higher priority permit
+    dp.acl.add(permit=False, dport=dport)
+    dp.acl.add(permit=False, dport=(0, 65535))                      # deny everything else
+    dp.commit()
+    s, i = _one(sc, flow=f)
+    assert P.meta_fields(dp.run(s, i).meta)[2][0] == 0
+    g = (f + 1) % 100
+    if sc.flow_dport[g] != dport:
+        s, i = _one(sc, flow=g)
+        assert P.meta_fields(dp.run(s, i).meta)[2][0] == 4
+
+
+@pytest.mark.parametrize("hops", [("ttl", "l2fwd"), ("hairpin",), ("vlan", "l2fwd"), ("drop",)])
+def test_other_hops(hops):
+    dp = DataPlane("cpu", flow_buckets=1 << 8)
+    sc = S.build_sfc(dp, n_pods=4, n_flows=64, n_acl=0, seed=2, hops=hops, install_flows=False)
+    acts = sc.actions.copy()
+    if "vlan" in hops:
+        acts[:, 2] = (acts[:, 2] & 0xFFFF) | (100 << 16)
+    dp.flows.insert_many(sc.keys, acts)
+    dp.commit()
+    s, i = _one(sc, flow=3)
+    r = dp.run(s, i)
+    op, ln, rs = P.meta_fields(r.meta)
+    fr, fl, vid = P.strip(r.out, ln)
+    if hops == ("drop",):
+        assert rs[0] == 7
+        return
+    assert rs[0] == 0
+    if "ttl" in hops:
+        assert fr[0, 22] == 63 and P.check_csums(fr, fl).all()
+    if hops == ("hairpin",):
+        assert op[0] == sc.pod_port[sc.flow_src_pod[3]]
+        assert np.array_equal(fr[0, 0:6], np.frombuffer(S.pod_mac(int(sc.flow_src_pod[3])), np.uint8))
+    if "vlan" in hops:
+        assert vid[0] == 100
