@@ -49,6 +49,9 @@ def parse():
     ap.add_argument("--acl-mode", default="mfma", choices=["mfma", "scalar"])
     ap.add_argument("--rotate", type=int, default=4)
     ap.add_argument("--no-lowlat", action="store_true", help="skip the small-batch latency probe")
+    ap.add_argument("--chunks", type=int, default=4, help="pipeline chunks per step (N > 1)")
+    ap.add_argument("--force-sharded", action="store_true",
+                    help="use the sharded multi-GPU pipeline even at N = 1 (measures its compute cost)")
     return ap.parse_args()
 
 
@@ -65,17 +68,23 @@ def main() -> None:
             raise SystemExit("--gpus > 1 must be launched with torch.distributed.run (one process per GPU)")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    sharded = world > 1 or a.force_sharded
+    if sharded:
+        if world == 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29533")
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
         dist.init_process_group("nccl", device_id=dev)
 
     from dpu_operator_amd.dataplane import scenario as S
     from dpu_operator_amd.dataplane.engine import DataPlane
     from dpu_operator_amd.ops import packets as P
-    from dpu_operator_amd.parallel.sharded import ShardedDataPlane, shard_filter
+    from dpu_operator_amd.parallel.sharded import PipelinedShardedDataPlane, ShardedDataPlane, shard_filter
 
     t_setup = time.time()
     flows_here = a.flows / world
-    buckets = 1 << max(10, int(math.ceil(math.log2(flows_here / 4))))  # <= 50% load, 8 slots
+    buckets = 1 << max(10, int(math.ceil(math.log2(flows_here / 2))))  # <= 50% load, 4 slots/bucket
     dp = DataPlane(device=str(dev), flow_buckets=buckets, hash_mode=a.hash, acl_mode=a.acl_mode)
     n_pods = a.pods_per_gpu * world
     pod_gpu = np.arange(n_pods) // a.pods_per_gpu
@@ -88,7 +97,7 @@ def main() -> None:
         pk, im = S.traffic(sc, a.batch, seed=1000 * rank + r + 1, src_pods=my_pods)
         batches.append((torch.from_numpy(pk).to(dev), torch.from_numpy(im.view(np.int32)).to(dev)))
         del pk, im
-    if world == 1:
+    if not sharded:
         out, meta, lat = dp.alloc_batch(a.batch)
 
         def step(k):
@@ -98,14 +107,14 @@ def main() -> None:
         def results():
             return meta.cpu().numpy().view(np.uint32), lat.cpu().numpy().view(np.uint32).astype(np.float64) * 0.01
     else:
-        eng = ShardedDataPlane(dp, rank, world, a.batch)
+        eng = PipelinedShardedDataPlane(dp, rank, world, a.batch, chunks=a.chunks)
 
         def step(k):
             pk, im = batches[k % a.rotate]
             eng.step(pk, im)
 
         def results():
-            return eng.out_meta.cpu().numpy().view(np.uint32), eng.latency_samples_us()
+            return eng.out_meta(), eng.latency_samples_us()
 
     setup_s = time.time() - t_setup
     for k in range(a.warmup):
@@ -143,7 +152,7 @@ def main() -> None:
     if not a.no_lowlat:
         nsm = 1 << 16
         pk, im = batches[0][0][:nsm].contiguous(), batches[0][1][:nsm].contiguous()
-        if world == 1:
+        if not sharded:
             o2, m2, l2 = dp.alloc_batch(nsm)
             for _ in range(20):
                 dp.run(pk, im, o2, m2, l2)
@@ -181,7 +190,8 @@ def main() -> None:
                 "model": f"1M-flow SFC: acl({a.acl} TCAM rules)->snat->l2fwd, 64B frames, {a.pods_per_gpu} pods/GPU",
                 "global_batch": world * a.batch,
                 "seq_len": 64,
-                "parallelism": "fused-1gpu" if world == 1 else f"flow-shard x{world} + 3x all-to-all (RCCL/xGMI)",
+                "parallelism": "fused-1gpu" if not sharded else
+                f"flow-shard x{world} + 3x all-to-all (RCCL/xGMI), {a.chunks}-chunk overlap",
             },
             "p50_latency_us": round(p50, 2),
             "p99_latency_us": round(p99, 2),
@@ -195,7 +205,7 @@ def main() -> None:
             "baseline_note": "reference publishes no numbers (BASELINE.md); 200GbE line rate at 64B = 297.6 Mpps",
         }
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if sharded:
         dist.barrier()
         dist.destroy_process_group()
 

@@ -32,9 +32,7 @@ TablesView tables_from(const py::dict& d) {
   t.ports = ptr<const PortEntry>(d, "ports");
   t.chains = ptr<const ChainEntry>(d, "chains");
   t.n_chains = val<uint32_t>(d, "n_chains", 0);
-  t.tags = ptr<const uint16_t>(d, "tags");
-  t.keys = ptr<const FlowKey>(d, "keys");
-  t.vals = ptr<const FlowAction>(d, "vals");
+  t.flows = ptr<const FlowSlot>(d, "flows");
   t.bucket_mask = val<uint32_t>(d, "bucket_mask", 0);
   t.macs = ptr<const MacEntry>(d, "macs");
   t.mac_mask = val<uint32_t>(d, "mac_mask", 0);
@@ -44,7 +42,7 @@ TablesView tables_from(const py::dict& d) {
   t.acl_permit = ptr<const uint8_t>(d, "acl_permit");
   t.n_acl = val<uint32_t>(d, "n_acl", 0);
   t.acl_default_permit = val<uint32_t>(d, "acl_default_permit", 1);
-  if (!t.ports || !t.chains || !t.tags || !t.keys || !t.vals || !t.rss_key)
+  if (!t.ports || !t.chains || !t.flows || !t.rss_key)
     throw std::invalid_argument("tables dict is missing a required buffer");
   if (t.n_acl && (!t.acl_value || !t.acl_mask || !t.acl_permit))
     throw std::invalid_argument("n_acl > 0 but ACL buffers missing");
@@ -112,17 +110,10 @@ PYBIND11_MODULE(_nfdp, m) {
       .def("find", [](const FlowTableHost& t, py::tuple k) {
         return t.find(FlowKey{k[0].cast<uint32_t>(), k[1].cast<uint32_t>(), k[2].cast<uint32_t>(), k[3].cast<uint32_t>()});
       })
-      .def("tags", [](const FlowTableHost& t) {
-        auto& v = t.tags();
-        return py::array_t<uint16_t>(v.size(), v.data());
-      })
-      .def("keys", [](const FlowTableHost& t) {
-        auto& v = t.keys();
-        return py::array_t<uint32_t>({(py::ssize_t)v.size(), (py::ssize_t)4}, reinterpret_cast<const uint32_t*>(v.data()));
-      })
-      .def("vals", [](const FlowTableHost& t) {
-        auto& v = t.vals();
-        return py::array_t<uint32_t>({(py::ssize_t)v.size(), (py::ssize_t)4}, reinterpret_cast<const uint32_t*>(v.data()));
+      .def("slots", [](const FlowTableHost& t) {
+        // [nbuckets*4, 8] uint32: key (4 words, meta |= 0x100 when used) + action (4 words)
+        auto& v = t.slots();
+        return py::array_t<uint32_t>({(py::ssize_t)v.size(), (py::ssize_t)8}, reinterpret_cast<const uint32_t*>(v.data()));
       })
       .def("take_dirty", [](FlowTableHost& t) {
         auto v = t.take_dirty();
@@ -145,7 +136,7 @@ PYBIND11_MODULE(_nfdp, m) {
   });
   m.def("table_hash", [](uint32_t h, uint32_t mask) {
     TableHash t = table_hash(h, mask);
-    return py::make_tuple(t.b1, t.b2, t.tag);
+    return py::make_tuple(t.b1, t.b2);
   });
   m.def("owner_of", &owner_of);
   m.def("build_acl_frags", [](U32Arr value, U32Arr mask) {
@@ -186,7 +177,7 @@ PYBIND11_MODULE(_nfdp, m) {
                            uint32_t n, uintptr_t flow_ctr, uintptr_t port_ctr, uintptr_t drop_ctr, uintptr_t t0,
                            uintptr_t lat, uintptr_t acl_wfrag, uintptr_t acl_cinit, uint32_t acl_tiles,
                            uintptr_t toep_frag, uintptr_t toep_tab, int hash_mode, int acl_mode, int num_cus,
-                           uintptr_t stream) {
+                           uintptr_t stream, uint32_t flags) {
     FusedLaunch f{};
     f.t = tables_from(tables);
     f.pkts = reinterpret_cast<const void*>(pkts);
@@ -204,6 +195,7 @@ PYBIND11_MODULE(_nfdp, m) {
     f.acl_tiles = acl_tiles;
     f.toep_frag = reinterpret_cast<const void*>(toep_frag);
     f.toep_tab = reinterpret_cast<const uint32_t*>(toep_tab);
+    f.flags = flags;
     if (!f.pkts || !f.inmeta || !f.out || !f.out_meta || !f.port_ctr || !f.drop_ctr)
       throw std::invalid_argument("launch_fused: null buffer");
     if (hash_mode == 2 && !f.toep_frag) throw std::invalid_argument("MFMA hash needs toeplitz frags");
@@ -216,13 +208,10 @@ PYBIND11_MODULE(_nfdp, m) {
   m.def("launch_stamp", [](uintptr_t dst, uintptr_t stream) {
     check(launch_stamp(reinterpret_cast<unsigned long long*>(dst), reinterpret_cast<hipStream_t>(stream)), "stamp");
   });
-  m.def("launch_bucket_update", [](uintptr_t idx, uint32_t nb, uintptr_t tag_rows, uintptr_t key_rows,
-                                   uintptr_t val_rows, uintptr_t tags, uintptr_t keys, uintptr_t vals,
+  m.def("launch_bucket_update", [](uintptr_t idx, uint32_t nb, uintptr_t rows, uintptr_t flows,
                                    uint32_t bucket_mask, uintptr_t stream) {
-    check(launch_bucket_update(reinterpret_cast<const uint32_t*>(idx), nb, reinterpret_cast<const void*>(tag_rows),
-                               reinterpret_cast<const void*>(key_rows), reinterpret_cast<const void*>(val_rows),
-                               reinterpret_cast<void*>(tags), reinterpret_cast<void*>(keys),
-                               reinterpret_cast<void*>(vals), bucket_mask, reinterpret_cast<hipStream_t>(stream)),
+    check(launch_bucket_update(reinterpret_cast<const uint32_t*>(idx), nb, reinterpret_cast<const void*>(rows),
+                               reinterpret_cast<void*>(flows), bucket_mask, reinterpret_cast<hipStream_t>(stream)),
           "bucket_update");
   });
   // ---------------- sharded (multi-GPU) stages: device=True -> HIP kernels, False -> CPU twins

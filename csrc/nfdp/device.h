@@ -115,28 +115,32 @@ __device__ __forceinline__ void classify_wave(const FlowKey& key, uint4* kx, con
   }
 }
 
-// Vectorized 2-choice bucket probe: one 16-B tag row per bucket, 16-B key compare on a tag hit.
-__device__ __forceinline__ int64_t flow_lookup_vec(const TablesView& t, const FlowKey& k, uint32_t h) {
+// 2-choice bucket probe.  A bucket is one 128-B line holding 4 x {key, action}; it is loaded
+// whole (8 x dwordx4, one line, one trip) and the action comes with the key, so a hit in the
+// first bucket costs a single dependent fetch.  The second bucket is touched only on a miss.
+__device__ __forceinline__ int64_t flow_probe(const TablesView& t, const FlowKey& k, uint32_t h, uint4& act) {
   const TableHash th = table_hash(h, t.bucket_mask);
-  const uint4* tags = reinterpret_cast<const uint4*>(t.tags);
-  const uint4* keys = reinterpret_cast<const uint4*>(t.keys);
+  const uint4* fl = reinterpret_cast<const uint4*>(t.flows);
+  const uint32_t used = k.meta | kSlotUsed;
 #pragma unroll
   for (int c = 0; c < 2; ++c) {
     const uint32_t b = c ? th.b2 : th.b1;
-    const uint4 tg = tags[b];
-    const uint32_t tw[4] = {tg.x, tg.y, tg.z, tg.w};
-    uint32_t m = 0;
+    const uint4* row = fl + (size_t)b * (kBucketSlots * 2);
+    uint4 r[kBucketSlots * 2];
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      m |= ((tw[s] & 0xFFFFu) == th.tag ? 1u : 0u) << (2 * s);
-      m |= ((tw[s] >> 16) == th.tag ? 1u : 0u) << (2 * s + 1);
+    for (int q = 0; q < kBucketSlots * 2; ++q) r[q] = row[q];
+    int hit = -1;
+#pragma unroll
+    for (int s = kBucketSlots - 1; s >= 0; --s) {
+      const uint4 e = r[2 * s];
+      if (e.x == k.src_ip && e.y == k.dst_ip && e.z == k.ports && e.w == used) hit = s;
     }
-    while (m) {
-      const uint32_t s = __builtin_ctz(m);
-      m &= m - 1;
-      const uint4 e = keys[(size_t)b * kBucketSlots + s];
-      if (e.x == k.src_ip && e.y == k.dst_ip && e.z == k.ports && e.w == k.meta)
-        return (int64_t)b * kBucketSlots + s;
+    if (hit >= 0) {
+      uint4 a = r[1];
+#pragma unroll
+      for (int s = 1; s < kBucketSlots; ++s) a = (hit == s) ? r[2 * s + 1] : a;
+      act = a;
+      return (int64_t)b * kBucketSlots + hit;
     }
   }
   return -1;

@@ -12,26 +12,23 @@ FlowTableHost::FlowTableHost(uint32_t nbuckets_pow2, const std::vector<uint8_t>&
     : nb_(nbuckets_pow2), rss_(rss_key) {
   if (nb_ < 2 || (nb_ & (nb_ - 1))) throw std::invalid_argument("nbuckets must be a power of two >= 2");
   if (rss_.size() < 20) throw std::invalid_argument("rss key must be >= 20 bytes");
-  tags_.assign((size_t)nb_ * kBucketSlots, 0);
-  keys_.assign((size_t)nb_ * kBucketSlots, FlowKey{0, 0, 0, 0});
-  vals_.assign((size_t)nb_ * kBucketSlots, FlowAction{});
+  slots_.assign((size_t)nb_ * kBucketSlots, FlowSlot{});
 }
 
-int FlowTableHost::find_in_bucket(uint32_t b, uint16_t tag, const FlowKey& k) const {
+int FlowTableHost::find_in_bucket(uint32_t b, const FlowKey& k) const {
+  const uint32_t used = k.meta | kSlotUsed;
   for (int s = 0; s < kBucketSlots; ++s) {
-    const size_t i = (size_t)b * kBucketSlots + s;
-    if (tags_[i] != tag) continue;
-    const FlowKey& e = keys_[i];
-    if (e.src_ip == k.src_ip && e.dst_ip == k.dst_ip && e.ports == k.ports && e.meta == k.meta) return s;
+    const FlowKey& e = slots_[(size_t)b * kBucketSlots + s].key;
+    if (e.src_ip == k.src_ip && e.dst_ip == k.dst_ip && e.ports == k.ports && e.meta == used) return s;
   }
   return -1;
 }
 
 int64_t FlowTableHost::find(const FlowKey& k) const {
   const TableHash th = table_hash(hash(k), mask());
-  int s = find_in_bucket(th.b1, th.tag, k);
+  int s = find_in_bucket(th.b1, k);
   if (s >= 0) return (int64_t)th.b1 * kBucketSlots + s;
-  s = find_in_bucket(th.b2, th.tag, k);
+  s = find_in_bucket(th.b2, k);
   if (s >= 0) return (int64_t)th.b2 * kBucketSlots + s;
   return -1;
 }
@@ -40,26 +37,29 @@ int64_t FlowTableHost::insert(const FlowKey& key, const FlowAction& act) {
   if (key.meta & 0xFF00u) throw std::invalid_argument("FlowKey.meta byte 1 must be zero");
   const int64_t existing = find(key);
   if (existing >= 0) {
-    vals_[existing] = act;
+    slots_[existing].act = act;
     dirty_.insert((uint32_t)(existing / kBucketSlots));
     return existing;
   }
   FlowKey k = key;
+  k.meta |= kSlotUsed;
   FlowAction a = act;
   int64_t first_slot = -1;   // where the NEW key ends up
   int64_t pending_from = -1; // slot the entry currently being placed was evicted from
   uint32_t avoid = 0xFFFFFFFFu;  // bucket the current entry was just evicted from
   // track the path so a failed insert can be rolled back
-  std::vector<std::tuple<size_t, uint16_t, FlowKey, FlowAction>> undo;
+  std::vector<std::pair<size_t, FlowSlot>> undo;
   std::vector<std::pair<int64_t, int64_t>> new_moves;
   for (int kick = 0; kick < 512; ++kick) {
-    const TableHash cur = table_hash(hash(k), mask());
+    FlowKey hk = k;
+    hk.meta &= ~kSlotUsed;
+    const TableHash cur = table_hash(hash(hk), mask());
     const uint32_t cand[2] = {cur.b1, cur.b2};
     for (int c = 0; c < 2; ++c) {
       for (int s = 0; s < kBucketSlots; ++s) {
         const size_t i = (size_t)cand[c] * kBucketSlots + s;
-        if (tags_[i] == 0) {
-          tags_[i] = cur.tag; keys_[i] = k; vals_[i] = a;
+        if (!(slots_[i].key.meta & kSlotUsed)) {
+          slots_[i].key = k; slots_[i].act = a;
           dirty_.insert(cand[c]);
           ++count_;
           if (first_slot < 0) first_slot = (int64_t)i;
@@ -74,10 +74,10 @@ int64_t FlowTableHost::insert(const FlowKey& key, const FlowAction& act) {
     if (vb == avoid) vb = (vb == cand[0]) ? cand[1] : cand[0];
     const int vs = (int)(rng_() % kBucketSlots);
     const size_t vi = (size_t)vb * kBucketSlots + vs;
-    undo.emplace_back(vi, tags_[vi], keys_[vi], vals_[vi]);
-    const FlowKey vk = keys_[vi];
-    const FlowAction va = vals_[vi];
-    tags_[vi] = cur.tag; keys_[vi] = k; vals_[vi] = a;
+    undo.emplace_back(vi, slots_[vi]);
+    const FlowKey vk = slots_[vi].key;
+    const FlowAction va = slots_[vi].act;
+    slots_[vi].key = k; slots_[vi].act = a;
     dirty_.insert(vb);
     if (first_slot < 0) first_slot = (int64_t)vi;
     if (pending_from >= 0) new_moves.emplace_back(pending_from, (int64_t)vi);
@@ -86,17 +86,14 @@ int64_t FlowTableHost::insert(const FlowKey& key, const FlowAction& act) {
     k = vk; a = va;
   }
   // roll back
-  for (auto it = undo.rbegin(); it != undo.rend(); ++it) {
-    const size_t i = std::get<0>(*it);
-    tags_[i] = std::get<1>(*it); keys_[i] = std::get<2>(*it); vals_[i] = std::get<3>(*it);
-  }
+  for (auto it = undo.rbegin(); it != undo.rend(); ++it) slots_[it->first] = it->second;
   throw std::runtime_error("flow table full (cuckoo insert failed after 512 kicks)");
 }
 
 bool FlowTableHost::erase(const FlowKey& k) {
   const int64_t i = find(k);
   if (i < 0) return false;
-  tags_[i] = 0; keys_[i] = FlowKey{0, 0, 0, 0}; vals_[i] = FlowAction{};
+  slots_[i] = FlowSlot{};
   dirty_.insert((uint32_t)(i / kBucketSlots));
   --count_;
   return true;
@@ -207,7 +204,7 @@ void oracle_run(const TablesView& t, const uint32_t* pkts, const uint32_t* inmet
       const int64_t slot = flow_lookup(t, st.key, h);
       if (slot >= 0) {
         hit = true;
-        act = t.vals[slot];
+        act = t.flows[slot].act;
         if (flow_ctr) flow_ctr[slot] += ctr_inc(st.wire_len);
       }
     }

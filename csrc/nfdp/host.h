@@ -27,9 +27,7 @@ class FlowTableHost {
   bool erase(const FlowKey& k);
   int64_t find(const FlowKey& k) const;
   uint32_t hash(const FlowKey& k) const { return toeplitz_scalar(k, rss_.data()); }
-  const std::vector<uint16_t>& tags() const { return tags_; }
-  const std::vector<FlowKey>& keys() const { return keys_; }
-  const std::vector<FlowAction>& vals() const { return vals_; }
+  const std::vector<FlowSlot>& slots() const { return slots_; }
   // dirty tracking
   std::vector<uint32_t> take_dirty();
   // slot moves performed by evictions since the last take (from, to), for counter migration
@@ -38,13 +36,11 @@ class FlowTableHost {
   const std::vector<uint8_t>& rss_key() const { return rss_; }
 
  private:
-  int find_in_bucket(uint32_t b, uint16_t tag, const FlowKey& k) const;
+  int find_in_bucket(uint32_t b, const FlowKey& k) const;
   uint32_t nb_;
   size_t count_ = 0;
   std::vector<uint8_t> rss_;
-  std::vector<uint16_t> tags_;
-  std::vector<FlowKey> keys_;
-  std::vector<FlowAction> vals_;
+  std::vector<FlowSlot> slots_;
   std::unordered_set<uint32_t> dirty_;
   std::vector<std::pair<int64_t, int64_t>> moves_;
   std::mt19937 rng_{12345};
@@ -82,13 +78,13 @@ struct FusedLaunch {
   const unsigned long long* t0; uint32_t* lat;
   const void* acl_wfrag; const void* acl_cinit; uint32_t acl_tiles;
   const void* toep_frag; const uint32_t* toep_tab;
+  uint32_t flags = 0;
 };
 hipError_t launch_fused(const FusedLaunch& f, const LaunchCfg& cfg, hipStream_t s);
 size_t fused_lds_bytes(int hash_mode, int acl_mode, uint32_t acl_tiles);
 hipError_t launch_stamp(unsigned long long* dst, hipStream_t s);
-hipError_t launch_bucket_update(const uint32_t* idx, uint32_t nb, const void* tag_rows,
-                                const void* key_rows, const void* val_rows, void* tags, void* keys,
-                                void* vals, uint32_t bucket_mask, hipStream_t s);
+hipError_t launch_bucket_update(const uint32_t* idx, uint32_t nb, const void* rows, void* flows,
+                                uint32_t bucket_mask, hipStream_t s);
 hipError_t launch_harvest(unsigned long long* ctr, unsigned long long* out, uint32_t n, hipStream_t s);
 
 }  // namespace nfdp

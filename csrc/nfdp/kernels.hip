@@ -34,6 +34,7 @@ struct FusedArgs {
   const v4i* toep_frag;           // [2][2][64] A fragments of the Toeplitz matrix
   const uint32_t* toep_tab;       // [16][256] byte tables (LDS hash variant)
   uint32_t acl_tiles;             // ceil(n_acl / 16)
+  uint32_t flags;                 // ablation: bit0 no port/drop counters, bit1 no latency samples
 };
 
 __device__ __forceinline__ size_t lds_align16(size_t x) { return (x + 15) & ~(size_t)15; }
@@ -111,10 +112,10 @@ __global__ __launch_bounds__(kBlock) void fused_kernel(FusedArgs a) {
     bool hit = false;
     FlowAction act = {};
     if (!st.reason && p.ipv4) {
-      const int64_t slot = flow_lookup_vec(a.t, st.key, hash);
+      uint4 v;
+      const int64_t slot = flow_probe(a.t, st.key, hash, v);
       if (slot >= 0) {
         hit = true;
-        const uint4 v = reinterpret_cast<const uint4*>(a.t.vals)[slot];
         act.chain_id = v.x & 0xFFFFu; act.out_port = v.x >> 16; act.nat_ip = v.y;
         act.nat_port = v.z & 0xFFFFu; act.vlan = v.z >> 16; act.flow_id = v.w;
         if (a.flow_ctr) atomicAdd(a.flow_ctr + slot, ctr_inc(st.wire_len));
@@ -130,19 +131,21 @@ __global__ __launch_bounds__(kBlock) void fused_kernel(FusedArgs a) {
       for (int q = 0; q < 4; ++q) dst[q] = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
       a.out_meta[i] = make_meta(e.out_port, olen, e.reason);
       // counters
-      if (st.in_port < kLdsPorts) {
+      if (a.flags & 1u) {
+      } else if (st.in_port < kLdsPorts) {
         atomicAdd(&pc[st.in_port], 1u); atomicAdd(&pc[kLdsPorts + st.in_port], st.wire_len);
       } else if (st.in_port < (uint32_t)kMaxPorts) {
         atomicAdd(a.port_ctr + 2 * st.in_port, ctr_inc(st.wire_len));
       }
-      if (e.reason) {
+      if (a.flags & 1u) {
+      } else if (e.reason) {
         atomicAdd(&drops[e.reason & (kNumReasons - 1)], 1u);
       } else if (e.out_port < kLdsPorts) {
         atomicAdd(&pc[2 * kLdsPorts + e.out_port], 1u); atomicAdd(&pc[3 * kLdsPorts + e.out_port], olen);
       } else {
         atomicAdd(a.port_ctr + 2 * e.out_port + 1, ctr_inc(olen));
       }
-      if (a.lat && (i & 15u) == 0) {
+      if (a.lat && !(a.flags & 2u) && (i & 15u) == 0) {
         const unsigned long long now = __builtin_amdgcn_s_memrealtime();
         a.lat[i >> 4] = (uint32_t)(now - t0);
       }
@@ -163,17 +166,14 @@ __global__ void stamp_kernel(unsigned long long* dst) {
 }
 
 // Scatter whole bucket rows (control-plane updates: a modified bucket is re-sent entire).
-__global__ void bucket_update_kernel(const uint32_t* idx, uint32_t nb, const uint4* tag_rows,
-                                     const uint4* key_rows, const uint4* val_rows, uint4* tags,
-                                     uint4* keys, uint4* vals, uint32_t bucket_mask) {
-  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;  // one thread per (bucket, slot)
-  const uint32_t bi = j / kBucketSlots, s = j % kBucketSlots;
+__global__ void bucket_update_kernel(const uint32_t* idx, uint32_t nb, const uint4* rows, uint4* flows,
+                                     uint32_t bucket_mask) {
+  const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;  // one thread per 16 B of a 128-B row
+  const uint32_t bi = j / (kBucketSlots * 2), q = j % (kBucketSlots * 2);
   if (bi >= nb) return;
   const uint32_t b = idx[bi];
   if (b > bucket_mask) return;
-  keys[(size_t)b * kBucketSlots + s] = key_rows[(size_t)bi * kBucketSlots + s];
-  vals[(size_t)b * kBucketSlots + s] = val_rows[(size_t)bi * kBucketSlots + s];
-  if (s == 0) tags[b] = tag_rows[bi];
+  flows[(size_t)b * kBucketSlots * 2 + q] = rows[(size_t)bi * kBucketSlots * 2 + q];
 }
 
 // Read-and-reset packed counters (harvest); host accumulates into 64-bit totals.
@@ -226,6 +226,7 @@ hipError_t launch_fused(const FusedLaunch& f, const LaunchCfg& cfg, hipStream_t 
   a.acl_tiles = f.acl_tiles;
   a.toep_frag = reinterpret_cast<const v4i*>(f.toep_frag);
   a.toep_tab = f.toep_tab;
+  a.flags = f.flags;
   if (cfg.acl_mode == kAclMfma && (f.acl_tiles == 0 || f.acl_tiles > 64)) return hipErrorInvalidValue;
   const int h = cfg.hash_mode, ac = cfg.acl_mode, cu = cfg.num_cus;
 #define NFDP_CASE(HH, AA) if (h == HH && ac == AA) return launch_fused_t<HH, AA>(a, cu, s);
@@ -241,15 +242,12 @@ hipError_t launch_stamp(unsigned long long* dst, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t launch_bucket_update(const uint32_t* idx, uint32_t nb, const void* tag_rows,
-                                const void* key_rows, const void* val_rows, void* tags, void* keys,
-                                void* vals, uint32_t bucket_mask, hipStream_t s) {
+hipError_t launch_bucket_update(const uint32_t* idx, uint32_t nb, const void* rows, void* flows,
+                                uint32_t bucket_mask, hipStream_t s) {
   if (nb == 0) return hipSuccess;
-  const uint32_t threads = nb * kBucketSlots;
+  const uint32_t threads = nb * kBucketSlots * 2;
   hipLaunchKernelGGL(bucket_update_kernel, dim3((threads + 255) / 256), dim3(256), 0, s, idx, nb,
-                     reinterpret_cast<const uint4*>(tag_rows), reinterpret_cast<const uint4*>(key_rows),
-                     reinterpret_cast<const uint4*>(val_rows), reinterpret_cast<uint4*>(tags),
-                     reinterpret_cast<uint4*>(keys), reinterpret_cast<uint4*>(vals), bucket_mask);
+                     reinterpret_cast<const uint4*>(rows), reinterpret_cast<uint4*>(flows), bucket_mask);
   return hipGetLastError();
 }
 

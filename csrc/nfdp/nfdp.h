@@ -27,7 +27,8 @@ namespace nfdp {
 constexpr int kSlotBytes = 64;         // one packet slot in HBM (60 B frame + room for one tag)
 constexpr int kSlotDwords = kSlotBytes / 4;
 constexpr int kMaxPorts = 4096;        // vport table size (VF / NF / wire / PR ports)
-constexpr int kBucketSlots = 8;        // flow-table bucket = 8 slots, 16-B tag row
+constexpr int kBucketSlots = 4;        // flow-table bucket = 4 x {key, action} = one 128-B line
+constexpr uint32_t kSlotUsed = 0x100u; // occupied marker, stored in FlowKey.meta byte 1
 constexpr uint16_t kPortNone = 0xFFFF; // dropped
 constexpr uint16_t kPortPunt = 0xFFFE; // to slow path (control plane upcall)
 constexpr int kMaxHops = 7;
@@ -108,6 +109,15 @@ struct alignas(16) FlowAction {  // 16 B value of an exact-match flow entry
 };
 static_assert(sizeof(FlowAction) == 16, "FlowAction");
 
+// One flow-table slot: key (meta |= kSlotUsed when occupied) + action.  A bucket is 4 slots =
+// 128 B = one cache line, so a probe is ONE line fetch (the tag-row + key + value design needed
+// three dependent fetches).
+struct alignas(16) FlowSlot {
+  FlowKey key;
+  FlowAction act;
+};
+static_assert(sizeof(FlowSlot) == 32, "FlowSlot");
+
 struct alignas(16) ChainEntry {  // 16 B
   uint8_t nhops;
   uint8_t hop[kMaxHops];
@@ -165,16 +175,14 @@ NFDP_HD uint32_t toeplitz_scalar(const FlowKey& k, const uint8_t* rss_key) {
   return h;
 }
 
-// Flow-table geometry derived from the Toeplitz hash.
-struct TableHash { uint32_t b1, b2; uint16_t tag; };
+// Flow-table geometry derived from the Toeplitz hash: two candidate buckets.
+struct TableHash { uint32_t b1, b2; };
 NFDP_HD TableHash table_hash(uint32_t h, uint32_t bucket_mask) {
   TableHash t;
   const uint32_t m = fmix32(h ^ 0x9e3779b9u);
   t.b1 = h & bucket_mask;
   t.b2 = (m ^ (m >> 7)) & bucket_mask;
   if (t.b2 == t.b1) t.b2 = (t.b1 + 1) & bucket_mask;  // two distinct choices
-  uint16_t tag = (uint16_t)(m >> 16);
-  t.tag = tag ? tag : 1;                                // 0 = empty slot
   return t;
 }
 // Shard (owner GPU) from the top bits of the hash: independent of the bucket (low) bits.
@@ -338,9 +346,7 @@ struct TablesView {
   const PortEntry* ports;        // kMaxPorts
   const ChainEntry* chains;      // n_chains
   uint32_t n_chains;
-  const uint16_t* tags;          // nbuckets * 8
-  const FlowKey* keys;           // nbuckets * 8
-  const FlowAction* vals;        // nbuckets * 8
+  const FlowSlot* flows;         // nbuckets * kBucketSlots (one 128-B line per bucket)
   uint32_t bucket_mask;          // nbuckets - 1 (power of two)
   const MacEntry* macs;          // n_mac (power of two)
   uint32_t mac_mask;
@@ -357,12 +363,11 @@ struct TablesView {
 NFDP_HD int64_t flow_lookup(const TablesView& t, const FlowKey& k, uint32_t h) {
   const TableHash th = table_hash(h, t.bucket_mask);
   uint32_t bk[2] = {th.b1, th.b2};
+  const uint32_t used = k.meta | kSlotUsed;
   for (int c = 0; c < 2; ++c) {
-    const uint16_t* tg = t.tags + (size_t)bk[c] * kBucketSlots;
     for (int s = 0; s < kBucketSlots; ++s) {
-      if (tg[s] != th.tag) continue;
-      const FlowKey& e = t.keys[(size_t)bk[c] * kBucketSlots + s];
-      if (e.src_ip == k.src_ip && e.dst_ip == k.dst_ip && e.ports == k.ports && e.meta == k.meta)
+      const FlowKey& e = t.flows[(size_t)bk[c] * kBucketSlots + s].key;
+      if (e.src_ip == k.src_ip && e.dst_ip == k.dst_ip && e.ports == k.ports && e.meta == used)
         return (int64_t)bk[c] * kBucketSlots + s;
     }
   }

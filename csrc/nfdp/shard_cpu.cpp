@@ -54,7 +54,7 @@ void owner_cpu(const OwnerArgs& a) {
       const int64_t slot = flow_lookup(a.t, k, h);
       uint32_t out[4] = {0, 0, 0, 0};
       if (slot >= 0) {
-        std::memcpy(out, &a.t.vals[slot], 12);
+        std::memcpy(out, &a.t.flows[slot].act, 12);
         out[3] = 1;
         if (a.flow_ctr) a.flow_ctr[slot] += ctr_inc(wlen);
       }

@@ -69,7 +69,8 @@ class DataPlane:
         self._dev: dict[str, object] = {}
         self._versions: dict[str, int] = {}
         self._acl_tiles = 1
-        self.flow_totals = np.zeros((self.flows.nbuckets * 8, 2), np.uint64)
+        self.count_flows = True  # per-flow packed counters (one 64-bit atomic per packet)
+        self.flow_totals = np.zeros((self.flows.nbuckets * 4, 2), np.uint64)
         if self.gpu:
             torch = _torch()
             if not torch.cuda.is_available():
@@ -114,7 +115,7 @@ class DataPlane:
         return int(b.data_ptr()) if self.gpu else int(b.ctypes.data)
 
     def _alloc_counters(self) -> None:
-        self._zeros("flow_ctr", self.flows.nbuckets * 8)
+        self._zeros("flow_ctr", self.flows.nbuckets * 4)
         self._zeros("port_ctr", T.MAX_PORTS * 2)
         self._zeros("drop_ctr", 16)
         self._zeros("t0", 1)
@@ -147,11 +148,9 @@ class DataPlane:
             self._versions["acl"] = self.acl.version
             sent["acl"] = n
         ft = self.flows.t
-        if full or "tags" not in self._dev:
+        if full or "flows" not in self._dev:
             self.harvest()
-            self._buf("tags", ft.tags())
-            self._buf("keys", ft.keys())
-            self._buf("vals", ft.vals())
+            self._buf("flows", ft.slots())
             ft.clear_dirty()
             sent["flows_full"] = len(self.flows)
         else:
@@ -166,27 +165,22 @@ class DataPlane:
 
     def _push_buckets(self, dirty: np.ndarray) -> None:
         ft = self.flows.t
-        tags = ft.tags().reshape(-1, 8)[dirty]
-        keys = ft.keys().reshape(-1, 8, 4)[dirty]
-        vals = ft.vals().reshape(-1, 8, 4)[dirty]
+        rows = ft.slots().reshape(-1, 32)[dirty]   # whole 128-B buckets
         if self.gpu:
             torch = _torch()
             up = {k: torch.from_numpy(np.ascontiguousarray(v).view(np.uint8).reshape(-1).copy()).to(self.tdev)
-                  for k, v in (("idx", dirty.astype(np.uint32)), ("tag", tags), ("key", keys), ("val", vals))}
+                  for k, v in (("idx", dirty.astype(np.uint32)), ("rows", rows))}
             s = torch.cuda.current_stream(self.tdev).cuda_stream
-            self.nf.launch_bucket_update(up["idx"].data_ptr(), len(dirty), up["tag"].data_ptr(), up["key"].data_ptr(),
-                                         up["val"].data_ptr(), self._ptr("tags"), self._ptr("keys"), self._ptr("vals"),
+            self.nf.launch_bucket_update(up["idx"].data_ptr(), len(dirty), up["rows"].data_ptr(), self._ptr("flows"),
                                          ft.mask, s)
             self._keepalive = up
         else:
-            self._dev["tags"].view(np.uint16).reshape(-1, 8)[dirty] = tags
-            self._dev["keys"].view(np.uint32).reshape(-1, 8, 4)[dirty] = keys
-            self._dev["vals"].view(np.uint32).reshape(-1, 8, 4)[dirty] = vals
+            self._dev["flows"].view(np.uint32).reshape(-1, 32)[dirty] = rows
 
     def tables_ptrs(self) -> dict:
         return {
             "ports": self._ptr("ports"), "chains": self._ptr("chains"), "n_chains": int(self.chains.n),
-            "tags": self._ptr("tags"), "keys": self._ptr("keys"), "vals": self._ptr("vals"),
+            "flows": self._ptr("flows"),
             "bucket_mask": int(self.flows.t.mask), "macs": self._ptr("macs"), "mac_mask": int(self.macs.mask),
             "rss_key": self._ptr("rss_key"), "acl_value": self._ptr("acl_value"), "acl_mask": self._ptr("acl_mask"),
             "acl_permit": self._ptr("acl_permit"), "n_acl": int(getattr(self, "_n_acl", 0)),
@@ -207,7 +201,8 @@ class DataPlane:
             lat = None
         return out, meta, lat
 
-    def run(self, pkts, inmeta, out=None, meta=None, lat=None, stamp: bool = True, stream=None) -> BatchResult:
+    def run(self, pkts, inmeta, out=None, meta=None, lat=None, stamp: bool = True, stream=None,
+            flags: int = 0) -> BatchResult:
         """Process one batch.  GPU: pkts/inmeta torch tensors on the device ([n,64] uint8 / [n]
         int32); CPU: numpy arrays (runs the C++ oracle)."""
         n = int(pkts.shape[0])
@@ -227,11 +222,12 @@ class DataPlane:
                 self.nf.launch_stamp(self._ptr("t0"), s)
             self.nf.launch_fused(
                 tp, pkts.data_ptr(), inmeta.data_ptr(), out.data_ptr(), meta.data_ptr(), n,
-                self._ptr("flow_ctr"), self._ptr("port_ctr"), self._ptr("drop_ctr"), self._ptr("t0"),
+                self._ptr("flow_ctr") if self.count_flows else 0, self._ptr("port_ctr"), self._ptr("drop_ctr"),
+                self._ptr("t0"),
                 lat.data_ptr() if lat is not None else 0,
                 self._ptr("acl_wfrag"), self._ptr("acl_cinit"), self._acl_tiles,
                 self._ptr("toep_frag"), self._ptr("toep_tab"),
-                self.hash_mode, self.acl_mode, self.num_cus, s,
+                self.hash_mode, self.acl_mode, self.num_cus, s, flags,
             )
             return BatchResult(out, meta, n, {"lat": lat})
         pk = np.ascontiguousarray(pkts, np.uint8)
@@ -248,7 +244,7 @@ class DataPlane:
         """Read-and-reset the packed per-flow counters into 64-bit host totals."""
         if "flow_ctr" not in self._dev:
             return
-        n = self.flows.nbuckets * 8
+        n = self.flows.nbuckets * 4
         if self.gpu:
             torch = _torch()
             tmp = torch.empty(n, dtype=torch.int64, device=self.tdev)

@@ -72,9 +72,7 @@ class ShardedDataPlane:
         self.out_meta = torch.zeros(batch, **i32)
         self.lat = torch.zeros((batch + 15) // 16, **i32)
         self.lat2 = torch.zeros((world * self.cap_pkt + 15) // 16, **i32)
-        self.port_ctr = dp._dev["port_ctr"]
-        self.drop_ctr = dp._dev["drop_ctr"]
-        self.t0 = dp._dev["t0"]
+        self.t0 = torch.zeros(1, dtype=torch.int64, device=self.dev)  # this engine's batch-release stamp
 
     @staticmethod
     def _p(t) -> int:
@@ -120,12 +118,12 @@ class ShardedDataPlane:
         app = dict(self._geom(), pkts=p(pkts), inmeta=p(inmeta), n=n, ref=p(self.ref), aux=p(self.aux),
                    recv_verdict=p(self.recv_verdict), out=p(self.out), out_meta=p(self.out_meta),
                    send_pkt=p(self.send_pkt), pcnt=p(self.pcnt), port_ctr=dp._ptr("port_ctr"),
-                   drop_ctr=dp._ptr("drop_ctr"), t0=dp._ptr("t0"), lat=p(self.lat))
+                   drop_ctr=dp._ptr("drop_ctr"), t0=p(self.t0), lat=p(self.lat))
         self.nf.shard_apply(dp.tables_ptrs(), app, self.gpu, dp.num_cus, self._stream())
 
     def phase_egress(self) -> None:
         dp, p = self.dp, self._p
-        eg = dict(self._geom(), recv_pkt=p(self.recv_pkt), port_ctr=dp._ptr("port_ctr"), t0=dp._ptr("t0"),
+        eg = dict(self._geom(), recv_pkt=p(self.recv_pkt), port_ctr=dp._ptr("port_ctr"), t0=p(self.t0),
                   lat=p(self.lat2))
         self.nf.shard_egress(eg, self.gpu, dp.num_cus, self._stream())
 
@@ -185,3 +183,68 @@ def simulate_step(engines: list, batches: list) -> None:
     _local_a2a(engines, "send_pkt", "recv_pkt", engines[0].pseg)
     for e in engines:
         e.phase_egress()
+
+
+class PipelinedShardedDataPlane:
+    """Chunked, software-pipelined sharded step: the batch is cut into `chunks` pieces and the
+    stages of different chunks overlap, so the xGMI all-to-alls (RCCL stream) run while the
+    compute stream processes other chunks.  Issue order per iteration k (chunk indices):
+
+        egress(k-3) | apply(k-2) -> a2a_pkt(k-2) | owner(k-1) -> a2a_verdict(k-1) |
+        ingress(k) -> a2a_desc(k)
+
+    each consumer waits only on its own collective (Work.wait() = a stream-side wait), and a ring
+    of 4 buffer sets is enough because a chunk's buffers are last touched 3 iterations after its
+    ingress.
+    """
+
+    RING = 4
+
+    def __init__(self, dp: DataPlane, rank: int, world: int, batch: int, chunks: int = 4, group=None, **kw):
+        self.chunks = max(1, chunks)
+        self.chunk = int(math.ceil(batch / self.chunks))
+        self.rank, self.world, self.batch, self.group = rank, world, batch, group
+        self.slots = [ShardedDataPlane(dp, rank, world, self.chunk, group=group, **kw)
+                      for _ in range(min(self.RING, self.chunks))]
+
+    def _slot(self, c: int) -> ShardedDataPlane:
+        return self.slots[c % len(self.slots)]
+
+    def _a2a(self, c: int, kind: str):
+        e = self._slot(c)
+        send, recv = {"d": (e.send_desc, e.recv_desc), "v": (e.send_verdict, e.recv_verdict),
+                      "p": (e.send_pkt, e.recv_pkt)}[kind]
+        return dist.all_to_all_single(recv, send, group=self.group, async_op=True)
+
+    def step(self, pkts: torch.Tensor, inmeta: torch.Tensor) -> None:
+        n = int(pkts.shape[0])
+        C = min(self.chunks, (n + self.chunk - 1) // self.chunk)
+        if len(self.slots) < min(self.RING, C):
+            raise RuntimeError("ring too small")
+        works = {}
+        for k in range(C + 3):
+            c = k - 3
+            if 0 <= c < C:
+                works.pop((c, "p")).wait()
+                self._slot(c).phase_egress()
+            c = k - 2
+            if 0 <= c < C:
+                works.pop((c, "v")).wait()
+                self._slot(c).phase_apply()
+                works[(c, "p")] = self._a2a(c, "p")
+            c = k - 1
+            if 0 <= c < C:
+                works.pop((c, "d")).wait()
+                self._slot(c).phase_owner()
+                works[(c, "v")] = self._a2a(c, "v")
+            c = k
+            if c < C:
+                lo, hi = c * self.chunk, min(n, (c + 1) * self.chunk)
+                self._slot(c).phase_ingress(pkts[lo:hi], inmeta[lo:hi])
+                works[(c, "d")] = self._a2a(c, "d")
+
+    def out_meta(self) -> np.ndarray:
+        return np.concatenate([e.out_meta.cpu().numpy().view(np.uint32)[: e._cur[2]] for e in self.slots])
+
+    def latency_samples_us(self) -> np.ndarray:
+        return np.concatenate([e.latency_samples_us() for e in self.slots])

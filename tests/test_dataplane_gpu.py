@@ -15,7 +15,7 @@ def _torch():
     return torch
 
 
-def _build(device, hash_mode="mfma", acl_mode="mfma", n_flows=1 << 14, n_acl=200, seed=0, buckets=1 << 12, **kw):
+def _build(device, hash_mode="mfma", acl_mode="mfma", n_flows=1 << 14, n_acl=200, seed=0, buckets=1 << 13, **kw):
     dp = DataPlane(device=device, flow_buckets=buckets, hash_mode=hash_mode, acl_mode=acl_mode)
     sc = S.build_sfc(dp, n_pods=16, n_flows=n_flows, n_acl=n_acl, seed=seed, **kw)
     # rules that really match traffic, at random priorities before the final permit
@@ -95,7 +95,7 @@ def test_incremental_flow_updates_on_device():
     rc = c.run(pk, im)
     torch.cuda.synchronize()
     assert np.array_equal(r.meta.cpu().numpy().view(np.uint32), rc.meta)
-    assert np.array_equal(g._dev["tags"].cpu().numpy(), g.flows.t.tags().view(np.uint8))
+    assert np.array_equal(g._dev["flows"].cpu().numpy(), g.flows.t.slots().view(np.uint8).reshape(-1))
 
 
 @pytest.mark.parametrize("world", [2, 4])
@@ -108,11 +108,11 @@ def test_sharded_kernels_simulated_ranks(world):
     n_pods = 4 * world
     pod_gpu = np.arange(n_pods) // 4
     engines, batches, refs = [], [], []
-    oracle_dp = DataPlane("cpu", flow_buckets=1 << 12)
+    oracle_dp = DataPlane("cpu", flow_buckets=1 << 14)
     sc0 = S.build_sfc(oracle_dp, n_pods=n_pods, n_flows=20000, n_acl=64, pod_gpu=pod_gpu)
     oracle_dp.commit()
     for r in range(world):
-        dp = DataPlane("cuda", flow_buckets=1 << 12)
+        dp = DataPlane("cuda", flow_buckets=1 << 13)
         sc = S.build_sfc(dp, n_pods=n_pods, n_flows=20000, n_acl=64, pod_gpu=pod_gpu, flow_filter=shard_filter(r, world))
         dp.commit(full=True)
         pk, im = S.traffic(sc, 6000, seed=20 + r, src_pods=np.where(pod_gpu == r)[0])

@@ -81,7 +81,7 @@ def test_acl_fragments_emulated(nf):
 
 
 def test_flow_table_cuckoo_high_load(nf):
-    ft = T.FlowTable(1 << 10)  # 8192 slots
+    ft = T.FlowTable(1 << 11)  # 8192 slots (4 per 128-B bucket)
     rng = np.random.default_rng(3)
     n = 7000  # 85% load: forces evictions
     keys = rng.integers(0, 2**32, (n, 4), dtype=np.uint64).astype(np.uint32)
@@ -90,10 +90,10 @@ def test_flow_table_cuckoo_high_load(nf):
     acts = T.flow_action(chain_id=1, out_port=np.arange(len(keys)) % 4096, flow_id=np.arange(len(keys)))
     ft.insert_many(keys, acts)
     assert len(ft) == len(keys)
-    vals = ft.t.vals()
+    slots = ft.t.slots()
     for i in rng.choice(len(keys), 300, replace=False):
         s = ft.find(keys[i])
-        assert s >= 0 and vals[s][3] == i
+        assert s >= 0 and slots[s][7] == i and slots[s][3] == (keys[i][3] | 0x100)
     # erase half, the rest still found
     for i in range(0, len(keys), 2):
         assert ft.erase(keys[i])
@@ -131,7 +131,7 @@ def test_packet_craft_checksums():
 
 @pytest.fixture(scope="module")
 def sfc():
-    dp = DataPlane("cpu", flow_buckets=1 << 12)
+    dp = DataPlane("cpu", flow_buckets=1 << 14)
     sc = S.build_sfc(dp, n_pods=8, n_flows=20000, n_acl=64, seed=0)
     dp.commit()
     return dp, sc

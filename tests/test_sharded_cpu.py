@@ -17,7 +17,7 @@ def _free_port() -> int:
     return p
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, pipelined=False):
     import sys
 
     import torch
@@ -34,23 +34,35 @@ def _worker(rank, world, port, q):
     try:
         n_pods = 4 * world
         pod_gpu = np.arange(n_pods) // 4
-        dp = DataPlane("cpu", flow_buckets=1 << 12)
+        dp = DataPlane("cpu", flow_buckets=1 << 13)
         sc = S.build_sfc(dp, n_pods=n_pods, n_flows=20000, n_acl=32, pod_gpu=pod_gpu,
                          flow_filter=shard_filter(rank, world))
         dp.commit()
         pk, im = S.traffic(sc, 3000, seed=10 + rank, src_pods=np.where(pod_gpu == rank)[0])
-        eng = ShardedDataPlane(dp, rank, world, 3000)
-        eng.step(torch.from_numpy(pk), torch.from_numpy(im.view(np.int32)))
-        rs = P.meta_fields(eng.out_meta.numpy().view(np.uint32))[2]
-        ref = DataPlane("cpu", flow_buckets=1 << 13)
+        if pipelined:
+            from dpu_operator_amd.parallel.sharded import PipelinedShardedDataPlane
+
+            peng = PipelinedShardedDataPlane(dp, rank, world, 3000, chunks=4)
+            peng.step(torch.from_numpy(pk), torch.from_numpy(im.view(np.int32)))
+            meta = peng.out_meta()
+            outs = np.concatenate([e.out.numpy()[: e._cur[2]] for e in peng.slots])
+            rxs = [e.received()[0] for e in peng.slots]
+            rx = np.concatenate(rxs)
+        else:
+            eng = ShardedDataPlane(dp, rank, world, 3000)
+            eng.step(torch.from_numpy(pk), torch.from_numpy(im.view(np.int32)))
+            meta = eng.out_meta.numpy().view(np.uint32)
+            outs = eng.out.numpy()
+            rx, _ = eng.received()
+        rs = P.meta_fields(meta)[2]
+        ref = DataPlane("cpu", flow_buckets=1 << 14)
         S.build_sfc(ref, n_pods=n_pods, n_flows=20000, n_acl=32, pod_gpu=pod_gpu)
         ref.commit()
         rr = ref.run(pk, im)
         rrs = P.meta_fields(rr.meta)[2]
         ok = bool(((rs == 10) | (rs == rrs)).all())
         loc = rs == 0
-        ok &= bool(np.array_equal(eng.out.numpy()[loc], rr.out[loc]))
-        rx, _ = eng.received()
+        ok &= bool(np.array_equal(outs[loc], rr.out[loc]))
         objs = [None] * world
         dist.all_gather_object(objs, rx.tobytes())
         allrx = b"".join(objs)
@@ -63,12 +75,12 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_sharded_gloo(world):
+@pytest.mark.parametrize("world,pipelined", [(2, False), (3, False), (2, True), (3, True)])
+def test_sharded_gloo(world, pipelined):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, pipelined)) for r in range(world)]
     for p in procs:
         p.start()
     res = [q.get(timeout=240) for _ in range(world)]

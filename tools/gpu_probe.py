@@ -90,7 +90,7 @@ def main():
     for (hm, am, nacl) in (("mfma", "mfma", 256), ("lds", "mfma", 256), ("lds", "scalar", 256), ("lds", "off", 0),
                            ("mfma", "mfma", 1024), ("lds", "scalar", 1024), ("mfma", "off", 0)):
         t0 = time.time()
-        g = DataPlane(device=dev, flow_buckets=1 << 18, hash_mode=hm, acl_mode=am)
+        g = DataPlane(device=dev, flow_buckets=1 << 19, hash_mode=hm, acl_mode=am)
         sc = S.build_sfc(g, n_pods=16, n_flows=1 << 20, n_acl=nacl, seed=1)
         g.commit(full=True)
         nb = 1 << 22
