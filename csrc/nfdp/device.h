@@ -122,26 +122,23 @@ __device__ __forceinline__ int64_t flow_probe(const TablesView& t, const FlowKey
   const TableHash th = table_hash(h, t.bucket_mask);
   const uint4* fl = reinterpret_cast<const uint4*>(t.flows);
   const uint32_t used = k.meta | kSlotUsed;
+  static_assert(kBucketSlots == 4, "probe is written for 4-slot buckets");
+  // Named registers, no private array: an indexed local array lands in scratch.
+  auto eq = [&](const uint4& e) {
+    return e.x == k.src_ip && e.y == k.dst_ip && e.z == k.ports && e.w == used;
+  };
+  uint32_t b = th.b1;
 #pragma unroll
   for (int c = 0; c < 2; ++c) {
-    const uint32_t b = c ? th.b2 : th.b1;
     const uint4* row = fl + (size_t)b * (kBucketSlots * 2);
-    uint4 r[kBucketSlots * 2];
-#pragma unroll
-    for (int q = 0; q < kBucketSlots * 2; ++q) r[q] = row[q];
-    int hit = -1;
-#pragma unroll
-    for (int s = kBucketSlots - 1; s >= 0; --s) {
-      const uint4 e = r[2 * s];
-      if (e.x == k.src_ip && e.y == k.dst_ip && e.z == k.ports && e.w == used) hit = s;
+    const uint4 k0 = row[0], a0 = row[1], k1 = row[2], a1 = row[3];
+    const uint4 k2 = row[4], a2 = row[5], k3 = row[6], a3 = row[7];
+    const bool m0 = eq(k0), m1 = eq(k1), m2 = eq(k2), m3 = eq(k3);
+    if (m0 | m1 | m2 | m3) {
+      act = m0 ? a0 : m1 ? a1 : m2 ? a2 : a3;
+      return (int64_t)b * kBucketSlots + (m0 ? 0 : m1 ? 1 : m2 ? 2 : 3);
     }
-    if (hit >= 0) {
-      uint4 a = r[1];
-#pragma unroll
-      for (int s = 1; s < kBucketSlots; ++s) a = (hit == s) ? r[2 * s + 1] : a;
-      act = a;
-      return (int64_t)b * kBucketSlots + hit;
-    }
+    b = th.b2;
   }
   return -1;
 }

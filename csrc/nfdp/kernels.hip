@@ -57,7 +57,7 @@ __host__ __device__ inline LdsLayout lds_layout(int hash_mode, int acl_mode, uin
 }
 
 template <int HASH, int ACL>
-__global__ __launch_bounds__(kBlock) void fused_kernel(FusedArgs a) {
+__global__ __launch_bounds__(kBlock, 4) void fused_kernel(FusedArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const LdsLayout L = lds_layout(HASH, ACL, a.acl_tiles);
   v4i* lw = reinterpret_cast<v4i*>(smem + L.acl_w);

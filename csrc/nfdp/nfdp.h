@@ -298,16 +298,24 @@ NFDP_HD void act_snat(Parsed& p, uint32_t new_ip, uint32_t new_port) {
   set_raw16(p.s, 24, ipc);
   set_raw32_at2(p.s, 26, new_ip);
   if (p.l4) {
+    // TCP csum at L4+16 (byte 50), UDP at L4+6 (byte 40).  Both offsets are compile-time
+    // constants on purpose: a runtime index into p.s[] would put the whole frame in scratch.
     const uint32_t proto = p.s[5] >> 24;
-    const int coff = proto == 6 ? 50 : 40;  // TCP csum at L4+16, UDP at L4+6
     const uint32_t old_port = raw16_at(p.s, 34);
-    if (coff + 2 <= (int)p.len) {
-      uint32_t c = raw16_at(p.s, coff);
-      if (proto == 6 || c != 0) {           // UDP csum 0 = disabled
+    if (proto == 6) {
+      if (52 <= p.len) {
+        uint32_t c = raw16_at(p.s, 50);
         c = csum_update32(c, old_ip, new_ip);
         c = csum_update16(c, old_port, new_port);
-        if (proto == 17 && c == 0) c = 0xFFFFu;
-        set_raw16(p.s, coff, c);
+        set_raw16(p.s, 50, c);
+      }
+    } else {
+      uint32_t c = raw16_at(p.s, 40);
+      if (c != 0) {                          // UDP csum 0 = disabled
+        c = csum_update32(c, old_ip, new_ip);
+        c = csum_update16(c, old_port, new_port);
+        if (c == 0) c = 0xFFFFu;
+        set_raw16(p.s, 40, c);
       }
     }
     set_raw16(p.s, 34, new_port);

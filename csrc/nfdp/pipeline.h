@@ -64,12 +64,15 @@ NFDP_HD EgressDecision chain_stage(const TablesView& t, Parsed& p, const Ingress
     e.out_port = (uint32_t)op;
   } else {
     e.out_port = act.out_port;
-    ChainEntry ch;
-    ch.nhops = 0;
-    if (act.chain_id < t.n_chains) ch = t.chains[act.chain_id];
-    const int nh = ch.nhops < kMaxHops ? ch.nhops : kMaxHops;
-    for (int i = 0; i < nh; ++i) {
-      const uint8_t op = ch.hop[i];
+    // nhops + 7 hop opcodes = the chain entry's first 8 bytes, read as one word and decoded with
+    // compile-time shifts (indexing a private hop[] array at run time would spill to scratch).
+    uint64_t hw = 0;
+    if (act.chain_id < t.n_chains) hw = *reinterpret_cast<const uint64_t*>(&t.chains[act.chain_id]);
+    const uint32_t nh = (uint32_t)(hw & 0xFFu);
+#pragma unroll
+    for (int i = 0; i < kMaxHops; ++i) {
+      if ((uint32_t)i >= nh) break;
+      const uint8_t op = (uint8_t)((hw >> (8 * (i + 1))) & 0xFFu);
       if (op == kHopAcl) {
         const bool permit = acl_rule >= 0 ? t.acl_permit[acl_rule] != 0 : t.acl_default_permit != 0;
         if (!permit) { e.reason = kAclDeny; e.out_port = kPortNone; return e; }

@@ -289,16 +289,19 @@ __global__ __launch_bounds__(256) void egress_kernel(EgressArgs a) {
 // ------------------------------------------------------------------------------------------
 template <int H, int A>
 static hipError_t launch_ingress_t(const IngressArgs& a, int num_cus, hipStream_t s) {
+  // static LDS of the kernel (reservation counters) + dynamic tables must fit 160 KiB
+  constexpr size_t kStatic = 2 * kMaxRanks * sizeof(uint32_t);
+  constexpr size_t kMaxDyn = 160 * 1024 - kStatic;
   const size_t lds = shard_lds(H, A, a.acl_tiles, false).total;
-  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  if (lds > kMaxDyn) return hipErrorInvalidValue;
   static bool attr = false;
   if (!attr) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&ingress_kernel<H, A>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxDyn);
     if (e != hipSuccess) return e;
     attr = true;
   }
-  int per_cu = (int)((160 * 1024) / lds);
+  int per_cu = (int)((160 * 1024) / (lds + kStatic));
   per_cu = per_cu < 1 ? 1 : (per_cu > 4 ? 4 : per_cu);
   uint32_t grid = (uint32_t)(per_cu * num_cus);
   const uint32_t need = (a.n + kBlock - 1) / kBlock;

@@ -79,8 +79,8 @@ def test_counters_match_oracle():
 def test_incremental_flow_updates_on_device():
     """Bucket-row pushes (bucket_update_kernel) keep HBM identical to the host table."""
     torch = _torch()
-    g, sc = _build("cuda", n_flows=4000, buckets=1 << 10)
-    c, _ = _build("cpu", n_flows=4000, buckets=1 << 10)
+    g, sc = _build("cuda", n_flows=4000, buckets=1 << 11)
+    c, _ = _build("cpu", n_flows=4000, buckets=1 << 11)
     rng = np.random.default_rng(11)
     # erase some flows, re-point others, add new ones
     for dp in (g, c):
