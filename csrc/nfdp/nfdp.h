@@ -59,6 +59,7 @@ enum PortFlags : uint32_t {
   kPortTagEgress = 1u << 3,     // push port.vlan on egress (K6 vlan_push to host VF)
   kPortVlanBridge = 1u << 4,    // ingress vid selects bridge id (K7)
   kPortTrust = 1u << 5,
+  kPortHasDefault = 1u << 6,    // L2 miss -> default_out instead of punt (OvS in_port=X,actions=output:Y)
 };
 
 // chain hop opcodes (built-in GPU network functions)
@@ -86,7 +87,7 @@ struct alignas(16) PortEntry {   // 32 B
   uint16_t gpu;                  // owning GPU rank (egress side)
   uint32_t peer_mac_lo;          // MAC of whatever is attached (pod / NF / next hop)
   uint16_t peer_mac_hi;
-  uint16_t pad0;
+  uint16_t default_out;          // with kPortHasDefault: egress port on an L2 (flow + MAC) miss
   uint32_t pad1, pad2;
 };
 static_assert(sizeof(PortEntry) == 32, "PortEntry");

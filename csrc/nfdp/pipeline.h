@@ -59,9 +59,17 @@ NFDP_HD EgressDecision chain_stage(const TablesView& t, Parsed& p, const Ingress
   if (e.reason) return e;
   bool vlan_done = false;
   if (!hit) {
+    // (bridge, dst MAC) table = OvS `in_port=X,dl_dst=M` / P4 l2_fwd; output == in_port is the
+    // OvS hairpin.  A miss falls back to the ingress port's default output (`in_port=X ->
+    // output:Y`, priority 10 in ovsdp.go:133-139) or is punted to the slow path.
     const int op = mac_lookup(t, st.bridge, dmac_lo(p.s), dmac_hi(p.s));
-    if (op < 0) { e.out_port = kPortPunt; e.reason = kNoRoute; return e; }
-    e.out_port = (uint32_t)op;
+    if (op >= 0) {
+      e.out_port = (uint32_t)op;
+    } else {
+      const PortEntry& ip = t.ports[st.in_port < (uint32_t)kMaxPorts ? st.in_port : 0];
+      if (!(ip.flags & kPortHasDefault)) { e.out_port = kPortPunt; e.reason = kNoRoute; return e; }
+      e.out_port = ip.default_out;
+    }
   } else {
     e.out_port = act.out_port;
     // nhops + 7 hop opcodes = the chain entry's first 8 bytes, read as one word and decoded with

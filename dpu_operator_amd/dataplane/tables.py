@@ -32,6 +32,7 @@ PORT_VLAN_ISOLATE = 1 << 2
 PORT_TAG_EGRESS = 1 << 3
 PORT_VLAN_BRIDGE = 1 << 4
 PORT_TRUST = 1 << 5
+PORT_HAS_DEFAULT = 1 << 6
 
 # hop opcodes (nfdp.h Hop)
 HOP_NONE, HOP_ACL, HOP_NAT, HOP_L2FWD, HOP_TTL, HOP_HAIRPIN, HOP_VLAN, HOP_DROP, HOP_PUNT = range(9)
@@ -50,7 +51,7 @@ PORT_DTYPE = np.dtype(
     [
         ("flags", "<u4"), ("vlan", "<u2"), ("bridge_id", "<u2"),
         ("mac_lo", "<u4"), ("mac_hi", "<u2"), ("gpu", "<u2"),
-        ("peer_mac_lo", "<u4"), ("peer_mac_hi", "<u2"), ("pad0", "<u2"),
+        ("peer_mac_lo", "<u4"), ("peer_mac_hi", "<u2"), ("default_out", "<u2"),
         ("pad1", "<u4"), ("pad2", "<u4"),
     ]
 )
@@ -117,12 +118,32 @@ class PortTable:
         self.version = 0
 
     def set(self, idx: int, *, flags=PORT_VALID, vlan=0, bridge_id=0, mac="00:00:00:00:00:00",
-            peer_mac="00:00:00:00:00:00", gpu=0) -> None:
+            peer_mac="00:00:00:00:00:00", gpu=0, default_out: int | None = None) -> None:
         if not 0 <= idx < MAX_PORTS:
             raise ValueError(f"port index {idx} out of range")
         lo, hi = mac_raw(mac)
         plo, phi = mac_raw(peer_mac)
-        self.a[idx] = (flags | PORT_VALID, vlan, bridge_id, lo, hi, gpu, plo, phi, 0, 0, 0)
+        if default_out is not None:
+            flags |= PORT_HAS_DEFAULT
+        self.a[idx] = (flags | PORT_VALID, vlan, bridge_id, lo, hi, gpu, plo, phi,
+                       0 if default_out is None else default_out, 0, 0)
+        self.version += 1
+
+    def update(self, idx: int, **fields) -> None:
+        """Change individual fields of an existing port (e.g. default_out when an NF appears)."""
+        for k, v in fields.items():
+            if k == "default_out":
+                if v is None:
+                    self.a[idx]["flags"] &= ~np.uint32(PORT_HAS_DEFAULT)
+                else:
+                    self.a[idx]["flags"] |= np.uint32(PORT_HAS_DEFAULT)
+                    self.a[idx]["default_out"] = v
+            elif k in ("mac", "peer_mac"):
+                lo, hi = mac_raw(v)
+                pre = "" if k == "mac" else "peer_"
+                self.a[idx][pre + "mac_lo"], self.a[idx][pre + "mac_hi"] = lo, hi
+            else:
+                self.a[idx][k] = v
         self.version += 1
 
     def clear(self, idx: int) -> None:

@@ -1,0 +1,9 @@
+from .registry import (  # noqa: F401
+    DEVICE_PLUGIN_VERSION,
+    HEALTHY,
+    UNHEALTHY,
+    GoogleEmpty,
+    deviceplugin,
+    opi,
+    vendor,
+)
