@@ -16,6 +16,19 @@ def new_cni_request(env: dict | None = None, stdin: bytes = b"") -> Request:
     return Request(env=keep, config=stdin)
 
 
+def _go_fields(d: dict, fields: set[str]) -> dict:
+    """Map JSON keys onto field names the way Go's encoding/json does: an exact key wins, else a
+    case-insensitive match (so `"EffectiveMac"` fills EffectiveMAC, as the reference's tests use)."""
+    lower = {f.lower(): f for f in fields}
+    out: dict = {}
+    for k, v in d.items():
+        if k in fields:
+            out[k] = v
+        elif k.lower() in lower and lower[k.lower()] not in d:
+            out.setdefault(lower[k.lower()], v)
+    return out
+
+
 def read_cni_config(b: bytes) -> NetConf:
     """Parse a network config (JSON) including an optional prevResult."""
     try:
@@ -25,12 +38,11 @@ def read_cni_config(b: bytes) -> NetConf:
     if not isinstance(d, dict):
         raise ValueError("network config must be a JSON object")
     conf = NetConf(raw=d)
-    for k, v in d.items():
-        if k in _NETCONF_FIELDS:
-            setattr(conf, k, v)
-    ovs = d.get("OrigVfState")
+    for k, v in _go_fields(d, _NETCONF_FIELDS).items():
+        setattr(conf, k, v)
+    ovs = _go_fields(d, {"OrigVfState"}).get("OrigVfState")
     if isinstance(ovs, dict):
-        conf.OrigVfState = VfState(**{k: v for k, v in ovs.items() if k in VfState.__dataclass_fields__})
+        conf.OrigVfState = VfState(**_go_fields(ovs, set(VfState.__dataclass_fields__)))
     if conf.prevResult is not None and not isinstance(conf.prevResult, dict):
         raise ValueError("prevResult must be an object")
     return conf

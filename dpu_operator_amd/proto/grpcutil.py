@@ -54,8 +54,8 @@ def retry_service_config(max_attempts: int = 40, initial: str = "1s", max_backof
         "methodConfig": [{
             "name": [{}],
             "waitForReady": True,
-            "retryPolicy": {"MaxAttempts": max_attempts, "InitialBackoff": initial, "MaxBackoff": max_backoff,
-                            "BackoffMultiplier": 2.0, "RetryableStatusCodes": ["UNAVAILABLE"]},
+            "retryPolicy": {"maxAttempts": max_attempts, "initialBackoff": initial, "maxBackoff": max_backoff,
+                            "backoffMultiplier": 2.0, "retryableStatusCodes": ["UNAVAILABLE"]},
         }]
     })
 

@@ -45,7 +45,7 @@ class PathManager:
         return os.path.basename(self.plugin_endpoint())
 
     def cni_path(self) -> str:
-        return "/var/lib/cni/bin/dpu-cni"
+        return self.wrap("/var/lib/cni/bin/dpu-cni")
 
     def vendor_plugin_socket(self) -> str:
         return self.wrap("/var/run/dpu-daemon/vendor-plugin/vendor-plugin.sock")

@@ -1,0 +1,274 @@
+"""GPU VSP: the Vendor Specific Plugin whose data plane is the MI355X pipeline.
+
+It implements the same four services as the reference's VSPs, but instead of programming OvS
+(marvell/main.go:347-563, ovs-dp/ovsdp.go:113-162) or P4 tables through p4rt-ctl
+(vendor/.../ipuplugin/bridgeport.go, p4rtclient.go) it writes rows of the GPU tables
+(dataplane/tables.py) and commits them to HBM between batches:
+
+* SetNumVfs(n)            -> n vports (netdevs handed to pods by the device plugin + CNI)
+* CreateBridgePort(hostP-V, mac, [vlan]) -> VF port: VLAN isolation (vid = logical bridge),
+                             spoof-check on the pod MAC, egress tagging, (bridge, MAC) entry
+* CreateNetworkFunction(in_mac, out_mac) -> NF steering, OvS-equivalent:
+      VF  -> NF-in                      (K11  in_port=vf,actions=output:nf_in)
+      NF-in, dst=VF MAC -> VF           (K12  in_port=nf_in,dl_dst=M,actions=output:vf)
+      NF-out, dst=VF MAC -> NF-out      (K13  hairpin, in_port action)
+      NF-out -> wire, wire -> NF-out    (K11 both ways)
+* gpu-nf:// chains from the SFC reconciler -> chain-table entries (NFs run inside the kernel)
+
+Ports: vport i = data-plane port i; the uplink ("wire", the RPM/SFP port of the reference's VSPs)
+is port 4000.  All mutations happen under the VSP lock and are committed atomically per RPC.
+"""
+from __future__ import annotations
+
+import logging
+import os
+import re
+import socket
+
+import numpy as np
+
+from ..cni.netlink import FakeNetlink, Link, NetlinkManager
+from ..dataplane import tables as T
+from ..dataplane.engine import DataPlane
+from .base import VspBase
+
+log = logging.getLogger("dpu.vsp.gpu")
+
+WIRE_PORT = 4000
+VF_BRIDGE = 1
+STEER_BRIDGE = 2      # no MAC entries: every frame takes its port's default output
+NF_BRIDGE_BASE = 100
+
+
+def _mac_str(b: bytes) -> str:
+    return ":".join(f"{x:02x}" for x in b)
+
+
+def _local_mac(i: int, salt: int) -> str:
+    return "02:%02x:%02x:%02x:%02x:%02x" % (0xD0 | (salt & 0xF), (i >> 16) & 0xFF, (i >> 8) & 0xFF, i & 0xFF, salt >> 4 & 0xFF)
+
+
+class GpuVsp(VspBase):
+    name = "amd-gpu-vsp"
+
+    def __init__(self, path_manager=None, device: str | None = None, nl: NetlinkManager | None = None,
+                 opi_port: int = 0, flow_buckets: int = 1 << 16, vport_prefix: str = "dpuvp",
+                 hash_mode: str = "mfma", acl_mode: str = "mfma"):
+        super().__init__(path_manager)
+        if device is None:
+            try:
+                import torch
+
+                device = "cuda" if torch.cuda.is_available() else "cpu"
+            except Exception:  # noqa: BLE001
+                device = "cpu"
+        self.device = device
+        self.nl = nl or FakeNetlink()
+        self.opi_port = opi_port
+        self.flow_buckets = flow_buckets
+        self.prefix = vport_prefix
+        self.hash_mode, self.acl_mode = hash_mode, acl_mode
+        self.dp: DataPlane | None = None
+        self.vports: dict[int, dict] = {}          # idx -> {name, mac, role, vlan, pod_mac}
+        self.bridge_ports: dict[str, int] = {}     # "hostP-V" -> vport idx
+        self.nfs: list[dict] = []                  # {in, out, in_mac, out_mac}
+        self.gpu_chains: dict[str, int] = {}
+        self.dpu_mode = True
+        self.healthy = True
+        self._salt = int.from_bytes(os.urandom(1), "little")
+
+    # ------------------------------------------------------------------ helpers
+    def _ensure_dp(self) -> DataPlane:
+        if self.dp is None:
+            self.dp = DataPlane(device=self.device, flow_buckets=self.flow_buckets, hash_mode=self.hash_mode,
+                                acl_mode=self.acl_mode)
+            self.dp.ports.set(WIRE_PORT, flags=T.PORT_VALID, bridge_id=VF_BRIDGE, mac="02:00:00:00:0f:a0")
+            self.dp.commit(full=True)
+        return self.dp
+
+    def _commit(self) -> None:
+        self.dp.commit()
+
+    def _vport_by_mac(self, mac: str) -> int:
+        mac = mac.lower()
+        for i, v in self.vports.items():
+            if v["mac"] == mac:
+                return i
+        # the NF pod may have been given the vport under another name: ask netlink
+        raise KeyError(f"no vport with MAC {mac}")
+
+    def _free_port(self) -> int:
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        p = s.getsockname()[1]
+        s.close()
+        return p
+
+    def _vf_ports(self) -> list[int]:
+        return sorted(self.bridge_ports.values())
+
+    def _program_port(self, i: int) -> None:
+        v = self.vports[i]
+        dp = self.dp
+        if v["role"] == "vf":
+            dp.ports.set(i, flags=T.PORT_VALID | T.PORT_SPOOFCHK | T.PORT_VLAN_ISOLATE | T.PORT_TAG_EGRESS,
+                         vlan=v["vlan"], bridge_id=VF_BRIDGE, mac=v["pod_mac"], peer_mac=v["pod_mac"],
+                         default_out=WIRE_PORT)
+        elif v["role"] in ("nf_in", "nf_out"):
+            dp.ports.set(i, flags=T.PORT_VALID, bridge_id=v["bridge"], mac=v["mac"], peer_mac=v["mac"])
+        else:
+            dp.ports.set(i, flags=T.PORT_VALID, bridge_id=VF_BRIDGE, mac=v["mac"], peer_mac=v["mac"],
+                         default_out=WIRE_PORT)
+
+    def _apply_steering(self) -> None:
+        """Recompute port programming + the (bridge, MAC) table from scratch (idempotent).
+
+        Without an NF, VFs and the wire share bridge 1 (plain L2 between pods, unknown dst -> wire).
+        With NFs chained NF0..NFk, VFs and the wire move to an empty "steer" bridge so every frame
+        misses the MAC table and takes its port's default output (OvS `in_port=X,actions=output:Y`):
+            VF -> NF0.in,  NFi.out -> NF(i+1).in (last -> wire),  wire -> NFk.out
+        and the NF-side bridges carry the return path:
+            (NF0.in bridge, VF MAC) -> VF;  (NFi.in bridge, VF MAC) -> NF(i-1).out;
+            (NFi.out bridge, VF MAC) -> NFi.out   (hairpin: pod-to-pod goes back through the NF)
+        """
+        dp = self.dp
+        for i in self.vports:
+            self._program_port(i)
+        dp.macs.a[:] = np.zeros((), T.MAC_DTYPE)
+        dp.macs.version += 1
+        vfs = self._vf_ports()
+        dp.ports.update(WIRE_PORT, default_out=None, bridge_id=VF_BRIDGE)
+        if not self.nfs:
+            for i in vfs:
+                dp.macs.insert(VF_BRIDGE, self.vports[i]["pod_mac"], i)
+        else:
+            for i in vfs:
+                dp.ports.update(i, default_out=self.nfs[0]["in"], bridge_id=STEER_BRIDGE)
+            for k, nfk in enumerate(self.nfs):
+                nxt = self.nfs[k + 1]["in"] if k + 1 < len(self.nfs) else WIRE_PORT
+                dp.ports.update(nfk["out"], default_out=nxt)
+                for i in vfs:
+                    m = self.vports[i]["pod_mac"]
+                    back = i if k == 0 else self.nfs[k - 1]["out"]
+                    dp.macs.insert(self.vports[nfk["in"]]["bridge"], m, back)          # K12
+                    dp.macs.insert(self.vports[nfk["out"]]["bridge"], m, nfk["out"])  # K13 hairpin
+            dp.ports.update(WIRE_PORT, default_out=self.nfs[-1]["out"], bridge_id=STEER_BRIDGE)
+        self._commit()
+
+    # ------------------------------------------------------------------ VSP hooks
+    def init(self, dpu_mode: bool, dpu_identifier: str):
+        self.dpu_mode = dpu_mode
+        self._ensure_dp()
+        if not self.opi_port:
+            self.opi_port = self._free_port()
+        return "127.0.0.1", self.opi_port
+
+    def set_num_vfs(self, n: int) -> int:
+        self._ensure_dp()
+        if n < 0 or n > 2048:
+            raise ValueError("vport count out of range")
+        for i in range(n):
+            if i in self.vports:
+                continue
+            name, mac = f"{self.prefix}{i}", _local_mac(i, self._salt)
+            if isinstance(self.nl, FakeNetlink):
+                self.nl.add_link(Link(name=name, mac=mac, up=True, kind="tap"))
+            self.vports[i] = {"name": name, "mac": mac, "role": "free", "vlan": 0, "pod_mac": mac, "bridge": VF_BRIDGE}
+            self._program_port(i)
+        for i in [i for i in self.vports if i >= n and self.vports[i]["role"] == "free"]:
+            self.dp.ports.clear(i)
+            del self.vports[i]
+        self._commit()
+        return n
+
+    def get_devices(self) -> dict[str, str]:
+        h = "Healthy" if self.healthy else "Unhealthy"
+        return {v["name"]: h for v in self.vports.values()}
+
+    def create_bridge_port(self, name, mac, ptype, logical_bridges):
+        m = re.fullmatch(r"host(\d+)-(\d+)", name)
+        if not m:
+            raise ValueError(f"bridge port name {name!r} is not host<pf>-<vf>")
+        vf = int(m.group(2))
+        if vf not in self.vports:
+            raise ValueError(f"VF {vf} does not exist (SetNumVfs first)")
+        vlan = int(logical_bridges[0]) if logical_bridges else vf + 2
+        if not 1 <= vlan <= 4094:
+            raise ValueError(f"logical bridge / vlan {vlan} out of range 1-4094")
+        v = self.vports[vf]
+        v.update(role="vf", vlan=vlan, pod_mac=_mac_str(mac) if mac else v["mac"])
+        self.bridge_ports[name] = vf
+        self._apply_steering()
+
+    def delete_bridge_port(self, name):
+        vf = self.bridge_ports.pop(name, None)
+        if vf is None:
+            return
+        v = self.vports[vf]
+        v.update(role="free", vlan=0, pod_mac=v["mac"])
+        self._apply_steering()
+
+    def create_network_function(self, inp: str, out: str):
+        i_in, i_out = self._vport_by_mac(inp), self._vport_by_mac(out)
+        k = len(self.nfs)
+        self.vports[i_in].update(role="nf_in", bridge=NF_BRIDGE_BASE + 2 * k)
+        self.vports[i_out].update(role="nf_out", bridge=NF_BRIDGE_BASE + 2 * k + 1)
+        self.nfs.append({"in": i_in, "out": i_out, "in_mac": inp.lower(), "out_mac": out.lower()})
+        self._apply_steering()
+
+    def delete_network_function(self, inp: str, out: str):
+        keep = []
+        for nf in self.nfs:
+            if nf["in_mac"] == inp.lower() and nf["out_mac"] == out.lower():
+                for i in (nf["in"], nf["out"]):
+                    self.vports[i].update(role="free", bridge=VF_BRIDGE)
+            else:
+                keep.append(nf)
+        self.nfs = keep
+        self._apply_steering()
+
+    def on_gpu_chain(self, sfc_name: str, kinds: list[str]) -> int:
+        with self._lock:
+            self._ensure_dp()
+            if sfc_name in self.gpu_chains:
+                cid = self.gpu_chains[sfc_name]
+                self.dp.chains.set(cid, kinds)
+            else:
+                cid = self.dp.chains.add(kinds)
+                self.gpu_chains[sfc_name] = cid
+            self._commit()
+            return cid
+
+    # ------------------------------------------------------------------ data path access
+    def install_flows(self, keys: np.ndarray, actions: np.ndarray) -> None:
+        with self._lock:
+            self._ensure_dp()
+            self.dp.flows.insert_many(keys, actions)
+            self._commit()
+
+    def process(self, frames: np.ndarray, in_ports) -> tuple[np.ndarray, np.ndarray]:
+        """Run a batch through the data plane: frames [n,64] uint8, in_ports [n] -> (out, meta)."""
+        from ..ops.packets import inmeta as mk_inmeta
+
+        with self._lock:
+            self._ensure_dp()
+            lens = np.array([self._frame_len(f) for f in frames], np.uint32)
+            im = mk_inmeta(np.asarray(in_ports), lens)
+            if self.dp.gpu:
+                import torch
+
+                r = self.dp.run(torch.from_numpy(np.ascontiguousarray(frames)).to(self.dp.tdev),
+                                torch.from_numpy(im.view(np.int32)).to(self.dp.tdev))
+                torch.cuda.synchronize()
+                return r.out.cpu().numpy(), r.meta.cpu().numpy().view(np.uint32)
+            r = self.dp.run(np.ascontiguousarray(frames), im)
+            return r.out, r.meta
+
+    @staticmethod
+    def _frame_len(f: np.ndarray) -> int:
+        et = (int(f[12]) << 8) | int(f[13])
+        off = 18 if et == 0x8100 else 14
+        et2 = (int(f[off - 2]) << 8) | int(f[off - 1])
+        if et2 == 0x0800:
+            return min(64, off + ((int(f[off + 2]) << 8) | int(f[off + 3])))
+        return 60 if et != 0x8100 else 64
