@@ -45,8 +45,17 @@ MODULES = {
     },
     "_agent": {
         "dir": CSRC / "agent",
-        "sources": ["mbox.cpp", "ctrl_net.cpp", "agent.cpp", "bindings.cpp"],
+        "sources": ["mbox.cpp", "ctrl_net.cpp", "config.cpp", "agent.cpp", "plugin_server.cpp", "bindings.cpp"],
         "hip": False,
+    },
+}
+
+# Standalone native executables (no Python): the node control agent daemon.
+EXES = {
+    "dpu-cp-agent": {
+        "dir": CSRC / "agent",
+        "module": "_agent",
+        "sources": ["mbox.cpp", "ctrl_net.cpp", "config.cpp", "agent.cpp", "plugin_server.cpp", "agent_main.cpp"],
     },
 }
 
@@ -104,6 +113,32 @@ def build_module(name: str, force: bool = False, verbose: bool = False) -> Path:
     return out
 
 
+def build_exe(name: str, force: bool = False, verbose: bool = False) -> Path:
+    """Link a standalone executable into dpu_operator_amd/native/bin/ (objects shared with the module)."""
+    spec = EXES[name]
+    d: Path = spec["dir"]
+    hdr = _newest_header(d)
+    objs, jobs = [], []
+    for s in spec["sources"]:
+        src = d / s
+        obj = BUILD / spec["module"] / (s + ".o")
+        objs.append(obj)
+        if force or not obj.exists() or obj.stat().st_mtime < max(src.stat().st_mtime, hdr):
+            jobs.append((src, obj))
+    for src, obj in jobs:
+        _compile(src, obj, False, verbose)
+    out = HERE / "bin" / name
+    out.parent.mkdir(exist_ok=True)
+    if force or jobs or not out.exists() or out.stat().st_mtime < max(o.stat().st_mtime for o in objs):
+        cmd = [shutil.which("g++") or "g++", "-pthread", *map(str, objs), "-o", str(out)]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"link failed: {name}\n{r.stdout}\n{r.stderr}")
+    return out
+
+
 def build_all(force: bool = False, verbose: bool = False) -> list[Path]:
     outs = []
     for name, spec in MODULES.items():
@@ -112,6 +147,8 @@ def build_all(force: bool = False, verbose: bool = False) -> list[Path]:
         if not all((spec["dir"] / s).exists() for s in spec["sources"]):
             continue
         outs.append(build_module(name, force=force, verbose=verbose))
+    for name in EXES:
+        outs.append(build_exe(name, force=force, verbose=verbose))
     return outs
 
 
