@@ -196,41 +196,53 @@ class MacTable:
             x = np.uint32(lo) ^ (np.uint32(hi) << np.uint32(16)) ^ (np.uint32(bridge) * np.uint32(0x9E3779B1))
         return int(fmix32(x)) & self.mask
 
-    def insert(self, bridge: int, mac, out_port: int) -> None:
-        lo, hi = mac_raw(mac)
+    # Deleted slots become tombstones (valid=2, bridge 0xFFFF which no port uses): the kernel's
+    # probe keeps walking over them (it stops only at valid == 0) and never matches them.
+    TOMBSTONE_BRIDGE = 0xFFFF
+
+    def _find(self, bridge: int, lo: int, hi: int) -> tuple[int, int]:
+        """-> (slot of the key or -1, first reusable slot or -1)."""
         h = self._h(bridge, lo, hi)
+        free = -1
         for p in range(16):
-            e = self.a[(h + p) & self.mask]
-            if not e["valid"] or (e["mac_lo"] == lo and e["mac_hi"] == hi and e["bridge_id"] == bridge):
-                self.a[(h + p) & self.mask] = (lo, hi, bridge, out_port, 1, 0)
-                self.version += 1
-                return
-        raise RuntimeError("MAC table probe limit reached")
+            i = (h + p) & self.mask
+            e = self.a[i]
+            if not e["valid"]:
+                return -1, free if free >= 0 else i
+            if e["valid"] == 2:
+                free = i if free < 0 else free
+            elif e["mac_lo"] == lo and e["mac_hi"] == hi and e["bridge_id"] == bridge:
+                return i, free
+        return -1, free
+
+    def insert(self, bridge: int, mac, out_port: int) -> None:
+        if not 0 <= bridge < self.TOMBSTONE_BRIDGE:
+            raise ValueError("bridge id must be in [0, 0xFFFF)")
+        lo, hi = mac_raw(mac)
+        at, free = self._find(bridge, lo, hi)
+        slot = at if at >= 0 else free
+        if slot < 0:
+            raise RuntimeError("MAC table probe limit reached")
+        self.a[slot] = (lo, hi, bridge, out_port, 1, 0)
+        self.version += 1
 
     def lookup(self, bridge: int, mac) -> int:
         lo, hi = mac_raw(mac)
-        h = self._h(bridge, lo, hi)
-        for p in range(16):
-            e = self.a[(h + p) & self.mask]
-            if not e["valid"]:
-                return -1
-            if e["mac_lo"] == lo and e["mac_hi"] == hi and e["bridge_id"] == bridge:
-                return int(e["out_port"])
-        return -1
+        at, _ = self._find(bridge, lo, hi)
+        return int(self.a[at]["out_port"]) if at >= 0 else -1
 
     def remove(self, bridge: int, mac) -> bool:
-        # rebuild the cluster to keep linear probing correct
-        entries = [(int(e["bridge_id"]), int(e["mac_lo"]), int(e["mac_hi"]), int(e["out_port"]))
-                   for e in self.a if e["valid"]]
         lo, hi = mac_raw(mac)
-        keep = [e for e in entries if not (e[0] == bridge and e[1] == lo and e[2] == hi)]
-        if len(keep) == len(entries):
+        at, _ = self._find(bridge, lo, hi)
+        if at < 0:
             return False
-        self.a[:] = np.zeros((), MAC_DTYPE)
-        for b, l, h, p in keep:
-            mac_b = bytes([l & 0xFF, (l >> 8) & 0xFF, (l >> 16) & 0xFF, (l >> 24) & 0xFF, h & 0xFF, (h >> 8) & 0xFF])
-            self.insert(b, mac_b, p)
+        self.a[at] = (0xFFFFFFFF, 0xFFFF, self.TOMBSTONE_BRIDGE, 0xFFFF, 2, 0)
+        self.version += 1
         return True
+
+    def clear(self) -> None:
+        self.a[:] = np.zeros((), MAC_DTYPE)
+        self.version += 1
 
 
 @dataclass

@@ -134,8 +134,7 @@ class GpuVsp(VspBase):
         dp = self.dp
         for i in self.vports:
             self._program_port(i)
-        dp.macs.a[:] = np.zeros((), T.MAC_DTYPE)
-        dp.macs.version += 1
+        dp.macs.clear()
         vfs = self._vf_ports()
         dp.ports.update(WIRE_PORT, default_out=None, bridge_id=VF_BRIDGE)
         if not self.nfs:
