@@ -42,6 +42,9 @@ TablesView tables_from(const py::dict& d) {
   t.acl_permit = ptr<const uint8_t>(d, "acl_permit");
   t.n_acl = val<uint32_t>(d, "n_acl", 0);
   t.acl_default_permit = val<uint32_t>(d, "acl_default_permit", 1);
+  t.lag_members = d.contains("lag_members") ? ptr<const uint16_t>(d, "lag_members") : nullptr;
+  t.n_lag_groups = val<uint32_t>(d, "n_lag_groups", 0);
+  if (t.n_lag_groups && !t.lag_members) throw std::invalid_argument("n_lag_groups > 0 but lag_members missing");
   if (!t.ports || !t.chains || !t.flows || !t.rss_key)
     throw std::invalid_argument("tables dict is missing a required buffer");
   if (t.n_acl && (!t.acl_value || !t.acl_mask || !t.acl_permit))

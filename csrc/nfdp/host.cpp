@@ -208,12 +208,12 @@ void oracle_run(const TablesView& t, const uint32_t* pkts, const uint32_t* inmet
         if (flow_ctr) flow_ctr[slot] += ctr_inc(st.wire_len);
       }
     }
-    const EgressDecision e = chain_stage(t, p, st, hit, act, acl);
+    const EgressDecision e = chain_stage(t, p, st, hit, act, acl, h);
     uint32_t o[kSlotDwords];
     emit(p, e.tci, e.push != 0, o);
     const uint32_t olen = e.reason ? 0u : p.len + (e.push ? 4u : 0u);
     std::memcpy(out + (size_t)i * kSlotDwords, o, sizeof(o));
-    out_meta[i] = make_meta(e.out_port, olen, e.reason);
+    out_meta[i] = make_meta(e.out_port, olen, e.reason, e.mirror != 0);
     if (port_ctr) {
       if (st.in_port < (uint32_t)kMaxPorts) port_ctr[2 * st.in_port] += ctr_inc(st.wire_len);
       if (!e.reason) port_ctr[2 * e.out_port + 1] += ctr_inc(olen);

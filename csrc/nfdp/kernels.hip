@@ -121,7 +121,7 @@ __global__ __launch_bounds__(kBlock, 4) void fused_kernel(FusedArgs a) {
         if (a.flow_ctr) atomicAdd(a.flow_ctr + slot, ctr_inc(st.wire_len));
       }
     }
-    const EgressDecision e = chain_stage(a.t, p, st, hit, act, acl_rule);
+    const EgressDecision e = chain_stage(a.t, p, st, hit, act, acl_rule, hash);
     if (valid) {
       uint32_t o[kSlotDwords];
       emit(p, e.tci, e.push != 0, o);
@@ -129,7 +129,7 @@ __global__ __launch_bounds__(kBlock, 4) void fused_kernel(FusedArgs a) {
       uint4* dst = a.out + (size_t)i * 4;
 #pragma unroll
       for (int q = 0; q < 4; ++q) dst[q] = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
-      a.out_meta[i] = make_meta(e.out_port, olen, e.reason);
+      a.out_meta[i] = make_meta(e.out_port, olen, e.reason, e.mirror != 0);
       // counters
       if (a.flags & 1u) {
       } else if (st.in_port < kLdsPorts) {

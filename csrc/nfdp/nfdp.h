@@ -60,7 +60,14 @@ enum PortFlags : uint32_t {
   kPortVlanBridge = 1u << 4,    // ingress vid selects bridge id (K7)
   kPortTrust = 1u << 5,
   kPortHasDefault = 1u << 6,    // L2 miss -> default_out instead of punt (OvS in_port=X,actions=output:Y)
+  kPortIngressTag = 1u << 7,    // frames from this port leave tagged with ext[11:0] (K6 add_vlan_and_send)
+  kPortMirror = 1u << 8,        // forwarded frames from this port are also copied to ext[31:16] (K9)
+  kPortLag = 1u << 9,           // egress to this port picks a LAG member by hash[2:0] (K8)
+  kPortVsiLookup = 1u << 10,    // L2 lookup keys on the target VSI (dst MAC byte 1) only (K3)
 };
+
+constexpr int kLagWays = 8;                 // members per LAG group (hash[2:0])
+constexpr uint32_t kMetaMirror = 1u << 31;  // egress meta: copy the frame to the in-port's mirror port
 
 // chain hop opcodes (built-in GPU network functions)
 enum Hop : uint8_t {
@@ -88,7 +95,8 @@ struct alignas(16) PortEntry {   // 32 B
   uint32_t peer_mac_lo;          // MAC of whatever is attached (pod / NF / next hop)
   uint16_t peer_mac_hi;
   uint16_t default_out;          // with kPortHasDefault: egress port on an L2 (flow + MAC) miss
-  uint32_t pad1, pad2;
+  uint32_t ext;                  // [11:0] ingress-push vid (kPortIngressTag); [31:16] mirror port (kPortMirror)
+  uint32_t lag;                  // LAG group index (kPortLag)
 };
 static_assert(sizeof(PortEntry) == 32, "PortEntry");
 
@@ -343,8 +351,8 @@ NFDP_HD void emit(const Parsed& p, uint32_t push_tci, bool push, uint32_t* out) 
   for (int i = 4; i < kSlotDwords; ++i) out[i] = push ? p.s[i - 1] : p.s[i];
 }
 
-NFDP_HD uint32_t make_meta(uint32_t out_port, uint32_t len, uint32_t reason) {
-  return (out_port & 0xFFFFu) | ((len & 0xFFu) << 16) | (reason << 24);
+NFDP_HD uint32_t make_meta(uint32_t out_port, uint32_t len, uint32_t reason, bool mirror = false) {
+  return (out_port & 0xFFFFu) | ((len & 0xFFu) << 16) | (reason << 24) | (mirror ? kMetaMirror : 0u);
 }
 
 // ----------------------------------------------------------------------------------------
@@ -366,6 +374,8 @@ struct TablesView {
   const uint8_t* acl_permit;     // n_acl (1 permit, 0 deny)
   uint32_t n_acl;
   uint32_t acl_default_permit;   // verdict when no rule matches
+  const uint16_t* lag_members;   // n_lag_groups * kLagWays egress ports (K8)
+  uint32_t n_lag_groups;
 };
 
 // Flow-table lookup (scalar).  Returns slot index or -1.

@@ -16,6 +16,8 @@ struct IngressState {
   uint32_t bridge;
   uint32_t reason;    // != 0: already dropped
   uint32_t wire_len;  // ingress length (bytes counted on rx)
+  uint32_t in_flags;  // ingress port flags (0 on a bad port)
+  uint32_t in_ext;    // ingress port ext word (ingress-push vid, mirror port)
   FlowKey key;
 };
 
@@ -28,10 +30,14 @@ NFDP_HD void ingress_stage(const TablesView& t, const uint32_t* d, uint32_t inme
   if (len < 14 || len > kSlotBytes) { st.reason = kMalformed; len = len < 14 ? 14 : kSlotBytes; }
   parse(d, len, p);
   st.bridge = 0;
+  st.in_flags = 0;
+  st.in_ext = 0;
   if (st.in_port >= (uint32_t)kMaxPorts) {
     st.reason = kBadPort;
   } else {
     const PortEntry pe = t.ports[st.in_port];
+    st.in_flags = pe.flags;
+    st.in_ext = pe.ext;
     if (!(pe.flags & kPortValid)) st.reason = st.reason ? st.reason : kBadPort;
     const uint32_t vid = p.tci & 0xFFFu;
     if ((pe.flags & kPortVlanIsolate) && p.tagged && vid != pe.vlan)
@@ -49,20 +55,26 @@ struct EgressDecision {
   uint32_t reason;
   uint32_t push;      // 1 -> insert an 802.1Q tag with `tci`
   uint32_t tci;
+  uint32_t mirror;    // 1 -> also copy to the ingress port's mirror port (meta bit 31)
 };
 
-// `hit`: flow entry found; `act`: its action; `acl_rule`: first matching ACL rule or -1.
+// `hit`: flow entry found; `act`: its action; `acl_rule`: first matching ACL rule or -1;
+// `hash`: the packet's Toeplitz hash (LAG member selection uses hash[2:0], K8).
 NFDP_HD EgressDecision chain_stage(const TablesView& t, Parsed& p, const IngressState& st,
-                                   bool hit, const FlowAction& act, int acl_rule) {
+                                   bool hit, const FlowAction& act, int acl_rule, uint32_t hash = 0) {
   EgressDecision e;
-  e.out_port = kPortNone; e.reason = st.reason; e.push = 0; e.tci = 0;
+  e.out_port = kPortNone; e.reason = st.reason; e.push = 0; e.tci = 0; e.mirror = 0;
   if (e.reason) return e;
   bool vlan_done = false;
   if (!hit) {
     // (bridge, dst MAC) table = OvS `in_port=X,dl_dst=M` / P4 l2_fwd; output == in_port is the
     // OvS hairpin.  A miss falls back to the ingress port's default output (`in_port=X ->
     // output:Y`, priority 10 in ovsdp.go:133-139) or is punted to the slow path.
-    const int op = mac_lookup(t, st.bridge, dmac_lo(p.s), dmac_hi(p.s));
+    // P4 vsi_to_vsi_loopback (K3): the target VSI is the dst MAC's second byte, so those ports
+    // look up (bridge, 00:VSI:00:00:00:00).
+    const bool vsi_key = (st.in_flags & kPortVsiLookup) != 0;
+    const int op = mac_lookup(t, st.bridge, vsi_key ? (dmac_lo(p.s) & 0xFF00u) : dmac_lo(p.s),
+                              vsi_key ? 0u : dmac_hi(p.s));
     if (op >= 0) {
       e.out_port = (uint32_t)op;
     } else {
@@ -70,6 +82,8 @@ NFDP_HD EgressDecision chain_stage(const TablesView& t, Parsed& p, const Ingress
       if (!(ip.flags & kPortHasDefault)) { e.out_port = kPortPunt; e.reason = kNoRoute; return e; }
       e.out_port = ip.default_out;
     }
+    // P4 add_vlan_and_send_to_port (K6): the source port's frames leave with its vid pushed.
+    if (st.in_flags & kPortIngressTag) { e.push = 1; e.tci = st.in_ext & 0xFFFu; vlan_done = true; }
   } else {
     e.out_port = act.out_port;
     // nhops + 7 hop opcodes = the chain entry's first 8 bytes, read as one word and decoded with
@@ -111,12 +125,20 @@ NFDP_HD EgressDecision chain_stage(const TablesView& t, Parsed& p, const Ingress
     }
   }
   if (e.out_port >= (uint32_t)kMaxPorts) { e.reason = kBadPort; e.out_port = kPortNone; return e; }
+  if (t.ports[e.out_port].flags & kPortLag) {
+    // LAG (K8): member = group[hash[2:0]] (tx_lag_table lag_group_id, hash/7)
+    const uint32_t g = t.ports[e.out_port].lag;
+    const uint32_t m = (t.lag_members && g < t.n_lag_groups) ? t.lag_members[g * kLagWays + (hash & 7u)] : kPortNone;
+    if (m >= (uint32_t)kMaxPorts) { e.reason = kBadPort; e.out_port = kPortNone; return e; }
+    e.out_port = m;
+  }
   const PortEntry& pe = t.ports[e.out_port];
   if (!(pe.flags & kPortValid)) { e.reason = kBadPort; e.out_port = kPortNone; return e; }
   if (!vlan_done && (pe.flags & kPortTagEgress) && pe.vlan) { e.push = 1; e.tci = pe.vlan & 0xFFFu; }
   if (p.len + (e.push ? 4u : 0u) > (uint32_t)kSlotBytes) {
     e.reason = kTooBig; e.out_port = kPortNone; return e;
   }
+  e.mirror = (st.in_flags & kPortMirror) ? 1u : 0u;  // mirror_and_send (K9)
   return e;
 }
 

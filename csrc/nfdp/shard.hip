@@ -116,7 +116,7 @@ __global__ __launch_bounds__(kBlock) void ingress_kernel(IngressArgs a) {
         }
       }
       a.ref[i] = ref;
-      a.aux[i] = (uint32_t)(acl + 1);
+      a.aux[i] = (uint32_t)(acl + 1) | ((hash & 7u) << 16);  // ACL rule + 1, LAG hash bits
     }
   }
 }
@@ -204,7 +204,7 @@ __global__ __launch_bounds__(kBlock) void apply_kernel(ApplyArgs a) {
       act.chain_id = v.x & 0xFFFFu; act.out_port = v.x >> 16; act.nat_ip = v.y;
       act.nat_port = v.z & 0xFFFFu; act.vlan = v.z >> 16;
     }
-    EgressDecision e = chain_stage(a.t, p, st, hit, act, (int)aux - 1);
+    EgressDecision e = chain_stage(a.t, p, st, hit, act, (int)(aux & 0xFFFFu) - 1, aux >> 16);
     uint32_t eg = a.g.rank;
     if (!e.reason) eg = a.t.ports[e.out_port].gpu;
     const bool remote = valid && !e.reason && eg != a.g.rank && eg < a.g.nranks;
@@ -219,11 +219,11 @@ __global__ __launch_bounds__(kBlock) void apply_kernel(ApplyArgs a) {
       if (remote && reason == kOk) {
         uint8_t* segp = a.send_pkt + eg * pseg;
         dst = reinterpret_cast<uint4*>(segp + 64 + (size_t)pos * 64);
-        reinterpret_cast<uint32_t*>(segp + pkt_meta_off(a.g.cap_pkt))[pos] = make_meta(e.out_port, olen, kOk);
+        reinterpret_cast<uint32_t*>(segp + pkt_meta_off(a.g.cap_pkt))[pos] = make_meta(e.out_port, olen, kOk, e.mirror != 0);
         a.out_meta[i] = make_meta(e.out_port, olen, kRemote);
       } else {
         dst = a.out + (size_t)i * 4;
-        a.out_meta[i] = make_meta(reason ? kPortNone : e.out_port, reason ? 0u : olen, reason);
+        a.out_meta[i] = make_meta(reason ? kPortNone : e.out_port, reason ? 0u : olen, reason, !reason && e.mirror != 0);
       }
 #pragma unroll
       for (int q = 0; q < 4; ++q) dst[q] = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);

@@ -31,7 +31,7 @@ void ingress_cpu(const IngressArgs& a) {
       }
     }
     a.ref[i] = ref;
-    a.aux[i] = (uint32_t)(acl + 1);
+    a.aux[i] = (uint32_t)(acl + 1) | ((h & 7u) << 16);
   }
   for (uint32_t o = 0; o < a.g.nranks; ++o) {
     const uint32_t hdr[4] = {a.cnt[o] < a.g.cap_desc ? a.cnt[o] : a.g.cap_desc, a.g.cap_desc, 0, 0};
@@ -84,7 +84,7 @@ void apply_cpu(const ApplyArgs& a) {
       act.chain_id = v[0] & 0xFFFFu; act.out_port = v[0] >> 16; act.nat_ip = v[1];
       act.nat_port = v[2] & 0xFFFFu; act.vlan = v[2] >> 16;
     }
-    const EgressDecision e = chain_stage(a.t, p, st, hit, act, (int)a.aux[i] - 1);
+    const EgressDecision e = chain_stage(a.t, p, st, hit, act, (int)(a.aux[i] & 0xFFFFu) - 1, a.aux[i] >> 16);
     uint32_t eg = a.g.rank;
     if (!e.reason) eg = a.t.ports[e.out_port].gpu;
     const bool remote = !e.reason && eg != a.g.rank && eg < a.g.nranks;
@@ -100,12 +100,12 @@ void apply_cpu(const ApplyArgs& a) {
     if (remote && reason == kOk) {
       uint8_t* segp = a.send_pkt + eg * pseg;
       std::memcpy(segp + 64 + (size_t)pos * 64, o, 64);
-      const uint32_t m = make_meta(e.out_port, olen, kOk);
+      const uint32_t m = make_meta(e.out_port, olen, kOk, e.mirror != 0);
       std::memcpy(segp + pkt_meta_off(a.g.cap_pkt) + 4 * (size_t)pos, &m, 4);
       a.out_meta[i] = make_meta(e.out_port, olen, kRemote);
     } else {
       std::memcpy(reinterpret_cast<uint8_t*>(a.out) + (size_t)i * 64, o, 64);
-      a.out_meta[i] = make_meta(reason ? kPortNone : e.out_port, reason ? 0u : olen, reason);
+      a.out_meta[i] = make_meta(reason ? kPortNone : e.out_port, reason ? 0u : olen, reason, !reason && e.mirror != 0);
     }
     if (st.in_port < (uint32_t)kMaxPorts) a.port_ctr[2 * st.in_port] += ctr_inc(st.wire_len);
     if (reason) a.drop_ctr[reason & (kNumReasons - 1)] += 1;

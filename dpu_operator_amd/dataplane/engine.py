@@ -61,6 +61,7 @@ class DataPlane:
         self.ports = T.PortTable()
         self.chains = T.ChainTable(chains)
         self.macs = T.MacTable(mac_slots)
+        self.lag = T.LagTable()
         self.acl = T.AclTable()
         self.flows = T.FlowTable(flow_buckets, rss_key)
         self.rss_key = rss_key
@@ -124,7 +125,7 @@ class DataPlane:
     def commit(self, full: bool = False) -> dict:
         """Push host table changes to the device.  Returns what was sent."""
         sent = {}
-        for name, model in (("ports", self.ports), ("chains", self.chains), ("macs", self.macs)):
+        for name, model in (("ports", self.ports), ("chains", self.chains), ("macs", self.macs), ("lag", self.lag)):
             if full or self._versions.get(name) != model.version or name not in self._dev:
                 self._buf(name, model.a)
                 self._versions[name] = model.version
@@ -185,6 +186,7 @@ class DataPlane:
             "rss_key": self._ptr("rss_key"), "acl_value": self._ptr("acl_value"), "acl_mask": self._ptr("acl_mask"),
             "acl_permit": self._ptr("acl_permit"), "n_acl": int(getattr(self, "_n_acl", 0)),
             "acl_default_permit": 1 if self.acl.default_permit else 0,
+            "lag_members": self._ptr("lag"), "n_lag_groups": int(self.lag.n),
         }
 
     # ------------------------------------------------------------------ run

@@ -1,0 +1,257 @@
+"""P4Info handling: a protobuf text-format reader and a P4Info helper.
+
+The reference drives the Intel IPU pipeline through `p4rt-ctl` (cmd/intelvsp/p4rt-ctl, P4Info
+helper :297-587) against the compiled pipeline's P4Info.  Here P4Info is
+plain data: `parse_text` reads any protobuf text-format document (messages, repeated fields,
+scalars, strings with escapes) into nested dicts/lists without needing the p4runtime protos, and
+`P4Info` indexes tables / match fields / actions / params by name, alias and id.
+
+`MI355X_P4INFO` is this framework's own P4Info for the linux-networking tables the GPU data
+plane implements (generated from `TABLES` below, same table/field names and widths as the
+reference pipeline so the same p4rt-ctl rule strings are accepted).
+"""
+from __future__ import annotations
+
+import re
+from dataclasses import dataclass, field
+
+_TOKEN = re.compile(r'\s*(?:(#[^\n]*)|([A-Za-z_][\w.]*)|("(?:[^"\\]|\\.)*")|(-?0x[0-9a-fA-F]+|-?\d+(?:\.\d+)?)|([{}:<>\[\],]))')
+
+
+def _unescape(s: str) -> str:
+    return bytes(s[1:-1], "utf-8").decode("unicode_escape")
+
+
+def parse_text(text: str) -> dict:
+    """Protobuf text format -> dict; every field maps to a list of values (repeated-safe)."""
+    toks: list[tuple[str, str]] = []
+    pos = 0
+    while pos < len(text):
+        m = _TOKEN.match(text, pos)
+        if not m or m.end() == pos:
+            if text[pos:].strip() == "":
+                break
+            raise ValueError(f"p4info text: unexpected input at offset {pos}: {text[pos:pos + 20]!r}")
+        pos = m.end()
+        if m.group(1):
+            continue
+        for kind, g in (("id", 2), ("str", 3), ("num", 4), ("p", 5)):
+            if m.group(g) is not None:
+                toks.append((kind, m.group(g)))
+                break
+    i = 0
+
+    def message(end: str | None) -> dict:
+        nonlocal i
+        out: dict[str, list] = {}
+        while i < len(toks):
+            kind, v = toks[i]
+            if kind == "p" and v == end:
+                i += 1
+                return out
+            if kind != "id":
+                raise ValueError(f"p4info text: expected a field name, got {v!r}")
+            name = v
+            i += 1
+            if toks[i] == ("p", ":"):
+                i += 1
+            kind, v = toks[i]
+            if kind == "p" and v in "{<":
+                i += 1
+                val = message("}" if v == "{" else ">")
+            elif kind == "str":
+                val = _unescape(v)
+                i += 1
+                while i < len(toks) and toks[i][0] == "str":  # adjacent literals concatenate
+                    val += _unescape(toks[i][1])
+                    i += 1
+            elif kind == "num":
+                val = int(v, 0) if re.fullmatch(r"-?(0x[0-9a-fA-F]+|\d+)", v) else float(v)
+                i += 1
+            else:  # enum identifier
+                val = v
+                i += 1
+            out.setdefault(name, []).append(val)
+        if end is not None:
+            raise ValueError("p4info text: unterminated message")
+        return out
+
+    return message(None)
+
+
+def _one(d: dict, k: str, default=None):
+    v = d.get(k)
+    return v[0] if v else default
+
+
+@dataclass
+class MatchField:
+    id: int
+    name: str
+    bitwidth: int
+    match_type: str  # EXACT / TERNARY / LPM / RANGE / OPTIONAL
+
+
+@dataclass
+class Param:
+    id: int
+    name: str
+    bitwidth: int
+
+
+@dataclass
+class Action:
+    id: int
+    name: str
+    alias: str
+    params: list[Param] = field(default_factory=list)
+
+
+@dataclass
+class Table:
+    id: int
+    name: str
+    alias: str
+    match_fields: list[MatchField]
+    action_ids: list[int]
+    size: int
+    const_default_action: int = 0
+
+    def field(self, name: str) -> MatchField:
+        for f in self.match_fields:
+            if f.name == name:
+                return f
+        raise KeyError(f"table {self.name} has no match field {name!r}")
+
+
+class P4Info:
+    def __init__(self, doc: dict):
+        self.tables: dict[str, Table] = {}
+        self.actions: dict[str, Action] = {}
+        self._tid: dict[int, Table] = {}
+        self._aid: dict[int, Action] = {}
+        for a in doc.get("actions", []):
+            pre = _one(a, "preamble", {})
+            act = Action(_one(pre, "id", 0), _one(pre, "name", ""), _one(pre, "alias", ""),
+                         [Param(_one(p, "id", 0), _one(p, "name", ""), _one(p, "bitwidth", 0)) for p in a.get("params", [])])
+            self.actions[act.name] = act
+            if act.alias:
+                self.actions.setdefault(act.alias, act)
+            self._aid[act.id] = act
+        for t in doc.get("tables", []):
+            pre = _one(t, "preamble", {})
+            mfs = [MatchField(_one(m, "id", 0), _one(m, "name", ""), _one(m, "bitwidth", 0), _one(m, "match_type", "EXACT"))
+                   for m in t.get("match_fields", [])]
+            tab = Table(_one(pre, "id", 0), _one(pre, "name", ""), _one(pre, "alias", ""), mfs,
+                        [_one(r, "id", 0) for r in t.get("action_refs", [])], _one(t, "size", 0),
+                        _one(t, "const_default_action_id", 0))
+            self.tables[tab.name] = tab
+            if tab.alias:
+                self.tables.setdefault(tab.alias, tab)
+            self._tid[tab.id] = tab
+
+    @classmethod
+    def from_text(cls, text: str) -> "P4Info":
+        return cls(parse_text(text))
+
+    def table(self, name_or_id) -> Table:
+        t = self._tid.get(name_or_id) if isinstance(name_or_id, int) else self.tables.get(name_or_id)
+        if t is None:
+            raise KeyError(f"unknown table {name_or_id!r}")
+        return t
+
+    def action(self, name_or_id) -> Action:
+        a = self._aid.get(name_or_id) if isinstance(name_or_id, int) else self.actions.get(name_or_id)
+        if a is None:
+            raise KeyError(f"unknown action {name_or_id!r}")
+        return a
+
+    def table_actions(self, table: Table) -> list[Action]:
+        return [self._aid[i] for i in table.action_ids if i in self._aid]
+
+
+# --------------------------------------------------------------------------------------------
+# The MI355X data plane's linux-networking subset (table, [(field, width, match)], [actions], size)
+C = "linux_networking_control."
+TABLES = [
+    ("tx_source_port", [("vmeta.common.vsi", 11, "TERNARY")], ["set_source_port", "drop"], 1024),
+    ("rx_source_port", [("vmeta.common.port_id", 2, "EXACT"), ("zero_padding", 16, "EXACT")],
+     ["set_source_port", "drop"], 1024),
+    ("tx_acc_vsi", [("vmeta.common.vsi", 11, "EXACT"), ("zero_padding", 16, "EXACT")],
+     ["l2_fwd_and_bypass_bridge", "drop"], 1024),
+    ("vsi_to_vsi_loopback", [("vmeta.common.vsi", 11, "EXACT"), ("target_vsi", 11, "EXACT")], ["fwd_to_vsi", "drop"], 1024),
+    ("source_port_to_pr_map", [("user_meta.cmeta.source_port", 16, "EXACT"), ("zero_padding", 8, "EXACT")],
+     ["fwd_to_vsi", "drop"], 1024),
+    ("rx_phy_port_to_pr_map", [("vmeta.common.port_id", 2, "EXACT"), ("zero_padding", 16, "EXACT")],
+     ["fwd_to_vsi", "mirror_and_send", "drop"], 1024),
+    ("source_port_to_bridge_map", [("user_meta.cmeta.source_port", 16, "TERNARY"),
+                                   ("hdrs.vlan_ext[vmeta.common.depth].hdr.vid", 12, "TERNARY")],
+     ["set_bridge_id", "drop"], 1024),
+    ("l2_fwd_rx_table", [("user_meta.pmeta.bridge_id", 8, "EXACT"), ("dst_mac", 48, "EXACT")], ["l2_fwd"], 1024),
+    # the reference VSP's l2_fwd_tx_table rule strings (p4rtclient.go:569) key on (dst_mac, tun_flag1_d0)
+    ("l2_fwd_tx_table", [("dst_mac", 48, "EXACT"), ("user_meta.pmeta.tun_flag1_d0", 8, "EXACT")], ["l2_fwd"], 1024),
+    ("sem_bypass", [("dst_mac", 48, "EXACT")], ["set_dest"], 1024),
+    ("handle_tx_from_host_to_ovs_and_ovs_to_wire_table", [("vmeta.common.vsi", 11, "EXACT"),
+                                                           ("user_meta.cmeta.bit32_zeros", 32, "EXACT")],
+     ["add_vlan_and_send_to_port", "set_dest"], 1024),
+    ("handle_rx_loopback_from_host_to_ovs_table", [("vmeta.common.vsi", 11, "EXACT"),
+                                                   ("user_meta.cmeta.bit32_zeros", 32, "EXACT")], ["set_dest"], 1024),
+    ("handle_tx_from_ovs_to_host_table", [("vmeta.common.vsi", 11, "EXACT"),
+                                          ("hdrs.dot1q_tag[vmeta.common.depth].hdr.vid", 12, "EXACT")],
+     ["remove_vlan_and_send_to_port", "set_dest"], 1024),
+    ("handle_rx_loopback_from_ovs_to_host_table", [("vmeta.misc_internal.vm_to_vm_or_port_to_port[27:17]", 11, "EXACT"),
+                                                   ("user_meta.cmeta.bit32_zeros", 32, "EXACT")], ["set_dest"], 1024),
+    ("vlan_push_mod_table", [("vmeta.common.mod_blob_ptr", 24, "EXACT")], ["vlan_push"], 1024),
+    ("vlan_pop_mod_table", [("vmeta.common.mod_blob_ptr", 24, "EXACT")], ["vlan_pop"], 1024),
+    ("tx_lag_table", [("user_meta.cmeta.lag_group_id", 8, "TERNARY"), ("hash", 3, "TERNARY")],
+     ["bypass", "set_egress_port", "drop"], 1024),
+    ("ipv4_lpm_root_lut", [("user_meta.cmeta.bit16_zeros", 16, "TERNARY")], ["ipv4_lpm_root_lut_action"], 1),
+    ("mir_prof", [("mirror_prof_key", 8, "EXACT")], ["mir_prof_action"], 256),
+]
+ACTIONS = {
+    "set_source_port": [("source_port", 16)],
+    "l2_fwd_and_bypass_bridge": [("port", 32)],
+    "fwd_to_vsi": [("port", 32)],
+    "mirror_and_send": [("port", 32), ("mirror_session_id", 16)],
+    "set_bridge_id": [("bridge_id", 8)],
+    "l2_fwd": [("port", 32)],
+    "set_dest": [("port_id", 32)],
+    "add_vlan_and_send_to_port": [("vlan_id", 12), ("port_id", 32)],
+    "remove_vlan_and_send_to_port": [("vlan_id", 12), ("port_id", 32)],
+    "vlan_push": [("pcp", 3), ("dei", 1), ("vlan_id", 12)],
+    "vlan_pop": [],
+    "bypass": [],
+    "drop": [],
+    "set_egress_port": [("router_interface_id", 16), ("egress_port", 32)],
+    "ipv4_lpm_root_lut_action": [("ipv4_table_lpm_root", 32)],
+    # subset of the pipeline's mirror profile parameters (the ones the VSP programs)
+    "mir_prof_action": [("port_dest_type", 32), ("vport_id", 32), ("mode", 1), ("dest_id", 16), ("func_valid", 1),
+                        ("store_vsi", 1)],
+}
+
+
+def _render_mi355x_p4info() -> str:
+    lines = ['pkg_info {', '  arch: "mi355x-nfdp"', '}']
+    aids = {}
+    for k, (name, params) in enumerate(ACTIONS.items()):
+        aid = 0x01000000 | (k + 1)
+        aids[name] = aid
+    for k, (tname, fields, acts, size) in enumerate(TABLES):
+        lines += ["tables {", "  preamble {", f"    id: {0x02000000 | (k + 1)}", f'    name: "{C}{tname}"',
+                  f'    alias: "{tname}"', "  }"]
+        for j, (fname, width, mt) in enumerate(fields):
+            lines += ["  match_fields {", f"    id: {j + 1}", f'    name: "{fname}"', f"    bitwidth: {width}",
+                      f"    match_type: {mt}", "  }"]
+        for a in acts:
+            lines += ["  action_refs {", f"    id: {aids[a]}", "  }"]
+        lines += [f"  size: {size}", "}"]
+    for name, params in ACTIONS.items():
+        lines += ["actions {", "  preamble {", f"    id: {aids[name]}", f'    name: "{C}{name}"', f'    alias: "{name}"', "  }"]
+        for j, (pname, width) in enumerate(params):
+            lines += ["  params {", f"    id: {j + 1}", f'    name: "{pname}"', f"    bitwidth: {width}", "  }"]
+        lines += ["}"]
+    return "\n".join(lines) + "\n"
+
+
+MI355X_P4INFO_TEXT = _render_mi355x_p4info()
+MI355X_P4INFO = P4Info.from_text(MI355X_P4INFO_TEXT)

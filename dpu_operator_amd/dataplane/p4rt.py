@@ -1,0 +1,376 @@
+"""P4Runtime-style table store for the linux-networking pipeline, compiled onto the GPU tables.
+
+Reference: the Intel IPU VSP programs the FXP pipeline through `p4rt-ctl add-entry/del-entry br0
+<table> <match,...,action=ctrl.act(args)>` (vendor/.../p4rtclient/p4rtclient.go:74-1155, SURVEY
+V11/NAT11, kernels K1-K9).  `P4Runtime` accepts exactly those entry strings, validates them
+against a P4Info (tables, match kinds, bit widths, action params, table sizes), keeps the entries
+(INSERT of an existing key -> ALREADY_EXISTS, DELETE of a missing key -> NOT_FOUND, full table ->
+RESOURCE_EXHAUSTED — the error vocabulary the VSP's retry logic keys on) and compiles the whole
+entry set onto the MI355X data plane:
+
+  K1 tx_source_port / rx_source_port      port -> source port (classification state)
+  K2 tx_acc_vsi                           port default output, bridge bypassed
+  K3 vsi_to_vsi_loopback                  (port bridge, MAC of the target VSI) -> port entries
+  K4 source_port_to_pr_map                source port -> port-representor default output
+  K5 l2_fwd_rx_table / l2_fwd_tx_table / sem_bypass   (bridge, dst MAC) -> port entries
+  K6 handle_tx_* / vlan_push/pop_mod      per-source VLAN push (PORT_INGRESS_TAG), pop on the way
+                                          back via (vid bridge, MAC) entries
+  K7 source_port_to_bridge_map            port bridge id (vid-keyed entries: bridge = vid)
+  K8 tx_lag_table                         LAG member table, hash[2:0]-indexed (PORT_LAG)
+  K9 mir_prof + mirror_and_send           PORT_MIRROR with the profile's destination vport
+A VSI is the second byte of its MAC and its vport is vsi + 16 (ipu-plugin utils.go:76-107); data-
+plane port number == vport.  Physical ports 0..3 are data-plane ports PHY_BASE + n.
+"""
+from __future__ import annotations
+
+import re
+import threading
+
+import numpy as np
+from dataclasses import dataclass, field
+
+from . import tables as T
+from .p4info import MI355X_P4INFO, P4Info
+
+VSI_TO_VPORT = 16
+PHY_BASE = 4000
+STEER_BRIDGE_BASE = 0xF000   # per-port private bridges (bypass / loopback domains)
+
+
+class P4Error(Exception):
+    def __init__(self, code: str, msg: str):
+        super().__init__(f"{code}: {msg}")
+        self.code = code
+
+
+def vport_for_vsi(vsi: int) -> int:
+    return vsi + VSI_TO_VPORT
+
+
+def vsi_of_mac(mac: str | bytes) -> int:
+    b = bytes.fromhex(mac.replace(":", "")) if isinstance(mac, str) else bytes(mac)
+    return b[1]
+
+
+def _int(v: str) -> int:
+    v = v.strip()
+    return int(v, 16) if v.lower().startswith("0x") else int(v)
+
+
+@dataclass
+class Entry:
+    table: str
+    key: tuple                  # ((field, value, mask), ...) in P4Info field order
+    priority: int = 0
+    action: str = ""
+    params: dict = field(default_factory=dict)
+
+    def text(self) -> str:
+        parts = []
+        for f, v, m in self.key:
+            full = (1 << 64) - 1
+            parts.append(f"{f}={v:#x}" + (f"/{m:#x}" if m != full and m is not None else ""))
+        if self.priority:
+            parts.append(f"priority={self.priority}")
+        args = ",".join(f"{k}={v}" for k, v in self.params.items())
+        parts.append(f"action={self.action}({args})")
+        return ",".join(parts)
+
+
+class P4Runtime:
+    def __init__(self, dataplane=None, p4info: P4Info = MI355X_P4INFO, lag_ports: dict[int, int] | None = None):
+        self.dp = dataplane
+        self.p4info = p4info
+        self.entries: dict[str, dict[tuple, Entry]] = {}
+        self.lag_ports = dict(lag_ports or {})  # LAG group -> data-plane port that fronts it
+        self._owned_ports: set[int] = set()
+        self._owned_macs: list[tuple[int, str]] = []
+        self._lock = threading.RLock()
+        self.stats = {"writes": 0, "compiles": 0}
+
+    # ------------------------------------------------------------------ parsing
+    def _table(self, name: str):
+        try:
+            return self.p4info.table(name)
+        except KeyError:
+            raise P4Error("NOT_FOUND", f"table {name} not in the loaded pipeline") from None
+
+    def parse(self, table: str, spec: str, need_action: bool = True) -> Entry:
+        t = self._table(table)
+        spec = spec.strip()
+        action, args = "", ""
+        m = re.search(r"(?:^|,)action=([\w.]+)(?:\((.*)\))?\s*$", spec)
+        if m:
+            action, args = m.group(1), m.group(2) or ""
+            spec = spec[: m.start()]
+        elif need_action:
+            raise P4Error("INVALID_ARGUMENT", "entry has no action")
+        given: dict[str, tuple[int, int | None]] = {}
+        priority = 0
+        for tok in filter(None, (x.strip() for x in spec.split(","))):
+            k, eq, v = tok.partition("=")
+            if not eq:
+                raise P4Error("INVALID_ARGUMENT", f"bad match token {tok!r}")
+            if k == "priority":
+                priority = _int(v)
+                continue
+            val, _, mask = v.partition("/")
+            try:
+                given[k] = (_int(val), _int(mask) if mask else None)
+            except ValueError:
+                raise P4Error("INVALID_ARGUMENT", f"bad value in {tok!r}") from None
+        key = []
+        ternary = False
+        for mf in t.match_fields:
+            if mf.name not in given:
+                raise P4Error("INVALID_ARGUMENT", f"missing match field {mf.name} for {t.name}")
+            v, msk = given.pop(mf.name)
+            full = (1 << mf.bitwidth) - 1
+            if v < 0 or v > full:
+                raise P4Error("INVALID_ARGUMENT", f"{mf.name}={v} exceeds {mf.bitwidth} bits")
+            if mf.match_type == "EXACT":
+                if msk is not None and msk != full:
+                    raise P4Error("INVALID_ARGUMENT", f"{mf.name} is an exact match; no mask allowed")
+                msk = full
+            else:
+                ternary = True
+                msk = full if msk is None else msk
+                if msk > full:
+                    raise P4Error("INVALID_ARGUMENT", f"mask of {mf.name} exceeds {mf.bitwidth} bits")
+                v &= msk
+            key.append((mf.name, v, msk))
+        if given:
+            raise P4Error("INVALID_ARGUMENT", f"unknown match field(s) {sorted(given)} for {t.name}")
+        if ternary and need_action and priority <= 0:
+            raise P4Error("INVALID_ARGUMENT", f"ternary table {t.name} needs priority > 0")
+        params: dict[str, int] = {}
+        if action:
+            try:
+                a = self.p4info.action(action)
+            except KeyError:
+                raise P4Error("INVALID_ARGUMENT", f"unknown action {action}") from None
+            if a.id not in t.action_ids:
+                raise P4Error("INVALID_ARGUMENT", f"action {a.name} not allowed in {t.name}")
+            vals = [x.strip() for x in args.split(",")] if args.strip() else []
+            named = [x for x in vals if "=" in x]
+            if named and len(named) != len(vals):
+                raise P4Error("INVALID_ARGUMENT", "mixing positional and named action arguments")
+            if named:
+                for x in named:
+                    k, _, v = x.partition("=")
+                    p = next((p for p in a.params if p.name == k), None)
+                    if p is None:
+                        raise P4Error("INVALID_ARGUMENT", f"action {a.name} has no parameter {k}")
+                    params[k] = _int(v)
+            else:
+                if len(vals) != len(a.params):
+                    raise P4Error("INVALID_ARGUMENT", f"action {a.name} takes {len(a.params)} arguments, got {len(vals)}")
+                params = {p.name: _int(v) for p, v in zip(a.params, vals)}
+            for p in a.params:
+                if p.name in params and params[p.name] >= (1 << p.bitwidth):
+                    raise P4Error("INVALID_ARGUMENT", f"{p.name}={params[p.name]} exceeds {p.bitwidth} bits")
+            action = a.name
+        return Entry(t.name, tuple(key), priority, action, params)
+
+    # ------------------------------------------------------------------ writes
+    def add_entry(self, table: str, spec: str) -> Entry:
+        with self._lock:
+            e = self.parse(table, spec)
+            tab = self.entries.setdefault(e.table, {})
+            k = (e.key, e.priority)
+            if k in tab:
+                raise P4Error("ALREADY_EXISTS", f"entry already exists in {e.table}")
+            if len(tab) >= self._table(e.table).size:
+                raise P4Error("RESOURCE_EXHAUSTED", f"table {e.table} is full ({self._table(e.table).size})")
+            tab[k] = e
+            self.stats["writes"] += 1
+            self.compile()
+            return e
+
+    def del_entry(self, table: str, spec: str) -> None:
+        with self._lock:
+            e = self.parse(table, spec, need_action=False)
+            tab = self.entries.get(e.table, {})
+            k = (e.key, e.priority)
+            if k not in tab:
+                raise P4Error("NOT_FOUND", f"no such entry in {e.table}")
+            del tab[k]
+            self.stats["writes"] += 1
+            self.compile()
+
+    def get_entries(self, table: str | None = None) -> list[Entry]:
+        with self._lock:
+            if table is not None:
+                return list(self.entries.get(self._table(table).name, {}).values())
+            return [e for t in self.entries.values() for e in t.values()]
+
+    def set_pipe(self, p4info: P4Info) -> None:
+        with self._lock:
+            self.p4info = p4info
+            self.entries.clear()
+            self.compile()
+
+    # ------------------------------------------------------------------ compile
+    def _rows(self, short: str) -> list[Entry]:
+        name = "linux_networking_control." + short
+        rows = list(self.entries.get(name, {}).values())
+        return sorted(rows, key=lambda e: -e.priority)
+
+    @staticmethod
+    def _k(e: Entry, i: int) -> tuple[int, int]:
+        return e.key[i][1], e.key[i][2]
+
+    def compile(self) -> None:
+        """Recompute every P4-derived port attribute, MAC entry and LAG group (idempotent)."""
+        if self.dp is None:
+            return
+        dp = self.dp
+        self.stats["compiles"] += 1
+        for bid, mac in self._owned_macs:
+            dp.macs.remove(bid, mac)
+        self._owned_macs = []
+        keep = {"flags", "vlan", "mac_lo", "mac_hi", "gpu", "peer_mac_lo", "peer_mac_hi"}
+        for p in self._owned_ports:
+            f = int(dp.ports.a[p]["flags"]) & ~(T.PORT_HAS_DEFAULT | T.PORT_INGRESS_TAG | T.PORT_MIRROR | T.PORT_LAG |
+                                                 T.PORT_VLAN_BRIDGE | T.PORT_VSI_LOOKUP)
+            row = {k: dp.ports.a[p][k] for k in keep}
+            dp.ports.a[p] = np.zeros((), T.PORT_DTYPE)
+            for k, v in row.items():
+                dp.ports.a[p][k] = v
+            dp.ports.a[p]["flags"] = f
+        dp.ports.version += 1
+        owned: set[int] = set()
+
+        def port(p: int) -> int:
+            if 0 <= p < VSI_TO_VPORT:   # action port numbers below 16 name physical ports
+                p = PHY_BASE + p
+            if not 0 <= p < T.MAX_PORTS:
+                raise P4Error("INVALID_ARGUMENT", f"port {p} outside the data plane")
+            if not dp.ports.valid(p):
+                dp.ports.set(p, flags=T.PORT_VALID)
+            owned.add(p)
+            return p
+
+        def add_mac(bridge: int, mac: str, out: int) -> None:
+            dp.macs.insert(bridge, mac, out)
+            self._owned_macs.append((bridge, mac))
+
+        # K1: source ports (a ternary VSI match applies to every VSI the pipeline references)
+        src: dict[int, int] = {}
+        known_vsis = {e.key[0][1] for t in ("tx_acc_vsi", "vsi_to_vsi_loopback", "handle_tx_from_host_to_ovs_and_ovs_to_wire_table",
+                                          "handle_rx_loopback_from_host_to_ovs_table") for e in self._rows(t)}
+        known_vsis |= {e.key[1][1] for e in self._rows("vsi_to_vsi_loopback")}
+        for e in reversed(self._rows("tx_source_port")):  # lowest priority first, higher overrides
+            v, m = self._k(e, 0)
+            targets = [v] if m == 0x7FF else sorted(x for x in known_vsis if (x & m) == v)
+            for vsi in targets:
+                src[port(vport_for_vsi(vsi))] = e.params["source_port"]
+        for e in self._rows("rx_source_port"):
+            src[port(PHY_BASE + self._k(e, 0)[0])] = e.params["source_port"]
+        # K7: bridge ids (highest priority wins per port)
+        bridge: dict[int, int] = {}
+        vlan_bridge: set[int] = set()
+        for e in self._rows("source_port_to_bridge_map"):
+            (sv, sm), (vv, vm) = self._k(e, 0), self._k(e, 1)
+            for p, sp in src.items():
+                if (sp & sm) == sv and p not in bridge:
+                    if vm == 0 or vv == 0:   # wildcard or untagged-only
+                        bridge[p] = e.params["bridge_id"]
+                    else:
+                        if vm != 0xFFF or vv != e.params["bridge_id"]:
+                            raise P4Error("INVALID_ARGUMENT",
+                                          "vid-keyed bridge mapping is supported as bridge_id == vid only")
+                        vlan_bridge.add(p)
+        for p, b in bridge.items():
+            dp.ports.update(p, bridge_id=b)
+        for p in vlan_bridge:
+            dp.ports.a[p]["flags"] |= T.PORT_VLAN_BRIDGE
+        # K4: source port -> port representor
+        pr: dict[int, int] = {e.key[0][1]: e.params["port"] for e in self._rows("source_port_to_pr_map")
+                              if e.action.endswith("fwd_to_vsi")}
+        for p, sp in src.items():
+            if sp in pr:
+                dp.ports.update(p, default_out=port(pr[sp]))
+        # K9 profiles + rx_phy_port_to_pr_map
+        # mir_prof vport_id is a VSI when store_vsi=1 (p4rtclient.go:1033-1037)
+        prof = {e.key[0][1]: (vport_for_vsi(e.params.get("vport_id", 0)) if e.params.get("store_vsi", 0)
+                              else e.params.get("vport_id", 0)) for e in self._rows("mir_prof")}
+        for e in self._rows("rx_phy_port_to_pr_map"):
+            p = port(PHY_BASE + e.key[0][1])
+            dp.ports.update(p, default_out=port(e.params["port"]))
+            if e.action.endswith("mirror_and_send"):
+                sess = e.params["mirror_session_id"]
+                if sess not in prof:
+                    raise P4Error("FAILED_PRECONDITION", f"mirror session {sess} has no mir_prof entry")
+                dp.ports.set_mirror(p, port(prof[sess]))
+        # K6: host <-> OvS VLAN handling (needs the vlan_push/pop mod blobs)
+        push_ok = {e.key[0][1] for e in self._rows("vlan_push_mod_table")}
+        pop_ok = {e.key[0][1] for e in self._rows("vlan_pop_mod_table")}
+        for e in self._rows("handle_tx_from_host_to_ovs_and_ovs_to_wire_table"):
+            p = port(vport_for_vsi(e.key[0][1]))
+            if e.action.endswith("add_vlan_and_send_to_port"):
+                dp.ports.update(p, default_out=port(e.params["port_id"]))
+                if e.params["vlan_id"] in push_ok:
+                    dp.ports.set_ingress_tag(p, e.params["vlan_id"])
+            else:
+                dp.ports.update(p, default_out=port(e.params["port_id"]))
+        for e in self._rows("handle_rx_loopback_from_host_to_ovs_table"):
+            p = port(vport_for_vsi(e.key[0][1]))
+            if not dp.ports.a[p]["flags"] & T.PORT_HAS_DEFAULT:
+                dp.ports.update(p, default_out=port(e.params["port_id"]))
+        for e in self._rows("handle_tx_from_ovs_to_host_table"):
+            mux = port(vport_for_vsi(e.key[0][1]))
+            vid = e.key[1][1]
+            dp.ports.a[mux]["flags"] |= T.PORT_VLAN_BRIDGE | T.PORT_VSI_LOOKUP
+            out = port(e.params["port_id"])
+            if e.params["vlan_id"] in pop_ok:
+                add_mac(vid, vsi_mac(out - VSI_TO_VPORT), out)  # tag popped at ingress parse
+        # K2: ACC bypass (overrides the PR map), on a private empty bridge
+        for e in self._rows("tx_acc_vsi"):
+            p = port(vport_for_vsi(e.key[0][1]))
+            dp.ports.update(p, default_out=port(e.params["port"]), bridge_id=STEER_BRIDGE_BASE + p % 0x0FFF)
+        # K3: VSI to VSI loopback: the source port looks up (its bridge, target VSI)
+        for e in self._rows("vsi_to_vsi_loopback"):
+            a, b = e.key[0][1], e.key[1][1]
+            p = port(vport_for_vsi(a))
+            if int(dp.ports.a[p]["bridge_id"]) == 0:
+                dp.ports.update(p, bridge_id=STEER_BRIDGE_BASE + p % 0x0FFF)
+            dp.ports.a[p]["flags"] |= T.PORT_VSI_LOOKUP
+            add_mac(int(dp.ports.a[p]["bridge_id"]), vsi_mac(b), port(e.params["port"]))
+        # K5: L2 forwarding
+        for e in self._rows("l2_fwd_rx_table"):
+            add_mac(e.key[0][1], _mac(e.key[1][1]), port(e.params["port"]))
+        for e in self._rows("l2_fwd_tx_table"):
+            add_mac(0, _mac(e.key[0][1]), port(e.params["port"]))
+        for e in self._rows("sem_bypass"):
+            add_mac(0, _mac(e.key[0][1]), port(e.params["port_id"]))
+        # K8: LAG
+        for grp, lag_port in self.lag_ports.items():
+            members = [T.PORT_NONE] * T.LAG_WAYS
+            any_member = False
+            for h in range(T.LAG_WAYS):
+                for e in self._rows("tx_lag_table"):
+                    (gv, gm), (hv, hm) = self._k(e, 0), self._k(e, 1)
+                    if (grp & gm) == gv and (h & hm) == hv:
+                        if e.action.endswith("set_egress_port"):
+                            members[h] = port(e.params["egress_port"])
+                            any_member = True
+                        break
+            p = port(lag_port)
+            if any_member:
+                for h, mport in enumerate(members):
+                    dp.lag.set_slot(grp, h, mport)
+                dp.ports.set_lag(p, grp)
+            else:
+                dp.ports.set_lag(p, None)
+        self._owned_ports = owned
+        dp.ports.version += 1
+
+
+def vsi_mac(vsi: int) -> str:
+    """The L2 key a VSI-lookup port matches: only byte 1 (the VSI) of the dst MAC is kept."""
+    return f"00:{vsi & 0xFF:02x}:00:00:00:00"
+
+
+def _mac(x: int) -> str:
+    return ":".join(f"{(x >> (8 * (5 - i))) & 0xFF:02x}" for i in range(6))

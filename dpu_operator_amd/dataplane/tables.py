@@ -33,6 +33,11 @@ PORT_TAG_EGRESS = 1 << 3
 PORT_VLAN_BRIDGE = 1 << 4
 PORT_TRUST = 1 << 5
 PORT_HAS_DEFAULT = 1 << 6
+PORT_INGRESS_TAG = 1 << 7   # frames from the port leave tagged with ext[11:0] (P4 add_vlan_and_send_to_port)
+PORT_MIRROR = 1 << 8        # forwarded frames are also copied to ext[31:16] (P4 mirror_and_send)
+PORT_LAG = 1 << 9           # egress picks member lag_members[lag][hash & 7] (P4 tx_lag_table)
+PORT_VSI_LOOKUP = 1 << 10   # L2 lookup on (bridge, 00:VSI:00:00:00:00), VSI = dst MAC byte 1 (P4 vsi_to_vsi_loopback)
+LAG_WAYS = 8
 
 # hop opcodes (nfdp.h Hop)
 HOP_NONE, HOP_ACL, HOP_NAT, HOP_L2FWD, HOP_TTL, HOP_HAIRPIN, HOP_VLAN, HOP_DROP, HOP_PUNT = range(9)
@@ -52,7 +57,7 @@ PORT_DTYPE = np.dtype(
         ("flags", "<u4"), ("vlan", "<u2"), ("bridge_id", "<u2"),
         ("mac_lo", "<u4"), ("mac_hi", "<u2"), ("gpu", "<u2"),
         ("peer_mac_lo", "<u4"), ("peer_mac_hi", "<u2"), ("default_out", "<u2"),
-        ("pad1", "<u4"), ("pad2", "<u4"),
+        ("ext", "<u4"), ("lag", "<u4"),
     ]
 )
 CHAIN_DTYPE = np.dtype([("nhops", "u1"), ("hop", "u1", (7,)), ("acl_id", "<u2"), ("flags", "<u2"), ("pad", "<u4")])
@@ -152,6 +157,63 @@ class PortTable:
 
     def valid(self, idx: int) -> bool:
         return bool(self.a[idx]["flags"] & PORT_VALID)
+
+    def _flag(self, idx: int, bit: int, on: bool) -> None:
+        if on:
+            self.a[idx]["flags"] |= np.uint32(bit)
+        else:
+            self.a[idx]["flags"] &= ~np.uint32(bit)
+
+    def set_ingress_tag(self, idx: int, vid: int | None) -> None:
+        """P4 add_vlan_and_send_to_port: frames from `idx` leave tagged with `vid` (None: off)."""
+        if vid is not None and not 1 <= vid <= 4094:
+            raise ValueError("vid must be 1..4094")
+        ext = int(self.a[idx]["ext"]) & ~0xFFF
+        self.a[idx]["ext"] = ext | (vid or 0)
+        self._flag(idx, PORT_INGRESS_TAG, vid is not None)
+        self.version += 1
+
+    def set_mirror(self, idx: int, mirror_port: int | None) -> None:
+        """P4 mirror_and_send: frames forwarded from `idx` are also copied to `mirror_port`."""
+        ext = int(self.a[idx]["ext"]) & 0xFFFF
+        self.a[idx]["ext"] = ext | ((mirror_port or 0) << 16)
+        self._flag(idx, PORT_MIRROR, mirror_port is not None)
+        self.version += 1
+
+    def set_lag(self, idx: int, group: int | None) -> None:
+        """Egress to `idx` (a LAG port) picks a member of `group` by hash[2:0]."""
+        self.a[idx]["lag"] = group or 0
+        self._flag(idx, PORT_LAG, group is not None)
+        self.version += 1
+
+    def mirror_port(self, idx: int) -> int | None:
+        return int(self.a[idx]["ext"]) >> 16 if self.a[idx]["flags"] & PORT_MIRROR else None
+
+
+class LagTable:
+    """LAG groups: `LAG_WAYS` member slots per group indexed by hash[2:0] (P4 tx_lag_table)."""
+
+    def __init__(self, groups: int = 64):
+        self.a = np.full(groups * LAG_WAYS, PORT_NONE, np.uint16)
+        self.n = 0
+        self.version = 0
+
+    def set_group(self, group: int, members: list[int]) -> None:
+        """Spread `members` over the 8 hash buckets (round robin, like equal-weight LAG)."""
+        if not 0 <= group < len(self.a) // LAG_WAYS:
+            raise ValueError("LAG group out of range")
+        if not members:
+            row = [PORT_NONE] * LAG_WAYS
+        else:
+            row = [members[i % len(members)] for i in range(LAG_WAYS)]
+        self.a[group * LAG_WAYS:(group + 1) * LAG_WAYS] = row
+        self.n = max(self.n, group + 1)
+        self.version += 1
+
+    def set_slot(self, group: int, hash_bits: int, port: int) -> None:
+        self.a[group * LAG_WAYS + (hash_bits & 7)] = port
+        self.n = max(self.n, group + 1)
+        self.version += 1
 
 
 class ChainTable:

@@ -227,6 +227,11 @@ def inmeta(in_port, lens) -> np.ndarray:
 
 
 def meta_fields(meta: np.ndarray) -> tuple[np.ndarray, np.ndarray, np.ndarray]:
-    """Egress metadata -> (out_port, len, reason)."""
+    """Egress metadata -> (out_port, len, reason).  Bit 31 (mirror request) is not part of reason."""
     m = np.asarray(meta, np.uint32)
-    return m & 0xFFFF, (m >> 16) & 0xFF, m >> 24
+    return m & 0xFFFF, (m >> 16) & 0xFF, (m >> 24) & 0x7F
+
+
+def meta_mirror(meta: np.ndarray) -> np.ndarray:
+    """Per-packet bool: the frame must also be copied to its ingress port's mirror port (K9)."""
+    return (np.asarray(meta, np.uint32) >> 31).astype(bool)

@@ -5,5 +5,6 @@ from .registry import (  # noqa: F401
     GoogleEmpty,
     deviceplugin,
     opi,
+    p4rt,
     vendor,
 )

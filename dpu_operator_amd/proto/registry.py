@@ -205,7 +205,31 @@ DP_FILE = _build(
     },
 )
 
-for _fd in (VENDOR_FILE, OPI_FILE, DP_FILE):
+# ---------------------------------------------------------------- MI355X P4 runtime (p4rt-ctl server)
+# The reference's p4rt-ctl speaks P4Runtime to infrap4d; this framework's pipeline server takes
+# the same rule strings in a small service (bridge + table + entry text), so p4rt-ctl semantics
+# (ALREADY_EXISTS / NOT_FOUND / INVALID_ARGUMENT in the error text) carry over unchanged.
+P4RT_FILE = _build(
+    "mi355x/p4rt.proto", "mi355x.p4rt.v1",
+    enums={"UpdateType": [("UNSPECIFIED", 0), ("INSERT", 1), ("MODIFY", 2), ("DELETE", 3)]},
+    messages={
+        "Update": [("type", 1, "UpdateType", "enum"), ("table", 2, "string"), ("entry", 3, "string")],
+        "WriteRequest": [("bridge", 1, "string"), ("updates", 2, "Update", "repeated")],
+        "WriteResponse": [("applied", 1, "int32")],
+        "ReadRequest": [("bridge", 1, "string"), ("table", 2, "string")],
+        "TableEntry": [("table", 1, "string"), ("entry", 2, "string")],
+        "ReadResponse": [("entries", 1, "TableEntry", "repeated")],
+        "SetPipeRequest": [("bridge", 1, "string"), ("p4info_text", 2, "string")],
+        "SetPipeResponse": [("tables", 1, "int32"), ("actions", 2, "int32")],
+        "GetPipeRequest": [("bridge", 1, "string")],
+        "GetPipeResponse": [("p4info_text", 1, "string")],
+    },
+    services={"P4rt": {"Write": ("WriteRequest", "WriteResponse"), "Read": ("ReadRequest", "ReadResponse"),
+                       "SetPipe": ("SetPipeRequest", "SetPipeResponse"),
+                       "GetPipe": ("GetPipeRequest", "GetPipeResponse")}},
+)
+
+for _fd in (VENDOR_FILE, OPI_FILE, DP_FILE, P4RT_FILE):
     POOL.Add(_fd)
 
 
@@ -235,6 +259,7 @@ class _Namespace:
 vendor = _Namespace("Vendor", VENDOR_FILE)
 opi = _Namespace(OPI_PKG, OPI_FILE)
 deviceplugin = _Namespace("v1beta1", DP_FILE)
+p4rt = _Namespace("mi355x.p4rt.v1", P4RT_FILE)
 GoogleEmpty = message_factory.GetMessageClass(POOL.FindMessageTypeByName("google.protobuf.Empty"))
 
 HEALTHY = "Healthy"

@@ -135,3 +135,68 @@ def test_sharded_kernels_simulated_ranks(world):
         rem = np.where(rs == 10)[0]
         assert len(rem) > 0
         assert all(rc.out[i].tobytes() in delivered for i in rem)
+
+
+def _p4_plane(device):
+    """Ports programmed through the P4 compile (K2-K9) and an OvS bridge, plus SFC flows."""
+    from dpu_operator_amd.dataplane.ovs import OvsSwitch
+    from dpu_operator_amd.dataplane.p4rt import P4Runtime
+    from dpu_operator_amd.dataplane.p4server import InProcessP4rtClient, Rule, program_rules
+    from dpu_operator_amd.vsp import intel_ipu as ipu
+
+    dp, sc = _build(device, n_flows=1 << 12)
+    rt = P4Runtime(dp, lag_ports={0: 4095})
+    c = InProcessP4rtClient({"br0": rt})
+    vfs = [f"00:{0x40 + i:02x}:00:00:00:01" for i in range(6)]
+    accs = [f"00:{0x60 + i:02x}:00:00:00:02" for i in range(6)]
+    rules = []
+    for v, a in zip(vfs, accs):
+        rules += ipu.host_vf_rules(v, a)
+    rules += ipu.peer_to_peer_rules(vfs)
+    rules += [Rule("add-entry", "br0", "linux_networking_control.tx_lag_table",
+                   f"user_meta.cmeta.lag_group_id=0/255,hash={h}/7,priority=1,"
+                   f"action=linux_networking_control.set_egress_port(0,{h % 3})") for h in range(8)]
+    rules += [Rule("add-entry", "br0", "linux_networking_control.tx_acc_vsi",
+                   "vmeta.common.vsi=101,zero_padding=0,action=linux_networking_control.l2_fwd_and_bypass_bridge(4095)")]
+    rules += ipu.primary_network_rules("00:70:00:00:00:04", "00:71:00:00:00:01")
+    rules += ipu.vf_vlan_rules("00:72:00:00:00:01", 9, port_mux_vsi=115)
+    assert program_rules(c, rules) == []
+    br = OvsSwitch(dp).add_br("br-gpu")
+    for i, n in enumerate(("a", "b", "nin", "nout")):
+        br.add_port(n, 3000 + i, mac=f"02:cc:00:00:00:{i:02x}")
+    br.add_flow("priority=10,in_port=a,actions=output:nin")
+    br.add_flow("priority=100,in_port=nout,dl_dst=02:cc:00:00:00:00,actions=in_port")
+    dp.commit(full=True)
+    return dp, sc, vfs
+
+
+def _p4_traffic(sc, vfs, n=1 << 14, seed=11):
+    rng = np.random.default_rng(seed)
+    pk, im = S.traffic(sc, n, seed=seed)
+    src_ports = np.array([0x40 + 16 + i for i in range(6)] + [101 + 16, 4000, 0x72 + 16, 115 + 16, 3000, 3003])
+    dst_macs = [bytes.fromhex(m.replace(":", "")) for m in vfs] + [bytes.fromhex("007100000001"),
+                                                                   bytes.fromhex("02cc00000000"), bytes(6)]
+    sel = rng.integers(0, len(src_ports), n)
+    dm = rng.integers(0, len(dst_macs), n)
+    for i in range(0, n, 2):  # half of the batch exercises the P4/OvS ports
+        pk[i, 0:6] = np.frombuffer(dst_macs[dm[i]], np.uint8)
+        im[i] = (im[i] & 0xFFFF0000) | src_ports[sel[i]]
+    return pk, im
+
+
+def test_p4_ovs_features_bit_exact():
+    """LAG (hash-selected member), mirror flag, VSI-keyed loopback, ingress VLAN push, OvS
+    hairpin: the GPU kernel must agree with the oracle bit for bit."""
+    torch = _torch()
+    cpu, sc, vfs = _p4_plane("cpu")
+    gpu, _, _ = _p4_plane("cuda")
+    pk, im = _p4_traffic(sc, vfs)
+    rc = cpu.run(pk, im)
+    rg = gpu.run(torch.from_numpy(pk).cuda(), torch.from_numpy(im.view(np.int32)).cuda())
+    torch.cuda.synchronize()
+    mg = rg.meta.cpu().numpy().view(np.uint32)
+    assert np.array_equal(mg, rc.meta)
+    assert np.array_equal(rg.out.cpu().numpy(), rc.out)
+    op = P.meta_fields(rc.meta)[0]
+    assert P.meta_mirror(rc.meta).any()
+    assert len({4000, 4001, 4002} & set(op.tolist())) == 3   # LAG spread over three members
