@@ -1,0 +1,87 @@
+"""`vsp` — run a Vendor Specific Plugin on the vendor-plugin socket.
+
+The reference builds one binary per vendor (cmd/intelvsp/intelvsp.go, marvell/main.go:823,
+intel-netsec/main.go:627, mock-vsp); here `--vendor` selects it:
+  amd-gpu    GPU VSP on the MI355X data plane (vsp/gpu.py)
+  mock       mock VSP (Init -> 127.0.0.1:50051, four healthy devices)
+  marvell    Marvell VSP; OvS-equivalent bridge on the GPU data plane (--debug-dp: log only)
+  netsec     Intel NetSec accelerator VSP on the GPU data plane
+  intel-ipu  Intel IPU VSP writing P4 rules to the pipeline server (--p4rt-addr)
+"""
+from __future__ import annotations
+
+import argparse
+import logging
+import signal
+import sys
+import threading
+
+from ..utils.paths import PathManager
+
+
+def build_vsp(a, pm: PathManager):
+    if a.vendor == "mock":
+        from ..vsp.base import MockVsp
+
+        return MockVsp(pm)
+    if a.vendor == "amd-gpu":
+        from ..vsp.gpu import GpuVsp
+
+        return GpuVsp(pm, device=a.device or None, flow_buckets=a.flow_buckets)
+    from ..cni.netlink import RtNetlink
+    from ..platform.platform import SysfsPlatform
+    from ..utils.cmdrunner import HostRunner
+
+    plat, nl, runner = SysfsPlatform(a.sys_root), RtNetlink(), HostRunner()
+
+    def dataplane():
+        from ..dataplane.engine import DataPlane
+
+        dp = DataPlane(device=a.device or "cuda", flow_buckets=a.flow_buckets)
+        dp.commit(full=True)
+        return dp
+
+    if a.vendor == "marvell":
+        from ..vsp import marvell as M
+
+        ddp = M.DebugDataPlane() if a.debug_dp else M.GpuOvsDataPlane(dataplane(), uplink_name=a.uplink)
+        return M.MarvellVsp(plat, nl, runner, ddp, pm, a.sys_root)
+    if a.vendor == "netsec":
+        from ..vsp.netsec import NetsecVsp
+
+        return NetsecVsp(plat, nl, runner, dataplane(), pm, a.sys_root)
+    if a.vendor == "intel-ipu":
+        from ..dataplane.p4server import GrpcP4rtClient
+        from ..vsp.intel_ipu import IntelIpuVsp
+
+        accs = [m.strip() for m in a.acc_macs.split(",") if m.strip()]
+        return IntelIpuVsp(GrpcP4rtClient(a.p4rt_addr), accs, path_manager=pm, mode=a.mode)
+    raise SystemExit(f"unknown vendor {a.vendor!r}")
+
+
+def main(argv=None, stop: threading.Event | None = None) -> int:
+    ap = argparse.ArgumentParser(prog="vsp")
+    ap.add_argument("--vendor", default="amd-gpu", choices=["amd-gpu", "mock", "marvell", "netsec", "intel-ipu"])
+    ap.add_argument("--root", default="/")
+    ap.add_argument("--sys-root", default="/")
+    ap.add_argument("--device", default="")
+    ap.add_argument("--flow-buckets", type=int, default=1 << 18)
+    ap.add_argument("--debug-dp", action="store_true")
+    ap.add_argument("--uplink", default="rpm0")
+    ap.add_argument("--p4rt-addr", default="127.0.0.1:9559")
+    ap.add_argument("--acc-macs", default="")
+    ap.add_argument("--mode", default="ipu")
+    a = ap.parse_args(argv)
+    logging.basicConfig(level=logging.INFO)
+    vsp = build_vsp(a, PathManager(a.root)).start()
+    stop = stop or threading.Event()
+    if threading.current_thread() is threading.main_thread():
+        signal.signal(signal.SIGTERM, lambda *_: stop.set())
+        signal.signal(signal.SIGINT, lambda *_: stop.set())
+    stop.wait()
+    vsp.stop()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -18,6 +18,7 @@ import threading
 from http.server import BaseHTTPRequestHandler
 from typing import Callable
 
+from ..utils.metrics import CONTROL
 from ..utils.paths import PathManager
 from . import logging as clog
 from .helper import read_cni_config
@@ -122,10 +123,17 @@ class Server:
                     return self._reply(404, b"404 page not found\n")
                 n = int(self.headers.get("Content-Length", "0") or 0)
                 body = self.rfile.read(n)
+                cmd = "unknown"
+                try:
+                    cmd = (json.loads(body or b"{}").get("env") or {}).get("CNI_COMMAND", "unknown")
+                except ValueError:
+                    pass
                 try:
                     out = server.handle_cni_request(body)
                 except Exception as e:  # noqa: BLE001 - any failure is a 400 with the message
+                    CONTROL.cni_requests.labels(cmd, "error").inc()
                     return self._reply(400, f"{e}\n".encode())
+                CONTROL.cni_requests.labels(cmd, "success").inc()
                 self._reply(200, out, "application/json")
 
             def _not_allowed(self):

@@ -24,6 +24,7 @@ from .. import vars as V
 from ..cni.sriov.utils import is_valid_pci_address
 from ..proto import DEVICE_PLUGIN_VERSION, HEALTHY, deviceplugin as dp
 from ..proto.grpcutil import Stub, service_handler, unix_target
+from ..utils.metrics import CONTROL
 from ..utils.paths import PathManager
 
 log = logging.getLogger("dpu.deviceplugin")
@@ -91,6 +92,7 @@ class DevicePluginServer:
             self._stop.wait(self.poll)
 
     def Allocate(self, request, context):
+        CONTROL.allocations.inc()
         resp = dp.AllocateResponse()
         for creq in request.container_requests:
             names = ""

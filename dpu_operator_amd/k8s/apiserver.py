@@ -339,6 +339,8 @@ class ApiServer:
             req = self._pod_requests(pod)
             placed = False
             for node in self.list("Node"):
+                if (node.get("spec") or {}).get("unschedulable"):
+                    continue  # cordoned (drain)
                 if not match_labels(node["metadata"].get("labels"), pod["spec"].get("nodeSelector")):
                     continue
                 alloc = {k: parse_quantity(v) for k, v in ((node.get("status") or {}).get("allocatable") or {}).items()}

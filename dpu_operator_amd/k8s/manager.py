@@ -17,6 +17,7 @@ from dataclasses import dataclass
 from typing import Callable, Protocol
 
 from .apiserver import ApiServer
+from ..utils.metrics import CONTROL
 
 log = logging.getLogger("dpu.manager")
 
@@ -121,6 +122,7 @@ class Manager:
         try:
             res = ctl.rec.reconcile(req) or Result()
             self.reconcile_count += 1
+            CONTROL.reconciles.labels(cname, "requeue" if (res.requeue or res.requeue_after) else "success").inc()
             if res.requeue_after > 0:
                 self._failures.pop(key, None)
                 self.enqueue(cname, req, res.requeue_after)
@@ -134,6 +136,7 @@ class Manager:
             n = self._failures.get(key, 0) + 1
             self._failures[key] = n
             self.errors.append((cname, req, repr(e)))
+            CONTROL.reconciles.labels(cname, "error").inc()
             log.warning("reconcile %s %s failed (%d): %s", cname, req, n, e)
             self.enqueue(cname, req, min(0.005 * (2 ** n), 1.0))
         return True

@@ -1,0 +1,170 @@
+"""Prometheus metrics + health probes.
+
+The reference exposes controller-runtime metrics on :18090 and probes on :18091 (cmd/main.go:50-51,
+SURVEY §5 "metrics").  Here one registry carries:
+* control-plane counters (reconciles, CNI requests by command/result, VSP RPCs, device-plugin
+  allocations) — `CONTROL` below, incremented by the components;
+* `DataPlaneCollector`: per-port rx/tx packets+bytes, drops by reason, installed flows, per-flow
+  counter harvests, batch latency quantiles — read from a DataPlane at scrape time (counters are
+  64-bit on the host, harvested from the packed device counters).
+`MetricsServer` serves /metrics (text exposition) and `ProbeServer` /healthz + /readyz with
+pluggable checks.
+"""
+from __future__ import annotations
+
+import threading
+from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
+
+from prometheus_client import CONTENT_TYPE_LATEST, CollectorRegistry, Counter, Gauge, Histogram, generate_latest
+from prometheus_client.core import CounterMetricFamily, GaugeMetricFamily
+
+REGISTRY = CollectorRegistry(auto_describe=True)
+
+
+class _Control:
+    def __init__(self, reg: CollectorRegistry):
+        self.reconciles = Counter("dpu_reconcile_total", "Reconcile calls", ["controller", "result"], registry=reg)
+        self.cni_requests = Counter("dpu_cni_requests_total", "CNI requests served", ["command", "result"], registry=reg)
+        self.vsp_calls = Counter("dpu_vsp_calls_total", "VSP RPCs", ["method", "result"], registry=reg)
+        self.allocations = Counter("dpu_device_plugin_allocations_total", "Device plugin Allocate calls", registry=reg)
+        self.devices = Gauge("dpu_devices", "Devices advertised to the kubelet", ["health"], registry=reg)
+        self.p4_writes = Counter("dpu_p4_writes_total", "P4 table writes", ["verb", "result"], registry=reg)
+        self.batch_seconds = Histogram("dpu_dataplane_batch_seconds", "Host-observed data-plane batch time",
+                                       buckets=(1e-5, 3e-5, 1e-4, 3e-4, 1e-3, 3e-3, 1e-2, 3e-2, 0.1), registry=reg)
+
+
+CONTROL = _Control(REGISTRY)
+
+
+class DataPlaneCollector:
+    """Scrape-time export of a DataPlane's counters (no per-packet Python work)."""
+
+    def __init__(self, dataplane, name: str = "gpu0", max_ports: int = 4096):
+        self.dp = dataplane
+        self.name = name
+        self.max_ports = max_ports
+
+    def collect(self):
+        from ..dataplane import tables as T
+
+        ctr = self.dp.port_counters()
+        labels = ["dataplane", "port"]
+        rx_p = CounterMetricFamily("dpu_port_rx_packets", "Packets received per port", labels=labels)
+        rx_b = CounterMetricFamily("dpu_port_rx_bytes", "Bytes received per port", labels=labels)
+        tx_p = CounterMetricFamily("dpu_port_tx_packets", "Packets transmitted per port", labels=labels)
+        tx_b = CounterMetricFamily("dpu_port_tx_bytes", "Bytes transmitted per port", labels=labels)
+        active = (ctr[:, 0] > 0) | (ctr[:, 2] > 0)
+        for port in active.nonzero()[0][: self.max_ports]:
+            lv = [self.name, str(int(port))]
+            rx_p.add_metric(lv, float(ctr[port, 0]))
+            rx_b.add_metric(lv, float(ctr[port, 1]))
+            tx_p.add_metric(lv, float(ctr[port, 2]))
+            tx_b.add_metric(lv, float(ctr[port, 3]))
+        yield from (rx_p, rx_b, tx_p, tx_b)
+        drops = CounterMetricFamily("dpu_drops", "Dropped packets by reason", labels=["dataplane", "reason"])
+        for reason, n in sorted(self.dp.drop_counters().items()):
+            drops.add_metric([self.name, reason], float(n))
+        yield drops
+        flows = GaugeMetricFamily("dpu_flows_installed", "Exact-match flows installed", labels=["dataplane"])
+        flows.add_metric([self.name], float(len(self.dp.flows)))
+        yield flows
+        cap = GaugeMetricFamily("dpu_flow_capacity", "Flow table slots", labels=["dataplane"])
+        cap.add_metric([self.name], float(self.dp.flows.nbuckets * 4))
+        yield cap
+        ports = GaugeMetricFamily("dpu_ports_valid", "Valid data-plane ports", labels=["dataplane"])
+        ports.add_metric([self.name], float((self.dp.ports.a["flags"] & T.PORT_VALID).astype(bool).sum()))
+        yield ports
+
+
+def register_dataplane(dataplane, name: str = "gpu0", registry: CollectorRegistry = REGISTRY) -> DataPlaneCollector:
+    c = DataPlaneCollector(dataplane, name)
+    registry.register(c)
+    return c
+
+
+class _Srv:
+    def __init__(self, address: str):
+        host, _, port = address.rpartition(":")
+        self.addr = (host or "0.0.0.0", int(port))
+        self._srv: ThreadingHTTPServer | None = None
+        self.port = 0
+
+    def _handler(self):
+        raise NotImplementedError
+
+    def start(self):
+        self._srv = ThreadingHTTPServer(self.addr, self._handler())
+        self._srv.daemon_threads = True
+        self.port = self._srv.server_address[1]
+        threading.Thread(target=self._srv.serve_forever, daemon=True).start()
+        return self
+
+    def stop(self) -> None:
+        if self._srv is not None:
+            self._srv.shutdown()
+            self._srv.server_close()
+
+
+class MetricsServer(_Srv):
+    def __init__(self, address: str = ":18090", registry: CollectorRegistry = REGISTRY):
+        super().__init__(address)
+        self.registry = registry
+
+    def _handler(self):
+        reg = self.registry
+
+        class H(BaseHTTPRequestHandler):
+            def log_message(self, *a):
+                pass
+
+            def do_GET(self):
+                if self.path.split("?")[0] != "/metrics":
+                    self.send_response(404)
+                    self.end_headers()
+                    return
+                body = generate_latest(reg)
+                self.send_response(200)
+                self.send_header("Content-Type", CONTENT_TYPE_LATEST)
+                self.send_header("Content-Length", str(len(body)))
+                self.end_headers()
+                self.wfile.write(body)
+
+        return H
+
+
+class ProbeServer(_Srv):
+    """/healthz and /readyz; each has a list of named check callables returning bool."""
+
+    def __init__(self, address: str = ":18091"):
+        super().__init__(address)
+        self.health: dict[str, callable] = {"ping": lambda: True}
+        self.ready: dict[str, callable] = {"ping": lambda: True}
+
+    def _handler(self):
+        outer = self
+
+        class H(BaseHTTPRequestHandler):
+            def log_message(self, *a):
+                pass
+
+            def do_GET(self):
+                checks = {"/healthz": outer.health, "/readyz": outer.ready}.get(self.path)
+                if checks is None:
+                    self.send_response(404)
+                    self.end_headers()
+                    return
+                failed = [n for n, fn in checks.items() if not _ok(fn)]
+                body = (b"ok" if not failed else ("failed: " + ",".join(failed)).encode())
+                self.send_response(200 if not failed else 500)
+                self.send_header("Content-Length", str(len(body)))
+                self.end_headers()
+                self.wfile.write(body)
+
+        return H
+
+
+def _ok(fn) -> bool:
+    try:
+        return bool(fn())
+    except Exception:  # noqa: BLE001
+        return False

@@ -18,6 +18,7 @@ import grpc
 
 from ..proto import GoogleEmpty, opi, vendor
 from ..proto.grpcutil import service_handler, unix_target
+from ..utils.metrics import CONTROL
 from ..utils.paths import PathManager
 
 log = logging.getLogger("dpu.vsp")
@@ -58,7 +59,13 @@ class VspBase:
     def _call(self, name, fn, *args):
         with self._lock:
             self.calls.append((name, args))
-            return fn(*args)
+            try:
+                out = fn(*args)
+            except Exception:
+                CONTROL.vsp_calls.labels(name, "error").inc()
+                raise
+            CONTROL.vsp_calls.labels(name, "success").inc()
+            return out
 
     def Init(self, request, context):
         try:
