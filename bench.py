@@ -8,11 +8,13 @@ whole chain:
     pod VF ingress (VLAN-isolated, spoof-checked)  ->  ACL (TCAM, 256 ternary rules, MFMA)  ->
     SNAT (per-flow state, 1M-flow exact-match table)  ->  L2 steer + egress VLAN tag  ->  pod VF
 
-N = 1: one fused HIP kernel.  N > 1 (one process per GPU, torchrun): the flow table is sharded
-across the GPUs; each step does ingress/classify -> all-to-all(16-B descriptors) -> owner lookup
--> all-to-all(16-B verdicts) -> apply chain -> all-to-all(64-B packets to the destination pod's
-GPU) -> egress, all on RCCL over xGMI.  Traffic is random pod->pod over 8 pods per GPU, so
-(N-1)/N of the packets cross GPUs.
+N = 1: one fused HIP kernel.  N > 1 (one process per GPU, torchrun), default `--mode replicated`:
+every GPU holds the full tables (1M flows = 64 MB of its 288 GB) and runs the fused kernel on its
+own ingress; frames for pods on other GPUs are written by the kernel into per-GPU segments and
+delivered with ONE all-to-all per chunk (RCCL over xGMI), chunks pipelined against compute.
+`--mode sharded`: the flow table is hash-partitioned instead (descriptor / verdict / packet
+all-to-alls).  Traffic is random pod->pod over 8 pods per GPU, so (N-1)/N of the packets cross
+GPUs.
 
 Data: synthetic (random-init 1M-flow table, random 5-tuples); inputs rotate over 4 pre-generated
 batches so no step re-reads a cached one.  Latency: per-packet time from the batch release stamp
@@ -50,6 +52,8 @@ def parse():
     ap.add_argument("--rotate", type=int, default=4)
     ap.add_argument("--no-lowlat", action="store_true", help="skip the small-batch latency probe")
     ap.add_argument("--chunks", type=int, default=4, help="pipeline chunks per step (N > 1)")
+    ap.add_argument("--mode", default="replicated", choices=["replicated", "sharded"],
+                    help="multi-GPU strategy for N > 1")
     ap.add_argument("--force-sharded", action="store_true",
                     help="use the sharded multi-GPU pipeline even at N = 1 (measures its compute cost)")
     return ap.parse_args()
@@ -80,16 +84,18 @@ def main() -> None:
     from dpu_operator_amd.dataplane import scenario as S
     from dpu_operator_amd.dataplane.engine import DataPlane
     from dpu_operator_amd.ops import packets as P
+    from dpu_operator_amd.parallel.replicated import ReplicatedDataPlane
     from dpu_operator_amd.parallel.sharded import PipelinedShardedDataPlane, ShardedDataPlane, shard_filter
 
+    replicated = sharded and world > 1 and a.mode == "replicated" and not a.force_sharded
     t_setup = time.time()
-    flows_here = a.flows / world
+    flows_here = a.flows if (replicated or world == 1) else a.flows / world
     buckets = 1 << max(10, int(math.ceil(math.log2(flows_here / 2))))  # <= 50% load, 4 slots/bucket
     dp = DataPlane(device=str(dev), flow_buckets=buckets, hash_mode=a.hash, acl_mode=a.acl_mode)
     n_pods = a.pods_per_gpu * world
     pod_gpu = np.arange(n_pods) // a.pods_per_gpu
     sc = S.build_sfc(dp, n_pods=n_pods, n_flows=a.flows, n_acl=a.acl, seed=0, pod_gpu=pod_gpu,
-                     flow_filter=shard_filter(rank, world) if world > 1 else None)
+                     flow_filter=shard_filter(rank, world) if (world > 1 and not replicated) else None)
     dp.commit(full=True)
     my_pods = np.where(pod_gpu == rank)[0]
     batches = []
@@ -106,6 +112,15 @@ def main() -> None:
 
         def results():
             return meta.cpu().numpy().view(np.uint32), lat.cpu().numpy().view(np.uint32).astype(np.float64) * 0.01
+    elif replicated:
+        eng = ReplicatedDataPlane(dp, rank, world, a.batch, chunks=a.chunks)
+
+        def step(k):
+            pk, im = batches[k % a.rotate]
+            eng.step(pk, im)
+
+        def results():
+            return eng.out_meta(), eng.latency_samples_us()
     else:
         eng = PipelinedShardedDataPlane(dp, rank, world, a.batch, chunks=a.chunks)
 
@@ -158,6 +173,12 @@ def main() -> None:
                 dp.run(pk, im, o2, m2, l2)
             torch.cuda.synchronize()
             ls = l2.cpu().numpy().view(np.uint32).astype(np.float64) * 0.01
+        elif replicated:
+            eng_s = ReplicatedDataPlane(dp, rank, world, nsm, chunks=1)
+            for _ in range(20):
+                eng_s.step(pk, im)
+            torch.cuda.synchronize()
+            ls = eng_s.latency_samples_us()
         else:
             eng_s = ShardedDataPlane(dp, rank, world, nsm)
             for _ in range(20):
@@ -191,7 +212,9 @@ def main() -> None:
                 "global_batch": world * a.batch,
                 "seq_len": 64,
                 "parallelism": "fused-1gpu" if not sharded else
-                f"flow-shard x{world} + 3x all-to-all (RCCL/xGMI), {a.chunks}-chunk overlap",
+                (f"replicated tables x{world}, fused kernel + 1x all-to-all of cross-GPU frames (RCCL/xGMI), "
+                 f"{a.chunks}-chunk overlap" if replicated else
+                 f"flow-shard x{world} + 3x all-to-all (RCCL/xGMI), {a.chunks}-chunk overlap"),
             },
             "p50_latency_us": round(p50, 2),
             "p99_latency_us": round(p99, 2),

@@ -285,6 +285,45 @@ PYBIND11_MODULE(_nfdp, m) {
     check(launch_egress(a, num_cus, reinterpret_cast<hipStream_t>(stream)), "shard_egress");
   });
 
+  // Replicated-table multi-GPU step: fused kernel with per-GPU egress segments (device=True) or
+  // its CPU twin (device=False).  d: tables-independent buffers + geometry (nranks, rank, cap_pkt).
+  m.def("fused_remote", [geom](py::dict tables, py::dict d, bool device, int hash_mode, int acl_mode, int num_cus,
+                               uintptr_t stream) {
+    ShardGeom g = geom(d);
+    FusedLaunch f{};
+    f.t = tables_from(tables);
+    f.pkts = ptr<const void>(d, "pkts"); f.inmeta = ptr<const uint32_t>(d, "inmeta");
+    f.out = ptr<void>(d, "out"); f.out_meta = ptr<uint32_t>(d, "out_meta"); f.n = val<uint32_t>(d, "n", 0);
+    f.flow_ctr = ptr<unsigned long long>(d, "flow_ctr"); f.port_ctr = ptr<unsigned long long>(d, "port_ctr");
+    f.drop_ctr = ptr<unsigned long long>(d, "drop_ctr");
+    f.t0 = ptr<const unsigned long long>(d, "t0"); f.lat = ptr<uint32_t>(d, "lat");
+    f.acl_wfrag = ptr<const void>(d, "acl_wfrag"); f.acl_cinit = ptr<const void>(d, "acl_cinit");
+    f.acl_tiles = val<uint32_t>(d, "acl_tiles", 1);
+    f.toep_frag = ptr<const void>(d, "toep_frag"); f.toep_tab = ptr<const uint32_t>(d, "toep_tab");
+    f.flags = val<uint32_t>(d, "flags", 0);
+    f.send_pkt = ptr<uint8_t>(d, "send_pkt"); f.pcnt = ptr<uint32_t>(d, "pcnt");
+    f.nranks = g.nranks; f.rank = g.rank; f.cap_pkt = g.cap_pkt;
+    if (!f.pkts || !f.inmeta || !f.out || !f.out_meta || !f.port_ctr || !f.drop_ctr || !f.send_pkt || !f.pcnt)
+      throw std::invalid_argument("fused_remote: null buffer");
+    if (g.nranks < 2) throw std::invalid_argument("fused_remote needs nranks >= 2");
+    if (!device) {
+      RemoteOut r{g.nranks, g.rank, g.cap_pkt, f.send_pkt, f.pcnt};
+      py::gil_scoped_release nogil;
+      oracle_run_remote(f.t, reinterpret_cast<const uint32_t*>(f.pkts), f.inmeta, f.n,
+                        reinterpret_cast<uint32_t*>(f.out), f.out_meta, reinterpret_cast<uint64_t*>(f.flow_ctr),
+                        reinterpret_cast<uint64_t*>(f.port_ctr), reinterpret_cast<uint64_t*>(f.drop_ctr), r);
+      return;
+    }
+    if (hash_mode == 2 && !f.toep_frag) throw std::invalid_argument("MFMA hash needs toeplitz frags");
+    if (hash_mode == 1 && !f.toep_tab) throw std::invalid_argument("LDS hash needs toeplitz table");
+    if (acl_mode == 1 && (!f.acl_wfrag || !f.acl_cinit)) throw std::invalid_argument("MFMA ACL needs frags");
+    LaunchCfg cfg;
+    cfg.hash_mode = hash_mode; cfg.acl_mode = acl_mode; cfg.num_cus = num_cus;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    check(launch_fused(f, cfg, s), "fused_remote");
+    check(launch_seg_headers(f.pcnt, f.send_pkt, g.nranks, pkt_seg_bytes(g.cap_pkt), g.cap_pkt, s), "seg_headers");
+  });
+
   m.def("launch_harvest", [](uintptr_t ctr, uintptr_t out, uint32_t n, uintptr_t stream) {
     check(launch_harvest(reinterpret_cast<unsigned long long*>(ctr), reinterpret_cast<unsigned long long*>(out), n,
                          reinterpret_cast<hipStream_t>(stream)), "harvest");

@@ -1,5 +1,8 @@
 // host.cpp — authoritative flow table (cuckoo), classification-table builders, CPU oracle.
 #include "host.h"
+#include "shard.h"
+
+#include <cstring>
 
 #include <algorithm>
 
@@ -219,6 +222,62 @@ void oracle_run(const TablesView& t, const uint32_t* pkts, const uint32_t* inmet
       if (!e.reason) port_ctr[2 * e.out_port + 1] += ctr_inc(olen);
     }
     if (drop_ctr && e.reason) drop_ctr[e.reason & (kNumReasons - 1)] += 1;
+  }
+}
+
+void oracle_run_remote(const TablesView& t, const uint32_t* pkts, const uint32_t* inmeta, uint32_t n,
+                       uint32_t* out, uint32_t* out_meta, uint64_t* flow_ctr, uint64_t* port_ctr,
+                       uint64_t* drop_ctr, const RemoteOut& r) {
+  const size_t pseg = pkt_seg_bytes(r.cap_pkt);
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t* d = pkts + (size_t)i * kSlotDwords;
+    Parsed p;
+    IngressState st;
+    ingress_stage(t, d, inmeta[i], p, st);
+    const uint32_t h = toeplitz_scalar(st.key, t.rss_key);
+    const int acl = acl_first_match(t, st.key);
+    bool hit = false;
+    FlowAction act = {};
+    if (!st.reason && p.ipv4) {
+      const int64_t slot = flow_lookup(t, st.key, h);
+      if (slot >= 0) {
+        hit = true;
+        act = t.flows[slot].act;
+        if (flow_ctr) flow_ctr[slot] += ctr_inc(st.wire_len);
+      }
+    }
+    const EgressDecision e = chain_stage(t, p, st, hit, act, acl, h);
+    const uint32_t eg = e.reason ? r.rank : (uint32_t)t.ports[e.out_port].gpu;
+    const bool remote = !e.reason && eg != r.rank && eg < r.nranks;
+    uint32_t reason = e.reason;
+    uint32_t pos = 0;
+    if (remote) {
+      pos = r.pcnt[eg]++;
+      if (pos >= r.cap_pkt) reason = kOverflow;
+    }
+    uint32_t o[kSlotDwords];
+    emit(p, e.tci, e.push != 0, o);
+    const uint32_t olen = reason ? 0u : p.len + (e.push ? 4u : 0u);
+    const bool to_peer = remote && reason == kOk;
+    if (to_peer) {
+      uint8_t* segp = r.send_pkt + eg * pseg;
+      std::memcpy(segp + 64 + (size_t)pos * 64, o, sizeof(o));
+      const uint32_t m = make_meta(e.out_port, olen, kOk, e.mirror != 0);
+      std::memcpy(segp + pkt_meta_off(r.cap_pkt) + 4 * (size_t)pos, &m, 4);
+      out_meta[i] = make_meta(e.out_port, olen, kRemote, e.mirror != 0);
+    } else {
+      std::memcpy(out + (size_t)i * kSlotDwords, o, sizeof(o));
+      out_meta[i] = make_meta(reason ? kPortNone : e.out_port, olen, reason, !reason && e.mirror != 0);
+    }
+    if (port_ctr) {
+      if (st.in_port < (uint32_t)kMaxPorts) port_ctr[2 * st.in_port] += ctr_inc(st.wire_len);
+      if (!reason && !to_peer) port_ctr[2 * e.out_port + 1] += ctr_inc(olen);
+    }
+    if (drop_ctr && reason) drop_ctr[reason & (kNumReasons - 1)] += 1;
+  }
+  for (uint32_t o = 0; o < r.nranks; ++o) {
+    const uint32_t hdr[4] = {r.pcnt[o] < r.cap_pkt ? r.pcnt[o] : r.cap_pkt, r.cap_pkt, 0, 0};
+    std::memcpy(r.send_pkt + o * pseg, hdr, 16);
   }
 }
 

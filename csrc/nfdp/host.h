@@ -64,6 +64,17 @@ struct OracleOut {
 void oracle_run(const TablesView& t, const uint32_t* pkts, const uint32_t* inmeta, uint32_t n,
                 uint32_t* out, uint32_t* out_meta, uint64_t* flow_ctr, uint64_t* port_ctr,
                 uint64_t* drop_ctr, uint32_t* hashes, int32_t* acl_rules);
+// Replicated multi-GPU twin of the fused REMOTE kernel: frames whose egress port belongs to
+// another rank are written to send_pkt segment[egress rank] (positions in arrival order, fill
+// counts in pcnt, headers written at the end), out_meta says kRemote for them.
+struct RemoteOut {
+  uint32_t nranks, rank, cap_pkt;
+  uint8_t* send_pkt;
+  uint32_t* pcnt;
+};
+void oracle_run_remote(const TablesView& t, const uint32_t* pkts, const uint32_t* inmeta, uint32_t n,
+                       uint32_t* out, uint32_t* out_meta, uint64_t* flow_ctr, uint64_t* port_ctr,
+                       uint64_t* drop_ctr, const RemoteOut& r);
 
 // ---- GPU launchers (kernels.hip) ----
 struct LaunchCfg {
@@ -79,6 +90,9 @@ struct FusedLaunch {
   const void* acl_wfrag; const void* acl_cinit; uint32_t acl_tiles;
   const void* toep_frag; const uint32_t* toep_tab;
   uint32_t flags = 0;
+  // replicated multi-GPU mode (nranks > 1): remote-egress frames go to per-GPU send segments
+  uint8_t* send_pkt = nullptr; uint32_t* pcnt = nullptr;
+  uint32_t nranks = 0, rank = 0, cap_pkt = 0;
 };
 hipError_t launch_fused(const FusedLaunch& f, const LaunchCfg& cfg, hipStream_t s);
 size_t fused_lds_bytes(int hash_mode, int acl_mode, uint32_t acl_tiles);

@@ -14,6 +14,7 @@
 //  * per-port counters aggregated in LDS, flushed once per workgroup; per-flow counters are one
 //    packed 64-bit atomic per packet.
 #include "device.h"
+#include "shard.h"
 
 namespace nfdp {
 
@@ -35,6 +36,12 @@ struct FusedArgs {
   const uint32_t* toep_tab;       // [16][256] byte tables (LDS hash variant)
   uint32_t acl_tiles;             // ceil(n_acl / 16)
   uint32_t flags;                 // ablation: bit0 no port/drop counters, bit1 no latency samples
+  // REMOTE variant (replicated tables, N GPUs): frames whose egress port lives on another GPU
+  // go to segment[egress gpu] of send_pkt (64-B slot + 4-B meta, fill count in pcnt) instead of
+  // out[i]; out_meta[i] then says kRemote.
+  uint8_t* send_pkt;
+  uint32_t* pcnt;
+  uint32_t nranks, rank, cap_pkt;
 };
 
 __device__ __forceinline__ size_t lds_align16(size_t x) { return (x + 15) & ~(size_t)15; }
@@ -56,9 +63,10 @@ __host__ __device__ inline LdsLayout lds_layout(int hash_mode, int acl_mode, uin
   return L;
 }
 
-template <int HASH, int ACL>
+template <int HASH, int ACL, bool REMOTE>
 __global__ __launch_bounds__(kBlock, 4) void fused_kernel(FusedArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ uint32_t rcnt[REMOTE ? kMaxRanks : 1], rbase[REMOTE ? kMaxRanks : 1];
   const LdsLayout L = lds_layout(HASH, ACL, a.acl_tiles);
   v4i* lw = reinterpret_cast<v4i*>(smem + L.acl_w);
   v4i* lc = reinterpret_cast<v4i*>(smem + L.acl_c);
@@ -122,14 +130,34 @@ __global__ __launch_bounds__(kBlock, 4) void fused_kernel(FusedArgs a) {
       }
     }
     const EgressDecision e = chain_stage(a.t, p, st, hit, act, acl_rule, hash);
+    bool to_peer = false;
+    uint32_t reason = e.reason;
+    uint4* dst = a.out + (size_t)i * 4;
+    if constexpr (REMOTE) {
+      // egress GPU of the frame; block-aggregated slot in that GPU's segment (all threads call)
+      const uint32_t eg = e.reason ? a.rank : (uint32_t)a.t.ports[e.out_port].gpu;
+      const bool remote = valid && !e.reason && eg != a.rank && eg < a.nranks;
+      const uint32_t pos = reserve_block(a.pcnt, eg, remote, a.nranks, rcnt, rbase);
+      if (remote) {
+        if (pos < a.cap_pkt) {
+          uint8_t* segp = a.send_pkt + (size_t)eg * pkt_seg_bytes(a.cap_pkt);
+          dst = reinterpret_cast<uint4*>(segp + 64 + (size_t)pos * 64);
+          reinterpret_cast<uint32_t*>(segp + pkt_meta_off(a.cap_pkt))[pos] =
+              make_meta(e.out_port, p.len + (e.push ? 4u : 0u), kOk, e.mirror != 0);
+          to_peer = true;
+        } else {
+          reason = kOverflow;
+        }
+      }
+    }
     if (valid) {
       uint32_t o[kSlotDwords];
       emit(p, e.tci, e.push != 0, o);
-      const uint32_t olen = e.reason ? 0u : p.len + (e.push ? 4u : 0u);
-      uint4* dst = a.out + (size_t)i * 4;
+      const uint32_t olen = reason ? 0u : p.len + (e.push ? 4u : 0u);
 #pragma unroll
       for (int q = 0; q < 4; ++q) dst[q] = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
-      a.out_meta[i] = make_meta(e.out_port, olen, e.reason, e.mirror != 0);
+      a.out_meta[i] = to_peer ? make_meta(e.out_port, olen, kRemote, e.mirror != 0)
+                              : make_meta(reason ? kPortNone : e.out_port, olen, reason, !reason && e.mirror != 0);
       // counters
       if (a.flags & 1u) {
       } else if (st.in_port < kLdsPorts) {
@@ -138,14 +166,16 @@ __global__ __launch_bounds__(kBlock, 4) void fused_kernel(FusedArgs a) {
         atomicAdd(a.port_ctr + 2 * st.in_port, ctr_inc(st.wire_len));
       }
       if (a.flags & 1u) {
-      } else if (e.reason) {
-        atomicAdd(&drops[e.reason & (kNumReasons - 1)], 1u);
+      } else if (reason) {
+        atomicAdd(&drops[reason & (kNumReasons - 1)], 1u);
+      } else if (to_peer) {
+        // tx is counted where the frame leaves: the egress GPU's egress_kernel
       } else if (e.out_port < kLdsPorts) {
         atomicAdd(&pc[2 * kLdsPorts + e.out_port], 1u); atomicAdd(&pc[3 * kLdsPorts + e.out_port], olen);
       } else {
         atomicAdd(a.port_ctr + 2 * e.out_port + 1, ctr_inc(olen));
       }
-      if (a.lat && !(a.flags & 2u) && (i & 15u) == 0) {
+      if (a.lat && !(a.flags & 2u) && (i & 15u) == 0 && !to_peer) {
         const unsigned long long now = __builtin_amdgcn_s_memrealtime();
         a.lat[i >> 4] = (uint32_t)(now - t0);
       }
@@ -190,14 +220,19 @@ size_t fused_lds_bytes(int hash_mode, int acl_mode, uint32_t acl_tiles) {
   return lds_layout(hash_mode, acl_mode, acl_tiles).total;
 }
 
-template <int H, int A>
+template <int H, int A, bool R>
 static hipError_t launch_fused_t(const FusedArgs& a, int num_cus, hipStream_t s) {
+  // static LDS (REMOTE reservation counters) + dynamic tables must fit 160 KiB
+  constexpr size_t kStatic = 2 * (R ? kMaxRanks : 1) * sizeof(uint32_t);
+  constexpr size_t kMaxDyn = 160 * 1024 - kStatic;
   const size_t lds = lds_layout(H, A, a.acl_tiles).total;
-  if (lds > 160 * 1024) return hipErrorInvalidValue;
+  if (lds > kMaxDyn) return hipErrorInvalidValue;
+  if (R && (a.nranks == 0 || a.nranks > kMaxRanks || a.rank >= a.nranks || !a.send_pkt || !a.pcnt))
+    return hipErrorInvalidValue;
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&fused_kernel<H, A>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&fused_kernel<H, A, R>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxDyn);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
@@ -207,7 +242,7 @@ static hipError_t launch_fused_t(const FusedArgs& a, int num_cus, hipStream_t s)
   uint32_t grid = (uint32_t)(per_cu * num_cus);
   if (need < grid) grid = need;
   if (grid == 0) return hipSuccess;
-  hipLaunchKernelGGL((fused_kernel<H, A>), dim3(grid), dim3(kBlock), lds, s, a);
+  hipLaunchKernelGGL((fused_kernel<H, A, R>), dim3(grid), dim3(kBlock), lds, s, a);
   return hipGetLastError();
 }
 
@@ -227,9 +262,14 @@ hipError_t launch_fused(const FusedLaunch& f, const LaunchCfg& cfg, hipStream_t 
   a.toep_frag = reinterpret_cast<const v4i*>(f.toep_frag);
   a.toep_tab = f.toep_tab;
   a.flags = f.flags;
+  a.send_pkt = f.send_pkt; a.pcnt = f.pcnt;
+  a.nranks = f.nranks; a.rank = f.rank; a.cap_pkt = f.cap_pkt;
+  const bool remote = f.nranks > 1;
   if (cfg.acl_mode == kAclMfma && (f.acl_tiles == 0 || f.acl_tiles > 64)) return hipErrorInvalidValue;
   const int h = cfg.hash_mode, ac = cfg.acl_mode, cu = cfg.num_cus;
-#define NFDP_CASE(HH, AA) if (h == HH && ac == AA) return launch_fused_t<HH, AA>(a, cu, s);
+#define NFDP_CASE(HH, AA)                                                                  \
+  if (h == HH && ac == AA)                                                                 \
+    return remote ? launch_fused_t<HH, AA, true>(a, cu, s) : launch_fused_t<HH, AA, false>(a, cu, s);
   NFDP_CASE(0, 0) NFDP_CASE(0, 1) NFDP_CASE(0, 2)
   NFDP_CASE(1, 0) NFDP_CASE(1, 1) NFDP_CASE(1, 2)
   NFDP_CASE(2, 0) NFDP_CASE(2, 1) NFDP_CASE(2, 2)

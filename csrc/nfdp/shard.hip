@@ -4,37 +4,6 @@
 
 namespace nfdp {
 
-constexpr uint32_t kMaxRanks = 64;
-
-// Block-aggregated slot reservation: waves claim offsets in LDS counters (one LDS atomic per
-// wave and destination), then ONE global atomic per (workgroup iteration, destination) turns
-// them into segment positions.  (A per-wave global atomic on one counter serialised 16K waves
-// per 1M packets: 200 us of a 1M-packet ingress pass.)  Called by every thread of the block.
-__device__ __forceinline__ uint32_t reserve_block(uint32_t* gcnt, uint32_t dest, bool active, uint32_t nranks,
-                                                  uint32_t* lcnt, uint32_t* lbase) {
-  const uint32_t lane = threadIdx.x & 63u;
-  const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  if (threadIdx.x < nranks) lcnt[threadIdx.x] = 0;
-  __syncthreads();
-  uint32_t off = 0;
-  for (uint32_t o = 0; o < nranks; ++o) {
-    const unsigned long long m = __ballot(active && dest == o);
-    if (m == 0) continue;
-    const int leader = __ffsll((long long)m) - 1;
-    uint32_t base = 0;
-    if ((int)lane == leader) base = atomicAdd(&lcnt[o], (uint32_t)__popcll(m));
-    base = __shfl(base, leader);
-    if (active && dest == o) off = base + (uint32_t)__popcll(m & lt);
-  }
-  __syncthreads();
-  if (threadIdx.x < nranks) {
-    const uint32_t c = lcnt[threadIdx.x];
-    lbase[threadIdx.x] = c ? atomicAdd(&gcnt[threadIdx.x], c) : 0u;
-  }
-  __syncthreads();
-  return active ? lbase[dest] + off : 0xFFFFFFFFu;
-}
-
 struct ShardLds {
   size_t acl_w, acl_c, toep_f, toep_t, kx, pc, total;
 };
