@@ -267,7 +267,7 @@ void oracle_run_remote(const TablesView& t, const uint32_t* pkts, const uint32_t
       out_meta[i] = make_meta(e.out_port, olen, kRemote, e.mirror != 0);
     } else {
       std::memcpy(out + (size_t)i * kSlotDwords, o, sizeof(o));
-      out_meta[i] = make_meta(reason ? kPortNone : e.out_port, olen, reason, !reason && e.mirror != 0);
+      out_meta[i] = make_meta(reason == kOverflow ? kPortNone : e.out_port, olen, reason, reason != kOverflow && e.mirror != 0);
     }
     if (port_ctr) {
       if (st.in_port < (uint32_t)kMaxPorts) port_ctr[2 * st.in_port] += ctr_inc(st.wire_len);

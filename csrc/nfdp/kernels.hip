@@ -157,7 +157,7 @@ __global__ __launch_bounds__(kBlock, 4) void fused_kernel(FusedArgs a) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) dst[q] = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
       a.out_meta[i] = to_peer ? make_meta(e.out_port, olen, kRemote, e.mirror != 0)
-                              : make_meta(reason ? kPortNone : e.out_port, olen, reason, !reason && e.mirror != 0);
+                              : make_meta(reason == kOverflow ? kPortNone : e.out_port, olen, reason, reason != kOverflow && e.mirror != 0);
       // counters
       if (a.flags & 1u) {
       } else if (st.in_port < kLdsPorts) {

@@ -192,7 +192,7 @@ __global__ __launch_bounds__(kBlock) void apply_kernel(ApplyArgs a) {
         a.out_meta[i] = make_meta(e.out_port, olen, kRemote);
       } else {
         dst = a.out + (size_t)i * 4;
-        a.out_meta[i] = make_meta(reason ? kPortNone : e.out_port, reason ? 0u : olen, reason, !reason && e.mirror != 0);
+        a.out_meta[i] = make_meta(reason == kOverflow ? kPortNone : e.out_port, reason ? 0u : olen, reason, reason != kOverflow && e.mirror != 0);
       }
 #pragma unroll
       for (int q = 0; q < 4; ++q) dst[q] = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);

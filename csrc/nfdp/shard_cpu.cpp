@@ -105,7 +105,7 @@ void apply_cpu(const ApplyArgs& a) {
       a.out_meta[i] = make_meta(e.out_port, olen, kRemote);
     } else {
       std::memcpy(reinterpret_cast<uint8_t*>(a.out) + (size_t)i * 64, o, 64);
-      a.out_meta[i] = make_meta(reason ? kPortNone : e.out_port, reason ? 0u : olen, reason, !reason && e.mirror != 0);
+      a.out_meta[i] = make_meta(reason == kOverflow ? kPortNone : e.out_port, reason ? 0u : olen, reason, reason != kOverflow && e.mirror != 0);
     }
     if (st.in_port < (uint32_t)kMaxPorts) a.port_ctr[2 * st.in_port] += ctr_inc(st.wire_len);
     if (reason) a.drop_ctr[reason & (kNumReasons - 1)] += 1;

@@ -27,7 +27,7 @@ def build_vsp(a, pm: PathManager):
     if a.vendor == "amd-gpu":
         from ..vsp.gpu import GpuVsp
 
-        return GpuVsp(pm, device=a.device or None, flow_buckets=a.flow_buckets)
+        return GpuVsp(pm, device=a.device or None, flow_buckets=a.flow_buckets, state_dir=a.state_dir or None)
     from ..cni.netlink import RtNetlink
     from ..platform.platform import SysfsPlatform
     from ..utils.cmdrunner import HostRunner
@@ -71,6 +71,7 @@ def main(argv=None, stop: threading.Event | None = None) -> int:
     ap.add_argument("--p4rt-addr", default="127.0.0.1:9559")
     ap.add_argument("--acc-macs", default="")
     ap.add_argument("--mode", default="ipu")
+    ap.add_argument("--state-dir", default="", help="amd-gpu: journal + snapshot directory (resume on restart)")
     a = ap.parse_args(argv)
     logging.basicConfig(level=logging.INFO)
     vsp = build_vsp(a, PathManager(a.root)).start()
@@ -79,6 +80,8 @@ def main(argv=None, stop: threading.Event | None = None) -> int:
         signal.signal(signal.SIGTERM, lambda *_: stop.set())
         signal.signal(signal.SIGINT, lambda *_: stop.set())
     stop.wait()
+    if getattr(vsp, "journal", None) is not None:
+        vsp.checkpoint()  # clean shutdown: snapshot so the next start skips the replay
     vsp.stop()
     return 0
 

@@ -18,7 +18,9 @@ import threading
 from http.server import BaseHTTPRequestHandler
 from typing import Callable
 
+from ..utils.faults import FAULTS
 from ..utils.metrics import CONTROL
+from ..utils.trace import TRACER
 from ..utils.paths import PathManager
 from . import logging as clog
 from .helper import read_cni_config
@@ -92,10 +94,12 @@ class Server:
         req = cni_request_to_pod_request(cr)
         clog.set_labels(req.net_name, req.container_id, req.netns, req.ifname)
         result = None
-        if req.command == CNI_ADD:
-            result = self.add_handler(req)
-        elif req.command == CNI_DEL:
-            result = self.del_handler(req)
+        FAULTS.check(f"cni.{req.command}")
+        with TRACER.span(f"cni.{req.command}", pod=f"{req.pod_namespace}/{req.pod_name}", ifname=req.ifname):
+            if req.command == CNI_ADD:
+                result = self.add_handler(req)
+            elif req.command == CNI_DEL:
+                result = self.del_handler(req)
         self.requests_served += 1
         return json.dumps({"Result": result}).encode()
 

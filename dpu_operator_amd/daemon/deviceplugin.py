@@ -24,6 +24,7 @@ from .. import vars as V
 from ..cni.sriov.utils import is_valid_pci_address
 from ..proto import DEVICE_PLUGIN_VERSION, HEALTHY, deviceplugin as dp
 from ..proto.grpcutil import Stub, service_handler, unix_target
+from ..utils.faults import FAULTS
 from ..utils.metrics import CONTROL
 from ..utils.paths import PathManager
 
@@ -80,6 +81,7 @@ class DevicePluginServer:
         old: dict | None = None
         while not self._stop.is_set() and context.is_active():
             try:
+                FAULTS.check("deviceplugin.GetDevices")
                 new = self.handler.get_devices()
             except Exception as e:  # noqa: BLE001
                 log.error("GetDevices failed: %s", e)

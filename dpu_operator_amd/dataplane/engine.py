@@ -18,6 +18,8 @@ from dataclasses import dataclass, field
 import numpy as np
 
 from ..native import nfdp as _nfdp_mod
+from ..utils.faults import FAULTS
+from ..utils.trace import TRACER
 from . import tables as T
 
 HASH_MODES = {"scalar": 0, "lds": 1, "mfma": 2}
@@ -124,6 +126,11 @@ class DataPlane:
     # ------------------------------------------------------------------ commit
     def commit(self, full: bool = False) -> dict:
         """Push host table changes to the device.  Returns what was sent."""
+        FAULTS.check("dataplane.commit")
+        with TRACER.span("dataplane.commit", full=full):
+            return self._commit(full)
+
+    def _commit(self, full: bool) -> dict:
         sent = {}
         for name, model in (("ports", self.ports), ("chains", self.chains), ("macs", self.macs), ("lag", self.lag)):
             if full or self._versions.get(name) != model.version or name not in self._dev:
@@ -207,6 +214,13 @@ class DataPlane:
             flags: int = 0) -> BatchResult:
         """Process one batch.  GPU: pkts/inmeta torch tensors on the device ([n,64] uint8 / [n]
         int32); CPU: numpy arrays (runs the C++ oracle)."""
+        n = int(pkts.shape[0])
+        if TRACER.enabled:
+            with TRACER.span("dataplane.run", n=n, gpu=self.gpu):
+                return self._run(pkts, inmeta, out, meta, lat, stamp, stream, flags)
+        return self._run(pkts, inmeta, out, meta, lat, stamp, stream, flags)
+
+    def _run(self, pkts, inmeta, out, meta, lat, stamp, stream, flags) -> BatchResult:
         n = int(pkts.shape[0])
         if out is None:
             out, meta, lat = self.alloc_batch(n)

@@ -18,10 +18,16 @@ import grpc
 
 from ..proto import GoogleEmpty, opi, vendor
 from ..proto.grpcutil import service_handler, unix_target
+from ..utils.faults import FAULTS, FaultError
 from ..utils.metrics import CONTROL
+from ..utils.trace import TRACER
 from ..utils.paths import PathManager
 
 log = logging.getLogger("dpu.vsp")
+
+
+def _fault_code(e: FaultError) -> grpc.StatusCode:
+    return grpc.StatusCode.UNAVAILABLE if e.kind == "unavailable" else grpc.StatusCode.INTERNAL
 
 
 class VspBase:
@@ -57,7 +63,8 @@ class VspBase:
 
     # -------------------------------------------------------------- wire adapters
     def _call(self, name, fn, *args):
-        with self._lock:
+        FAULTS.check(f"vsp.{name}")
+        with self._lock, TRACER.span(f"vsp.{name}"):
             self.calls.append((name, args))
             try:
                 out = fn(*args)
@@ -65,11 +72,17 @@ class VspBase:
                 CONTROL.vsp_calls.labels(name, "error").inc()
                 raise
             CONTROL.vsp_calls.labels(name, "success").inc()
+            self._journal(name, args)
             return out
+
+    def _journal(self, name: str, args: tuple) -> None:
+        """Hook for state journaling of mutating RPCs (see vsp/gpu.py)."""
 
     def Init(self, request, context):
         try:
             ip, port = self._call("Init", self.init, request.dpu_mode, request.dpu_identifier)
+        except FaultError as e:
+            context.abort(grpc.StatusCode.UNAVAILABLE if e.kind == "unavailable" else grpc.StatusCode.INTERNAL, str(e))
         except Exception as e:  # noqa: BLE001
             context.abort(grpc.StatusCode.INTERNAL, f"Init failed: {e}")
         return vendor.IpPort(ip=ip, port=port)
@@ -77,6 +90,8 @@ class VspBase:
     def CreateNetworkFunction(self, request, context):
         try:
             self._call("CreateNetworkFunction", self.create_network_function, request.input, request.output)
+        except FaultError as e:
+            context.abort(_fault_code(e), str(e))
         except Exception as e:  # noqa: BLE001
             context.abort(grpc.StatusCode.INTERNAL, str(e))
         return vendor.Empty()
@@ -84,12 +99,17 @@ class VspBase:
     def DeleteNetworkFunction(self, request, context):
         try:
             self._call("DeleteNetworkFunction", self.delete_network_function, request.input, request.output)
+        except FaultError as e:
+            context.abort(_fault_code(e), str(e))
         except Exception as e:  # noqa: BLE001
             context.abort(grpc.StatusCode.INTERNAL, str(e))
         return vendor.Empty()
 
     def GetDevices(self, request, context):
-        devs = self._call("GetDevices", self.get_devices)
+        try:
+            devs = self._call("GetDevices", self.get_devices)
+        except FaultError as e:
+            context.abort(_fault_code(e), str(e))
         resp = vendor.DeviceListResponse()
         for did, health in devs.items():
             resp.devices[did].ID = did
@@ -99,6 +119,8 @@ class VspBase:
     def SetNumVfs(self, request, context):
         try:
             n = self._call("SetNumVfs", self.set_num_vfs, request.vf_cnt)
+        except FaultError as e:
+            context.abort(_fault_code(e), str(e))
         except Exception as e:  # noqa: BLE001
             context.abort(grpc.StatusCode.INTERNAL, f"SetNumVfs failed: {e}")
         return vendor.VfCount(vf_cnt=n)
@@ -108,6 +130,8 @@ class VspBase:
         try:
             self._call("CreateBridgePort", self.create_bridge_port, bp.name, bytes(bp.spec.mac_address),
                        bp.spec.ptype, list(bp.spec.logical_bridges))
+        except FaultError as e:
+            context.abort(_fault_code(e), str(e))
         except Exception as e:  # noqa: BLE001
             context.abort(grpc.StatusCode.INTERNAL, f"CreateBridgePort failed: {e}")
         out = opi.BridgePort()
@@ -118,6 +142,8 @@ class VspBase:
     def DeleteBridgePort(self, request, context):
         try:
             self._call("DeleteBridgePort", self.delete_bridge_port, request.name)
+        except FaultError as e:
+            context.abort(_fault_code(e), str(e))
         except Exception as e:  # noqa: BLE001
             context.abort(grpc.StatusCode.INTERNAL, f"DeleteBridgePort failed: {e}")
         return GoogleEmpty()

@@ -17,6 +17,13 @@ It implements the same four services as the reference's VSPs, but instead of pro
 
 Ports: vport i = data-plane port i; the uplink ("wire", the RPM/SFP port of the reference's VSPs)
 is port 4000.  All mutations happen under the VSP lock and are committed atomically per RPC.
+
+Checkpoint / resume (the reference's VSPs lose all state on restart): with `state_dir`
+every successful mutating RPC is appended to a write-ahead journal (utils/journal.py) before the
+RPC returns; `checkpoint()` writes a JSON state snapshot plus a data-plane snapshot (flows,
+counters; dataplane/snapshot.py) and truncates the journal.  A new GpuVsp on the same directory
+restores snapshot -> data plane -> journal tail, so vport MACs, bridge ports, NF steering, GPU
+chains and installed flows survive a crash of the VSP process.
 """
 from __future__ import annotations
 
@@ -30,6 +37,7 @@ import numpy as np
 from ..cni.netlink import FakeNetlink, Link, NetlinkManager
 from ..dataplane import tables as T
 from ..dataplane.engine import DataPlane
+from ..utils.journal import Journal
 from .base import VspBase
 
 log = logging.getLogger("dpu.vsp.gpu")
@@ -38,6 +46,27 @@ WIRE_PORT = 4000
 VF_BRIDGE = 1
 STEER_BRIDGE = 2      # no MAC entries: every frame takes its port's default output
 NF_BRIDGE_BASE = 100
+
+# journaled RPC -> hook; args are JSON-encoded (bytes as {"hex": ...})
+_MUTATING = {"SetNumVfs": "set_num_vfs", "CreateBridgePort": "create_bridge_port",
+             "DeleteBridgePort": "delete_bridge_port", "CreateNetworkFunction": "create_network_function",
+             "DeleteNetworkFunction": "delete_network_function", "Init": "init", "GpuChain": "on_gpu_chain"}
+
+
+def _enc(a):
+    if isinstance(a, (bytes, bytearray)):
+        return {"hex": bytes(a).hex()}
+    if isinstance(a, (list, tuple)):
+        return [_enc(x) for x in a]
+    return a
+
+
+def _dec(a):
+    if isinstance(a, dict) and set(a) == {"hex"}:
+        return bytes.fromhex(a["hex"])
+    if isinstance(a, list):
+        return [_dec(x) for x in a]
+    return a
 
 
 def _mac_str(b: bytes) -> str:
@@ -53,7 +82,7 @@ class GpuVsp(VspBase):
 
     def __init__(self, path_manager=None, device: str | None = None, nl: NetlinkManager | None = None,
                  opi_port: int = 0, flow_buckets: int = 1 << 16, vport_prefix: str = "dpuvp",
-                 hash_mode: str = "mfma", acl_mode: str = "mfma"):
+                 hash_mode: str = "mfma", acl_mode: str = "mfma", state_dir: str | None = None):
         super().__init__(path_manager)
         if device is None:
             try:
@@ -76,6 +105,12 @@ class GpuVsp(VspBase):
         self.dpu_mode = True
         self.healthy = True
         self._salt = int.from_bytes(os.urandom(1), "little")
+        self.chain_kinds: dict[str, list[str]] = {}
+        self.journal = Journal(state_dir, "gpu-vsp") if state_dir else None
+        self._replaying = False
+        self.restored = 0
+        if self.journal is not None:
+            self._restore()
 
     # ------------------------------------------------------------------ helpers
     def _ensure_dp(self) -> DataPlane:
@@ -103,6 +138,12 @@ class GpuVsp(VspBase):
         p = s.getsockname()[1]
         s.close()
         return p
+
+    def _ensure_tap(self, name: str, mac: str) -> None:
+        """Create the vport netdev unless it exists in any namespace (a restart must not
+        duplicate a vport that the CNI already moved into a pod)."""
+        if isinstance(self.nl, FakeNetlink) and not any(name in links for links in self.nl.ns.values()):
+            self.nl.add_link(Link(name=name, mac=mac, up=True, kind="tap"))
 
     def _vf_ports(self) -> list[int]:
         return sorted(self.bridge_ports.values())
@@ -170,8 +211,7 @@ class GpuVsp(VspBase):
             if i in self.vports:
                 continue
             name, mac = f"{self.prefix}{i}", _local_mac(i, self._salt)
-            if isinstance(self.nl, FakeNetlink):
-                self.nl.add_link(Link(name=name, mac=mac, up=True, kind="tap"))
+            self._ensure_tap(name, mac)
             self.vports[i] = {"name": name, "mac": mac, "role": "free", "vlan": 0, "pod_mac": mac, "bridge": VF_BRIDGE}
             self._program_port(i)
         for i in [i for i in self.vports if i >= n and self.vports[i]["role"] == "free"]:
@@ -235,8 +275,72 @@ class GpuVsp(VspBase):
             else:
                 cid = self.dp.chains.add(kinds)
                 self.gpu_chains[sfc_name] = cid
+            self.chain_kinds[sfc_name] = list(kinds)
             self._commit()
+            self._journal("GpuChain", (sfc_name, list(kinds)))
             return cid
+
+    # ------------------------------------------------------------------ checkpoint / resume
+    def _journal(self, name: str, args: tuple) -> None:
+        if self.journal is None or self._replaying or name not in _MUTATING:
+            return
+        self.journal.append({"rpc": name, "args": _enc(list(args))})
+        if self.journal.needs_compaction():
+            self.checkpoint()
+
+    def _state(self) -> dict:
+        return {"salt": self._salt, "dpu_mode": self.dpu_mode, "opi_port": self.opi_port,
+                "vports": {str(i): v for i, v in self.vports.items()}, "bridge_ports": self.bridge_ports,
+                "nfs": self.nfs, "gpu_chains": {k: [cid, self.chain_kinds.get(k, [])] for k, cid in self.gpu_chains.items()},
+                "dp_snapshot": self.dp is not None}
+
+    def _dp_snap_path(self) -> str:
+        return os.path.join(os.path.dirname(self.journal.log_path), "gpu-vsp.dp.npz")
+
+    def checkpoint(self) -> None:
+        """Snapshot control state + data-plane tables, then truncate the journal."""
+        from ..dataplane import snapshot
+
+        with self._lock:
+            if self.journal is None:
+                raise RuntimeError("GpuVsp was created without state_dir")
+            if self.dp is not None:
+                snapshot.save(self.dp, self._dp_snap_path())
+            self.journal.compact(self._state())
+
+    def _restore(self) -> None:
+        from ..dataplane import snapshot
+
+        snap, recs = self.journal.load()
+        if snap is None and not recs:
+            self.journal.append({"rpc": "_meta", "salt": self._salt})
+            return
+        self._replaying = True
+        try:
+            with self._lock:
+                if snap is not None:
+                    self._salt = int(snap["salt"])
+                    self.dpu_mode = bool(snap["dpu_mode"])
+                    self.opi_port = self.opi_port or int(snap.get("opi_port") or 0)
+                    self.vports = {int(i): v for i, v in snap["vports"].items()}
+                    self.bridge_ports = {k: int(v) for k, v in snap["bridge_ports"].items()}
+                    self.nfs = snap["nfs"]
+                    if snap.get("dp_snapshot"):
+                        dp = self._ensure_dp()
+                        snapshot.load(dp, self._dp_snap_path())
+                        for name, (cid, kinds) in snap["gpu_chains"].items():
+                            self.gpu_chains[name] = int(cid)
+                            self.chain_kinds[name] = list(kinds)
+                    for v in self.vports.values():
+                        self._ensure_tap(v["name"], v["mac"])
+                for r in recs:
+                    if r["rpc"] == "_meta":
+                        self._salt = int(r["salt"])
+                        continue
+                    getattr(self, _MUTATING[r["rpc"]])(*_dec(r["args"]))
+                    self.restored += 1
+        finally:
+            self._replaying = False
 
     # ------------------------------------------------------------------ data path access
     def install_flows(self, keys: np.ndarray, actions: np.ndarray) -> None:

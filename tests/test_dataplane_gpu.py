@@ -245,3 +245,21 @@ def test_replicated_remote_kernel_matches_cpu_twin():
         assert np.array_equal(g.dp.port_counters(), c.dp.port_counters())
         assert g.dp.drop_counters() == c.dp.drop_counters()
     assert n_remote > (1 << 14)  # 3/4 of the traffic crossed "GPUs"
+
+
+def test_snapshot_restore_cpu_to_gpu(tmp_path):
+    """A CPU-side checkpoint restores onto the GPU tables and forwards bit-identically."""
+    from dpu_operator_amd.dataplane import snapshot
+
+    torch = _torch()
+    c, sc = _build("cpu", n_flows=3000, buckets=1 << 11)
+    path = str(tmp_path / "dp.npz")
+    snapshot.save(c, path)
+    g = DataPlane(device="cuda", flow_buckets=1 << 11, hash_mode="mfma", acl_mode="mfma")
+    snapshot.load(g, path)
+    pk, im = S.traffic(sc, 8192, seed=9)
+    r = g.run(torch.from_numpy(pk).cuda(), torch.from_numpy(im.view(np.int32)).cuda())
+    rc = c.run(pk, im)
+    torch.cuda.synchronize()
+    assert np.array_equal(r.meta.cpu().numpy().view(np.uint32), rc.meta)
+    assert np.array_equal(r.out.cpu().numpy(), rc.out)
