@@ -190,8 +190,19 @@ void Agent::set_link(const FnKey& k, bool up) {
   m.data.resize(sizeof(Notify));
   std::memcpy(m.data.data(), &n, sizeof(Notify));
   {
+    // Coalesce: a link notification still waiting for ring space is overwritten with the newest
+    // state instead of queueing another one, so a flapping link cannot grow the queue (or delay
+    // responses queued behind it) without bound — the host only needs the current state.
     std::lock_guard<std::mutex> g(out_mu_);
-    out_.push_back(std::move(m));
+    bool merged = false;
+    for (auto it = out_.rbegin(); it != out_.rend(); ++it) {
+      if ((it->hdr.flags & kFlagNotify) && it->hdr.fn == m.hdr.fn && it->hdr.vf_idx == m.hdr.vf_idx) {
+        std::memcpy(it->data.data(), &n, sizeof(Notify));
+        merged = true;
+        break;
+      }
+    }
+    if (!merged) out_.push_back(std::move(m));
   }
   if (plugin_) plugin_->broadcast_event(up ? PluginServer::kEvLinkUp : PluginServer::kEvLinkDown, {});
   std::lock_guard<std::mutex> g(cnt_mu_);
@@ -245,6 +256,20 @@ HostCtrl::HostCtrl(const std::string& mbox_path, uint32_t host_version)
   last_hb_change_ = clock_t_::now();
 }
 
+namespace {
+// Announces a priority waiter on HostCtrl::mu_ until the lock is taken.
+struct PriorityLock {
+  explicit PriorityLock(std::atomic<int>& c) : c_(c) { c_.fetch_add(1, std::memory_order_acq_rel); }
+  void acquired() {
+    if (!done_) c_.fetch_sub(1, std::memory_order_acq_rel);
+    done_ = true;
+  }
+  ~PriorityLock() { acquired(); }
+  std::atomic<int>& c_;
+  bool done_ = false;
+};
+}  // namespace
+
 bool HostCtrl::wait_ready(int timeout_ms) {
   const auto dl = clock_t_::now() + std::chrono::milliseconds(timeout_ms);
   Info& in = mbox_.info();
@@ -278,6 +303,7 @@ void HostCtrl::drain(int timeout_ms, uint16_t want_id, Response* out, bool* got)
         Notify n;
         std::memset(&n, 0, sizeof(n));
         std::memcpy(&n, m.data.data(), m.hdr.sz < sizeof(n) ? m.hdr.sz : sizeof(n));
+        if (notes_.size() >= kMaxPendingNotes) notes_.erase(notes_.begin());  // keep the newest
         notes_.push_back(n);
       } else if (m.hdr.flags & kFlagCustom) {
         custom_.push_back(m);
@@ -290,6 +316,8 @@ void HostCtrl::drain(int timeout_ms, uint16_t want_id, Response* out, bool* got)
 }
 
 Response HostCtrl::request(uint32_t pem, uint32_t pf, int32_t vf, Request req, int timeout_ms) {
+  // yield to resets / notification drains waiting for the lock (std::mutex is not fair)
+  while (prio_.load(std::memory_order_acquire) > 0) std::this_thread::yield();
   std::lock_guard<std::mutex> g(mu_);
   MsgHdr h{};
   h.fn = MsgHdr::make_fn(pem, pf, vf >= 0);
@@ -312,7 +340,9 @@ Response HostCtrl::request(uint32_t pem, uint32_t pf, int32_t vf, Request req, i
 }
 
 std::vector<Notify> HostCtrl::take_notifications() {
+  PriorityLock pl(prio_);
   std::lock_guard<std::mutex> g(mu_);
+  pl.acquired();
   Response r;
   bool got;
   drain(0, 0, &r, &got);
@@ -322,7 +352,9 @@ std::vector<Notify> HostCtrl::take_notifications() {
 }
 
 std::vector<Msg> HostCtrl::take_custom() {
+  PriorityLock pl(prio_);
   std::lock_guard<std::mutex> g(mu_);
+  pl.acquired();
   Response r;
   bool got;
   drain(0, 0, &r, &got);
@@ -359,7 +391,9 @@ void HostCtrl::host_heartbeat() { mbox_.info().host_heartbeat.fetch_add(1, std::
 uint64_t HostCtrl::fw_heartbeat() const { return mbox_.info().fw_heartbeat.load(std::memory_order_acquire); }
 
 bool HostCtrl::reset(int timeout_ms) {
+  PriorityLock pl(prio_);
   std::lock_guard<std::mutex> g(mu_);
+  pl.acquired();
   Info& in = mbox_.info();
   const uint64_t want = in.host_resets.fetch_add(1, std::memory_order_acq_rel) + 1;
   const auto dl = clock_t_::now() + std::chrono::milliseconds(timeout_ms);

@@ -77,6 +77,7 @@ class Agent {
 // Host-side client: what the host netdev driver does with the mailbox.
 class HostCtrl {
  public:
+  static constexpr size_t kMaxPendingNotes = 4096;
   explicit HostCtrl(const std::string& mbox_path, uint32_t host_version = kCpVersionMax);
   bool wait_ready(int timeout_ms);
   // Synchronous request for function (pem, pf, vf|-1); throws on timeout.
@@ -99,6 +100,7 @@ class HostCtrl {
   uint32_t host_version_;
   uint16_t next_id_ = 1;
   std::mutex mu_;
+  std::atomic<int> prio_{0};  // resets / drains waiting for mu_: requests back off
   std::vector<Notify> notes_;
   std::vector<Msg> custom_;
   uint64_t last_hb_ = 0;

@@ -139,6 +139,30 @@ def build_exe(name: str, force: bool = False, verbose: bool = False) -> Path:
     return out
 
 
+AGENT_CORE = ["mbox.cpp", "ctrl_net.cpp", "config.cpp", "agent.cpp", "plugin_server.cpp"]
+SANITIZERS = {"tsan": ["-fsanitize=thread"], "asan": ["-fsanitize=address,undefined", "-fno-omit-frame-pointer"]}
+
+
+def build_sanitized(kind: str, verbose: bool = False) -> Path:
+    """Host-only sanitizer build of the agent stress driver (csrc/agent/stress_main.cpp).
+    GPU sanitizers are unavailable on the MI355X pool; the native runtime is pure host code."""
+    d = CSRC / "agent"
+    out = BUILD / "sanitize" / f"agent-stress-{kind}"
+    out.parent.mkdir(parents=True, exist_ok=True)
+    srcs = [d / s for s in AGENT_CORE + ["stress_main.cpp"]]
+    newest = max(max(s.stat().st_mtime for s in srcs), _newest_header(d))
+    if out.exists() and out.stat().st_mtime >= newest:
+        return out
+    cmd = [shutil.which("g++") or "g++", "-std=c++17", "-O1", "-g", "-pthread", *SANITIZERS[kind],
+           *map(str, srcs), "-o", str(out)]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"sanitizer build failed ({kind})\n{r.stdout}\n{r.stderr}")
+    return out
+
+
 def build_all(force: bool = False, verbose: bool = False) -> list[Path]:
     outs = []
     for name, spec in MODULES.items():

@@ -239,3 +239,23 @@ def test_standalone_binary(tmp):
         p.send_signal(signal.SIGTERM)
         out, err = p.communicate(timeout=10)
     assert p.returncode == 0 and "stopped" in out
+
+
+@pytest.mark.parametrize("kind", ["tsan", "asan"])
+def test_agent_sanitizer_stress(kind):
+    """Race / memory-error detection on the native agent: ring torture + agent under concurrent
+    requests, link flaps, stats updates, notification drains and PERST resets (host-only
+    sanitizer build of csrc/agent/stress_main.cpp)."""
+    import subprocess
+
+    from dpu_operator_amd.native.build import build_sanitized
+
+    try:
+        exe = build_sanitized(kind)
+    except RuntimeError as e:  # toolchain without the sanitizer runtime
+        pytest.skip(str(e)[:200])
+    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1", ASAN_OPTIONS="detect_leaks=1:abort_on_error=1:verify_asan_link_order=0",
+               UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
+    r = subprocess.run([str(exe), "1.5"], capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.strip().endswith("ok")

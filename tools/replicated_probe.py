@@ -56,7 +56,7 @@ def probe(world: int, batch: int, flows: int, iters: int = 20) -> dict:
     torch.cuda.synchronize()
     te = (time.perf_counter() - t0) * 1e3 / iters
     fused_ms = tf / iters
-    meta = eng.out_meta()
+    meta = eng.out_meta_t.cpu().numpy().view(np.uint32)[:batch]
     remote = float(np.mean(((meta >> 24) & 0x7F) == 10))
     return {"world": world, "batch": batch, "fused_remote_ms": round(fused_ms, 4), "egress_ms": round(te, 4),
             "gpps_fused": round(batch / fused_ms / 1e6, 3), "remote_fraction": round(remote, 4),
