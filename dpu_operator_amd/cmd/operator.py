@@ -19,6 +19,7 @@ import threading
 from .. import vars as V
 from ..api.v1 import crd_manifests
 from ..controller.operator import setup_operator
+from ..api.scheme import SCHEME
 from ..k8s.apiserver import AlreadyExists, ApiServer
 from ..k8s.leader import LeaderElector
 from ..utils.metrics import MetricsServer, ProbeServer
@@ -44,7 +45,7 @@ def build_parser() -> argparse.ArgumentParser:
 class Operator:
     def __init__(self, args, api: ApiServer | None = None, image_manager=None):
         self.args = args
-        self.api = api or ApiServer()
+        self.api = api or ApiServer(scheme=SCHEME)
         for crd in crd_manifests():
             try:
                 self.api.create(crd)

@@ -96,7 +96,10 @@ Admission = Callable[[str, dict, dict | None], object]
 
 
 class ApiServer:
-    def __init__(self, scheduler: bool = True):
+    def __init__(self, scheduler: bool = True, scheme=None):
+        """`scheme` (api/scheme.py): when given, objects of unregistered kinds / apiVersions
+        and schema violations are rejected with BadRequest, as a real API server does."""
+        self.scheme = scheme
         self._lock = threading.RLock()
         self._objs: dict[tuple[str, str, str], dict] = {}
         self._rv = itertools.count(1)
@@ -146,11 +149,20 @@ class ApiServer:
                 raise Forbidden(f'admission webhook denied the request: {e}') from e
         return obj
 
+    def _check_scheme(self, obj: dict) -> None:
+        if self.scheme is None:
+            return
+        try:
+            self.scheme.check(obj)
+        except ValueError as e:
+            raise BadRequest(str(e)) from e
+
     # ------------------------------------------------------------------ CRUD
     def create(self, obj: dict) -> dict:
         obj = copy.deepcopy(obj)
         if "kind" not in obj or not (obj.get("metadata") or {}).get("name"):
             raise BadRequest("object needs kind and metadata.name")
+        self._check_scheme(obj)
         md = obj.setdefault("metadata", {})
         if obj["kind"] not in CLUSTER_SCOPED:
             md.setdefault("namespace", "default")
@@ -196,6 +208,7 @@ class ApiServer:
 
     def update(self, obj: dict, subresource: str | None = None) -> dict:
         obj = copy.deepcopy(obj)
+        self._check_scheme(obj)
         k = key_of(obj)
         with self._lock:
             cur = self._objs.get(k)
