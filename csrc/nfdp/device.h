@@ -88,10 +88,26 @@ __device__ __forceinline__ void classify_wave(const FlowKey& key, uint4* kx, con
     for (uint32_t nt = 0; nt < acl_tiles; ++nt) {
       const v4i a0 = lw[(nt * 2 + 0) * 64 + lane], a1 = lw[(nt * 2 + 1) * 64 + lane];
       const v4i c = lc[nt * 4 + g];
-      const uint32_t rb = nt * 16u + 4u * g;
+      // Pass 1: does ANY packet of the wave match ANY rule of this tile?  (mismatch counts are
+      // >= 0, so a zero minimum = a match.)  Most tiles of a deny-list ACL match nothing, and
+      // then the priority epilogue below — 10 VALU per 16 packets — is skipped wave-uniformly.
+      uint32_t z = 0xFFFFFFFFu;
 #pragma unroll
       for (int tt = 0; tt < 4; ++tt) {
         v4i acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a0, bf[tt][0], c, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a1, bf[tt][1], acc, 0, 0, 0);
+        z = min(z, min(min((uint32_t)acc[0], (uint32_t)acc[1]), min((uint32_t)acc[2], (uint32_t)acc[3])));
+      }
+      if (!__any(z == 0u)) continue;
+      // Pass 2 (rare): recompute the tile with the (mismatch << 10 | rule) first-match epilogue.
+      // The bias goes through an opaque copy so the MFMAs are not CSE'd with pass 1 (keeping
+      // pass-1 accumulators alive would cost 16 VGPRs at the kernel's register peak).
+      v4i c2 = c;
+      asm volatile("" : "+v"(c2));
+      const uint32_t rb = nt * 16u + 4u * g;
+#pragma unroll
+      for (int tt = 0; tt < 4; ++tt) {
+        v4i acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a0, bf[tt][0], c2, 0, 0, 0);
         acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a1, bf[tt][1], acc, 0, 0, 0);
         const uint32_t e0 = ((uint32_t)acc[0] << 10) | (rb + 0);
         const uint32_t e1 = ((uint32_t)acc[1] << 10) | (rb + 1);

@@ -35,7 +35,7 @@ struct FusedArgs {
   const v4i* toep_frag;           // [2][2][64] A fragments of the Toeplitz matrix
   const uint32_t* toep_tab;       // [16][256] byte tables (LDS hash variant)
   uint32_t acl_tiles;             // ceil(n_acl / 16)
-  uint32_t flags;                 // ablation: bit0 no port/drop counters, bit1 no latency samples
+  uint32_t flags;                 // bit0 no port/drop counters, bit1 no latency samples, bit2 no flow counts
   // REMOTE variant (replicated tables, N GPUs): frames whose egress port lives on another GPU
   // go to segment[egress gpu] of send_pkt (64-B slot + 4-B meta, fill count in pcnt) instead of
   // out[i]; out_meta[i] then says kRemote.
@@ -47,8 +47,11 @@ struct FusedArgs {
 __device__ __forceinline__ size_t lds_align16(size_t x) { return (x + 15) & ~(size_t)15; }
 
 struct LdsLayout {
-  size_t acl_w, acl_c, toep_f, toep_t, kx, pc, drops, total;
+  size_t acl_w, acl_c, toep_f, toep_t, kx, pc, drops, tports, tchain, tperm, total;
+  bool tabs;  // small tables (ports < kLdsPorts, chain words, ACL verdicts) staged in LDS
 };
+constexpr uint32_t kLdsChains = 256;
+constexpr size_t kLdsTabBytes = kLdsPorts * sizeof(PortEntry) + kLdsChains * 8 + 1024;
 __host__ __device__ inline LdsLayout lds_layout(int hash_mode, int acl_mode, uint32_t acl_tiles) {
   LdsLayout L;
   size_t o = 0;
@@ -59,8 +62,56 @@ __host__ __device__ inline LdsLayout lds_layout(int hash_mode, int acl_mode, uin
   L.kx = o; o += kWaves * 64 * 16;
   L.pc = o; o += kLdsPorts * 4 * 4;
   L.drops = o; o += kNumReasons * 4;
+  o = (o + 15) & ~(size_t)15;
+  // The staged tables must not cost a resident block: within 80 KiB (two blocks per CU, the
+  // VGPR-bound maximum) or, for layouts already at one block per CU, within the 160 KiB.
+  const size_t with = o + kLdsTabBytes;
+  L.tabs = (o <= 80 * 1024) ? (with <= 80 * 1024) : (with <= 160 * 1024 - 1024);
+  L.tports = o; L.tchain = o + kLdsPorts * sizeof(PortEntry); L.tperm = L.tchain + kLdsChains * 8;
+  if (L.tabs) o = with;
   L.total = (o + 15) & ~(size_t)15;
   return L;
+}
+
+// Table-access policy of the fused kernel (pipeline.h DirectTables contract): LDS copies for
+// ports < kLdsPorts, the first kLdsChains chain words and every ACL verdict; global memory for
+// the rest (or for everything when the layout has no room: L.tabs false -> nport = nchain = 0).
+struct LdsTables {
+  const TablesView& t;
+  const PortEntry* lport;
+  const uint64_t* lchain;
+  const uint8_t* lperm;
+  uint32_t nport, nchain;
+  bool lds_perm;
+  __device__ __forceinline__ PortEntry port(uint32_t i) const { return i < nport ? lport[i] : t.ports[i]; }
+  __device__ __forceinline__ uint64_t chain_word(uint32_t c) const {
+    if (c < nchain) return lchain[c];
+    return c < t.n_chains ? *reinterpret_cast<const uint64_t*>(&t.chains[c]) : 0ull;
+  }
+  __device__ __forceinline__ bool permit(int r) const {
+    if (r < 0) return t.acl_default_permit != 0;
+    return (lds_perm ? lperm[r] : t.acl_permit[r]) != 0;
+  }
+};
+
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+constexpr int kBufCfg = 0x00020000;  // buffer resource word 3 (gfx9 family raw buffer)
+constexpr int kStreamAux = 2;        // nt: frames are read once / written once (streaming)
+
+__device__ __forceinline__ void load_slot(const uint4* pk4, const uint32_t* inmeta, uint32_t i, uint32_t n,
+                                          uint32_t* d, uint32_t& im) {
+  if (i < n) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint4 v = pk4[(size_t)i * 4 + q];
+      d[4 * q] = v.x; d[4 * q + 1] = v.y; d[4 * q + 2] = v.z; d[4 * q + 3] = v.w;
+    }
+    im = inmeta[i];
+  } else {
+#pragma unroll
+    for (int q = 0; q < kSlotDwords; ++q) d[q] = 0;
+    im = 0;
+  }
 }
 
 template <int HASH, int ACL, bool REMOTE>
@@ -88,54 +139,84 @@ __global__ __launch_bounds__(kBlock, 4) void fused_kernel(FusedArgs a) {
     for (uint32_t i = threadIdx.x; i < 4096; i += kBlock) ltab[i] = a.toep_tab[i];
   for (uint32_t i = threadIdx.x; i < kLdsPorts * 4; i += kBlock) pc[i] = 0;
   if (threadIdx.x < kNumReasons) drops[threadIdx.x] = 0;
+  PortEntry* lport = reinterpret_cast<PortEntry*>(smem + L.tports);
+  uint64_t* lchain = reinterpret_cast<uint64_t*>(smem + L.tchain);
+  uint8_t* lperm = smem + L.tperm;
+  const uint32_t nchain = L.tabs ? min(a.t.n_chains, kLdsChains) : 0u;
+  const bool lds_perm = L.tabs && a.t.n_acl <= 1024;
+  if (L.tabs) {
+    const uint4* gp = reinterpret_cast<const uint4*>(a.t.ports);
+    uint4* lp = reinterpret_cast<uint4*>(lport);
+    for (uint32_t i = threadIdx.x; i < kLdsPorts * 2; i += kBlock) lp[i] = gp[i];
+    for (uint32_t i = threadIdx.x; i < nchain; i += kBlock) lchain[i] = *reinterpret_cast<const uint64_t*>(&a.t.chains[i]);
+    if (lds_perm)
+      for (uint32_t i = threadIdx.x; i < a.t.n_acl; i += kBlock) lperm[i] = a.t.acl_permit[i];
+  }
+  const LdsTables ta{a.t, lport, lchain, lperm, L.tabs ? (uint32_t)kLdsPorts : 0u, nchain, lds_perm};
   __syncthreads();
 
   const unsigned long long t0 = a.t0 ? *a.t0 : 0ull;
   const uint4* pk4 = a.pkts;
-  for (uint32_t base = blockIdx.x * kBlock; base < a.n; base += gridDim.x * kBlock) {
+  const uint32_t stride = gridDim.x * kBlock;
+  // Software pipeline over the grid-stride loop.  s_waitcnt vmcnt retires loads, stores and
+  // atomics together in issue order, so the next slot's frame is loaded BEFORE this slot's
+  // flow-counter atomic and output stores: waiting for the frame never waits for them, and the
+  // atomic (a memory-side RMW, the longest trip of the iteration) completes under the next
+  // slot's parse + classification.
+  uint32_t dn[kSlotDwords];
+  uint32_t imn;
+  load_slot(pk4, a.inmeta, blockIdx.x * kBlock + threadIdx.x, a.n, dn, imn);
+  // raw buffer views (num_records = valid bytes; offsets past it read 0 / drop the store)
+  const __amdgpu_buffer_rsrc_t r_pk = __builtin_amdgcn_make_buffer_rsrc((void*)a.pkts, (short)0, (int)(a.n * 64u), kBufCfg);
+  const __amdgpu_buffer_rsrc_t r_im = __builtin_amdgcn_make_buffer_rsrc((void*)a.inmeta, (short)0, (int)(a.n * 4u), kBufCfg);
+  const __amdgpu_buffer_rsrc_t r_out = __builtin_amdgcn_make_buffer_rsrc((void*)a.out, (short)0, (int)(a.n * 64u), kBufCfg);
+  const __amdgpu_buffer_rsrc_t r_meta = __builtin_amdgcn_make_buffer_rsrc((void*)a.out_meta, (short)0, (int)(a.n * 4u), kBufCfg);
+  const __amdgpu_buffer_rsrc_t r_lat = __builtin_amdgcn_make_buffer_rsrc((void*)a.lat, (short)0,
+                                                                          a.lat ? (int)(((a.n + 15u) >> 4) * 4u) : 0, kBufCfg);
+  const uint32_t ctr_mask = min(a.t.bucket_mask * kBucketSlots + (kBucketSlots - 1), 4095u);
+  for (uint32_t base = blockIdx.x * kBlock; base < a.n; base += stride) {
     const uint32_t i = base + threadIdx.x;
     const bool valid = i < a.n;
-    uint32_t d[kSlotDwords];
-    uint32_t im = 0;
-    if (valid) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const uint4 v = pk4[(size_t)i * 4 + q];
-        d[4 * q] = v.x; d[4 * q + 1] = v.y; d[4 * q + 2] = v.z; d[4 * q + 3] = v.w;
-      }
-      im = a.inmeta[i];
-    } else {
-#pragma unroll
-      for (int q = 0; q < kSlotDwords; ++q) d[q] = 0;
-    }
     Parsed p;
     IngressState st;
-    ingress_stage(a.t, d, im, p, st);
+    ingress_stage(a.t, ta, dn, imn, p, st);  // copies the frame into p.s: dn is free for the prefetch
+
     if (!valid) st.reason = kMalformed;
 
     uint32_t hash = 0;
     int acl_rule = -1;
     classify_wave<HASH, ACL>(st.key, kx, lw, lc, a.acl_tiles, lt, ltab, a.t, hash, acl_rule);
+    if constexpr (!REMOTE) {
+      // prefetch the next slot now: it lands under this slot's probe and chain
+      const uint32_t nx = i + stride;
+      const uint32_t fo = nx < a.n ? nx * 64u : 0x80000000u;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const v4u v = __builtin_amdgcn_raw_buffer_load_b128(r_pk, fo + 16u * q, 0, kStreamAux);
+        dn[4 * q] = v.x; dn[4 * q + 1] = v.y; dn[4 * q + 2] = v.z; dn[4 * q + 3] = v.w;
+      }
+      imn = __builtin_amdgcn_raw_buffer_load_b32(r_im, nx < a.n ? nx * 4u : 0x80000000u, 0, kStreamAux);
+    }
 
     bool hit = false;
     FlowAction act = {};
+    int64_t slot = -1;
     if (!st.reason && p.ipv4) {
       uint4 v;
-      const int64_t slot = flow_probe(a.t, st.key, hash, v);
+      slot = flow_probe(a.t, st.key, hash, v);
       if (slot >= 0) {
         hit = true;
         act.chain_id = v.x & 0xFFFFu; act.out_port = v.x >> 16; act.nat_ip = v.y;
         act.nat_port = v.z & 0xFFFFu; act.vlan = v.z >> 16; act.flow_id = v.w;
-        if (a.flow_ctr) atomicAdd(a.flow_ctr + slot, ctr_inc(st.wire_len));
       }
     }
-    const EgressDecision e = chain_stage(a.t, p, st, hit, act, acl_rule, hash);
+    const EgressDecision e = chain_stage(a.t, ta, p, st, hit, act, acl_rule, hash);
     bool to_peer = false;
     uint32_t reason = e.reason;
     uint4* dst = a.out + (size_t)i * 4;
     if constexpr (REMOTE) {
       // egress GPU of the frame; block-aggregated slot in that GPU's segment (all threads call)
-      const uint32_t eg = e.reason ? a.rank : (uint32_t)a.t.ports[e.out_port].gpu;
+      const uint32_t eg = e.reason ? a.rank : (uint32_t)ta.port(e.out_port).gpu;
       const bool remote = valid && !e.reason && eg != a.rank && eg < a.nranks;
       const uint32_t pos = reserve_block(a.pcnt, eg, remote, a.nranks, rcnt, rbase);
       if (remote) {
@@ -150,23 +231,18 @@ __global__ __launch_bounds__(kBlock, 4) void fused_kernel(FusedArgs a) {
         }
       }
     }
-    if (valid) {
-      uint32_t o[kSlotDwords];
-      emit(p, e.tci, e.push != 0, o);
-      const uint32_t olen = reason ? 0u : p.len + (e.push ? 4u : 0u);
-#pragma unroll
-      for (int q = 0; q < 4; ++q) dst[q] = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
-      a.out_meta[i] = to_peer ? make_meta(e.out_port, olen, kRemote, e.mirror != 0)
-                              : make_meta(reason == kOverflow ? kPortNone : e.out_port, olen, reason, reason != kOverflow && e.mirror != 0);
-      // counters
-      if (a.flags & 1u) {
-      } else if (st.in_port < kLdsPorts) {
+    const uint32_t olen = reason ? 0u : p.len + (e.push ? 4u : 0u);
+    const uint32_t meta = to_peer ? make_meta(e.out_port, olen, kRemote, e.mirror != 0)
+                                  : make_meta(reason == kOverflow ? kPortNone : e.out_port, olen, reason,
+                                              reason != kOverflow && e.mirror != 0);
+    // port / drop counters: LDS, global only for ports >= kLdsPorts (issued before the tail)
+    if (valid && !(a.flags & 1u)) {
+      if (st.in_port < kLdsPorts) {
         atomicAdd(&pc[st.in_port], 1u); atomicAdd(&pc[kLdsPorts + st.in_port], st.wire_len);
       } else if (st.in_port < (uint32_t)kMaxPorts) {
         atomicAdd(a.port_ctr + 2 * st.in_port, ctr_inc(st.wire_len));
       }
-      if (a.flags & 1u) {
-      } else if (reason) {
+      if (reason) {
         atomicAdd(&drops[reason & (kNumReasons - 1)], 1u);
       } else if (to_peer) {
         // tx is counted where the frame leaves: the egress GPU's egress_kernel
@@ -175,9 +251,34 @@ __global__ __launch_bounds__(kBlock, 4) void fused_kernel(FusedArgs a) {
       } else {
         atomicAdd(a.port_ctr + 2 * e.out_port + 1, ctr_inc(olen));
       }
-      if (a.lat && !(a.flags & 2u) && (i & 15u) == 0 && !to_peer) {
-        const unsigned long long now = __builtin_amdgcn_s_memrealtime();
-        a.lat[i >> 4] = (uint32_t)(now - t0);
+    }
+    uint32_t o[kSlotDwords];
+    emit(p, e.tci, e.push != 0, o);
+    const bool sample = a.lat && !(a.flags & 2u) && (i & 15u) == 0 && !to_peer;
+    const uint32_t lat_now = sample ? (uint32_t)(__builtin_amdgcn_s_memrealtime() - t0) : 0u;
+    if constexpr (!REMOTE) {
+      // Fixed-count tail: every lane issues the same vector-memory instructions with no branch
+      // around them (out-of-range buffer offsets are dropped by the hardware; a miss adds 0),
+      // so the compiler can wait for the prefetched frame with vmcnt(N > 0) at the loop head
+      // instead of draining this slot's atomic and stores.
+      const uint32_t cslot = hit ? (uint32_t)slot : (i & ctr_mask);
+      atomicAdd(a.flow_ctr + cslot, (hit && !(a.flags & 4u)) ? ctr_inc(st.wire_len) : 0ull);
+      const uint32_t so = valid ? i * 64u : 0x80000000u;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        v4u v = {o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]};
+        __builtin_amdgcn_raw_buffer_store_b128(v, r_out, so + 16u * q, 0, kStreamAux);
+      }
+      __builtin_amdgcn_raw_buffer_store_b32(meta, r_meta, valid ? i * 4u : 0x80000000u, 0, kStreamAux);
+      __builtin_amdgcn_raw_buffer_store_b32(lat_now, r_lat, sample ? (i >> 4) * 4u : 0x80000000u, 0, 0);
+    } else {
+      load_slot(pk4, a.inmeta, i + stride, a.n, dn, imn);
+      if (hit && a.flow_ctr && !(a.flags & 4u)) atomicAdd(a.flow_ctr + slot, ctr_inc(st.wire_len));
+      if (valid) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) dst[q] = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
+        a.out_meta[i] = meta;
+        if (sample) a.lat[i >> 4] = lat_now;
       }
     }
   }
@@ -229,6 +330,8 @@ static hipError_t launch_fused_t(const FusedArgs& a, int num_cus, hipStream_t s)
   if (lds > kMaxDyn) return hipErrorInvalidValue;
   if (R && (a.nranks == 0 || a.nranks > kMaxRanks || a.rank >= a.nranks || !a.send_pkt || !a.pcnt))
     return hipErrorInvalidValue;
+  // the 1-GPU variant's fixed-count tail: buffer views need n * 64 B < 2 GiB and a counter table
+  if (!R && (a.n >= (1u << 25) || !a.flow_ctr || !a.out_meta)) return hipErrorInvalidValue;
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&fused_kernel<H, A, R>),

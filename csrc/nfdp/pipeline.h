@@ -21,7 +21,21 @@ struct IngressState {
   FlowKey key;
 };
 
-NFDP_HD void ingress_stage(const TablesView& t, const uint32_t* d, uint32_t inmeta, Parsed& p,
+// Table-access policy of the stages.  The oracle and the sharded kernels read the small tables
+// straight from memory (DirectTables); the fused kernel passes a policy that serves them from
+// LDS copies staged once per workgroup, so the per-packet path has no dependent global loads
+// besides the frame and the flow bucket.
+struct DirectTables {
+  const TablesView& t;
+  NFDP_HD PortEntry port(uint32_t i) const { return t.ports[i]; }
+  NFDP_HD uint64_t chain_word(uint32_t c) const {  // nhops + 7 hop opcodes (first 8 B of the entry)
+    return c < t.n_chains ? *reinterpret_cast<const uint64_t*>(&t.chains[c]) : 0ull;
+  }
+  NFDP_HD bool permit(int rule) const { return rule >= 0 ? t.acl_permit[rule] != 0 : t.acl_default_permit != 0; }
+};
+
+template <class TA>
+NFDP_HD void ingress_stage(const TablesView& t, const TA& ta, const uint32_t* d, uint32_t inmeta, Parsed& p,
                            IngressState& st) {
   st.in_port = inmeta & 0xFFFFu;
   uint32_t len = (inmeta >> 16) & 0xFFu;
@@ -35,7 +49,7 @@ NFDP_HD void ingress_stage(const TablesView& t, const uint32_t* d, uint32_t inme
   if (st.in_port >= (uint32_t)kMaxPorts) {
     st.reason = kBadPort;
   } else {
-    const PortEntry pe = t.ports[st.in_port];
+    const PortEntry pe = ta.port(st.in_port);
     st.in_flags = pe.flags;
     st.in_ext = pe.ext;
     if (!(pe.flags & kPortValid)) st.reason = st.reason ? st.reason : kBadPort;
@@ -49,6 +63,9 @@ NFDP_HD void ingress_stage(const TablesView& t, const uint32_t* d, uint32_t inme
   }
   st.key = make_key(p, st.bridge);
 }
+NFDP_HD void ingress_stage(const TablesView& t, const uint32_t* d, uint32_t inmeta, Parsed& p, IngressState& st) {
+  ingress_stage(t, DirectTables{t}, d, inmeta, p, st);
+}
 
 struct EgressDecision {
   uint32_t out_port;
@@ -60,8 +77,9 @@ struct EgressDecision {
 
 // `hit`: flow entry found; `act`: its action; `acl_rule`: first matching ACL rule or -1;
 // `hash`: the packet's Toeplitz hash (LAG member selection uses hash[2:0], K8).
-NFDP_HD EgressDecision chain_stage(const TablesView& t, Parsed& p, const IngressState& st,
-                                   bool hit, const FlowAction& act, int acl_rule, uint32_t hash = 0) {
+template <class TA>
+NFDP_HD EgressDecision chain_stage(const TablesView& t, const TA& ta, Parsed& p, const IngressState& st,
+                                   bool hit, const FlowAction& act, int acl_rule, uint32_t hash) {
   EgressDecision e;
   e.out_port = kPortNone; e.reason = st.reason; e.push = 0; e.tci = 0; e.mirror = 0;
   if (e.reason) return e;
@@ -78,7 +96,7 @@ NFDP_HD EgressDecision chain_stage(const TablesView& t, Parsed& p, const Ingress
     if (op >= 0) {
       e.out_port = (uint32_t)op;
     } else {
-      const PortEntry& ip = t.ports[st.in_port < (uint32_t)kMaxPorts ? st.in_port : 0];
+      const PortEntry ip = ta.port(st.in_port < (uint32_t)kMaxPorts ? st.in_port : 0);
       if (!(ip.flags & kPortHasDefault)) { e.out_port = kPortPunt; e.reason = kNoRoute; return e; }
       e.out_port = ip.default_out;
     }
@@ -88,22 +106,20 @@ NFDP_HD EgressDecision chain_stage(const TablesView& t, Parsed& p, const Ingress
     e.out_port = act.out_port;
     // nhops + 7 hop opcodes = the chain entry's first 8 bytes, read as one word and decoded with
     // compile-time shifts (indexing a private hop[] array at run time would spill to scratch).
-    uint64_t hw = 0;
-    if (act.chain_id < t.n_chains) hw = *reinterpret_cast<const uint64_t*>(&t.chains[act.chain_id]);
+    const uint64_t hw = ta.chain_word(act.chain_id);
     const uint32_t nh = (uint32_t)(hw & 0xFFu);
 #pragma unroll
     for (int i = 0; i < kMaxHops; ++i) {
       if ((uint32_t)i >= nh) break;
       const uint8_t op = (uint8_t)((hw >> (8 * (i + 1))) & 0xFFu);
       if (op == kHopAcl) {
-        const bool permit = acl_rule >= 0 ? t.acl_permit[acl_rule] != 0 : t.acl_default_permit != 0;
-        if (!permit) { e.reason = kAclDeny; e.out_port = kPortNone; return e; }
+        if (!ta.permit(acl_rule)) { e.reason = kAclDeny; e.out_port = kPortNone; return e; }
       } else if (op == kHopNat) {
         if (p.ipv4) act_snat(p, act.nat_ip, act.nat_port);
       } else if (op == kHopL2Fwd) {
         e.out_port = act.out_port;
         if (e.out_port < (uint32_t)kMaxPorts) {
-          const PortEntry& pe = t.ports[e.out_port];
+          const PortEntry pe = ta.port(e.out_port);
           set_dmac(p.s, pe.peer_mac_lo, pe.peer_mac_hi);
           set_smac(p.s, pe.mac_lo, pe.mac_hi);
         }
@@ -125,14 +141,15 @@ NFDP_HD EgressDecision chain_stage(const TablesView& t, Parsed& p, const Ingress
     }
   }
   if (e.out_port >= (uint32_t)kMaxPorts) { e.reason = kBadPort; e.out_port = kPortNone; return e; }
-  if (t.ports[e.out_port].flags & kPortLag) {
+  PortEntry pe = ta.port(e.out_port);
+  if (pe.flags & kPortLag) {
     // LAG (K8): member = group[hash[2:0]] (tx_lag_table lag_group_id, hash/7)
-    const uint32_t g = t.ports[e.out_port].lag;
+    const uint32_t g = pe.lag;
     const uint32_t m = (t.lag_members && g < t.n_lag_groups) ? t.lag_members[g * kLagWays + (hash & 7u)] : kPortNone;
     if (m >= (uint32_t)kMaxPorts) { e.reason = kBadPort; e.out_port = kPortNone; return e; }
     e.out_port = m;
+    pe = ta.port(m);
   }
-  const PortEntry& pe = t.ports[e.out_port];
   if (!(pe.flags & kPortValid)) { e.reason = kBadPort; e.out_port = kPortNone; return e; }
   if (!vlan_done && (pe.flags & kPortTagEgress) && pe.vlan) { e.push = 1; e.tci = pe.vlan & 0xFFFu; }
   if (p.len + (e.push ? 4u : 0u) > (uint32_t)kSlotBytes) {
@@ -140,6 +157,10 @@ NFDP_HD EgressDecision chain_stage(const TablesView& t, Parsed& p, const Ingress
   }
   e.mirror = (st.in_flags & kPortMirror) ? 1u : 0u;  // mirror_and_send (K9)
   return e;
+}
+NFDP_HD EgressDecision chain_stage(const TablesView& t, Parsed& p, const IngressState& st, bool hit,
+                                   const FlowAction& act, int acl_rule, uint32_t hash = 0) {
+  return chain_stage(t, DirectTables{t}, p, st, hit, act, acl_rule, hash);
 }
 
 // Counter record helpers: packed (pkts << 40) | bytes in one 64-bit word so a packet costs a

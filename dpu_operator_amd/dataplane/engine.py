@@ -73,6 +73,7 @@ class DataPlane:
         self._versions: dict[str, int] = {}
         self._acl_tiles = 1
         self.count_flows = True  # per-flow packed counters (one 64-bit atomic per packet)
+        self.MAX_LAUNCH = 1 << 24
         self.flow_totals = np.zeros((self.flows.nbuckets * 4, 2), np.uint64)
         if self.gpu:
             torch = _torch()
@@ -236,15 +237,21 @@ class DataPlane:
             s = stream if stream is not None else torch.cuda.current_stream(self.tdev).cuda_stream
             if stamp:
                 self.nf.launch_stamp(self._ptr("t0"), s)
-            self.nf.launch_fused(
-                tp, pkts.data_ptr(), inmeta.data_ptr(), out.data_ptr(), meta.data_ptr(), n,
-                self._ptr("flow_ctr") if self.count_flows else 0, self._ptr("port_ctr"), self._ptr("drop_ctr"),
-                self._ptr("t0"),
-                lat.data_ptr() if lat is not None else 0,
-                self._ptr("acl_wfrag"), self._ptr("acl_cinit"), self._acl_tiles,
-                self._ptr("toep_frag"), self._ptr("toep_tab"),
-                self.hash_mode, self.acl_mode, self.num_cus, s, flags,
-            )
+            if not self.count_flows:
+                flags |= 4  # the kernel always gets the counter table; bit 2 makes it add 0
+            # one launch covers < 2^25 slots (32-bit buffer views); bigger batches are split
+            for lo in range(0, n, self.MAX_LAUNCH):
+                m = min(self.MAX_LAUNCH, n - lo)
+                self.nf.launch_fused(
+                    tp, pkts.data_ptr() + 64 * lo, inmeta.data_ptr() + 4 * lo, out.data_ptr() + 64 * lo,
+                    meta.data_ptr() + 4 * lo, m,
+                    self._ptr("flow_ctr"), self._ptr("port_ctr"), self._ptr("drop_ctr"),
+                    self._ptr("t0"),
+                    lat.data_ptr() + 4 * (lo // 16) if lat is not None else 0,
+                    self._ptr("acl_wfrag"), self._ptr("acl_cinit"), self._acl_tiles,
+                    self._ptr("toep_frag"), self._ptr("toep_tab"),
+                    self.hash_mode, self.acl_mode, self.num_cus, s, flags,
+                )
             return BatchResult(out, meta, n, {"lat": lat})
         pk = np.ascontiguousarray(pkts, np.uint8)
         im = np.ascontiguousarray(inmeta, np.uint32)

@@ -32,10 +32,9 @@ def main():
         if base is None:
             base = (g, sc)
     g0, sc = base
-    variants["noFlowCtr"] = (g0, 0, False)
     variants["noPortCtr"] = (g0, 1, True)
-    variants["noCounters"] = (g0, 1, False)
     variants["noCounters+noLat"] = (g0, 3, False)
+
     pk, im = S.traffic(sc, a.batch, seed=5)
     tp = torch.from_numpy(pk).to(dev)
     ti = torch.from_numpy(im.view(np.int32)).to(dev)
