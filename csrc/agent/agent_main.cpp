@@ -15,14 +15,24 @@
 
 #include "agent.h"
 #include "plugin_server.h"
+#include "soc.h"
 
 static volatile std::sig_atomic_t g_stop = 0;
 static void on_signal(int) { g_stop = 1; }
 
 int main(int argc, char** argv) {
   if (argc < 2 || !std::strcmp(argv[1], "-h") || !std::strcmp(argv[1], "--help")) {
-    std::fprintf(stderr, "usage: %s <file.cfg> [--mbox PATH] [--size BYTES] [--max-msgs N] [--plugin-port P]\n", argv[0]);
+    std::fprintf(stderr, "usage: %s <file.cfg> [--mbox PATH] [--size BYTES] [--max-msgs N] [--plugin-port P]\n"
+                         "       %s --list-gpus [SYS_ROOT]\n", argv[0], argv[0]);
     return 2;
+  }
+  if (!std::strcmp(argv[1], "--list-gpus")) {  // soc detection (the reference's soc.c role)
+    const char* root = argc > 2 ? argv[2] : "/";
+    for (const agent::GpuInfo& g : agent::detect_gpus(root))
+      std::printf("{\"node\": %d, \"model\": \"%s\", \"gfx\": \"%s\", \"cus\": %u, \"xcc\": %u, \"vram_gib\": %.0f, "
+                  "\"numa\": %d, \"pci\": \"%s\"}\n", g.node, g.model_name.c_str(), g.gfx_arch.c_str(), g.cu_count,
+                  g.num_xcc, g.vram_bytes / 1073741824.0, g.numa_node, g.pci.c_str());
+    return 0;
   }
   std::string cfg_path = argv[1], mbox = "/var/run/dpu-daemon/ctrl-mbox";
   uint32_t size = 32768;

@@ -7,6 +7,7 @@
 #include "agent.h"
 #include "config.h"
 #include "plugin_server.h"
+#include "soc.h"
 
 namespace py = pybind11;
 using namespace agent;
@@ -115,6 +116,23 @@ MsgHdr mkhdr(uint32_t pem, uint32_t pf, int32_t vf, uint32_t flags, uint16_t msg
 }  // namespace
 
 PYBIND11_MODULE(_agent, m) {
+  m.def("detect_gpus", [](const std::string& root) {
+    py::list out;
+    for (const GpuInfo& g : detect_gpus(root)) {
+      py::dict d;
+      d["node"] = g.node; d["gfx_target_version"] = g.gfx_target_version; d["gfx_arch"] = g.gfx_arch;
+      d["vendor_id"] = g.vendor_id; d["device_id"] = g.device_id; d["model"] = g.model_name;
+      d["model_bit"] = g.model; d["simd_count"] = g.simd_count; d["cu_count"] = g.cu_count;
+      d["num_xcc"] = g.num_xcc; d["simd_per_cu"] = g.simd_per_cu; d["wave_front_size"] = g.wave_front_size;
+      d["lds_size_kb"] = g.lds_size_kb; d["vram_bytes"] = g.vram_bytes; d["numa_node"] = g.numa_node;
+      d["pci"] = g.pci;
+      out.append(d);
+    }
+    return out;
+  }, py::arg("sys_root") = "/", "AMD Instinct GPUs from the KFD topology (soc.h)");
+  m.attr("GPU_CDNA3") = (uint32_t)kGpuCdna3;
+  m.attr("GPU_CDNA4") = (uint32_t)kGpuCdna4;
+
   m.doc() = "MI355X node control agent: shared-memory control mailbox, ctrl-net handler, plugin relay";
   m.attr("CP_VERSION_MIN") = kCpVersionMin;
   m.attr("CP_VERSION_MAX") = kCpVersionMax;

@@ -34,10 +34,14 @@ DEFAULT_VF_COUNT = 8
 
 
 class DeviceHandler:
-    def __init__(self, vsp, dpu_mode: bool, vf_count: int = DEFAULT_VF_COUNT):
+    def __init__(self, vsp, dpu_mode: bool, vf_count: int = DEFAULT_VF_COUNT, numa_of=None):
+        """`numa_of(device_id) -> int` (optional): NUMA node advertised to kubelet's topology
+        manager (-1 = unknown); e.g. devutils.get_numa_node for PCI ids, or the data-plane GPU's
+        node for GPU vports."""
         self.vsp = vsp
         self.dpu_mode = dpu_mode
         self.vf_count = vf_count
+        self.numa_of = numa_of
         self._setup = threading.Event()
 
     def setup_devices(self) -> None:
@@ -73,6 +77,12 @@ class DevicePluginServer:
         self._stop = threading.Event()
         self.registered = False
 
+    def _device(self, dev_id: str, health: str):
+        numa = self.handler.numa_of(dev_id) if self.handler.numa_of else -1
+        if numa is not None and numa >= 0:
+            return dp.Device(ID=dev_id, health=health, topology=dp.TopologyInfo(nodes=[dp.NUMANode(ID=numa)]))
+        return dp.Device(ID=dev_id, health=health)
+
     # ------------------------------------------------------------------ gRPC service
     def GetDevicePluginOptions(self, request, context):
         return dp.DevicePluginOptions(pre_start_required=False, get_preferred_allocation_available=False)
@@ -89,7 +99,7 @@ class DevicePluginServer:
                 return
             if new != old:
                 self.devices = dict(new)
-                yield dp.ListAndWatchResponse(devices=[dp.Device(ID=i, health=h) for i, h in sorted(new.values())])
+                yield dp.ListAndWatchResponse(devices=[self._device(i, h) for i, h in sorted(new.values())])
                 old = new
             self._stop.wait(self.poll)
 

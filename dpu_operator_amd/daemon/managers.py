@@ -51,12 +51,12 @@ class _Base:
     kind = "base"
 
     def __init__(self, vsp, api: ApiServer | None, path_manager: PathManager | None, dpu_mode: bool,
-                 dp_poll: float = 5.0, register_device_plugin: bool = True):
+                 dp_poll: float = 5.0, register_device_plugin: bool = True, numa_of=None):
         self.vsp = vsp
         self.api = api
         self.pm = path_manager or PathManager("/")
         self.addr, self.port = "", 0
-        self.dp = DevicePluginServer(DeviceHandler(vsp, dpu_mode), self.pm, poll=dp_poll)
+        self.dp = DevicePluginServer(DeviceHandler(vsp, dpu_mode, numa_of=numa_of), self.pm, poll=dp_poll)
         self.register_dp = register_device_plugin
         self.cni: CniServer | None = None
         self.manager: Manager | None = None
@@ -272,8 +272,17 @@ class ColocatedSideManager:
 
     def __init__(self, vsp, sriov_manager, nl: NetlinkManager, api: ApiServer | None = None,
                  path_manager: PathManager | None = None, ipam: HostLocalIpam | None = None, on_gpu_chain=None, **kw):
+        if "numa_of" not in kw:
+            # GPU vports live on the data-plane GPU: advertise its NUMA node (KFD topology)
+            try:
+                from .devutils import data_plane_numa
+
+                node = data_plane_numa((path_manager or PathManager("/")).root)
+            except Exception:  # noqa: BLE001 - no KFD on this host / native module unavailable
+                node = -1
+            kw["numa_of"] = (lambda _dev, n=node: n) if node >= 0 else None
         self.dpu = DpuSideManager(vsp, nl, api, path_manager, ipam, on_gpu_chain, **kw)
-        self.host = HostSideManager(vsp, sriov_manager, None, path_manager, **kw)
+        self.host = HostSideManager(vsp, sriov_manager, None, path_manager, **{k: v for k, v in kw.items() if k != "numa_of"})
         self.pm = self.dpu.pm
 
     def start_vsp(self) -> None:

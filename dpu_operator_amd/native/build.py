@@ -45,7 +45,7 @@ MODULES = {
     },
     "_agent": {
         "dir": CSRC / "agent",
-        "sources": ["mbox.cpp", "ctrl_net.cpp", "config.cpp", "agent.cpp", "plugin_server.cpp", "bindings.cpp"],
+        "sources": ["mbox.cpp", "ctrl_net.cpp", "config.cpp", "agent.cpp", "plugin_server.cpp", "soc.cpp", "bindings.cpp"],
         "hip": False,
     },
 }
@@ -55,7 +55,7 @@ EXES = {
     "dpu-cp-agent": {
         "dir": CSRC / "agent",
         "module": "_agent",
-        "sources": ["mbox.cpp", "ctrl_net.cpp", "config.cpp", "agent.cpp", "plugin_server.cpp", "agent_main.cpp"],
+        "sources": ["mbox.cpp", "ctrl_net.cpp", "config.cpp", "agent.cpp", "plugin_server.cpp", "soc.cpp", "agent_main.cpp"],
     },
 }
 
@@ -139,7 +139,7 @@ def build_exe(name: str, force: bool = False, verbose: bool = False) -> Path:
     return out
 
 
-AGENT_CORE = ["mbox.cpp", "ctrl_net.cpp", "config.cpp", "agent.cpp", "plugin_server.cpp"]
+AGENT_CORE = ["mbox.cpp", "ctrl_net.cpp", "config.cpp", "agent.cpp", "plugin_server.cpp", "soc.cpp"]
 SANITIZERS = {"tsan": ["-fsanitize=thread"], "asan": ["-fsanitize=address,undefined", "-fno-omit-frame-pointer"]}
 
 
