@@ -54,6 +54,9 @@ def parse():
     ap.add_argument("--chunks", type=int, default=4, help="pipeline chunks per step (N > 1)")
     ap.add_argument("--mode", default="replicated", choices=["replicated", "sharded"],
                     help="multi-GPU strategy for N > 1")
+    ap.add_argument("--io", default="device", choices=["device", "host"],
+                    help="device: batches resident in HBM (DPU wire side); host: pinned host slots, SDMA up/down "
+                         "around every kernel (1 GPU)")
     ap.add_argument("--force-sharded", action="store_true",
                     help="use the sharded multi-GPU pipeline even at N = 1 (measures its compute cost)")
     return ap.parse_args()
@@ -103,7 +106,31 @@ def main() -> None:
         pk, im = S.traffic(sc, a.batch, seed=1000 * rank + r + 1, src_pods=my_pods)
         batches.append((torch.from_numpy(pk).to(dev), torch.from_numpy(im.view(np.int32)).to(dev)))
         del pk, im
-    if not sharded:
+    drain = None
+    if not sharded and a.io == "host":
+        from dpu_operator_amd.dataplane.pktio import HostPath
+
+        hp = HostPath(dp, a.batch, depth=3)
+        for s in range(hp.depth):  # the NIC side fills the pinned slots; synthetic frames here
+            pk, im = batches[s % a.rotate]
+            hp.load(s, pk.cpu().numpy(), im.cpu().numpy())
+        batch_ms = []
+
+        def step(k):
+            s = k % hp.depth
+            if k >= hp.depth:
+                hp.wait(s)
+                batch_ms.append(hp.timings_ms(s)["total"])
+            hp.submit(s, a.batch)
+
+        def drain():
+            for s in range(hp.depth):
+                hp.wait(s)
+
+        def results():
+            _, m = hp.results(0)
+            return np.array(m), np.array(batch_ms[-64:]) * 1e3
+    elif not sharded:
         out, meta, lat = dp.alloc_batch(a.batch)
 
         def step(k):
@@ -134,6 +161,8 @@ def main() -> None:
     setup_s = time.time() - t_setup
     for k in range(a.warmup):
         step(k)
+    if drain:
+        drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -141,6 +170,8 @@ def main() -> None:
     t0 = time.perf_counter()
     for k in range(a.steps):
         step(a.warmup + k)
+    if drain:
+        drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -164,7 +195,7 @@ def main() -> None:
 
     # small-batch latency probe (outside the timed region): 64K packets per step, fused/sharded alike
     p50_small = None
-    if not a.no_lowlat:
+    if not a.no_lowlat and a.io == "device":
         nsm = 1 << 16
         pk, im = batches[0][0][:nsm].contiguous(), batches[0][1][:nsm].contiguous()
         if not sharded:
@@ -215,6 +246,7 @@ def main() -> None:
                 (f"replicated tables x{world}, fused kernel + 1x all-to-all of cross-GPU frames (RCCL/xGMI), "
                  f"{a.chunks}-chunk overlap" if replicated else
                  f"flow-shard x{world} + 3x all-to-all (RCCL/xGMI), {a.chunks}-chunk overlap"),
+                "io": a.io if not sharded else "device",
             },
             "p50_latency_us": round(p50, 2),
             "p99_latency_us": round(p99, 2),

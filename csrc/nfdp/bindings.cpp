@@ -7,6 +7,7 @@
 #include <pybind11/stl.h>
 
 #include "host.h"
+#include "pktio.h"
 #include "shard.h"
 
 namespace py = pybind11;
@@ -323,6 +324,58 @@ PYBIND11_MODULE(_nfdp, m) {
     check(launch_fused(f, cfg, s), "fused_remote");
     check(launch_seg_headers(f.pcnt, f.send_pkt, g.nranks, pkt_seg_bytes(g.cap_pkt), g.cap_pkt, s), "seg_headers");
   });
+
+  // Host <-> HBM packet I/O engine (pinned host slots, SDMA streams, event-chained kernel).
+  py::class_<PacketIo>(m, "PacketIo")
+      .def(py::init<uint32_t, uint32_t>(), py::arg("capacity"), py::arg("depth") = 3)
+      .def_property_readonly("capacity", &PacketIo::capacity)
+      .def_property_readonly("depth", &PacketIo::depth)
+      .def("host_in", [](py::object self, uint32_t s) {
+        PacketIo& io = self.cast<PacketIo&>();
+        if (s >= io.depth()) throw std::out_of_range("slot");
+        return py::array_t<uint8_t>({(py::ssize_t)io.capacity(), (py::ssize_t)64}, io.host_in(s), self);
+      })
+      .def("host_inmeta", [](py::object self, uint32_t s) {
+        PacketIo& io = self.cast<PacketIo&>();
+        if (s >= io.depth()) throw std::out_of_range("slot");
+        return py::array_t<uint32_t>({(py::ssize_t)io.capacity()}, io.host_inmeta(s), self);
+      })
+      .def("host_out", [](py::object self, uint32_t s) {
+        PacketIo& io = self.cast<PacketIo&>();
+        if (s >= io.depth()) throw std::out_of_range("slot");
+        return py::array_t<uint8_t>({(py::ssize_t)io.capacity(), (py::ssize_t)64}, io.host_out(s), self);
+      })
+      .def("host_meta", [](py::object self, uint32_t s) {
+        PacketIo& io = self.cast<PacketIo&>();
+        if (s >= io.depth()) throw std::out_of_range("slot");
+        return py::array_t<uint32_t>({(py::ssize_t)io.capacity()}, io.host_meta(s), self);
+      })
+      .def("dev_lat", [](PacketIo& io, uint32_t s) { return reinterpret_cast<uintptr_t>(io.dev_lat(s)); })
+      .def("submit", [](PacketIo& io, uint32_t s, uint32_t n, py::dict tables, py::dict d, int hash_mode, int acl_mode,
+                        int num_cus) {
+        FusedLaunch f{};
+        f.t = tables_from(tables);
+        f.flow_ctr = ptr<unsigned long long>(d, "flow_ctr"); f.port_ctr = ptr<unsigned long long>(d, "port_ctr");
+        f.drop_ctr = ptr<unsigned long long>(d, "drop_ctr"); f.t0 = ptr<const unsigned long long>(d, "t0");
+        f.acl_wfrag = ptr<const void>(d, "acl_wfrag"); f.acl_cinit = ptr<const void>(d, "acl_cinit");
+        f.acl_tiles = val<uint32_t>(d, "acl_tiles", 1);
+        f.toep_frag = ptr<const void>(d, "toep_frag"); f.toep_tab = ptr<const uint32_t>(d, "toep_tab");
+        f.flags = val<uint32_t>(d, "flags", 0);
+        if (!f.flow_ctr || !f.port_ctr || !f.drop_ctr) throw std::invalid_argument("pktio submit: null counters");
+        if (hash_mode == 2 && !f.toep_frag) throw std::invalid_argument("MFMA hash needs toeplitz frags");
+        if (hash_mode == 1 && !f.toep_tab) throw std::invalid_argument("LDS hash needs toeplitz table");
+        if (acl_mode == 1 && (!f.acl_wfrag || !f.acl_cinit)) throw std::invalid_argument("MFMA ACL needs frags");
+        LaunchCfg cfg;
+        cfg.hash_mode = hash_mode; cfg.acl_mode = acl_mode; cfg.num_cus = num_cus;
+        io.submit(s, n, f, cfg);
+      })
+      .def("wait", [](PacketIo& io, uint32_t s) { py::gil_scoped_release nogil; io.wait(s); })
+      .def("ready", &PacketIo::ready)
+      .def("timings", [](PacketIo& io, uint32_t s) {
+        float a, b, c, t;
+        io.timings(s, &a, &b, &c, &t);
+        return py::make_tuple(a, b, c, t);
+      });
 
   m.def("launch_harvest", [](uintptr_t ctr, uintptr_t out, uint32_t n, uintptr_t stream) {
     check(launch_harvest(reinterpret_cast<unsigned long long*>(ctr), reinterpret_cast<unsigned long long*>(out), n,
