@@ -1,6 +1,8 @@
 // agent.cpp — fw-side control agent loop and the host-side control client (see agent.h).
 #include "agent.h"
 
+#include <algorithm>
+
 #include <cstring>
 #include <stdexcept>
 
@@ -160,6 +162,7 @@ void Agent::loop() {
   const auto hb_every = std::chrono::milliseconds(cfg_.hb_interval_ms ? cfg_.hb_interval_ms : 1000);
   auto next_hb = clock_t_::now();
   while (running_.load(std::memory_order_relaxed)) {
+    const uint32_t seen = mbox_.h2f().bell();
     handle_reset();
     process_host(max_msgs_);
     flush_out();
@@ -170,9 +173,18 @@ void Agent::loop() {
       std::lock_guard<std::mutex> g(cnt_mu_);
       cnt_.heartbeats++;
     }
-    // The mailbox is polled (the reference polls too, loop.c); 200 us keeps the request
-    // round-trip well under a millisecond without burning a core.
-    std::this_thread::sleep_for(std::chrono::microseconds(200));
+    // Sleep on the H2F doorbell (host requests, resets, status changes and local link events
+    // ring it) until the next heartbeat is due; with requests left over from the per-iteration
+    // budget, or F2H records waiting for ring space, only briefly.
+    bool backlog;
+    {
+      std::lock_guard<std::mutex> g(out_mu_);
+      backlog = !out_.empty();
+    }
+    if (mbox_.h2f().used() != 0 && !backlog) continue;
+    const auto us = std::chrono::duration_cast<std::chrono::microseconds>(next_hb - clock_t_::now()).count();
+    const int cap = backlog ? 200 : 20000;
+    mbox_.h2f().wait_bell(seen, (int)std::max<int64_t>(0, std::min<int64_t>(us, cap)));
   }
 }
 
@@ -204,6 +216,7 @@ void Agent::set_link(const FnKey& k, bool up) {
     }
     if (!merged) out_.push_back(std::move(m));
   }
+  mbox_.h2f().ring();  // wake the fw loop to flush it
   if (plugin_) plugin_->broadcast_event(up ? PluginServer::kEvLinkUp : PluginServer::kEvLinkDown, {});
   std::lock_guard<std::mutex> g(cnt_mu_);
   cnt_.notifications++;
@@ -241,6 +254,7 @@ void Agent::send_custom(const MsgHdr& h, const std::vector<uint8_t>& data) {
     std::lock_guard<std::mutex> g(out_mu_);
     out_.push_back(std::move(m));
   }
+  mbox_.h2f().ring();
   std::lock_guard<std::mutex> g(cnt_mu_);
   cnt_.custom_out++;
 }
@@ -284,13 +298,17 @@ bool HostCtrl::wait_ready(int timeout_ms) {
   return false;
 }
 
-void HostCtrl::set_status(Status s) { mbox_.info().host_status.store((uint64_t)s, std::memory_order_release); }
+void HostCtrl::set_status(Status s) {
+  mbox_.info().host_status.store((uint64_t)s, std::memory_order_release);
+  mbox_.h2f().ring();
+}
 
 void HostCtrl::drain(int timeout_ms, uint16_t want_id, Response* out, bool* got) {
   const auto dl = clock_t_::now() + std::chrono::milliseconds(timeout_ms);
   Msg m;
   *got = false;
   for (;;) {
+    const uint32_t seen = mbox_.f2h().bell();  // read before popping: a later push cannot be missed
     while (mbox_.f2h().pop(m)) {
       if (m.hdr.flags & kFlagResp) {
         if (m.hdr.msg_id == want_id && m.hdr.sz >= sizeof(RespHdr)) {
@@ -310,8 +328,10 @@ void HostCtrl::drain(int timeout_ms, uint16_t want_id, Response* out, bool* got)
       }
       if (*got) return;
     }
-    if (want_id == 0 || clock_t_::now() >= dl) return;
-    std::this_thread::sleep_for(std::chrono::microseconds(100));
+    if (want_id == 0) return;
+    const auto us = std::chrono::duration_cast<std::chrono::microseconds>(dl - clock_t_::now()).count();
+    if (us <= 0) return;
+    mbox_.f2h().wait_bell(seen, (int)std::min<int64_t>(us, 20000));  // F2H doorbell (the fw rang it)
   }
 }
 
@@ -396,6 +416,7 @@ bool HostCtrl::reset(int timeout_ms) {
   pl.acquired();
   Info& in = mbox_.info();
   const uint64_t want = in.host_resets.fetch_add(1, std::memory_order_acq_rel) + 1;
+  mbox_.h2f().ring();  // PERST: wake the fw loop
   const auto dl = clock_t_::now() + std::chrono::milliseconds(timeout_ms);
   while (clock_t_::now() < dl) {
     if (in.fw_resets.load(std::memory_order_acquire) >= want &&

@@ -1,6 +1,13 @@
 // mbox.cpp — shared-memory control mailbox (see mbox.h for the layout).
 #include "mbox.h"
 
+#include <linux/futex.h>
+#include <sys/syscall.h>
+#include <unistd.h>
+
+#include <climits>
+#include <ctime>
+
 #include <fcntl.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
@@ -46,6 +53,7 @@ bool Ring::push(const MsgHdr& h, const void* payload) {
   copy_in(p, &h, sizeof(MsgHdr));
   if (h.sz) copy_in((p + (uint32_t)sizeof(MsgHdr)) % sz, payload, h.sz);
   ctl_->prod.store((p + rec) % sz, std::memory_order_release);
+  ring();
   return true;
 }
 
@@ -65,6 +73,28 @@ bool Ring::pop(Msg& out) {
   if (out.hdr.sz) copy_out((c + (uint32_t)sizeof(MsgHdr)) % sz, out.data.data(), out.hdr.sz);
   ctl_->cons.store((c + rec) % sz, std::memory_order_release);
   return true;
+}
+
+static long futex(std::atomic<uint32_t>* w, int op, uint32_t val, const timespec* ts) {
+  static_assert(sizeof(std::atomic<uint32_t>) == sizeof(uint32_t), "futex word");
+  return syscall(SYS_futex, reinterpret_cast<uint32_t*>(w), op, val, ts, nullptr, 0);
+}
+
+void Ring::ring() {
+  ctl_->bell.fetch_add(1, std::memory_order_seq_cst);
+  if (!waiters_ || waiters_->load(std::memory_order_seq_cst) != 0) futex(&ctl_->bell, FUTEX_WAKE, INT32_MAX, nullptr);
+}
+
+bool Ring::wait_bell(uint32_t seen, int timeout_us) {
+  if (bell() != seen) return true;
+  if (timeout_us <= 0) return false;
+  if (waiters_) waiters_->fetch_add(1, std::memory_order_seq_cst);
+  if (bell() == seen) {
+    timespec ts{timeout_us / 1000000, (long)(timeout_us % 1000000) * 1000};
+    futex(&ctl_->bell, FUTEX_WAIT, seen, &ts);  // EAGAIN if it already moved, ETIMEDOUT, or woken
+  }
+  if (waiters_) waiters_->fetch_sub(1, std::memory_order_seq_cst);
+  return bell() != seen;
 }
 
 void Ring::reset() {
@@ -89,8 +119,9 @@ static uint8_t* map_file(const std::string& path, uint32_t size, bool create) {
 
 void Mailbox::bind() {
   auto* q = reinterpret_cast<QCtl*>(mem_ + kInfoBytes);
-  h2f_ = Ring(&q[0], mem_ + kHeaderBytes);
-  f2h_ = Ring(&q[1], mem_ + kHeaderBytes + qsz_);
+  Info& in = info();
+  h2f_ = Ring(&q[0], mem_ + kHeaderBytes, &in.h2f_waiters);
+  f2h_ = Ring(&q[1], mem_ + kHeaderBytes + qsz_, &in.f2h_waiters);
 }
 
 Mailbox Mailbox::create(const std::string& path, uint32_t size) {

@@ -71,7 +71,9 @@ struct alignas(8) Info {
   std::atomic<uint64_t> host_status;    // 24
   std::atomic<uint64_t> host_heartbeat; // 32
   std::atomic<uint64_t> host_resets;    // 40   host-requested resets ("PERST") so far
-  uint8_t pad0[136 - 48];
+  std::atomic<uint32_t> h2f_waiters;    // 48   fw-side threads sleeping on the H2F doorbell
+  std::atomic<uint32_t> f2h_waiters;    // 52   host-side threads sleeping on the F2H doorbell
+  uint8_t pad0[136 - 56];
   std::atomic<uint64_t> fw_version;     // 136  min << 32 | max
   std::atomic<uint64_t> fw_status;      // 144
   std::atomic<uint64_t> fw_heartbeat;   // 152
@@ -86,15 +88,24 @@ struct alignas(8) QCtl {
   std::atomic<uint32_t> prod;
   std::atomic<uint32_t> cons;
   uint32_t sz;
-  uint32_t rsvd;
+  std::atomic<uint32_t> bell;  // doorbell: bumped on every push, futex word for sleeping consumers
 };
 static_assert(sizeof(QCtl) == kQCtlBytes, "queue control is 16 bytes");
 
 // One direction of the mailbox.
+//
+// Doorbells (the role of the reference's OEI interrupt triggers, cnxk.c:177-230): the producer
+// bumps `bell` after publishing a record and FUTEX_WAKEs only when the consumer side announced a
+// sleeper in `waiters`; a consumer sleeps with FUTEX_WAIT on `bell` (a shared-mapping futex works
+// across processes) instead of polling.  waiters++ / re-check / wait on the consumer and
+// bell++ / check waiters on the producer, both seq_cst, cannot lose a wakeup.
 class Ring {
  public:
   Ring() = default;
-  Ring(QCtl* ctl, uint8_t* base) : ctl_(ctl), base_(base) {}
+  Ring(QCtl* ctl, uint8_t* base, std::atomic<uint32_t>* waiters = nullptr) : ctl_(ctl), base_(base), waiters_(waiters) {}
+  uint32_t bell() const { return ctl_->bell.load(std::memory_order_seq_cst); }
+  void ring();                                     // bump the doorbell, wake sleepers
+  bool wait_bell(uint32_t seen, int timeout_us);   // true once bell != seen (woken or already)
   uint32_t size() const { return ctl_->sz; }
   uint32_t used() const;
   uint32_t space() const;  // bytes a producer may still write
@@ -109,6 +120,7 @@ class Ring {
   void copy_out(uint32_t off, void* dst, uint32_t n) const;
   QCtl* ctl_ = nullptr;
   uint8_t* base_ = nullptr;
+  std::atomic<uint32_t>* waiters_ = nullptr;
 };
 
 // A mapped mailbox region.  `create` formats a new region (fw side owns formatting, as the

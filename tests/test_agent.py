@@ -259,3 +259,20 @@ def test_agent_sanitizer_stress(kind):
     r = subprocess.run([str(exe), "1.5"], capture_output=True, text=True, timeout=120, env=env)
     assert r.returncode == 0, r.stdout + r.stderr
     assert r.stdout.strip().endswith("ok")
+
+
+def test_doorbell_request_latency(running):
+    """Requests wake the agent through the H2F futex doorbell and responses wake the host through
+    the F2H one: the round trip is not bounded below by a polling period."""
+    _, host = running
+    for _ in range(20):
+        host.request(0, 0, 1, H2F.MTU)
+    ts = []
+    for _ in range(200):
+        t = time.perf_counter()
+        host.request(0, 0, 1, H2F.MTU)
+        ts.append(time.perf_counter() - t)
+    ts.sort()
+    p50_us = ts[len(ts) // 2] * 1e6
+    print(f"mailbox round trip p50 {p50_us:.1f} us")
+    assert p50_us < 150, f"p50 mailbox round trip {p50_us:.0f} us"
