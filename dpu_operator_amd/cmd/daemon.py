@@ -21,7 +21,12 @@ def main(argv=None, api=None, stop: threading.Event | None = None) -> int:
     ap.add_argument("--mode", default="auto")
     ap.add_argument("--root", default="/", help="path-manager root (tests)")
     ap.add_argument("--cni-src", default="/dpu-cni")
+    ap.add_argument("--node-config", default="", help="node policy YAML (config.py); also DPU_NODE_CONFIG")
     a = ap.parse_args(argv)
+    if a.node_config:
+        from ..config import NodeConfig, set_node_config
+
+        set_node_config(NodeConfig.load(a.node_config))
     logging.basicConfig(level=logging.DEBUG)
     from ..cni.netlink import RtNetlink
     from ..cni.sriov import SriovManager

@@ -16,6 +16,7 @@ import signal
 import sys
 import threading
 
+from ..config import NodeConfig, node_config, set_node_config
 from ..utils.paths import PathManager
 
 
@@ -27,7 +28,10 @@ def build_vsp(a, pm: PathManager):
     if a.vendor == "amd-gpu":
         from ..vsp.gpu import GpuVsp
 
-        return GpuVsp(pm, device=a.device or None, flow_buckets=a.flow_buckets, state_dir=a.state_dir or None)
+        cfg = node_config()
+        return GpuVsp(pm, device=a.device or None, flow_buckets=a.flow_buckets or cfg.flow_buckets,
+                      hash_mode=cfg.hash_mode, acl_mode=cfg.acl_mode,
+                      state_dir=a.state_dir or cfg.vsp_state_dir or None)
     from ..cni.netlink import RtNetlink
     from ..platform.platform import SysfsPlatform
     from ..utils.cmdrunner import HostRunner
@@ -37,7 +41,7 @@ def build_vsp(a, pm: PathManager):
     def dataplane():
         from ..dataplane.engine import DataPlane
 
-        dp = DataPlane(device=a.device or "cuda", flow_buckets=a.flow_buckets)
+        dp = DataPlane(device=a.device or "cuda", flow_buckets=a.flow_buckets or node_config().flow_buckets)
         dp.commit(full=True)
         return dp
 
@@ -65,7 +69,8 @@ def main(argv=None, stop: threading.Event | None = None) -> int:
     ap.add_argument("--root", default="/")
     ap.add_argument("--sys-root", default="/")
     ap.add_argument("--device", default="")
-    ap.add_argument("--flow-buckets", type=int, default=1 << 18)
+    ap.add_argument("--flow-buckets", type=int, default=0, help="0 = node config (default 2^18)")
+    ap.add_argument("--node-config", default="", help="node policy YAML (config.py); also DPU_NODE_CONFIG")
     ap.add_argument("--debug-dp", action="store_true")
     ap.add_argument("--uplink", default="rpm0")
     ap.add_argument("--p4rt-addr", default="127.0.0.1:9559")
@@ -73,6 +78,8 @@ def main(argv=None, stop: threading.Event | None = None) -> int:
     ap.add_argument("--mode", default="ipu")
     ap.add_argument("--state-dir", default="", help="amd-gpu: journal + snapshot directory (resume on restart)")
     a = ap.parse_args(argv)
+    if a.node_config:
+        set_node_config(NodeConfig.load(a.node_config))
     logging.basicConfig(level=logging.INFO)
     vsp = build_vsp(a, PathManager(a.root)).start()
     stop = stop or threading.Event()

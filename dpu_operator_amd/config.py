@@ -1,0 +1,96 @@
+"""Node policy configuration.
+
+The reference hard-codes its node policy (SURVEY §5 "Config / flag system"): 8 VFs
+(dpudevicehandler.go:89), LogicalBridge / VLAN = vf + 2 (hostsidemanager.go:67,188), PF 0, two
+DPU devices per NF pod (sfc.go:54-59), comm-channel port 8085 and fe80::1/::2, bridge names.
+Here those values are one typed config with the reference's values as defaults, loaded from a
+YAML file (SafeLoader) named by `DPU_NODE_CONFIG` or `--node-config`, overridable per field by
+`DPU_CFG_<FIELD>` environment variables.  Components read `node_config()`; tests swap it with
+`set_node_config()`.
+"""
+from __future__ import annotations
+
+import dataclasses
+import os
+from dataclasses import dataclass, field
+
+from . import vars as V
+
+
+@dataclass
+class NodeConfig:
+    # device plumbing
+    vf_count: int = 8                  # VFs / GPU vports created at start-up
+    pf: int = 0                        # host PF whose VFs back pod interfaces
+    logical_bridge_offset: int = 2     # LogicalBridge (= VF VLAN) = vf + offset
+    nf_devices_per_pod: int = 2        # DPU devices an NF pod requests (ingress + egress)
+    resource_name: str = V.RESOURCE_NAME
+    nf_nad_name: str = V.NF_NAD_NAME
+    # vendor comm channel (Marvell / NetSec VSPs)
+    comm_port: int = 8085
+    comm_ipv6_dpu: str = "fe80::1"
+    comm_ipv6_host: str = "fe80::2"
+    # GPU data plane
+    flow_buckets: int = 1 << 18        # 4 slots each: 1M flows at 50 % load per 2^19
+    hash_mode: str = "lds"             # lds | mfma | scalar
+    acl_mode: str = "mfma"             # mfma | scalar | off
+    wire_port: int = 4000
+    vsp_state_dir: str = ""            # journal + snapshots (checkpoint/resume); "" = off
+    # daemon cadences (seconds)
+    device_poll: float = 5.0           # ListAndWatch refresh (deviceplugin.go:109)
+    detect_poll: float = 1.0           # platform detection (daemon.go:88)
+    extra: dict = field(default_factory=dict)
+
+    @classmethod
+    def load(cls, path: str | None = None, env: dict | None = None) -> "NodeConfig":
+        env = os.environ if env is None else env
+        path = path or env.get("DPU_NODE_CONFIG", "")
+        data: dict = {}
+        if path:
+            import yaml
+
+            with open(path) as f:
+                data = yaml.load(f, Loader=yaml.SafeLoader) or {}
+            if not isinstance(data, dict):
+                raise ValueError(f"{path}: node config must be a mapping")
+        names = {f.name: f for f in dataclasses.fields(cls)}
+        unknown = set(data) - set(names)
+        if unknown:
+            raise ValueError(f"unknown node config keys: {sorted(unknown)}")
+        cfg = cls(**data)
+        for name, f in names.items():
+            v = env.get(f"DPU_CFG_{name.upper()}")
+            if v is None or name == "extra":
+                continue
+            cur = getattr(cfg, name)
+            setattr(cfg, name, type(cur)(v) if not isinstance(cur, bool) else v.lower() in ("1", "true", "yes"))
+        cfg.validate()
+        return cfg
+
+    def validate(self) -> None:
+        if not 0 <= self.vf_count <= 2048:
+            raise ValueError("vf_count out of range")
+        if not 1 <= self.logical_bridge_offset + max(self.vf_count - 1, 0) <= 4094:
+            raise ValueError("logical bridges must stay within VLAN 1-4094")
+        if self.nf_devices_per_pod < 1:
+            raise ValueError("nf_devices_per_pod must be >= 1")
+        if self.hash_mode not in ("lds", "mfma", "scalar") or self.acl_mode not in ("mfma", "scalar", "off"):
+            raise ValueError("unknown hash / ACL mode")
+
+    def logical_bridge(self, vf: int) -> int:
+        return vf + self.logical_bridge_offset
+
+
+_CURRENT: NodeConfig | None = None
+
+
+def node_config() -> NodeConfig:
+    global _CURRENT
+    if _CURRENT is None:
+        _CURRENT = NodeConfig.load()
+    return _CURRENT
+
+
+def set_node_config(cfg: NodeConfig | None) -> None:
+    global _CURRENT
+    _CURRENT = cfg

@@ -34,12 +34,16 @@ DEFAULT_VF_COUNT = 8
 
 
 class DeviceHandler:
-    def __init__(self, vsp, dpu_mode: bool, vf_count: int = DEFAULT_VF_COUNT, numa_of=None):
+    def __init__(self, vsp, dpu_mode: bool, vf_count: int | None = None, numa_of=None):
         """`numa_of(device_id) -> int` (optional): NUMA node advertised to kubelet's topology
         manager (-1 = unknown); e.g. devutils.get_numa_node for PCI ids, or the data-plane GPU's
         node for GPU vports."""
         self.vsp = vsp
         self.dpu_mode = dpu_mode
+        if vf_count is None:
+            from ..config import node_config
+
+            vf_count = node_config().vf_count
         self.vf_count = vf_count
         self.numa_of = numa_of
         self._setup = threading.Event()

@@ -32,6 +32,7 @@ from ..cni.types import PodRequest
 from ..k8s.apiserver import ApiServer
 from ..k8s.manager import Manager
 from ..proto import GoogleEmpty, opi
+from ..config import node_config
 from ..proto.grpcutil import Stub, retry_service_config, service_handler
 from ..utils.paths import PathManager
 from .deviceplugin import DeviceHandler, DevicePluginServer
@@ -123,7 +124,7 @@ class HostSideManager(_Base):
         req = opi.CreateBridgePortRequest(bridge_port=opi.BridgePort(
             name=f"host{pf}-{vf}",
             spec=opi.BridgePortSpec(ptype=opi.BRIDGE_PORT_TYPE_ACCESS, mac_address=parse_mac(mac),
-                                    logical_bridges=[str(vf + 2)])))
+                                    logical_bridges=[str(node_config().logical_bridge(vf))])))
         return client.CreateBridgePort(req, timeout=60)
 
     def delete_bridge_port(self, pf: int, vf: int, vlan: int, mac: str) -> None:

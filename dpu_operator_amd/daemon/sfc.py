@@ -17,6 +17,7 @@ import logging
 
 from .. import vars as V
 from ..api.v1 import KIND_SFC, ServiceFunctionChain
+from ..config import node_config
 from ..k8s.apiserver import ApiServer, NotFound, set_controller_reference
 from ..k8s.manager import Request, Result
 
@@ -25,14 +26,17 @@ GPU_NF_PREFIX = "gpu-nf://"
 
 
 def network_function_pod(name: str, image: str) -> dict:
+    cfg = node_config()
+    nets = ", ".join([cfg.nf_nad_name] * cfg.nf_devices_per_pod)
     return {
         "apiVersion": "v1", "kind": "Pod",
         "metadata": {"name": name, "namespace": V.NAMESPACE,
-                     "annotations": {"k8s.v1.cni.cncf.io/networks": f"{V.NF_NAD_NAME}, {V.NF_NAD_NAME}"}},
+                     "annotations": {"k8s.v1.cni.cncf.io/networks": nets}},
         "spec": {"containers": [{
             "name": name, "image": image,
             "ports": [{"name": "web", "containerPort": 8080}],
-            "resources": {"requests": {V.RESOURCE_NAME: "2"}, "limits": {V.RESOURCE_NAME: "2"}},
+            "resources": {"requests": {cfg.resource_name: str(cfg.nf_devices_per_pod)},
+                          "limits": {cfg.resource_name: str(cfg.nf_devices_per_pod)}},
             "securityContext": {"privileged": True,
                                 "capabilities": {"drop": ["ALL"], "add": ["NET_RAW", "NET_ADMIN"]}},
         }]},

@@ -37,6 +37,7 @@ import numpy as np
 from ..cni.netlink import FakeNetlink, Link, NetlinkManager
 from ..dataplane import tables as T
 from ..dataplane.engine import DataPlane
+from ..config import node_config
 from ..utils.journal import Journal
 from .base import VspBase
 
@@ -231,7 +232,7 @@ class GpuVsp(VspBase):
         vf = int(m.group(2))
         if vf not in self.vports:
             raise ValueError(f"VF {vf} does not exist (SetNumVfs first)")
-        vlan = int(logical_bridges[0]) if logical_bridges else vf + 2
+        vlan = int(logical_bridges[0]) if logical_bridges else node_config().logical_bridge(vf)
         if not 1 <= vlan <= 4094:
             raise ValueError(f"logical bridge / vlan {vlan} out of range 1-4094")
         v = self.vports[vf]

@@ -259,3 +259,32 @@ def test_proto_wire_round_trip():
     assert vendor.NFRequest.FromString(nf.SerializeToString()) == nf
     # field numbers on the wire (golden bytes): Device{ID=1 "x", health=2 "Healthy"}
     assert dp.Device(ID="x", health="Healthy").SerializeToString() == b"\x0a\x01x\x12\x07Healthy"
+
+
+# ------------------------------------------------------------------------------ node policy config
+def test_node_config_file_env_and_wiring(tmp_path):
+    from dpu_operator_amd.config import NodeConfig, node_config, set_node_config
+    from dpu_operator_amd.daemon.deviceplugin import DeviceHandler
+    from dpu_operator_amd.daemon.sfc import network_function_pod
+
+    d = NodeConfig()
+    assert (d.vf_count, d.logical_bridge(3), d.nf_devices_per_pod, d.comm_port) == (8, 5, 2, 8085)
+    p = tmp_path / "node.yaml"
+    p.write_text("vf_count: 16\nlogical_bridge_offset: 100\nnf_devices_per_pod: 3\n")
+    cfg = NodeConfig.load(str(p), env={"DPU_CFG_HASH_MODE": "mfma"})
+    assert cfg.vf_count == 16 and cfg.logical_bridge(0) == 100 and cfg.hash_mode == "mfma"
+    with pytest.raises(ValueError):
+        NodeConfig.load(str(p), env={"DPU_CFG_HASH_MODE": "bogus"})
+    bad = tmp_path / "bad.yaml"
+    bad.write_text("no_such_key: 1\n")
+    with pytest.raises(ValueError):
+        NodeConfig.load(str(bad), env={})
+    set_node_config(cfg)
+    try:
+        assert DeviceHandler(None, True).vf_count == 16
+        pod = network_function_pod("nf", "img")
+        assert pod["spec"]["containers"][0]["resources"]["requests"][V.RESOURCE_NAME] == "3"
+        assert pod["metadata"]["annotations"]["k8s.v1.cni.cncf.io/networks"].count(V.NF_NAD_NAME) == 3
+        assert node_config() is cfg
+    finally:
+        set_node_config(None)
