@@ -8,6 +8,7 @@
 
 #include "host.h"
 #include "pktio.h"
+#include "ring.h"
 #include "shard.h"
 
 namespace py = pybind11;
@@ -375,6 +376,62 @@ PYBIND11_MODULE(_nfdp, m) {
         float a, b, c, t;
         io.timings(s, &a, &b, &c, &t);
         return py::make_tuple(a, b, c, t);
+      });
+
+  // Blocking copy between any two addresses (device or host; unified addressing).
+  m.def("memcpy", [](uintptr_t dst, uintptr_t src, size_t nbytes) {
+    py::gil_scoped_release nogil;
+    check(hipMemcpy(reinterpret_cast<void*>(dst), reinterpret_cast<const void*>(src), nbytes, hipMemcpyDefault),
+          "memcpy");
+  });
+
+  // Persistent ring kernel (low-latency path): the host publishes 64-packet chunks, resident
+  // waves process them as they appear, completion flags come back through pinned host memory.
+  py::class_<RingEngine>(m, "RingEngine")
+      .def(py::init<uint32_t, int, int, bool>(), py::arg("capacity"), py::arg("num_cus"), py::arg("wgs_per_cu") = 1,
+           py::arg("coop") = true)
+      .def_property_readonly("capacity", &RingEngine::capacity)
+      .def_property_readonly("running", &RingEngine::running)
+      .def_property_readonly("published", &RingEngine::published)
+      .def("dev_in", [](RingEngine& r) { return reinterpret_cast<uintptr_t>(r.dev_in()); })
+      .def("dev_inmeta", [](RingEngine& r) { return reinterpret_cast<uintptr_t>(r.dev_inmeta()); })
+      .def("dev_out", [](RingEngine& r) { return reinterpret_cast<uintptr_t>(r.dev_out()); })
+      .def("dev_meta", [](RingEngine& r) { return reinterpret_cast<uintptr_t>(r.dev_meta()); })
+      .def("dev_svc", [](RingEngine& r) { return reinterpret_cast<uintptr_t>(r.dev_svc()); })
+      .def("start", [](RingEngine& r, py::dict tables, py::dict d, int hash_mode, int acl_mode, int num_cus,
+                       double deadline_s) {
+        FusedLaunch f{};
+        f.t = tables_from(tables);
+        f.flow_ctr = ptr<unsigned long long>(d, "flow_ctr"); f.port_ctr = ptr<unsigned long long>(d, "port_ctr");
+        f.drop_ctr = ptr<unsigned long long>(d, "drop_ctr");
+        f.acl_wfrag = ptr<const void>(d, "acl_wfrag"); f.acl_cinit = ptr<const void>(d, "acl_cinit");
+        f.acl_tiles = val<uint32_t>(d, "acl_tiles", 1);
+        f.toep_frag = ptr<const void>(d, "toep_frag"); f.toep_tab = ptr<const uint32_t>(d, "toep_tab");
+        f.flags = val<uint32_t>(d, "flags", 0);
+        if (!f.port_ctr || !f.drop_ctr) throw std::invalid_argument("ring start: null counters");
+        if (hash_mode == 2 && !f.toep_frag) throw std::invalid_argument("MFMA hash needs toeplitz frags");
+        if (hash_mode == 1 && !f.toep_tab) throw std::invalid_argument("LDS hash needs toeplitz table");
+        if (acl_mode == 1 && (!f.acl_wfrag || !f.acl_cinit)) throw std::invalid_argument("MFMA ACL needs frags");
+        LaunchCfg cfg;
+        cfg.hash_mode = hash_mode; cfg.acl_mode = acl_mode; cfg.num_cus = num_cus;
+        r.start(f, cfg, deadline_s);
+      })
+      .def("stop", [](RingEngine& r, double timeout_s) { py::gil_scoped_release nogil; r.stop(timeout_s); },
+           py::arg("timeout_s") = 30.0)
+      .def("completed", &RingEngine::completed)
+      .def("publish", &RingEngine::publish)
+      .def("wait", [](RingEngine& r, uint64_t end, double timeout_s) {
+        py::gil_scoped_release nogil;
+        return r.wait(end, timeout_s);
+      })
+      .def("probe", [](RingEngine& r, uint32_t batches, uint32_t batch, uint32_t inflight) {
+        double el = 0;
+        std::vector<double> v;
+        {
+          py::gil_scoped_release nogil;
+          v = r.probe(batches, batch, inflight, &el);
+        }
+        return py::make_tuple(py::array_t<double>(v.size(), v.data()), el);
       });
 
   m.def("launch_harvest", [](uintptr_t ctr, uintptr_t out, uint32_t n, uintptr_t stream) {

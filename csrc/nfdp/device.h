@@ -34,7 +34,10 @@ template <int HASH, int ACL>
 __device__ __forceinline__ void classify_wave(const FlowKey& key, uint4* kx, const v4i* lw,
                                               const v4i* lc, uint32_t acl_tiles, const v4i* lt,
                                               const uint32_t* ltab, const TablesView& t,
-                                              uint32_t& hash, int& acl_rule) {
+                                              uint32_t& hash, int& acl_rule, uint32_t tile0 = 0,
+                                              uint32_t tstep = 1, uint32_t* best_out = nullptr) {
+  // tile0 / tstep: this wave scans rule tiles tile0, tile0 + tstep, ... (cooperating waves split
+  // one chunk's ACL); best_out: the raw (mismatch << 10 | rule) minimum, for combining partials.
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t g = lane >> 4, col = lane & 15u;
   v4i bf[4][2];
@@ -85,7 +88,7 @@ __device__ __forceinline__ void classify_wave(const FlowKey& key, uint4* kx, con
   // ---- ACL (TCAM) ----
   if constexpr (ACL == kAclMfma) {
     uint32_t best[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
-    for (uint32_t nt = 0; nt < acl_tiles; ++nt) {
+    for (uint32_t nt = tile0; nt < acl_tiles; nt += tstep) {
       const v4i a0 = lw[(nt * 2 + 0) * 64 + lane], a1 = lw[(nt * 2 + 1) * 64 + lane];
       const v4i c = lc[nt * 4 + g];
       // Pass 1: does ANY packet of the wave match ANY rule of this tile?  (mismatch counts are
@@ -122,6 +125,7 @@ __device__ __forceinline__ void classify_wave(const FlowKey& key, uint4* kx, con
       best[tt] = min(best[tt], (uint32_t)__shfl_xor(best[tt], 32));
     }
     const uint32_t b = pick4(g, best[0], best[1], best[2], best[3]);
+    if (best_out) *best_out = b;
     acl_rule = (b >> 10) == 0 ? (int)(b & 1023u) : -1;
     if (acl_rule >= (int)t.n_acl) acl_rule = -1;
   } else if constexpr (ACL == kAclScalar) {
@@ -129,6 +133,49 @@ __device__ __forceinline__ void classify_wave(const FlowKey& key, uint4* kx, con
   } else {
     acl_rule = -1;
   }
+}
+
+// Small tables staged in LDS by the fused and ring kernels (ports < kLdsPorts, chain words,
+// ACL verdicts).
+constexpr uint32_t kLdsChains = 256;
+constexpr size_t kLdsTabBytes = kLdsPorts * sizeof(PortEntry) + kLdsChains * 8 + 1024;
+
+// Table-access policy of the fused kernel (pipeline.h DirectTables contract): LDS copies for
+// ports < kLdsPorts, the first kLdsChains chain words and every ACL verdict; global memory for
+// the rest (or for everything when the layout has no room: L.tabs false -> nport = nchain = 0).
+struct LdsTables {
+  const TablesView& t;
+  const PortEntry* lport;
+  const uint64_t* lchain;
+  const uint8_t* lperm;
+  uint32_t nport, nchain;
+  bool lds_perm;
+  __device__ __forceinline__ PortEntry port(uint32_t i) const { return i < nport ? lport[i] : t.ports[i]; }
+  __device__ __forceinline__ uint64_t chain_word(uint32_t c) const {
+    if (c < nchain) return lchain[c];
+    return c < t.n_chains ? *reinterpret_cast<const uint64_t*>(&t.chains[c]) : 0ull;
+  }
+  __device__ __forceinline__ bool permit(int r) const {
+    if (r < 0) return t.acl_default_permit != 0;
+    return (lds_perm ? lperm[r] : t.acl_permit[r]) != 0;
+  }
+};
+
+// Stage the small tables into LDS (caller provides the three regions; all threads of the block
+// call it, a __syncthreads() must follow).  Returns the table-access policy over the copies.
+__device__ __forceinline__ LdsTables stage_lds_tables(const TablesView& t, PortEntry* lport, uint64_t* lchain,
+                                                      uint8_t* lperm, bool enabled, uint32_t nthreads) {
+  const uint32_t nchain = enabled ? min(t.n_chains, kLdsChains) : 0u;
+  const bool lds_perm = enabled && t.n_acl <= 1024;
+  if (enabled) {
+    const uint4* gp = reinterpret_cast<const uint4*>(t.ports);
+    uint4* lp = reinterpret_cast<uint4*>(lport);
+    for (uint32_t i = threadIdx.x; i < kLdsPorts * 2; i += nthreads) lp[i] = gp[i];
+    for (uint32_t i = threadIdx.x; i < nchain; i += nthreads) lchain[i] = *reinterpret_cast<const uint64_t*>(&t.chains[i]);
+    if (lds_perm)
+      for (uint32_t i = threadIdx.x; i < t.n_acl; i += nthreads) lperm[i] = t.acl_permit[i];
+  }
+  return LdsTables{t, lport, lchain, lperm, enabled ? (uint32_t)kLdsPorts : 0u, nchain, lds_perm};
 }
 
 // 2-choice bucket probe.  A bucket is one 128-B line holding 4 x {key, action}; it is loaded
@@ -157,6 +204,38 @@ __device__ __forceinline__ int64_t flow_probe(const TablesView& t, const FlowKey
     b = th.b2;
   }
   return -1;
+}
+
+// Sum of a u32 over the 64 lanes (EXEC must be full): two quad permutes and two row rotates
+// leave every lane of a 16-lane row holding the row sum (DPP: no LDS crossbar round trips), then
+// four readlanes add the rows.
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+  v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xb1, 0xf, 0xf, false);   // quad_perm [1,0,3,2]
+  v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x4e, 0xf, 0xf, false);   // quad_perm [2,3,0,1]
+  v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x124, 0xf, 0xf, false);  // row_ror:4
+  v += (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x128, 0xf, 0xf, false);  // row_ror:8
+  return __builtin_amdgcn_readlane(v, 15) + __builtin_amdgcn_readlane(v, 31) +
+         __builtin_amdgcn_readlane(v, 47) + __builtin_amdgcn_readlane(v, 63);
+}
+
+// Wave-aggregated counter update: lanes whose `idx` is equal are summed and ONE atomic per
+// distinct index is issued.  Same-address atomics serialise at the memory side; a chunk of 64
+// packets from a handful of ports otherwise costs 64 back-to-back RMWs on a few counter words.
+// `inc` = bytes (< 2^16) when `packed` (the word is pkts << 40 | bytes), else a plain count.
+// EXEC must be full.
+__device__ __forceinline__ void wave_counter_add(unsigned long long* ctr, uint32_t idx, uint32_t inc, bool packed,
+                                                 bool active) {
+  unsigned long long pending = __ballot(active);
+  while (pending) {
+    const int leader = __ffsll((long long)pending) - 1;
+    const uint32_t k = __builtin_amdgcn_readlane(idx, leader);
+    const bool mine = active && idx == k;
+    const unsigned long long m = __ballot(mine);
+    const uint32_t sum = wave_sum_u32(mine ? inc : 0u);  // bytes (or count) of the group
+    const unsigned long long v = packed ? (((unsigned long long)__popcll(m) << 40) | sum) : (unsigned long long)sum;
+    if ((int)(threadIdx.x & 63u) == leader) atomicAdd(ctr + k, v);
+    pending &= ~m;
+  }
 }
 
 // ---- multi-GPU output segments (shared by the fused REMOTE variant and the sharded stages) ----

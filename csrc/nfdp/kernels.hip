@@ -50,8 +50,6 @@ struct LdsLayout {
   size_t acl_w, acl_c, toep_f, toep_t, kx, pc, drops, tports, tchain, tperm, total;
   bool tabs;  // small tables (ports < kLdsPorts, chain words, ACL verdicts) staged in LDS
 };
-constexpr uint32_t kLdsChains = 256;
-constexpr size_t kLdsTabBytes = kLdsPorts * sizeof(PortEntry) + kLdsChains * 8 + 1024;
 __host__ __device__ inline LdsLayout lds_layout(int hash_mode, int acl_mode, uint32_t acl_tiles) {
   LdsLayout L;
   size_t o = 0;
@@ -72,27 +70,6 @@ __host__ __device__ inline LdsLayout lds_layout(int hash_mode, int acl_mode, uin
   L.total = (o + 15) & ~(size_t)15;
   return L;
 }
-
-// Table-access policy of the fused kernel (pipeline.h DirectTables contract): LDS copies for
-// ports < kLdsPorts, the first kLdsChains chain words and every ACL verdict; global memory for
-// the rest (or for everything when the layout has no room: L.tabs false -> nport = nchain = 0).
-struct LdsTables {
-  const TablesView& t;
-  const PortEntry* lport;
-  const uint64_t* lchain;
-  const uint8_t* lperm;
-  uint32_t nport, nchain;
-  bool lds_perm;
-  __device__ __forceinline__ PortEntry port(uint32_t i) const { return i < nport ? lport[i] : t.ports[i]; }
-  __device__ __forceinline__ uint64_t chain_word(uint32_t c) const {
-    if (c < nchain) return lchain[c];
-    return c < t.n_chains ? *reinterpret_cast<const uint64_t*>(&t.chains[c]) : 0ull;
-  }
-  __device__ __forceinline__ bool permit(int r) const {
-    if (r < 0) return t.acl_default_permit != 0;
-    return (lds_perm ? lperm[r] : t.acl_permit[r]) != 0;
-  }
-};
 
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 constexpr int kBufCfg = 0x00020000;  // buffer resource word 3 (gfx9 family raw buffer)
@@ -142,17 +119,7 @@ __global__ __launch_bounds__(kBlock, 4) void fused_kernel(FusedArgs a) {
   PortEntry* lport = reinterpret_cast<PortEntry*>(smem + L.tports);
   uint64_t* lchain = reinterpret_cast<uint64_t*>(smem + L.tchain);
   uint8_t* lperm = smem + L.tperm;
-  const uint32_t nchain = L.tabs ? min(a.t.n_chains, kLdsChains) : 0u;
-  const bool lds_perm = L.tabs && a.t.n_acl <= 1024;
-  if (L.tabs) {
-    const uint4* gp = reinterpret_cast<const uint4*>(a.t.ports);
-    uint4* lp = reinterpret_cast<uint4*>(lport);
-    for (uint32_t i = threadIdx.x; i < kLdsPorts * 2; i += kBlock) lp[i] = gp[i];
-    for (uint32_t i = threadIdx.x; i < nchain; i += kBlock) lchain[i] = *reinterpret_cast<const uint64_t*>(&a.t.chains[i]);
-    if (lds_perm)
-      for (uint32_t i = threadIdx.x; i < a.t.n_acl; i += kBlock) lperm[i] = a.t.acl_permit[i];
-  }
-  const LdsTables ta{a.t, lport, lchain, lperm, L.tabs ? (uint32_t)kLdsPorts : 0u, nchain, lds_perm};
+  const LdsTables ta = stage_lds_tables(a.t, lport, lchain, lperm, L.tabs, kBlock);
   __syncthreads();
 
   const unsigned long long t0 = a.t0 ? *a.t0 : 0ull;

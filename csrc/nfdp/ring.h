@@ -1,0 +1,123 @@
+// ring.h — low-latency persistent data path: a resident kernel polls an ingress ring.
+//
+// The batch engine (kernels.hip, pktio.hip) pays a kernel launch and a batch-release barrier per
+// batch, which sets the floor of its per-packet latency.  The ring engine removes both: a
+// persistent kernel stays resident on the CUs and its waves claim 64-packet chunks of an ingress
+// ring as soon as the producer publishes them.  This is the GPU counterpart of the reference's
+// always-on DPU datapath (FXP / OvS-DPDK PMD threads polling their rings) and of the Octeon
+// control agent's poll loop (octep_cp_agent main.c:307-311), built the CDNA4 way:
+//
+//   host (or NIC)                          GPU (persistent ring_kernel, 64-wide waves)
+//   -------------                          ------------------------------------------
+//   frames -> ring slots [R x 64 B]        wave: ticket t = atomicAdd(claim, 1)  (chunk t = slots
+//   ctl.prod += n   (release store,                 64t .. 64t+63 mod R, one packet per lane)
+//                    pinned coherent       only the FRONTIER wave (64t == dprod) polls ctl.prod over
+//                    host memory)            PCIe and mirrors it into device memory (dprod); every
+//                                            other wave polls dprod in HBM/L2 -> one PCIe poller
+//                                          process the chunk: ingress, MFMA hash/ACL, flow probe,
+//                                            chain, emit (same stages as the fused kernel)
+//   poll flags[t % (R/64)] == t+1   <----  release fence (system scope), flags[t] = t + 1
+//
+// Drain semantics: `stop` makes a wave exit only while it WAITS for an unpublished chunk, and
+// tickets are claimed in order, so every chunk published before the stop is processed.  Every
+// wave also exits on a device-side deadline (s_memrealtime), so the grid always drains even if
+// the host dies.  Tables are staged at launch; a control-plane commit restarts the kernel
+// (stop -> drain -> relaunch, tens of µs) so a session never sees a torn table.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <vector>
+
+#include "host.h"
+
+namespace nfdp {
+
+// Bit 63 of the published-packet counter is the stop flag: one 64-bit word carries both, so a
+// wave that sees "stop" also sees the final count (no ordering between two words to get right).
+constexpr uint64_t kRingStop = 1ull << 63;
+
+// Host -> device control block, pinned coherent host memory (one 64-B line).
+struct alignas(64) RingCtl {
+  uint64_t prod;   // packets published (cumulative, multiple of 64) | kRingStop
+  uint32_t pad[14];
+};
+static_assert(sizeof(RingCtl) == 64, "RingCtl");
+
+// Device-resident ring state (HBM): the ticket counter and the prod mirror on separate 128-B
+// lines, so claim atomics and the waiters' polls do not contend for one line.
+struct alignas(128) RingDevState {
+  uint32_t claim;  // next chunk ticket
+  uint32_t pad0[31];
+  uint64_t dprod;  // device mirror of ctl.prod (advanced by the frontier wave), bit 63 = stop
+  uint32_t pad1[30];
+};
+static_assert(sizeof(RingDevState) == 256, "RingDevState");
+
+class RingEngine {
+ public:
+  // capacity: ring slots (power of two, >= 64).  wgs_per_cu: resident 256-thread workgroups per CU.
+  // coop: the 4 waves of a workgroup share each chunk (ACL tiles split 4 ways: lowest latency);
+  // otherwise every wave takes its own chunks (highest throughput).
+  RingEngine(uint32_t capacity, int num_cus, int wgs_per_cu = 1, bool coop = true);
+  ~RingEngine();
+  RingEngine(const RingEngine&) = delete;
+  RingEngine& operator=(const RingEngine&) = delete;
+
+  uint32_t capacity() const { return cap_; }
+  bool running() const { return running_; }
+  // device ring buffers (the producer stages frames here before publishing them)
+  void* dev_in() const { return d_in_; }
+  uint32_t* dev_inmeta() const { return d_im_; }
+  void* dev_out() const { return d_out_; }
+  uint32_t* dev_meta() const { return d_meta_; }
+  uint32_t* dev_svc() const { return d_svc_; }  // per-chunk device service time (ticks, 100 MHz)
+
+  // Launch the persistent kernel over the tables/counters in `f` (pkts/out/n are ignored).
+  void start(const FusedLaunch& f, const LaunchCfg& cfg, double deadline_s);
+  // Drain published chunks, stop every wave, wait for the grid to exit (throws on timeout).
+  void stop(double timeout_s = 30.0);
+
+  uint64_t published() const { return prod_; }
+  uint64_t completed();  // packets whose chunks all completed (in order)
+  // Publish n packets (multiple of 64) starting at ring position published() % capacity.
+  // Throws if the ring lacks room (producer must wait for completions).
+  uint64_t publish(uint32_t n);
+  // Spin until every chunk below `end` completed; false on timeout.
+  bool wait(uint64_t end, double timeout_s);
+
+  // Closed-loop probe run entirely in C++ (no Python in the timed loop): `batches` batches of
+  // `batch` packets, at most `inflight` outstanding.  Returns per-batch publish->completion
+  // latencies (µs, host steady clock) and sets *elapsed_s to the wall time of the whole run.
+  std::vector<double> probe(uint32_t batches, uint32_t batch, uint32_t inflight, double* elapsed_s);
+
+ private:
+  bool chunk_done(uint64_t chunk) const;
+  uint32_t cap_, nch_;
+  int num_cus_, wgs_;
+  bool coop_;
+  RingCtl* ctl_ = nullptr;        // pinned, coherent
+  uint32_t* flags_ = nullptr;     // pinned, coherent: [nch] completion sequence numbers
+  RingDevState* st_ = nullptr;    // device
+  uint8_t* d_in_ = nullptr;
+  uint32_t* d_im_ = nullptr;
+  uint8_t* d_out_ = nullptr;
+  uint32_t* d_meta_ = nullptr;
+  uint32_t* d_svc_ = nullptr;
+  hipStream_t stream_{};
+  uint64_t prod_ = 0;             // host copy of ctl->prod
+  uint64_t floor_ = 0;            // chunks < floor_ are complete
+  bool running_ = false;
+};
+
+// Launch the persistent kernel (ring.hip).  Exposed for the engine only.
+struct RingLaunch {
+  FusedLaunch f;
+  const void* pkts; const uint32_t* inmeta; void* out; uint32_t* out_meta;
+  uint32_t ring_mask;
+  RingCtl* ctl; uint32_t* flags; RingDevState* st; uint32_t* svc;
+  unsigned long long deadline_ticks;
+};
+hipError_t launch_ring(const RingLaunch& r, const LaunchCfg& cfg, int wgs_per_cu, bool coop, hipStream_t s);
+
+}  // namespace nfdp

@@ -1,0 +1,441 @@
+// ring.hip — persistent ring kernel + host engine (see ring.h for the protocol).
+#include "ring.h"
+
+#include <immintrin.h>
+
+#include <chrono>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <thread>
+
+#include "device.h"
+
+namespace nfdp {
+
+constexpr int kRingBlock = 256;            // 4 independent waves per workgroup
+constexpr int kRingWaves = kRingBlock / 64;
+
+struct RingArgs {
+  TablesView t;
+  const uint4* pkts; const uint32_t* inmeta; uint4* out; uint32_t* out_meta;
+  uint32_t ring_mask;
+  RingCtl* ctl; uint32_t* flags; RingDevState* st; uint32_t* svc;
+  unsigned long long* flow_ctr; unsigned long long* port_ctr; unsigned long long* drop_ctr;
+  const v4i* acl_wfrag; const v4i* acl_cinit; uint32_t acl_tiles;
+  const v4i* toep_frag; const uint32_t* toep_tab;
+  unsigned long long deadline;
+  uint32_t flags_bits;  // bit2: no per-flow counts; bits 3/4: diagnostics (kRingNo*)
+};
+// Diagnostic knobs (cost attribution only): skip the per-chunk acquire / system release fence.
+// Without the release fence an off-GPU consumer may see a chunk's flag before its frames.
+constexpr uint32_t kRingNoAcquire = 1u << 3;
+constexpr uint32_t kRingNoRelease = 1u << 4;
+// Phase trace: drain the memory counters at each stage boundary and stamp it (svc[chunk][0..6];
+// [7] is always the chunk's total service time).  Serialises the stages — attribution only.
+constexpr uint32_t kRingTrace = 1u << 5;
+constexpr int kSvcWords = 8;
+
+struct RingLds { size_t acl_w, acl_c, toep_f, toep_t, kx, tports, tchain, tperm, total; };
+__host__ __device__ inline RingLds ring_lds(int hash_mode, int acl_mode, uint32_t acl_tiles) {
+  RingLds L;
+  size_t o = 0;
+  L.acl_w = o; if (acl_mode == kAclMfma) o += (size_t)acl_tiles * 2 * 64 * 16;
+  L.acl_c = o; if (acl_mode == kAclMfma) o += (size_t)acl_tiles * 4 * 16;
+  L.toep_f = o; if (hash_mode == kHashMfma) o += 2 * 2 * 64 * 16;
+  L.toep_t = o; if (hash_mode == kHashLds) o += 16 * 256 * 4;
+  L.kx = o; o += kRingWaves * 64 * 16;
+  L.tports = o; o += kLdsPorts * sizeof(PortEntry);
+  L.tchain = o; o += kLdsChains * 8;
+  L.tperm = o; o += 1024;
+  L.total = (o + 15) & ~(size_t)15;
+  return L;
+}
+
+__device__ __forceinline__ unsigned long long rfl64(unsigned long long v) {
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+  return ((unsigned long long)hi << 32) | lo;
+}
+
+// Claim the next chunk ticket and wait until it is published.  Returns false when the wave must
+// exit (stop seen with nothing left for this ticket, or the device deadline passed).
+//
+// Polling uses RELAXED loads (scope bits only: they bypass the non-coherent caches without the
+// cache invalidate an acquire load carries — polling waves must not flush the L2 that holds the
+// flow table); the caller fences once the chunk is seen.  Waves far from the frontier back off
+// (s_sleep grows with the distance in chunks), so ~1K waiting waves do not turn the prod mirror
+// into a hot spot that slows the waves doing work.
+__device__ __forceinline__ bool ring_wait_chunk(const RingArgs& a, uint32_t lane, unsigned long long t_begin,
+                                                uint32_t& tk_out) {
+  uint32_t tk = 0;
+  if (lane == 0) tk = atomicAdd(&a.st->claim, 1u);
+  tk = __builtin_amdgcn_readfirstlane(tk);
+  tk_out = tk;
+  const unsigned long long first = (unsigned long long)tk * 64ull;
+  const unsigned long long need = first + 64ull;
+  for (;;) {
+    unsigned long long v = 0;
+    if (lane == 0) {
+      v = __hip_atomic_load(&a.st->dprod, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if ((v & ~kRingStop) < need && v == first) {
+        // frontier wave (its chunk is the first unpublished one): the only PCIe poller
+        const unsigned long long hv = __hip_atomic_load(&a.ctl->prod, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (hv > v) {
+          __hip_atomic_fetch_max(&a.st->dprod, hv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          v = hv;
+        }
+      }
+    }
+    v = rfl64(v);
+    const unsigned long long avail = v & ~kRingStop;
+    if (avail >= need) return true;
+    if (v & kRingStop) return false;  // stop and final count come in one word: nothing more will arrive
+    if (__builtin_amdgcn_s_memrealtime() - t_begin > a.deadline) return false;
+    const unsigned long long dist = (first - avail) >> 6;  // chunks ahead of the frontier
+    if (dist == 0) __builtin_amdgcn_s_sleep(1);
+    else if (dist < 8) __builtin_amdgcn_s_sleep(4);
+    else if (dist < 64) __builtin_amdgcn_s_sleep(32);
+    else __builtin_amdgcn_s_sleep(127);
+  }
+}
+
+// COOP = false: the 4 waves of a workgroup claim and process chunks independently (throughput).
+// COOP = true (latency): the workgroup processes ONE chunk at a time — wave 0 claims and polls,
+// all 4 waves parse the chunk and each scans a quarter of the ACL rule tiles on its own SIMD
+// (the single-wave MFMA chain is the longest stage of a chunk), wave 0 combines the partial
+// first-match minima through LDS and finishes the chunk.
+template <int HASH, int ACL, bool COOP>
+__global__ __launch_bounds__(kRingBlock) void ring_kernel(RingArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  __shared__ uint32_t coop_ctl[2];                            // ticket, go
+  __shared__ uint32_t coop_best[COOP ? kRingWaves : 1][64];   // per-wave ACL partial minima
+  const RingLds L = ring_lds(HASH, ACL, a.acl_tiles);
+  v4i* lw = reinterpret_cast<v4i*>(smem + L.acl_w);
+  v4i* lc = reinterpret_cast<v4i*>(smem + L.acl_c);
+  v4i* lt = reinterpret_cast<v4i*>(smem + L.toep_f);
+  uint32_t* ltab = reinterpret_cast<uint32_t*>(smem + L.toep_t);
+  if constexpr (ACL == kAclMfma) {
+    const uint32_t nw = a.acl_tiles * 2 * 64, nc = a.acl_tiles * 4;
+    for (uint32_t i = threadIdx.x; i < nw; i += kRingBlock) lw[i] = a.acl_wfrag[i];
+    for (uint32_t i = threadIdx.x; i < nc; i += kRingBlock) lc[i] = a.acl_cinit[i];
+  }
+  if constexpr (HASH == kHashMfma)
+    for (uint32_t i = threadIdx.x; i < 256; i += kRingBlock) lt[i] = a.toep_frag[i];
+  if constexpr (HASH == kHashLds)
+    for (uint32_t i = threadIdx.x; i < 4096; i += kRingBlock) ltab[i] = a.toep_tab[i];
+  // ports / chain words / ACL verdicts in LDS: the per-packet path's only global loads are the
+  // frame and the flow bucket (a session never sees a table change: commit relaunches the grid)
+  const LdsTables ta = stage_lds_tables(a.t, reinterpret_cast<PortEntry*>(smem + L.tports),
+                                        reinterpret_cast<uint64_t*>(smem + L.tchain), smem + L.tperm, true, kRingBlock);
+  __syncthreads();
+
+  const uint32_t wave = threadIdx.x >> 6;
+  uint4* kx = reinterpret_cast<uint4*>(smem + L.kx) + wave * 64;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t nch_mask = a.ring_mask >> 6;  // R/64 - 1
+  const unsigned long long t_begin = __builtin_amdgcn_s_memrealtime();
+
+  for (;;) {
+    uint32_t tk = 0;
+    if constexpr (COOP) {
+      if (wave == 0) {
+        const bool go = ring_wait_chunk(a, lane, t_begin, tk);
+        if (lane == 0) { coop_ctl[0] = tk; coop_ctl[1] = go ? 1u : 0u; }
+      }
+      __syncthreads();
+      tk = __builtin_amdgcn_readfirstlane(coop_ctl[0]);
+      if (!__builtin_amdgcn_readfirstlane(coop_ctl[1])) break;
+    } else {
+      if (!ring_wait_chunk(a, lane, t_begin, tk)) break;
+    }
+    if (!(a.flags_bits & kRingNoAcquire))
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the chunk's frames are published data
+    const unsigned long long t_avail = __builtin_amdgcn_s_memrealtime();
+    const bool trace = (a.flags_bits & kRingTrace) != 0 && wave == 0;
+    uint32_t tr0 = 0, tr1 = 0, tr2 = 0, tr3 = 0, tr4 = 0, tr5 = 0;
+#define NFDP_RING_MARK(var)                                                 \
+  if (trace) {                                                              \
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");             \
+    var = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_avail);          \
+  }
+
+    // ---- one packet per lane: the fused kernel's stages ----
+    const uint32_t i = (tk * 64u + lane) & a.ring_mask;
+    uint32_t d[kSlotDwords];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint4 v = a.pkts[(size_t)i * 4 + q];
+      d[4 * q] = v.x; d[4 * q + 1] = v.y; d[4 * q + 2] = v.z; d[4 * q + 3] = v.w;
+    }
+    const uint32_t im = a.inmeta[i];
+    NFDP_RING_MARK(tr0)
+    Parsed p;
+    IngressState st;
+    ingress_stage(a.t, ta, d, im, p, st);
+    uint32_t hash = 0;
+    int acl_rule = -1;
+    if constexpr (COOP && ACL == kAclMfma) {
+      uint32_t b = 0xFFFFFFFFu;
+      classify_wave<HASH, ACL>(st.key, kx, lw, lc, a.acl_tiles, lt, ltab, a.t, hash, acl_rule, wave, kRingWaves, &b);
+      coop_best[wave][lane] = b;
+      __syncthreads();
+      if (wave != 0) continue;  // helpers go back to wait for the next chunk
+      b = min(min(coop_best[0][lane], coop_best[1][lane]), min(coop_best[2][lane], coop_best[3][lane]));
+      acl_rule = (b >> 10) == 0 ? (int)(b & 1023u) : -1;
+      if (acl_rule >= (int)a.t.n_acl) acl_rule = -1;
+    } else {
+      if (COOP && wave != 0) continue;  // nothing to share without the MFMA ACL
+      classify_wave<HASH, ACL>(st.key, kx, lw, lc, a.acl_tiles, lt, ltab, a.t, hash, acl_rule);
+    }
+    NFDP_RING_MARK(tr1)
+    bool hit = false;
+    FlowAction act = {};
+    int64_t slot = -1;
+    if (!st.reason && p.ipv4) {
+      uint4 v;
+      slot = flow_probe(a.t, st.key, hash, v);
+      if (slot >= 0) {
+        hit = true;
+        act.chain_id = v.x & 0xFFFFu; act.out_port = v.x >> 16; act.nat_ip = v.y;
+        act.nat_port = v.z & 0xFFFFu; act.vlan = v.z >> 16; act.flow_id = v.w;
+      }
+    }
+    NFDP_RING_MARK(tr2)
+    const EgressDecision e = chain_stage(a.t, ta, p, st, hit, act, acl_rule, hash);
+    const uint32_t olen = e.reason ? 0u : p.len + (e.push ? 4u : 0u);
+    uint32_t o[kSlotDwords];
+    emit(p, e.tci, e.push != 0, o);
+    uint4* dst = a.out + (size_t)i * 4;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) dst[q] = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
+    a.out_meta[i] = make_meta(e.out_port, olen, e.reason, e.mirror != 0);
+    NFDP_RING_MARK(tr3)
+
+    // ---- completion: the chunk's frames are visible before its flag ----
+    if (!(a.flags_bits & kRingNoRelease)) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    else __builtin_amdgcn_s_waitcnt(0);  // diagnostic: order only this wave's stores (no L2 writeback)
+    NFDP_RING_MARK(tr4)
+    if (lane == 0) {
+      if (a.svc) a.svc[(size_t)(tk & nch_mask) * kSvcWords + 7] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_avail);
+      __hip_atomic_store(&a.flags[tk & nch_mask], tk + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+
+    // ---- counters, off the latency path (after the flag): per-port / per-reason words are
+    // shared by the whole chunk -> wave-aggregated; per-flow words are (nearly) distinct per
+    // packet -> one atomic each.  They complete before the grid exits (harvest reads after stop).
+    wave_counter_add(a.port_ctr, 2 * st.in_port, st.wire_len, true, st.in_port < (uint32_t)kMaxPorts);
+    wave_counter_add(a.drop_ctr, e.reason & (kNumReasons - 1), 1u, false, e.reason != 0);
+    wave_counter_add(a.port_ctr, 2 * e.out_port + 1, olen, true, e.reason == 0);
+    if (hit && a.flow_ctr && !(a.flags_bits & 4u)) atomicAdd(a.flow_ctr + slot, ctr_inc(st.wire_len));
+    NFDP_RING_MARK(tr5)
+#undef NFDP_RING_MARK
+    if (trace && lane == 0 && a.svc) {
+      uint32_t* sv = a.svc + (size_t)(tk & nch_mask) * kSvcWords;
+      sv[0] = tr0; sv[1] = tr1; sv[2] = tr2; sv[3] = tr3; sv[4] = tr4; sv[5] = tr5; sv[6] = 0;
+    }
+  }
+}
+
+template <int H, int A, bool C>
+static hipError_t launch_ring_t(const RingArgs& a, int num_cus, int wgs, hipStream_t s) {
+  const size_t lds = ring_lds(H, A, a.acl_tiles).total;
+  if (lds > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&ring_kernel<H, A, C>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  if ((lds + 2048) * (size_t)wgs > 160 * 1024) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((ring_kernel<H, A, C>), dim3((uint32_t)(num_cus * wgs)), dim3(kRingBlock), lds, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_ring(const RingLaunch& r, const LaunchCfg& cfg, int wgs_per_cu, bool coop, hipStream_t s) {
+  RingArgs a;
+  a.t = r.f.t;
+  a.pkts = reinterpret_cast<const uint4*>(r.pkts);
+  a.inmeta = r.inmeta;
+  a.out = reinterpret_cast<uint4*>(r.out);
+  a.out_meta = r.out_meta;
+  a.ring_mask = r.ring_mask;
+  a.ctl = r.ctl; a.flags = r.flags; a.st = r.st; a.svc = r.svc;
+  a.flow_ctr = r.f.flow_ctr; a.port_ctr = r.f.port_ctr; a.drop_ctr = r.f.drop_ctr;
+  a.acl_wfrag = reinterpret_cast<const v4i*>(r.f.acl_wfrag);
+  a.acl_cinit = reinterpret_cast<const v4i*>(r.f.acl_cinit);
+  a.acl_tiles = r.f.acl_tiles;
+  a.toep_frag = reinterpret_cast<const v4i*>(r.f.toep_frag);
+  a.toep_tab = r.f.toep_tab;
+  a.deadline = r.deadline_ticks;
+  a.flags_bits = r.f.flags;
+  if (!a.port_ctr || !a.drop_ctr || !a.ctl || !a.flags || !a.st) return hipErrorInvalidValue;
+  if (((r.ring_mask + 1) & r.ring_mask) != 0 || r.ring_mask < 63) return hipErrorInvalidValue;
+  if (cfg.acl_mode == kAclMfma && (a.acl_tiles == 0 || a.acl_tiles > 64 || !a.acl_wfrag || !a.acl_cinit))
+    return hipErrorInvalidValue;
+  if (cfg.hash_mode == kHashMfma && !a.toep_frag) return hipErrorInvalidValue;
+  if (cfg.hash_mode == kHashLds && !a.toep_tab) return hipErrorInvalidValue;
+  if (wgs_per_cu < 1 || wgs_per_cu > 8 || cfg.num_cus < 1) return hipErrorInvalidValue;
+  const int h = cfg.hash_mode, ac = cfg.acl_mode;
+#define NFDP_RCASE(HH, AA)                                                                   \
+  if (h == HH && ac == AA)                                                                   \
+    return coop ? launch_ring_t<HH, AA, true>(a, cfg.num_cus, wgs_per_cu, s)                 \
+                : launch_ring_t<HH, AA, false>(a, cfg.num_cus, wgs_per_cu, s);
+  NFDP_RCASE(0, 0) NFDP_RCASE(0, 1) NFDP_RCASE(0, 2)
+  NFDP_RCASE(1, 0) NFDP_RCASE(1, 1) NFDP_RCASE(1, 2)
+  NFDP_RCASE(2, 0) NFDP_RCASE(2, 1) NFDP_RCASE(2, 2)
+#undef NFDP_RCASE
+  return hipErrorInvalidValue;
+}
+
+// ------------------------------------------------------------------------------------------
+// Host engine
+// ------------------------------------------------------------------------------------------
+namespace {
+void ck(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string("ring: ") + what + ": " + hipGetErrorString(e));
+}
+using Clock = std::chrono::steady_clock;
+inline double secs(Clock::time_point a, Clock::time_point b) { return std::chrono::duration<double>(b - a).count(); }
+}  // namespace
+
+RingEngine::RingEngine(uint32_t capacity, int num_cus, int wgs_per_cu, bool coop)
+    : cap_(capacity), nch_(capacity / 64), num_cus_(num_cus), wgs_(wgs_per_cu), coop_(coop) {
+  if (capacity < 64 || (capacity & (capacity - 1)) || capacity > (1u << 24))
+    throw std::invalid_argument("ring: capacity must be a power of two in [64, 2^24]");
+  if (num_cus < 1 || wgs_per_cu < 1 || wgs_per_cu > 8) throw std::invalid_argument("ring: bad grid");
+  // control line + completion flags: pinned, coherent (the GPU polls / writes them over PCIe)
+  ck(hipHostMalloc(reinterpret_cast<void**>(&ctl_), sizeof(RingCtl), hipHostMallocCoherent | hipHostMallocMapped),
+     "host alloc ctl");
+  ck(hipHostMalloc(reinterpret_cast<void**>(&flags_), (size_t)nch_ * 4, hipHostMallocCoherent | hipHostMallocMapped),
+     "host alloc flags");
+  std::memset(ctl_, 0, sizeof(RingCtl));
+  std::memset(flags_, 0, (size_t)nch_ * 4);
+  ck(hipMalloc(reinterpret_cast<void**>(&st_), sizeof(RingDevState)), "dev alloc state");
+  ck(hipMalloc(reinterpret_cast<void**>(&d_in_), (size_t)capacity * 64), "dev alloc in");
+  ck(hipMalloc(reinterpret_cast<void**>(&d_im_), (size_t)capacity * 4), "dev alloc inmeta");
+  ck(hipMalloc(reinterpret_cast<void**>(&d_out_), (size_t)capacity * 64), "dev alloc out");
+  ck(hipMalloc(reinterpret_cast<void**>(&d_meta_), (size_t)capacity * 4), "dev alloc meta");
+  ck(hipMalloc(reinterpret_cast<void**>(&d_svc_), (size_t)nch_ * 4 * kSvcWords), "dev alloc svc");
+  ck(hipMemset(d_in_, 0, (size_t)capacity * 64), "memset");
+  ck(hipMemset(d_im_, 0, (size_t)capacity * 4), "memset");
+  ck(hipMemset(d_svc_, 0, (size_t)nch_ * 4 * kSvcWords), "memset");
+  ck(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "stream");
+}
+
+RingEngine::~RingEngine() {
+  try {
+    if (running_) stop(60.0);
+  } catch (...) {
+  }
+  (void)hipStreamSynchronize(stream_);
+  (void)hipStreamDestroy(stream_);
+  for (void* d : {(void*)st_, (void*)d_in_, (void*)d_im_, (void*)d_out_, (void*)d_meta_, (void*)d_svc_}) (void)hipFree(d);
+  (void)hipHostFree(ctl_);
+  (void)hipHostFree(flags_);
+}
+
+void RingEngine::start(const FusedLaunch& f, const LaunchCfg& cfg, double deadline_s) {
+  if (running_) throw std::runtime_error("ring: already running");
+  if (!(deadline_s > 0.0) || deadline_s > 3600.0) throw std::invalid_argument("ring: deadline in (0, 3600] s");
+  if (completed() != prod_) throw std::runtime_error("ring: previous session left chunks unprocessed");
+  // resume at the published position: tickets restart at prod/64, nothing outstanding
+  RingDevState s{};
+  s.claim = (uint32_t)(prod_ / 64);
+  s.dprod = prod_;
+  __atomic_store_n(&ctl_->prod, prod_, __ATOMIC_RELEASE);
+  ck(hipMemcpyAsync(st_, &s, sizeof(s), hipMemcpyHostToDevice, stream_), "state upload");
+  ck(hipStreamSynchronize(stream_), "state upload");  // `s` lives on this stack frame
+  RingLaunch r;
+  r.f = f;
+  r.pkts = d_in_; r.inmeta = d_im_; r.out = d_out_; r.out_meta = d_meta_;
+  r.ring_mask = cap_ - 1;
+  void* dctl = nullptr;
+  void* dflags = nullptr;
+  ck(hipHostGetDevicePointer(&dctl, ctl_, 0), "device ptr ctl");
+  ck(hipHostGetDevicePointer(&dflags, flags_, 0), "device ptr flags");
+  r.ctl = reinterpret_cast<RingCtl*>(dctl);
+  r.flags = reinterpret_cast<uint32_t*>(dflags);
+  r.st = st_;
+  r.svc = d_svc_;
+  r.deadline_ticks = (unsigned long long)(deadline_s * 1e8);  // s_memrealtime: 100 MHz
+  ck(launch_ring(r, cfg, wgs_, coop_, stream_), "launch");
+  running_ = true;
+}
+
+void RingEngine::stop(double timeout_s) {
+  if (!running_) return;
+  __atomic_store_n(&ctl_->prod, prod_ | kRingStop, __ATOMIC_RELEASE);
+  const auto t0 = Clock::now();
+  for (;;) {
+    const hipError_t q = hipStreamQuery(stream_);
+    if (q == hipSuccess) break;
+    if (q != hipErrorNotReady) { running_ = false; ck(q, "kernel"); }
+    if (secs(t0, Clock::now()) > timeout_s) throw std::runtime_error("ring: kernel did not drain before the timeout");
+    std::this_thread::sleep_for(std::chrono::microseconds(50));
+  }
+  running_ = false;
+  (void)completed();
+  if (floor_ * 64 != prod_) throw std::runtime_error("ring: stopped with published chunks unprocessed");
+}
+
+bool RingEngine::chunk_done(uint64_t chunk) const {
+  return __atomic_load_n(&flags_[chunk & (nch_ - 1)], __ATOMIC_ACQUIRE) == (uint32_t)(chunk + 1);
+}
+
+uint64_t RingEngine::completed() {
+  const uint64_t end = prod_ / 64;
+  while (floor_ < end && chunk_done(floor_)) ++floor_;
+  return floor_ * 64;
+}
+
+uint64_t RingEngine::publish(uint32_t n) {
+  if (!running_) throw std::runtime_error("ring: not running");
+  if (n == 0 || (n & 63u)) throw std::invalid_argument("ring: publish a positive multiple of 64 packets");
+  if (prod_ + n - completed() > cap_) throw std::runtime_error("ring: no room (wait for completions)");
+  prod_ += n;
+  __atomic_store_n(&ctl_->prod, prod_, __ATOMIC_RELEASE);
+  return prod_;
+}
+
+bool RingEngine::wait(uint64_t end, double timeout_s) {
+  if (end > prod_) throw std::invalid_argument("ring: waiting for unpublished packets");
+  const auto t0 = Clock::now();
+  uint32_t spin = 0;
+  while (completed() < end) {
+    _mm_pause();
+    if ((++spin & 1023u) == 0 && secs(t0, Clock::now()) > timeout_s) return false;
+  }
+  return true;
+}
+
+std::vector<double> RingEngine::probe(uint32_t batches, uint32_t batch, uint32_t inflight, double* elapsed_s) {
+  if (!running_) throw std::runtime_error("ring: not running");
+  if (batch == 0 || (batch & 63u) || inflight == 0 || (uint64_t)batch * inflight > cap_)
+    throw std::invalid_argument("ring: probe needs batch % 64 == 0 and batch * inflight <= capacity");
+  std::vector<double> lat;
+  lat.reserve(batches);
+  std::vector<Clock::time_point> t_pub(inflight);
+  std::vector<uint64_t> end(inflight);
+  uint32_t issued = 0, done = 0;
+  const auto t_start = Clock::now();
+  while (done < batches) {
+    while (issued < batches && issued - done < inflight) {
+      const uint32_t k = issued % inflight;
+      t_pub[k] = Clock::now();
+      end[k] = publish(batch);
+      ++issued;
+    }
+    const uint32_t k = done % inflight;  // batches complete in publication order (floor scan)
+    uint32_t spin = 0;
+    while (completed() < end[k]) {
+      _mm_pause();
+      if ((++spin & 0xFFFFu) == 0 && secs(t_start, Clock::now()) > 60.0)
+        throw std::runtime_error("ring: probe timed out waiting for completions");
+    }
+    lat.push_back(std::chrono::duration<double, std::micro>(Clock::now() - t_pub[k]).count());
+    ++done;
+  }
+  if (elapsed_s) *elapsed_s = secs(t_start, Clock::now());
+  return lat;
+}
+
+}  // namespace nfdp

@@ -128,8 +128,18 @@ class DataPlane:
     def commit(self, full: bool = False) -> dict:
         """Push host table changes to the device.  Returns what was sent."""
         FAULTS.check("dataplane.commit")
+        # resident ring kernels (dataplane/ring.py) staged the old tables: drain and stop them
+        # before any buffer is replaced, relaunch them over the new version afterwards
+        rings = [r for r in getattr(self, "_rings", []) if r.running]
+        for r in rings:
+            r.stop()
         with TRACER.span("dataplane.commit", full=full):
-            return self._commit(full)
+            sent = self._commit(full)
+        if rings:
+            _torch().cuda.current_stream(self.tdev).synchronize()
+            for r in rings:
+                r.resume()
+        return sent
 
     def _commit(self, full: bool) -> dict:
         sent = {}

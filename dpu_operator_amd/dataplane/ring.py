@@ -1,0 +1,151 @@
+"""Low-latency data path: a persistent HIP kernel polling an ingress ring (csrc/nfdp/ring.hip).
+
+The batch engine (`DataPlane.run`) launches one kernel per batch, so a packet's latency includes
+the launch and the wait for the whole batch.  `RingPath` keeps a kernel resident on the CUs:
+64-packet chunks are processed as soon as the producer publishes them, and completion flags come
+back through pinned host memory, so a pod-to-pod hop costs a few µs instead of a launch.  This is
+the GPU form of the always-on datapath the reference configures but never runs itself (the
+Intel FXP / OvS-DPDK PMD loop, and the Octeon agent's 1 ms poll loop,
+octep_cp_agent/main.c:307-311).
+
+Usage::
+
+    ring = RingPath(dp, capacity=1 << 16)
+    ring.stage(frames, inmeta)          # fill ring slots (a NIC would DMA into them)
+    ring.start()
+    end = ring.publish(4096)            # hand 4096 packets to the resident kernel
+    ring.wait(end)
+    lat_us, elapsed = ring.probe(batches=2000, batch=64, inflight=1)
+    ring.stop()                         # drains every published chunk, then the grid exits
+    out, meta = ring.results()
+
+While a ring runs, do NOT synchronize the whole device (torch.cuda.synchronize(), a blocking
+copy on the default stream): that waits for the resident kernel.  `DataPlane.commit()` restarts
+active rings itself so a table update never races a running session.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .engine import DataPlane
+
+
+class RingPath:
+    def __init__(self, dp: DataPlane, capacity: int = 1 << 16, wgs_per_cu: int = 1, deadline_s: float = 120.0,
+                 knobs: int = 0, coop: bool = True):
+        """coop=True: a workgroup's 4 waves share each chunk (ACL rule tiles split 4 ways) —
+        lowest latency.  coop=False: every wave takes its own chunks — highest throughput."""
+        if not dp.gpu:
+            raise RuntimeError("RingPath needs a GPU data plane")
+        if capacity < 64 or capacity & (capacity - 1):
+            raise ValueError("capacity must be a power of two >= 64")
+        self.dp = dp
+        self.capacity = int(capacity)
+        self.deadline_s = float(deadline_s)
+        self.knobs = int(knobs) & 0x38  # diagnostic knobs (ring.hip kRingNo*/kRingTrace), cost attribution only
+        self.coop = bool(coop)
+        self.eng = dp.nf.RingEngine(self.capacity, int(dp.num_cus), int(wgs_per_cu), self.coop)
+        self._staged = 0
+        rings = getattr(dp, "_rings", None)
+        if rings is None:
+            dp._rings = rings = []
+        rings.append(self)
+
+    # ------------------------------------------------------------------ staging
+    def stage(self, frames, inmeta) -> int:
+        """Copy frames into the ring slots, repeated cyclically to fill all of them (a replayed
+        trace).  Must be called while the ring is stopped."""
+        if self.eng.running:
+            raise RuntimeError("stage() while the ring runs")
+        torch = _torch()
+        f = frames if isinstance(frames, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(frames))
+        m = inmeta if isinstance(inmeta, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(inmeta).view(np.int32))
+        f = f.to(self.dp.tdev).reshape(-1, 64).contiguous()
+        m = m.to(self.dp.tdev).view(torch.int32).reshape(-1).contiguous()
+        n = int(f.shape[0])
+        if n == 0 or m.numel() != n:
+            raise ValueError("frames / inmeta size mismatch")
+        reps = (self.capacity + n - 1) // n
+        f = f.repeat(reps, 1)[: self.capacity].contiguous()
+        m = m.repeat(reps)[: self.capacity].contiguous()
+        torch.cuda.current_stream(self.dp.tdev).synchronize()
+        nf = self.dp.nf
+        nf.memcpy(self.eng.dev_in(), f.data_ptr(), self.capacity * 64)
+        nf.memcpy(self.eng.dev_inmeta(), m.data_ptr(), self.capacity * 4)
+        self._staged = n
+        return n
+
+    # ------------------------------------------------------------------ session
+    def _args(self) -> dict:
+        dp = self.dp
+        return {"flow_ctr": dp._ptr("flow_ctr"), "port_ctr": dp._ptr("port_ctr"), "drop_ctr": dp._ptr("drop_ctr"),
+                "acl_wfrag": dp._ptr("acl_wfrag"), "acl_cinit": dp._ptr("acl_cinit"), "acl_tiles": dp._acl_tiles,
+                "toep_frag": dp._ptr("toep_frag"), "toep_tab": dp._ptr("toep_tab"),
+                "flags": (0 if dp.count_flows else 4) | self.knobs}
+
+    @property
+    def running(self) -> bool:
+        return bool(self.eng.running)
+
+    def start(self) -> None:
+        self.dp.commit()
+        _torch().cuda.current_stream(self.dp.tdev).synchronize()  # tables are in HBM before launch
+        self.eng.start(self.dp.tables_ptrs(), self._args(), self.dp.hash_mode, self.dp.acl_mode,
+                       int(self.dp.num_cus), self.deadline_s)
+
+    def stop(self, timeout_s: float = 30.0) -> None:
+        self.eng.stop(timeout_s)
+
+    def resume(self) -> None:
+        """Relaunch over the current device tables (DataPlane.commit stops, updates, resumes)."""
+        self.eng.start(self.dp.tables_ptrs(), self._args(), self.dp.hash_mode, self.dp.acl_mode,
+                       int(self.dp.num_cus), self.deadline_s)
+
+    def publish(self, n: int) -> int:
+        return int(self.eng.publish(int(n)))
+
+    def completed(self) -> int:
+        return int(self.eng.completed())
+
+    def wait(self, end: int, timeout_s: float = 10.0) -> None:
+        if not self.eng.wait(int(end), float(timeout_s)):
+            raise TimeoutError(f"ring: packets below {end} not completed within {timeout_s} s")
+
+    def probe(self, batches: int, batch: int = 64, inflight: int = 1) -> tuple[np.ndarray, float]:
+        """Closed-loop publish -> completion latencies (µs, host clock) and total elapsed seconds."""
+        lat, el = self.eng.probe(int(batches), int(batch), int(inflight))
+        return np.asarray(lat), float(el)
+
+    # ------------------------------------------------------------------ results
+    def results(self) -> tuple[np.ndarray, np.ndarray]:
+        """Egress slots and metadata of the whole ring (read after stop())."""
+        if self.eng.running:
+            raise RuntimeError("results() while the ring runs (stop it first)")
+        out = np.empty((self.capacity, 64), np.uint8)
+        meta = np.empty(self.capacity, np.uint32)
+        self.dp.nf.memcpy(out.ctypes.data, self.eng.dev_out(), out.nbytes)
+        self.dp.nf.memcpy(meta.ctypes.data, self.eng.dev_meta(), meta.nbytes)
+        return out, meta
+
+    def service_ticks(self, phases: bool = False) -> np.ndarray:
+        """Per-chunk device service time (chunk visible -> flag written), 10 ns ticks.  With
+        phases=True: [chunks, 8] stage stamps (filled when the ring runs with the trace knob)."""
+        if self.eng.running:
+            raise RuntimeError("service_ticks() while the ring runs")
+        t = np.empty((self.capacity // 64, 8), np.uint32)
+        self.dp.nf.memcpy(t.ctypes.data, self.eng.dev_svc(), t.nbytes)
+        return t if phases else t[:, 7].copy()
+
+    def close(self) -> None:
+        if self.eng.running:
+            self.eng.stop(30.0)
+        rings = getattr(self.dp, "_rings", [])
+        if self in rings:
+            rings.remove(self)
+
+
+def _torch():
+    import torch
+
+    return torch
+

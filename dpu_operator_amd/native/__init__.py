@@ -22,6 +22,13 @@ def _load(name: str, autobuild: bool = True):
         return _cache[name]
     if str(_HERE) not in sys.path:
         sys.path.insert(0, str(_HERE))
+    # torch first: it loads its ROCm runtime libraries into the global symbol scope, and the
+    # extension's HIP runtime must bind to that same HSA runtime.  Loaded the other way round the
+    # process ends up with two HSA runtimes and the extension's sees no device.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     try:
         mod = importlib.import_module(name)
     except ImportError:

@@ -40,7 +40,7 @@ def _includes() -> list[str]:
 MODULES = {
     "_nfdp": {
         "dir": CSRC / "nfdp",
-        "sources": ["kernels.hip", "shard.hip", "pktio.hip", "host.cpp", "shard_cpu.cpp", "bindings.cpp"],
+        "sources": ["kernels.hip", "shard.hip", "pktio.hip", "ring.hip", "host.cpp", "shard_cpu.cpp", "bindings.cpp"],
         "hip": True,
     },
     "_agent": {
