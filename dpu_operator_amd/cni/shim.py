@@ -5,8 +5,8 @@ CNI environment + stdin into a Request, POSTs it to the daemon's CNI server over
 and prints the daemon's Result converted to the requested cniVersion.  DEL ignores the result,
 CHECK is a no-op, VERSION prints the supported versions.
 
-Run as ``python -m dpu_operator_amd.cni.shim`` (the daemon installs a launcher script at
-/var/lib/cni/bin/dpu-cni, see daemon.prepare_cni()).
+Run as ``python -m dpu_operator_amd.cni.shim``.  What the daemon installs on the host is the static
+native twin of this module, csrc/cni/dpu_cni.cpp (kubelet execs it outside any container).
 """
 from __future__ import annotations
 

@@ -57,6 +57,13 @@ EXES = {
         "module": "_agent",
         "sources": ["mbox.cpp", "ctrl_net.cpp", "config.cpp", "agent.cpp", "plugin_server.cpp", "soc.cpp", "agent_main.cpp"],
     },
+    # The CNI plugin kubelet execs on the host: static, no Python / package needed there.
+    "dpu-cni": {
+        "dir": CSRC / "cni",
+        "module": "_cni",
+        "sources": ["dpu_cni.cpp"],
+        "ldflags": ["-static"],
+    },
 }
 
 
@@ -130,7 +137,7 @@ def build_exe(name: str, force: bool = False, verbose: bool = False) -> Path:
     out = HERE / "bin" / name
     out.parent.mkdir(exist_ok=True)
     if force or jobs or not out.exists() or out.stat().st_mtime < max(o.stat().st_mtime for o in objs):
-        cmd = [shutil.which("g++") or "g++", "-pthread", *map(str, objs), "-o", str(out)]
+        cmd = [shutil.which("g++") or "g++", "-pthread", *map(str, objs), *spec.get("ldflags", []), "-o", str(out)]
         if verbose:
             print(" ".join(cmd), flush=True)
         r = subprocess.run(cmd, capture_output=True, text=True)

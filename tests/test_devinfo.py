@@ -73,9 +73,9 @@ def test_agent_binary_lists_gpus(sysfs):
     import json
     import subprocess
 
-    from dpu_operator_amd.native.build import HERE
+    from dpu_operator_amd.native.build import build_exe
 
-    out = subprocess.run([str(HERE / "bin" / "dpu-cp-agent"), "--list-gpus", sysfs], capture_output=True, text=True,
+    out = subprocess.run([str(build_exe("dpu-cp-agent")), "--list-gpus", sysfs], capture_output=True, text=True,
                          timeout=30, check=True).stdout.splitlines()
     gpus = [json.loads(x) for x in out]
     assert [g["model"] for g in gpus] == ["MI355X", "MI355X"] and gpus[0]["cus"] == 256 and gpus[1]["pci"] == "0000:07:00.0"
