@@ -9,10 +9,11 @@
 //        iff its mismatch count is 0; first match by min((mismatch << 10) | rule)
 //    (v_mfma_i32_16x16x64_i8; rules/hash bits are the M rows, 16 packets the N columns), with
 //    the rule fragments staged once per workgroup in LDS;
-//  * exact-match flow lookup: 16-B tag row per bucket (8 x u16), 2 choices, then one 16-B key
-//    compare and one 16-B action load (tables sized for HBM: 1M flows = 68 MB, 288 GB ok);
+//  * exact-match flow lookup: 2-choice cuckoo, a bucket = 4 x {16-B key, 16-B action} = one
+//    128-B line, so a hit in the first bucket is ONE dependent fetch (1M flows = 64 MB of HBM);
 //  * per-port counters aggregated in LDS, flushed once per workgroup; per-flow counters are one
 //    packed 64-bit atomic per packet.
+// The persistent low-latency variant of the same stages lives in ring.hip.
 #include "device.h"
 #include "shard.h"
 
