@@ -25,18 +25,42 @@ struct RingArgs {
   const v4i* acl_wfrag; const v4i* acl_cinit; uint32_t acl_tiles;
   const v4i* toep_frag; const uint32_t* toep_tab;
   unsigned long long deadline;
-  uint32_t flags_bits;  // bit2: no per-flow counts; bits 3/4: diagnostics (kRingNo*)
+  uint32_t flags_bits;  // bit2: no per-flow counts; bits 5/6: diagnostics (kRingTrace, kRingNoCounters)
 };
-// Diagnostic knobs (cost attribution only): skip the per-chunk acquire / system release fence.
-// Without the release fence an off-GPU consumer may see a chunk's flag before its frames.
-constexpr uint32_t kRingNoAcquire = 1u << 3;
-constexpr uint32_t kRingNoRelease = 1u << 4;
+// Frames are read and written with system-coherent buffer ops (sc0 sc1): the loads never hit a
+// stale L2 line of a slot a producer (host / NIC DMA) rewrote, and the stores write through to
+// HBM, so completion needs only "my stores are done" (s_waitcnt) before the flag — no per-chunk
+// L2 invalidate / writeback, which serialised the ring at ~1.5 Gpps under load.
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+constexpr int kSysAux = 1 | 16;  // cache-policy bits: sc0 | sc1 (gfx940+)
+constexpr int kBufRaw = 0x00020000;
 // Phase trace: drain the memory counters at each stage boundary and stamp it (svc[chunk][0..6];
 // [7] is always the chunk's total service time).  Serialises the stages — attribution only.
 constexpr uint32_t kRingTrace = 1u << 5;
 constexpr int kSvcWords = 8;
+constexpr uint32_t kRingNoCounters = 1u << 6;  // diagnostic: skip every counter update
 
-struct RingLds { size_t acl_w, acl_c, toep_f, toep_t, kx, tports, tchain, tperm, total; };
+struct RingLds { size_t acl_w, acl_c, toep_f, toep_t, kx, tports, tchain, tperm, pc, drops, total; };
+
+// Port / drop counters of a workgroup accumulate in LDS (u32) and are moved to the global packed
+// counters by whichever wave flushes (atomic exchange: every count moves exactly once).  A wave
+// flushes when it runs out of published work and every kFlushChunks chunks; the last wave to
+// exit flushes the rest, so the totals are exact once the grid has drained.
+constexpr uint32_t kFlushChunks = 256;
+__device__ __forceinline__ void flush_lds_counters(uint32_t* pc, uint32_t* drops, unsigned long long* port_ctr,
+                                                   unsigned long long* drop_ctr) {
+  const uint32_t lane = threadIdx.x & 63u;
+  for (uint32_t q = lane; q < kLdsPorts; q += 64) {
+    const uint32_t rp = atomicExch(&pc[q], 0u), rb = atomicExch(&pc[kLdsPorts + q], 0u);
+    if (rp | rb) atomicAdd(port_ctr + 2 * q, ((unsigned long long)rp << 40) | rb);
+    const uint32_t tp = atomicExch(&pc[2 * kLdsPorts + q], 0u), tb = atomicExch(&pc[3 * kLdsPorts + q], 0u);
+    if (tp | tb) atomicAdd(port_ctr + 2 * q + 1, ((unsigned long long)tp << 40) | tb);
+  }
+  if (lane < kNumReasons) {
+    const uint32_t d = atomicExch(&drops[lane], 0u);
+    if (d) atomicAdd(drop_ctr + lane, (unsigned long long)d);
+  }
+}
 __host__ __device__ inline RingLds ring_lds(int hash_mode, int acl_mode, uint32_t acl_tiles) {
   RingLds L;
   size_t o = 0;
@@ -48,6 +72,8 @@ __host__ __device__ inline RingLds ring_lds(int hash_mode, int acl_mode, uint32_
   L.tports = o; o += kLdsPorts * sizeof(PortEntry);
   L.tchain = o; o += kLdsChains * 8;
   L.tperm = o; o += 1024;
+  L.pc = o; o += kLdsPorts * 4 * 4;     // [rx_pk, rx_by, tx_pk, tx_by][kLdsPorts] u32
+  L.drops = o; o += kNumReasons * 4;
   L.total = (o + 15) & ~(size_t)15;
   return L;
 }
@@ -63,11 +89,12 @@ __device__ __forceinline__ unsigned long long rfl64(unsigned long long v) {
 //
 // Polling uses RELAXED loads (scope bits only: they bypass the non-coherent caches without the
 // cache invalidate an acquire load carries — polling waves must not flush the L2 that holds the
-// flow table); the caller fences once the chunk is seen.  Waves far from the frontier back off
+// flow table).  Waves far from the frontier back off
 // (s_sleep grows with the distance in chunks), so ~1K waiting waves do not turn the prod mirror
 // into a hot spot that slows the waves doing work.
+template <class OnIdle>
 __device__ __forceinline__ bool ring_wait_chunk(const RingArgs& a, uint32_t lane, unsigned long long t_begin,
-                                                uint32_t& tk_out) {
+                                                uint32_t& tk_out, OnIdle on_idle) {
   uint32_t tk = 0;
   if (lane == 0) tk = atomicAdd(&a.st->claim, 1u);
   tk = __builtin_amdgcn_readfirstlane(tk);
@@ -90,6 +117,7 @@ __device__ __forceinline__ bool ring_wait_chunk(const RingArgs& a, uint32_t lane
     v = rfl64(v);
     const unsigned long long avail = v & ~kRingStop;
     if (avail >= need) return true;
+    on_idle();                        // no published work for this wave: settle its bookkeeping
     if (v & kRingStop) return false;  // stop and final count come in one word: nothing more will arrive
     if (__builtin_amdgcn_s_memrealtime() - t_begin > a.deadline) return false;
     const unsigned long long dist = (first - avail) >> 6;  // chunks ahead of the frontier
@@ -128,7 +156,23 @@ __global__ __launch_bounds__(kRingBlock) void ring_kernel(RingArgs a) {
   // frame and the flow bucket (a session never sees a table change: commit relaunches the grid)
   const LdsTables ta = stage_lds_tables(a.t, reinterpret_cast<PortEntry*>(smem + L.tports),
                                         reinterpret_cast<uint64_t*>(smem + L.tchain), smem + L.tperm, true, kRingBlock);
+  uint32_t* pc = reinterpret_cast<uint32_t*>(smem + L.pc);
+  uint32_t* drops = reinterpret_cast<uint32_t*>(smem + L.drops);
+  for (uint32_t i = threadIdx.x; i < kLdsPorts * 4; i += kRingBlock) pc[i] = 0;
+  if (threadIdx.x < kNumReasons) drops[threadIdx.x] = 0;
   __syncthreads();
+
+  // raw buffer views over the ring (capacity <= 2^24 slots: byte offsets fit 32 bits)
+  const uint32_t rbytes = (a.ring_mask + 1u) * 64u;
+  const __amdgpu_buffer_rsrc_t r_pk = __builtin_amdgcn_make_buffer_rsrc((void*)a.pkts, (short)0, (int)rbytes, kBufRaw);
+  const __amdgpu_buffer_rsrc_t r_im = __builtin_amdgcn_make_buffer_rsrc((void*)a.inmeta, (short)0, (int)(rbytes / 16), kBufRaw);
+  const __amdgpu_buffer_rsrc_t r_out = __builtin_amdgcn_make_buffer_rsrc((void*)a.out, (short)0, (int)rbytes, kBufRaw);
+  const __amdgpu_buffer_rsrc_t r_meta = __builtin_amdgcn_make_buffer_rsrc((void*)a.out_meta, (short)0, (int)(rbytes / 16), kBufRaw);
+  const bool counters = !(a.flags_bits & kRingNoCounters);
+  uint32_t since_flush = 0;  // chunks this wave added to the LDS counters since its last flush
+  auto on_idle = [&]() {
+    if (since_flush) { flush_lds_counters(pc, drops, a.port_ctr, a.drop_ctr); since_flush = 0; }
+  };
 
   const uint32_t wave = threadIdx.x >> 6;
   uint4* kx = reinterpret_cast<uint4*>(smem + L.kx) + wave * 64;
@@ -140,17 +184,15 @@ __global__ __launch_bounds__(kRingBlock) void ring_kernel(RingArgs a) {
     uint32_t tk = 0;
     if constexpr (COOP) {
       if (wave == 0) {
-        const bool go = ring_wait_chunk(a, lane, t_begin, tk);
+        const bool go = ring_wait_chunk(a, lane, t_begin, tk, on_idle);
         if (lane == 0) { coop_ctl[0] = tk; coop_ctl[1] = go ? 1u : 0u; }
       }
       __syncthreads();
       tk = __builtin_amdgcn_readfirstlane(coop_ctl[0]);
       if (!__builtin_amdgcn_readfirstlane(coop_ctl[1])) break;
     } else {
-      if (!ring_wait_chunk(a, lane, t_begin, tk)) break;
+      if (!ring_wait_chunk(a, lane, t_begin, tk, on_idle)) break;
     }
-    if (!(a.flags_bits & kRingNoAcquire))
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the chunk's frames are published data
     const unsigned long long t_avail = __builtin_amdgcn_s_memrealtime();
     const bool trace = (a.flags_bits & kRingTrace) != 0 && wave == 0;
     uint32_t tr0 = 0, tr1 = 0, tr2 = 0, tr3 = 0, tr4 = 0, tr5 = 0;
@@ -165,10 +207,10 @@ __global__ __launch_bounds__(kRingBlock) void ring_kernel(RingArgs a) {
     uint32_t d[kSlotDwords];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const uint4 v = a.pkts[(size_t)i * 4 + q];
+      const v4u v = __builtin_amdgcn_raw_buffer_load_b128(r_pk, i * 64u + 16u * q, 0, kSysAux);
       d[4 * q] = v.x; d[4 * q + 1] = v.y; d[4 * q + 2] = v.z; d[4 * q + 3] = v.w;
     }
-    const uint32_t im = a.inmeta[i];
+    const uint32_t im = __builtin_amdgcn_raw_buffer_load_b32(r_im, i * 4u, 0, kSysAux);
     NFDP_RING_MARK(tr0)
     Parsed p;
     IngressState st;
@@ -206,28 +248,41 @@ __global__ __launch_bounds__(kRingBlock) void ring_kernel(RingArgs a) {
     const uint32_t olen = e.reason ? 0u : p.len + (e.push ? 4u : 0u);
     uint32_t o[kSlotDwords];
     emit(p, e.tci, e.push != 0, o);
-    uint4* dst = a.out + (size_t)i * 4;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) dst[q] = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
-    a.out_meta[i] = make_meta(e.out_port, olen, e.reason, e.mirror != 0);
+    for (int q = 0; q < 4; ++q) {
+      const v4u v = {o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]};
+      __builtin_amdgcn_raw_buffer_store_b128(v, r_out, i * 64u + 16u * q, 0, kSysAux);
+    }
+    __builtin_amdgcn_raw_buffer_store_b32(make_meta(e.out_port, olen, e.reason, e.mirror != 0), r_meta, i * 4u, 0, kSysAux);
     NFDP_RING_MARK(tr3)
 
-    // ---- completion: the chunk's frames are visible before its flag ----
-    if (!(a.flags_bits & kRingNoRelease)) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-    else __builtin_amdgcn_s_waitcnt(0);  // diagnostic: order only this wave's stores (no L2 writeback)
+    // ---- completion: the chunk's write-through stores are done before its flag is written ----
+    __builtin_amdgcn_s_waitcnt(0);
     NFDP_RING_MARK(tr4)
     if (lane == 0) {
       if (a.svc) a.svc[(size_t)(tk & nch_mask) * kSvcWords + 7] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_avail);
       __hip_atomic_store(&a.flags[tk & nch_mask], tk + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 
-    // ---- counters, off the latency path (after the flag): per-port / per-reason words are
-    // shared by the whole chunk -> wave-aggregated; per-flow words are (nearly) distinct per
-    // packet -> one atomic each.  They complete before the grid exits (harvest reads after stop).
-    wave_counter_add(a.port_ctr, 2 * st.in_port, st.wire_len, true, st.in_port < (uint32_t)kMaxPorts);
-    wave_counter_add(a.drop_ctr, e.reason & (kNumReasons - 1), 1u, false, e.reason != 0);
-    wave_counter_add(a.port_ctr, 2 * e.out_port + 1, olen, true, e.reason == 0);
-    if (hit && a.flow_ctr && !(a.flags_bits & 4u)) atomicAdd(a.flow_ctr + slot, ctr_inc(st.wire_len));
+    // ---- counters, off the latency path (after the flag): port / drop counters into the
+    // workgroup's LDS (flushed when idle, every kFlushChunks chunks and at exit), per-flow words
+    // (nearly distinct per packet) straight to the global table.
+    if (counters) {
+      if (st.in_port < (uint32_t)kLdsPorts) {
+        atomicAdd(&pc[st.in_port], 1u); atomicAdd(&pc[kLdsPorts + st.in_port], st.wire_len);
+      } else if (st.in_port < (uint32_t)kMaxPorts) {
+        atomicAdd(a.port_ctr + 2 * st.in_port, ctr_inc(st.wire_len));
+      }
+      if (e.reason) {
+        atomicAdd(&drops[e.reason & (kNumReasons - 1)], 1u);
+      } else if (e.out_port < (uint32_t)kLdsPorts) {
+        atomicAdd(&pc[2 * kLdsPorts + e.out_port], 1u); atomicAdd(&pc[3 * kLdsPorts + e.out_port], olen);
+      } else {
+        atomicAdd(a.port_ctr + 2 * e.out_port + 1, ctr_inc(olen));
+      }
+      if (hit && a.flow_ctr && !(a.flags_bits & 4u)) atomicAdd(a.flow_ctr + slot, ctr_inc(st.wire_len));
+      if (++since_flush >= kFlushChunks) on_idle();
+    }
     NFDP_RING_MARK(tr5)
 #undef NFDP_RING_MARK
     if (trace && lane == 0 && a.svc) {
@@ -235,6 +290,7 @@ __global__ __launch_bounds__(kRingBlock) void ring_kernel(RingArgs a) {
       sv[0] = tr0; sv[1] = tr1; sv[2] = tr2; sv[3] = tr3; sv[4] = tr4; sv[5] = tr5; sv[6] = 0;
     }
   }
+  on_idle();  // exit: whatever this wave counted since its last flush reaches the global table
 }
 
 template <int H, int A, bool C>

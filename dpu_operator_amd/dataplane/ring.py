@@ -42,7 +42,7 @@ class RingPath:
         self.dp = dp
         self.capacity = int(capacity)
         self.deadline_s = float(deadline_s)
-        self.knobs = int(knobs) & 0x38  # diagnostic knobs (ring.hip kRingNo*/kRingTrace), cost attribution only
+        self.knobs = int(knobs) & 0x60  # diagnostic knobs (ring.hip kRingTrace / kRingNoCounters), attribution only
         self.coop = bool(coop)
         self.eng = dp.nf.RingEngine(self.capacity, int(dp.num_cus), int(wgs_per_cu), self.coop)
         self._staged = 0

@@ -20,12 +20,12 @@ def main():
     dp.commit(full=True)
     pk, im = S.traffic(sc, 1 << 16, seed=1)
     rows = []
-    for wgs, knobs, coop in ((1, 0, True), (1, 32, True), (1, 0, False), (2, 0, False)):
+    for wgs, knobs, coop in ((1, 0, True), (1, 32, True), (1, 0, False), (1, 64, False), (2, 0, False)):
         ring = RingPath(dp, capacity=1 << 16, wgs_per_cu=wgs, deadline_s=60.0, knobs=knobs, coop=coop)
         ring.stage(pk, im)
         ring.start()
         res = {"wgs": wgs, "knobs": knobs, "coop": coop}
-        for batch, inflight, nb in ((64, 16, 3000), (1024, 16, 2000), (4096, 16, 1000), (64, 1, 3000)):
+        for batch, inflight, nb in ((64, 16, 3000), (1024, 16, 2000), (4096, 16, 1000), (8192, 7, 500), (64, 1, 3000)):
             lat, el = ring.probe(nb, batch, inflight)
             lat = lat[nb // 10:]
             res[f"b{batch}x{inflight}"] = {"p50_us": round(float(np.median(lat)), 2),
