@@ -388,8 +388,9 @@ PYBIND11_MODULE(_nfdp, m) {
   // Persistent ring kernel (low-latency path): the host publishes 64-packet chunks, resident
   // waves process them as they appear, completion flags come back through pinned host memory.
   py::class_<RingEngine>(m, "RingEngine")
-      .def(py::init<uint32_t, int, int, bool>(), py::arg("capacity"), py::arg("num_cus"), py::arg("wgs_per_cu") = 1,
-           py::arg("coop") = true)
+      .def(py::init<uint32_t, int, int, bool, bool>(), py::arg("capacity"), py::arg("num_cus"),
+           py::arg("wgs_per_cu") = 1, py::arg("coop") = true, py::arg("host_slots") = false)
+      .def_property_readonly("host_slots", &RingEngine::host_slots)
       .def_property_readonly("capacity", &RingEngine::capacity)
       .def_property_readonly("running", &RingEngine::running)
       .def_property_readonly("published", &RingEngine::published)

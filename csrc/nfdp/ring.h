@@ -59,13 +59,15 @@ class RingEngine {
   // capacity: ring slots (power of two, >= 64).  wgs_per_cu: resident 256-thread workgroups per CU.
   // coop: the 4 waves of a workgroup share each chunk (ACL tiles split 4 ways: lowest latency);
   // otherwise every wave takes its own chunks (highest throughput).
-  RingEngine(uint32_t capacity, int num_cus, int wgs_per_cu = 1, bool coop = true);
+  // host_slots: ring slots in pinned coherent host memory instead of HBM (zero-copy host I/O).
+  RingEngine(uint32_t capacity, int num_cus, int wgs_per_cu = 1, bool coop = true, bool host_slots = false);
   ~RingEngine();
   RingEngine(const RingEngine&) = delete;
   RingEngine& operator=(const RingEngine&) = delete;
 
   uint32_t capacity() const { return cap_; }
   bool running() const { return running_; }
+  bool host_slots() const { return host_slots_; }
   // device ring buffers (the producer stages frames here before publishing them)
   void* dev_in() const { return d_in_; }
   uint32_t* dev_inmeta() const { return d_im_; }
@@ -96,6 +98,8 @@ class RingEngine {
   uint32_t cap_, nch_;
   int num_cus_, wgs_;
   bool coop_;
+  bool host_slots_;
+  std::vector<void*> host_ptrs_;  // host_slots: pinned allocations to free
   RingCtl* ctl_ = nullptr;        // pinned, coherent
   uint32_t* flags_ = nullptr;     // pinned, coherent: [nch] completion sequence numbers
   RingDevState* st_ = nullptr;    // device

@@ -353,8 +353,8 @@ using Clock = std::chrono::steady_clock;
 inline double secs(Clock::time_point a, Clock::time_point b) { return std::chrono::duration<double>(b - a).count(); }
 }  // namespace
 
-RingEngine::RingEngine(uint32_t capacity, int num_cus, int wgs_per_cu, bool coop)
-    : cap_(capacity), nch_(capacity / 64), num_cus_(num_cus), wgs_(wgs_per_cu), coop_(coop) {
+RingEngine::RingEngine(uint32_t capacity, int num_cus, int wgs_per_cu, bool coop, bool host_slots)
+    : cap_(capacity), nch_(capacity / 64), num_cus_(num_cus), wgs_(wgs_per_cu), coop_(coop), host_slots_(host_slots) {
   if (capacity < 64 || (capacity & (capacity - 1)) || capacity > (1u << 24))
     throw std::invalid_argument("ring: capacity must be a power of two in [64, 2^24]");
   if (num_cus < 1 || wgs_per_cu < 1 || wgs_per_cu > 8) throw std::invalid_argument("ring: bad grid");
@@ -366,13 +366,26 @@ RingEngine::RingEngine(uint32_t capacity, int num_cus, int wgs_per_cu, bool coop
   std::memset(ctl_, 0, sizeof(RingCtl));
   std::memset(flags_, 0, (size_t)nch_ * 4);
   ck(hipMalloc(reinterpret_cast<void**>(&st_), sizeof(RingDevState)), "dev alloc state");
-  ck(hipMalloc(reinterpret_cast<void**>(&d_in_), (size_t)capacity * 64), "dev alloc in");
-  ck(hipMalloc(reinterpret_cast<void**>(&d_im_), (size_t)capacity * 4), "dev alloc inmeta");
-  ck(hipMalloc(reinterpret_cast<void**>(&d_out_), (size_t)capacity * 64), "dev alloc out");
-  ck(hipMalloc(reinterpret_cast<void**>(&d_meta_), (size_t)capacity * 4), "dev alloc meta");
+  // Slots: HBM (the wire side is the GPU: NIC DMA into device memory), or pinned coherent host
+  // memory (host-resident rings — pod vhost / AF_XDP style): the kernel's system-coherent buffer
+  // ops then read and write the frames over PCIe directly, with no separate copy step.
+  auto slot_alloc = [&](void** p, size_t bytes, const char* what) {
+    if (host_slots_) {
+      void* h = nullptr;
+      ck(hipHostMalloc(&h, bytes, hipHostMallocCoherent | hipHostMallocMapped), what);
+      std::memset(h, 0, bytes);
+      ck(hipHostGetDevicePointer(p, h, 0), what);
+      host_ptrs_.push_back(h);
+    } else {
+      ck(hipMalloc(p, bytes), what);
+      ck(hipMemset(*p, 0, bytes), what);
+    }
+  };
+  slot_alloc(reinterpret_cast<void**>(&d_in_), (size_t)capacity * 64, "alloc in");
+  slot_alloc(reinterpret_cast<void**>(&d_im_), (size_t)capacity * 4, "alloc inmeta");
+  slot_alloc(reinterpret_cast<void**>(&d_out_), (size_t)capacity * 64, "alloc out");
+  slot_alloc(reinterpret_cast<void**>(&d_meta_), (size_t)capacity * 4, "alloc meta");
   ck(hipMalloc(reinterpret_cast<void**>(&d_svc_), (size_t)nch_ * 4 * kSvcWords), "dev alloc svc");
-  ck(hipMemset(d_in_, 0, (size_t)capacity * 64), "memset");
-  ck(hipMemset(d_im_, 0, (size_t)capacity * 4), "memset");
   ck(hipMemset(d_svc_, 0, (size_t)nch_ * 4 * kSvcWords), "memset");
   ck(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "stream");
 }
@@ -384,7 +397,12 @@ RingEngine::~RingEngine() {
   }
   (void)hipStreamSynchronize(stream_);
   (void)hipStreamDestroy(stream_);
-  for (void* d : {(void*)st_, (void*)d_in_, (void*)d_im_, (void*)d_out_, (void*)d_meta_, (void*)d_svc_}) (void)hipFree(d);
+  for (void* d : {(void*)st_, (void*)d_svc_}) (void)hipFree(d);
+  if (host_slots_) {
+    for (void* h : host_ptrs_) (void)hipHostFree(h);
+  } else {
+    for (void* d : {(void*)d_in_, (void*)d_im_, (void*)d_out_, (void*)d_meta_}) (void)hipFree(d);
+  }
   (void)hipHostFree(ctl_);
   (void)hipHostFree(flags_);
 }

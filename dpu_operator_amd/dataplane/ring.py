@@ -32,9 +32,11 @@ from .engine import DataPlane
 
 class RingPath:
     def __init__(self, dp: DataPlane, capacity: int = 1 << 16, wgs_per_cu: int = 1, deadline_s: float = 120.0,
-                 knobs: int = 0, coop: bool = True):
+                 knobs: int = 0, coop: bool = True, host_slots: bool = False):
         """coop=True: a workgroup's 4 waves share each chunk (ACL rule tiles split 4 ways) —
-        lowest latency.  coop=False: every wave takes its own chunks — highest throughput."""
+        lowest latency.  coop=False: every wave takes its own chunks — highest throughput.
+        host_slots=True: the ring slots live in pinned host memory and the resident kernel reads /
+        writes the frames over PCIe itself (zero-copy host rings, e.g. pod vhost / AF_XDP)."""
         if not dp.gpu:
             raise RuntimeError("RingPath needs a GPU data plane")
         if capacity < 64 or capacity & (capacity - 1):
@@ -44,7 +46,8 @@ class RingPath:
         self.deadline_s = float(deadline_s)
         self.knobs = int(knobs) & 0x60  # diagnostic knobs (ring.hip kRingTrace / kRingNoCounters), attribution only
         self.coop = bool(coop)
-        self.eng = dp.nf.RingEngine(self.capacity, int(dp.num_cus), int(wgs_per_cu), self.coop)
+        self.host_slots = bool(host_slots)
+        self.eng = dp.nf.RingEngine(self.capacity, int(dp.num_cus), int(wgs_per_cu), self.coop, self.host_slots)
         self._staged = 0
         rings = getattr(dp, "_rings", None)
         if rings is None:

@@ -232,8 +232,11 @@ def test_daemon_side_manager_failure_stops_serve(pm):
     assert isinstance(err, RuntimeError) and "never came up" in str(err)
 
 
-def test_colocated_gpu_node_end_to_end(pm):
-    """MI355X node: daemon -> ColocatedSideManager -> GPU VSP (CPU oracle) -> steering verified."""
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+def test_colocated_gpu_node_end_to_end(pm, device):
+    """MI355X node: daemon -> ColocatedSideManager -> GPU VSP -> steering verified, on the C++
+    oracle (cpu) and on the HIP kernels (cuda): CNI ADDs and OPI CreateBridgePort program the
+    tables, then frames go through the data plane."""
     from dpu_operator_amd.ops import packets as P
     from dpu_operator_amd.vsp.gpu import WIRE_PORT, GpuVsp
 
@@ -241,7 +244,7 @@ def test_colocated_gpu_node_end_to_end(pm):
     api = ApiServer()
     nl = FakeNetlink()
     kubelet = FakeKubelet(pm, api).start()
-    gvsp = GpuVsp(path_manager=pm, device="cpu", nl=nl, flow_buckets=1 << 8)
+    gvsp = GpuVsp(path_manager=pm, device=device, nl=nl, flow_buckets=1 << 8)
     gvsp.start()
     plat = FakePlatform("AMD server", [PciDevice("0000:05:00.0", "1002", "75a3", class_code=0x120000)])
     d = Daemon(plat, "auto", api, None, pm, nl=nl, tick=0.05, manager_kw={"dp_poll": 0.05})

@@ -34,12 +34,12 @@ def test_ring_needs_gpu():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("coop", [True, False])
-def test_ring_bit_exact_and_counters(coop):
+@pytest.mark.parametrize("coop,host_slots", [(True, False), (False, False), (True, True)])
+def test_ring_bit_exact_and_counters(coop, host_slots):
     g, sc = _build("cuda")
     c, _ = _build("cpu")
     pk, im = _traffic(sc)
-    ring = RingPath(g, capacity=CAP, deadline_s=30.0, coop=coop)
+    ring = RingPath(g, capacity=CAP, deadline_s=30.0, coop=coop, host_slots=host_slots)
     try:
         ring.stage(pk, im)
         ring.start()
@@ -132,5 +132,25 @@ def test_ring_probe_latency():
     assert len(lat) == 400 and len(lat2) == 200
     p50 = float(np.median(lat[40:]))
     print(f"ring p50 {p50:.2f} us  p99 {np.percentile(lat[40:], 99):.2f} us; "
+          f"loaded p50 {np.median(lat2):.2f} us, {200 * 1024 / el2 / 1e6:.1f} Mpps")
+    assert 0 < p50 < 2000
+
+
+@pytest.mark.gpu
+def test_ring_host_slots_latency():
+    """Zero-copy host rings: the resident kernel reads/writes the frames in pinned host memory."""
+    g, sc = _build("cuda")
+    pk, im = _traffic(sc)
+    ring = RingPath(g, capacity=CAP, deadline_s=60.0, host_slots=True)
+    try:
+        ring.stage(pk, im)
+        ring.start()
+        lat, _ = ring.probe(batches=400, batch=64, inflight=1)
+        lat2, el2 = ring.probe(batches=200, batch=1024, inflight=4)
+        ring.stop()
+    finally:
+        ring.close()
+    p50 = float(np.median(lat[40:]))
+    print(f"host-slot ring p50 {p50:.2f} us  p99 {np.percentile(lat[40:], 99):.2f} us; "
           f"loaded p50 {np.median(lat2):.2f} us, {200 * 1024 / el2 / 1e6:.1f} Mpps")
     assert 0 < p50 < 2000
