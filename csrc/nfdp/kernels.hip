@@ -19,6 +19,16 @@
 
 namespace nfdp {
 
+// Fused-kernel geometry (overridable at build time for occupancy experiments).
+#ifndef NFDP_FUSED_BLOCK
+#define NFDP_FUSED_BLOCK 512
+#endif
+#ifndef NFDP_FUSED_WAVES_PER_EU
+#define NFDP_FUSED_WAVES_PER_EU 4
+#endif
+constexpr int kFB = NFDP_FUSED_BLOCK;
+constexpr int kFWaves = kFB / 64;
+
 struct FusedArgs {
   TablesView t;
   const uint4* pkts;              // n slots of 64 B
@@ -58,7 +68,7 @@ __host__ __device__ inline LdsLayout lds_layout(int hash_mode, int acl_mode, uin
   L.acl_c = o; if (acl_mode == kAclMfma) o += (size_t)acl_tiles * 4 * 16;
   L.toep_f = o; if (hash_mode == kHashMfma) o += 2 * 2 * 64 * 16;
   L.toep_t = o; if (hash_mode == kHashLds) o += 16 * 256 * 4;
-  L.kx = o; o += kWaves * 64 * 16;
+  L.kx = o; o += kFWaves * 64 * 16;
   L.pc = o; o += kLdsPorts * 4 * 4;
   L.drops = o; o += kNumReasons * 4;
   o = (o + 15) & ~(size_t)15;
@@ -93,7 +103,7 @@ __device__ __forceinline__ void load_slot(const uint4* pk4, const uint32_t* inme
 }
 
 template <int HASH, int ACL, bool REMOTE>
-__global__ __launch_bounds__(kBlock, 4) void fused_kernel(FusedArgs a) {
+__global__ __launch_bounds__(kFB, NFDP_FUSED_WAVES_PER_EU) void fused_kernel(FusedArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ uint32_t rcnt[REMOTE ? kMaxRanks : 1], rbase[REMOTE ? kMaxRanks : 1];
   const LdsLayout L = lds_layout(HASH, ACL, a.acl_tiles);
@@ -108,24 +118,24 @@ __global__ __launch_bounds__(kBlock, 4) void fused_kernel(FusedArgs a) {
   // ---- stage classification tables + zero counters ----
   if constexpr (ACL == kAclMfma) {
     const uint32_t nw = a.acl_tiles * 2 * 64, nc = a.acl_tiles * 4;
-    for (uint32_t i = threadIdx.x; i < nw; i += kBlock) lw[i] = a.acl_wfrag[i];
-    for (uint32_t i = threadIdx.x; i < nc; i += kBlock) lc[i] = a.acl_cinit[i];
+    for (uint32_t i = threadIdx.x; i < nw; i += kFB) lw[i] = a.acl_wfrag[i];
+    for (uint32_t i = threadIdx.x; i < nc; i += kFB) lc[i] = a.acl_cinit[i];
   }
   if constexpr (HASH == kHashMfma)
-    for (uint32_t i = threadIdx.x; i < 256; i += kBlock) lt[i] = a.toep_frag[i];
+    for (uint32_t i = threadIdx.x; i < 256; i += kFB) lt[i] = a.toep_frag[i];
   if constexpr (HASH == kHashLds)
-    for (uint32_t i = threadIdx.x; i < 4096; i += kBlock) ltab[i] = a.toep_tab[i];
-  for (uint32_t i = threadIdx.x; i < kLdsPorts * 4; i += kBlock) pc[i] = 0;
+    for (uint32_t i = threadIdx.x; i < 4096; i += kFB) ltab[i] = a.toep_tab[i];
+  for (uint32_t i = threadIdx.x; i < kLdsPorts * 4; i += kFB) pc[i] = 0;
   if (threadIdx.x < kNumReasons) drops[threadIdx.x] = 0;
   PortEntry* lport = reinterpret_cast<PortEntry*>(smem + L.tports);
   uint64_t* lchain = reinterpret_cast<uint64_t*>(smem + L.tchain);
   uint8_t* lperm = smem + L.tperm;
-  const LdsTables ta = stage_lds_tables(a.t, lport, lchain, lperm, L.tabs, kBlock);
+  const LdsTables ta = stage_lds_tables(a.t, lport, lchain, lperm, L.tabs, kFB);
   __syncthreads();
 
   const unsigned long long t0 = a.t0 ? *a.t0 : 0ull;
   const uint4* pk4 = a.pkts;
-  const uint32_t stride = gridDim.x * kBlock;
+  const uint32_t stride = gridDim.x * kFB;
   // Software pipeline over the grid-stride loop.  s_waitcnt vmcnt retires loads, stores and
   // atomics together in issue order, so the next slot's frame is loaded BEFORE this slot's
   // flow-counter atomic and output stores: waiting for the frame never waits for them, and the
@@ -133,7 +143,7 @@ __global__ __launch_bounds__(kBlock, 4) void fused_kernel(FusedArgs a) {
   // slot's parse + classification.
   uint32_t dn[kSlotDwords];
   uint32_t imn;
-  load_slot(pk4, a.inmeta, blockIdx.x * kBlock + threadIdx.x, a.n, dn, imn);
+  load_slot(pk4, a.inmeta, blockIdx.x * kFB + threadIdx.x, a.n, dn, imn);
   // raw buffer views (num_records = valid bytes; offsets past it read 0 / drop the store)
   const __amdgpu_buffer_rsrc_t r_pk = __builtin_amdgcn_make_buffer_rsrc((void*)a.pkts, (short)0, (int)(a.n * 64u), kBufCfg);
   const __amdgpu_buffer_rsrc_t r_im = __builtin_amdgcn_make_buffer_rsrc((void*)a.inmeta, (short)0, (int)(a.n * 4u), kBufCfg);
@@ -142,7 +152,7 @@ __global__ __launch_bounds__(kBlock, 4) void fused_kernel(FusedArgs a) {
   const __amdgpu_buffer_rsrc_t r_lat = __builtin_amdgcn_make_buffer_rsrc((void*)a.lat, (short)0,
                                                                           a.lat ? (int)(((a.n + 15u) >> 4) * 4u) : 0, kBufCfg);
   const uint32_t ctr_mask = min(a.t.bucket_mask * kBucketSlots + (kBucketSlots - 1), 4095u);
-  for (uint32_t base = blockIdx.x * kBlock; base < a.n; base += stride) {
+  for (uint32_t base = blockIdx.x * kFB; base < a.n; base += stride) {
     const uint32_t i = base + threadIdx.x;
     const bool valid = i < a.n;
     Parsed p;
@@ -251,7 +261,7 @@ __global__ __launch_bounds__(kBlock, 4) void fused_kernel(FusedArgs a) {
     }
   }
   __syncthreads();
-  for (uint32_t q = threadIdx.x; q < kLdsPorts; q += kBlock) {
+  for (uint32_t q = threadIdx.x; q < kLdsPorts; q += kFB) {
     if (pc[q]) atomicAdd(a.port_ctr + 2 * q, ((unsigned long long)pc[q] << 40) | pc[kLdsPorts + q]);
     if (pc[2 * kLdsPorts + q])
       atomicAdd(a.port_ctr + 2 * q + 1, ((unsigned long long)pc[2 * kLdsPorts + q] << 40) | pc[3 * kLdsPorts + q]);
@@ -309,11 +319,11 @@ static hipError_t launch_fused_t(const FusedArgs& a, int num_cus, hipStream_t s)
   }
   int per_cu = (int)((160 * 1024) / (lds ? lds : 1));
   per_cu = per_cu < 1 ? 1 : (per_cu > 4 ? 4 : per_cu);
-  const uint32_t need = (a.n + kBlock - 1) / kBlock;
+  const uint32_t need = (a.n + kFB - 1) / kFB;
   uint32_t grid = (uint32_t)(per_cu * num_cus);
   if (need < grid) grid = need;
   if (grid == 0) return hipSuccess;
-  hipLaunchKernelGGL((fused_kernel<H, A, R>), dim3(grid), dim3(kBlock), lds, s, a);
+  hipLaunchKernelGGL((fused_kernel<H, A, R>), dim3(grid), dim3(kFB), lds, s, a);
   return hipGetLastError();
 }
 

@@ -76,7 +76,9 @@ def _compile(src: Path, obj: Path, hip: bool, verbose: bool) -> None:
     obj.parent.mkdir(parents=True, exist_ok=True)
     common = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function", *_includes(), "-I", str(src.parent)]
     if hip:
-        cmd = [HIPCC, "-x", "hip", f"--offload-arch={ARCH}", "-munsafe-fp-atomics", *common, "-c", str(src), "-o", str(obj)]
+        extra = os.environ.get("NFDP_HIPCC_FLAGS", "").split()  # build-time experiments (-D...)
+        cmd = [HIPCC, "-x", "hip", f"--offload-arch={ARCH}", "-munsafe-fp-atomics", *common, *extra, "-c", str(src),
+               "-o", str(obj)]
     else:
         cxx = shutil.which("g++") or "g++"
         cmd = [cxx, *common, "-pthread", "-c", str(src), "-o", str(obj)]
