@@ -238,6 +238,66 @@ __device__ __forceinline__ void wave_counter_add(unsigned long long* ctr, uint32
   }
 }
 
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+
+// ---- coalesced frame I/O (tools/copy_bench.hip: 6.4 TB/s vs 1.4 TB/s for per-lane slots) ----
+// A wave's 64 slots are one contiguous 4-KiB run.  Each dwordx4 instruction covers 1 KiB of it
+// lane-contiguously (16 full 64-B lines) instead of 16 B of 64 different lines, and the wave's
+// 1-KiB LDS scratch (the classify key exchange, `kx`) transposes 16 packets per pass between
+// "chunk per lane" and "packet per lane".  Chunk c = 64 q + lane of the run is part c & 3 of
+// packet c >> 2.  EXEC must be full.  Offsets at or beyond the buffer's num_records (slots
+// past n, or `run` = kNoRun) read 0 / drop the store.  `run` is wave-uniform: it rides in the
+// instruction's SGPR offset, the lane part is one loop-invariant VGPR plus the immediate.
+constexpr uint32_t kNoRun = 0x80000000u;
+
+template <int AUX>
+__device__ __forceinline__ void wave_frames_load(__amdgpu_buffer_rsrc_t r, uint32_t run, v4u c[4]) {
+  const uint32_t lane = threadIdx.x & 63u;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) c[q] = __builtin_amdgcn_raw_buffer_load_b128(r, lane * 16u + q * 1024u, run, AUX);
+}
+
+__device__ __forceinline__ void wave_frames_to_lanes(uint4* kx, const v4u c[4], uint32_t* d) {
+  const uint32_t lane = threadIdx.x & 63u;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    kx[lane] = make_uint4(c[q].x, c[q].y, c[q].z, c[q].w);
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    if ((lane >> 4) == (uint32_t)q) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint4 v = kx[4u * (lane & 15u) + k];
+        d[4 * k] = v.x; d[4 * k + 1] = v.y; d[4 * k + 2] = v.z; d[4 * k + 3] = v.w;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  }
+}
+
+// `skip`: bit p set -> packet p of the run is not stored (its frame went elsewhere).
+template <int AUX>
+__device__ __forceinline__ void wave_frames_store(uint4* kx, const uint32_t* o, __amdgpu_buffer_rsrc_t r, uint32_t run,
+                                                  unsigned long long skip = 0ull) {
+  const uint32_t lane = threadIdx.x & 63u;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    if ((lane >> 4) == (uint32_t)q) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) kx[4u * (lane & 15u) + k] = make_uint4(o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]);
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    const uint4 v = kx[lane];
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    const v4u w = {v.x, v.y, v.z, v.w};
+    const bool drop = (skip >> (16u * q + (lane >> 2))) & 1ull;
+    __builtin_amdgcn_raw_buffer_store_b128(w, r, drop ? kNoRun : lane * 16u + q * 1024u, run, AUX);
+  }
+}
+
 // ---- multi-GPU output segments (shared by the fused REMOTE variant and the sharded stages) ----
 constexpr uint32_t kMaxRanks = 64;
 

@@ -1,8 +1,9 @@
 // kernels.hip — CDNA4 (gfx950) data-plane kernels.
 //
 // Design (MI355X-first, see docs/DATAPLANE.md):
-//  * one packet per lane, 64-B slots loaded as 4 x dwordx4, 8 waves per workgroup, grid sized
-//    to the CU count x the LDS-admitted blocks per CU, grid-stride over the batch;
+//  * one packet per lane, 8 waves per workgroup, grid sized to the CU count x the LDS-admitted
+//    blocks per CU, grid-stride over the batch; a wave's 64 slots are one 4-KiB run moved with
+//    lane-contiguous dwordx4 loads/stores and transposed through LDS (coalesced frame I/O);
 //  * classification is ONE int8 MFMA GEMM over the bit-expanded 128-bit FlowKey:
 //      - Toeplitz RSS hash = GF(2) product  key_bits[16 pkts x 128] x T[128 x 32], parity (&1)
 //      - TCAM / priority ACL = key_bits x W[128 x R] + bias, W in {-1,0,+1}; a rule matches
@@ -82,7 +83,6 @@ __host__ __device__ inline LdsLayout lds_layout(int hash_mode, int acl_mode, uin
   return L;
 }
 
-typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 constexpr int kBufCfg = 0x00020000;  // buffer resource word 3 (gfx9 family raw buffer)
 constexpr int kStreamAux = 2;        // nt: frames are read once / written once (streaming)
 
@@ -143,10 +143,18 @@ __global__ __launch_bounds__(kFB, NFDP_FUSED_WAVES_PER_EU) void fused_kernel(Fus
   // slot's parse + classification.
   uint32_t dn[kSlotDwords];
   uint32_t imn;
-  load_slot(pk4, a.inmeta, blockIdx.x * kFB + threadIdx.x, a.n, dn, imn);
   // raw buffer views (num_records = valid bytes; offsets past it read 0 / drop the store)
   const __amdgpu_buffer_rsrc_t r_pk = __builtin_amdgcn_make_buffer_rsrc((void*)a.pkts, (short)0, (int)(a.n * 64u), kBufCfg);
   const __amdgpu_buffer_rsrc_t r_im = __builtin_amdgcn_make_buffer_rsrc((void*)a.inmeta, (short)0, (int)(a.n * 4u), kBufCfg);
+  // first 4-KiB run of this wave (prefetched frames arrive chunk-per-lane in cn)
+  const uint32_t wave0 = __builtin_amdgcn_readfirstlane(threadIdx.x) & ~63u;  // wave-uniform (SGPR)
+  auto run_of = [&](uint32_t base) { return base + wave0 < a.n ? (base + wave0) * 64u : kNoRun; };
+  v4u cn[4];
+  {
+    wave_frames_load<kStreamAux>(r_pk, run_of(blockIdx.x * kFB), cn);
+    const uint32_t i0 = blockIdx.x * kFB + threadIdx.x;
+    imn = __builtin_amdgcn_raw_buffer_load_b32(r_im, i0 < a.n ? i0 * 4u : kNoRun, 0, kStreamAux);
+  }
   const __amdgpu_buffer_rsrc_t r_out = __builtin_amdgcn_make_buffer_rsrc((void*)a.out, (short)0, (int)(a.n * 64u), kBufCfg);
   const __amdgpu_buffer_rsrc_t r_meta = __builtin_amdgcn_make_buffer_rsrc((void*)a.out_meta, (short)0, (int)(a.n * 4u), kBufCfg);
   const __amdgpu_buffer_rsrc_t r_lat = __builtin_amdgcn_make_buffer_rsrc((void*)a.lat, (short)0,
@@ -155,6 +163,7 @@ __global__ __launch_bounds__(kFB, NFDP_FUSED_WAVES_PER_EU) void fused_kernel(Fus
   for (uint32_t base = blockIdx.x * kFB; base < a.n; base += stride) {
     const uint32_t i = base + threadIdx.x;
     const bool valid = i < a.n;
+    wave_frames_to_lanes(kx, cn, dn);
     Parsed p;
     IngressState st;
     ingress_stage(a.t, ta, dn, imn, p, st);  // copies the frame into p.s: dn is free for the prefetch
@@ -167,13 +176,8 @@ __global__ __launch_bounds__(kFB, NFDP_FUSED_WAVES_PER_EU) void fused_kernel(Fus
     if constexpr (!REMOTE) {
       // prefetch the next slot now: it lands under this slot's probe and chain
       const uint32_t nx = i + stride;
-      const uint32_t fo = nx < a.n ? nx * 64u : 0x80000000u;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const v4u v = __builtin_amdgcn_raw_buffer_load_b128(r_pk, fo + 16u * q, 0, kStreamAux);
-        dn[4 * q] = v.x; dn[4 * q + 1] = v.y; dn[4 * q + 2] = v.z; dn[4 * q + 3] = v.w;
-      }
-      imn = __builtin_amdgcn_raw_buffer_load_b32(r_im, nx < a.n ? nx * 4u : 0x80000000u, 0, kStreamAux);
+      wave_frames_load<kStreamAux>(r_pk, run_of(base + stride), cn);
+      imn = __builtin_amdgcn_raw_buffer_load_b32(r_im, nx < a.n ? nx * 4u : kNoRun, 0, kStreamAux);
     }
 
     bool hit = false;
@@ -241,23 +245,24 @@ __global__ __launch_bounds__(kFB, NFDP_FUSED_WAVES_PER_EU) void fused_kernel(Fus
       // instead of draining this slot's atomic and stores.
       const uint32_t cslot = hit ? (uint32_t)slot : (i & ctr_mask);
       atomicAdd(a.flow_ctr + cslot, (hit && !(a.flags & 4u)) ? ctr_inc(st.wire_len) : 0ull);
-      const uint32_t so = valid ? i * 64u : 0x80000000u;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        v4u v = {o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]};
-        __builtin_amdgcn_raw_buffer_store_b128(v, r_out, so + 16u * q, 0, kStreamAux);
-      }
-      __builtin_amdgcn_raw_buffer_store_b32(meta, r_meta, valid ? i * 4u : 0x80000000u, 0, kStreamAux);
-      __builtin_amdgcn_raw_buffer_store_b32(lat_now, r_lat, sample ? (i >> 4) * 4u : 0x80000000u, 0, 0);
+      wave_frames_store<kStreamAux>(kx, o, r_out, run_of(base));
+      __builtin_amdgcn_raw_buffer_store_b32(meta, r_meta, valid ? i * 4u : kNoRun, 0, kStreamAux);
+      __builtin_amdgcn_raw_buffer_store_b32(lat_now, r_lat, sample ? (i >> 4) * 4u : kNoRun, 0, 0);
     } else {
-      load_slot(pk4, a.inmeta, i + stride, a.n, dn, imn);
       if (hit && a.flow_ctr && !(a.flags & 4u)) atomicAdd(a.flow_ctr + slot, ctr_inc(st.wire_len));
-      if (valid) {
+      // frames for a peer: per lane into its segment slot; local frames: coalesced into out[]
+      if (to_peer) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) dst[q] = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
+      }
+      wave_frames_store<kStreamAux>(kx, o, r_out, run_of(base), __ballot(to_peer));
+      if (valid) {
         a.out_meta[i] = meta;
         if (sample) a.lat[i >> 4] = lat_now;
       }
+      const uint32_t nx = i + stride;
+      wave_frames_load<kStreamAux>(r_pk, run_of(base + stride), cn);
+      imn = __builtin_amdgcn_raw_buffer_load_b32(r_im, nx < a.n ? nx * 4u : kNoRun, 0, kStreamAux);
     }
   }
   __syncthreads();

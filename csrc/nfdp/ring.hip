@@ -31,7 +31,6 @@ struct RingArgs {
 // stale L2 line of a slot a producer (host / NIC DMA) rewrote, and the stores write through to
 // HBM, so completion needs only "my stores are done" (s_waitcnt) before the flag — no per-chunk
 // L2 invalidate / writeback, which serialised the ring at ~1.5 Gpps under load.
-typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 constexpr int kSysAux = 1 | 16;  // cache-policy bits: sc0 | sc1 (gfx940+)
 constexpr int kBufRaw = 0x00020000;
 // Phase trace: drain the memory counters at each stage boundary and stamp it (svc[chunk][0..6];
@@ -204,11 +203,13 @@ __global__ __launch_bounds__(kRingBlock) void ring_kernel(RingArgs a) {
 
     // ---- one packet per lane: the fused kernel's stages ----
     const uint32_t i = (tk * 64u + lane) & a.ring_mask;
+    // the chunk's 64 slots are one 4-KiB run: lane-contiguous loads, transposed through LDS
+    const uint32_t run = __builtin_amdgcn_readfirstlane(((tk * 64u) & a.ring_mask) * 64u);
     uint32_t d[kSlotDwords];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const v4u v = __builtin_amdgcn_raw_buffer_load_b128(r_pk, i * 64u + 16u * q, 0, kSysAux);
-      d[4 * q] = v.x; d[4 * q + 1] = v.y; d[4 * q + 2] = v.z; d[4 * q + 3] = v.w;
+    {
+      v4u c[4];
+      wave_frames_load<kSysAux>(r_pk, run, c);
+      wave_frames_to_lanes(kx, c, d);
     }
     const uint32_t im = __builtin_amdgcn_raw_buffer_load_b32(r_im, i * 4u, 0, kSysAux);
     NFDP_RING_MARK(tr0)
@@ -248,11 +249,7 @@ __global__ __launch_bounds__(kRingBlock) void ring_kernel(RingArgs a) {
     const uint32_t olen = e.reason ? 0u : p.len + (e.push ? 4u : 0u);
     uint32_t o[kSlotDwords];
     emit(p, e.tci, e.push != 0, o);
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const v4u v = {o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]};
-      __builtin_amdgcn_raw_buffer_store_b128(v, r_out, i * 64u + 16u * q, 0, kSysAux);
-    }
+    wave_frames_store<kSysAux>(kx, o, r_out, run);
     __builtin_amdgcn_raw_buffer_store_b32(make_meta(e.out_port, olen, e.reason, e.mirror != 0), r_meta, i * 4u, 0, kSysAux);
     NFDP_RING_MARK(tr3)
 

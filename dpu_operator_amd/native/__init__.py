@@ -22,6 +22,9 @@ def _load(name: str, autobuild: bool = True):
         return _cache[name]
     if str(_HERE) not in sys.path:
         sys.path.insert(0, str(_HERE))
+    variant = os.environ.get("NFDP_EXT_DIR")  # build-flag experiments (native/build.py NFDP_BUILD_OUT)
+    if variant and sys.path[0] != variant:
+        sys.path.insert(0, variant)
     # torch first: it loads its ROCm runtime libraries into the global symbol scope, and the
     # extension's HIP runtime must bind to that same HSA runtime.  Loaded the other way round the
     # process ends up with two HSA runtimes and the extension's sees no device.

@@ -25,6 +25,11 @@ HERE = Path(__file__).resolve().parent
 REPO = HERE.parent.parent
 CSRC = REPO / "csrc"
 BUILD = REPO / "build" / "native"
+# Experiment variants: NFDP_BUILD_OUT=<dir> puts the module (and its objects) there instead of
+# next to this file; load it with NFDP_EXT_DIR=<dir> (see __init__.py).
+VARIANT_OUT = os.environ.get("NFDP_BUILD_OUT")
+if VARIANT_OUT:
+    BUILD = BUILD / ("variant-" + Path(VARIANT_OUT).name)
 ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
 HIPCC = str(ROCM / "bin" / "hipcc")
 ARCH = "gfx950"
@@ -91,10 +96,25 @@ def _compile(src: Path, obj: Path, hip: bool, verbose: bool) -> None:
         print(r.stderr, file=sys.stderr)
 
 
+def _flags_changed(name: str, hip: bool) -> bool:
+    """True when the experiment flags differ from the ones the objects were built with (the
+    stamp is rewritten), so an NFDP_HIPCC_FLAGS build never survives into a default build."""
+    flags = os.environ.get("NFDP_HIPCC_FLAGS", "").strip() if hip else ""
+    stamp = BUILD / name / "flags.stamp"
+    old = stamp.read_text() if stamp.exists() else None
+    if old == flags:
+        return False
+    stamp.parent.mkdir(parents=True, exist_ok=True)
+    stamp.write_text(flags)
+    return True
+
+
 def build_module(name: str, force: bool = False, verbose: bool = False) -> Path:
     spec = MODULES[name]
     d: Path = spec["dir"]
-    out = HERE / f"{name}{EXT}"
+    out = (Path(VARIANT_OUT) if VARIANT_OUT else HERE) / f"{name}{EXT}"
+    out.parent.mkdir(parents=True, exist_ok=True)
+    force = _flags_changed(name, spec["hip"]) or force
     hdr = _newest_header(d)
     objs = []
     jobs = []
