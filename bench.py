@@ -62,6 +62,9 @@ def parse():
                          "around every kernel (1 GPU)")
     ap.add_argument("--force-sharded", action="store_true",
                     help="use the sharded multi-GPU pipeline even at N = 1 (measures its compute cost)")
+    ap.add_argument("--rehearse", action="store_true",
+                    help="correctness rehearsal of the N-GPU path on a 1-GPU box: every rank on cuda:0, gloo "
+                         "with host-staged exchanges (RCCL refuses two ranks on one device); not a measurement")
     return ap.parse_args()
 
 
@@ -76,8 +79,11 @@ def main() -> None:
     if world != a.gpus:
         if world == 1 and a.gpus > 1:
             raise SystemExit("--gpus > 1 must be launched with torch.distributed.run (one process per GPU)")
+    if a.rehearse:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    cdev = torch.device("cpu") if a.rehearse else dev  # where the small stats collectives run
     sharded = world > 1 or a.force_sharded
     if sharded:
         if world == 1:
@@ -85,7 +91,10 @@ def main() -> None:
             os.environ.setdefault("MASTER_PORT", "29533")
             os.environ.setdefault("RANK", "0")
             os.environ.setdefault("WORLD_SIZE", "1")
-        dist.init_process_group("nccl", device_id=dev)
+        if a.rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     from dpu_operator_amd.dataplane import scenario as S
     from dpu_operator_amd.dataplane.engine import DataPlane
@@ -180,7 +189,7 @@ def main() -> None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -190,7 +199,7 @@ def main() -> None:
     p50 = float(np.median(lat_us)) if len(lat_us) else float("nan")
     p99 = float(np.percentile(lat_us, 99)) if len(lat_us) else float("nan")
     if world > 1:
-        st = torch.tensor([p50, p99, fwd_local], dtype=torch.float64, device=dev)
+        st = torch.tensor([p50, p99, fwd_local], dtype=torch.float64, device=cdev)
         g = [torch.zeros_like(st) for _ in range(world)]
         dist.all_gather(g, st)
         arr = torch.stack(g).cpu().numpy()
@@ -221,7 +230,7 @@ def main() -> None:
             ls = eng_s.latency_samples_us()
         p50_small = float(np.median(ls)) if len(ls) else None
         if world > 1:
-            t = torch.tensor([p50_small or 0.0], dtype=torch.float64, device=dev)
+            t = torch.tensor([p50_small or 0.0], dtype=torch.float64, device=cdev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             p50_small = float(t.item())
 
@@ -294,6 +303,8 @@ def main() -> None:
             "setup_s": round(setup_s, 1),
             "baseline_note": "reference publishes no numbers (BASELINE.md); 200GbE line rate at 64B = 297.6 Mpps",
         }
+        if a.rehearse:
+            line["rehearsal"] = "all ranks on cuda:0, gloo host-staged exchange: correctness only, not a measurement"
         print(json.dumps(line), flush=True)
     if sharded:
         dist.barrier()

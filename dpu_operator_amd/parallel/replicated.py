@@ -39,6 +39,13 @@ class _Slot:
         self.lat2 = torch.zeros((world * cap + 15) // 16, **i32)
 
 
+class _Done:
+    """Completed-work handle of a synchronous (host-staged) exchange."""
+
+    def wait(self) -> None:
+        pass
+
+
 class ReplicatedDataPlane:
     RING = 3
 
@@ -67,6 +74,9 @@ class ReplicatedDataPlane:
         self.t0 = torch.zeros(1, dtype=torch.int64, device=self.dev)
         self.hash_mode = dp.hash_mode if dp.hash_mode != 0 else 1
         self.acl_mode = dp.acl_mode
+        # gloo with device buffers (the 1-GPU rehearsal of the N-GPU path: every rank on one card):
+        # the exchange is staged through host memory.  RCCL exchanges device buffers directly.
+        self.host_staged = self.gpu and dist.get_backend(group) == "gloo"
 
     @staticmethod
     def _p(t) -> int:
@@ -98,6 +108,14 @@ class ReplicatedDataPlane:
                   t0=p(self.t0) if self.gpu else 0, lat=p(s.lat2) if self.gpu else 0)
         self.nf.shard_egress(eg, self.gpu, self.dp.num_cus, self._stream())
 
+    def _exchange(self, s: _Slot):
+        if not self.host_staged:
+            return dist.all_to_all_single(s.recv, s.send, group=self.group, async_op=True)
+        recv = torch.empty(s.recv.shape, dtype=s.recv.dtype)
+        dist.all_to_all_single(recv, s.send.cpu(), group=self.group)
+        s.recv.copy_(recv)
+        return _Done()
+
     def step(self, pkts: torch.Tensor, inmeta: torch.Tensor) -> None:
         n = int(pkts.shape[0])
         if n > self.batch:
@@ -115,7 +133,7 @@ class ReplicatedDataPlane:
                 s = self.slots[k % len(self.slots)]
                 lo, hi = k * self.chunk, min(n, (k + 1) * self.chunk)
                 self._fused(s, lo, hi, pkts, inmeta)
-                works[k] = dist.all_to_all_single(s.recv, s.send, group=self.group, async_op=True)
+                works[k] = self._exchange(s)
             c = k - 1
             if c >= 0:
                 works.pop(c).wait()
@@ -160,7 +178,7 @@ class ReplicatedDataPlane:
         """Sum the per-GPU per-flow partials across ranks -> [slots, 2] (pkts, bytes) on every rank."""
         self.dp.harvest()
         t = torch.from_numpy(self.dp.flow_totals.view(np.int64).copy())
-        if self.gpu:
+        if self.gpu and not self.host_staged:
             t = t.to(self.dev)
         dist.all_reduce(t, group=self.group)
         return t.cpu().numpy().view(np.uint64)

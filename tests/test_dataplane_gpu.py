@@ -283,3 +283,28 @@ def test_host_path_pipeline_matches_oracle():
         assert np.array_equal(meta, rc.meta) and np.array_equal(out, rc.out)
     t = hp.timings_ms(0)
     assert t["total"] >= t["kernel"] > 0
+
+
+def test_bench_multirank_rehearsal_on_one_gpu():
+    """The N-GPU bench path end to end (torchrun, one process per rank, replicated tables, fused
+    REMOTE kernel, exchange, egress kernel, stats collectives) with 2 ranks sharing cuda:0 over
+    gloo (RCCL refuses two ranks on one device).  Every packet must be forwarded."""
+    import json
+    import os
+    import socket
+    import subprocess
+    import sys
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2", "--steps", "2",
+           "--warmup", "1", "--batch", str(1 << 16), "--flows", str(1 << 16), "--rehearse"]
+    r = subprocess.run(cmd, cwd=repo, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert line["n_gpus"] == 2 and line["forwarded_fraction"] == 1.0
+    assert line["config"]["global_batch"] == 2 << 16
