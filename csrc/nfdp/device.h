@@ -298,6 +298,44 @@ __device__ __forceinline__ void wave_frames_store(uint4* kx, const uint32_t* o, 
   }
 }
 
+// Coalesced store of the frames a wave sends to peers.  The lanes bound for one peer hold one
+// contiguous run of slots in that peer's segment (reserve_block hands out wave-contiguous
+// positions), so each run is written lane-contiguously, 16 packets per pass through the wave's
+// 1-KiB LDS scratch, instead of 4 x 16 B per lane at a 64-B stride.  `send` lanes only (their
+// `pos` < `cap`); segment d starts at byte d * seg_bytes, its slot 0 at +64.  EXEC must be full.
+template <int AUX>
+__device__ __forceinline__ void wave_segment_store(uint4* kx, const uint32_t* o, __amdgpu_buffer_rsrc_t r, bool send,
+                                                   uint32_t dest, uint32_t pos, uint32_t seg_bytes, uint32_t cap) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const unsigned long long lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+  unsigned long long pending = __ballot(send);
+  while (pending) {
+    const int leader = __ffsll((long long)pending) - 1;
+    const uint32_t d = __builtin_amdgcn_readlane(dest, leader);
+    const bool mine = send && dest == d;
+    const unsigned long long m = __ballot(mine);
+    pending &= ~m;
+    const uint32_t cnt = (uint32_t)__popcll(m);
+    const uint32_t p0 = __builtin_amdgcn_readlane(pos, leader);  // the leader has rank 0 in the run
+    const uint32_t rk = (uint32_t)__popcll(m & lt);
+    for (uint32_t sub = 0; sub < cnt; sub += 16) {
+      if (mine && rk >= sub && rk < sub + 16) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) kx[4u * (rk - sub) + k] = make_uint4(o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]);
+      }
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      const uint4 v = kx[lane];
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      const uint32_t n4 = min(16u, cnt - sub) * 4u;
+      const bool ok = lane < n4 && p0 + sub + (lane >> 2) < cap;
+      const v4u w = {v.x, v.y, v.z, v.w};
+      __builtin_amdgcn_raw_buffer_store_b128(w, r, ok ? lane * 16u : kNoRun, d * seg_bytes + 64u + (p0 + sub) * 64u, AUX);
+    }
+  }
+}
+
 // ---- multi-GPU output segments (shared by the fused REMOTE variant and the sharded stages) ----
 constexpr uint32_t kMaxRanks = 64;
 

@@ -160,6 +160,9 @@ __global__ __launch_bounds__(kFB, NFDP_FUSED_WAVES_PER_EU) void fused_kernel(Fus
   const __amdgpu_buffer_rsrc_t r_lat = __builtin_amdgcn_make_buffer_rsrc((void*)a.lat, (short)0,
                                                                           a.lat ? (int)(((a.n + 15u) >> 4) * 4u) : 0, kBufCfg);
   const uint32_t ctr_mask = min(a.t.bucket_mask * kBucketSlots + (kBucketSlots - 1), 4095u);
+  // REMOTE: the per-peer segments (< 2 GiB in all, checked at launch)
+  const __amdgpu_buffer_rsrc_t r_send = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.send_pkt, (short)0, REMOTE ? (int)(a.nranks * pkt_seg_bytes(a.cap_pkt)) : 0, kBufCfg);
   for (uint32_t base = blockIdx.x * kFB; base < a.n; base += stride) {
     const uint32_t i = base + threadIdx.x;
     const bool valid = i < a.n;
@@ -195,16 +198,15 @@ __global__ __launch_bounds__(kFB, NFDP_FUSED_WAVES_PER_EU) void fused_kernel(Fus
     const EgressDecision e = chain_stage(a.t, ta, p, st, hit, act, acl_rule, hash);
     bool to_peer = false;
     uint32_t reason = e.reason;
-    uint4* dst = a.out + (size_t)i * 4;
+    uint32_t eg = 0, pos = 0;
     if constexpr (REMOTE) {
       // egress GPU of the frame; block-aggregated slot in that GPU's segment (all threads call)
-      const uint32_t eg = e.reason ? a.rank : (uint32_t)ta.port(e.out_port).gpu;
+      eg = e.reason ? a.rank : (uint32_t)ta.port(e.out_port).gpu;
       const bool remote = valid && !e.reason && eg != a.rank && eg < a.nranks;
-      const uint32_t pos = reserve_block(a.pcnt, eg, remote, a.nranks, rcnt, rbase);
+      pos = reserve_block(a.pcnt, eg, remote, a.nranks, rcnt, rbase);
       if (remote) {
         if (pos < a.cap_pkt) {
           uint8_t* segp = a.send_pkt + (size_t)eg * pkt_seg_bytes(a.cap_pkt);
-          dst = reinterpret_cast<uint4*>(segp + 64 + (size_t)pos * 64);
           reinterpret_cast<uint32_t*>(segp + pkt_meta_off(a.cap_pkt))[pos] =
               make_meta(e.out_port, p.len + (e.push ? 4u : 0u), kOk, e.mirror != 0);
           to_peer = true;
@@ -251,10 +253,7 @@ __global__ __launch_bounds__(kFB, NFDP_FUSED_WAVES_PER_EU) void fused_kernel(Fus
     } else {
       if (hit && a.flow_ctr && !(a.flags & 4u)) atomicAdd(a.flow_ctr + slot, ctr_inc(st.wire_len));
       // frames for a peer: per lane into its segment slot; local frames: coalesced into out[]
-      if (to_peer) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) dst[q] = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
-      }
+      wave_segment_store<kStreamAux>(kx, o, r_send, to_peer, eg, pos, (uint32_t)pkt_seg_bytes(a.cap_pkt), a.cap_pkt);
       wave_frames_store<kStreamAux>(kx, o, r_out, run_of(base), __ballot(to_peer));
       if (valid) {
         a.out_meta[i] = meta;
@@ -311,7 +310,8 @@ static hipError_t launch_fused_t(const FusedArgs& a, int num_cus, hipStream_t s)
   constexpr size_t kMaxDyn = 160 * 1024 - kStatic;
   const size_t lds = lds_layout(H, A, a.acl_tiles).total;
   if (lds > kMaxDyn) return hipErrorInvalidValue;
-  if (R && (a.nranks == 0 || a.nranks > kMaxRanks || a.rank >= a.nranks || !a.send_pkt || !a.pcnt))
+  if (R && (a.nranks == 0 || a.nranks > kMaxRanks || a.rank >= a.nranks || !a.send_pkt || !a.pcnt ||
+            (size_t)a.nranks * pkt_seg_bytes(a.cap_pkt) >= (1ull << 31) || a.n >= (1u << 25)))
     return hipErrorInvalidValue;
   // the 1-GPU variant's fixed-count tail: buffer views need n * 64 B < 2 GiB and a counter table
   if (!R && (a.n >= (1u << 25) || !a.flow_ctr || !a.out_meta)) return hipErrorInvalidValue;

@@ -76,7 +76,7 @@ class ReplicatedDataPlane:
         self.acl_mode = dp.acl_mode
         # gloo with device buffers (the 1-GPU rehearsal of the N-GPU path: every rank on one card):
         # the exchange is staged through host memory.  RCCL exchanges device buffers directly.
-        self.host_staged = self.gpu and dist.get_backend(group) == "gloo"
+        self.host_staged = self.gpu and dist.is_initialized() and dist.get_backend(group) == "gloo"
 
     @staticmethod
     def _p(t) -> int:
