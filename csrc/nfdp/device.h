@@ -150,14 +150,29 @@ struct LdsTables {
   const uint8_t* lperm;
   uint32_t nport, nchain;
   bool lds_perm;
-  __device__ __forceinline__ PortEntry port(uint32_t i) const { return i < nport ? lport[i] : t.ports[i]; }
+  // Each accessor reads LDS with ds_read and takes the global fallback behind a wave-uniform
+  // branch.  A per-lane `lds ? lptr[i] : gptr[i]` select makes the compiler merge the two
+  // pointers into one generic pointer and issue FLAT loads, which count against vmcnt AND
+  // lgkmcnt: every table read then waited for the in-flight frame prefetch and stores.
+  __device__ __forceinline__ PortEntry port(uint32_t i) const {
+    if (nport == 0) return t.ports[i];
+    PortEntry pe = lport[i < nport ? i : 0u];
+    if (__builtin_expect(__any(i >= nport), 0)) {
+      if (i >= nport) pe = t.ports[i];
+    }
+    return pe;
+  }
   __device__ __forceinline__ uint64_t chain_word(uint32_t c) const {
-    if (c < nchain) return lchain[c];
-    return c < t.n_chains ? *reinterpret_cast<const uint64_t*>(&t.chains[c]) : 0ull;
+    uint64_t w = nchain ? lchain[c < nchain ? c : 0u] : 0ull;
+    if (__builtin_expect(__any(c >= nchain), 0)) {
+      if (c >= nchain) w = c < t.n_chains ? *reinterpret_cast<const uint64_t*>(&t.chains[c]) : 0ull;
+    }
+    return w;
   }
   __device__ __forceinline__ bool permit(int r) const {
     if (r < 0) return t.acl_default_permit != 0;
-    return (lds_perm ? lperm[r] : t.acl_permit[r]) != 0;
+    if (lds_perm) return lperm[r] != 0;
+    return t.acl_permit[r] != 0;
   }
 };
 
