@@ -205,6 +205,31 @@ def main() -> None:
         arr = torch.stack(g).cpu().numpy()
         p50, p99, fwd_local = float(np.median(arr[:, 0])), float(np.max(arr[:, 1])), float(np.mean(arr[:, 2]))
 
+    # exchange alone (outside the timed region, N > 1 replicated): the step's all-to-alls with no
+    # compute around them -> achieved xGMI bandwidth per GPU and the exchange floor of a step
+    xchg = None
+    if replicated:
+        s0 = eng.slots[0]
+        for _ in range(3):
+            eng._exchange(s0).wait()
+        torch.cuda.synchronize()
+        dist.barrier()
+        reps = 10
+        t1 = time.perf_counter()
+        for _ in range(reps):
+            eng._exchange(s0).wait()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t1
+        tt = torch.tensor([el], dtype=torch.float64, device=cdev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt.item())
+        n_chunks = (a.batch + eng.chunk - 1) // eng.chunk
+        peer_bytes = (world - 1) * eng.pseg  # what one GPU sends over its links per all-to-all
+        xchg = {"a2a_ms": round(el / reps * 1e3, 4), "a2a_per_step": n_chunks,
+                "exchange_ms_per_step": round(el / reps * n_chunks * 1e3, 4),
+                "xgmi_bytes_out_per_gpu_per_step": peer_bytes * n_chunks,
+                "xgmi_gbps_out_per_gpu": round(peer_bytes / (el / reps) / 1e9, 1)}
+
     # small-batch latency probe (outside the timed region): 64K packets per step, fused/sharded alike
     p50_small = None
     if not a.no_lowlat and a.io == "device":
@@ -295,6 +320,7 @@ def main() -> None:
             # persistent ring kernel: 64-packet chunks, host-clock publish -> completion RTT
             "p50_latency_us_ring": None if not ring or "p50_us" not in ring else ring["p50_us"],
             "ring": ring,
+            "exchange": xchg,
             "forwarded_fraction": round(fwd_local, 6),
             "flows": a.flows,
             "batch_per_gpu": a.batch,

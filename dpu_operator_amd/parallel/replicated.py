@@ -109,6 +109,7 @@ class ReplicatedDataPlane:
         self.nf.shard_egress(eg, self.gpu, self.dp.num_cus, self._stream())
 
     def _exchange(self, s: _Slot):
+        """Start the all-to-all of one chunk's segments; returns a handle with wait()."""
         if not self.host_staged:
             return dist.all_to_all_single(s.recv, s.send, group=self.group, async_op=True)
         recv = torch.empty(s.recv.shape, dtype=s.recv.dtype)

@@ -308,3 +308,4 @@ def test_bench_multirank_rehearsal_on_one_gpu():
     line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
     assert line["n_gpus"] == 2 and line["forwarded_fraction"] == 1.0
     assert line["config"]["global_batch"] == 2 << 16
+    assert line["exchange"]["a2a_per_step"] >= 1 and line["exchange"]["xgmi_bytes_out_per_gpu_per_step"] > 0
