@@ -29,7 +29,25 @@ __device__ __forceinline__ uint32_t pick4(uint32_t g, uint32_t a, uint32_t b, ui
   return g == 0 ? a : g == 1 ? b : g == 2 ? c : d;
 }
 
+// 8 bits -> 8 FP4 (e2m1) nibbles: bit i -> nibble i = 1.0 (0x2) or 0.0.  Shift-and-mask spread
+// (a multiply spread would carry between overlapping copies at nibble pitch).
+__device__ __forceinline__ uint32_t spread8_fp4(uint32_t n) {
+  uint32_t x = (n | (n << 12)) & 0x000F000Fu;
+  x = (x | (x << 6)) & 0x03030303u;
+  return ((x << 1) | (x << 4)) & 0x22222222u;
+}
+typedef int v8i_t __attribute__((ext_vector_type(8)));
+typedef float v4f_t __attribute__((ext_vector_type(4)));
+constexpr int kE8M0One = 0x7F7F7F7F;  // block scales 2^0 (every byte)
+
 // Wave-level classification over the wave's 64 packets (one per lane).  EXEC must be full.
+// ACL (TCAM) on the gfx950 block-scaled FP4 MFMA: v_mfma_scale_f32_16x16x128_f8f6f4 with e2m1
+// operands covers the whole 128-bit key in ONE instruction per 16 rules x 16 packets (the i8
+// form needs two 16x16x64) at the same cycles: half the matrix time and half the B-operand
+// registers.  Rule weights {-1, 0, +1} and key bits {0, 1} are exact in e2m1, the FP32 sums
+// (|x| <= 128) are exact integers.  Lane l holds K = 32 (l >> 4) + j, j < 32, i.e. bit j of key
+// word l >> 4, as nibble j (tools/fp4_probe.hip pins the operand and C/D maps on exact data).
+// The MFMA Toeplitz hash keeps the i8 form (it needs the parity of integer sums).
 template <int HASH, int ACL>
 __device__ __forceinline__ void classify_wave(const FlowKey& key, uint4* kx, const v4i* lw,
                                               const v4i* lc, uint32_t acl_tiles, const v4i* lt,
@@ -40,7 +58,8 @@ __device__ __forceinline__ void classify_wave(const FlowKey& key, uint4* kx, con
   // one chunk's ACL); best_out: the raw (mismatch << 10 | rule) minimum, for combining partials.
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t g = lane >> 4, col = lane & 15u;
-  v4i bf[4][2];
+  v4i bf[4][2];   // i8 B operands (MFMA hash)
+  v4i bq[4];      // FP4 B operands (MFMA ACL)
   if constexpr (HASH == kHashMfma || ACL == kAclMfma) {
     kx[lane] = make_uint4(key.src_ip, key.dst_ip, key.ports, key.meta);
     __builtin_amdgcn_wave_barrier();
@@ -48,10 +67,19 @@ __device__ __forceinline__ void classify_wave(const FlowKey& key, uint4* kx, con
 #pragma unroll
     for (int tt = 0; tt < 4; ++tt) {
       const uint32_t* src = reinterpret_cast<const uint32_t*>(kx + 16 * tt + col);
-      const uint32_t wlo = src[g >> 1], whi = src[2 + (g >> 1)];
-      const uint32_t sh = 16u * (g & 1u);
-      bf[tt][0] = expand16((wlo >> sh) & 0xFFFFu);
-      bf[tt][1] = expand16((whi >> sh) & 0xFFFFu);
+      if constexpr (HASH == kHashMfma) {
+        const uint32_t wlo = src[g >> 1], whi = src[2 + (g >> 1)];
+        const uint32_t sh = 16u * (g & 1u);
+        bf[tt][0] = expand16((wlo >> sh) & 0xFFFFu);
+        bf[tt][1] = expand16((whi >> sh) & 0xFFFFu);
+      }
+      if constexpr (ACL == kAclMfma) {
+        const uint32_t w = src[g];
+        bq[tt][0] = (int)spread8_fp4(w & 0xFFu);
+        bq[tt][1] = (int)spread8_fp4((w >> 8) & 0xFFu);
+        bq[tt][2] = (int)spread8_fp4((w >> 16) & 0xFFu);
+        bq[tt][3] = (int)spread8_fp4(w >> 24);
+      }
     }
   }
   // ---- hash ----
@@ -89,29 +117,30 @@ __device__ __forceinline__ void classify_wave(const FlowKey& key, uint4* kx, con
   if constexpr (ACL == kAclMfma) {
     uint32_t best[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
     for (uint32_t nt = tile0; nt < acl_tiles; nt += tstep) {
-      const v4i a0 = lw[(nt * 2 + 0) * 64 + lane], a1 = lw[(nt * 2 + 1) * 64 + lane];
-      const v4i c = lc[nt * 4 + g];
+      const v4i a4 = lw[nt * 64 + lane];
+      const v8i_t a = {a4[0], a4[1], a4[2], a4[3], 0, 0, 0, 0};
+      const v4i ci = lc[nt * 4 + g];
+      const v4f_t c = {__int_as_float(ci[0]), __int_as_float(ci[1]), __int_as_float(ci[2]), __int_as_float(ci[3])};
       // Pass 1: does ANY packet of the wave match ANY rule of this tile?  (mismatch counts are
       // >= 0, so a zero minimum = a match.)  Most tiles of a deny-list ACL match nothing, and
-      // then the priority epilogue below — 10 VALU per 16 packets — is skipped wave-uniformly.
-      uint32_t z = 0xFFFFFFFFu;
+      // then the priority epilogue below is skipped wave-uniformly.
+      float z = 1.0e30f;
 #pragma unroll
       for (int tt = 0; tt < 4; ++tt) {
-        v4i acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a0, bf[tt][0], c, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a1, bf[tt][1], acc, 0, 0, 0);
-        z = min(z, min(min((uint32_t)acc[0], (uint32_t)acc[1]), min((uint32_t)acc[2], (uint32_t)acc[3])));
+        const v8i_t b = {bq[tt][0], bq[tt][1], bq[tt][2], bq[tt][3], 0, 0, 0, 0};
+        const v4f_t acc = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 4, 4, 0, kE8M0One, 0, kE8M0One);
+        z = fminf(z, fminf(fminf(acc[0], acc[1]), fminf(acc[2], acc[3])));
       }
-      if (!__any(z == 0u)) continue;
+      if (!__any(z == 0.0f)) continue;
       // Pass 2 (rare): recompute the tile with the (mismatch << 10 | rule) first-match epilogue.
-      // The bias goes through an opaque copy so the MFMAs are not CSE'd with pass 1 (keeping
-      // pass-1 accumulators alive would cost 16 VGPRs at the kernel's register peak).
-      v4i c2 = c;
+      // The bias goes through an opaque copy so the MFMAs are not CSE'd with pass 1.
+      v4f_t c2 = c;
       asm volatile("" : "+v"(c2));
       const uint32_t rb = nt * 16u + 4u * g;
 #pragma unroll
       for (int tt = 0; tt < 4; ++tt) {
-        v4i acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a0, bf[tt][0], c2, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_i32_16x16x64_i8(a1, bf[tt][1], acc, 0, 0, 0);
+        const v8i_t b = {bq[tt][0], bq[tt][1], bq[tt][2], bq[tt][3], 0, 0, 0, 0};
+        const v4f_t acc = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c2, 4, 4, 0, kE8M0One, 0, kE8M0One);
         const uint32_t e0 = ((uint32_t)acc[0] << 10) | (rb + 0);
         const uint32_t e1 = ((uint32_t)acc[1] << 10) | (rb + 1);
         const uint32_t e2 = ((uint32_t)acc[2] << 10) | (rb + 2);

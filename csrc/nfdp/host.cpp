@@ -116,9 +116,12 @@ std::vector<std::pair<int64_t, int64_t>> FlowTableHost::take_moves() {
 }
 
 // ------------------------------------------------------------------------------------------
-// Classification tables in MFMA fragment layout.
-// A operand of v_mfma_i32_16x16x64_i8: lane l holds row (l & 15), k = 16*(l >> 4) + j, j<16.
-// k-step s covers key bits [64 s, 64 s + 64); key bit b = LSB-first over the 4 LE dwords.
+// ACL (TCAM) tables in the layout of the FP4 MFMA A operand (device.h classify_wave):
+// v_mfma_scale_f32_16x16x128_f8f6f4, e2m1: lane l holds rule row (l & 15) of the tile and
+// K = 32 (l >> 4) + j for j < 32 as nibble j (little-endian nibbles of 4 dwords); K = key bit,
+// LSB-first over the 4 LE key dwords.  Weights: cared bit set -> -1.0 (0xA), cared bit clear ->
+// +1.0 (0x2), don't care -> 0.  C init = the rule's count of cared set bits (f32 bits), so
+// mismatch = bias + sum(w * bit) is 0 exactly on a ternary match.
 // ------------------------------------------------------------------------------------------
 static inline int key_bit(const uint32_t* w, int b) { return (w[b >> 5] >> (b & 31)) & 1; }
 
@@ -128,28 +131,31 @@ AclFrags build_acl_frags(const uint32_t* value, const uint32_t* mask, uint32_t n
   f.tiles = (n + 15) / 16;
   if (f.tiles == 0) f.tiles = 1;
   const uint32_t npad = f.tiles * 16;
-  f.wfrag.assign((size_t)f.tiles * 2 * 64 * 16, 0);
+  f.wfrag.assign((size_t)f.tiles * 64 * 16, 0);
   f.cinit.assign((size_t)f.tiles * 16, 0);
-  std::vector<int32_t> bias(npad, 1);  // padded rules never match (mismatch >= 1)
+  std::vector<float> bias(npad, 1.0f);  // padded rules never match (mismatch >= 1)
   for (uint32_t r = 0; r < n; ++r) {
     int32_t bb = 0;
     for (int b = 0; b < 128; ++b)
       if (key_bit(mask + 4 * r, b) && key_bit(value + 4 * r, b)) ++bb;
-    bias[r] = bb;
+    bias[r] = (float)bb;
   }
   for (uint32_t nt = 0; nt < f.tiles; ++nt)
-    for (int s = 0; s < 2; ++s)
-      for (int l = 0; l < 64; ++l)
-        for (int j = 0; j < 16; ++j) {
-          const uint32_t r = nt * 16 + (l & 15);
-          const int b = 64 * s + 16 * (l >> 4) + j;
-          int8_t w = 0;
-          if (r < n && key_bit(mask + 4 * r, b)) w = key_bit(value + 4 * r, b) ? -1 : 1;
-          f.wfrag[(((size_t)nt * 2 + s) * 64 + l) * 16 + j] = w;
-        }
+    for (int l = 0; l < 64; ++l)
+      for (int j = 0; j < 32; ++j) {
+        const uint32_t r = nt * 16 + (l & 15);
+        const int b = 32 * (l >> 4) + j;
+        uint8_t w = 0;
+        if (r < n && key_bit(mask + 4 * r, b)) w = key_bit(value + 4 * r, b) ? 0xA : 0x2;
+        uint8_t& byte = reinterpret_cast<uint8_t&>(f.wfrag[((size_t)nt * 64 + l) * 16 + j / 2]);
+        byte = (uint8_t)(byte | (w << (4 * (j & 1))));
+      }
   for (uint32_t nt = 0; nt < f.tiles; ++nt)
     for (int g = 0; g < 4; ++g)
-      for (int r = 0; r < 4; ++r) f.cinit[((size_t)nt * 4 + g) * 4 + r] = bias[nt * 16 + 4 * g + r];
+      for (int r = 0; r < 4; ++r) {
+        const float v = bias[nt * 16 + 4 * g + r];
+        std::memcpy(&f.cinit[((size_t)nt * 4 + g) * 4 + r], &v, 4);
+      }
   return f;
 }
 

@@ -48,8 +48,8 @@ class FlowTableHost {
 
 // Device-layout classification tables.
 struct AclFrags {
-  std::vector<int8_t> wfrag;   // [tiles][2][64][16]
-  std::vector<int32_t> cinit;  // [tiles][4][4]
+  std::vector<int8_t> wfrag;   // [tiles][64][16]: FP4 (e2m1) A fragments, 32 nibbles per lane
+  std::vector<int32_t> cinit;  // [tiles][4][4]: f32 bit patterns of the rule biases
   uint32_t tiles = 0;
 };
 AclFrags build_acl_frags(const uint32_t* value, const uint32_t* mask, uint32_t n);

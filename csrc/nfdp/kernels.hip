@@ -65,7 +65,7 @@ struct LdsLayout {
 __host__ __device__ inline LdsLayout lds_layout(int hash_mode, int acl_mode, uint32_t acl_tiles) {
   LdsLayout L;
   size_t o = 0;
-  L.acl_w = o; if (acl_mode == kAclMfma) o += (size_t)acl_tiles * 2 * 64 * 16;
+  L.acl_w = o; if (acl_mode == kAclMfma) o += (size_t)acl_tiles * 64 * 16;
   L.acl_c = o; if (acl_mode == kAclMfma) o += (size_t)acl_tiles * 4 * 16;
   L.toep_f = o; if (hash_mode == kHashMfma) o += 2 * 2 * 64 * 16;
   L.toep_t = o; if (hash_mode == kHashLds) o += 16 * 256 * 4;
@@ -117,7 +117,7 @@ __global__ __launch_bounds__(kFB, NFDP_FUSED_WAVES_PER_EU) void fused_kernel(Fus
 
   // ---- stage classification tables + zero counters ----
   if constexpr (ACL == kAclMfma) {
-    const uint32_t nw = a.acl_tiles * 2 * 64, nc = a.acl_tiles * 4;
+    const uint32_t nw = a.acl_tiles * 64, nc = a.acl_tiles * 4;
     for (uint32_t i = threadIdx.x; i < nw; i += kFB) lw[i] = a.acl_wfrag[i];
     for (uint32_t i = threadIdx.x; i < nc; i += kFB) lc[i] = a.acl_cinit[i];
   }

@@ -63,7 +63,7 @@ __device__ __forceinline__ void flush_lds_counters(uint32_t* pc, uint32_t* drops
 __host__ __device__ inline RingLds ring_lds(int hash_mode, int acl_mode, uint32_t acl_tiles) {
   RingLds L;
   size_t o = 0;
-  L.acl_w = o; if (acl_mode == kAclMfma) o += (size_t)acl_tiles * 2 * 64 * 16;
+  L.acl_w = o; if (acl_mode == kAclMfma) o += (size_t)acl_tiles * 64 * 16;
   L.acl_c = o; if (acl_mode == kAclMfma) o += (size_t)acl_tiles * 4 * 16;
   L.toep_f = o; if (hash_mode == kHashMfma) o += 2 * 2 * 64 * 16;
   L.toep_t = o; if (hash_mode == kHashLds) o += 16 * 256 * 4;
@@ -143,7 +143,7 @@ __global__ __launch_bounds__(kRingBlock) void ring_kernel(RingArgs a) {
   v4i* lt = reinterpret_cast<v4i*>(smem + L.toep_f);
   uint32_t* ltab = reinterpret_cast<uint32_t*>(smem + L.toep_t);
   if constexpr (ACL == kAclMfma) {
-    const uint32_t nw = a.acl_tiles * 2 * 64, nc = a.acl_tiles * 4;
+    const uint32_t nw = a.acl_tiles * 64, nc = a.acl_tiles * 4;
     for (uint32_t i = threadIdx.x; i < nw; i += kRingBlock) lw[i] = a.acl_wfrag[i];
     for (uint32_t i = threadIdx.x; i < nc; i += kRingBlock) lc[i] = a.acl_cinit[i];
   }

@@ -10,7 +10,7 @@ struct ShardLds {
 __host__ __device__ inline ShardLds shard_lds(int hash_mode, int acl_mode, uint32_t acl_tiles, bool ports) {
   ShardLds L;
   size_t o = 0;
-  L.acl_w = o; if (acl_mode == kAclMfma) o += (size_t)acl_tiles * 2 * 64 * 16;
+  L.acl_w = o; if (acl_mode == kAclMfma) o += (size_t)acl_tiles * 64 * 16;
   L.acl_c = o; if (acl_mode == kAclMfma) o += (size_t)acl_tiles * 4 * 16;
   L.toep_f = o; if (hash_mode == kHashMfma) o += 2 * 2 * 64 * 16;
   L.toep_t = o; if (hash_mode == kHashLds) o += 16 * 256 * 4;
@@ -36,7 +36,7 @@ __global__ __launch_bounds__(kBlock) void ingress_kernel(IngressArgs a) {
   if constexpr (ACL == kAclMfma) {
     const v4i* gw = reinterpret_cast<const v4i*>(a.acl_wfrag);
     const v4i* gc = reinterpret_cast<const v4i*>(a.acl_cinit);
-    for (uint32_t i = threadIdx.x; i < a.acl_tiles * 128; i += kBlock) lw[i] = gw[i];
+    for (uint32_t i = threadIdx.x; i < a.acl_tiles * 64; i += kBlock) lw[i] = gw[i];
     for (uint32_t i = threadIdx.x; i < a.acl_tiles * 4; i += kBlock) lc[i] = gc[i];
   }
   if constexpr (HASH == kHashMfma) {

@@ -59,18 +59,22 @@ def test_acl_fragments_emulated(nf):
     val = rng.integers(0, 2**32, (n, 4), dtype=np.uint64).astype(np.uint32)
     msk = (rng.integers(0, 2**32, (n, 4), dtype=np.uint64) & rng.integers(0, 2**32, (n, 4), dtype=np.uint64)).astype(np.uint32)
     w, c, tiles = nf.build_acl_frags(val, msk)
-    w = w.reshape(tiles, 2, 64, 16).astype(np.int64)
-    c = c.reshape(tiles, 4, 4)
+    # FP4 (e2m1) A fragments of v_mfma_scale_f32_16x16x128_f8f6f4: lane l, nibble j = K 32(l>>4)+j
+    w = w.view(np.uint8).reshape(tiles, 64, 16)
+    nib = np.stack([w & 0xF, w >> 4], axis=-1).reshape(tiles, 64, 32)
+    e2m1 = {0x0: 0, 0x2: 1, 0xA: -1}
+    assert set(np.unique(nib).tolist()) <= set(e2m1)
+    val_of = np.vectorize(e2m1.get)(nib).astype(np.int64)
+    c = c.view(np.float32).reshape(tiles, 4, 4)
     W = np.zeros((128, tiles * 16), np.int64)
     bias = np.zeros(tiles * 16, np.int64)
     for nt in range(tiles):
-        for s in range(2):
-            for l in range(64):
-                for j in range(16):
-                    W[64 * s + 16 * (l >> 4) + j, nt * 16 + (l & 15)] = w[nt, s, l, j]
+        for l in range(64):
+            for j in range(32):
+                W[32 * (l >> 4) + j, nt * 16 + (l & 15)] = val_of[nt, l, j]
         for g in range(4):
             for r in range(4):
-                bias[nt * 16 + 4 * g + r] = c[nt, g, r]
+                bias[nt * 16 + 4 * g + r] = int(c[nt, g, r])
     keys = np.concatenate([val & msk, rng.integers(0, 2**32, (200, 4), dtype=np.uint64).astype(np.uint32)])
     bits = ((keys[:, :, None] >> np.arange(32, dtype=np.uint32)) & 1).reshape(len(keys), 128).astype(np.int64)
     mism = bits @ W + bias
