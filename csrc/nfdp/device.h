@@ -250,6 +250,73 @@ __device__ __forceinline__ int64_t flow_probe(const TablesView& t, const FlowKey
   return -1;
 }
 
+// Wave-cooperative first-bucket probe.  Instead of every lane fetching its own 128-B bucket as
+// 8 x 16 B (each dwordx4 instruction touching 64 different lines), 8 lanes fetch one bucket:
+// instruction j brings the first-choice buckets of packets 8j..8j+7, 8 whole lines.  Lane L of
+// instruction j holds chunk L & 7 (even = slot key, odd = slot action) of packet 8j + (L >> 3)'s
+// bucket, compares key chunks against that packet's key (read from the wave's LDS scratch), and
+// the matching slot's action lane hands its chunk over through the same scratch.  Packets with
+// no match in the first bucket probe the second one per lane (flow_probe's tail; rare at the
+// table's <= 50 % load).  Same results as flow_probe.  `probe` false -> slot -1.  EXEC full.
+__device__ __forceinline__ int64_t flow_probe_wave(const TablesView& t, const FlowKey& k, uint32_t h, bool probe,
+                                                   uint4* kx, uint4& act) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t c = lane & 7u, q = lane >> 3;
+  const uint32_t b1 = h & t.bucket_mask;
+  const uint4* fl = reinterpret_cast<const uint4*>(t.flows);
+  // key as stored (meta | used); a non-probing packet gets a w no slot can hold
+  kx[lane] = make_uint4(k.src_ip, k.dst_ip, k.ports, probe ? (k.meta | kSlotUsed) : 0xFFFFFFFFu);
+  uint4 v[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const uint32_t bj = (uint32_t)__shfl((int)b1, 8 * j + (int)q);
+    v[j] = fl[(size_t)bj * (kBucketSlots * 2) + c];
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  unsigned long long m[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const uint4 kk = kx[8 * j + q];
+    const bool hit = !(c & 1u) && v[j].x == kk.x && v[j].y == kk.y && v[j].z == kk.z && v[j].w == kk.w;
+    m[j] = __ballot(hit);
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  // the action lane (key lane + 1) of a matching slot writes packet 8j + q's action
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+    if ((c & 1u) && ((m[j] >> (lane - 1)) & 1ull)) kx[8 * j + q] = v[j];
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  // this lane's packet is 8 (lane >> 3) + (lane & 7): its bits are byte (lane & 7) of m[lane >> 3]
+  unsigned long long mine = 0;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) mine = (q == (uint32_t)j) ? m[j] : mine;
+  const uint32_t sel = (uint32_t)(mine >> (8u * c)) & 0x55u;
+  int64_t slot = -1;
+  if (sel) {
+    act = kx[lane];
+    slot = (int64_t)b1 * kBucketSlots + (__builtin_ctz(sel) >> 1);
+  } else if (probe) {
+    // second choice, per lane (the first bucket missed)
+    const TableHash th = table_hash(h, t.bucket_mask);
+    const uint4* row = fl + (size_t)th.b2 * (kBucketSlots * 2);
+    const uint32_t used = k.meta | kSlotUsed;
+    auto eq = [&](const uint4& e) { return e.x == k.src_ip && e.y == k.dst_ip && e.z == k.ports && e.w == used; };
+    const uint4 k0 = row[0], a0 = row[1], k1 = row[2], a1 = row[3];
+    const uint4 k2 = row[4], a2 = row[5], k3 = row[6], a3 = row[7];
+    const bool n0 = eq(k0), n1 = eq(k1), n2 = eq(k2), n3 = eq(k3);
+    if (n0 | n1 | n2 | n3) {
+      act = n0 ? a0 : n1 ? a1 : n2 ? a2 : a3;
+      slot = (int64_t)th.b2 * kBucketSlots + (n0 ? 0 : n1 ? 1 : n2 ? 2 : 3);
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  return slot;
+}
+
 // Sum of a u32 over the 64 lanes (EXEC must be full): two quad permutes and two row rotates
 // leave every lane of a 16-lane row holding the row sum (DPP: no LDS crossbar round trips), then
 // four readlanes add the rows.

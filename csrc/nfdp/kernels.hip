@@ -186,9 +186,15 @@ __global__ __launch_bounds__(kFB, NFDP_FUSED_WAVES_PER_EU) void fused_kernel(Fus
     bool hit = false;
     FlowAction act = {};
     int64_t slot = -1;
+#ifndef NFDP_LANE_PROBE
+    {
+      uint4 v;
+      slot = flow_probe_wave(a.t, st.key, hash, !st.reason && p.ipv4, kx, v);
+#else
     if (!st.reason && p.ipv4) {
       uint4 v;
       slot = flow_probe(a.t, st.key, hash, v);
+#endif
       if (slot >= 0) {
         hit = true;
         act.chain_id = v.x & 0xFFFFu; act.out_port = v.x >> 16; act.nat_ip = v.y;
