@@ -302,7 +302,7 @@ def main() -> None:
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "uint8 packets / int8 MFMA classify",
+            "dtype": "uint8 packets / FP4 (e2m1) MFMA ACL classify",
             "data": "synthetic (random 1M-flow table, random pod->pod 5-tuples, 64B frames)",
             "config": {
                 "model": f"1M-flow SFC: acl({a.acl} TCAM rules)->snat->l2fwd, 64B frames, {a.pods_per_gpu} pods/GPU",

@@ -454,12 +454,17 @@ constexpr uint32_t kMaxRanks = 64;
 // wave and destination), then ONE global atomic per (workgroup iteration, destination) turns
 // them into segment positions.  (A per-wave global atomic on one counter serialised 16K waves
 // per 1M packets: 200 us of a 1M-packet ingress pass.)  Called by every thread of the block.
+// Double-buffered use in a loop (`lnext` != nullptr): `lcnt` arrives zeroed (the previous call
+// zeroed it as its `lnext`; zero both before the loop), and this call zeroes `lnext` while it
+// publishes the bases, which saves the leading barrier: two per call instead of three.
 __device__ __forceinline__ uint32_t reserve_block(uint32_t* gcnt, uint32_t dest, bool active, uint32_t nranks,
-                                                  uint32_t* lcnt, uint32_t* lbase) {
+                                                  uint32_t* lcnt, uint32_t* lbase, uint32_t* lnext = nullptr) {
   const uint32_t lane = threadIdx.x & 63u;
   const unsigned long long lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-  if (threadIdx.x < nranks) lcnt[threadIdx.x] = 0;
-  __syncthreads();
+  if (!lnext) {
+    if (threadIdx.x < nranks) lcnt[threadIdx.x] = 0;
+    __syncthreads();
+  }
   uint32_t off = 0;
   for (uint32_t o = 0; o < nranks; ++o) {
     const unsigned long long m = __ballot(active && dest == o);
@@ -474,6 +479,7 @@ __device__ __forceinline__ uint32_t reserve_block(uint32_t* gcnt, uint32_t dest,
   if (threadIdx.x < nranks) {
     const uint32_t c = lcnt[threadIdx.x];
     lbase[threadIdx.x] = c ? atomicAdd(&gcnt[threadIdx.x], c) : 0u;
+    if (lnext) lnext[threadIdx.x] = 0;
   }
   __syncthreads();
   return active ? lbase[dest] + off : 0xFFFFFFFFu;

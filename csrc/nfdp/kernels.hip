@@ -4,14 +4,16 @@
 //  * one packet per lane, 8 waves per workgroup, grid sized to the CU count x the LDS-admitted
 //    blocks per CU, grid-stride over the batch; a wave's 64 slots are one 4-KiB run moved with
 //    lane-contiguous dwordx4 loads/stores and transposed through LDS (coalesced frame I/O);
-//  * classification is ONE int8 MFMA GEMM over the bit-expanded 128-bit FlowKey:
-//      - Toeplitz RSS hash = GF(2) product  key_bits[16 pkts x 128] x T[128 x 32], parity (&1)
+//  * classification is MFMA GEMMs over the bit-expanded 128-bit FlowKey (rules / hash bits are
+//    the M rows, 16 packets the N columns, fragments staged once per workgroup in LDS):
 //      - TCAM / priority ACL = key_bits x W[128 x R] + bias, W in {-1,0,+1}; a rule matches
-//        iff its mismatch count is 0; first match by min((mismatch << 10) | rule)
-//    (v_mfma_i32_16x16x64_i8; rules/hash bits are the M rows, 16 packets the N columns), with
-//    the rule fragments staged once per workgroup in LDS;
+//        iff its mismatch count is 0; first match by min((mismatch << 10) | rule); block-scaled
+//        FP4 v_mfma_scale_f32_16x16x128_f8f6f4, the whole key in one instruction (device.h)
+//      - Toeplitz RSS hash = LDS byte tables, or GF(2) product key_bits x T[128 x 32] with
+//        parity (&1) on v_mfma_i32_16x16x64_i8
 //  * exact-match flow lookup: 2-choice cuckoo, a bucket = 4 x {16-B key, 16-B action} = one
-//    128-B line, so a hit in the first bucket is ONE dependent fetch (1M flows = 64 MB of HBM);
+//    128-B line fetched wave-cooperatively (8 lanes per line), so a hit in the first bucket is
+//    ONE dependent fetch (1M flows = 64 MB of HBM);
 //  * per-port counters aggregated in LDS, flushed once per workgroup; per-flow counters are one
 //    packed 64-bit atomic per packet.
 // The persistent low-latency variant of the same stages lives in ring.hip.
@@ -86,26 +88,10 @@ __host__ __device__ inline LdsLayout lds_layout(int hash_mode, int acl_mode, uin
 constexpr int kBufCfg = 0x00020000;  // buffer resource word 3 (gfx9 family raw buffer)
 constexpr int kStreamAux = 2;        // nt: frames are read once / written once (streaming)
 
-__device__ __forceinline__ void load_slot(const uint4* pk4, const uint32_t* inmeta, uint32_t i, uint32_t n,
-                                          uint32_t* d, uint32_t& im) {
-  if (i < n) {
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const uint4 v = pk4[(size_t)i * 4 + q];
-      d[4 * q] = v.x; d[4 * q + 1] = v.y; d[4 * q + 2] = v.z; d[4 * q + 3] = v.w;
-    }
-    im = inmeta[i];
-  } else {
-#pragma unroll
-    for (int q = 0; q < kSlotDwords; ++q) d[q] = 0;
-    im = 0;
-  }
-}
-
 template <int HASH, int ACL, bool REMOTE>
 __global__ __launch_bounds__(kFB, NFDP_FUSED_WAVES_PER_EU) void fused_kernel(FusedArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  __shared__ uint32_t rcnt[REMOTE ? kMaxRanks : 1], rbase[REMOTE ? kMaxRanks : 1];
+  __shared__ uint32_t rcnt[REMOTE ? 2 * kMaxRanks : 1], rbase[REMOTE ? kMaxRanks : 1];  // rcnt double-buffered
   const LdsLayout L = lds_layout(HASH, ACL, a.acl_tiles);
   v4i* lw = reinterpret_cast<v4i*>(smem + L.acl_w);
   v4i* lc = reinterpret_cast<v4i*>(smem + L.acl_c);
@@ -127,6 +113,8 @@ __global__ __launch_bounds__(kFB, NFDP_FUSED_WAVES_PER_EU) void fused_kernel(Fus
     for (uint32_t i = threadIdx.x; i < 4096; i += kFB) ltab[i] = a.toep_tab[i];
   for (uint32_t i = threadIdx.x; i < kLdsPorts * 4; i += kFB) pc[i] = 0;
   if (threadIdx.x < kNumReasons) drops[threadIdx.x] = 0;
+  if constexpr (REMOTE)
+    if (threadIdx.x < 2 * kMaxRanks) rcnt[threadIdx.x] = 0;
   PortEntry* lport = reinterpret_cast<PortEntry*>(smem + L.tports);
   uint64_t* lchain = reinterpret_cast<uint64_t*>(smem + L.tchain);
   uint8_t* lperm = smem + L.tperm;
@@ -163,7 +151,8 @@ __global__ __launch_bounds__(kFB, NFDP_FUSED_WAVES_PER_EU) void fused_kernel(Fus
   // REMOTE: the per-peer segments (< 2 GiB in all, checked at launch)
   const __amdgpu_buffer_rsrc_t r_send = __builtin_amdgcn_make_buffer_rsrc(
       (void*)a.send_pkt, (short)0, REMOTE ? (int)(a.nranks * pkt_seg_bytes(a.cap_pkt)) : 0, kBufCfg);
-  for (uint32_t base = blockIdx.x * kFB; base < a.n; base += stride) {
+  uint32_t it = 0;  // loop iteration (REMOTE reservation buffers alternate)
+  for (uint32_t base = blockIdx.x * kFB; base < a.n; base += stride, ++it) {
     const uint32_t i = base + threadIdx.x;
     const bool valid = i < a.n;
     wave_frames_to_lanes(kx, cn, dn);
@@ -209,7 +198,8 @@ __global__ __launch_bounds__(kFB, NFDP_FUSED_WAVES_PER_EU) void fused_kernel(Fus
       // egress GPU of the frame; block-aggregated slot in that GPU's segment (all threads call)
       eg = e.reason ? a.rank : (uint32_t)ta.port(e.out_port).gpu;
       const bool remote = valid && !e.reason && eg != a.rank && eg < a.nranks;
-      pos = reserve_block(a.pcnt, eg, remote, a.nranks, rcnt, rbase);
+      pos = reserve_block(a.pcnt, eg, remote, a.nranks, rcnt + (it & 1u) * kMaxRanks, rbase,
+                          rcnt + (~it & 1u) * kMaxRanks);
       if (remote) {
         if (pos < a.cap_pkt) {
           uint8_t* segp = a.send_pkt + (size_t)eg * pkt_seg_bytes(a.cap_pkt);
@@ -312,7 +302,7 @@ size_t fused_lds_bytes(int hash_mode, int acl_mode, uint32_t acl_tiles) {
 template <int H, int A, bool R>
 static hipError_t launch_fused_t(const FusedArgs& a, int num_cus, hipStream_t s) {
   // static LDS (REMOTE reservation counters) + dynamic tables must fit 160 KiB
-  constexpr size_t kStatic = 2 * (R ? kMaxRanks : 1) * sizeof(uint32_t);
+  constexpr size_t kStatic = 3 * (R ? kMaxRanks : 1) * sizeof(uint32_t);  // rcnt[2][..] + rbase
   constexpr size_t kMaxDyn = 160 * 1024 - kStatic;
   const size_t lds = lds_layout(H, A, a.acl_tiles).total;
   if (lds > kMaxDyn) return hipErrorInvalidValue;
