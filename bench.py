@@ -211,13 +211,13 @@ def main() -> None:
     if replicated:
         s0 = eng.slots[0]
         for _ in range(3):
-            eng._exchange(s0).wait()
+            eng.exchange(s0).wait()
         torch.cuda.synchronize()
         dist.barrier()
         reps = 10
         t1 = time.perf_counter()
         for _ in range(reps):
-            eng._exchange(s0).wait()
+            eng.exchange(s0).wait()
         torch.cuda.synchronize()
         el = time.perf_counter() - t1
         tt = torch.tensor([el], dtype=torch.float64, device=cdev)

@@ -108,7 +108,7 @@ class ReplicatedDataPlane:
                   t0=p(self.t0) if self.gpu else 0, lat=p(s.lat2) if self.gpu else 0)
         self.nf.shard_egress(eg, self.gpu, self.dp.num_cus, self._stream())
 
-    def _exchange(self, s: _Slot):
+    def exchange(self, s: _Slot):
         """Start the all-to-all of one chunk's segments; returns a handle with wait()."""
         if not self.host_staged:
             return dist.all_to_all_single(s.recv, s.send, group=self.group, async_op=True)
@@ -134,7 +134,7 @@ class ReplicatedDataPlane:
                 s = self.slots[k % len(self.slots)]
                 lo, hi = k * self.chunk, min(n, (k + 1) * self.chunk)
                 self._fused(s, lo, hi, pkts, inmeta)
-                works[k] = self._exchange(s)
+                works[k] = self.exchange(s)
             c = k - 1
             if c >= 0:
                 works.pop(c).wait()
