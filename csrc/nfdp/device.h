@@ -274,26 +274,22 @@ __device__ __forceinline__ int64_t flow_probe_wave(const TablesView& t, const Fl
   }
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-  unsigned long long m[8];
+  // Per instruction j: compare, then the action lane of a matching slot overwrites packet
+  // 8j + q's scratch entry (its key is no longer needed: only instruction j reads it).  The
+  // packet lanes 8j..8j+7 take their match byte from this j's ballot (one mask live at a time).
+  uint32_t sel = 0;
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const uint4 kk = kx[8 * j + q];
     const bool hit = !(c & 1u) && v[j].x == kk.x && v[j].y == kk.y && v[j].z == kk.z && v[j].w == kk.w;
-    m[j] = __ballot(hit);
+    const unsigned long long m = __ballot(hit);
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    if ((c & 1u) && ((m >> (lane - 1)) & 1ull)) kx[8 * j + q] = v[j];
+    if (q == (uint32_t)j) sel = (uint32_t)(m >> (8u * c)) & 0x55u;
   }
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-  // the action lane (key lane + 1) of a matching slot writes packet 8j + q's action
-#pragma unroll
-  for (int j = 0; j < 8; ++j)
-    if ((c & 1u) && ((m[j] >> (lane - 1)) & 1ull)) kx[8 * j + q] = v[j];
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-  // this lane's packet is 8 (lane >> 3) + (lane & 7): its bits are byte (lane & 7) of m[lane >> 3]
-  unsigned long long mine = 0;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) mine = (q == (uint32_t)j) ? m[j] : mine;
-  const uint32_t sel = (uint32_t)(mine >> (8u * c)) & 0x55u;
   int64_t slot = -1;
   if (sel) {
     act = kx[lane];
