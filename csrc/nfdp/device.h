@@ -124,14 +124,23 @@ __device__ __forceinline__ void classify_wave(const FlowKey& key, uint4* kx, con
       // Pass 1: does ANY packet of the wave match ANY rule of this tile?  (mismatch counts are
       // >= 0, so a zero minimum = a match.)  Most tiles of a deny-list ACL match nothing, and
       // then the priority epilogue below is skipped wave-uniformly.
-      float z = 1.0e30f;
+      // Four independent accumulators: the MFMAs issue back to back instead of each waiting
+      // for the previous result.  The sums are non-negative integers and +0.0 exactly on a match
+      // (a -1 weight implies a bias >= 1, and x + (-x) rounds to +0), so the minimum is taken on
+      // the f32 bit patterns with integer min3 (no NaN canonicalization) and tested against 0.
+      v4f_t acc[4];
 #pragma unroll
       for (int tt = 0; tt < 4; ++tt) {
         const v8i_t b = {bq[tt][0], bq[tt][1], bq[tt][2], bq[tt][3], 0, 0, 0, 0};
-        const v4f_t acc = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 4, 4, 0, kE8M0One, 0, kE8M0One);
-        z = fminf(z, fminf(fminf(acc[0], acc[1]), fminf(acc[2], acc[3])));
+        acc[tt] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 4, 4, 0, kE8M0One, 0, kE8M0One);
       }
-      if (!__any(z == 0.0f)) continue;
+      uint32_t z = 0xFFFFFFFFu;
+#pragma unroll
+      for (int tt = 0; tt < 4; ++tt) {
+        z = min(z, min(__float_as_uint(acc[tt][0]), __float_as_uint(acc[tt][1])));
+        z = min(z, min(__float_as_uint(acc[tt][2]), __float_as_uint(acc[tt][3])));
+      }
+      if (!__any(z == 0u)) continue;
       // Pass 2 (rare): recompute the tile with the (mismatch << 10 | rule) first-match epilogue.
       // The bias goes through an opaque copy so the MFMAs are not CSE'd with pass 1.
       v4f_t c2 = c;
