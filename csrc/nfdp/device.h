@@ -116,6 +116,53 @@ __device__ __forceinline__ void classify_wave(const FlowKey& key, uint4* kx, con
   // ---- ACL (TCAM) ----
   if constexpr (ACL == kAclMfma) {
     uint32_t best[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+    // Two tiles per pass-1 test (eight independent MFMAs in flight before the wave-uniform
+    // branch) pays in the MFMA-hash kernels: same-box A/B mfma+ACL1024 6.9-7.0 -> 7.4 Gpps.  In
+    // the LDS-hash kernels the extra live accumulators spill (5 -> 28 VGPRs) and ACL256 drops
+    // 15.2 -> 13.7 Gpps, so they keep one tile per test (profiles/r1_s4_acl_pairs_ab.log).
+    if constexpr (HASH == kHashMfma) {
+    // Pass 2 of one tile (see below): the (mismatch << 10 | rule) first-match epilogue.
+    auto epilogue = [&](uint32_t nt, const v8i_t& a, v4f_t c2) {
+      asm volatile("" : "+v"(c2));
+      const uint32_t rb = nt * 16u + 4u * g;
+#pragma unroll
+      for (int tt = 0; tt < 4; ++tt) {
+        const v8i_t b = {bq[tt][0], bq[tt][1], bq[tt][2], bq[tt][3], 0, 0, 0, 0};
+        const v4f_t acc = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c2, 4, 4, 0, kE8M0One, 0, kE8M0One);
+        const uint32_t e0 = ((uint32_t)acc[0] << 10) | (rb + 0);
+        const uint32_t e1 = ((uint32_t)acc[1] << 10) | (rb + 1);
+        const uint32_t e2 = ((uint32_t)acc[2] << 10) | (rb + 2);
+        const uint32_t e3 = ((uint32_t)acc[3] << 10) | (rb + 3);
+        best[tt] = min(best[tt], min(min(e0, e1), min(e2, e3)));
+      }
+    };
+    // An odd last tile is tested twice (pass 2 is idempotent under min).
+    for (uint32_t nt = tile0; nt < acl_tiles; nt += 2 * tstep) {
+      const uint32_t nu = nt + tstep < acl_tiles ? nt + tstep : nt;
+      const v4i a4 = lw[nt * 64 + lane], a4u = lw[nu * 64 + lane];
+      const v8i_t a = {a4[0], a4[1], a4[2], a4[3], 0, 0, 0, 0};
+      const v8i_t au = {a4u[0], a4u[1], a4u[2], a4u[3], 0, 0, 0, 0};
+      const v4i ci = lc[nt * 4 + g], ciu = lc[nu * 4 + g];
+      const v4f_t c = {__int_as_float(ci[0]), __int_as_float(ci[1]), __int_as_float(ci[2]), __int_as_float(ci[3])};
+      const v4f_t cu = {__int_as_float(ciu[0]), __int_as_float(ciu[1]), __int_as_float(ciu[2]), __int_as_float(ciu[3])};
+      v4f_t acc[8];
+#pragma unroll
+      for (int tt = 0; tt < 4; ++tt) {
+        const v8i_t b = {bq[tt][0], bq[tt][1], bq[tt][2], bq[tt][3], 0, 0, 0, 0};
+        acc[tt] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 4, 4, 0, kE8M0One, 0, kE8M0One);
+        acc[4 + tt] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(au, b, cu, 4, 4, 0, kE8M0One, 0, kE8M0One);
+      }
+      uint32_t z = 0xFFFFFFFFu;
+#pragma unroll
+      for (int tt = 0; tt < 8; ++tt) {
+        z = min(z, min(__float_as_uint(acc[tt][0]), __float_as_uint(acc[tt][1])));
+        z = min(z, min(__float_as_uint(acc[tt][2]), __float_as_uint(acc[tt][3])));
+      }
+      if (!__any(z == 0u)) continue;
+      epilogue(nt, a, c);
+      epilogue(nu, au, cu);
+    }
+    } else {
     for (uint32_t nt = tile0; nt < acl_tiles; nt += tstep) {
       const v4i a4 = lw[nt * 64 + lane];
       const v8i_t a = {a4[0], a4[1], a4[2], a4[3], 0, 0, 0, 0};
@@ -156,6 +203,7 @@ __device__ __forceinline__ void classify_wave(const FlowKey& key, uint4* kx, con
         const uint32_t e3 = ((uint32_t)acc[3] << 10) | (rb + 3);
         best[tt] = min(best[tt], min(min(e0, e1), min(e2, e3)));
       }
+    }
     }
 #pragma unroll
     for (int tt = 0; tt < 4; ++tt) {
