@@ -102,11 +102,14 @@ static_assert(sizeof(QCtl) == kQCtlBytes, "queue control is 16 bytes");
 class Ring {
  public:
   Ring() = default;
-  Ring(QCtl* ctl, uint8_t* base, std::atomic<uint32_t>* waiters = nullptr) : ctl_(ctl), base_(base), waiters_(waiters) {}
+  // `sz` is the queue size validated by Mailbox::open/create; it is cached here so a peer that
+  // rewrites the shared `sz` field cannot steer copies outside the region.
+  Ring(QCtl* ctl, uint8_t* base, uint32_t sz, std::atomic<uint32_t>* waiters = nullptr)
+      : ctl_(ctl), base_(base), sz_(sz), waiters_(waiters) {}
   uint32_t bell() const { return ctl_->bell.load(std::memory_order_seq_cst); }
   void ring();                                     // bump the doorbell, wake sleepers
   bool wait_bell(uint32_t seen, int timeout_us);   // true once bell != seen (woken or already)
-  uint32_t size() const { return ctl_->sz; }
+  uint32_t size() const { return sz_; }
   uint32_t used() const;
   uint32_t space() const;  // bytes a producer may still write
   // Returns false (nothing written) when the record does not fit.
@@ -118,8 +121,12 @@ class Ring {
  private:
   void copy_in(uint32_t off, const void* src, uint32_t n);
   void copy_out(uint32_t off, void* dst, uint32_t n) const;
+  // Shared cursors are peer-writable: a cursor outside [0, sz) or not 8-aligned means the ring
+  // is corrupt.  Resets the ring and throws (same path as an oversized record).
+  uint32_t cursor(const std::atomic<uint32_t>& c, std::memory_order mo) const;
   QCtl* ctl_ = nullptr;
   uint8_t* base_ = nullptr;
+  uint32_t sz_ = 0;
   std::atomic<uint32_t>* waiters_ = nullptr;
 };
 

@@ -5,13 +5,21 @@ A `coordination.k8s.io/v1` Lease named by the election id holds `holderIdentity`
 missing or expired lease and renews it every `renew` seconds; writes use the API server's
 optimistic concurrency, so two candidates racing for one lease cannot both win (the loser sees
 Conflict / AlreadyExists).  `on_started` / `on_stopped` fire on gaining / losing leadership.
+
+Failure handling follows controller-runtime's renew deadline: a leader that fails to renew
+(Conflict, transport or API errors alike) keeps leadership only until `renew_deadline` seconds
+after its last successful renew, which is shorter than the lease duration, so it steps down
+before another candidate can take the expired lease.  No exception ever ends the election loop.
 """
 from __future__ import annotations
 
+import logging
 import threading
 import time
 
 from .apiserver import AlreadyExists, ApiServer, Conflict, NotFound
+
+log = logging.getLogger("dpu.leader")
 
 
 def _now() -> float:
@@ -21,13 +29,19 @@ def _now() -> float:
 class LeaderElector:
     def __init__(self, api: ApiServer, lease_name: str, namespace: str, identity: str,
                  lease_duration: float = 15.0, renew: float = 2.0, on_started=None, on_stopped=None,
-                 release_on_cancel: bool = True):
+                 release_on_cancel: bool = True, renew_deadline: float | None = None):
         self.api = api
         self.name, self.ns, self.identity = lease_name, namespace, identity
         self.duration, self.renew = lease_duration, renew
         self.on_started, self.on_stopped = on_started, on_stopped
         self.release_on_cancel = release_on_cancel
+        # controller-runtime defaults: lease 15 s, renew deadline 10 s, retry period 2 s
+        self.renew_deadline = renew_deadline if renew_deadline is not None else lease_duration * 2 / 3
+        if not renew < self.renew_deadline < lease_duration:
+            raise ValueError("need renew period < renew deadline < lease duration")
         self.leader = False
+        self.errors = 0
+        self._last_renew = 0.0
         self._stop = threading.Event()
         self._t: threading.Thread | None = None
 
@@ -73,9 +87,23 @@ class LeaderElector:
             if self.on_stopped:
                 self.on_stopped()
 
+    def _tick(self) -> None:
+        try:
+            ok = self.try_acquire_or_renew()
+        except Exception as e:  # noqa: BLE001 - API/transport failure counts as a failed renew
+            self.errors += 1
+            log.warning("leader election %s/%s: renew failed: %s", self.ns, self.name, e)
+            ok = False
+        now = time.monotonic()
+        if ok:
+            self._last_renew = now
+            self._set(True)
+        elif not self.leader or now - self._last_renew >= self.renew_deadline:
+            self._set(False)
+
     def _run(self) -> None:
         while not self._stop.is_set():
-            self._set(self.try_acquire_or_renew())
+            self._tick()
             self._stop.wait(self.renew)
 
     def start(self) -> "LeaderElector":
@@ -93,6 +121,6 @@ class LeaderElector:
                 if cur["spec"].get("holderIdentity") == self.identity:
                     cur["spec"]["holderIdentity"] = ""
                     self.api.update(cur)
-            except (Conflict, NotFound):
+            except Exception:  # noqa: BLE001 - best effort: the lease expires on its own
                 pass
         self._set(False)

@@ -5,6 +5,12 @@ resume": only the CNI NetConf cache survives).  Components here append one JSON 
 mutation (fsync'd before the RPC returns), periodically compact to a snapshot, and replay the
 snapshot + tail on start.  A torn last line (crash mid-append) is ignored.
 Files: <dir>/<name>.jsonl (log), <dir>/<name>.snap.json (snapshot, atomically replaced).
+
+Every record carries a monotonically increasing ``seq``; a snapshot stores the last ``seq`` it
+covers (``_journal_seq``).  Compaction replaces the snapshot first and truncates the log second,
+so a crash between the two leaves records the new snapshot already contains: ``load`` skips
+every record at or below the snapshot's sequence number instead of replaying it twice (replay is
+not idempotent, e.g. NF creation appends).
 """
 from __future__ import annotations
 
@@ -21,10 +27,18 @@ class Journal:
         self.compact_every = compact_every
         self._lock = threading.Lock()
         self._n = 0
+        snap, recs = self._read()
+        self._seq = max([int((snap or {}).get("_journal_seq", 0))] + [int(r.get("seq", 0)) for r in recs])
+
+    @property
+    def seq(self) -> int:
+        """Sequence number of the last appended record."""
+        return self._seq
 
     def append(self, rec: dict) -> None:
-        line = json.dumps(rec, separators=(",", ":")) + "\n"
         with self._lock:
+            self._seq += 1
+            line = json.dumps(dict(rec, seq=self._seq), separators=(",", ":")) + "\n"
             with open(self.log_path, "a") as f:
                 f.write(line)
                 f.flush()
@@ -38,7 +52,7 @@ class Journal:
         tmp = self.snap_path + ".tmp"
         with self._lock:
             with open(tmp, "w") as f:
-                json.dump(state, f)
+                json.dump(dict(state, _journal_seq=self._seq), f)
                 f.flush()
                 os.fsync(f.fileno())
             os.replace(tmp, self.snap_path)
@@ -48,6 +62,12 @@ class Journal:
             self._n = 0
 
     def load(self) -> tuple[dict | None, list[dict]]:
+        """-> (snapshot or None, log records newer than the snapshot)."""
+        snap, recs = self._read()
+        floor = int((snap or {}).get("_journal_seq", 0))
+        return snap, [r for r in recs if int(r.get("seq", floor + 1)) > floor]
+
+    def _read(self) -> tuple[dict | None, list[dict]]:
         snap = None
         if os.path.exists(self.snap_path):
             with open(self.snap_path) as f:

@@ -51,7 +51,10 @@ NF_BRIDGE_BASE = 100
 # journaled RPC -> hook; args are JSON-encoded (bytes as {"hex": ...})
 _MUTATING = {"SetNumVfs": "set_num_vfs", "CreateBridgePort": "create_bridge_port",
              "DeleteBridgePort": "delete_bridge_port", "CreateNetworkFunction": "create_network_function",
-             "DeleteNetworkFunction": "delete_network_function", "Init": "init", "GpuChain": "on_gpu_chain"}
+             "DeleteNetworkFunction": "delete_network_function", "Init": "init", "GpuChain": "on_gpu_chain",
+             "InstallFlows": "_install_flows_rec"}
+# installs up to this many flows are journaled record-by-record; bigger bulk loads checkpoint
+JOURNAL_FLOWS_MAX = 4096
 
 
 def _enc(a):
@@ -295,19 +298,30 @@ class GpuVsp(VspBase):
                 "nfs": self.nfs, "gpu_chains": {k: [cid, self.chain_kinds.get(k, [])] for k, cid in self.gpu_chains.items()},
                 "dp_snapshot": self.dp is not None}
 
-    def _dp_snap_path(self) -> str:
-        return os.path.join(os.path.dirname(self.journal.log_path), "gpu-vsp.dp.npz")
+    def _dp_snap_path(self, gen: int) -> str:
+        return os.path.join(os.path.dirname(self.journal.log_path), f"gpu-vsp.dp.{gen}.npz")
 
     def checkpoint(self) -> None:
-        """Snapshot control state + data-plane tables, then truncate the journal."""
+        """Snapshot control state + data-plane tables, then truncate the journal.
+
+        The data-plane snapshot is written under a generation name (the journal sequence number)
+        that the JSON snapshot names, so a crash between the two writes restores the previous
+        generation consistently instead of pairing a new .npz with an old JSON state."""
         from ..dataplane import snapshot
 
         with self._lock:
             if self.journal is None:
                 raise RuntimeError("GpuVsp was created without state_dir")
+            state = self._state()
+            gen = self.journal.seq
             if self.dp is not None:
-                snapshot.save(self.dp, self._dp_snap_path())
-            self.journal.compact(self._state())
+                snapshot.save(self.dp, self._dp_snap_path(gen))
+                state["dp_snapshot"] = os.path.basename(self._dp_snap_path(gen))
+            self.journal.compact(state)
+            d = os.path.dirname(self.journal.log_path)
+            for f in os.listdir(d):  # older generations are unreachable now
+                if f.startswith("gpu-vsp.dp.") and f.endswith(".npz") and f != state.get("dp_snapshot"):
+                    os.unlink(os.path.join(d, f))
 
     def _restore(self) -> None:
         from ..dataplane import snapshot
@@ -328,7 +342,7 @@ class GpuVsp(VspBase):
                     self.nfs = snap["nfs"]
                     if snap.get("dp_snapshot"):
                         dp = self._ensure_dp()
-                        snapshot.load(dp, self._dp_snap_path())
+                        snapshot.load(dp, os.path.join(os.path.dirname(self.journal.log_path), snap["dp_snapshot"]))
                         for name, (cid, kinds) in snap["gpu_chains"].items():
                             self.gpu_chains[name] = int(cid)
                             self.chain_kinds[name] = list(kinds)
@@ -345,10 +359,24 @@ class GpuVsp(VspBase):
 
     # ------------------------------------------------------------------ data path access
     def install_flows(self, keys: np.ndarray, actions: np.ndarray) -> None:
+        """Install exact-match flows.  Durable with `state_dir`: small installs are journaled,
+        bulk loads (> JOURNAL_FLOWS_MAX) take a checkpoint before returning."""
+        keys = np.ascontiguousarray(keys, np.uint32).reshape(-1, 4)
+        actions = np.ascontiguousarray(actions, np.uint32).reshape(-1, 4)
         with self._lock:
             self._ensure_dp()
             self.dp.flows.insert_many(keys, actions)
             self._commit()
+            if self.journal is None or self._replaying:
+                return
+            if len(keys) <= JOURNAL_FLOWS_MAX:
+                self._journal("InstallFlows", (keys.tobytes(), actions.tobytes()))
+            else:
+                self.checkpoint()
+
+    def _install_flows_rec(self, keys: bytes, actions: bytes) -> None:
+        self.install_flows(np.frombuffer(keys, np.uint32).reshape(-1, 4),
+                           np.frombuffer(actions, np.uint32).reshape(-1, 4))
 
     def process(self, frames: np.ndarray, in_ports) -> tuple[np.ndarray, np.ndarray]:
         """Run a batch through the data plane: frames [n,64] uint8, in_ports [n] -> (out, meta)."""

@@ -67,6 +67,39 @@ def test_ring_fifo_wraparound_and_full(tmp):
         A.Mailbox.create(str(tmp / "small"), 300)
 
 
+def _poke(path, off, fmt, *vals):
+    with open(path, "r+b") as f:
+        f.seek(off)
+        f.write(struct.pack(fmt, *vals))
+
+
+def test_ring_rejects_peer_corrupted_cursors_and_geometry(tmp):
+    """The region is peer-writable: cursors >= sz or unaligned, mismatched or oversized queue
+    sizes must be rejected instead of steering memcpy outside the mapping."""
+    path = str(tmp / "mb")
+    mb = A.Mailbox.create(path, 288 + 2 * 256)
+    assert mb.h2f_push(0, 1, -1, 1, 7, b"abc")
+    _poke(path, 256, "<I", 4096)            # H2F prod far beyond sz
+    with pytest.raises(RuntimeError, match="cursor"):
+        mb.h2f_pop()
+    assert mb.h2f_pop() is None             # the corrupt ring was reset, not read
+    _poke(path, 256 + 4, "<I", 13)          # H2F cons not 8-aligned
+    with pytest.raises(RuntimeError, match="cursor"):
+        mb.h2f_push(0, 1, -1, 1, 8, b"x")
+    # the shared sz field is ignored after binding (cached) ...
+    _poke(path, 256 + 8, "<I", 1 << 30)
+    assert mb.h2f_push(0, 1, -1, 1, 9, b"ok") and mb.h2f_pop()[6] == b"ok"
+    # ... and a region whose queues no longer fit is refused at open
+    with pytest.raises(RuntimeError, match="geometry"):
+        A.Mailbox.open(path)
+    _poke(path, 256 + 8, "<I", 256)
+    _poke(path, 272 + 8, "<I", 128)         # H2F and F2H sizes disagree
+    with pytest.raises(RuntimeError, match="geometry"):
+        A.Mailbox.open(path)
+    _poke(path, 272 + 8, "<I", 256)
+    assert A.Mailbox.open(path).queue_bytes == 256
+
+
 def test_parse_reference_soc_config():
     if not REF_CFG.exists():
         pytest.skip("reference config not mounted")

@@ -89,6 +89,36 @@ def test_leader_election_single_leader_and_failover():
     assert events[:2] == ["a+", "b+"]
 
 
+def test_leader_survives_transient_errors_and_steps_down_at_renew_deadline():
+    """API errors never kill the election thread; a leader whose renews keep failing gives up
+    leadership at the renew deadline, before its lease could expire."""
+    api = ApiServer()
+    events = []
+    a = LeaderElector(api, "lock2", V.NAMESPACE, "a", lease_duration=0.6, renew=0.05, renew_deadline=0.3,
+                      on_started=lambda: events.append("+"), on_stopped=lambda: events.append("-")).start()
+    assert wait_until(lambda: a.leader, 2)
+    real = api.update
+    fails = {"n": 0}
+
+    def flaky(obj):
+        if fails["n"] < 2:        # two transport errors: shorter than the deadline -> still leader
+            fails["n"] += 1
+            raise OSError("connection reset")
+        return real(obj)
+
+    api.update = flaky
+    time.sleep(0.25)
+    assert a.leader and a._t.is_alive() and a.errors == 2
+    api.update = lambda obj: (_ for _ in ()).throw(OSError("apiserver down"))
+    t0 = time.monotonic()
+    assert wait_until(lambda: not a.leader, 2)
+    assert time.monotonic() - t0 < 0.6 and a._t.is_alive()   # stepped down before lease expiry
+    api.update = real
+    assert wait_until(lambda: a.leader, 2)                     # and re-acquires once healthy
+    a.stop()
+    assert events[:3] == ["+", "-", "+"]
+
+
 def test_admission_endpoint():
     ok = review_response({"request": {"uid": "1", "operation": "CREATE", "object": _cfg("dpu")}})
     assert ok["response"]["allowed"]

@@ -42,7 +42,7 @@ def test_journal_snapshot_and_torn_tail(tmp):
     with open(j.log_path, "a") as f:
         f.write('{"i": 4, "trunc')  # crash mid-append
     snap, recs = Journal(tmp, "t").load()
-    assert snap == {"upto": 2} and recs == [{"i": 3}]
+    assert snap == {"upto": 2, "_journal_seq": 3} and recs == [{"i": 3, "seq": 4}]
 
 
 def test_dataplane_snapshot_roundtrip(tmp):
@@ -118,6 +118,48 @@ def test_gpu_vsp_checkpoint_then_tail(tmp):
     assert b.restored == 1 and b.bridge_ports == {} and len(b.nfs) == 1
     assert b.dp.flows.find(keys[0]) >= 0
     assert b.vports[0]["role"] == "free"
+
+
+def test_gpu_vsp_flows_survive_without_checkpoint(tmp):
+    """Flows installed after the last checkpoint are journaled: a crash before the
+    next checkpoint must not lose them; bulk installs checkpoint instead."""
+    from dpu_operator_amd.vsp import gpu as G
+
+    pm = PathManager(tmp)
+    sd = os.path.join(tmp, "state")
+    a = G.GpuVsp(pm, device="cpu", nl=FakeNetlink(), flow_buckets=1 << 12, state_dir=sd)
+    _populate(a)
+    keys = np.array([[0x0A000002, 0x08080808, (1234 << 16) | 53, 17],
+                     [0x0A000003, 0x08080404, (999 << 16) | 80, 6]], np.uint32)
+    acts = np.zeros((2, 4), np.uint32)
+    acts[:, 0] = 5 << 16
+    a.install_flows(keys, acts)              # no checkpoint afterwards
+    b = G.GpuVsp(pm, device="cpu", nl=FakeNetlink(), flow_buckets=1 << 12, state_dir=sd)
+    assert all(b.dp.flows.find(k) >= 0 for k in keys)
+    big = np.zeros((G.JOURNAL_FLOWS_MAX + 1, 4), np.uint32)
+    big[:, 0] = 0x0B000000 + np.arange(len(big))
+    big[:, 3] = 17
+    b.install_flows(big, np.zeros_like(big))
+    assert os.path.getsize(b.journal.log_path) == 0     # bulk load -> checkpoint, no giant record
+    c = G.GpuVsp(pm, device="cpu", nl=FakeNetlink(), flow_buckets=1 << 12, state_dir=sd)
+    assert len(c.dp.flows) == len(big) + 2
+
+
+def test_journal_compaction_crash_does_not_replay_twice(tmp):
+    """Crash between snapshot replace and log truncate: records covered by the snapshot carry
+    seq <= _journal_seq and are skipped on load."""
+    j = Journal(tmp, "t")
+    for i in range(3):
+        j.append({"i": i})
+    log = open(j.log_path).read()
+    j.compact({"upto": 3})
+    with open(j.log_path, "w") as f:   # the truncate "never happened"
+        f.write(log)
+    j2 = Journal(tmp, "t")
+    snap, recs = j2.load()
+    assert snap["upto"] == 3 and recs == []
+    j2.append({"i": 3})
+    assert [r["i"] for r in j2.load()[1]] == [3] and j2.seq == 4
 
 
 def test_fault_injector_semantics():

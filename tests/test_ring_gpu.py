@@ -12,9 +12,9 @@ from dpu_operator_amd.dataplane.ring import RingPath
 CAP = 8192
 
 
-def _build(device, n_flows=4000, seed=0):
-    dp = DataPlane(device=device, flow_buckets=1 << 11, hash_mode="lds", acl_mode="mfma")
-    sc = S.build_sfc(dp, n_pods=16, n_flows=n_flows, n_acl=64, seed=seed)
+def _build(device, n_flows=4000, seed=0, hash_mode="lds", n_acl=64):
+    dp = DataPlane(device=device, flow_buckets=1 << 11, hash_mode=hash_mode, acl_mode="mfma")
+    sc = S.build_sfc(dp, n_pods=16, n_flows=n_flows, n_acl=n_acl, seed=seed)
     dp.commit(full=True)
     return dp, sc
 
@@ -34,10 +34,15 @@ def test_ring_needs_gpu():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("coop,host_slots", [(True, False), (False, False), (True, True)])
-def test_ring_bit_exact_and_counters(coop, host_slots):
-    g, sc = _build("cuda")
-    c, _ = _build("cpu")
+@pytest.mark.parametrize("coop,host_slots,hash_mode,n_acl", [
+    (True, False, "lds", 64), (False, False, "lds", 64), (True, True, "lds", 64),
+    # MFMA-hash kernels test two rule tiles per pass-1 branch; with coop each of the 4 waves scans
+    # tiles wave, wave+4, ... so 200 rules (13 tiles, not a multiple of 8) exercise the nu == nt
+    # clamp across waves
+    (True, False, "mfma", 200), (False, False, "mfma", 200)])
+def test_ring_bit_exact_and_counters(coop, host_slots, hash_mode, n_acl):
+    g, sc = _build("cuda", hash_mode=hash_mode, n_acl=n_acl)
+    c, _ = _build("cpu", hash_mode=hash_mode, n_acl=n_acl)
     pk, im = _traffic(sc)
     ring = RingPath(g, capacity=CAP, deadline_s=30.0, coop=coop, host_slots=host_slots)
     try:
