@@ -46,12 +46,30 @@ TablesView tables_from(const py::dict& d) {
   t.acl_default_permit = val<uint32_t>(d, "acl_default_permit", 1);
   t.lag_members = d.contains("lag_members") ? ptr<const uint16_t>(d, "lag_members") : nullptr;
   t.n_lag_groups = val<uint32_t>(d, "n_lag_groups", 0);
+  t.flood = ptr<const uint16_t>(d, "flood");
+  t.n_flood = t.flood ? val<uint32_t>(d, "n_flood", 0) : 0u;
   if (t.n_lag_groups && !t.lag_members) throw std::invalid_argument("n_lag_groups > 0 but lag_members missing");
   if (!t.ports || !t.chains || !t.flows || !t.rss_key)
     throw std::invalid_argument("tables dict is missing a required buffer");
   if (t.n_acl && (!t.acl_value || !t.acl_mask || !t.acl_permit))
     throw std::invalid_argument("n_acl > 0 but ACL buffers missing");
   return t;
+}
+
+// Side outputs (replicas + learn events): a dict of buffer addresses and capacities, or None.
+SideOut side_from(const py::object& o) {
+  SideOut so{};
+  if (o.is_none()) return so;
+  const py::dict d = o.cast<py::dict>();
+  so.rep_hdr = ptr<uint32_t>(d, "rep_hdr"); so.rep_meta = ptr<uint32_t>(d, "rep_meta");
+  so.rep_src = ptr<uint32_t>(d, "rep_src"); so.cap_rep = val<uint32_t>(d, "cap_rep", 0);
+  so.learn = ptr<uint32_t>(d, "learn"); so.cap_learn = val<uint32_t>(d, "cap_learn", 0);
+  so.cnt = ptr<uint32_t>(d, "cnt");
+  so.list = ptr<uint32_t>(d, "list"); so.cap_list = val<uint32_t>(d, "cap_list", 0);
+  if (!so.cnt) throw std::invalid_argument("side outputs need a 'cnt' buffer (4 x u32)");
+  if (so.cap_rep && (!so.rep_hdr || !so.rep_meta || !so.rep_src)) throw std::invalid_argument("side: replica buffers missing");
+  if (so.cap_learn && !so.learn) throw std::invalid_argument("side: learn buffer missing");
+  return so;
 }
 
 void check(hipError_t e, const char* what) {
@@ -70,6 +88,9 @@ PYBIND11_MODULE(_nfdp, m) {
   m.attr("PORT_NONE") = kPortNone;
   m.attr("PORT_PUNT") = kPortPunt;
   m.attr("NUM_REASONS") = (int)kNumReasons;
+  m.attr("MAX_FRAME") = kMaxFrame;
+  m.attr("FLOOD_WAYS") = kFloodWays;
+  m.attr("ENCAP_BYTES") = kEncapBytes;
 
   py::class_<FlowTableHost>(m, "FlowTable")
       .def(py::init([](uint32_t nb, py::bytes rss) {
@@ -167,14 +188,26 @@ PYBIND11_MODULE(_nfdp, m) {
 
   m.def("oracle_run", [](py::dict tables, uintptr_t pkts, uintptr_t inmeta, uint32_t n, uintptr_t out,
                          uintptr_t out_meta, uintptr_t flow_ctr, uintptr_t port_ctr, uintptr_t drop_ctr,
-                         uintptr_t hashes, uintptr_t acl) {
+                         uintptr_t hashes, uintptr_t acl, py::object side) {
     TablesView t = tables_from(tables);
+    const SideOut so = side_from(side);
     py::gil_scoped_release nogil;
     oracle_run(t, reinterpret_cast<const uint32_t*>(pkts), reinterpret_cast<const uint32_t*>(inmeta), n,
                reinterpret_cast<uint32_t*>(out), reinterpret_cast<uint32_t*>(out_meta),
                reinterpret_cast<uint64_t*>(flow_ctr), reinterpret_cast<uint64_t*>(port_ctr),
                reinterpret_cast<uint64_t*>(drop_ctr), reinterpret_cast<uint32_t*>(hashes),
-               reinterpret_cast<int32_t*>(acl));
+               reinterpret_cast<int32_t*>(acl), so.cnt ? &so : nullptr);
+  }, py::arg("tables"), py::arg("pkts"), py::arg("inmeta"), py::arg("n"), py::arg("out"), py::arg("out_meta"),
+     py::arg("flow_ctr"), py::arg("port_ctr"), py::arg("drop_ctr"), py::arg("hashes"), py::arg("acl"),
+     py::arg("side") = py::none());
+  m.def("mac_learn_cpu", [](uintptr_t macs, uint32_t mask, uintptr_t events, uint32_t n, uint32_t stamp) {
+    return mac_learn_cpu(reinterpret_cast<MacEntry*>(macs), mask, reinterpret_cast<const uint32_t*>(events), n, stamp);
+  });
+  m.def("launch_mac_learn", [](uintptr_t macs, uint32_t mask, uintptr_t events, uintptr_t n_events, uint32_t cap,
+                               uint32_t stamp, uintptr_t dropped, uintptr_t stream) {
+    check(launch_mac_learn(reinterpret_cast<MacEntry*>(macs), mask, reinterpret_cast<const uint32_t*>(events),
+                           reinterpret_cast<const uint32_t*>(n_events), cap, stamp, reinterpret_cast<uint32_t*>(dropped),
+                           reinterpret_cast<hipStream_t>(stream)), "mac_learn");
   });
 
   m.def("fused_lds_bytes", &fused_lds_bytes);
@@ -182,8 +215,9 @@ PYBIND11_MODULE(_nfdp, m) {
                            uint32_t n, uintptr_t flow_ctr, uintptr_t port_ctr, uintptr_t drop_ctr, uintptr_t t0,
                            uintptr_t lat, uintptr_t acl_wfrag, uintptr_t acl_cinit, uint32_t acl_tiles,
                            uintptr_t toep_frag, uintptr_t toep_tab, int hash_mode, int acl_mode, int num_cus,
-                           uintptr_t stream, uint32_t flags) {
+                           uintptr_t stream, uint32_t flags, py::object side) {
     FusedLaunch f{};
+    f.side = side_from(side);
     f.t = tables_from(tables);
     f.pkts = reinterpret_cast<const void*>(pkts);
     f.inmeta = reinterpret_cast<const uint32_t*>(inmeta);
@@ -209,7 +243,11 @@ PYBIND11_MODULE(_nfdp, m) {
     LaunchCfg cfg;
     cfg.hash_mode = hash_mode; cfg.acl_mode = acl_mode; cfg.num_cus = num_cus;
     check(launch_fused(f, cfg, reinterpret_cast<hipStream_t>(stream)), "launch_fused");
-  });
+  }, py::arg("tables"), py::arg("pkts"), py::arg("inmeta"), py::arg("out"), py::arg("out_meta"), py::arg("n"),
+     py::arg("flow_ctr"), py::arg("port_ctr"), py::arg("drop_ctr"), py::arg("t0"), py::arg("lat"),
+     py::arg("acl_wfrag"), py::arg("acl_cinit"), py::arg("acl_tiles"), py::arg("toep_frag"), py::arg("toep_tab"),
+     py::arg("hash_mode"), py::arg("acl_mode"), py::arg("num_cus"), py::arg("stream"), py::arg("flags") = 0,
+     py::arg("side") = py::none());
   m.def("launch_stamp", [](uintptr_t dst, uintptr_t stream) {
     check(launch_stamp(reinterpret_cast<unsigned long long*>(dst), reinterpret_cast<hipStream_t>(stream)), "stamp");
   });
@@ -228,6 +266,7 @@ PYBIND11_MODULE(_nfdp, m) {
     return g;
   };
   m.def("desc_seg_bytes", [](uint32_t cap) { return desc_seg_bytes(cap); });
+  m.def("verdict_seg_bytes", [](uint32_t cap) { return verdict_seg_bytes(cap); });
   m.def("pkt_seg_bytes", [](uint32_t cap) { return pkt_seg_bytes(cap); });
   m.def("pkt_meta_off", [](uint32_t cap) { return pkt_meta_off(cap); });
   m.def("shard_ingress", [geom](py::dict tables, py::dict d, bool device, int hash_mode, int acl_mode, int num_cus,

@@ -404,6 +404,32 @@ __device__ __forceinline__ void wave_counter_add(unsigned long long* ctr, uint32
 
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 
+// GPU sink of pipeline.h side_stage: one global atomic per replica / learn event (rare paths:
+// flooding, mirroring, ARP-trap and learning ports only).  Replica tx and ARP-trap counts go
+// straight to the global counters.
+struct GpuSideSink {
+  const SideOut& so;
+  unsigned long long* port_ctr;
+  unsigned long long* drop_ctr;
+  __device__ __forceinline__ void rep(const uint32_t* hdr, uint32_t meta, uint32_t src) {
+    const uint32_t pos = atomicAdd(so.cnt + 0, 1u);
+    if (pos >= so.cap_rep) { atomicAdd(so.cnt + 2, 1u); return; }
+    uint4* dst = reinterpret_cast<uint4*>(so.rep_hdr) + (size_t)pos * 4;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) dst[q] = make_uint4(hdr[4 * q], hdr[4 * q + 1], hdr[4 * q + 2], hdr[4 * q + 3]);
+    so.rep_meta[pos] = meta;
+    so.rep_src[pos] = src;
+    const uint32_t r = meta_reason(meta), port = meta_port(meta);
+    if (r) atomicAdd(drop_ctr + r, 1ull);
+    else if (port < (uint32_t)kMaxPorts) atomicAdd(port_ctr + 2 * port + 1, ctr_inc(meta_len(meta)));
+  }
+  __device__ __forceinline__ void learn(uint32_t bridge, uint32_t lo, uint32_t hi, uint32_t port) {
+    const uint32_t pos = atomicAdd(so.cnt + 1, 1u);
+    if (pos >= so.cap_learn) { atomicAdd(so.cnt + 3, 1u); return; }
+    reinterpret_cast<uint4*>(so.learn)[pos] = make_uint4(lo, (hi & 0xFFFFu) | (bridge << 16), port, 0u);
+  }
+};
+
 // ---- coalesced frame I/O (tools/copy_bench.hip: 6.4 TB/s vs 1.4 TB/s for per-lane slots) ----
 // A wave's 64 slots are one contiguous 4-KiB run.  Each dwordx4 instruction covers 1 KiB of it
 // lane-contiguously (16 full 64-B lines) instead of 16 B of 64 different lines, and the wave's

@@ -195,9 +195,58 @@ std::vector<uint32_t> build_toeplitz_table(const uint8_t* rss_key) {
 // ------------------------------------------------------------------------------------------
 // CPU oracle
 // ------------------------------------------------------------------------------------------
+namespace {
+// Sequential sink of pipeline.h side_stage (replica positions in packet order; the GPU's are in
+// atomic order, so tests compare replica sets).
+struct CpuSideSink {
+  const SideOut& so;
+  uint64_t* port_ctr;
+  uint64_t* drop_ctr;
+  void rep(const uint32_t* hdr, uint32_t meta, uint32_t src) {
+    const uint32_t pos = so.cnt[0]++;
+    if (pos >= so.cap_rep) { ++so.cnt[2]; return; }
+    std::memcpy(so.rep_hdr + (size_t)pos * kSlotDwords, hdr, kSlotBytes);
+    so.rep_meta[pos] = meta;
+    so.rep_src[pos] = src;
+    const uint32_t r = meta_reason(meta), port = meta_port(meta);
+    if (r) { if (drop_ctr) drop_ctr[r] += 1; }
+    else if (port < (uint32_t)kMaxPorts && port_ctr) port_ctr[2 * port + 1] += ctr_inc(meta_len(meta));
+  }
+  void learn(uint32_t bridge, uint32_t lo, uint32_t hi, uint32_t port) {
+    const uint32_t pos = so.cnt[1]++;
+    if (pos >= so.cap_learn) { ++so.cnt[3]; return; }
+    uint32_t* e = so.learn + (size_t)pos * 4;
+    e[0] = lo; e[1] = (hi & 0xFFFFu) | (bridge << 16); e[2] = port; e[3] = 0;
+  }
+};
+}  // namespace
+
+uint32_t mac_learn_cpu(MacEntry* macs, uint32_t mask, const uint32_t* ev, uint32_t n, uint32_t stamp) {
+  uint32_t dropped = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint32_t lo = ev[4 * i], hi = ev[4 * i + 1] & 0xFFFFu, br = ev[4 * i + 1] >> 16, port = ev[4 * i + 2];
+    const uint32_t h = mac_hash(br, lo, hi) & mask;
+    bool done = false;
+    for (int probe = 0; probe < 16 && !done; ++probe) {
+      MacEntry& e = macs[(h + probe) & mask];
+      if (e.valid == kMacEmpty) {
+        e.mac_lo = lo; e.mac_hi = (uint16_t)hi; e.bridge_id = (uint16_t)br; e.out_port = (uint16_t)port;
+        e.valid = kMacLearned; e.stamp = stamp;
+        done = true;
+      } else if ((e.valid == kMacStatic || e.valid == kMacLearned) && e.mac_lo == lo && e.mac_hi == hi &&
+                 e.bridge_id == br) {
+        if (e.valid == kMacLearned) { e.out_port = (uint16_t)port; e.stamp = stamp; }
+        done = true;
+      }
+    }
+    if (!done) ++dropped;
+  }
+  return dropped;
+}
+
 void oracle_run(const TablesView& t, const uint32_t* pkts, const uint32_t* inmeta, uint32_t n,
                 uint32_t* out, uint32_t* out_meta, uint64_t* flow_ctr, uint64_t* port_ctr,
-                uint64_t* drop_ctr, uint32_t* hashes, int32_t* acl_rules) {
+                uint64_t* drop_ctr, uint32_t* hashes, int32_t* acl_rules, const SideOut* side) {
   for (uint32_t i = 0; i < n; ++i) {
     const uint32_t* d = pkts + (size_t)i * kSlotDwords;
     Parsed p;
@@ -222,12 +271,27 @@ void oracle_run(const TablesView& t, const uint32_t* pkts, const uint32_t* inmet
     emit(p, e.tci, e.push != 0, o);
     const uint32_t olen = e.reason ? 0u : p.len + (e.push ? 4u : 0u);
     std::memcpy(out + (size_t)i * kSlotDwords, o, sizeof(o));
-    out_meta[i] = make_meta(e.out_port, olen, e.reason, e.mirror != 0);
+    out_meta[i] = make_meta(e.out_port, olen, e.reason, false, !e.reason && e.flood);
+    if (side && side->cnt && side_needed(st, p, e)) {
+      const uint32_t q = side->cnt[5]++;
+      if (q < side->cap_list) side->list[q] = i;
+      else ++side->cnt[6];
+    }
     if (port_ctr) {
       if (st.in_port < (uint32_t)kMaxPorts) port_ctr[2 * st.in_port] += ctr_inc(st.wire_len);
       if (!e.reason) port_ctr[2 * e.out_port + 1] += ctr_inc(olen);
     }
     if (drop_ctr && e.reason) drop_ctr[e.reason & (kNumReasons - 1)] += 1;
+  }
+  // side pass (GPU: side_kernel after the fused kernel)
+  if (side && side->cnt) {
+    CpuSideSink sk{*side, port_ctr, drop_ctr};
+    const uint32_t nl = std::min(side->cnt[5], side->cap_list);
+    for (uint32_t j = 0; j < nl; ++j) {
+      const uint32_t i = side->list[j];
+      side_stage(t, DirectTables{t}, pkts + (size_t)i * kSlotDwords, inmeta[i], out + (size_t)i * kSlotDwords,
+                 out_meta[i], i, sk);
+    }
   }
 }
 
@@ -268,12 +332,12 @@ void oracle_run_remote(const TablesView& t, const uint32_t* pkts, const uint32_t
     if (to_peer) {
       uint8_t* segp = r.send_pkt + eg * pseg;
       std::memcpy(segp + 64 + (size_t)pos * 64, o, sizeof(o));
-      const uint32_t m = make_meta(e.out_port, olen, kOk, e.mirror != 0);
+      const uint32_t m = make_meta(e.out_port, olen, kOk);
       std::memcpy(segp + pkt_meta_off(r.cap_pkt) + 4 * (size_t)pos, &m, 4);
-      out_meta[i] = make_meta(e.out_port, olen, kRemote, e.mirror != 0);
+      out_meta[i] = make_meta(e.out_port, olen, kRemote);
     } else {
       std::memcpy(out + (size_t)i * kSlotDwords, o, sizeof(o));
-      out_meta[i] = make_meta(reason == kOverflow ? kPortNone : e.out_port, olen, reason, reason != kOverflow && e.mirror != 0);
+      out_meta[i] = make_meta(reason == kOverflow ? kPortNone : e.out_port, olen, reason, false, !reason && e.flood);
     }
     if (port_ctr) {
       if (st.in_port < (uint32_t)kMaxPorts) port_ctr[2 * st.in_port] += ctr_inc(st.wire_len);

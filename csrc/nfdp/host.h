@@ -63,7 +63,13 @@ struct OracleOut {
 };
 void oracle_run(const TablesView& t, const uint32_t* pkts, const uint32_t* inmeta, uint32_t n,
                 uint32_t* out, uint32_t* out_meta, uint64_t* flow_ctr, uint64_t* port_ctr,
-                uint64_t* drop_ctr, uint32_t* hashes, int32_t* acl_rules);
+                uint64_t* drop_ctr, uint32_t* hashes, int32_t* acl_rules, const SideOut* side = nullptr);
+// MAC learning: apply learn events {mac_lo, mac_hi | bridge << 16, port, 0} to the MAC table
+// (learned entries carry `stamp`; static entries are never overridden).  Returns the number of
+// events that found no slot within the probe limit.  GPU twin: launch_mac_learn.
+uint32_t mac_learn_cpu(MacEntry* macs, uint32_t mac_mask, const uint32_t* events, uint32_t n, uint32_t stamp);
+hipError_t launch_mac_learn(MacEntry* macs, uint32_t mac_mask, const uint32_t* events, const uint32_t* n_events,
+                            uint32_t cap, uint32_t stamp, uint32_t* dropped, hipStream_t s);
 // Replicated multi-GPU twin of the fused REMOTE kernel: frames whose egress port belongs to
 // another rank are written to send_pkt segment[egress rank] (positions in arrival order, fill
 // counts in pcnt, headers written at the end), out_meta says kRemote for them.
@@ -93,6 +99,7 @@ struct FusedLaunch {
   // replicated multi-GPU mode (nranks > 1): remote-egress frames go to per-GPU send segments
   uint8_t* send_pkt = nullptr; uint32_t* pcnt = nullptr;
   uint32_t nranks = 0, rank = 0, cap_pkt = 0;
+  SideOut side{};  // side outputs (flood / mirror / ARP replicas, learn events); cnt null = off
 };
 hipError_t launch_fused(const FusedLaunch& f, const LaunchCfg& cfg, hipStream_t s);
 size_t fused_lds_bytes(int hash_mode, int acl_mode, uint32_t acl_tiles);

@@ -56,6 +56,7 @@ struct FusedArgs {
   uint8_t* send_pkt;
   uint32_t* pcnt;
   uint32_t nranks, rank, cap_pkt;
+  SideOut side;                   // flood / mirror / ARP replicas + learn events (side.cnt null: off)
 };
 
 __device__ __forceinline__ size_t lds_align16(size_t x) { return (x + 15) & ~(size_t)15; }
@@ -204,7 +205,7 @@ __global__ __launch_bounds__(kFB, NFDP_FUSED_WAVES_PER_EU) void fused_kernel(Fus
         if (pos < a.cap_pkt) {
           uint8_t* segp = a.send_pkt + (size_t)eg * pkt_seg_bytes(a.cap_pkt);
           reinterpret_cast<uint32_t*>(segp + pkt_meta_off(a.cap_pkt))[pos] =
-              make_meta(e.out_port, p.len + (e.push ? 4u : 0u), kOk, e.mirror != 0);
+              make_meta(e.out_port, p.len + (e.push ? 4u : 0u), kOk);
           to_peer = true;
         } else {
           reason = kOverflow;
@@ -212,9 +213,9 @@ __global__ __launch_bounds__(kFB, NFDP_FUSED_WAVES_PER_EU) void fused_kernel(Fus
       }
     }
     const uint32_t olen = reason ? 0u : p.len + (e.push ? 4u : 0u);
-    const uint32_t meta = to_peer ? make_meta(e.out_port, olen, kRemote, e.mirror != 0)
-                                  : make_meta(reason == kOverflow ? kPortNone : e.out_port, olen, reason,
-                                              reason != kOverflow && e.mirror != 0);
+    const uint32_t meta = to_peer ? make_meta(e.out_port, olen, kRemote)
+                                  : make_meta(reason == kOverflow ? kPortNone : e.out_port, olen, reason, false,
+                                              !reason && e.flood);
     // port / drop counters: LDS, global only for ports >= kLdsPorts (issued before the tail)
     if (valid && !(a.flags & 1u)) {
       if (st.in_port < kLdsPorts) {
@@ -234,6 +235,18 @@ __global__ __launch_bounds__(kFB, NFDP_FUSED_WAVES_PER_EU) void fused_kernel(Fus
     }
     uint32_t o[kSlotDwords];
     emit(p, e.tci, e.push != 0, o);
+    if (a.side.cnt) {
+      // flood / mirror / ARP-trap / learning packets go on the side list (side_kernel emits their
+      // replicas and learn events after this kernel): a wave-uniform skip in the common case
+      const bool sn = valid && side_needed(st, p, e);
+      if (__builtin_expect(__any(sn), 0)) {
+        if (sn) {
+          const uint32_t q = atomicAdd(a.side.cnt + 5, 1u);
+          if (q < a.side.cap_list) a.side.list[q] = i;
+          else atomicAdd(a.side.cnt + 6, 1u);
+        }
+      }
+    }
     const bool sample = a.lat && !(a.flags & 2u) && (i & 15u) == 0 && !to_peer;
     const uint32_t lat_now = sample ? (uint32_t)(__builtin_amdgcn_s_memrealtime() - t0) : 0u;
     if constexpr (!REMOTE) {
@@ -270,6 +283,30 @@ __global__ __launch_bounds__(kFB, NFDP_FUSED_WAVES_PER_EU) void fused_kernel(Fus
     atomicAdd(a.drop_ctr + threadIdx.x, (unsigned long long)drops[threadIdx.x]);
 }
 
+// Side pass (pipeline.h side_stage) over the packets the per-packet kernel put on the side list:
+// flood replicas, mirror and ARP copies, learn events.  Reads the list length on the device.
+struct SideArgs {
+  TablesView t;
+  const uint4* pkts; const uint32_t* inmeta; const uint4* out; const uint32_t* out_meta;
+  SideOut side;
+  unsigned long long* port_ctr; unsigned long long* drop_ctr;
+};
+__global__ __launch_bounds__(256) void side_kernel(SideArgs a) {
+  const uint32_t n = min(a.side.cnt[5], a.side.cap_list);
+  for (uint32_t j = blockIdx.x * 256 + threadIdx.x; j < n; j += gridDim.x * 256) {
+    const uint32_t i = a.side.list[j];
+    uint32_t d[kSlotDwords], o[kSlotDwords];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint4 v = a.pkts[(size_t)i * 4 + q], w = a.out[(size_t)i * 4 + q];
+      d[4 * q] = v.x; d[4 * q + 1] = v.y; d[4 * q + 2] = v.z; d[4 * q + 3] = v.w;
+      o[4 * q] = w.x; o[4 * q + 1] = w.y; o[4 * q + 2] = w.z; o[4 * q + 3] = w.w;
+    }
+    GpuSideSink sk{a.side, a.port_ctr, a.drop_ctr};
+    side_stage(a.t, DirectTables{a.t}, d, a.inmeta[i], o, a.out_meta[i], i, sk);
+  }
+}
+
 __global__ void stamp_kernel(unsigned long long* dst) {
   if (threadIdx.x == 0) *dst = __builtin_amdgcn_s_memrealtime();
 }
@@ -283,6 +320,60 @@ __global__ void bucket_update_kernel(const uint32_t* idx, uint32_t nb, const uin
   const uint32_t b = idx[bi];
   if (b > bucket_mask) return;
   flows[(size_t)b * kBucketSlots * 2 + q] = rows[(size_t)bi * kBucketSlots * 2 + q];
+}
+
+// MAC learning (OvS NORMAL) on the GPU: one thread per learn event, lock-free insert into the
+// open-addressed (bridge, MAC) table.  An empty slot is claimed with a CAS on its port/valid word
+// (-> kMacClaim), the key and stamp are written, and a release store publishes kMacLearned.  A
+// thread that sees a claimed slot re-reads it (a claimer publishes within the same loop
+// iteration, so lanes of one wave never wait on each other); a known key only refreshes the
+// port and stamp of a learned entry (static entries win).  Lookups running concurrently (the
+// persistent ring) skip claimed slots and continue probing.
+__global__ __launch_bounds__(256) void mac_learn_kernel(MacEntry* macs, uint32_t mask, const uint4* ev,
+                                                        const uint32_t* n_events, uint32_t cap, uint32_t stamp,
+                                                        uint32_t* dropped) {
+  const uint32_t n = min(*n_events, cap);
+  uint32_t* base = reinterpret_cast<uint32_t*>(macs);
+  for (uint32_t j = blockIdx.x * 256 + threadIdx.x; j < n; j += gridDim.x * 256) {
+    const uint4 v = ev[j];
+    const uint32_t lo = v.x, hi = v.y & 0xFFFFu, br = v.y >> 16, port = v.z & 0xFFFFu;
+    const uint32_t key1 = hi | (br << 16);
+    const uint32_t h = mac_hash(br, lo, hi) & mask;
+    uint32_t probe = 0, spins = 0;
+    bool done = false;
+    while (!done && probe < 16) {
+      uint32_t* w = base + (size_t)((h + probe) & mask) * 4;
+      const uint32_t w2 = __hip_atomic_load(w + 2, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t valid = w2 >> 16;
+      if (valid == kMacClaim) {  // another wave is inserting here: re-read
+        if (++spins > (1u << 16)) break;
+        __builtin_amdgcn_s_sleep(1);
+        continue;
+      }
+      if (valid == kMacEmpty) {
+        if (atomicCAS(w + 2, w2, (0xFFFFu << 16) | port) == w2) {
+          __hip_atomic_store(w + 0, lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(w + 1, key1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(w + 3, stamp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(w + 2, ((uint32_t)kMacLearned << 16) | port, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+          done = true;
+        }
+        continue;  // lost the race: the slot is claimed now, re-read it
+      }
+      const uint32_t k0 = __hip_atomic_load(w + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t k1 = __hip_atomic_load(w + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if ((valid == kMacStatic || valid == kMacLearned) && k0 == lo && k1 == key1) {
+        if (valid == kMacLearned) {
+          __hip_atomic_store(w + 3, stamp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(w + 2, ((uint32_t)kMacLearned << 16) | port, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        done = true;
+        continue;
+      }
+      ++probe;
+    }
+    if (!done) atomicAdd(dropped, 1u);
+  }
 }
 
 // Read-and-reset packed counters (harvest); host accumulates into 64-bit totals.
@@ -325,6 +416,11 @@ static hipError_t launch_fused_t(const FusedArgs& a, int num_cus, hipStream_t s)
   if (need < grid) grid = need;
   if (grid == 0) return hipSuccess;
   hipLaunchKernelGGL((fused_kernel<H, A, R>), dim3(grid), dim3(kFB), lds, s, a);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || !a.side.cnt || a.side.cap_list == 0) return e;
+  SideArgs sa{a.t, a.pkts, a.inmeta, a.out, a.out_meta, a.side, a.port_ctr, a.drop_ctr};
+  const uint32_t sg = (a.side.cap_list + 255) / 256 < 512 ? (a.side.cap_list + 255) / 256 : 512;
+  hipLaunchKernelGGL(side_kernel, dim3(sg), dim3(256), 0, s, sa);
   return hipGetLastError();
 }
 
@@ -346,6 +442,10 @@ hipError_t launch_fused(const FusedLaunch& f, const LaunchCfg& cfg, hipStream_t 
   a.flags = f.flags;
   a.send_pkt = f.send_pkt; a.pcnt = f.pcnt;
   a.nranks = f.nranks; a.rank = f.rank; a.cap_pkt = f.cap_pkt;
+  a.side = f.side;
+  if (a.side.cnt && ((a.side.cap_rep && (!a.side.rep_hdr || !a.side.rep_meta || !a.side.rep_src)) ||
+                     (a.side.cap_learn && !a.side.learn) || (a.side.cap_list && !a.side.list)))
+    return hipErrorInvalidValue;
   const bool remote = f.nranks > 1;
   if (cfg.acl_mode == kAclMfma && (f.acl_tiles == 0 || f.acl_tiles > 64)) return hipErrorInvalidValue;
   const int h = cfg.hash_mode, ac = cfg.acl_mode, cu = cfg.num_cus;
@@ -370,6 +470,16 @@ hipError_t launch_bucket_update(const uint32_t* idx, uint32_t nb, const void* ro
   const uint32_t threads = nb * kBucketSlots * 2;
   hipLaunchKernelGGL(bucket_update_kernel, dim3((threads + 255) / 256), dim3(256), 0, s, idx, nb,
                      reinterpret_cast<const uint4*>(rows), reinterpret_cast<uint4*>(flows), bucket_mask);
+  return hipGetLastError();
+}
+
+hipError_t launch_mac_learn(MacEntry* macs, uint32_t mac_mask, const uint32_t* events, const uint32_t* n_events,
+                            uint32_t cap, uint32_t stamp, uint32_t* dropped, hipStream_t s) {
+  if (!macs || !events || !n_events || !dropped || ((mac_mask + 1) & mac_mask)) return hipErrorInvalidValue;
+  if (cap == 0) return hipSuccess;
+  const uint32_t grid = (cap + 255) / 256 < 256 ? (cap + 255) / 256 : 256;
+  hipLaunchKernelGGL(mac_learn_kernel, dim3(grid), dim3(256), 0, s, macs, mac_mask,
+                     reinterpret_cast<const uint4*>(events), n_events, cap, stamp, dropped);
   return hipGetLastError();
 }
 

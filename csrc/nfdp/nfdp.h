@@ -24,13 +24,16 @@ namespace nfdp {
 // ----------------------------------------------------------------------------------------
 // Constants
 // ----------------------------------------------------------------------------------------
-constexpr int kSlotBytes = 64;         // one packet slot in HBM (60 B frame + room for one tag)
+constexpr int kSlotBytes = 64;         // header slot in HBM: the first min(len, 64) bytes of a frame
 constexpr int kSlotDwords = kSlotBytes / 4;
-constexpr int kMaxPorts = 4096;        // vport table size (VF / NF / wire / PR ports)
+constexpr uint32_t kMaxFrame = 9600;   // longest L2 frame (jumbo 9216 + tags); 14-bit length fields
+constexpr int kFloodWays = 16;         // member ports per flood group (bridge)
+constexpr int kMaxPorts = 4094;        // vport table rows (VF / NF / wire / PR ports); 4094/4095 = meta sentinels
 constexpr int kBucketSlots = 4;        // flow-table bucket = 4 x {key, action} = one 128-B line
 constexpr uint32_t kSlotUsed = 0x100u; // occupied marker, stored in FlowKey.meta byte 1
 constexpr uint16_t kPortNone = 0xFFFF; // dropped
 constexpr uint16_t kPortPunt = 0xFFFE; // to slow path (control plane upcall)
+// (kMaxPorts real ports; the 12-bit egress meta port field keeps 0xFFF / 0xFFE for none / punt)
 constexpr int kMaxHops = 7;
 constexpr int kAclKeyBits = 128;       // ACL / hash key = the 16-byte FlowKey
 
@@ -48,6 +51,7 @@ enum Reason : uint32_t {
   kMalformed = 9,
   kRemote = 10,    // not a drop: handed to the egress GPU over xGMI (multi-GPU path)
   kOverflow = 11,  // exchange segment full (multi-GPU path)
+  kArpTrap = 12,   // ARP copy trapped to the slow path (P4 always_trap_arp_table)
   kNumReasons = 16,
 };
 
@@ -64,10 +68,11 @@ enum PortFlags : uint32_t {
   kPortMirror = 1u << 8,        // forwarded frames from this port are also copied to ext[31:16] (K9)
   kPortLag = 1u << 9,           // egress to this port picks a LAG member by hash[2:0] (K8)
   kPortVsiLookup = 1u << 10,    // L2 lookup keys on the target VSI (dst MAC byte 1) only (K3)
+  kPortLearn = 1u << 11,        // (bridge, src MAC) -> in_port is learned from this port's frames (OvS NORMAL)
+  kPortArpTrap = 1u << 12,      // ARP frames from this port are also copied to the slow path
 };
 
 constexpr int kLagWays = 8;                 // members per LAG group (hash[2:0])
-constexpr uint32_t kMetaMirror = 1u << 31;  // egress meta: copy the frame to the in-port's mirror port
 
 // chain hop opcodes (built-in GPU network functions)
 enum Hop : uint8_t {
@@ -96,7 +101,8 @@ struct alignas(16) PortEntry {   // 32 B
   uint16_t peer_mac_hi;
   uint16_t default_out;          // with kPortHasDefault: egress port on an L2 (flow + MAC) miss
   uint32_t ext;                  // [11:0] ingress-push vid (kPortIngressTag); [31:16] mirror port (kPortMirror)
-  uint32_t lag;                  // LAG group index (kPortLag)
+  uint16_t lag;                  // LAG group index (kPortLag)
+  uint16_t mtu;                  // egress MTU in L3 bytes (frame - 14, untagged); 0 = kMaxFrame only
 };
 static_assert(sizeof(PortEntry) == 32, "PortEntry");
 
@@ -141,9 +147,10 @@ struct alignas(16) MacEntry {    // 16 B, (bridge, dst-mac) -> port  (K5)
   uint16_t mac_hi;
   uint16_t bridge_id;
   uint16_t out_port;
-  uint16_t valid;
-  uint32_t pad;
+  uint16_t valid;                // kMacEmpty / kMacStatic / kMacTomb / kMacLearned (kMacClaim while inserting)
+  uint32_t stamp;                // learned entries: last-seen stamp (host aging); static: 0
 };
+enum MacValid : uint16_t { kMacEmpty = 0, kMacStatic = 1, kMacTomb = 2, kMacLearned = 3, kMacClaim = 0xFFFF };
 static_assert(sizeof(MacEntry) == 16, "MacEntry");
 
 // Verdict returned by the flow owner to the ingress GPU (multi-GPU path).
@@ -200,16 +207,21 @@ NFDP_HD uint32_t owner_of(uint32_t h, uint32_t nshards) {
 }
 
 // ----------------------------------------------------------------------------------------
-// Parsing.  A packet is 16 little-endian dwords.  `s` is the *normalized* (untagged) view:
-// an 802.1Q tag (4 B at offset 12) is removed by a one-dword shift, since 4 B = 1 dword.
+// Parsing.  A header slot is 16 little-endian dwords = the first min(len, 64) bytes of the
+// frame; `len` is the whole frame's length (up to kMaxFrame).  The payload beyond the slot stays
+// where the I/O layer put it: no stage reads it (every rewrite - MACs, tag, SNAT with RFC 1624
+// incremental checksums, TTL - falls in the first 56 bytes of the normalized view).  `s` is the
+// *normalized* (untagged) view: an 802.1Q tag (4 B at offset 12) is removed by a one-dword
+// shift, since 4 B = 1 dword.
 // ----------------------------------------------------------------------------------------
 struct Parsed {
-  uint32_t s[kSlotDwords];  // normalized frame (untagged layout), bytes beyond len are junk
-  uint32_t len;             // normalized length in bytes (tag removed)
+  uint32_t s[kSlotDwords];  // normalized header (untagged layout), bytes beyond len / the slot are junk
+  uint32_t len;             // normalized length of the WHOLE frame in bytes (tag removed)
   uint32_t tci;             // 802.1Q TCI (0 if untagged)
   bool tagged;
   bool ipv4;                // IPv4 with IHL=5, first fragment, fully inside the slot
   bool l4;                  // TCP or UDP ports present
+  bool arp;                 // EtherType 0x0806
 };
 
 NFDP_HD uint32_t be16_at(const uint32_t* s, int byte) {  // byte offset must be even
@@ -247,6 +259,7 @@ NFDP_HD void parse(const uint32_t* d, uint32_t len, Parsed& p) {
   p.ipv4 = et2 == 0x0800u && verihl == 0x45u && p.len >= 34 && (frag & 0x1FFFu) == 0;
   const uint32_t proto = p.s[5] >> 24;
   p.l4 = p.ipv4 && (proto == 6 || proto == 17) && p.len >= 38;
+  p.arp = et2 == 0x0806u;
 }
 
 NFDP_HD uint32_t dmac_lo(const uint32_t* s) { return s[0]; }
@@ -351,8 +364,32 @@ NFDP_HD void emit(const Parsed& p, uint32_t push_tci, bool push, uint32_t* out) 
   for (int i = 4; i < kSlotDwords; ++i) out[i] = push ? p.s[i - 1] : p.s[i];
 }
 
-NFDP_HD uint32_t make_meta(uint32_t out_port, uint32_t len, uint32_t reason, bool mirror = false) {
-  return (out_port & 0xFFFFu) | ((len & 0xFFu) << 16) | (reason << 24) | (mirror ? kMetaMirror : 0u);
+// Egress metadata word: port[11:0] (0xFFF none, 0xFFE punt) | olen[25:12] | reason[29:26] |
+// xhdr[30] (prepend the packet's 64-B outer-header record: tunnel encap) | flood[31].  The frame that leaves
+// is  ohdr[0:hl] ++ in_frame[to:len]  with  d = olen - 50*xhdr - len,  hl = min(64, min(len, 64) + d),
+// to = hl - d  (out_tail below): the payload is never copied by the pipeline.
+constexpr uint32_t kMetaXhdr = 1u << 30;
+constexpr uint32_t kMetaFlood = 1u << 31;  // primary copy of a flooded frame (side pass emits the rest)
+constexpr uint32_t kEncapBytes = 50;   // outer Ethernet + IPv4 + UDP + VXLAN/GENEVE (no options)
+NFDP_HD uint32_t make_meta(uint32_t out_port, uint32_t len, uint32_t reason, bool xhdr = false, bool flood = false) {
+  return (out_port & 0xFFFu) | ((len & 0x3FFFu) << 12) | ((reason & 0xFu) << 26) | (xhdr ? kMetaXhdr : 0u) |
+         (flood ? kMetaFlood : 0u);
+}
+NFDP_HD uint32_t meta_port(uint32_t m) {
+  const uint32_t p = m & 0xFFFu;
+  return p >= 0xFFEu ? (p | 0xF000u) : p;
+}
+NFDP_HD uint32_t meta_len(uint32_t m) { return (m >> 12) & 0x3FFFu; }
+NFDP_HD uint32_t meta_reason(uint32_t m) { return (m >> 26) & 0xFu; }
+// Header bytes `hl` of the out slot that are valid and the offset `to` in the input frame where the
+// unchanged tail continues (both from the in/out lengths; `xhdr` bytes excluded).
+NFDP_HD void out_tail(uint32_t in_len, uint32_t olen, bool xhdr, uint32_t& hl, uint32_t& to) {
+  const int d = (int)olen - (xhdr ? (int)kEncapBytes : 0) - (int)in_len;
+  const int h_in = in_len < (uint32_t)kSlotBytes ? (int)in_len : kSlotBytes;
+  int h = h_in + d;
+  if (h > kSlotBytes) h = kSlotBytes;
+  hl = (uint32_t)h;
+  to = (uint32_t)(h - d);
 }
 
 // ----------------------------------------------------------------------------------------
@@ -376,6 +413,24 @@ struct TablesView {
   uint32_t acl_default_permit;   // verdict when no rule matches
   const uint16_t* lag_members;   // n_lag_groups * kLagWays egress ports (K8)
   uint32_t n_lag_groups;
+  const uint16_t* flood;         // n_flood * kFloodWays member ports per bridge (kPortNone padded)
+  uint32_t n_flood;              // bridges [0, n_flood) have a flood group
+};
+
+// Side outputs of a batch (pipeline.h side_stage): replicas (flood members, mirror copies, ARP
+// slow-path copies) and MAC-learn events, appended at positions claimed with one atomic each.
+// cnt: [0] replicas, [1] learn events, [2] replicas dropped (full), [3] learn events dropped,
+// [4] learn events with no free slot (learn kernel), [5] side-list entries, [6] side-list dropped.
+struct SideOut {
+  uint32_t* rep_hdr;             // cap_rep x 64-B header slots
+  uint32_t* rep_meta;            // cap_rep egress meta words
+  uint32_t* rep_src;             // cap_rep source packet indices (whose input frame holds the tail)
+  uint32_t cap_rep;
+  uint32_t* learn;               // cap_learn x {mac_lo, mac_hi | bridge << 16, port, 0}
+  uint32_t cap_learn;
+  uint32_t* cnt;                 // 8 counters (nullptr: side outputs disabled); [5] side-list length
+  uint32_t* list;                // packets flagged by the per-packet kernel for the side pass
+  uint32_t cap_list;
 };
 
 // Flow-table lookup (scalar).  Returns slot index or -1.
@@ -393,13 +448,19 @@ NFDP_HD int64_t flow_lookup(const TablesView& t, const FlowKey& k, uint32_t h) {
   return -1;
 }
 
+NFDP_HD uint32_t mac_hash(uint32_t bridge, uint32_t lo, uint32_t hi) {
+  return fmix32(lo ^ (hi << 16) ^ (bridge * 0x9E3779B1u));
+}
+
 NFDP_HD int mac_lookup(const TablesView& t, uint32_t bridge, uint32_t lo, uint32_t hi) {
   if (!t.macs) return -1;
-  uint32_t h = fmix32(lo ^ (hi << 16) ^ (bridge * 0x9E3779B1u)) & t.mac_mask;
+  const uint32_t h = mac_hash(bridge, lo, hi) & t.mac_mask;
   for (int probe = 0; probe < 16; ++probe) {
     const MacEntry& e = t.macs[(h + probe) & t.mac_mask];
-    if (!e.valid) return -1;
-    if (e.mac_lo == lo && e.mac_hi == (hi & 0xFFFFu) && e.bridge_id == bridge) return e.out_port;
+    if (e.valid == kMacEmpty) return -1;
+    if ((e.valid == kMacStatic || e.valid == kMacLearned) && e.mac_lo == lo && e.mac_hi == (hi & 0xFFFFu) &&
+        e.bridge_id == bridge)
+      return e.out_port;
   }
   return -1;
 }

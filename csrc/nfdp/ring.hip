@@ -250,7 +250,7 @@ __global__ __launch_bounds__(kRingBlock) void ring_kernel(RingArgs a) {
     uint32_t o[kSlotDwords];
     emit(p, e.tci, e.push != 0, o);
     wave_frames_store<kSysAux>(kx, o, r_out, run);
-    __builtin_amdgcn_raw_buffer_store_b32(make_meta(e.out_port, olen, e.reason, e.mirror != 0), r_meta, i * 4u, 0, kSysAux);
+    __builtin_amdgcn_raw_buffer_store_b32(make_meta(e.out_port, olen, e.reason, false, !e.reason && e.flood), r_meta, i * 4u, 0, kSysAux);
     NFDP_RING_MARK(tr3)
 
     // ---- completion: the chunk's write-through stores are done before its flag is written ----

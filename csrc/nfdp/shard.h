@@ -3,7 +3,7 @@
 //
 // One step on rank r of N (per batch of B packets):
 //   1. ingress  : parse, port checks, MFMA hash + TCAM ACL, owner = hash shard;
-//                 write a 16-B descriptor (the FlowKey + wire length) into segment[owner]
+//                 write a 32-B descriptor (the FlowKey + wire length) into segment[owner]
 //   2. all-to-all(descriptors)                          [RCCL over xGMI]
 //   3. owner    : exact-match lookup in the local 1/N of the flow table, per-flow counters,
 //                 16-B verdict into the mirrored position
@@ -13,7 +13,7 @@
 //                 segment[egress gpu] (64-B slot + 4-B meta)
 //   6. all-to-all(packets)                              [RCCL over xGMI]
 //   7. egress   : tx counters + latency stamps for packets received from peers
-// Only 16 + 16 B per packet cross xGMI for the flow state; the 64-B payload crosses once, and
+// Only 32 + 16 B per packet cross xGMI for the flow state; the 64-B payload crosses once, and
 // only when the destination pod lives on another GPU.  All segments are fixed capacity so the
 // collectives have static splits (no host round trip per step); segment slot 0 is a header
 // carrying the fill count.
@@ -29,7 +29,10 @@ struct ShardGeom {
   uint32_t cap_pkt;   // packets per destination segment
 };
 
-NFDP_HD size_t desc_seg_bytes(uint32_t cap) { return (size_t)(cap + 1) * 16; }
+// Descriptor = 32 B {FlowKey, wire_len, 0, 0, 0} (a 16-bit frame length no longer fits the key's
+// spare byte); verdict = 16 B.  Slot 0 of every segment is the {count, cap} header.
+NFDP_HD size_t desc_seg_bytes(uint32_t cap) { return (size_t)(cap + 1) * 32; }
+NFDP_HD size_t verdict_seg_bytes(uint32_t cap) { return (size_t)(cap + 1) * 16; }
 NFDP_HD size_t pkt_meta_off(uint32_t cap) { return 64 + (size_t)cap * 64; }
 NFDP_HD size_t pkt_seg_bytes(uint32_t cap) {
   return pkt_meta_off(cap) + (((size_t)cap * 4 + 63) & ~(size_t)63);
@@ -38,17 +41,7 @@ NFDP_HD size_t pkt_seg_bytes(uint32_t cap) {
 constexpr uint32_t kRefNone = 0xFFFFFFFFu;      // no flow lookup (non-IP / dropped at ingress)
 constexpr uint32_t kRefOverflow = 0xFFFFFFFEu;  // descriptor segment was full
 
-NFDP_HD FlowKey make_desc(const FlowKey& k, uint32_t wire_len) {
-  FlowKey d = k;
-  d.meta |= (wire_len & 0xFFu) << 8;
-  return d;
-}
-NFDP_HD FlowKey desc_key(const FlowKey& d, uint32_t& wire_len) {
-  FlowKey k = d;
-  wire_len = (d.meta >> 8) & 0xFFu;
-  k.meta &= ~0xFF00u;
-  return k;
-}
+
 NFDP_HD Verdict make_verdict(bool hit, const FlowAction& a) {
   Verdict v;
   v.chain_id = a.chain_id; v.out_port = a.out_port; v.nat_ip = a.nat_ip;

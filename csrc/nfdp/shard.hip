@@ -76,9 +76,9 @@ __global__ __launch_bounds__(kBlock) void ingress_kernel(IngressArgs a) {
       uint32_t ref = kRefNone;
       if (need) {
         if (pos < a.g.cap_desc) {
-          const FlowKey dk = make_desc(st.key, st.wire_len);
-          uint4* dst = reinterpret_cast<uint4*>(a.send_desc + owner * seg) + 1 + pos;
-          *dst = make_uint4(dk.src_ip, dk.dst_ip, dk.ports, dk.meta);
+          uint4* dst = reinterpret_cast<uint4*>(a.send_desc + owner * seg) + 2 * (1 + pos);
+          dst[0] = make_uint4(st.key.src_ip, st.key.dst_ip, st.key.ports, st.key.meta);
+          dst[1] = make_uint4(st.wire_len, 0u, 0u, 0u);
           ref = (owner << 24) | pos;
         } else {
           ref = kRefOverflow;
@@ -105,16 +105,16 @@ __global__ __launch_bounds__(256) void owner_kernel(OwnerArgs a) {
   __shared__ uint32_t ltab[16 * 256];
   for (uint32_t i = threadIdx.x; i < 4096; i += 256) ltab[i] = a.toep_tab[i];
   __syncthreads();
-  const size_t seg = desc_seg_bytes(a.g.cap_desc);
+  const size_t seg = desc_seg_bytes(a.g.cap_desc), vseg = verdict_seg_bytes(a.g.cap_desc);
   const uint32_t total = a.g.nranks * a.g.cap_desc;
   for (uint32_t idx = blockIdx.x * 256 + threadIdx.x; idx < total; idx += gridDim.x * 256) {
     const uint32_t s = idx / a.g.cap_desc, j = idx % a.g.cap_desc;
     const uint4* src = reinterpret_cast<const uint4*>(a.recv_desc + s * seg);
     const uint32_t count = src[0].x;
     if (j >= count) continue;
-    const uint4 dv = src[1 + j];
-    uint32_t wlen;
-    const FlowKey k = desc_key(FlowKey{dv.x, dv.y, dv.z, dv.w}, wlen);
+    const uint4 dv = src[2 * (1 + j)];
+    const uint32_t wlen = src[2 * (1 + j) + 1].x;
+    const FlowKey k{dv.x, dv.y, dv.z, dv.w};
     const uint32_t w[4] = {k.src_ip, k.dst_ip, k.ports, k.meta};
     uint32_t h = 0;
 #pragma unroll
@@ -126,7 +126,7 @@ __global__ __launch_bounds__(256) void owner_kernel(OwnerArgs a) {
       out = make_uint4(v.x, v.y, v.z, 1u);  // same packing as FlowAction, status=1
       if (a.flow_ctr) atomicAdd(a.flow_ctr + slot, ctr_inc(wlen));
     }
-    reinterpret_cast<uint4*>(a.send_verdict + s * seg)[1 + j] = out;
+    reinterpret_cast<uint4*>(a.send_verdict + s * vseg)[1 + j] = out;
   }
 }
 
@@ -140,7 +140,7 @@ __global__ __launch_bounds__(kBlock) void apply_kernel(ApplyArgs a) {
   for (uint32_t i = threadIdx.x; i < kLdsPorts * 4; i += kBlock) pc[i] = 0;
   if (threadIdx.x < kNumReasons) drops[threadIdx.x] = 0;
   __syncthreads();
-  const size_t dseg = desc_seg_bytes(a.g.cap_desc);
+  const size_t dseg = verdict_seg_bytes(a.g.cap_desc);
   const size_t pseg = pkt_seg_bytes(a.g.cap_pkt);
   const unsigned long long t0 = a.t0 ? *a.t0 : 0ull;
   for (uint32_t base = blockIdx.x * kBlock; base < a.n; base += gridDim.x * kBlock) {
@@ -188,11 +188,11 @@ __global__ __launch_bounds__(kBlock) void apply_kernel(ApplyArgs a) {
       if (remote && reason == kOk) {
         uint8_t* segp = a.send_pkt + eg * pseg;
         dst = reinterpret_cast<uint4*>(segp + 64 + (size_t)pos * 64);
-        reinterpret_cast<uint32_t*>(segp + pkt_meta_off(a.g.cap_pkt))[pos] = make_meta(e.out_port, olen, kOk, e.mirror != 0);
+        reinterpret_cast<uint32_t*>(segp + pkt_meta_off(a.g.cap_pkt))[pos] = make_meta(e.out_port, olen, kOk);
         a.out_meta[i] = make_meta(e.out_port, olen, kRemote);
       } else {
         dst = a.out + (size_t)i * 4;
-        a.out_meta[i] = make_meta(reason == kOverflow ? kPortNone : e.out_port, reason ? 0u : olen, reason, reason != kOverflow && e.mirror != 0);
+        a.out_meta[i] = make_meta(reason == kOverflow ? kPortNone : e.out_port, reason ? 0u : olen, reason, false, !reason && e.flood);
       }
 #pragma unroll
       for (int q = 0; q < 4; ++q) dst[q] = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
@@ -240,7 +240,7 @@ __global__ __launch_bounds__(256) void egress_kernel(EgressArgs a) {
     const uint32_t count = reinterpret_cast<const uint32_t*>(segp)[0];
     if (j >= count) continue;
     const uint32_t m = reinterpret_cast<const uint32_t*>(segp + pkt_meta_off(a.g.cap_pkt))[j];
-    const uint32_t port = m & 0xFFFFu, len = (m >> 16) & 0xFFu;
+    const uint32_t port = meta_port(m), len = meta_len(m);
     if (port < kLdsPorts) {
       atomicAdd(&pc[port], 1u); atomicAdd(&pc[kLdsPorts + port], len);
     } else if (port < (uint32_t)kMaxPorts) {

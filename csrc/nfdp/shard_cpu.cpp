@@ -23,8 +23,8 @@ void ingress_cpu(const IngressArgs& a) {
       const uint32_t owner = owner_of(h, a.g.nranks);
       const uint32_t pos = a.cnt[owner]++;
       if (pos < a.g.cap_desc) {
-        const FlowKey dk = make_desc(st.key, st.wire_len);
-        std::memcpy(a.send_desc + owner * seg + 16 * (1 + (size_t)pos), &dk, 16);
+        const uint32_t dsc[8] = {st.key.src_ip, st.key.dst_ip, st.key.ports, st.key.meta, st.wire_len, 0, 0, 0};
+        std::memcpy(a.send_desc + owner * seg + 32 * (1 + (size_t)pos), dsc, 32);
         ref = (owner << 24) | pos;
       } else {
         ref = kRefOverflow;
@@ -40,16 +40,16 @@ void ingress_cpu(const IngressArgs& a) {
 }
 
 void owner_cpu(const OwnerArgs& a) {
-  const size_t seg = desc_seg_bytes(a.g.cap_desc);
+  const size_t seg = desc_seg_bytes(a.g.cap_desc), vseg = verdict_seg_bytes(a.g.cap_desc);
   for (uint32_t s = 0; s < a.g.nranks; ++s) {
     uint32_t hdr[4];
     std::memcpy(hdr, a.recv_desc + s * seg, 16);
-    std::memcpy(a.send_verdict + s * seg, hdr, 16);
+    std::memcpy(a.send_verdict + s * vseg, hdr, 16);
     for (uint32_t j = 0; j < hdr[0] && j < a.g.cap_desc; ++j) {
-      FlowKey dk;
-      std::memcpy(&dk, a.recv_desc + s * seg + 16 * (1 + (size_t)j), 16);
-      uint32_t wlen;
-      const FlowKey k = desc_key(dk, wlen);
+      uint32_t dsc[8];
+      std::memcpy(dsc, a.recv_desc + s * seg + 32 * (1 + (size_t)j), 32);
+      const FlowKey k{dsc[0], dsc[1], dsc[2], dsc[3]};
+      const uint32_t wlen = dsc[4];
       const uint32_t h = toeplitz_scalar(k, a.t.rss_key);
       const int64_t slot = flow_lookup(a.t, k, h);
       uint32_t out[4] = {0, 0, 0, 0};
@@ -58,13 +58,13 @@ void owner_cpu(const OwnerArgs& a) {
         out[3] = 1;
         if (a.flow_ctr) a.flow_ctr[slot] += ctr_inc(wlen);
       }
-      std::memcpy(a.send_verdict + s * seg + 16 * (1 + (size_t)j), out, 16);
+      std::memcpy(a.send_verdict + s * vseg + 16 * (1 + (size_t)j), out, 16);
     }
   }
 }
 
 void apply_cpu(const ApplyArgs& a) {
-  const size_t dseg = desc_seg_bytes(a.g.cap_desc);
+  const size_t dseg = verdict_seg_bytes(a.g.cap_desc);
   const size_t pseg = pkt_seg_bytes(a.g.cap_pkt);
   for (uint32_t i = 0; i < a.n; ++i) {
     uint32_t d[kSlotDwords];
@@ -100,12 +100,12 @@ void apply_cpu(const ApplyArgs& a) {
     if (remote && reason == kOk) {
       uint8_t* segp = a.send_pkt + eg * pseg;
       std::memcpy(segp + 64 + (size_t)pos * 64, o, 64);
-      const uint32_t m = make_meta(e.out_port, olen, kOk, e.mirror != 0);
+      const uint32_t m = make_meta(e.out_port, olen, kOk);
       std::memcpy(segp + pkt_meta_off(a.g.cap_pkt) + 4 * (size_t)pos, &m, 4);
       a.out_meta[i] = make_meta(e.out_port, olen, kRemote);
     } else {
       std::memcpy(reinterpret_cast<uint8_t*>(a.out) + (size_t)i * 64, o, 64);
-      a.out_meta[i] = make_meta(reason == kOverflow ? kPortNone : e.out_port, reason ? 0u : olen, reason, reason != kOverflow && e.mirror != 0);
+      a.out_meta[i] = make_meta(reason == kOverflow ? kPortNone : e.out_port, reason ? 0u : olen, reason, false, !reason && e.flood);
     }
     if (st.in_port < (uint32_t)kMaxPorts) a.port_ctr[2 * st.in_port] += ctr_inc(st.wire_len);
     if (reason) a.drop_ctr[reason & (kNumReasons - 1)] += 1;
@@ -128,7 +128,7 @@ void egress_cpu(const EgressArgs& a) {
     for (uint32_t j = 0; j < count && j < a.g.cap_pkt; ++j) {
       uint32_t m;
       std::memcpy(&m, segp + pkt_meta_off(a.g.cap_pkt) + 4 * (size_t)j, 4);
-      const uint32_t port = m & 0xFFFFu, len = (m >> 16) & 0xFFu;
+      const uint32_t port = meta_port(m), len = meta_len(m);
       if (port < (uint32_t)kMaxPorts) a.port_ctr[2 * port + 1] += ctr_inc(len);
     }
   }

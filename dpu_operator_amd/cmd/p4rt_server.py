@@ -3,7 +3,7 @@ set-pipe, vendor/.../infrapod/infrapod.go).
 
 Hosts bridge `br0` on a DataPlane (GPU by default) behind the p4rt-ctl service on --address
 (127.0.0.1:9559), loads the MI355X linux-networking P4Info (or --p4info FILE), optional LAG
-group -> port mapping (--lag 0:4095).
+group -> port mapping (--lag 0:4093).
 """
 from __future__ import annotations
 

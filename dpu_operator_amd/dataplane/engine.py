@@ -64,6 +64,7 @@ class DataPlane:
         self.chains = T.ChainTable(chains)
         self.macs = T.MacTable(mac_slots)
         self.lag = T.LagTable()
+        self.flood = T.FloodTable()
         self.acl = T.AclTable()
         self.flows = T.FlowTable(flow_buckets, rss_key)
         self.rss_key = rss_key
@@ -75,6 +76,10 @@ class DataPlane:
         self.count_flows = True  # per-flow packed counters (one 64-bit atomic per packet)
         self.MAX_LAUNCH = 1 << 24
         self.flow_totals = np.zeros((self.flows.nbuckets * 4, 2), np.uint64)
+        # side outputs (flood / mirror / ARP replicas, learn events) and MAC learning state
+        self.cap_rep, self.cap_learn = 1 << 16, 1 << 14
+        self.stamp = 0                 # batch counter: the learned entries' last-seen stamp
+        self._learned_on_device = False
         if self.gpu:
             torch = _torch()
             if not torch.cuda.is_available():
@@ -143,7 +148,10 @@ class DataPlane:
 
     def _commit(self, full: bool) -> dict:
         sent = {}
-        for name, model in (("ports", self.ports), ("chains", self.chains), ("macs", self.macs), ("lag", self.lag)):
+        if self._learned_on_device and (full or self._versions.get("macs") != self.macs.version):
+            self.pull_learned()  # the host re-uploads the MAC table: keep what the GPU learned
+        for name, model in (("ports", self.ports), ("chains", self.chains), ("macs", self.macs), ("lag", self.lag),
+                            ("flood", self.flood)):
             if full or self._versions.get(name) != model.version or name not in self._dev:
                 self._buf(name, model.a)
                 self._versions[name] = model.version
@@ -205,7 +213,75 @@ class DataPlane:
             "acl_permit": self._ptr("acl_permit"), "n_acl": int(getattr(self, "_n_acl", 0)),
             "acl_default_permit": 1 if self.acl.default_permit else 0,
             "lag_members": self._ptr("lag"), "n_lag_groups": int(self.lag.n),
+            "flood": self._ptr("flood") if self.flood.n else 0, "n_flood": int(self.flood.n),
         }
+
+    # ------------------------------------------------------------------ side outputs / learning
+    SIDE_FLAGS = T.PORT_LEARN | T.PORT_ARP_TRAP | T.PORT_MIRROR
+
+    def side_active(self) -> bool:
+        """Replicas / learn events can occur: a flood group or a learning / ARP-trap / mirror port."""
+        return self.flood.n > 0 or bool(np.any(self.ports.a["flags"] & np.uint32(self.SIDE_FLAGS)))
+
+    def _side_buffers(self) -> dict:
+        if "side_cnt" not in self._dev:
+            self._zeros("side_hdr", self.cap_rep * 16, np.uint32)
+            self._zeros("side_meta", self.cap_rep, np.uint32)
+            self._zeros("side_src", self.cap_rep, np.uint32)
+            self._zeros("side_learn", self.cap_learn * 4, np.uint32)
+            self._zeros("side_list", self.cap_rep, np.uint32)
+            self._zeros("side_cnt", 8, np.uint32)
+        self._dev["side_cnt"][:] = 0
+        return {"rep_hdr": self._ptr("side_hdr"), "rep_meta": self._ptr("side_meta"), "rep_src": self._ptr("side_src"),
+                "cap_rep": self.cap_rep, "learn": self._ptr("side_learn"), "cap_learn": self.cap_learn,
+                "cnt": self._ptr("side_cnt"), "list": self._ptr("side_list"), "cap_list": self.cap_rep}
+
+    def _apply_learn(self, stream=None) -> None:
+        """Apply this batch's learn events to the device MAC table (GPU: mac_learn_kernel on the
+        batch's stream, no host sync; CPU: the sequential twin)."""
+        self.stamp += 1
+        if self.gpu:
+            s = stream if stream is not None else _torch().cuda.current_stream(self.tdev).cuda_stream
+            cnt = self._ptr("side_cnt")
+            self.nf.launch_mac_learn(self._ptr("macs"), int(self.macs.mask), self._ptr("side_learn"), cnt + 4,
+                                     self.cap_learn, self.stamp, cnt + 16, s)
+        else:
+            c = self._dev["side_cnt"]
+            n = int(min(c[1], self.cap_learn))
+            if n:
+                c[4] += self.nf.mac_learn_cpu(self._ptr("macs"), int(self.macs.mask), self._ptr("side_learn"), n,
+                                              self.stamp)
+        self._learned_on_device = True
+
+    def side_result(self) -> dict:
+        """Replicas and learn counts of the last batch (synchronises on a GPU)."""
+        if "side_cnt" not in self._dev:
+            return {"n_rep": 0, "n_learn": 0}
+        g = (lambda k: self._dev[k].cpu().numpy().view(np.uint32)) if self.gpu else (lambda k: self._dev[k])
+        c = g("side_cnt")
+        n = int(min(c[0], self.cap_rep))
+        return {"n_rep": n, "rep_hdr": g("side_hdr").reshape(-1, 64 // 4)[:n].view(np.uint8).reshape(n, 64).copy(),
+                "rep_meta": g("side_meta")[:n].copy(), "rep_src": g("side_src")[:n].copy(),
+                "n_learn": int(c[1]), "rep_dropped": int(c[2]), "learn_dropped": int(c[3]),
+                "learn_unplaced": int(c[4]), "n_side": int(c[5]), "side_dropped": int(c[6])}
+
+    def pull_learned(self) -> int:
+        """Fold the entries the data plane learned into the host MAC model."""
+        if "macs" not in self._dev:
+            return 0
+        raw = self._dev["macs"]
+        arr = (raw.cpu().numpy() if self.gpu else raw).view(T.MAC_DTYPE)
+        n = self.macs.merge_learned(arr)
+        self._learned_on_device = False
+        return n
+
+    def age_macs(self, max_age: int) -> int:
+        """Host aging of learned MAC entries (older than `max_age` batches); commits the table."""
+        self.pull_learned()
+        n = self.macs.age(self.stamp, max_age)
+        if n:
+            self.commit()
+        return n
 
     # ------------------------------------------------------------------ run
     def alloc_batch(self, n: int):
@@ -249,6 +325,7 @@ class DataPlane:
                 self.nf.launch_stamp(self._ptr("t0"), s)
             if not self.count_flows:
                 flags |= 4  # the kernel always gets the counter table; bit 2 makes it add 0
+            side = self._side_buffers() if self.side_active() else None
             # one launch covers < 2^25 slots (32-bit buffer views); bigger batches are split
             for lo in range(0, n, self.MAX_LAUNCH):
                 m = min(self.MAX_LAUNCH, n - lo)
@@ -260,16 +337,21 @@ class DataPlane:
                     lat.data_ptr() + 4 * (lo // 16) if lat is not None else 0,
                     self._ptr("acl_wfrag"), self._ptr("acl_cinit"), self._acl_tiles,
                     self._ptr("toep_frag"), self._ptr("toep_tab"),
-                    self.hash_mode, self.acl_mode, self.num_cus, s, flags,
+                    self.hash_mode, self.acl_mode, self.num_cus, s, flags, side,
                 )
+            if side is not None:
+                self._apply_learn(s)
             return BatchResult(out, meta, n, {"lat": lat})
         pk = np.ascontiguousarray(pkts, np.uint8)
         im = np.ascontiguousarray(inmeta, np.uint32)
         hashes = np.zeros(n, np.uint32)
         acl = np.zeros(n, np.int32)
+        side = self._side_buffers() if self.side_active() else None
         self.nf.oracle_run(tp, pk.ctypes.data, im.ctypes.data, n, out.ctypes.data, meta.ctypes.data,
                            self._ptr("flow_ctr"), self._ptr("port_ctr"), self._ptr("drop_ctr"),
-                           hashes.ctypes.data, acl.ctypes.data)
+                           hashes.ctypes.data, acl.ctypes.data, side)
+        if side is not None:
+            self._apply_learn()
         return BatchResult(out, meta, n, {"hash": hashes, "acl": acl})
 
     # ------------------------------------------------------------------ counters

@@ -244,7 +244,7 @@ class P4Runtime:
         def port(p: int) -> int:
             if 0 <= p < VSI_TO_VPORT:   # action port numbers below 16 name physical ports
                 p = PHY_BASE + p
-            if not 0 <= p < T.MAX_PORTS:
+            if not 0 <= p < T.MAX_PORT_ID:
                 raise P4Error("INVALID_ARGUMENT", f"port {p} outside the data plane")
             if not dp.ports.valid(p):
                 dp.ports.set(p, flags=T.PORT_VALID)

@@ -146,3 +146,120 @@ def traffic(sc: Scenario, n: int, seed: int = 1, flows: np.ndarray | None = None
         payload_seed=seed,
     )
     return slots, P.inmeta(sc.pod_port[s], lens)
+
+
+# Simple IMIX (7 x 64 B, 4 x 576 B, 1 x 1500 B wire packets, FCS included) and the jumbo size.
+IMIX_SIMPLE = ((64, 7), (576, 4), (1500, 1))
+IMIX_JUMBO = ((64, 7), (576, 4), (1500, 1), (9000, 1))
+
+
+def imix_sizes(n: int, mix=IMIX_SIMPLE, seed: int = 0) -> np.ndarray:
+    """Per-packet wire sizes (FCS included) drawn from a weighted mix."""
+    sizes = np.array([sz for sz, _ in mix])
+    w = np.array([wt for _, wt in mix], np.float64)
+    return np.random.default_rng(seed).choice(sizes, n, p=w / w.sum())
+
+
+def traffic_frames(sc: Scenario, n: int, sizes: np.ndarray, seed: int = 1, flows: np.ndarray | None = None):
+    """Like ``traffic`` with per-packet sizes (64..9600: the tagged frame in memory = the untagged
+    frame + FCS on the wire, the bench's 64-B convention): returns (header slots uint8[n,64], inmeta, frames uint8[n, max_len], lens).  The frames
+    are what the I/O layer holds; the data plane reads only the header slots."""
+    rng = np.random.default_rng(seed)
+    f = rng.integers(0, len(sc.keys), n) if flows is None else flows[rng.integers(0, len(flows), n)]
+    sizes = np.asarray(sizes, np.int64)
+    lens = np.zeros(n, np.uint32)
+    width = int(sizes.max())
+    frames = np.zeros((n, max(width, 64)), np.uint8)
+    for sz in np.unique(sizes):
+        idx = np.where(sizes == sz)[0]
+        s, d = sc.flow_src_pod[f[idx]], sc.flow_dst_pod[f[idx]]
+        smac = np.frombuffer(b"".join(pod_mac(int(i)) for i in range(sc.n_pods)), np.uint8).reshape(-1, 6)[s]
+        fr, ln = P.craft_full(len(idx), dmac=GW_MAC, smac=smac, src_ip=POD_NET + s, dst_ip=POD_NET + d,
+                              sport=sc.flow_sport[f[idx]], dport=sc.flow_dport[f[idx]], proto=17,
+                              vlan=(s % 4094) + 2, frame_len=int(sz) - 4, payload_seed=seed + int(sz))
+        frames[idx, : fr.shape[1]] = fr[:, : frames.shape[1]]
+        lens[idx] = ln
+    src = sc.flow_src_pod[f]
+    return P.header_slots(frames, lens), P.inmeta(sc.pod_port[src], lens), frames, lens
+
+
+def install_deny_flows(dp, sc: Scenario, k: int = 4096, seed: int = 11) -> dict:
+    """Flows the ACL hop denies: dst 192.168.(r % 256).x, dport 1000 + r for deny rule r of
+    build_sfc's ACL (r % 8 != 7), from random pods, on the scenario's chain."""
+    from . import tables as T2
+
+    rng = np.random.default_rng(seed)
+    n_rules = max(len(dp.acl.rules) - 1, 1)
+    r = rng.integers(0, n_rules, 4 * k)
+    r = r[r % 8 != 7][:k]
+    src = rng.integers(0, sc.n_pods, len(r))
+    dst_ip = 0xC0A80000 + ((r % 256) << 8) + rng.integers(1, 255, len(r))
+    sport = rng.integers(1024, 65536, len(r))
+    dport = 1000 + r
+    keys = T2.flow_key(POD_NET + src, dst_ip, sport, dport, 17, sc.bridge)
+    acts = T2.flow_action(chain_id=sc.chain_id, out_port=sc.pod_port[(src + 1) % sc.n_pods], nat_ip=NAT_NET + 1,
+                          nat_port=2000, vlan=0, flow_id=0)
+    dp.flows.insert_many(keys, acts)
+    return {"src": src, "dst_ip": dst_ip, "sport": sport, "dport": dport}
+
+
+def traffic_mixed(sc: Scenario, deny: dict, n: int, seed: int = 1, miss: float = 0.05, deny_frac: float = 0.02,
+                  malformed: float = 0.001, src_pods: np.ndarray | None = None):
+    """The bench's realistic mix: `miss` of the packets hit no flow (random source port -> L2
+    fallback -> slow-path punt), `deny_frac` hit flows the ACL denies, `malformed` carry an
+    impossible length; the rest are the headline's forwarded pod->pod flows."""
+    pk, im = traffic(sc, n, seed=seed, src_pods=src_pods)
+    rng = np.random.default_rng(seed + 101)
+    u = rng.random(n)
+    mi = np.where(u < miss)[0]
+    pk[mi, 38:40] = rng.integers(0, 256, (len(mi), 2), dtype=np.uint8)   # sport bytes (tagged: L4 at 38)
+    di = np.where((u >= miss) & (u < miss + deny_frac))[0]
+    if len(di):
+        j = rng.integers(0, len(deny["src"]), len(di))
+        s = deny["src"][j]
+        smac = np.frombuffer(b"".join(pod_mac(int(i)) for i in range(sc.n_pods)), np.uint8).reshape(-1, 6)[s]
+        dpk, dl = P.craft(len(di), dmac=GW_MAC, smac=smac, src_ip=POD_NET + s, dst_ip=deny["dst_ip"][j],
+                          sport=deny["sport"][j], dport=deny["dport"][j], proto=17, vlan=(s % 4094) + 2)
+        pk[di] = dpk
+        im[di] = P.inmeta(sc.pod_port[s], dl)
+    bi = np.where((u >= miss + deny_frac) & (u < miss + deny_frac + malformed))[0]
+    im[bi] = (im[bi] & 0xFFFF) | (10 << 16)
+    return pk, im
+
+
+def with_sizes(pk: np.ndarray, im: np.ndarray, sizes: np.ndarray) -> tuple[np.ndarray, np.ndarray]:
+    """Turn 64-B tagged header slots into the headers of frames of `sizes` bytes (the payload
+    beyond the slot is the I/O layer's and never read): IPv4 / UDP lengths and the IPv4 header
+    checksum follow the size; the UDP checksum is set to 0 (none)."""
+    pk = pk.copy()
+    sizes = np.asarray(sizes, np.uint32)
+    tot = sizes - 18                     # tagged: 14 + 4 tag
+    pk[:, 20] = (tot >> 8) & 0xFF
+    pk[:, 21] = tot & 0xFF
+    pk[:, 42] = ((tot - 20) >> 8) & 0xFF
+    pk[:, 43] = (tot - 20) & 0xFF
+    pk[:, 44:46] = 0
+    pk[:, 28:30] = 0
+    w = (pk[:, 18:38:2].astype(np.uint32) << 8) | pk[:, 19:38:2]
+    c = w.sum(axis=1)
+    c = (c & 0xFFFF) + (c >> 16)
+    c = (c & 0xFFFF) + (c >> 16)
+    c = ~c & 0xFFFF
+    pk[:, 28] = (c >> 8) & 0xFF
+    pk[:, 29] = c & 0xFF
+    return pk, (im & 0xFFFF) | (sizes << 16)
+
+
+def add_acl_rules(dp, total: int, seed: int = 5) -> None:
+    """Grow build_sfc's ACL to `total` rules (more deny rules before the final permit)."""
+    rng = np.random.default_rng(seed)
+    final = dp.acl.rules.pop()
+    r = len(dp.acl.rules)
+    while len(dp.acl.rules) < total - 1:
+        if r % 8 == 7:
+            dp.acl.add(permit=False, dport=int(rng.integers(1, 1024)), proto=17)
+        else:
+            dp.acl.add(permit=False, dst=f"192.168.{r % 256}.0/24", dport=int(1000 + r))
+        r += 1
+    dp.acl.rules.append(final)
+    dp.acl.version += 1

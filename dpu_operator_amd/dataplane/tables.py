@@ -21,9 +21,11 @@ import numpy as np
 from ..native import nfdp as _nfdp_mod
 from ..ops.packets import ip_raw, mac_raw, port_raw
 
-MAX_PORTS = 4096
+MAX_PORTS = 4096        # port table rows (buffer sizes)
+MAX_PORT_ID = 4094      # usable port ids: 4094 / 4095 encode none / punt in the 12-bit egress meta port
 PORT_NONE = 0xFFFF
 PORT_PUNT = 0xFFFE
+FLOOD_WAYS = 16         # nfdp.h kFloodWays
 
 # port flags (nfdp.h PortFlags)
 PORT_VALID = 1 << 0
@@ -37,6 +39,8 @@ PORT_INGRESS_TAG = 1 << 7   # frames from the port leave tagged with ext[11:0] (
 PORT_MIRROR = 1 << 8        # forwarded frames are also copied to ext[31:16] (P4 mirror_and_send)
 PORT_LAG = 1 << 9           # egress picks member lag_members[lag][hash & 7] (P4 tx_lag_table)
 PORT_VSI_LOOKUP = 1 << 10   # L2 lookup on (bridge, 00:VSI:00:00:00:00), VSI = dst MAC byte 1 (P4 vsi_to_vsi_loopback)
+PORT_LEARN = 1 << 11        # (bridge, src MAC) -> port learned from this port's frames (OvS NORMAL)
+PORT_ARP_TRAP = 1 << 12     # ARP frames from this port are also copied to the slow path (always_trap_arp_table)
 LAG_WAYS = 8
 
 # hop opcodes (nfdp.h Hop)
@@ -49,7 +53,8 @@ HOP_NAMES = {
 # reasons (nfdp.h Reason)
 REASONS = {
     0: "ok", 1: "bad_port", 2: "vlan_drop", 3: "spoof", 4: "acl_deny", 5: "no_route",
-    6: "too_big", 7: "chain_drop", 8: "ttl_expired", 9: "malformed",
+    6: "too_big", 7: "chain_drop", 8: "ttl_expired", 9: "malformed", 10: "remote", 11: "overflow",
+    12: "arp_trap",
 }
 
 PORT_DTYPE = np.dtype(
@@ -57,13 +62,14 @@ PORT_DTYPE = np.dtype(
         ("flags", "<u4"), ("vlan", "<u2"), ("bridge_id", "<u2"),
         ("mac_lo", "<u4"), ("mac_hi", "<u2"), ("gpu", "<u2"),
         ("peer_mac_lo", "<u4"), ("peer_mac_hi", "<u2"), ("default_out", "<u2"),
-        ("ext", "<u4"), ("lag", "<u4"),
+        ("ext", "<u4"), ("lag", "<u2"), ("mtu", "<u2"),
     ]
 )
 CHAIN_DTYPE = np.dtype([("nhops", "u1"), ("hop", "u1", (7,)), ("acl_id", "<u2"), ("flags", "<u2"), ("pad", "<u4")])
 MAC_DTYPE = np.dtype(
-    [("mac_lo", "<u4"), ("mac_hi", "<u2"), ("bridge_id", "<u2"), ("out_port", "<u2"), ("valid", "<u2"), ("pad", "<u4")]
+    [("mac_lo", "<u4"), ("mac_hi", "<u2"), ("bridge_id", "<u2"), ("out_port", "<u2"), ("valid", "<u2"), ("stamp", "<u4")]
 )
+MAC_EMPTY, MAC_STATIC, MAC_TOMB, MAC_LEARNED = 0, 1, 2, 3   # nfdp.h MacValid
 assert PORT_DTYPE.itemsize == 32 and CHAIN_DTYPE.itemsize == 16 and MAC_DTYPE.itemsize == 16
 
 # Microsoft RSS verification key (40 B) — standard Toeplitz key.
@@ -123,15 +129,17 @@ class PortTable:
         self.version = 0
 
     def set(self, idx: int, *, flags=PORT_VALID, vlan=0, bridge_id=0, mac="00:00:00:00:00:00",
-            peer_mac="00:00:00:00:00:00", gpu=0, default_out: int | None = None) -> None:
-        if not 0 <= idx < MAX_PORTS:
+            peer_mac="00:00:00:00:00:00", gpu=0, default_out: int | None = None, mtu: int = 0) -> None:
+        if not 0 <= idx < MAX_PORT_ID:
             raise ValueError(f"port index {idx} out of range")
+        if not 0 <= mtu <= 0xFFFF:
+            raise ValueError("mtu must be in [0, 65535] (0 = no per-port limit)")
         lo, hi = mac_raw(mac)
         plo, phi = mac_raw(peer_mac)
         if default_out is not None:
             flags |= PORT_HAS_DEFAULT
         self.a[idx] = (flags | PORT_VALID, vlan, bridge_id, lo, hi, gpu, plo, phi,
-                       0 if default_out is None else default_out, 0, 0)
+                       0 if default_out is None else default_out, 0, 0, mtu)
         self.version += 1
 
     def update(self, idx: int, **fields) -> None:
@@ -157,6 +165,22 @@ class PortTable:
 
     def valid(self, idx: int) -> bool:
         return bool(self.a[idx]["flags"] & PORT_VALID)
+
+    def set_flag(self, idx: int, bit: int, on: bool = True) -> None:
+        self._flag(idx, bit, on)
+        self.version += 1
+
+    def set_link(self, idx: int, up: bool) -> None:
+        """Link state (ctrl-net LINK_STATUS / RX_STATE): a down port neither receives nor sends."""
+        self._flag(idx, PORT_VALID, up)
+        self.version += 1
+
+    def set_mtu(self, idx: int, mtu: int) -> None:
+        """Egress MTU in L3 bytes (ctrl-net SET_MTU); frames above it are dropped as too_big."""
+        if not 0 <= mtu <= 0xFFFF:
+            raise ValueError("mtu must be in [0, 65535]")
+        self.a[idx]["mtu"] = mtu
+        self.version += 1
 
     def _flag(self, idx: int, bit: int, on: bool) -> None:
         if on:
@@ -188,6 +212,38 @@ class PortTable:
 
     def mirror_port(self, idx: int) -> int | None:
         return int(self.a[idx]["ext"]) >> 16 if self.a[idx]["flags"] & PORT_MIRROR else None
+
+
+class FloodTable:
+    """Per-bridge flood groups (OvS NORMAL broadcast / unknown-unicast flooding): up to
+    ``FLOOD_WAYS`` member ports per bridge, indexed by bridge id."""
+
+    def __init__(self, bridges: int = 4096):
+        self.a = np.full((bridges, FLOOD_WAYS), PORT_NONE, np.uint16)
+        self.n = 0
+        self.version = 0
+
+    def set_members(self, bridge: int, ports: list[int]) -> None:
+        if not 0 <= bridge < len(self.a):
+            raise ValueError("bridge id out of range")
+        if len(ports) > FLOOD_WAYS:
+            raise ValueError(f"at most {FLOOD_WAYS} flood members per bridge")
+        self.a[bridge] = PORT_NONE
+        self.a[bridge, : len(ports)] = ports
+        self.n = max(self.n, bridge + 1) if ports else self.n
+        self.version += 1
+
+    def add_member(self, bridge: int, port: int) -> None:
+        cur = [int(p) for p in self.a[bridge] if p != PORT_NONE]
+        if port not in cur:
+            self.set_members(bridge, cur + [port])
+
+    def remove_member(self, bridge: int, port: int) -> None:
+        cur = [int(p) for p in self.a[bridge] if p != PORT_NONE and p != port]
+        self.set_members(bridge, cur)
+
+    def members(self, bridge: int) -> list[int]:
+        return [int(p) for p in self.a[bridge] if p != PORT_NONE]
 
 
 class LagTable:
@@ -260,6 +316,8 @@ class MacTable:
 
     # Deleted slots become tombstones (valid=2, bridge 0xFFFF which no port uses): the kernel's
     # probe keeps walking over them (it stops only at valid == 0) and never matches them.
+    # Learned entries (valid=3) are inserted by the data plane itself (mac_learn_kernel) and
+    # folded back into this model with merge_learned() before the host uploads the table.
     TOMBSTONE_BRIDGE = 0xFFFF
 
     def _find(self, bridge: int, lo: int, hi: int) -> tuple[int, int]:
@@ -271,7 +329,7 @@ class MacTable:
             e = self.a[i]
             if not e["valid"]:
                 return -1, free if free >= 0 else i
-            if e["valid"] == 2:
+            if e["valid"] == MAC_TOMB:
                 free = i if free < 0 else free
             elif e["mac_lo"] == lo and e["mac_hi"] == hi and e["bridge_id"] == bridge:
                 return i, free
@@ -285,8 +343,51 @@ class MacTable:
         slot = at if at >= 0 else free
         if slot < 0:
             raise RuntimeError("MAC table probe limit reached")
-        self.a[slot] = (lo, hi, bridge, out_port, 1, 0)
+        self.a[slot] = (lo, hi, bridge, out_port, MAC_STATIC, 0)
         self.version += 1
+
+    def insert_learned(self, bridge: int, lo: int, hi: int, out_port: int, stamp: int) -> bool:
+        """Merge one entry the data plane learned (static entries win).  False: no slot."""
+        at, free = self._find(bridge, lo, hi)
+        if at >= 0:
+            if self.a[at]["valid"] == MAC_STATIC:
+                return True
+            slot = at
+        else:
+            slot = free
+        if slot < 0:
+            return False
+        self.a[slot] = (lo, hi, bridge, out_port, MAC_LEARNED, stamp)
+        self.version += 1
+        return True
+
+    def merge_learned(self, dev: np.ndarray) -> int:
+        """Fold the device table's learned entries (valid == 3) into this host model."""
+        n = 0
+        for e in dev[dev["valid"] == MAC_LEARNED]:
+            n += self.insert_learned(int(e["bridge_id"]), int(e["mac_lo"]), int(e["mac_hi"]), int(e["out_port"]),
+                                     int(e["stamp"]))
+        return n
+
+    def age(self, now: int, max_age: int) -> int:
+        """Remove learned entries last seen more than `max_age` stamps ago (host aging)."""
+        old = np.where((self.a["valid"] == MAC_LEARNED) & ((now - self.a["stamp"].astype(np.int64)) > max_age))[0]
+        for i in old:
+            self.a[i] = (0xFFFFFFFF, 0xFFFF, self.TOMBSTONE_BRIDGE, 0xFFFF, MAC_TOMB, 0)
+        if len(old):
+            self.version += 1
+        return len(old)
+
+    def learned(self) -> list[tuple[int, str, int]]:
+        """(bridge, mac, port) of every learned entry."""
+        from ..ops.packets import mac_str
+
+        out = []
+        for e in self.a[self.a["valid"] == MAC_LEARNED]:
+            lo, hi = int(e["mac_lo"]), int(e["mac_hi"])
+            raw = bytes([lo & 0xFF, lo >> 8 & 0xFF, lo >> 16 & 0xFF, lo >> 24 & 0xFF, hi & 0xFF, hi >> 8 & 0xFF])
+            out.append((int(e["bridge_id"]), mac_str(raw), int(e["out_port"])))
+        return out
 
     def lookup(self, bridge: int, mac) -> int:
         lo, hi = mac_raw(mac)
@@ -298,7 +399,7 @@ class MacTable:
         at, _ = self._find(bridge, lo, hi)
         if at < 0:
             return False
-        self.a[at] = (0xFFFFFFFF, 0xFFFF, self.TOMBSTONE_BRIDGE, 0xFFFF, 2, 0)
+        self.a[at] = (0xFFFFFFFF, 0xFFFF, self.TOMBSTONE_BRIDGE, 0xFFFF, MAC_TOMB, 0)
         self.version += 1
         return True
 

@@ -1,17 +1,25 @@
-"""Vectorized synthetic packet crafting / checking (numpy), 64-byte slots.
+"""Vectorized synthetic packet crafting / checking (numpy): header slots + full frames.
 
-Used by tests, the benchmark and the traffic generator.  Frames are written into fixed 64-B
-slots (the data-plane slot size, ``_nfdp.SLOT_BYTES``); a "64-byte packet" on the wire is a
-60-byte frame plus 4-byte FCS, so an untagged 64-B packet occupies 60 B of its slot and a
-VLAN-tagged one the full 64 B.
+Used by tests, the benchmark and the traffic generator.  The data plane reads a 64-B header
+slot per packet (``_nfdp.SLOT_BYTES``): the first min(len, 64) bytes of the frame, with the
+whole frame's length in the ingress meta word.  The payload beyond the slot stays where the I/O
+layer put it (``craft_full`` returns it).  A "64-byte packet" on the wire is a 60-byte frame plus
+4-byte FCS, so an untagged 64-B packet occupies 60 B of its slot and a VLAN-tagged one 64 B.
+
+Egress meta word (nfdp.h make_meta): port[11:0] (0xFFF none, 0xFFE punt) | len[25:12] |
+reason[29:26] | xhdr[30].  The frame that leaves is ``ohdr[:hl] ++ in_frame[to:len]``
+(``out_tail``/``assemble``).
 """
 from __future__ import annotations
 
 import numpy as np
 
 SLOT = 64
+MAX_FRAME = 9600      # nfdp.h kMaxFrame
+ENCAP_BYTES = 50      # nfdp.h kEncapBytes (outer Ethernet + IPv4 + UDP + VXLAN/GENEVE)
 ETH_IPV4 = 0x0800
 ETH_VLAN = 0x8100
+ETH_ARP = 0x0806
 
 
 def mac_bytes(mac) -> np.ndarray:
@@ -91,15 +99,71 @@ def craft(
     frame_len: int = 60,
     payload_seed: int = 0,
 ) -> tuple[np.ndarray, np.ndarray]:
-    """Craft n IPv4 UDP/TCP frames into 64-B slots.
+    """Craft n IPv4 UDP/TCP frames; returns their 64-B header slots.
 
     Per-packet arrays (length n) or scalars for every field.  ``dmac``/``smac`` are [n,6] or [6]
     uint8.  ``vlan``: None (untagged) or per-packet VID array (-1 = untagged).  ``frame_len`` is
-    the untagged L2 length (<= 60 so a tag still fits the slot).  Returns (slots uint8[n,64],
-    lens uint32[n]) with valid IPv4 and L4 checksums.
+    the untagged L2 length without FCS (42..9596).  Returns (slots uint8[n,64], lens uint32[n])
+    with valid IPv4 and L4 checksums over the whole frame; ``craft_full`` also returns the frames.
     """
-    if frame_len < 42 or frame_len > 60:
-        raise ValueError("frame_len must be in [42, 60] (untagged, without FCS)")
+    frames, lens = craft_full(n, dmac=dmac, smac=smac, src_ip=src_ip, dst_ip=dst_ip, sport=sport, dport=dport,
+                              proto=proto, ttl=ttl, vlan=vlan, frame_len=frame_len, payload_seed=payload_seed)
+    return header_slots(frames, lens), lens
+
+
+def craft_arp(n: int, *, smac, sender_ip, target_ip, op: int = 1, vlan=None, dmac="ff:ff:ff:ff:ff:ff"):
+    """n ARP frames (request by default, broadcast), padded to 60 B (+4 with a tag).
+    Returns (frames uint8[n, 64], lens)."""
+    fr = np.zeros((n, 64), np.uint8)
+    fr[:, 0:6] = mac_bytes(dmac)
+    fr[:, 6:12] = np.broadcast_to(mac_bytes(smac) if np.ndim(smac) <= 1 else np.asarray(smac, np.uint8), (n, 6))
+    _put16(fr, 12, np.full(n, ETH_ARP))
+    _put16(fr, 14, np.full(n, 1))          # htype Ethernet
+    _put16(fr, 16, np.full(n, ETH_IPV4))   # ptype IPv4
+    fr[:, 18], fr[:, 19] = 6, 4
+    _put16(fr, 20, np.full(n, op))
+    fr[:, 22:28] = fr[:, 6:12]
+    _put32(fr, 28, np.broadcast_to(np.asarray(sender_ip, np.uint32), (n,)))
+    _put32(fr, 38, np.broadcast_to(np.asarray(target_ip, np.uint32), (n,)))
+    lens = np.full(n, 60, np.uint32)
+    if vlan is not None:
+        t = fr.copy()
+        fr[:, 12:14] = (0x81, 0x00)
+        fr[:, 14] = (int(vlan) >> 8) & 0x0F
+        fr[:, 15] = int(vlan) & 0xFF
+        fr[:, 16:64] = t[:, 12:60]
+        lens[:] = 64
+    return fr, lens
+
+
+def header_slots(frames: np.ndarray, lens: np.ndarray) -> np.ndarray:
+    """[n, stride] frames -> [n, 64] header slots (first min(len, 64) bytes, zero padded)."""
+    slots = np.zeros((frames.shape[0], SLOT), np.uint8)
+    w = min(SLOT, frames.shape[1])
+    slots[:, :w] = frames[:, :w]
+    cols = np.arange(SLOT)[None, :]
+    slots[cols >= np.asarray(lens, np.int64)[:, None]] = 0
+    return slots
+
+
+def craft_full(
+    n: int,
+    *,
+    dmac,
+    smac,
+    src_ip,
+    dst_ip,
+    sport,
+    dport,
+    proto: int = 17,
+    ttl: int = 64,
+    vlan=None,
+    frame_len: int = 60,
+    payload_seed: int = 0,
+) -> tuple[np.ndarray, np.ndarray]:
+    """Like ``craft`` but returns the whole frames: (frames uint8[n, frame_len + 4], lens)."""
+    if frame_len < 42 or frame_len > MAX_FRAME - 4:
+        raise ValueError(f"frame_len must be in [42, {MAX_FRAME - 4}] (untagged, without FCS)")
     l3 = np.zeros((n, frame_len), np.uint8)
     dm = np.broadcast_to(mac_bytes(dmac) if np.ndim(dmac) <= 1 else np.asarray(dmac, np.uint8), (n, 6))
     sm = np.broadcast_to(mac_bytes(smac) if np.ndim(smac) <= 1 else np.asarray(smac, np.uint8), (n, 6))
@@ -135,24 +199,24 @@ def craft(
     _put16(l3, 24, _csum16(_be16_words(l3, 14, 34)))
     if proto in (6, 17):
         set_l4_csum(l3, proto)
-    slots = np.zeros((n, SLOT), np.uint8)
+    frames = np.zeros((n, max(frame_len + 4, SLOT)), np.uint8)
     lens = np.full(n, frame_len, np.uint32)
     if vlan is None:
-        slots[:, :frame_len] = l3
+        frames[:, :frame_len] = l3
     else:
         vid = np.broadcast_to(np.asarray(vlan, np.int64), (n,))
         tagged = vid >= 0
-        slots[~tagged, :frame_len] = l3[~tagged]
+        frames[~tagged, :frame_len] = l3[~tagged]
         t = np.where(tagged)[0]
         if len(t):
-            slots[t, 0:12] = l3[t, 0:12]
-            slots[t, 12] = 0x81
-            slots[t, 13] = 0x00
-            slots[t, 14] = (vid[t] >> 8) & 0x0F
-            slots[t, 15] = vid[t] & 0xFF
-            slots[t, 16 : frame_len + 4] = l3[t, 12:frame_len]
+            frames[t, 0:12] = l3[t, 0:12]
+            frames[t, 12] = 0x81
+            frames[t, 13] = 0x00
+            frames[t, 14] = (vid[t] >> 8) & 0x0F
+            frames[t, 15] = vid[t] & 0xFF
+            frames[t, 16 : frame_len + 4] = l3[t, 12:frame_len]
             lens[t] = frame_len + 4
-    return slots, lens
+    return frames, lens
 
 
 def set_l4_csum(l3: np.ndarray, proto: int) -> None:
@@ -222,16 +286,44 @@ def check_csums(frames: np.ndarray, lens: np.ndarray) -> np.ndarray:
 
 
 def inmeta(in_port, lens) -> np.ndarray:
-    """Per-packet ingress metadata word: in_port | len << 16."""
+    """Per-packet ingress metadata word: in_port | len << 16 (len = whole frame, <= 9600)."""
     return (np.asarray(in_port, np.uint32) & 0xFFFF) | (np.asarray(lens, np.uint32) << 16)
 
 
+def make_meta(port, length, reason=0, xhdr=False) -> np.ndarray:
+    """nfdp.h make_meta (vectorized)."""
+    return ((np.asarray(port, np.uint32) & 0xFFF) | ((np.asarray(length, np.uint32) & 0x3FFF) << 12)
+            | ((np.asarray(reason, np.uint32) & 0xF) << 26) | (np.asarray(xhdr, np.uint32) << 30)).astype(np.uint32)
+
+
 def meta_fields(meta: np.ndarray) -> tuple[np.ndarray, np.ndarray, np.ndarray]:
-    """Egress metadata -> (out_port, len, reason).  Bit 31 (mirror request) is not part of reason."""
+    """Egress metadata -> (out_port, len, reason); port 0xFFF / 0xFFE read back as 0xFFFF / 0xFFFE."""
     m = np.asarray(meta, np.uint32)
-    return m & 0xFFFF, (m >> 16) & 0xFF, (m >> 24) & 0x7F
+    port = m & 0xFFF
+    port = np.where(port >= 0xFFE, port | 0xF000, port)
+    return port, (m >> 12) & 0x3FFF, (m >> 26) & 0xF
 
 
-def meta_mirror(meta: np.ndarray) -> np.ndarray:
-    """Per-packet bool: the frame must also be copied to its ingress port's mirror port (K9)."""
-    return (np.asarray(meta, np.uint32) >> 31).astype(bool)
+def meta_xhdr(meta: np.ndarray) -> np.ndarray:
+    """Per-packet bool: prepend the packet's 64-B outer-header record (tunnel encap)."""
+    return ((np.asarray(meta, np.uint32) >> 30) & 1).astype(bool)
+
+
+def out_tail(in_len, olen, xhdr=False):
+    """nfdp.h out_tail: (hl, to) - valid header bytes of the out slot, tail offset in the input."""
+    d = np.asarray(olen, np.int64) - np.where(xhdr, ENCAP_BYTES, 0) - np.asarray(in_len, np.int64)
+    h = np.minimum(np.minimum(np.asarray(in_len, np.int64), SLOT) + d, SLOT)
+    return h, h - d
+
+
+def assemble(ohdr: np.ndarray, meta: int, in_frame: np.ndarray, in_len: int, xhdr_rec: np.ndarray | None = None) -> bytes:
+    """The frame that leaves for one packet: [outer header] ++ ohdr[:hl] ++ in_frame[to:in_len]."""
+    _, olen, _ = meta_fields(np.array([meta], np.uint32))
+    x = bool(meta_xhdr(np.array([meta], np.uint32))[0])
+    hl, to = out_tail(in_len, int(olen[0]), x)
+    hl, to = int(hl), int(to)
+    pre = bytes(np.asarray(xhdr_rec, np.uint8)[:ENCAP_BYTES]) if x else b""
+    out = pre + bytes(np.asarray(ohdr, np.uint8)[:hl]) + bytes(np.asarray(in_frame, np.uint8)[to:in_len])
+    if len(out) != int(olen[0]):
+        raise ValueError(f"assembled {len(out)} bytes, meta says {int(olen[0])}")
+    return out

@@ -2,7 +2,7 @@
 
 The flow table is hash-partitioned across ranks (owner = top bits of the Toeplitz hash, the same
 bits an RSS indirection table would use).  Every rank keeps the full (small) port / chain / MAC /
-ACL tables.  A step moves, per packet, a 16-B descriptor to the flow owner and a 16-B verdict
+ACL tables.  A step moves, per packet, a 32-B descriptor to the flow owner and a 16-B verdict
 back; the 64-B payload crosses xGMI at most once, to the GPU that owns the destination pod.
 All exchange segments have static capacity, so each collective is a fixed-size
 ``all_to_all_single`` (one xGMI link per peer, no ring) and the step never round-trips to the host.
@@ -51,6 +51,7 @@ class ShardedDataPlane:
         self.cap_desc = int(math.ceil(per * slack + 6 * math.sqrt(per) + 256))
         self.cap_pkt = self.cap_desc
         self.dseg = self.nf.desc_seg_bytes(self.cap_desc)
+        self.vseg = self.nf.verdict_seg_bytes(self.cap_desc)
         self.pseg = self.nf.pkt_seg_bytes(self.cap_pkt)
         self.hash_mode = dp.hash_mode if hash_mode is None else hash_mode
         if self.hash_mode == 0:
@@ -60,8 +61,8 @@ class ShardedDataPlane:
         i32 = dict(dtype=torch.int32, device=self.dev)
         self.send_desc = torch.zeros(world * self.dseg, **u8)
         self.recv_desc = torch.zeros(world * self.dseg, **u8)
-        self.send_verdict = torch.zeros(world * self.dseg, **u8)
-        self.recv_verdict = torch.zeros(world * self.dseg, **u8)
+        self.send_verdict = torch.zeros(world * self.vseg, **u8)
+        self.recv_verdict = torch.zeros(world * self.vseg, **u8)
         self.send_pkt = torch.zeros(world * self.pseg, **u8)
         self.recv_pkt = torch.zeros(world * self.pseg, **u8)
         self.cnt = torch.zeros(world, **i32)
@@ -177,7 +178,7 @@ def simulate_step(engines: list, batches: list) -> None:
     _local_a2a(engines, "send_desc", "recv_desc", engines[0].dseg)
     for e in engines:
         e.phase_owner()
-    _local_a2a(engines, "send_verdict", "recv_verdict", engines[0].dseg)
+    _local_a2a(engines, "send_verdict", "recv_verdict", engines[0].vseg)
     for e in engines:
         e.phase_apply()
     _local_a2a(engines, "send_pkt", "recv_pkt", engines[0].pseg)

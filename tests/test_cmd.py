@@ -174,7 +174,7 @@ def test_pipeline_server_entry():
     dp.commit(full=True)
     port = _free_port()
     stop = threading.Event()
-    t = threading.Thread(target=p4rt_server.main, args=([f"--address=127.0.0.1:{port}", "--lag", "0:4095"],),
+    t = threading.Thread(target=p4rt_server.main, args=([f"--address=127.0.0.1:{port}", "--lag", "0:4093"],),
                          kwargs={"stop": stop, "dataplane": dp}, daemon=True)
     t.start()
     try:

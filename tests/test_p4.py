@@ -41,7 +41,11 @@ def send(dp, in_port, dmac, smac=VF_A, vlan=None, sport=1):
     dp.commit()
     r = dp.run(frames, P.inmeta(np.array([in_port]), lens))
     op, ln, reason = P.meta_fields(r.meta)
-    return int(op[0]), int(reason[0]), r.out[0], bool(P.meta_mirror(r.meta)[0]), int(r.extra["hash"][0])
+    # K9: the mirror copy is a replica (side output) addressed to the ingress port's mirror port
+    sr = dp.side_result()
+    mp = dp.ports.mirror_port(in_port)
+    mirror = mp is not None and sr["n_rep"] > 0 and bool(np.any(P.meta_fields(sr["rep_meta"])[0] == mp))
+    return int(op[0]), int(reason[0]), r.out[0], mirror, int(r.extra["hash"][0])
 
 
 def test_text_format_parser():
@@ -129,14 +133,14 @@ def test_host_vf_fxp_semantics(dp):
 
 
 def test_lag_mirror_vlan_bridge(dp):
-    rt = P4Runtime(dp, lag_ports={0: 4095})
+    rt = P4Runtime(dp, lag_ports={0: 4093})
     c = InProcessP4rtClient({"br0": rt})
     # LAG group 0 spread over phy ports 0/1 by hash[2:0]
     rules = [Rule("add-entry", "br0", C + "tx_lag_table",
                   f"user_meta.cmeta.lag_group_id=0/255,hash={h}/7,priority=1,"
                   f"action=linux_networking_control.set_egress_port(0,{h % 2})") for h in range(8)]
     rules.append(Rule("add-entry", "br0", C + "tx_acc_vsi",
-                      "vmeta.common.vsi=8,zero_padding=0,action=linux_networking_control.l2_fwd_and_bypass_bridge(4095)"))
+                      "vmeta.common.vsi=8,zero_padding=0,action=linux_networking_control.l2_fwd_and_bypass_bridge(4093)"))
     assert program_rules(c, rules) == []
     seen = set()
     for sport in range(1, 40):
