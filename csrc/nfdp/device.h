@@ -40,22 +40,47 @@ typedef int v8i_t __attribute__((ext_vector_type(8)));
 typedef float v4f_t __attribute__((ext_vector_type(4)));
 constexpr int kE8M0One = 0x7F7F7F7F;  // block scales 2^0 (every byte)
 
+// ACL (TCAM) rule tiles: 16 rules x 128 key bits per tile.  Up to kLdsAclTiles tiles are staged
+// in LDS (A fragments + C init); tiles beyond that are read from the global copy (L2-resident)
+// when their prefilter lets a wave through.  The global C-init buffer is followed by the
+// per-tile prefilters [tiles][8] and the per-group (8 tiles) prefilters [groups][8] (host.cpp
+// build_acl_frags).
+constexpr uint32_t kLdsAclTiles = 64;
+constexpr uint32_t kAclGroup = 8;
+constexpr uint32_t kAclIdxBits = 12;                      // rule index bits: up to 4096 rules
+constexpr uint32_t kAclMaxRules = 1u << kAclIdxBits;
+constexpr int kE8M0Idx = 0x8B8B8B8B;                      // block scales 2^12 = 2^kAclIdxBits
+struct AclView {
+  const v4i* lw; const v4i* lc;   // LDS: first min(tiles, kLdsAclTiles) tiles
+  const v4i* gw; const v4i* gc;   // global: all tiles (+ prefilters after gc's tiles * 4 entries)
+  uint32_t tiles;
+};
+NFDP_HD uint32_t acl_groups(uint32_t tiles) { return (tiles + kAclGroup - 1) / kAclGroup; }
+// Raw first-match value (mismatch << 12 | rule) -> rule index or -1.
+NFDP_HD int acl_rule_of(uint32_t b, uint32_t n_acl) {
+  const int r = (b >> kAclIdxBits) == 0 ? (int)(b & (kAclMaxRules - 1)) : -1;
+  return r >= (int)n_acl ? -1 : r;
+}
+
 // Wave-level classification over the wave's 64 packets (one per lane).  EXEC must be full.
 // ACL (TCAM) on the gfx950 block-scaled FP4 MFMA: v_mfma_scale_f32_16x16x128_f8f6f4 with e2m1
-// operands covers the whole 128-bit key in ONE instruction per 16 rules x 16 packets (the i8
-// form needs two 16x16x64) at the same cycles: half the matrix time and half the B-operand
-// registers.  Rule weights {-1, 0, +1} and key bits {0, 1} are exact in e2m1, the FP32 sums
-// (|x| <= 128) are exact integers.  Lane l holds K = 32 (l >> 4) + j, j < 32, i.e. bit j of key
-// word l >> 4, as nibble j (tools/fp4_probe.hip pins the operand and C/D maps on exact data).
+// operands covers the whole 128-bit key in ONE instruction per 16 rules x 16 packets.  Rule
+// weights {-1, 0, +1} and key bits {0, 1} are exact in e2m1; the A block scale 2^12 turns them
+// into {-4096, 0, +4096} and the C init of rule r is bias_r * 4096 + r, so every accumulator IS
+// (mismatch << 12) | r, exactly (|x| < 2^20 in f32).  First match = an integer min over the f32
+// bit patterns (all values are >= 0): no second pass, and rules may sit in any tile in any
+// order (the host groups similar rules).  Lane l holds K = 32 (l >> 4) + j, j < 32, i.e. bit j
+// of key word l >> 4, as nibble j (tools/fp4_probe.hip pins the operand and C/D maps).
+// Prefilter: a tile (and a group of 8 tiles) carries the bits ALL its rules care about and agree
+// on; a wave skips it - no LDS reads, no MFMAs - unless one of its packets has those bits.
 // The MFMA Toeplitz hash keeps the i8 form (it needs the parity of integer sums).
 template <int HASH, int ACL>
-__device__ __forceinline__ void classify_wave(const FlowKey& key, uint4* kx, const v4i* lw,
-                                              const v4i* lc, uint32_t acl_tiles, const v4i* lt,
+__device__ __forceinline__ void classify_wave(const FlowKey& key, uint4* kx, const AclView& av, const v4i* lt,
                                               const uint32_t* ltab, const TablesView& t,
                                               uint32_t& hash, int& acl_rule, uint32_t tile0 = 0,
                                               uint32_t tstep = 1, uint32_t* best_out = nullptr) {
   // tile0 / tstep: this wave scans rule tiles tile0, tile0 + tstep, ... (cooperating waves split
-  // one chunk's ACL); best_out: the raw (mismatch << 10 | rule) minimum, for combining partials.
+  // one chunk's ACL); best_out: the raw (mismatch << 12 | rule) minimum, for combining partials.
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t g = lane >> 4, col = lane & 15u;
   v4i bf[4][2];   // i8 B operands (MFMA hash)
@@ -116,104 +141,71 @@ __device__ __forceinline__ void classify_wave(const FlowKey& key, uint4* kx, con
   // ---- ACL (TCAM) ----
   if constexpr (ACL == kAclMfma) {
     uint32_t best[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
-    // Two tiles per pass-1 test (eight independent MFMAs in flight before the wave-uniform
-    // branch) pays in the MFMA-hash kernels: same-box A/B mfma+ACL1024 6.9-7.0 -> 7.4 Gpps.  In
-    // the LDS-hash kernels the extra live accumulators spill (5 -> 28 VGPRs) and ACL256 drops
-    // 15.2 -> 13.7 Gpps, so they keep one tile per test (profiles/r1_s4_acl_pairs_ab.log).
-    if constexpr (HASH == kHashMfma) {
-    // Pass 2 of one tile (see below): the (mismatch << 10 | rule) first-match epilogue.
-    auto epilogue = [&](uint32_t nt, const v8i_t& a, v4f_t c2) {
-      asm volatile("" : "+v"(c2));
-      const uint32_t rb = nt * 16u + 4u * g;
-#pragma unroll
-      for (int tt = 0; tt < 4; ++tt) {
-        const v8i_t b = {bq[tt][0], bq[tt][1], bq[tt][2], bq[tt][3], 0, 0, 0, 0};
-        const v4f_t acc = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c2, 4, 4, 0, kE8M0One, 0, kE8M0One);
-        const uint32_t e0 = ((uint32_t)acc[0] << 10) | (rb + 0);
-        const uint32_t e1 = ((uint32_t)acc[1] << 10) | (rb + 1);
-        const uint32_t e2 = ((uint32_t)acc[2] << 10) | (rb + 2);
-        const uint32_t e3 = ((uint32_t)acc[3] << 10) | (rb + 3);
-        best[tt] = min(best[tt], min(min(e0, e1), min(e2, e3)));
-      }
+    // prefilters through the constant address space: wave-uniform s_load (lgkmcnt), so testing
+    // one never waits for the frame prefetch in flight (vmcnt)
+    typedef const __attribute__((address_space(4))) uint32_t* cu32;
+    const cu32 pf = (cu32)(reinterpret_cast<const uint32_t*>(av.gc) + (size_t)av.tiles * 16);  // [tiles][8]
+    const cu32 gpf = pf + (size_t)av.tiles * 8;                                                // [groups][8]
+    auto pass = [&](cu32 f) {
+      const uint32_t x = ((key.src_ip & f[0]) ^ f[4]) | ((key.dst_ip & f[1]) ^ f[5]) |
+                         ((key.ports & f[2]) ^ f[6]) | ((key.meta & f[3]) ^ f[7]);
+      return __any(x == 0u);
     };
-    // An odd last tile is tested twice (pass 2 is idempotent under min).
-    for (uint32_t nt = tile0; nt < acl_tiles; nt += 2 * tstep) {
-      const uint32_t nu = nt + tstep < acl_tiles ? nt + tstep : nt;
-      const v4i a4 = lw[nt * 64 + lane], a4u = lw[nu * 64 + lane];
+    // tiles past the LDS copy: buffer loads (a distinct path the compiler cannot merge with the
+    // ds_reads into FLAT loads)
+    const __amdgpu_buffer_rsrc_t r_gw = __builtin_amdgcn_make_buffer_rsrc((void*)av.gw, (short)0,
+                                                                         (int)(av.tiles * 1024u), 0x00020000);
+    const __amdgpu_buffer_rsrc_t r_gc = __builtin_amdgcn_make_buffer_rsrc((void*)av.gc, (short)0,
+                                                                         (int)(av.tiles * 64u), 0x00020000);
+    auto run_tile = [&](const v4i& a4, const v4i& ci) {
       const v8i_t a = {a4[0], a4[1], a4[2], a4[3], 0, 0, 0, 0};
-      const v8i_t au = {a4u[0], a4u[1], a4u[2], a4u[3], 0, 0, 0, 0};
-      const v4i ci = lc[nt * 4 + g], ciu = lc[nu * 4 + g];
       const v4f_t c = {__int_as_float(ci[0]), __int_as_float(ci[1]), __int_as_float(ci[2]), __int_as_float(ci[3])};
-      const v4f_t cu = {__int_as_float(ciu[0]), __int_as_float(ciu[1]), __int_as_float(ciu[2]), __int_as_float(ciu[3])};
-      v4f_t acc[8];
-#pragma unroll
-      for (int tt = 0; tt < 4; ++tt) {
-        const v8i_t b = {bq[tt][0], bq[tt][1], bq[tt][2], bq[tt][3], 0, 0, 0, 0};
-        acc[tt] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 4, 4, 0, kE8M0One, 0, kE8M0One);
-        acc[4 + tt] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(au, b, cu, 4, 4, 0, kE8M0One, 0, kE8M0One);
-      }
-      uint32_t z = 0xFFFFFFFFu;
-#pragma unroll
-      for (int tt = 0; tt < 8; ++tt) {
-        z = min(z, min(__float_as_uint(acc[tt][0]), __float_as_uint(acc[tt][1])));
-        z = min(z, min(__float_as_uint(acc[tt][2]), __float_as_uint(acc[tt][3])));
-      }
-      if (!__any(z == 0u)) continue;
-      epilogue(nt, a, c);
-      epilogue(nu, au, cu);
-    }
-    } else {
-    for (uint32_t nt = tile0; nt < acl_tiles; nt += tstep) {
-      const v4i a4 = lw[nt * 64 + lane];
-      const v8i_t a = {a4[0], a4[1], a4[2], a4[3], 0, 0, 0, 0};
-      const v4i ci = lc[nt * 4 + g];
-      const v4f_t c = {__int_as_float(ci[0]), __int_as_float(ci[1]), __int_as_float(ci[2]), __int_as_float(ci[3])};
-      // Pass 1: does ANY packet of the wave match ANY rule of this tile?  (mismatch counts are
-      // >= 0, so a zero minimum = a match.)  Most tiles of a deny-list ACL match nothing, and
-      // then the priority epilogue below is skipped wave-uniformly.
-      // Four independent accumulators: the MFMAs issue back to back instead of each waiting
-      // for the previous result.  The sums are non-negative integers and +0.0 exactly on a match
-      // (a -1 weight implies a bias >= 1, and x + (-x) rounds to +0), so the minimum is taken on
-      // the f32 bit patterns with integer min3 (no NaN canonicalization) and tested against 0.
+      // four independent accumulators (one per 16-packet group) issue back to back
       v4f_t acc[4];
 #pragma unroll
       for (int tt = 0; tt < 4; ++tt) {
         const v8i_t b = {bq[tt][0], bq[tt][1], bq[tt][2], bq[tt][3], 0, 0, 0, 0};
-        acc[tt] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 4, 4, 0, kE8M0One, 0, kE8M0One);
+        acc[tt] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 4, 4, 0, kE8M0Idx, 0, kE8M0One);
       }
-      uint32_t z = 0xFFFFFFFFu;
 #pragma unroll
       for (int tt = 0; tt < 4; ++tt) {
-        z = min(z, min(__float_as_uint(acc[tt][0]), __float_as_uint(acc[tt][1])));
-        z = min(z, min(__float_as_uint(acc[tt][2]), __float_as_uint(acc[tt][3])));
+        best[tt] = min(best[tt], min(min(__float_as_uint(acc[tt][0]), __float_as_uint(acc[tt][1])),
+                                     min(__float_as_uint(acc[tt][2]), __float_as_uint(acc[tt][3]))));
       }
-      if (!__any(z == 0u)) continue;
-      // Pass 2 (rare): recompute the tile with the (mismatch << 10 | rule) first-match epilogue.
-      // The bias goes through an opaque copy so the MFMAs are not CSE'd with pass 1.
-      v4f_t c2 = c;
-      asm volatile("" : "+v"(c2));
-      const uint32_t rb = nt * 16u + 4u * g;
-#pragma unroll
-      for (int tt = 0; tt < 4; ++tt) {
-        const v8i_t b = {bq[tt][0], bq[tt][1], bq[tt][2], bq[tt][3], 0, 0, 0, 0};
-        const v4f_t acc = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c2, 4, 4, 0, kE8M0One, 0, kE8M0One);
-        const uint32_t e0 = ((uint32_t)acc[0] << 10) | (rb + 0);
-        const uint32_t e1 = ((uint32_t)acc[1] << 10) | (rb + 1);
-        const uint32_t e2 = ((uint32_t)acc[2] << 10) | (rb + 2);
-        const uint32_t e3 = ((uint32_t)acc[3] << 10) | (rb + 3);
-        best[tt] = min(best[tt], min(min(e0, e1), min(e2, e3)));
+    };
+    // Two phases so that the LDS-resident tiles never share a join point with global loads (the
+    // wait there would be vmcnt(0): the frame prefetch in flight).  Groups of 8 tiles never
+    // straddle kLdsAclTiles (a multiple of 8).
+    const uint32_t ngroups = acl_groups(av.tiles);
+    const uint32_t lds_groups = min(ngroups, kLdsAclTiles / kAclGroup);
+    for (uint32_t gi = 0; gi < lds_groups; ++gi) {
+      if (!pass(gpf + 8 * gi)) continue;
+      const uint32_t t_beg = gi * kAclGroup, t_end = min(av.tiles, t_beg + kAclGroup);
+      // this wave's first tile of the group (tiles == tile0 mod tstep)
+      for (uint32_t nt = t_beg + (tile0 + tstep - t_beg % tstep) % tstep; nt < t_end; nt += tstep) {
+        if (!pass(pf + 8 * nt)) continue;
+        run_tile(av.lw[nt * 64 + lane], av.lc[nt * 4 + g]);
       }
     }
+    for (uint32_t gi = lds_groups; gi < ngroups; ++gi) {
+      if (!pass(gpf + 8 * gi)) continue;
+      const uint32_t t_beg = gi * kAclGroup, t_end = min(av.tiles, t_beg + kAclGroup);
+      for (uint32_t nt = t_beg + (tile0 + tstep - t_beg % tstep) % tstep; nt < t_end; nt += tstep) {
+        if (!pass(pf + 8 * nt)) continue;
+        run_tile(__builtin_bit_cast(v4i, __builtin_amdgcn_raw_buffer_load_b128(r_gw, (nt * 64u + lane) * 16u, 0, 0)),
+                 __builtin_bit_cast(v4i, __builtin_amdgcn_raw_buffer_load_b128(r_gc, (nt * 4u + g) * 16u, 0, 0)));
+      }
     }
 #pragma unroll
     for (int tt = 0; tt < 4; ++tt) {
       best[tt] = min(best[tt], (uint32_t)__shfl_xor(best[tt], 16));
       best[tt] = min(best[tt], (uint32_t)__shfl_xor(best[tt], 32));
     }
-    const uint32_t b = pick4(g, best[0], best[1], best[2], best[3]);
+    const uint32_t bb = pick4(g, best[0], best[1], best[2], best[3]);
+    // f32 bits -> the exact integer (mismatch << 12 | rule); "no tile ran" stays all-ones
+    const uint32_t b = bb == 0xFFFFFFFFu ? bb : (uint32_t)__uint_as_float(bb);
     if (best_out) *best_out = b;
-    acl_rule = (b >> 10) == 0 ? (int)(b & 1023u) : -1;
-    if (acl_rule >= (int)t.n_acl) acl_rule = -1;
+    acl_rule = acl_rule_of(b, t.n_acl);
   } else if constexpr (ACL == kAclScalar) {
     acl_rule = acl_first_match(t, key);
   } else {
@@ -267,7 +259,7 @@ struct LdsTables {
 __device__ __forceinline__ LdsTables stage_lds_tables(const TablesView& t, PortEntry* lport, uint64_t* lchain,
                                                       uint8_t* lperm, bool enabled, uint32_t nthreads) {
   const uint32_t nchain = enabled ? min(t.n_chains, kLdsChains) : 0u;
-  const bool lds_perm = enabled && t.n_acl <= 1024;
+  const bool lds_perm = enabled && t.n_acl <= 1024;  // verdict bytes staged for the first 1024 rules
   if (enabled) {
     const uint4* gp = reinterpret_cast<const uint4*>(t.ports);
     uint4* lp = reinterpret_cast<uint4*>(lport);

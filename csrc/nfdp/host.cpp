@@ -5,6 +5,7 @@
 #include <cstring>
 
 #include <algorithm>
+#include <tuple>
 
 namespace nfdp {
 
@@ -120,42 +121,98 @@ std::vector<std::pair<int64_t, int64_t>> FlowTableHost::take_moves() {
 // v_mfma_scale_f32_16x16x128_f8f6f4, e2m1: lane l holds rule row (l & 15) of the tile and
 // K = 32 (l >> 4) + j for j < 32 as nibble j (little-endian nibbles of 4 dwords); K = key bit,
 // LSB-first over the 4 LE key dwords.  Weights: cared bit set -> -1.0 (0xA), cared bit clear ->
-// +1.0 (0x2), don't care -> 0.  C init = the rule's count of cared set bits (f32 bits), so
-// mismatch = bias + sum(w * bit) is 0 exactly on a ternary match.
+// +1.0 (0x2), don't care -> 0; the kernel scales A by 2^12.  C init of the row holding rule r =
+// bias_r * 4096 + r (bias = the rule's count of cared set bits), so the accumulator is exactly
+// (mismatch << 12) | r and 0 mismatches = a ternary match of rule r.
+// Rules are placed in tiles by field signature (similar rules together) and every tile / group
+// of kAclGroup tiles gets a prefilter: the key bits all of its rules care about and agree on.
+// Output buffer `cinit` = [tiles][4][4] C init | [tiles][8] tile prefilters (mask[4], value[4]) |
+// [groups][8] group prefilters.
 // ------------------------------------------------------------------------------------------
 static inline int key_bit(const uint32_t* w, int b) { return (w[b >> 5] >> (b & 31)) & 1; }
+static inline uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+
+namespace {
+// common cared-and-agreeing bits of a rule set -> (mask[4], value[4]); an empty set admits nothing
+void prefilter(const uint32_t* value, const uint32_t* mask, const uint32_t* rules, uint32_t nr, uint32_t* out) {
+  if (nr == 0) {
+    for (int w = 0; w < 4; ++w) { out[w] = 0xFFFFFFFFu; out[4 + w] = 0; }
+    out[7] = kSlotUsed;  // key.meta byte 1 is always 0 in a packet key: nothing passes
+    return;
+  }
+  for (int w = 0; w < 4; ++w) {
+    uint32_t cm = 0xFFFFFFFFu, diff = 0;
+    const uint32_t v0 = value[4 * rules[0] + w] & mask[4 * rules[0] + w];
+    for (uint32_t k = 0; k < nr; ++k) {
+      const uint32_t r = rules[k];
+      cm &= mask[4 * r + w];
+      diff |= (value[4 * r + w] & mask[4 * r + w]) ^ v0;
+    }
+    cm &= ~diff;
+    out[w] = cm;
+    out[4 + w] = v0 & cm;
+  }
+}
+}  // namespace
 
 AclFrags build_acl_frags(const uint32_t* value, const uint32_t* mask, uint32_t n) {
-  if (n > 1024) throw std::invalid_argument("ACL supports at most 1024 rules (10-bit rule index)");
+  if (n > 4096) throw std::invalid_argument("ACL supports at most 4096 rules (12-bit rule index)");
   AclFrags f;
   f.tiles = (n + 15) / 16;
   if (f.tiles == 0) f.tiles = 1;
   const uint32_t npad = f.tiles * 16;
+  const uint32_t groups = (f.tiles + 7) / 8;
+  // placement: sort by (dst, ports, src, meta) masks then values, in network byte order, so a tile
+  // holds rules of one shape over neighbouring values (e.g. consecutive /24s, low dports)
+  std::vector<uint32_t> order(n);
+  for (uint32_t r = 0; r < n; ++r) order[r] = r;
+  auto sig = [&](uint32_t r) {
+    const uint32_t* v = value + 4 * r;
+    const uint32_t* m = mask + 4 * r;
+    auto p16 = [](uint32_t raw) { return ((raw & 0xFFu) << 8) | ((raw >> 8) & 0xFFu); };
+    const uint32_t mp = (p16(m[2] >> 16) << 16) | p16(m[2] & 0xFFFFu), vp = (p16(v[2] >> 16) << 16) | p16(v[2] & 0xFFFFu);
+    return std::make_tuple(bswap32(m[1]), mp, bswap32(m[0]), m[3], bswap32(v[1] & m[1]), vp & mp, bswap32(v[0] & m[0]),
+                           v[3] & m[3], r);
+  };
+  std::sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return sig(x) < sig(y); });
   f.wfrag.assign((size_t)f.tiles * 64 * 16, 0);
-  f.cinit.assign((size_t)f.tiles * 16, 0);
-  std::vector<float> bias(npad, 1.0f);  // padded rules never match (mismatch >= 1)
-  for (uint32_t r = 0; r < n; ++r) {
-    int32_t bb = 0;
-    for (int b = 0; b < 128; ++b)
-      if (key_bit(mask + 4 * r, b) && key_bit(value + 4 * r, b)) ++bb;
-    bias[r] = (float)bb;
-  }
+  f.cinit.assign((size_t)f.tiles * 16 + (size_t)f.tiles * 8 + (size_t)groups * 8, 0);
+  std::vector<int64_t> row_rule(npad, -1);
+  for (uint32_t k = 0; k < n; ++k) row_rule[k] = order[k];
   for (uint32_t nt = 0; nt < f.tiles; ++nt)
     for (int l = 0; l < 64; ++l)
       for (int j = 0; j < 32; ++j) {
-        const uint32_t r = nt * 16 + (l & 15);
+        const int64_t r = row_rule[nt * 16 + (l & 15)];
         const int b = 32 * (l >> 4) + j;
         uint8_t w = 0;
-        if (r < n && key_bit(mask + 4 * r, b)) w = key_bit(value + 4 * r, b) ? 0xA : 0x2;
+        if (r >= 0 && key_bit(mask + 4 * r, b)) w = key_bit(value + 4 * r, b) ? 0xA : 0x2;
         uint8_t& byte = reinterpret_cast<uint8_t&>(f.wfrag[((size_t)nt * 64 + l) * 16 + j / 2]);
         byte = (uint8_t)(byte | (w << (4 * (j & 1))));
       }
-  for (uint32_t nt = 0; nt < f.tiles; ++nt)
-    for (int g = 0; g < 4; ++g)
-      for (int r = 0; r < 4; ++r) {
-        const float v = bias[nt * 16 + 4 * g + r];
-        std::memcpy(&f.cinit[((size_t)nt * 4 + g) * 4 + r], &v, 4);
-      }
+  for (uint32_t k = 0; k < npad; ++k) {
+    const int64_t r = row_rule[k];
+    float c;
+    if (r < 0) {
+      c = 4096.0f + 4095.0f;  // padding: mismatch >= 1 -> never a match
+    } else {
+      int32_t bb = 0;
+      for (int b = 0; b < 128; ++b)
+        if (key_bit(mask + 4 * r, b) && key_bit(value + 4 * r, b)) ++bb;
+      c = (float)bb * 4096.0f + (float)r;
+    }
+    const uint32_t nt = k / 16, row = k % 16;
+    std::memcpy(&f.cinit[((size_t)nt * 4 + row / 4) * 4 + row % 4], &c, 4);
+  }
+  uint32_t* pf = reinterpret_cast<uint32_t*>(f.cinit.data()) + (size_t)f.tiles * 16;
+  uint32_t* gpf = pf + (size_t)f.tiles * 8;
+  for (uint32_t nt = 0; nt < f.tiles; ++nt) {
+    const uint32_t b = nt * 16, e = std::min(n, b + 16);
+    prefilter(value, mask, order.data() + b, e > b ? e - b : 0, pf + 8 * nt);
+  }
+  for (uint32_t g = 0; g < groups; ++g) {
+    const uint32_t b = g * 128, e = std::min(n, b + 128);
+    prefilter(value, mask, order.data() + b, e > b ? e - b : 0, gpf + 8 * g);
+  }
   return f;
 }
 

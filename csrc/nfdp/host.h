@@ -49,7 +49,8 @@ class FlowTableHost {
 // Device-layout classification tables.
 struct AclFrags {
   std::vector<int8_t> wfrag;   // [tiles][64][16]: FP4 (e2m1) A fragments, 32 nibbles per lane
-  std::vector<int32_t> cinit;  // [tiles][4][4]: f32 bit patterns of the rule biases
+  std::vector<int32_t> cinit;  // [tiles][4][4] f32 C init (bias * 4096 + rule) | [tiles][8] tile
+                               // prefilters | [groups of 8 tiles][8] group prefilters
   uint32_t tiles = 0;
 };
 AclFrags build_acl_frags(const uint32_t* value, const uint32_t* mask, uint32_t n);

@@ -68,8 +68,9 @@ struct LdsLayout {
 __host__ __device__ inline LdsLayout lds_layout(int hash_mode, int acl_mode, uint32_t acl_tiles) {
   LdsLayout L;
   size_t o = 0;
-  L.acl_w = o; if (acl_mode == kAclMfma) o += (size_t)acl_tiles * 64 * 16;
-  L.acl_c = o; if (acl_mode == kAclMfma) o += (size_t)acl_tiles * 4 * 16;
+  const uint32_t lt = acl_tiles < kLdsAclTiles ? acl_tiles : kLdsAclTiles;
+  L.acl_w = o; if (acl_mode == kAclMfma) o += (size_t)lt * 64 * 16;
+  L.acl_c = o; if (acl_mode == kAclMfma) o += (size_t)lt * 4 * 16;
   L.toep_f = o; if (hash_mode == kHashMfma) o += 2 * 2 * 64 * 16;
   L.toep_t = o; if (hash_mode == kHashLds) o += 16 * 256 * 4;
   L.kx = o; o += kFWaves * 64 * 16;
@@ -104,10 +105,11 @@ __global__ __launch_bounds__(kFB, NFDP_FUSED_WAVES_PER_EU) void fused_kernel(Fus
 
   // ---- stage classification tables + zero counters ----
   if constexpr (ACL == kAclMfma) {
-    const uint32_t nw = a.acl_tiles * 64, nc = a.acl_tiles * 4;
+    const uint32_t lt_ = min(a.acl_tiles, kLdsAclTiles), nw = lt_ * 64, nc = lt_ * 4;
     for (uint32_t i = threadIdx.x; i < nw; i += kFB) lw[i] = a.acl_wfrag[i];
     for (uint32_t i = threadIdx.x; i < nc; i += kFB) lc[i] = a.acl_cinit[i];
   }
+  const AclView av{lw, lc, a.acl_wfrag, a.acl_cinit, a.acl_tiles};
   if constexpr (HASH == kHashMfma)
     for (uint32_t i = threadIdx.x; i < 256; i += kFB) lt[i] = a.toep_frag[i];
   if constexpr (HASH == kHashLds)
@@ -165,7 +167,7 @@ __global__ __launch_bounds__(kFB, NFDP_FUSED_WAVES_PER_EU) void fused_kernel(Fus
 
     uint32_t hash = 0;
     int acl_rule = -1;
-    classify_wave<HASH, ACL>(st.key, kx, lw, lc, a.acl_tiles, lt, ltab, a.t, hash, acl_rule);
+    classify_wave<HASH, ACL>(st.key, kx, av, lt, ltab, a.t, hash, acl_rule);
     if constexpr (!REMOTE) {
       // prefetch the next slot now: it lands under this slot's probe and chain
       const uint32_t nx = i + stride;
@@ -447,7 +449,7 @@ hipError_t launch_fused(const FusedLaunch& f, const LaunchCfg& cfg, hipStream_t 
                      (a.side.cap_learn && !a.side.learn) || (a.side.cap_list && !a.side.list)))
     return hipErrorInvalidValue;
   const bool remote = f.nranks > 1;
-  if (cfg.acl_mode == kAclMfma && (f.acl_tiles == 0 || f.acl_tiles > 64)) return hipErrorInvalidValue;
+  if (cfg.acl_mode == kAclMfma && (f.acl_tiles == 0 || f.acl_tiles > kAclMaxRules / 16)) return hipErrorInvalidValue;
   const int h = cfg.hash_mode, ac = cfg.acl_mode, cu = cfg.num_cus;
 #define NFDP_CASE(HH, AA)                                                                  \
   if (h == HH && ac == AA)                                                                 \

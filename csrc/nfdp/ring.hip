@@ -63,8 +63,9 @@ __device__ __forceinline__ void flush_lds_counters(uint32_t* pc, uint32_t* drops
 __host__ __device__ inline RingLds ring_lds(int hash_mode, int acl_mode, uint32_t acl_tiles) {
   RingLds L;
   size_t o = 0;
-  L.acl_w = o; if (acl_mode == kAclMfma) o += (size_t)acl_tiles * 64 * 16;
-  L.acl_c = o; if (acl_mode == kAclMfma) o += (size_t)acl_tiles * 4 * 16;
+  const uint32_t lt = acl_tiles < kLdsAclTiles ? acl_tiles : kLdsAclTiles;
+  L.acl_w = o; if (acl_mode == kAclMfma) o += (size_t)lt * 64 * 16;
+  L.acl_c = o; if (acl_mode == kAclMfma) o += (size_t)lt * 4 * 16;
   L.toep_f = o; if (hash_mode == kHashMfma) o += 2 * 2 * 64 * 16;
   L.toep_t = o; if (hash_mode == kHashLds) o += 16 * 256 * 4;
   L.kx = o; o += kRingWaves * 64 * 16;
@@ -143,10 +144,11 @@ __global__ __launch_bounds__(kRingBlock) void ring_kernel(RingArgs a) {
   v4i* lt = reinterpret_cast<v4i*>(smem + L.toep_f);
   uint32_t* ltab = reinterpret_cast<uint32_t*>(smem + L.toep_t);
   if constexpr (ACL == kAclMfma) {
-    const uint32_t nw = a.acl_tiles * 64, nc = a.acl_tiles * 4;
+    const uint32_t lt_ = min(a.acl_tiles, kLdsAclTiles), nw = lt_ * 64, nc = lt_ * 4;
     for (uint32_t i = threadIdx.x; i < nw; i += kRingBlock) lw[i] = a.acl_wfrag[i];
     for (uint32_t i = threadIdx.x; i < nc; i += kRingBlock) lc[i] = a.acl_cinit[i];
   }
+  const AclView av{lw, lc, a.acl_wfrag, a.acl_cinit, a.acl_tiles};
   if constexpr (HASH == kHashMfma)
     for (uint32_t i = threadIdx.x; i < 256; i += kRingBlock) lt[i] = a.toep_frag[i];
   if constexpr (HASH == kHashLds)
@@ -220,16 +222,15 @@ __global__ __launch_bounds__(kRingBlock) void ring_kernel(RingArgs a) {
     int acl_rule = -1;
     if constexpr (COOP && ACL == kAclMfma) {
       uint32_t b = 0xFFFFFFFFu;
-      classify_wave<HASH, ACL>(st.key, kx, lw, lc, a.acl_tiles, lt, ltab, a.t, hash, acl_rule, wave, kRingWaves, &b);
+      classify_wave<HASH, ACL>(st.key, kx, av, lt, ltab, a.t, hash, acl_rule, wave, kRingWaves, &b);
       coop_best[wave][lane] = b;
       __syncthreads();
       if (wave != 0) continue;  // helpers go back to wait for the next chunk
       b = min(min(coop_best[0][lane], coop_best[1][lane]), min(coop_best[2][lane], coop_best[3][lane]));
-      acl_rule = (b >> 10) == 0 ? (int)(b & 1023u) : -1;
-      if (acl_rule >= (int)a.t.n_acl) acl_rule = -1;
+      acl_rule = acl_rule_of(b, a.t.n_acl);
     } else {
       if (COOP && wave != 0) continue;  // nothing to share without the MFMA ACL
-      classify_wave<HASH, ACL>(st.key, kx, lw, lc, a.acl_tiles, lt, ltab, a.t, hash, acl_rule);
+      classify_wave<HASH, ACL>(st.key, kx, av, lt, ltab, a.t, hash, acl_rule);
     }
     NFDP_RING_MARK(tr1)
     bool hit = false;
@@ -322,7 +323,7 @@ hipError_t launch_ring(const RingLaunch& r, const LaunchCfg& cfg, int wgs_per_cu
   a.flags_bits = r.f.flags;
   if (!a.port_ctr || !a.drop_ctr || !a.ctl || !a.flags || !a.st) return hipErrorInvalidValue;
   if (((r.ring_mask + 1) & r.ring_mask) != 0 || r.ring_mask < 63) return hipErrorInvalidValue;
-  if (cfg.acl_mode == kAclMfma && (a.acl_tiles == 0 || a.acl_tiles > 64 || !a.acl_wfrag || !a.acl_cinit))
+  if (cfg.acl_mode == kAclMfma && (a.acl_tiles == 0 || a.acl_tiles > kAclMaxRules / 16 || !a.acl_wfrag || !a.acl_cinit))
     return hipErrorInvalidValue;
   if (cfg.hash_mode == kHashMfma && !a.toep_frag) return hipErrorInvalidValue;
   if (cfg.hash_mode == kHashLds && !a.toep_tab) return hipErrorInvalidValue;

@@ -10,8 +10,9 @@ struct ShardLds {
 __host__ __device__ inline ShardLds shard_lds(int hash_mode, int acl_mode, uint32_t acl_tiles, bool ports) {
   ShardLds L;
   size_t o = 0;
-  L.acl_w = o; if (acl_mode == kAclMfma) o += (size_t)acl_tiles * 64 * 16;
-  L.acl_c = o; if (acl_mode == kAclMfma) o += (size_t)acl_tiles * 4 * 16;
+  const uint32_t lt = acl_tiles < kLdsAclTiles ? acl_tiles : kLdsAclTiles;
+  L.acl_w = o; if (acl_mode == kAclMfma) o += (size_t)lt * 64 * 16;
+  L.acl_c = o; if (acl_mode == kAclMfma) o += (size_t)lt * 4 * 16;
   L.toep_f = o; if (hash_mode == kHashMfma) o += 2 * 2 * 64 * 16;
   L.toep_t = o; if (hash_mode == kHashLds) o += 16 * 256 * 4;
   L.kx = o; o += kWaves * 64 * 16;
@@ -36,9 +37,11 @@ __global__ __launch_bounds__(kBlock) void ingress_kernel(IngressArgs a) {
   if constexpr (ACL == kAclMfma) {
     const v4i* gw = reinterpret_cast<const v4i*>(a.acl_wfrag);
     const v4i* gc = reinterpret_cast<const v4i*>(a.acl_cinit);
-    for (uint32_t i = threadIdx.x; i < a.acl_tiles * 64; i += kBlock) lw[i] = gw[i];
-    for (uint32_t i = threadIdx.x; i < a.acl_tiles * 4; i += kBlock) lc[i] = gc[i];
+    const uint32_t lt_ = min(a.acl_tiles, kLdsAclTiles);
+    for (uint32_t i = threadIdx.x; i < lt_ * 64; i += kBlock) lw[i] = gw[i];
+    for (uint32_t i = threadIdx.x; i < lt_ * 4; i += kBlock) lc[i] = gc[i];
   }
+  const AclView av{lw, lc, reinterpret_cast<const v4i*>(a.acl_wfrag), reinterpret_cast<const v4i*>(a.acl_cinit), a.acl_tiles};
   if constexpr (HASH == kHashMfma) {
     const v4i* gt = reinterpret_cast<const v4i*>(a.toep_frag);
     for (uint32_t i = threadIdx.x; i < 256; i += kBlock) lt[i] = gt[i];
@@ -68,7 +71,7 @@ __global__ __launch_bounds__(kBlock) void ingress_kernel(IngressArgs a) {
     ingress_stage(a.t, d, im, p, st);
     uint32_t hash = 0;
     int acl = -1;
-    classify_wave<HASH, ACL>(st.key, kx, lw, lc, a.acl_tiles, lt, ltab, a.t, hash, acl);
+    classify_wave<HASH, ACL>(st.key, kx, av, lt, ltab, a.t, hash, acl);
     const bool need = valid && !st.reason && p.ipv4;
     const uint32_t owner = owner_of(hash, a.g.nranks);
     const uint32_t pos = reserve_block(a.cnt, owner, need, a.g.nranks, rcnt, rbase);
@@ -282,7 +285,7 @@ static hipError_t launch_ingress_t(const IngressArgs& a, int num_cus, hipStream_
 
 hipError_t launch_ingress(const IngressArgs& a, int hash_mode, int acl_mode, int num_cus, hipStream_t s) {
   if (a.g.nranks == 0 || a.g.nranks > kMaxRanks || a.g.cap_desc >= (1u << 24)) return hipErrorInvalidValue;
-  if (acl_mode == kAclMfma && (a.acl_tiles == 0 || a.acl_tiles > 64)) return hipErrorInvalidValue;
+  if (acl_mode == kAclMfma && (a.acl_tiles == 0 || a.acl_tiles > kAclMaxRules / 16)) return hipErrorInvalidValue;
 #define NFDP_CASE(HH, AA) if (hash_mode == HH && acl_mode == AA) return launch_ingress_t<HH, AA>(a, num_cus, s);
   NFDP_CASE(1, 0) NFDP_CASE(1, 1) NFDP_CASE(1, 2)
   NFDP_CASE(2, 0) NFDP_CASE(2, 1) NFDP_CASE(2, 2)

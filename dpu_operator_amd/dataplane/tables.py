@@ -433,9 +433,10 @@ def range_to_prefixes(lo: int, hi: int, width: int = 16) -> list[tuple[int, int]
 
 
 class AclTable:
-    """Priority-ordered ternary rules (index = priority, first match wins), <= 1024 rules."""
+    """Priority-ordered ternary rules (index = priority, first match wins), <= 4096 rules
+    (12-bit rule index in the MFMA accumulator; the P4 tables hold 1024)."""
 
-    MAX_RULES = 1024
+    MAX_RULES = 4096
 
     def __init__(self, default_permit: bool = True):
         self.rules: list[AclRule] = []
@@ -444,7 +445,7 @@ class AclTable:
 
     def add_raw(self, value, mask, permit: bool) -> int:
         if len(self.rules) >= self.MAX_RULES:
-            raise RuntimeError("ACL full (1024 rules = P4 table capacity)")
+            raise RuntimeError(f"ACL full ({self.MAX_RULES} rules)")
         v = np.asarray(value, np.uint32) & np.asarray(mask, np.uint32)
         self.rules.append(AclRule(v, np.asarray(mask, np.uint32), bool(permit)))
         self.version += 1

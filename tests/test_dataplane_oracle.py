@@ -52,12 +52,9 @@ def test_toeplitz_mfma_fragments_emulated(nf):
     assert np.array_equal(h, nf.toeplitz(keys, T.RSS_KEY))
 
 
-def test_acl_fragments_emulated(nf):
-    """TCAM-as-GEMM: mismatch = bias + bits @ W must be 0 exactly on ternary matches."""
-    rng = np.random.default_rng(2)
-    n = 40
-    val = rng.integers(0, 2**32, (n, 4), dtype=np.uint64).astype(np.uint32)
-    msk = (rng.integers(0, 2**32, (n, 4), dtype=np.uint64) & rng.integers(0, 2**32, (n, 4), dtype=np.uint64)).astype(np.uint32)
+def _acl_emulate(nf, val, msk, keys):
+    """Emulate classify_wave's ACL on the host from the device buffers: A block-scaled by 2^12,
+    C init = bias * 4096 + rule, first match = min over the tiles/groups the prefilters admit."""
     w, c, tiles = nf.build_acl_frags(val, msk)
     # FP4 (e2m1) A fragments of v_mfma_scale_f32_16x16x128_f8f6f4: lane l, nibble j = K 32(l>>4)+j
     w = w.view(np.uint8).reshape(tiles, 64, 16)
@@ -65,23 +62,71 @@ def test_acl_fragments_emulated(nf):
     e2m1 = {0x0: 0, 0x2: 1, 0xA: -1}
     assert set(np.unique(nib).tolist()) <= set(e2m1)
     val_of = np.vectorize(e2m1.get)(nib).astype(np.int64)
-    c = c.view(np.float32).reshape(tiles, 4, 4)
+    groups = (tiles + 7) // 8
+    cinit = c[: tiles * 16].view(np.float32).reshape(tiles, 4, 4)
+    pf = c[tiles * 16: tiles * 24].view(np.uint32).reshape(tiles, 8)
+    gpf = c[tiles * 24: tiles * 24 + groups * 8].view(np.uint32).reshape(groups, 8)
     W = np.zeros((128, tiles * 16), np.int64)
-    bias = np.zeros(tiles * 16, np.int64)
+    C = np.zeros(tiles * 16, np.int64)
     for nt in range(tiles):
         for l in range(64):
             for j in range(32):
                 W[32 * (l >> 4) + j, nt * 16 + (l & 15)] = val_of[nt, l, j]
         for g in range(4):
             for r in range(4):
-                bias[nt * 16 + 4 * g + r] = int(c[nt, g, r])
-    keys = np.concatenate([val & msk, rng.integers(0, 2**32, (200, 4), dtype=np.uint64).astype(np.uint32)])
+                C[nt * 16 + 4 * g + r] = int(cinit[nt, g, r])
     bits = ((keys[:, :, None] >> np.arange(32, dtype=np.uint32)) & 1).reshape(len(keys), 128).astype(np.int64)
-    mism = bits @ W + bias
-    assert (mism >= 0).all()
-    ref = np.all(((keys[:, None, :] ^ val[None]) & msk[None]) == 0, axis=2)
-    assert np.array_equal(mism[:, :n] == 0, ref)
-    assert (mism[:, n:] > 0).all()  # padding rules never match
+    acc = 4096 * (bits @ W) + C                     # == (mismatch << 12) | rule, exactly
+    assert (acc >= 0).all() and (acc < 2 ** 24).all()
+
+    def passes(f):
+        return np.all(((keys & f[:4]) ^ f[4:]) == 0, axis=1)
+
+    best = np.full(len(keys), 2 ** 32 - 1, np.int64)
+    for nt in range(tiles):
+        ok = passes(pf[nt]) & passes(gpf[nt // 8])
+        tile_min = acc[:, nt * 16:(nt + 1) * 16].min(axis=1)
+        # a wave runs the tile if ANY of its packets passes; min is idempotent, so running it for
+        # all packets of such a wave changes nothing: the per-packet test suffices here
+        best = np.where(ok, np.minimum(best, tile_min), best)
+    return np.where(best < 4096, best, -1), acc
+
+
+def test_acl_fragments_emulated(nf):
+    """TCAM-as-GEMM: the scaled accumulator encodes (mismatch << 12 | rule); with the tile and
+    group prefilters the first match equals the scalar priority scan."""
+    rng = np.random.default_rng(2)
+    n = 300
+    val = rng.integers(0, 2**32, (n, 4), dtype=np.uint64).astype(np.uint32)
+    msk = (rng.integers(0, 2**32, (n, 4), dtype=np.uint64) & rng.integers(0, 2**32, (n, 4), dtype=np.uint64)).astype(np.uint32)
+    msk[::3, 0] = 0xFFFFFFFF  # some rule shapes repeat
+    val &= msk
+    keys = np.concatenate([val | (rng.integers(0, 2**32, (n, 4), dtype=np.uint64).astype(np.uint32) & ~msk),
+                           rng.integers(0, 2**32, (300, 4), dtype=np.uint64).astype(np.uint32)])
+    got, acc = _acl_emulate(nf, val, msk, keys)
+    m = np.all(((keys[:, None, :] ^ val[None]) & msk[None]) == 0, axis=2)
+    ref = np.where(m.any(axis=1), m.argmax(axis=1), -1)
+    assert np.array_equal(got, ref)
+    assert (got[:n] >= 0).all()
+
+
+def test_acl_prefilter_skips_bench_rules(nf):
+    """The bench's deny rules (dst 192.168.x/24 + dport, udp dport < 1024) are grouped so that pod
+    traffic (10.128/16, dports >= 1024) passes only the final permit's tile."""
+    from dpu_operator_amd.dataplane import scenario as S
+    from dpu_operator_amd.dataplane.engine import DataPlane
+
+    dp = DataPlane(device="cpu", flow_buckets=1 << 10)
+    sc = S.build_sfc(dp, n_pods=8, n_flows=1024, n_acl=256, seed=0)
+    S.add_acl_rules(dp, 1024)
+    val, msk, _, n = dp.acl.arrays()
+    w, c, tiles = nf.build_acl_frags(val[:n], msk[:n])
+    pf = c[tiles * 16: tiles * 24].view(np.uint32).reshape(tiles, 8)
+    keys = sc.keys[:512]
+    admitted = sum(int(np.any(np.all(((keys & f[:4]) ^ f[4:]) == 0, axis=1))) for f in pf)
+    assert tiles == 64 and admitted <= 2
+    got, _ = _acl_emulate(nf, val[:n], msk[:n], keys)
+    assert (got == n - 1).all()  # every pod flow ends on the final permit
 
 
 def test_flow_table_cuckoo_high_load(nf):
