@@ -8,13 +8,15 @@ whole chain:
     pod VF ingress (VLAN-isolated, spoof-checked)  ->  ACL (TCAM, 256 ternary rules, MFMA)  ->
     SNAT (per-flow state, 1M-flow exact-match table)  ->  L2 steer + egress VLAN tag  ->  pod VF
 
-N = 1: one fused HIP kernel.  N > 1 (one process per GPU, torchrun), default `--mode replicated`:
-every GPU holds the full tables (1M flows = 64 MB of its 288 GB) and runs the fused kernel on its
-own ingress; frames for pods on other GPUs are written by the kernel into per-GPU segments and
-delivered with ONE all-to-all per chunk (RCCL over xGMI), chunks pipelined against compute.
-`--mode sharded`: the flow table is hash-partitioned instead (descriptor / verdict / packet
-all-to-alls).  Traffic is random pod->pod over 8 pods per GPU, so (N-1)/N of the packets cross
-GPUs.
+N = 1: one fused HIP kernel.  N > 1 (one process per GPU, torchrun), default `--mode rss`
+(parallel/rss.py): flow-affine sharding - GPU k owns the flows whose Toeplitz hash maps to it
+(`--flows` per GPU shard, N x 1M in total: weak scaling), the I/O layer steers packets to their
+owner as host RSS does, and the owner runs the whole chain and egresses itself (pod rings are
+host memory every GPU can write).  `--remote-frac` (default 1 %) of every batch is traffic the
+producer could NOT steer: the fused kernel sends those packets' header slots to their owner,
+one all-to-all per step (RCCL over xGMI) overlapped with the next step's kernel, and the owner
+processes them.  `--mode replicated` (every GPU holds all flows, frames to pods on other GPUs
+cross xGMI) and `--mode sharded` (descriptor / verdict / packet all-to-alls) are kept.
 
 Data: synthetic (random-init 1M-flow table, random 5-tuples); inputs rotate over 4 pre-generated
 batches so no step re-reads a cached one.  Latency: per-packet time from the batch release stamp
@@ -57,8 +59,10 @@ def parse():
     ap.add_argument("--no-variants", action="store_true", help="skip the mixed / ACL1024 / IMIX measurements")
     ap.add_argument("--variant-steps", type=int, default=30)
     ap.add_argument("--chunks", type=int, default=4, help="pipeline chunks per step (N > 1)")
-    ap.add_argument("--mode", default="replicated", choices=["replicated", "sharded"],
+    ap.add_argument("--mode", default="rss", choices=["rss", "replicated", "sharded"],
                     help="multi-GPU strategy for N > 1")
+    ap.add_argument("--remote-frac", type=float, default=0.01,
+                    help="rss: fraction of each batch the producer could not steer to its owner GPU")
     ap.add_argument("--io", default="device", choices=["device", "host"],
                     help="device: batches resident in HBM (DPU wire side); host: pinned host slots, SDMA up/down "
                          "around every kernel (1 GPU)")
@@ -156,22 +160,29 @@ def main() -> None:
     from dpu_operator_amd.dataplane.engine import DataPlane
     from dpu_operator_amd.ops import packets as P
     from dpu_operator_amd.parallel.replicated import ReplicatedDataPlane
+    from dpu_operator_amd.parallel.rss import RssShardedDataPlane, flow_owner, rss_traffic
     from dpu_operator_amd.parallel.sharded import PipelinedShardedDataPlane, ShardedDataPlane, shard_filter
 
     replicated = sharded and world > 1 and a.mode == "replicated" and not a.force_sharded
+    rss = sharded and world > 1 and a.mode == "rss" and not a.force_sharded
     t_setup = time.time()
-    flows_here = a.flows if (replicated or world == 1) else a.flows / world
+    total_flows = a.flows * world if rss else a.flows  # rss: --flows per GPU shard (weak scaling)
+    flows_here = a.flows if (replicated or rss or world == 1) else a.flows / world
     buckets = 1 << max(10, int(math.ceil(math.log2(flows_here / 2))))  # <= 50% load, 4 slots/bucket
     dp = DataPlane(device=str(dev), flow_buckets=buckets, hash_mode=a.hash, acl_mode=a.acl_mode)
     n_pods = a.pods_per_gpu * world
     pod_gpu = np.arange(n_pods) // a.pods_per_gpu
-    sc = S.build_sfc(dp, n_pods=n_pods, n_flows=a.flows, n_acl=a.acl, seed=0, pod_gpu=pod_gpu,
+    sc = S.build_sfc(dp, n_pods=n_pods, n_flows=total_flows, n_acl=a.acl, seed=0, pod_gpu=pod_gpu,
                      flow_filter=shard_filter(rank, world) if (world > 1 and not replicated) else None)
     dp.commit(full=True)
     my_pods = np.where(pod_gpu == rank)[0]
+    owner = flow_owner(sc.keys, world, dp.flows.rss_key) if rss else None
     batches = []
     for r in range(a.rotate):
-        pk, im = S.traffic(sc, a.batch, seed=1000 * rank + r + 1, src_pods=my_pods)
+        if rss:
+            pk, im = rss_traffic(sc, a.batch, rank, world, owner, a.remote_frac, seed=1000 * rank + r + 1)
+        else:
+            pk, im = S.traffic(sc, a.batch, seed=1000 * rank + r + 1, src_pods=my_pods)
         batches.append((torch.from_numpy(pk).to(dev), torch.from_numpy(im.view(np.int32)).to(dev)))
         del pk, im
     drain = None
@@ -207,6 +218,18 @@ def main() -> None:
 
         def results():
             return meta.cpu().numpy().view(np.uint32), lat.cpu().numpy().view(np.uint32).astype(np.float64) * 0.01
+    elif rss:
+        eng = RssShardedDataPlane(dp, rank, world, a.batch, remote_frac=a.remote_frac)
+
+        def step(k):
+            pk, im = batches[k % a.rotate]
+            eng.step(pk, im)
+
+        def drain():
+            eng.flush()
+
+        def results():
+            return eng.out_meta(), eng.latency_samples_us()
     elif replicated:
         eng = ReplicatedDataPlane(dp, rank, world, a.batch, chunks=a.chunks)
 
@@ -251,7 +274,7 @@ def main() -> None:
 
     meta_np, lat_us = results()
     _, _, reasons = P.meta_fields(meta_np)
-    fwd_local = float(np.mean((reasons == 0) | (reasons == 10)))
+    fwd_local = float(np.mean((reasons == 0) | (reasons == 10)))  # 10: handed to its owner / egress GPU
     p50 = float(np.median(lat_us)) if len(lat_us) else float("nan")
     p99 = float(np.percentile(lat_us, 99)) if len(lat_us) else float("nan")
     if world > 1:
@@ -264,6 +287,27 @@ def main() -> None:
     # exchange alone (outside the timed region, N > 1 replicated): the step's all-to-alls with no
     # compute around them -> achieved xGMI bandwidth per GPU and the exchange floor of a step
     xchg = None
+    if rss:
+        s0 = eng.slots[0]
+        for _ in range(3):
+            eng.exchange(s0).wait()
+        torch.cuda.synchronize()
+        dist.barrier()
+        reps = 20
+        t1 = time.perf_counter()
+        for _ in range(reps):
+            eng.exchange(s0).wait()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t1
+        tt = torch.tensor([el], dtype=torch.float64, device=cdev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt.item())
+        peer_bytes = (world - 1) * eng.pseg
+        xchg = {"a2a_ms": round(el / reps * 1e3, 4), "a2a_per_step": 1,
+                "remote_frac": a.remote_frac, "segment_cap_per_peer": eng.cap,
+                "xgmi_bytes_out_per_gpu_per_step": peer_bytes,
+                "xgmi_gbps_out_per_gpu": round(peer_bytes / (el / reps) / 1e9, 2),
+                "note": "overlapped with the next step's kernel in the timed region"}
     if replicated:
         s0 = eng.slots[0]
         for _ in range(3):
@@ -297,6 +341,13 @@ def main() -> None:
                 dp.run(pk, im, o2, m2, l2)
             torch.cuda.synchronize()
             ls = l2.cpu().numpy().view(np.uint32).astype(np.float64) * 0.01
+        elif rss:
+            eng_s = RssShardedDataPlane(dp, rank, world, nsm, remote_frac=a.remote_frac)
+            for _ in range(20):
+                eng_s.step(pk, im)
+            eng_s.flush()
+            torch.cuda.synchronize()
+            ls = eng_s.latency_samples_us()
         elif replicated:
             eng_s = ReplicatedDataPlane(dp, rank, world, nsm, chunks=1)
             for _ in range(20):
@@ -372,7 +423,10 @@ def main() -> None:
                 "global_batch": world * a.batch,
                 "seq_len": 64,
                 "parallelism": "fused-1gpu" if not sharded else
-                (f"replicated tables x{world}, fused kernel + 1x all-to-all of cross-GPU frames (RCCL/xGMI), "
+                (f"rss flow-shard x{world} ({a.flows} flows/GPU, {total_flows} total), owner-local chain + egress, "
+                 f"{a.remote_frac:.1%} misdirected headers -> owner: 1x all-to-all/step (RCCL/xGMI), overlapped"
+                 if rss else
+                 f"replicated tables x{world}, fused kernel + 1x all-to-all of cross-GPU frames (RCCL/xGMI), "
                  f"{a.chunks}-chunk overlap" if replicated else
                  f"flow-shard x{world} + 3x all-to-all (RCCL/xGMI), {a.chunks}-chunk overlap"),
                 "io": a.io if not sharded else "device",
@@ -389,7 +443,7 @@ def main() -> None:
             "value_acl1024": None if not variants else variants["acl1024_mpps"],
             "imix": None if not variants else variants["imix"],
             "variants": variants,
-            "flows": a.flows,
+            "flows": total_flows,
             "batch_per_gpu": a.batch,
             "hash": a.hash,
             "acl_mode": a.acl_mode,

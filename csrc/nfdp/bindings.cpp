@@ -215,7 +215,7 @@ PYBIND11_MODULE(_nfdp, m) {
                            uint32_t n, uintptr_t flow_ctr, uintptr_t port_ctr, uintptr_t drop_ctr, uintptr_t t0,
                            uintptr_t lat, uintptr_t acl_wfrag, uintptr_t acl_cinit, uint32_t acl_tiles,
                            uintptr_t toep_frag, uintptr_t toep_tab, int hash_mode, int acl_mode, int num_cus,
-                           uintptr_t stream, uint32_t flags, py::object side) {
+                           uintptr_t stream, uint32_t flags, py::object side, uintptr_t n_dev) {
     FusedLaunch f{};
     f.side = side_from(side);
     f.t = tables_from(tables);
@@ -235,6 +235,7 @@ PYBIND11_MODULE(_nfdp, m) {
     f.toep_frag = reinterpret_cast<const void*>(toep_frag);
     f.toep_tab = reinterpret_cast<const uint32_t*>(toep_tab);
     f.flags = flags;
+    f.n_dev = reinterpret_cast<const uint32_t*>(n_dev);
     if (!f.pkts || !f.inmeta || !f.out || !f.out_meta || !f.port_ctr || !f.drop_ctr)
       throw std::invalid_argument("launch_fused: null buffer");
     if (hash_mode == 2 && !f.toep_frag) throw std::invalid_argument("MFMA hash needs toeplitz frags");
@@ -247,7 +248,23 @@ PYBIND11_MODULE(_nfdp, m) {
      py::arg("flow_ctr"), py::arg("port_ctr"), py::arg("drop_ctr"), py::arg("t0"), py::arg("lat"),
      py::arg("acl_wfrag"), py::arg("acl_cinit"), py::arg("acl_tiles"), py::arg("toep_frag"), py::arg("toep_tab"),
      py::arg("hash_mode"), py::arg("acl_mode"), py::arg("num_cus"), py::arg("stream"), py::arg("flags") = 0,
-     py::arg("side") = py::none());
+     py::arg("side") = py::none(), py::arg("n_dev") = 0);
+  m.def("gather", [](uintptr_t recv, uint32_t nranks, uint32_t rank, uint32_t cap, uintptr_t pkts, uintptr_t inmeta,
+                     uintptr_t n_dev, bool device, uintptr_t stream) -> uint32_t {
+    const size_t seg = pkt_seg_bytes(cap), moff = pkt_meta_off(cap);
+    if (rank >= nranks || nranks > 64 || seg >= (1ull << 32)) throw std::invalid_argument("gather: bad geometry");
+    if (!device) {
+      py::gil_scoped_release nogil;
+      const uint32_t n = gather_cpu(reinterpret_cast<const uint8_t*>(recv), nranks, rank, cap, (uint32_t)seg,
+                                    (uint32_t)moff, reinterpret_cast<uint32_t*>(pkts), reinterpret_cast<uint32_t*>(inmeta));
+      if (n_dev) *reinterpret_cast<uint32_t*>(n_dev) = n;
+      return n;
+    }
+    check(launch_gather(reinterpret_cast<const uint8_t*>(recv), nranks, rank, cap, (uint32_t)seg, (uint32_t)moff,
+                        reinterpret_cast<void*>(pkts), reinterpret_cast<uint32_t*>(inmeta),
+                        reinterpret_cast<uint32_t*>(n_dev), reinterpret_cast<hipStream_t>(stream)), "gather");
+    return 0;
+  });
   m.def("launch_stamp", [](uintptr_t dst, uintptr_t stream) {
     check(launch_stamp(reinterpret_cast<unsigned long long*>(dst), reinterpret_cast<hipStream_t>(stream)), "stamp");
   });
@@ -344,11 +361,12 @@ PYBIND11_MODULE(_nfdp, m) {
     f.flags = val<uint32_t>(d, "flags", 0);
     f.send_pkt = ptr<uint8_t>(d, "send_pkt"); f.pcnt = ptr<uint32_t>(d, "pcnt");
     f.nranks = g.nranks; f.rank = g.rank; f.cap_pkt = g.cap_pkt;
+    f.steer = val<uint32_t>(d, "steer", 0);
     if (!f.pkts || !f.inmeta || !f.out || !f.out_meta || !f.port_ctr || !f.drop_ctr || !f.send_pkt || !f.pcnt)
       throw std::invalid_argument("fused_remote: null buffer");
     if (g.nranks < 2) throw std::invalid_argument("fused_remote needs nranks >= 2");
     if (!device) {
-      RemoteOut r{g.nranks, g.rank, g.cap_pkt, f.send_pkt, f.pcnt};
+      RemoteOut r{g.nranks, g.rank, g.cap_pkt, f.send_pkt, f.pcnt, f.steer};
       py::gil_scoped_release nogil;
       oracle_run_remote(f.t, reinterpret_cast<const uint32_t*>(f.pkts), f.inmeta, f.n,
                         reinterpret_cast<uint32_t*>(f.out), f.out_meta, reinterpret_cast<uint64_t*>(f.flow_ctr),

@@ -363,6 +363,10 @@ void oracle_run_remote(const TablesView& t, const uint32_t* pkts, const uint32_t
     ingress_stage(t, d, inmeta[i], p, st);
     const uint32_t h = toeplitz_scalar(st.key, t.rss_key);
     const int acl = acl_first_match(t, st.key);
+    // flow-owner steering: another GPU's flow goes to its owner as it came in
+    const uint32_t owner = owner_of(h, r.nranks);
+    const bool to_owner = r.steer && !st.reason && p.ipv4 && owner != r.rank;
+    if (to_owner) st.reason = kRemote;
     bool hit = false;
     FlowAction act = {};
     if (!st.reason && p.ipv4) {
@@ -374,8 +378,8 @@ void oracle_run_remote(const TablesView& t, const uint32_t* pkts, const uint32_t
       }
     }
     const EgressDecision e = chain_stage(t, p, st, hit, act, acl, h);
-    const uint32_t eg = e.reason ? r.rank : (uint32_t)t.ports[e.out_port].gpu;
-    const bool remote = !e.reason && eg != r.rank && eg < r.nranks;
+    const uint32_t eg = r.steer ? owner : (e.reason ? r.rank : (uint32_t)t.ports[e.out_port].gpu);
+    const bool remote = r.steer ? to_owner : (!e.reason && eg != r.rank && eg < r.nranks);
     uint32_t reason = e.reason;
     uint32_t pos = 0;
     if (remote) {
@@ -383,29 +387,46 @@ void oracle_run_remote(const TablesView& t, const uint32_t* pkts, const uint32_t
       if (pos >= r.cap_pkt) reason = kOverflow;
     }
     uint32_t o[kSlotDwords];
-    emit(p, e.tci, e.push != 0, o);
+    emit(p, to_owner ? p.tci : e.tci, to_owner ? p.tagged : e.push != 0, o);
     const uint32_t olen = reason ? 0u : p.len + (e.push ? 4u : 0u);
-    const bool to_peer = remote && reason == kOk;
+    const bool to_peer = remote && reason != kOverflow;
     if (to_peer) {
       uint8_t* segp = r.send_pkt + eg * pseg;
       std::memcpy(segp + 64 + (size_t)pos * 64, o, sizeof(o));
-      const uint32_t m = make_meta(e.out_port, olen, kOk);
+      const uint32_t m = r.steer ? inmeta[i] : make_meta(e.out_port, olen, kOk);
       std::memcpy(segp + pkt_meta_off(r.cap_pkt) + 4 * (size_t)pos, &m, 4);
-      out_meta[i] = make_meta(e.out_port, olen, kRemote);
+      out_meta[i] = make_meta(r.steer ? kPortNone : e.out_port, r.steer ? st.wire_len : olen, kRemote);
     } else {
       std::memcpy(out + (size_t)i * kSlotDwords, o, sizeof(o));
       out_meta[i] = make_meta(reason == kOverflow ? kPortNone : e.out_port, olen, reason, false, !reason && e.flood);
     }
-    if (port_ctr) {
+    const bool counted_by_owner = to_owner && to_peer;
+    if (port_ctr && !counted_by_owner) {
       if (st.in_port < (uint32_t)kMaxPorts) port_ctr[2 * st.in_port] += ctr_inc(st.wire_len);
       if (!reason && !to_peer) port_ctr[2 * e.out_port + 1] += ctr_inc(olen);
     }
-    if (drop_ctr && reason) drop_ctr[reason & (kNumReasons - 1)] += 1;
+    if (drop_ctr && reason && !counted_by_owner) drop_ctr[reason & (kNumReasons - 1)] += 1;
   }
   for (uint32_t o = 0; o < r.nranks; ++o) {
     const uint32_t hdr[4] = {r.pcnt[o] < r.cap_pkt ? r.pcnt[o] : r.cap_pkt, r.cap_pkt, 0, 0};
     std::memcpy(r.send_pkt + o * pseg, hdr, 16);
   }
+}
+
+uint32_t gather_cpu(const uint8_t* recv, uint32_t nranks, uint32_t rank, uint32_t cap, uint32_t seg_bytes,
+                    uint32_t meta_off, uint32_t* pkts, uint32_t* inmeta) {
+  uint32_t n = 0;
+  for (uint32_t s = 0; s < nranks; ++s) {
+    if (s == rank) continue;
+    const uint8_t* seg = recv + (size_t)s * seg_bytes;
+    uint32_t c;
+    std::memcpy(&c, seg, 4);
+    c = std::min(c, cap);
+    std::memcpy(pkts + (size_t)n * kSlotDwords, seg + 64, (size_t)c * kSlotBytes);
+    std::memcpy(inmeta + n, seg + meta_off, (size_t)c * 4);
+    n += c;
+  }
+  return n;
 }
 
 }  // namespace nfdp

@@ -78,7 +78,13 @@ struct RemoteOut {
   uint32_t nranks, rank, cap_pkt;
   uint8_t* send_pkt;
   uint32_t* pcnt;
+  uint32_t steer = 0;  // 1: flow-owner steering (input header + ingress meta to the owner)
 };
+// Receive side of flow-owner steering (GPU: launch_gather): segments -> dense batch; returns n.
+uint32_t gather_cpu(const uint8_t* recv, uint32_t nranks, uint32_t rank, uint32_t cap, uint32_t seg_bytes,
+                    uint32_t meta_off, uint32_t* pkts, uint32_t* inmeta);
+hipError_t launch_gather(const uint8_t* recv, uint32_t nranks, uint32_t rank, uint32_t cap, uint32_t seg_bytes,
+                         uint32_t meta_off, void* pkts, uint32_t* inmeta, uint32_t* n_dev, hipStream_t s);
 void oracle_run_remote(const TablesView& t, const uint32_t* pkts, const uint32_t* inmeta, uint32_t n,
                        uint32_t* out, uint32_t* out_meta, uint64_t* flow_ctr, uint64_t* port_ctr,
                        uint64_t* drop_ctr, const RemoteOut& r);
@@ -101,6 +107,8 @@ struct FusedLaunch {
   uint8_t* send_pkt = nullptr; uint32_t* pcnt = nullptr;
   uint32_t nranks = 0, rank = 0, cap_pkt = 0;
   SideOut side{};  // side outputs (flood / mirror / ARP replicas, learn events); cnt null = off
+  uint32_t steer = 0;              // REMOTE: 1 = send packets of other GPUs' flow shards to their owner
+  const uint32_t* n_dev = nullptr; // device-side count (<= n)
 };
 hipError_t launch_fused(const FusedLaunch& f, const LaunchCfg& cfg, hipStream_t s);
 size_t fused_lds_bytes(int hash_mode, int acl_mode, uint32_t acl_tiles);

@@ -57,6 +57,11 @@ struct FusedArgs {
   uint32_t* pcnt;
   uint32_t nranks, rank, cap_pkt;
   SideOut side;                   // flood / mirror / ARP replicas + learn events (side.cnt null: off)
+  uint32_t steer;                 // REMOTE: 0 = by egress GPU (after the chain), 1 = by flow owner
+                                  // (owner_of(hash) right after classification: the INPUT header +
+                                  // ingress meta go to the owner, which runs the whole pipeline)
+  const uint32_t* n_dev;          // optional device-side packet count (<= n): batches whose size only
+                                  // the GPU knows (packets gathered from the exchange)
 };
 
 __device__ __forceinline__ size_t lds_align16(size_t x) { return (x + 15) & ~(size_t)15; }
@@ -125,7 +130,7 @@ __global__ __launch_bounds__(kFB, NFDP_FUSED_WAVES_PER_EU) void fused_kernel(Fus
   __syncthreads();
 
   const unsigned long long t0 = a.t0 ? *a.t0 : 0ull;
-  const uint4* pk4 = a.pkts;
+  const uint32_t n = a.n_dev ? min(a.n, *a.n_dev) : a.n;
   const uint32_t stride = gridDim.x * kFB;
   // Software pipeline over the grid-stride loop.  s_waitcnt vmcnt retires loads, stores and
   // atomics together in issue order, so the next slot's frame is loaded BEFORE this slot's
@@ -139,12 +144,12 @@ __global__ __launch_bounds__(kFB, NFDP_FUSED_WAVES_PER_EU) void fused_kernel(Fus
   const __amdgpu_buffer_rsrc_t r_im = __builtin_amdgcn_make_buffer_rsrc((void*)a.inmeta, (short)0, (int)(a.n * 4u), kBufCfg);
   // first 4-KiB run of this wave (prefetched frames arrive chunk-per-lane in cn)
   const uint32_t wave0 = __builtin_amdgcn_readfirstlane(threadIdx.x) & ~63u;  // wave-uniform (SGPR)
-  auto run_of = [&](uint32_t base) { return base + wave0 < a.n ? (base + wave0) * 64u : kNoRun; };
+  auto run_of = [&](uint32_t base) { return base + wave0 < n ? (base + wave0) * 64u : kNoRun; };
   v4u cn[4];
   {
     wave_frames_load<kStreamAux>(r_pk, run_of(blockIdx.x * kFB), cn);
     const uint32_t i0 = blockIdx.x * kFB + threadIdx.x;
-    imn = __builtin_amdgcn_raw_buffer_load_b32(r_im, i0 < a.n ? i0 * 4u : kNoRun, 0, kStreamAux);
+    imn = __builtin_amdgcn_raw_buffer_load_b32(r_im, i0 < n ? i0 * 4u : kNoRun, 0, kStreamAux);
   }
   const __amdgpu_buffer_rsrc_t r_out = __builtin_amdgcn_make_buffer_rsrc((void*)a.out, (short)0, (int)(a.n * 64u), kBufCfg);
   const __amdgpu_buffer_rsrc_t r_meta = __builtin_amdgcn_make_buffer_rsrc((void*)a.out_meta, (short)0, (int)(a.n * 4u), kBufCfg);
@@ -155,9 +160,9 @@ __global__ __launch_bounds__(kFB, NFDP_FUSED_WAVES_PER_EU) void fused_kernel(Fus
   const __amdgpu_buffer_rsrc_t r_send = __builtin_amdgcn_make_buffer_rsrc(
       (void*)a.send_pkt, (short)0, REMOTE ? (int)(a.nranks * pkt_seg_bytes(a.cap_pkt)) : 0, kBufCfg);
   uint32_t it = 0;  // loop iteration (REMOTE reservation buffers alternate)
-  for (uint32_t base = blockIdx.x * kFB; base < a.n; base += stride, ++it) {
+  for (uint32_t base = blockIdx.x * kFB; base < n; base += stride, ++it) {
     const uint32_t i = base + threadIdx.x;
-    const bool valid = i < a.n;
+    const bool valid = i < n;
     wave_frames_to_lanes(kx, cn, dn);
     Parsed p;
     IngressState st;
@@ -168,11 +173,22 @@ __global__ __launch_bounds__(kFB, NFDP_FUSED_WAVES_PER_EU) void fused_kernel(Fus
     uint32_t hash = 0;
     int acl_rule = -1;
     classify_wave<HASH, ACL>(st.key, kx, av, lt, ltab, a.t, hash, acl_rule);
+    // flow-owner steering (REMOTE, steer = 1): a packet of another GPU's flow shard leaves now,
+    // as it came in; its owner runs the whole pipeline on it
+    bool to_owner = false;
+    uint32_t owner = a.rank;
+    if constexpr (REMOTE) {
+      if (a.steer) {
+        owner = owner_of(hash, a.nranks);
+        to_owner = valid && !st.reason && p.ipv4 && owner != a.rank;
+        if (to_owner) st.reason = kRemote;  // no local probe / chain / counters
+      }
+    }
     if constexpr (!REMOTE) {
       // prefetch the next slot now: it lands under this slot's probe and chain
       const uint32_t nx = i + stride;
       wave_frames_load<kStreamAux>(r_pk, run_of(base + stride), cn);
-      imn = __builtin_amdgcn_raw_buffer_load_b32(r_im, nx < a.n ? nx * 4u : kNoRun, 0, kStreamAux);
+      imn = __builtin_amdgcn_raw_buffer_load_b32(r_im, nx < n ? nx * 4u : kNoRun, 0, kStreamAux);
     }
 
     bool hit = false;
@@ -198,28 +214,30 @@ __global__ __launch_bounds__(kFB, NFDP_FUSED_WAVES_PER_EU) void fused_kernel(Fus
     uint32_t reason = e.reason;
     uint32_t eg = 0, pos = 0;
     if constexpr (REMOTE) {
-      // egress GPU of the frame; block-aggregated slot in that GPU's segment (all threads call)
-      eg = e.reason ? a.rank : (uint32_t)ta.port(e.out_port).gpu;
-      const bool remote = valid && !e.reason && eg != a.rank && eg < a.nranks;
+      // egress GPU of the frame (or the flow owner when steering); block-aggregated slot in that
+      // GPU's segment (all threads call)
+      eg = a.steer ? owner : (e.reason ? a.rank : (uint32_t)ta.port(e.out_port).gpu);
+      const bool remote = a.steer ? to_owner : (valid && !e.reason && eg != a.rank && eg < a.nranks);
       pos = reserve_block(a.pcnt, eg, remote, a.nranks, rcnt + (it & 1u) * kMaxRanks, rbase,
                           rcnt + (~it & 1u) * kMaxRanks);
       if (remote) {
         if (pos < a.cap_pkt) {
           uint8_t* segp = a.send_pkt + (size_t)eg * pkt_seg_bytes(a.cap_pkt);
           reinterpret_cast<uint32_t*>(segp + pkt_meta_off(a.cap_pkt))[pos] =
-              make_meta(e.out_port, p.len + (e.push ? 4u : 0u), kOk);
+              a.steer ? imn : make_meta(e.out_port, p.len + (e.push ? 4u : 0u), kOk);
           to_peer = true;
         } else {
           reason = kOverflow;
         }
       }
     }
+    if (to_owner && !to_peer) reason = kOverflow;  // the owner's segment was full: dropped here
     const uint32_t olen = reason ? 0u : p.len + (e.push ? 4u : 0u);
-    const uint32_t meta = to_peer ? make_meta(e.out_port, olen, kRemote)
+    const uint32_t meta = to_peer ? make_meta(a.steer ? kPortNone : e.out_port, a.steer ? st.wire_len : olen, kRemote)
                                   : make_meta(reason == kOverflow ? kPortNone : e.out_port, olen, reason, false,
                                               !reason && e.flood);
     // port / drop counters: LDS, global only for ports >= kLdsPorts (issued before the tail)
-    if (valid && !(a.flags & 1u)) {
+    if (valid && !(a.flags & 1u) && !(to_owner && to_peer)) {  // a steered packet is counted by its owner
       if (st.in_port < kLdsPorts) {
         atomicAdd(&pc[st.in_port], 1u); atomicAdd(&pc[kLdsPorts + st.in_port], st.wire_len);
       } else if (st.in_port < (uint32_t)kMaxPorts) {
@@ -236,7 +254,8 @@ __global__ __launch_bounds__(kFB, NFDP_FUSED_WAVES_PER_EU) void fused_kernel(Fus
       }
     }
     uint32_t o[kSlotDwords];
-    emit(p, e.tci, e.push != 0, o);
+    // a steered packet travels as it came in (p is untouched: the chain never ran on it)
+    emit(p, to_owner ? p.tci : e.tci, to_owner ? p.tagged : e.push != 0, o);
     if (a.side.cnt) {
       // flood / mirror / ARP-trap / learning packets go on the side list (side_kernel emits their
       // replicas and learn events after this kernel): a wave-uniform skip in the common case
@@ -272,7 +291,7 @@ __global__ __launch_bounds__(kFB, NFDP_FUSED_WAVES_PER_EU) void fused_kernel(Fus
       }
       const uint32_t nx = i + stride;
       wave_frames_load<kStreamAux>(r_pk, run_of(base + stride), cn);
-      imn = __builtin_amdgcn_raw_buffer_load_b32(r_im, nx < a.n ? nx * 4u : kNoRun, 0, kStreamAux);
+      imn = __builtin_amdgcn_raw_buffer_load_b32(r_im, nx < n ? nx * 4u : kNoRun, 0, kStreamAux);
     }
   }
   __syncthreads();
@@ -306,6 +325,35 @@ __global__ __launch_bounds__(256) void side_kernel(SideArgs a) {
     }
     GpuSideSink sk{a.side, a.port_ctr, a.drop_ctr};
     side_stage(a.t, DirectTables{a.t}, d, a.inmeta[i], o, a.out_meta[i], i, sk);
+  }
+}
+
+// Exchange receive side of flow-owner steering: the segments peers filled (64-B header slots +
+// ingress meta, count in each segment header) -> one dense batch; the total goes to *n_dev so the
+// fused kernel that follows processes exactly what arrived, with no host round trip.
+__global__ __launch_bounds__(256) void gather_kernel(const uint8_t* recv, uint32_t nranks, uint32_t rank, uint32_t cap,
+                                                     uint32_t seg_bytes, uint32_t meta_off, uint4* pkts, uint32_t* inmeta,
+                                                     uint32_t* n_dev) {
+  const uint32_t total = nranks * cap;
+  for (uint32_t idx = blockIdx.x * 256 + threadIdx.x; idx < total; idx += gridDim.x * 256) {
+    const uint32_t s = idx / cap, j = idx % cap;
+    if (s == rank) continue;
+    const uint32_t* hdr = reinterpret_cast<const uint32_t*>(recv + (size_t)s * seg_bytes);
+    const uint32_t c = min(hdr[0], cap);
+    if (j >= c) continue;
+    uint32_t base = 0;
+    for (uint32_t q = 0; q < s; ++q)
+      if (q != rank) base += min(reinterpret_cast<const uint32_t*>(recv + (size_t)q * seg_bytes)[0], cap);
+    const uint4* src = reinterpret_cast<const uint4*>(recv + (size_t)s * seg_bytes + 64 + (size_t)j * 64);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) pkts[(size_t)(base + j) * 4 + k] = src[k];
+    inmeta[base + j] = reinterpret_cast<const uint32_t*>(recv + (size_t)s * seg_bytes + meta_off)[j];
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    uint32_t t = 0;
+    for (uint32_t q = 0; q < nranks; ++q)
+      if (q != rank) t += min(reinterpret_cast<const uint32_t*>(recv + (size_t)q * seg_bytes)[0], cap);
+    *n_dev = t;
   }
 }
 
@@ -445,6 +493,8 @@ hipError_t launch_fused(const FusedLaunch& f, const LaunchCfg& cfg, hipStream_t 
   a.send_pkt = f.send_pkt; a.pcnt = f.pcnt;
   a.nranks = f.nranks; a.rank = f.rank; a.cap_pkt = f.cap_pkt;
   a.side = f.side;
+  a.steer = f.steer;
+  a.n_dev = f.n_dev;
   if (a.side.cnt && ((a.side.cap_rep && (!a.side.rep_hdr || !a.side.rep_meta || !a.side.rep_src)) ||
                      (a.side.cap_learn && !a.side.learn) || (a.side.cap_list && !a.side.list)))
     return hipErrorInvalidValue;
@@ -459,6 +509,18 @@ hipError_t launch_fused(const FusedLaunch& f, const LaunchCfg& cfg, hipStream_t 
   NFDP_CASE(2, 0) NFDP_CASE(2, 1) NFDP_CASE(2, 2)
 #undef NFDP_CASE
   return hipErrorInvalidValue;
+}
+
+hipError_t launch_gather(const uint8_t* recv, uint32_t nranks, uint32_t rank, uint32_t cap, uint32_t seg_bytes,
+                         uint32_t meta_off, void* pkts, uint32_t* inmeta, uint32_t* n_dev, hipStream_t s) {
+  if (!recv || !pkts || !inmeta || !n_dev || rank >= nranks || nranks > kMaxRanks) return hipErrorInvalidValue;
+  const uint32_t total = nranks * cap;
+  uint32_t grid = (total + 255) / 256;
+  if (grid > 1024) grid = 1024;
+  if (grid == 0) grid = 1;
+  hipLaunchKernelGGL(gather_kernel, dim3(grid), dim3(256), 0, s, recv, nranks, rank, cap, seg_bytes, meta_off,
+                     reinterpret_cast<uint4*>(pkts), inmeta, n_dev);
+  return hipGetLastError();
 }
 
 hipError_t launch_stamp(unsigned long long* dst, hipStream_t s) {

@@ -354,6 +354,24 @@ class DataPlane:
             self._apply_learn()
         return BatchResult(out, meta, n, {"hash": hashes, "acl": acl})
 
+    def launch(self, pkts: int, inmeta: int, n: int, out: int, meta: int, lat: int = 0, t0: int | None = None,
+               stream: int | None = None, n_dev: int = 0, flags: int = 0) -> None:
+        """Pointer-level fused launch on the GPU (no batch checks): `n_dev` (optional) is a device
+        word holding the real packet count (<= n), for batches whose size only the GPU knows."""
+        if not self.gpu:
+            raise RuntimeError("launch() is the GPU path; use run() for the oracle")
+        s = stream if stream is not None else _torch().cuda.current_stream(self.tdev).cuda_stream
+        if not self.count_flows:
+            flags |= 4
+        self.nf.launch_fused(
+            self.tables_ptrs(), pkts, inmeta, out, meta, n,
+            self._ptr("flow_ctr"), self._ptr("port_ctr"), self._ptr("drop_ctr"),
+            self._ptr("t0") if t0 is None else t0, lat,
+            self._ptr("acl_wfrag"), self._ptr("acl_cinit"), self._acl_tiles,
+            self._ptr("toep_frag"), self._ptr("toep_tab"),
+            self.hash_mode, self.acl_mode, self.num_cus, s, flags, None, n_dev,
+        )
+
     # ------------------------------------------------------------------ counters
     def harvest(self) -> None:
         """Read-and-reset the packed per-flow counters into 64-bit host totals."""

@@ -289,10 +289,12 @@ def test_host_path_pipeline_matches_oracle():
     assert t["total"] >= t["kernel"] > 0
 
 
-def test_bench_multirank_rehearsal_on_one_gpu():
-    """The N-GPU bench path end to end (torchrun, one process per rank, replicated tables, fused
-    REMOTE kernel, exchange, egress kernel, stats collectives) with 2 ranks sharing cuda:0 over
-    gloo (RCCL refuses two ranks on one device).  Every packet must be forwarded."""
+@pytest.mark.parametrize("mode,n", [("rss", 2), ("rss", 4), ("replicated", 2)])
+def test_bench_multirank_rehearsal_on_one_gpu(mode, n):
+    """The N-GPU bench path end to end (torchrun, one process per rank; rss: flow-shard tables,
+    owner-steering REMOTE kernel, exchange, gather + fused kernel on what arrived; replicated:
+    fused REMOTE kernel, exchange, egress kernel; stats collectives) with the ranks sharing cuda:0
+    over gloo (RCCL refuses two ranks on one device).  Every packet must be forwarded."""
     import json
     import os
     import socket
@@ -304,12 +306,13 @@ def test_bench_multirank_rehearsal_on_one_gpu():
     port = s.getsockname()[1]
     s.close()
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2", "--steps", "2",
-           "--warmup", "1", "--batch", str(1 << 16), "--flows", str(1 << 16), "--rehearse"]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", str(n), "--steps", "2",
+           "--warmup", "1", "--batch", str(1 << 16), "--flows", str(1 << 16), "--rehearse", "--mode", mode,
+           "--remote-frac", "0.05", "--no-variants"]
     r = subprocess.run(cmd, cwd=repo, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stderr[-2000:]
     line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
-    assert line["n_gpus"] == 2 and line["forwarded_fraction"] == 1.0
-    assert line["config"]["global_batch"] == 2 << 16
+    assert line["n_gpus"] == n and line["forwarded_fraction"] == 1.0
+    assert line["config"]["global_batch"] == n << 16
     assert line["exchange"]["a2a_per_step"] >= 1 and line["exchange"]["xgmi_bytes_out_per_gpu_per_step"] > 0
