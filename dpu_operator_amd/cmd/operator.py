@@ -3,8 +3,9 @@
 Flags kept: --metrics-bind-address (:18090), --health-probe-bind-address (:18091), --bindata,
 --leader-elect (Lease id `1e46962d.openshift.io`), webhook server on :9443 with certificates from
 --cert-dir (tls.crt / tls.key), ENABLE_WEBHOOKS=false disables the webhook.  Controllers:
-DpuOperatorConfig + ServiceFunctionChain.  Without a cluster API endpoint in this environment the
-operator runs against an API server object it is handed (or a standalone in-process one).
+DpuOperatorConfig + ServiceFunctionChain.  The API is the cluster's (k8s/rest.py RestClient:
+--kubeconfig, $KUBECONFIG or the in-cluster service account, as controller-runtime's
+GetConfigOrDie); --standalone runs against an in-process API server instead (demos, tests).
 """
 from __future__ import annotations
 
@@ -39,13 +40,28 @@ def build_parser() -> argparse.ArgumentParser:
     ap.add_argument("--identity", default=f"{socket.gethostname()}_{os.getpid()}")
     ap.add_argument("--lease-duration", type=float, default=15.0)
     ap.add_argument("--renew-interval", type=float, default=2.0)
+    ap.add_argument("--kubeconfig", default="", help="cluster API config (default: $KUBECONFIG, then in-cluster)")
+    ap.add_argument("--standalone", action="store_true", help="in-process API server (no cluster)")
     return ap
+
+
+def cluster_api(args):
+    """The cluster API client, or an in-process ApiServer with --standalone; exits without one."""
+    if getattr(args, "standalone", False):
+        return ApiServer(scheme=SCHEME)
+    from ..k8s.rest import connect
+
+    api = connect(args.kubeconfig or None)
+    if api is None:
+        raise SystemExit("no cluster configuration (--kubeconfig, $KUBECONFIG or in-cluster service account); "
+                         "use --standalone for an in-process API server")
+    return api
 
 
 class Operator:
     def __init__(self, args, api: ApiServer | None = None, image_manager=None):
         self.args = args
-        self.api = api or ApiServer(scheme=SCHEME)
+        self.api = api if api is not None else cluster_api(args)
         for crd in crd_manifests():
             try:
                 self.api.create(crd)

@@ -116,10 +116,18 @@ class ApiServer:
     def register_mutating(self, kind: str, fn: Admission) -> None:
         self._mutating[kind].append(fn)
 
-    def watch(self, kind: str, fn: Watcher, replay: bool = True) -> Callable[[], None]:
+    def watch(self, kind: str, fn: Watcher, replay: bool = True, namespace: str | None = None) -> Callable[[], None]:
+        if namespace is not None and kind not in CLUSTER_SCOPED:
+            inner = fn
+
+            def fn(etype: str, obj: dict, _inner=inner) -> None:  # noqa: F811 - namespace-filtered watch
+                if (obj.get("metadata") or {}).get("namespace", "") == namespace:
+                    _inner(etype, obj)
         with self._lock:
             self._watchers[kind].append(fn)
-            existing = [copy.deepcopy(o) for k, o in self._objs.items() if k[0] == kind] if replay else []
+            existing = [copy.deepcopy(o) for k, o in self._objs.items()
+                        if k[0] == kind and (namespace is None or kind in CLUSTER_SCOPED or k[1] == namespace)] \
+                if replay else []
         for o in existing:
             fn("ADDED", o)
 

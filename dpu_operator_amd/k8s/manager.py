@@ -100,9 +100,9 @@ class Manager:
 
     def _subscribe(self) -> None:
         for ctl in self._ctls:
-            self._cancels.append(self.api.watch(ctl.kind, self._on_event(ctl, False)))
+            self._cancels.append(self.api.watch(ctl.kind, self._on_event(ctl, False), namespace=ctl.namespace))
             for k in ctl.owns:
-                self._cancels.append(self.api.watch(k, self._on_event(ctl, True), replay=False))
+                self._cancels.append(self.api.watch(k, self._on_event(ctl, True), replay=False, namespace=ctl.namespace))
 
     def _process_one(self, block: bool, timeout: float) -> bool:
         with self._cv:
