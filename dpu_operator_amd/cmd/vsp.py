@@ -29,9 +29,14 @@ def build_vsp(a, pm: PathManager):
         from ..vsp.gpu import GpuVsp
 
         cfg = node_config()
+        nl = None
+        if a.live:
+            from ..cni.netlink import RtNetlink
+
+            nl = RtNetlink()
         return GpuVsp(pm, device=a.device or None, flow_buckets=a.flow_buckets or cfg.flow_buckets,
                       hash_mode=cfg.hash_mode, acl_mode=cfg.acl_mode,
-                      state_dir=a.state_dir or cfg.vsp_state_dir or None)
+                      state_dir=a.state_dir or cfg.vsp_state_dir or None, nl=nl, live=a.live)
     from ..cni.netlink import RtNetlink
     from ..platform.platform import SysfsPlatform
     from ..utils.cmdrunner import HostRunner
@@ -77,6 +82,8 @@ def main(argv=None, stop: threading.Event | None = None) -> int:
     ap.add_argument("--acc-macs", default="")
     ap.add_argument("--mode", default="ipu")
     ap.add_argument("--state-dir", default="", help="amd-gpu: journal + snapshot directory (resume on restart)")
+    ap.add_argument("--live", action="store_true",
+                    help="amd-gpu: vports are real TAP netdevs and pod traffic flows through the data plane")
     a = ap.parse_args(argv)
     if a.node_config:
         set_node_config(NodeConfig.load(a.node_config))

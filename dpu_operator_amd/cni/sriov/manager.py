@@ -165,7 +165,11 @@ class SriovManager:
                     undo.append(lambda: self.ipam.release(conf.name, req.container_id, req.ifname))
                     self.nl.addr_add(req.ifname, ip["address"], req.netns)
                     ips.append(dict(ip, interface=0))
-                    announce(req.ifname, mac, [ip["address"]])
+                    # GARP / NA from inside the pod netns, where the VF now lives (packet.go:166-198)
+                    try:
+                        self.nl.run_in_ns(req.netns, lambda: announce(req.ifname, mac, [ip["address"]]))
+                    except OSError as e:
+                        clog.warning(f"announce {req.ifname} in {req.netns}: {e}")
             U.save_net_conf(req.container_id, self.cache_dir, req.ifname, conf.to_json())
             undo.append(lambda: U.clean_cached_net_conf(U.cache_path(self.cache_dir, req.container_id, req.ifname)))
             self.allocator.save_allocated_pci(conf.deviceID, req.netns)

@@ -48,7 +48,17 @@ def unsolicited_na_frame(src_mac: str, ip: str) -> bytes:
     return eth + ip6 + body
 
 
-def announce(ifname: str, mac: str, ips: list[str]) -> int:
+def announce(ifname: str, mac: str, ips: list[str], netns: str = "") -> int:
+    """Send a GARP (IPv4) / unsolicited NA (IPv6) per address out of `ifname` - inside `netns`
+    (the pod's namespace, where the VF lives after SetupVF; packet.go:166-198 runs in the
+    container's netns too).  Returns the number of frames sent."""
+    if netns:
+        from ..netlink import in_netns
+
+        try:
+            return in_netns(netns, lambda: announce(ifname, mac, ips))
+        except OSError:
+            return 0
     sent = 0
     try:
         s = socket.socket(socket.AF_PACKET, socket.SOCK_RAW)

@@ -1,0 +1,199 @@
+"""Live packet path: vport netdevs <-> the data plane.
+
+The reference moves real frames between pod netdevs through veth pairs and the OvS bridge
+(vspnetutils.go:141-208, marvell/main.go:105-154).  Here every data-plane port that
+faces a pod or an NF is a TAP netdev owned by the VSP: the CNI moves it into the pod's network
+namespace like any DPU netdev (networkfn.go:233-317), and the VSP keeps its file descriptor, so
+what the pod sends arrives on that fd and what the VSP writes to it is what the pod receives.
+
+``LivePath`` is the loop between those fds and the pipeline:
+
+    poll(all vport fds) -> read bursts (up to `burst` frames, every port) -> header slots
+      (first 64 B) + ingress meta (port | len << 16); the frames stay in host memory
+    -> DataPlane.run: the fused HIP kernel on the GPU (batch uploaded to HBM) or the oracle
+    -> every forwarded frame: ohdr[:hl] ++ frame[to:len] (nfdp.h out_tail) written to the egress
+       port's fd; flood / mirror replicas the same way from the side outputs; ARP copies trapped to
+       the slow path go to `on_punt`; frames for ports without a netdev (the uplink when none is
+       attached) are counted as `no_netdev`.
+
+Frames are whole Ethernet frames without FCS (TAP, IFF_NO_PI).  MAC learning, flooding, VLAN
+tags, SNAT etc. are the pipeline's; this loop only moves bytes.
+"""
+from __future__ import annotations
+
+import errno
+import fcntl
+import logging
+import os
+import select
+import struct
+import threading
+import time
+
+import numpy as np
+
+from ..ops import packets as P
+
+log = logging.getLogger("dpu.netio")
+
+TUNSETIFF = 0x400454CA
+IFF_TAP, IFF_NO_PI = 0x0002, 0x1000
+
+
+class TapPort:
+    """A TAP netdev whose fd the data plane owns (non-blocking)."""
+
+    def __init__(self, name: str, mac: str | None = None, nl=None):
+        if len(name) > 15:
+            raise ValueError("interface names are at most 15 characters")
+        self.name = name
+        self.fd = os.open("/dev/net/tun", os.O_RDWR | os.O_NONBLOCK)
+        try:
+            fcntl.ioctl(self.fd, TUNSETIFF, struct.pack("16sH", name.encode(), IFF_TAP | IFF_NO_PI))
+        except OSError:
+            os.close(self.fd)
+            raise
+        if mac and nl is not None:
+            nl.link_set_hw_addr(name, mac)
+        self.rx = self.tx = self.tx_err = 0
+
+    def read(self) -> bytes | None:
+        try:
+            f = os.read(self.fd, 1 << 16)
+        except BlockingIOError:
+            return None
+        except OSError as e:
+            if e.errno in (errno.EAGAIN, errno.EIO):  # EIO: the netdev is down
+                return None
+            raise
+        self.rx += 1
+        return f
+
+    def write(self, frame: bytes) -> bool:
+        try:
+            os.write(self.fd, frame)
+            self.tx += 1
+            return True
+        except OSError:  # down / no carrier: the frame is lost, as on a wire
+            self.tx_err += 1
+            return False
+
+    def close(self) -> None:
+        if self.fd >= 0:
+            os.close(self.fd)
+            self.fd = -1
+
+
+class LivePath:
+    def __init__(self, dp, ports: dict, burst: int = 256, on_punt=None):
+        self.dp = dp
+        self.ports = dict(ports)          # data-plane port -> TapPort (anything with read/write/fd)
+        self.burst = burst
+        self.on_punt = on_punt            # f(frame: bytes, in_port: int, reason: int)
+        self.stats = {"rx": 0, "tx": 0, "replicas": 0, "punt": 0, "drop": 0, "no_netdev": 0, "batches": 0}
+        self._stop = threading.Event()
+        self._t: threading.Thread | None = None
+        self._lock = threading.Lock()     # port map changes vs the loop
+        self.error: BaseException | None = None
+
+    # ------------------------------------------------------------------ port map
+    def add_port(self, idx: int, port) -> None:
+        with self._lock:
+            self.ports[idx] = port
+
+    def remove_port(self, idx: int):
+        with self._lock:
+            return self.ports.pop(idx, None)
+
+    # ------------------------------------------------------------------ one cycle
+    def _gather(self, timeout: float) -> tuple[list[bytes], list[int]]:
+        with self._lock:
+            items = list(self.ports.items())
+        if not items:
+            time.sleep(timeout)
+            return [], []
+        p = select.poll()
+        fd2port = {}
+        for idx, port in items:
+            p.register(port.fd, select.POLLIN)
+            fd2port[port.fd] = (idx, port)
+        frames, src = [], []
+        for fd, _ev in p.poll(int(timeout * 1000)):
+            idx, port = fd2port[fd]
+            while len(frames) < self.burst:
+                f = port.read()
+                if f is None:
+                    break
+                if 14 <= len(f) <= P.MAX_FRAME:
+                    frames.append(f)
+                    src.append(idx)
+        return frames, src
+
+    def _send(self, port_idx: int, frame: bytes) -> None:
+        port = self.ports.get(port_idx)
+        if port is None:
+            self.stats["no_netdev"] += 1
+        elif port.write(frame):
+            self.stats["tx"] += 1
+
+    def poll_once(self, timeout: float = 0.05) -> int:
+        frames, src = self._gather(timeout)
+        n = len(frames)
+        if not n:
+            return 0
+        lens = np.array([len(f) for f in frames], np.uint32)
+        slots = np.zeros((n, 64), np.uint8)
+        for i, f in enumerate(frames):
+            h = f[:64]
+            slots[i, : len(h)] = np.frombuffer(h, np.uint8)
+        im = P.inmeta(np.array(src, np.uint32), lens)
+        if self.dp.gpu:
+            import torch
+
+            r = self.dp.run(torch.from_numpy(slots).to(self.dp.tdev), torch.from_numpy(im.view(np.int32)).to(self.dp.tdev))
+            out = r.out.cpu().numpy()
+            meta = r.meta.cpu().numpy().view(np.uint32)
+        else:
+            r = self.dp.run(slots, im)
+            out, meta = r.out, r.meta
+        side = self.dp.side_result() if self.dp.side_active() else {"n_rep": 0}
+        self.stats["rx"] += n
+        self.stats["batches"] += 1
+        port, _, reason = P.meta_fields(meta)
+        for i in range(n):
+            if reason[i]:
+                self.stats["drop"] += 1
+                continue
+            self._send(int(port[i]), P.assemble(out[i], int(meta[i]), np.frombuffer(frames[i], np.uint8), int(lens[i])))
+        for k in range(side.get("n_rep", 0)):
+            s = int(side["rep_src"][k])
+            m = int(side["rep_meta"][k])
+            rp, _, rr = P.meta_fields(np.array([m], np.uint32))
+            fr = P.assemble(side["rep_hdr"][k], m, np.frombuffer(frames[s], np.uint8), int(lens[s]))
+            if int(rr[0]):
+                self.stats["punt"] += 1
+                if self.on_punt:
+                    self.on_punt(fr, src[s], int(rr[0]))
+            else:
+                self.stats["replicas"] += 1
+                self._send(int(rp[0]), fr)
+        return n
+
+    # ------------------------------------------------------------------ thread
+    def _run(self) -> None:
+        try:
+            while not self._stop.is_set():
+                self.poll_once(0.02)
+        except BaseException as e:  # noqa: BLE001 - surfaced through .error
+            self.error = e
+            log.exception("live path stopped")
+
+    def start(self) -> "LivePath":
+        self._t = threading.Thread(target=self._run, daemon=True, name="dpu-livepath")
+        self._t.start()
+        return self
+
+    def stop(self) -> None:
+        self._stop.set()
+        if self._t is not None:
+            self._t.join(timeout=5)

@@ -1,0 +1,81 @@
+"""Network-namespace helpers for live-path tests: endpoints (netns + a data-plane TAP moved into
+it, addressed and up) and an ICMP echo client that runs inside a namespace."""
+from __future__ import annotations
+
+import os
+import socket
+import struct
+import time
+
+from ..cni.netlink import RtNetlink, create_netns, delete_netns, in_netns
+
+
+def privileged() -> bool:
+    """True when this process can create network namespaces and TAP devices."""
+    if not os.path.exists("/dev/net/tun"):
+        return False
+    path = f"/var/run/netns/dpu-probe-{os.getpid()}"
+    try:
+        create_netns(path)
+    except OSError:
+        return False
+    delete_netns(path)
+    return True
+
+
+def _csum(b: bytes) -> int:
+    if len(b) % 2:
+        b += b"\0"
+    s = sum(struct.unpack(f"!{len(b) // 2}H", b))
+    s = (s & 0xFFFF) + (s >> 16)
+    s = (s & 0xFFFF) + (s >> 16)
+    return ~s & 0xFFFF
+
+
+def ping(ns: str, dst: str, timeout: float = 3.0, ident: int = 0x4D49, seq: int = 1, payload: bytes = b"mi355x") -> float | None:
+    """One ICMP echo from inside netns `ns`; the RTT in seconds or None."""
+
+    def run():
+        s = socket.socket(socket.AF_INET, socket.SOCK_RAW, socket.IPPROTO_ICMP)
+        s.settimeout(0.2)
+        try:
+            hdr = struct.pack("!BBHHH", 8, 0, 0, ident, seq)
+            pkt = struct.pack("!BBHHH", 8, 0, _csum(hdr + payload), ident, seq) + payload
+            end = time.monotonic() + timeout
+            t0 = time.monotonic()
+            s.sendto(pkt, (dst, 0))
+            last = t0
+            while time.monotonic() < end:
+                if time.monotonic() - last > 0.5:  # retry: the first try may wait for ARP
+                    t0 = last = time.monotonic()
+                    s.sendto(pkt, (dst, 0))
+                try:
+                    data, addr = s.recvfrom(65535)
+                except socket.timeout:
+                    continue
+                ihl = (data[0] & 0xF) * 4
+                t, _c, _ck, i, q = struct.unpack_from("!BBHHH", data, ihl)
+                if t == 0 and i == ident and q == seq and addr[0] == dst:
+                    return time.monotonic() - t0
+            return None
+        finally:
+            s.close()
+
+    return in_netns(ns, run)
+
+
+class Endpoint:
+    """A namespace with one interface: `ifname` moved in, `cidr` assigned, interface + lo up."""
+
+    def __init__(self, ns_name: str, ifname: str, cidr: str, nl: RtNetlink | None = None):
+        self.nl = nl or RtNetlink()
+        self.ns = create_netns(f"/var/run/netns/{ns_name}")
+        self.ifname = ifname
+        self.nl.link_set_ns(ifname, self.ns)
+        self.nl.link_set_up("lo", self.ns)
+        self.nl.addr_add(ifname, cidr, self.ns)
+        self.nl.link_set_up(ifname, self.ns)
+        self.mac = self.nl.link_by_name(ifname, self.ns).mac
+
+    def close(self) -> None:
+        delete_netns(self.ns)

@@ -17,6 +17,16 @@ It implements the same four services as the reference's VSPs, but instead of pro
 
 Ports: vport i = data-plane port i; the uplink ("wire", the RPM/SFP port of the reference's VSPs)
 is port 4000.  All mutations happen under the VSP lock and are committed atomically per RPC.
+Without an NF, VFs and the wire form one L2 bridge: known pod MACs are forwarded directly,
+broadcast / unknown unicast is flooded (wire first, then the other VFs), like OvS NORMAL on the
+reference's br-mrv0.
+
+Live mode (`live=True`, `vsp --live`): every vport is a real TAP netdev (dataplane/netio.py)
+whose fd the VSP keeps; the CNI moves it into the pod / NF namespace and dataplane/netio.py's
+LivePath moves the frames between those fds and the pipeline (GPU kernel or oracle), so pods
+exchange real traffic through the data plane.  A live vport is the pod-facing side of the VF, where
+the port VLAN is already stripped: VF ports are then programmed without VLAN isolation / egress
+tagging (spoof-check stays).
 
 Checkpoint / resume (the reference's VSPs lose all state on restart): with `state_dir`
 every successful mutating RPC is appended to a write-ahead journal (utils/journal.py) before the
@@ -86,7 +96,8 @@ class GpuVsp(VspBase):
 
     def __init__(self, path_manager=None, device: str | None = None, nl: NetlinkManager | None = None,
                  opi_port: int = 0, flow_buckets: int = 1 << 16, vport_prefix: str = "dpuvp",
-                 hash_mode: str = "mfma", acl_mode: str = "mfma", state_dir: str | None = None):
+                 hash_mode: str = "mfma", acl_mode: str = "mfma", state_dir: str | None = None,
+                 live: bool = False, uplink=None):
         super().__init__(path_manager)
         if device is None:
             try:
@@ -110,6 +121,10 @@ class GpuVsp(VspBase):
         self.healthy = True
         self._salt = int.from_bytes(os.urandom(1), "little")
         self.chain_kinds: dict[str, list[str]] = {}
+        self.live = live
+        self.taps: dict[int, object] = {}       # live mode: port -> TapPort
+        self.livepath = None
+        self.uplink = uplink                    # live mode: netdev (read/write/fd) of the wire port
         self.journal = Journal(state_dir, "gpu-vsp") if state_dir else None
         self._replaying = False
         self.restored = 0
@@ -156,7 +171,8 @@ class GpuVsp(VspBase):
         v = self.vports[i]
         dp = self.dp
         if v["role"] == "vf":
-            dp.ports.set(i, flags=T.PORT_VALID | T.PORT_SPOOFCHK | T.PORT_VLAN_ISOLATE | T.PORT_TAG_EGRESS,
+            vlan_flags = 0 if self.live else T.PORT_VLAN_ISOLATE | T.PORT_TAG_EGRESS
+            dp.ports.set(i, flags=T.PORT_VALID | T.PORT_SPOOFCHK | vlan_flags,
                          vlan=v["vlan"], bridge_id=VF_BRIDGE, mac=v["pod_mac"], peer_mac=v["pod_mac"],
                          default_out=WIRE_PORT)
         elif v["role"] in ("nf_in", "nf_out"):
@@ -182,9 +198,13 @@ class GpuVsp(VspBase):
         dp.macs.clear()
         vfs = self._vf_ports()
         dp.ports.update(WIRE_PORT, default_out=None, bridge_id=VF_BRIDGE)
+        dp.flood.set_members(VF_BRIDGE, [])
         if not self.nfs:
+            # one L2 bridge: pod MACs forwarded, broadcast / unknown unicast flooded (wire first)
             for i in vfs:
                 dp.macs.insert(VF_BRIDGE, self.vports[i]["pod_mac"], i)
+                dp.ports.update(i, default_out=None)
+            dp.flood.set_members(VF_BRIDGE, [WIRE_PORT] + vfs[: T.FLOOD_WAYS - 1])
         else:
             for i in vfs:
                 dp.ports.update(i, default_out=self.nfs[0]["in"], bridge_id=STEER_BRIDGE)
@@ -203,6 +223,13 @@ class GpuVsp(VspBase):
     def init(self, dpu_mode: bool, dpu_identifier: str):
         self.dpu_mode = dpu_mode
         self._ensure_dp()
+        if self.live and self.livepath is None:
+            from ..dataplane.netio import LivePath
+
+            ports = dict(self.taps)
+            if self.uplink is not None:
+                ports[WIRE_PORT] = self.uplink
+            self.livepath = LivePath(self.dp, ports).start()
         if not self.opi_port:
             self.opi_port = self._free_port()
         return "127.0.0.1", self.opi_port
@@ -215,12 +242,26 @@ class GpuVsp(VspBase):
             if i in self.vports:
                 continue
             name, mac = f"{self.prefix}{i}", _local_mac(i, self._salt)
-            self._ensure_tap(name, mac)
+            if self.live:
+                from ..dataplane.netio import TapPort
+
+                tap = TapPort(name, mac, self.nl)
+                self.nl.link_set_up(name)
+                self.taps[i] = tap
+                if self.livepath is not None:
+                    self.livepath.add_port(i, tap)
+            else:
+                self._ensure_tap(name, mac)
             self.vports[i] = {"name": name, "mac": mac, "role": "free", "vlan": 0, "pod_mac": mac, "bridge": VF_BRIDGE}
             self._program_port(i)
         for i in [i for i in self.vports if i >= n and self.vports[i]["role"] == "free"]:
             self.dp.ports.clear(i)
             del self.vports[i]
+            tap = self.taps.pop(i, None)
+            if tap is not None:
+                if self.livepath is not None:
+                    self.livepath.remove_port(i)
+                tap.close()
         self._commit()
         return n
 
@@ -269,6 +310,14 @@ class GpuVsp(VspBase):
                 keep.append(nf)
         self.nfs = keep
         self._apply_steering()
+
+    def stop_live(self) -> None:
+        if self.livepath is not None:
+            self.livepath.stop()
+            self.livepath = None
+        for tap in self.taps.values():
+            tap.close()
+        self.taps.clear()
 
     def on_gpu_chain(self, sfc_name: str, kinds: list[str]) -> int:
         with self._lock:
