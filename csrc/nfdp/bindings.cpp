@@ -48,6 +48,18 @@ TablesView tables_from(const py::dict& d) {
   t.n_lag_groups = val<uint32_t>(d, "n_lag_groups", 0);
   t.flood = ptr<const uint16_t>(d, "flood");
   t.n_flood = t.flood ? val<uint32_t>(d, "n_flood", 0) : 0u;
+  t.lpm24 = ptr<const uint32_t>(d, "lpm24");
+  t.lpm8 = ptr<const uint32_t>(d, "lpm8");
+  t.n_lpm8 = t.lpm8 ? val<uint32_t>(d, "n_lpm8", 0) : 0u;
+  t.nexthops = ptr<const NextHop>(d, "nexthops");
+  t.n_nexthops = t.nexthops ? val<uint32_t>(d, "n_nexthops", 0) : 0u;
+  t.ecmp = ptr<const uint16_t>(d, "ecmp");
+  t.n_ecmp = t.ecmp ? val<uint32_t>(d, "n_ecmp", 0) : 0u;
+  t.tunnels = ptr<const TunnelEntry>(d, "tunnels");
+  t.n_tunnels = t.tunnels ? val<uint32_t>(d, "n_tunnels", 0) : 0u;
+  t.terms = ptr<const TermEntry>(d, "terms");
+  t.term_mask = t.terms ? val<uint32_t>(d, "term_mask", 0) : 0u;
+  if (t.terms && ((t.term_mask + 1) & t.term_mask)) throw std::invalid_argument("term table size must be a power of two");
   if (t.n_lag_groups && !t.lag_members) throw std::invalid_argument("n_lag_groups > 0 but lag_members missing");
   if (!t.ports || !t.chains || !t.flows || !t.rss_key)
     throw std::invalid_argument("tables dict is missing a required buffer");
@@ -66,6 +78,7 @@ SideOut side_from(const py::object& o) {
   so.learn = ptr<uint32_t>(d, "learn"); so.cap_learn = val<uint32_t>(d, "cap_learn", 0);
   so.cnt = ptr<uint32_t>(d, "cnt");
   so.list = ptr<uint32_t>(d, "list"); so.cap_list = val<uint32_t>(d, "cap_list", 0);
+  so.xhdr = ptr<uint32_t>(d, "xhdr");
   if (!so.cnt) throw std::invalid_argument("side outputs need a 'cnt' buffer (4 x u32)");
   if (so.cap_rep && (!so.rep_hdr || !so.rep_meta || !so.rep_src)) throw std::invalid_argument("side: replica buffers missing");
   if (so.cap_learn && !so.learn) throw std::invalid_argument("side: learn buffer missing");
@@ -91,6 +104,15 @@ PYBIND11_MODULE(_nfdp, m) {
   m.attr("MAX_FRAME") = kMaxFrame;
   m.attr("FLOOD_WAYS") = kFloodWays;
   m.attr("ENCAP_BYTES") = kEncapBytes;
+  m.def("make_outer", [](py::bytes te_raw, uint32_t inner_len, uint32_t hash) {
+    std::string s = te_raw;
+    if (s.size() != sizeof(TunnelEntry)) throw std::invalid_argument("tunnel entry must be 32 bytes");
+    TunnelEntry te;
+    std::memcpy(&te, s.data(), sizeof(te));
+    uint32_t x[kSlotDwords];
+    make_outer(te, inner_len, hash, x);
+    return py::bytes(reinterpret_cast<const char*>(x), kEncapBytes);
+  });
 
   py::class_<FlowTableHost>(m, "FlowTable")
       .def(py::init([](uint32_t nb, py::bytes rss) {

@@ -415,6 +415,12 @@ struct GpuSideSink {
     if (r) atomicAdd(drop_ctr + r, 1ull);
     else if (port < (uint32_t)kMaxPorts) atomicAdd(port_ctr + 2 * port + 1, ctr_inc(meta_len(meta)));
   }
+  __device__ __forceinline__ void xhdr(const uint32_t* hdr, uint32_t src) {
+    if (!so.xhdr) return;
+    uint4* dst = reinterpret_cast<uint4*>(so.xhdr) + (size_t)src * 4;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) dst[q] = make_uint4(hdr[4 * q], hdr[4 * q + 1], hdr[4 * q + 2], hdr[4 * q + 3]);
+  }
   __device__ __forceinline__ void learn(uint32_t bridge, uint32_t lo, uint32_t hi, uint32_t port) {
     const uint32_t pos = atomicAdd(so.cnt + 1, 1u);
     if (pos >= so.cap_learn) { atomicAdd(so.cnt + 3, 1u); return; }

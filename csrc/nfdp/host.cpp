@@ -269,6 +269,9 @@ struct CpuSideSink {
     if (r) { if (drop_ctr) drop_ctr[r] += 1; }
     else if (port < (uint32_t)kMaxPorts && port_ctr) port_ctr[2 * port + 1] += ctr_inc(meta_len(meta));
   }
+  void xhdr(const uint32_t* hdr, uint32_t src) {
+    if (so.xhdr) std::memcpy(so.xhdr + (size_t)src * kSlotDwords, hdr, kSlotBytes);
+  }
   void learn(uint32_t bridge, uint32_t lo, uint32_t hi, uint32_t port) {
     const uint32_t pos = so.cnt[1]++;
     if (pos >= so.cap_learn) { ++so.cnt[3]; return; }
@@ -326,9 +329,9 @@ void oracle_run(const TablesView& t, const uint32_t* pkts, const uint32_t* inmet
     const EgressDecision e = chain_stage(t, p, st, hit, act, acl, h);
     uint32_t o[kSlotDwords];
     emit(p, e.tci, e.push != 0, o);
-    const uint32_t olen = e.reason ? 0u : p.len + (e.push ? 4u : 0u);
+    const uint32_t olen = egress_len(p, e);
     std::memcpy(out + (size_t)i * kSlotDwords, o, sizeof(o));
-    out_meta[i] = make_meta(e.out_port, olen, e.reason, false, !e.reason && e.flood);
+    out_meta[i] = make_meta(e.out_port, olen, e.reason, !e.reason && e.xhdr, !e.reason && e.flood);
     if (side && side->cnt && side_needed(st, p, e)) {
       const uint32_t q = side->cnt[5]++;
       if (q < side->cap_list) side->list[q] = i;
@@ -388,17 +391,18 @@ void oracle_run_remote(const TablesView& t, const uint32_t* pkts, const uint32_t
     }
     uint32_t o[kSlotDwords];
     emit(p, to_owner ? p.tci : e.tci, to_owner ? p.tagged : e.push != 0, o);
-    const uint32_t olen = reason ? 0u : p.len + (e.push ? 4u : 0u);
+    const uint32_t olen = reason == e.reason ? egress_len(p, e) : 0u;
     const bool to_peer = remote && reason != kOverflow;
     if (to_peer) {
       uint8_t* segp = r.send_pkt + eg * pseg;
       std::memcpy(segp + 64 + (size_t)pos * 64, o, sizeof(o));
-      const uint32_t m = r.steer ? inmeta[i] : make_meta(e.out_port, olen, kOk);
+      const uint32_t m = r.steer ? inmeta[i] : make_meta(e.out_port, olen, kOk, e.xhdr != 0);
       std::memcpy(segp + pkt_meta_off(r.cap_pkt) + 4 * (size_t)pos, &m, 4);
       out_meta[i] = make_meta(r.steer ? kPortNone : e.out_port, r.steer ? st.wire_len : olen, kRemote);
     } else {
       std::memcpy(out + (size_t)i * kSlotDwords, o, sizeof(o));
-      out_meta[i] = make_meta(reason == kOverflow ? kPortNone : e.out_port, olen, reason, false, !reason && e.flood);
+      out_meta[i] = make_meta(reason == kOverflow ? kPortNone : e.out_port, olen, reason, !reason && e.xhdr,
+                              !reason && e.flood);
     }
     const bool counted_by_owner = to_owner && to_peer;
     if (port_ctr && !counted_by_owner) {

@@ -224,7 +224,7 @@ __global__ __launch_bounds__(kFB, NFDP_FUSED_WAVES_PER_EU) void fused_kernel(Fus
         if (pos < a.cap_pkt) {
           uint8_t* segp = a.send_pkt + (size_t)eg * pkt_seg_bytes(a.cap_pkt);
           reinterpret_cast<uint32_t*>(segp + pkt_meta_off(a.cap_pkt))[pos] =
-              a.steer ? imn : make_meta(e.out_port, p.len + (e.push ? 4u : 0u), kOk);
+              a.steer ? imn : make_meta(e.out_port, egress_len(p, e), kOk, e.xhdr != 0);
           to_peer = true;
         } else {
           reason = kOverflow;
@@ -232,10 +232,10 @@ __global__ __launch_bounds__(kFB, NFDP_FUSED_WAVES_PER_EU) void fused_kernel(Fus
       }
     }
     if (to_owner && !to_peer) reason = kOverflow;  // the owner's segment was full: dropped here
-    const uint32_t olen = reason ? 0u : p.len + (e.push ? 4u : 0u);
+    const uint32_t olen = reason == e.reason ? egress_len(p, e) : 0u;
     const uint32_t meta = to_peer ? make_meta(a.steer ? kPortNone : e.out_port, a.steer ? st.wire_len : olen, kRemote)
-                                  : make_meta(reason == kOverflow ? kPortNone : e.out_port, olen, reason, false,
-                                              !reason && e.flood);
+                                  : make_meta(reason == kOverflow ? kPortNone : e.out_port, olen, reason,
+                                              !reason && e.xhdr, !reason && e.flood);
     // port / drop counters: LDS, global only for ports >= kLdsPorts (issued before the tail)
     if (valid && !(a.flags & 1u) && !(to_owner && to_peer)) {  // a steered packet is counted by its owner
       if (st.in_port < kLdsPorts) {

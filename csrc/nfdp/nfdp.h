@@ -52,6 +52,7 @@ enum Reason : uint32_t {
   kRemote = 10,    // not a drop: handed to the egress GPU over xGMI (multi-GPU path)
   kOverflow = 11,  // exchange segment full (multi-GPU path)
   kArpTrap = 12,   // ARP copy trapped to the slow path (P4 always_trap_arp_table)
+  kRecirc = 13,    // tunnel terminated: recirculate frame[len - olen:] with in_port = meta port (decap)
   kNumReasons = 16,
 };
 
@@ -70,6 +71,9 @@ enum PortFlags : uint32_t {
   kPortVsiLookup = 1u << 10,    // L2 lookup keys on the target VSI (dst MAC byte 1) only (K3)
   kPortLearn = 1u << 11,        // (bridge, src MAC) -> in_port is learned from this port's frames (OvS NORMAL)
   kPortArpTrap = 1u << 12,      // ARP frames from this port are also copied to the slow path
+  kPortRouted = 1u << 13,       // router interface: IPv4 to this port's MAC is routed (LPM) on a flow miss
+  kPortTunnel = 1u << 14,       // egress via this port = VXLAN / GENEVE encap with tunnel[lag] (OvS tunnel port)
+  kPortVtep = 1u << 15,         // underlay port: UDP 4789 / 6081 to ext (local VTEP IPv4) is terminated
 };
 
 constexpr int kLagWays = 8;                 // members per LAG group (hash[2:0])
@@ -85,6 +89,7 @@ enum Hop : uint8_t {
   kHopVlan = 6,     // push (1..4094) / pop (0xFFFF) flow.vlan
   kHopDrop = 7,
   kHopPunt = 8,
+  kHopRoute = 9,    // IPv4 LPM (ipv4_table) -> nexthop / ECMP group -> MACs, port; TTL - 1
 };
 
 // ----------------------------------------------------------------------------------------
@@ -152,6 +157,45 @@ struct alignas(16) MacEntry {    // 16 B, (bridge, dst-mac) -> port  (K5)
 };
 enum MacValid : uint16_t { kMacEmpty = 0, kMacStatic = 1, kMacTomb = 2, kMacLearned = 3, kMacClaim = 0xFFFF };
 static_assert(sizeof(MacEntry) == 16, "MacEntry");
+
+// ---- L3 (P4 ipv4_table + nexthop_table + ecmp_hash_table + rif_mod_table) ----
+// IPv4 LPM as DIR-24-8: tbl24[dst >> 8] is a result or (kLpmExt | g) = tbl8 group g, whose
+// entry [dst & 0xFF] is the result.  Result: 0 = no route; kind[31:30] 1 = nexthop, 2 = ECMP
+// group; id[15:0].
+constexpr uint32_t kLpmExt = 1u << 31;
+constexpr uint32_t kRouteNh = 1u << 30, kRouteEcmp = 2u << 30;
+constexpr int kEcmpWays = 8;            // members per ECMP group, selected by hash[2:0]
+struct alignas(16) NextHop {     // 16 B
+  uint32_t dmac_lo;              // neighbour MAC (raw bytes 0..3)
+  uint16_t dmac_hi;
+  uint16_t port;                 // egress port (a LAG / tunnel port resolves further)
+  uint32_t smac_lo;              // router interface MAC (rif_mod_table)
+  uint16_t smac_hi;
+  uint16_t valid;
+};
+static_assert(sizeof(NextHop) == 16, "NextHop");
+
+// ---- tunnels (VXLAN / GENEVE, IPv4 underlay) ----
+enum TunnelType : uint16_t { kTunVxlan = 1, kTunGeneve = 2 };
+struct alignas(16) TunnelEntry { // 32 B: the outer headers of one tunnel port
+  uint32_t src_ip, dst_ip;       // raw (network order) underlay addresses
+  uint16_t sport;                // raw; 0 = 0xC000 | hash (entropy, RFC 7348)
+  uint16_t dport;                // raw (4789 / 6081)
+  uint32_t vni;                  // host order, 24 bits
+  uint32_t smac_lo; uint16_t smac_hi;
+  uint16_t out_port;             // underlay port the encapsulated frame leaves on
+  uint32_t dmac_lo; uint16_t dmac_hi;
+  uint16_t type;                 // TunnelType
+};
+static_assert(sizeof(TunnelEntry) == 32, "TunnelEntry");
+struct alignas(16) TermEntry {   // 16 B: (outer src ip, vni) -> tunnel port (ipv4_tunnel_term_table)
+  uint32_t src_ip;               // raw
+  uint32_t vni;
+  uint16_t port;
+  uint16_t valid;
+  uint32_t pad;
+};
+static_assert(sizeof(TermEntry) == 16, "TermEntry");
 
 // Verdict returned by the flow owner to the ingress GPU (multi-GPU path).
 struct alignas(16) Verdict {     // 16 B
@@ -415,7 +459,48 @@ struct TablesView {
   uint32_t n_lag_groups;
   const uint16_t* flood;         // n_flood * kFloodWays member ports per bridge (kPortNone padded)
   uint32_t n_flood;              // bridges [0, n_flood) have a flood group
+  const uint32_t* lpm24;         // 1 << 24 entries (nullable: no routes)
+  const uint32_t* lpm8;          // n_lpm8 * 256
+  uint32_t n_lpm8;
+  const NextHop* nexthops;       // n_nexthops
+  uint32_t n_nexthops;
+  const uint16_t* ecmp;          // n_ecmp * kEcmpWays nexthop ids
+  uint32_t n_ecmp;
+  const TunnelEntry* tunnels;    // n_tunnels (indexed by a tunnel port's `lag`)
+  uint32_t n_tunnels;
+  const TermEntry* terms;        // term_mask + 1 slots, open addressing (nullable)
+  uint32_t term_mask;
 };
+
+NFDP_HD uint32_t lpm_lookup(const TablesView& t, uint32_t dst /* host order */) {
+  if (!t.lpm24) return 0;
+  const uint32_t e = t.lpm24[dst >> 8];
+  if (!(e & kLpmExt)) return e;
+  const uint32_t g = e & ~kLpmExt;
+  return g < t.n_lpm8 ? t.lpm8[(size_t)g * 256 + (dst & 0xFFu)] : 0u;
+}
+// route result -> nexthop id (ECMP by hash[2:0]) or -1
+NFDP_HD int route_nexthop(const TablesView& t, uint32_t r, uint32_t hash) {
+  const uint32_t id = r & 0xFFFFu;
+  if ((r & (3u << 30)) == kRouteNh) return id < t.n_nexthops ? (int)id : -1;
+  if ((r & (3u << 30)) == kRouteEcmp && t.ecmp && id < t.n_ecmp) {
+    const uint32_t nh = t.ecmp[id * kEcmpWays + (hash & (kEcmpWays - 1))];
+    return nh < t.n_nexthops ? (int)nh : -1;
+  }
+  return -1;
+}
+NFDP_HD uint32_t term_hash(uint32_t src_ip, uint32_t vni) { return fmix32(src_ip ^ (vni * 0x9E3779B1u)); }
+// (outer src ip raw, vni) -> tunnel port or -1
+NFDP_HD int term_lookup(const TablesView& t, uint32_t src_ip, uint32_t vni) {
+  if (!t.terms) return -1;
+  const uint32_t h = term_hash(src_ip, vni);
+  for (uint32_t q = 0; q < 8; ++q) {
+    const TermEntry& e = t.terms[(h + q) & t.term_mask];
+    if (!e.valid) return -1;
+    if (e.src_ip == src_ip && e.vni == vni) return e.port;
+  }
+  return -1;
+}
 
 // Side outputs of a batch (pipeline.h side_stage): replicas (flood members, mirror copies, ARP
 // slow-path copies) and MAC-learn events, appended at positions claimed with one atomic each.
@@ -431,6 +516,7 @@ struct SideOut {
   uint32_t* cnt;                 // 8 counters (nullptr: side outputs disabled); [5] side-list length
   uint32_t* list;                // packets flagged by the per-packet kernel for the side pass
   uint32_t cap_list;
+  uint32_t* xhdr;                // [batch] x 64-B outer-header records of tunnel-encapsulated packets
 };
 
 // Flow-table lookup (scalar).  Returns slot index or -1.

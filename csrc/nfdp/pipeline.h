@@ -75,13 +75,25 @@ struct EgressDecision {
   uint32_t mirror;    // 1 -> the ingress frame is also copied to the ingress port's mirror port (K9)
   uint32_t flood;     // bridge + 1 when the frame is flooded: out_port is the group's first member,
                       // side_stage emits a replica per further member
+  uint32_t xhdr;      // 1 -> out_port is a tunnel port: the side pass writes the 50-B outer header
+  uint32_t inner_len; // kRecirc: length of the decapsulated inner frame
 };
+
+// Length of the frame that leaves (the meta word's len): inner frame for a recirculation, tag and
+// outer-header bytes included otherwise, 0 for drops.
+NFDP_HD uint32_t egress_len(const Parsed& p, const EgressDecision& e) {
+  if (e.reason == kRecirc) return e.inner_len;
+  if (e.reason) return 0u;
+  return p.len + (e.push ? 4u : 0u) + (e.xhdr ? kEncapBytes : 0u);
+}
+
+NFDP_HD uint32_t byte_at(const uint32_t* s, int off) { return (s[off >> 2] >> (8 * (off & 3))) & 0xFFu; }
 
 // Final egress checks on a chosen port: LAG member (K8), validity, egress tag (K6), MTU.
 // Returns a drop reason (0 = ok); `port`/`push`/`tci` are updated in place.
 template <class TA>
 NFDP_HD uint32_t finish_port(const TablesView& t, const TA& ta, uint32_t& port, uint32_t hash, bool vlan_done,
-                             uint32_t& push, uint32_t& tci, uint32_t l2len) {
+                             uint32_t& push, uint32_t& tci, uint32_t l2len, uint32_t* xhdr = nullptr) {
   if (port >= (uint32_t)kMaxPorts) return kBadPort;
   PortEntry pe = ta.port(port);
   if (pe.flags & kPortLag) {
@@ -94,8 +106,32 @@ NFDP_HD uint32_t finish_port(const TablesView& t, const TA& ta, uint32_t& port, 
   }
   if (!(pe.flags & kPortValid)) return kBadPort;
   if (!vlan_done && (pe.flags & kPortTagEgress) && pe.vlan) { push = 1; tci = pe.vlan & 0xFFFu; }
+  // tunnel port (OvS vxlan / geneve port, P4 l2_to_tunnel_v4): encapsulated by the side pass
+  uint32_t enc = 0;
+  if (pe.flags & kPortTunnel) {
+    if (!t.tunnels || pe.lag >= t.n_tunnels) return kBadPort;
+    enc = kEncapBytes;
+    if (xhdr) *xhdr = 1;
+  }
   // l2len is untagged: the L3 size is l2len - 14 whatever the tagging
-  if (l2len + (push ? 4u : 0u) > kMaxFrame || (pe.mtu && l2len - 14u > pe.mtu)) return kTooBig;
+  if (l2len + (push ? 4u : 0u) + enc > kMaxFrame || (pe.mtu && l2len - 14u > pe.mtu)) return kTooBig;
+  return kOk;
+}
+
+// IPv4 routing on the normalized frame (P4 ipv4_table LPM -> ecmp_hash_table -> nexthop_table,
+// rif_mod_table for the source MAC): TTL - 1 with the checksum update, neighbour / router MACs,
+// egress port.  Returns a drop reason (0 = routed, e.out_port set).
+NFDP_HD uint32_t route_ipv4(const TablesView& t, Parsed& p, uint32_t hash, uint32_t& out_port) {
+  if (!p.ipv4) return kNoRoute;
+  const uint32_t dst = __builtin_bswap32(raw32_at2(p.s, 30));
+  const int nh = route_nexthop(t, lpm_lookup(t, dst), hash);
+  if (nh < 0) return kNoRoute;
+  const NextHop n = t.nexthops[nh];
+  if (!n.valid) return kNoRoute;
+  if (!act_ttl(p)) return kTtlExpired;
+  set_dmac(p.s, n.dmac_lo, n.dmac_hi);
+  set_smac(p.s, n.smac_lo, n.smac_hi);
+  out_port = n.port;
   return kOk;
 }
 
@@ -106,9 +142,40 @@ NFDP_HD EgressDecision chain_stage(const TablesView& t, const TA& ta, Parsed& p,
                                    bool hit, const FlowAction& act, int acl_rule, uint32_t hash) {
   EgressDecision e;
   e.out_port = kPortNone; e.reason = st.reason; e.push = 0; e.tci = 0; e.mirror = 0; e.flood = 0;
+  e.xhdr = 0; e.inner_len = 0;
   if (e.reason) return e;
   bool vlan_done = false;
   if (!hit) {
+    // tunnel termination on an underlay port (ipv4_tunnel_term_table + rx_ipv4_tunnel_source_port):
+    // UDP 4789 (VXLAN) / 6081 (GENEVE, no options) to the local VTEP -> recirculate the inner
+    // frame as received on the tunnel's port (P4 do_recirculate; the I/O layer re-injects it)
+    if ((st.in_flags & kPortVtep) && p.ipv4 && (p.s[5] >> 24) == 17u && p.len >= 64u &&
+        raw32_at2(p.s, 30) == st.in_ext) {
+      const uint32_t dport = be16_at(p.s, 36);
+      const bool vx = dport == 4789u, gn = dport == 6081u && (byte_at(p.s, 42) & 0x3Fu) == 0u;
+      if (vx || gn) {
+        const uint32_t vni = (byte_at(p.s, 46) << 16) | (byte_at(p.s, 47) << 8) | byte_at(p.s, 48);
+        const int tp = term_lookup(t, raw32_at2(p.s, 26), vni);
+        if (tp >= 0) {
+          e.reason = kRecirc; e.out_port = (uint32_t)tp; e.inner_len = p.len - kEncapBytes;
+          return e;
+        }
+      }
+    }
+    // router interface (kPortRouted): IPv4 addressed to the port's own MAC is routed
+    if ((st.in_flags & kPortRouted) && p.ipv4) {
+      const PortEntry ip = ta.port(st.in_port);
+      if (dmac_lo(p.s) == ip.mac_lo && dmac_hi(p.s) == ip.mac_hi) {
+        uint32_t op = kPortNone;
+        const uint32_t r = route_ipv4(t, p, hash, op);
+        if (r) { e.reason = r; e.out_port = r == kNoRoute ? kPortPunt : kPortNone; return e; }
+        e.out_port = op;
+        const uint32_t r2 = finish_port(t, ta, e.out_port, hash, false, e.push, e.tci, p.len, &e.xhdr);
+        if (r2) { e.reason = r2; e.out_port = kPortNone; e.xhdr = 0; return e; }
+        e.mirror = (st.in_flags & kPortMirror) ? 1u : 0u;
+        return e;
+      }
+    }
     // (bridge, dst MAC) table = OvS `in_port=X,dl_dst=M` / P4 l2_fwd; output == in_port is the
     // OvS hairpin.  A miss falls back to the ingress port's default output (`in_port=X ->
     // output:Y`, priority 10 in ovsdp.go:133-139) or is punted to the slow path.
@@ -177,11 +244,16 @@ NFDP_HD EgressDecision chain_stage(const TablesView& t, const TA& ta, Parsed& p,
         e.reason = kChainDrop; e.out_port = kPortNone; return e;
       } else if (op == kHopPunt) {
         e.reason = kNoRoute; e.out_port = kPortPunt; return e;
+      } else if (op == kHopRoute) {
+        uint32_t rp = kPortNone;
+        const uint32_t r = route_ipv4(t, p, hash, rp);
+        if (r) { e.reason = r; e.out_port = r == kNoRoute ? kPortPunt : kPortNone; return e; }
+        e.out_port = rp;
       }
     }
   }
-  const uint32_t r = finish_port(t, ta, e.out_port, hash, vlan_done, e.push, e.tci, p.len);
-  if (r) { e.reason = r; e.out_port = kPortNone; e.flood = 0; return e; }
+  const uint32_t r = finish_port(t, ta, e.out_port, hash, vlan_done, e.push, e.tci, p.len, &e.xhdr);
+  if (r) { e.reason = r; e.out_port = kPortNone; e.flood = 0; e.xhdr = 0; return e; }
   e.mirror = (st.in_flags & kPortMirror) ? 1u : 0u;  // mirror_and_send (K9)
   return e;
 }
@@ -190,16 +262,44 @@ NFDP_HD EgressDecision chain_stage(const TablesView& t, Parsed& p, const Ingress
   return chain_stage(t, DirectTables{t}, p, st, hit, act, acl_rule, hash);
 }
 
+// Outer headers of a tunnel port for an inner frame of `inner_len` bytes (50 B: Ethernet,
+// IPv4 with DF and its checksum, UDP with the entropy source port and checksum 0, VXLAN flags
+// 0x08 + VNI or GENEVE 0x6558 + VNI), as 16 LE dwords.
+NFDP_HD void make_outer(const TunnelEntry& te, uint32_t inner_len, uint32_t hash, uint32_t* x) {
+  uint8_t b[kSlotBytes];
+  for (int i = 0; i < kSlotBytes; ++i) b[i] = 0;
+  auto put32 = [&](int o, uint32_t raw) { b[o] = raw & 0xFF; b[o + 1] = (raw >> 8) & 0xFF; b[o + 2] = (raw >> 16) & 0xFF; b[o + 3] = raw >> 24; };
+  auto be16 = [&](int o, uint32_t v) { b[o] = (v >> 8) & 0xFF; b[o + 1] = v & 0xFF; };
+  put32(0, te.dmac_lo); b[4] = te.dmac_hi & 0xFF; b[5] = te.dmac_hi >> 8;
+  put32(6, te.smac_lo); b[10] = te.smac_hi & 0xFF; b[11] = te.smac_hi >> 8;
+  be16(12, 0x0800);
+  b[14] = 0x45; be16(16, 20 + 8 + 8 + inner_len); be16(20, 0x4000); b[22] = 64; b[23] = 17;
+  put32(26, te.src_ip); put32(30, te.dst_ip);
+  if (te.sport) { b[34] = te.sport & 0xFF; b[35] = te.sport >> 8; } else { be16(34, 0xC000u | (hash & 0x3FFFu)); }
+  b[36] = te.dport & 0xFF; b[37] = te.dport >> 8;
+  be16(38, 8 + 8 + inner_len);
+  if (te.type == kTunGeneve) { be16(44, 0x6558); } else { b[42] = 0x08; }
+  b[46] = (te.vni >> 16) & 0xFF; b[47] = (te.vni >> 8) & 0xFF; b[48] = te.vni & 0xFF;
+  uint32_t c = 0;
+  for (int o = 14; o < 34; o += 2) c += ((uint32_t)b[o] << 8) | b[o + 1];
+  c = (c & 0xFFFFu) + (c >> 16);
+  c = (c & 0xFFFFu) + (c >> 16);
+  be16(24, ~c & 0xFFFFu);
+  for (int i = 0; i < kSlotDwords; ++i)
+    x[i] = (uint32_t)b[4 * i] | ((uint32_t)b[4 * i + 1] << 8) | ((uint32_t)b[4 * i + 2] << 16) | ((uint32_t)b[4 * i + 3] << 24);
+}
+
 // Side outputs: flood replicas, the K9 mirror copy, the ARP slow-path copy and MAC-learn events.
 // The per-packet kernels only FLAG the packets that need them (side_needed -> the packet's index
 // is appended to a side list; a flooded frame's primary copy carries kMetaFlood) and a separate
 // pass (side_stage: side_kernel on the GPU, sequential in the oracle) emits them from the
 // packet's input slot + ingress meta and its output slot + egress meta.  The hot kernel keeps its
 // register budget; replicas are rare (flooding, mirroring, ARP-trap and learning ports only).
-// `Sink` provides rep(hdr, meta, src) and learn(bridge, lo, hi, port).  Every replica follows the
+// `Sink` provides rep(hdr, meta, src), learn(bridge, lo, hi, port) and xhdr(hdr, src) (the
+// tunnel outer-header record of packet src).  Every replica follows the
 // out_tail() rule against its source packet's input frame.
 NFDP_HD bool side_needed(const IngressState& st, const Parsed& p, const EgressDecision& e) {
-  return (!e.reason && (e.flood || e.mirror)) ||
+  return (!e.reason && (e.flood || e.mirror || e.xhdr)) ||
          (!st.reason && ((st.in_flags & kPortLearn) || (p.arp && (st.in_flags & kPortArpTrap))));
 }
 
@@ -218,6 +318,18 @@ NFDP_HD void side_stage(const TablesView& t, const TA& ta, const uint32_t* d_in,
   // ARP to the slow path (P4 always_trap_arp_table): the ingress frame, punted
   if (p.arp && (st.in_flags & kPortArpTrap)) sink.rep(d_in, make_meta(kPortPunt, st.wire_len, kArpTrap), src);
   if (meta_reason(ometa)) return;
+  // tunnel encap: the outer Ethernet / IPv4 / UDP / VXLAN|GENEVE header record of this packet
+  if (ometa & kMetaXhdr) {
+    const uint32_t tp = meta_port(ometa);
+    if (tp < (uint32_t)kMaxPorts) {
+      const PortEntry pe = ta.port(tp);
+      if ((pe.flags & kPortTunnel) && t.tunnels && pe.lag < t.n_tunnels) {
+        uint32_t x[kSlotDwords];
+        make_outer(t.tunnels[pe.lag], meta_len(ometa) - kEncapBytes, toeplitz_scalar(st.key, t.rss_key), x);
+        sink.xhdr(x, src);
+      }
+    }
+  }
   // mirror_and_send (K9): the frame as it leaves, also to the ingress port's mirror port
   if (st.in_flags & kPortMirror) {
     const uint32_t mp = st.in_ext >> 16;
@@ -236,7 +348,9 @@ NFDP_HD void side_stage(const TablesView& t, const TA& ta, const uint32_t* d_in,
       if (first) { first = false; continue; }
       uint32_t push = (st.in_flags & kPortIngressTag) ? 1u : 0u;
       uint32_t tci = push ? (st.in_ext & 0xFFFu) : 0u;
-      if (finish_port(t, ta, m, toeplitz_scalar(st.key, t.rss_key), push != 0, push, tci, p.len) != kOk) continue;
+      uint32_t xh = 0;  // tunnel members are not flooded: remote MACs come from l2_to_tunnel entries
+      if (finish_port(t, ta, m, toeplitz_scalar(st.key, t.rss_key), push != 0, push, tci, p.len, &xh) != kOk || xh)
+        continue;
       uint32_t c[kSlotDwords];
       emit(p, tci, push != 0, c);
       sink.rep(c, make_meta(m, p.len + (push ? 4u : 0u), kOk), src);

@@ -247,11 +247,11 @@ __global__ __launch_bounds__(kRingBlock) void ring_kernel(RingArgs a) {
     }
     NFDP_RING_MARK(tr2)
     const EgressDecision e = chain_stage(a.t, ta, p, st, hit, act, acl_rule, hash);
-    const uint32_t olen = e.reason ? 0u : p.len + (e.push ? 4u : 0u);
+    const uint32_t olen = egress_len(p, e);
     uint32_t o[kSlotDwords];
     emit(p, e.tci, e.push != 0, o);
     wave_frames_store<kSysAux>(kx, o, r_out, run);
-    __builtin_amdgcn_raw_buffer_store_b32(make_meta(e.out_port, olen, e.reason, false, !e.reason && e.flood), r_meta, i * 4u, 0, kSysAux);
+    __builtin_amdgcn_raw_buffer_store_b32(make_meta(e.out_port, olen, e.reason, !e.reason && e.xhdr, !e.reason && e.flood), r_meta, i * 4u, 0, kSysAux);
     NFDP_RING_MARK(tr3)
 
     // ---- completion: the chunk's write-through stores are done before its flag is written ----

@@ -184,18 +184,18 @@ __global__ __launch_bounds__(kBlock) void apply_kernel(ApplyArgs a) {
     if (valid) {
       uint32_t o[kSlotDwords];
       emit(p, e.tci, e.push != 0, o);
-      const uint32_t olen = e.reason ? 0u : p.len + (e.push ? 4u : 0u);
+      const uint32_t olen = egress_len(p, e);
       uint32_t reason = e.reason;
       if (remote && pos >= a.g.cap_pkt) reason = kOverflow;
       uint4* dst;
       if (remote && reason == kOk) {
         uint8_t* segp = a.send_pkt + eg * pseg;
         dst = reinterpret_cast<uint4*>(segp + 64 + (size_t)pos * 64);
-        reinterpret_cast<uint32_t*>(segp + pkt_meta_off(a.g.cap_pkt))[pos] = make_meta(e.out_port, olen, kOk);
+        reinterpret_cast<uint32_t*>(segp + pkt_meta_off(a.g.cap_pkt))[pos] = make_meta(e.out_port, olen, kOk, e.xhdr != 0);
         a.out_meta[i] = make_meta(e.out_port, olen, kRemote);
       } else {
         dst = a.out + (size_t)i * 4;
-        a.out_meta[i] = make_meta(reason == kOverflow ? kPortNone : e.out_port, reason ? 0u : olen, reason, false, !reason && e.flood);
+        a.out_meta[i] = make_meta(reason == kOverflow ? kPortNone : e.out_port, reason == e.reason ? olen : 0u, reason, !reason && e.xhdr, !reason && e.flood);
       }
 #pragma unroll
       for (int q = 0; q < 4; ++q) dst[q] = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);

@@ -90,7 +90,7 @@ void apply_cpu(const ApplyArgs& a) {
     const bool remote = !e.reason && eg != a.g.rank && eg < a.g.nranks;
     uint32_t o[kSlotDwords];
     emit(p, e.tci, e.push != 0, o);
-    const uint32_t olen = e.reason ? 0u : p.len + (e.push ? 4u : 0u);
+    const uint32_t olen = egress_len(p, e);
     uint32_t reason = e.reason;
     uint32_t pos = 0;
     if (remote) {
@@ -100,12 +100,12 @@ void apply_cpu(const ApplyArgs& a) {
     if (remote && reason == kOk) {
       uint8_t* segp = a.send_pkt + eg * pseg;
       std::memcpy(segp + 64 + (size_t)pos * 64, o, 64);
-      const uint32_t m = make_meta(e.out_port, olen, kOk);
+      const uint32_t m = make_meta(e.out_port, olen, kOk, e.xhdr != 0);
       std::memcpy(segp + pkt_meta_off(a.g.cap_pkt) + 4 * (size_t)pos, &m, 4);
       a.out_meta[i] = make_meta(e.out_port, olen, kRemote);
     } else {
       std::memcpy(reinterpret_cast<uint8_t*>(a.out) + (size_t)i * 64, o, 64);
-      a.out_meta[i] = make_meta(reason == kOverflow ? kPortNone : e.out_port, reason ? 0u : olen, reason, false, !reason && e.flood);
+      a.out_meta[i] = make_meta(reason == kOverflow ? kPortNone : e.out_port, reason == e.reason ? olen : 0u, reason, !reason && e.xhdr, !reason && e.flood);
     }
     if (st.in_port < (uint32_t)kMaxPorts) a.port_ctr[2 * st.in_port] += ctr_inc(st.wire_len);
     if (reason) a.drop_ctr[reason & (kNumReasons - 1)] += 1;

@@ -65,6 +65,11 @@ class DataPlane:
         self.macs = T.MacTable(mac_slots)
         self.lag = T.LagTable()
         self.flood = T.FloodTable()
+        self.routes = T.RouteTable()
+        self.nexthops = T.NextHopTable()
+        self.ecmp = T.EcmpTable()
+        self.tunnels = T.TunnelTable()
+        self.terms = T.TermTable()
         self.acl = T.AclTable()
         self.flows = T.FlowTable(flow_buckets, rss_key)
         self.rss_key = rss_key
@@ -151,11 +156,19 @@ class DataPlane:
         if self._learned_on_device and (full or self._versions.get("macs") != self.macs.version):
             self.pull_learned()  # the host re-uploads the MAC table: keep what the GPU learned
         for name, model in (("ports", self.ports), ("chains", self.chains), ("macs", self.macs), ("lag", self.lag),
-                            ("flood", self.flood)):
+                            ("flood", self.flood), ("nexthops", self.nexthops), ("ecmp", self.ecmp),
+                            ("tunnels", self.tunnels), ("terms", self.terms)):
             if full or self._versions.get(name) != model.version or name not in self._dev:
                 self._buf(name, model.a)
                 self._versions[name] = model.version
                 sent[name] = model.a.nbytes
+        if len(self.routes) and (full or self._versions.get("routes") != self.routes.version or "lpm24" not in self._dev):
+            t24, t8 = self.routes.build()   # DIR-24-8: 64 MB tbl24 + tbl8 groups
+            self._buf("lpm24", t24)
+            self._buf("lpm8", t8)
+            self._n_lpm8 = len(t8) // 256
+            self._versions["routes"] = self.routes.version
+            sent["routes"] = len(self.routes)
         if full or "rss_key" not in self._dev:
             key = np.frombuffer(self.rss_key, np.uint8)
             self._buf("rss_key", key)
@@ -214,16 +227,24 @@ class DataPlane:
             "acl_default_permit": 1 if self.acl.default_permit else 0,
             "lag_members": self._ptr("lag"), "n_lag_groups": int(self.lag.n),
             "flood": self._ptr("flood") if self.flood.n else 0, "n_flood": int(self.flood.n),
+            "lpm24": self._ptr("lpm24") if len(self.routes) else 0, "lpm8": self._ptr("lpm8") if len(self.routes) else 0,
+            "n_lpm8": int(getattr(self, "_n_lpm8", 0)),
+            "nexthops": self._ptr("nexthops"), "n_nexthops": int(self.nexthops.n),
+            "ecmp": self._ptr("ecmp"), "n_ecmp": int(self.ecmp.n),
+            "tunnels": self._ptr("tunnels") if self.tunnels.n else 0, "n_tunnels": int(self.tunnels.n),
+            "terms": self._ptr("terms") if self.terms.n else 0, "term_mask": int(self.terms.mask),
         }
 
     # ------------------------------------------------------------------ side outputs / learning
-    SIDE_FLAGS = T.PORT_LEARN | T.PORT_ARP_TRAP | T.PORT_MIRROR
+    SIDE_FLAGS = T.PORT_LEARN | T.PORT_ARP_TRAP | T.PORT_MIRROR | T.PORT_TUNNEL
 
     def side_active(self) -> bool:
         """Replicas / learn events can occur: a flood group or a learning / ARP-trap / mirror port."""
         return self.flood.n > 0 or bool(np.any(self.ports.a["flags"] & np.uint32(self.SIDE_FLAGS)))
 
-    def _side_buffers(self) -> dict:
+    def _side_buffers(self, n: int = 0) -> dict:
+        if self.tunnels.n and (self._dev.get("side_xhdr") is None or len(self._dev["side_xhdr"]) < n * 16):
+            self._zeros("side_xhdr", max(n, 1024) * 16, np.uint32)   # outer-header record per packet
         if "side_cnt" not in self._dev:
             self._zeros("side_hdr", self.cap_rep * 16, np.uint32)
             self._zeros("side_meta", self.cap_rep, np.uint32)
@@ -234,7 +255,8 @@ class DataPlane:
         self._dev["side_cnt"][:] = 0
         return {"rep_hdr": self._ptr("side_hdr"), "rep_meta": self._ptr("side_meta"), "rep_src": self._ptr("side_src"),
                 "cap_rep": self.cap_rep, "learn": self._ptr("side_learn"), "cap_learn": self.cap_learn,
-                "cnt": self._ptr("side_cnt"), "list": self._ptr("side_list"), "cap_list": self.cap_rep}
+                "cnt": self._ptr("side_cnt"), "list": self._ptr("side_list"), "cap_list": self.cap_rep,
+                "xhdr": self._ptr("side_xhdr") if self.tunnels.n else 0}
 
     def _apply_learn(self, stream=None) -> None:
         """Apply this batch's learn events to the device MAC table (GPU: mac_learn_kernel on the
@@ -263,7 +285,8 @@ class DataPlane:
         return {"n_rep": n, "rep_hdr": g("side_hdr").reshape(-1, 64 // 4)[:n].view(np.uint8).reshape(n, 64).copy(),
                 "rep_meta": g("side_meta")[:n].copy(), "rep_src": g("side_src")[:n].copy(),
                 "n_learn": int(c[1]), "rep_dropped": int(c[2]), "learn_dropped": int(c[3]),
-                "learn_unplaced": int(c[4]), "n_side": int(c[5]), "side_dropped": int(c[6])}
+                "learn_unplaced": int(c[4]), "n_side": int(c[5]), "side_dropped": int(c[6]),
+                "xhdr": g("side_xhdr").reshape(-1, 16).view(np.uint8).reshape(-1, 64) if self.tunnels.n else None}
 
     def pull_learned(self) -> int:
         """Fold the entries the data plane learned into the host MAC model."""
@@ -325,7 +348,7 @@ class DataPlane:
                 self.nf.launch_stamp(self._ptr("t0"), s)
             if not self.count_flows:
                 flags |= 4  # the kernel always gets the counter table; bit 2 makes it add 0
-            side = self._side_buffers() if self.side_active() else None
+            side = self._side_buffers(n) if self.side_active() else None
             # one launch covers < 2^25 slots (32-bit buffer views); bigger batches are split
             for lo in range(0, n, self.MAX_LAUNCH):
                 m = min(self.MAX_LAUNCH, n - lo)
@@ -346,7 +369,7 @@ class DataPlane:
         im = np.ascontiguousarray(inmeta, np.uint32)
         hashes = np.zeros(n, np.uint32)
         acl = np.zeros(n, np.int32)
-        side = self._side_buffers() if self.side_active() else None
+        side = self._side_buffers(n) if self.side_active() else None
         self.nf.oracle_run(tp, pk.ctypes.data, im.ctypes.data, n, out.ctypes.data, meta.ctypes.data,
                            self._ptr("flow_ctr"), self._ptr("port_ctr"), self._ptr("drop_ctr"),
                            hashes.ctypes.data, acl.ctypes.data, side)

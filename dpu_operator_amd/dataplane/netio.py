@@ -14,7 +14,10 @@ what the pod sends arrives on that fd and what the VSP writes to it is what the 
     -> every forwarded frame: ohdr[:hl] ++ frame[to:len] (nfdp.h out_tail) written to the egress
        port's fd; flood / mirror replicas the same way from the side outputs; ARP copies trapped to
        the slow path go to `on_punt`; frames for ports without a netdev (the uplink when none is
-       attached) are counted as `no_netdev`.
+       attached) are counted as `no_netdev`;
+    -> tunnel ports: the side pass's 50-B outer header is prepended and the frame leaves on the
+       tunnel's underlay port; terminated tunnel traffic (reason `recirc`) is re-injected, inner
+       frame only, as received on the tunnel port, in the next cycle (P4 do_recirculate).
 
 Frames are whole Ethernet frames without FCS (TAP, IFF_NO_PI).  MAC learning, flooding, VLAN
 tags, SNAT etc. are the pipeline's; this loop only moves bytes.
@@ -95,6 +98,8 @@ class LivePath:
         self._t: threading.Thread | None = None
         self._lock = threading.Lock()     # port map changes vs the loop
         self.error: BaseException | None = None
+        self._recirc: list[tuple[bytes, int]] = []
+        self.stats["recirc"] = 0
 
     # ------------------------------------------------------------------ port map
     def add_port(self, idx: int, port) -> None:
@@ -118,6 +123,10 @@ class LivePath:
             p.register(port.fd, select.POLLIN)
             fd2port[port.fd] = (idx, port)
         frames, src = [], []
+        if self._recirc:  # decapsulated frames re-enter first, without waiting
+            frames, src = [f for f, _ in self._recirc], [q for _, q in self._recirc]
+            self._recirc = []
+            timeout = 0
         for fd, _ev in p.poll(int(timeout * 1000)):
             idx, port = fd2port[fd]
             while len(frames) < self.burst:
@@ -130,6 +139,9 @@ class LivePath:
         return frames, src
 
     def _send(self, port_idx: int, frame: bytes) -> None:
+        a = self.dp.ports.a
+        if 0 <= port_idx < len(a) and a[port_idx]["flags"] & (1 << 14):  # tunnel port: its underlay
+            port_idx = int(self.dp.tunnels.a[int(a[port_idx]["lag"])]["out_port"])
         port = self.ports.get(port_idx)
         if port is None:
             self.stats["no_netdev"] += 1
@@ -159,12 +171,18 @@ class LivePath:
         side = self.dp.side_result() if self.dp.side_active() else {"n_rep": 0}
         self.stats["rx"] += n
         self.stats["batches"] += 1
-        port, _, reason = P.meta_fields(meta)
+        port, olen, reason = P.meta_fields(meta)
+        xh = side.get("xhdr")
         for i in range(n):
+            if reason[i] == 13:  # tunnel terminated: the inner frame re-enters on the tunnel port
+                self._recirc.append((frames[i][int(lens[i]) - int(olen[i]):], int(port[i])))
+                self.stats["recirc"] += 1
+                continue
             if reason[i]:
                 self.stats["drop"] += 1
                 continue
-            self._send(int(port[i]), P.assemble(out[i], int(meta[i]), np.frombuffer(frames[i], np.uint8), int(lens[i])))
+            rec = xh[i] if (xh is not None and P.meta_xhdr(meta[i:i + 1])[0]) else None
+            self._send(int(port[i]), P.assemble(out[i], int(meta[i]), np.frombuffer(frames[i], np.uint8), int(lens[i]), rec))
         for k in range(side.get("n_rep", 0)):
             s = int(side["rep_src"][k])
             m = int(side["rep_meta"][k])

@@ -41,20 +41,23 @@ PORT_LAG = 1 << 9           # egress picks member lag_members[lag][hash & 7] (P4
 PORT_VSI_LOOKUP = 1 << 10   # L2 lookup on (bridge, 00:VSI:00:00:00:00), VSI = dst MAC byte 1 (P4 vsi_to_vsi_loopback)
 PORT_LEARN = 1 << 11        # (bridge, src MAC) -> port learned from this port's frames (OvS NORMAL)
 PORT_ARP_TRAP = 1 << 12     # ARP frames from this port are also copied to the slow path (always_trap_arp_table)
+PORT_ROUTED = 1 << 13       # router interface: IPv4 to the port's own MAC is routed (LPM) on a flow miss
+PORT_TUNNEL = 1 << 14       # tunnel port: egress = VXLAN / GENEVE encap with tunnels[lag]
+PORT_VTEP = 1 << 15         # underlay port: VXLAN / GENEVE to ext (local VTEP IPv4, raw) is terminated
 LAG_WAYS = 8
 
 # hop opcodes (nfdp.h Hop)
-HOP_NONE, HOP_ACL, HOP_NAT, HOP_L2FWD, HOP_TTL, HOP_HAIRPIN, HOP_VLAN, HOP_DROP, HOP_PUNT = range(9)
+HOP_NONE, HOP_ACL, HOP_NAT, HOP_L2FWD, HOP_TTL, HOP_HAIRPIN, HOP_VLAN, HOP_DROP, HOP_PUNT, HOP_ROUTE = range(10)
 HOP_NAMES = {
     "acl": HOP_ACL, "nat": HOP_NAT, "l2fwd": HOP_L2FWD, "ttl": HOP_TTL, "hairpin": HOP_HAIRPIN,
-    "vlan": HOP_VLAN, "drop": HOP_DROP, "punt": HOP_PUNT,
+    "vlan": HOP_VLAN, "drop": HOP_DROP, "punt": HOP_PUNT, "route": HOP_ROUTE,
 }
 
 # reasons (nfdp.h Reason)
 REASONS = {
     0: "ok", 1: "bad_port", 2: "vlan_drop", 3: "spoof", 4: "acl_deny", 5: "no_route",
     6: "too_big", 7: "chain_drop", 8: "ttl_expired", 9: "malformed", 10: "remote", 11: "overflow",
-    12: "arp_trap",
+    12: "arp_trap", 13: "recirc",
 }
 
 PORT_DTYPE = np.dtype(
@@ -70,6 +73,17 @@ MAC_DTYPE = np.dtype(
     [("mac_lo", "<u4"), ("mac_hi", "<u2"), ("bridge_id", "<u2"), ("out_port", "<u2"), ("valid", "<u2"), ("stamp", "<u4")]
 )
 MAC_EMPTY, MAC_STATIC, MAC_TOMB, MAC_LEARNED = 0, 1, 2, 3   # nfdp.h MacValid
+NH_DTYPE = np.dtype([("dmac_lo", "<u4"), ("dmac_hi", "<u2"), ("port", "<u2"), ("smac_lo", "<u4"), ("smac_hi", "<u2"),
+                     ("valid", "<u2")])
+TUNNEL_DTYPE = np.dtype([("src_ip", "<u4"), ("dst_ip", "<u4"), ("sport", "<u2"), ("dport", "<u2"), ("vni", "<u4"),
+                         ("smac_lo", "<u4"), ("smac_hi", "<u2"), ("out_port", "<u2"), ("dmac_lo", "<u4"),
+                         ("dmac_hi", "<u2"), ("type", "<u2")])
+TERM_DTYPE = np.dtype([("src_ip", "<u4"), ("vni", "<u4"), ("port", "<u2"), ("valid", "<u2"), ("pad", "<u4")])
+assert NH_DTYPE.itemsize == 16 and TUNNEL_DTYPE.itemsize == 32 and TERM_DTYPE.itemsize == 16
+TUN_VXLAN, TUN_GENEVE = 1, 2
+VXLAN_PORT, GENEVE_PORT = 4789, 6081
+LPM_EXT, ROUTE_NH, ROUTE_ECMP = 1 << 31, 1 << 30, 2 << 30
+ECMP_WAYS = 8
 assert PORT_DTYPE.itemsize == 32 and CHAIN_DTYPE.itemsize == 16 and MAC_DTYPE.itemsize == 16
 
 # Microsoft RSS verification key (40 B) — standard Toeplitz key.
@@ -212,6 +226,160 @@ class PortTable:
 
     def mirror_port(self, idx: int) -> int | None:
         return int(self.a[idx]["ext"]) >> 16 if self.a[idx]["flags"] & PORT_MIRROR else None
+
+
+class RouteTable:
+    """IPv4 routes (P4 ipv4_table, LPM) -> nexthop id or ECMP group, compiled to the DIR-24-8 arrays
+    the kernels read (nfdp.h lpm_lookup): tbl24 (2^24 x u32, 64 MB of HBM) + 256-entry tbl8
+    groups for prefixes longer than /24."""
+
+    def __init__(self):
+        self.routes: dict[tuple[int, int], int] = {}
+        self.version = 0
+
+    @staticmethod
+    def _net(cidr) -> tuple[int, int]:
+        n = ipaddress.IPv4Network(cidr, strict=False)
+        return int(n.network_address), n.prefixlen
+
+    def add(self, cidr, nexthop: int | None = None, ecmp_group: int | None = None) -> None:
+        if (nexthop is None) == (ecmp_group is None):
+            raise ValueError("a route points at exactly one of nexthop / ecmp_group")
+        res = (ROUTE_NH | nexthop) if nexthop is not None else (ROUTE_ECMP | ecmp_group)
+        if (nexthop or ecmp_group or 0) > 0xFFFF:
+            raise ValueError("nexthop / group id must fit 16 bits")
+        self.routes[self._net(cidr)] = res
+        self.version += 1
+
+    def remove(self, cidr) -> bool:
+        ok = self.routes.pop(self._net(cidr), None) is not None
+        self.version += ok
+        return ok
+
+    def __len__(self) -> int:
+        return len(self.routes)
+
+    def lookup(self, ip) -> int:
+        """Reference LPM (longest prefix wins), for tests: the route result or 0."""
+        x = int(ipaddress.IPv4Address(ip)) if not isinstance(ip, (int, np.integer)) else int(ip)
+        best, res = -1, 0
+        for (net, plen), r in self.routes.items():
+            m = 0 if plen == 0 else (0xFFFFFFFF << (32 - plen)) & 0xFFFFFFFF
+            if (x & m) == net and plen > best:
+                best, res = plen, r
+        return res
+
+    def build(self) -> tuple[np.ndarray, np.ndarray]:
+        t24 = np.zeros(1 << 24, np.uint32)
+        t8: list[np.ndarray] = []
+        for (net, plen), res in sorted(self.routes.items(), key=lambda kv: kv[0][1]):
+            if plen <= 24:  # ascending prefix length: longer prefixes overwrite shorter ones
+                lo = net >> 8
+                t24[lo:lo + (1 << (24 - plen))] = res
+            else:
+                i = net >> 8
+                if not t24[i] & LPM_EXT:
+                    t8.append(np.full(256, t24[i], np.uint32))
+                    t24[i] = LPM_EXT | (len(t8) - 1)
+                g = int(t24[i] & ~np.uint32(LPM_EXT))
+                lo = net & 0xFF
+                t8[g][lo:lo + (1 << (32 - plen))] = res
+        tbl8 = np.concatenate(t8) if t8 else np.zeros(256, np.uint32)
+        return t24, tbl8
+
+
+class NextHopTable:
+    """nexthop_table + rif_mod_table: id -> (egress port, neighbour MAC, router-interface MAC)."""
+
+    def __init__(self, capacity: int = 4096):
+        self.a = np.zeros(capacity, NH_DTYPE)
+        self.n = 0
+        self.version = 0
+
+    def set(self, nh: int, port: int, dmac, smac) -> None:
+        if not 0 <= nh < len(self.a):
+            raise ValueError("nexthop id out of range")
+        dlo, dhi = mac_raw(dmac)
+        slo, shi = mac_raw(smac)
+        self.a[nh] = (dlo, dhi, port, slo, shi, 1)
+        self.n = max(self.n, nh + 1)
+        self.version += 1
+
+    def clear(self, nh: int) -> None:
+        self.a[nh] = np.zeros((), NH_DTYPE)
+        self.version += 1
+
+
+class EcmpTable:
+    """ECMP groups (ecmp_hash_table): ECMP_WAYS nexthop ids per group, member = hash[2:0]."""
+
+    def __init__(self, groups: int = 1024):
+        self.a = np.zeros(groups * ECMP_WAYS, np.uint16)
+        self.n = 0
+        self.version = 0
+
+    def set_group(self, g: int, nexthops: list[int]) -> None:
+        if not nexthops:
+            raise ValueError("an ECMP group needs members")
+        self.a[g * ECMP_WAYS:(g + 1) * ECMP_WAYS] = [nexthops[i % len(nexthops)] for i in range(ECMP_WAYS)]
+        self.n = max(self.n, g + 1)
+        self.version += 1
+
+    def set_slot(self, g: int, h: int, nh: int) -> None:
+        self.a[g * ECMP_WAYS + (h & (ECMP_WAYS - 1))] = nh
+        self.n = max(self.n, g + 1)
+        self.version += 1
+
+
+class TunnelTable:
+    """VXLAN / GENEVE tunnels (vxlan_encap_mod_table / geneve_encap_mod_table + l2_to_tunnel_v4):
+    the outer headers of a tunnel port.  Addresses host-order ints / dotted strings in."""
+
+    def __init__(self, capacity: int = 1024):
+        self.a = np.zeros(capacity, TUNNEL_DTYPE)
+        self.n = 0
+        self.version = 0
+
+    def set(self, idx: int, *, src, dst, vni: int, out_port: int, smac, dmac, kind: int = TUN_VXLAN,
+            dport: int | None = None, sport: int = 0) -> None:
+        dport = dport or (VXLAN_PORT if kind == TUN_VXLAN else GENEVE_PORT)
+        slo, shi = mac_raw(smac)
+        dlo, dhi = mac_raw(dmac)
+        self.a[idx] = (int(ip_raw(np.uint32(ip_to_int(src)))), int(ip_raw(np.uint32(ip_to_int(dst)))),
+                       int(port_raw(np.uint32(sport))) if sport else 0, int(port_raw(np.uint32(dport))),
+                       vni & 0xFFFFFF, slo, shi, out_port, dlo, dhi, kind)
+        self.n = max(self.n, idx + 1)
+        self.version += 1
+
+    def bytes_of(self, idx: int) -> bytes:
+        return self.a[idx].tobytes()
+
+
+class TermTable:
+    """Tunnel termination (ipv4_tunnel_term_table + rx_ipv4_tunnel_source_port):
+    (outer source IPv4, VNI) -> the tunnel port the inner frame re-enters on."""
+
+    def __init__(self, slots: int = 1024):
+        if slots & (slots - 1):
+            raise ValueError("term table size must be a power of two")
+        self.a = np.zeros(slots, TERM_DTYPE)
+        self.mask = slots - 1
+        self.n = 0
+        self.version = 0
+
+    def insert(self, src, vni: int, port: int) -> None:
+        raw = int(ip_raw(np.uint32(ip_to_int(src))))
+        with np.errstate(over="ignore"):
+            h = int(fmix32(np.uint32(raw) ^ (np.uint32(vni) * np.uint32(0x9E3779B1))))
+        for q in range(8):
+            i = (h + q) & self.mask
+            was = bool(self.a[i]["valid"])
+            if not was or (self.a[i]["src_ip"] == raw and self.a[i]["vni"] == vni):
+                self.a[i] = (raw, vni, port, 1, 0)
+                self.n += 0 if was else 1
+                self.version += 1
+                return
+        raise RuntimeError("term table probe limit reached")
 
 
 class FloodTable:

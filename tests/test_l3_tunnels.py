@@ -1,0 +1,236 @@
+"""L3 routing (P4 ipv4_table LPM, nexthop_table, ecmp_hash_table, rif_mod_table) and VXLAN /
+GENEVE tunnels (encap on tunnel ports, termination + recirculation) on the data plane.
+
+Expectations are computed independently: a Python longest-prefix match over the route set,
+field-by-field frame models, full IPv4 / UDP checksum verification of the assembled frames.
+The GPU tests hold the HIP kernels to the oracle bit for bit (outer-header records included)."""
+import ipaddress
+
+import numpy as np
+import pytest
+
+from dpu_operator_amd.dataplane import tables as T
+from dpu_operator_amd.dataplane.engine import DataPlane
+from dpu_operator_amd.ops import packets as P
+
+RMAC = ["02:40:00:00:00:0a", "02:40:00:00:00:0b", "02:40:00:00:00:0c", "02:40:00:00:00:0d"]
+NBR = ["02:50:00:00:00:0a", "02:50:00:00:00:0b", "02:50:00:00:00:0c", "02:50:00:00:00:0d"]
+
+
+def _router(device):
+    dp = DataPlane(device=device, flow_buckets=1 << 10)
+    for i in range(4):
+        dp.ports.set(10 + i, flags=T.PORT_VALID | T.PORT_ROUTED, mac=RMAC[i], bridge_id=20 + i)
+        dp.nexthops.set(i + 1, 10 + i, dmac=NBR[i], smac=RMAC[i])
+    dp.ecmp.set_group(0, [2, 3])
+    dp.routes.add("10.1.0.0/16", nexthop=2)
+    dp.routes.add("10.1.2.0/24", nexthop=3)
+    dp.routes.add("10.1.2.128/25", ecmp_group=0)
+    dp.routes.add("10.1.2.200/32", nexthop=4)
+    dp.routes.add("0.0.0.0/0", nexthop=1)
+    dp.commit(full=True)
+    return dp
+
+
+def _l3_trace(n=512, seed=0):
+    rng = np.random.default_rng(seed)
+    pool = ["10.1.9.9", "10.1.2.5", "10.1.2.129", "10.1.2.250", "10.1.2.200", "8.8.8.8", "10.2.0.1"]
+    dsts = np.array([int(ipaddress.IPv4Address(pool[i])) for i in rng.integers(0, len(pool), n)], np.uint32)
+    ttl = np.where(rng.random(n) < 0.05, 1, 64)
+    frames, lens = [], []
+    for sz in (64, 1500):
+        idx = np.arange(n)[(np.arange(n) % 2) == (sz == 1500)]
+        fr, ln = P.craft_full(len(idx), dmac=RMAC[0], smac=NBR[0], src_ip=0x0A090001, dst_ip=dsts[idx],
+                              sport=rng.integers(1024, 65535, len(idx)), dport=80, proto=17, frame_len=sz - 4)
+        frames.append((idx, fr, ln))
+    full = np.zeros((n, 1500), np.uint8)
+    lens = np.zeros(n, np.uint32)
+    for idx, fr, ln in frames:
+        full[idx, : fr.shape[1]] = fr[:, :1500]
+        lens[idx] = ln
+    full[ttl == 1, 22] = 1
+    # TTL change needs the IPv4 checksum redone for those
+    for i in np.where(ttl == 1)[0]:
+        full[i, 24:26] = 0
+        w = (full[i, 14:34:2].astype(np.uint32) << 8) | full[i, 15:34:2]
+        c = int(w.sum())
+        c = (c & 0xFFFF) + (c >> 16)
+        c = (c & 0xFFFF) + (c >> 16)
+        full[i, 24], full[i, 25] = (~c >> 8) & 0xFF, ~c & 0xFF
+    return P.header_slots(full, lens), P.inmeta(np.full(n, 10), lens), full, lens, dsts, ttl
+
+
+def test_routing_oracle_model():
+    dp = _router("cpu")
+    slots, im, frames, lens, dsts, ttl = _l3_trace()
+    r = dp.run(slots, im)
+    port, olen, reason = P.meta_fields(r.meta)
+    h = r.extra["hash"]
+    for i in range(len(dsts)):
+        res = dp.routes.lookup(int(dsts[i]))
+        if ttl[i] == 1:
+            assert reason[i] == 8  # ttl_expired
+            continue
+        nh = res & 0xFFFF if res & T.ROUTE_NH else int(dp.ecmp.a[(res & 0xFFFF) * 8 + (int(h[i]) & 7)])
+        assert (reason[i], port[i]) == (0, 9 + nh), (i, hex(res))
+        o = P.assemble(r.out[i], int(r.meta[i]), frames[i], int(lens[i]))
+        assert o[0:6] == bytes.fromhex(NBR[nh - 1].replace(":", "")) and o[6:12] == bytes.fromhex(RMAC[nh - 1].replace(":", ""))
+        assert o[22] == 63 and len(o) == lens[i]
+        assert P.check_csums(np.frombuffer(o, np.uint8)[None], np.array([len(o)]))[0]
+    ecmp_nh = {int(dp.ecmp.a[(int(h[i]) & 7)]) for i in range(len(dsts))
+               if ttl[i] != 1 and dp.routes.lookup(int(dsts[i])) & T.ROUTE_ECMP}
+    assert ecmp_nh == {2, 3}  # both ECMP members used
+
+
+def test_route_hop_in_a_chain_and_no_route():
+    dp = DataPlane(device="cpu", flow_buckets=1 << 10)
+    dp.ports.set(1, flags=T.PORT_VALID, mac="02:00:00:00:00:01")
+    dp.ports.set(2, flags=T.PORT_VALID, mac="02:00:00:00:00:02")
+    dp.nexthops.set(0, 2, dmac=NBR[1], smac=RMAC[1])
+    dp.routes.add("192.0.2.0/24", nexthop=0)
+    cid = dp.chains.add(["nat", "route"])
+    keys = T.flow_key([0x0A000001, 0x0A000001], [0xC0000205, 0xC6336405], [5, 5], [7, 7], 17, 0)
+    dp.flows.insert_many(keys, np.repeat(T.flow_action(chain_id=cid, out_port=1, nat_ip=0xC6336401, nat_port=999), 2, axis=0))
+    dp.commit(full=True)
+    fr, ln = P.craft(2, dmac="02:00:00:00:00:01", smac="02:00:00:00:00:99", src_ip=0x0A000001,
+                     dst_ip=np.array([0xC0000205, 0xC6336405], np.uint32), sport=5, dport=7)
+    r = dp.run(fr, P.inmeta(np.array([1, 1]), ln))
+    port, _, reason = P.meta_fields(r.meta)
+    assert (int(port[0]), int(reason[0])) == (2, 0)                 # SNAT then routed
+    assert (int(port[1]), int(reason[1])) == (T.PORT_PUNT, 5)       # no route -> slow path
+    assert bytes(r.out[0][26:30]) == bytes([198, 51, 100, 1]) and r.out[0][22] == 63
+
+
+LOCAL_VTEP, REMOTE_VTEP = "192.0.2.1", "192.0.2.2"
+POD_MAC, REMOTE_MAC = "02:00:00:00:aa:01", "02:00:00:00:bb:01"
+
+
+def _overlay(device, kind=T.TUN_VXLAN):
+    """Pod port 1 on bridge 3; tunnel port 20 -> underlay port 30 (VTEP 192.0.2.1); remote MAC behind
+    the tunnel (l2_to_tunnel_v4); (192.0.2.2, vni 5000) terminates onto port 20."""
+    dp = DataPlane(device=device, flow_buckets=1 << 10)
+    dp.ports.set(1, flags=T.PORT_VALID, bridge_id=3, mac=POD_MAC)
+    dp.ports.set(20, flags=T.PORT_VALID | T.PORT_TUNNEL, bridge_id=3)
+    dp.ports.set_lag(20, None)
+    dp.ports.a[20]["lag"] = 0
+    dp.ports.a[20]["flags"] |= T.PORT_TUNNEL
+    dp.ports.set(30, flags=T.PORT_VALID | T.PORT_VTEP, mac="02:00:00:00:0e:01")
+    dp.ports.a[30]["ext"] = int(P.ip_raw(np.uint32(int(ipaddress.IPv4Address(LOCAL_VTEP)))))
+    dp.tunnels.set(0, src=LOCAL_VTEP, dst=REMOTE_VTEP, vni=5000, out_port=30, smac="02:00:00:00:0e:01",
+                   dmac="02:00:00:00:0e:02", kind=kind)
+    dp.terms.insert(REMOTE_VTEP, 5000, 20)
+    dp.macs.insert(3, REMOTE_MAC, 20)
+    dp.macs.insert(3, POD_MAC, 1)
+    dp.ports.version += 1
+    dp.commit(full=True)
+    return dp
+
+
+def _encap_trace():
+    frames, lens = [], []
+    for sz in (64, 700, 1400):
+        f, ln = P.craft_full(1, dmac=REMOTE_MAC, smac=POD_MAC, src_ip=0x0A000001, dst_ip=0x0A000002, sport=1234,
+                             dport=80, frame_len=sz - 4)
+        frames.append(f[0, : ln[0]])
+        lens.append(int(ln[0]))
+    arena = np.zeros((3, 1500), np.uint8)
+    for i, f in enumerate(frames):
+        arena[i, : len(f)] = f
+    return P.header_slots(arena, np.array(lens)), P.inmeta(np.ones(3), np.array(lens)), arena, np.array(lens, np.uint32)
+
+
+def _check_outer(o: bytes, inner: bytes, kind) -> None:
+    assert o[12:14] == b"\x08\x00" and o[14] == 0x45 and o[23] == 17
+    w = np.frombuffer(o[14:34], ">u2").astype(np.uint32)
+    c = int(w.sum())
+    assert ((c & 0xFFFF) + (c >> 16)) & 0xFFFF == 0xFFFF                         # IPv4 header checksum
+    assert int.from_bytes(o[16:18], "big") == len(o) - 14                        # total length
+    assert o[26:30] == ipaddress.IPv4Address(LOCAL_VTEP).packed and o[30:34] == ipaddress.IPv4Address(REMOTE_VTEP).packed
+    assert int.from_bytes(o[36:38], "big") == (4789 if kind == T.TUN_VXLAN else 6081)
+    assert int.from_bytes(o[34:36], "big") >= 0xC000                             # entropy source port
+    assert int.from_bytes(o[38:40], "big") == len(o) - 34
+    assert o[42] == (0x08 if kind == T.TUN_VXLAN else 0x00) and int.from_bytes(o[46:49], "big") == 5000
+    if kind == T.TUN_GENEVE:
+        assert o[44:46] == b"\x65\x58"
+    assert o[50:] == inner
+
+
+@pytest.mark.parametrize("kind", [T.TUN_VXLAN, T.TUN_GENEVE])
+def test_encap_terminate_recirculate_oracle(kind):
+    dp = _overlay("cpu", kind)
+    slots, im, arena, lens = _encap_trace()
+    r = dp.run(slots, im)
+    side = dp.side_result()
+    port, olen, reason = P.meta_fields(r.meta)
+    assert (port == 20).all() and (reason == 0).all() and (olen == lens + 50).all()
+    assert P.meta_xhdr(r.meta).all()
+    outs = [P.assemble(r.out[i], int(r.meta[i]), arena[i], int(lens[i]), side["xhdr"][i]) for i in range(3)]
+    for i, o in enumerate(outs):
+        _check_outer(o, bytes(arena[i, : lens[i]]), kind)
+    # the reverse direction: the remote VTEP's encapsulation arrives on the underlay port
+    back = []
+    for o in outs:
+        b = bytearray(o)
+        b[26:30], b[30:34] = o[30:34], o[26:30]  # remote -> local
+        inner = bytearray(b[50:])
+        inner[0:6], inner[6:12] = inner[6:12], inner[0:6]  # reply to the pod
+        b[50:] = inner
+        back.append(bytes(b))
+    bl = np.array([len(b) for b in back], np.uint32)
+    barena = np.zeros((3, 1500), np.uint8)
+    for i, b in enumerate(back):
+        barena[i, : len(b)] = np.frombuffer(b, np.uint8)
+    r2 = dp.run(P.header_slots(barena, bl), P.inmeta(np.full(3, 30), bl))
+    p2, l2, rs2 = P.meta_fields(r2.meta)
+    assert (rs2 == 13).all() and (p2 == 20).all() and (l2 == bl - 50).all()   # terminated -> recirculate
+    # recirculation: the inner frame re-enters on the tunnel port and is bridged to the pod
+    inner = np.zeros((3, 1500), np.uint8)
+    for i in range(3):
+        inner[i, : l2[i]] = barena[i, 50: 50 + l2[i]]
+    r3 = dp.run(P.header_slots(inner, l2), P.inmeta(np.full(3, 20), l2))
+    p3, l3, rs3 = P.meta_fields(r3.meta)
+    assert (rs3 == 0).all() and (p3 == 1).all() and (l3 == l2).all()
+    assert dp.drop_counters().get("recirc") == 3
+
+
+def test_unknown_vni_is_not_terminated():
+    dp = _overlay("cpu")
+    slots, im, arena, lens = _encap_trace()
+    r = dp.run(slots, im)
+    o = bytearray(P.assemble(r.out[0], int(r.meta[0]), arena[0], int(lens[0]), dp.side_result()["xhdr"][0]))
+    o[26:30], o[30:34] = o[30:34], o[26:30]
+    o[48] ^= 1  # other VNI
+    fr = np.frombuffer(bytes(o), np.uint8)[None]
+    r2 = dp.run(P.header_slots(fr, np.array([len(o)])), P.inmeta(np.array([30]), np.array([len(o)])))
+    assert P.meta_fields(r2.meta)[2][0] == 5  # no_route (punted), not recirculated
+
+
+@pytest.mark.gpu
+def test_routing_gpu_bit_exact():
+    import torch
+
+    c, g = _router("cpu"), _router("cuda")
+    slots, im, *_ = _l3_trace(4096, seed=3)
+    rc = c.run(slots, im)
+    rg = g.run(torch.from_numpy(slots).cuda(), torch.from_numpy(im.view(np.int32)).cuda())
+    torch.cuda.synchronize()
+    assert np.array_equal(rg.meta.cpu().numpy().view(np.uint32), rc.meta)
+    assert np.array_equal(rg.out.cpu().numpy(), rc.out)
+    assert np.array_equal(g.port_counters(), c.port_counters())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", [T.TUN_VXLAN, T.TUN_GENEVE])
+def test_tunnels_gpu_bit_exact(kind):
+    import torch
+
+    c, g = _overlay("cpu", kind), _overlay("cuda", kind)
+    slots, im, arena, lens = _encap_trace()
+    rc = c.run(slots, im)
+    sc = c.side_result()
+    rg = g.run(torch.from_numpy(slots).cuda(), torch.from_numpy(im.view(np.int32)).cuda())
+    torch.cuda.synchronize()
+    sg = g.side_result()
+    assert np.array_equal(rg.meta.cpu().numpy().view(np.uint32), rc.meta)
+    assert np.array_equal(rg.out.cpu().numpy(), rc.out)
+    assert np.array_equal(sg["xhdr"][:3], sc["xhdr"][:3])
