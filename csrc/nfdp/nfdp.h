@@ -160,10 +160,10 @@ static_assert(sizeof(MacEntry) == 16, "MacEntry");
 
 // ---- L3 (P4 ipv4_table + nexthop_table + ecmp_hash_table + rif_mod_table) ----
 // IPv4 LPM as DIR-24-8: tbl24[dst >> 8] is a result or (kLpmExt | g) = tbl8 group g, whose
-// entry [dst & 0xFF] is the result.  Result: 0 = no route; kind[31:30] 1 = nexthop, 2 = ECMP
-// group; id[15:0].
+// entry [dst & 0xFF] is the result.  Result: 0 = no route; kind[29:28] 1 = nexthop, 2 = ECMP
+// group; id[15:0] (bit 31 stays free for the tbl24 extension flag).
 constexpr uint32_t kLpmExt = 1u << 31;
-constexpr uint32_t kRouteNh = 1u << 30, kRouteEcmp = 2u << 30;
+constexpr uint32_t kRouteNh = 1u << 28, kRouteEcmp = 2u << 28;
 constexpr int kEcmpWays = 8;            // members per ECMP group, selected by hash[2:0]
 struct alignas(16) NextHop {     // 16 B
   uint32_t dmac_lo;              // neighbour MAC (raw bytes 0..3)
@@ -482,8 +482,8 @@ NFDP_HD uint32_t lpm_lookup(const TablesView& t, uint32_t dst /* host order */) 
 // route result -> nexthop id (ECMP by hash[2:0]) or -1
 NFDP_HD int route_nexthop(const TablesView& t, uint32_t r, uint32_t hash) {
   const uint32_t id = r & 0xFFFFu;
-  if ((r & (3u << 30)) == kRouteNh) return id < t.n_nexthops ? (int)id : -1;
-  if ((r & (3u << 30)) == kRouteEcmp && t.ecmp && id < t.n_ecmp) {
+  if ((r & (3u << 28)) == kRouteNh) return id < t.n_nexthops ? (int)id : -1;
+  if ((r & (3u << 28)) == kRouteEcmp && t.ecmp && id < t.n_ecmp) {
     const uint32_t nh = t.ecmp[id * kEcmpWays + (hash & (kEcmpWays - 1))];
     return nh < t.n_nexthops ? (int)nh : -1;
   }

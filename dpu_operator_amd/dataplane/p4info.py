@@ -207,6 +207,32 @@ TABLES = [
      ["bypass", "set_egress_port", "drop"], 1024),
     ("ipv4_lpm_root_lut", [("user_meta.cmeta.bit16_zeros", 16, "TERNARY")], ["ipv4_lpm_root_lut_action"], 1),
     ("mir_prof", [("mirror_prof_key", 8, "EXACT")], ["mir_prof_action"], 256),
+    # L3 (p4info.txt:696-871): LPM routes, nexthops, ECMP, router-interface MACs
+    ("ipv4_table", [("ipv4_table_lpm_root", 32, "EXACT"), ("ipv4_dst_match", 32, "LPM")],
+     ["ipv4_set_nexthop_id", "ecmp_hash_action", "NoAction"], 1024),
+    ("ecmp_hash_table", [("flex", 16, "TERNARY"), ("hash", 3, "TERNARY")], ["set_nexthop_id", "NoAction"], 1024),
+    ("nexthop_table", [("user_meta.cmeta.nexthop_id", 16, "EXACT"), ("bit16_zeros", 8, "EXACT")],
+     ["set_nexthop_info_dmac", "set_nexthop_lag", "drop", "NoAction"], 1024),
+    ("ecmp_nexthop_table", [("user_meta.cmeta.nexthop_id", 16, "TERNARY")], ["ecmp_set_nexthop_info_dmac", "drop"], 1024),
+    ("rif_mod_table_start", [("rif_mod_map_id0", 11, "EXACT")], ["set_src_mac_start", "NoAction"], 1024),
+    ("rif_mod_table_mid", [("rif_mod_map_id1", 11, "EXACT")], ["set_src_mac_mid", "NoAction"], 1024),
+    ("rif_mod_table_last", [("rif_mod_map_id2", 11, "EXACT")], ["set_src_mac_last", "NoAction"], 1024),
+    # tunnels (p4info.txt:258-556, 930-1110)
+    ("l2_to_tunnel_v4", [("hdrs.mac[vmeta.common.depth].da", 48, "EXACT")], ["set_tunnel_v4", "drop", "do_recirculate"], 1024),
+    ("vxlan_encap_mod_table", [("vmeta.common.mod_blob_ptr", 24, "EXACT")], ["vxlan_encap", "NoAction"], 1024),
+    ("vxlan_encap_vlan_pop_mod_table", [("vmeta.common.mod_blob_ptr", 24, "EXACT")], ["vxlan_encap_vlan_pop", "NoAction"], 1024),
+    ("geneve_encap_mod_table", [("vmeta.common.mod_blob_ptr", 24, "EXACT")], ["geneve_encap", "NoAction"], 1024),
+    ("vxlan_decap_mod_table", [("vmeta.common.mod_blob_ptr", 24, "EXACT")], ["vxlan_decap_outer_hdr", "NoAction"], 1024),
+    ("geneve_decap_mod_table", [("vmeta.common.mod_blob_ptr", 24, "EXACT")], ["geneve_decap_outer_hdr", "NoAction"], 1024),
+    ("ipv4_tunnel_term_table", [("ipv4_src", 32, "EXACT"), ("vni", 24, "EXACT")],
+     ["set_vxlan_decap_outer_hdr", "set_geneve_decap_outer_hdr", "trap_enable"], 1024),
+    ("rx_ipv4_tunnel_source_port", [("ipv4_src", 32, "EXACT"), ("vni", 24, "EXACT")], ["set_source_port", "drop"], 1024),
+    # LAG rx, smac learning check, ARP trap (p4info.txt:168, 783, 1011)
+    ("rx_lag_table", [("vmeta.common.port_id", 2, "EXACT"), ("user_meta.cmeta.lag_group_id", 8, "EXACT")],
+     ["fwd_to_vsi", "drop"], 1024),
+    ("l2_fwd_smac_table", [("hdrs.mac[vmeta.common.depth].sa", 48, "EXACT"), ("user_meta.pmeta.bridge_id", 8, "EXACT")],
+     ["NoAction", "fwd_to_cp"], 1024),
+    ("always_trap_arp_table", [("hdrs.inval.data", 16, "EXACT")], ["do_trap_enable"], 1024),
 ]
 ACTIONS = {
     "set_source_port": [("source_port", 16)],
@@ -227,6 +253,28 @@ ACTIONS = {
     # subset of the pipeline's mirror profile parameters (the ones the VSP programs)
     "mir_prof_action": [("port_dest_type", 32), ("vport_id", 32), ("mode", 1), ("dest_id", 16), ("func_valid", 1),
                         ("store_vsi", 1)],
+    "NoAction": [],
+    "ipv4_set_nexthop_id": [("nexthop_id", 16)],
+    "ecmp_hash_action": [("ecmp_group_id", 16)],
+    "set_nexthop_id": [("nexthop_id", 16)],
+    "set_nexthop_info_dmac": [("router_interface_id", 16), ("egress_port", 32), ("dmac_high", 16), ("dmac_low", 32)],
+    "set_nexthop_lag": [("lag_group_id", 8), ("dmac_high", 16), ("dmac_low", 32)],
+    "ecmp_set_nexthop_info_dmac": [("router_interface_id", 16), ("egress_port", 32), ("dmac_high", 16), ("dmac_low", 32)],
+    "set_src_mac_start": [("arg", 16)],
+    "set_src_mac_mid": [("arg", 16)],
+    "set_src_mac_last": [("arg", 16)],
+    "set_tunnel_v4": [("dst_addr", 32)],
+    "do_recirculate": [],
+    "vxlan_encap": [("src_addr", 32), ("dst_addr", 32), ("src_port", 16), ("dst_port", 16), ("vni", 24)],
+    "vxlan_encap_vlan_pop": [("src_addr", 32), ("dst_addr", 32), ("src_port", 16), ("dst_port", 16), ("vni", 24)],
+    "geneve_encap": [("src_addr", 32), ("dst_addr", 32), ("src_port", 16), ("dst_port", 16), ("vni", 24)],
+    "vxlan_decap_outer_hdr": [],
+    "geneve_decap_outer_hdr": [],
+    "set_vxlan_decap_outer_hdr": [("tunnel_id", 20)],
+    "set_geneve_decap_outer_hdr": [("tunnel_id", 20)],
+    "trap_enable": [],
+    "fwd_to_cp": [],
+    "do_trap_enable": [],
 }
 
 

@@ -23,6 +23,7 @@ plane port number == vport.  Physical ports 0..3 are data-plane ports PHY_BASE +
 """
 from __future__ import annotations
 
+import ipaddress
 import re
 import threading
 
@@ -34,6 +35,7 @@ from .p4info import MI355X_P4INFO, P4Info
 
 VSI_TO_VPORT = 16
 PHY_BASE = 4000
+TUNNEL_PORT_BASE = 3800      # data-plane ports of P4 tunnels (encap by destination, decap by tunnel_id)
 STEER_BRIDGE_BASE = 0xF000   # per-port private bridges (bypass / loopback domains)
 
 
@@ -54,6 +56,10 @@ def vsi_of_mac(mac: str | bytes) -> int:
 
 def _int(v: str) -> int:
     v = v.strip()
+    if v.count(".") == 3:                       # dotted IPv4
+        return int(ipaddress.IPv4Address(v))
+    if v.count(":") == 5:                       # MAC
+        return int(v.replace(":", ""), 16)
     return int(v, 16) if v.lower().startswith("0x") else int(v)
 
 
@@ -85,6 +91,9 @@ class P4Runtime:
         self.lag_ports = dict(lag_ports or {})  # LAG group -> data-plane port that fronts it
         self._owned_ports: set[int] = set()
         self._owned_macs: list[tuple[int, str]] = []
+        self._owned_routes: list[str] = []
+        self._owned_nh: set[int] = set()
+        self._owned_tunnels = False
         self._lock = threading.RLock()
         self.stats = {"writes": 0, "compiles": 0}
 
@@ -132,6 +141,12 @@ class P4Runtime:
                 if msk is not None and msk != full:
                     raise P4Error("INVALID_ARGUMENT", f"{mf.name} is an exact match; no mask allowed")
                 msk = full
+            elif mf.match_type == "LPM":       # value/prefix-length
+                plen = mf.bitwidth if msk is None else msk
+                if not 0 <= plen <= mf.bitwidth:
+                    raise P4Error("INVALID_ARGUMENT", f"prefix length of {mf.name} out of range")
+                msk = (full << (mf.bitwidth - plen)) & full
+                v &= msk
             else:
                 ternary = True
                 msk = full if msk is None else msk
@@ -363,8 +378,147 @@ class P4Runtime:
                 dp.ports.set_lag(p, grp)
             else:
                 dp.ports.set_lag(p, None)
+        self._compile_l3_tunnels(dp, port, add_mac, src)
         self._owned_ports = owned
         dp.ports.version += 1
+
+    def _compile_l3_tunnels(self, dp, port, add_mac, src: dict) -> None:
+        """L3 (ipv4_table, ecmp_hash_table, nexthop / ecmp_nexthop tables, rif_mod_table_*), tunnels
+        (l2_to_tunnel_v4, *_encap_mod_table, ipv4_tunnel_term_table, rx_ipv4_tunnel_source_port),
+        rx_lag_table, l2_fwd_smac_table and always_trap_arp_table onto the GPU tables."""
+        for cidr in self._owned_routes:
+            dp.routes.remove(cidr)
+        self._owned_routes = []
+        for nh in self._owned_nh:
+            dp.nexthops.clear(nh)
+        self._owned_nh = set()
+        # router-interface MACs: start | mid | last 16-bit parts
+        rif: dict[int, list[int]] = {}
+        for i, part in enumerate(("start", "mid", "last")):
+            for e in self._rows(f"rif_mod_table_{part}"):
+                if e.action.endswith(f"set_src_mac_{part}"):
+                    rif.setdefault(e.key[0][1], [0, 0, 0])[i] = e.params["arg"]
+
+        def mac_of(v: int) -> str:
+            return ":".join(f"{(v >> (8 * (5 - k))) & 0xFF:02x}" for k in range(6))
+
+        def rif_mac(r: int) -> str:
+            a = rif.get(r, [0, 0, 0])
+            return mac_of((a[0] << 32) | (a[1] << 16) | a[2])
+
+        def nexthop(nh: int, e: Entry) -> None:
+            dmac = mac_of((e.params["dmac_high"] << 32) | e.params["dmac_low"])
+            if e.action.endswith("set_nexthop_lag"):
+                lagp = self.lag_ports.get(e.params["lag_group_id"])
+                if lagp is None:
+                    raise P4Error("FAILED_PRECONDITION", f"LAG group {e.params['lag_group_id']} has no port")
+                dp.nexthops.set(nh, port(lagp), dmac=dmac, smac=mac_of(0))
+            else:
+                dp.nexthops.set(nh, port(e.params["egress_port"]), dmac=dmac, smac=rif_mac(e.params["router_interface_id"]))
+            self._owned_nh.add(nh)
+
+        for e in self._rows("ecmp_nexthop_table"):
+            if e.action.endswith("ecmp_set_nexthop_info_dmac"):
+                v, m = self._k(e, 0)
+                for nh in ([v] if m == 0xFFFF else [x for x in range(dp.nexthops.a.shape[0]) if (x & m) == v]):
+                    nexthop(nh, e)
+        for e in self._rows("nexthop_table"):
+            if e.action.endswith(("set_nexthop_info_dmac", "set_nexthop_lag")):
+                nexthop(e.key[0][1], e)
+        groups = set()
+        for e in self._rows("ipv4_table"):
+            net, msk = self._k(e, 1)
+            plen = bin(msk).count("1")
+            cidr = f"{ipaddress.IPv4Address(net)}/{plen}"
+            if e.action.endswith("ipv4_set_nexthop_id"):
+                dp.routes.add(cidr, nexthop=e.params["nexthop_id"])
+            elif e.action.endswith("ecmp_hash_action"):
+                dp.routes.add(cidr, ecmp_group=e.params["ecmp_group_id"])
+                groups.add(e.params["ecmp_group_id"])
+            else:
+                continue
+            self._owned_routes.append(cidr)
+        for g in groups:
+            for h in range(T.ECMP_WAYS):
+                for e in self._rows("ecmp_hash_table"):  # highest priority first
+                    (fv, fm), (hv, hm) = self._k(e, 0), self._k(e, 1)
+                    if (g & fm) == fv and (h & hm) == hv:
+                        if e.action.endswith("set_nexthop_id"):
+                            dp.ecmp.set_slot(g, h, e.params["nexthop_id"])
+                        break
+        # tunnels: one tunnel port per destination VTEP; parameters from the encap mod tables
+        encap: dict[int, tuple[int, Entry]] = {}
+        for kind, tab in ((T.TUN_VXLAN, "vxlan_encap_mod_table"), (T.TUN_VXLAN, "vxlan_encap_vlan_pop_mod_table"),
+                          (T.TUN_GENEVE, "geneve_encap_mod_table")):
+            for e in self._rows(tab):
+                if e.params:
+                    encap[e.params["dst_addr"]] = (kind, e)
+        tunnels = [e for e in self._rows("l2_to_tunnel_v4") if e.action.endswith("set_tunnel_v4")]
+        local_vteps = {e.params["src_addr"] for _, e in encap.values()}
+        bridges = {int(dp.ports.a[p]["bridge_id"]) for p in src} | {0}
+        for k, e in enumerate(sorted({e.params["dst_addr"] for e in tunnels})):
+            if e not in encap:
+                raise P4Error("FAILED_PRECONDITION", f"tunnel to {ipaddress.IPv4Address(e)} has no encap mod entry")
+            kind, me = encap[e]
+            tp = port(TUNNEL_PORT_BASE + k)
+            # underlay: routed like any IPv4 destination, else the first physical port
+            r = dp.routes.lookup(e)
+            nh = (r & 0xFFFF) if r & T.ROUTE_NH else None
+            if nh is not None and dp.nexthops.a[nh]["valid"]:
+                n = dp.nexthops.a[nh]
+                out, dmac, smac = int(n["port"]), int(n["dmac_lo"]) | int(n["dmac_hi"]) << 32, int(n["smac_lo"]) | int(n["smac_hi"]) << 32
+                raw = lambda x: ":".join(f"{(x >> (8 * b)) & 0xFF:02x}" for b in range(6))  # noqa: E731
+                dmac_s, smac_s = raw(dmac), raw(smac)
+            else:
+                out, dmac_s, smac_s = port(PHY_BASE), "ff:ff:ff:ff:ff:ff", mac_of(0)
+            dp.tunnels.set(k, src=me.params["src_addr"], dst=e, vni=me.params["vni"], out_port=out, smac=smac_s,
+                           dmac=dmac_s, kind=kind, dport=me.params["dst_port"] or None, sport=me.params["src_port"])
+            dp.ports.a[tp]["flags"] |= T.PORT_TUNNEL
+            dp.ports.a[tp]["lag"] = k
+            for ent in tunnels:
+                if ent.params["dst_addr"] == e:
+                    for b in bridges:
+                        add_mac(b, _mac(ent.key[0][1]), tp)
+        # termination: (outer src, vni) -> the tunnel_id's port, which is a source port
+        sp_of = {(e.key[0][1], e.key[1][1]): e.params["source_port"] for e in self._rows("rx_ipv4_tunnel_source_port")
+                 if e.action.endswith("set_source_port")}
+        terms = [e for e in self._rows("ipv4_tunnel_term_table") if "decap" in e.action]
+        if terms or self._owned_tunnels:
+            dp.terms.a[:] = np.zeros((), T.TERM_DTYPE)
+            dp.terms.n = 0
+            dp.terms.version += 1
+        for e in terms:
+            s_ip, vni = e.key[0][1], e.key[1][1]
+            tp = port(TUNNEL_PORT_BASE + 128 + (e.params["tunnel_id"] & 0x7F))
+            dp.terms.insert(str(ipaddress.IPv4Address(s_ip)), vni, tp)
+            if (s_ip, vni) in sp_of:
+                bm = {e2.key[0][1]: e2.params["bridge_id"] for e2 in self._rows("source_port_to_bridge_map")
+                      if e2.key[0][2] == 0xFFFF and e2.action.endswith("set_bridge_id")}
+                if sp_of[(s_ip, vni)] in bm:
+                    dp.ports.update(tp, bridge_id=bm[sp_of[(s_ip, vni)]])
+        if terms and local_vteps:
+            vtep = next(iter(local_vteps))
+            for k in range(4):
+                pp = port(PHY_BASE + k)
+                dp.ports.a[pp]["flags"] |= T.PORT_VTEP
+                dp.ports.a[pp]["ext"] = int(T.ip_raw(np.uint32(vtep))) if hasattr(T, "ip_raw") else int(
+                    np.uint32(int.from_bytes(ipaddress.IPv4Address(vtep).packed, "little")))
+        self._owned_tunnels = bool(tunnels or terms)
+        # rx LAG: frames from a member physical port enter as the LAG's vport
+        for e in self._rows("rx_lag_table"):
+            if e.action.endswith("fwd_to_vsi"):
+                dp.ports.update(port(PHY_BASE + e.key[0][1]), default_out=port(e.params["port"]))
+        # l2_fwd_smac_table present: its bridges learn (OvS-style, in the data plane)
+        learn_bridges = {e.key[1][1] for e in self._rows("l2_fwd_smac_table")}
+        trap = bool(self._rows("always_trap_arp_table"))
+        for p in list(src) + [p for p in range(len(dp.ports.a)) if dp.ports.a[p]["flags"] & T.PORT_VALID and p in self._all_ports(dp)]:
+            if int(dp.ports.a[p]["bridge_id"]) in learn_bridges:
+                dp.ports.a[p]["flags"] |= T.PORT_LEARN
+            if trap:
+                dp.ports.a[p]["flags"] |= T.PORT_ARP_TRAP
+
+    def _all_ports(self, dp) -> set:
+        return set(self._owned_ports)
 
 
 def vsi_mac(vsi: int) -> str:

@@ -82,7 +82,7 @@ TERM_DTYPE = np.dtype([("src_ip", "<u4"), ("vni", "<u4"), ("port", "<u2"), ("val
 assert NH_DTYPE.itemsize == 16 and TUNNEL_DTYPE.itemsize == 32 and TERM_DTYPE.itemsize == 16
 TUN_VXLAN, TUN_GENEVE = 1, 2
 VXLAN_PORT, GENEVE_PORT = 4789, 6081
-LPM_EXT, ROUTE_NH, ROUTE_ECMP = 1 << 31, 1 << 30, 2 << 30
+LPM_EXT, ROUTE_NH, ROUTE_ECMP = 1 << 31, 1 << 28, 2 << 28
 ECMP_WAYS = 8
 assert PORT_DTYPE.itemsize == 32 and CHAIN_DTYPE.itemsize == 16 and MAC_DTYPE.itemsize == 16
 
