@@ -232,7 +232,9 @@ TABLES = [
      ["fwd_to_vsi", "drop"], 1024),
     ("l2_fwd_smac_table", [("hdrs.mac[vmeta.common.depth].sa", 48, "EXACT"), ("user_meta.pmeta.bridge_id", 8, "EXACT")],
      ["NoAction", "fwd_to_cp"], 1024),
-    ("always_trap_arp_table", [("hdrs.inval.data", 16, "EXACT")], ["do_trap_enable"], 1024),
+    # the compiled pipeline names both key fields hdrs.inval.data (p4info.txt:168-190): values bind in order
+    ("always_trap_arp_table", [("hdrs.inval.data", 16, "EXACT"), ("hdrs.inval.data", 16, "EXACT")],
+     ["do_trap_enable"], 1024),
 ]
 ACTIONS = {
     "set_source_port": [("source_port", 16)],

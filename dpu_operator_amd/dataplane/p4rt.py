@@ -114,7 +114,7 @@ class P4Runtime:
             spec = spec[: m.start()]
         elif need_action:
             raise P4Error("INVALID_ARGUMENT", "entry has no action")
-        given: dict[str, tuple[int, int | None]] = {}
+        given: dict[str, list[tuple[int, int | None]]] = {}
         priority = 0
         for tok in filter(None, (x.strip() for x in spec.split(","))):
             k, eq, v = tok.partition("=")
@@ -125,15 +125,17 @@ class P4Runtime:
                 continue
             val, _, mask = v.partition("/")
             try:
-                given[k] = (_int(val), _int(mask) if mask else None)
+                given.setdefault(k, []).append((_int(val), _int(mask) if mask else None))
             except ValueError:
                 raise P4Error("INVALID_ARGUMENT", f"bad value in {tok!r}") from None
         key = []
         ternary = False
         for mf in t.match_fields:
-            if mf.name not in given:
+            if not given.get(mf.name):
                 raise P4Error("INVALID_ARGUMENT", f"missing match field {mf.name} for {t.name}")
-            v, msk = given.pop(mf.name)
+            v, msk = given[mf.name].pop(0)  # repeated field names bind in order
+            if not given[mf.name]:
+                del given[mf.name]
             full = (1 << mf.bitwidth) - 1
             if v < 0 or v > full:
                 raise P4Error("INVALID_ARGUMENT", f"{mf.name}={v} exceeds {mf.bitwidth} bits")

@@ -88,7 +88,7 @@ def test_lag_rx_smac_and_arp_trap_tables(rt):
     rt.add_entry(C + "tx_acc_vsi", "vmeta.common.vsi=5,zero_padding=0,action=linux_networking_control.l2_fwd_and_bypass_bridge(40)")
     rt.add_entry(C + "l2_fwd_smac_table", "hdrs.mac[vmeta.common.depth].sa=02:00:00:00:00:01,user_meta.pmeta.bridge_id=0,"
                  "action=linux_networking_control.NoAction()")
-    rt.add_entry(C + "always_trap_arp_table", "hdrs.inval.data=0x806,action=linux_networking_control.do_trap_enable()")
+    rt.add_entry(C + "always_trap_arp_table", "hdrs.inval.data=0x806,hdrs.inval.data=0,action=linux_networking_control.do_trap_enable()")
     owned = [p for p in range(len(dp.ports.a)) if dp.ports.a[p]["flags"] & T.PORT_ARP_TRAP]
     assert owned and all(dp.ports.a[p]["flags"] & T.PORT_VALID for p in owned)
     assert any(dp.ports.a[p]["flags"] & T.PORT_LEARN for p in owned)
