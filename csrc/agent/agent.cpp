@@ -42,6 +42,7 @@ void Agent::load_interfaces() {
   }
   net_.fw_info.hb_interval_ms = cfg_.hb_interval_ms;
   net_.fw_info.hb_miss_count = cfg_.hb_miss_count;
+  net_.bump();  // (re)loaded state: the data plane re-applies it
 }
 
 void Agent::start(int plugin_port) {

@@ -212,6 +212,7 @@ PYBIND11_MODULE(_agent, m) {
       .def("stop", &Agent::stop, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("running", &Agent::running)
       .def_property_readonly("plugin_port", &Agent::plugin_port)
+      .def_property_readonly("state_gen", [](Agent& a) { return a.ctrl().state_gen(); })
       .def("set_link", [](Agent& a, uint32_t pem, uint32_t pf, int32_t vf, bool up) { a.set_link(fk(pem, pf, vf), up); },
            py::arg("pem"), py::arg("pf"), py::arg("vf"), py::arg("up"))
       .def("update_stats", [](Agent& a, uint32_t pem, uint32_t pf, int32_t vf, uint64_t rx_pkts, uint64_t rx_bytes,

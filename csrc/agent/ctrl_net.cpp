@@ -20,6 +20,7 @@ bool CtrlNet::has(const FnKey& k) const {
 void CtrlNet::set_link(const FnKey& k, State s) {
   std::lock_guard<std::mutex> g(mu_);
   ifs_[k].link = s;
+  bump();
 }
 
 void CtrlNet::set_stats(const FnKey& k, const RxStats& rx, const TxStats& tx) {
@@ -64,6 +65,7 @@ Response CtrlNet::handle(const FnKey& k, const Request& req, uint64_t host_ver) 
       if (set) {
         if (req.val16 < min_mtu || req.val16 > max_mtu) { r.hdr.reply = (uint16_t)Reply::InvalidParam; break; }
         s.mtu = req.val16;
+        bump();
       }
       r.val16 = s.mtu;
       break;
@@ -71,6 +73,7 @@ Response CtrlNet::handle(const FnKey& k, const Request& req, uint64_t host_ver) 
       if (set) {
         if (req.mac[0] & 1) { r.hdr.reply = (uint16_t)Reply::InvalidParam; break; }  // multicast
         std::memcpy(s.mac, req.mac, 6);
+        bump();
       }
       std::memcpy(r.mac, s.mac, 6);
       break;
@@ -84,6 +87,7 @@ Response CtrlNet::handle(const FnKey& k, const Request& req, uint64_t host_ver) 
       if (set) {
         if (req.val16 > 1) { r.hdr.reply = (uint16_t)Reply::InvalidParam; break; }
         s.link = (State)req.val16;
+        bump();
       }
       r.val16 = (uint16_t)s.link;
       break;
@@ -91,6 +95,7 @@ Response CtrlNet::handle(const FnKey& k, const Request& req, uint64_t host_ver) 
       if (set) {
         if (req.val16 > 1) { r.hdr.reply = (uint16_t)Reply::InvalidParam; break; }
         s.rx = (State)req.val16;
+        bump();
       }
       r.val16 = (uint16_t)s.rx;
       break;
@@ -112,6 +117,7 @@ Response CtrlNet::handle(const FnKey& k, const Request& req, uint64_t host_ver) 
       s.removed = true;
       s.link = State::Down;
       s.rx = State::Down;
+      bump();
       break;
     case H2F::Offloads:
       if (set) s.offloads = req.offloads;

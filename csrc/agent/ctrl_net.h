@@ -7,6 +7,7 @@
 // struct) without a serializer.  Interface statistics come from the GPU data plane's per-port
 // counters (PortStats is filled by the control plane from DataPlane.port_counters()).
 #pragma once
+#include <atomic>
 #include <cstdint>
 #include <cstring>
 #include <map>
@@ -135,8 +136,13 @@ class CtrlNet {
   void set_stats(const FnKey& k, const RxStats& rx, const TxStats& tx);
   std::map<FnKey, IfState> snapshot() const;
   std::mutex& mutex() const { return mu_; }
+  // Bumped by every change of an interface's MTU, MAC, link, RX state or removal: the data-plane
+  // side polls it and re-applies the interface table to the GPU port flags when it moved.
+  uint64_t state_gen() const { return gen_.load(std::memory_order_acquire); }
+  void bump() { gen_.fetch_add(1, std::memory_order_acq_rel); }
 
  private:
+  std::atomic<uint64_t> gen_{0};
   mutable std::mutex mu_;
   std::map<FnKey, IfState> ifs_;
 };

@@ -74,6 +74,8 @@ enum PortFlags : uint32_t {
   kPortRouted = 1u << 13,       // router interface: IPv4 to this port's MAC is routed (LPM) on a flow miss
   kPortTunnel = 1u << 14,       // egress via this port = VXLAN / GENEVE encap with tunnel[lag] (OvS tunnel port)
   kPortVtep = 1u << 15,         // underlay port: UDP 4789 / 6081 to ext (local VTEP IPv4) is terminated
+  kPortRxOff = 1u << 16,        // ctrl-net RX_STATE down: the function takes no frames (egress dropped)
+  kPortLinkDown = 1u << 17,     // ctrl-net LINK_STATUS down / DEV_REMOVE: neither receives nor sends
 };
 
 constexpr int kLagWays = 8;                 // members per LAG group (hash[2:0])

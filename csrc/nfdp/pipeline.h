@@ -52,7 +52,7 @@ NFDP_HD void ingress_stage(const TablesView& t, const TA& ta, const uint32_t* d,
     const PortEntry pe = ta.port(st.in_port);
     st.in_flags = pe.flags;
     st.in_ext = pe.ext;
-    if (!(pe.flags & kPortValid)) st.reason = st.reason ? st.reason : kBadPort;
+    if ((pe.flags & (kPortValid | kPortLinkDown)) != kPortValid) st.reason = st.reason ? st.reason : kBadPort;
     const uint32_t vid = p.tci & 0xFFFu;
     if ((pe.flags & kPortVlanIsolate) && p.tagged && vid != pe.vlan)
       st.reason = st.reason ? st.reason : kVlanDrop;
@@ -89,6 +89,11 @@ NFDP_HD uint32_t egress_len(const Parsed& p, const EgressDecision& e) {
 
 NFDP_HD uint32_t byte_at(const uint32_t* s, int off) { return (s[off >> 2] >> (8 * (off & 3))) & 0xFFu; }
 
+// A port takes frames when it is configured, its link is up and its function's RX is enabled.
+NFDP_HD bool port_can_egress(uint32_t flags) {
+  return (flags & (kPortValid | kPortLinkDown | kPortRxOff)) == kPortValid;
+}
+
 // Final egress checks on a chosen port: LAG member (K8), validity, egress tag (K6), MTU.
 // Returns a drop reason (0 = ok); `port`/`push`/`tci` are updated in place.
 template <class TA>
@@ -104,7 +109,7 @@ NFDP_HD uint32_t finish_port(const TablesView& t, const TA& ta, uint32_t& port, 
     port = m;
     pe = ta.port(m);
   }
-  if (!(pe.flags & kPortValid)) return kBadPort;
+  if (!port_can_egress(pe.flags)) return kBadPort;
   if (!vlan_done && (pe.flags & kPortTagEgress) && pe.vlan) { push = 1; tci = pe.vlan & 0xFFFu; }
   // tunnel port (OvS vxlan / geneve port, P4 l2_to_tunnel_v4): encapsulated by the side pass
   uint32_t enc = 0;
@@ -333,7 +338,7 @@ NFDP_HD void side_stage(const TablesView& t, const TA& ta, const uint32_t* d_in,
   // mirror_and_send (K9): the frame as it leaves, also to the ingress port's mirror port
   if (st.in_flags & kPortMirror) {
     const uint32_t mp = st.in_ext >> 16;
-    if (mp < (uint32_t)kMaxPorts && (ta.port(mp).flags & kPortValid)) sink.rep(o, make_meta(mp, meta_len(ometa), kOk), src);
+    if (mp < (uint32_t)kMaxPorts && port_can_egress(ta.port(mp).flags)) sink.rep(o, make_meta(mp, meta_len(ometa), kOk), src);
   }
   // flood: one replica per further member of the bridge's group (the frame itself went to the
   // first member).  Flooding happens on the L2 path only, where no NF rewrote the frame, so the

@@ -7,6 +7,13 @@ intel-netsec/main.go:627, mock-vsp); here `--vendor` selects it:
   marvell    Marvell VSP; OvS-equivalent bridge on the GPU data plane (--debug-dp: log only)
   netsec     Intel NetSec accelerator VSP on the GPU data plane
   intel-ipu  Intel IPU VSP writing P4 rules to the pipeline server (--p4rt-addr)
+
+amd-gpu extras:
+  --metrics-bind-address  serve the data plane's metrics (per-port counters, drops, flows, the
+                          packet-path latency histograms) on /metrics of this address
+  --agent-mbox PATH       run the node control agent (csrc/agent) on this mailbox and close its
+                          loops with the data plane: ctrl-net MTU / link / RX state -> GPU port
+                          table, port counters -> agent interface statistics (cpagent.AgentBridge)
 """
 from __future__ import annotations
 
@@ -84,11 +91,16 @@ def main(argv=None, stop: threading.Event | None = None) -> int:
     ap.add_argument("--state-dir", default="", help="amd-gpu: journal + snapshot directory (resume on restart)")
     ap.add_argument("--live", action="store_true",
                     help="amd-gpu: vports are real TAP netdevs and pod traffic flows through the data plane")
+    ap.add_argument("--metrics-bind-address", default="", help="amd-gpu: data-plane /metrics address (off if empty)")
+    ap.add_argument("--agent-mbox", default="", help="amd-gpu: run the node control agent on this mailbox path")
+    ap.add_argument("--agent-config", default="", help="agent SoC config file (default: one PF + --agent-vfs VFs)")
+    ap.add_argument("--agent-vfs", type=int, default=8)
     a = ap.parse_args(argv)
     if a.node_config:
         set_node_config(NodeConfig.load(a.node_config))
     logging.basicConfig(level=logging.INFO)
     vsp = build_vsp(a, PathManager(a.root)).start()
+    services = _extras(a, vsp)
     stop = stop or threading.Event()
     if threading.current_thread() is threading.main_thread():
         signal.signal(signal.SIGTERM, lambda *_: stop.set())
@@ -97,7 +109,37 @@ def main(argv=None, stop: threading.Event | None = None) -> int:
     if getattr(vsp, "journal", None) is not None:
         vsp.checkpoint()  # clean shutdown: snapshot so the next start skips the replay
     vsp.stop()
+    for svc in reversed(services):
+        svc.stop()
     return 0
+
+
+def _extras(a, vsp) -> list:
+    """Metrics server and node agent around a GPU VSP; returns what to stop at shutdown."""
+    out = []
+    if a.vendor != "amd-gpu":
+        return out
+    if a.metrics_bind_address:
+        from prometheus_client import CollectorRegistry
+
+        from ..utils.metrics import MetricsServer, register_dataplane
+
+        reg = CollectorRegistry()
+        register_dataplane(lambda: vsp.dp, "gpu0", reg)
+        vsp.metrics = MetricsServer(a.metrics_bind_address, reg).start()
+        out.append(vsp.metrics)
+    if a.agent_mbox:
+        from .. import cpagent
+        from ..native import agent as native_agent
+
+        A = native_agent()
+        cfg = open(a.agent_config).read() if a.agent_config else cpagent.default_config(n_vfs=a.agent_vfs)
+        ag = A.Agent(a.agent_mbox, cfg)
+        ag.start()
+        vsp.agent = ag
+        vsp.attach_agent(ag)
+        out.append(ag)
+    return out
 
 
 if __name__ == "__main__":

@@ -62,7 +62,8 @@ def default_config(n_vfs: int = 8, hb_interval_ms: int = 1000, hb_miss_count: in
 
 
 class StatsBridge:
-    """Periodically copy DataPlane per-port counters into the agent's interface statistics."""
+    """Periodically copy DataPlane per-port counters into the agent's interface statistics.
+    `dataplane` is a DataPlane or a callable returning one (None while it does not exist yet)."""
 
     def __init__(self, agent, dataplane, period_s: float = 1.0):
         self.agent = agent
@@ -72,7 +73,10 @@ class StatsBridge:
         self._t: threading.Thread | None = None
 
     def sync_once(self) -> int:
-        ctr = self.dp.port_counters()
+        dp = self.dp() if callable(self.dp) else self.dp
+        if dp is None:
+            return 0
+        ctr = dp.port_counters()
         drops = 0
         n = 0
         for pem, pf, vf in self.agent.functions():
@@ -90,6 +94,98 @@ class StatsBridge:
                 self.sync_once()
 
         self._t = threading.Thread(target=run, daemon=True, name="agent-stats")
+        self._t.start()
+        return self
+
+    def stop(self) -> None:
+        self._stop.set()
+        if self._t is not None:
+            self._t.join(timeout=5)
+
+
+class DataPlanePorts:
+    """`set_port_state` target for a bare DataPlane (a VSP implements the same method itself)."""
+
+    def __init__(self, dataplane):
+        self.dp = dataplane
+
+    def set_port_state(self, port: int, link: bool, rx: bool, mtu: int) -> None:
+        p = self.dp.ports
+        p.set_link(port, link)
+        p.set_rx(port, rx)
+        p.set_mtu(port, mtu)
+        self.dp.commit()
+
+
+class PortStateSync:
+    """ctrl-net interface state -> GPU port flags (the control loop of the reference's
+    octep_cp_agent loop.c:107-288, where SET_MTU / LINK_STATUS / RX_STATE / DEV_REMOVE reconfigure
+    the SoC interface).  The agent bumps `state_gen` on every such change; `sync_once` re-applies
+    each function's state to its data-plane port when it moved:
+        link down or removed -> PORT_LINK_DOWN (the port neither receives nor sends)
+        RX state off         -> PORT_RX_OFF    (nothing is delivered to the port)
+        MTU                  -> port egress MTU (larger frames dropped as too_big)
+    `target` has `set_port_state(port, link, rx, mtu)` (GpuVsp, or DataPlanePorts)."""
+
+    def __init__(self, agent, target):
+        self.agent = agent
+        self.target = target
+        self.gen = -1
+        self.applied: dict[int, tuple] = {}
+
+    def sync_once(self, force: bool = False) -> int:
+        g = self.agent.state_gen
+        if g == self.gen and not force:
+            return 0
+        self.gen = g
+        n = 0
+        for pem, pf, vf in self.agent.functions():
+            s = self.agent.iface(pem, pf, vf)
+            port = s["dp_port"]
+            if port < 0:
+                continue
+            st = (bool(s["link"]) and not s["removed"], bool(s["rx"]) and not s["removed"], int(s["mtu"]))
+            if self.applied.get(port) == st and not force:
+                continue
+            self.target.set_port_state(port, *st)
+            self.applied[port] = st
+            n += 1
+        return n
+
+
+class AgentBridge:
+    """One thread that keeps the agent and the data plane in step: interface state -> port flags
+    every `state_period_s` (cheap: one atomic read when nothing changed), port counters -> agent
+    interface statistics every `stats_period_s`."""
+
+    def __init__(self, agent, target, dataplane, state_period_s: float = 0.05, stats_period_s: float = 1.0):
+        self.state = PortStateSync(agent, target)
+        self.stats = StatsBridge(agent, dataplane, stats_period_s)
+        self.state_period = state_period_s
+        self.stats_period = stats_period_s
+        self._stop = threading.Event()
+        self._t: threading.Thread | None = None
+        self.errors = 0
+
+    def _run(self) -> None:
+        import logging
+        import time
+
+        log = logging.getLogger("dpu.cpagent")
+        next_stats = time.monotonic() + self.stats_period
+        while not self._stop.wait(self.state_period):
+            try:
+                self.state.sync_once()
+                if time.monotonic() >= next_stats:
+                    next_stats += self.stats_period
+                    self.stats.sync_once()
+            except Exception:  # noqa: BLE001 - the loop outlives a bad sync; counted and logged
+                self.errors += 1
+                log.exception("agent bridge sync failed")
+
+    def start(self) -> "AgentBridge":
+        self.state.sync_once(force=True)
+        self._t = threading.Thread(target=self._run, daemon=True, name="agent-bridge")
         self._t.start()
         return self
 

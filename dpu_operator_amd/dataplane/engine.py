@@ -19,6 +19,7 @@ import numpy as np
 
 from ..native import nfdp as _nfdp_mod
 from ..utils.faults import FAULTS
+from ..utils.latency import LatencyStats
 from ..utils.trace import TRACER
 from . import tables as T
 
@@ -81,6 +82,7 @@ class DataPlane:
         self.count_flows = True  # per-flow packed counters (one 64-bit atomic per packet)
         self.MAX_LAUNCH = 1 << 24
         self.flow_totals = np.zeros((self.flows.nbuckets * 4, 2), np.uint64)
+        self.latency = LatencyStats()   # packet-path latency histograms (utils/latency.py)
         # side outputs (flood / mirror / ARP replicas, learn events) and MAC learning state
         self.cap_rep, self.cap_learn = 1 << 16, 1 << 14
         self.stamp = 0                 # batch counter: the learned entries' last-seen stamp
@@ -433,6 +435,19 @@ class DataPlane:
         raw = self._dev["drop_ctr"]
         raw = raw.cpu().numpy().view(np.uint64) if self.gpu else raw
         return {T.REASONS.get(i, str(i)): int(v) for i, v in enumerate(raw) if v}
+
+    TICK_S = 1e-8  # s_memrealtime: 100 MHz
+
+    def fold_device_latency(self, res: "BatchResult") -> int:
+        """Fold a GPU batch's sampled per-packet latencies (ticks since the batch's t0 stamp, one
+        sample per 16 packets) into the `device` histogram; returns the number of samples."""
+        lat = res.extra.get("lat") if self.gpu else None
+        if lat is None:
+            return 0
+        ticks = lat[: (res.n + 15) // 16].cpu().numpy().view(np.uint32)
+        ticks = ticks[ticks > 0]
+        self.latency.observe_many("device", ticks.astype(np.float64) * self.TICK_S)
+        return int(ticks.size)
 
     def reset_counters(self) -> None:
         self._alloc_counters()

@@ -19,6 +19,10 @@ what the pod sends arrives on that fd and what the VSP writes to it is what the 
        tunnel's underlay port; terminated tunnel traffic (reason `recirc`) is re-injected, inner
        frame only, as received on the tunnel port, in the next cycle (P4 do_recirculate).
 
+Every cycle records its stage times (rx / pipeline / side / tx / batch) and, on the GPU, the
+kernel's sampled per-packet latencies into `dp.latency` (utils/latency.py), which the data-plane
+metrics collector exports as `dpu_packet_latency_seconds{stage=...}` histograms.
+
 Frames are whole Ethernet frames without FCS (TAP, IFF_NO_PI).  MAC learning, flooding, VLAN
 tags, SNAT etc. are the pipeline's; this loop only moves bytes.
 """
@@ -127,7 +131,9 @@ class LivePath:
             frames, src = [f for f, _ in self._recirc], [q for _, q in self._recirc]
             self._recirc = []
             timeout = 0
-        for fd, _ev in p.poll(int(timeout * 1000)):
+        ready = p.poll(int(timeout * 1000))
+        self._t_ready = time.perf_counter()   # frames are waiting: the batch's clock starts here
+        for fd, _ev in ready:
             idx, port = fd2port[fd]
             while len(frames) < self.burst:
                 f = port.read()
@@ -149,10 +155,14 @@ class LivePath:
             self.stats["tx"] += 1
 
     def poll_once(self, timeout: float = 0.05) -> int:
+        self._t_ready = time.perf_counter()
         frames, src = self._gather(timeout)
         n = len(frames)
         if not n:
             return 0
+        t_start = self._t_ready
+        lat = self.dp.latency
+        t_rx = time.perf_counter()
         lens = np.array([len(f) for f in frames], np.uint32)
         slots = np.zeros((n, 64), np.uint8)
         for i, f in enumerate(frames):
@@ -165,10 +175,14 @@ class LivePath:
             r = self.dp.run(torch.from_numpy(slots).to(self.dp.tdev), torch.from_numpy(im.view(np.int32)).to(self.dp.tdev))
             out = r.out.cpu().numpy()
             meta = r.meta.cpu().numpy().view(np.uint32)
+            t_pipe = time.perf_counter()
+            self.dp.fold_device_latency(r)
         else:
             r = self.dp.run(slots, im)
             out, meta = r.out, r.meta
+            t_pipe = time.perf_counter()
         side = self.dp.side_result() if self.dp.side_active() else {"n_rep": 0}
+        t_side = time.perf_counter()
         self.stats["rx"] += n
         self.stats["batches"] += 1
         port, olen, reason = P.meta_fields(meta)
@@ -195,6 +209,12 @@ class LivePath:
             else:
                 self.stats["replicas"] += 1
                 self._send(int(rp[0]), fr)
+        t_end = time.perf_counter()
+        lat.observe("rx", t_rx - t_start)
+        lat.observe("pipeline", t_pipe - t_rx)
+        lat.observe("side", t_side - t_pipe)
+        lat.observe("tx", t_end - t_side)
+        lat.observe("batch", t_end - t_start)
         return n
 
     # ------------------------------------------------------------------ thread

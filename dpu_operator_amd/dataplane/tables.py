@@ -44,6 +44,8 @@ PORT_ARP_TRAP = 1 << 12     # ARP frames from this port are also copied to the s
 PORT_ROUTED = 1 << 13       # router interface: IPv4 to the port's own MAC is routed (LPM) on a flow miss
 PORT_TUNNEL = 1 << 14       # tunnel port: egress = VXLAN / GENEVE encap with tunnels[lag]
 PORT_VTEP = 1 << 15         # underlay port: VXLAN / GENEVE to ext (local VTEP IPv4, raw) is terminated
+PORT_RX_OFF = 1 << 16       # ctrl-net RX_STATE down: frames to the port are dropped (bad_port)
+PORT_LINK_DOWN = 1 << 17    # ctrl-net LINK_STATUS down / DEV_REMOVE: the port neither receives nor sends
 LAG_WAYS = 8
 
 # hop opcodes (nfdp.h Hop)
@@ -185,8 +187,14 @@ class PortTable:
         self.version += 1
 
     def set_link(self, idx: int, up: bool) -> None:
-        """Link state (ctrl-net LINK_STATUS / RX_STATE): a down port neither receives nor sends."""
-        self._flag(idx, PORT_VALID, up)
+        """Link state (ctrl-net LINK_STATUS, DEV_REMOVE): a down port neither receives nor sends.
+        Kept apart from PORT_VALID, so link flaps never undo the port's configuration."""
+        self._flag(idx, PORT_LINK_DOWN, not up)
+        self.version += 1
+
+    def set_rx(self, idx: int, on: bool) -> None:
+        """RX state (ctrl-net RX_STATE): with RX off nothing is delivered to the port."""
+        self._flag(idx, PORT_RX_OFF, not on)
         self.version += 1
 
     def set_mtu(self, idx: int, mtu: int) -> None:

@@ -16,7 +16,7 @@ import threading
 from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 
 from prometheus_client import CONTENT_TYPE_LATEST, CollectorRegistry, Counter, Gauge, Histogram, generate_latest
-from prometheus_client.core import CounterMetricFamily, GaugeMetricFamily
+from prometheus_client.core import CounterMetricFamily, GaugeMetricFamily, HistogramMetricFamily
 
 REGISTRY = CollectorRegistry(auto_describe=True)
 
@@ -37,17 +37,29 @@ CONTROL = _Control(REGISTRY)
 
 
 class DataPlaneCollector:
-    """Scrape-time export of a DataPlane's counters (no per-packet Python work)."""
+    """Scrape-time export of a DataPlane's counters (no per-packet Python work).  `dataplane` is a
+    DataPlane or a callable returning one (a VSP creates its data plane on Init: nothing is
+    exported before that)."""
 
     def __init__(self, dataplane, name: str = "gpu0", max_ports: int = 4096):
-        self.dp = dataplane
+        self._dp = dataplane
         self.name = name
         self.max_ports = max_ports
 
+    @property
+    def dp(self):
+        return self._dp() if callable(self._dp) else self._dp
+
     def collect(self):
+        dp = self.dp
+        if dp is None:
+            return
+        yield from self._collect(dp)
+
+    def _collect(self, dp):
         from ..dataplane import tables as T
 
-        ctr = self.dp.port_counters()
+        ctr = dp.port_counters()
         labels = ["dataplane", "port"]
         rx_p = CounterMetricFamily("dpu_port_rx_packets", "Packets received per port", labels=labels)
         rx_b = CounterMetricFamily("dpu_port_rx_bytes", "Bytes received per port", labels=labels)
@@ -62,18 +74,32 @@ class DataPlaneCollector:
             tx_b.add_metric(lv, float(ctr[port, 3]))
         yield from (rx_p, rx_b, tx_p, tx_b)
         drops = CounterMetricFamily("dpu_drops", "Dropped packets by reason", labels=["dataplane", "reason"])
-        for reason, n in sorted(self.dp.drop_counters().items()):
+        for reason, n in sorted(dp.drop_counters().items()):
             drops.add_metric([self.name, reason], float(n))
         yield drops
         flows = GaugeMetricFamily("dpu_flows_installed", "Exact-match flows installed", labels=["dataplane"])
-        flows.add_metric([self.name], float(len(self.dp.flows)))
+        flows.add_metric([self.name], float(len(dp.flows)))
         yield flows
         cap = GaugeMetricFamily("dpu_flow_capacity", "Flow table slots", labels=["dataplane"])
-        cap.add_metric([self.name], float(self.dp.flows.nbuckets * 4))
+        cap.add_metric([self.name], float(dp.flows.nbuckets * 4))
         yield cap
         ports = GaugeMetricFamily("dpu_ports_valid", "Valid data-plane ports", labels=["dataplane"])
-        ports.add_metric([self.name], float((self.dp.ports.a["flags"] & T.PORT_VALID).astype(bool).sum()))
+        f = dp.ports.a["flags"]
+        ports.add_metric([self.name], float((f & T.PORT_VALID).astype(bool).sum()))
         yield ports
+        down = GaugeMetricFamily("dpu_ports_down", "Valid ports whose link is down or RX is off",
+                                 labels=["dataplane", "state"])
+        valid = (f & T.PORT_VALID).astype(bool)
+        down.add_metric([self.name, "link_down"], float((valid & (f & T.PORT_LINK_DOWN).astype(bool)).sum()))
+        down.add_metric([self.name, "rx_off"], float((valid & (f & T.PORT_RX_OFF).astype(bool)).sum()))
+        yield down
+        lat = HistogramMetricFamily("dpu_packet_latency_seconds",
+                                    "Packet-path latency by stage (utils/latency.py: rx, pipeline, side, tx, "
+                                    "batch per live batch; device per sampled packet)", labels=["dataplane", "stage"])
+        for stage, h in dp.latency.items():
+            b, total = h.buckets()
+            lat.add_metric([self.name, stage], b, total)
+        yield lat
 
 
 def register_dataplane(dataplane, name: str = "gpu0", registry: CollectorRegistry = REGISTRY) -> DataPlaneCollector:

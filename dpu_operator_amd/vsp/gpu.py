@@ -125,6 +125,8 @@ class GpuVsp(VspBase):
         self.taps: dict[int, object] = {}       # live mode: port -> TapPort
         self.livepath = None
         self.uplink = uplink                    # live mode: netdev (read/write/fd) of the wire port
+        self.port_state: dict[int, tuple[bool, bool, int]] = {}  # port -> (link, rx, mtu) from the agent
+        self.agent_bridge = None
         self.journal = Journal(state_dir, "gpu-vsp") if state_dir else None
         self._replaying = False
         self.restored = 0
@@ -137,6 +139,7 @@ class GpuVsp(VspBase):
             self.dp = DataPlane(device=self.device, flow_buckets=self.flow_buckets, hash_mode=self.hash_mode,
                                 acl_mode=self.acl_mode)
             self.dp.ports.set(WIRE_PORT, flags=T.PORT_VALID, bridge_id=VF_BRIDGE, mac="02:00:00:00:0f:a0")
+            self._apply_port_state(WIRE_PORT)
             self.dp.commit(full=True)
         return self.dp
 
@@ -180,6 +183,41 @@ class GpuVsp(VspBase):
         else:
             dp.ports.set(i, flags=T.PORT_VALID, bridge_id=VF_BRIDGE, mac=v["mac"], peer_mac=v["mac"],
                          default_out=WIRE_PORT)
+        self._apply_port_state(i)
+
+    def _apply_port_state(self, i: int) -> None:
+        st = self.port_state.get(i)
+        if st is None or self.dp is None:
+            return
+        link, rx, mtu = st
+        self.dp.ports.set_link(i, link)
+        self.dp.ports.set_rx(i, rx)
+        self.dp.ports.set_mtu(i, mtu)
+
+    # ------------------------------------------------------------------ node agent
+    def set_port_state(self, port: int, link: bool, rx: bool, mtu: int) -> None:
+        """ctrl-net interface state of the function backed by `port` (cpagent.PortStateSync):
+        kept across re-programming of the port, applied to the GPU port table now if it exists."""
+        with self._lock:
+            self.port_state[port] = (bool(link), bool(rx), int(mtu))
+            if self.dp is not None and (port in self.vports or port == WIRE_PORT):
+                self._apply_port_state(port)
+                self._commit()
+
+    def attach_agent(self, agent, state_period_s: float = 0.05, stats_period_s: float = 1.0):
+        """Close the loops with the node agent: interface state -> GPU port flags, port
+        counters -> the agent's interface statistics (cpagent.AgentBridge)."""
+        from ..cpagent import AgentBridge
+
+        self.agent_bridge = AgentBridge(agent, self, lambda: self.dp, state_period_s, stats_period_s).start()
+        return self.agent_bridge
+
+    def stop(self) -> None:
+        if self.agent_bridge is not None:
+            self.agent_bridge.stop()
+            self.agent_bridge = None
+        self.stop_live()
+        super().stop()
 
     def _apply_steering(self) -> None:
         """Recompute port programming + the (bridge, MAC) table from scratch (idempotent).

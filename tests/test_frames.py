@@ -201,6 +201,47 @@ def test_imix_frames_gpu_bit_exact():
     assert np.array_equal(g.port_counters(), cpu.port_counters())
 
 
+def _port_states(dp, sc):
+    """Agent-driven port states (cpagent.PortStateSync): pod 0 link down, pod 1 RX off, pod 2 MTU 576."""
+    pods = [int(p) for p in sc.pod_port]
+    dp.ports.set_link(pods[0], False)
+    dp.ports.set_rx(pods[1], False)
+    dp.ports.set_mtu(pods[2], 576)
+    dp.commit()
+    return pods
+
+
+def test_port_states_oracle():
+    dp, sc = _sfc("cpu")
+    pods = _port_states(dp, sc)
+    slots, im, frames, lens = _imix(sc)
+    r = dp.run(slots, im)
+    port, _, rs = P.meta_fields(r.meta)
+    inp = im & 0xFFFF
+    assert (rs[inp == pods[0]] == 1).all()                          # bad_port: a down link sends nothing
+    assert (rs[inp == pods[1]] == 0).any()                          # RX off still transmits
+    fwd = rs == 0
+    assert not np.isin(port[fwd], pods[:2]).any()                   # nothing delivered to either
+    to2 = (port == pods[2]) & fwd
+    assert to2.any() and (lens[to2] - 14 <= 576).all()
+
+
+@pytest.mark.gpu
+def test_port_states_gpu_bit_exact():
+    torch = _torch()
+    cpu, sc = _sfc("cpu")
+    g, _ = _sfc("cuda")
+    _port_states(cpu, sc)
+    _port_states(g, sc)
+    slots, im, _, _ = _imix(sc, n=4096)
+    rc = cpu.run(slots, im)
+    r = g.run(torch.from_numpy(slots).cuda(), torch.from_numpy(im.view(np.int32)).cuda())
+    torch.cuda.synchronize()
+    assert np.array_equal(r.meta.cpu().numpy().view(np.uint32), rc.meta)
+    assert np.array_equal(r.out.cpu().numpy(), rc.out)
+    assert cpu.drop_counters() == g.drop_counters()
+
+
 @pytest.mark.gpu
 def test_flood_learn_arp_mirror_gpu_bit_exact():
     cpu, gpu = _bridge("cpu"), _bridge("cuda")

@@ -62,6 +62,9 @@ def test_ping_between_namespaces_through_the_data_plane():
         assert (7, eps[0].mac) in learned and (7, eps[1].mac) in learned
         pc = dp.port_counters()
         assert pc[0, 0] >= 2 and pc[1, 0] >= 2         # rx on both ports
+        stages = dict(dp.latency.items())                # per-stage latency of every live batch
+        assert {"rx", "pipeline", "side", "tx", "batch"} <= set(stages)
+        assert stages["batch"].count == live.stats["batches"] and stages["batch"].quantile(0.5) < 0.5
     finally:
         _teardown(taps, eps, live)
 
