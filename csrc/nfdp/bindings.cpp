@@ -152,6 +152,13 @@ PYBIND11_MODULE(_nfdp, m) {
         }
         return slots;
       })
+      .def("erase_many", [](FlowTableHost& t, U32Arr keys) {
+        if (keys.ndim() != 2 || keys.shape(1) != 4) throw std::invalid_argument("erase_many expects [n,4] uint32 keys");
+        auto k = keys.unchecked<2>();
+        size_t n = 0;
+        for (py::ssize_t i = 0; i < keys.shape(0); ++i) n += t.erase(FlowKey{k(i, 0), k(i, 1), k(i, 2), k(i, 3)}) ? 1 : 0;
+        return n;
+      })
       .def("erase", [](FlowTableHost& t, py::tuple k) {
         return t.erase(FlowKey{k[0].cast<uint32_t>(), k[1].cast<uint32_t>(), k[2].cast<uint32_t>(), k[3].cast<uint32_t>()});
       })
@@ -458,6 +465,18 @@ PYBIND11_MODULE(_nfdp, m) {
       });
 
   // Blocking copy between any two addresses (device or host; unified addressing).
+  // Copy on a private non-blocking stream: never ordered behind a resident (ring) kernel.
+  m.def("memcpy_nb", [](uintptr_t dst, uintptr_t src, size_t nbytes) {
+    py::gil_scoped_release nogil;
+    static hipStream_t s = [] {
+      hipStream_t x{};
+      check(hipStreamCreateWithFlags(&x, hipStreamNonBlocking), "stream");
+      return x;
+    }();
+    check(hipMemcpyAsync(reinterpret_cast<void*>(dst), reinterpret_cast<const void*>(src), nbytes, hipMemcpyDefault, s),
+          "memcpy_nb");
+    check(hipStreamSynchronize(s), "memcpy_nb");
+  });
   m.def("memcpy", [](uintptr_t dst, uintptr_t src, size_t nbytes) {
     py::gil_scoped_release nogil;
     check(hipMemcpy(reinterpret_cast<void*>(dst), reinterpret_cast<const void*>(src), nbytes, hipMemcpyDefault),
@@ -494,8 +513,16 @@ PYBIND11_MODULE(_nfdp, m) {
         if (acl_mode == 1 && (!f.acl_wfrag || !f.acl_cinit)) throw std::invalid_argument("MFMA ACL needs frags");
         LaunchCfg cfg;
         cfg.hash_mode = hash_mode; cfg.acl_mode = acl_mode; cfg.num_cus = num_cus;
-        r.start(f, cfg, deadline_s);
+        r.start(f, cfg, deadline_s, ptr<const void>(tables, "flows_alt"));
       })
+      .def("flip", &RingEngine::flip)
+      .def("grace_over", &RingEngine::grace_over)
+      .def("wait_grace", [](RingEngine& r, double timeout_s) {
+        py::gil_scoped_release nogil;
+        return r.wait_grace(timeout_s);
+      }, py::arg("timeout_s") = 10.0)
+      .def_property_readonly("epoch", &RingEngine::epoch)
+      .def("set_epoch", &RingEngine::set_epoch)
       .def("stop", [](RingEngine& r, double timeout_s) { py::gil_scoped_release nogil; r.stop(timeout_s); },
            py::arg("timeout_s") = 30.0)
       .def("completed", &RingEngine::completed)

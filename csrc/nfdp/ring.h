@@ -21,12 +21,22 @@
 // Drain semantics: `stop` makes a wave exit only while it WAITS for an unpublished chunk, and
 // tickets are claimed in order, so every chunk published before the stop is processed.  Every
 // wave also exits on a device-side deadline (s_memrealtime), so the grid always drains even if
-// the host dies.  Tables are staged at launch; a control-plane commit restarts the kernel
-// (stop -> drain -> relaunch, tens of µs) so a session never sees a torn table.
+// the host dies.
+//
+// Table updates under a running ring (epoch flip, no relaunch): the flow table is double
+// buffered.  The published word carries a 7-bit epoch next to the packet count
+// (stop | count << 7 | epoch); a wave takes the epoch of the word that published its chunk and
+// probes copy `epoch & 1`.  The control plane writes its bucket changes into the copy no wave
+// reads, flips the epoch (flip(), carried by the next publish), and before it writes that other
+// copy again waits for the grace period: every chunk published before the flip has completed
+// (wait_grace()), so no wave still reads it.  A lookup therefore never sees a half-written
+// bucket, without retries or per-bucket locks on the packet path.  The small tables staged in LDS
+// (ports, chains, ACL) still take the stop -> drain -> relaunch path.
 #pragma once
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <mutex>
 #include <vector>
 
 #include "host.h"
@@ -36,10 +46,19 @@ namespace nfdp {
 // Bit 63 of the published-packet counter is the stop flag: one 64-bit word carries both, so a
 // wave that sees "stop" also sees the final count (no ordering between two words to get right).
 constexpr uint64_t kRingStop = 1ull << 63;
+constexpr uint32_t kRingEpochBits = 7;
+constexpr uint64_t kRingEpochMask = (1ull << kRingEpochBits) - 1;
+// published word = stop | count << 7 | epoch: count-major, so the frontier's atomic max keeps
+// the newest count whatever the epoch does (the epoch only changes with a new count or in place)
+__host__ __device__ inline uint64_t ring_word(uint64_t count, uint32_t epoch) {
+  return (count << kRingEpochBits) | (epoch & kRingEpochMask);
+}
+__host__ __device__ inline uint64_t ring_count(uint64_t w) { return (w & ~kRingStop) >> kRingEpochBits; }
+__host__ __device__ inline uint32_t ring_epoch(uint64_t w) { return (uint32_t)(w & kRingEpochMask); }
 
 // Host -> device control block, pinned coherent host memory (one 64-B line).
 struct alignas(64) RingCtl {
-  uint64_t prod;   // packets published (cumulative, multiple of 64) | kRingStop
+  uint64_t prod;   // ring_word(packets published, epoch) | kRingStop
   uint32_t pad[14];
 };
 static_assert(sizeof(RingCtl) == 64, "RingCtl");
@@ -47,8 +66,8 @@ static_assert(sizeof(RingCtl) == 64, "RingCtl");
 // Device-resident ring state (HBM): the ticket counter and the prod mirror on separate 128-B
 // lines, so claim atomics and the waiters' polls do not contend for one line.
 struct alignas(128) RingDevState {
-  uint32_t claim;  // next chunk ticket
-  uint32_t pad0[31];
+  uint64_t claim;  // next chunk ticket (64-bit: tickets never wrap)
+  uint32_t pad0[30];
   uint64_t dprod;  // device mirror of ctl.prod (advanced by the frontier wave), bit 63 = stop
   uint32_t pad1[30];
 };
@@ -76,17 +95,33 @@ class RingEngine {
   uint32_t* dev_svc() const { return d_svc_; }  // per-chunk device service time (ticks, 100 MHz)
 
   // Launch the persistent kernel over the tables/counters in `f` (pkts/out/n are ignored).
-  void start(const FusedLaunch& f, const LaunchCfg& cfg, double deadline_s);
+  // flows_alt: the second flow-table copy (epoch & 1 == 1); null = single copy (no live flips).
+  void start(const FusedLaunch& f, const LaunchCfg& cfg, double deadline_s, const void* flows_alt = nullptr);
   // Drain published chunks, stop every wave, wait for the grid to exit (throws on timeout).
   void stop(double timeout_s = 30.0);
 
-  uint64_t published() const { return prod_; }
+  uint64_t published() const {
+    std::lock_guard<std::mutex> g(mu_);
+    return prod_;
+  }
   uint64_t completed();  // packets whose chunks all completed (in order)
   // Publish n packets (multiple of 64) starting at ring position published() % capacity.
   // Throws if the ring lacks room (producer must wait for completions).
   uint64_t publish(uint32_t n);
   // Spin until every chunk below `end` completed; false on timeout.
   bool wait(uint64_t end, double timeout_s);
+
+  // Epoch flip (see the header comment): the waves switch to flow-table copy `epoch & 1` for
+  // every chunk published from now on.  Throws unless the previous flip's grace period is over.
+  uint32_t flip();
+  // Grace period of the last flip: every chunk published before it has completed.
+  bool grace_over() { return completed() >= flip_prod(); }
+  bool wait_grace(double timeout_s);
+  uint32_t epoch() const {
+    std::lock_guard<std::mutex> g(mu_);
+    return epoch_;
+  }
+  void set_epoch(uint32_t e);   // only while stopped
 
   // Closed-loop probe run entirely in C++ (no Python in the timed loop): `batches` batches of
   // `batch` packets, at most `inflight` outstanding.  Returns per-batch publish->completion
@@ -95,6 +130,13 @@ class RingEngine {
 
  private:
   bool chunk_done(uint64_t chunk) const;
+  uint64_t flip_prod() const {
+    std::lock_guard<std::mutex> g(mu_);
+    return flip_prod_;
+  }
+  // publish / flip / completion scans may come from different host threads (a producer thread
+  // and the control plane's commit): the host-side ring state is guarded
+  mutable std::mutex mu_;
   uint32_t cap_, nch_;
   int num_cus_, wgs_;
   bool coop_;
@@ -111,6 +153,8 @@ class RingEngine {
   hipStream_t stream_{};
   uint64_t prod_ = 0;             // host copy of ctl->prod
   uint64_t floor_ = 0;            // chunks < floor_ are complete
+  uint32_t epoch_ = 0;            // current flow-table epoch (copy epoch_ & 1)
+  uint64_t flip_prod_ = 0;        // packets published before the last flip
   bool running_ = false;
 };
 
@@ -121,6 +165,7 @@ struct RingLaunch {
   uint32_t ring_mask;
   RingCtl* ctl; uint32_t* flags; RingDevState* st; uint32_t* svc;
   unsigned long long deadline_ticks;
+  const void* flows_alt;  // second flow-table copy (epoch & 1 == 1); f.t.flows is copy 0
 };
 hipError_t launch_ring(const RingLaunch& r, const LaunchCfg& cfg, int wgs_per_cu, bool coop, hipStream_t s);
 

@@ -25,6 +25,7 @@ struct RingArgs {
   const v4i* acl_wfrag; const v4i* acl_cinit; uint32_t acl_tiles;
   const v4i* toep_frag; const uint32_t* toep_tab;
   unsigned long long deadline;
+  const void* flows2[2];  // flow-table copies by epoch parity (the same pointer twice if not double buffered)
   uint32_t flags_bits;  // bit2: no per-flow counts; bits 5/6: diagnostics (kRingTrace, kRingNoCounters)
 };
 // Frames are read and written with system-coherent buffer ops (sc0 sc1): the loads never hit a
@@ -94,18 +95,18 @@ __device__ __forceinline__ unsigned long long rfl64(unsigned long long v) {
 // into a hot spot that slows the waves doing work.
 template <class OnIdle>
 __device__ __forceinline__ bool ring_wait_chunk(const RingArgs& a, uint32_t lane, unsigned long long t_begin,
-                                                uint32_t& tk_out, OnIdle on_idle) {
-  uint32_t tk = 0;
-  if (lane == 0) tk = atomicAdd(&a.st->claim, 1u);
-  tk = __builtin_amdgcn_readfirstlane(tk);
+                                                unsigned long long& tk_out, uint32_t& epoch_out, OnIdle on_idle) {
+  unsigned long long tk = 0;
+  if (lane == 0) tk = atomicAdd(&a.st->claim, 1ull);
+  tk = rfl64(tk);
   tk_out = tk;
-  const unsigned long long first = (unsigned long long)tk * 64ull;
+  const unsigned long long first = tk * 64ull;
   const unsigned long long need = first + 64ull;
   for (;;) {
     unsigned long long v = 0;
     if (lane == 0) {
       v = __hip_atomic_load(&a.st->dprod, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if ((v & ~kRingStop) < need && v == first) {
+      if (ring_count(v) < need && ring_count(v) == first && !(v & kRingStop)) {
         // frontier wave (its chunk is the first unpublished one): the only PCIe poller
         const unsigned long long hv = __hip_atomic_load(&a.ctl->prod, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         if (hv > v) {
@@ -115,8 +116,14 @@ __device__ __forceinline__ bool ring_wait_chunk(const RingArgs& a, uint32_t lane
       }
     }
     v = rfl64(v);
-    const unsigned long long avail = v & ~kRingStop;
-    if (avail >= need) return true;
+    const unsigned long long avail = ring_count(v);
+    if (avail >= need) {
+      // the word that published this chunk (or a later one) names the flow-table copy: a word
+      // older than the last flip has count <= the flip point, so only chunks below it (the
+      // grace period's) can still use the previous copy
+      epoch_out = ring_epoch(v);
+      return true;
+    }
     on_idle();                        // no published work for this wave: settle its bookkeeping
     if (v & kRingStop) return false;  // stop and final count come in one word: nothing more will arrive
     if (__builtin_amdgcn_s_memrealtime() - t_begin > a.deadline) return false;
@@ -136,7 +143,8 @@ __device__ __forceinline__ bool ring_wait_chunk(const RingArgs& a, uint32_t lane
 template <int HASH, int ACL, bool COOP>
 __global__ __launch_bounds__(kRingBlock) void ring_kernel(RingArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  __shared__ uint32_t coop_ctl[2];                            // ticket, go
+  __shared__ unsigned long long coop_tk;                      // ticket
+  __shared__ uint32_t coop_ctl[2];                            // go, epoch
   __shared__ uint32_t coop_best[COOP ? kRingWaves : 1][64];   // per-wave ACL partial minima
   const RingLds L = ring_lds(HASH, ACL, a.acl_tiles);
   v4i* lw = reinterpret_cast<v4i*>(smem + L.acl_w);
@@ -182,17 +190,19 @@ __global__ __launch_bounds__(kRingBlock) void ring_kernel(RingArgs a) {
   const unsigned long long t_begin = __builtin_amdgcn_s_memrealtime();
 
   for (;;) {
-    uint32_t tk = 0;
+    unsigned long long tk = 0;
+    uint32_t epoch = 0;
     if constexpr (COOP) {
       if (wave == 0) {
-        const bool go = ring_wait_chunk(a, lane, t_begin, tk, on_idle);
-        if (lane == 0) { coop_ctl[0] = tk; coop_ctl[1] = go ? 1u : 0u; }
+        const bool go = ring_wait_chunk(a, lane, t_begin, tk, epoch, on_idle);
+        if (lane == 0) { coop_tk = tk; coop_ctl[0] = go ? 1u : 0u; coop_ctl[1] = epoch; }
       }
       __syncthreads();
-      tk = __builtin_amdgcn_readfirstlane(coop_ctl[0]);
-      if (!__builtin_amdgcn_readfirstlane(coop_ctl[1])) break;
+      tk = rfl64(coop_tk);
+      epoch = __builtin_amdgcn_readfirstlane(coop_ctl[1]);
+      if (!__builtin_amdgcn_readfirstlane(coop_ctl[0])) break;
     } else {
-      if (!ring_wait_chunk(a, lane, t_begin, tk, on_idle)) break;
+      if (!ring_wait_chunk(a, lane, t_begin, tk, epoch, on_idle)) break;
     }
     const unsigned long long t_avail = __builtin_amdgcn_s_memrealtime();
     const bool trace = (a.flags_bits & kRingTrace) != 0 && wave == 0;
@@ -204,9 +214,10 @@ __global__ __launch_bounds__(kRingBlock) void ring_kernel(RingArgs a) {
   }
 
     // ---- one packet per lane: the fused kernel's stages ----
-    const uint32_t i = (tk * 64u + lane) & a.ring_mask;
+    const uint32_t tk32 = (uint32_t)tk;  // slot / flag positions are modulo the ring (<= 2^24 slots)
+    const uint32_t i = (tk32 * 64u + lane) & a.ring_mask;
     // the chunk's 64 slots are one 4-KiB run: lane-contiguous loads, transposed through LDS
-    const uint32_t run = __builtin_amdgcn_readfirstlane(((tk * 64u) & a.ring_mask) * 64u);
+    const uint32_t run = __builtin_amdgcn_readfirstlane(((tk32 * 64u) & a.ring_mask) * 64u);
     uint32_t d[kSlotDwords];
     {
       v4u c[4];
@@ -238,7 +249,9 @@ __global__ __launch_bounds__(kRingBlock) void ring_kernel(RingArgs a) {
     int64_t slot = -1;
     if (!st.reason && p.ipv4) {
       uint4 v;
-      slot = flow_probe(a.t, st.key, hash, v);
+      TablesView tv = a.t;
+      tv.flows = static_cast<const FlowSlot*>(a.flows2[epoch & 1u]);
+      slot = flow_probe(tv, st.key, hash, v);
       if (slot >= 0) {
         hit = true;
         act.chain_id = v.x & 0xFFFFu; act.out_port = v.x >> 16; act.nat_ip = v.y;
@@ -258,8 +271,8 @@ __global__ __launch_bounds__(kRingBlock) void ring_kernel(RingArgs a) {
     __builtin_amdgcn_s_waitcnt(0);
     NFDP_RING_MARK(tr4)
     if (lane == 0) {
-      if (a.svc) a.svc[(size_t)(tk & nch_mask) * kSvcWords + 7] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_avail);
-      __hip_atomic_store(&a.flags[tk & nch_mask], tk + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (a.svc) a.svc[(size_t)(tk32 & nch_mask) * kSvcWords + 7] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_avail);
+      __hip_atomic_store(&a.flags[tk32 & nch_mask], tk32 + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 
     // ---- counters, off the latency path (after the flag): port / drop counters into the
@@ -284,7 +297,7 @@ __global__ __launch_bounds__(kRingBlock) void ring_kernel(RingArgs a) {
     NFDP_RING_MARK(tr5)
 #undef NFDP_RING_MARK
     if (trace && lane == 0 && a.svc) {
-      uint32_t* sv = a.svc + (size_t)(tk & nch_mask) * kSvcWords;
+      uint32_t* sv = a.svc + (size_t)(tk32 & nch_mask) * kSvcWords;
       sv[0] = tr0; sv[1] = tr1; sv[2] = tr2; sv[3] = tr3; sv[4] = tr4; sv[5] = tr5; sv[6] = 0;
     }
   }
@@ -320,6 +333,8 @@ hipError_t launch_ring(const RingLaunch& r, const LaunchCfg& cfg, int wgs_per_cu
   a.toep_frag = reinterpret_cast<const v4i*>(r.f.toep_frag);
   a.toep_tab = r.f.toep_tab;
   a.deadline = r.deadline_ticks;
+  a.flows2[0] = r.f.t.flows;
+  a.flows2[1] = r.flows_alt ? r.flows_alt : r.f.t.flows;
   a.flags_bits = r.f.flags;
   if (!a.port_ctr || !a.drop_ctr || !a.ctl || !a.flags || !a.st) return hipErrorInvalidValue;
   if (((r.ring_mask + 1) & r.ring_mask) != 0 || r.ring_mask < 63) return hipErrorInvalidValue;
@@ -405,15 +420,15 @@ RingEngine::~RingEngine() {
   (void)hipHostFree(flags_);
 }
 
-void RingEngine::start(const FusedLaunch& f, const LaunchCfg& cfg, double deadline_s) {
+void RingEngine::start(const FusedLaunch& f, const LaunchCfg& cfg, double deadline_s, const void* flows_alt) {
   if (running_) throw std::runtime_error("ring: already running");
   if (!(deadline_s > 0.0) || deadline_s > 3600.0) throw std::invalid_argument("ring: deadline in (0, 3600] s");
   if (completed() != prod_) throw std::runtime_error("ring: previous session left chunks unprocessed");
   // resume at the published position: tickets restart at prod/64, nothing outstanding
   RingDevState s{};
-  s.claim = (uint32_t)(prod_ / 64);
-  s.dprod = prod_;
-  __atomic_store_n(&ctl_->prod, prod_, __ATOMIC_RELEASE);
+  s.claim = prod_ / 64;
+  s.dprod = ring_word(prod_, epoch_);
+  __atomic_store_n(&ctl_->prod, ring_word(prod_, epoch_), __ATOMIC_RELEASE);
   ck(hipMemcpyAsync(st_, &s, sizeof(s), hipMemcpyHostToDevice, stream_), "state upload");
   ck(hipStreamSynchronize(stream_), "state upload");  // `s` lives on this stack frame
   RingLaunch r;
@@ -429,13 +444,17 @@ void RingEngine::start(const FusedLaunch& f, const LaunchCfg& cfg, double deadli
   r.st = st_;
   r.svc = d_svc_;
   r.deadline_ticks = (unsigned long long)(deadline_s * 1e8);  // s_memrealtime: 100 MHz
+  r.flows_alt = flows_alt;
   ck(launch_ring(r, cfg, wgs_, coop_, stream_), "launch");
   running_ = true;
 }
 
 void RingEngine::stop(double timeout_s) {
   if (!running_) return;
-  __atomic_store_n(&ctl_->prod, prod_ | kRingStop, __ATOMIC_RELEASE);
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    __atomic_store_n(&ctl_->prod, ring_word(prod_, epoch_) | kRingStop, __ATOMIC_RELEASE);
+  }
   const auto t0 = Clock::now();
   for (;;) {
     const hipError_t q = hipStreamQuery(stream_);
@@ -445,8 +464,7 @@ void RingEngine::stop(double timeout_s) {
     std::this_thread::sleep_for(std::chrono::microseconds(50));
   }
   running_ = false;
-  (void)completed();
-  if (floor_ * 64 != prod_) throw std::runtime_error("ring: stopped with published chunks unprocessed");
+  if (completed() != published()) throw std::runtime_error("ring: stopped with published chunks unprocessed");
 }
 
 bool RingEngine::chunk_done(uint64_t chunk) const {
@@ -454,6 +472,7 @@ bool RingEngine::chunk_done(uint64_t chunk) const {
 }
 
 uint64_t RingEngine::completed() {
+  std::lock_guard<std::mutex> g(mu_);
   const uint64_t end = prod_ / 64;
   while (floor_ < end && chunk_done(floor_)) ++floor_;
   return floor_ * 64;
@@ -462,14 +481,44 @@ uint64_t RingEngine::completed() {
 uint64_t RingEngine::publish(uint32_t n) {
   if (!running_) throw std::runtime_error("ring: not running");
   if (n == 0 || (n & 63u)) throw std::invalid_argument("ring: publish a positive multiple of 64 packets");
-  if (prod_ + n - completed() > cap_) throw std::runtime_error("ring: no room (wait for completions)");
+  const uint64_t done = completed();
+  std::lock_guard<std::mutex> g(mu_);
+  if (prod_ + n - done > cap_) throw std::runtime_error("ring: no room (wait for completions)");
   prod_ += n;
-  __atomic_store_n(&ctl_->prod, prod_, __ATOMIC_RELEASE);
+  __atomic_store_n(&ctl_->prod, ring_word(prod_, epoch_), __ATOMIC_RELEASE);
   return prod_;
 }
 
+uint32_t RingEngine::flip() {
+  if (!grace_over()) throw std::runtime_error("ring: flip before the previous flip's grace period ended");
+  std::lock_guard<std::mutex> g(mu_);
+  epoch_ = (epoch_ + 1) & (uint32_t)kRingEpochMask;
+  flip_prod_ = prod_;
+  // same count, new epoch: chunks published from here on carry it (the frontier mirrors a word
+  // only when its count grows, so this store alone changes nothing for waiting waves)
+  if (running_) __atomic_store_n(&ctl_->prod, ring_word(prod_, epoch_), __ATOMIC_RELEASE);
+  return epoch_;
+}
+
+bool RingEngine::wait_grace(double timeout_s) {
+  const auto t0 = Clock::now();
+  uint32_t spin = 0;
+  while (!grace_over()) {
+    _mm_pause();
+    if ((++spin & 1023u) == 0 && secs(t0, Clock::now()) > timeout_s) return false;
+  }
+  return true;
+}
+
+void RingEngine::set_epoch(uint32_t e) {
+  if (running_) throw std::runtime_error("ring: set_epoch while running");
+  std::lock_guard<std::mutex> g(mu_);
+  epoch_ = e & (uint32_t)kRingEpochMask;
+  flip_prod_ = prod_;
+}
+
 bool RingEngine::wait(uint64_t end, double timeout_s) {
-  if (end > prod_) throw std::invalid_argument("ring: waiting for unpublished packets");
+  if (end > published()) throw std::invalid_argument("ring: waiting for unpublished packets");
   const auto t0 = Clock::now();
   uint32_t spin = 0;
   while (completed() < end) {

@@ -83,6 +83,9 @@ class DataPlane:
         self.MAX_LAUNCH = 1 << 24
         self.flow_totals = np.zeros((self.flows.nbuckets * 4, 2), np.uint64)
         self.latency = LatencyStats()   # packet-path latency histograms (utils/latency.py)
+        self._flow_active = 0           # flow-table copy in use (double buffered under running rings)
+        self._flow_lag = np.zeros(0, np.int64)
+        self.flip_stats = {"flips": 0, "grace_s": 0.0, "update_s": 0.0, "buckets": 0}
         # side outputs (flood / mirror / ARP replicas, learn events) and MAC learning state
         self.cap_rep, self.cap_learn = 1 << 16, 1 << 14
         self.stamp = 0                 # batch counter: the learned entries' last-seen stamp
@@ -138,11 +141,17 @@ class DataPlane:
 
     # ------------------------------------------------------------------ commit
     def commit(self, full: bool = False) -> dict:
-        """Push host table changes to the device.  Returns what was sent."""
+        """Push host table changes to the device.  Returns what was sent.
+
+        With resident ring kernels (dataplane/ring.py) running: a commit that changes only flows
+        is applied under the running rings by an epoch flip of the double-buffered flow table
+        (`_commit_flows_live`, no stall); any other change drains and stops the rings, updates the
+        tables and relaunches them (their small tables are staged in LDS at launch)."""
         FAULTS.check("dataplane.commit")
-        # resident ring kernels (dataplane/ring.py) staged the old tables: drain and stop them
-        # before any buffer is replaced, relaunch them over the new version afterwards
         rings = [r for r in getattr(self, "_rings", []) if r.running]
+        if rings and not full and self._only_flows_pending():
+            with TRACER.span("dataplane.commit_live"):
+                return self._commit_flows_live(rings)
         for r in rings:
             r.stop()
         with TRACER.span("dataplane.commit", full=full):
@@ -153,13 +162,73 @@ class DataPlane:
                 r.resume()
         return sent
 
+    def _models(self):
+        return (("ports", self.ports), ("chains", self.chains), ("macs", self.macs), ("lag", self.lag),
+                ("flood", self.flood), ("nexthops", self.nexthops), ("ecmp", self.ecmp),
+                ("tunnels", self.tunnels), ("terms", self.terms))
+
+    def _only_flows_pending(self) -> bool:
+        """True when the device is current in everything but (possibly) flow buckets."""
+        if "flows" not in self._dev or "rss_key" not in self._dev or "acl_value" not in self._dev:
+            return False
+        if any(self._versions.get(n) != m.version or n not in self._dev for n, m in self._models()):
+            return False
+        if len(self.routes) and (self._versions.get("routes") != self.routes.version or "lpm24" not in self._dev):
+            return False
+        return self._versions.get("acl") == self.acl.version
+
+    # ------------------------------------------------------------------ live flow updates
+    # Double-buffered flow table: copy 0 = "flows", copy 1 = "flows_b"; tables_ptrs() and the
+    # batch path use copy `_flow_active`, a ring kernel the copy its chunk's epoch names.  An
+    # update writes the inactive copy (the rows changed by this commit plus those the copy missed
+    # at the previous flip), flips, and the next update first waits for the flip's grace period.
+    def enable_flow_flip(self) -> None:
+        if not self.gpu or "flows_b" in self._dev:
+            return
+        self.commit()
+        self._dev["flows_b"] = self._dev["flows"].clone()
+        self._flow_lag = np.zeros(0, np.int64)
+
+    def _flows_key(self, copy: int) -> str:
+        return "flows_b" if copy else "flows"
+
+    def flow_copy_ptrs(self) -> tuple[int, int]:
+        return self._ptr("flows"), self._ptr("flows_b") or self._ptr("flows")
+
+    def _commit_flows_live(self, rings) -> dict:
+        ft = self.flows.t
+        dirty = ft.take_dirty()
+        moves = ft.take_moves()
+        if not len(dirty):
+            return {}
+        if moves:
+            self.harvest()  # counters of moved slots are attributed before the move
+        if "flows_b" not in self._dev:
+            raise RuntimeError("live flow updates need enable_flow_flip() before the rings start")
+        t0 = time.perf_counter()
+        for r in rings:
+            if not r.eng.wait_grace(10.0):
+                raise TimeoutError("ring: grace period of the previous flow-table flip did not end")
+        t1 = time.perf_counter()
+        rows = np.union1d(dirty, self._flow_lag)
+        inactive = self._flow_active ^ 1
+        self._push_buckets(rows, self._flows_key(inactive))
+        _torch().cuda.current_stream(self.tdev).synchronize()   # the copy is complete before any wave can pick it
+        self._flow_active = inactive
+        for r in rings:
+            r.eng.flip()
+        self._flow_lag = dirty
+        self.flip_stats["flips"] += 1
+        self.flip_stats["grace_s"] += t1 - t0
+        self.flip_stats["update_s"] += time.perf_counter() - t1
+        self.flip_stats["buckets"] += int(len(rows))
+        return {"flow_buckets": int(len(dirty)), "flip": self._flow_active}
+
     def _commit(self, full: bool) -> dict:
         sent = {}
         if self._learned_on_device and (full or self._versions.get("macs") != self.macs.version):
             self.pull_learned()  # the host re-uploads the MAC table: keep what the GPU learned
-        for name, model in (("ports", self.ports), ("chains", self.chains), ("macs", self.macs), ("lag", self.lag),
-                            ("flood", self.flood), ("nexthops", self.nexthops), ("ecmp", self.ecmp),
-                            ("tunnels", self.tunnels), ("terms", self.terms)):
+        for name, model in self._models():
             if full or self._versions.get(name) != model.version or name not in self._dev:
                 self._buf(name, model.a)
                 self._versions[name] = model.version
@@ -193,6 +262,9 @@ class DataPlane:
         if full or "flows" not in self._dev:
             self.harvest()
             self._buf("flows", ft.slots())
+            if "flows_b" in self._dev:   # both copies current: nothing lags
+                self._buf("flows_b", ft.slots())
+                self._flow_lag = np.zeros(0, np.int64)
             ft.clear_dirty()
             sent["flows_full"] = len(self.flows)
         else:
@@ -202,10 +274,13 @@ class DataPlane:
                 if moves:
                     self.harvest()  # counters of moved slots are attributed before the move
                 sent["flow_buckets"] = int(len(dirty))
-                self._push_buckets(dirty)
+                self._push_buckets(np.union1d(dirty, self._flow_lag) if "flows_b" in self._dev else dirty, "flows")
+                if "flows_b" in self._dev:
+                    self._push_buckets(np.union1d(dirty, self._flow_lag), "flows_b")
+                    self._flow_lag = np.zeros(0, np.int64)
         return sent
 
-    def _push_buckets(self, dirty: np.ndarray) -> None:
+    def _push_buckets(self, dirty: np.ndarray, dst: str = "flows") -> None:
         ft = self.flows.t
         rows = ft.slots().reshape(-1, 32)[dirty]   # whole 128-B buckets
         if self.gpu:
@@ -213,16 +288,16 @@ class DataPlane:
             up = {k: torch.from_numpy(np.ascontiguousarray(v).view(np.uint8).reshape(-1).copy()).to(self.tdev)
                   for k, v in (("idx", dirty.astype(np.uint32)), ("rows", rows))}
             s = torch.cuda.current_stream(self.tdev).cuda_stream
-            self.nf.launch_bucket_update(up["idx"].data_ptr(), len(dirty), up["rows"].data_ptr(), self._ptr("flows"),
+            self.nf.launch_bucket_update(up["idx"].data_ptr(), len(dirty), up["rows"].data_ptr(), self._ptr(dst),
                                          ft.mask, s)
             self._keepalive = up
         else:
-            self._dev["flows"].view(np.uint32).reshape(-1, 32)[dirty] = rows
+            self._dev[dst].view(np.uint32).reshape(-1, 32)[dirty] = rows
 
     def tables_ptrs(self) -> dict:
         return {
             "ports": self._ptr("ports"), "chains": self._ptr("chains"), "n_chains": int(self.chains.n),
-            "flows": self._ptr("flows"),
+            "flows": self._ptr(self._flows_key(self._flow_active)),
             "bucket_mask": int(self.flows.t.mask), "macs": self._ptr("macs"), "mac_mask": int(self.macs.mask),
             "rss_key": self._ptr("rss_key"), "acl_value": self._ptr("acl_value"), "acl_mask": self._ptr("acl_mask"),
             "acl_permit": self._ptr("acl_permit"), "n_acl": int(getattr(self, "_n_acl", 0)),

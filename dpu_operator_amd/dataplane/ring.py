@@ -20,8 +20,13 @@ Usage::
     out, meta = ring.results()
 
 While a ring runs, do NOT synchronize the whole device (torch.cuda.synchronize(), a blocking
-copy on the default stream): that waits for the resident kernel.  `DataPlane.commit()` restarts
-active rings itself so a table update never races a running session.
+copy on the default stream): that waits for the resident kernel.
+
+Table updates while rings run (`DataPlane.commit()`): flow inserts / erases / action changes are
+applied without stopping the rings — the flow table is double buffered on the device, the commit
+writes the copy no wave reads and flips the epoch carried by the published word; the next commit
+first waits for the flip's grace period (every chunk published before it completed; ring.h).
+Changes to the LDS-staged tables (ports, chains, ACL, ...) drain, stop and relaunch the rings.
 """
 from __future__ import annotations
 
@@ -90,10 +95,17 @@ class RingPath:
     def running(self) -> bool:
         return bool(self.eng.running)
 
+    def _tables(self) -> dict:
+        t = self.dp.tables_ptrs()
+        t["flows"], t["flows_alt"] = self.dp.flow_copy_ptrs()   # copies by epoch parity
+        return t
+
     def start(self) -> None:
+        self.dp.enable_flow_flip()   # commits; second flow-table copy for live updates
         self.dp.commit()
         _torch().cuda.current_stream(self.dp.tdev).synchronize()  # tables are in HBM before launch
-        self.eng.start(self.dp.tables_ptrs(), self._args(), self.dp.hash_mode, self.dp.acl_mode,
+        self.eng.set_epoch(self.dp._flow_active)
+        self.eng.start(self._tables(), self._args(), self.dp.hash_mode, self.dp.acl_mode,
                        int(self.dp.num_cus), self.deadline_s)
 
     def stop(self, timeout_s: float = 30.0) -> None:
@@ -101,7 +113,8 @@ class RingPath:
 
     def resume(self) -> None:
         """Relaunch over the current device tables (DataPlane.commit stops, updates, resumes)."""
-        self.eng.start(self.dp.tables_ptrs(), self._args(), self.dp.hash_mode, self.dp.acl_mode,
+        self.eng.set_epoch(self.dp._flow_active)
+        self.eng.start(self._tables(), self._args(), self.dp.hash_mode, self.dp.acl_mode,
                        int(self.dp.num_cus), self.deadline_s)
 
     def publish(self, n: int) -> int:
@@ -128,6 +141,18 @@ class RingPath:
         meta = np.empty(self.capacity, np.uint32)
         self.dp.nf.memcpy(out.ctypes.data, self.eng.dev_out(), out.nbytes)
         self.dp.nf.memcpy(meta.ctypes.data, self.eng.dev_meta(), meta.nbytes)
+        return out, meta
+
+    def peek(self, start: int = 0, n: int | None = None) -> tuple[np.ndarray, np.ndarray]:
+        """Egress slots / metadata of ring slots [start, start + n) while the ring may run: only
+        slots of completed chunks that no later publish reused hold meaningful data."""
+        n = self.capacity - start if n is None else n
+        if start < 0 or n < 0 or start + n > self.capacity:
+            raise ValueError("peek range outside the ring")
+        out = np.empty((n, 64), np.uint8)
+        meta = np.empty(n, np.uint32)
+        self.dp.nf.memcpy_nb(out.ctypes.data, self.eng.dev_out() + 64 * start, out.nbytes)
+        self.dp.nf.memcpy_nb(meta.ctypes.data, self.eng.dev_meta() + 4 * start, meta.nbytes)
         return out, meta
 
     def service_ticks(self, phases: bool = False) -> np.ndarray:

@@ -121,10 +121,10 @@ def build_sfc(
 
 
 def traffic(sc: Scenario, n: int, seed: int = 1, flows: np.ndarray | None = None, frame_len: int = 60,
-            src_pods: np.ndarray | None = None) -> tuple[np.ndarray, np.ndarray]:
+            src_pods: np.ndarray | None = None, return_flows: bool = False):
     """n packets of uniformly random flows (optionally restricted to `flows` indices, or to flows
     whose source pod is in `src_pods`): tagged 64-B frames from the source pod's VF.
-    Returns (slots uint8[n,64], inmeta uint32[n])."""
+    Returns (slots uint8[n,64], inmeta uint32[n]) [, flow index per packet]."""
     rng = np.random.default_rng(seed)
     pool = flows
     if src_pods is not None:
@@ -145,6 +145,8 @@ def traffic(sc: Scenario, n: int, seed: int = 1, flows: np.ndarray | None = None
         frame_len=frame_len,
         payload_seed=seed,
     )
+    if return_flows:
+        return slots, P.inmeta(sc.pod_port[s], lens), f
     return slots, P.inmeta(sc.pod_port[s], lens)
 
 

@@ -694,5 +694,8 @@ class FlowTable:
     def erase(self, key) -> bool:
         return self.t.erase(tuple(int(x) for x in key))
 
+    def erase_many(self, keys: np.ndarray) -> int:
+        return int(self.t.erase_many(np.ascontiguousarray(keys, np.uint32)))
+
     def find(self, key) -> int:
         return self.t.find(tuple(int(x) for x in key))
