@@ -74,11 +74,17 @@ NFDP_HD int acl_rule_of(uint32_t b, uint32_t n_acl) {
 // Prefilter: a tile (and a group of 8 tiles) carries the bits ALL its rules care about and agree
 // on; a wave skips it - no LDS reads, no MFMAs - unless one of its packets has those bits.
 // The MFMA Toeplitz hash keeps the i8 form (it needs the parity of integer sums).
-template <int HASH, int ACL>
+struct NoHashHook {
+  __device__ void operator()(uint32_t) const {}
+};
+
+template <int HASH, int ACL, class OnHash = NoHashHook>
 __device__ __forceinline__ void classify_wave(const FlowKey& key, uint4* kx, const AclView& av, const v4i* lt,
                                               const uint32_t* ltab, const TablesView& t,
                                               uint32_t& hash, int& acl_rule, uint32_t tile0 = 0,
-                                              uint32_t tstep = 1, uint32_t* best_out = nullptr) {
+                                              uint32_t tstep = 1, uint32_t* best_out = nullptr,
+                                              OnHash on_hash = OnHash{}) {
+  // on_hash(hash) runs between the hash and the ACL (e.g. to issue the flow-bucket fetch early)
   // tile0 / tstep: this wave scans rule tiles tile0, tile0 + tstep, ... (cooperating waves split
   // one chunk's ACL); best_out: the raw (mismatch << 12 | rule) minimum, for combining partials.
   const uint32_t lane = threadIdx.x & 63u;
@@ -138,6 +144,7 @@ __device__ __forceinline__ void classify_wave(const FlowKey& key, uint4* kx, con
   } else {
     hash = toeplitz_scalar(key, t.rss_key);
   }
+  on_hash(hash);
   // ---- ACL (TCAM) ----
   if constexpr (ACL == kAclMfma) {
     uint32_t best[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
@@ -307,20 +314,43 @@ __device__ __forceinline__ int64_t flow_probe(const TablesView& t, const FlowKey
 // the matching slot's action lane hands its chunk over through the same scratch.  Packets with
 // no match in the first bucket probe the second one per lane (flow_probe's tail; rare at the
 // table's <= 50 % load).  Same results as flow_probe.  `probe` false -> slot -1.  EXEC full.
-__device__ __forceinline__ int64_t flow_probe_wave(const TablesView& t, const FlowKey& k, uint32_t h, bool probe,
-                                                   uint4* kx, uint4& act) {
+// The probe in two halves, so the bucket fetch can be issued as soon as the hash is known and
+// its latency overlap the ACL classification (fused kernel, NFDP_PROBE_EARLY): issue = the eight
+// wave-cooperative line loads, finish = key compare, action hand-over and the second choice.
+#ifndef NFDP_PROBE_AUX
+#define NFDP_PROBE_AUX -1   // >= 0: bucket loads as raw buffer loads with these cache-policy bits
+#endif
+__device__ __forceinline__ void flow_probe_issue(const TablesView& t, uint32_t h, uint4 (&v)[8]) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t c = lane & 7u, q = lane >> 3;
+  const uint32_t b1 = h & t.bucket_mask;
+#if NFDP_PROBE_AUX >= 0
+  const __amdgpu_buffer_rsrc_t r_fl = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)t.flows, (short)0, (int)((t.bucket_mask + 1u) * (uint32_t)(kBucketSlots * 32)), 0x00020000);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const uint32_t bj = (uint32_t)__shfl((int)b1, 8 * j + (int)q);
+    v[j] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r_fl, bj * (uint32_t)(kBucketSlots * 32) + c * 16u,
+                                                                          0, NFDP_PROBE_AUX));
+  }
+#else
+  const uint4* fl = reinterpret_cast<const uint4*>(t.flows);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const uint32_t bj = (uint32_t)__shfl((int)b1, 8 * j + (int)q);
+    v[j] = fl[(size_t)bj * (kBucketSlots * 2) + c];
+  }
+#endif
+}
+
+__device__ __forceinline__ int64_t flow_probe_finish(const TablesView& t, const FlowKey& k, uint32_t h, bool probe,
+                                                     uint4* kx, const uint4 (&v)[8], uint4& act) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t c = lane & 7u, q = lane >> 3;
   const uint32_t b1 = h & t.bucket_mask;
   const uint4* fl = reinterpret_cast<const uint4*>(t.flows);
   // key as stored (meta | used); a non-probing packet gets a w no slot can hold
   kx[lane] = make_uint4(k.src_ip, k.dst_ip, k.ports, probe ? (k.meta | kSlotUsed) : 0xFFFFFFFFu);
-  uint4 v[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const uint32_t bj = (uint32_t)__shfl((int)b1, 8 * j + (int)q);
-    v[j] = fl[(size_t)bj * (kBucketSlots * 2) + c];
-  }
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
   // Per instruction j: compare, then the action lane of a matching slot overwrites packet
@@ -360,6 +390,13 @@ __device__ __forceinline__ int64_t flow_probe_wave(const TablesView& t, const Fl
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
   return slot;
+}
+
+__device__ __forceinline__ int64_t flow_probe_wave(const TablesView& t, const FlowKey& k, uint32_t h, bool probe,
+                                                   uint4* kx, uint4& act) {
+  uint4 v[8];
+  flow_probe_issue(t, h, v);
+  return flow_probe_finish(t, k, h, probe, kx, v, act);
 }
 
 // Sum of a u32 over the 64 lanes (EXEC must be full): two quad permutes and two row rotates

@@ -26,6 +26,20 @@ namespace nfdp {
 #ifndef NFDP_FUSED_BLOCK
 #define NFDP_FUSED_BLOCK 512
 #endif
+// Early bucket fetch (EARLY instances): the flow-bucket loads are issued between the hash and the
+// ACL, so their latency runs under the rule-tile MFMA chain.  Holding the eight bucket lines
+// through the ACL needs ~170 VGPRs, i.e. 2 waves / SIMD instead of 4: it pays when the ACL is
+// long (many rule tiles survive the prefilter) and loses when it is short, so the launcher picks
+// it from the rule-tile count (kEarlyAclTiles).
+#ifndef NFDP_EARLY_WAVES_PER_EU
+#define NFDP_EARLY_WAVES_PER_EU 2
+#endif
+#ifndef NFDP_EARLY_ACL_TILES
+#define NFDP_EARLY_ACL_TILES 1    // every MFMA-ACL launch (r2 A/B: +0.5 % at 256 rules, +16 % at 1024)
+#endif
+constexpr uint32_t kEarlyAclTiles = NFDP_EARLY_ACL_TILES;
+constexpr uint32_t kFlagNoEarly = 1u << 8;     // launch flag: never the early-fetch instance (A/B)
+constexpr uint32_t kFlagForceEarly = 1u << 9;  // launch flag: the early-fetch instance at any rule count (A/B)
 #ifndef NFDP_FUSED_WAVES_PER_EU
 #define NFDP_FUSED_WAVES_PER_EU 4
 #endif
@@ -49,7 +63,7 @@ struct FusedArgs {
   const v4i* toep_frag;           // [2][2][64] A fragments of the Toeplitz matrix
   const uint32_t* toep_tab;       // [16][256] byte tables (LDS hash variant)
   uint32_t acl_tiles;             // ceil(n_acl / 16)
-  uint32_t flags;                 // bit0 no port/drop counters, bit1 no latency samples, bit2 no flow counts
+  uint32_t flags;                 // bit0 no port/drop counters, bit1 no latency samples, bit2 no flow counts, bit8 no early fetch
   // REMOTE variant (replicated tables, N GPUs): frames whose egress port lives on another GPU
   // go to segment[egress gpu] of send_pkt (64-B slot + 4-B meta, fill count in pcnt) instead of
   // out[i]; out_meta[i] then says kRemote.
@@ -95,8 +109,8 @@ __host__ __device__ inline LdsLayout lds_layout(int hash_mode, int acl_mode, uin
 constexpr int kBufCfg = 0x00020000;  // buffer resource word 3 (gfx9 family raw buffer)
 constexpr int kStreamAux = 2;        // nt: frames are read once / written once (streaming)
 
-template <int HASH, int ACL, bool REMOTE>
-__global__ __launch_bounds__(kFB, NFDP_FUSED_WAVES_PER_EU) void fused_kernel(FusedArgs a) {
+template <int HASH, int ACL, bool REMOTE, bool EARLY>
+__global__ __launch_bounds__(kFB, EARLY ? NFDP_EARLY_WAVES_PER_EU : NFDP_FUSED_WAVES_PER_EU) void fused_kernel(FusedArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ uint32_t rcnt[REMOTE ? 2 * kMaxRanks : 1], rbase[REMOTE ? kMaxRanks : 1];  // rcnt double-buffered
   const LdsLayout L = lds_layout(HASH, ACL, a.acl_tiles);
@@ -172,7 +186,14 @@ __global__ __launch_bounds__(kFB, NFDP_FUSED_WAVES_PER_EU) void fused_kernel(Fus
 
     uint32_t hash = 0;
     int acl_rule = -1;
-    classify_wave<HASH, ACL>(st.key, kx, av, lt, ltab, a.t, hash, acl_rule);
+    uint4 bv[8];
+    if constexpr (EARLY) {
+      // the bucket fetch leaves as soon as the hash is known: its latency runs under the ACL
+      classify_wave<HASH, ACL>(st.key, kx, av, lt, ltab, a.t, hash, acl_rule, 0, 1, nullptr,
+                               [&](uint32_t h) { flow_probe_issue(a.t, h, bv); });
+    } else {
+      classify_wave<HASH, ACL>(st.key, kx, av, lt, ltab, a.t, hash, acl_rule);
+    }
     // flow-owner steering (REMOTE, steer = 1): a packet of another GPU's flow shard leaves now,
     // as it came in; its owner runs the whole pipeline on it
     bool to_owner = false;
@@ -197,7 +218,8 @@ __global__ __launch_bounds__(kFB, NFDP_FUSED_WAVES_PER_EU) void fused_kernel(Fus
 #ifndef NFDP_LANE_PROBE
     {
       uint4 v;
-      slot = flow_probe_wave(a.t, st.key, hash, !st.reason && p.ipv4, kx, v);
+      if constexpr (EARLY) slot = flow_probe_finish(a.t, st.key, hash, !st.reason && p.ipv4, kx, bv, v);
+      else slot = flow_probe_wave(a.t, st.key, hash, !st.reason && p.ipv4, kx, v);
 #else
     if (!st.reason && p.ipv4) {
       uint4 v;
@@ -440,7 +462,7 @@ size_t fused_lds_bytes(int hash_mode, int acl_mode, uint32_t acl_tiles) {
   return lds_layout(hash_mode, acl_mode, acl_tiles).total;
 }
 
-template <int H, int A, bool R>
+template <int H, int A, bool R, bool E = false>
 static hipError_t launch_fused_t(const FusedArgs& a, int num_cus, hipStream_t s) {
   // static LDS (REMOTE reservation counters) + dynamic tables must fit 160 KiB
   constexpr size_t kStatic = 3 * (R ? kMaxRanks : 1) * sizeof(uint32_t);  // rcnt[2][..] + rbase
@@ -454,7 +476,7 @@ static hipError_t launch_fused_t(const FusedArgs& a, int num_cus, hipStream_t s)
   if (!R && (a.n >= (1u << 25) || !a.flow_ctr || !a.out_meta)) return hipErrorInvalidValue;
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&fused_kernel<H, A, R>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&fused_kernel<H, A, R, E>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxDyn);
     if (e != hipSuccess) return e;
     attr_set = true;
@@ -465,7 +487,7 @@ static hipError_t launch_fused_t(const FusedArgs& a, int num_cus, hipStream_t s)
   uint32_t grid = (uint32_t)(per_cu * num_cus);
   if (need < grid) grid = need;
   if (grid == 0) return hipSuccess;
-  hipLaunchKernelGGL((fused_kernel<H, A, R>), dim3(grid), dim3(kFB), lds, s, a);
+  hipLaunchKernelGGL((fused_kernel<H, A, R, E>), dim3(grid), dim3(kFB), lds, s, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || !a.side.cnt || a.side.cap_list == 0) return e;
   SideArgs sa{a.t, a.pkts, a.inmeta, a.out, a.out_meta, a.side, a.port_ctr, a.drop_ctr};
@@ -501,6 +523,14 @@ hipError_t launch_fused(const FusedLaunch& f, const LaunchCfg& cfg, hipStream_t 
   const bool remote = f.nranks > 1;
   if (cfg.acl_mode == kAclMfma && (f.acl_tiles == 0 || f.acl_tiles > kAclMaxRules / 16)) return hipErrorInvalidValue;
   const int h = cfg.hash_mode, ac = cfg.acl_mode, cu = cfg.num_cus;
+  const bool early = ac == kAclMfma && !(f.flags & kFlagNoEarly) &&
+                     (f.acl_tiles >= kEarlyAclTiles || (f.flags & kFlagForceEarly));
+  if (early) {
+    if (h == kHashLds) return remote ? launch_fused_t<kHashLds, kAclMfma, true, true>(a, cu, s)
+                                     : launch_fused_t<kHashLds, kAclMfma, false, true>(a, cu, s);
+    if (h == kHashMfma) return remote ? launch_fused_t<kHashMfma, kAclMfma, true, true>(a, cu, s)
+                                      : launch_fused_t<kHashMfma, kAclMfma, false, true>(a, cu, s);
+  }
 #define NFDP_CASE(HH, AA)                                                                  \
   if (h == HH && ac == AA)                                                                 \
     return remote ? launch_fused_t<HH, AA, true>(a, cu, s) : launch_fused_t<HH, AA, false>(a, cu, s);

@@ -89,6 +89,10 @@ NFDP_HD uint32_t egress_len(const Parsed& p, const EgressDecision& e) {
 
 NFDP_HD uint32_t byte_at(const uint32_t* s, int off) { return (s[off >> 2] >> (8 * (off & 3))) & 0xFFu; }
 
+#ifndef NFDP_L3_ON
+#define NFDP_L3_ON true
+#endif
+
 // A port takes frames when it is configured, its link is up and its function's RX is enabled.
 NFDP_HD bool port_can_egress(uint32_t flags) {
   return (flags & (kPortValid | kPortLinkDown | kPortRxOff)) == kPortValid;
@@ -113,7 +117,7 @@ NFDP_HD uint32_t finish_port(const TablesView& t, const TA& ta, uint32_t& port, 
   if (!vlan_done && (pe.flags & kPortTagEgress) && pe.vlan) { push = 1; tci = pe.vlan & 0xFFFu; }
   // tunnel port (OvS vxlan / geneve port, P4 l2_to_tunnel_v4): encapsulated by the side pass
   uint32_t enc = 0;
-  if (pe.flags & kPortTunnel) {
+  if (NFDP_L3_ON && (pe.flags & kPortTunnel)) {
     if (!t.tunnels || pe.lag >= t.n_tunnels) return kBadPort;
     enc = kEncapBytes;
     if (xhdr) *xhdr = 1;
@@ -154,7 +158,7 @@ NFDP_HD EgressDecision chain_stage(const TablesView& t, const TA& ta, Parsed& p,
     // tunnel termination on an underlay port (ipv4_tunnel_term_table + rx_ipv4_tunnel_source_port):
     // UDP 4789 (VXLAN) / 6081 (GENEVE, no options) to the local VTEP -> recirculate the inner
     // frame as received on the tunnel's port (P4 do_recirculate; the I/O layer re-injects it)
-    if ((st.in_flags & kPortVtep) && p.ipv4 && (p.s[5] >> 24) == 17u && p.len >= 64u &&
+    if (NFDP_L3_ON && (st.in_flags & kPortVtep) && p.ipv4 && (p.s[5] >> 24) == 17u && p.len >= 64u &&
         raw32_at2(p.s, 30) == st.in_ext) {
       const uint32_t dport = be16_at(p.s, 36);
       const bool vx = dport == 4789u, gn = dport == 6081u && (byte_at(p.s, 42) & 0x3Fu) == 0u;
@@ -168,7 +172,7 @@ NFDP_HD EgressDecision chain_stage(const TablesView& t, const TA& ta, Parsed& p,
       }
     }
     // router interface (kPortRouted): IPv4 addressed to the port's own MAC is routed
-    if ((st.in_flags & kPortRouted) && p.ipv4) {
+    if (NFDP_L3_ON && (st.in_flags & kPortRouted) && p.ipv4) {
       const PortEntry ip = ta.port(st.in_port);
       if (dmac_lo(p.s) == ip.mac_lo && dmac_hi(p.s) == ip.mac_hi) {
         uint32_t op = kPortNone;
@@ -249,7 +253,7 @@ NFDP_HD EgressDecision chain_stage(const TablesView& t, const TA& ta, Parsed& p,
         e.reason = kChainDrop; e.out_port = kPortNone; return e;
       } else if (op == kHopPunt) {
         e.reason = kNoRoute; e.out_port = kPortPunt; return e;
-      } else if (op == kHopRoute) {
+      } else if (NFDP_L3_ON && op == kHopRoute) {
         uint32_t rp = kPortNone;
         const uint32_t r = route_ipv4(t, p, hash, rp);
         if (r) { e.reason = r; e.out_port = r == kNoRoute ? kPortPunt : kPortNone; return e; }

@@ -24,6 +24,7 @@ def main():
     base = None
     for name, hm, am, nacl in (("lds+mfmaACL256", "lds", "mfma", 256), ("mfma+mfmaACL256", "mfma", "mfma", 256),
                                ("lds+aclOff", "lds", "off", 256), ("mfma+mfmaACL1024", "mfma", "mfma", 1024),
+                               ("lds+mfmaACL1024", "lds", "mfma", 1024), ("mfma+mfmaACL512", "mfma", "mfma", 512),
                                ("lds+scalarACL256", "lds", "scalar", 256)):
         g = DataPlane(device=dev, flow_buckets=1 << 19, hash_mode=hm, acl_mode=am)
         sc = S.build_sfc(g, n_pods=8, n_flows=1 << 20, n_acl=nacl, seed=0)
@@ -32,6 +33,10 @@ def main():
         if base is None:
             base = (g, sc)
     g0, sc = base
+    for k in ("mfma+mfmaACL1024", "lds+mfmaACL1024", "mfma+mfmaACL512"):
+        variants[k + "/noEarly"] = (variants[k][0], 256, True)   # kernels.hip kFlagNoEarly
+    for k in ("mfma+mfmaACL512", "lds+mfmaACL256"):
+        variants[k + "/early"] = (variants[k][0], 512, True)     # kernels.hip kFlagForceEarly
     variants["noPortCtr"] = (g0, 1, True)
     variants["noCounters+noLat"] = (g0, 3, False)
 
