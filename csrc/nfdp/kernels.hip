@@ -35,7 +35,7 @@ namespace nfdp {
 #define NFDP_EARLY_WAVES_PER_EU 2
 #endif
 #ifndef NFDP_EARLY_ACL_TILES
-#define NFDP_EARLY_ACL_TILES 1    // every MFMA-ACL launch (r2 A/B: +0.5 % at 256 rules, +16 % at 1024)
+#define NFDP_EARLY_ACL_TILES 33   // > 512 rules (r2 A/B: -9 % at 256 rules, +13-17 % at 1024)
 #endif
 constexpr uint32_t kEarlyAclTiles = NFDP_EARLY_ACL_TILES;
 constexpr uint32_t kFlagNoEarly = 1u << 8;     // launch flag: never the early-fetch instance (A/B)

@@ -33,7 +33,7 @@ def main():
         if base is None:
             base = (g, sc)
     g0, sc = base
-    for k in ("mfma+mfmaACL1024", "lds+mfmaACL1024", "mfma+mfmaACL512"):
+    for k in ("mfma+mfmaACL1024", "lds+mfmaACL1024", "mfma+mfmaACL512", "lds+mfmaACL256"):
         variants[k + "/noEarly"] = (variants[k][0], 256, True)   # kernels.hip kFlagNoEarly
     for k in ("mfma+mfmaACL512", "lds+mfmaACL256"):
         variants[k + "/early"] = (variants[k][0], 512, True)     # kernels.hip kFlagForceEarly

@@ -10,7 +10,7 @@ for pass in 1 2; do
     for v in "$V" ""; do
       echo "variant=${v:-default} pass=$pass"
       NFDP_EXT_DIR="$v" timeout -k 10 200 python tools/ablate.py --rounds 3 > gpurun_out/abn_run.log 2>&1 || exit 1
-      grep -E "lds\+mfmaACL256|lds\+aclOff|mfma\+mfmaACL1024" gpurun_out/abn_run.log
+      grep -E "ACL256|aclOff|ACL1024" gpurun_out/abn_run.log
     done
   done
 done
