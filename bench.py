@@ -87,7 +87,7 @@ def _time_fused(dp, batches, steps, torch):
 
 
 def measure_variants(a, dp, sc, dev, torch, S, P) -> dict:
-    """Mixed traffic, 1024-rule ACL and IMIX sizes on the headline's data plane (1 GPU)."""
+    """Mixed traffic, L3-routed SFC, 1024-rule ACL and IMIX sizes on the headline's data plane (1 GPU)."""
     res = {"steps": a.variant_steps}
     n = a.batch
     # IMIX (7 x 64, 4 x 576, 1 x 1500): same flows, frame lengths from the mix
@@ -116,6 +116,19 @@ def measure_variants(a, dp, sc, dev, torch, S, P) -> dict:
     res["mixed_mpps"] = round(n * a.variant_steps / el / 1e6, 1)
     res["mixed_dispositions"] = {k: round(float(np.mean(rs == v)), 4) for k, v in
                                  (("ok", 0), ("acl_deny", 4), ("no_route", 5), ("malformed", 9))}
+    # L3-routed SFC: acl -> nat -> route (pod /32s through 8-way ECMP, 100K background prefixes
+    # in the DIR-24-8 FIB), same flows and traffic as the headline
+    info = S.install_l3_routes(dp, sc)
+    dp.commit()
+    pk, im = S.traffic(sc, n, seed=9101)
+    b = [(torch.from_numpy(pk).to(dev), torch.from_numpy(im.view(np.int32)).to(dev))]
+    el, meta = _time_fused(dp, b, a.variant_steps, torch)
+    res["l3_mpps"] = round(n * a.variant_steps / el / 1e6, 1)
+    res["l3_forwarded_fraction"] = round(float(np.mean(P.meta_fields(meta.cpu().numpy().view(np.uint32))[2] == 0)), 4)
+    res["l3_fib"] = info
+    dp.chains.set(sc.chain_id, ["acl", "nat", "l2fwd"])
+    dp.commit()
+    del b
     # ACL1024 on the headline traffic
     S.add_acl_rules(dp, 1024)
     dp.commit()
@@ -441,6 +454,7 @@ def main() -> None:
             "forwarded_fraction": round(fwd_local, 6),
             "value_mixed": None if not variants else variants["mixed_mpps"],
             "value_acl1024": None if not variants else variants["acl1024_mpps"],
+            "value_l3": None if not variants else variants["l3_mpps"],
             "imix": None if not variants else variants["imix"],
             "variants": variants,
             "flows": total_flows,

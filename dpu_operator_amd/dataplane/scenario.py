@@ -12,6 +12,8 @@ from __future__ import annotations
 
 from dataclasses import dataclass
 
+import ipaddress
+
 import numpy as np
 
 from ..ops import packets as P
@@ -265,3 +267,38 @@ def add_acl_rules(dp, total: int, seed: int = 5) -> None:
         r += 1
     dp.acl.rules.append(final)
     dp.acl.version += 1
+
+
+ROUTER_MAC = "02:00:00:00:fe:01"
+
+
+def install_l3_routes(dp, sc: Scenario, n_background: int = 100_000, seed: int = 13) -> dict:
+    """Turn the SFC into an L3-routed SFC: the chain becomes acl -> nat -> route, every pod IP is a
+    /32 route through an 8-way ECMP group of nexthops whose members all reach that pod (one
+    neighbour MAC per member), and `n_background` random prefixes (/8 - /28, outside the pod
+    network) fill the DIR-24-8 table like a real FIB.  Returns what was installed; the caller
+    restores the chain with `dp.chains.set(sc.chain_id, hops)`."""
+    rng = np.random.default_rng(seed)
+    nh = 0
+    for d in range(sc.n_pods):
+        members = []
+        for w in range(8):
+            mac = bytes([0x02, 0x60, 0, 0, d & 0xFF, w])
+            dp.nexthops.set(nh, int(sc.pod_port[d]), dmac=mac, smac=ROUTER_MAC)
+            members.append(nh)
+            nh += 1
+        dp.ecmp.set_group(d, members)
+        dp.routes.add(f"{ipaddress.IPv4Address(POD_NET + d)}/32", ecmp_group=d)
+    sink = nh
+    dp.nexthops.set(sink, int(sc.pod_port[0]), dmac=bytes([0x02, 0x60, 0, 0, 0xFF, 0xFF]), smac=ROUTER_MAC)
+    plen = rng.integers(8, 29, n_background)
+    base = rng.integers(0x0B000000, 0xDF000000, n_background, dtype=np.int64)
+    added = 0
+    for b, pl in zip(base.tolist(), plen.tolist()):
+        net = b & ~((1 << (32 - pl)) - 1) & 0xFFFFFFFF
+        if (net >> 16) == (POD_NET >> 16) or (net >> 24) == (POD_NET >> 24):
+            continue
+        dp.routes.add(f"{ipaddress.IPv4Address(net)}/{pl}", nexthop=sink)
+        added += 1
+    dp.chains.set(sc.chain_id, ["acl", "nat", "route"])
+    return {"pod_routes": sc.n_pods, "ecmp_ways": 8, "background_prefixes": added, "nexthops": nh + 1}

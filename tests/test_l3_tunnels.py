@@ -234,3 +234,34 @@ def test_tunnels_gpu_bit_exact(kind):
     assert np.array_equal(rg.meta.cpu().numpy().view(np.uint32), rc.meta)
     assert np.array_equal(rg.out.cpu().numpy(), rc.out)
     assert np.array_equal(sg["xhdr"][:3], sc["xhdr"][:3])
+
+
+def test_l3_routed_sfc_scenario():
+    """The bench's L3-routed SFC variant (scenario.install_l3_routes): acl -> nat -> route with
+    pod /32s through 8-way ECMP over 100K background prefixes.  Checked against the flows' own
+    destinations: egress = the destination pod's port, dst MAC = one of that pod's 8 neighbours
+    (hash-selected), src MAC = the router's, TTL - 1 with a valid checksum, SNAT applied."""
+    from dpu_operator_amd.dataplane import scenario as S
+
+    dp = DataPlane(device="cpu", flow_buckets=1 << 12)
+    sc = S.build_sfc(dp, n_pods=8, n_flows=4000, n_acl=32)
+    dp.commit(full=True)
+    info = S.install_l3_routes(dp, sc, n_background=20_000)
+    dp.commit()
+    assert info["background_prefixes"] > 19_000
+    pk, im, fl = S.traffic(sc, 2048, seed=4, return_flows=True)
+    r = dp.run(pk, im)
+    port, _, reason = P.meta_fields(r.meta)
+    assert (reason == 0).all()
+    dst = sc.flow_dst_pod[fl]
+    assert np.array_equal(port, sc.pod_port[dst])
+    lens = im >> 16
+    for i in range(0, 2048, 7):
+        o = P.assemble(r.out[i], int(r.meta[i]), pk[i], int(lens[i]))
+        u = o[:12] + o[16:] if o[12:14] == b"\x81\x00" else o
+        assert u[0:4] == bytes([0x02, 0x60, 0, 0]) and u[4] == int(dst[i])     # one of the pod's neighbours
+        assert u[6:12] == bytes.fromhex(S.ROUTER_MAC.replace(":", ""))
+        assert u[22] == 63                                                        # TTL 64 -> 63
+        assert u[26:30] == int(sc.actions[fl[i], 1]).to_bytes(4, "little")       # SNAT source
+        assert P.check_csums(np.frombuffer(u, np.uint8)[None], np.array([len(u)]))[0]
+    assert len({int(r.out[i, 5]) for i in range(2048)}) == 8                     # all ECMP members used

@@ -77,7 +77,7 @@ def _worker(rank, world, port, q, steps, frac):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,frac", [(2, 0.2), (3, 0.1), (4, 0.05)])
+@pytest.mark.parametrize("world,frac", [(2, 0.2), (3, 0.1), (4, 0.05), (8, 0.05)])
 def test_rss_gloo(world, frac):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
