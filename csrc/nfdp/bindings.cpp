@@ -491,12 +491,19 @@ PYBIND11_MODULE(_nfdp, m) {
       .def_property_readonly("host_slots", &RingEngine::host_slots)
       .def_property_readonly("capacity", &RingEngine::capacity)
       .def_property_readonly("running", &RingEngine::running)
+      .def("alive", &RingEngine::alive)
       .def_property_readonly("published", &RingEngine::published)
       .def("dev_in", [](RingEngine& r) { return reinterpret_cast<uintptr_t>(r.dev_in()); })
       .def("dev_inmeta", [](RingEngine& r) { return reinterpret_cast<uintptr_t>(r.dev_inmeta()); })
       .def("dev_out", [](RingEngine& r) { return reinterpret_cast<uintptr_t>(r.dev_out()); })
       .def("dev_meta", [](RingEngine& r) { return reinterpret_cast<uintptr_t>(r.dev_meta()); })
       .def("dev_svc", [](RingEngine& r) { return reinterpret_cast<uintptr_t>(r.dev_svc()); })
+      .def("host_view", [](RingEngine& r) {
+        // host addresses of the pinned slot buffers (host_slots rings): in, inmeta, out, meta
+        if (!r.host_slots()) throw std::runtime_error("ring: host_view needs host_slots=True");
+        return py::make_tuple(reinterpret_cast<uintptr_t>(r.host_ptr(0)), reinterpret_cast<uintptr_t>(r.host_ptr(1)),
+                              reinterpret_cast<uintptr_t>(r.host_ptr(2)), reinterpret_cast<uintptr_t>(r.host_ptr(3)));
+      })
       .def("start", [](RingEngine& r, py::dict tables, py::dict d, int hash_mode, int acl_mode, int num_cus,
                        double deadline_s) {
         FusedLaunch f{};
@@ -507,6 +514,9 @@ PYBIND11_MODULE(_nfdp, m) {
         f.acl_tiles = val<uint32_t>(d, "acl_tiles", 1);
         f.toep_frag = ptr<const void>(d, "toep_frag"); f.toep_tab = ptr<const uint32_t>(d, "toep_tab");
         f.flags = val<uint32_t>(d, "flags", 0);
+        if (d.contains("side")) f.side = side_from(d["side"]);
+        if (f.side.cnt && (!f.side.list || f.side.cap_list < r.capacity()))
+          throw std::invalid_argument("ring side list must hold a whole ring");
         if (!f.port_ctr || !f.drop_ctr) throw std::invalid_argument("ring start: null counters");
         if (hash_mode == 2 && !f.toep_frag) throw std::invalid_argument("MFMA hash needs toeplitz frags");
         if (hash_mode == 1 && !f.toep_tab) throw std::invalid_argument("LDS hash needs toeplitz table");
@@ -516,6 +526,7 @@ PYBIND11_MODULE(_nfdp, m) {
         r.start(f, cfg, deadline_s, ptr<const void>(tables, "flows_alt"));
       })
       .def("flip", &RingEngine::flip)
+      .def("bump_epoch", &RingEngine::bump_epoch)
       .def("grace_over", &RingEngine::grace_over)
       .def("wait_grace", [](RingEngine& r, double timeout_s) {
         py::gil_scoped_release nogil;
@@ -541,6 +552,15 @@ PYBIND11_MODULE(_nfdp, m) {
         return py::make_tuple(py::array_t<double>(v.size(), v.data()), el);
       });
 
+  m.def("launch_side", [](py::dict tables, uintptr_t pkts, uintptr_t inmeta, uintptr_t out, uintptr_t out_meta,
+                          py::object side, uintptr_t port_ctr, uintptr_t drop_ctr, uintptr_t stream) {
+    const TablesView t = tables_from(tables);
+    const SideOut so = side_from(side);
+    check(launch_side(t, reinterpret_cast<const void*>(pkts), reinterpret_cast<const uint32_t*>(inmeta),
+                      reinterpret_cast<const void*>(out), reinterpret_cast<const uint32_t*>(out_meta), so,
+                      reinterpret_cast<unsigned long long*>(port_ctr), reinterpret_cast<unsigned long long*>(drop_ctr),
+                      reinterpret_cast<hipStream_t>(stream)), "launch_side");
+  });
   m.def("launch_harvest", [](uintptr_t ctr, uintptr_t out, uint32_t n, uintptr_t stream) {
     check(launch_harvest(reinterpret_cast<unsigned long long*>(ctr), reinterpret_cast<unsigned long long*>(out), n,
                          reinterpret_cast<hipStream_t>(stream)), "harvest");

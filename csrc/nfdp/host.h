@@ -111,6 +111,11 @@ struct FusedLaunch {
   const uint32_t* n_dev = nullptr; // device-side count (<= n)
 };
 hipError_t launch_fused(const FusedLaunch& f, const LaunchCfg& cfg, hipStream_t s);
+// Side pass alone (flood / mirror / ARP replicas, learn events, tunnel headers) over a side list
+// another kernel filled (the persistent ring kernel): slots / meta are that kernel's buffers.
+hipError_t launch_side(const TablesView& t, const void* pkts, const uint32_t* inmeta, const void* out,
+                       const uint32_t* out_meta, const SideOut& side, unsigned long long* port_ctr,
+                       unsigned long long* drop_ctr, hipStream_t s);
 size_t fused_lds_bytes(int hash_mode, int acl_mode, uint32_t acl_tiles);
 hipError_t launch_stamp(unsigned long long* dst, hipStream_t s);
 hipError_t launch_bucket_update(const uint32_t* idx, uint32_t nb, const void* rows, void* flows,

@@ -490,8 +490,17 @@ static hipError_t launch_fused_t(const FusedArgs& a, int num_cus, hipStream_t s)
   hipLaunchKernelGGL((fused_kernel<H, A, R, E>), dim3(grid), dim3(kFB), lds, s, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || !a.side.cnt || a.side.cap_list == 0) return e;
-  SideArgs sa{a.t, a.pkts, a.inmeta, a.out, a.out_meta, a.side, a.port_ctr, a.drop_ctr};
-  const uint32_t sg = (a.side.cap_list + 255) / 256 < 512 ? (a.side.cap_list + 255) / 256 : 512;
+  return launch_side(a.t, a.pkts, a.inmeta, a.out, a.out_meta, a.side, a.port_ctr, a.drop_ctr, s);
+}
+
+hipError_t launch_side(const TablesView& t, const void* pkts, const uint32_t* inmeta, const void* out,
+                       const uint32_t* out_meta, const SideOut& side, unsigned long long* port_ctr,
+                       unsigned long long* drop_ctr, hipStream_t s) {
+  if (!side.cnt || side.cap_list == 0) return hipSuccess;
+  if (!pkts || !inmeta || !out || !out_meta || !side.list || !port_ctr || !drop_ctr) return hipErrorInvalidValue;
+  SideArgs sa{t, reinterpret_cast<const uint4*>(pkts), inmeta, reinterpret_cast<const uint4*>(out), out_meta, side,
+              port_ctr, drop_ctr};
+  const uint32_t sg = (side.cap_list + 255) / 256 < 512 ? (side.cap_list + 255) / 256 : 512;
   hipLaunchKernelGGL(side_kernel, dim3(sg), dim3(256), 0, s, sa);
   return hipGetLastError();
 }

@@ -30,7 +30,10 @@
 // reads, flips the epoch (flip(), carried by the next publish), and before it writes that other
 // copy again waits for the grace period: every chunk published before the flip has completed
 // (wait_grace()), so no wave still reads it.  A lookup therefore never sees a half-written
-// bucket, without retries or per-bucket locks on the packet path.  The small tables staged in LDS
+// bucket, without retries or per-bucket locks on the packet path.  A wave that sees a new epoch
+// first drops its cached table lines (agent-scope acquire: CU L1 and XCD L2), so a copy rewritten
+// since the wave last read it is never served from a stale line; bump_epoch() (epoch + 2, same
+// copy) does only that, for tables changed in place.  The small tables staged in LDS
 // (ports, chains, ACL) still take the stop -> drain -> relaunch path.
 #pragma once
 #include <hip/hip_runtime.h>
@@ -46,6 +49,9 @@ namespace nfdp {
 // Bit 63 of the published-packet counter is the stop flag: one 64-bit word carries both, so a
 // wave that sees "stop" also sees the final count (no ordering between two words to get right).
 constexpr uint64_t kRingStop = 1ull << 63;
+// Ingress meta of a filler slot (a burst that is not a multiple of 64 packets is padded to whole
+// chunks): processed like any slot, but it counts nowhere and never reaches the side list.
+constexpr uint32_t kRingPadMeta = 0xFFFFFFFFu;
 constexpr uint32_t kRingEpochBits = 7;
 constexpr uint64_t kRingEpochMask = (1ull << kRingEpochBits) - 1;
 // published word = stop | count << 7 | epoch: count-major, so the frontier's atomic max keeps
@@ -86,6 +92,8 @@ class RingEngine {
 
   uint32_t capacity() const { return cap_; }
   bool running() const { return running_; }
+  // The grid is still resident (false once every wave left: stop, or the device deadline passed).
+  bool alive() const { return running_ && hipStreamQuery(stream_) == hipErrorNotReady; }
   bool host_slots() const { return host_slots_; }
   // device ring buffers (the producer stages frames here before publishing them)
   void* dev_in() const { return d_in_; }
@@ -93,6 +101,8 @@ class RingEngine {
   void* dev_out() const { return d_out_; }
   uint32_t* dev_meta() const { return d_meta_; }
   uint32_t* dev_svc() const { return d_svc_; }  // per-chunk device service time (ticks, 100 MHz)
+  // host_slots rings: host addresses of the pinned in / inmeta / out / meta buffers
+  void* host_ptr(int i) const { return host_slots_ && i >= 0 && i < (int)host_ptrs_.size() ? host_ptrs_[i] : nullptr; }
 
   // Launch the persistent kernel over the tables/counters in `f` (pkts/out/n are ignored).
   // flows_alt: the second flow-table copy (epoch & 1 == 1); null = single copy (no live flips).
@@ -117,6 +127,9 @@ class RingEngine {
   // Grace period of the last flip: every chunk published before it has completed.
   bool grace_over() { return completed() >= flip_prod(); }
   bool wait_grace(double timeout_s);
+  // Epoch + 2 (same flow-table copy): chunks published from now on make their waves drop cached
+  // table lines first (after the host changed a table in place, e.g. MAC learning).
+  uint32_t bump_epoch();
   uint32_t epoch() const {
     std::lock_guard<std::mutex> g(mu_);
     return epoch_;

@@ -26,6 +26,7 @@ struct RingArgs {
   const v4i* toep_frag; const uint32_t* toep_tab;
   unsigned long long deadline;
   const void* flows2[2];  // flow-table copies by epoch parity (the same pointer twice if not double buffered)
+  SideOut side;           // side list (cnt null = off): slots needing replicas / learn events / outer headers
   uint32_t flags_bits;  // bit2: no per-flow counts; bits 5/6: diagnostics (kRingTrace, kRingNoCounters)
 };
 // Frames are read and written with system-coherent buffer ops (sc0 sc1): the loads never hit a
@@ -188,6 +189,7 @@ __global__ __launch_bounds__(kRingBlock) void ring_kernel(RingArgs a) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t nch_mask = a.ring_mask >> 6;  // R/64 - 1
   const unsigned long long t_begin = __builtin_amdgcn_s_memrealtime();
+  uint32_t seen_epoch = 0xFFFFFFFFu;  // epoch of this wave's previous chunk
 
   for (;;) {
     unsigned long long tk = 0;
@@ -205,6 +207,14 @@ __global__ __launch_bounds__(kRingBlock) void ring_kernel(RingArgs a) {
       if (!ring_wait_chunk(a, lane, t_begin, tk, epoch, on_idle)) break;
     }
     const unsigned long long t_avail = __builtin_amdgcn_s_memrealtime();
+    if (epoch != seen_epoch) {
+      // A new epoch: the host rewrote a table this kernel reads with ordinary cached loads (the
+      // flow-table copy it now names, or the MAC table after learning).  The lines this wave's
+      // CU L1 and its XCD's L2 still hold may be stale - this grid never sees the cache
+      // invalidate a kernel launch brings - so drop them (agent-scope acquire) before probing.
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      seen_epoch = epoch;
+    }
     const bool trace = (a.flags_bits & kRingTrace) != 0 && wave == 0;
     uint32_t tr0 = 0, tr1 = 0, tr2 = 0, tr3 = 0, tr4 = 0, tr5 = 0;
 #define NFDP_RING_MARK(var)                                                 \
@@ -265,6 +275,19 @@ __global__ __launch_bounds__(kRingBlock) void ring_kernel(RingArgs a) {
     emit(p, e.tci, e.push != 0, o);
     wave_frames_store<kSysAux>(kx, o, r_out, run);
     __builtin_amdgcn_raw_buffer_store_b32(make_meta(e.out_port, olen, e.reason, !e.reason && e.xhdr, !e.reason && e.flood), r_meta, i * 4u, 0, kSysAux);
+    const bool pad = im == kRingPadMeta;  // filler slot of a partial burst: no counters, no side work
+    if (a.side.cnt) {
+      // flood / mirror / ARP-trap / learning / tunnel packets go on the side list; the host runs
+      // the side pass over them once the chunk's flag is seen (before the flag: vmcnt covers it)
+      const bool sn = !pad && side_needed(st, p, e);
+      if (__builtin_expect(__any(sn), 0)) {
+        if (sn) {
+          const uint32_t q = atomicAdd(a.side.cnt + 5, 1u);
+          if (q < a.side.cap_list) a.side.list[q] = i;
+          else atomicAdd(a.side.cnt + 6, 1u);
+        }
+      }
+    }
     NFDP_RING_MARK(tr3)
 
     // ---- completion: the chunk's write-through stores are done before its flag is written ----
@@ -278,7 +301,7 @@ __global__ __launch_bounds__(kRingBlock) void ring_kernel(RingArgs a) {
     // ---- counters, off the latency path (after the flag): port / drop counters into the
     // workgroup's LDS (flushed when idle, every kFlushChunks chunks and at exit), per-flow words
     // (nearly distinct per packet) straight to the global table.
-    if (counters) {
+    if (counters && !pad) {
       if (st.in_port < (uint32_t)kLdsPorts) {
         atomicAdd(&pc[st.in_port], 1u); atomicAdd(&pc[kLdsPorts + st.in_port], st.wire_len);
       } else if (st.in_port < (uint32_t)kMaxPorts) {
@@ -333,6 +356,7 @@ hipError_t launch_ring(const RingLaunch& r, const LaunchCfg& cfg, int wgs_per_cu
   a.toep_frag = reinterpret_cast<const v4i*>(r.f.toep_frag);
   a.toep_tab = r.f.toep_tab;
   a.deadline = r.deadline_ticks;
+  a.side = r.f.side;
   a.flows2[0] = r.f.t.flows;
   a.flows2[1] = r.flows_alt ? r.flows_alt : r.f.t.flows;
   a.flags_bits = r.f.flags;
@@ -496,6 +520,13 @@ uint32_t RingEngine::flip() {
   flip_prod_ = prod_;
   // same count, new epoch: chunks published from here on carry it (the frontier mirrors a word
   // only when its count grows, so this store alone changes nothing for waiting waves)
+  if (running_) __atomic_store_n(&ctl_->prod, ring_word(prod_, epoch_), __ATOMIC_RELEASE);
+  return epoch_;
+}
+
+uint32_t RingEngine::bump_epoch() {
+  std::lock_guard<std::mutex> g(mu_);
+  epoch_ = (epoch_ + 2) & (uint32_t)kRingEpochMask;
   if (running_) __atomic_store_n(&ctl_->prod, ring_word(prod_, epoch_), __ATOMIC_RELEASE);
   return epoch_;
 }

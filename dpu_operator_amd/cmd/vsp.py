@@ -43,7 +43,8 @@ def build_vsp(a, pm: PathManager):
             nl = RtNetlink()
         return GpuVsp(pm, device=a.device or None, flow_buckets=a.flow_buckets or cfg.flow_buckets,
                       hash_mode=cfg.hash_mode, acl_mode=cfg.acl_mode,
-                      state_dir=a.state_dir or cfg.vsp_state_dir or None, nl=nl, live=a.live)
+                      state_dir=a.state_dir or cfg.vsp_state_dir or None, nl=nl, live=a.live,
+                      live_engine=a.live_engine)
     from ..cni.netlink import RtNetlink
     from ..platform.platform import SysfsPlatform
     from ..utils.cmdrunner import HostRunner
@@ -91,6 +92,8 @@ def main(argv=None, stop: threading.Event | None = None) -> int:
     ap.add_argument("--state-dir", default="", help="amd-gpu: journal + snapshot directory (resume on restart)")
     ap.add_argument("--live", action="store_true",
                     help="amd-gpu: vports are real TAP netdevs and pod traffic flows through the data plane")
+    ap.add_argument("--live-engine", default="batch", choices=["batch", "ring"],
+                    help="amd-gpu --live: fused kernel per poll cycle, or the persistent ring kernel on pinned host slots")
     ap.add_argument("--metrics-bind-address", default="", help="amd-gpu: data-plane /metrics address (off if empty)")
     ap.add_argument("--agent-mbox", default="", help="amd-gpu: run the node control agent on this mailbox path")
     ap.add_argument("--agent-config", default="", help="agent SoC config file (default: one PF + --agent-vfs VFs)")

@@ -19,6 +19,19 @@ what the pod sends arrives on that fd and what the VSP writes to it is what the 
        tunnel's underlay port; terminated tunnel traffic (reason `recirc`) is re-injected, inner
        frame only, as received on the tunnel port, in the next cycle (P4 do_recirculate).
 
+Two engines run the pipeline under this loop:
+  engine="batch" (default)  DataPlane.run per cycle: header slots uploaded, fused kernel, side kernel
+  engine="ring"             the persistent ring kernel with its slots in pinned host memory
+                            (RingPath host_slots=True): the loop writes header slots + in-meta
+                            straight into the ring (bursts padded to whole 64-packet chunks with
+                            filler slots that count nowhere), publishes, waits for the completion
+                            flags, reads egress slots + meta from the same pinned buffers and runs
+                            the side kernel over the ring's side list.  No launch per burst, no
+                            copies: the resident kernel reads and writes the host slots over PCIe.
+                            Table commits keep working (flow updates by epoch flip, anything else
+                            drains and relaunches the ring between bursts); a ring that outlives its
+                            device deadline is relaunched.
+
 Every cycle records its stage times (rx / pipeline / side / tx / batch) and, on the GPU, the
 kernel's sampled per-packet latencies into `dp.latency` (utils/latency.py), which the data-plane
 metrics collector exports as `dpu_packet_latency_seconds{stage=...}` histograms.
@@ -92,7 +105,17 @@ class TapPort:
 
 
 class LivePath:
-    def __init__(self, dp, ports: dict, burst: int = 256, on_punt=None):
+    def __init__(self, dp, ports: dict, burst: int = 256, on_punt=None, engine: str = "batch",
+                 ring_capacity: int = 4096):
+        if engine not in ("batch", "ring"):
+            raise ValueError("engine is 'batch' or 'ring'")
+        if engine == "ring" and not dp.gpu:
+            raise ValueError("the ring engine needs a GPU data plane")
+        self.engine = engine
+        self.ring_capacity = int(ring_capacity)
+        self.ring = None
+        if engine == "ring" and burst > self.ring_capacity:
+            raise ValueError("burst must fit the ring")
         self.dp = dp
         self.ports = dict(ports)          # data-plane port -> TapPort (anything with read/write/fd)
         self.burst = burst
@@ -161,7 +184,6 @@ class LivePath:
         if not n:
             return 0
         t_start = self._t_ready
-        lat = self.dp.latency
         t_rx = time.perf_counter()
         lens = np.array([len(f) for f in frames], np.uint32)
         slots = np.zeros((n, 64), np.uint8)
@@ -169,6 +191,10 @@ class LivePath:
             h = f[:64]
             slots[i, : len(h)] = np.frombuffer(h, np.uint8)
         im = P.inmeta(np.array(src, np.uint32), lens)
+        if self.engine == "ring":
+            out, meta, side, t_pipe = self._run_ring(slots, im)
+            t_side = time.perf_counter()
+            return self._deliver(frames, src, lens, out, meta, side, t_start, t_rx, t_pipe, t_side)
         if self.dp.gpu:
             import torch
 
@@ -183,6 +209,48 @@ class LivePath:
             t_pipe = time.perf_counter()
         side = self.dp.side_result() if self.dp.side_active() else {"n_rep": 0}
         t_side = time.perf_counter()
+        return self._deliver(frames, src, lens, out, meta, side, t_start, t_rx, t_pipe, t_side)
+
+    def _run_ring(self, slots: np.ndarray, im: np.ndarray):
+        """One burst through the persistent ring (host slots): returns out, meta, side, t_pipe."""
+        from .ring import RingPath
+
+        if self.ring is None:
+            self.ring = RingPath(self.dp, capacity=self.ring_capacity, host_slots=True, coop=True, side=True,
+                                 deadline_s=3600.0)
+            self.ring.start()
+            self._rin, self._rim, self._rout, self._rmeta = self.ring.host_arrays()
+            self.stats["ring_relaunch"] = 0
+        ring, n, c = self.ring, len(slots), self.ring_capacity
+        n_pad = (n + 63) & ~63
+        with ring.lock:
+            if ring.ensure_alive():
+                self.stats["ring_relaunch"] += 1
+            pos = int(ring.eng.published) % c
+            idx = (pos + np.arange(n_pad)) % c
+            self._rin[idx[:n]] = slots
+            self._rim[idx[:n]] = im
+            self._rim[idx[n:]] = 0xFFFFFFFF          # filler slots (ring.h kRingPadMeta)
+            ring.reset_side()
+            end = ring.publish(n_pad)
+            ring.wait(end, 5.0)
+            out = self._rout[idx[:n]].copy()
+            meta = self._rmeta[idx[:n]].copy()
+            t_pipe = time.perf_counter()
+            side = {"n_rep": 0}
+            if self.dp.side_active():
+                side = ring.side_pass()
+                if side.get("n_learn"):
+                    ring.eng.bump_epoch()             # learned MACs: the next chunks drop cached lines
+                if side.get("n_rep"):                 # ring slot -> burst index
+                    side["rep_src"] = (side["rep_src"].astype(np.int64) - pos) % c
+                if side.get("xhdr") is not None:
+                    side["xhdr"] = side["xhdr"][idx[:n]]
+        return out, meta, side, t_pipe
+
+    def _deliver(self, frames, src, lens, out, meta, side, t_start, t_rx, t_pipe, t_side) -> int:
+        n = len(frames)
+        lat = self.dp.latency
         self.stats["rx"] += n
         self.stats["batches"] += 1
         port, olen, reason = P.meta_fields(meta)
@@ -235,3 +303,6 @@ class LivePath:
         self._stop.set()
         if self._t is not None:
             self._t.join(timeout=5)
+        if self.ring is not None:
+            self.ring.close()
+            self.ring = None

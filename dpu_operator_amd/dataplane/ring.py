@@ -30,6 +30,9 @@ Changes to the LDS-staged tables (ports, chains, ACL, ...) drain, stop and relau
 """
 from __future__ import annotations
 
+import ctypes
+import threading
+
 import numpy as np
 
 from .engine import DataPlane
@@ -37,11 +40,13 @@ from .engine import DataPlane
 
 class RingPath:
     def __init__(self, dp: DataPlane, capacity: int = 1 << 16, wgs_per_cu: int = 1, deadline_s: float = 120.0,
-                 knobs: int = 0, coop: bool = True, host_slots: bool = False):
+                 knobs: int = 0, coop: bool = True, host_slots: bool = False, side: bool = False):
         """coop=True: a workgroup's 4 waves share each chunk (ACL rule tiles split 4 ways) —
         lowest latency.  coop=False: every wave takes its own chunks — highest throughput.
         host_slots=True: the ring slots live in pinned host memory and the resident kernel reads /
-        writes the frames over PCIe itself (zero-copy host rings, e.g. pod vhost / AF_XDP)."""
+        writes the frames over PCIe itself (zero-copy host rings, e.g. pod vhost / AF_XDP).
+        side=True: the kernel puts packets that need replicas / learn events / outer headers on
+        the data plane's side list; `side_pass()` runs the side kernel over them (live path)."""
         if not dp.gpu:
             raise RuntimeError("RingPath needs a GPU data plane")
         if capacity < 64 or capacity & (capacity - 1):
@@ -54,6 +59,13 @@ class RingPath:
         self.host_slots = bool(host_slots)
         self.eng = dp.nf.RingEngine(self.capacity, int(dp.num_cus), int(wgs_per_cu), self.coop, self.host_slots)
         self._staged = 0
+        self.side = bool(side)
+        if self.side and self.capacity > dp.cap_rep:
+            raise ValueError(f"a side-list ring holds at most {dp.cap_rep} slots")
+        self._side = None
+        # a burst (publish -> wait -> read) and a stop / relaunch for a table commit exclude
+        # each other: DataPlane.commit() may run on another thread (the VSP's RPCs)
+        self.lock = threading.RLock()
         rings = getattr(dp, "_rings", None)
         if rings is None:
             dp._rings = rings = []
@@ -86,10 +98,14 @@ class RingPath:
     # ------------------------------------------------------------------ session
     def _args(self) -> dict:
         dp = self.dp
-        return {"flow_ctr": dp._ptr("flow_ctr"), "port_ctr": dp._ptr("port_ctr"), "drop_ctr": dp._ptr("drop_ctr"),
-                "acl_wfrag": dp._ptr("acl_wfrag"), "acl_cinit": dp._ptr("acl_cinit"), "acl_tiles": dp._acl_tiles,
-                "toep_frag": dp._ptr("toep_frag"), "toep_tab": dp._ptr("toep_tab"),
-                "flags": (0 if dp.count_flows else 4) | self.knobs}
+        a = {"flow_ctr": dp._ptr("flow_ctr"), "port_ctr": dp._ptr("port_ctr"), "drop_ctr": dp._ptr("drop_ctr"),
+             "acl_wfrag": dp._ptr("acl_wfrag"), "acl_cinit": dp._ptr("acl_cinit"), "acl_tiles": dp._acl_tiles,
+             "toep_frag": dp._ptr("toep_frag"), "toep_tab": dp._ptr("toep_tab"),
+             "flags": (0 if dp.count_flows else 4) | self.knobs}
+        if self.side:
+            self._side = dp._side_buffers(self.capacity)
+            a["side"] = self._side
+        return a
 
     @property
     def running(self) -> bool:
@@ -109,13 +125,57 @@ class RingPath:
                        int(self.dp.num_cus), self.deadline_s)
 
     def stop(self, timeout_s: float = 30.0) -> None:
-        self.eng.stop(timeout_s)
+        with self.lock:
+            self.eng.stop(timeout_s)
 
     def resume(self) -> None:
         """Relaunch over the current device tables (DataPlane.commit stops, updates, resumes)."""
-        self.eng.set_epoch(self.dp._flow_active)
-        self.eng.start(self._tables(), self._args(), self.dp.hash_mode, self.dp.acl_mode,
-                       int(self.dp.num_cus), self.deadline_s)
+        with self.lock:
+            _torch().cuda.current_stream(self.dp.tdev).synchronize()
+            self.eng.set_epoch(self.dp._flow_active)
+            self.eng.start(self._tables(), self._args(), self.dp.hash_mode, self.dp.acl_mode,
+                           int(self.dp.num_cus), self.deadline_s)
+
+    def ensure_alive(self) -> bool:
+        """Relaunch a ring whose grid left on its own (device deadline); True if it was relaunched."""
+        with self.lock:
+            if self.eng.running and not self.eng.alive():
+                self.eng.stop(5.0)
+                self.resume()
+                return True
+        return False
+
+    # ------------------------------------------------------------------ live I/O (host slots)
+    def host_arrays(self) -> tuple[np.ndarray, np.ndarray, np.ndarray, np.ndarray]:
+        """numpy views of the pinned slot buffers (host_slots rings): in [C,64] u8, inmeta [C] u32,
+        out [C,64] u8, meta [C] u32.  The producer writes `in` / `inmeta` before publishing."""
+        c = self.capacity
+        pin, pim, pout, pmeta = self.eng.host_view()
+
+        def view(ptr, n, dt):
+            return np.ctypeslib.as_array((ctypes.c_uint8 * (n * np.dtype(dt).itemsize)).from_address(ptr)).view(dt)
+
+        return (view(pin, c * 64, np.uint8).reshape(c, 64), view(pim, c, np.uint32),
+                view(pout, c * 64, np.uint8).reshape(c, 64), view(pmeta, c, np.uint32))
+
+    def reset_side(self) -> None:
+        """Empty the side list before a burst (the ring must be idle: every published chunk done)."""
+        if self._side is not None:
+            self.dp._dev["side_cnt"][:] = 0
+            _torch().cuda.current_stream(self.dp.tdev).synchronize()
+
+    def side_pass(self) -> dict:
+        """Side kernel over what the ring put on the side list since reset_side() (replicas,
+        learn events applied to the device MAC table, tunnel outer headers); rep_src are ring
+        slot indices.  Call once the burst's chunks completed."""
+        if self._side is None:
+            return {"n_rep": 0}
+        dp = self.dp
+        s = _torch().cuda.current_stream(dp.tdev).cuda_stream
+        dp.nf.launch_side(dp.tables_ptrs(), self.eng.dev_in(), self.eng.dev_inmeta(), self.eng.dev_out(),
+                          self.eng.dev_meta(), self._side, dp._ptr("port_ctr"), dp._ptr("drop_ctr"), s)
+        dp._apply_learn(s)
+        return dp.side_result()
 
     def publish(self, n: int) -> int:
         return int(self.eng.publish(int(n)))

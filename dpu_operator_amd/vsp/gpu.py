@@ -97,7 +97,7 @@ class GpuVsp(VspBase):
     def __init__(self, path_manager=None, device: str | None = None, nl: NetlinkManager | None = None,
                  opi_port: int = 0, flow_buckets: int = 1 << 16, vport_prefix: str = "dpuvp",
                  hash_mode: str = "mfma", acl_mode: str = "mfma", state_dir: str | None = None,
-                 live: bool = False, uplink=None):
+                 live: bool = False, uplink=None, live_engine: str = "batch"):
         super().__init__(path_manager)
         if device is None:
             try:
@@ -122,6 +122,7 @@ class GpuVsp(VspBase):
         self._salt = int.from_bytes(os.urandom(1), "little")
         self.chain_kinds: dict[str, list[str]] = {}
         self.live = live
+        self.live_engine = live_engine              # "batch" (fused kernel per cycle) or "ring" (resident kernel)
         self.taps: dict[int, object] = {}       # live mode: port -> TapPort
         self.livepath = None
         self.uplink = uplink                    # live mode: netdev (read/write/fd) of the wire port
@@ -267,7 +268,7 @@ class GpuVsp(VspBase):
             ports = dict(self.taps)
             if self.uplink is not None:
                 ports[WIRE_PORT] = self.uplink
-            self.livepath = LivePath(self.dp, ports).start()
+            self.livepath = LivePath(self.dp, ports, engine=self.live_engine if self.dp.gpu else "batch").start()
         if not self.opi_port:
             self.opi_port = self._free_port()
         return "127.0.0.1", self.opi_port

@@ -1,0 +1,146 @@
+"""The live packet loop (dataplane/netio.py LivePath) over socket-pair "netdevs": no privileges
+needed, so it runs everywhere (the TAP + network-namespace version is tests/test_livepath.py).
+
+A socket pair stands in for each vport: the test writes frames into one end (what the pod sends)
+and reads what the data plane delivered from the same end (what the pod receives).  The bridge is
+OvS-NORMAL style (learning, ARP copies to the slow path, flooding, a mirror port), the traffic mixes
+broadcast ARP, unknown unicast, learned unicast and jumbo frames.
+
+* CPU: the batch engine over the C++ oracle; delivered frames are checked against the bridge's
+  expected behaviour.
+* GPU: the persistent ring kernel with its slots in pinned host memory (engine="ring") must
+  deliver exactly what the oracle's batch loop delivers (per port, as multisets: replicas come off
+  the side list in atomic order).
+"""
+from __future__ import annotations
+
+import socket
+
+import numpy as np
+import pytest
+
+from dpu_operator_amd.dataplane import tables as T
+from dpu_operator_amd.dataplane.engine import DataPlane
+from dpu_operator_amd.dataplane.netio import LivePath
+from dpu_operator_amd.ops import packets as P
+
+MACS = ["02:00:00:00:0a:01", "02:00:00:00:0b:01", "02:00:00:00:0c:01", "02:00:00:00:0d:01"]
+BR = 5
+
+
+class SockPort:
+    """A vport made of a datagram socket pair: `a` is the data plane's end, `b` the pod's."""
+
+    def __init__(self):
+        self.a, self.b = socket.socketpair(socket.AF_UNIX, socket.SOCK_DGRAM)
+        for s in (self.a, self.b):
+            s.setsockopt(socket.SOL_SOCKET, socket.SO_SNDBUF, 1 << 21)
+            s.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 1 << 21)
+        self.a.setblocking(False)
+        self.b.setblocking(False)
+        self.fd = self.a.fileno()
+
+    # data-plane side (LivePath)
+    def read(self):
+        try:
+            return self.a.recv(1 << 16)
+        except BlockingIOError:
+            return None
+
+    def write(self, frame: bytes) -> bool:
+        self.a.send(frame)
+        return True
+
+    # pod side (the test)
+    def inject(self, frame: bytes) -> None:
+        self.b.send(frame)
+
+    def drain(self) -> list[bytes]:
+        out = []
+        while True:
+            try:
+                out.append(self.b.recv(1 << 16))
+            except BlockingIOError:
+                return out
+
+    def close(self) -> None:
+        self.a.close()
+        self.b.close()
+
+
+def _bridge(device):
+    dp = DataPlane(device=device, flow_buckets=1 << 10, mac_slots=1 << 10)
+    for p in range(4):
+        dp.ports.set(p, flags=T.PORT_VALID | T.PORT_LEARN | T.PORT_ARP_TRAP, bridge_id=BR)
+    dp.flood.set_members(BR, [0, 1, 2, 3])
+    dp.ports.set_mirror(2, 3)
+    dp.commit(full=True)
+    return dp
+
+
+def _frame(dst, src, size, seq):
+    fr, ln = P.craft_full(1, dmac=dst, smac=src, src_ip=0x0A000001 + seq, dst_ip=0x0A000002, sport=1000 + seq,
+                          dport=2000, frame_len=size, payload_seed=seq)
+    return bytes(fr[0, : int(ln[0])])
+
+
+def _trace():
+    """(in_port, frame) bursts: ARP broadcast, replies, unknown unicast, learned unicast, jumbo."""
+    arp, al = P.craft_arp(1, smac=MACS[0], sender_ip=0x0A000001, target_ip=0x0A000002)
+    b1 = [(0, bytes(arp[0, : int(al[0])]))]
+    b2 = [(1, _frame(MACS[0], MACS[1], 64, 1)), (2, _frame("02:00:00:00:0f:0f", MACS[2], 200, 2))]
+    b3 = [(0, _frame(MACS[1], MACS[0], 1500, 3)), (0, _frame(MACS[2], MACS[0], 9000, 4)),
+          (3, _frame(MACS[0], MACS[3], 576, 5)), (2, _frame(MACS[0], MACS[2], 64, 6))]
+    return [b1, b2, b3]
+
+
+def _run(dp, engine):
+    ports = {i: SockPort() for i in range(4)}
+    punts = []
+    live = LivePath(dp, ports, engine=engine, ring_capacity=1024,
+                    on_punt=lambda f, p, r: punts.append((p, r, f)))
+    got = []
+    try:
+        for burst in _trace():
+            for p, f in burst:
+                ports[p].inject(f)
+            n = 0
+            for _ in range(20):
+                n += live.poll_once(0.05)
+                if n >= len(burst):
+                    break
+            assert n == len(burst)
+            got.append({p: sorted(ports[p].drain()) for p in ports})
+        return got, punts, live.stats, dp
+    finally:
+        live.stop()
+        for p in ports.values():
+            p.close()
+
+
+def test_batch_engine_over_socket_ports_oracle():
+    got, punts, stats, dp = _run(_bridge("cpu"), "batch")
+    b1, b2, b3 = got
+    # ARP broadcast from port 0: flooded to 1, 2, 3 and copied to the slow path
+    assert [len(b1[p]) for p in range(4)] == [0, 1, 1, 1]
+    assert [r for _, r, _ in punts] == [12]
+    # the reply to the learned MAC goes to port 0 only; unknown unicast from port 2 floods to
+    # 0, 1, 3, and port 3 (port 2's mirror) also gets the mirror copy
+    assert [len(b2[p]) for p in range(4)] == [2, 1, 0, 2]
+    # learned unicast incl. a 9000-B jumbo frame
+    assert any(len(f) == 9000 for f in b3[2]) and any(len(f) == 1500 for f in b3[1])
+    assert stats["rx"] == 7 and stats["replicas"] == 6
+    assert [len(f) for f in b3[3]] == [64]          # port 2's mirror copy of its frame to port 0
+    dp.pull_learned()
+    assert {(b, m) for b, m, _ in dp.macs.learned()} >= {(BR, MACS[0]), (BR, MACS[1]), (BR, MACS[2])}
+
+
+@pytest.mark.gpu
+def test_ring_engine_matches_batch_oracle():
+    want, wpunts, _, _ = _run(_bridge("cpu"), "batch")
+    got, gpunts, stats, dp = _run(_bridge("cuda"), "ring")
+    assert got == want
+    assert sorted((p, r, f) for p, r, f in gpunts) == sorted((p, r, f) for p, r, f in wpunts)
+    assert stats["rx"] == 7 and stats.get("ring_relaunch") == 0
+    dp.pull_learned()
+    assert {(b, m) for b, m, _ in dp.macs.learned()} >= {(BR, MACS[0]), (BR, MACS[1]), (BR, MACS[2])}

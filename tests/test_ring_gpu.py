@@ -211,6 +211,7 @@ def test_ring_live_flow_churn_no_torn_lookups():
     fresh_base = 0x0B000000
     stop = threading.Event()
     stats = {"ops": 0, "commits": 0, "err": None}
+    committed = {"ver": ver.copy()}   # versions every commit so far has made visible
 
     def updater():
         erased = np.zeros(0, np.int64)
@@ -240,7 +241,9 @@ def test_ring_live_flow_churn_no_torn_lookups():
                     dp.flows.erase_many(fresh_live)
                 fresh_live = fk
                 k += 1
+                snap = ver.copy()
                 dp.commit()
+                committed["ver"] = snap
                 stats["ops"] += 1000 + 2 * 500 + 2 * 1000
                 stats["commits"] += 1
         except BaseException as e:  # noqa: BLE001
@@ -257,7 +260,9 @@ def test_ring_live_flow_churn_no_torn_lookups():
         th.start()
         p99 = []
         while time.perf_counter() - t0 < 3.0 and stats["err"] is None:
+            v_lo = committed["ver"].copy()           # committed before the lap's first publish
             lat, _ = ring.probe(batches=CAPL // 1024, batch=1024, inflight=2)   # one lap, host-paced
+            v_hi = ver.copy()
             p99.append(np.percentile(lat, 99))
             out, meta = ring.peek()
             port, _, reason = __import__("dpu_operator_amd.ops.packets", fromlist=["x"]).meta_fields(meta)
@@ -266,7 +271,10 @@ def test_ring_live_flow_churn_no_torn_lookups():
             nat_port = out[:, 38:40].copy().view("<u2").ravel().astype(np.uint32)
             f_ip = nat_ip >> 12
             v_ip = nat_ip & 0xFFF
-            good = ok & (f_ip == fl) & (nat_port == ((fl.astype(np.uint32) * 7 + v_ip) & 0xFFFF)) & (v_ip <= (ver[fl] & 0xFFF))
+            # the action of the flow itself, whole, and no older than what was committed before
+            # the lap began (a stale cached bucket line would show an older version)
+            good = (ok & (f_ip == fl) & (nat_port == ((fl.astype(np.uint32) * 7 + v_ip) & 0xFFFF))
+                    & (v_ip >= (v_lo[fl] & 0xFFF)) & (v_ip <= (v_hi[fl] & 0xFFF)))
             torn += int((ok & ~good).sum())
             hits += int(good.sum())
             is_churn = fl >= NT // 2
