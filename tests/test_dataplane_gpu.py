@@ -316,3 +316,32 @@ def test_bench_multirank_rehearsal_on_one_gpu(mode, n):
     assert line["n_gpus"] == n and line["forwarded_fraction"] == 1.0
     assert line["config"]["global_batch"] == n << 16
     assert line["exchange"]["a2a_per_step"] >= 1 and line["exchange"]["xgmi_bytes_out_per_gpu_per_step"] > 0
+
+
+@pytest.mark.gpu
+def test_batch_larger_than_one_launch():
+    """A batch of 2^24 + 64K packets (1.1 GB of header slots): DataPlane.run splits it into
+    launches of <= 2^24 slots (32-bit buffer views); every slot and every counter matches the
+    oracle."""
+    import torch
+
+    from dpu_operator_amd.dataplane import scenario as S
+    from dpu_operator_amd.dataplane.engine import DataPlane
+
+    g = DataPlane(device="cuda", flow_buckets=1 << 12)
+    c = DataPlane(device="cpu", flow_buckets=1 << 12)
+    for dp in (g, c):
+        sc = S.build_sfc(dp, n_pods=8, n_flows=4096, n_acl=64, seed=0)
+        dp.commit(full=True)
+    pk1, im1 = S.traffic(sc, 1 << 20, seed=3)
+    n = (1 << 24) + (1 << 16)
+    reps = n // len(pk1) + 1
+    pk = np.tile(pk1, (reps, 1))[:n]
+    im = np.tile(im1, reps)[:n]
+    assert g.MAX_LAUNCH < n
+    r = g.run(torch.from_numpy(pk).cuda(), torch.from_numpy(im.view(np.int32)).cuda())
+    torch.cuda.synchronize()
+    rc = c.run(pk, im)
+    assert np.array_equal(r.meta.cpu().numpy().view(np.uint32), rc.meta)
+    assert np.array_equal(r.out.cpu().numpy(), rc.out)
+    assert np.array_equal(g.port_counters(), c.port_counters())
