@@ -379,6 +379,31 @@ def main() -> None:
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             p50_small = float(t.item())
 
+    # host round trip of a small batch (outside the timed region, 1 GPU): submit -> results ready
+    # on the host clock, with per-batch launches vs one replay of the captured HIP graph
+    rtt = None
+    if not a.no_lowlat and world == 1 and a.io == "device" and not sharded:
+        nb = 256
+        pk, im = batches[0][0][:nb].contiguous(), batches[0][1][:nb].contiguous()
+        o3, m3, l3 = dp.alloc_batch(nb)
+        gr = dp.capture(nb)
+
+        def _rtt(fn, reps=300):
+            for _ in range(20):
+                fn()
+            torch.cuda.synchronize()
+            ts = []
+            for _ in range(reps):
+                t = time.perf_counter()
+                fn()
+                torch.cuda.synchronize()
+                ts.append((time.perf_counter() - t) * 1e6)
+            return float(np.median(ts))
+
+        rtt = {"batch": nb, "launch_p50_us": round(_rtt(lambda: dp.run(pk, im, o3, m3, l3)), 2),
+               "graph_p50_us": round(_rtt(lambda: gr()), 2)}
+        del gr
+
     # low-latency path (outside the timed region): persistent ring kernel, host publishes 64-packet
     # chunks and times publish -> completion flag on its own clock (dataplane/ring.py)
     ring = None
@@ -447,6 +472,7 @@ def main() -> None:
             "p50_latency_us": round(p50, 2),
             "p99_latency_us": round(p99, 2),
             "p50_latency_us_64k_batch": None if p50_small is None else round(p50_small, 2),
+            "small_batch_host_rtt": rtt,
             # persistent ring kernel: 64-packet chunks, host-clock publish -> completion RTT
             "p50_latency_us_ring": None if not ring or "p50_us" not in ring else ring["p50_us"],
             "ring": ring,

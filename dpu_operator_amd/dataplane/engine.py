@@ -83,6 +83,7 @@ class DataPlane:
         self.MAX_LAUNCH = 1 << 24
         self.flow_totals = np.zeros((self.flows.nbuckets * 4, 2), np.uint64)
         self.latency = LatencyStats()   # packet-path latency histograms (utils/latency.py)
+        self._gen = 0                   # bumped whenever a device buffer address changes
         self._flow_active = 0           # flow-table copy in use (double buffered under running rings)
         self._flow_lag = np.zeros(0, np.int64)
         self.flip_stats = {"flips": 0, "grace_s": 0.0, "update_s": 0.0, "buckets": 0}
@@ -109,6 +110,7 @@ class DataPlane:
     # ------------------------------------------------------------------ buffers
     def _buf(self, name: str, arr: np.ndarray):
         """Upload/replace a host array as a device buffer (torch uint8 view on GPU)."""
+        self._gen += 1  # device addresses change: captured graphs must be re-captured
         arr = np.ascontiguousarray(arr)
         if self.gpu:
             torch = _torch()
@@ -119,6 +121,7 @@ class DataPlane:
         return self._dev[name]
 
     def _zeros(self, name: str, n: int, dtype=np.uint64):
+        self._gen += 1
         if self.gpu:
             torch = _torch()
             tdt = {np.uint64: torch.int64, np.uint32: torch.int32, np.uint8: torch.uint8}[dtype]
@@ -215,6 +218,7 @@ class DataPlane:
         self._push_buckets(rows, self._flows_key(inactive))
         _torch().cuda.current_stream(self.tdev).synchronize()   # the copy is complete before any wave can pick it
         self._flow_active = inactive
+        self._gen += 1
         for r in rings:
             r.eng.flip()
         self._flow_lag = dirty
@@ -454,6 +458,10 @@ class DataPlane:
             self._apply_learn()
         return BatchResult(out, meta, n, {"hash": hashes, "acl": acl})
 
+    def capture(self, n: int) -> "GraphedRun":
+        """A batch of n slots as a captured HIP graph (see GraphedRun)."""
+        return GraphedRun(self, n)
+
     def launch(self, pkts: int, inmeta: int, n: int, out: int, meta: int, lat: int = 0, t0: int | None = None,
                stream: int | None = None, n_dev: int = 0, flags: int = 0) -> None:
         """Pointer-level fused launch on the GPU (no batch checks): `n_dev` (optional) is a device
@@ -527,3 +535,55 @@ class DataPlane:
     def reset_counters(self) -> None:
         self._alloc_counters()
         self.flow_totals[:] = 0
+
+
+class GraphedRun:
+    """`DataPlane.run` over fixed device buffers, captured once as a HIP graph
+    (torch.cuda.CUDAGraph is hipGraph on ROCm): a replay is ONE graph launch for the batch-release
+    stamp, the fused kernel and (when side outputs are active) the side and learn kernels, instead
+    of several host launches - what a launch-bound loop of small batches pays for.
+
+        g = dp.capture(64)
+        r = g(pkts, inmeta)          # copies into the captured input buffers, replays
+
+    The graph holds the tables' device addresses: a commit that reallocates a buffer (or flips the
+    flow-table copy) bumps the data plane's generation and the next call re-captures.  Replays
+    reuse the capture's MAC-learning stamp (aging counts graph replays as one batch)."""
+
+    def __init__(self, dp: DataPlane, n: int):
+        if not dp.gpu:
+            raise RuntimeError("graphs are a GPU feature")
+        torch = _torch()
+        self.dp, self.n = dp, int(n)
+        self.pkts = torch.zeros((self.n, 64), dtype=torch.uint8, device=dp.tdev)
+        self.inmeta = torch.zeros(self.n, dtype=torch.int32, device=dp.tdev)
+        self.out, self.meta, self.lat = dp.alloc_batch(self.n)
+        self.captures = 0
+        self._capture()
+
+    def _capture(self) -> None:
+        torch = _torch()
+        dp = self.dp
+        dp.commit()
+        s = torch.cuda.Stream(dp.tdev)
+        s.wait_stream(torch.cuda.current_stream(dp.tdev))
+        with torch.cuda.stream(s):       # warm-up: one-time kernel attributes, side buffers
+            for _ in range(2):
+                dp.run(self.pkts, self.inmeta, self.out, self.meta, self.lat)
+        torch.cuda.current_stream(dp.tdev).wait_stream(s)
+        torch.cuda.synchronize(dp.tdev)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            dp.run(self.pkts, self.inmeta, self.out, self.meta, self.lat)
+        self.gen = dp._gen
+        self.captures += 1
+
+    def __call__(self, pkts=None, inmeta=None) -> BatchResult:
+        if self.dp._gen != self.gen:
+            self._capture()
+        if pkts is not None:
+            self.pkts.copy_(pkts, non_blocking=True)
+            self.inmeta.copy_(inmeta.view(self.inmeta.dtype) if inmeta.dtype != self.inmeta.dtype else inmeta,
+                              non_blocking=True)
+        self.graph.replay()
+        return BatchResult(self.out, self.meta, self.n, {"lat": self.lat})

@@ -345,3 +345,42 @@ def test_batch_larger_than_one_launch():
     assert np.array_equal(r.meta.cpu().numpy().view(np.uint32), rc.meta)
     assert np.array_equal(r.out.cpu().numpy(), rc.out)
     assert np.array_equal(g.port_counters(), c.port_counters())
+
+
+@pytest.mark.gpu
+def test_graphed_run_matches_oracle_and_recaptures_after_commit():
+    """DataPlane.capture(n): the stamp + fused (+ side + learn) launches of a batch replayed as one
+    HIP graph.  Replays over new inputs match the oracle; a commit that reallocates a table makes
+    the next call re-capture (the graph holds device addresses)."""
+    import torch
+
+    from dpu_operator_amd.dataplane import scenario as S
+    from dpu_operator_amd.dataplane.engine import DataPlane
+
+    g = DataPlane(device="cuda", flow_buckets=1 << 12)
+    c = DataPlane(device="cpu", flow_buckets=1 << 12)
+    for dp in (g, c):
+        sc = S.build_sfc(dp, n_pods=8, n_flows=4096, n_acl=64, seed=0)
+        dp.commit(full=True)
+    gr = g.capture(4096)
+    for seed in (1, 2):
+        pk, im = S.traffic(sc, 4096, seed=seed)
+        r = gr(torch.from_numpy(pk).cuda(), torch.from_numpy(im.view(np.int32)).cuda())
+        torch.cuda.synchronize()
+        rc = c.run(pk, im)
+        assert np.array_equal(r.meta.cpu().numpy().view(np.uint32), rc.meta)
+        assert np.array_equal(r.out.cpu().numpy(), rc.out)
+    assert gr.captures == 1
+    for dp in (g, c):                      # a new ACL rule (before the final permit): buffers reallocated
+        final = dp.acl.rules.pop()
+        dp.acl.add(permit=False, dst="10.128.0.3/32")
+        dp.acl.rules.append(final)
+        dp.acl.version += 1
+        dp.commit()
+    pk, im = S.traffic(sc, 4096, seed=3)
+    r = gr(torch.from_numpy(pk).cuda(), torch.from_numpy(im.view(np.int32)).cuda())
+    torch.cuda.synchronize()
+    rc = c.run(pk, im)
+    assert gr.captures == 2
+    assert np.array_equal(r.meta.cpu().numpy().view(np.uint32), rc.meta)
+    assert (P.meta_fields(rc.meta)[2] == 4).any()     # the new deny rule fired
