@@ -2,6 +2,7 @@
 // plane.  Buffers cross the boundary as raw addresses (torch HBM tensors or numpy host arrays),
 // so no copies and no torch headers are involved; the HIP stream is passed as an integer
 // (torch.cuda.current_stream().cuda_stream).
+#include <algorithm>
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
@@ -48,6 +49,12 @@ TablesView tables_from(const py::dict& d) {
   t.n_lag_groups = val<uint32_t>(d, "n_lag_groups", 0);
   t.flood = ptr<const uint16_t>(d, "flood");
   t.n_flood = t.flood ? val<uint32_t>(d, "n_flood", 0) : 0u;
+  t.lpm6 = ptr<const Lpm6Entry>(d, "lpm6");
+  t.lpm6_mask = t.lpm6 ? val<uint32_t>(d, "lpm6_mask", 0) : 0u;
+  t.lpm6_lens = ptr<const uint8_t>(d, "lpm6_lens");
+  t.n_lpm6_lens = t.lpm6_lens ? val<uint32_t>(d, "n_lpm6_lens", 0) : 0u;
+  if (t.lpm6 && ((t.lpm6_mask + 1) & t.lpm6_mask)) throw std::invalid_argument("lpm6 table size must be a power of two");
+  if (t.n_lpm6_lens > 129) throw std::invalid_argument("at most 129 IPv6 prefix lengths");
   t.lpm24 = ptr<const uint32_t>(d, "lpm24");
   t.lpm8 = ptr<const uint32_t>(d, "lpm8");
   t.n_lpm8 = t.lpm8 ? val<uint32_t>(d, "n_lpm8", 0) : 0u;
@@ -194,6 +201,50 @@ PYBIND11_MODULE(_nfdp, m) {
     return py::make_tuple(t.b1, t.b2);
   });
   m.def("owner_of", &owner_of);
+  // IPv6 FIB (nfdp.h lpm6_lookup): routes [n, 6] = (a0..a3 host-order masked prefix, plen, result)
+  // -> open-addressing table [slots, 8] u32 (<= 50 % load, every entry within kLpm6Probe of its
+  // home slot) + the distinct lengths, longest first.
+  m.def("build_lpm6", [](U32Arr routes) {
+    if (routes.ndim() != 2 || routes.shape(1) != 6) throw std::invalid_argument("build_lpm6 expects [n,6] uint32");
+    const size_t n = routes.shape(0);
+    auto r = routes.unchecked<2>();
+    std::vector<uint8_t> lens;
+    bool seen[129] = {};
+    for (size_t i = 0; i < n; ++i) {
+      if (r(i, 4) > 128) throw std::invalid_argument("IPv6 prefix length > 128");
+      if (!seen[r(i, 4)]) { seen[r(i, 4)] = true; lens.push_back((uint8_t)r(i, 4)); }
+    }
+    std::sort(lens.begin(), lens.end(), [](uint8_t x, uint8_t y) { return x > y; });
+    size_t slots = 16;
+    while (slots < 2 * n) slots <<= 1;
+    std::vector<Lpm6Entry> tab;
+    for (;;) {
+      tab.assign(slots, Lpm6Entry{{0, 0, 0, 0}, kLpm6Empty, 0, {0, 0}});
+      bool ok = true;
+      for (size_t i = 0; i < n && ok; ++i) {
+        const uint32_t a[4] = {r(i, 0), r(i, 1), r(i, 2), r(i, 3)};
+        const uint32_t h = lpm6_hash(a, r(i, 4)) & (uint32_t)(slots - 1);
+        ok = false;
+        for (int probe = 0; probe < kLpm6Probe; ++probe) {
+          Lpm6Entry& e = tab[(h + probe) & (slots - 1)];
+          if (e.plen == kLpm6Empty || (e.plen == r(i, 4) && e.a[0] == a[0] && e.a[1] == a[1] && e.a[2] == a[2] && e.a[3] == a[3])) {
+            for (int w = 0; w < 4; ++w) e.a[w] = a[w];
+            e.plen = r(i, 4); e.result = r(i, 5);
+            ok = true;
+            break;
+          }
+        }
+      }
+      if (ok) break;
+      slots <<= 1;
+    }
+    py::array_t<uint32_t> t({(py::ssize_t)slots, (py::ssize_t)8});
+    std::memcpy(t.mutable_data(), tab.data(), slots * sizeof(Lpm6Entry));
+    py::array_t<uint8_t> l((py::ssize_t)std::max<size_t>(lens.size(), 1));
+    if (!lens.empty()) std::memcpy(l.mutable_data(), lens.data(), lens.size());
+    else l.mutable_data()[0] = 0;
+    return py::make_tuple(t, l, (uint32_t)lens.size());
+  });
   m.def("build_acl_frags", [](U32Arr value, U32Arr mask) {
     if (value.ndim() != 2 || value.shape(1) != 4 || mask.ndim() != 2 || mask.shape(1) != 4 ||
         value.shape(0) != mask.shape(0))

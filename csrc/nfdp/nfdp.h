@@ -268,6 +268,7 @@ struct Parsed {
   bool ipv4;                // IPv4 with IHL=5, first fragment, fully inside the slot
   bool l4;                  // TCP or UDP ports present
   bool arp;                 // EtherType 0x0806
+  bool ipv6;                // EtherType 0x86DD, fixed header inside the slot (routed; L2 otherwise)
 };
 
 NFDP_HD uint32_t be16_at(const uint32_t* s, int byte) {  // byte offset must be even
@@ -306,6 +307,7 @@ NFDP_HD void parse(const uint32_t* d, uint32_t len, Parsed& p) {
   const uint32_t proto = p.s[5] >> 24;
   p.l4 = p.ipv4 && (proto == 6 || proto == 17) && p.len >= 38;
   p.arp = et2 == 0x0806u;
+  p.ipv6 = et2 == 0x86DDu && p.len >= 54 && (p.s[3] >> 20 & 0xFu) == 6u;
 }
 
 NFDP_HD uint32_t dmac_lo(const uint32_t* s) { return s[0]; }
@@ -320,12 +322,23 @@ NFDP_HD void set_smac(uint32_t* s, uint32_t lo, uint32_t hi) {
   s[2] = (lo >> 16) | (hi << 16);
 }
 
+// IPv6 keys fold each address into 32 bits (RSS / ECMP hashing and classification; IPv6 packets
+// are routed or bridged, never looked up in the exact-match flow table) and set bit 8 of meta.
+constexpr uint32_t kKeyV6 = 1u << 8;
+
 NFDP_HD FlowKey make_key(const Parsed& p, uint32_t zone) {
   FlowKey k;
   k.src_ip = raw32_at2(p.s, 26);
   k.dst_ip = raw32_at2(p.s, 30);
   k.ports = p.l4 ? raw32_at2(p.s, 34) : 0u;
   k.meta = (p.s[5] >> 24) | (zone << 16);
+  if (p.ipv6) {
+    const uint32_t nh = p.s[5] & 0xFFu;  // next header (byte 20)
+    k.src_ip = raw32_at2(p.s, 22) ^ raw32_at2(p.s, 26) ^ raw32_at2(p.s, 30) ^ raw32_at2(p.s, 34);
+    k.dst_ip = raw32_at2(p.s, 38) ^ raw32_at2(p.s, 42) ^ raw32_at2(p.s, 46) ^ raw32_at2(p.s, 50);
+    k.ports = ((nh == 6u || nh == 17u) && p.len >= 58) ? raw32_at2(p.s, 54) : 0u;
+    k.meta = nh | kKeyV6 | (zone << 16);
+  }
   return k;
 }
 
@@ -442,6 +455,17 @@ NFDP_HD void out_tail(uint32_t in_len, uint32_t olen, bool xhdr, uint32_t& hl, u
 // Pipeline parameters (kernarg / oracle argument).  Raw pointers into HBM (or host memory
 // for the oracle).  Everything is sized by the control plane; the kernels never allocate.
 // ----------------------------------------------------------------------------------------
+// One IPv6 route: prefix words in host order (a[0] = most significant 32 bits), already masked to
+// `plen` bits; plen 0xFF = empty slot.  32 B.
+struct Lpm6Entry {
+  uint32_t a[4];
+  uint32_t plen;
+  uint32_t result;   // kRouteNh | nexthop or kRouteEcmp | group (as IPv4)
+  uint32_t pad[2];
+};
+constexpr uint32_t kLpm6Empty = 0xFFu;
+constexpr int kLpm6Probe = 16;
+
 struct TablesView {
   const PortEntry* ports;        // kMaxPorts
   const ChainEntry* chains;      // n_chains
@@ -472,6 +496,12 @@ struct TablesView {
   uint32_t n_tunnels;
   const TermEntry* terms;        // term_mask + 1 slots, open addressing (nullable)
   uint32_t term_mask;
+  // IPv6 FIB (P4 ipv6_table): one open-addressing table over (prefix, length) and the distinct
+  // prefix lengths present, longest first; a lookup probes the lengths in that order
+  const Lpm6Entry* lpm6;         // lpm6_mask + 1 slots (nullable: no IPv6 routes)
+  uint32_t lpm6_mask;
+  const uint8_t* lpm6_lens;      // n_lpm6_lens lengths, descending
+  uint32_t n_lpm6_lens;
 };
 
 NFDP_HD uint32_t lpm_lookup(const TablesView& t, uint32_t dst /* host order */) {
@@ -493,6 +523,31 @@ NFDP_HD int route_nexthop(const TablesView& t, uint32_t r, uint32_t hash) {
 }
 NFDP_HD uint32_t term_hash(uint32_t src_ip, uint32_t vni) { return fmix32(src_ip ^ (vni * 0x9E3779B1u)); }
 // (outer src ip raw, vni) -> tunnel port or -1
+NFDP_HD uint32_t lpm6_hash(const uint32_t* a, uint32_t plen) {
+  return fmix32(a[0] ^ fmix32(a[1] ^ fmix32(a[2] ^ fmix32(a[3] ^ (plen * 0x9E3779B9u)))));
+}
+// Longest-prefix match of an IPv6 destination (host-order words): probe each present prefix
+// length, longest first.  Returns the route result or 0.
+NFDP_HD uint32_t lpm6_lookup(const TablesView& t, const uint32_t* dst) {
+  if (!t.lpm6 || !t.lpm6_lens) return 0;
+  for (uint32_t li = 0; li < t.n_lpm6_lens; ++li) {
+    const uint32_t plen = t.lpm6_lens[li];
+    uint32_t m[4];
+    for (int w = 0; w < 4; ++w) {
+      const int bits = (int)plen - 32 * w;
+      const uint32_t mask = bits >= 32 ? 0xFFFFFFFFu : (bits <= 0 ? 0u : ~(0xFFFFFFFFu >> bits));
+      m[w] = dst[w] & mask;
+    }
+    uint32_t h = lpm6_hash(m, plen) & t.lpm6_mask;
+    for (int probe = 0; probe < kLpm6Probe; ++probe) {
+      const Lpm6Entry& e = t.lpm6[(h + probe) & t.lpm6_mask];
+      if (e.plen == kLpm6Empty) break;
+      if (e.plen == plen && e.a[0] == m[0] && e.a[1] == m[1] && e.a[2] == m[2] && e.a[3] == m[3]) return e.result;
+    }
+  }
+  return 0;
+}
+
 NFDP_HD int term_lookup(const TablesView& t, uint32_t src_ip, uint32_t vni) {
   if (!t.terms) return -1;
   const uint32_t h = term_hash(src_ip, vni);

@@ -147,6 +147,29 @@ NFDP_HD uint32_t route_ipv4(const TablesView& t, Parsed& p, uint32_t hash, uint3
   return kOk;
 }
 
+// IPv6 routing (P4 ipv6_table): LPM on the destination, hop limit - 1 (no header checksum in
+// IPv6), neighbour / router MACs, egress port.  Returns a drop reason (0 = routed).
+NFDP_HD uint32_t route_ipv6(const TablesView& t, Parsed& p, uint32_t hash, uint32_t& out_port) {
+  if (!p.ipv6) return kNoRoute;
+  uint32_t dst[4];
+  for (int w = 0; w < 4; ++w) dst[w] = __builtin_bswap32(raw32_at2(p.s, 38 + 4 * w));
+  const int nh = route_nexthop(t, lpm6_lookup(t, dst), hash);
+  if (nh < 0) return kNoRoute;
+  const NextHop n = t.nexthops[nh];
+  if (!n.valid) return kNoRoute;
+  const uint32_t hl = byte_at(p.s, 21);
+  if (hl <= 1u) return kTtlExpired;
+  p.s[5] = (p.s[5] & ~(0xFFu << 8)) | ((hl - 1u) << 8);
+  set_dmac(p.s, n.dmac_lo, n.dmac_hi);
+  set_smac(p.s, n.smac_lo, n.smac_hi);
+  out_port = n.port;
+  return kOk;
+}
+
+NFDP_HD uint32_t route_ip(const TablesView& t, Parsed& p, uint32_t hash, uint32_t& out_port) {
+  return p.ipv6 ? route_ipv6(t, p, hash, out_port) : route_ipv4(t, p, hash, out_port);
+}
+
 // `hit`: flow entry found; `act`: its action; `acl_rule`: first matching ACL rule or -1;
 // `hash`: the packet's Toeplitz hash (LAG member selection uses hash[2:0], K8).
 template <class TA>
@@ -175,11 +198,11 @@ NFDP_HD EgressDecision chain_stage(const TablesView& t, const TA& ta, Parsed& p,
       }
     }
     // router interface (kPortRouted): IPv4 addressed to the port's own MAC is routed
-    if (NFDP_L3_ON && (st.in_flags & kPortRouted) && p.ipv4) {
+    if (NFDP_L3_ON && (st.in_flags & kPortRouted) && (p.ipv4 || p.ipv6)) {
       const PortEntry ip = ta.port(st.in_port);
       if (dmac_lo(p.s) == ip.mac_lo && dmac_hi(p.s) == ip.mac_hi) {
         uint32_t op = kPortNone;
-        const uint32_t r = route_ipv4(t, p, hash, op);
+        const uint32_t r = route_ip(t, p, hash, op);
         if (r) { e.reason = r; e.out_port = r == kNoRoute ? kPortPunt : kPortNone; return e; }
         e.out_port = op;
         const uint32_t r2 = finish_port(t, ta, e.out_port, hash, false, e.push, e.tci, p.len, &e.xhdr);
@@ -264,7 +287,7 @@ NFDP_HD EgressDecision chain_stage(const TablesView& t, const TA& ta, Parsed& p,
         e.reason = kNoRoute; e.out_port = kPortPunt; return e;
       } else if (NFDP_L3_ON && op == kHopRoute) {
         uint32_t rp = kPortNone;
-        const uint32_t r = route_ipv4(t, p, hash, rp);
+        const uint32_t r = route_ip(t, p, hash, rp);
         if (r) { e.reason = r; e.out_port = r == kNoRoute ? kPortPunt : kPortNone; return e; }
         e.out_port = rp;
       }

@@ -67,6 +67,7 @@ class DataPlane:
         self.lag = T.LagTable()
         self.flood = T.FloodTable()
         self.routes = T.RouteTable()
+        self.routes6 = T.Route6Table()
         self.nexthops = T.NextHopTable()
         self.ecmp = T.EcmpTable()
         self.tunnels = T.TunnelTable()
@@ -178,6 +179,8 @@ class DataPlane:
             return False
         if len(self.routes) and (self._versions.get("routes") != self.routes.version or "lpm24" not in self._dev):
             return False
+        if len(self.routes6) and (self._versions.get("routes6") != self.routes6.version or "lpm6" not in self._dev):
+            return False
         return self._versions.get("acl") == self.acl.version
 
     # ------------------------------------------------------------------ live flow updates
@@ -244,6 +247,13 @@ class DataPlane:
             self._n_lpm8 = len(t8) // 256
             self._versions["routes"] = self.routes.version
             sent["routes"] = len(self.routes)
+        if len(self.routes6) and (full or self._versions.get("routes6") != self.routes6.version or "lpm6" not in self._dev):
+            tab, lens, nl = self.routes6.build()
+            self._buf("lpm6", tab)
+            self._buf("lpm6_lens", lens)
+            self._lpm6 = (len(tab) - 1, int(nl))
+            self._versions["routes6"] = self.routes6.version
+            sent["routes6"] = len(self.routes6)
         if full or "rss_key" not in self._dev:
             key = np.frombuffer(self.rss_key, np.uint8)
             self._buf("rss_key", key)
@@ -314,6 +324,10 @@ class DataPlane:
             "ecmp": self._ptr("ecmp"), "n_ecmp": int(self.ecmp.n),
             "tunnels": self._ptr("tunnels") if self.tunnels.n else 0, "n_tunnels": int(self.tunnels.n),
             "terms": self._ptr("terms") if self.terms.n else 0, "term_mask": int(self.terms.mask),
+            "lpm6": self._ptr("lpm6") if len(self.routes6) else 0,
+            "lpm6_mask": int(getattr(self, "_lpm6", (0, 0))[0]),
+            "lpm6_lens": self._ptr("lpm6_lens") if len(self.routes6) else 0,
+            "n_lpm6_lens": int(getattr(self, "_lpm6", (0, 0))[1]),
         }
 
     # ------------------------------------------------------------------ side outputs / learning

@@ -210,6 +210,9 @@ TABLES = [
     # L3 (p4info.txt:696-871): LPM routes, nexthops, ECMP, router-interface MACs
     ("ipv4_table", [("ipv4_table_lpm_root", 32, "EXACT"), ("ipv4_dst_match", 32, "LPM")],
      ["ipv4_set_nexthop_id", "ecmp_hash_action", "NoAction"], 1024),
+    ("ipv6_lpm_root_lut", [("user_meta.cmeta.bit16_zeros", 16, "TERNARY")], ["ipv6_lpm_root_lut_action"], 1),
+    ("ipv6_table", [("ipv6_table_lpm_root", 32, "EXACT"), ("ipv6_dst_match", 128, "LPM")],
+     ["ipv6_set_nexthop_id", "ecmp_v6_hash_action", "NoAction"], 1024),
     ("ecmp_hash_table", [("flex", 16, "TERNARY"), ("hash", 3, "TERNARY")], ["set_nexthop_id", "NoAction"], 1024),
     ("nexthop_table", [("user_meta.cmeta.nexthop_id", 16, "EXACT"), ("bit16_zeros", 8, "EXACT")],
      ["set_nexthop_info_dmac", "set_nexthop_lag", "drop", "NoAction"], 1024),
@@ -222,10 +225,16 @@ TABLES = [
     ("vxlan_encap_mod_table", [("vmeta.common.mod_blob_ptr", 24, "EXACT")], ["vxlan_encap", "NoAction"], 1024),
     ("vxlan_encap_vlan_pop_mod_table", [("vmeta.common.mod_blob_ptr", 24, "EXACT")], ["vxlan_encap_vlan_pop", "NoAction"], 1024),
     ("geneve_encap_mod_table", [("vmeta.common.mod_blob_ptr", 24, "EXACT")], ["geneve_encap", "NoAction"], 1024),
+    ("geneve_encap_vlan_pop_mod_table", [("vmeta.common.mod_blob_ptr", 24, "EXACT")], ["geneve_encap_vlan_pop", "NoAction"], 1024),
+    ("vxlan_decap_and_push_vlan_mod_table", [("vmeta.common.mod_blob_ptr", 24, "EXACT")],
+     ["vxlan_decap_and_push_vlan", "NoAction"], 1024),
+    ("geneve_decap_and_push_vlan_mod_table", [("vmeta.common.mod_blob_ptr", 24, "EXACT")],
+     ["geneve_decap_and_push_vlan", "NoAction"], 1024),
     ("vxlan_decap_mod_table", [("vmeta.common.mod_blob_ptr", 24, "EXACT")], ["vxlan_decap_outer_hdr", "NoAction"], 1024),
     ("geneve_decap_mod_table", [("vmeta.common.mod_blob_ptr", 24, "EXACT")], ["geneve_decap_outer_hdr", "NoAction"], 1024),
     ("ipv4_tunnel_term_table", [("ipv4_src", 32, "EXACT"), ("vni", 24, "EXACT")],
-     ["set_vxlan_decap_outer_hdr", "set_geneve_decap_outer_hdr", "trap_enable"], 1024),
+     ["set_vxlan_decap_outer_hdr", "set_vxlan_decap_outer_and_push_vlan", "set_geneve_decap_outer_hdr",
+      "set_geneve_decap_outer_and_push_vlan", "trap_enable"], 1024),
     ("rx_ipv4_tunnel_source_port", [("ipv4_src", 32, "EXACT"), ("vni", 24, "EXACT")], ["set_source_port", "drop"], 1024),
     # LAG rx, smac learning check, ARP trap (p4info.txt:168, 783, 1011)
     ("rx_lag_table", [("vmeta.common.port_id", 2, "EXACT"), ("user_meta.cmeta.lag_group_id", 8, "EXACT")],
@@ -257,6 +266,9 @@ ACTIONS = {
                         ("store_vsi", 1)],
     "NoAction": [],
     "ipv4_set_nexthop_id": [("nexthop_id", 16)],
+    "ipv6_set_nexthop_id": [("nexthop_id", 16)],
+    "ecmp_v6_hash_action": [("ecmp_group_id", 16)],
+    "ipv6_lpm_root_lut_action": [("ipv6_table_lpm_root", 32)],
     "ecmp_hash_action": [("ecmp_group_id", 16)],
     "set_nexthop_id": [("nexthop_id", 16)],
     "set_nexthop_info_dmac": [("router_interface_id", 16), ("egress_port", 32), ("dmac_high", 16), ("dmac_low", 32)],
@@ -270,6 +282,11 @@ ACTIONS = {
     "vxlan_encap": [("src_addr", 32), ("dst_addr", 32), ("src_port", 16), ("dst_port", 16), ("vni", 24)],
     "vxlan_encap_vlan_pop": [("src_addr", 32), ("dst_addr", 32), ("src_port", 16), ("dst_port", 16), ("vni", 24)],
     "geneve_encap": [("src_addr", 32), ("dst_addr", 32), ("src_port", 16), ("dst_port", 16), ("vni", 24)],
+    "geneve_encap_vlan_pop": [("src_addr", 32), ("dst_addr", 32), ("src_port", 16), ("dst_port", 16), ("vni", 24)],
+    "vxlan_decap_and_push_vlan": [("pcp", 3), ("dei", 1), ("vlan_id", 12)],
+    "geneve_decap_and_push_vlan": [("pcp", 3), ("dei", 1), ("vlan_id", 12)],
+    "set_vxlan_decap_outer_and_push_vlan": [("tunnel_id", 20)],
+    "set_geneve_decap_outer_and_push_vlan": [("tunnel_id", 20)],
     "vxlan_decap_outer_hdr": [],
     "geneve_decap_outer_hdr": [],
     "set_vxlan_decap_outer_hdr": [("tunnel_id", 20)],

@@ -54,12 +54,17 @@ def vsi_of_mac(mac: str | bytes) -> int:
     return b[1]
 
 
+_MAC_RE = re.compile(r"^[0-9a-fA-F]{2}(:[0-9a-fA-F]{2}){5}$")
+
+
 def _int(v: str) -> int:
     v = v.strip()
-    if v.count(".") == 3:                       # dotted IPv4
+    if v.count(".") == 3 and ":" not in v:      # dotted IPv4
         return int(ipaddress.IPv4Address(v))
-    if v.count(":") == 5:                       # MAC
+    if _MAC_RE.match(v):                        # MAC
         return int(v.replace(":", ""), 16)
+    if ":" in v:                                # IPv6 (incl. "::" forms)
+        return int(ipaddress.IPv6Address(v))
     return int(v, 16) if v.lower().startswith("0x") else int(v)
 
 
@@ -385,11 +390,11 @@ class P4Runtime:
         dp.ports.version += 1
 
     def _compile_l3_tunnels(self, dp, port, add_mac, src: dict) -> None:
-        """L3 (ipv4_table, ecmp_hash_table, nexthop / ecmp_nexthop tables, rif_mod_table_*), tunnels
+        """L3 (ipv4_table, ipv6_table, ecmp_hash_table, nexthop / ecmp_nexthop tables, rif_mod_table_*), tunnels
         (l2_to_tunnel_v4, *_encap_mod_table, ipv4_tunnel_term_table, rx_ipv4_tunnel_source_port),
         rx_lag_table, l2_fwd_smac_table and always_trap_arp_table onto the GPU tables."""
         for cidr in self._owned_routes:
-            dp.routes.remove(cidr)
+            (dp.routes6 if ":" in cidr else dp.routes).remove(cidr)
         self._owned_routes = []
         for nh in self._owned_nh:
             dp.nexthops.clear(nh)
@@ -440,6 +445,18 @@ class P4Runtime:
             else:
                 continue
             self._owned_routes.append(cidr)
+        for e in self._rows("ipv6_table"):
+            net, msk = self._k(e, 1)
+            plen = bin(msk).count("1")
+            cidr = f"{ipaddress.IPv6Address(net)}/{plen}"
+            if e.action.endswith("ipv6_set_nexthop_id"):
+                dp.routes6.add(cidr, nexthop=e.params["nexthop_id"])
+            elif e.action.endswith("ecmp_v6_hash_action"):
+                dp.routes6.add(cidr, ecmp_group=e.params["ecmp_group_id"])
+                groups.add(e.params["ecmp_group_id"])
+            else:
+                continue
+            self._owned_routes.append(cidr)
         for g in groups:
             for h in range(T.ECMP_WAYS):
                 for e in self._rows("ecmp_hash_table"):  # highest priority first
@@ -451,7 +468,7 @@ class P4Runtime:
         # tunnels: one tunnel port per destination VTEP; parameters from the encap mod tables
         encap: dict[int, tuple[int, Entry]] = {}
         for kind, tab in ((T.TUN_VXLAN, "vxlan_encap_mod_table"), (T.TUN_VXLAN, "vxlan_encap_vlan_pop_mod_table"),
-                          (T.TUN_GENEVE, "geneve_encap_mod_table")):
+                          (T.TUN_GENEVE, "geneve_encap_mod_table"), (T.TUN_GENEVE, "geneve_encap_vlan_pop_mod_table")):
             for e in self._rows(tab):
                 if e.params:
                     encap[e.params["dst_addr"]] = (kind, e)
@@ -493,6 +510,15 @@ class P4Runtime:
             s_ip, vni = e.key[0][1], e.key[1][1]
             tp = port(TUNNEL_PORT_BASE + 128 + (e.params["tunnel_id"] & 0x7F))
             dp.terms.insert(str(ipaddress.IPv4Address(s_ip)), vni, tp)
+            if e.action.endswith("_and_push_vlan"):
+                # decap + push VLAN (vxlan/geneve_decap_and_push_vlan_mod_table, blob = tunnel_id):
+                # the inner frame leaves the termination port with that vid pushed (K6 semantics)
+                tab = "geneve_decap_and_push_vlan_mod_table" if "geneve" in e.action else "vxlan_decap_and_push_vlan_mod_table"
+                me = next((m for m in self._rows(tab) if m.key[0][1] == e.params["tunnel_id"] and m.params), None)
+                if me is None:
+                    raise P4Error("FAILED_PRECONDITION", f"{e.action} for tunnel {e.params['tunnel_id']} has no {tab} entry")
+                dp.ports.a[tp]["flags"] |= T.PORT_INGRESS_TAG
+                dp.ports.a[tp]["ext"] = (int(dp.ports.a[tp]["ext"]) & ~0xFFF) | (me.params["vlan_id"] & 0xFFF)
             if (s_ip, vni) in sp_of:
                 bm = {e2.key[0][1]: e2.params["bridge_id"] for e2 in self._rows("source_port_to_bridge_map")
                       if e2.key[0][2] == 0xFFFF and e2.action.endswith("set_bridge_id")}

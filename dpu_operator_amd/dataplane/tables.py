@@ -296,6 +296,58 @@ class RouteTable:
         return t24, tbl8
 
 
+class Route6Table:
+    """IPv6 routes (P4 ipv6_table, LPM) -> nexthop id or ECMP group.  Compiled (native
+    `build_lpm6`) to one open-addressing table over (masked prefix, length) plus the distinct
+    lengths present, longest first; the kernels probe the lengths in that order (nfdp.h
+    lpm6_lookup): a handful of probes for a real FIB's few lengths, no 2^24-entry array."""
+
+    def __init__(self):
+        self.routes: dict[tuple[int, int], int] = {}
+        self.version = 0
+
+    @staticmethod
+    def _net(cidr) -> tuple[int, int]:
+        n = ipaddress.IPv6Network(cidr, strict=False)
+        return int(n.network_address), n.prefixlen
+
+    def add(self, cidr, nexthop: int | None = None, ecmp_group: int | None = None) -> None:
+        if (nexthop is None) == (ecmp_group is None):
+            raise ValueError("a route points at exactly one of nexthop / ecmp_group")
+        if (nexthop or ecmp_group or 0) > 0xFFFF:
+            raise ValueError("nexthop / group id must fit 16 bits")
+        self.routes[self._net(cidr)] = (ROUTE_NH | nexthop) if nexthop is not None else (ROUTE_ECMP | ecmp_group)
+        self.version += 1
+
+    def remove(self, cidr) -> bool:
+        ok = self.routes.pop(self._net(cidr), None) is not None
+        self.version += ok
+        return ok
+
+    def __len__(self) -> int:
+        return len(self.routes)
+
+    def lookup(self, ip) -> int:
+        """Reference LPM for tests: the route result or 0."""
+        x = int(ipaddress.IPv6Address(ip)) if not isinstance(ip, (int, np.integer)) else int(ip)
+        best, res = -1, 0
+        for (net, plen), r in self.routes.items():
+            m = 0 if plen == 0 else ((1 << 128) - 1) ^ ((1 << (128 - plen)) - 1)
+            if (x & m) == net and plen > best:
+                best, res = plen, r
+        return res
+
+    def build(self):
+        """-> (table [slots, 8] u32, lengths u8, n_lengths)."""
+        from ..native import nfdp
+
+        rows = np.zeros((len(self.routes), 6), np.uint32)
+        for i, ((net, plen), res) in enumerate(self.routes.items()):
+            rows[i, :4] = [(net >> (96 - 32 * w)) & 0xFFFFFFFF for w in range(4)]
+            rows[i, 4], rows[i, 5] = plen, res
+        return nfdp().build_lpm6(rows)
+
+
 class NextHopTable:
     """nexthop_table + rif_mod_table: id -> (egress port, neighbour MAC, router-interface MAC)."""
 

@@ -136,6 +136,53 @@ def craft_arp(n: int, *, smac, sender_ip, target_ip, op: int = 1, vlan=None, dma
     return fr, lens
 
 
+def craft6_full(n: int, *, dmac, smac, src6, dst6, sport, dport, hop_limit=64, frame_len: int = 78,
+                payload_seed: int = 0) -> tuple[np.ndarray, np.ndarray]:
+    """n IPv6 / UDP frames (whole frames, untagged, no FCS) with a valid UDP checksum.
+    `src6` / `dst6`: one address or a sequence of n (str or int); per-packet hop limits and
+    ports allowed.  Returns (frames uint8[n, frame_len], lens)."""
+    import ipaddress
+
+    if frame_len < 62 or frame_len > MAX_FRAME - 4:
+        raise ValueError("frame_len must hold Ethernet + IPv6 + UDP")
+
+    def addrs(a):
+        seq = a if isinstance(a, (list, tuple, np.ndarray)) else [a] * n
+        return np.array([list(int(ipaddress.IPv6Address(x) if not isinstance(x, (int, np.integer)) else int(x))
+                              .to_bytes(16, "big")) for x in seq], np.uint8)
+
+    fr = np.zeros((n, frame_len), np.uint8)
+    fr[:, 0:6] = np.broadcast_to(mac_bytes(dmac) if np.ndim(dmac) <= 1 else np.asarray(dmac, np.uint8), (n, 6))
+    fr[:, 6:12] = np.broadcast_to(mac_bytes(smac) if np.ndim(smac) <= 1 else np.asarray(smac, np.uint8), (n, 6))
+    _put16(fr, 12, np.full(n, 0x86DD))
+    fr[:, 14] = 0x60
+    plen = frame_len - 54
+    _put16(fr, 18, np.full(n, plen))
+    fr[:, 20] = 17
+    fr[:, 21] = np.broadcast_to(np.asarray(hop_limit, np.uint8), (n,))
+    fr[:, 22:38] = addrs(src6)
+    fr[:, 38:54] = addrs(dst6)
+    _put16(fr, 54, np.broadcast_to(np.asarray(sport, np.uint32), (n,)))
+    _put16(fr, 56, np.broadcast_to(np.asarray(dport, np.uint32), (n,)))
+    _put16(fr, 58, np.full(n, plen))
+    rng = np.random.default_rng(payload_seed)
+    fr[:, 62:] = rng.integers(0, 256, (n, frame_len - 62), dtype=np.uint8)
+    # UDP checksum over the IPv6 pseudo-header (src, dst, length, next header) + UDP header + data
+    seg = fr[:, 54:].copy()
+    if seg.shape[1] & 1:
+        seg = np.concatenate([seg, np.zeros((n, 1), np.uint8)], axis=1)
+    words = (seg[:, 0::2].astype(np.uint64) << 8) | seg[:, 1::2]
+    ps = fr[:, 22:54]
+    pw = (ps[:, 0::2].astype(np.uint64) << 8) | ps[:, 1::2]
+    c = words.sum(axis=1) + pw.sum(axis=1) + plen + 17
+    while (c >> 16).any():
+        c = (c & 0xFFFF) + (c >> 16)
+    c = (~c) & 0xFFFF
+    c[c == 0] = 0xFFFF
+    _put16(fr, 60, c.astype(np.uint32))
+    return fr, np.full(n, frame_len, np.uint32)
+
+
 def header_slots(frames: np.ndarray, lens: np.ndarray) -> np.ndarray:
     """[n, stride] frames -> [n, 64] header slots (first min(len, 64) bytes, zero padded)."""
     slots = np.zeros((frames.shape[0], SLOT), np.uint8)

@@ -98,3 +98,68 @@ def test_pipeline_table_count():
     from dpu_operator_amd.dataplane.p4info import MI355X_P4INFO
 
     assert len(MI355X_P4INFO.tables) >= 38
+
+
+def test_ipv6_table_entries_route_packets(rt):
+    """ipv6_table (p4info.txt:871: ipv6_table_lpm_root exact + ipv6_dst_match LPM /128) with
+    ipv6_set_nexthop_id and ecmp_v6_hash_action, compiled onto the IPv6 FIB; the root LUT is
+    accepted (the GPU FIB needs no root split)."""
+    dp = rt.dp
+    add = rt.add_entry
+    add(C + "ipv6_lpm_root_lut", "user_meta.cmeta.bit16_zeros=0/0,priority=1,"
+        "action=linux_networking_control.ipv6_lpm_root_lut_action(0)")
+    for nh in (1, 2):
+        add(C + "nexthop_table", f"user_meta.cmeta.nexthop_id={nh},bit16_zeros=0,"
+            f"action=linux_networking_control.set_nexthop_info_dmac(5,{nh},0x0250,0x0000000{nh})")
+    add(C + "ipv6_table", "ipv6_table_lpm_root=0,ipv6_dst_match=2001:db8::/32,"
+        "action=linux_networking_control.ipv6_set_nexthop_id(1)")
+    add(C + "ipv6_table", "ipv6_table_lpm_root=0,ipv6_dst_match=2001:db8:5::/48,"
+        "action=linux_networking_control.ecmp_v6_hash_action(4)")
+    for h in range(8):
+        add(C + "ecmp_hash_table", f"flex=4,hash={h},priority=10,"
+            f"action=linux_networking_control.set_nexthop_id({1 + (h & 1)})")
+    with pytest.raises(P4Error):  # beyond 128 bits
+        add(C + "ipv6_table", "ipv6_table_lpm_root=0,ipv6_dst_match=2001:db8::/129,"
+            "action=linux_networking_control.NoAction()")
+    assert len(dp.routes6) == 2
+    assert dp.routes6.lookup("2001:db8:5::1") == T.ROUTE_ECMP | 4
+    dp.ports.set(PHY_BASE + 1, flags=T.PORT_VALID | T.PORT_ROUTED, mac="02:40:00:00:00:01")
+    dp.commit()
+
+    def send6(dst, sport=9):
+        fr, ln = P.craft6_full(1, dmac="02:40:00:00:00:01", smac="02:00:00:00:00:99", src6="2001:db8:9::1",
+                               dst6=dst, sport=sport, dport=80)
+        r = dp.run(P.header_slots(fr, ln), P.inmeta(np.array([PHY_BASE + 1]), ln))
+        op, _, rs = P.meta_fields(r.meta)
+        return int(op[0]), int(rs[0]), r.out[0]
+
+    op, rs, out = send6("2001:db8:1::1")
+    assert (op, rs) == (PHY_BASE + 1, 0) and bytes(out[0:6]) == bytes.fromhex("025000000001") and out[21] == 63
+    assert {send6("2001:db8:5::7", sport=s)[0] for s in range(1, 40)} == {PHY_BASE + 1, PHY_BASE + 2}
+    assert send6("2600::1")[1] == 5  # no route
+    rt.del_entry(C + "ipv6_table", "ipv6_table_lpm_root=0,ipv6_dst_match=2001:db8::/32")
+    assert len(dp.routes6) == 1
+
+
+def test_geneve_vlan_pop_encap_and_decap_push_vlan(rt):
+    """geneve_encap_vlan_pop_mod_table (GENEVE encap of the untagged inner frame) and
+    set_geneve_decap_outer_and_push_vlan + geneve_decap_and_push_vlan_mod_table: the terminated
+    inner frame leaves its tunnel's port with the mod entry's vid pushed."""
+    dp = rt.dp
+    add = rt.add_entry
+    add(C + "geneve_encap_vlan_pop_mod_table", "vmeta.common.mod_blob_ptr=9,"
+        "action=linux_networking_control.geneve_encap_vlan_pop(192.0.2.1,192.0.2.3,0,6081,9000)")
+    add(C + "l2_to_tunnel_v4", "hdrs.mac[vmeta.common.depth].da=02:00:00:00:cc:01,"
+        "action=linux_networking_control.set_tunnel_v4(192.0.2.3)")
+    add(C + "geneve_decap_and_push_vlan_mod_table", "vmeta.common.mod_blob_ptr=2,"
+        "action=linux_networking_control.geneve_decap_and_push_vlan(0,0,321)")
+    add(C + "ipv4_tunnel_term_table", "ipv4_src=192.0.2.3,vni=9000,"
+        "action=linux_networking_control.set_geneve_decap_outer_and_push_vlan(2)")
+    assert dp.tunnels.n == 1 and int(dp.tunnels.a[0]["type"]) == T.TUN_GENEVE
+    tp = TUNNEL_PORT_BASE + 128 + 2
+    assert dp.ports.a[tp]["flags"] & T.PORT_INGRESS_TAG and int(dp.ports.a[tp]["ext"]) & 0xFFF == 321
+    # an inner frame re-entering on the termination port leaves tagged with vid 321
+    dp.ports.update(tp, bridge_id=0, default_out=5)
+    dp.ports.set(5, flags=T.PORT_VALID, bridge_id=0)
+    op, rs, out = _send(dp, tp, "02:00:00:00:00:05", "10.0.0.9")
+    assert (op, rs) == (5, 0) and bytes(out[12:16]) == b"\x81\x00" + (321).to_bytes(2, "big")
