@@ -223,7 +223,7 @@ PYBIND11_MODULE(_nfdp, m) {
       bool ok = true;
       for (size_t i = 0; i < n && ok; ++i) {
         const uint32_t a[4] = {r(i, 0), r(i, 1), r(i, 2), r(i, 3)};
-        const uint32_t h = lpm6_hash(a, r(i, 4)) & (uint32_t)(slots - 1);
+        const uint32_t h = lpm6_hash(a[0], a[1], a[2], a[3], r(i, 4)) & (uint32_t)(slots - 1);
         ok = false;
         for (int probe = 0; probe < kLpm6Probe; ++probe) {
           Lpm6Entry& e = tab[(h + probe) & (slots - 1)];

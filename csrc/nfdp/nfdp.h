@@ -18,6 +18,9 @@
 #include <stdint.h>
 
 #define NFDP_HD __host__ __device__ __forceinline__
+#ifndef NFDP_IPV6
+#define NFDP_IPV6 1
+#endif
 
 namespace nfdp {
 
@@ -307,7 +310,11 @@ NFDP_HD void parse(const uint32_t* d, uint32_t len, Parsed& p) {
   const uint32_t proto = p.s[5] >> 24;
   p.l4 = p.ipv4 && (proto == 6 || proto == 17) && p.len >= 38;
   p.arp = et2 == 0x0806u;
+#if NFDP_IPV6
   p.ipv6 = et2 == 0x86DDu && p.len >= 54 && (p.s[3] >> 20 & 0xFu) == 6u;
+#else
+  p.ipv6 = false;
+#endif
 }
 
 NFDP_HD uint32_t dmac_lo(const uint32_t* s) { return s[0]; }
@@ -322,23 +329,12 @@ NFDP_HD void set_smac(uint32_t* s, uint32_t lo, uint32_t hi) {
   s[2] = (lo >> 16) | (hi << 16);
 }
 
-// IPv6 keys fold each address into 32 bits (RSS / ECMP hashing and classification; IPv6 packets
-// are routed or bridged, never looked up in the exact-match flow table) and set bit 8 of meta.
-constexpr uint32_t kKeyV6 = 1u << 8;
-
 NFDP_HD FlowKey make_key(const Parsed& p, uint32_t zone) {
   FlowKey k;
   k.src_ip = raw32_at2(p.s, 26);
   k.dst_ip = raw32_at2(p.s, 30);
   k.ports = p.l4 ? raw32_at2(p.s, 34) : 0u;
   k.meta = (p.s[5] >> 24) | (zone << 16);
-  if (p.ipv6) {
-    const uint32_t nh = p.s[5] & 0xFFu;  // next header (byte 20)
-    k.src_ip = raw32_at2(p.s, 22) ^ raw32_at2(p.s, 26) ^ raw32_at2(p.s, 30) ^ raw32_at2(p.s, 34);
-    k.dst_ip = raw32_at2(p.s, 38) ^ raw32_at2(p.s, 42) ^ raw32_at2(p.s, 46) ^ raw32_at2(p.s, 50);
-    k.ports = ((nh == 6u || nh == 17u) && p.len >= 58) ? raw32_at2(p.s, 54) : 0u;
-    k.meta = nh | kKeyV6 | (zone << 16);
-  }
   return k;
 }
 
@@ -523,26 +519,27 @@ NFDP_HD int route_nexthop(const TablesView& t, uint32_t r, uint32_t hash) {
 }
 NFDP_HD uint32_t term_hash(uint32_t src_ip, uint32_t vni) { return fmix32(src_ip ^ (vni * 0x9E3779B1u)); }
 // (outer src ip raw, vni) -> tunnel port or -1
-NFDP_HD uint32_t lpm6_hash(const uint32_t* a, uint32_t plen) {
-  return fmix32(a[0] ^ fmix32(a[1] ^ fmix32(a[2] ^ fmix32(a[3] ^ (plen * 0x9E3779B9u)))));
+NFDP_HD uint32_t lpm6_hash(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3, uint32_t plen) {
+  return fmix32(a0 ^ fmix32(a1 ^ fmix32(a2 ^ fmix32(a3 ^ (plen * 0x9E3779B9u)))));
 }
-// Longest-prefix match of an IPv6 destination (host-order words): probe each present prefix
-// length, longest first.  Returns the route result or 0.
-NFDP_HD uint32_t lpm6_lookup(const TablesView& t, const uint32_t* dst) {
+NFDP_HD uint32_t lpm6_word_mask(uint32_t plen, int w) {
+  const int bits = (int)plen - 32 * w;
+  return bits >= 32 ? 0xFFFFFFFFu : (bits <= 0 ? 0u : ~(0xFFFFFFFFu >> bits));
+}
+// Longest-prefix match of an IPv6 destination (host-order words d0 = most significant): probe
+// each present prefix length, longest first.  Returns the route result or 0.  Scalars only (no
+// private arrays): this runs inside the hot kernels' register budget.
+NFDP_HD uint32_t lpm6_lookup(const TablesView& t, uint32_t d0, uint32_t d1, uint32_t d2, uint32_t d3) {
   if (!t.lpm6 || !t.lpm6_lens) return 0;
   for (uint32_t li = 0; li < t.n_lpm6_lens; ++li) {
     const uint32_t plen = t.lpm6_lens[li];
-    uint32_t m[4];
-    for (int w = 0; w < 4; ++w) {
-      const int bits = (int)plen - 32 * w;
-      const uint32_t mask = bits >= 32 ? 0xFFFFFFFFu : (bits <= 0 ? 0u : ~(0xFFFFFFFFu >> bits));
-      m[w] = dst[w] & mask;
-    }
-    uint32_t h = lpm6_hash(m, plen) & t.lpm6_mask;
+    const uint32_t m0 = d0 & lpm6_word_mask(plen, 0), m1 = d1 & lpm6_word_mask(plen, 1);
+    const uint32_t m2 = d2 & lpm6_word_mask(plen, 2), m3 = d3 & lpm6_word_mask(plen, 3);
+    const uint32_t h = lpm6_hash(m0, m1, m2, m3, plen) & t.lpm6_mask;
     for (int probe = 0; probe < kLpm6Probe; ++probe) {
       const Lpm6Entry& e = t.lpm6[(h + probe) & t.lpm6_mask];
       if (e.plen == kLpm6Empty) break;
-      if (e.plen == plen && e.a[0] == m[0] && e.a[1] == m[1] && e.a[2] == m[2] && e.a[3] == m[3]) return e.result;
+      if (e.plen == plen && e.a[0] == m0 && e.a[1] == m1 && e.a[2] == m2 && e.a[3] == m3) return e.result;
     }
   }
   return 0;

@@ -148,12 +148,15 @@ NFDP_HD uint32_t route_ipv4(const TablesView& t, Parsed& p, uint32_t hash, uint3
 }
 
 // IPv6 routing (P4 ipv6_table): LPM on the destination, hop limit - 1 (no header checksum in
-// IPv6), neighbour / router MACs, egress port.  Returns a drop reason (0 = routed).
-NFDP_HD uint32_t route_ipv6(const TablesView& t, Parsed& p, uint32_t hash, uint32_t& out_port) {
-  if (!p.ipv6) return kNoRoute;
-  uint32_t dst[4];
-  for (int w = 0; w < 4; ++w) dst[w] = __builtin_bswap32(raw32_at2(p.s, 38 + 4 * w));
-  const int nh = route_nexthop(t, lpm6_lookup(t, dst), hash);
+// IPv6), neighbour / router MACs, egress port.  ECMP members are picked by a hash of the IPv6
+// addresses and ports (the packet's Toeplitz hash covers IPv4 fields only).  Returns a drop
+// reason (0 = routed).  Only the routed-interface miss path calls it (IPv6 never hits a flow).
+NFDP_HD uint32_t route_ipv6(const TablesView& t, Parsed& p, uint32_t& out_port) {
+  const uint32_t d0 = __builtin_bswap32(raw32_at2(p.s, 38)), d1 = __builtin_bswap32(raw32_at2(p.s, 42));
+  const uint32_t d2 = __builtin_bswap32(raw32_at2(p.s, 46)), d3 = __builtin_bswap32(raw32_at2(p.s, 50));
+  const uint32_t h6 = fmix32(d0 ^ d1 ^ d2 ^ d3 ^ raw32_at2(p.s, 22) ^ raw32_at2(p.s, 26) ^ raw32_at2(p.s, 30) ^
+                             raw32_at2(p.s, 34) ^ (p.len >= 58 ? raw32_at2(p.s, 54) : 0u));
+  const int nh = route_nexthop(t, lpm6_lookup(t, d0, d1, d2, d3), h6);
   if (nh < 0) return kNoRoute;
   const NextHop n = t.nexthops[nh];
   if (!n.valid) return kNoRoute;
@@ -164,10 +167,6 @@ NFDP_HD uint32_t route_ipv6(const TablesView& t, Parsed& p, uint32_t hash, uint3
   set_smac(p.s, n.smac_lo, n.smac_hi);
   out_port = n.port;
   return kOk;
-}
-
-NFDP_HD uint32_t route_ip(const TablesView& t, Parsed& p, uint32_t hash, uint32_t& out_port) {
-  return p.ipv6 ? route_ipv6(t, p, hash, out_port) : route_ipv4(t, p, hash, out_port);
 }
 
 // `hit`: flow entry found; `act`: its action; `acl_rule`: first matching ACL rule or -1;
@@ -202,7 +201,7 @@ NFDP_HD EgressDecision chain_stage(const TablesView& t, const TA& ta, Parsed& p,
       const PortEntry ip = ta.port(st.in_port);
       if (dmac_lo(p.s) == ip.mac_lo && dmac_hi(p.s) == ip.mac_hi) {
         uint32_t op = kPortNone;
-        const uint32_t r = route_ip(t, p, hash, op);
+        const uint32_t r = p.ipv6 ? route_ipv6(t, p, op) : route_ipv4(t, p, hash, op);
         if (r) { e.reason = r; e.out_port = r == kNoRoute ? kPortPunt : kPortNone; return e; }
         e.out_port = op;
         const uint32_t r2 = finish_port(t, ta, e.out_port, hash, false, e.push, e.tci, p.len, &e.xhdr);
@@ -287,7 +286,7 @@ NFDP_HD EgressDecision chain_stage(const TablesView& t, const TA& ta, Parsed& p,
         e.reason = kNoRoute; e.out_port = kPortPunt; return e;
       } else if (NFDP_L3_ON && op == kHopRoute) {
         uint32_t rp = kPortNone;
-        const uint32_t r = route_ip(t, p, hash, rp);
+        const uint32_t r = route_ipv4(t, p, hash, rp);
         if (r) { e.reason = r; e.out_port = r == kNoRoute ? kPortPunt : kPortNone; return e; }
         e.out_port = rp;
       }
