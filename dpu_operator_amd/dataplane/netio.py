@@ -213,14 +213,8 @@ class LivePath:
 
     def _run_ring(self, slots: np.ndarray, im: np.ndarray):
         """One burst through the persistent ring (host slots): returns out, meta, side, t_pipe."""
-        from .ring import RingPath
-
         if self.ring is None:
-            self.ring = RingPath(self.dp, capacity=self.ring_capacity, host_slots=True, coop=True, side=True,
-                                 deadline_s=3600.0)
-            self.ring.start()
-            self._rin, self._rim, self._rout, self._rmeta = self.ring.host_arrays()
-            self.stats["ring_relaunch"] = 0
+            self._ring_init()
         ring, n, c = self.ring, len(slots), self.ring_capacity
         n_pad = (n + 63) & ~63
         with ring.lock:
@@ -247,6 +241,17 @@ class LivePath:
                 if side.get("xhdr") is not None:
                     side["xhdr"] = side["xhdr"][idx[:n]]
         return out, meta, side, t_pipe
+
+    def _ring_init(self) -> None:
+        """Launch the resident kernel (commits the data plane: call from the thread that owns
+        table changes, i.e. start(), not the loop thread)."""
+        from .ring import RingPath
+
+        self.ring = RingPath(self.dp, capacity=self.ring_capacity, host_slots=True, coop=True, side=True,
+                             deadline_s=3600.0)
+        self.ring.start()
+        self._rin, self._rim, self._rout, self._rmeta = self.ring.host_arrays()
+        self.stats["ring_relaunch"] = 0
 
     def _deliver(self, frames, src, lens, out, meta, side, t_start, t_rx, t_pipe, t_side) -> int:
         n = len(frames)
@@ -295,6 +300,8 @@ class LivePath:
             log.exception("live path stopped")
 
     def start(self) -> "LivePath":
+        if self.engine == "ring" and self.ring is None:
+            self._ring_init()
         self._t = threading.Thread(target=self._run, daemon=True, name="dpu-livepath")
         self._t.start()
         return self
