@@ -64,7 +64,8 @@ def test_ping_between_namespaces_through_the_data_plane():
         assert pc[0, 0] >= 2 and pc[1, 0] >= 2         # rx on both ports
         stages = dict(dp.latency.items())                # per-stage latency of every live batch
         assert {"rx", "pipeline", "side", "tx", "batch"} <= set(stages)
-        assert stages["batch"].count == live.stats["batches"] and stages["batch"].quantile(0.5) < 0.5
+        assert abs(stages["batch"].count - live.stats["batches"]) <= 1   # the loop thread may be mid-cycle
+        assert stages["batch"].quantile(0.5) < 0.5
     finally:
         _teardown(taps, eps, live)
 
