@@ -141,6 +141,9 @@ __device__ __forceinline__ void classify_wave(const FlowKey& key, uint4* kx, con
 #pragma unroll
     for (int b = 0; b < 16; ++b) h ^= ltab[b * 256 + ((w[b >> 2] >> (8 * (b & 3))) & 0xFFu)];
     hash = h;
+#ifdef NFDP_ABL_NO_HASH  // cost attribution only (wrong results): a two-instruction stand-in hash
+    hash = (key.src_ip ^ key.ports) * 0x9E3779B1u;
+#endif
   } else {
     hash = toeplitz_scalar(key, t.rss_key);
   }

@@ -231,7 +231,12 @@ __global__ __launch_bounds__(kFB, EARLY ? NFDP_EARLY_WAVES_PER_EU : NFDP_FUSED_W
         act.nat_port = v.z & 0xFFFFu; act.vlan = v.z >> 16; act.flow_id = v.w;
       }
     }
+#ifndef NFDP_ABL_NO_CHAIN
     const EgressDecision e = chain_stage(a.t, ta, p, st, hit, act, acl_rule, hash);
+#else  // cost attribution only (wrong results): no chain, the flow's port
+    EgressDecision e{};
+    e.out_port = hit ? act.out_port : kPortNone; e.reason = st.reason;
+#endif
     bool to_peer = false;
     uint32_t reason = e.reason;
     uint32_t eg = 0, pos = 0;
@@ -277,7 +282,12 @@ __global__ __launch_bounds__(kFB, EARLY ? NFDP_EARLY_WAVES_PER_EU : NFDP_FUSED_W
     }
     uint32_t o[kSlotDwords];
     // a steered packet travels as it came in (p is untouched: the chain never ran on it)
+#ifndef NFDP_ABL_NO_EMIT
     emit(p, to_owner ? p.tci : e.tci, to_owner ? p.tagged : e.push != 0, o);
+#else  // cost attribution only (wrong results): the normalized header as is
+#pragma unroll
+    for (int q = 0; q < kSlotDwords; ++q) o[q] = p.s[q];
+#endif
     if (a.side.cnt) {
       // flood / mirror / ARP-trap / learning packets go on the side list (side_kernel emits their
       // replicas and learn events after this kernel): a wave-uniform skip in the common case
