@@ -1,10 +1,14 @@
 """Network-namespace helpers for live-path tests: endpoints (netns + a data-plane TAP moved into
-it, addressed and up) and an ICMP echo client that runs inside a namespace."""
+it, addressed and up), an ICMP echo client that runs inside a namespace, and a bump-in-the-wire
+network function (a namespace whose two interfaces forward every frame to each other, like the
+reference e2e's NF pod between its ingress and egress DPU netdevs)."""
 from __future__ import annotations
 
 import os
+import select
 import socket
 import struct
+import threading
 import time
 
 from ..cni.netlink import RtNetlink, create_netns, delete_netns, in_netns
@@ -78,4 +82,67 @@ class Endpoint:
         self.mac = self.nl.link_by_name(ifname, self.ns).mac
 
     def close(self) -> None:
+        delete_netns(self.ns)
+
+
+class WireNF:
+    """An NF pod: namespace `ns_name` holding `if_in` and `if_out` (moved in and brought up, no
+    addresses) and a thread that copies every frame received on one to the other (AF_PACKET
+    sockets opened inside the namespace)."""
+
+    ETH_P_ALL = 0x0003
+
+    def __init__(self, ns_name: str, if_in: str, if_out: str, nl: RtNetlink | None = None):
+        self.nl = nl or RtNetlink()
+        self.ns = create_netns(f"/var/run/netns/{ns_name}")
+        self.ifs = (if_in, if_out)
+        self.macs = []
+        for i in self.ifs:
+            self.nl.link_set_ns(i, self.ns)
+            self.nl.link_set_up(i, self.ns)
+            self.macs.append(self.nl.link_by_name(i, self.ns).mac)
+        self.forwarded = 0
+        self._stop = threading.Event()
+        self._ready = threading.Event()
+        self._t = threading.Thread(target=self._run, daemon=True, name=f"nf-{ns_name}")
+        self._t.start()
+        self._ready.wait(5)
+
+    def _run(self) -> None:
+        from ..cni.netlink import setns_current_thread
+
+        setns_current_thread(self.ns)
+        socks = []
+        for i in self.ifs:
+            s = socket.socket(socket.AF_PACKET, socket.SOCK_RAW, socket.htons(self.ETH_P_ALL))
+            s.bind((i, 0))
+            s.setblocking(False)
+            socks.append(s)
+        self._ready.set()
+        try:
+            while not self._stop.is_set():
+                r, _, _ = select.select(socks, [], [], 0.05)
+                for s in r:
+                    peer = socks[1 - socks.index(s)]
+                    while True:
+                        try:
+                            data, addr = s.recvfrom(65535)
+                        except BlockingIOError:
+                            break
+                        except OSError:                      # interface went down / away: NF is done
+                            return
+                        if addr[2] == socket.PACKET_OUTGOING:   # our own transmissions
+                            continue
+                        try:
+                            peer.send(data)
+                        except OSError:
+                            return
+                        self.forwarded += 1
+        finally:
+            for s in socks:
+                s.close()
+
+    def close(self) -> None:
+        self._stop.set()
+        self._t.join(5)
         delete_netns(self.ns)

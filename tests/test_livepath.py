@@ -108,3 +108,42 @@ def test_gpu_vsp_live_vports_carry_pod_traffic():
         vsp.stop_live()
         for e in eps:
             e.close()
+
+
+def test_gpu_vsp_sfc_pod_to_external_through_the_nf():
+    """The reference e2e's NF scenario (e2e_test.go: pod <-> NF <-> external) on live netdevs:
+    a pod VF, an NF pod with ingress / egress vports (a bump-in-the-wire forwarder in its own
+    namespace) and the uplink to an "external" host.  CreateNetworkFunction steers
+    VF -> NF-in and NF-out -> wire; replies come back wire -> NF-out -> NF -> NF-in -> VF by the
+    pod's MAC (OvS K11-K13 rules, GPU tables here).  The pod pings the external host, and every
+    packet crosses the NF."""
+    from dpu_operator_amd.cni.netlink import RtNetlink
+    from dpu_operator_amd.dataplane.netio import TapPort
+    from dpu_operator_amd.vsp.gpu import GpuVsp
+
+    nl = RtNetlink()
+    wire = TapPort("lvwire")
+    nl.link_set_up("lvwire")
+    vsp = GpuVsp(device="cpu", nl=nl, flow_buckets=1 << 10, vport_prefix="lvn", live=True, uplink=wire)
+    eps, nf = [], None
+    try:
+        vsp.init(True, "")
+        vsp.set_num_vfs(3)
+        pod_mac = "02:5e:00:00:01:01"
+        nl.link_set_hw_addr("lvn0", pod_mac)
+        vsp.create_bridge_port("host0-0", bytes(int(x, 16) for x in pod_mac.split(":")), 1, ["2"])
+        eps.append(NS.Endpoint("lvn-pod", "lvn0", "10.95.0.1/24", nl))
+        eps.append(NS.Endpoint("lvn-ext", "lvwire", "10.95.0.100/24", nl))
+        nf = NS.WireNF("lvn-nf", "lvn1", "lvn2", nl)
+        vsp.create_network_function(nf.macs[0], nf.macs[1])
+        assert NS.ping(eps[0].ns, "10.95.0.100", timeout=5) is not None, (vsp.livepath.stats, vsp.livepath.error)
+        assert NS.ping(eps[1].ns, "10.95.0.1", timeout=5) is not None
+        assert nf.forwarded >= 4                      # ARP + echo both ways went through the NF
+        assert vsp.livepath.error is None
+    finally:
+        if nf is not None:
+            nf.close()
+        vsp.stop_live()
+        for e in eps:
+            e.close()
+        wire.close()
