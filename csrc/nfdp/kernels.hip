@@ -235,7 +235,8 @@ __global__ __launch_bounds__(kFB, EARLY ? NFDP_EARLY_WAVES_PER_EU : NFDP_FUSED_W
     const EgressDecision e = chain_stage(a.t, ta, p, st, hit, act, acl_rule, hash);
 #else  // cost attribution only (wrong results): no chain, the flow's port
     EgressDecision e{};
-    e.out_port = hit ? act.out_port : kPortNone; e.reason = st.reason;
+    e.out_port = hit ? act.out_port : kPortNone;
+    e.reason = st.reason ? st.reason : (hit ? kOk : kNoRoute);   // a miss never egresses to kPortNone
 #endif
     bool to_peer = false;
     uint32_t reason = e.reason;

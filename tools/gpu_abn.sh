@@ -5,12 +5,12 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-for pass in 1 2; do
+for pass in $(seq 1 "${PASSES:-2}"); do
   for V in "$@"; do
     for v in "$V" ""; do
-      echo "variant=${v:-default} pass=$pass"
+      echo "variant=${v:-default} pass=$pass" | tee -a gpurun_out/abn_results.txt
       NFDP_EXT_DIR="$v" timeout -k 10 200 python tools/ablate.py --rounds 3 > gpurun_out/abn_run.log 2>&1 || exit 1
-      grep -E "ACL256|aclOff|ACL1024" gpurun_out/abn_run.log
+      grep -E "ACL256|aclOff|ACL1024" gpurun_out/abn_run.log | tee -a gpurun_out/abn_results.txt
     done
   done
 done
