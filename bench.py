@@ -418,18 +418,27 @@ def main() -> None:
             lat1, _ = rp.probe(batches=4000, batch=64, inflight=1)
             rp.stop()
             rp.close()
-            # loaded: throughput ring (every wave takes its own chunks), 32 x 4096 packets in flight
-            rq = RingPath(dp, capacity=1 << 17, wgs_per_cu=2, deadline_s=60.0, coop=False)
+            # loaded: throughput ring (every wave takes its own chunks), 32 x 4096 packets in flight.
+            # One trial is a few ms of GPU work, so a single host-thread stall (the host both
+            # publishes and reaps) can halve it: 5 trials of 10000 batches, the median reported.
+            rq = RingPath(dp, capacity=1 << 17, wgs_per_cu=2, deadline_s=120.0, coop=False)
             rq.stage(batches[0][0][: 1 << 17], batches[0][1][: 1 << 17])
             rq.start()
-            lat2, el2 = rq.probe(batches=2000, batch=4096, inflight=32)
+            rq.probe(batches=500, batch=4096, inflight=32)  # warm-up
+            trials, lat2 = [], []
+            for _ in range(5):
+                lt, el2 = rq.probe(batches=10000, batch=4096, inflight=32)
+                trials.append(10000 * 4096 / el2 / 1e6)
+                lat2.append(lt[200:])
             rq.stop()
             rq.close()
             lat1 = lat1[400:]
+            lat2 = np.concatenate(lat2)
             ring = {"p50_us": round(float(np.median(lat1)), 2), "p99_us": round(float(np.percentile(lat1, 99)), 2),
-                    "loaded_mpps": round(2000 * 4096 / el2 / 1e6, 1),
-                    "loaded_p50_us": round(float(np.median(lat2[200:])), 2),
-                    "loaded_p99_us": round(float(np.percentile(lat2[200:], 99)), 2)}
+                    "loaded_mpps": round(float(np.median(trials)), 1),
+                    "loaded_mpps_trials": [round(x, 1) for x in trials],
+                    "loaded_p50_us": round(float(np.median(lat2)), 2),
+                    "loaded_p99_us": round(float(np.percentile(lat2, 99)), 2)}
         except Exception as ex:  # the headline number must still be reported
             ring = {"error": str(ex)[:200]}
 
