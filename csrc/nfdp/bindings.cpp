@@ -64,6 +64,9 @@ TablesView tables_from(const py::dict& d) {
   t.n_ecmp = t.ecmp ? val<uint32_t>(d, "n_ecmp", 0) : 0u;
   t.tunnels = ptr<const TunnelEntry>(d, "tunnels");
   t.n_tunnels = t.tunnels ? val<uint32_t>(d, "n_tunnels", 0) : 0u;
+  t.tunnels6 = ptr<const Tunnel6Entry>(d, "tunnels6");
+  t.n_tunnels6 = t.tunnels6 ? val<uint32_t>(d, "n_tunnels6", 0) : 0u;
+  t.vtep6_fold = val<uint32_t>(d, "vtep6_fold", 0);
   t.terms = ptr<const TermEntry>(d, "terms");
   t.term_mask = t.terms ? val<uint32_t>(d, "term_mask", 0) : 0u;
   if (t.terms && ((t.term_mask + 1) & t.term_mask)) throw std::invalid_argument("term table size must be a power of two");
@@ -111,14 +114,25 @@ PYBIND11_MODULE(_nfdp, m) {
   m.attr("MAX_FRAME") = kMaxFrame;
   m.attr("FLOOD_WAYS") = kFloodWays;
   m.attr("ENCAP_BYTES") = kEncapBytes;
+  m.attr("ENCAP6_BYTES") = kEncap6Bytes;
+  m.attr("XHDR_BYTES") = kXhdrBytes;
+  m.attr("PORT_TUNNEL6") = (uint32_t)kPortTunnel6;
+  m.def("vtep6_fold", [](uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3) { return vtep6_fold(a0, a1, a2, a3); });
+  // outer headers of a tunnel entry (32-B IPv4-underlay or 64-B IPv6-underlay entry bytes)
   m.def("make_outer", [](py::bytes te_raw, uint32_t inner_len, uint32_t hash) {
     std::string s = te_raw;
-    if (s.size() != sizeof(TunnelEntry)) throw std::invalid_argument("tunnel entry must be 32 bytes");
-    TunnelEntry te;
+    uint32_t x[kXhdrBytes / 4] = {};
+    if (s.size() == sizeof(TunnelEntry)) {
+      TunnelEntry te;
+      std::memcpy(&te, s.data(), sizeof(te));
+      make_outer(te, inner_len, hash, x);
+      return py::bytes(reinterpret_cast<const char*>(x), kEncapBytes);
+    }
+    if (s.size() != sizeof(Tunnel6Entry)) throw std::invalid_argument("tunnel entry must be 32 (IPv4) or 64 (IPv6) bytes");
+    Tunnel6Entry te;
     std::memcpy(&te, s.data(), sizeof(te));
-    uint32_t x[kSlotDwords];
-    make_outer(te, inner_len, hash, x);
-    return py::bytes(reinterpret_cast<const char*>(x), kEncapBytes);
+    make_outer6(te, inner_len, hash, x);
+    return py::bytes(reinterpret_cast<const char*>(x), kEncap6Bytes);
   });
 
   py::class_<FlowTableHost>(m, "FlowTable")

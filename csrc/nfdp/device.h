@@ -457,9 +457,9 @@ struct GpuSideSink {
   }
   __device__ __forceinline__ void xhdr(const uint32_t* hdr, uint32_t src) {
     if (!so.xhdr) return;
-    uint4* dst = reinterpret_cast<uint4*>(so.xhdr) + (size_t)src * 4;
+    uint4* dst = reinterpret_cast<uint4*>(so.xhdr) + (size_t)src * (kXhdrBytes / 16);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) dst[q] = make_uint4(hdr[4 * q], hdr[4 * q + 1], hdr[4 * q + 2], hdr[4 * q + 3]);
+    for (int q = 0; q < kXhdrBytes / 16; ++q) dst[q] = make_uint4(hdr[4 * q], hdr[4 * q + 1], hdr[4 * q + 2], hdr[4 * q + 3]);
   }
   __device__ __forceinline__ void learn(uint32_t bridge, uint32_t lo, uint32_t hi, uint32_t port) {
     const uint32_t pos = atomicAdd(so.cnt + 1, 1u);

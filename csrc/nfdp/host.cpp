@@ -270,7 +270,7 @@ struct CpuSideSink {
     else if (port < (uint32_t)kMaxPorts && port_ctr) port_ctr[2 * port + 1] += ctr_inc(meta_len(meta));
   }
   void xhdr(const uint32_t* hdr, uint32_t src) {
-    if (so.xhdr) std::memcpy(so.xhdr + (size_t)src * kSlotDwords, hdr, kSlotBytes);
+    if (so.xhdr) std::memcpy(so.xhdr + (size_t)src * (kXhdrBytes / 4), hdr, kXhdrBytes);
   }
   void learn(uint32_t bridge, uint32_t lo, uint32_t hi, uint32_t port) {
     const uint32_t pos = so.cnt[1]++;

@@ -56,6 +56,8 @@ enum Reason : uint32_t {
   kOverflow = 11,  // exchange segment full (multi-GPU path)
   kArpTrap = 12,   // ARP copy trapped to the slow path (P4 always_trap_arp_table)
   kRecirc = 13,    // tunnel terminated: recirculate frame[len - olen:] with in_port = meta port (decap)
+  kRecirc6 = 14,   // IPv6-underlay VXLAN / GENEVE to the local VTEP: the VNI lies past the header slot, so
+                   // the I/O layer finishes ipv6_tunnel_term_table on the whole frame (decap, recirculate)
   kNumReasons = 16,
 };
 
@@ -79,6 +81,7 @@ enum PortFlags : uint32_t {
   kPortVtep = 1u << 15,         // underlay port: UDP 4789 / 6081 to ext (local VTEP IPv4) is terminated
   kPortRxOff = 1u << 16,        // ctrl-net RX_STATE down: the function takes no frames (egress dropped)
   kPortLinkDown = 1u << 17,     // ctrl-net LINK_STATUS down / DEV_REMOVE: neither receives nor sends
+  kPortTunnel6 = 1u << 18,      // with kPortTunnel: IPv6 underlay, the tunnel is tunnels6[lag]
 };
 
 constexpr int kLagWays = 8;                 // members per LAG group (hash[2:0])
@@ -193,6 +196,19 @@ struct alignas(16) TunnelEntry { // 32 B: the outer headers of one tunnel port
   uint16_t type;                 // TunnelType
 };
 static_assert(sizeof(TunnelEntry) == 32, "TunnelEntry");
+struct alignas(16) Tunnel6Entry { // 64 B: IPv6-underlay tunnel (P4 vxlan / geneve_encap_v6_mod_table)
+  uint32_t src[4], dst[4];       // raw (network order) underlay addresses
+  uint16_t sport;                // raw; 0 = 0xC000 | hash
+  uint16_t dport;                // raw
+  uint32_t vni;                  // host order, 24 bits
+  uint32_t smac_lo; uint16_t smac_hi;
+  uint16_t out_port;
+  uint32_t dmac_lo; uint16_t dmac_hi;
+  uint16_t type;                 // TunnelType
+  uint32_t tc_flow;              // traffic class [27:20] | flow label [19:0] (0 = hash-derived label)
+  uint32_t hop_limit;            // [7:0] (0 = 64)
+};
+static_assert(sizeof(Tunnel6Entry) == 64, "Tunnel6Entry");
 struct alignas(16) TermEntry {   // 16 B: (outer src ip, vni) -> tunnel port (ipv4_tunnel_term_table)
   uint32_t src_ip;               // raw
   uint32_t vni;
@@ -420,12 +436,21 @@ NFDP_HD void emit(const Parsed& p, uint32_t push_tci, bool push, uint32_t* out) 
 }
 
 // Egress metadata word: port[11:0] (0xFFF none, 0xFFE punt) | olen[25:12] | reason[29:26] |
-// xhdr[30] (prepend the packet's 64-B outer-header record: tunnel encap) | flood[31].  The frame that leaves
-// is  ohdr[0:hl] ++ in_frame[to:len]  with  d = olen - 50*xhdr - len,  hl = min(64, min(len, 64) + d),
+// xhdr[30] (prepend the packet's outer-header record: tunnel encap, x = 50 B for an IPv4 underlay, 70 B
+// for IPv6, ethertype at record bytes 12..13) | flood[31].  The frame that leaves is
+// xrec[0:x] ++ ohdr[0:hl] ++ in_frame[to:len]  with  d = olen - x - len,  hl = min(64, min(len, 64) + d),
 // to = hl - d  (out_tail below): the payload is never copied by the pipeline.
+// 32-bit fold of an IPv6 address (raw words): the hot kernel's cheap "to the local VTEP?" test.
+// The exact address and the (source, VNI) key are checked by the termination resolver.
+NFDP_HD uint32_t vtep6_fold(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3) {
+  const uint32_t h = a0 ^ ((a1 << 8) | (a1 >> 24)) ^ ((a2 << 16) | (a2 >> 16)) ^ ((a3 << 24) | (a3 >> 8));
+  return h ? h : 1u;
+}
 constexpr uint32_t kMetaXhdr = 1u << 30;
 constexpr uint32_t kMetaFlood = 1u << 31;  // primary copy of a flooded frame (side pass emits the rest)
 constexpr uint32_t kEncapBytes = 50;   // outer Ethernet + IPv4 + UDP + VXLAN/GENEVE (no options)
+constexpr uint32_t kEncap6Bytes = 70;  // outer Ethernet + IPv6 + UDP + VXLAN/GENEVE (no options)
+constexpr int kXhdrBytes = 128;        // one packet's outer-header record (side pass output)
 NFDP_HD uint32_t make_meta(uint32_t out_port, uint32_t len, uint32_t reason, bool xhdr = false, bool flood = false) {
   return (out_port & 0xFFFu) | ((len & 0x3FFFu) << 12) | ((reason & 0xFu) << 26) | (xhdr ? kMetaXhdr : 0u) |
          (flood ? kMetaFlood : 0u);
@@ -437,9 +462,9 @@ NFDP_HD uint32_t meta_port(uint32_t m) {
 NFDP_HD uint32_t meta_len(uint32_t m) { return (m >> 12) & 0x3FFFu; }
 NFDP_HD uint32_t meta_reason(uint32_t m) { return (m >> 26) & 0xFu; }
 // Header bytes `hl` of the out slot that are valid and the offset `to` in the input frame where the
-// unchanged tail continues (both from the in/out lengths; `xhdr` bytes excluded).
-NFDP_HD void out_tail(uint32_t in_len, uint32_t olen, bool xhdr, uint32_t& hl, uint32_t& to) {
-  const int d = (int)olen - (xhdr ? (int)kEncapBytes : 0) - (int)in_len;
+// unchanged tail continues (both from the in/out lengths; the `xlen` outer-header bytes excluded).
+NFDP_HD void out_tail(uint32_t in_len, uint32_t olen, uint32_t xlen, uint32_t& hl, uint32_t& to) {
+  const int d = (int)olen - (int)xlen - (int)in_len;
   const int h_in = in_len < (uint32_t)kSlotBytes ? (int)in_len : kSlotBytes;
   int h = h_in + d;
   if (h > kSlotBytes) h = kSlotBytes;
@@ -490,6 +515,9 @@ struct TablesView {
   uint32_t n_ecmp;
   const TunnelEntry* tunnels;    // n_tunnels (indexed by a tunnel port's `lag`)
   uint32_t n_tunnels;
+  const Tunnel6Entry* tunnels6;  // n_tunnels6 (kPortTunnel6 ports' `lag`)
+  uint32_t n_tunnels6;
+  uint32_t vtep6_fold;           // vtep6_fold() of the local IPv6 VTEP address (0: no IPv6 VTEP)
   const TermEntry* terms;        // term_mask + 1 slots, open addressing (nullable)
   uint32_t term_mask;
   // IPv6 FIB (P4 ipv6_table): one open-addressing table over (prefix, length) and the distinct
@@ -570,7 +598,7 @@ struct SideOut {
   uint32_t* cnt;                 // 8 counters (nullptr: side outputs disabled); [5] side-list length
   uint32_t* list;                // packets flagged by the per-packet kernel for the side pass
   uint32_t cap_list;
-  uint32_t* xhdr;                // [batch] x 64-B outer-header records of tunnel-encapsulated packets
+  uint32_t* xhdr;                // [batch] x kXhdrBytes outer-header records of tunnel-encapsulated packets
 };
 
 // Flow-table lookup (scalar).  Returns slot index or -1.

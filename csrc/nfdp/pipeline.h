@@ -75,16 +75,17 @@ struct EgressDecision {
   uint32_t mirror;    // 1 -> the ingress frame is also copied to the ingress port's mirror port (K9)
   uint32_t flood;     // bridge + 1 when the frame is flooded: out_port is the group's first member,
                       // side_stage emits a replica per further member
-  uint32_t xhdr;      // 1 -> out_port is a tunnel port: the side pass writes the 50-B outer header
-  uint32_t inner_len; // kRecirc: length of the decapsulated inner frame
+  uint32_t xhdr;      // outer-header bytes (50 IPv4 / 70 IPv6 underlay) when out_port is a tunnel port:
+                      // the side pass writes them; 0 otherwise
+  uint32_t inner_len; // kRecirc / kRecirc6: length of the decapsulated inner frame
 };
 
 // Length of the frame that leaves (the meta word's len): inner frame for a recirculation, tag and
 // outer-header bytes included otherwise, 0 for drops.
 NFDP_HD uint32_t egress_len(const Parsed& p, const EgressDecision& e) {
-  if (e.reason == kRecirc) return e.inner_len;
+  if (e.reason == kRecirc || e.reason == kRecirc6) return e.inner_len;
   if (e.reason) return 0u;
-  return p.len + (e.push ? 4u : 0u) + (e.xhdr ? kEncapBytes : 0u);
+  return p.len + (e.push ? 4u : 0u) + e.xhdr;
 }
 
 NFDP_HD uint32_t byte_at(const uint32_t* s, int off) { return (s[off >> 2] >> (8 * (off & 3))) & 0xFFu; }
@@ -118,12 +119,13 @@ NFDP_HD uint32_t finish_port(const TablesView& t, const TA& ta, uint32_t& port, 
   }
   if (!port_can_egress(pe.flags)) return kBadPort;
   if (!vlan_done && (pe.flags & kPortTagEgress) && pe.vlan) { push = 1; tci = pe.vlan & 0xFFFu; }
-  // tunnel port (OvS vxlan / geneve port, P4 l2_to_tunnel_v4): encapsulated by the side pass
+  // tunnel port (OvS vxlan / geneve port, P4 l2_to_tunnel_v4 / _v6): encapsulated by the side pass
   uint32_t enc = 0;
   if (NFDP_L3_ON && (pe.flags & kPortTunnel)) {
-    if (!t.tunnels || pe.lag >= t.n_tunnels) return kBadPort;
-    enc = kEncapBytes;
-    if (xhdr) *xhdr = 1;
+    const bool v6 = (pe.flags & kPortTunnel6) != 0;
+    if (v6 ? (!t.tunnels6 || pe.lag >= t.n_tunnels6) : (!t.tunnels || pe.lag >= t.n_tunnels)) return kBadPort;
+    enc = v6 ? kEncap6Bytes : kEncapBytes;
+    if (xhdr) *xhdr = enc;
   }
   // l2len is untagged: the L3 size is l2len - 14 whatever the tagging
   if (l2len + (push ? 4u : 0u) + enc > kMaxFrame || (pe.mtu && l2len - 14u > pe.mtu)) return kTooBig;
@@ -182,17 +184,34 @@ NFDP_HD EgressDecision chain_stage(const TablesView& t, const TA& ta, Parsed& p,
   if (!hit) {
     // tunnel termination on an underlay port (ipv4_tunnel_term_table + rx_ipv4_tunnel_source_port):
     // UDP 4789 (VXLAN) / 6081 (GENEVE, no options) to the local VTEP -> recirculate the inner
-    // frame as received on the tunnel's port (P4 do_recirculate; the I/O layer re-injects it)
-    if (NFDP_L3_ON && (st.in_flags & kPortVtep) && p.ipv4 && (p.s[5] >> 24) == 17u && p.len >= 64u &&
-        raw32_at2(p.s, 30) == st.in_ext) {
-      const uint32_t dport = be16_at(p.s, 36);
-      const bool vx = dport == 4789u, gn = dport == 6081u && (byte_at(p.s, 42) & 0x3Fu) == 0u;
-      if (vx || gn) {
-        const uint32_t vni = (byte_at(p.s, 46) << 16) | (byte_at(p.s, 47) << 8) | byte_at(p.s, 48);
-        const int tp = term_lookup(t, raw32_at2(p.s, 26), vni);
-        if (tp >= 0) {
-          e.reason = kRecirc; e.out_port = (uint32_t)tp; e.inner_len = p.len - kEncapBytes;
-          return e;
+    // frame as received on the tunnel's port (P4 do_recirculate; the I/O layer re-injects it).
+    // IPv6 underlay (ipv6_tunnel_term_table): the VNI (frame bytes 66..68) lies past the 64-B
+    // header slot, so the kernel recognises the tunnel (destination folded against the local IPv6
+    // VTEP) and the I/O layer finishes the (source, VNI) lookup and the decap (kRecirc6).  One
+    // block for both families: offsets by family, so the cold path stays one region.
+    if (NFDP_L3_ON && (st.in_flags & kPortVtep) && (p.ipv4 || (p.ipv6 && t.vtep6_fold))) {
+      const bool v6 = p.ipv6;
+      const uint32_t enc = v6 ? kEncap6Bytes : kEncapBytes;
+      const bool to_me = v6 ? vtep6_fold(raw32_at2(p.s, 38), raw32_at2(p.s, 42), raw32_at2(p.s, 46),
+                                         raw32_at2(p.s, 50)) == t.vtep6_fold
+                            : raw32_at2(p.s, 30) == st.in_ext;
+      const uint32_t proto = v6 ? byte_at(p.s, 20) : (p.s[5] >> 24);
+      if (to_me && proto == 17u && p.len >= enc + 14u) {
+        // constant offsets only (a run-time index into p.s would move the header to scratch)
+        const uint32_t dport = v6 ? be16_at(p.s, 56) : be16_at(p.s, 36);
+        const uint32_t gopt = v6 ? byte_at(p.s, 62) : byte_at(p.s, 42);
+        const bool vx = dport == 4789u, gn = dport == 6081u && (gopt & 0x3Fu) == 0u;
+        if (vx || gn) {
+          if (v6) {
+            e.reason = kRecirc6; e.out_port = kPortNone; e.inner_len = p.len - kEncap6Bytes;
+            return e;
+          }
+          const uint32_t vni = (byte_at(p.s, 46) << 16) | (byte_at(p.s, 47) << 8) | byte_at(p.s, 48);
+          const int tp = term_lookup(t, raw32_at2(p.s, 26), vni);
+          if (tp >= 0) {
+            e.reason = kRecirc; e.out_port = (uint32_t)tp; e.inner_len = p.len - kEncapBytes;
+            return e;
+          }
         }
       }
     }
@@ -329,6 +348,32 @@ NFDP_HD void make_outer(const TunnelEntry& te, uint32_t inner_len, uint32_t hash
     x[i] = (uint32_t)b[4 * i] | ((uint32_t)b[4 * i + 1] << 8) | ((uint32_t)b[4 * i + 2] << 16) | ((uint32_t)b[4 * i + 3] << 24);
 }
 
+// IPv6-underlay outer headers (70 B: Ethernet, IPv6 with next header UDP, UDP with the entropy
+// source port and a zero checksum as RFC 6935 / 6936 allow for tunnel encapsulations, VXLAN or
+// GENEVE + VNI).  The flow label is the entry's or, if 0, 20 bits of the packet hash (RFC 6438).
+// `x` holds kXhdrBytes / 4 LE dwords.
+NFDP_HD void make_outer6(const Tunnel6Entry& te, uint32_t inner_len, uint32_t hash, uint32_t* x) {
+  uint8_t b[kXhdrBytes];
+  for (int i = 0; i < kXhdrBytes; ++i) b[i] = 0;
+  auto put32 = [&](int o, uint32_t raw) { b[o] = raw & 0xFF; b[o + 1] = (raw >> 8) & 0xFF; b[o + 2] = (raw >> 16) & 0xFF; b[o + 3] = raw >> 24; };
+  auto be16 = [&](int o, uint32_t v) { b[o] = (v >> 8) & 0xFF; b[o + 1] = v & 0xFF; };
+  put32(0, te.dmac_lo); b[4] = te.dmac_hi & 0xFF; b[5] = te.dmac_hi >> 8;
+  put32(6, te.smac_lo); b[10] = te.smac_hi & 0xFF; b[11] = te.smac_hi >> 8;
+  be16(12, 0x86DD);
+  const uint32_t fl = (te.tc_flow & 0xFFFFFu) ? (te.tc_flow & 0xFFFFFu) : (hash & 0xFFFFFu);
+  const uint32_t vtf = (6u << 28) | (((te.tc_flow >> 20) & 0xFFu) << 20) | fl;
+  be16(14, vtf >> 16); be16(16, vtf & 0xFFFFu);
+  be16(18, 8 + 8 + inner_len); b[20] = 17; b[21] = (te.hop_limit & 0xFFu) ? (te.hop_limit & 0xFFu) : 64u;
+  for (int k = 0; k < 4; ++k) { put32(22 + 4 * k, te.src[k]); put32(38 + 4 * k, te.dst[k]); }
+  if (te.sport) { b[54] = te.sport & 0xFF; b[55] = te.sport >> 8; } else { be16(54, 0xC000u | (hash & 0x3FFFu)); }
+  b[56] = te.dport & 0xFF; b[57] = te.dport >> 8;
+  be16(58, 8 + 8 + inner_len);
+  if (te.type == kTunGeneve) { be16(64, 0x6558); } else { b[62] = 0x08; }
+  b[66] = (te.vni >> 16) & 0xFF; b[67] = (te.vni >> 8) & 0xFF; b[68] = te.vni & 0xFF;
+  for (int i = 0; i < kXhdrBytes / 4; ++i)
+    x[i] = (uint32_t)b[4 * i] | ((uint32_t)b[4 * i + 1] << 8) | ((uint32_t)b[4 * i + 2] << 16) | ((uint32_t)b[4 * i + 3] << 24);
+}
+
 // Side outputs: flood replicas, the K9 mirror copy, the ARP slow-path copy and MAC-learn events.
 // The per-packet kernels only FLAG the packets that need them (side_needed -> the packet's index
 // is appended to a side list; a flooded frame's primary copy carries kMetaFlood) and a separate
@@ -358,13 +403,19 @@ NFDP_HD void side_stage(const TablesView& t, const TA& ta, const uint32_t* d_in,
   // ARP to the slow path (P4 always_trap_arp_table): the ingress frame, punted
   if (p.arp && (st.in_flags & kPortArpTrap)) sink.rep(d_in, make_meta(kPortPunt, st.wire_len, kArpTrap), src);
   if (meta_reason(ometa)) return;
-  // tunnel encap: the outer Ethernet / IPv4 / UDP / VXLAN|GENEVE header record of this packet
+  // tunnel encap: the outer Ethernet / IPv4|IPv6 / UDP / VXLAN|GENEVE header record of this packet
   if (ometa & kMetaXhdr) {
     const uint32_t tp = meta_port(ometa);
     if (tp < (uint32_t)kMaxPorts) {
       const PortEntry pe = ta.port(tp);
-      if ((pe.flags & kPortTunnel) && t.tunnels && pe.lag < t.n_tunnels) {
-        uint32_t x[kSlotDwords];
+      uint32_t x[kXhdrBytes / 4];
+      if ((pe.flags & kPortTunnel) && (pe.flags & kPortTunnel6)) {
+        if (t.tunnels6 && pe.lag < t.n_tunnels6) {
+          make_outer6(t.tunnels6[pe.lag], meta_len(ometa) - kEncap6Bytes, toeplitz_scalar(st.key, t.rss_key), x);
+          sink.xhdr(x, src);
+        }
+      } else if ((pe.flags & kPortTunnel) && t.tunnels && pe.lag < t.n_tunnels) {
+        for (int i = kSlotDwords; i < kXhdrBytes / 4; ++i) x[i] = 0;
         make_outer(t.tunnels[pe.lag], meta_len(ometa) - kEncapBytes, toeplitz_scalar(st.key, t.rss_key), x);
         sink.xhdr(x, src);
       }

@@ -72,6 +72,9 @@ class DataPlane:
         self.ecmp = T.EcmpTable()
         self.tunnels = T.TunnelTable()
         self.terms = T.TermTable()
+        self.tunnels6 = T.Tunnel6Table()
+        self.vtep6 = T.Vtep6()
+        self.terms6 = T.Term6Table()     # host side: finished by resolve_recirc6 on the whole frame
         self.acl = T.AclTable()
         self.flows = T.FlowTable(flow_buckets, rss_key)
         self.rss_key = rss_key
@@ -169,7 +172,8 @@ class DataPlane:
     def _models(self):
         return (("ports", self.ports), ("chains", self.chains), ("macs", self.macs), ("lag", self.lag),
                 ("flood", self.flood), ("nexthops", self.nexthops), ("ecmp", self.ecmp),
-                ("tunnels", self.tunnels), ("terms", self.terms))
+                ("tunnels", self.tunnels), ("terms", self.terms), ("tunnels6", self.tunnels6),
+                ("vtep6", self.vtep6))   # vtep6: a kernarg fold, listed for the version tracking
 
     def _only_flows_pending(self) -> bool:
         """True when the device is current in everything but (possibly) flow buckets."""
@@ -328,6 +332,8 @@ class DataPlane:
             "lpm6_mask": int(getattr(self, "_lpm6", (0, 0))[0]),
             "lpm6_lens": self._ptr("lpm6_lens") if len(self.routes6) else 0,
             "n_lpm6_lens": int(getattr(self, "_lpm6", (0, 0))[1]),
+            "tunnels6": self._ptr("tunnels6") if self.tunnels6.n else 0, "n_tunnels6": int(self.tunnels6.n),
+            "vtep6_fold": int(self.nf.vtep6_fold(*(int(x) for x in self.vtep6.a))) if self.vtep6.active else 0,
         }
 
     # ------------------------------------------------------------------ side outputs / learning
@@ -337,9 +343,15 @@ class DataPlane:
         """Replicas / learn events can occur: a flood group or a learning / ARP-trap / mirror port."""
         return self.flood.n > 0 or bool(np.any(self.ports.a["flags"] & np.uint32(self.SIDE_FLAGS)))
 
+    XHDR_WORDS = 32   # nfdp.h kXhdrBytes / 4: one packet's outer-header record
+
+    def _tunnels_on(self) -> bool:
+        return bool(self.tunnels.n or self.tunnels6.n)
+
     def _side_buffers(self, n: int = 0) -> dict:
-        if self.tunnels.n and (self._dev.get("side_xhdr") is None or len(self._dev["side_xhdr"]) < n * 16):
-            self._zeros("side_xhdr", max(n, 1024) * 16, np.uint32)   # outer-header record per packet
+        w = self.XHDR_WORDS
+        if self._tunnels_on() and (self._dev.get("side_xhdr") is None or len(self._dev["side_xhdr"]) < n * w):
+            self._zeros("side_xhdr", max(n, 1024) * w, np.uint32)   # outer-header record per packet
         if "side_cnt" not in self._dev:
             self._zeros("side_hdr", self.cap_rep * 16, np.uint32)
             self._zeros("side_meta", self.cap_rep, np.uint32)
@@ -351,7 +363,7 @@ class DataPlane:
         return {"rep_hdr": self._ptr("side_hdr"), "rep_meta": self._ptr("side_meta"), "rep_src": self._ptr("side_src"),
                 "cap_rep": self.cap_rep, "learn": self._ptr("side_learn"), "cap_learn": self.cap_learn,
                 "cnt": self._ptr("side_cnt"), "list": self._ptr("side_list"), "cap_list": self.cap_rep,
-                "xhdr": self._ptr("side_xhdr") if self.tunnels.n else 0}
+                "xhdr": self._ptr("side_xhdr") if self._tunnels_on() else 0}
 
     def _apply_learn(self, stream=None) -> None:
         """Apply this batch's learn events to the device MAC table (GPU: mac_learn_kernel on the
@@ -381,7 +393,22 @@ class DataPlane:
                 "rep_meta": g("side_meta")[:n].copy(), "rep_src": g("side_src")[:n].copy(),
                 "n_learn": int(c[1]), "rep_dropped": int(c[2]), "learn_dropped": int(c[3]),
                 "learn_unplaced": int(c[4]), "n_side": int(c[5]), "side_dropped": int(c[6]),
-                "xhdr": g("side_xhdr").reshape(-1, 16).view(np.uint8).reshape(-1, 64) if self.tunnels.n else None}
+                "xhdr": (g("side_xhdr").reshape(-1, self.XHDR_WORDS).view(np.uint8).reshape(-1, 4 * self.XHDR_WORDS)
+                         if self._tunnels_on() else None)}
+
+    def resolve_recirc6(self, frame: bytes) -> tuple[int, bytes] | None:
+        """Finish the termination of a frame the kernel marked recirc6 (IPv6-underlay VXLAN /
+        GENEVE to the local VTEP): (tunnel port, inner frame) from ipv6_tunnel_term_table on the
+        whole frame (its VNI lies past the header slot), or None when no tunnel matches (the frame
+        then goes to the slow path)."""
+        fr = bytes(frame)
+        if not self.vtep6.active or fr[38:54] != self.vtep6.a.tobytes():   # the kernel compared a fold
+            return None
+        r = self.terms6.lookup(fr)
+        if r is None:
+            return None
+        port, off = r
+        return port, bytes(frame[off:])
 
     def pull_learned(self) -> int:
         """Fold the entries the data plane learned into the host MAC model."""

@@ -265,6 +265,16 @@ class LivePath:
                 self._recirc.append((frames[i][int(lens[i]) - int(olen[i]):], int(port[i])))
                 self.stats["recirc"] += 1
                 continue
+            if reason[i] == 14:  # IPv6-underlay tunnel to the local VTEP: the VNI lookup needs the whole frame
+                r6 = self.dp.resolve_recirc6(frames[i][: int(lens[i])])
+                if r6 is not None:
+                    self._recirc.append((r6[1], r6[0]))
+                    self.stats["recirc"] += 1
+                else:
+                    self.stats["punt"] += 1
+                    if self.on_punt:
+                        self.on_punt(bytes(frames[i][: int(lens[i])]), src[i], 5)
+                continue
             if reason[i]:
                 self.stats["drop"] += 1
                 continue

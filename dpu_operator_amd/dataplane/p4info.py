@@ -236,6 +236,18 @@ TABLES = [
      ["set_vxlan_decap_outer_hdr", "set_vxlan_decap_outer_and_push_vlan", "set_geneve_decap_outer_hdr",
       "set_geneve_decap_outer_and_push_vlan", "trap_enable"], 1024),
     ("rx_ipv4_tunnel_source_port", [("ipv4_src", 32, "EXACT"), ("vni", 24, "EXACT")], ["set_source_port", "drop"], 1024),
+    # IPv6 underlay tunnels
+    ("l2_to_tunnel_v6", [("hdrs.mac[vmeta.common.depth].da", 48, "EXACT")], ["set_tunnel_v6", "do_recirculate", "drop"], 1024),
+    ("vxlan_encap_v6_mod_table", [("vmeta.common.mod_blob_ptr", 24, "EXACT")], ["vxlan_encap_v6", "NoAction"], 1024),
+    ("vxlan_encap_v6_vlan_pop_mod_table", [("vmeta.common.mod_blob_ptr", 24, "EXACT")],
+     ["vxlan_encap_v6_vlan_pop", "NoAction"], 1024),
+    ("geneve_encap_v6_mod_table", [("vmeta.common.mod_blob_ptr", 24, "EXACT")], ["geneve_encap_v6", "NoAction"], 1024),
+    ("geneve_encap_v6_vlan_pop_mod_table", [("vmeta.common.mod_blob_ptr", 24, "EXACT")],
+     ["geneve_encap_v6_vlan_pop", "NoAction"], 1024),
+    ("ipv6_tunnel_term_table", [("ipv6_src", 128, "EXACT"), ("vni", 24, "EXACT")],
+     ["set_vxlan_decap_outer_hdr", "set_vxlan_decap_outer_and_push_vlan", "set_geneve_decap_outer_hdr",
+      "set_geneve_decap_outer_and_push_vlan", "NoAction"], 1024),
+    ("rx_ipv6_tunnel_source_port", [("ipv6_src", 128, "EXACT"), ("vni", 24, "EXACT")], ["set_source_port", "drop"], 1024),
     # LAG rx, smac learning check, ARP trap (p4info.txt:168, 783, 1011)
     ("rx_lag_table", [("vmeta.common.port_id", 2, "EXACT"), ("user_meta.cmeta.lag_group_id", 8, "EXACT")],
      ["fwd_to_vsi", "drop"], 1024),
@@ -278,6 +290,10 @@ ACTIONS = {
     "set_src_mac_mid": [("arg", 16)],
     "set_src_mac_last": [("arg", 16)],
     "set_tunnel_v4": [("dst_addr", 32)],
+    "set_tunnel_v6": [("ipv6_1", 32), ("ipv6_2", 32), ("ipv6_3", 32), ("ipv6_4", 32)],
+    **{a: [("src_addr", 128), ("dst_addr", 128), ("ds", 6), ("ecn", 2), ("flow_label", 20), ("hop_limit", 8),
+           ("src_port", 16), ("dst_port", 16), ("vni", 24)]
+       for a in ("vxlan_encap_v6", "vxlan_encap_v6_vlan_pop", "geneve_encap_v6", "geneve_encap_v6_vlan_pop")},
     "do_recirculate": [],
     "vxlan_encap": [("src_addr", 32), ("dst_addr", 32), ("src_port", 16), ("dst_port", 16), ("vni", 24)],
     "vxlan_encap_vlan_pop": [("src_addr", 32), ("dst_addr", 32), ("src_port", 16), ("dst_port", 16), ("vni", 24)],

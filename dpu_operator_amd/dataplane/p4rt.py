@@ -389,6 +389,85 @@ class P4Runtime:
         self._owned_ports = owned
         dp.ports.version += 1
 
+    def _compile_tunnels_v6(self, dp, port, add_mac, bridges, mac_of) -> bool:
+        """IPv6-underlay tunnels: l2_to_tunnel_v6 + {vxlan,geneve}_encap_v6[_vlan_pop]_mod_table onto
+        PORT_TUNNEL6 ports (tunnels6), ipv6_tunnel_term_table + rx_ipv6_tunnel_source_port onto the
+        local IPv6 VTEP (kernel recognition) and the host termination table (terms6)."""
+        encap: dict[int, tuple[int, Entry]] = {}
+        for kind, tab in ((T.TUN_VXLAN, "vxlan_encap_v6_mod_table"), (T.TUN_VXLAN, "vxlan_encap_v6_vlan_pop_mod_table"),
+                          (T.TUN_GENEVE, "geneve_encap_v6_mod_table"), (T.TUN_GENEVE, "geneve_encap_v6_vlan_pop_mod_table")):
+            for e in self._rows(tab):
+                if e.params:
+                    encap[e.params["dst_addr"]] = (kind, e)
+        tunnels = [e for e in self._rows("l2_to_tunnel_v6") if e.action.endswith("set_tunnel_v6")]
+
+        def dst_of(e: Entry) -> int:
+            p = e.params
+            return (p["ipv6_1"] << 96) | (p["ipv6_2"] << 64) | (p["ipv6_3"] << 32) | p["ipv6_4"]
+
+        dsts = sorted({dst_of(e) for e in tunnels})
+        if len(dsts) > 64:
+            raise P4Error("RESOURCE_EXHAUSTED", "at most 64 IPv6-underlay tunnel destinations")
+        terms = [e for e in self._rows("ipv6_tunnel_term_table") if "decap" in e.action]
+        if not (tunnels or terms or self._owned_tunnels):
+            return False            # tunnels6 / terms6 / vtep6 set outside P4Runtime stay as they are
+        dp.tunnels6.n = 0
+        dp.tunnels6.version += 1
+        for k, d in enumerate(dsts):
+            if d not in encap:
+                raise P4Error("FAILED_PRECONDITION", f"tunnel to {ipaddress.IPv6Address(d)} has no v6 encap mod entry")
+            kind, me = encap[d]
+            tp = port(TUNNEL_PORT_BASE + 64 + k)
+            r = dp.routes6.lookup(d) if len(dp.routes6) else 0
+            nh = (r & 0xFFFF) if r & T.ROUTE_NH else None
+            raw = lambda x: ":".join(f"{(x >> (8 * b)) & 0xFF:02x}" for b in range(6))  # noqa: E731
+            if nh is not None and dp.nexthops.a[nh]["valid"]:
+                n = dp.nexthops.a[nh]
+                out = int(n["port"])
+                dmac_s = raw(int(n["dmac_lo"]) | int(n["dmac_hi"]) << 32)
+                smac_s = raw(int(n["smac_lo"]) | int(n["smac_hi"]) << 32)
+            else:
+                out, dmac_s, smac_s = port(PHY_BASE), "ff:ff:ff:ff:ff:ff", mac_of(0)
+            p = me.params
+            dp.tunnels6.set(k, src=p["src_addr"], dst=d, vni=p["vni"], out_port=out, smac=smac_s, dmac=dmac_s,
+                            kind=kind, dport=p["dst_port"] or None, sport=p["src_port"],
+                            traffic_class=(p["ds"] << 2) | p["ecn"], flow_label=p["flow_label"],
+                            hop_limit=p["hop_limit"] or 64)
+            dp.ports.a[tp]["flags"] |= T.PORT_VALID | T.PORT_TUNNEL | T.PORT_TUNNEL6
+            dp.ports.a[tp]["lag"] = k
+            for ent in tunnels:
+                if dst_of(ent) == d:
+                    for b in bridges:
+                        add_mac(b, _mac(ent.key[0][1]), tp)
+        # termination: recognised by the kernel against the local IPv6 VTEP, finished on the host
+        dp.terms6.clear()
+        sp_of = {(e.key[0][1], e.key[1][1]): e.params["source_port"] for e in self._rows("rx_ipv6_tunnel_source_port")
+                 if e.action.endswith("set_source_port")}
+        bm = {e2.key[0][1]: e2.params["bridge_id"] for e2 in self._rows("source_port_to_bridge_map")
+              if e2.key[0][2] == 0xFFFF and e2.action.endswith("set_bridge_id")}
+        for e in terms:
+            s6, vni = e.key[0][1], e.key[1][1]
+            tp = port(TUNNEL_PORT_BASE + 128 + (e.params["tunnel_id"] & 0x7F))
+            dp.ports.a[tp]["flags"] |= T.PORT_VALID
+            dp.terms6.insert(s6, vni, tp)
+            if e.action.endswith("_and_push_vlan"):
+                tab = "geneve_decap_and_push_vlan_mod_table" if "geneve" in e.action else "vxlan_decap_and_push_vlan_mod_table"
+                me = next((m for m in self._rows(tab) if m.key[0][1] == e.params["tunnel_id"] and m.params), None)
+                if me is None:
+                    raise P4Error("FAILED_PRECONDITION", f"{e.action} for tunnel {e.params['tunnel_id']} has no {tab} entry")
+                dp.ports.a[tp]["flags"] |= T.PORT_INGRESS_TAG
+                dp.ports.a[tp]["ext"] = (int(dp.ports.a[tp]["ext"]) & ~0xFFF) | (me.params["vlan_id"] & 0xFFF)
+            if sp_of.get((s6, vni)) in bm:
+                dp.ports.update(tp, bridge_id=bm[sp_of[(s6, vni)]])
+        local6 = {e.params["src_addr"] for _, e in encap.values()}
+        if terms and local6:
+            dp.vtep6.set(min(local6))
+            for k in range(4):
+                dp.ports.a[port(PHY_BASE + k)]["flags"] |= T.PORT_VTEP
+        elif dp.vtep6.active:
+            dp.vtep6.clear()
+        return bool(tunnels or terms)
+
     def _compile_l3_tunnels(self, dp, port, add_mac, src: dict) -> None:
         """L3 (ipv4_table, ipv6_table, ecmp_hash_table, nexthop / ecmp_nexthop tables, rif_mod_table_*), tunnels
         (l2_to_tunnel_v4, *_encap_mod_table, ipv4_tunnel_term_table, rx_ipv4_tunnel_source_port),
@@ -475,7 +554,10 @@ class P4Runtime:
         tunnels = [e for e in self._rows("l2_to_tunnel_v4") if e.action.endswith("set_tunnel_v4")]
         local_vteps = {e.params["src_addr"] for _, e in encap.values()}
         bridges = {int(dp.ports.a[p]["bridge_id"]) for p in src} | {0}
-        for k, e in enumerate(sorted({e.params["dst_addr"] for e in tunnels})):
+        v4_dsts = sorted({e.params["dst_addr"] for e in tunnels})
+        if len(v4_dsts) > 64:
+            raise P4Error("RESOURCE_EXHAUSTED", "at most 64 IPv4-underlay tunnel destinations")
+        for k, e in enumerate(v4_dsts):
             if e not in encap:
                 raise P4Error("FAILED_PRECONDITION", f"tunnel to {ipaddress.IPv4Address(e)} has no encap mod entry")
             kind, me = encap[e]
@@ -531,7 +613,8 @@ class P4Runtime:
                 dp.ports.a[pp]["flags"] |= T.PORT_VTEP
                 dp.ports.a[pp]["ext"] = int(T.ip_raw(np.uint32(vtep))) if hasattr(T, "ip_raw") else int(
                     np.uint32(int.from_bytes(ipaddress.IPv4Address(vtep).packed, "little")))
-        self._owned_tunnels = bool(tunnels or terms)
+        tun6 = self._compile_tunnels_v6(dp, port, add_mac, bridges, mac_of)
+        self._owned_tunnels = bool(tunnels or terms or tun6)
         # rx LAG: frames from a member physical port enter as the LAG's vport
         for e in self._rows("rx_lag_table"):
             if e.action.endswith("fwd_to_vsi"):

@@ -46,6 +46,7 @@ PORT_TUNNEL = 1 << 14       # tunnel port: egress = VXLAN / GENEVE encap with tu
 PORT_VTEP = 1 << 15         # underlay port: VXLAN / GENEVE to ext (local VTEP IPv4, raw) is terminated
 PORT_RX_OFF = 1 << 16       # ctrl-net RX_STATE down: frames to the port are dropped (bad_port)
 PORT_LINK_DOWN = 1 << 17    # ctrl-net LINK_STATUS down / DEV_REMOVE: the port neither receives nor sends
+PORT_TUNNEL6 = 1 << 18      # with PORT_TUNNEL: IPv6 underlay, the tunnel is tunnels6[lag]
 LAG_WAYS = 8
 
 # hop opcodes (nfdp.h Hop)
@@ -59,7 +60,7 @@ HOP_NAMES = {
 REASONS = {
     0: "ok", 1: "bad_port", 2: "vlan_drop", 3: "spoof", 4: "acl_deny", 5: "no_route",
     6: "too_big", 7: "chain_drop", 8: "ttl_expired", 9: "malformed", 10: "remote", 11: "overflow",
-    12: "arp_trap", 13: "recirc",
+    12: "arp_trap", 13: "recirc", 14: "recirc6",
 }
 
 PORT_DTYPE = np.dtype(
@@ -81,7 +82,11 @@ TUNNEL_DTYPE = np.dtype([("src_ip", "<u4"), ("dst_ip", "<u4"), ("sport", "<u2"),
                          ("smac_lo", "<u4"), ("smac_hi", "<u2"), ("out_port", "<u2"), ("dmac_lo", "<u4"),
                          ("dmac_hi", "<u2"), ("type", "<u2")])
 TERM_DTYPE = np.dtype([("src_ip", "<u4"), ("vni", "<u4"), ("port", "<u2"), ("valid", "<u2"), ("pad", "<u4")])
+TUNNEL6_DTYPE = np.dtype([("src", "<u4", (4,)), ("dst", "<u4", (4,)), ("sport", "<u2"), ("dport", "<u2"), ("vni", "<u4"),
+                          ("smac_lo", "<u4"), ("smac_hi", "<u2"), ("out_port", "<u2"), ("dmac_lo", "<u4"),
+                          ("dmac_hi", "<u2"), ("type", "<u2"), ("tc_flow", "<u4"), ("hop_limit", "<u4")])
 assert NH_DTYPE.itemsize == 16 and TUNNEL_DTYPE.itemsize == 32 and TERM_DTYPE.itemsize == 16
+assert TUNNEL6_DTYPE.itemsize == 64
 TUN_VXLAN, TUN_GENEVE = 1, 2
 VXLAN_PORT, GENEVE_PORT = 4789, 6081
 LPM_EXT, ROUTE_NH, ROUTE_ECMP = 1 << 31, 1 << 28, 2 << 28
@@ -413,6 +418,96 @@ class TunnelTable:
 
     def bytes_of(self, idx: int) -> bytes:
         return self.a[idx].tobytes()
+
+
+def ip6_raw(addr) -> np.ndarray:
+    """IPv6 address (text / int) -> the 16 network-order bytes as 4 little-endian u32 words."""
+    a = ipaddress.IPv6Address(int(addr) if isinstance(addr, (int, np.integer)) else addr)
+    return np.frombuffer(a.packed, "<u4").copy()
+
+
+class Tunnel6Table:
+    """IPv6-underlay VXLAN / GENEVE tunnels (vxlan_encap_v6_mod_table / geneve_encap_v6_mod_table +
+    l2_to_tunnel_v6): the outer headers of a PORT_TUNNEL | PORT_TUNNEL6 port."""
+
+    def __init__(self, capacity: int = 256):
+        self.a = np.zeros(capacity, TUNNEL6_DTYPE)
+        self.n = 0
+        self.version = 0
+
+    def set(self, idx: int, *, src, dst, vni: int, out_port: int, smac, dmac, kind: int = TUN_VXLAN,
+            dport: int | None = None, sport: int = 0, traffic_class: int = 0, flow_label: int = 0,
+            hop_limit: int = 64) -> None:
+        dport = dport or (VXLAN_PORT if kind == TUN_VXLAN else GENEVE_PORT)
+        slo, shi = mac_raw(smac)
+        dlo, dhi = mac_raw(dmac)
+        e = self.a[idx]
+        e["src"], e["dst"] = ip6_raw(src), ip6_raw(dst)
+        e["sport"] = int(port_raw(np.uint32(sport))) if sport else 0
+        e["dport"] = int(port_raw(np.uint32(dport)))
+        e["vni"] = vni & 0xFFFFFF
+        e["smac_lo"], e["smac_hi"], e["out_port"], e["dmac_lo"], e["dmac_hi"] = slo, shi, out_port, dlo, dhi
+        e["type"] = kind
+        e["tc_flow"] = ((traffic_class & 0xFF) << 20) | (flow_label & 0xFFFFF)
+        e["hop_limit"] = hop_limit & 0xFF
+        self.a[idx] = e
+        self.n = max(self.n, idx + 1)
+        self.version += 1
+
+    def bytes_of(self, idx: int) -> bytes:
+        return self.a[idx].tobytes()
+
+
+class Vtep6:
+    """The local IPv6 VTEP address: VTEP (underlay) ports hand IPv6 VXLAN / GENEVE addressed to it to
+    the termination path (kernel reason recirc6, Term6Table finishes it)."""
+
+    def __init__(self):
+        self.a = np.zeros(4, np.uint32)
+        self.active = False
+        self.version = 0
+
+    def set(self, addr) -> None:
+        self.a[:] = ip6_raw(addr)
+        self.active = True
+        self.version += 1
+
+    def clear(self) -> None:
+        self.a[:] = 0
+        self.active = False
+        self.version += 1
+
+
+class Term6Table:
+    """ipv6_tunnel_term_table + rx_ipv6_tunnel_source_port: (outer IPv6 source, VNI) -> the tunnel
+    port the inner frame re-enters on.  The VNI lies past the 64-B header slot (frame bytes
+    66..68), so the kernel only recognises the tunnel (reason recirc6) and this host table is
+    consulted on the whole frame by the I/O layer (`DataPlane.resolve_recirc6`)."""
+
+    def __init__(self):
+        self.entries: dict[tuple[int, int], int] = {}
+        self.version = 0
+
+    def insert(self, src, vni: int, port: int) -> None:
+        self.entries[(int(ipaddress.IPv6Address(int(src) if isinstance(src, (int, np.integer)) else src)),
+                      vni & 0xFFFFFF)] = int(port)
+        self.version += 1
+
+    def clear(self) -> None:
+        self.entries.clear()
+        self.version += 1
+
+    def lookup(self, frame: bytes) -> tuple[int, int] | None:
+        """(tunnel port, inner offset) of an IPv6 VXLAN / GENEVE frame, or None."""
+        if len(frame) < 84:
+            return None
+        src = int.from_bytes(frame[22:38], "big")
+        vni = int.from_bytes(frame[66:69], "big")
+        p = self.entries.get((src, vni))
+        return None if p is None else (p, 70)
+
+    def __len__(self) -> int:
+        return len(self.entries)
 
 
 class TermTable:

@@ -7,8 +7,9 @@ layer put it (``craft_full`` returns it).  A "64-byte packet" on the wire is a 6
 4-byte FCS, so an untagged 64-B packet occupies 60 B of its slot and a VLAN-tagged one 64 B.
 
 Egress meta word (nfdp.h make_meta): port[11:0] (0xFFF none, 0xFFE punt) | len[25:12] |
-reason[29:26] | xhdr[30].  The frame that leaves is ``ohdr[:hl] ++ in_frame[to:len]``
-(``out_tail``/``assemble``).
+reason[29:26] | xhdr[30].  The frame that leaves is ``xrec[:x] ++ ohdr[:hl] ++ in_frame[to:len]``
+(``out_tail``/``assemble``; x = the outer-header bytes of a tunnel-encapsulated packet, 50 for an
+IPv4 underlay, 70 for IPv6, read off its record's ethertype).
 """
 from __future__ import annotations
 
@@ -17,6 +18,7 @@ import numpy as np
 SLOT = 64
 MAX_FRAME = 9600      # nfdp.h kMaxFrame
 ENCAP_BYTES = 50      # nfdp.h kEncapBytes (outer Ethernet + IPv4 + UDP + VXLAN/GENEVE)
+ENCAP6_BYTES = 70     # nfdp.h kEncap6Bytes (outer Ethernet + IPv6 + UDP + VXLAN/GENEVE)
 ETH_IPV4 = 0x0800
 ETH_VLAN = 0x8100
 ETH_ARP = 0x0806
@@ -352,13 +354,20 @@ def meta_fields(meta: np.ndarray) -> tuple[np.ndarray, np.ndarray, np.ndarray]:
 
 
 def meta_xhdr(meta: np.ndarray) -> np.ndarray:
-    """Per-packet bool: prepend the packet's 64-B outer-header record (tunnel encap)."""
+    """Per-packet bool: prepend the packet's outer-header record (tunnel encap)."""
     return ((np.asarray(meta, np.uint32) >> 30) & 1).astype(bool)
 
 
-def out_tail(in_len, olen, xhdr=False):
-    """nfdp.h out_tail: (hl, to) - valid header bytes of the out slot, tail offset in the input."""
-    d = np.asarray(olen, np.int64) - np.where(xhdr, ENCAP_BYTES, 0) - np.asarray(in_len, np.int64)
+def xhdr_len(rec) -> int:
+    """Outer-header bytes of an outer-header record: 70 when it carries IPv6 (ethertype 0x86DD), else 50."""
+    r = np.asarray(rec, np.uint8)
+    return ENCAP6_BYTES if (int(r[12]) << 8 | int(r[13])) == 0x86DD else ENCAP_BYTES
+
+
+def out_tail(in_len, olen, xlen=0):
+    """nfdp.h out_tail: (hl, to) - valid header bytes of the out slot, tail offset in the input
+    (`xlen`: outer-header bytes of an encapsulated packet, 0 otherwise)."""
+    d = np.asarray(olen, np.int64) - np.asarray(xlen, np.int64) - np.asarray(in_len, np.int64)
     h = np.minimum(np.minimum(np.asarray(in_len, np.int64), SLOT) + d, SLOT)
     return h, h - d
 
@@ -367,9 +376,12 @@ def assemble(ohdr: np.ndarray, meta: int, in_frame: np.ndarray, in_len: int, xhd
     """The frame that leaves for one packet: [outer header] ++ ohdr[:hl] ++ in_frame[to:in_len]."""
     _, olen, _ = meta_fields(np.array([meta], np.uint32))
     x = bool(meta_xhdr(np.array([meta], np.uint32))[0])
-    hl, to = out_tail(in_len, int(olen[0]), x)
+    if x and xhdr_rec is None:
+        raise ValueError("meta says encapsulated but no outer-header record given")
+    xl = xhdr_len(xhdr_rec) if x else 0
+    hl, to = out_tail(in_len, int(olen[0]), xl)
     hl, to = int(hl), int(to)
-    pre = bytes(np.asarray(xhdr_rec, np.uint8)[:ENCAP_BYTES]) if x else b""
+    pre = bytes(np.asarray(xhdr_rec, np.uint8)[:xl]) if x else b""
     out = pre + bytes(np.asarray(ohdr, np.uint8)[:hl]) + bytes(np.asarray(in_frame, np.uint8)[to:in_len])
     if len(out) != int(olen[0]):
         raise ValueError(f"assembled {len(out)} bytes, meta says {int(olen[0])}")

@@ -265,3 +265,134 @@ def test_l3_routed_sfc_scenario():
         assert u[26:30] == int(sc.actions[fl[i], 1]).to_bytes(4, "little")       # SNAT source
         assert P.check_csums(np.frombuffer(u, np.uint8)[None], np.array([len(u)]))[0]
     assert len({int(r.out[i, 5]) for i in range(2048)}) == 8                     # all ECMP members used
+
+
+# ---- IPv6 underlay (P4 vxlan / geneve_encap_v6_mod_table, l2_to_tunnel_v6, ipv6_tunnel_term_table) ----
+LOCAL6, REMOTE6, TRANSIT6 = "2001:db8:f::1", "2001:db8:f::2", "2001:db8:f::99"
+
+
+def _overlay6(device, kind=T.TUN_VXLAN):
+    """As _overlay, over an IPv6 underlay: tunnel port 21 (tunnels6[0]) -> underlay port 30 whose
+    local VTEP is 2001:db8:f::1; (2001:db8:f::2, vni 7000) terminates onto port 21."""
+    dp = DataPlane(device=device, flow_buckets=1 << 10)
+    dp.ports.set(1, flags=T.PORT_VALID, bridge_id=3, mac=POD_MAC)
+    dp.ports.set(21, flags=T.PORT_VALID | T.PORT_TUNNEL | T.PORT_TUNNEL6, bridge_id=3)
+    dp.ports.a[21]["lag"] = 0
+    dp.ports.set(30, flags=T.PORT_VALID | T.PORT_VTEP, mac="02:00:00:00:0e:01")
+    dp.tunnels6.set(0, src=LOCAL6, dst=REMOTE6, vni=7000, out_port=30, smac="02:00:00:00:0e:01",
+                    dmac="02:00:00:00:0e:02", kind=kind, traffic_class=0x28)
+    dp.vtep6.set(LOCAL6)
+    dp.terms6.insert(REMOTE6, 7000, 21)
+    dp.macs.insert(3, REMOTE_MAC, 21)
+    dp.macs.insert(3, POD_MAC, 1)
+    dp.ports.version += 1
+    dp.commit(full=True)
+    return dp
+
+
+def _check_outer6(o: bytes, inner: bytes, kind) -> None:
+    assert o[12:14] == b"\x86\xdd"
+    vtf = int.from_bytes(o[14:18], "big")
+    assert vtf >> 28 == 6 and (vtf >> 20) & 0xFF == 0x28 and vtf & 0xFFFFF               # version, class, label
+    assert int.from_bytes(o[18:20], "big") == len(o) - 54 and o[20] == 17 and o[21] == 64  # payload, UDP, hops
+    assert o[22:38] == ipaddress.IPv6Address(LOCAL6).packed and o[38:54] == ipaddress.IPv6Address(REMOTE6).packed
+    assert int.from_bytes(o[54:56], "big") >= 0xC000
+    assert int.from_bytes(o[56:58], "big") == (4789 if kind == T.TUN_VXLAN else 6081)
+    assert int.from_bytes(o[58:60], "big") == len(o) - 54 and o[60:62] == b"\0\0"        # RFC 6935 zero csum
+    assert o[62] == (0x08 if kind == T.TUN_VXLAN else 0x00) and int.from_bytes(o[66:69], "big") == 7000
+    if kind == T.TUN_GENEVE:
+        assert o[64:66] == b"\x65\x58"
+    assert o[70:] == inner
+
+
+def _reverse6(outs):
+    back = []
+    for o in outs:
+        b = bytearray(o)
+        b[22:38], b[38:54] = o[38:54], o[22:38]  # remote -> local
+        inner = bytearray(b[70:])
+        inner[0:6], inner[6:12] = inner[6:12], inner[0:6]
+        b[70:] = inner
+        back.append(bytes(b))
+    bl = np.array([len(b) for b in back], np.uint32)
+    arena = np.zeros((len(back), 1600), np.uint8)
+    for i, b in enumerate(back):
+        arena[i, : len(b)] = np.frombuffer(b, np.uint8)
+    return back, arena, bl
+
+
+@pytest.mark.parametrize("kind", [T.TUN_VXLAN, T.TUN_GENEVE])
+def test_ipv6_underlay_encap_terminate_recirculate(kind):
+    dp = _overlay6("cpu", kind)
+    slots, im, arena, lens = _encap_trace()
+    r = dp.run(slots, im)
+    side = dp.side_result()
+    port, olen, reason = P.meta_fields(r.meta)
+    assert (port == 21).all() and (reason == 0).all() and (olen == lens + 70).all() and P.meta_xhdr(r.meta).all()
+    outs = [P.assemble(r.out[i], int(r.meta[i]), arena[i], int(lens[i]), side["xhdr"][i]) for i in range(3)]
+    for i, o in enumerate(outs):
+        _check_outer6(o, bytes(arena[i, : lens[i]]), kind)
+    back, barena, bl = _reverse6(outs)
+    r2 = dp.run(P.header_slots(barena, bl), P.inmeta(np.full(3, 30), bl))
+    p2, l2, rs2 = P.meta_fields(r2.meta)
+    assert (rs2 == 14).all() and (p2 == T.PORT_NONE).all() and (l2 == bl - 70).all()   # recirc6
+    for i in range(3):
+        tp, inner = dp.resolve_recirc6(back[i])
+        assert tp == 21 and inner == back[i][70:]
+        r3 = dp.run(P.header_slots(np.frombuffer(inner, np.uint8)[None], np.array([len(inner)])),
+                    P.inmeta(np.array([21]), np.array([len(inner)])))
+        p3, l3, rs3 = P.meta_fields(r3.meta)
+        assert (int(rs3[0]), int(p3[0]), int(l3[0])) == (0, 1, len(inner))           # bridged to the pod
+    assert dp.drop_counters().get("recirc6") == 3
+
+
+def test_ipv6_underlay_unknown_vni_and_transit():
+    dp = _overlay6("cpu")
+    slots, im, arena, lens = _encap_trace()
+    r = dp.run(slots, im)
+    o = P.assemble(r.out[1], int(r.meta[1]), arena[1], int(lens[1]), dp.side_result()["xhdr"][1])
+    back, barena, bl = _reverse6([o])
+    wrong_vni = bytearray(back[0])
+    wrong_vni[68] ^= 1
+    assert dp.resolve_recirc6(bytes(wrong_vni)) is None                  # no (source, VNI) entry: slow path
+    transit = bytearray(back[0])
+    transit[38:54] = ipaddress.IPv6Address(TRANSIT6).packed               # not to this VTEP
+    fr = np.frombuffer(bytes(transit), np.uint8)[None]
+    r2 = dp.run(P.header_slots(fr, bl), P.inmeta(np.array([30]), bl))
+    assert P.meta_fields(r2.meta)[2][0] != 14                            # bridged / punted, not terminated
+    assert dp.resolve_recirc6(bytes(transit)) is None
+
+
+def test_ipv6_outer_header_binding_matches_model():
+    """The native make_outer (64-B entry) against _check_outer6's field model."""
+    dp = _overlay6("cpu")
+    inner = bytes(range(60))
+    x = dp.nf.make_outer(dp.tunnels6.bytes_of(0), len(inner), 0x12345)
+    assert len(x) == 70
+    _check_outer6(x + inner, inner, T.TUN_VXLAN)
+    assert int.from_bytes(x[15:18], "big") & 0xFFFFF == 0x12345 & 0xFFFFF          # hash-derived flow label
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", [T.TUN_VXLAN, T.TUN_GENEVE])
+def test_ipv6_tunnels_gpu_bit_exact(kind):
+    import torch
+
+    c, g = _overlay6("cpu", kind), _overlay6("cuda", kind)
+    slots, im, arena, lens = _encap_trace()
+    rc = c.run(slots, im)
+    sc = c.side_result()
+    rg = g.run(torch.from_numpy(slots).cuda(), torch.from_numpy(im.view(np.int32)).cuda())
+    torch.cuda.synchronize()
+    sg = g.side_result()
+    assert np.array_equal(rg.meta.cpu().numpy().view(np.uint32), rc.meta)
+    assert np.array_equal(rg.out.cpu().numpy(), rc.out)
+    assert np.array_equal(sg["xhdr"][:3], sc["xhdr"][:3])
+    outs = [P.assemble(rc.out[i], int(rc.meta[i]), arena[i], int(lens[i]), sc["xhdr"][i]) for i in range(3)]
+    _, barena, bl = _reverse6(outs)
+    s2, i2 = P.header_slots(barena, bl), P.inmeta(np.full(3, 30), bl)
+    r2c = c.run(s2, i2)
+    r2g = g.run(torch.from_numpy(s2).cuda(), torch.from_numpy(i2.view(np.int32)).cuda())
+    torch.cuda.synchronize()
+    assert np.array_equal(r2g.meta.cpu().numpy().view(np.uint32), r2c.meta)
+    assert (P.meta_fields(r2c.meta)[2] == 14).all()

@@ -163,3 +163,48 @@ def test_geneve_vlan_pop_encap_and_decap_push_vlan(rt):
     dp.ports.set(5, flags=T.PORT_VALID, bridge_id=0)
     op, rs, out = _send(dp, tp, "02:00:00:00:00:05", "10.0.0.9")
     assert (op, rs) == (5, 0) and bytes(out[12:16]) == b"\x81\x00" + (321).to_bytes(2, "big")
+
+
+def test_ipv6_underlay_tunnel_tables(rt):
+    """l2_to_tunnel_v6 + vxlan_encap_v6_mod_table (p4info.txt: set_tunnel_v6 ipv6_1..4, the encap's
+    128-bit addresses, ds / ecn / flow label / hop limit), ipv6_tunnel_term_table and
+    rx_ipv6_tunnel_source_port: the IPv6 encap leaves on the tunnel's port with a 70-B outer header,
+    and the reverse direction is recognised on the underlay port (recirc6) and resolved to the
+    termination port, whose source-port bridge mapping applies."""
+    dp = rt.dp
+    add = rt.add_entry
+    add(C + "vxlan_encap_v6_mod_table", "vmeta.common.mod_blob_ptr=11,action=linux_networking_control.vxlan_encap_v6("
+        "2001:db8:f::1,2001:db8:f::2,10,0,0xabcde,32,0,4789,7100)")
+    add(C + "l2_to_tunnel_v6", "hdrs.mac[vmeta.common.depth].da=02:00:00:00:dd:01,"
+        "action=linux_networking_control.set_tunnel_v6(0x20010db8,0x000f0000,0x00000000,0x00000002)")
+    add(C + "ipv6_tunnel_term_table", "ipv6_src=2001:db8:f::2,vni=7100,action=linux_networking_control.set_vxlan_decap_outer_hdr(3)")
+    add(C + "rx_ipv6_tunnel_source_port", "ipv6_src=2001:db8:f::2,vni=7100,action=linux_networking_control.set_source_port(44)")
+    add(C + "source_port_to_bridge_map", "user_meta.cmeta.source_port=44/0xffff,hdrs.vlan_ext[vmeta.common.depth].hdr.vid=0/0,"
+        "priority=1,action=linux_networking_control.set_bridge_id(6)")
+    tport = TUNNEL_PORT_BASE + 64
+    assert dp.tunnels6.n == 1 and dp.ports.a[tport]["flags"] & T.PORT_TUNNEL6
+    e = dp.tunnels6.a[0]
+    assert int(e["tc_flow"]) == ((10 << 2) << 20 | 0xABCDE) and int(e["hop_limit"]) == 32
+    assert dp.vtep6.active and dp.ports.a[PHY_BASE]["flags"] & T.PORT_VTEP and len(dp.terms6) == 1
+    dp.ports.set(1, flags=T.PORT_VALID, bridge_id=0)
+    fr, ln = P.craft(1, dmac="02:00:00:00:dd:01", smac="02:00:00:00:00:77", src_ip=0x0A000001, dst_ip=0x0A000002,
+                     sport=9, dport=80)
+    dp.commit()
+    r = dp.run(fr, P.inmeta(np.array([1]), ln))
+    op, olen, rs = P.meta_fields(r.meta)
+    assert (int(op[0]), int(rs[0]), int(olen[0])) == (tport, 0, int(ln[0]) + 70)
+    o = P.assemble(r.out[0], int(r.meta[0]), fr[0], int(ln[0]), dp.side_result()["xhdr"][0])
+    assert o[12:14] == b"\x86\xdd" and o[38:54] == ipaddress.IPv6Address("2001:db8:f::2").packed
+    assert int.from_bytes(o[14:18], "big") & 0xFFFFF == 0xABCDE and o[21] == 32
+    assert int.from_bytes(o[66:69], "big") == 7100
+    # reverse: from the remote VTEP to the local one, on the underlay port
+    b = bytearray(o)
+    b[22:38], b[38:54] = o[38:54], o[22:38]
+    arr = np.frombuffer(bytes(b), np.uint8)[None]
+    r2 = dp.run(P.header_slots(arr, np.array([len(b)])), P.inmeta(np.array([PHY_BASE]), np.array([len(b)])))
+    assert int(P.meta_fields(r2.meta)[2][0]) == 14
+    tp, inner = dp.resolve_recirc6(bytes(b))
+    assert tp == TUNNEL_PORT_BASE + 128 + 3 and inner == bytes(b[70:])
+    assert int(dp.ports.a[tp]["bridge_id"]) == 6
+    rt.del_entry(C + "ipv6_tunnel_term_table", "ipv6_src=2001:db8:f::2,vni=7100")
+    assert len(dp.terms6) == 0 and not dp.vtep6.active
