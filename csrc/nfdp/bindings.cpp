@@ -8,6 +8,7 @@
 #include <pybind11/stl.h>
 
 #include "host.h"
+#include "ipsec.h"
 #include "pktio.h"
 #include "ring.h"
 #include "shard.h"
@@ -93,6 +94,29 @@ SideOut side_from(const py::object& o) {
   if (so.cap_rep && (!so.rep_hdr || !so.rep_meta || !so.rep_src)) throw std::invalid_argument("side: replica buffers missing");
   if (so.cap_learn && !so.learn) throw std::invalid_argument("side: learn buffer missing");
   return so;
+}
+
+// ESP batch (ipsec.h EspBatch) from a dict of buffer addresses and sizes.
+EspBatch esp_from(const py::dict& d) {
+  EspBatch a{};
+  a.in = ptr<const uint8_t>(d, "in"); a.in_stride = val<uint32_t>(d, "in_stride", 0);
+  a.in_len = ptr<const uint32_t>(d, "in_len");
+  a.out = ptr<uint8_t>(d, "out"); a.out_stride = val<uint32_t>(d, "out_stride", 0);
+  a.out_len = ptr<uint32_t>(d, "out_len"); a.status = ptr<uint32_t>(d, "status");
+  a.sa = ptr<const EspSa>(d, "sa"); a.n_sa = val<uint32_t>(d, "n_sa", 0);
+  a.spd = ptr<const SpdEntry>(d, "spd"); a.spd_mask = val<uint32_t>(d, "spd_mask", 0);
+  a.rxsa = ptr<const RxSaEntry>(d, "rxsa"); a.rxsa_mask = val<uint32_t>(d, "rxsa_mask", 0);
+  a.seq = ptr<const uint32_t>(d, "seq");
+  a.out_sa = ptr<uint32_t>(d, "out_sa"); a.out_seq = ptr<uint32_t>(d, "out_seq");
+  a.n = val<uint32_t>(d, "n", 0);
+  if (a.n && (!a.in || !a.out || !a.in_len || !a.out_len || !a.status || !a.sa))
+    throw std::invalid_argument("esp batch: missing buffer");
+  if ((a.in_stride & 15u) || (a.out_stride & 15u) || a.in_stride < 64u || a.out_stride < 128u)
+    throw std::invalid_argument("esp batch: strides must be multiples of 16 (>= 64 in, >= 128 out)");
+  if (a.spd && ((a.spd_mask + 1) & a.spd_mask)) throw std::invalid_argument("esp: SPD size must be a power of two");
+  if (a.rxsa && ((a.rxsa_mask + 1) & a.rxsa_mask)) throw std::invalid_argument("esp: RX SA size must be a power of two");
+  if (a.n_sa > (uint32_t)kEspMaxSa) throw std::invalid_argument("esp: too many SAs");
+  return a;
 }
 
 void check(hipError_t e, const char* what) {
@@ -625,6 +649,32 @@ PYBIND11_MODULE(_nfdp, m) {
                       reinterpret_cast<const void*>(out), reinterpret_cast<const uint32_t*>(out_meta), so,
                       reinterpret_cast<unsigned long long*>(port_ctr), reinterpret_cast<unsigned long long*>(drop_ctr),
                       reinterpret_cast<hipStream_t>(stream)), "launch_side");
+  });
+  // ---- IPsec ESP engine ----
+  m.attr("ESP_SA_BYTES") = (int)sizeof(EspSa);
+  m.attr("ESP_CLEAR_OFF") = kClearOff;
+  m.attr("ESP_OFF") = kEspOff;
+  m.def("esp_tables", []() {
+    const EspTables t = esp_host_tables();
+    return py::make_tuple(py::bytes(reinterpret_cast<const char*>(t.te0), 1024),
+                          py::bytes(reinterpret_cast<const char*>(t.sbox), 256),
+                          py::bytes(reinterpret_cast<const char*>(t.rem), 128));
+  });
+  m.def("esp_build_sa", [](py::bytes key, py::bytes salt, uint32_t spi, uint32_t mode, uint32_t src_raw,
+                           uint32_t dst_raw, uint32_t smac_lo, uint32_t smac_hi, uint32_t dmac_lo, uint32_t dmac_hi) {
+    std::string k = key, sl = salt;
+    if (sl.size() != 4) throw std::invalid_argument("ESP: salt must be 4 bytes");
+    const EspSa sa = esp_build_sa(reinterpret_cast<const uint8_t*>(k.data()), k.size(),
+                                  reinterpret_cast<const uint8_t*>(sl.data()), spi, mode, src_raw, dst_raw, smac_lo,
+                                  (uint16_t)smac_hi, dmac_lo, (uint16_t)dmac_hi);
+    return py::bytes(reinterpret_cast<const char*>(&sa), sizeof(sa));
+  });
+  m.def("esp_run_cpu", [](bool enc, py::dict d) { esp_run_cpu(esp_from(d), enc); });
+  m.def("launch_esp", [](bool enc, py::dict d, uintptr_t te0, uintptr_t sbox, uintptr_t rem, int num_cus,
+                         uintptr_t stream) {
+    check(launch_esp(esp_from(d), enc, reinterpret_cast<const uint32_t*>(te0), reinterpret_cast<const uint8_t*>(sbox),
+                     reinterpret_cast<const uint64_t*>(rem), num_cus, reinterpret_cast<hipStream_t>(stream)),
+          "launch_esp");
   });
   m.def("launch_harvest", [](uintptr_t ctr, uintptr_t out, uint32_t n, uintptr_t stream) {
     check(launch_harvest(reinterpret_cast<unsigned long long*>(ctr), reinterpret_cast<unsigned long long*>(out), n,

@@ -113,6 +113,18 @@ struct FusedLaunch {
 hipError_t launch_fused(const FusedLaunch& f, const LaunchCfg& cfg, hipStream_t s);
 // Side pass alone (flood / mirror / ARP replicas, learn events, tunnel headers) over a side list
 // another kernel filled (the persistent ring kernel): slots / meta are that kernel's buffers.
+// IPsec ESP engine (ipsec.h / ipsec.hip / ipsec_cpu.cpp)
+struct EspBatch;
+struct EspSa;
+struct EspTables;
+hipError_t launch_esp(const EspBatch& a, bool enc, const uint32_t* te0, const uint8_t* sbox, const uint64_t* rem,
+                      int num_cus, hipStream_t s);
+EspTables esp_host_tables();
+EspSa esp_build_sa(const uint8_t* key, size_t key_len, const uint8_t* salt, uint32_t spi, uint32_t mode,
+                   uint32_t src_ip, uint32_t dst_ip, uint32_t smac_lo, uint16_t smac_hi, uint32_t dmac_lo,
+                   uint16_t dmac_hi);
+void esp_run_cpu(const EspBatch& a, bool enc);
+
 hipError_t launch_side(const TablesView& t, const void* pkts, const uint32_t* inmeta, const void* out,
                        const uint32_t* out_meta, const SideOut& side, unsigned long long* port_ctr,
                        unsigned long long* drop_ctr, hipStream_t s);

@@ -75,6 +75,7 @@ class DataPlane:
         self.tunnels6 = T.Tunnel6Table()
         self.vtep6 = T.Vtep6()
         self.terms6 = T.Term6Table()     # host side: finished by resolve_recirc6 on the whole frame
+        self._ipsec = None               # ESP engine (dataplane/ipsec.py), created on first use
         self.acl = T.AclTable()
         self.flows = T.FlowTable(flow_buckets, rss_key)
         self.rss_key = rss_key
@@ -395,6 +396,15 @@ class DataPlane:
                 "learn_unplaced": int(c[4]), "n_side": int(c[5]), "side_dropped": int(c[6]),
                 "xhdr": (g("side_xhdr").reshape(-1, self.XHDR_WORDS).view(np.uint8).reshape(-1, 4 * self.XHDR_WORDS)
                          if self._tunnels_on() else None)}
+
+    @property
+    def ipsec(self):
+        """The IPsec ESP engine of this data plane (SA database, SPD, inbound SA table, kernels)."""
+        if self._ipsec is None:
+            from .ipsec import IpsecEngine
+
+            self._ipsec = IpsecEngine(device=str(self.tdev) if self.gpu else "cpu", num_cus=self.num_cus)
+        return self._ipsec
 
     def resolve_recirc6(self, frame: bytes) -> tuple[int, bytes] | None:
         """Finish the termination of a frame the kernel marked recirc6 (IPv6-underlay VXLAN /

@@ -248,6 +248,22 @@ TABLES = [
      ["set_vxlan_decap_outer_hdr", "set_vxlan_decap_outer_and_push_vlan", "set_geneve_decap_outer_hdr",
       "set_geneve_decap_outer_and_push_vlan", "NoAction"], 1024),
     ("rx_ipv6_tunnel_source_port", [("ipv6_src", 128, "EXACT"), ("vni", 24, "EXACT")], ["set_source_port", "drop"], 1024),
+    # IPsec (the IPU's inline crypto engine; here the ESP kernels, dataplane/ipsec.py)
+    ("ipsec_spd", [("hdrs.ipv4[vmeta.common.depth].dst_ip", 32, "EXACT"), ("hdrs.ipv4[vmeta.common.depth].protocol", 8, "EXACT")],
+     ["ipsec_protect_set_metadata", "ipsec_bypass", "NoAction"], 1024),
+    ("ipsec_tx_sa_classification_table", [("hdrs.ipv4[vmeta.common.depth].dst_ip", 32, "EXACT"),
+                                          ("hdrs.ipv4[vmeta.common.depth].protocol", 8, "EXACT"),
+                                          ("user_meta.cmeta.is_tunnel", 1, "EXACT")],
+     ["tx_ipsec_transport", "tx_ipsec_transport_with_underlay", "tx_ipsec_tunnel", "tx_ipsec_tunnel_v6", "drop",
+      "NoAction"], 1024),
+    ("ipsec_tunnel_table", [("vmeta.common.saidx", 24, "EXACT"), ("bit16_zeros", 13, "EXACT")],
+     ["set_ipsec_tunnel", "NoAction"], 1024),
+    ("ipsec_tunnel_encap_mod_table", [("vmeta.common.mod_blob_ptr", 24, "EXACT")], ["ipsec_tunnel_encap_mod", "NoAction"], 1024),
+    ("ipv4_ipsec_tunnel_term_table", [("ipv4_src", 32, "EXACT"), ("ipv4_dst", 32, "EXACT")],
+     ["decap_ipsec_tunnel_hdr", "do_recirculate"], 1024),
+    ("MainControlDecrypt.ipsec_rx_sa_classification_table",
+     [("hdrs.ipv4[vmeta.common.depth].src_ip", 32, "EXACT"), ("hdrs.ipv4[vmeta.common.depth].dst_ip", 32, "EXACT"),
+      ("hdrs.esp.spi", 32, "EXACT")], ["MainControlDecrypt.ipsec_decrypt", "MainControlDecrypt.ipsec_bypass"], 1024),
     # LAG rx, smac learning check, ARP trap (p4info.txt:168, 783, 1011)
     ("rx_lag_table", [("vmeta.common.port_id", 2, "EXACT"), ("user_meta.cmeta.lag_group_id", 8, "EXACT")],
      ["fwd_to_vsi", "drop"], 1024),
@@ -310,6 +326,17 @@ ACTIONS = {
     "trap_enable": [],
     "fwd_to_cp": [],
     "do_trap_enable": [],
+    "ipsec_protect_set_metadata": [("saidx", 24)],
+    "ipsec_bypass": [],
+    "tx_ipsec_transport": [],
+    "tx_ipsec_transport_with_underlay": [],
+    "tx_ipsec_tunnel": [("dst_addr", 32)],
+    "tx_ipsec_tunnel_v6": [("dst_addr_1", 32), ("dst_addr_2", 32), ("dst_addr_3", 16)],
+    "set_ipsec_tunnel": [("tunnel_id", 24)],
+    "ipsec_tunnel_encap_mod": [("ipsec_src_addr", 32), ("ipsec_dst_addr", 32), ("proto", 8)],
+    "decap_ipsec_tunnel_hdr": [],
+    "MainControlDecrypt.ipsec_decrypt": [("saidx", 24)],
+    "MainControlDecrypt.ipsec_bypass": [],
 }
 
 
@@ -320,8 +347,9 @@ def _render_mi355x_p4info() -> str:
         aid = 0x01000000 | (k + 1)
         aids[name] = aid
     for k, (tname, fields, acts, size) in enumerate(TABLES):
-        lines += ["tables {", "  preamble {", f"    id: {0x02000000 | (k + 1)}", f'    name: "{C}{tname}"',
-                  f'    alias: "{tname}"', "  }"]
+        full = tname if "." in tname else C + tname   # a name with a control prefix is used as is
+        lines += ["tables {", "  preamble {", f"    id: {0x02000000 | (k + 1)}", f'    name: "{full}"',
+                  f'    alias: "{tname.split(".")[-1]}"', "  }"]
         for j, (fname, width, mt) in enumerate(fields):
             lines += ["  match_fields {", f"    id: {j + 1}", f'    name: "{fname}"', f"    bitwidth: {width}",
                       f"    match_type: {mt}", "  }"]
@@ -329,7 +357,9 @@ def _render_mi355x_p4info() -> str:
             lines += ["  action_refs {", f"    id: {aids[a]}", "  }"]
         lines += [f"  size: {size}", "}"]
     for name, params in ACTIONS.items():
-        lines += ["actions {", "  preamble {", f"    id: {aids[name]}", f'    name: "{C}{name}"', f'    alias: "{name}"', "  }"]
+        full = name if "." in name else C + name
+        lines += ["actions {", "  preamble {", f"    id: {aids[name]}", f'    name: "{full}"',
+                  f'    alias: "{name.split(".")[-1]}"', "  }"]
         for j, (pname, width) in enumerate(params):
             lines += ["  params {", f"    id: {j + 1}", f'    name: "{pname}"', f"    bitwidth: {width}", "  }"]
         lines += ["}"]

@@ -234,7 +234,7 @@ class P4Runtime:
 
     # ------------------------------------------------------------------ compile
     def _rows(self, short: str) -> list[Entry]:
-        name = "linux_networking_control." + short
+        name = short if "." in short else "linux_networking_control." + short
         rows = list(self.entries.get(name, {}).values())
         return sorted(rows, key=lambda e: -e.priority)
 
@@ -386,8 +386,73 @@ class P4Runtime:
             else:
                 dp.ports.set_lag(p, None)
         self._compile_l3_tunnels(dp, port, add_mac, src)
+        self._compile_ipsec(dp)
         self._owned_ports = owned
         dp.ports.version += 1
+
+    def _compile_ipsec(self, dp) -> None:
+        """IPsec tables onto the ESP engine (dataplane/ipsec.py): ipsec_spd (protect with SA saidx /
+        bypass), ipsec_tx_sa_classification_table (transport, or tunnel to dst_addr; drop),
+        ipsec_tunnel_table + ipsec_tunnel_encap_mod_table (an SA's tunnel outer addresses),
+        ipsec_rx_sa_classification_table (inbound (src, dst, SPI) -> SA) and
+        ipv4_ipsec_tunnel_term_table (inbound SAs of those (src, dst) decapsulate a tunnel).  The SA
+        key material itself comes from the IPsec control plane (`dp.ipsec.add_sa`), as the IPU's
+        crypto SAD does; SA modes are applied to SAs that exist."""
+        names = ("ipsec_spd", "ipsec_tx_sa_classification_table", "ipsec_tunnel_table", "ipsec_tunnel_encap_mod_table",
+                 "ipv4_ipsec_tunnel_term_table", "MainControlDecrypt.ipsec_rx_sa_classification_table")
+        rows = {n: self._rows(n) for n in names}
+        if not any(rows.values()) and not getattr(self, "_owned_ipsec", False):
+            return
+        eng = dp.ipsec
+        for key in list(eng.spd_rules):
+            eng.spd_rules.pop(key)
+        eng.rx_rules.clear()
+        drops = set()
+        modes: dict[tuple[int, int], tuple[int, int | None]] = {}
+        for e in rows["ipsec_tx_sa_classification_table"]:
+            d, p = e.key[0][1], e.key[1][1]
+            if e.action.endswith("tx_ipsec_tunnel_v6"):
+                raise P4Error("UNIMPLEMENTED", "IPsec tunnels over an IPv6 underlay are not supported")
+            if e.action.endswith("drop"):
+                drops.add((d, p))
+            elif e.action.endswith("tx_ipsec_tunnel"):
+                modes[(d, p)] = (2, e.params["dst_addr"])
+            elif e.action.endswith(("tx_ipsec_transport", "tx_ipsec_transport_with_underlay")):
+                modes[(d, p)] = (1, None)
+        tun_of = {e.key[0][1]: e.params["tunnel_id"] for e in rows["ipsec_tunnel_table"] if e.action.endswith("set_ipsec_tunnel")}
+        encap = {e.key[0][1]: e.params for e in rows["ipsec_tunnel_encap_mod_table"] if e.action.endswith("ipsec_tunnel_encap_mod")}
+        from . import ipsec as I
+
+        raw = lambda v: str(ipaddress.IPv4Address(v))  # noqa: E731
+        for e in rows["ipsec_spd"]:
+            d, p = e.key[0][1], e.key[1][1]
+            if (d, p) in drops:
+                eng.set_spd(raw(d), p, I.DROP)
+            elif e.action.endswith("ipsec_protect_set_metadata"):
+                sa = e.params["saidx"]
+                eng.set_spd(raw(d), p, I.PROTECT, sa)
+                m = modes.get((d, p))
+                if sa in eng.sa_info and m is not None:
+                    if m[0] == 2:
+                        enc = encap.get(tun_of.get(sa, -1), {})
+                        eng.set_sa_mode(sa, I.TUNNEL, src=raw(enc["ipsec_src_addr"]) if enc else None,
+                                        dst=raw(enc.get("ipsec_dst_addr", m[1])) if enc else raw(m[1]))
+                    else:
+                        eng.set_sa_mode(sa, I.TRANSPORT)
+            elif e.action.endswith("ipsec_bypass"):
+                eng.set_spd(raw(d), p, I.BYPASS)
+        terms = {(e.key[0][1], e.key[1][1]) for e in rows["ipv4_ipsec_tunnel_term_table"]}
+        for e in rows["MainControlDecrypt.ipsec_rx_sa_classification_table"]:
+            if not e.action.endswith("ipsec_decrypt"):
+                continue
+            s_, d_, spi = e.key[0][1], e.key[1][1], e.key[2][1]
+            sa = e.params["saidx"]
+            eng.set_rx_sa(raw(s_), raw(d_), spi, sa)
+            if sa in eng.sa_info:
+                eng.set_sa_mode(sa, I.TUNNEL if (s_, d_) in terms else I.TRANSPORT)
+        eng._rebuild_spd()
+        eng._rebuild_rx()
+        self._owned_ipsec = any(rows.values())
 
     def _compile_tunnels_v6(self, dp, port, add_mac, bridges, mac_of) -> bool:
         """IPv6-underlay tunnels: l2_to_tunnel_v6 + {vxlan,geneve}_encap_v6[_vlan_pop]_mod_table onto

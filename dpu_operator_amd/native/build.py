@@ -45,7 +45,8 @@ def _includes() -> list[str]:
 MODULES = {
     "_nfdp": {
         "dir": CSRC / "nfdp",
-        "sources": ["kernels.hip", "shard.hip", "pktio.hip", "ring.hip", "host.cpp", "shard_cpu.cpp", "bindings.cpp"],
+        "sources": ["kernels.hip", "shard.hip", "pktio.hip", "ring.hip", "ipsec.hip", "host.cpp", "shard_cpu.cpp",
+                    "ipsec_cpu.cpp", "bindings.cpp"],
         "hip": True,
     },
     "_agent": {
