@@ -127,6 +127,12 @@ class LivePath:
         self.error: BaseException | None = None
         self._recirc: list[tuple[bytes, int]] = []
         self.stats["recirc"] = 0
+        # IPsec boundary (dataplane/ipsec.py, the GPU ESP engine): ESP arriving on these ports is
+        # authenticated + decrypted before the header pipeline, frames leaving them pass the SPD
+        # (protect -> ESP, bypass, drop) in one batch per cycle
+        self.ipsec_ports: set[int] = set()
+        self._esp_out: list[tuple[int, bytes]] = []
+        self.stats.update(esp_in=0, esp_out=0, esp_drop=0)
 
     # ------------------------------------------------------------------ port map
     def add_port(self, idx: int, port) -> None:
@@ -170,16 +176,60 @@ class LivePath:
     def _send(self, port_idx: int, frame: bytes) -> None:
         a = self.dp.ports.a
         if 0 <= port_idx < len(a) and a[port_idx]["flags"] & (1 << 14):  # tunnel port: its underlay
-            port_idx = int(self.dp.tunnels.a[int(a[port_idx]["lag"])]["out_port"])
+            tab = self.dp.tunnels6 if a[port_idx]["flags"] & (1 << 18) else self.dp.tunnels
+            port_idx = int(tab.a[int(a[port_idx]["lag"])]["out_port"])
+        if port_idx in self.ipsec_ports:
+            self._esp_out.append((port_idx, frame))   # encrypted as one batch at the end of the cycle
+            return
+        self._write(port_idx, frame)
+
+    def _write(self, port_idx: int, frame: bytes) -> None:
         port = self.ports.get(port_idx)
         if port is None:
             self.stats["no_netdev"] += 1
         elif port.write(frame):
             self.stats["tx"] += 1
 
+    def _esp_inbound(self, frames: list, src: list) -> tuple[list, list]:
+        """Decrypt the ESP frames of the batch that arrived on IPsec ports (one kernel launch);
+        no SA -> slow path, authentication / replay failure -> dropped."""
+        idx = [i for i, (f, p) in enumerate(zip(frames, src))
+               if p in self.ipsec_ports and len(f) >= 34 and f[12:14] == b"\x08\x00" and f[23] == 50]
+        if not idx:
+            return frames, src
+        dec, st = self.dp.ipsec.decrypt([frames[i] for i in idx])
+        keep = np.ones(len(frames), bool)
+        frames = list(frames)
+        for k, i in enumerate(idx):
+            if dec[k] is not None:
+                frames[i] = dec[k]
+                self.stats["esp_in"] += 1
+            else:
+                keep[i] = False
+                if int(st[k]) == 4 and self.on_punt:       # no SA: the IPsec control plane's business
+                    self.on_punt(bytes(frames[i]), src[i], 5)
+                    self.stats["punt"] += 1
+                else:
+                    self.stats["esp_drop"] += 1
+        return [f for f, k in zip(frames, keep) if k], [p for p, k in zip(src, keep) if k]
+
+    def _esp_flush(self) -> None:
+        if not self._esp_out:
+            return
+        out, self._esp_out = self._esp_out, []
+        enc, _ = self.dp.ipsec.encrypt([f for _, f in out])
+        for (port_idx, _), f in zip(out, enc):
+            if f is None:
+                self.stats["esp_drop"] += 1
+            else:
+                self.stats["esp_out"] += 1
+                self._write(port_idx, f)
+
     def poll_once(self, timeout: float = 0.05) -> int:
         self._t_ready = time.perf_counter()
         frames, src = self._gather(timeout)
+        if self.ipsec_ports and frames:
+            frames, src = self._esp_inbound(frames, src)
         n = len(frames)
         if not n:
             return 0
@@ -292,6 +342,7 @@ class LivePath:
             else:
                 self.stats["replicas"] += 1
                 self._send(int(rp[0]), fr)
+        self._esp_flush()
         t_end = time.perf_counter()
         lat.observe("rx", t_rx - t_start)
         lat.observe("pipeline", t_pipe - t_rx)

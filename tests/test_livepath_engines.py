@@ -144,3 +144,66 @@ def test_ring_engine_matches_batch_oracle():
     assert stats["rx"] == 7 and stats.get("ring_relaunch") == 0
     dp.pull_learned()
     assert {(b, m) for b, m, _ in dp.macs.learned()} >= {(BR, MACS[0]), (BR, MACS[1]), (BR, MACS[2])}
+
+
+def test_ipsec_boundary_on_the_uplink():
+    """Port 3 is the uplink with the ESP engine at its boundary: pod traffic to the protected
+    destination leaves it as ESP (tunnel mode), other traffic in clear (SPD bypass); ESP from the
+    peer is authenticated, decrypted and bridged to the pod; a tampered packet is dropped."""
+    from dpu_operator_amd.dataplane import ipsec as I
+
+    dp = DataPlane(device="cpu", flow_buckets=1 << 10)
+    for p in (0, 3):
+        dp.ports.set(p, flags=T.PORT_VALID, bridge_id=BR)
+    dp.macs.insert(BR, MACS[3], 3)
+    dp.macs.insert(BR, MACS[0], 0)
+    dp.commit(full=True)
+    eng = dp.ipsec
+    eng.add_sa(0, key=bytes(range(16)), salt=b"\x01\x02\x03\x04", spi=0x11, mode=I.TUNNEL, src="192.0.2.1",
+               dst="192.0.2.2", smac=MACS[0], dmac=MACS[3])
+    eng.add_sa(1, key=bytes(range(16, 32)), salt=b"\x05\x06\x07\x08", spi=0x22, mode=I.TUNNEL,
+               src="192.0.2.2", dst="192.0.2.1")
+    eng.set_spd("10.0.0.2", 17, I.PROTECT, 0)
+    eng.set_rx_sa("192.0.2.2", "192.0.2.1", 0x22, 1)
+    # the peer's engine: the mirror image (its SA 0 = our SA 1)
+    peer = I.IpsecEngine()
+    peer.add_sa(0, key=bytes(range(16, 32)), salt=b"\x05\x06\x07\x08", spi=0x22, mode=I.TUNNEL, src="192.0.2.2",
+                dst="192.0.2.1", smac=MACS[3], dmac=MACS[0])
+    peer.set_spd("10.0.0.1", 17, I.PROTECT, 0)
+    peer.add_sa(1, key=bytes(range(16)), salt=b"\x01\x02\x03\x04", spi=0x11, mode=I.TUNNEL)
+    peer.set_rx_sa("192.0.2.1", "192.0.2.2", 0x11, 1)
+    ports = {0: SockPort(), 3: SockPort()}
+    live = LivePath(dp, ports)
+    live.ipsec_ports = {3}
+    try:
+        prot = _frame(MACS[3], MACS[0], 300, 1)                      # to 10.0.0.2: protected
+        clear = bytes(bytearray(prot[:30]) + bytes([10, 0, 0, 9]) + prot[34:])   # to 10.0.0.9: bypass
+        ports[0].inject(prot)
+        ports[0].inject(clear)
+        for _ in range(10):
+            if live.poll_once(0.05):
+                break
+        out = ports[3].drain()
+        assert len(out) == 2 and live.stats["esp_out"] == 2
+        esp = next(f for f in out if f[23] == 50)
+        assert clear in out and int.from_bytes(esp[34:38], "big") == 0x11
+        dec, st = peer.decrypt([esp])
+        assert st[0] == I.DONE and dec[0][14:] == prot[14:]
+        # the peer answers through its SA; a tampered copy is dropped
+        fr, ln = P.craft_full(1, dmac=MACS[0], smac=MACS[3], src_ip=0x0A000002, dst_ip=0x0A000001, sport=7, dport=9,
+                              frame_len=500)
+        reply = bytes(fr[0, : int(ln[0])])
+        enc, _ = peer.encrypt([reply, reply])
+        bad = bytearray(enc[1])
+        bad[100] ^= 1
+        ports[3].inject(enc[0])
+        ports[3].inject(bytes(bad))
+        for _ in range(10):
+            if live.poll_once(0.05):
+                break
+        got = ports[0].drain()
+        assert len(got) == 1 and got[0][14:] == reply[14:] and live.stats["esp_in"] == 1 and live.stats["esp_drop"] == 1
+    finally:
+        live.stop()
+        for p in ports.values():
+            p.close()
