@@ -264,6 +264,10 @@ TABLES = [
     ("MainControlDecrypt.ipsec_rx_sa_classification_table",
      [("hdrs.ipv4[vmeta.common.depth].src_ip", 32, "EXACT"), ("hdrs.ipv4[vmeta.common.depth].dst_ip", 32, "EXACT"),
       ("hdrs.esp.spi", 32, "EXACT")], ["MainControlDecrypt.ipsec_decrypt", "MainControlDecrypt.ipsec_bypass"], 1024),
+    # keyless exact-match-engine housekeeping tables whose only action is NoAction (p4info.txt):
+    # entries are accepted and, as in the pipeline, change nothing
+    ("lem_exception", [], ["NoAction"], 1024),
+    ("lem_clear", [], ["NoAction"], 1024),
     # LAG rx, smac learning check, ARP trap (p4info.txt:168, 783, 1011)
     ("rx_lag_table", [("vmeta.common.port_id", 2, "EXACT"), ("user_meta.cmeta.lag_group_id", 8, "EXACT")],
      ["fwd_to_vsi", "drop"], 1024),

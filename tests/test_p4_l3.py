@@ -208,3 +208,14 @@ def test_ipv6_underlay_tunnel_tables(rt):
     assert int(dp.ports.a[tp]["bridge_id"]) == 6
     rt.del_entry(C + "ipv6_tunnel_term_table", "ipv6_src=2001:db8:f::2,vni=7100")
     assert len(dp.terms6) == 0 and not dp.vtep6.active
+
+
+def test_keyless_lem_tables_accept_noaction(rt):
+    """lem_exception / lem_clear (keyless, NoAction only in the p4info): one entry each is
+    accepted, a second is ALREADY_EXISTS, and nothing in the data plane changes."""
+    before = rt.dp.ports.a.copy()
+    for t in ("lem_exception", "lem_clear"):
+        rt.add_entry(C + t, "action=linux_networking_control.NoAction()")
+        with pytest.raises(P4Error):
+            rt.add_entry(C + t, "action=linux_networking_control.NoAction()")
+    assert (rt.dp.ports.a == before).all()
