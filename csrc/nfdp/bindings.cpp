@@ -658,7 +658,7 @@ PYBIND11_MODULE(_nfdp, m) {
     const EspTables t = esp_host_tables();
     return py::make_tuple(py::bytes(reinterpret_cast<const char*>(t.te0), 1024),
                           py::bytes(reinterpret_cast<const char*>(t.sbox), 256),
-                          py::bytes(reinterpret_cast<const char*>(t.rem), 128));
+                          py::bytes(reinterpret_cast<const char*>(t.rem), 2048));
   });
   m.def("esp_build_sa", [](py::bytes key, py::bytes salt, uint32_t spi, uint32_t mode, uint32_t src_raw,
                            uint32_t dst_raw, uint32_t smac_lo, uint32_t smac_hi, uint32_t dmac_lo, uint32_t dmac_hi) {

@@ -32,7 +32,7 @@ enum EspStatus : uint32_t {
   kEspNoSa = 4,       // inbound: no SA for (src, dst, SPI): slow path
 };
 
-struct alignas(16) EspSa {       // 544 B
+struct alignas(16) EspSa {       // 4384 B
   uint32_t rk[60];               // AES round keys, big-endian words; 4 * (nr + 1) used
   uint32_t nr;                   // 10 (AES-128-GCM) / 14 (AES-256-GCM); 0 = empty slot
   uint32_t salt;                 // RFC 4106 salt: the 4 key-material bytes, raw (network order)
@@ -42,9 +42,10 @@ struct alignas(16) EspSa {       // 544 B
   uint32_t smac_lo, dmac_lo;     // tunnel mode outer MACs (raw bytes 0..3)
   uint16_t smac_hi, dmac_hi;
   uint32_t pad[3];
-  uint64_t htab[16][2];          // GHASH 4-bit table of H = E_K(0): (hi, lo) 64-bit halves
+  uint64_t htab[256][2];         // GHASH 8-bit table: byte b (as the block's first byte) times
+                                 // H = E_K(0), (hi, lo) 64-bit halves of the big-endian block
 };
-static_assert(sizeof(EspSa) == 544, "EspSa");
+static_assert(sizeof(EspSa) == 4384, "EspSa");
 
 // ipsec_spd + ipsec_tx_sa_classification: (dst IPv4, protocol) -> protect with SA / bypass / drop
 enum SpdAction : uint8_t { kSpdEmpty = 0, kSpdProtect = 1, kSpdBypass = 2, kSpdDrop = 3 };
@@ -77,7 +78,7 @@ NFDP_HD uint32_t rotr32(uint32_t x, int r) { return (x >> r) | (x << (32 - r)); 
 struct EspTables {
   const uint32_t* te0;   // [256] (2s, s, s, 3s) big-endian word of S-box byte s
   const uint8_t* sbox;   // [256]
-  const uint64_t* rem;   // [16] GHASH 4-bit reduction constants (<< 48)
+  const uint64_t* rem;   // [256] GHASH 8-bit reduction constants
 };
 
 // AES encryption of one block given as 4 big-endian words.
@@ -108,19 +109,18 @@ NFDP_HD void aes_block(const EspTables& tb, const uint32_t* rk, uint32_t nr, con
             ((uint32_t)sb[(s1 >> 8) & 0xFF] << 8) | sb[s2 & 0xFF]) ^ k[3];
 }
 
-// X = X * H in GF(2^128) (GCM bit order), X as (hi, lo) of the big-endian block; 4-bit table.
+// X = X * H in GF(2^128) (GCM bit order), X as (hi, lo) of the big-endian block; 8-bit table
+// (Shoup): one table entry and one reduction constant per byte, last byte first.
 NFDP_HD void ghash_mul(const EspTables& tb, const uint64_t (*ht)[2], uint64_t& xh, uint64_t& xl) {
   uint64_t zh = 0, zl = 0;
+#pragma unroll
   for (int cnt = 15; cnt >= 0; --cnt) {
     const uint32_t b = cnt >= 8 ? (uint32_t)(xl >> (8 * (15 - cnt))) & 0xFFu : (uint32_t)(xh >> (8 * (7 - cnt))) & 0xFFu;
-    for (int half = 0; half < 2; ++half) {
-      const uint32_t nib = half ? (b >> 4) : (b & 0xFu);
-      const uint32_t rem = (uint32_t)zl & 0xFu;
-      zl = (zh << 60) | (zl >> 4);
-      zh = (zh >> 4) ^ tb.rem[rem];
-      zh ^= ht[nib][0];
-      zl ^= ht[nib][1];
-    }
+    const uint32_t rem = (uint32_t)zl & 0xFFu;
+    zl = (zh << 56) | (zl >> 8);
+    zh = (zh >> 8) ^ tb.rem[rem];
+    zh ^= ht[b][0];
+    zl ^= ht[b][1];
   }
   xh = zh; xl = zl;
 }
@@ -153,20 +153,33 @@ NFDP_HD void gcm_run(const EspTables& tb, const EspSa& sa, uint32_t iv_hi, uint3
   uint64_t xh = 0, xl = 0;
   const uint32_t aad[4] = {sa.spi, seq, 0u, 0u};
   ghash_block(tb, sa.htab, xh, xl, aad);
-  for (uint32_t b = 0; 4 * b < nw; ++b) {
-    ctr[3] = 2u + b;
-    uint32_t ks[4];
-    aes_block(tb, sa.rk, sa.nr, ctr, ks);
-    uint32_t cbe[4] = {0u, 0u, 0u, 0u};
-    for (int q = 0; q < 4; ++q) {
-      const uint32_t j = 4 * b + q;
-      if (j >= nw) break;
-      const uint32_t in = src_word(j);
-      const uint32_t out = in ^ bswap32_(ks[q]);
-      st32(dst + 4 * j, out);
-      cbe[q] = bswap32_(enc ? out : in);
+  // 64-B groups (4 blocks): a lane's payload is read and written a whole cache line at a time,
+  // so the line is not evicted between its blocks while 64 lanes stream 64 different packets
+  for (uint32_t base = 0; base < nw; base += 16u) {
+    uint32_t w[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) w[q] = (base + q < nw) ? src_word(base + q) : 0u;
+#pragma unroll
+    for (int blk = 0; blk < 4; ++blk) {
+      const uint32_t j0 = base + 4u * blk;
+      if (j0 >= nw) break;
+      ctr[3] = 2u + j0 / 4u;
+      uint32_t ks[4];
+      aes_block(tb, sa.rk, sa.nr, ctr, ks);
+      uint32_t cbe[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if (j0 + q >= nw) break;
+        const uint32_t in = w[4 * blk + q];
+        const uint32_t out = in ^ bswap32_(ks[q]);
+        w[4 * blk + q] = out;
+        cbe[q] = bswap32_(enc ? out : in);
+      }
+      ghash_block(tb, sa.htab, xh, xl, cbe);
     }
-    ghash_block(tb, sa.htab, xh, xl, cbe);
+#pragma unroll
+    for (int q = 0; q < 16; ++q)
+      if (base + q < nw) st32(dst + 4 * (base + q), w[q]);
   }
   const uint32_t lens[4] = {0u, 64u, 0u, nw * 32u};   // len(AAD) = 64 bits || len(C) in bits
   ghash_block(tb, sa.htab, xh, xl, lens);

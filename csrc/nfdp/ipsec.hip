@@ -1,5 +1,5 @@
-// IPsec ESP (AES-GCM) kernels: one lane per packet, AES T-table + S-box + GHASH reduction
-// constants staged in LDS (1.4 KB per workgroup); per-SA round keys and GHASH tables are read
+// IPsec ESP (AES-GCM) kernels: one lane per packet, AES T-table + S-box + GHASH 8-bit reduction
+// constants staged in LDS (3.3 KB per workgroup); per-SA round keys and GHASH tables are read
 // through the vector L1 (a batch usually touches few SAs).  See ipsec.h for the frame layout.
 #include <hip/hip_runtime.h>
 
@@ -9,16 +9,17 @@
 namespace nfdp {
 
 constexpr int kEspBlock = 256;
+// Both held to 4 waves / SIMD (<= 128 VGPRs, no spills); profiles/r2_s25_esp_ab.txt, r2_s26_esp_ab.txt
 
 template <bool ENC>
-__global__ __launch_bounds__(kEspBlock) void esp_kernel(EspBatch a, const uint32_t* te0_g, const uint8_t* sbox_g,
+__global__ __launch_bounds__(kEspBlock, 4) void esp_kernel(EspBatch a, const uint32_t* te0_g, const uint8_t* sbox_g,
                                                         const uint64_t* rem_g) {
   __shared__ uint32_t te0[256];
   __shared__ uint8_t sbox[256];
-  __shared__ uint64_t rem[16];
+  __shared__ uint64_t rem[256];
   te0[threadIdx.x] = te0_g[threadIdx.x];
   sbox[threadIdx.x] = sbox_g[threadIdx.x];
-  if (threadIdx.x < 16) rem[threadIdx.x] = rem_g[threadIdx.x];
+  rem[threadIdx.x] = rem_g[threadIdx.x];
   __syncthreads();
   const EspTables tb{te0, sbox, rem};
   for (uint32_t i = blockIdx.x * kEspBlock + threadIdx.x; i < a.n; i += gridDim.x * kEspBlock) {

@@ -86,8 +86,8 @@ def test_known_answer_h_and_key_schedule():
     e = I.IpsecEngine()
     e.add_sa(0, key=bytes(16), salt=bytes(4), spi=1)
     w = e.sa[0].view(np.uint64)
-    # htab[8] = H = E_K(0) as (hi, lo); EspSa: rk 240 B, 8 words, pad 12 B -> htab at byte 288
-    hi, lo = int(w[288 // 8 + 16]), int(w[288 // 8 + 17])
+    # htab[0x80] = H = E_K(0) as (hi, lo); EspSa: rk 240 B, 8 words, pad 12 B -> htab at byte 288
+    hi, lo = int(w[(288 + 0x80 * 16) // 8]), int(w[(288 + 0x80 * 16) // 8 + 1])
     assert f"{hi:016x}{lo:016x}" == "66e94bd4ef8a2c3b884cfa59ca342b2e"
 
 
