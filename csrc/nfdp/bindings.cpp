@@ -656,7 +656,7 @@ PYBIND11_MODULE(_nfdp, m) {
   m.attr("ESP_OFF") = kEspOff;
   m.def("esp_tables", []() {
     const EspTables t = esp_host_tables();
-    return py::make_tuple(py::bytes(reinterpret_cast<const char*>(t.te0), 1024),
+    return py::make_tuple(py::bytes(reinterpret_cast<const char*>(t.te0), 4096),
                           py::bytes(reinterpret_cast<const char*>(t.sbox), 256),
                           py::bytes(reinterpret_cast<const char*>(t.rem), 2048));
   });

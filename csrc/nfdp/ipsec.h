@@ -74,9 +74,14 @@ NFDP_HD uint32_t bswap32_(uint32_t x) {
 }
 NFDP_HD uint32_t rotr32(uint32_t x, int r) { return (x >> r) | (x << (32 - r)); }
 
+#ifndef NFDP_ESP_TTABLES4
+#define NFDP_ESP_TTABLES4 1   // four T-tables (4 KB of LDS) instead of Te0 + rotations
+#endif
+
 // Table access (LDS on the GPU, plain arrays on the host).
 struct EspTables {
-  const uint32_t* te0;   // [256] (2s, s, s, 3s) big-endian word of S-box byte s
+  const uint32_t* te0;   // [256] (2s, s, s, 3s) big-endian word of S-box byte s; with
+                         // NFDP_ESP_TTABLES4 [4][256]: Te0 and its byte rotations Te1..Te3
   const uint8_t* sbox;   // [256]
   const uint64_t* rem;   // [256] GHASH 8-bit reduction constants
 };
@@ -87,6 +92,13 @@ NFDP_HD void aes_block(const EspTables& tb, const uint32_t* rk, uint32_t nr, con
   const uint32_t* te = tb.te0;
   for (uint32_t r = 1; r < nr; ++r) {
     const uint32_t* k = rk + 4 * r;
+#if NFDP_ESP_TTABLES4
+    const uint32_t *e1 = te + 256, *e2 = te + 512, *e3 = te + 768;
+    const uint32_t t0 = te[s0 >> 24] ^ e1[(s1 >> 16) & 0xFF] ^ e2[(s2 >> 8) & 0xFF] ^ e3[s3 & 0xFF] ^ k[0];
+    const uint32_t t1 = te[s1 >> 24] ^ e1[(s2 >> 16) & 0xFF] ^ e2[(s3 >> 8) & 0xFF] ^ e3[s0 & 0xFF] ^ k[1];
+    const uint32_t t2 = te[s2 >> 24] ^ e1[(s3 >> 16) & 0xFF] ^ e2[(s0 >> 8) & 0xFF] ^ e3[s1 & 0xFF] ^ k[2];
+    const uint32_t t3 = te[s3 >> 24] ^ e1[(s0 >> 16) & 0xFF] ^ e2[(s1 >> 8) & 0xFF] ^ e3[s2 & 0xFF] ^ k[3];
+#else
     const uint32_t t0 = te[s0 >> 24] ^ rotr32(te[(s1 >> 16) & 0xFF], 8) ^ rotr32(te[(s2 >> 8) & 0xFF], 16) ^
                         rotr32(te[s3 & 0xFF], 24) ^ k[0];
     const uint32_t t1 = te[s1 >> 24] ^ rotr32(te[(s2 >> 16) & 0xFF], 8) ^ rotr32(te[(s3 >> 8) & 0xFF], 16) ^
@@ -95,6 +107,7 @@ NFDP_HD void aes_block(const EspTables& tb, const uint32_t* rk, uint32_t nr, con
                         rotr32(te[s1 & 0xFF], 24) ^ k[2];
     const uint32_t t3 = te[s3 >> 24] ^ rotr32(te[(s0 >> 16) & 0xFF], 8) ^ rotr32(te[(s1 >> 8) & 0xFF], 16) ^
                         rotr32(te[s2 & 0xFF], 24) ^ k[3];
+#endif
     s0 = t0; s1 = t1; s2 = t2; s3 = t3;
   }
   const uint8_t* sb = tb.sbox;

@@ -14,10 +14,10 @@ constexpr int kEspBlock = 256;
 template <bool ENC>
 __global__ __launch_bounds__(kEspBlock, 4) void esp_kernel(EspBatch a, const uint32_t* te0_g, const uint8_t* sbox_g,
                                                         const uint64_t* rem_g) {
-  __shared__ uint32_t te0[256];
+  __shared__ uint32_t te0[NFDP_ESP_TTABLES4 ? 1024 : 256];
   __shared__ uint8_t sbox[256];
   __shared__ uint64_t rem[256];
-  te0[threadIdx.x] = te0_g[threadIdx.x];
+  for (int k = threadIdx.x; k < (NFDP_ESP_TTABLES4 ? 1024 : 256); k += kEspBlock) te0[k] = te0_g[k];
   sbox[threadIdx.x] = sbox_g[threadIdx.x];
   rem[threadIdx.x] = rem_g[threadIdx.x];
   __syncthreads();
