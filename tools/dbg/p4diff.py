@@ -1,19 +1,30 @@
-import sys, numpy as np, torch
+"""Debug: which rows / byte positions of the P4-feature trace differ between the GPU kernel
+(whatever NFDP_EXT_DIR selects) and the oracle."""
+import sys
+
+import numpy as np
+import torch
+
 sys.path.insert(0, ".")
 sys.path.insert(0, "tests")
-from test_dataplane_gpu import _p4_plane, _p4_traffic
-from dpu_operator_amd.ops import packets as P
-cpu, sc, vfs = _p4_plane("cpu")
-gpu, _, _ = _p4_plane("cuda")
-pk, im = _p4_traffic(sc, vfs)
+import test_dataplane_gpu as T  # noqa: E402
+
+cpu, sc, vfs = T._p4_plane("cpu")
+gpu, _, _ = T._p4_plane("cuda")
+pk, im = T._p4_traffic(sc, vfs)
 rc = cpu.run(pk, im)
 rg = gpu.run(torch.from_numpy(pk).cuda(), torch.from_numpy(im.view(np.int32)).cuda())
 torch.cuda.synchronize()
 og = rg.out.cpu().numpy()
-bad = np.where((og != rc.out).any(1))[0]
-print("nbad", len(bad), "of", len(pk))
-for i in bad[:6]:
-    print(i, P.meta_fields(rc.meta[i:i+1]), "in", pk[i][:20].tobytes().hex())
-    print(" cpu", rc.out[i].tobytes().hex())
-    print(" gpu", og[i].tobytes().hex())
+bad = np.nonzero((og != rc.out).any(axis=1))[0]
+print("rows differ:", len(bad), "of", len(og))
+if len(bad):
+    cols = np.nonzero((og[bad] != rc.out[bad]).any(axis=0))[0]
+    print("byte columns:", cols.tolist())
+    print("rows mod 64:", np.bincount(bad % 64, minlength=64).tolist())
+    print("rows // 1024 (block):", np.bincount(bad // 1024).tolist())
+    for r in bad[:4]:
+        print(r, "in ", pk[r].tobytes().hex())
+        print(r, "cpu", rc.out[r].tobytes().hex())
+        print(r, "gpu", og[r].tobytes().hex())
 print("side cpu", cpu.side_result()["n_rep"], "gpu", gpu.side_result()["n_rep"])
