@@ -207,3 +207,51 @@ def test_ipsec_boundary_on_the_uplink():
         live.stop()
         for p in ports.values():
             p.close()
+
+
+def test_ipv6_underlay_tunnel_through_the_live_path():
+    """Pod -> IPv6-underlay VXLAN tunnel port -> underlay netdev carries the 70-B outer header; the
+    reply arriving on the underlay is recognised by the kernel (recirc6), resolved on the whole
+    frame (the VNI lies past the header slot) and re-enters on the tunnel port, bridged to the pod."""
+    import ipaddress
+
+    dp = DataPlane(device="cpu", flow_buckets=1 << 10)
+    dp.ports.set(1, flags=T.PORT_VALID, bridge_id=BR)
+    dp.ports.set(21, flags=T.PORT_VALID | T.PORT_TUNNEL | T.PORT_TUNNEL6, bridge_id=BR)
+    dp.ports.a[21]["lag"] = 0
+    dp.ports.set(30, flags=T.PORT_VALID | T.PORT_VTEP)
+    dp.tunnels6.set(0, src="2001:db8:f::1", dst="2001:db8:f::2", vni=7000, out_port=30, smac=MACS[2], dmac=MACS[3])
+    dp.vtep6.set("2001:db8:f::1")
+    dp.terms6.insert("2001:db8:f::2", 7000, 21)
+    dp.macs.insert(BR, MACS[1], 21)
+    dp.macs.insert(BR, MACS[0], 1)
+    dp.commit(full=True)
+    ports = {1: SockPort(), 30: SockPort()}
+    live = LivePath(dp, ports)
+    try:
+        f = _frame(MACS[1], MACS[0], 300, 1)
+        ports[1].inject(f)
+        for _ in range(10):
+            if live.poll_once(0.05):
+                break
+        out = ports[30].drain()
+        assert len(out) == 1 and out[0][12:14] == b"\x86\xdd" and out[0][70:] == f
+        # the remote VTEP's reply: outer addresses swapped, inner MACs swapped
+        b = bytearray(out[0])
+        b[22:38], b[38:54] = out[0][38:54], out[0][22:38]
+        inner = bytearray(b[70:])
+        inner[0:6], inner[6:12] = inner[6:12], inner[0:6]
+        b[70:] = inner
+        ports[30].inject(bytes(b))
+        got = []
+        for _ in range(10):
+            live.poll_once(0.05)
+            got += ports[1].drain()
+            if got:
+                break
+        assert got == [bytes(inner)] and live.stats["recirc"] == 1
+        assert ipaddress.IPv6Address(bytes(b[22:38])) == ipaddress.IPv6Address("2001:db8:f::2")
+    finally:
+        live.stop()
+        for p in ports.values():
+            p.close()
