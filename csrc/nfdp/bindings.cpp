@@ -71,6 +71,9 @@ TablesView tables_from(const py::dict& d) {
   t.terms = ptr<const TermEntry>(d, "terms");
   t.term_mask = t.terms ? val<uint32_t>(d, "term_mask", 0) : 0u;
   if (t.terms && ((t.term_mask + 1) & t.term_mask)) throw std::invalid_argument("term table size must be a power of two");
+  t.vmmac = ptr<const VmMacEntry>(d, "vmmac");
+  t.vmmac_mask = t.vmmac ? val<uint32_t>(d, "vmmac_mask", 0) : 0u;
+  if (t.vmmac && ((t.vmmac_mask + 1) & t.vmmac_mask)) throw std::invalid_argument("vmmac table size must be a power of two");
   if (t.n_lag_groups && !t.lag_members) throw std::invalid_argument("n_lag_groups > 0 but lag_members missing");
   if (!t.ports || !t.chains || !t.flows || !t.rss_key)
     throw std::invalid_argument("tables dict is missing a required buffer");

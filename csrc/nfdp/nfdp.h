@@ -217,6 +217,17 @@ struct alignas(16) TermEntry {   // 16 B: (outer src ip, vni) -> tunnel port (ip
   uint32_t pad;
 };
 static_assert(sizeof(TermEntry) == 16, "TermEntry");
+// VM IPv4 -> MAC maps (P4 vm_src_ip4_mac_map_table / vm_dst_ip4_mac_map_table): a routed
+// packet from a mapped source gets that source MAC, one to a mapped destination that
+// destination MAC.  Open addressing over (ip, kind); kind 0 = empty slot.
+constexpr uint32_t kVmMacSrc = 1, kVmMacDst = 2;
+struct alignas(16) VmMacEntry {  // 16 B
+  uint32_t ip;                   // raw (network byte order as loaded)
+  uint32_t kind;                 // kVmMacSrc | kVmMacDst, 0 = empty
+  uint32_t mac_lo, mac_hi;       // set_smac / set_dmac operands
+};
+static_assert(sizeof(VmMacEntry) == 16, "VmMacEntry");
+constexpr int kVmMacProbe = 8;
 
 // Verdict returned by the flow owner to the ingress GPU (multi-GPU path).
 struct alignas(16) Verdict {     // 16 B
@@ -520,6 +531,8 @@ struct TablesView {
   uint32_t vtep6_fold;           // vtep6_fold() of the local IPv6 VTEP address (0: no IPv6 VTEP)
   const TermEntry* terms;        // term_mask + 1 slots, open addressing (nullable)
   uint32_t term_mask;
+  const VmMacEntry* vmmac;       // vmmac_mask + 1 slots, open addressing (nullable: no VM MAC maps)
+  uint32_t vmmac_mask;
   // IPv6 FIB (P4 ipv6_table): one open-addressing table over (prefix, length) and the distinct
   // prefix lengths present, longest first; a lookup probes the lengths in that order
   const Lpm6Entry* lpm6;         // lpm6_mask + 1 slots (nullable: no IPv6 routes)
@@ -571,6 +584,19 @@ NFDP_HD uint32_t lpm6_lookup(const TablesView& t, uint32_t d0, uint32_t d1, uint
     }
   }
   return 0;
+}
+
+NFDP_HD uint32_t vmmac_hash(uint32_t ip, uint32_t kind) { return fmix32(ip ^ (kind * 0x85EBCA77u)); }
+// (raw IPv4, kind) -> slot or -1
+NFDP_HD int vmmac_lookup(const TablesView& t, uint32_t ip, uint32_t kind) {
+  const uint32_t h = vmmac_hash(ip, kind);
+  for (int q = 0; q < kVmMacProbe; ++q) {
+    const uint32_t i = (h + (uint32_t)q) & t.vmmac_mask;
+    const VmMacEntry& e = t.vmmac[i];
+    if (!e.kind) return -1;
+    if (e.ip == ip && e.kind == kind) return (int)i;
+  }
+  return -1;
 }
 
 NFDP_HD int term_lookup(const TablesView& t, uint32_t src_ip, uint32_t vni) {

@@ -134,7 +134,8 @@ NFDP_HD uint32_t finish_port(const TablesView& t, const TA& ta, uint32_t& port, 
 
 // IPv4 routing on the normalized frame (P4 ipv4_table LPM -> ecmp_hash_table -> nexthop_table,
 // rif_mod_table for the source MAC): TTL - 1 with the checksum update, neighbour / router MACs,
-// egress port.  Returns a drop reason (0 = routed, e.out_port set).
+// egress port.  Returns a drop reason (0 = routed, e.out_port set).  The
+// vm_{src,dst}_ip4_mac_map_table overrides follow in chain_stage (vm_mac_map).
 NFDP_HD uint32_t route_ipv4(const TablesView& t, Parsed& p, uint32_t hash, uint32_t& out_port) {
   if (!p.ipv4) return kNoRoute;
   const uint32_t dst = __builtin_bswap32(raw32_at2(p.s, 30));
@@ -147,6 +148,18 @@ NFDP_HD uint32_t route_ipv4(const TablesView& t, Parsed& p, uint32_t hash, uint3
   set_smac(p.s, n.smac_lo, n.smac_hi);
   out_port = n.port;
   return kOk;
+}
+
+// VM IPv4 -> MAC overrides of a routed IPv4 packet (P4 vm_src_ip4_mac_map_table /
+// vm_dst_ip4_mac_map_table).  One call site per kernel (chain_stage's tail) keeps it to one
+// inlined copy; callers test t.vmmac (wave-uniform) first.
+NFDP_HD void vm_mac_map(const TablesView& t, Parsed& p) {
+  for (uint32_t kind = kVmMacSrc; kind <= kVmMacDst; ++kind) {
+    const int i = vmmac_lookup(t, raw32_at2(p.s, kind == kVmMacSrc ? 26 : 30), kind);
+    if (i < 0) continue;
+    const VmMacEntry m = t.vmmac[i];
+    if (kind == kVmMacSrc) set_smac(p.s, m.mac_lo, m.mac_hi); else set_dmac(p.s, m.mac_lo, m.mac_hi);
+  }
 }
 
 // IPv6 routing (P4 ipv6_table): LPM on the destination, hop limit - 1 (no header checksum in
@@ -223,6 +236,7 @@ NFDP_HD EgressDecision chain_stage(const TablesView& t, const TA& ta, Parsed& p,
         const uint32_t r = p.ipv6 ? route_ipv6(t, p, op) : route_ipv4(t, p, hash, op);
         if (r) { e.reason = r; e.out_port = r == kNoRoute ? kPortPunt : kPortNone; return e; }
         e.out_port = op;
+        if (t.vmmac && p.ipv4) vm_mac_map(t, p);
         const uint32_t r2 = finish_port(t, ta, e.out_port, hash, false, e.push, e.tci, p.len, &e.xhdr);
         if (r2) { e.reason = r2; e.out_port = kPortNone; e.xhdr = 0; return e; }
         e.mirror = (st.in_flags & kPortMirror) ? 1u : 0u;

@@ -72,6 +72,7 @@ class DataPlane:
         self.ecmp = T.EcmpTable()
         self.tunnels = T.TunnelTable()
         self.terms = T.TermTable()
+        self.vmmac = T.VmMacTable()
         self.tunnels6 = T.Tunnel6Table()
         self.vtep6 = T.Vtep6()
         self.terms6 = T.Term6Table()     # host side: finished by resolve_recirc6 on the whole frame
@@ -173,7 +174,8 @@ class DataPlane:
     def _models(self):
         return (("ports", self.ports), ("chains", self.chains), ("macs", self.macs), ("lag", self.lag),
                 ("flood", self.flood), ("nexthops", self.nexthops), ("ecmp", self.ecmp),
-                ("tunnels", self.tunnels), ("terms", self.terms), ("tunnels6", self.tunnels6),
+                ("tunnels", self.tunnels), ("terms", self.terms), ("vmmac", self.vmmac),
+                ("tunnels6", self.tunnels6),
                 ("vtep6", self.vtep6))   # vtep6: a kernarg fold, listed for the version tracking
 
     def _only_flows_pending(self) -> bool:
@@ -329,6 +331,7 @@ class DataPlane:
             "ecmp": self._ptr("ecmp"), "n_ecmp": int(self.ecmp.n),
             "tunnels": self._ptr("tunnels") if self.tunnels.n else 0, "n_tunnels": int(self.tunnels.n),
             "terms": self._ptr("terms") if self.terms.n else 0, "term_mask": int(self.terms.mask),
+            "vmmac": self._ptr("vmmac") if self.vmmac.n else 0, "vmmac_mask": int(self.vmmac.mask),
             "lpm6": self._ptr("lpm6") if len(self.routes6) else 0,
             "lpm6_mask": int(getattr(self, "_lpm6", (0, 0))[0]),
             "lpm6_lens": self._ptr("lpm6_lens") if len(self.routes6) else 0,

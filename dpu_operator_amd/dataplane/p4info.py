@@ -276,8 +276,18 @@ TABLES = [
     # the compiled pipeline names both key fields hdrs.inval.data (p4info.txt:168-190): values bind in order
     ("always_trap_arp_table", [("hdrs.inval.data", 16, "EXACT"), ("hdrs.inval.data", 16, "EXACT")],
      ["do_trap_enable"], 1024),
+    # RX recirculation (p4info.txt:189-212, const default do_recirculate, 0 SEM slots in the
+    # compiled pipeline): the GPU pipeline recirculates terminated tunnel traffic by itself, so
+    # entries are accepted and change nothing
+    ("always_recirculate_table", [("hdrs.inval.data", 16, "EXACT"), ("hdrs.inval.data", 16, "EXACT")],
+     ["do_recirculate"], 1024),
+    # VM IPv4 -> MAC maps (p4info.txt:1393-1440): routed packets' source / destination MAC
+    ("vm_src_ip4_mac_map_table", [("ipv4_src", 32, "EXACT")], ["vm_src_ip4_mac_map_action", "NoAction"], 1024),
+    ("vm_dst_ip4_mac_map_table", [("ipv4_dst", 32, "EXACT")], ["vm_dst_ip4_mac_map_action", "NoAction"], 1024),
 ]
 ACTIONS = {
+    "vm_src_ip4_mac_map_action": [("smac_high", 16), ("smac_mid", 16), ("smac_low", 16)],
+    "vm_dst_ip4_mac_map_action": [("dmac_high", 16), ("dmac_mid", 16), ("dmac_low", 16)],
     "set_source_port": [("source_port", 16)],
     "l2_fwd_and_bypass_bridge": [("port", 32)],
     "fwd_to_vsi": [("port", 32)],

@@ -536,7 +536,8 @@ class P4Runtime:
     def _compile_l3_tunnels(self, dp, port, add_mac, src: dict) -> None:
         """L3 (ipv4_table, ipv6_table, ecmp_hash_table, nexthop / ecmp_nexthop tables, rif_mod_table_*), tunnels
         (l2_to_tunnel_v4, *_encap_mod_table, ipv4_tunnel_term_table, rx_ipv4_tunnel_source_port),
-        rx_lag_table, l2_fwd_smac_table and always_trap_arp_table onto the GPU tables."""
+        vm_{src,dst}_ip4_mac_map_table, rx_lag_table, l2_fwd_smac_table and always_trap_arp_table onto
+        the GPU tables."""
         for cidr in self._owned_routes:
             (dp.routes6 if ":" in cidr else dp.routes).remove(cidr)
         self._owned_routes = []
@@ -601,6 +602,16 @@ class P4Runtime:
             else:
                 continue
             self._owned_routes.append(cidr)
+        # VM IPv4 -> MAC maps: overrides applied to routed IPv4 after the nexthop's MACs
+        vm_rows = [(kind, e) for kind, tab in ((T.VMMAC_SRC, "vm_src_ip4_mac_map"), (T.VMMAC_DST, "vm_dst_ip4_mac_map"))
+                   for e in self._rows(f"{tab}_table") if e.action.endswith(f"{tab}_action")]
+        if vm_rows or getattr(self, "_owned_vmmac", False):
+            dp.vmmac.clear()
+            for kind, e in vm_rows:
+                x = "smac" if kind == T.VMMAC_SRC else "dmac"
+                v = (e.params[f"{x}_high"] << 32) | (e.params[f"{x}_mid"] << 16) | e.params[f"{x}_low"]
+                dp.vmmac.set(str(ipaddress.IPv4Address(e.key[0][1])), kind, mac_of(v))
+        self._owned_vmmac = bool(vm_rows)
         for g in groups:
             for h in range(T.ECMP_WAYS):
                 for e in self._rows("ecmp_hash_table"):  # highest priority first

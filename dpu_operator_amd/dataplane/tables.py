@@ -82,6 +82,8 @@ TUNNEL_DTYPE = np.dtype([("src_ip", "<u4"), ("dst_ip", "<u4"), ("sport", "<u2"),
                          ("smac_lo", "<u4"), ("smac_hi", "<u2"), ("out_port", "<u2"), ("dmac_lo", "<u4"),
                          ("dmac_hi", "<u2"), ("type", "<u2")])
 TERM_DTYPE = np.dtype([("src_ip", "<u4"), ("vni", "<u4"), ("port", "<u2"), ("valid", "<u2"), ("pad", "<u4")])
+VMMAC_DTYPE = np.dtype([("ip", "<u4"), ("kind", "<u4"), ("mac_lo", "<u4"), ("mac_hi", "<u4")])   # nfdp.h VmMacEntry
+VMMAC_SRC, VMMAC_DST = 1, 2
 TUNNEL6_DTYPE = np.dtype([("src", "<u4", (4,)), ("dst", "<u4", (4,)), ("sport", "<u2"), ("dport", "<u2"), ("vni", "<u4"),
                           ("smac_lo", "<u4"), ("smac_hi", "<u2"), ("out_port", "<u2"), ("dmac_lo", "<u4"),
                           ("dmac_hi", "<u2"), ("type", "<u2"), ("tc_flow", "<u4"), ("hop_limit", "<u4")])
@@ -535,6 +537,62 @@ class TermTable:
                 self.version += 1
                 return
         raise RuntimeError("term table probe limit reached")
+
+
+class VmMacTable:
+    """VM IPv4 -> MAC maps (P4 vm_src_ip4_mac_map_table / vm_dst_ip4_mac_map_table): a routed
+    packet from a mapped source IP leaves with that MAC as its source MAC, one to a mapped
+    destination IP with that MAC as its destination MAC (nfdp.h vmmac_lookup, applied in
+    pipeline.h route_ipv4 after the nexthop's MACs).  Open addressing over (ip, kind)."""
+
+    PROBE = 8
+
+    def __init__(self, slots: int = 4096):
+        if slots & (slots - 1):
+            raise ValueError("vmmac table size must be a power of two")
+        self.a = np.zeros(slots, VMMAC_DTYPE)
+        self.mask = slots - 1
+        self.n = 0
+        self.version = 0
+
+    @staticmethod
+    def _hash(raw: int, kind: int) -> int:
+        with np.errstate(over="ignore"):
+            return int(fmix32(np.uint32(raw) ^ (np.uint32(kind) * np.uint32(0x85EBCA77))))
+
+    def set(self, ip, kind: int, mac) -> None:
+        if kind not in (VMMAC_SRC, VMMAC_DST):
+            raise ValueError("kind must be VMMAC_SRC or VMMAC_DST")
+        raw = int(ip_raw(np.uint32(ip_to_int(ip))))
+        lo, hi = mac_raw(mac)
+        h = self._hash(raw, kind)
+        for q in range(self.PROBE):
+            i = (h + q) & self.mask
+            was = int(self.a[i]["kind"])
+            if not was or (self.a[i]["ip"] == raw and was == kind):
+                self.a[i] = (raw, kind, lo, hi)
+                self.n += 0 if was else 1
+                self.version += 1
+                return
+        raise RuntimeError("vmmac table probe limit reached")
+
+    def clear(self) -> None:
+        if self.n:
+            self.a[:] = np.zeros((), VMMAC_DTYPE)
+            self.n = 0
+            self.version += 1
+
+    def lookup(self, ip, kind: int):
+        """(mac_lo, mac_hi) or None (host-side twin of vmmac_lookup)."""
+        raw = int(ip_raw(np.uint32(ip_to_int(ip))))
+        h = self._hash(raw, kind)
+        for q in range(self.PROBE):
+            e = self.a[(h + q) & self.mask]
+            if not e["kind"]:
+                return None
+            if e["ip"] == raw and e["kind"] == kind:
+                return int(e["mac_lo"]), int(e["mac_hi"])
+        return None
 
 
 class FloodTable:

@@ -17,8 +17,17 @@ RMAC = ["02:40:00:00:00:0a", "02:40:00:00:00:0b", "02:40:00:00:00:0c", "02:40:00
 NBR = ["02:50:00:00:00:0a", "02:50:00:00:00:0b", "02:50:00:00:00:0c", "02:50:00:00:00:0d"]
 
 
-def _router(device):
+VM_DST = {"10.1.2.5": "02:66:00:00:00:05", "10.1.2.200": "02:66:00:00:00:c8"}   # vm_dst_ip4_mac_map
+VM_SRC = {"10.9.0.1": "02:77:00:00:00:01"}                                        # vm_src_ip4_mac_map
+
+
+def _router(device, vmmac=False):
     dp = DataPlane(device=device, flow_buckets=1 << 10)
+    if vmmac:
+        for ip, mac in VM_DST.items():
+            dp.vmmac.set(ip, T.VMMAC_DST, mac)
+        for ip, mac in VM_SRC.items():
+            dp.vmmac.set(ip, T.VMMAC_SRC, mac)
     for i in range(4):
         dp.ports.set(10 + i, flags=T.PORT_VALID | T.PORT_ROUTED, mac=RMAC[i], bridge_id=20 + i)
         dp.nexthops.set(i + 1, 10 + i, dmac=NBR[i], smac=RMAC[i])
@@ -80,6 +89,27 @@ def test_routing_oracle_model():
     ecmp_nh = {int(dp.ecmp.a[(int(h[i]) & 7)]) for i in range(len(dsts))
                if ttl[i] != 1 and dp.routes.lookup(int(dsts[i])) & T.ROUTE_ECMP}
     assert ecmp_nh == {2, 3}  # both ECMP members used
+
+
+def test_vm_mac_maps_oracle_model():
+    """VM IPv4 -> MAC maps on routed traffic: mapped destinations get the map's dmac, the mapped
+    source (every packet of the trace) the map's smac; port, TTL and checksums as without maps."""
+    dp = _router("cpu", vmmac=True)
+    slots, im, frames, lens, dsts, ttl = _l3_trace()
+    r = dp.run(slots, im)
+    port, olen, reason = P.meta_fields(r.meta)
+    for i in range(len(dsts)):
+        if ttl[i] == 1:
+            continue
+        assert reason[i] == 0
+        o = P.assemble(r.out[i], int(r.meta[i]), frames[i], int(lens[i]))
+        d = str(ipaddress.IPv4Address(int(dsts[i])))
+        if d in VM_DST:
+            assert o[0:6] == bytes.fromhex(VM_DST[d].replace(":", ""))
+        else:
+            assert o[0:6] == bytes.fromhex(NBR[int(port[i]) - 10].replace(":", ""))
+        assert o[6:12] == bytes.fromhex(VM_SRC["10.9.0.1"].replace(":", ""))
+        assert P.check_csums(np.frombuffer(o, np.uint8)[None], np.array([len(o)]))[0]
 
 
 def test_route_hop_in_a_chain_and_no_route():
@@ -206,10 +236,11 @@ def test_unknown_vni_is_not_terminated():
 
 
 @pytest.mark.gpu
-def test_routing_gpu_bit_exact():
+@pytest.mark.parametrize("vmmac", [False, True])
+def test_routing_gpu_bit_exact(vmmac):
     import torch
 
-    c, g = _router("cpu"), _router("cuda")
+    c, g = _router("cpu", vmmac), _router("cuda", vmmac)
     slots, im, *_ = _l3_trace(4096, seed=3)
     rc = c.run(slots, im)
     rg = g.run(torch.from_numpy(slots).cuda(), torch.from_numpy(im.view(np.int32)).cuda())

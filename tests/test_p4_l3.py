@@ -219,3 +219,76 @@ def test_keyless_lem_tables_accept_noaction(rt):
         with pytest.raises(P4Error):
             rt.add_entry(C + t, "action=linux_networking_control.NoAction()")
     assert (rt.dp.ports.a == before).all()
+
+
+def _l3_one_nexthop(rt):
+    add = rt.add_entry
+    for part, v in (("start", 0x0240), ("mid", 0x0000), ("last", 0x0001)):
+        add(C + f"rif_mod_table_{part}", f"rif_mod_map_id{('start', 'mid', 'last').index(part)}=5,"
+            f"action=linux_networking_control.set_src_mac_{part}({v:#06x})")
+    add(C + "nexthop_table", "user_meta.cmeta.nexthop_id=1,bit16_zeros=0,"
+        "action=linux_networking_control.set_nexthop_info_dmac(5,1,0x0250,0x00000001)")
+    add(C + "ipv4_table", "ipv4_table_lpm_root=0,ipv4_dst_match=10.20.0.0/16,"
+        "action=linux_networking_control.ipv4_set_nexthop_id(1)")
+    rt.dp.ports.set(PHY_BASE + 1, flags=T.PORT_VALID | T.PORT_ROUTED, mac="02:40:00:00:00:01")
+
+
+def test_vm_ip4_mac_map_tables_rewrite_routed_macs(rt):
+    """vm_dst_ip4_mac_map_table / vm_src_ip4_mac_map_table (p4info.txt:1393-1440): a routed packet
+    to a mapped destination leaves with the mapped dmac instead of the nexthop's, one from a
+    mapped source with the mapped smac instead of the router interface's; others are unchanged.
+    Expected bytes are written out by hand here (independent of the oracle)."""
+    dp = rt.dp
+    _l3_one_nexthop(rt)
+    rt.add_entry(C + "vm_dst_ip4_mac_map_table", "ipv4_dst=10.20.7.7,"
+                 "action=linux_networking_control.vm_dst_ip4_mac_map_action(0x0266,0x7788,0x99aa)")
+    rt.add_entry(C + "vm_src_ip4_mac_map_table", "ipv4_src=10.0.0.1,"
+                 "action=linux_networking_control.vm_src_ip4_mac_map_action(0x02ab,0xcdef,0x0102)")
+    assert dp.vmmac.n == 2
+    op, rs, out = _send(dp, PHY_BASE + 1, "02:40:00:00:00:01", "10.20.7.7")   # src 10.0.0.1 (mapped)
+    assert (op, rs) == (PHY_BASE + 1, 0)
+    assert bytes(out[0:6]) == bytes.fromhex("0266778899aa")
+    assert bytes(out[6:12]) == bytes.fromhex("02abcdef0102") and out[22] == 63
+    op, rs, out = _send(dp, PHY_BASE + 1, "02:40:00:00:00:01", "10.20.7.8")   # unmapped destination
+    assert bytes(out[0:6]) == bytes.fromhex("025000000001") and bytes(out[6:12]) == bytes.fromhex("02abcdef0102")
+    rt.del_entry(C + "vm_src_ip4_mac_map_table", "ipv4_src=10.0.0.1")
+    op, rs, out = _send(dp, PHY_BASE + 1, "02:40:00:00:00:01", "10.20.7.7")
+    assert bytes(out[0:6]) == bytes.fromhex("0266778899aa") and bytes(out[6:12]) == bytes.fromhex("024000000001")
+    rt.del_entry(C + "vm_dst_ip4_mac_map_table", "ipv4_dst=10.20.7.7")
+    assert dp.vmmac.n == 0 and dp.tables_ptrs()["vmmac"] == 0
+    op, rs, out = _send(dp, PHY_BASE + 1, "02:40:00:00:00:01", "10.20.7.7")
+    assert bytes(out[0:6]) == bytes.fromhex("025000000001")
+
+
+def test_vmmac_table_probe_and_twin():
+    t = T.VmMacTable(slots=16)
+    for k in range(10):
+        t.set(f"10.1.0.{k}", T.VMMAC_DST, f"02:00:00:00:01:{k:02x}")
+    t.set("10.1.0.3", T.VMMAC_SRC, "02:00:00:00:02:03")
+    t.set("10.1.0.3", T.VMMAC_DST, "02:00:00:00:03:03")   # overwrite in place
+    assert t.n == 11
+    assert t.lookup("10.1.0.3", T.VMMAC_DST) == T.mac_raw("02:00:00:00:03:03")
+    assert t.lookup("10.1.0.3", T.VMMAC_SRC) == T.mac_raw("02:00:00:00:02:03")
+    assert t.lookup("10.1.0.99", T.VMMAC_SRC) is None
+    with pytest.raises(ValueError):
+        t.set("10.1.0.1", 3, "02:00:00:00:00:01")
+
+
+def test_always_recirculate_table_accepts_entries(rt):
+    before = rt.dp.ports.a.copy()
+    rt.add_entry(C + "always_recirculate_table", "hdrs.inval.data=1,hdrs.inval.data=0,"
+                 "action=linux_networking_control.do_recirculate()")
+    assert (rt.dp.ports.a == before).all()
+
+
+def test_all_reference_tables_compiled():
+    """Every table of the reference's linux_networking p4info has a definition here."""
+    from dpu_operator_amd.dataplane.p4info import TABLES, P4Info
+
+    from test_p4 import REF_P4INFO
+
+    if not REF_P4INFO.exists():
+        pytest.skip("reference P4Info not mounted")
+    ref = P4Info.from_text(REF_P4INFO.read_text())
+    names = {t.name.split(".")[-1] for t in ref.tables.values()}
+    assert names <= {t[0].split(".")[-1] for t in TABLES} and len(names) == 55
