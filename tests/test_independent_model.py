@@ -1,4 +1,4 @@
-"""An independent model of the bench's headline pipeline, checked against the C++ oracle byte for byte.
+"""An independent model of the bench's headline pipeline, checked byte for byte against the C++ oracle and the GPU.
 
 The GPU tests hold the HIP kernels to the oracle bit-exactly, but the oracle shares the per-packet
 stages (pipeline.h / nfdp.h) with the kernels, so a semantic bug in a shared stage would pass them.
@@ -10,10 +10,11 @@ the key words read straight from the frame bytes, checksums are recomputed from 
 incremental update).  Traffic is the bench's mixed trace (flow misses, ACL denies, malformed
 lengths) so every disposition of the headline path is exercised.
 
-Transitively this validates the GPU: tests/test_dataplane_gpu.py holds the kernels bit-exact to
-the oracle on the same scenario.
+The cuda variant holds the HIP kernels (MFMA Toeplitz hash, FP4-MFMA ACL, wave-cooperative probe)
+to the same model directly.
 """
 import numpy as np
+import pytest
 
 from dpu_operator_amd.dataplane import scenario as S
 from dpu_operator_amd.dataplane import tables as T
@@ -78,14 +79,24 @@ def _model(frame: bytes, in_port: int, ln: int, sc, flows: dict, acl, default_pe
     return OK, out_port, out
 
 
-def test_headline_pipeline_matches_independent_model():
-    dp = DataPlane(device="cpu", flow_buckets=1 << 14)
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+def test_headline_pipeline_matches_independent_model(device):
+    """device=cpu: the C++ oracle; device=cuda: the HIP kernels themselves (MFMA hash + FP4 ACL)."""
+    dp = DataPlane(device=device, flow_buckets=1 << 14, hash_mode="mfma", acl_mode="mfma")
     sc = S.build_sfc(dp, n_pods=8, n_flows=20000, n_acl=256, seed=0)
     deny = S.install_deny_flows(dp, sc, k=512)
     dp.commit(full=True)
     pk, im = S.traffic_mixed(sc, deny, 6000, seed=7)
-    r = dp.run(pk, im)
-    port, olen, reason = P.meta_fields(r.meta)
+    if device == "cuda":
+        import torch
+
+        r = dp.run(torch.from_numpy(pk).cuda(), torch.from_numpy(im.view(np.int32)).cuda())
+        torch.cuda.synchronize()
+        meta, out = r.meta.cpu().numpy().view(np.uint32), r.out.cpu().numpy()
+    else:
+        r = dp.run(pk, im)
+        meta, out = r.meta, r.out
+    port, olen, reason = P.meta_fields(meta)
 
     flows = {}
     for k in range(len(sc.keys)):
@@ -108,7 +119,7 @@ def test_headline_pipeline_matches_independent_model():
             assert int(port[i]) == want_port, i
         if want is not None:
             assert int(olen[i]) == len(want)
-            assert bytes(r.out[i][: len(want)]) == want, i
+            assert bytes(out[i][: len(want)]) == want, i
     # every disposition of the mixed trace occurred
     assert seen.get(OK, 0) > 5000 and seen.get(NOROUTE, 0) > 100 and seen.get(DENY, 0) > 50
     assert seen.get(MALFORMED, 0) >= 1
