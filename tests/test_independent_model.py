@@ -123,3 +123,40 @@ def test_headline_pipeline_matches_independent_model(device):
     # every disposition of the mixed trace occurred
     assert seen.get(OK, 0) > 5000 and seen.get(NOROUTE, 0) > 100 and seen.get(DENY, 0) > 50
     assert seen.get(MALFORMED, 0) >= 1
+
+
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+def test_imix_frames_match_independent_model(device):
+    """Header-split IMIX frames (64 / 576 / 1500 / 9000 B): the data plane sees only the 64-B
+    header slot; the frame that leaves = egress header slot ++ the payload left in place
+    (P.assemble).  The model works on the whole frame and must give the same bytes."""
+    dp = DataPlane(device=device, flow_buckets=1 << 14, hash_mode="mfma", acl_mode="mfma")
+    sc = S.build_sfc(dp, n_pods=8, n_flows=20000, n_acl=256, seed=0)
+    dp.commit(full=True)
+    sizes = S.imix_sizes(800, S.IMIX_JUMBO, seed=3)
+    slots, im, frames, lens = S.traffic_frames(sc, len(sizes), sizes, seed=4)
+    if device == "cuda":
+        import torch
+
+        r = dp.run(torch.from_numpy(slots).cuda(), torch.from_numpy(im.view(np.int32)).cuda())
+        torch.cuda.synchronize()
+        meta, out = r.meta.cpu().numpy().view(np.uint32), r.out.cpu().numpy()
+    else:
+        r = dp.run(slots, im)
+        meta, out = r.meta, r.out
+    flows = {}
+    for k in range(len(sc.keys)):
+        s, d = S.POD_NET + int(sc.flow_src_pod[k]), S.POD_NET + int(sc.flow_dst_pod[k])
+        flows[(s.to_bytes(4, "big"), d.to_bytes(4, "big"), int(sc.flow_sport[k]), int(sc.flow_dport[k]))] = (
+            int(sc.pod_port[sc.flow_dst_pod[k]]), S.NAT_NET + (k % 250) + 1, 1024 + (k % 60000))
+    acl = [(r_.value.astype(np.uint64), r_.mask.astype(np.uint64), r_.permit) for r_ in dp.acl.rules]
+    big = 0
+    for i in range(len(sizes)):
+        ln = int(lens[i])
+        want_reason, want_port, want = _model(bytes(frames[i][:ln]), int(im[i]) & 0xFFFF, ln, sc, flows, acl,
+                                              dp.acl.default_permit)
+        assert want_reason == OK
+        got = P.assemble(out[i], int(meta[i]), frames[i], ln)
+        assert got == want, (i, ln)
+        big += ln > 64
+    assert big > 200
