@@ -4,9 +4,11 @@ The reference exposes controller-runtime metrics on :18090 and probes on :18091 
 SURVEY §5 "metrics").  Here one registry carries:
 * control-plane counters (reconciles, CNI requests by command/result, VSP RPCs, device-plugin
   allocations) — `CONTROL` below, incremented by the components;
-* `DataPlaneCollector`: per-port rx/tx packets+bytes, drops by reason, installed flows, per-flow
-  counter harvests, batch latency quantiles — read from a DataPlane at scrape time (counters are
-  64-bit on the host, harvested from the packed device counters).
+* `DataPlaneCollector`: per-port rx/tx packets+bytes, drops by reason, installed flows, entries
+  per table (flows, MACs static / learned, ACL rules, routes, nexthops, ECMP / LAG / flood groups,
+  tunnels, VM MAC maps), flow-table hits / misses, packet-path latency histograms — read from a
+  DataPlane at scrape time (counters are 64-bit on the host, harvested from the packed device
+  counters).
 `MetricsServer` serves /metrics (text exposition) and `ProbeServer` /healthz + /readyz with
 pluggable checks.
 """
@@ -93,6 +95,18 @@ class DataPlaneCollector:
         down.add_metric([self.name, "link_down"], float((valid & (f & T.PORT_LINK_DOWN).astype(bool)).sum()))
         down.add_metric([self.name, "rx_off"], float((valid & (f & T.PORT_RX_OFF).astype(bool)).sum()))
         yield down
+        # per-table occupancy and flow-table hit / miss (per-table hit/miss)
+        ent = GaugeMetricFamily("dpu_table_entries", "Entries per data-plane table", labels=["dataplane", "table"])
+        for name, n in _table_sizes(dp).items():
+            ent.add_metric([self.name, name], float(n))
+        yield ent
+        hits = int(dp.flow_totals[:, 0].sum()) if getattr(dp, "flow_totals", None) is not None else 0
+        past_ingress = int(ctr[:, 0].sum()) - sum(n for r, n in dp.drop_counters().items() if r in _INGRESS_DROPS)
+        hm = CounterMetricFamily("dpu_flow_lookups", "Exact-match flow lookups past ingress checks, by result (hits "
+                                 "as of the last per-flow counter harvest)", labels=["dataplane", "result"])
+        hm.add_metric([self.name, "hit"], float(hits))
+        hm.add_metric([self.name, "miss"], float(max(past_ingress - hits, 0)))
+        yield hm
         lat = HistogramMetricFamily("dpu_packet_latency_seconds",
                                     "Packet-path latency by stage (utils/latency.py: rx, pipeline, side, tx, "
                                     "batch per live batch; device per sampled packet)", labels=["dataplane", "stage"])
@@ -100,6 +114,32 @@ class DataPlaneCollector:
             b, total = h.buckets()
             lat.add_metric([self.name, stage], b, total)
         yield lat
+
+
+# drop reasons decided before the flow lookup (ingress_stage)
+_INGRESS_DROPS = ("bad_port", "vlan_drop", "spoof", "malformed")
+
+
+def _table_sizes(dp) -> dict:
+    """Occupancy of every table the data plane holds (attributes a DataPlane may lack are skipped)."""
+    from ..dataplane import tables as T
+
+    out = {"flows": len(dp.flows), "acl_rules": len(dp.acl.rules), "chains": int(dp.chains.n)}
+    v = dp.macs.a["valid"]
+    out["macs_static"] = int((v == T.MAC_STATIC).sum())
+    out["macs_learned"] = int((v == T.MAC_LEARNED).sum())
+    for name, attr in (("routes_v4", "routes"), ("routes_v6", "routes6"), ("tunnel_terms", "terms"),
+                       ("vm_mac_maps", "vmmac")):
+        t = getattr(dp, attr, None)
+        if t is None:
+            continue
+        out[name] = len(t) if hasattr(t, "__len__") else int(getattr(t, "n", 0))
+    for name, attr in (("nexthops", "nexthops"), ("ecmp_groups", "ecmp"), ("lag_groups", "lag"), ("tunnels_v4", "tunnels"),
+                       ("tunnels_v6", "tunnels6"), ("flood_groups", "flood")):
+        t = getattr(dp, attr, None)
+        if t is not None:
+            out[name] = int(getattr(t, "n", 0))
+    return out
 
 
 def register_dataplane(dataplane, name: str = "gpu0", registry: CollectorRegistry = REGISTRY) -> DataPlaneCollector:

@@ -225,6 +225,7 @@ def test_dataplane_metrics_exporter():
     dp.commit(full=True)
     pk, im = S.traffic(sc, 1000)
     dp.run(pk, im)
+    dp.harvest()
     reg = CollectorRegistry()
     register_dataplane(dp, "gpu0", reg)
     srv = MetricsServer("127.0.0.1:0", reg).start()
@@ -233,8 +234,13 @@ def test_dataplane_metrics_exporter():
         text = body.decode()
         assert code == 200
         assert 'dpu_flows_installed{dataplane="gpu0"} 512.0' in text
+        assert 'dpu_table_entries{dataplane="gpu0",table="flows"} 512.0' in text
+        assert 'dpu_table_entries{dataplane="gpu0",table="macs_static"} 4.0' in text
+        assert 'dpu_table_entries{dataplane="gpu0",table="acl_rules"} 8.0' in text
         rx = sum(float(line.split()[-1]) for line in text.splitlines() if line.startswith("dpu_port_rx_packets_total"))
         assert rx == 1000
+        assert 'dpu_flow_lookups_total{dataplane="gpu0",result="hit"} 1000.0' in text
+        assert 'dpu_flow_lookups_total{dataplane="gpu0",result="miss"} 0.0' in text
         assert _get(srv.port, "/other")[0] == 404
     finally:
         srv.stop()
