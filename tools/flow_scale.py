@@ -1,13 +1,15 @@
 """Flow-table scale sweep on one MI355X: the headline SFC (ACL 256 -> SNAT -> L2, 64-B frames,
-4M-packet batches) with 1M, 16M and 64M flows (tables of 64 MB, 1 GB and 4 GB at 50 % load), so
-the random bucket fetch moves from Infinity-Cache-resident to HBM-bound.  One JSON line per size.
+4M-packet batches) with 1M, 16M, 64M (and 256M) flows (tables of 64 MB, 1 GB, 4 GB and 16 GB at
+50 % load), so the random bucket fetch moves from Infinity-Cache-resident to HBM-bound.  One JSON
+line per size.
 
-python tools/flow_scale.py [--flows 1M,16M,64M] [--steps 20]
+python tools/flow_scale.py [--flows 1M,16M,64M,256M] [--steps 20]
 """
 import argparse
 import gc
 import json
 import sys
+import threading
 import time
 
 import numpy as np
@@ -31,6 +33,10 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--batch", type=int, default=1 << 22)
     a = ap.parse_args()
+    # large builds run minutes on the host: a heartbeat line every 30 s shows progress
+    t_start = time.time()
+    threading.Thread(target=lambda: [(time.sleep(30), print(f"# ... {time.time() - t_start:.0f} s", flush=True))
+                                     for _ in iter(int, 1)], daemon=True).start()
     for f in [size(x) for x in a.flows.split(",")]:
         t0 = time.time()
         print(f"# building {f} flows", flush=True)
