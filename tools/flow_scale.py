@@ -9,7 +9,6 @@ import argparse
 import gc
 import json
 import sys
-import threading
 import time
 
 import numpy as np
@@ -33,10 +32,9 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--batch", type=int, default=1 << 22)
     a = ap.parse_args()
-    # large builds run minutes on the host: a heartbeat line every 30 s shows progress
-    t_start = time.time()
-    threading.Thread(target=lambda: [(time.sleep(30), print(f"# ... {time.time() - t_start:.0f} s", flush=True))
-                                     for _ in iter(int, 1)], daemon=True).start()
+    # a 256M-flow build runs ~7 min on the host, mostly in native / numpy calls that hold the GIL
+    # (a Python heartbeat thread stalls with them): run it beside a shell heartbeat that appends
+    # to a file under gpurun_out/ (profiles/r2_s42_flow_scale_256m.log)
     for f in [size(x) for x in a.flows.split(",")]:
         t0 = time.time()
         print(f"# building {f} flows", flush=True)
