@@ -257,6 +257,10 @@ NFDP_HD void esp_encrypt_one(const EspTables& tb, const EspBatch& a, uint32_t i)
   if (olen + kEspOff > a.out_stride) { a.status[i] = kEspDrop; return; }
   const uint32_t nxt = tun ? 4u : f[23];
   const uint32_t seq = a.seq[i];
+  // Sequence number 0 is never sent (RFC 4303 3.3.3: the first packet is 1, the counter never
+  // cycles).  The host hands out 0 when an SA's 32-bit space is exhausted or the host SPD does
+  // not protect the packet: dropping here is what keeps the GCM nonce (0^32 || seq) unique.
+  if (seq == 0u) { a.status[i] = kEspDrop; return; }
   uint8_t* slot = a.out + (size_t)i * a.out_stride;
   // header: 52 bytes from slot + 12 (2 bytes before the frame are zero), 13 aligned dwords
   uint8_t h[52];

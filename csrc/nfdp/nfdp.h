@@ -30,7 +30,13 @@ namespace nfdp {
 constexpr int kSlotBytes = 64;         // header slot in HBM: the first min(len, 64) bytes of a frame
 constexpr int kSlotDwords = kSlotBytes / 4;
 constexpr uint32_t kMaxFrame = 9600;   // longest L2 frame (jumbo 9216 + tags); 14-bit length fields
-constexpr int kFloodWays = 16;         // member ports per flood group (bridge)
+constexpr int kFloodWays = 16;         // entries per flood-group row (bridge head row or overflow row)
+// A flood-group entry >= kFloodLink (and != kPortNone) links to overflow row (entry - kFloodLink)
+// of the same table: groups of any size are chains of 16-entry rows, 15 members + a link each.
+// The host keeps a group's first two members in its head row, so the hot kernel's first-member
+// search never follows a link; the side pass walks the whole chain.
+constexpr uint16_t kFloodLink = 0x8000;
+constexpr uint32_t kFloodMaxRows = 0x7000;   // link targets (rows) below this
 constexpr int kMaxPorts = 4094;        // vport table rows (VF / NF / wire / PR ports); 4094/4095 = meta sentinels
 constexpr int kBucketSlots = 4;        // flow-table bucket = 4 x {key, action} = one 128-B line
 constexpr uint32_t kSlotUsed = 0x100u; // occupied marker, stored in FlowKey.meta byte 1
@@ -515,7 +521,8 @@ struct TablesView {
   uint32_t acl_default_permit;   // verdict when no rule matches
   const uint16_t* lag_members;   // n_lag_groups * kLagWays egress ports (K8)
   uint32_t n_lag_groups;
-  const uint16_t* flood;         // n_flood * kFloodWays member ports per bridge (kPortNone padded)
+  const uint16_t* flood;         // n_flood head rows of kFloodWays entries per bridge (kPortNone padded),
+                                 // then overflow rows reached through kFloodLink entries
   uint32_t n_flood;              // bridges [0, n_flood) have a flood group
   const uint32_t* lpm24;         // 1 << 24 entries (nullable: no routes)
   const uint32_t* lpm8;          // n_lpm8 * 256

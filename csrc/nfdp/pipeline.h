@@ -264,7 +264,7 @@ NFDP_HD EgressDecision chain_stage(const TablesView& t, const TA& ta, Parsed& p,
         uint32_t first = kPortNone;
         for (int j = 0; j < kFloodWays; ++j) {
           const uint32_t m = fg[j];
-          if (m == kPortNone) break;
+          if (m >= kFloodLink) break;   // end of the group (or a link: never before two members)
           if (m != st.in_port) { first = m; break; }
         }
         if (first == kPortNone) { e.reason = kNoRoute; e.out_port = kPortNone; return e; }
@@ -446,9 +446,17 @@ NFDP_HD void side_stage(const TablesView& t, const TA& ta, const uint32_t* d_in,
   if ((ometa & kMetaFlood) && t.flood && st.bridge < t.n_flood) {
     const uint16_t* fg = t.flood + (size_t)st.bridge * kFloodWays;
     bool first = true;
+    uint32_t hops = 0;   // rows followed (bounded: a corrupt chain cannot loop forever)
     for (int j = 0; j < kFloodWays; ++j) {
       uint32_t m = fg[j];
       if (m == kPortNone) break;
+      if (m >= kFloodLink) {        // overflow row of a group beyond 15 members
+        const uint32_t row = m - kFloodLink;
+        if (row >= kFloodMaxRows || ++hops > kFloodMaxRows) break;
+        fg = t.flood + (size_t)row * kFloodWays;
+        j = -1;
+        continue;
+      }
       if (m == st.in_port) continue;
       if (first) { first = false; continue; }
       uint32_t push = (st.in_flags & kPortIngressTag) ? 1u : 0u;

@@ -38,7 +38,9 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <cstdint>
+#include <deque>
 #include <mutex>
 #include <vector>
 
@@ -59,6 +61,11 @@ constexpr uint64_t kRingEpochMask = (1ull << kRingEpochBits) - 1;
 __host__ __device__ inline uint64_t ring_word(uint64_t count, uint32_t epoch) {
   return (count << kRingEpochBits) | (epoch & kRingEpochMask);
 }
+// Epoch aliasing guard: the host lets at most kRingEpochMask epoch changes happen within
+// kEpochAliasHostUs; a wave whose previous chunk is older than kEpochAliasTicks (half of it, in
+// s_memrealtime ticks) drops its cached table lines whatever epoch value it sees.
+constexpr uint32_t kEpochAliasHostUs = 100;
+constexpr unsigned long long kEpochAliasTicks = kEpochAliasHostUs * 100ull / 2;   // 100 MHz
 __host__ __device__ inline uint64_t ring_count(uint64_t w) { return (w & ~kRingStop) >> kRingEpochBits; }
 __host__ __device__ inline uint32_t ring_epoch(uint64_t w) { return (uint32_t)(w & kRingEpochMask); }
 
@@ -143,6 +150,8 @@ class RingEngine {
 
  private:
   bool chunk_done(uint64_t chunk) const;
+  void pace_epoch_change();
+  std::deque<std::chrono::steady_clock::time_point> epoch_changes_;   // last kRingEpochMask changes
   uint64_t flip_prod() const {
     std::lock_guard<std::mutex> g(mu_);
     return flip_prod_;

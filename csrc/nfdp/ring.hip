@@ -190,6 +190,7 @@ __global__ __launch_bounds__(kRingBlock) void ring_kernel(RingArgs a) {
   const uint32_t nch_mask = a.ring_mask >> 6;  // R/64 - 1
   const unsigned long long t_begin = __builtin_amdgcn_s_memrealtime();
   uint32_t seen_epoch = 0xFFFFFFFFu;  // epoch of this wave's previous chunk
+  unsigned long long seen_t = 0;      // when this wave took its previous chunk
 
   for (;;) {
     unsigned long long tk = 0;
@@ -207,14 +208,18 @@ __global__ __launch_bounds__(kRingBlock) void ring_kernel(RingArgs a) {
       if (!ring_wait_chunk(a, lane, t_begin, tk, epoch, on_idle)) break;
     }
     const unsigned long long t_avail = __builtin_amdgcn_s_memrealtime();
-    if (epoch != seen_epoch) {
+    if (epoch != seen_epoch || t_avail - seen_t > kEpochAliasTicks) {
       // A new epoch: the host rewrote a table this kernel reads with ordinary cached loads (the
       // flow-table copy it now names, or the MAC table after learning).  The lines this wave's
       // CU L1 and its XCD's L2 still hold may be stale - this grid never sees the cache
       // invalidate a kernel launch brings - so drop them (agent-scope acquire) before probing.
+      // The epoch is 7 bits: a wave idle through a multiple of 128 changes would see its old
+      // value again.  The host spaces any 128 consecutive changes over >= kEpochAliasHostUs, so a
+      // wave whose previous chunk is older than half of that invalidates regardless.
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       seen_epoch = epoch;
     }
+    seen_t = t_avail;
     const bool trace = (a.flags_bits & kRingTrace) != 0 && wave == 0;
     uint32_t tr0 = 0, tr1 = 0, tr2 = 0, tr3 = 0, tr4 = 0, tr5 = 0;
 #define NFDP_RING_MARK(var)                                                 \
@@ -513,9 +518,22 @@ uint64_t RingEngine::publish(uint32_t n) {
   return prod_;
 }
 
+void RingEngine::pace_epoch_change() {
+  // (mu_ held) at most kRingEpochMask changes within kEpochAliasHostUs: the value a wave saw
+  // cannot come round again before its idle-time invalidation (ring_kernel) takes over
+  const auto now = Clock::now();
+  if (epoch_changes_.size() >= kRingEpochMask) {
+    const auto ready = epoch_changes_.front() + std::chrono::microseconds(kEpochAliasHostUs);
+    while (Clock::now() < ready) _mm_pause();
+    epoch_changes_.pop_front();
+  }
+  epoch_changes_.push_back(now > Clock::now() ? now : Clock::now());
+}
+
 uint32_t RingEngine::flip() {
   if (!grace_over()) throw std::runtime_error("ring: flip before the previous flip's grace period ended");
   std::lock_guard<std::mutex> g(mu_);
+  pace_epoch_change();
   epoch_ = (epoch_ + 1) & (uint32_t)kRingEpochMask;
   flip_prod_ = prod_;
   // same count, new epoch: chunks published from here on carry it (the frontier mirrors a word
@@ -526,6 +544,7 @@ uint32_t RingEngine::flip() {
 
 uint32_t RingEngine::bump_epoch() {
   std::lock_guard<std::mutex> g(mu_);
+  pace_epoch_change();
   epoch_ = (epoch_ + 2) & (uint32_t)kRingEpochMask;
   if (running_) __atomic_store_n(&ctl_->prod, ring_word(prod_, epoch_), __ATOMIC_RELEASE);
   return epoch_;

@@ -34,6 +34,7 @@ STATUS = {BYPASSED: "bypass", DONE: "done", DROPPED: "drop", AUTH_FAIL: "auth_fa
 CLEAR_OFF, ESP_OFF = 2, 14
 ESP_OVERHEAD = 50 + 16 + 3 + 2     # outer header + ICV + worst-case padding + trailer
 REPLAY_WINDOW = 64
+SEQ_MAX = 0xFFFFFFFF                # last outbound sequence number of an SA (no extended sequence numbers)
 
 
 def _raw_ip(ip) -> int:
@@ -62,10 +63,14 @@ class IpsecEngine:
         self.rx_rules: dict[tuple[int, int, int], int] = {}            # (src raw, dst raw, spi) -> sa
         self.next_seq = np.ones(max_sa, np.uint64)                     # outbound: next sequence number
         self.replay: dict[int, list[int]] = {}                         # inbound: sa -> [top, bitmap]
+        # SAs whose 32-bit outbound sequence space is used up: they protect nothing more (their
+        # packets are dropped) until the control plane installs a new key (`on_rekey(sa)` asks)
+        self.exhausted: set[int] = set()
+        self.on_rekey = None
         self.version = 0
         self._dev: dict[str, object] = {}
         self._dev_version = -1
-        self.stats = {k: 0 for k in ("enc", "dec", "bypass", "drop", "auth_fail", "no_sa", "replay")}
+        self.stats = {k: 0 for k in ("enc", "dec", "bypass", "drop", "auth_fail", "no_sa", "replay", "seq_exhausted")}
         te0, sbox, rem = self.nf.esp_tables()
         self._tabs = (np.frombuffer(te0, np.uint32).copy(), np.frombuffer(sbox, np.uint8).copy(),
                       np.frombuffer(rem, np.uint64).copy())
@@ -80,10 +85,16 @@ class IpsecEngine:
         dlo, dhi = mac_raw(dmac)
         raw = self.nf.esp_build_sa(bytes(key), bytes(salt), spi & 0xFFFFFFFF, mode, _raw_ip(src), _raw_ip(dst),
                                    int(slo), int(shi), int(dlo), int(dhi))
+        ident = (bytes(key), bytes(salt), spi & 0xFFFFFFFF)
+        prev = self.sa_info.get(idx)
         self.sa[idx] = np.frombuffer(raw, np.uint8)
-        self.sa_info[idx] = {"spi": spi, "mode": mode, "src": src, "dst": dst}
-        self.next_seq[idx] = 1
-        self.replay.pop(idx, None)
+        self.sa_info[idx] = {"spi": spi, "mode": mode, "src": src, "dst": dst, "ident": ident}
+        if prev is None or prev.get("ident") != ident:
+            # a new key: its counters start over.  Re-installing the SAME key material (a restart,
+            # a mode change) keeps them: resetting would reuse GCM nonces under that key.
+            self.next_seq[idx] = 1
+            self.replay.pop(idx, None)
+            self.exhausted.discard(idx)
         self.version += 1
 
     def set_sa_mode(self, idx: int, mode: int, src=None, dst=None) -> None:
@@ -182,9 +193,35 @@ class IpsecEngine:
         for s in np.unique(sa[sa >= 0]):
             idx = np.nonzero(sa == s)[0]
             base = int(self.next_seq[s])
-            seq[idx] = (base + np.arange(len(idx))) & 0xFFFFFFFF
-            self.next_seq[s] = base + len(idx)
+            # sequence numbers 1 .. 2^32 - 1, never cycled (RFC 4303 3.3.3); past the end a packet
+            # gets 0, which the kernel drops
+            ok = max(0, min(len(idx), SEQ_MAX + 1 - base))
+            seq[idx[:ok]] = base + np.arange(ok, dtype=np.int64)
+            self.next_seq[s] = base + ok
+            if ok < len(idx):
+                self.stats["seq_exhausted"] += len(idx) - ok
+                if s not in self.exhausted:
+                    self.exhausted.add(int(s))
+                    if self.on_rekey is not None:
+                        self.on_rekey(int(s))
         return seq
+
+    def replace_rules(self, spd: dict, rx: dict, sa_modes=()) -> None:
+        """Swap in a complete SPD / inbound-SA rule set at once (P4 compile): both device arrays
+        are rebuilt from the new sets, and the SA modes applied, only after everything is known."""
+        old_spd, old_rx = self.spd_rules, self.rx_rules
+        self.spd_rules = {(_raw_ip(d), p & 0xFF): v for (d, p), v in spd.items()}
+        self.rx_rules = {(_raw_ip(s), _raw_ip(d), spi & 0xFFFFFFFF): sa for (s, d, spi), sa in rx.items()}
+        try:
+            self._rebuild_spd()
+            self._rebuild_rx()
+        except Exception:
+            self.spd_rules, self.rx_rules = old_spd, old_rx
+            self._rebuild_spd()
+            self._rebuild_rx()
+            raise
+        for sa, mode, src, dst in sa_modes:
+            self.set_sa_mode(sa, mode, src=src, dst=dst)
 
     def _device_tables(self):
         if self._dev_version == self.version and self._dev:

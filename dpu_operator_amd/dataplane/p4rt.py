@@ -45,6 +45,14 @@ class P4Error(Exception):
         self.code = code
 
 
+# Actions of the reference's p4info whose semantics cannot be pinned from it (docs/DATAPLANE.md
+# "L3 and tunnels"): refused at write time with UNIMPLEMENTED.
+UNSUPPORTED_ACTIONS = {
+    "tx_ipsec_tunnel_v6": "IPsec tunnels over an IPv6 underlay are not supported "
+                          "(the p4info carries 80 of the 128 outer-destination bits)",
+}
+
+
 def vport_for_vsi(vsi: int) -> int:
     return vsi + VSI_TO_VPORT
 
@@ -204,9 +212,19 @@ class P4Runtime:
                 raise P4Error("ALREADY_EXISTS", f"entry already exists in {e.table}")
             if len(tab) >= self._table(e.table).size:
                 raise P4Error("RESOURCE_EXHAUSTED", f"table {e.table} is full ({self._table(e.table).size})")
+            if e.action and e.action.rsplit(".", 1)[-1] in UNSUPPORTED_ACTIONS:
+                # refused before it is stored: a stored entry would make every later compile fail
+                raise P4Error("UNIMPLEMENTED", UNSUPPORTED_ACTIONS[e.action.rsplit(".", 1)[-1]])
             tab[k] = e
             self.stats["writes"] += 1
-            self.compile()
+            try:
+                self.compile()
+            except Exception:
+                # transactional write: the entry that made the compile fail is taken back out and
+                # the previous table state recompiled, so the runtime never stays stuck
+                del tab[k]
+                self.compile()
+                raise
             return e
 
     def del_entry(self, table: str, spec: str) -> None:
@@ -218,7 +236,12 @@ class P4Runtime:
                 raise P4Error("NOT_FOUND", f"no such entry in {e.table}")
             del tab[k]
             self.stats["writes"] += 1
-            self.compile()
+            try:
+                self.compile()
+            except Exception:
+                tab[k] = e
+                self.compile()
+                raise
 
     def get_entries(self, table: str | None = None) -> list[Entry]:
         with self._lock:
@@ -404,15 +427,15 @@ class P4Runtime:
         if not any(rows.values()) and not getattr(self, "_owned_ipsec", False):
             return
         eng = dp.ipsec
-        for key in list(eng.spd_rules):
-            eng.spd_rules.pop(key)
-        eng.rx_rules.clear()
+        # Everything is validated and computed into locals first; the engine's rule sets are
+        # swapped only once the whole compile succeeded (a half-applied SPD would let the kernel
+        # protect traffic with a stale SPD while the host hands out sequence number 0).
         drops = set()
         modes: dict[tuple[int, int], tuple[int, int | None]] = {}
         for e in rows["ipsec_tx_sa_classification_table"]:
             d, p = e.key[0][1], e.key[1][1]
             if e.action.endswith("tx_ipsec_tunnel_v6"):
-                raise P4Error("UNIMPLEMENTED", "IPsec tunnels over an IPv6 underlay are not supported")
+                raise P4Error("UNIMPLEMENTED", UNSUPPORTED_ACTIONS["tx_ipsec_tunnel_v6"])
             if e.action.endswith("drop"):
                 drops.add((d, p))
             elif e.action.endswith("tx_ipsec_tunnel"):
@@ -424,34 +447,36 @@ class P4Runtime:
         from . import ipsec as I
 
         raw = lambda v: str(ipaddress.IPv4Address(v))  # noqa: E731
+        spd: dict = {}
+        sa_modes: list[tuple] = []
         for e in rows["ipsec_spd"]:
             d, p = e.key[0][1], e.key[1][1]
             if (d, p) in drops:
-                eng.set_spd(raw(d), p, I.DROP)
+                spd[(raw(d), p)] = (I.DROP, 0)
             elif e.action.endswith("ipsec_protect_set_metadata"):
                 sa = e.params["saidx"]
-                eng.set_spd(raw(d), p, I.PROTECT, sa)
+                spd[(raw(d), p)] = (I.PROTECT, sa)
                 m = modes.get((d, p))
                 if sa in eng.sa_info and m is not None:
                     if m[0] == 2:
                         enc = encap.get(tun_of.get(sa, -1), {})
-                        eng.set_sa_mode(sa, I.TUNNEL, src=raw(enc["ipsec_src_addr"]) if enc else None,
-                                        dst=raw(enc.get("ipsec_dst_addr", m[1])) if enc else raw(m[1]))
+                        sa_modes.append((sa, I.TUNNEL, raw(enc["ipsec_src_addr"]) if enc else None,
+                                         raw(enc.get("ipsec_dst_addr", m[1])) if enc else raw(m[1])))
                     else:
-                        eng.set_sa_mode(sa, I.TRANSPORT)
+                        sa_modes.append((sa, I.TRANSPORT, None, None))
             elif e.action.endswith("ipsec_bypass"):
-                eng.set_spd(raw(d), p, I.BYPASS)
+                spd[(raw(d), p)] = (I.BYPASS, 0)
         terms = {(e.key[0][1], e.key[1][1]) for e in rows["ipv4_ipsec_tunnel_term_table"]}
+        rx: dict = {}
         for e in rows["MainControlDecrypt.ipsec_rx_sa_classification_table"]:
             if not e.action.endswith("ipsec_decrypt"):
                 continue
             s_, d_, spi = e.key[0][1], e.key[1][1], e.key[2][1]
             sa = e.params["saidx"]
-            eng.set_rx_sa(raw(s_), raw(d_), spi, sa)
+            rx[(raw(s_), raw(d_), spi)] = sa
             if sa in eng.sa_info:
-                eng.set_sa_mode(sa, I.TUNNEL if (s_, d_) in terms else I.TRANSPORT)
-        eng._rebuild_spd()
-        eng._rebuild_rx()
+                sa_modes.append((sa, I.TUNNEL if (s_, d_) in terms else I.TRANSPORT, None, None))
+        eng.replace_rules(spd, rx, sa_modes)
         self._owned_ipsec = any(rows.values())
 
     def _compile_tunnels_v6(self, dp, port, add_mac, bridges, mac_of) -> bool:

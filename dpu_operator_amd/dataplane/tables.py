@@ -595,36 +595,84 @@ class VmMacTable:
         return None
 
 
+FLOOD_LINK = 0x8000      # nfdp.h kFloodLink: an entry >= this (!= PORT_NONE) links to overflow row entry - FLOOD_LINK
+FLOOD_MAX_ROWS = 0x7000  # nfdp.h kFloodMaxRows
+
+
 class FloodTable:
-    """Per-bridge flood groups (OvS NORMAL broadcast / unknown-unicast flooding): up to
-    ``FLOOD_WAYS`` member ports per bridge, indexed by bridge id."""
+    """Per-bridge flood groups (OvS NORMAL broadcast / unknown-unicast flooding), any size.
+
+    Row b (< ``bridges``) is bridge b's head row of ``FLOOD_WAYS`` entries.  A group of up to 16
+    members fills its head row; a bigger one keeps 15 members per row and links the 16th entry
+    to an overflow row (rows >= ``bridges``, allocated on demand and recycled), so the kernel's
+    first-member search stays inside the head row and the side pass follows the chain."""
 
     def __init__(self, bridges: int = 4096):
+        self.bridges = bridges
         self.a = np.full((bridges, FLOOD_WAYS), PORT_NONE, np.uint16)
         self.n = 0
         self.version = 0
+        self._rows: dict[int, list[int]] = {}   # bridge -> its overflow rows
+        self._free: list[int] = []
+
+    def _alloc_row(self) -> int:
+        if self._free:
+            r = self._free.pop()
+        else:
+            r = len(self.a)
+            if r >= FLOOD_MAX_ROWS:
+                raise ValueError("flood table: out of overflow rows")
+            grow = max(64, len(self.a) // 4)
+            self.a = np.vstack([self.a, np.full((grow, FLOOD_WAYS), PORT_NONE, np.uint16)])
+            self._free.extend(range(len(self.a) - 1, r, -1))
+        self.a[r] = PORT_NONE
+        return r
 
     def set_members(self, bridge: int, ports: list[int]) -> None:
-        if not 0 <= bridge < len(self.a):
+        if not 0 <= bridge < self.bridges:
             raise ValueError("bridge id out of range")
-        if len(ports) > FLOOD_WAYS:
-            raise ValueError(f"at most {FLOOD_WAYS} flood members per bridge")
+        ports = [int(p) for p in ports]
+        if any(not 0 <= p < MAX_PORTS for p in ports):
+            raise ValueError("flood member out of range")
+        for r in self._rows.pop(bridge, []):
+            self.a[r] = PORT_NONE
+            self._free.append(r)
         self.a[bridge] = PORT_NONE
-        self.a[bridge, : len(ports)] = ports
+        rows, row, rest = [], bridge, ports
+        while len(rest) > FLOOD_WAYS:
+            nxt = self._alloc_row()
+            rows.append(nxt)
+            self.a[row, : FLOOD_WAYS - 1] = rest[: FLOOD_WAYS - 1]
+            self.a[row, FLOOD_WAYS - 1] = FLOOD_LINK + nxt
+            rest, row = rest[FLOOD_WAYS - 1:], nxt
+        self.a[row, : len(rest)] = rest
+        if rows:
+            self._rows[bridge] = rows
         self.n = max(self.n, bridge + 1) if ports else self.n
         self.version += 1
 
     def add_member(self, bridge: int, port: int) -> None:
-        cur = [int(p) for p in self.a[bridge] if p != PORT_NONE]
+        cur = self.members(bridge)
         if port not in cur:
             self.set_members(bridge, cur + [port])
 
     def remove_member(self, bridge: int, port: int) -> None:
-        cur = [int(p) for p in self.a[bridge] if p != PORT_NONE and p != port]
-        self.set_members(bridge, cur)
+        self.set_members(bridge, [p for p in self.members(bridge) if p != port])
 
     def members(self, bridge: int) -> list[int]:
-        return [int(p) for p in self.a[bridge] if p != PORT_NONE]
+        out, row = [], bridge
+        for _ in range(FLOOD_MAX_ROWS):
+            for p in self.a[row]:
+                p = int(p)
+                if p == PORT_NONE:
+                    return out
+                if p >= FLOOD_LINK:
+                    row = p - FLOOD_LINK
+                    break
+                out.append(p)
+            else:
+                return out
+        return out
 
 
 class LagTable:

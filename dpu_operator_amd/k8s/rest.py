@@ -359,6 +359,7 @@ class _Watch:
     def __init__(self, client: RestClient, kind: str, fn, replay: bool, namespace: str | None):
         self.c, self.kind, self.fn, self.replay, self.ns = client, kind, fn, replay, namespace
         self.rv: str | None = None
+        self.known: dict[tuple[str, str], dict] = {}   # last state of every object the handler saw
         self._stop = threading.Event()
         self.ready = threading.Event()
         self._sock = None
@@ -384,12 +385,38 @@ class _Watch:
         except Exception:  # a broken handler must not kill the reflector
             log.exception("watch handler for %s failed", self.kind)
 
+    @staticmethod
+    def _key(obj: dict) -> tuple[str, str]:
+        md = obj.get("metadata") or {}
+        return md.get("namespace") or "", md.get("name") or ""
+
+    def _track(self, etype: str, obj: dict) -> None:
+        if etype == "DELETED":
+            self.known.pop(self._key(obj), None)
+        elif etype in ("ADDED", "MODIFIED"):
+            self.known[self._key(obj)] = obj
+
     def _list(self, first: bool) -> None:
+        """List, then reconcile the handler's view with it (a reflector's Replace): on a re-list
+        after a 410 / expired watch, objects that vanished during the gap produce DELETED (with
+        their last known state), objects already known MODIFIED, new ones ADDED."""
         lst = self.c._list_raw(self.kind, self.ns)
         self.rv = (lst.get("metadata") or {}).get("resourceVersion")
-        if self.replay or not first:
-            for o in lst.get("items", []):
-                self._emit("ADDED", o)
+        items = lst.get("items", [])
+        if first:
+            for o in items:
+                self._track("ADDED", o)
+                if self.replay:
+                    self._emit("ADDED", o)
+            return
+        now = {self._key(o): o for o in items}
+        for k in [k for k in self.known if k not in now]:
+            gone = self.known.pop(k)
+            self._emit("DELETED", gone)
+        for k, o in now.items():
+            t = "MODIFIED" if k in self.known else "ADDED"
+            self.known[k] = o
+            self._emit(t, o)
 
     def _run(self) -> None:
         backoff = 0.05
@@ -444,6 +471,7 @@ class _Watch:
                     self.rv = rv
                 if t == "BOOKMARK" or self._stop.is_set():
                     continue
+                self._track(t, obj)
                 self._emit(t, obj)
         finally:
             self._sock = None

@@ -243,7 +243,7 @@ class GpuVsp(VspBase):
             for i in vfs:
                 dp.macs.insert(VF_BRIDGE, self.vports[i]["pod_mac"], i)
                 dp.ports.update(i, default_out=None)
-            dp.flood.set_members(VF_BRIDGE, [WIRE_PORT] + vfs[: T.FLOOD_WAYS - 1])
+            dp.flood.set_members(VF_BRIDGE, [WIRE_PORT] + vfs)   # chained rows: every VF
         else:
             for i in vfs:
                 dp.ports.update(i, default_out=self.nfs[0]["in"], bridge_id=STEER_BRIDGE)

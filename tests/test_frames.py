@@ -167,6 +167,47 @@ def test_flood_learn_arp_mirror_oracle():
     assert {(b, m) for b, m, _ in dp.macs.learned()} >= {(BR, A), (BR, B), (BR, C)}
 
 
+def _big_bridge(device, n=64):
+    """n ports on one bridge, more than one 16-entry flood row: the group is a chain of rows."""
+    dp = DataPlane(device=device, flow_buckets=1 << 10, mac_slots=1 << 10)
+    for p in range(n):
+        dp.ports.set(p, flags=T.PORT_VALID | T.PORT_LEARN | T.PORT_ARP_TRAP, bridge_id=BR)
+    dp.flood.set_members(BR, list(range(n)))
+    dp.commit(full=True)
+    return dp
+
+
+def _broadcast_from(dp, port, to_dev=False):
+    arp, al = P.craft_arp(1, smac=A, sender_ip=0x0A000001, target_ip=0x0A000002)
+    slots, im = P.header_slots(arp, al), P.inmeta(np.array([port]), al)
+    if to_dev:
+        torch = _torch()
+        r = dp.run(torch.from_numpy(slots).cuda(), torch.from_numpy(im.view(np.int32)).cuda())
+        torch.cuda.synchronize()
+        return r.out.cpu().numpy(), r.meta.cpu().numpy().view(np.uint32), dp.side_result()
+    r = dp.run(slots, im)
+    return r.out, r.meta, dp.side_result()
+
+
+def test_flood_groups_beyond_one_row_oracle():
+    """64 VFs on one bridge: a broadcast ARP reaches all 63 peers (primary copy + 62 replicas),
+    plus the ARP slow-path copy; membership changes recycle the overflow rows."""
+    dp = _big_bridge("cpu")
+    assert dp.flood.members(BR) == list(range(64)) and len(dp.flood.a) > 4096
+    for src in (0, 17, 63):
+        _, m, sr = _broadcast_from(dp, src)
+        p0, _, r0 = P.meta_fields(m)
+        got = [int(p0[0])] + [int(x) for x, rr in zip(*P.meta_fields(sr["rep_meta"])[::2]) if rr == 0]
+        assert int(r0[0]) == 0 and sorted(got) == [q for q in range(64) if q != src]
+        assert (P.meta_fields(sr["rep_meta"])[2] == 12).sum() == 1       # one ARP copy punted
+    rows = len(dp.flood._free)
+    dp.flood.set_members(BR, list(range(40)))
+    dp.flood.set_members(BR, list(range(64)))
+    assert len(dp.flood._free) == rows                                   # rows reused, not leaked
+    dp.flood.remove_member(BR, 5)
+    assert 5 not in dp.flood.members(BR) and len(dp.flood.members(BR)) == 63
+
+
 def test_mac_aging():
     dp = _bridge("cpu")
     _run_l2(dp)
@@ -254,6 +295,16 @@ def test_flood_learn_arp_mirror_gpu_bit_exact():
     assert sorted(cpu.macs.learned()) == sorted(gpu.macs.learned())
     assert np.array_equal(cpu.port_counters(), gpu.port_counters())
     assert cpu.drop_counters() == gpu.drop_counters()
+
+
+@pytest.mark.gpu
+def test_flood_groups_beyond_one_row_gpu_bit_exact():
+    cpu, gpu = _big_bridge("cpu"), _big_bridge("cuda")
+    for src in (0, 40):
+        oc, mc, sc_ = _broadcast_from(cpu, src)
+        og, mg, sg = _broadcast_from(gpu, src, to_dev=True)
+        assert np.array_equal(mc, mg) and np.array_equal(oc, og)
+        assert _reps(sc_) == _reps(sg) and sg["n_rep"] == 63          # 62 replicas + the ARP copy
 
 
 @pytest.mark.gpu

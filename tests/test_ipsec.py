@@ -190,10 +190,84 @@ def test_p4_ipsec_tables_compile_onto_the_engine():
     assert eng.sa_info[6]["mode"] == I.TUNNEL
     out, st = eng.encrypt(_frames(["10.0.0.2"], [200]))
     assert st[0] == I.DONE and out[0][26:34] == bytes([192, 0, 2, 8, 192, 0, 2, 9])
-    with pytest.raises(Exception):
+    from dpu_operator_amd.dataplane.p4rt import P4Error
+
+    with pytest.raises(P4Error) as ei:
         rt.add_entry(C + "ipsec_tx_sa_classification_table", "hdrs.ipv4[vmeta.common.depth].dst_ip=10.0.0.7,"
                      "hdrs.ipv4[vmeta.common.depth].protocol=6,user_meta.cmeta.is_tunnel=1,"
                      "action=linux_networking_control.tx_ipsec_tunnel_v6(1,2,3)")
+    assert ei.value.code == "UNIMPLEMENTED"
+    # the refused write left nothing behind: the SPD still protects, sequence numbers keep
+    # counting (never 0, never reused) and later writes compile
+    assert eng.spd_rules and not rt.get_entries(C + "ipsec_tx_sa_classification_table")[1:]
+    out2, st2 = eng.encrypt(_frames(["10.0.0.2"] * 3, [200, 300, 400]))
+    assert (st2 == I.DONE).all()
+    seqs = [int.from_bytes(o[38:42], "big") for o in out2]
+    assert seqs == [2, 3, 4]
+    rt.add_entry(C + "ipsec_spd", "hdrs.ipv4[vmeta.common.depth].dst_ip=10.0.0.9,hdrs.ipv4[vmeta.common.depth].protocol=17,"
+                 "action=linux_networking_control.ipsec_bypass()")
+    assert len(eng.spd_rules) == 2
+
+
+def test_failed_compile_rolls_back_the_write():
+    """A write whose compile fails is taken back out: the runtime is not stuck on it."""
+    from dpu_operator_amd.dataplane.engine import DataPlane
+    from dpu_operator_amd.dataplane.p4rt import P4Runtime
+
+    dp = DataPlane(device="cpu", flow_buckets=1 << 10)
+    rt = P4Runtime(dp)
+    C = "linux_networking_control."
+    calls = {"n": 0}
+    real = rt._compile_ipsec
+
+    def boom(d):
+        calls["n"] += 1
+        if calls["n"] == 2:
+            raise RuntimeError("injected compile failure")
+        return real(d)
+
+    rt._compile_ipsec = boom
+    rt.add_entry(C + "ipsec_spd", "hdrs.ipv4[vmeta.common.depth].dst_ip=10.0.0.2,hdrs.ipv4[vmeta.common.depth].protocol=17,"
+                 "action=linux_networking_control.ipsec_bypass()")
+    with pytest.raises(RuntimeError):
+        rt.add_entry(C + "ipsec_spd", "hdrs.ipv4[vmeta.common.depth].dst_ip=10.0.0.3,hdrs.ipv4[vmeta.common.depth].protocol=17,"
+                     "action=linux_networking_control.ipsec_bypass()")
+    assert len(rt.get_entries(C + "ipsec_spd")) == 1
+    rt.add_entry(C + "ipsec_spd", "hdrs.ipv4[vmeta.common.depth].dst_ip=10.0.0.4,hdrs.ipv4[vmeta.common.depth].protocol=17,"
+                 "action=linux_networking_control.ipsec_bypass()")
+    assert len(dp.ipsec.spd_rules) == 2
+
+
+def test_sequence_space_exhaustion_stops_protecting_and_asks_for_a_rekey():
+    """RFC 4303 3.3.3: the outbound counter never cycles.  Near 2^32 the last numbers go out,
+    then the SA protects nothing more (drop, never IV reuse) and the control plane is asked to
+    rekey; re-installing the same key keeps the counter, a new key restarts it."""
+    e = _engine()
+    asked = []
+    e.on_rekey = asked.append
+    e.next_seq[0] = I.SEQ_MAX - 1
+    out, st = e.encrypt(_frames(["10.0.0.2"] * 4, [100] * 4))
+    assert list(st) == [I.DONE, I.DONE, I.DROPPED, I.DROPPED]
+    assert [int.from_bytes(o[38:42], "big") for o in out[:2]] == [I.SEQ_MAX - 1, I.SEQ_MAX]
+    assert out[2] is None and out[3] is None and asked == [0] and e.stats["seq_exhausted"] == 2
+    # same key material again (a restart): still exhausted, nothing is sent with a reused nonce
+    e.add_sa(0, key=KEY128, salt=SALT, spi=0x1001, mode=I.TUNNEL, src="192.0.2.1", dst="192.0.2.2",
+             smac="02:00:00:00:0e:01", dmac="02:00:00:00:0e:02")
+    _, st2 = e.encrypt(_frames(["10.0.0.2"], [100]))
+    assert st2[0] == I.DROPPED
+    # a new key: counting restarts at 1
+    e.add_sa(0, key=bytes(range(50, 66)), salt=SALT, spi=0x1003, mode=I.TUNNEL, src="192.0.2.1", dst="192.0.2.2")
+    out3, st3 = e.encrypt(_frames(["10.0.0.2"], [100]))
+    assert st3[0] == I.DONE and int.from_bytes(out3[0][38:42], "big") == 1
+
+
+def test_packets_the_host_spd_does_not_protect_are_never_sent_with_seq_0():
+    """Stale device SPD vs an emptied host rule set: the kernel sees seq 0 and drops."""
+    e = _engine()
+    e._device_tables()                 # device copy says PROTECT
+    e.spd_rules.clear()                # host rules gone without a rebuild (the advisor's case)
+    out, st = e.encrypt(_frames(["10.0.0.2"], [100]))
+    assert st[0] == I.DROPPED and out[0] is None
 
 
 @pytest.mark.gpu

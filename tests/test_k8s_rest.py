@@ -187,6 +187,35 @@ def test_watch_relists_after_410(tmp_path):
         srv.stop()
 
 
+def test_relist_after_gap_emits_deletes_and_modifies(tmp_path):
+    """A re-list (after 410 Gone) is a Replace: objects deleted while the watch was down produce
+    DELETED with their last known state, known objects MODIFIED, new ones ADDED."""
+    backing = ApiServer()
+    backing.create(_cm("x"))
+    backing.create(_cm("z", data={"k": "last"}))
+    srv = KubeApiServer(backing).start()
+    try:
+        c = R.RestClient(R.ClusterConfig(server=srv.url))
+        got = []
+        w = R._Watch(c, "ConfigMap", lambda t, o: got.append((t, o["metadata"]["name"], o.get("data"))), True, None)
+        w._list(first=True)
+        assert sorted((t, n) for t, n, _ in got) == [("ADDED", "x"), ("ADDED", "z")]
+        got.clear()
+        backing.delete("ConfigMap", "z", "default")      # during the gap
+        backing.create(_cm("n"))
+        w._list(first=False)
+        assert ("DELETED", "z", {"k": "last"}) in got
+        assert ("MODIFIED", "x", {}) in got and ("ADDED", "n", {}) in got and len(got) == 3
+        assert set(w.known) == {("default", "x"), ("default", "n")}
+        # events on the stream keep the known set current
+        w._track("DELETED", backing.get("ConfigMap", "n", "default"))
+        got.clear()
+        w._list(first=False)
+        assert ("ADDED", "n", {}) in got
+    finally:
+        srv.stop()
+
+
 def test_unauthorized_without_token(tmp_path):
     srv = KubeApiServer(ApiServer(), token="t").start()
     try:
