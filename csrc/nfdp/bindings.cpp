@@ -8,10 +8,12 @@
 #include <pybind11/stl.h>
 
 #include "host.h"
+#include "iox.h"
 #include "ipsec.h"
 #include "pktio.h"
 #include "ring.h"
 #include "shard.h"
+#include "trafgen.h"
 
 namespace py = pybind11;
 using namespace nfdp;
@@ -683,4 +685,152 @@ PYBIND11_MODULE(_nfdp, m) {
     check(launch_harvest(reinterpret_cast<unsigned long long*>(ctr), reinterpret_cast<unsigned long long*>(out), n,
                          reinterpret_cast<hipStream_t>(stream)), "harvest");
   });
+
+  // ---- native packet I/O engine (iox.h): ports, backends, engine; pod-side memif tools ----
+  using namespace nfdp::iox;
+  py::class_<Port, std::shared_ptr<Port>>(m, "IoPort")
+      .def_property_readonly("kind", &Port::kind)
+      .def("counters", [](Port& p) {
+        return py::dict(py::arg("rx") = p.rx_pkts.load(), py::arg("tx") = p.tx_pkts.load(),
+                        py::arg("tx_full") = p.tx_full.load(), py::arg("rx_bytes") = p.rx_bytes.load(),
+                        py::arg("tx_bytes") = p.tx_bytes.load());
+      });
+  py::class_<MemifPort, Port, std::shared_ptr<MemifPort>>(m, "MemifPort")
+      .def(py::init<const std::string&, uint32_t, uint32_t>(), py::arg("path"), py::arg("ring_size") = 1024,
+           py::arg("buf_size") = 2048)
+      .def_property_readonly("path", &MemifPort::path);
+  py::class_<PacketPort, Port, std::shared_ptr<PacketPort>>(m, "PacketPort")
+      .def(py::init<const std::string&, uint32_t, uint32_t>(), py::arg("ifname"), py::arg("frames") = 1024,
+           py::arg("frame_size") = 2048);
+  py::class_<FdPort, Port, std::shared_ptr<FdPort>>(m, "FdPort")
+      .def(py::init<int, uint32_t, uint32_t>(), py::arg("fd"), py::arg("nbufs") = 256, py::arg("buf_size") = 9728);
+  py::class_<Backend, std::shared_ptr<Backend>>(m, "IoBackend")
+      .def_property_readonly("capacity", &Backend::capacity)
+      .def("published", &Backend::published)
+      .def("completed", &Backend::completed);
+  py::class_<GpuBackend, Backend, std::shared_ptr<GpuBackend>>(m, "GpuBackend")
+      .def(py::init<RingEngine*>(), py::arg("ring"), py::keep_alive<1, 2>());
+  py::class_<OracleBackend, Backend, std::shared_ptr<OracleBackend>>(m, "OracleBackend")
+      .def(py::init<uint32_t>(), py::arg("capacity"))
+      .def("configure", [](OracleBackend& b, py::dict tables, uintptr_t flow_ctr, uintptr_t port_ctr, uintptr_t drop_ctr,
+                           py::object side) {
+        const TablesView t = tables_from(tables);
+        const SideOut so = side_from(side);
+        b.configure(t, reinterpret_cast<uint64_t*>(flow_ctr), reinterpret_cast<uint64_t*>(port_ctr),
+                    reinterpret_cast<uint64_t*>(drop_ctr), so, const_cast<MacEntry*>(t.macs), t.mac_mask);
+      })
+      .def_readwrite("stamp", &OracleBackend::stamp);
+  py::class_<Engine>(m, "IoEngine")
+      .def(py::init<uint32_t, uint32_t>(), py::arg("burst") = 256, py::arg("inflight") = 8)
+      .def("add_backend", &Engine::add_backend)
+      .def("add_port", &Engine::add_port)
+      .def("remove_port", &Engine::remove_port)
+      .def("port", &Engine::port)
+      .def("set_steering", [](Engine& e, py::buffer ports, py::bytes rss) {
+        py::buffer_info bi = ports.request();
+        const size_t n = (size_t)bi.size * bi.itemsize / sizeof(PortEntry);
+        std::vector<PortEntry> v(n);
+        std::memcpy(v.data(), bi.ptr, n * sizeof(PortEntry));
+        std::string k = rss;
+        e.set_steering(v, std::vector<uint8_t>(k.begin(), k.end()));
+      })
+      .def("set_redirect", &Engine::set_redirect)
+      .def("set_side_ports", &Engine::set_side_ports)
+      .def("set_side_always", &Engine::set_side_always)
+      .def("inject", [](Engine& e, uint32_t port, py::bytes f) {
+        std::string s = f;
+        e.inject(port, reinterpret_cast<const uint8_t*>(s.data()), (uint32_t)s.size());
+      })
+      .def("start", &Engine::start)
+      .def("stop", [](Engine& e) { py::gil_scoped_release nogil; e.stop(); })
+      .def("pause", [](Engine& e) { py::gil_scoped_release nogil; e.pause(); })
+      .def("resume", &Engine::resume)
+      .def("inject_failure", &Engine::inject_failure)
+      .def_property_readonly("running", &Engine::running)
+      .def("error", &Engine::error)
+      .def("stats", &Engine::stats)
+      .def("owner_of_frame", [](const Engine& e, py::bytes f, uint32_t port) {
+        std::string s = f;
+        return e.owner_of_frame(reinterpret_cast<const uint8_t*>(s.data()), (uint32_t)s.size(), port);
+      })
+      .def("take_punts", [](Engine& e, size_t max) {
+        py::list out;
+        for (auto& p : e.take_punts(max))
+          out.append(py::make_tuple(py::bytes(reinterpret_cast<const char*>(p.frame.data()), p.frame.size()),
+                                    (int)p.in_port, (int)p.reason));
+        return out;
+      }, py::arg("max") = 1024)
+      .def("take_latency_us", [](Engine& e) {
+        auto v = e.take_latency_us();
+        return py::array_t<double>(v.size(), v.data());
+      });
+  // pod side of a memif vport (tests / tools): frames in, frames out
+  struct MemifEndpoint {
+    std::unique_ptr<memif::Region> reg;
+    memif::Producer prod;
+    memif::Consumer cons;
+  };
+  py::class_<MemifEndpoint>(m, "MemifEndpoint")
+      .def(py::init([](const std::string& path) {
+        auto* e = new MemifEndpoint;
+        e->reg.reset(new memif::Region(path, false));
+        e->prod.init(e->reg.get(), 0);
+        e->cons.init(e->reg.get(), 1);
+        e->reg->hdr()->peer_up.store(1);
+        return e;
+      }))
+      .def("send", [](MemifEndpoint& e, py::list frames) {
+        uint32_t n = 0;
+        for (auto f : frames) {
+          std::string s = f.cast<py::bytes>();
+          if (!e.prod.put(reinterpret_cast<const uint8_t*>(s.data()), (uint32_t)s.size())) break;
+          ++n;
+        }
+        e.prod.commit();
+        return n;
+      })
+      .def("recv", [](MemifEndpoint& e, uint32_t max) {
+        py::list out;
+        uint32_t n = std::min(e.cons.available(), max);
+        for (uint32_t i = 0; i < n; ++i) {
+          uint32_t len = 0;
+          const uint8_t* p = e.cons.get(len);
+          out.append(py::bytes(reinterpret_cast<const char*>(p), len));
+        }
+        e.cons.release_to(e.cons.next);
+        return out;
+      }, py::arg("max") = 4096);
+  // pod-side generator / sink (trafgen.h); pods: list of (path, frames [k, stride] u8, lens [k] u32)
+  m.def("trafgen_run", [](py::list pods, double duration_s, double warmup_s, double rate_pps, uint32_t threads,
+                          uint32_t burst, uint32_t inflight) {
+    std::vector<trafgen::Pod> v;
+    for (auto o : pods) {
+      py::tuple t = o.cast<py::tuple>();
+      trafgen::Pod p;
+      p.path = t[0].cast<std::string>();
+      auto fr = t[1].cast<py::array_t<uint8_t, py::array::c_style | py::array::forcecast>>();
+      auto ln = t[2].cast<U32Arr>();
+      if (fr.ndim() != 2 || ln.ndim() != 1 || fr.shape(0) != ln.shape(0)) throw std::invalid_argument("trafgen: frames [k, stride], lens [k]");
+      p.stride = (uint32_t)fr.shape(1);
+      p.frames.assign(fr.data(), fr.data() + fr.size());
+      p.lens.assign(ln.data(), ln.data() + ln.size());
+      for (uint32_t x : p.lens) if (x > p.stride) throw std::invalid_argument("trafgen: len > stride");
+      v.push_back(std::move(p));
+    }
+    trafgen::Config c;
+    c.duration_s = duration_s; c.warmup_s = warmup_s; c.rate_pps = rate_pps; c.threads = threads; c.burst = burst;
+    c.inflight = inflight;
+    trafgen::Result r;
+    {
+      py::gil_scoped_release nogil;
+      r = trafgen::run(v, c);
+    }
+    py::dict d;
+    d["sent"] = r.sent; d["received"] = r.received; d["tx_full"] = r.tx_full; d["bad"] = r.bad;
+    d["elapsed_s"] = r.elapsed_s;
+    d["lat_us"] = py::array_t<double>(r.lat_us.size(), r.lat_us.data());
+    d["rx_per_pod"] = r.rx_per_pod; d["tx_per_pod"] = r.tx_per_pod;
+    return d;
+  }, py::arg("pods"), py::arg("duration_s") = 1.0, py::arg("warmup_s") = 0.1, py::arg("rate_pps") = 0.0,
+     py::arg("threads") = 1, py::arg("burst") = 32, py::arg("inflight") = 0);
 }

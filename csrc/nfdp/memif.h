@@ -1,0 +1,201 @@
+// memif.h — shared-memory packet interface between a pod (or NF) and the data plane.
+//
+// The reference's DPU data ports are kernel-bypass: OvS-DPDK ports bound with
+// `type=dpdk options:dpdk-devargs=<pci>` on a netdev-datapath bridge
+// (internal/daemon/vendor-specific-plugins/marvell/ovs-dp/ovsdp.go:39-55), or FXP silicon queues.
+// The MI355X data plane's equivalent for container endpoints is a shared-memory vport: one
+// region (a /dev/shm file, or any fd that can be mmap'ed) per vport holding two single-producer
+// single-consumer descriptor rings and their frame buffers.  No syscall on the fast path: the
+// pod's application writes a frame and bumps `head` (release); the I/O engine (iox.h) reads it,
+// copies its 64-B header slot into the GPU ring and later bumps `tail` once the egress copy no
+// longer needs the payload (the frame stays in place while the GPU works on its header).
+//
+//   region  = [Hdr 64 B][Ctl ring 0 | Ctl ring 1, 128 B each][Desc ring 0][Desc ring 1]
+//             [buffers ring 0][buffers ring 1]
+//   ring 0  = pod -> data plane (the pod produces),  ring 1 = data plane -> pod (the engine produces)
+//   slot i of a ring always uses buffer i (the consumer returns slots in order).
+//
+// Header-only, no HIP: the I/O engine, the pod-side endpoint and the standalone traffic tool
+// (csrc/pktgen) share it.
+#pragma once
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <atomic>
+#include <cstdint>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+
+namespace nfdp {
+namespace memif {
+
+constexpr uint64_t kMagic = 0x4d49463335355846ull;   // "FX553FIM"
+constexpr uint32_t kVersion = 1;
+
+struct alignas(64) Hdr {
+  uint64_t magic;
+  uint32_t version;
+  uint32_t ring_size;      // slots per ring (power of two)
+  uint32_t buf_size;       // bytes per frame buffer (>= the largest frame)
+  uint32_t flags;
+  uint8_t mac[8];          // the vport's MAC (informational, set by the data plane)
+  std::atomic<uint32_t> peer_up;   // pod side attached (informational)
+  uint32_t pad[5];
+};
+static_assert(sizeof(Hdr) == 64, "memif Hdr");
+
+struct alignas(64) Ctl {
+  std::atomic<uint32_t> head;   // written by the producer
+  uint32_t pad0[15];
+  std::atomic<uint32_t> tail;   // written by the consumer
+  uint32_t pad1[15];
+};
+static_assert(sizeof(Ctl) == 128, "memif Ctl");
+
+struct Desc {
+  uint32_t len;
+  uint32_t flags;
+};
+
+inline size_t region_bytes(uint32_t ring_size, uint32_t buf_size) {
+  return sizeof(Hdr) + 2 * sizeof(Ctl) + 2 * (size_t)ring_size * sizeof(Desc) + 2 * (size_t)ring_size * buf_size;
+}
+
+// A mapped region (either side).  `create` sizes and initialises it; otherwise it attaches.
+class Region {
+ public:
+  Region() = default;
+  Region(const std::string& path, bool create, uint32_t ring_size = 1024, uint32_t buf_size = 2048) { open(path, create, ring_size, buf_size); }
+  ~Region() { close(); }
+  Region(const Region&) = delete;
+  Region& operator=(const Region&) = delete;
+
+  void open(const std::string& path, bool create, uint32_t ring_size, uint32_t buf_size) {
+    if (create) {
+      if (ring_size < 2 || (ring_size & (ring_size - 1)) || ring_size > (1u << 20))
+        throw std::invalid_argument("memif: ring_size must be a power of two in [2, 2^20]");
+      if (buf_size < 64 || buf_size > (1u << 16) || (buf_size & 63))
+        throw std::invalid_argument("memif: buf_size must be a multiple of 64 in [64, 65536]");
+      fd_ = ::open(path.c_str(), O_RDWR | O_CREAT | O_TRUNC, 0600);
+      if (fd_ < 0) throw std::runtime_error("memif: cannot create " + path);
+      bytes_ = region_bytes(ring_size, buf_size);
+      if (ftruncate(fd_, (off_t)bytes_) != 0) { close(); throw std::runtime_error("memif: ftruncate " + path); }
+    } else {
+      fd_ = ::open(path.c_str(), O_RDWR);
+      if (fd_ < 0) throw std::runtime_error("memif: cannot open " + path);
+      struct stat st {};
+      if (fstat(fd_, &st) != 0 || (size_t)st.st_size < sizeof(Hdr)) { close(); throw std::runtime_error("memif: bad region " + path); }
+      bytes_ = (size_t)st.st_size;
+    }
+    // MAP_POPULATE: the page tables are filled now, not on the fast path (a first-touch fault
+    // costs ~1-2 us in a VM, i.e. more than the whole per-frame budget)
+    base_ = static_cast<uint8_t*>(mmap(nullptr, bytes_, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_POPULATE, fd_, 0));
+    if (base_ == MAP_FAILED) { base_ = nullptr; close(); throw std::runtime_error("memif: mmap " + path); }
+    if (create) {
+      std::memset(base_, 0, bytes_);   // allocates every page of the region up front
+      hdr()->version = kVersion;
+      hdr()->ring_size = ring_size;
+      hdr()->buf_size = buf_size;
+      std::atomic_thread_fence(std::memory_order_release);
+      hdr()->magic = kMagic;
+    } else if (hdr()->magic != kMagic || hdr()->version != kVersion ||
+               bytes_ < region_bytes(hdr()->ring_size, hdr()->buf_size)) {
+      close();
+      throw std::runtime_error("memif: " + path + " is not a memif region");
+    }
+    path_ = path;
+  }
+  void close() {
+    if (base_) munmap(base_, bytes_);
+    base_ = nullptr;
+    if (fd_ >= 0) ::close(fd_);
+    fd_ = -1;
+  }
+  bool is_open() const { return base_ != nullptr; }
+  const std::string& path() const { return path_; }
+  Hdr* hdr() const { return reinterpret_cast<Hdr*>(base_); }
+  uint32_t ring_size() const { return hdr()->ring_size; }
+  uint32_t mask() const { return hdr()->ring_size - 1; }
+  uint32_t buf_size() const { return hdr()->buf_size; }
+  Ctl* ctl(int r) const { return reinterpret_cast<Ctl*>(base_ + sizeof(Hdr)) + r; }
+  Desc* desc(int r) const {
+    return reinterpret_cast<Desc*>(base_ + sizeof(Hdr) + 2 * sizeof(Ctl)) + (size_t)r * ring_size();
+  }
+  uint8_t* buf(int r, uint32_t slot) const {
+    uint8_t* b0 = base_ + sizeof(Hdr) + 2 * sizeof(Ctl) + 2 * (size_t)ring_size() * sizeof(Desc);
+    return b0 + ((size_t)r * ring_size() + (slot & mask())) * buf_size();
+  }
+
+ private:
+  int fd_ = -1;
+  uint8_t* base_ = nullptr;
+  size_t bytes_ = 0;
+  std::string path_;
+};
+
+// Producer side of one ring: reserve -> fill buffer -> commit (batched head publication).
+struct Producer {
+  const Region* r = nullptr;
+  int ring = 0;
+  uint32_t head = 0;         // private copy (published with commit())
+  uint32_t tail_cache = 0;   // last tail seen
+  void init(const Region* reg, int rg) {
+    r = reg; ring = rg;
+    head = r->ctl(rg)->head.load(std::memory_order_relaxed);
+    tail_cache = r->ctl(rg)->tail.load(std::memory_order_acquire);
+  }
+  uint32_t room() {
+    if (head - tail_cache >= r->ring_size()) tail_cache = r->ctl(ring)->tail.load(std::memory_order_acquire);
+    return r->ring_size() - (head - tail_cache);
+  }
+  // Write one frame assembled from up to three pieces; false when the ring is full or the frame
+  // does not fit a buffer.
+  bool put(const uint8_t* a, uint32_t na, const uint8_t* b = nullptr, uint32_t nb = 0, const uint8_t* c = nullptr,
+           uint32_t nc = 0) {
+    const uint32_t n = na + nb + nc;
+    if (n > r->buf_size() || room() == 0) return false;
+    uint8_t* dst = r->buf(ring, head);
+    if (na) std::memcpy(dst, a, na);
+    if (nb) std::memcpy(dst + na, b, nb);
+    if (nc) std::memcpy(dst + na + nb, c, nc);
+    Desc& d = r->desc(ring)[head & r->mask()];
+    d.len = n;
+    d.flags = 0;
+    ++head;
+    return true;
+  }
+  void commit() { r->ctl(ring)->head.store(head, std::memory_order_release); }
+};
+
+// Consumer side of one ring.  `next` walks received frames; `release` hands slots back in order.
+struct Consumer {
+  const Region* r = nullptr;
+  int ring = 0;
+  uint32_t next = 0;         // next slot to read
+  uint32_t head_cache = 0;
+  void init(const Region* reg, int rg) {
+    r = reg; ring = rg;
+    next = r->ctl(rg)->tail.load(std::memory_order_relaxed);
+    head_cache = r->ctl(rg)->head.load(std::memory_order_acquire);
+  }
+  uint32_t available() {
+    if (head_cache == next) head_cache = r->ctl(ring)->head.load(std::memory_order_acquire);
+    return head_cache - next;
+  }
+  // Frame at the read cursor (valid until released); advances the cursor.
+  const uint8_t* get(uint32_t& len) {
+    const Desc& d = r->desc(ring)[next & r->mask()];
+    len = d.len < r->buf_size() ? d.len : r->buf_size();
+    const uint8_t* p = r->buf(ring, next);
+    ++next;
+    return p;
+  }
+  // Return every slot below `upto` to the producer.
+  void release_to(uint32_t upto) { r->ctl(ring)->tail.store(upto, std::memory_order_release); }
+};
+
+}  // namespace memif
+}  // namespace nfdp

@@ -98,6 +98,8 @@ class RingEngine {
   RingEngine& operator=(const RingEngine&) = delete;
 
   uint32_t capacity() const { return cap_; }
+  int device() const { return device_; }                 // HIP device the ring lives on
+  const FusedLaunch& launch() const { return launch_; }  // tables / counters / side buffers of the session
   bool running() const { return running_; }
   // The grid is still resident (false once every wave left: stop, or the device deadline passed).
   bool alive() const { return running_ && hipStreamQuery(stream_) == hipErrorNotReady; }
@@ -178,6 +180,8 @@ class RingEngine {
   uint32_t epoch_ = 0;            // current flow-table epoch (copy epoch_ & 1)
   uint64_t flip_prod_ = 0;        // packets published before the last flip
   bool running_ = false;
+  int device_ = 0;
+  FusedLaunch launch_{};
 };
 
 // Launch the persistent kernel (ring.hip).  Exposed for the engine only.

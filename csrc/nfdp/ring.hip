@@ -400,6 +400,7 @@ RingEngine::RingEngine(uint32_t capacity, int num_cus, int wgs_per_cu, bool coop
   if (capacity < 64 || (capacity & (capacity - 1)) || capacity > (1u << 24))
     throw std::invalid_argument("ring: capacity must be a power of two in [64, 2^24]");
   if (num_cus < 1 || wgs_per_cu < 1 || wgs_per_cu > 8) throw std::invalid_argument("ring: bad grid");
+  ck(hipGetDevice(&device_), "get device");
   // control line + completion flags: pinned, coherent (the GPU polls / writes them over PCIe)
   ck(hipHostMalloc(reinterpret_cast<void**>(&ctl_), sizeof(RingCtl), hipHostMallocCoherent | hipHostMallocMapped),
      "host alloc ctl");
@@ -460,6 +461,7 @@ void RingEngine::start(const FusedLaunch& f, const LaunchCfg& cfg, double deadli
   __atomic_store_n(&ctl_->prod, ring_word(prod_, epoch_), __ATOMIC_RELEASE);
   ck(hipMemcpyAsync(st_, &s, sizeof(s), hipMemcpyHostToDevice, stream_), "state upload");
   ck(hipStreamSynchronize(stream_), "state upload");  // `s` lives on this stack frame
+  launch_ = f;
   RingLaunch r;
   r.f = f;
   r.pkts = d_in_; r.inmeta = d_im_; r.out = d_out_; r.out_meta = d_meta_;

@@ -157,19 +157,28 @@ class DataPlane:
         (`_commit_flows_live`, no stall); any other change drains and stops the rings, updates the
         tables and relaunches them (their small tables are staged in LDS at launch)."""
         FAULTS.check("dataplane.commit")
-        rings = [r for r in getattr(self, "_rings", []) if r.running]
-        if rings and not full and self._only_flows_pending():
-            with TRACER.span("dataplane.commit_live"):
-                return self._commit_flows_live(rings)
-        for r in rings:
-            r.stop()
-        with TRACER.span("dataplane.commit", full=full):
-            sent = self._commit(full)
-        if rings:
-            _torch().cuda.current_stream(self.tdev).synchronize()
+        # native I/O engines (dataplane/native_io.py) feeding this data plane: nothing in flight
+        # while tables move, then they re-read the new tables
+        hooks = list(getattr(self, "_io_hooks", ()))
+        for h in hooks:
+            h.pre_commit(self)
+        try:
+            rings = [r for r in getattr(self, "_rings", []) if r.running]
+            if rings and not full and self._only_flows_pending():
+                with TRACER.span("dataplane.commit_live"):
+                    return self._commit_flows_live(rings)
             for r in rings:
-                r.resume()
-        return sent
+                r.stop()
+            with TRACER.span("dataplane.commit", full=full):
+                sent = self._commit(full)
+            if rings:
+                _torch().cuda.current_stream(self.tdev).synchronize()
+                for r in rings:
+                    r.resume()
+            return sent
+        finally:
+            for h in hooks:
+                h.post_commit(self)
 
     def _models(self):
         return (("ports", self.ports), ("chains", self.chains), ("macs", self.macs), ("lag", self.lag),

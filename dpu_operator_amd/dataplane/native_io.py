@@ -1,0 +1,296 @@
+"""Native live packet path: the C++ I/O engine (csrc/nfdp/iox.{h,cpp}) between vports and the data
+plane, with Python only configuring it.
+
+``netio.LivePath`` moves every frame through a Python loop (os.read / os.write per frame, header
+slots copied in Python).  ``NativeLivePath`` hands the same job to the native engine:
+
+    vports (memif shared-memory rings, AF_PACKET rings on veth ends, TAP fds)
+      -> engine rx thread: 64-B header slots + ingress meta straight into the pinned host slots of
+         the owner GPU's persistent ring kernel (RSS owner = owner_of(toeplitz(FlowKey), N))
+      -> engine tx thread per GPU: completion -> egress frames assembled from the rewritten header
+         and the payload still in the rx buffer; replicas / learn events / outer headers through
+         the side kernel; recirculation re-enters natively; slow-path frames come back here
+         (`on_punt`).
+
+One engine drives every data plane it is given: ``NativeLivePath([dp_gpu0, dp_gpu1, ...], ports)``
+steers each flow to its owner GPU (the flow table of a multi-GPU data plane is sharded the same
+way, dataplane/multi.py).  Without a GPU the backends are the bit-exact C++ oracle, so the whole
+native path is tested on CPU (tests/test_native_io.py).
+
+Table commits: the engine is paused around every commit of any of its data planes (no frame is
+in flight while tables move; ring kernels are drained / relaunched by the commit itself), then the
+oracle backends are re-pointed at the new tables and the side / tunnel / steering inputs refreshed.
+
+Health: a failed engine (a ring that stopped completing, an I/O error) sets ``error`` and
+``healthy = False``; with ``auto_restart`` the supervisor thread rebuilds the engine in place.
+"""
+from __future__ import annotations
+
+import logging
+import os
+import threading
+import time
+
+import numpy as np
+
+from . import tables as T
+
+log = logging.getLogger("dpu.native_io")
+
+SIDE_PORT_FLAGS = T.PORT_LEARN | T.PORT_ARP_TRAP | T.PORT_MIRROR
+
+
+class MemifVport:
+    """A shared-memory vport (csrc/nfdp/memif.h): the data plane owns the region file; the pod
+    (or NF) side attaches to `path` (nf.MemifEndpoint, the trafgen tool, a DPDK memif-style app)."""
+
+    def __init__(self, path: str, ring_size: int = 1024, buf_size: int = 2048):
+        self.path, self.ring_size, self.buf_size = path, int(ring_size), int(buf_size)
+
+    def make(self, nf):
+        return nf.MemifPort(self.path, self.ring_size, self.buf_size)
+
+
+class PacketVport:
+    """The VSP-side end of a veth pair, read and written through AF_PACKET TPACKET_V2 rings."""
+
+    def __init__(self, ifname: str, frames: int = 1024, frame_size: int = 2048):
+        self.ifname, self.frames, self.frame_size = ifname, int(frames), int(frame_size)
+
+    def make(self, nf):
+        return nf.PacketPort(self.ifname, self.frames, self.frame_size)
+
+
+def _make_port(nf, spec):
+    if hasattr(spec, "make"):
+        return spec.make(nf)
+    if hasattr(spec, "fd"):            # netio.TapPort and anything else with a packet fd
+        return nf.FdPort(int(spec.fd))
+    raise TypeError(f"unsupported vport {spec!r}")
+
+
+class NativeLivePath:
+    def __init__(self, dps, ports: dict, burst: int = 256, ring_capacity: int = 4096, inflight: int = 8,
+                 on_punt=None, auto_restart: bool = True):
+        from ..native import nfdp
+
+        self.nf = nfdp()
+        self.dps = list(dps) if isinstance(dps, (list, tuple)) else [dps]
+        if not self.dps:
+            raise ValueError("at least one data plane")
+        self.gpu = self.dps[0].gpu
+        if any(d.gpu != self.gpu for d in self.dps):
+            raise ValueError("data planes must all be GPU or all CPU")
+        if ring_capacity < 64 or ring_capacity & (ring_capacity - 1):
+            raise ValueError("ring_capacity must be a power of two >= 64")
+        self.burst, self.capacity, self.inflight = int(burst), int(ring_capacity), int(inflight)
+        self.specs = dict(ports)
+        self.on_punt = on_punt
+        self.auto_restart = auto_restart
+        self.error: str | None = None
+        self.healthy = True
+        self.restarts = 0
+        self._lock = threading.RLock()
+        self._eng = None
+        self._ports: dict[int, object] = {}
+        self._rings = []
+        self._backends = []
+        self._sup: threading.Thread | None = None
+        self._stop = threading.Event()
+        self._totals: dict[str, int] = {}
+        self.punts = 0
+
+    # ------------------------------------------------------------------ lifecycle
+    def start(self) -> "NativeLivePath":
+        with self._lock:
+            self._build()
+        self._stop.clear()
+        self._sup = threading.Thread(target=self._supervise, daemon=True, name="dpu-native-io")
+        self._sup.start()
+        return self
+
+    def _build(self) -> None:
+        nf = self.nf
+        eng = nf.IoEngine(self.burst, self.inflight)
+        self._rings, self._backends = [], []
+        for dp in self.dps:
+            if self.gpu:
+                import torch
+
+                from .ring import RingPath
+
+                with torch.cuda.device(dp.tdev):
+                    ring = RingPath(dp, capacity=self.capacity, host_slots=True, coop=True, side=True,
+                                    deadline_s=3600.0)
+                    ring.start()
+                self._rings.append(ring)
+                be = nf.GpuBackend(ring.eng)
+            else:
+                be = nf.OracleBackend(self.capacity)
+            self._backends.append(be)
+            eng.add_backend(be)
+            if self not in getattr(dp, "_io_hooks", []):
+                dp._io_hooks = getattr(dp, "_io_hooks", []) + [self]
+            dp._learned_on_device = True     # the engine learns into the device MAC table: commits pull first
+        for idx, spec in self.specs.items():
+            p = self._ports.get(idx)
+            if p is None:
+                p = self._ports[idx] = _make_port(nf, spec)
+            eng.add_port(int(idx), p)
+        self._eng = eng
+        self._refresh()
+        eng.start()
+
+    def stop(self) -> None:
+        self._stop.set()
+        if self._sup is not None:
+            self._sup.join(timeout=5)
+            self._sup = None
+        with self._lock:
+            self._teardown()
+        for dp in self.dps:
+            hooks = getattr(dp, "_io_hooks", [])
+            if self in hooks:
+                hooks.remove(self)
+
+    def _teardown(self) -> None:
+        if self._eng is not None:
+            self._accumulate()
+            self._eng.stop()
+            self._sync_stamps()
+        for r in self._rings:
+            r.close()
+        self._rings = []
+        self._eng = None
+
+    def _sync_stamps(self) -> None:
+        for dp, be in zip(self.dps, self._backends):
+            st = getattr(be, "stamp", None)
+            if st is not None:
+                dp.stamp = max(dp.stamp, int(st))
+
+    # ------------------------------------------------------------------ table commits (DataPlane hooks)
+    def pre_commit(self, dp) -> None:
+        if self._eng is not None and self._eng.running:
+            self._eng.pause()
+
+    def post_commit(self, dp) -> None:
+        if self._eng is None:
+            return
+        self._refresh()
+        self._eng.resume()
+
+    def _refresh(self) -> None:
+        """Point the oracle backends at the current tables; side ports, tunnel redirects, steering."""
+        eng = self._eng
+        for dp, be in zip(self.dps, self._backends):
+            if not self.gpu:
+                side = dp._side_buffers(self.capacity) if dp.side_active() else None
+                be.configure(dp.tables_ptrs(), dp._ptr("flow_ctr"), dp._ptr("port_ctr"), dp._ptr("drop_ctr"), side)
+        dp0 = self.dps[0]
+        a = dp0.ports.a
+        flags = a["flags"].astype(np.uint32)
+        eng.set_side_ports([int(i) for i in np.nonzero(flags & np.uint32(SIDE_PORT_FLAGS))[0]])
+        for i in np.nonzero(flags & np.uint32(T.PORT_TUNNEL))[0]:
+            tab = dp0.tunnels6 if flags[i] & T.PORT_TUNNEL6 else dp0.tunnels
+            lag = int(a[i]["lag"])
+            if lag < len(tab.a):
+                eng.set_redirect(int(i), int(tab.a[lag]["out_port"]))
+        if len(self.dps) > 1:
+            eng.set_steering(np.ascontiguousarray(a), bytes(dp0.rss_key))
+
+    # ------------------------------------------------------------------ ports
+    def add_port(self, idx: int, spec) -> None:
+        with self._lock:
+            self.specs[idx] = spec
+            p = self._ports[idx] = _make_port(self.nf, spec)
+            if self._eng is not None:
+                self._eng.add_port(int(idx), p)
+
+    def remove_port(self, idx: int):
+        with self._lock:
+            self.specs.pop(idx, None)
+            self._ports.pop(idx, None)
+            if self._eng is not None:
+                return self._eng.remove_port(int(idx))
+
+    def port(self, idx: int):
+        return self._ports.get(idx)
+
+    # ------------------------------------------------------------------ slow path + supervision
+    def poll_punts(self) -> int:
+        eng = self._eng
+        if eng is None:
+            return 0
+        n = 0
+        for frame, in_port, reason in eng.take_punts(1024):
+            n += 1
+            if reason == 14:        # IPv6-underlay tunnel to the local VTEP: the VNI needs the whole frame
+                r6 = self.dps[0].resolve_recirc6(frame)
+                if r6 is not None:
+                    eng.inject(int(r6[0]), bytes(r6[1]))
+                    continue
+                reason = 5
+            self.punts += 1
+            if self.on_punt is not None:
+                try:
+                    self.on_punt(frame, in_port, reason)
+                except Exception:  # noqa: BLE001 - a slow-path handler must not stop the path
+                    log.exception("punt handler failed")
+        return n
+
+    def _supervise(self) -> None:
+        while not self._stop.wait(0.005):
+            self.poll_punts()
+            eng = self._eng
+            if eng is None:
+                continue
+            err = eng.error()
+            if err:
+                self.error = err
+                self.healthy = False
+                log.error("native I/O engine failed: %s", err)
+                if not self.auto_restart:
+                    continue
+                with self._lock:
+                    try:
+                        self._teardown()
+                        self._build()
+                        self.restarts += 1
+                        self.healthy = True
+                        log.warning("native I/O engine restarted (%d)", self.restarts)
+                    except Exception as e:  # noqa: BLE001
+                        self.error = f"restart failed: {e}"
+                        log.exception("native I/O engine restart failed")
+                        time.sleep(0.5)
+
+    # ------------------------------------------------------------------ observability
+    def _accumulate(self) -> None:
+        if self._eng is None:
+            return
+        for k, v in self._eng.stats().items():
+            self._totals[k] = self._totals.get(k, 0) + int(v)
+
+    @property
+    def stats(self) -> dict:
+        s = dict(self._totals)
+        if self._eng is not None:
+            for k, v in self._eng.stats().items():
+                s[k] = s.get(k, 0) + int(v)
+        s["punt_handled"] = self.punts
+        s["restarts"] = self.restarts
+        return s
+
+    def latency_us(self) -> np.ndarray:
+        """Engine-side rx -> tx time of every burst since the last call (µs)."""
+        return np.asarray(self._eng.take_latency_us()) if self._eng is not None else np.zeros(0)
+
+    def fault(self, what: str = "injected") -> None:
+        """Test hook: make the engine fail as an I/O error would (the supervisor restarts it)."""
+        if self._eng is not None:
+            self._eng.inject_failure(what)
+
+
+def memif_dir() -> str:
+    d = os.environ.get("DPU_MEMIF_DIR") or ("/dev/shm" if os.path.isdir("/dev/shm") else "/tmp")
+    return d

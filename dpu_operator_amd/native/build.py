@@ -46,7 +46,7 @@ MODULES = {
     "_nfdp": {
         "dir": CSRC / "nfdp",
         "sources": ["kernels.hip", "shard.hip", "pktio.hip", "ring.hip", "ipsec.hip", "host.cpp", "shard_cpu.cpp",
-                    "ipsec_cpu.cpp", "bindings.cpp"],
+                    "ipsec_cpu.cpp", "iox.cpp", "bindings.cpp"],
         "hip": True,
     },
     "_agent": {

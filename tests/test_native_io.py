@@ -1,0 +1,212 @@
+"""Native I/O engine (csrc/nfdp/iox.{h,cpp}, dataplane/native_io.py): shared-memory vports ->
+C++ rx thread -> data plane (C++ oracle backend here; the persistent ring kernel on a GPU) -> C++
+tx thread -> vports.  Every test checks the frames that come out against the oracle run of the
+same frames assembled by ops/packets.assemble (the Python LivePath's rule), so the native path is
+bit-exact with the batch path."""
+import os
+import time
+
+import numpy as np
+import pytest
+
+from dpu_operator_amd.dataplane import scenario as S
+from dpu_operator_amd.dataplane import tables as T
+from dpu_operator_amd.dataplane.engine import DataPlane
+from dpu_operator_amd.dataplane.native_io import MemifVport, NativeLivePath, memif_dir
+from dpu_operator_amd.native import nfdp
+from dpu_operator_amd.ops import packets as P
+
+
+def _until(fn, t=5.0):
+    end = time.monotonic() + t
+    while time.monotonic() < end:
+        v = fn()
+        if v:
+            return v
+        time.sleep(0.002)
+    return fn()
+
+
+def _sfc(device, n_pods=4, n_flows=4096):
+    dp = DataPlane(device=device, flow_buckets=1 << 12)
+    sc = S.build_sfc(dp, n_pods=n_pods, n_flows=n_flows, n_acl=64, seed=0)
+    dp.commit(full=True)
+    return dp, sc
+
+
+@pytest.fixture
+def tmp_path():
+    """Regions on tmpfs (/dev/shm): a disk-backed MAP_SHARED file pays writeback faults."""
+    import shutil
+    import tempfile
+    from pathlib import Path
+
+    d = Path(tempfile.mkdtemp(prefix="dpu-iox-", dir=memif_dir()))
+    yield d
+    shutil.rmtree(d, ignore_errors=True)
+
+
+def _vports(tmp_path, n, tag="v"):
+    return {i: MemifVport(str(tmp_path / f"{tag}{i}"), ring_size=4096) for i in range(n)}
+
+
+def _expected(dp_ref, slots, im):
+    """Oracle run of the same frames: egress frames grouped by destination port."""
+    r = dp_ref.run(slots, im)
+    port, olen, reason = P.meta_fields(r.meta)
+    exp: dict[int, list[bytes]] = {}
+    lens = im >> 16
+    for i in np.nonzero(reason == 0)[0]:
+        f = P.assemble(r.out[i], int(r.meta[i]), slots[i], int(lens[i]))
+        exp.setdefault(int(port[i]), []).append(f)
+    return exp, int((reason != 0).sum())
+
+
+def test_memif_sfc_bit_exact_with_the_batch_path(tmp_path):
+    nf = nfdp()
+    dp, sc = _sfc("cpu")
+    ref, _ = _sfc("cpu")
+    slots, im = S.traffic(sc, 2000, seed=3)
+    exp, drops = _expected(ref, slots, im)
+    live = NativeLivePath(dp, _vports(tmp_path, sc.n_pods), burst=128, ring_capacity=1024).start()
+    try:
+        eps = {i: nf.MemifEndpoint(str(tmp_path / f"v{i}")) for i in range(sc.n_pods)}
+        src = im & 0xFFFF
+        for i in range(sc.n_pods):
+            fr = [bytes(slots[k, : int(im[k] >> 16)]) for k in np.nonzero(src == i)[0]]
+            sent = 0
+            while sent < len(fr):
+                sent += eps[i].send(fr[sent:])
+        got: dict[int, list[bytes]] = {i: [] for i in range(sc.n_pods)}
+
+        def drained():
+            for i in range(sc.n_pods):
+                got[i] += eps[i].recv()
+            return sum(map(len, got.values())) >= sum(map(len, exp.values()))
+
+        assert _until(drained), (live.stats, live.error)
+        for port, frames in exp.items():
+            assert sorted(got[port]) == sorted(frames), port
+        st = live.stats
+        assert st["rx"] == len(slots) and st["tx"] == len(slots) - drops and live.error is None
+        assert np.array_equal(dp.port_counters(), ref.port_counters())
+        dp.harvest(); ref.harvest()
+        assert np.array_equal(dp.flow_totals, ref.flow_totals)
+    finally:
+        live.stop()
+
+
+def test_trafgen_through_the_native_path(tmp_path):
+    """The C++ pod-side generator / sink (trafgen.h) drives all vports; every frame sent in the
+    measured window arrives, and one-way latencies come back."""
+    nf = nfdp()
+    dp, sc = _sfc("cpu")
+    live = NativeLivePath(dp, _vports(tmp_path, sc.n_pods, "t"), burst=256, ring_capacity=2048).start()
+    try:
+        pods = []
+        for i in range(sc.n_pods):
+            slots, im = S.traffic(sc, 256, seed=10 + i, src_pods=np.array([i]))
+            pods.append((str(tmp_path / f"t{i}"), slots, (im >> 16).astype(np.uint32)))
+        r = nf.trafgen_run(pods, duration_s=0.3, warmup_s=0.05, threads=2, inflight=256)
+        assert r["sent"] > 1000 and r["bad"] == 0
+        assert len(r["lat_us"]) and np.median(r["lat_us"]) > 0
+        # frames still in flight at the end of the window arrive afterwards: nothing is lost
+        eps = [nf.MemifEndpoint(p[0]) for p in pods]
+        late = [0]
+
+        def drained():
+            late[0] += sum(len(e.recv()) for e in eps)
+            return r["received"] + late[0] >= r["sent"]
+
+        _until(drained, 5.0)
+        assert r["received"] + late[0] + live.stats["tx_full"] >= r["sent"], (r["received"], late[0], live.stats)
+        assert live.error is None
+    finally:
+        live.stop()
+
+
+def test_flood_learn_and_arp_punt_native(tmp_path):
+    """OvS NORMAL through the native path: broadcast ARP flooded to every other member (primary +
+    replicas from the side pass), its copy punted to the slow path, the source MAC learned."""
+    nf = nfdp()
+    dp = DataPlane(device="cpu", flow_buckets=1 << 10, mac_slots=1 << 10)
+    for p in range(4):
+        dp.ports.set(p, flags=T.PORT_VALID | T.PORT_LEARN | T.PORT_ARP_TRAP, bridge_id=5)
+    dp.flood.set_members(5, [0, 1, 2, 3])
+    dp.commit(full=True)
+    punts = []
+    live = NativeLivePath(dp, _vports(tmp_path, 4, "f"), on_punt=lambda f, p, r: punts.append((p, r))).start()
+    try:
+        eps = {i: nf.MemifEndpoint(str(tmp_path / f"f{i}")) for i in range(4)}
+        arp, al = P.craft_arp(1, smac="02:00:00:00:0a:01", sender_ip=0x0A000001, target_ip=0x0A000002)
+        assert eps[0].send([bytes(arp[0, : al[0]])]) == 1
+        got = {}
+        assert _until(lambda: all(got.setdefault(i, []) or got[i].extend(eps[i].recv()) or got[i] for i in (1, 2, 3)))
+        assert all(g == [bytes(arp[0, : al[0]])] for g in (got[1], got[2], got[3]))
+        assert _until(lambda: punts) and punts[0] == (0, 12)
+        dp.pull_learned()
+        assert (5, "02:00:00:00:0a:01", 0) in dp.macs.learned()
+        assert live.stats["replicas"] == 2 and live.stats["side_passes"] >= 1
+    finally:
+        live.stop()
+
+
+def test_commit_under_traffic_and_failure_restart(tmp_path):
+    """Table commits while the engine runs (paused around each one), then an injected engine
+    failure: unhealthy, restarted by the supervisor, forwarding again."""
+    nf = nfdp()
+    dp, sc = _sfc("cpu")
+    live = NativeLivePath(dp, _vports(tmp_path, sc.n_pods, "c"), ring_capacity=1024).start()
+    try:
+        eps = {i: nf.MemifEndpoint(str(tmp_path / f"c{i}")) for i in range(sc.n_pods)}
+        slots, im = S.traffic(sc, 64, seed=4, src_pods=np.array([0]))
+        frames = [bytes(slots[k, : int(im[k] >> 16)]) for k in range(len(slots))]
+
+        def rx_all():
+            return sum(len(eps[i].recv()) for i in range(sc.n_pods))
+
+        for rnd in range(5):
+            eps[0].send(frames)
+            dp.ports.set_mtu(3, 1400 + rnd)       # a port-table change: a full commit mid-traffic
+            dp.commit()
+        seen = [0]
+        assert _until(lambda: seen.__setitem__(0, seen[0] + rx_all()) or seen[0] >= 5 * 64), (seen, live.stats)
+        live.fault("injected I/O failure")
+        assert _until(lambda: live.restarts >= 1), live.error
+        assert live.healthy and "injected" in (live.error or "")
+        eps[0].send(frames)
+        seen = [0]
+        assert _until(lambda: seen.__setitem__(0, seen[0] + rx_all()) or seen[0] >= 64), (seen, live.stats)
+    finally:
+        live.stop()
+
+
+@pytest.mark.gpu
+def test_native_path_gpu_ring_bit_exact(tmp_path):
+    """The GPU backend: header slots into the persistent ring kernel's pinned host slots."""
+    nf = nfdp()
+    dp, sc = _sfc("cuda")
+    ref, _ = _sfc("cpu")
+    slots, im = S.traffic(sc, 3000, seed=5)
+    exp, drops = _expected(ref, slots, im)
+    live = NativeLivePath(dp, _vports(tmp_path, sc.n_pods, "g"), burst=256, ring_capacity=4096).start()
+    try:
+        eps = {i: nf.MemifEndpoint(str(tmp_path / f"g{i}")) for i in range(sc.n_pods)}
+        src = im & 0xFFFF
+        for i in range(sc.n_pods):
+            fr = [bytes(slots[k, : int(im[k] >> 16)]) for k in np.nonzero(src == i)[0]]
+            sent = 0
+            while sent < len(fr):
+                sent += eps[i].send(fr[sent:])
+        got: dict[int, list[bytes]] = {i: [] for i in range(sc.n_pods)}
+
+        def drained():
+            for i in range(sc.n_pods):
+                got[i] += eps[i].recv()
+            return sum(map(len, got.values())) >= sum(map(len, exp.values()))
+
+        assert _until(drained, 10), (live.stats, live.error)
+        for port, frames in exp.items():
+            assert sorted(got[port]) == sorted(frames), port
+    finally:
+        live.stop()

@@ -1,0 +1,123 @@
+"""Live pod-to-pod benchmark of the native packet path (csrc/nfdp/iox + memif vports).
+
+Pods are shared-memory vports (csrc/nfdp/memif.h) driven by the C++ generator / sink
+(csrc/nfdp/trafgen.h: every frame carries its send time, so one-way pod -> pod latency is read on
+one clock).  Between them: the native I/O engine and the headline pipeline (1M flows, 256-rule
+ACL -> SNAT -> L2 steer) on the persistent ring kernel of the GPU, or the C++ oracle on the CPU
+(`--device cpu`, the comparator: same I/O engine, CPU pipeline).
+
+Measured, per device:
+  * `mpps`          : aggregate frames delivered per second with every pod sending as fast as its
+                      vport accepts (64-B frames, 8 pods, random pod -> pod flows);
+  * `p50/p99_us`    : one-way latency of that saturated run (queueing included);
+  * `idle_p50/p99`  : closed loop, one frame in flight (the unloaded pod -> pod latency);
+  * `half_p50/p99`  : offered load at half the measured maximum.
+
+    python tools/live_bench.py [--device cuda|cpu] [--duration 1.0] [--flows 1048576]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import shutil
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from dpu_operator_amd.dataplane import scenario as S  # noqa: E402
+from dpu_operator_amd.dataplane.engine import DataPlane  # noqa: E402
+from dpu_operator_amd.dataplane.native_io import MemifVport, NativeLivePath, memif_dir  # noqa: E402
+from dpu_operator_amd.native import nfdp  # noqa: E402
+
+
+def _pct(x, q):
+    return round(float(np.percentile(x, q)), 2) if len(x) else None
+
+
+def drain(nf, pods, live, quiet_s: float = 0.05, limit_s: float = 10.0) -> int:
+    """Let the engine deliver what the previous phase left queued; empty the pods' rx rings."""
+    eps = [nf.MemifEndpoint(p[0]) for p in pods]
+    n, last, t_end = 0, time.perf_counter(), time.perf_counter() + limit_s
+    prev = live.stats.get("tx", 0)
+    while time.perf_counter() < t_end:
+        k = sum(len(e.recv()) for e in eps)
+        cur = live.stats.get("tx", 0)
+        n += k
+        if k or cur != prev:
+            last, prev = time.perf_counter(), cur
+        elif time.perf_counter() - last > quiet_s:
+            break
+        time.sleep(0.002)
+    return n
+
+
+def run(device: str = "cuda", n_pods: int = 8, flows: int = 1 << 20, n_acl: int = 256, duration: float = 1.0,
+        threads: int = 4, burst: int = 512, inflight: int = 16, ring_capacity: int = 16384,
+        hash_mode: str = "lds") -> dict:
+    nf = nfdp()
+    t0 = time.perf_counter()
+    dp = DataPlane(device=device, flow_buckets=max(1 << 12, 1 << int(np.ceil(np.log2(max(flows, 1) / 2)))),
+                   hash_mode=hash_mode if device != "cpu" else "mfma")
+    sc = S.build_sfc(dp, n_pods=n_pods, n_flows=flows, n_acl=n_acl, seed=0)
+    dp.commit(full=True)
+    d = tempfile.mkdtemp(prefix="dpu-live-", dir=memif_dir())
+    ports = {int(sc.pod_port[i]): MemifVport(os.path.join(d, f"pod{i}"), ring_size=4096) for i in range(n_pods)}
+    live = NativeLivePath(dp, ports, burst=burst, ring_capacity=ring_capacity, inflight=inflight).start()
+    setup_s = time.perf_counter() - t0
+    try:
+        pods = []
+        for i in range(n_pods):
+            slots, im = S.traffic(sc, 4096, seed=100 + i, src_pods=np.array([i]))
+            pods.append((ports[int(sc.pod_port[i])].path, slots, (im >> 16).astype(np.uint32)))
+        out = {"device": device, "pods": n_pods, "flows": int(len(sc.keys)), "acl_rules": n_acl, "frame_bytes": 64,
+               "setup_s": round(setup_s, 1)}
+        # saturated: every pod as fast as its vport takes frames
+        r = nf.trafgen_run(pods, duration_s=duration, warmup_s=0.2, threads=threads, burst=32)
+        mpps = r["received"] / duration / 1e6
+        out.update(mpps=round(mpps, 3), offered_mpps=round(r["sent"] / duration / 1e6, 3),
+                   p50_us=_pct(r["lat_us"], 50), p99_us=_pct(r["lat_us"], 99))
+        drain(nf, pods, live)
+        # unloaded: closed loop, one frame in flight
+        r1 = nf.trafgen_run(pods, duration_s=min(duration, 0.5), warmup_s=0.05, threads=1, burst=1, inflight=1)
+        out.update(idle_p50_us=_pct(r1["lat_us"], 50), idle_p99_us=_pct(r1["lat_us"], 99),
+                   idle_frames=int(r1["received"]))
+        drain(nf, pods, live)
+        # half load
+        if mpps > 0:
+            r2 = nf.trafgen_run(pods, duration_s=min(duration, 0.5), warmup_s=0.1, threads=threads, burst=8,
+                                rate_pps=0.5 * mpps * 1e6)
+            out.update(half_load_mpps=round(r2["received"] / min(duration, 0.5) / 1e6, 3),
+                       half_p50_us=_pct(r2["lat_us"], 50), half_p99_us=_pct(r2["lat_us"], 99))
+        st = live.stats
+        out["engine"] = {k: int(v) for k, v in st.items() if k in ("rx", "tx", "drop", "bursts", "tx_full",
+                                                                    "side_passes", "punt", "rx_wait_tx")}
+        lat = live.latency_us()
+        out["engine_burst_p50_us"] = _pct(lat, 50)
+        out["error"] = live.error
+        return out
+    finally:
+        live.stop()
+        shutil.rmtree(d, ignore_errors=True)
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--device", default="cuda")
+    ap.add_argument("--duration", type=float, default=1.0)
+    ap.add_argument("--flows", type=int, default=1 << 20)
+    ap.add_argument("--pods", type=int, default=8)
+    ap.add_argument("--threads", type=int, default=4)
+    ap.add_argument("--burst", type=int, default=512)
+    ap.add_argument("--inflight", type=int, default=16)
+    a = ap.parse_args()
+    print(json.dumps(run(a.device, a.pods, a.flows, duration=a.duration, threads=a.threads, burst=a.burst,
+                         inflight=a.inflight)), flush=True)
+
+
+if __name__ == "__main__":
+    main()
