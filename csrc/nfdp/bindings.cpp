@@ -721,7 +721,8 @@ PYBIND11_MODULE(_nfdp, m) {
       })
       .def_readwrite("stamp", &OracleBackend::stamp);
   py::class_<Engine>(m, "IoEngine")
-      .def(py::init<uint32_t, uint32_t>(), py::arg("burst") = 256, py::arg("inflight") = 8)
+      .def(py::init<uint32_t, uint32_t, uint32_t>(), py::arg("burst") = 256, py::arg("inflight") = 64,
+           py::arg("tx_workers") = 1)
       .def("add_backend", &Engine::add_backend)
       .def("add_port", &Engine::add_port)
       .def("remove_port", &Engine::remove_port)

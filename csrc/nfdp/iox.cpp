@@ -387,8 +387,10 @@ void OracleBackend::side_pass(SideBatch& out) {
 }
 
 // ---------------------------------------------------------------------------------- Engine
-Engine::Engine(uint32_t burst, uint32_t inflight) : burst_(burst), inflight_(std::max<uint32_t>(inflight, 1)) {
+Engine::Engine(uint32_t burst, uint32_t inflight, uint32_t tx_workers)
+    : burst_(burst), inflight_(std::max<uint32_t>(inflight, 1)), workers_(std::max<uint32_t>(tx_workers, 1)) {
   if (burst_ < 1 || burst_ > (1u << 16)) throw std::invalid_argument("iox: burst in [1, 65536]");
+  if (workers_ > 16) throw std::invalid_argument("iox: at most 16 tx workers per backend");
   ports_ = std::make_shared<PortTab>((size_t)kMaxPorts + 2);
   redirect_.assign((size_t)kMaxPorts + 2, 0xFFFFFFFFu);
   side_ports_.assign((size_t)kMaxPorts + 2, 0);
@@ -406,6 +408,7 @@ void Engine::add_backend(std::shared_ptr<Backend> b) {
   if (run_) throw std::runtime_error("iox: add backends before start()");
   auto L = std::make_unique<Lane>();
   L->be = std::move(b);
+  L->slots.reset(new Burst[inflight_]);
   lanes_.push_back(std::move(L));
 }
 
@@ -479,15 +482,19 @@ void Engine::start() {
   }
   run_ = true;
   pause_ = false;
-  for (auto& L : lanes_) L->th = std::thread(&Engine::tx_loop, this, L.get());
+  for (auto& L : lanes_)
+    for (uint32_t w = 0; w < workers_; ++w) L->th.emplace_back(&Engine::tx_loop, this, L.get(), w);
   rx_th_ = std::thread(&Engine::rx_loop, this);
 }
 
 void Engine::stop() {
   const bool was = run_.exchange(false);
   if (rx_th_.joinable()) rx_th_.join();
-  for (auto& L : lanes_)
-    if (L->th.joinable()) L->th.join();
+  for (auto& L : lanes_) {
+    for (auto& t : L->th)
+      if (t.joinable()) t.join();
+    L->th.clear();
+  }
   (void)was;
 }
 
@@ -497,7 +504,7 @@ void Engine::pause() {
   const auto t0 = Clock::now();
   for (;;) {
     bool idle = paused_ack_.load();
-    for (auto& L : lanes_) idle = idle && L->n_inflight.load() == 0;
+    for (auto& L : lanes_) idle = idle && L->done.load() == L->head;
     if (idle || !run_) return;
     if (Clock::now() - t0 > std::chrono::seconds(10)) throw std::runtime_error("iox: pause timed out");
     std::this_thread::sleep_for(std::chrono::microseconds(20));
@@ -600,7 +607,7 @@ void Engine::rx_loop() {
       // the fullest lane (frames are steered after they are read)
       uint32_t take = burst_;
       for (auto& L : lanes_) {
-        if (!L->be->ready() || L->n_inflight.load(std::memory_order_acquire) >= inflight_) {
+        if (!L->be->ready() || L->head - L->done.load(std::memory_order_acquire) >= inflight_) {
           take = 0;
           st_wait_tx_.fetch_add(1, std::memory_order_relaxed);
           break;
@@ -654,10 +661,13 @@ void Engine::rx_loop() {
         const uint64_t start = be.published();
         uint32_t* im = be.in_meta();
         const uint32_t cmask = be.capacity() - 1;
-        Burst b;
+        Burst& b = L->slots[L->head % inflight_];   // free: head - done < inflight
         b.start = start;
         b.end = start + npad;
         b.t_rx_ns = t_rx;
+        b.side = false;
+        b.reps.clear();
+        b.xhdr.clear();
         for (uint32_t i = 0; i < k; ++i) {
           const Pkt& q = L->stage[i];
           uint8_t* slot = be.in_slot((uint32_t)(start + i));
@@ -670,11 +680,10 @@ void Engine::rx_loop() {
         for (uint32_t i = k; i < npad; ++i) im[(start + i) & cmask] = kRingPadMeta;
         b.pkts.swap(L->stage);
         L->stage.clear();
-        {
-          std::lock_guard<std::mutex> g(L->mu);
-          L->inflight.push_back(std::move(b));
-          L->n_inflight.fetch_add(1, std::memory_order_release);
-        }
+        b.id = L->head;
+        b.left.store(workers_, std::memory_order_relaxed);
+        b.state.store(1, std::memory_order_release);
+        ++L->head;
         const uint64_t tp0 = now_ns();
         be.publish(npad);
         st_pub_ns_.fetch_add(now_ns() - tp0, std::memory_order_relaxed);
@@ -687,7 +696,7 @@ void Engine::rx_loop() {
   }
 }
 
-void Engine::side_pass(Lane* L) {
+void Engine::side_pass(Lane* L, uint64_t from_id) {
   std::lock_guard<std::mutex> pg(L->pub_mu);   // no publish on this lane during the pass
   Backend& be = *L->be;
   const auto t0 = Clock::now();
@@ -698,40 +707,63 @@ void Engine::side_pass(Lane* L) {
   SideBatch sb;
   be.side_pass(sb);
   st_side_.fetch_add(1, std::memory_order_relaxed);
-  const uint32_t cmask = be.capacity() - 1;
-  for (auto& r : sb.reps) L->stash[r.src_pos & cmask].push_back(r);
-  if (!sb.xall.empty()) L->xall.swap(sb.xall);
+  // Every listed packet belongs to a burst not delivered yet (earlier bursts were covered by
+  // earlier passes): hand each replica / outer header to its burst, from_id .. head - 1.
+  const uint32_t cap = be.capacity();
+  auto burst_of = [&](uint32_t pos) -> Burst* {
+    for (uint64_t id = from_id; id < L->head; ++id) {
+      Burst& b = L->slots[id % inflight_];
+      if (((pos - (uint32_t)b.start) & (cap - 1)) < (uint32_t)b.pkts.size()) return &b;
+    }
+    return nullptr;
+  };
+  for (auto& r : sb.reps) {
+    Burst* b = burst_of(r.src_pos & (cap - 1));
+    if (b) b->reps.push_back(r);
+  }
+  if (!sb.xall.empty()) {
+    for (uint64_t id = from_id; id < L->head; ++id) {
+      Burst& b = L->slots[id % inflight_];
+      for (uint32_t i = 0; i < (uint32_t)b.pkts.size(); ++i) {
+        const uint32_t pos = (uint32_t)((b.start + i) & (cap - 1));
+        if (be.out_meta()[pos] & kMetaXhdr)
+          b.xhdr.emplace_back(pos, std::vector<uint8_t>(sb.xall.begin() + (size_t)pos * kXhdrBytes,
+                                                        sb.xall.begin() + (size_t)(pos + 1) * kXhdrBytes));
+      }
+    }
+  }
   L->side_upto = be.published();
 }
 
-void Engine::deliver(Lane* L, Burst& b) {
+void Engine::deliver(Lane* L, Burst& b, uint32_t w, std::vector<Port*>& touched) {
   Backend& be = *L->be;
   const uint32_t cmask = be.capacity() - 1;
   const uint32_t* om = be.out_meta();
   auto tab = std::atomic_load(&ports_);
-  std::vector<Port*> touched;
+  auto mine = [&](uint32_t port) {
+    if (port < redirect_.size() && redirect_[port] != 0xFFFFFFFFu) port = redirect_[port];
+    return port % workers_ == w;
+  };
   for (uint32_t i = 0; i < (uint32_t)b.pkts.size(); ++i) {
     const Pkt& q = b.pkts[i];
     const uint32_t pos = (uint32_t)((b.start + i) & cmask);
     const uint32_t meta = om[pos];
     const uint32_t reason = meta_reason(meta), oport = meta_port(meta), olen = meta_len(meta);
     if (reason == 0) {
+      if (!mine(oport)) continue;
       const uint8_t* x = nullptr;
       uint32_t xl = 0;
       if (meta & kMetaXhdr) {
-        if (L->xall.size() >= (size_t)(pos + 1) * kXhdrBytes) {
-          x = L->xall.data() + (size_t)pos * kXhdrBytes;
-          xl = xhdr_len(x);
-        } else {
-          st_drop_.fetch_add(1, std::memory_order_relaxed);   // no outer header: never sent bare
-          q.holder->complete(q.seq);
-          continue;
-        }
+        for (const auto& e : b.xhdr)
+          if (e.first == pos) { x = e.second.data(); xl = xhdr_len(x); break; }
+        if (!x) { st_drop_.fetch_add(1, std::memory_order_relaxed); continue; }   // never sent bare
       }
       uint32_t hl = 0, to = 0;
       out_tail(q.len, olen, xl, hl, to);
       if (to > q.len) to = q.len;
       send(*tab, oport, x, xl, be.out_slot(pos), hl, q.data + to, q.len - to, touched);
+    } else if (w != 0) {
+      continue;
     } else if (reason == kRecirc && olen <= q.len) {
       recirc_->push(oport, q.data + (q.len - olen), olen);   // terminated tunnel: the inner frame re-enters
       st_recirc_.fetch_add(1, std::memory_order_relaxed);
@@ -740,65 +772,74 @@ void Engine::deliver(Lane* L, Burst& b) {
     } else {
       st_drop_.fetch_add(1, std::memory_order_relaxed);
     }
-    auto it = L->stash.find(pos);
-    if (it != L->stash.end()) {
-      for (const Replica& r : it->second) {
-        uint32_t hl = 0, to = 0;
-        const uint32_t rlen = meta_len(r.meta), rr = meta_reason(r.meta);
-        out_tail(q.len, rlen, 0, hl, to);
-        if (to > q.len) to = q.len;
-        if (rr) {
-          punt(q.port, rr, r.hdr, hl, q.data + to, q.len - to);   // ARP trap: the slow path's copy
-        } else {
-          send(*tab, meta_port(r.meta), nullptr, 0, r.hdr, hl, q.data + to, q.len - to, touched);
-          st_reps_.fetch_add(1, std::memory_order_relaxed);
-        }
-      }
-      L->stash.erase(it);
-    }
-    q.holder->complete(q.seq);
   }
-  for (Port* p : touched) p->flush();
-  const double us = (double)(now_ns() - b.t_rx_ns) * 1e-3;
-  std::lock_guard<std::mutex> g(lat_mu_);
-  if (lat_us_.size() < (1u << 20)) lat_us_.push_back(us);
+  for (const Replica& r : b.reps) {
+    const uint32_t i = (uint32_t)((r.src_pos - (uint32_t)b.start) & cmask);
+    const Pkt& q = b.pkts[i];
+    uint32_t hl = 0, to = 0;
+    const uint32_t rlen = meta_len(r.meta), rr = meta_reason(r.meta);
+    out_tail(q.len, rlen, 0, hl, to);
+    if (to > q.len) to = q.len;
+    if (rr) {
+      if (w == 0) punt(q.port, rr, r.hdr, hl, q.data + to, q.len - to);   // ARP trap: the slow path's copy
+    } else if (mine(meta_port(r.meta))) {
+      send(*tab, meta_port(r.meta), nullptr, 0, r.hdr, hl, q.data + to, q.len - to, touched);
+      st_reps_.fetch_add(1, std::memory_order_relaxed);
+    }
+  }
 }
 
-void Engine::tx_loop(Lane* L) {
+void Engine::finish(Lane* L, Burst& b) {
+  for (const Pkt& q : b.pkts) q.holder->complete(q.seq);
+  const double us = (double)(now_ns() - b.t_rx_ns) * 1e-3;
+  {
+    std::lock_guard<std::mutex> g(lat_mu_);
+    if (lat_us_.size() < (1u << 20)) lat_us_.push_back(us);
+  }
+  b.pkts.clear();
+  b.reps.clear();
+  b.xhdr.clear();
+  b.state.store(0, std::memory_order_release);
+  L->done.fetch_add(1, std::memory_order_release);
+}
+
+void Engine::tx_loop(Lane* L, uint32_t w) {
   try {
     L->be->thread_init();
     const uint32_t cmask = L->be->capacity() - 1;
-    for (;;) {
-      Burst* b = nullptr;
-      {
-        std::lock_guard<std::mutex> g(L->mu);
-        if (!L->inflight.empty()) b = &L->inflight.front();
-      }
-      if (!b) {
-        if (!run_) break;
-        _mm_pause();
-        continue;
-      }
-      const auto t0 = Clock::now();
+    std::vector<Port*> touched;
+    for (uint64_t cur = 0;;) {
+      Burst& b = L->slots[cur % inflight_];
+      const uint32_t want = w == 0 ? 1u : 2u;
       uint32_t spin = 0;
-      while (L->be->completed() < b->end) {
+      while (!(b.state.load(std::memory_order_acquire) >= want && b.id == cur)) {
+        if (!run_ && L->done.load() == L->head) return;
         _mm_pause();
-        if ((++spin & 0xFFFu) == 0 && Clock::now() - t0 > std::chrono::seconds(5))
-          throw std::runtime_error("tx: burst not completed within 5 s (ring stopped?)");
+        if ((++spin & 0xFFFFu) == 0) std::this_thread::yield();
       }
-      bool side = b->side;
-      const uint32_t* om = L->be->out_meta();
-      for (uint64_t p = b->start; p < b->start + b->pkts.size() && !side; ++p)
-        side = (om[p & cmask] & (kMetaFlood | kMetaXhdr)) != 0;
-      if (side && b->end > L->side_upto) side_pass(L);
+      if (w == 0) {
+        // leader: completion, side pass, then the burst is ready for every worker
+        const auto t0 = Clock::now();
+        spin = 0;
+        while (L->be->completed() < b.end) {
+          _mm_pause();
+          if ((++spin & 0xFFFu) == 0 && Clock::now() - t0 > std::chrono::seconds(5))
+            throw std::runtime_error("tx: burst not completed within 5 s (ring stopped?)");
+        }
+        bool side = b.side;
+        const uint32_t* om = L->be->out_meta();
+        for (uint64_t p = b.start; p < b.start + b.pkts.size() && !side; ++p)
+          side = (om[p & cmask] & (kMetaFlood | kMetaXhdr)) != 0;
+        if (side && b.end > L->side_upto) side_pass(L, cur);
+        b.state.store(2, std::memory_order_release);
+      }
       const uint64_t td0 = now_ns();
-      deliver(L, *b);
+      touched.clear();
+      deliver(L, b, w, touched);
+      for (Port* p : touched) p->flush();
       st_deliver_ns_.fetch_add(now_ns() - td0, std::memory_order_relaxed);
-      {
-        std::lock_guard<std::mutex> g(L->mu);
-        L->inflight.pop_front();
-        L->n_inflight.fetch_sub(1, std::memory_order_release);
-      }
+      if (b.left.fetch_sub(1, std::memory_order_acq_rel) == 1) finish(L, b);
+      ++cur;
     }
   } catch (const std::exception& e) {
     fail(std::string("tx: ") + e.what());

@@ -260,7 +260,10 @@ struct Punt {
 
 class Engine {
  public:
-  Engine(uint32_t burst, uint32_t inflight_bursts);
+  // burst: frames per publish (at most); inflight: bursts in flight per backend; tx_workers:
+  // delivery threads per backend (each owns the egress ports with port % tx_workers == its index,
+  // so frames of one port leave in order)
+  Engine(uint32_t burst, uint32_t inflight_bursts, uint32_t tx_workers = 1);
   ~Engine();
   void add_backend(std::shared_ptr<Backend> b);       // index = GPU (shard) number
   void add_port(uint32_t id, std::shared_ptr<Port> p);
@@ -287,35 +290,39 @@ class Engine {
  private:
   struct Pkt { uint32_t port; uint32_t seq; const uint8_t* data; uint32_t len; Port* holder; };
   struct Burst {
-    uint64_t start, end;   // ring positions [start, start + n_pad)
+    uint64_t id = ~0ull;   // burst number on its lane (slot = id % inflight)
+    uint64_t start = 0, end = 0;   // ring positions [start, end)
     std::vector<Pkt> pkts;
     bool side = false;
-    uint64_t t_rx_ns;
+    uint64_t t_rx_ns = 0;
+    std::vector<Replica> reps;                                    // side-pass output for this burst
+    std::vector<std::pair<uint32_t, std::vector<uint8_t>>> xhdr;  // (position, outer-header record)
+    std::atomic<uint32_t> state{0};   // 0 free, 1 published, 2 ready to deliver (completed + side done)
+    std::atomic<uint32_t> left{0};    // delivery workers still working on it
   };
-  struct Lane {                 // one backend + its tx thread
+  struct Lane {                 // one backend + its delivery workers
     std::shared_ptr<Backend> be;
-    std::mutex mu;              // inflight queue
-    std::mutex pub_mu;          // rx thread's staging + publish vs the tx thread's side pass
-    std::deque<Burst> inflight;
-    std::atomic<uint32_t> n_inflight{0};
-    std::thread th;
+    std::mutex pub_mu;          // rx thread's staging + publish vs the leader's side pass
+    std::unique_ptr<Burst[]> slots;
+    uint64_t head = 0;          // rx thread: next burst id
+    std::atomic<uint64_t> done{0};   // bursts fully delivered (in order)
+    std::vector<std::thread> th;
     std::vector<Pkt> stage;     // rx thread: frames bound for this backend
-    std::unordered_map<uint32_t, std::vector<Replica>> stash;   // side results by source slot
-    std::vector<uint8_t> xall;  // outer-header records of the last side pass
-    uint64_t side_upto = 0;     // published count covered by the last side pass
+    uint64_t side_upto = 0;     // published count covered by the last side pass (leader only)
   };
   using PortTab = std::vector<std::shared_ptr<Port>>;
   void rx_loop();
-  void tx_loop(Lane* L);
-  void deliver(Lane* L, Burst& b);
-  void side_pass(Lane* L);
+  void tx_loop(Lane* L, uint32_t w);
+  void deliver(Lane* L, Burst& b, uint32_t w, std::vector<Port*>& touched);
+  void finish(Lane* L, Burst& b);
+  void side_pass(Lane* L, uint64_t from_id);
   bool needs_side(uint32_t in_port) const;
   void send(const PortTab& tab, uint32_t port, const uint8_t* x, uint32_t nx, const uint8_t* h, uint32_t nh,
             const uint8_t* t, uint32_t nt, std::vector<Port*>& touched);
   void punt(uint32_t in_port, uint32_t reason, const uint8_t* a, uint32_t na, const uint8_t* b, uint32_t nb);
   void fail(const std::string& what);
 
-  uint32_t burst_, inflight_;
+  uint32_t burst_, inflight_, workers_;
   std::vector<std::unique_ptr<Lane>> lanes_;
   mutable std::mutex ports_mu_;
   std::shared_ptr<const PortTab> ports_;              // copy-on-write snapshot, by port id

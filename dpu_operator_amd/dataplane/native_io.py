@@ -70,8 +70,8 @@ def _make_port(nf, spec):
 
 
 class NativeLivePath:
-    def __init__(self, dps, ports: dict, burst: int = 256, ring_capacity: int = 4096, inflight: int = 8,
-                 on_punt=None, auto_restart: bool = True):
+    def __init__(self, dps, ports: dict, burst: int = 256, ring_capacity: int = 4096, inflight: int = 64,
+                 on_punt=None, auto_restart: bool = True, tx_workers: int = 2):
         from ..native import nfdp
 
         self.nf = nfdp()
@@ -84,6 +84,7 @@ class NativeLivePath:
         if ring_capacity < 64 or ring_capacity & (ring_capacity - 1):
             raise ValueError("ring_capacity must be a power of two >= 64")
         self.burst, self.capacity, self.inflight = int(burst), int(ring_capacity), int(inflight)
+        self.tx_workers = int(tx_workers)
         self.specs = dict(ports)
         self.on_punt = on_punt
         self.auto_restart = auto_restart
@@ -111,7 +112,7 @@ class NativeLivePath:
 
     def _build(self) -> None:
         nf = self.nf
-        eng = nf.IoEngine(self.burst, self.inflight)
+        eng = nf.IoEngine(self.burst, self.inflight, self.tx_workers)
         self._rings, self._backends = [], []
         for dp in self.dps:
             if self.gpu:

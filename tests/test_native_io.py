@@ -62,13 +62,14 @@ def _expected(dp_ref, slots, im):
     return exp, int((reason != 0).sum())
 
 
-def test_memif_sfc_bit_exact_with_the_batch_path(tmp_path):
+@pytest.mark.parametrize("workers", [1, 3])
+def test_memif_sfc_bit_exact_with_the_batch_path(tmp_path, workers):
     nf = nfdp()
     dp, sc = _sfc("cpu")
     ref, _ = _sfc("cpu")
     slots, im = S.traffic(sc, 2000, seed=3)
     exp, drops = _expected(ref, slots, im)
-    live = NativeLivePath(dp, _vports(tmp_path, sc.n_pods), burst=128, ring_capacity=1024).start()
+    live = NativeLivePath(dp, _vports(tmp_path, sc.n_pods), burst=128, ring_capacity=1024, tx_workers=workers).start()
     try:
         eps = {i: nf.MemifEndpoint(str(tmp_path / f"v{i}")) for i in range(sc.n_pods)}
         src = im & 0xFFFF
@@ -125,11 +126,12 @@ def test_trafgen_through_the_native_path(tmp_path):
         live.stop()
 
 
-def test_flood_learn_and_arp_punt_native(tmp_path):
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+def test_flood_learn_and_arp_punt_native(tmp_path, device):
     """OvS NORMAL through the native path: broadcast ARP flooded to every other member (primary +
     replicas from the side pass), its copy punted to the slow path, the source MAC learned."""
     nf = nfdp()
-    dp = DataPlane(device="cpu", flow_buckets=1 << 10, mac_slots=1 << 10)
+    dp = DataPlane(device=device, flow_buckets=1 << 10, mac_slots=1 << 10)
     for p in range(4):
         dp.ports.set(p, flags=T.PORT_VALID | T.PORT_LEARN | T.PORT_ARP_TRAP, bridge_id=5)
     dp.flood.set_members(5, [0, 1, 2, 3])

@@ -57,8 +57,8 @@ def drain(nf, pods, live, quiet_s: float = 0.05, limit_s: float = 10.0) -> int:
 
 
 def run(device: str = "cuda", n_pods: int = 8, flows: int = 1 << 20, n_acl: int = 256, duration: float = 1.0,
-        threads: int = 4, burst: int = 512, inflight: int = 16, ring_capacity: int = 16384,
-        hash_mode: str = "lds") -> dict:
+        threads: int = 4, burst: int = 512, inflight: int = 192, ring_capacity: int = 16384,
+        hash_mode: str = "lds", tx_workers: int = 2) -> dict:
     nf = nfdp()
     t0 = time.perf_counter()
     dp = DataPlane(device=device, flow_buckets=max(1 << 12, 1 << int(np.ceil(np.log2(max(flows, 1) / 2)))),
@@ -67,14 +67,15 @@ def run(device: str = "cuda", n_pods: int = 8, flows: int = 1 << 20, n_acl: int 
     dp.commit(full=True)
     d = tempfile.mkdtemp(prefix="dpu-live-", dir=memif_dir())
     ports = {int(sc.pod_port[i]): MemifVport(os.path.join(d, f"pod{i}"), ring_size=4096) for i in range(n_pods)}
-    live = NativeLivePath(dp, ports, burst=burst, ring_capacity=ring_capacity, inflight=inflight).start()
+    live = NativeLivePath(dp, ports, burst=burst, ring_capacity=ring_capacity, inflight=inflight,
+                          tx_workers=tx_workers).start()
     setup_s = time.perf_counter() - t0
     try:
         pods = []
         for i in range(n_pods):
             slots, im = S.traffic(sc, 4096, seed=100 + i, src_pods=np.array([i]))
             pods.append((ports[int(sc.pod_port[i])].path, slots, (im >> 16).astype(np.uint32)))
-        out = {"device": device, "pods": n_pods, "flows": int(len(sc.keys)), "acl_rules": n_acl, "frame_bytes": 64,
+        out = {"device": device, "tx_workers": tx_workers, "inflight_bursts": inflight, "pods": n_pods, "flows": int(len(sc.keys)), "acl_rules": n_acl, "frame_bytes": 64,
                "setup_s": round(setup_s, 1)}
         # saturated: every pod as fast as its vport takes frames
         r = nf.trafgen_run(pods, duration_s=duration, warmup_s=0.2, threads=threads, burst=32)
@@ -113,10 +114,11 @@ def main() -> None:
     ap.add_argument("--pods", type=int, default=8)
     ap.add_argument("--threads", type=int, default=4)
     ap.add_argument("--burst", type=int, default=512)
-    ap.add_argument("--inflight", type=int, default=16)
+    ap.add_argument("--inflight", type=int, default=192)
+    ap.add_argument("--tx-workers", type=int, default=2)
     a = ap.parse_args()
     print(json.dumps(run(a.device, a.pods, a.flows, duration=a.duration, threads=a.threads, burst=a.burst,
-                         inflight=a.inflight)), flush=True)
+                         inflight=a.inflight, tx_workers=a.tx_workers)), flush=True)
 
 
 if __name__ == "__main__":
