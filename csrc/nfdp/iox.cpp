@@ -482,6 +482,7 @@ void Engine::start() {
   }
   run_ = true;
   pause_ = false;
+  for (auto& L : lanes_) L->freed_pos.store(L->be->published());
   for (auto& L : lanes_)
     for (uint32_t w = 0; w < workers_; ++w) L->th.emplace_back(&Engine::tx_loop, this, L.get(), w);
   rx_th_ = std::thread(&Engine::rx_loop, this);
@@ -612,7 +613,8 @@ void Engine::rx_loop() {
           st_wait_tx_.fetch_add(1, std::memory_order_relaxed);
           break;
         }
-        const uint64_t used = L->be->published() - L->be->completed();
+        // slots are reusable once DELIVERED (their out slot / meta read), not merely completed
+        const uint64_t used = L->be->published() - L->freed_pos.load(std::memory_order_acquire);
         const uint64_t room = L->be->capacity() > used ? L->be->capacity() - used : 0;
         take = (uint32_t)std::min<uint64_t>(take, room & ~63ull);
       }
@@ -799,6 +801,7 @@ void Engine::finish(Lane* L, Burst& b) {
   b.pkts.clear();
   b.reps.clear();
   b.xhdr.clear();
+  L->freed_pos.store(b.end, std::memory_order_release);
   b.state.store(0, std::memory_order_release);
   L->done.fetch_add(1, std::memory_order_release);
 }

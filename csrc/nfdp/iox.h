@@ -306,6 +306,7 @@ class Engine {
     std::unique_ptr<Burst[]> slots;
     uint64_t head = 0;          // rx thread: next burst id
     std::atomic<uint64_t> done{0};   // bursts fully delivered (in order)
+    std::atomic<uint64_t> freed_pos{0};   // ring position below which every slot is delivered (reusable)
     std::vector<std::thread> th;
     std::vector<Pkt> stage;     // rx thread: frames bound for this backend
     uint64_t side_upto = 0;     // published count covered by the last side pass (leader only)
