@@ -631,7 +631,7 @@ PYBIND11_MODULE(_nfdp, m) {
       .def("stop", [](RingEngine& r, double timeout_s) { py::gil_scoped_release nogil; r.stop(timeout_s); },
            py::arg("timeout_s") = 30.0)
       .def("completed", &RingEngine::completed)
-      .def("publish", &RingEngine::publish)
+      .def("publish", &RingEngine::publish, py::arg("n"), py::arg("check_room") = true)
       .def("wait", [](RingEngine& r, uint64_t end, double timeout_s) {
         py::gil_scoped_release nogil;
         return r.wait(end, timeout_s);

@@ -570,15 +570,16 @@ void Engine::punt(uint32_t in_port, uint32_t reason, const uint8_t* a, uint32_t 
 }
 
 void Engine::send(const PortTab& tab, uint32_t port, const uint8_t* x, uint32_t nx, const uint8_t* h, uint32_t nh,
-                  const uint8_t* t, uint32_t nt, std::vector<Port*>& touched) {
+                  const uint8_t* t, uint32_t nt, std::vector<Port*>& touched, TxTally& tally) {
   if (port < redirect_.size() && redirect_[port] != 0xFFFFFFFFu) port = redirect_[port];   // tunnel -> underlay
   Port* p = port < tab.size() ? tab[port].get() : nullptr;
-  if (!p) { st_no_port_.fetch_add(1, std::memory_order_relaxed); return; }
+  if (!p) { ++tally.no_port; return; }
   if (p->tx(x, nx, h, nh, t, nt)) {
-    st_tx_.fetch_add(1, std::memory_order_relaxed);
-    if (std::find(touched.begin(), touched.end(), p) == touched.end()) touched.push_back(p);
+    ++tally.tx;
+    if (touched.empty() || touched.back() != p)
+      if (std::find(touched.begin(), touched.end(), p) == touched.end()) touched.push_back(p);
   } else {
-    st_tx_full_.fetch_add(1, std::memory_order_relaxed);
+    ++tally.full;
   }
 }
 
@@ -746,7 +747,14 @@ void Engine::deliver(Lane* L, Burst& b, uint32_t w, std::vector<Port*>& touched)
     if (port < redirect_.size() && redirect_[port] != 0xFFFFFFFFu) port = redirect_[port];
     return port % workers_ == w;
   };
-  for (uint32_t i = 0; i < (uint32_t)b.pkts.size(); ++i) {
+  TxTally tally;
+  const uint32_t np = (uint32_t)b.pkts.size();
+  constexpr uint32_t kAhead = 8;   // out slots / payloads of later packets are fetched ahead
+  for (uint32_t i = 0; i < np; ++i) {
+    if (i + kAhead < np) {
+      const uint32_t pa = (uint32_t)((b.start + i + kAhead) & cmask);
+      if (meta_port(om[pa]) % workers_ == w) __builtin_prefetch(be.out_slot(pa), 0, 0);
+    }
     const Pkt& q = b.pkts[i];
     const uint32_t pos = (uint32_t)((b.start + i) & cmask);
     const uint32_t meta = om[pos];
@@ -758,12 +766,12 @@ void Engine::deliver(Lane* L, Burst& b, uint32_t w, std::vector<Port*>& touched)
       if (meta & kMetaXhdr) {
         for (const auto& e : b.xhdr)
           if (e.first == pos) { x = e.second.data(); xl = xhdr_len(x); break; }
-        if (!x) { st_drop_.fetch_add(1, std::memory_order_relaxed); continue; }   // never sent bare
+        if (!x) { ++tally.drop; continue; }   // never sent bare
       }
       uint32_t hl = 0, to = 0;
       out_tail(q.len, olen, xl, hl, to);
       if (to > q.len) to = q.len;
-      send(*tab, oport, x, xl, be.out_slot(pos), hl, q.data + to, q.len - to, touched);
+      send(*tab, oport, x, xl, be.out_slot(pos), hl, q.data + to, q.len - to, touched, tally);
     } else if (w != 0) {
       continue;
     } else if (reason == kRecirc && olen <= q.len) {
@@ -772,7 +780,7 @@ void Engine::deliver(Lane* L, Burst& b, uint32_t w, std::vector<Port*>& touched)
     } else if (reason == kRecirc6) {
       punt(q.port, reason, q.data, q.len, nullptr, 0);       // the VNI lookup needs the whole frame
     } else {
-      st_drop_.fetch_add(1, std::memory_order_relaxed);
+      ++tally.drop;
     }
   }
   for (const Replica& r : b.reps) {
@@ -785,10 +793,16 @@ void Engine::deliver(Lane* L, Burst& b, uint32_t w, std::vector<Port*>& touched)
     if (rr) {
       if (w == 0) punt(q.port, rr, r.hdr, hl, q.data + to, q.len - to);   // ARP trap: the slow path's copy
     } else if (mine(meta_port(r.meta))) {
-      send(*tab, meta_port(r.meta), nullptr, 0, r.hdr, hl, q.data + to, q.len - to, touched);
-      st_reps_.fetch_add(1, std::memory_order_relaxed);
+      send(*tab, meta_port(r.meta), nullptr, 0, r.hdr, hl, q.data + to, q.len - to, touched, tally);
+      ++tally.reps;
     }
   }
+  // one atomic per counter per burst (per-packet atomics on shared lines cost more than the copy)
+  if (tally.tx) st_tx_.fetch_add(tally.tx, std::memory_order_relaxed);
+  if (tally.full) st_tx_full_.fetch_add(tally.full, std::memory_order_relaxed);
+  if (tally.no_port) st_no_port_.fetch_add(tally.no_port, std::memory_order_relaxed);
+  if (tally.drop) st_drop_.fetch_add(tally.drop, std::memory_order_relaxed);
+  if (tally.reps) st_reps_.fetch_add(tally.reps, std::memory_order_relaxed);
 }
 
 void Engine::finish(Lane* L, Burst& b) {
@@ -824,10 +838,14 @@ void Engine::tx_loop(Lane* L, uint32_t w) {
         // leader: completion, side pass, then the burst is ready for every worker
         const auto t0 = Clock::now();
         spin = 0;
-        while (L->be->completed() < b.end) {
+        while (!L->be->range_done(b.start, b.end)) {
           _mm_pause();
-          if ((++spin & 0xFFFu) == 0 && Clock::now() - t0 > std::chrono::seconds(5))
-            throw std::runtime_error("tx: burst not completed within 5 s (ring stopped?)");
+          if ((++spin & 0xFFFu) == 0) {
+            const auto waited = Clock::now() - t0;
+            if (waited > std::chrono::milliseconds(200) && !L->be->alive())
+              throw std::runtime_error("tx: the ring kernel is gone (device deadline or fault)");
+            if (waited > std::chrono::seconds(5)) throw std::runtime_error("tx: burst not completed within 5 s");
+          }
         }
         bool side = b.side;
         const uint32_t* om = L->be->out_meta();

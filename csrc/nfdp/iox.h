@@ -60,7 +60,9 @@ class Port {
   void complete(uint32_t seq) { done_[seq & mask_].store(1, std::memory_order_release); }
   void reclaim();
   virtual std::string kind() const = 0;
-  std::atomic<uint64_t> rx_pkts{0}, tx_pkts{0}, tx_full{0}, rx_bytes{0}, tx_bytes{0};
+  // rx counters (rx thread) and tx counters (one delivery worker per port) on separate lines
+  alignas(64) std::atomic<uint64_t> rx_pkts{0}, rx_bytes{0};
+  alignas(64) std::atomic<uint64_t> tx_pkts{0}, tx_full{0}, tx_bytes{0};
 
  protected:
   virtual bool tx_locked(const uint8_t* a, uint32_t na, const uint8_t* b, uint32_t nb, const uint8_t* c, uint32_t nc) = 0;
@@ -186,7 +188,9 @@ class Backend {
   virtual uint64_t published() = 0;
   virtual uint64_t publish(uint32_t n) = 0;        // multiple of 64
   virtual uint64_t completed() = 0;
+  virtual bool range_done(uint64_t start, uint64_t end) = 0;   // positions [start, end) processed
   virtual bool ready() = 0;                         // can take a publish now (ring running)
+  virtual bool alive() { return true; }             // the pipeline still makes progress (slow check)
   // Side pass over every completed slot the pipeline listed since the last pass (call only when
   // completed() == published(): nothing is in flight).
   virtual void side_pass(SideBatch& out) = 0;
@@ -203,9 +207,11 @@ class GpuBackend : public Backend {
   const uint8_t* out_slot(uint32_t pos) override { return out_ + (size_t)(pos & (capacity() - 1)) * kSlotBytes; }
   const uint32_t* out_meta() override { return om_; }
   uint64_t published() override { return ring_->published(); }
-  uint64_t publish(uint32_t n) override { return ring_->publish(n); }
+  uint64_t publish(uint32_t n) override { return ring_->publish(n, false); }
   uint64_t completed() override { return ring_->completed(); }
-  bool ready() override { return ring_->running() && ring_->alive(); }
+  bool range_done(uint64_t start, uint64_t end) override { return ring_->range_done(start, end); }
+  bool ready() override { return ring_->running(); }
+  bool alive() override { return ring_->alive(); }
   void side_pass(SideBatch& out) override;
   void thread_init() override;
   uint32_t stamp = 1;
@@ -228,6 +234,7 @@ class OracleBackend : public Backend {
   uint64_t published() override { return prod_; }
   uint64_t publish(uint32_t n) override;
   uint64_t completed() override { return prod_; }
+  bool range_done(uint64_t, uint64_t end) override { return end <= prod_; }
   bool ready() override { return configured_; }
   void side_pass(SideBatch& out) override;
   // tables / counters / side buffers of the CPU DataPlane (replaced after every commit, while
@@ -318,8 +325,9 @@ class Engine {
   void finish(Lane* L, Burst& b);
   void side_pass(Lane* L, uint64_t from_id);
   bool needs_side(uint32_t in_port) const;
+  struct TxTally { uint64_t tx = 0, full = 0, no_port = 0, drop = 0, reps = 0; };
   void send(const PortTab& tab, uint32_t port, const uint8_t* x, uint32_t nx, const uint8_t* h, uint32_t nh,
-            const uint8_t* t, uint32_t nt, std::vector<Port*>& touched);
+            const uint8_t* t, uint32_t nt, std::vector<Port*>& touched, TxTally& tally);
   void punt(uint32_t in_port, uint32_t reason, const uint8_t* a, uint32_t na, const uint8_t* b, uint32_t nb);
   void fail(const std::string& what);
 

@@ -126,7 +126,14 @@ class RingEngine {
   uint64_t completed();  // packets whose chunks all completed (in order)
   // Publish n packets (multiple of 64) starting at ring position published() % capacity.
   // Throws if the ring lacks room (producer must wait for completions).
-  uint64_t publish(uint32_t n);
+  uint64_t publish(uint32_t n, bool check_room = true);
+  // Every chunk of ring positions [start, end) completed (lock-free flag reads; chunks complete
+  // out of order across waves, so this looks at each of them).
+  bool range_done(uint64_t start, uint64_t end) const {
+    for (uint64_t c = start / 64; c < (end + 63) / 64; ++c)
+      if (!chunk_done(c)) return false;
+    return true;
+  }
   // Spin until every chunk below `end` completed; false on timeout.
   bool wait(uint64_t end, double timeout_s);
 

@@ -509,12 +509,14 @@ uint64_t RingEngine::completed() {
   return floor_ * 64;
 }
 
-uint64_t RingEngine::publish(uint32_t n) {
+uint64_t RingEngine::publish(uint32_t n, bool check_room) {
   if (!running_) throw std::runtime_error("ring: not running");
   if (n == 0 || (n & 63u)) throw std::invalid_argument("ring: publish a positive multiple of 64 packets");
-  const uint64_t done = completed();
+  // check_room = false: the producer tracks slot reuse itself (the native I/O engine frees slots
+  // only after it has read their results, a stricter bound than completion)
+  const uint64_t done = completed();   // also keeps the in-order floor current (amortised scan)
   std::lock_guard<std::mutex> g(mu_);
-  if (prod_ + n - done > cap_) throw std::runtime_error("ring: no room (wait for completions)");
+  if (check_room && prod_ + n - done > cap_) throw std::runtime_error("ring: no room (wait for completions)");
   prod_ += n;
   __atomic_store_n(&ctl_->prod, ring_word(prod_, epoch_), __ATOMIC_RELEASE);
   return prod_;

@@ -159,10 +159,16 @@ class NativeLivePath:
             self._accumulate()
             self._eng.stop()
             self._sync_stamps()
+        errs = []
         for r in self._rings:
-            r.close()
+            try:
+                r.close()
+            except Exception as e:  # noqa: BLE001 - close every ring, report the first failure
+                errs.append(e)
         self._rings = []
         self._eng = None
+        if errs:
+            raise errs[0]
 
     def _sync_stamps(self) -> None:
         for dp, be in zip(self.dps, self._backends):

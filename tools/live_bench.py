@@ -101,8 +101,14 @@ def run(device: str = "cuda", n_pods: int = 8, flows: int = 1 << 20, n_acl: int 
         out["engine_burst_p50_us"] = _pct(lat, 50)
         out["error"] = live.error
         return out
+    except BaseException:
+        print(json.dumps({"error": live.error, "stats": {k: int(v) for k, v in live.stats.items()}}), file=sys.stderr)
+        raise
     finally:
-        live.stop()
+        try:
+            live.stop()
+        except Exception as e:  # noqa: BLE001 - report, the measurement above stands
+            print(f"stop: {e}", file=sys.stderr)
         shutil.rmtree(d, ignore_errors=True)
 
 
