@@ -57,6 +57,8 @@ def parse():
     ap.add_argument("--rotate", type=int, default=4)
     ap.add_argument("--no-lowlat", action="store_true", help="skip the small-batch latency probe")
     ap.add_argument("--no-variants", action="store_true", help="skip the mixed / ACL1024 / IMIX measurements")
+    ap.add_argument("--no-live", action="store_true", help="skip the live pod-to-pod (native I/O engine) block")
+    ap.add_argument("--live-workers", type=int, default=8, help="native I/O engine delivery threads")
     ap.add_argument("--variant-steps", type=int, default=30)
     ap.add_argument("--chunks", type=int, default=4, help="pipeline chunks per step (N > 1)")
     ap.add_argument("--mode", default="rss", choices=["rss", "replicated", "sharded"],
@@ -449,6 +451,23 @@ def main() -> None:
     if world == 1 and a.io == "device" and not a.no_variants:
         variants = measure_variants(a, dp, sc, dev, torch, S, P)
 
+    # live pod -> pod path (1 GPU, after the timed region): shared-memory pod vports, the native C++
+    # I/O engine (csrc/nfdp/iox) and the persistent ring kernel; C++ pod generator / sinks measure
+    # delivered Mpps and one-way latency on one clock (tools/live_bench.py)
+    live = None
+    if world == 1 and a.io == "device" and not a.no_live:
+        try:
+            import importlib.util
+
+            spec = importlib.util.spec_from_file_location(
+                "live_bench", os.path.join(os.path.dirname(os.path.abspath(__file__)), "tools", "live_bench.py"))
+            lb = importlib.util.module_from_spec(spec)
+            spec.loader.exec_module(lb)
+            live = lb.run(device=str(dev), n_pods=a.pods_per_gpu, flows=a.flows, n_acl=a.acl, duration=0.5,
+                          threads=6, tx_workers=a.live_workers, hash_mode=a.hash)
+        except Exception as ex:  # the headline number must still be reported
+            live = {"error": str(ex)[:200]}
+
     total_pkts = world * a.batch * a.steps
     mpps = total_pkts / elapsed / 1e6
     if rank == 0:
@@ -492,6 +511,9 @@ def main() -> None:
             "value_l3": None if not variants else variants["l3_mpps"],
             "imix": None if not variants else variants["imix"],
             "variants": variants,
+            # live pod -> pod through the native I/O engine + ring kernel (memif vports, 64-B frames)
+            "live": live,
+            "p50_latency_us_pod": None if not live or "idle_p50_us" not in live else live["idle_p50_us"],
             "flows": total_flows,
             "batch_per_gpu": a.batch,
             "hash": a.hash,
