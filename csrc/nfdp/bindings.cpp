@@ -765,6 +765,24 @@ PYBIND11_MODULE(_nfdp, m) {
         auto v = e.take_latency_us();
         return py::array_t<double>(v.size(), v.data());
       });
+  m.def("owner_of_frames", [](py::array_t<uint8_t, py::array::c_style | py::array::forcecast> slots, U32Arr inmeta,
+                              py::buffer ports, py::bytes rss, uint32_t n) {
+    if (slots.ndim() != 2 || slots.shape(1) != kSlotBytes || inmeta.ndim() != 1 || inmeta.shape(0) != slots.shape(0))
+      throw std::invalid_argument("owner_of_frames: slots [n, 64] u8, inmeta [n] u32");
+    py::buffer_info bi = ports.request();
+    if ((size_t)bi.size * bi.itemsize < (size_t)kMaxPorts * sizeof(PortEntry)) throw std::invalid_argument("port table too small");
+    std::string k = rss;
+    if (k.size() < 20) throw std::invalid_argument("rss key too short");
+    const size_t cnt = slots.shape(0);
+    py::array_t<uint32_t> out(cnt);
+    auto o = out.mutable_data();
+    const uint8_t* sp = slots.data();
+    const uint32_t* ip = inmeta.data();
+    const auto* pt = static_cast<const PortEntry*>(bi.ptr);
+    for (size_t i = 0; i < cnt; ++i)
+      o[i] = frame_owner(sp + i * kSlotBytes, ip[i] >> 16, ip[i] & 0xFFFFu, pt, reinterpret_cast<const uint8_t*>(k.data()), n);
+    return out;
+  });
   // pod side of a memif vport (tests / tools): frames in, frames out
   struct MemifEndpoint {
     std::unique_ptr<memif::Region> reg;

@@ -458,19 +458,26 @@ bool Engine::needs_side(uint32_t in_port) const {
   return side_always_.load(std::memory_order_relaxed) || (in_port < side_ports_.size() && side_ports_[in_port]);
 }
 
+uint32_t frame_owner(const uint8_t* hdr, uint32_t len, uint32_t in_port, const PortEntry* ports, const uint8_t* rss_key,
+                     uint32_t n) {
+  if (n <= 1) return 0;
+  if (!ports || !rss_key) return in_port % n;
+  uint32_t d[kSlotDwords] = {};
+  std::memcpy(d, hdr, std::min<uint32_t>(len, kSlotBytes));
+  TablesView tv{};
+  tv.ports = ports;
+  Parsed p;
+  IngressState st;
+  ingress_stage(tv, DirectTables{tv}, d, (in_port & 0xFFFFu) | (std::min<uint32_t>(len, kMaxFrame) << 16), p, st);
+  if (!st.reason && p.ipv4) return owner_of(toeplitz_scalar(st.key, rss_key), n);
+  return in_port % n;
+}
+
 uint32_t Engine::owner_of_frame(const uint8_t* f, uint32_t len, uint32_t in_port) const {
   const uint32_t n = (uint32_t)lanes_.size();
   if (n <= 1) return 0;
   if (steer_ports_.empty() || rss_key_.empty()) return in_port % n;
-  uint32_t d[kSlotDwords] = {};
-  std::memcpy(d, f, std::min<uint32_t>(len, kSlotBytes));
-  TablesView tv{};
-  tv.ports = steer_ports_.data();
-  Parsed p;
-  IngressState st;
-  ingress_stage(tv, DirectTables{tv}, d, (in_port & 0xFFFFu) | (std::min<uint32_t>(len, kMaxFrame) << 16), p, st);
-  if (!st.reason && p.ipv4) return owner_of(toeplitz_scalar(st.key, rss_key_.data()), n);
-  return in_port % n;
+  return frame_owner(f, len, in_port, steer_ports_.data(), rss_key_.data(), n);
 }
 
 void Engine::start() {

@@ -38,6 +38,12 @@
 namespace nfdp {
 namespace iox {
 
+// Owner GPU of a frame (RSS): owner_of(toeplitz(FlowKey), n) for IPv4 frames the ingress stage
+// accepts (the key the flow table is sharded by), in_port % n otherwise.  `hdr` holds the first
+// min(len, 64) bytes; `ports` is the port table (kMaxPorts rows).
+uint32_t frame_owner(const uint8_t* hdr, uint32_t len, uint32_t in_port, const PortEntry* ports, const uint8_t* rss_key,
+                     uint32_t n);
+
 // ---------------------------------------------------------------------------------- ports
 struct RxRef {
   const uint8_t* data;

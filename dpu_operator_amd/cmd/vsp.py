@@ -44,7 +44,8 @@ def build_vsp(a, pm: PathManager):
         return GpuVsp(pm, device=a.device or None, flow_buckets=a.flow_buckets or cfg.flow_buckets,
                       hash_mode=cfg.hash_mode, acl_mode=cfg.acl_mode,
                       state_dir=a.state_dir or cfg.vsp_state_dir or None, nl=nl, live=a.live,
-                      live_engine=a.live_engine)
+                      live_engine=a.live_engine, gpus=a.gpus if a.gpus == "all" else int(a.gpus),
+                      vport_kind=a.vport_kind, tx_workers=a.io_workers)
     from ..cni.netlink import RtNetlink
     from ..platform.platform import SysfsPlatform
     from ..utils.cmdrunner import HostRunner
@@ -92,8 +93,14 @@ def main(argv=None, stop: threading.Event | None = None) -> int:
     ap.add_argument("--state-dir", default="", help="amd-gpu: journal + snapshot directory (resume on restart)")
     ap.add_argument("--live", action="store_true",
                     help="amd-gpu: vports are real TAP netdevs and pod traffic flows through the data plane")
-    ap.add_argument("--live-engine", default="batch", choices=["batch", "ring"],
-                    help="amd-gpu --live: fused kernel per poll cycle, or the persistent ring kernel on pinned host slots")
+    ap.add_argument("--live-engine", default="batch", choices=["batch", "ring", "native"],
+                    help="amd-gpu --live: fused kernel per poll cycle (Python loop), the persistent ring kernel on "
+                         "pinned host slots (Python loop), or the native C++ I/O engine + ring kernel")
+    ap.add_argument("--gpus", default="1", help="amd-gpu: GPUs behind the VSP (a number or 'all'): tables "
+                    "replicated, flows sharded by RSS owner, the native engine steering frames to their owner")
+    ap.add_argument("--vport-kind", default="tap", choices=["tap", "memif"],
+                    help="amd-gpu --live: vports as TAP netdevs or shared-memory (memif) regions")
+    ap.add_argument("--io-workers", type=int, default=4, help="native engine delivery threads per GPU")
     ap.add_argument("--metrics-bind-address", default="", help="amd-gpu: data-plane /metrics address (off if empty)")
     ap.add_argument("--agent-mbox", default="", help="amd-gpu: run the node control agent on this mailbox path")
     ap.add_argument("--agent-config", default="", help="agent SoC config file (default: one PF + --agent-vfs VFs)")
@@ -128,7 +135,7 @@ def _extras(a, vsp) -> list:
         from ..utils.metrics import MetricsServer, register_dataplane
 
         reg = CollectorRegistry()
-        register_dataplane(lambda: vsp.dp, "gpu0", reg)
+        register_dataplane(lambda: vsp.dp, "gpu0" if vsp.gpus == 1 else f"gpu0-{vsp.gpus - 1}", reg)
         vsp.metrics = MetricsServer(a.metrics_bind_address, reg).start()
         out.append(vsp.metrics)
     if a.agent_mbox:

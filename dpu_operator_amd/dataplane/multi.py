@@ -1,0 +1,192 @@
+"""All of a node's GPUs behind one data plane: small tables replicated, flows sharded by RSS owner.
+
+The reference runs ONE data-plane owner per node covering every port (the dpu-daemon DaemonSet,
+internal/controller/bindata/daemon/99.daemonset.yaml:20-21, with its VFs requested in
+dpudevicehandler.go:89).  On an MI355X node that owner is eight GPUs.  ``MultiDataPlane`` gives
+the VSP the same table API as a single ``DataPlane`` while spreading the work:
+
+* every small table model (ports, chains, MAC, LAG, flood, FIB, nexthops, ECMP, tunnels, ACL, ...)
+  is ONE host object shared by all planes; a commit uploads it to every GPU (replicated: each GPU
+  runs the whole chain for the flows it owns);
+* the flow table is sharded: flow f lives only on GPU ``owner_of(toeplitz(f), N)`` (its counters
+  too), the same owner the native I/O engine computes on ingress (csrc/nfdp/iox.cpp
+  `owner_of_frame`), so a packet always meets its flow entry;
+* MAC learning happens on whichever GPU saw the frame; ``pull_learned`` folds every GPU's learned
+  entries into the shared model and the next commit replicates them;
+* counters: port / drop counters are summed over the GPUs, flow counters come from the owner.
+
+The planes are ordinary ``DataPlane`` objects on ``cuda:0 .. cuda:N-1`` (or CPU oracle planes in
+tests).  One process drives them: the live path needs no GPU-to-GPU traffic because the host
+steers every frame to its owner's ring (pod rings are host memory every GPU can reach).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .engine import BatchResult, DataPlane
+
+# table models shared by all planes (one host object, replicated to every device)
+SHARED_MODELS = ("ports", "chains", "macs", "lag", "flood", "routes", "routes6", "nexthops", "ecmp", "tunnels",
+                 "terms", "vmmac", "tunnels6", "vtep6", "terms6", "acl")
+
+
+class ShardedFlows:
+    """The flow-table API of one DataPlane (insert_many / erase_many / find / len) over the
+    per-GPU shards: every key goes to (and is looked up on) its owner only."""
+
+    def __init__(self, planes: list[DataPlane]):
+        self.planes = planes
+        self.rss_key = planes[0].flows.rss_key
+
+    def owner(self, keys: np.ndarray) -> np.ndarray:
+        from ..native import nfdp
+
+        keys = np.ascontiguousarray(np.asarray(keys, np.uint32).reshape(-1, 4))
+        h = nfdp().toeplitz(keys, self.rss_key).astype(np.uint64)
+        return ((h * np.uint64(len(self.planes))) >> np.uint64(32)).astype(np.int64)
+
+    def __len__(self) -> int:
+        return sum(len(p.flows) for p in self.planes)
+
+    @property
+    def nbuckets(self) -> int:
+        return self.planes[0].flows.nbuckets
+
+    def insert_many(self, keys: np.ndarray, actions: np.ndarray) -> np.ndarray:
+        keys = np.ascontiguousarray(keys, np.uint32).reshape(-1, 4)
+        actions = np.ascontiguousarray(actions, np.uint32).reshape(-1, 4)
+        own = self.owner(keys)
+        slots = np.full(len(keys), -1, np.int64)
+        for g, p in enumerate(self.planes):
+            sel = np.nonzero(own == g)[0]
+            if len(sel):
+                slots[sel] = p.flows.insert_many(keys[sel], actions[sel])
+        return slots
+
+    def insert(self, key, action) -> int:
+        return int(self.insert_many(np.asarray([key], np.uint32), np.asarray([action], np.uint32))[0])
+
+    def erase_many(self, keys: np.ndarray) -> int:
+        keys = np.ascontiguousarray(keys, np.uint32).reshape(-1, 4)
+        own = self.owner(keys)
+        return sum(p.flows.erase_many(keys[own == g]) for g, p in enumerate(self.planes) if (own == g).any())
+
+    def erase(self, key) -> bool:
+        return self.erase_many(np.asarray([key], np.uint32)) == 1
+
+    def find(self, key) -> int:
+        g = int(self.owner(np.asarray([key], np.uint32))[0])
+        return self.planes[g].flows.find(key)
+
+
+class MultiDataPlane:
+    def __init__(self, devices: list[str], **kw):
+        if not devices:
+            raise ValueError("at least one device")
+        self.planes = [DataPlane(device=d, **kw) for d in devices]
+        p0 = self.planes[0]
+        for dp in self.planes[1:]:
+            for name in SHARED_MODELS:
+                setattr(dp, name, getattr(p0, name))
+        self.flows = ShardedFlows(self.planes)
+        self.n = len(self.planes)
+
+    # table models, modes, device facts: plane 0's (shared objects)
+    def __getattr__(self, name):
+        if name in ("planes", "flows", "n"):
+            raise AttributeError(name)
+        return getattr(self.planes[0], name)
+
+    @property
+    def gpu(self) -> bool:
+        return self.planes[0].gpu
+
+    # ------------------------------------------------------------------ commit / learning
+    def commit(self, full: bool = False) -> dict:
+        # learned MACs of every GPU reach the shared model before it is re-uploaded anywhere
+        if any(getattr(p, "_learned_on_device", False) for p in self.planes):
+            mv = self.planes[0].macs.version
+            if any(p._versions.get("macs") != mv for p in self.planes) or full:
+                self.pull_learned()
+        sent = {}
+        for g, p in enumerate(self.planes):
+            for k, v in p.commit(full).items():
+                sent[f"{k}@{g}"] = v
+        return sent
+
+    def pull_learned(self) -> int:
+        return sum(p.pull_learned() for p in self.planes)
+
+    def harvest(self) -> None:
+        for p in self.planes:
+            p.harvest()
+
+    # ------------------------------------------------------------------ counters
+    def port_counters(self) -> np.ndarray:
+        return sum(p.port_counters() for p in self.planes)
+
+    def drop_counters(self) -> dict:
+        out: dict[str, int] = {}
+        for p in self.planes:
+            for k, v in p.drop_counters().items():
+                out[k] = out.get(k, 0) + v
+        return out
+
+    def flow_counters(self, key) -> tuple[int, int]:
+        g = int(self.flows.owner(np.asarray([key], np.uint32))[0])
+        return self.planes[g].flow_counters(key)
+
+    def reset_counters(self) -> None:
+        for p in self.planes:
+            p.reset_counters()
+
+    # ------------------------------------------------------------------ batches
+    def owners(self, pkts: np.ndarray, inmeta: np.ndarray) -> np.ndarray:
+        """Owner GPU of each packet, exactly as the native I/O engine steers it on ingress."""
+        from ..native import nfdp
+
+        return np.asarray(nfdp().owner_of_frames(np.ascontiguousarray(pkts, np.uint8),
+                                                 np.ascontiguousarray(inmeta, np.uint32),
+                                                 np.ascontiguousarray(self.ports.a), bytes(self.flows.rss_key),
+                                                 self.n), np.int64)
+
+    def run(self, pkts, inmeta, **kw) -> BatchResult:
+        """A batch split by owner, each part through its GPU, results back in arrival order
+        (host arrays in and out; the multi-GPU live path is the native engine's job)."""
+        if self.gpu:
+            import torch
+
+            pk = pkts.cpu().numpy() if isinstance(pkts, torch.Tensor) else np.asarray(pkts)
+            im = inmeta.cpu().numpy().view(np.uint32) if isinstance(inmeta, torch.Tensor) else np.asarray(inmeta)
+        else:
+            pk, im = np.asarray(pkts), np.asarray(inmeta, np.uint32)
+        n = len(pk)
+        own = self.owners(pk, im)
+        out = np.zeros((n, 64), np.uint8)
+        meta = np.zeros(n, np.uint32)
+        for g, p in enumerate(self.planes):
+            sel = np.nonzero(own == g)[0]
+            if not len(sel):
+                continue
+            if p.gpu:
+                import torch
+
+                r = p.run(torch.from_numpy(pk[sel].copy()).to(p.tdev), torch.from_numpy(im[sel].view(np.int32).copy()).to(p.tdev))
+                torch.cuda.synchronize(p.tdev)
+                out[sel] = r.out.cpu().numpy()
+                meta[sel] = r.meta.cpu().numpy().view(np.uint32)
+            else:
+                r = p.run(pk[sel], im[sel])
+                out[sel], meta[sel] = r.out, r.meta
+        return BatchResult(out, meta, n, {"owner": own})
+
+
+def visible_devices() -> list[str]:
+    """Every MI355X this process can see (cuda:0 .. cuda:N-1), or ['cpu'] without one."""
+    try:
+        import torch
+
+        n = torch.cuda.device_count() if torch.cuda.is_available() else 0
+    except Exception:  # noqa: BLE001
+        n = 0
+    return [f"cuda:{i}" for i in range(n)] or ["cpu"]

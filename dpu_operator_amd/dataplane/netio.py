@@ -125,6 +125,8 @@ class LivePath:
         self._t: threading.Thread | None = None
         self._lock = threading.Lock()     # port map changes vs the loop
         self.error: BaseException | None = None
+        self.healthy = True
+        self.restarts = 0
         self._recirc: list[tuple[bytes, int]] = []
         self.stats["recirc"] = 0
         # IPsec boundary (dataplane/ipsec.py, the GPU ESP engine): ESP arriving on these ports is
@@ -226,6 +228,9 @@ class LivePath:
                 self._write(port_idx, f)
 
     def poll_once(self, timeout: float = 0.05) -> int:
+        from ..utils.faults import FAULTS
+
+        FAULTS.check("livepath.poll")
         self._t_ready = time.perf_counter()
         frames, src = self._gather(timeout)
         if self.ipsec_ports and frames:
@@ -353,12 +358,32 @@ class LivePath:
 
     # ------------------------------------------------------------------ thread
     def _run(self) -> None:
-        try:
-            while not self._stop.is_set():
+        """The loop survives its own failures: an exception marks the path unhealthy (the VSP
+        reports its vports unhealthy to the device plugin), the engine state is rebuilt (a ring
+        that failed is relaunched) and forwarding resumes after a backoff; the first successful
+        cycle marks it healthy again."""
+        backoff = 0.05
+        while not self._stop.is_set():
+            try:
                 self.poll_once(0.02)
-        except BaseException as e:  # noqa: BLE001 - surfaced through .error
-            self.error = e
-            log.exception("live path stopped")
+                if not self.healthy:
+                    self.healthy = True
+                    backoff = 0.05
+                    log.warning("live path recovered (restart %d)", self.restarts)
+            except BaseException as e:  # noqa: BLE001 - surfaced through .error / .healthy
+                self.error = e
+                self.healthy = False
+                self.restarts += 1
+                log.exception("live path cycle failed; restarting")
+                if self.ring is not None:
+                    try:
+                        self.ring.close()
+                    except Exception:  # noqa: BLE001
+                        pass
+                    self.ring = None      # relaunched by the next ring cycle
+                self._recirc = []
+                self._stop.wait(backoff)
+                backoff = min(backoff * 2, 2.0)
 
     def start(self) -> "LivePath":
         if self.engine == "ring" and self.ring is None:

@@ -18,6 +18,9 @@ _USED = 0x100  # kSlotUsed marker in key.meta byte 1 (nfdp.h)
 
 
 def _flows(dp) -> tuple[np.ndarray, np.ndarray, np.ndarray]:
+    if hasattr(dp, "planes"):       # MultiDataPlane: every GPU's shard
+        parts = [_flows(p) for p in dp.planes]
+        return tuple(np.concatenate([x[i] for x in parts]) for i in range(3))
     slots = dp.flows.t.slots()
     occ = (slots[:, 3] & _USED) != 0
     keys = slots[occ, 0:4].copy()
@@ -62,9 +65,14 @@ def load(dp, path: str) -> dict:
         dp.lag.version += 1
         keys, acts, totals = z["flow_keys"], z["flow_actions"], z["flow_totals"]
         if len(keys):
-            slots = dp.flows.insert_many(keys, acts)
-            if np.any(np.asarray(slots) < 0):
+            slots = np.asarray(dp.flows.insert_many(keys, acts), np.int64)
+            if np.any(slots < 0):
                 raise RuntimeError("flow table too small for the snapshot")
-            dp.flow_totals[np.asarray(slots, np.int64)] = totals
+            if hasattr(dp, "planes"):   # counters follow their flow to its owner GPU
+                own = dp.flows.owner(keys)
+                for g, p in enumerate(dp.planes):
+                    p.flow_totals[slots[own == g]] = totals[own == g]
+            else:
+                dp.flow_totals[slots] = totals
     dp.commit(full=True)
     return {"flows": int(len(keys)), "acl": len(dp.acl.rules)}

@@ -97,7 +97,8 @@ class GpuVsp(VspBase):
     def __init__(self, path_manager=None, device: str | None = None, nl: NetlinkManager | None = None,
                  opi_port: int = 0, flow_buckets: int = 1 << 16, vport_prefix: str = "dpuvp",
                  hash_mode: str = "mfma", acl_mode: str = "mfma", state_dir: str | None = None,
-                 live: bool = False, uplink=None, live_engine: str = "batch"):
+                 live: bool = False, uplink=None, live_engine: str = "batch", gpus=1, vport_kind: str = "tap",
+                 memif_dir: str | None = None, tx_workers: int = 4):
         super().__init__(path_manager)
         if device is None:
             try:
@@ -107,6 +108,18 @@ class GpuVsp(VspBase):
             except Exception:  # noqa: BLE001
                 device = "cpu"
         self.device = device
+        # the node's GPUs behind this VSP: 1 (self.device), N, or "all" visible MI355X (dataplane/multi.py:
+        # small tables replicated, flows sharded by RSS owner, one native I/O engine steering to them)
+        from ..dataplane.multi import visible_devices
+
+        if gpus == "all":
+            gpus = len(visible_devices()) if device != "cpu" else 1
+        self.gpus = max(1, int(gpus))
+        if vport_kind not in ("tap", "memif"):
+            raise ValueError("vport_kind is 'tap' (netdev) or 'memif' (shared-memory vport)")
+        self.vport_kind = vport_kind
+        self.memif_dir = memif_dir
+        self.tx_workers = int(tx_workers)
         self.nl = nl or FakeNetlink()
         self.opi_port = opi_port
         self.flow_buckets = flow_buckets
@@ -122,7 +135,12 @@ class GpuVsp(VspBase):
         self._salt = int.from_bytes(os.urandom(1), "little")
         self.chain_kinds: dict[str, list[str]] = {}
         self.live = live
-        self.live_engine = live_engine              # "batch" (fused kernel per cycle) or "ring" (resident kernel)
+        if live_engine not in ("batch", "ring", "native"):
+            raise ValueError("live_engine is 'batch', 'ring' or 'native'")
+        if (self.gpus > 1 or vport_kind == "memif") and live:
+            live_engine = "native"                  # the C++ engine: RSS steering / shared-memory vports
+        self.live_engine = live_engine              # "batch" (fused kernel per cycle), "ring" (resident
+                                                    # kernel) or "native" (C++ I/O engine, iox.cpp)
         self.taps: dict[int, object] = {}       # live mode: port -> TapPort
         self.livepath = None
         self.uplink = uplink                    # live mode: netdev (read/write/fd) of the wire port
@@ -137,8 +155,16 @@ class GpuVsp(VspBase):
     # ------------------------------------------------------------------ helpers
     def _ensure_dp(self) -> DataPlane:
         if self.dp is None:
-            self.dp = DataPlane(device=self.device, flow_buckets=self.flow_buckets, hash_mode=self.hash_mode,
-                                acl_mode=self.acl_mode)
+            kw = dict(flow_buckets=self.flow_buckets, hash_mode=self.hash_mode, acl_mode=self.acl_mode)
+            if self.gpus > 1:
+                from ..dataplane.multi import MultiDataPlane, visible_devices
+
+                devs = visible_devices() if self.device != "cpu" else ["cpu"] * self.gpus
+                if self.device != "cpu" and len(devs) < self.gpus:
+                    raise RuntimeError(f"{self.gpus} GPUs requested, {len(devs)} visible")
+                self.dp = MultiDataPlane(devs[: self.gpus], **kw)
+            else:
+                self.dp = DataPlane(device=self.device, **kw)
             self.dp.ports.set(WIRE_PORT, flags=T.PORT_VALID, bridge_id=VF_BRIDGE, mac="02:00:00:00:0f:a0")
             self._apply_port_state(WIRE_PORT)
             self.dp.commit(full=True)
@@ -263,12 +289,18 @@ class GpuVsp(VspBase):
         self.dpu_mode = dpu_mode
         self._ensure_dp()
         if self.live and self.livepath is None:
-            from ..dataplane.netio import LivePath
-
             ports = dict(self.taps)
             if self.uplink is not None:
                 ports[WIRE_PORT] = self.uplink
-            self.livepath = LivePath(self.dp, ports, engine=self.live_engine if self.dp.gpu else "batch").start()
+            if self.live_engine == "native":
+                from ..dataplane.native_io import NativeLivePath
+
+                planes = self.dp.planes if hasattr(self.dp, "planes") else [self.dp]
+                self.livepath = NativeLivePath(planes, ports, tx_workers=self.tx_workers).start()
+            else:
+                from ..dataplane.netio import LivePath
+
+                self.livepath = LivePath(self.dp, ports, engine=self.live_engine if self.dp.gpu else "batch").start()
         if not self.opi_port:
             self.opi_port = self._free_port()
         return "127.0.0.1", self.opi_port
@@ -281,7 +313,14 @@ class GpuVsp(VspBase):
             if i in self.vports:
                 continue
             name, mac = f"{self.prefix}{i}", _local_mac(i, self._salt)
-            if self.live:
+            if self.live and self.vport_kind == "memif":
+                from ..dataplane.native_io import MemifVport, memif_dir
+
+                vp = MemifVport(os.path.join(self.memif_dir or memif_dir(), f"{name}.memif"))
+                self.taps[i] = vp
+                if self.livepath is not None:
+                    self.livepath.add_port(i, vp)
+            elif self.live:
                 from ..dataplane.netio import TapPort
 
                 tap = TapPort(name, mac, self.nl)
@@ -300,13 +339,26 @@ class GpuVsp(VspBase):
             if tap is not None:
                 if self.livepath is not None:
                     self.livepath.remove_port(i)
-                tap.close()
+                if hasattr(tap, "close"):
+                    tap.close()
         self._commit()
         return n
 
+    def data_path_healthy(self) -> bool:
+        """The VSP and its live packet path: a failed / restarting path makes every vport
+        unhealthy, so the device plugin stops handing them out (ListAndWatch)."""
+        lp = self.livepath
+        return self.healthy and (lp is None or bool(getattr(lp, "healthy", True)))
+
     def get_devices(self) -> dict[str, str]:
-        h = "Healthy" if self.healthy else "Unhealthy"
+        h = "Healthy" if self.data_path_healthy() else "Unhealthy"
         return {v["name"]: h for v in self.vports.values()}
+
+    def vport_path(self, idx: int) -> str | None:
+        """Shared-memory vports: the region a pod attaches to (mounted into the pod by the device
+        plugin / CNI the way vhost-user and memif sockets are)."""
+        v = self.taps.get(idx)
+        return getattr(v, "path", None) if self.vport_kind == "memif" else None
 
     def create_bridge_port(self, name, mac, ptype, logical_bridges):
         m = re.fullmatch(r"host(\d+)-(\d+)", name)
@@ -355,7 +407,8 @@ class GpuVsp(VspBase):
             self.livepath.stop()
             self.livepath = None
         for tap in self.taps.values():
-            tap.close()
+            if hasattr(tap, "close"):
+                tap.close()
         self.taps.clear()
 
     def on_gpu_chain(self, sfc_name: str, kinds: list[str]) -> int:
@@ -474,6 +527,9 @@ class GpuVsp(VspBase):
             self._ensure_dp()
             lens = np.array([self._frame_len(f) for f in frames], np.uint32)
             im = mk_inmeta(np.asarray(in_ports), lens)
+            if hasattr(self.dp, "planes"):      # several GPUs: split by owner, host arrays back
+                r = self.dp.run(np.ascontiguousarray(frames), im)
+                return r.out, r.meta
             if self.dp.gpu:
                 import torch
 
