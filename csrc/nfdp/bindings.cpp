@@ -338,8 +338,12 @@ PYBIND11_MODULE(_nfdp, m) {
                            uint32_t n, uintptr_t flow_ctr, uintptr_t port_ctr, uintptr_t drop_ctr, uintptr_t t0,
                            uintptr_t lat, uintptr_t acl_wfrag, uintptr_t acl_cinit, uint32_t acl_tiles,
                            uintptr_t toep_frag, uintptr_t toep_tab, int hash_mode, int acl_mode, int num_cus,
-                           uintptr_t stream, uint32_t flags, py::object side, uintptr_t n_dev) {
+                           uintptr_t stream, uint32_t flags, py::object side, uintptr_t n_dev, uintptr_t steer_list,
+                           uintptr_t steer_cnt, uint32_t nranks, uint32_t rank) {
     FusedLaunch f{};
+    f.steer_list = reinterpret_cast<uint32_t*>(steer_list);
+    f.steer_cnt = reinterpret_cast<uint32_t*>(steer_cnt);
+    if (f.steer_list) { f.nranks = nranks; f.rank = rank; }
     f.side = side_from(side);
     f.t = tables_from(tables);
     f.pkts = reinterpret_cast<const void*>(pkts);
@@ -371,7 +375,15 @@ PYBIND11_MODULE(_nfdp, m) {
      py::arg("flow_ctr"), py::arg("port_ctr"), py::arg("drop_ctr"), py::arg("t0"), py::arg("lat"),
      py::arg("acl_wfrag"), py::arg("acl_cinit"), py::arg("acl_tiles"), py::arg("toep_frag"), py::arg("toep_tab"),
      py::arg("hash_mode"), py::arg("acl_mode"), py::arg("num_cus"), py::arg("stream"), py::arg("flags") = 0,
-     py::arg("side") = py::none(), py::arg("n_dev") = 0);
+     py::arg("side") = py::none(), py::arg("n_dev") = 0, py::arg("steer_list") = 0, py::arg("steer_cnt") = 0,
+     py::arg("nranks") = 0, py::arg("rank") = 0);
+  m.def("launch_steer", [](uintptr_t out, uintptr_t inmeta, uintptr_t list, uintptr_t list_cnt, uint32_t cap_list,
+                           uintptr_t send, uintptr_t pcnt, uint32_t nranks, uint32_t cap, uintptr_t stream) {
+    check(launch_steer(reinterpret_cast<const void*>(out), reinterpret_cast<const uint32_t*>(inmeta),
+                       reinterpret_cast<const uint32_t*>(list), reinterpret_cast<const uint32_t*>(list_cnt), cap_list,
+                       reinterpret_cast<uint8_t*>(send), reinterpret_cast<uint32_t*>(pcnt), nranks, cap,
+                       reinterpret_cast<hipStream_t>(stream)), "launch_steer");
+  });
   m.def("gather", [](uintptr_t recv, uint32_t nranks, uint32_t rank, uint32_t cap, uintptr_t pkts, uintptr_t inmeta,
                      uintptr_t n_dev, bool device, uintptr_t stream) -> uint32_t {
     const size_t seg = pkt_seg_bytes(cap), moff = pkt_meta_off(cap);

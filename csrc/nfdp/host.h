@@ -109,7 +109,15 @@ struct FusedLaunch {
   SideOut side{};  // side outputs (flood / mirror / ARP replicas, learn events); cnt null = off
   uint32_t steer = 0;              // REMOTE: 1 = send packets of other GPUs' flow shards to their owner
   const uint32_t* n_dev = nullptr; // device-side count (<= n)
+  // steer-by-list (1-GPU instances with nranks > 1): other GPUs' packets listed, not processed
+  uint32_t* steer_list = nullptr;
+  uint32_t* steer_cnt = nullptr;
 };
+// Second half of steer-by-list: listed packets -> their owners' exchange segments (count-first,
+// segments sized for the whole batch).
+hipError_t launch_steer(const void* out, const uint32_t* inmeta, const uint32_t* list, const uint32_t* list_cnt,
+                        uint32_t cap_list, uint8_t* send, uint32_t* pcnt, uint32_t nranks, uint32_t cap,
+                        hipStream_t s);
 hipError_t launch_fused(const FusedLaunch& f, const LaunchCfg& cfg, hipStream_t s);
 // Side pass alone (flood / mirror / ARP replicas, learn events, tunnel headers) over a side list
 // another kernel filled (the persistent ring kernel): slots / meta are that kernel's buffers.

@@ -76,6 +76,13 @@ struct FusedArgs {
                                   // ingress meta go to the owner, which runs the whole pipeline)
   const uint32_t* n_dev;          // optional device-side packet count (<= n): batches whose size only
                                   // the GPU knows (packets gathered from the exchange)
+  // Flow-owner steering by list (1-GPU instances, nranks > 1): a packet of another GPU's flow
+  // shard is not probed / chained / counted here; its index | owner << 26 is appended to
+  // steer_list (wave-aggregated, sized for the whole batch) and steer_kernel copies it to the
+  // owner's exchange segment afterwards.  The hot instance keeps its register budget and its
+  // fixed-count store tail; only a wave-uniform owner test is added.
+  uint32_t* steer_list;
+  uint32_t* steer_cnt;
 };
 
 __device__ __forceinline__ size_t lds_align16(size_t x) { return (x + 15) & ~(size_t)15; }
@@ -109,7 +116,7 @@ __host__ __device__ inline LdsLayout lds_layout(int hash_mode, int acl_mode, uin
 constexpr int kBufCfg = 0x00020000;  // buffer resource word 3 (gfx9 family raw buffer)
 constexpr int kStreamAux = 2;        // nt: frames are read once / written once (streaming)
 
-template <int HASH, int ACL, bool REMOTE, bool EARLY>
+template <int HASH, int ACL, bool REMOTE, bool EARLY, bool LIST = false>
 __global__ __launch_bounds__(kFB, EARLY ? NFDP_EARLY_WAVES_PER_EU : NFDP_FUSED_WAVES_PER_EU) void fused_kernel(FusedArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ uint32_t rcnt[REMOTE ? 2 * kMaxRanks : 1], rbase[REMOTE ? kMaxRanks : 1];  // rcnt double-buffered
@@ -194,8 +201,8 @@ __global__ __launch_bounds__(kFB, EARLY ? NFDP_EARLY_WAVES_PER_EU : NFDP_FUSED_W
     } else {
       classify_wave<HASH, ACL>(st.key, kx, av, lt, ltab, a.t, hash, acl_rule);
     }
-    // flow-owner steering (REMOTE, steer = 1): a packet of another GPU's flow shard leaves now,
-    // as it came in; its owner runs the whole pipeline on it
+    // flow-owner steering (REMOTE steer = 1, or the 1-GPU instance's steer list): a packet of
+    // another GPU's flow shard leaves now, as it came in; its owner runs the whole pipeline on it
     bool to_owner = false;
     uint32_t owner = a.rank;
     if constexpr (REMOTE) {
@@ -203,6 +210,22 @@ __global__ __launch_bounds__(kFB, EARLY ? NFDP_EARLY_WAVES_PER_EU : NFDP_FUSED_W
         owner = owner_of(hash, a.nranks);
         to_owner = valid && !st.reason && p.ipv4 && owner != a.rank;
         if (to_owner) st.reason = kRemote;  // no local probe / chain / counters
+      }
+    } else if constexpr (LIST) {   // separate instances: the 1-GPU hot kernel is untouched
+      // steer list: the append happens here, so the owner id is dead before the probe / chain
+      // (the hot instance's register budget stays what it was)
+      const uint32_t own = owner_of(hash, a.nranks);
+      to_owner = valid && !st.reason && p.ipv4 && own != a.rank;
+      if (to_owner) st.reason = kRemote;
+      const unsigned long long m = __ballot(to_owner);
+      if (__builtin_expect(m != 0ull, 0)) {
+        const uint32_t lane = threadIdx.x & 63u;
+        const int leader = __ffsll((long long)m) - 1;
+        uint32_t base = 0;
+        if ((int)lane == leader) base = atomicAdd(a.steer_cnt, (uint32_t)__popcll(m));
+        base = __shfl(base, leader);
+        const unsigned long long lt = lane ? (~0ull >> (64 - lane)) : 0ull;
+        if (to_owner) a.steer_list[base + (uint32_t)__popcll(m & lt)] = i | (own << 26);
       }
     }
     if constexpr (!REMOTE) {
@@ -259,13 +282,16 @@ __global__ __launch_bounds__(kFB, EARLY ? NFDP_EARLY_WAVES_PER_EU : NFDP_FUSED_W
         }
       }
     }
-    if (to_owner && !to_peer) reason = kOverflow;  // the owner's segment was full: dropped here
+    if (REMOTE && to_owner && !to_peer) reason = kOverflow;  // the owner's segment was full: dropped here
+    const bool listed = LIST && to_owner;                     // steer list: always delivered to the owner
     const uint32_t olen = reason == e.reason ? egress_len(p, e) : 0u;
-    const uint32_t meta = to_peer ? make_meta(a.steer ? kPortNone : e.out_port, a.steer ? st.wire_len : olen, kRemote)
-                                  : make_meta(reason == kOverflow ? kPortNone : e.out_port, olen, reason,
-                                              !reason && e.xhdr, !reason && e.flood);
+    const uint32_t meta = (to_peer || listed)
+                              ? make_meta((a.steer || listed) ? kPortNone : e.out_port,
+                                          (a.steer || listed) ? st.wire_len : olen, kRemote)
+                              : make_meta(reason == kOverflow ? kPortNone : e.out_port, olen, reason,
+                                          !reason && e.xhdr, !reason && e.flood);
     // port / drop counters: LDS, global only for ports >= kLdsPorts (issued before the tail)
-    if (valid && !(a.flags & 1u) && !(to_owner && to_peer)) {  // a steered packet is counted by its owner
+    if (valid && !(a.flags & 1u) && !(to_owner && (to_peer || listed))) {  // a steered packet is counted by its owner
       if (st.in_port < kLdsPorts) {
         atomicAdd(&pc[st.in_port], 1u); atomicAdd(&pc[kLdsPorts + st.in_port], st.wire_len);
       } else if (st.in_port < (uint32_t)kMaxPorts) {
@@ -301,7 +327,7 @@ __global__ __launch_bounds__(kFB, EARLY ? NFDP_EARLY_WAVES_PER_EU : NFDP_FUSED_W
         }
       }
     }
-    const bool sample = a.lat && !(a.flags & 2u) && (i & 15u) == 0 && !to_peer;
+    const bool sample = a.lat && !(a.flags & 2u) && (i & 15u) == 0 && !to_peer && !listed;
     const uint32_t lat_now = sample ? (uint32_t)(__builtin_amdgcn_s_memrealtime() - t0) : 0u;
     if constexpr (!REMOTE) {
       // Fixed-count tail: every lane issues the same vector-memory instructions with no branch
@@ -390,6 +416,29 @@ __global__ __launch_bounds__(256) void gather_kernel(const uint8_t* recv, uint32
   }
 }
 
+// Steer-list mode, second half: every listed packet (index | owner << 26) goes to its owner's
+// exchange segment - the slot as it came in (re-emitted by the fused kernel into out[i]) and its
+// ingress meta, at a position claimed per owner.  Segments are sized for the whole batch
+// (count-first exchange: nothing can overflow).  Then the segment headers carry the counts.
+__global__ __launch_bounds__(256) void steer_kernel(const uint4* out, const uint32_t* inmeta, const uint32_t* list,
+                                                    const uint32_t* list_cnt, uint32_t cap_list, uint8_t* send,
+                                                    uint32_t* pcnt, uint32_t nranks, uint32_t cap, uint32_t seg_bytes,
+                                                    uint32_t meta_off) {
+  const uint32_t n = min(*list_cnt, cap_list);
+  for (uint32_t j = blockIdx.x * 256 + threadIdx.x; j < n; j += gridDim.x * 256) {
+    const uint32_t e = list[j];
+    const uint32_t i = e & ((1u << 26) - 1u), o = e >> 26;
+    if (o >= nranks) continue;
+    const uint32_t pos = atomicAdd(&pcnt[o], 1u);
+    if (pos >= cap) continue;   // cannot happen with cap = batch (kept as a guard)
+    uint8_t* seg = send + (size_t)o * seg_bytes;
+    uint4* dst = reinterpret_cast<uint4*>(seg + 64 + (size_t)pos * 64);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) dst[k] = out[(size_t)i * 4 + k];
+    reinterpret_cast<uint32_t*>(seg + meta_off)[pos] = inmeta[i];
+  }
+}
+
 __global__ void stamp_kernel(unsigned long long* dst) {
   if (threadIdx.x == 0) *dst = __builtin_amdgcn_s_memrealtime();
 }
@@ -473,7 +522,7 @@ size_t fused_lds_bytes(int hash_mode, int acl_mode, uint32_t acl_tiles) {
   return lds_layout(hash_mode, acl_mode, acl_tiles).total;
 }
 
-template <int H, int A, bool R, bool E = false>
+template <int H, int A, bool R, bool E = false, bool LS = false>
 static hipError_t launch_fused_t(const FusedArgs& a, int num_cus, hipStream_t s) {
   // static LDS (REMOTE reservation counters) + dynamic tables must fit 160 KiB
   constexpr size_t kStatic = 3 * (R ? kMaxRanks : 1) * sizeof(uint32_t);  // rcnt[2][..] + rbase
@@ -487,7 +536,7 @@ static hipError_t launch_fused_t(const FusedArgs& a, int num_cus, hipStream_t s)
   if (!R && (a.n >= (1u << 25) || !a.flow_ctr || !a.out_meta)) return hipErrorInvalidValue;
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&fused_kernel<H, A, R, E>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&fused_kernel<H, A, R, E, LS>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxDyn);
     if (e != hipSuccess) return e;
     attr_set = true;
@@ -498,7 +547,7 @@ static hipError_t launch_fused_t(const FusedArgs& a, int num_cus, hipStream_t s)
   uint32_t grid = (uint32_t)(per_cu * num_cus);
   if (need < grid) grid = need;
   if (grid == 0) return hipSuccess;
-  hipLaunchKernelGGL((fused_kernel<H, A, R, E>), dim3(grid), dim3(kFB), lds, s, a);
+  hipLaunchKernelGGL((fused_kernel<H, A, R, E, LS>), dim3(grid), dim3(kFB), lds, s, a);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || !a.side.cnt || a.side.cap_list == 0) return e;
   return launch_side(a.t, a.pkts, a.inmeta, a.out, a.out_meta, a.side, a.port_ctr, a.drop_ctr, s);
@@ -537,14 +586,27 @@ hipError_t launch_fused(const FusedLaunch& f, const LaunchCfg& cfg, hipStream_t 
   a.side = f.side;
   a.steer = f.steer;
   a.n_dev = f.n_dev;
+  a.steer_list = f.steer_list;
+  a.steer_cnt = f.steer_cnt;
+  if (f.steer_list && (!f.steer_cnt || f.nranks < 2 || f.nranks > kMaxRanks || f.rank >= f.nranks || f.n >= (1u << 26)))
+    return hipErrorInvalidValue;
   if (a.side.cnt && ((a.side.cap_rep && (!a.side.rep_hdr || !a.side.rep_meta || !a.side.rep_src)) ||
                      (a.side.cap_learn && !a.side.learn) || (a.side.cap_list && !a.side.list)))
     return hipErrorInvalidValue;
-  const bool remote = f.nranks > 1;
+  const bool remote = f.nranks > 1 && !f.steer_list;   // steer list: the 1-GPU instances
   if (cfg.acl_mode == kAclMfma && (f.acl_tiles == 0 || f.acl_tiles > kAclMaxRules / 16)) return hipErrorInvalidValue;
   const int h = cfg.hash_mode, ac = cfg.acl_mode, cu = cfg.num_cus;
   const bool early = ac == kAclMfma && !(f.flags & kFlagNoEarly) &&
                      (f.acl_tiles >= kEarlyAclTiles || (f.flags & kFlagForceEarly));
+  if (f.steer_list) {   // flow-owner steering by list: the LIST instances (multi-GPU RSS)
+#define NFDP_LCASE(HH, AA)                                                                 \
+    if (h == HH && ac == AA)                                                               \
+      return (early && AA == kAclMfma) ? launch_fused_t<HH, AA, false, true, true>(a, cu, s) \
+                                       : launch_fused_t<HH, AA, false, false, true>(a, cu, s);
+    NFDP_LCASE(1, 1) NFDP_LCASE(1, 2) NFDP_LCASE(2, 1) NFDP_LCASE(2, 2)
+#undef NFDP_LCASE
+    return hipErrorInvalidValue;   // (scalar hash / scalar ACL: the REMOTE steer instances)
+  }
   if (early) {
     if (h == kHashLds) return remote ? launch_fused_t<kHashLds, kAclMfma, true, true>(a, cu, s)
                                      : launch_fused_t<kHashLds, kAclMfma, false, true>(a, cu, s);
@@ -570,6 +632,19 @@ hipError_t launch_gather(const uint8_t* recv, uint32_t nranks, uint32_t rank, ui
   if (grid == 0) grid = 1;
   hipLaunchKernelGGL(gather_kernel, dim3(grid), dim3(256), 0, s, recv, nranks, rank, cap, seg_bytes, meta_off,
                      reinterpret_cast<uint4*>(pkts), inmeta, n_dev);
+  return hipGetLastError();
+}
+
+hipError_t launch_steer(const void* out, const uint32_t* inmeta, const uint32_t* list, const uint32_t* list_cnt,
+                        uint32_t cap_list, uint8_t* send, uint32_t* pcnt, uint32_t nranks, uint32_t cap,
+                        hipStream_t s) {
+  if (!out || !inmeta || !list || !list_cnt || !send || !pcnt || nranks < 2 || nranks > kMaxRanks)
+    return hipErrorInvalidValue;
+  if (pkt_seg_bytes(cap) * nranks >= (1ull << 40)) return hipErrorInvalidValue;
+  uint32_t grid = (cap_list + 255) / 256;
+  grid = grid < 1 ? 1 : (grid > 1024 ? 1024 : grid);
+  hipLaunchKernelGGL(steer_kernel, dim3(grid), dim3(256), 0, s, reinterpret_cast<const uint4*>(out), inmeta, list,
+                     list_cnt, cap_list, send, pcnt, nranks, cap, (uint32_t)pkt_seg_bytes(cap), (uint32_t)pkt_meta_off(cap));
   return hipGetLastError();
 }
 

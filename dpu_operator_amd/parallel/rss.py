@@ -41,19 +41,31 @@ def flow_owner(keys: np.ndarray, world: int, rss_key: bytes) -> np.ndarray:
 
 
 class _Slot:
-    def __init__(self, dev, world: int, pseg: int):
+    def __init__(self, dev, world: int, pseg: int, batch: int, gpu: bool):
         self.send = torch.zeros(world * pseg, dtype=torch.uint8, device=dev)
         self.recv = torch.zeros(world * pseg, dtype=torch.uint8, device=dev)
-        self.pcnt = torch.zeros(world, dtype=torch.int32, device=dev)
+        self.pcnt = torch.zeros(world, dtype=torch.int32, device=dev)    # packets this rank sends to each peer
+        self.rcnt = torch.zeros(world, dtype=torch.int32, device=dev)    # packets each peer sends this rank
         self.t0 = torch.zeros(1, dtype=torch.int64, device=dev)
-
-
-class _Done:
-    def wait(self) -> None:
-        pass
+        self.list = torch.zeros(max(batch, 1), dtype=torch.int32, device=dev)   # steer list (GPU)
+        self.list_cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.ev = torch.cuda.Event() if gpu else None     # local step (kernel + steer) done
+        self.cev = torch.cuda.Event() if gpu else None    # exchange done
 
 
 class RssShardedDataPlane:
+    """Count-first, loss-free flow-owner exchange.
+
+    Per step on rank r: the 1-GPU fused kernel in steer-list mode (LIST instances: packets of other
+    GPUs' flows are listed, not processed; the hot instance is untouched) + steer_kernel copying
+    the listed input slots into per-owner segments sized for the WHOLE batch, so nothing can
+    overflow whatever the misdirected fraction.  The exchange then moves exactly what was written:
+    the per-peer counts first (one all-to-all of N ints), then one grouped send/recv of the slot
+    and meta bytes each peer actually has (NCCL P2P over xGMI: each peer on its own link), on a
+    communication stream that overlaps the next step's kernel.  The host learns the counts while
+    the GPU runs that next kernel, so the count round trip costs no GPU time.
+    """
+
     def __init__(self, dp: DataPlane, rank: int, world: int, batch: int, remote_frac: float = 0.01,
                  group=None):
         if world < 2:
@@ -61,22 +73,24 @@ class RssShardedDataPlane:
         self.dp, self.nf = dp, dp.nf
         self.rank, self.world, self.group = rank, world, group
         self.batch = batch
+        self.remote_frac = remote_frac      # informational: the exchange is sized by counts, not by this
         self.gpu = dp.gpu
         self.dev = dp.tdev if self.gpu else torch.device("cpu")
-        per = batch * max(remote_frac, 0.0) / (world - 1)
-        self.cap = int(math.ceil((per * 1.25 + 6 * math.sqrt(per) + 64) / 64)) * 64
-        self.pseg = self.nf.pkt_seg_bytes(self.cap)
-        self.slots = [_Slot(self.dev, world, self.pseg) for _ in range(2)]
+        self.cap = max(int(batch), 64)      # a segment holds the whole batch: loss-free at any fraction
+        self.pseg = int(self.nf.pkt_seg_bytes(self.cap))
+        self.moff = int(self.nf.pkt_meta_off(self.cap))
+        self.slots = [_Slot(self.dev, world, self.pseg, batch, self.gpu) for _ in range(2)]
         u8, i32 = dict(dtype=torch.uint8, device=self.dev), dict(dtype=torch.int32, device=self.dev)
         self.out = torch.zeros((batch, 64), **u8)
         self.out_meta_t = torch.zeros(batch, **i32)
         self.lat = torch.zeros((batch + 15) // 16, **i32)
-        nr = world * self.cap                       # received packets of one step (upper bound)
-        self.rx_pkts = torch.zeros((nr, 64), **u8)
-        self.rx_inmeta = torch.zeros(nr, **i32)
-        self.rx_out = torch.zeros((nr, 64), **u8)
-        self.rx_meta = torch.zeros(nr, **i32)
-        self.rx_lat = torch.zeros((nr + 15) // 16, **i32)
+        nr = world * self.cap if not self.gpu else max(int(batch * min(1.0, max(remote_frac, 0.0)) * 4) + 4096, 65536)
+        self.rx_cap = min(nr, world * self.cap)
+        self.rx_pkts = torch.zeros((self.rx_cap, 64), **u8)
+        self.rx_inmeta = torch.zeros(self.rx_cap, **i32)
+        self.rx_out = torch.zeros((self.rx_cap, 64), **u8)
+        self.rx_meta = torch.zeros(self.rx_cap, **i32)
+        self.rx_lat = torch.zeros((self.rx_cap + 15) // 16, **i32)
         self.rx_n = torch.zeros(1, **i32)
         self.n = 0
         self.k = 0
@@ -84,6 +98,11 @@ class RssShardedDataPlane:
         self.hash_mode = dp.hash_mode if dp.hash_mode != 0 else 1
         self.acl_mode = dp.acl_mode
         self.host_staged = self.gpu and dist.is_initialized() and dist.get_backend(group) == "gloo"
+        # LIST instances exist for the LDS / MFMA hash with the MFMA / no ACL; others use REMOTE steer
+        self.use_list = self.gpu and self.hash_mode in (1, 2) and self.acl_mode in (1, 2)
+        self.comm = torch.cuda.Stream(self.dev) if self.gpu and not self.host_staged else None
+        self.hcnt = torch.zeros((2, world), dtype=torch.int32).pin_memory() if self.gpu else torch.zeros((2, world), dtype=torch.int32)
+        self.stats = {"sent": 0, "received": 0, "steps": 0, "max_peer": 0}
 
     @staticmethod
     def _p(t) -> int:
@@ -92,23 +111,99 @@ class RssShardedDataPlane:
     def _stream(self) -> int:
         return torch.cuda.current_stream(self.dev).cuda_stream if self.gpu else 0
 
-    def _remote(self, s: _Slot, pkts: torch.Tensor, inmeta: torch.Tensor, n: int) -> None:
+    def _local(self, s: _Slot, pkts: torch.Tensor, inmeta: torch.Tensor, n: int) -> None:
+        """This rank's share: its own flows through the whole pipeline, other GPUs' packets into
+        their owners' segments (count in pcnt)."""
         dp, p = self.dp, self._p
         s.pcnt.zero_()
-        d = dict(nranks=self.world, rank=self.rank, cap_desc=0, cap_pkt=self.cap, steer=1,
-                 pkts=p(pkts), inmeta=p(inmeta), out=p(self.out), out_meta=p(self.out_meta_t), n=n,
-                 flow_ctr=dp._ptr("flow_ctr") if dp.count_flows else 0, port_ctr=dp._ptr("port_ctr"),
-                 drop_ctr=dp._ptr("drop_ctr"), t0=p(s.t0) if self.gpu else 0, lat=p(self.lat) if self.gpu else 0,
-                 acl_wfrag=dp._ptr("acl_wfrag"), acl_cinit=dp._ptr("acl_cinit"), acl_tiles=dp._acl_tiles,
-                 toep_frag=dp._ptr("toep_frag"), toep_tab=dp._ptr("toep_tab"), send_pkt=p(s.send), pcnt=p(s.pcnt),
-                 flags=0)
-        self.nf.fused_remote(dp.tables_ptrs(), d, self.gpu, self.hash_mode, self.acl_mode, dp.num_cus, self._stream())
+        if self.use_list:
+            s.list_cnt.zero_()
+            st = self._stream()
+            self.nf.launch_fused(dp.tables_ptrs(), p(pkts), p(inmeta), p(self.out), p(self.out_meta_t), n,
+                                 dp._ptr("flow_ctr"), dp._ptr("port_ctr"), dp._ptr("drop_ctr"), p(s.t0), p(self.lat),
+                                 dp._ptr("acl_wfrag"), dp._ptr("acl_cinit"), dp._acl_tiles, dp._ptr("toep_frag"),
+                                 dp._ptr("toep_tab"), self.hash_mode, self.acl_mode, dp.num_cus, st,
+                                 0 if dp.count_flows else 4, None, 0, p(s.list), p(s.list_cnt), self.world, self.rank)
+            self.nf.launch_steer(p(self.out), p(inmeta), p(s.list), p(s.list_cnt), n, p(s.send), p(s.pcnt),
+                                 self.world, self.cap, st)
+        else:
+            d = dict(nranks=self.world, rank=self.rank, cap_desc=0, cap_pkt=self.cap, steer=1,
+                     pkts=p(pkts), inmeta=p(inmeta), out=p(self.out), out_meta=p(self.out_meta_t), n=n,
+                     flow_ctr=dp._ptr("flow_ctr") if dp.count_flows else 0, port_ctr=dp._ptr("port_ctr"),
+                     drop_ctr=dp._ptr("drop_ctr"), t0=p(s.t0) if self.gpu else 0, lat=p(self.lat) if self.gpu else 0,
+                     acl_wfrag=dp._ptr("acl_wfrag"), acl_cinit=dp._ptr("acl_cinit"), acl_tiles=dp._acl_tiles,
+                     toep_frag=dp._ptr("toep_frag"), toep_tab=dp._ptr("toep_tab"), send_pkt=p(s.send),
+                     pcnt=p(s.pcnt), flags=0)
+            self.nf.fused_remote(dp.tables_ptrs(), d, self.gpu, self.hash_mode, self.acl_mode, dp.num_cus,
+                                 self._stream())
+        if self.gpu:
+            s.ev.record(torch.cuda.current_stream(self.dev))
+
+    def _views(self, buf: torch.Tensor, j: int, c: int) -> tuple[torch.Tensor, torch.Tensor]:
+        b = j * self.pseg
+        return buf[b + 64: b + 64 + 64 * c], buf[b + self.moff: b + self.moff + 4 * c]
+
+    def _p2p(self, send: torch.Tensor, recv: torch.Tensor, sc, rc) -> list:
+        ops = []
+        for j in range(self.world):
+            if j == self.rank:
+                continue
+            if sc[j]:
+                a, m = self._views(send, j, int(sc[j]))
+                ops += [dist.P2POp(dist.isend, a, j, self.group, 0), dist.P2POp(dist.isend, m, j, self.group, 1)]
+            if rc[j]:
+                a, m = self._views(recv, j, int(rc[j]))
+                ops += [dist.P2POp(dist.irecv, a, j, self.group, 0), dist.P2POp(dist.irecv, m, j, self.group, 1)]
+        return dist.batch_isend_irecv(ops) if ops else []
+
+    def exchange(self, s: _Slot):
+        """Counts first, then exactly the bytes each peer has (no fixed-capacity segments on the
+        wire, no overflow)."""
+        w = self.world
+        if self.comm is not None:
+            cs = self.comm
+            with torch.cuda.stream(cs):
+                cs.wait_event(s.ev)
+                dist.all_to_all_single(s.rcnt, s.pcnt, group=self.group)
+                self.hcnt[0].copy_(s.pcnt, non_blocking=True)
+                self.hcnt[1].copy_(s.rcnt, non_blocking=True)
+                # the gather kernel reads each receive segment's count from its header
+                s.recv.view(w, self.pseg)[:, :4].view(torch.int32)[:, 0].copy_(s.rcnt)
+                cs.synchronize()                  # host: counts (the GPU runs the next step's kernel meanwhile)
+                sc, rc = self.hcnt[0].numpy().copy(), self.hcnt[1].numpy().copy()
+                for wk in self._p2p(s.send, s.recv, sc, rc):
+                    wk.wait()                     # makes the comm stream wait for the transfers
+                s.cev.record(cs)
+        else:
+            # gloo (CPU ranks, or a GPU rehearsal staged through the host)
+            pc = s.pcnt.cpu()
+            rcv = torch.zeros_like(pc)
+            dist.all_to_all_single(rcv, pc, group=self.group)
+            sc, rc = pc.numpy(), rcv.numpy()
+            send = s.send.cpu() if self.gpu else s.send
+            recv = torch.zeros_like(send) if self.gpu else s.recv
+            for wk in self._p2p(send, recv, sc, rc):
+                wk.wait()
+            recv.view(w, self.pseg)[:, :4].view(torch.int32)[:, 0].copy_(rcv)
+            if self.gpu:
+                s.recv.copy_(recv)
+            s.rcnt.copy_(rcv)
+        self.stats["sent"] += int(sum(sc))
+        self.stats["received"] += int(sum(rc))
+        self.stats["max_peer"] = max(self.stats["max_peer"], int(max(sc)) if len(sc) else 0)
+        return s
 
     def _receive(self, s: _Slot) -> None:
         """Gather what peers sent (device-side count) and run the whole pipeline on it."""
         p = self._p
-        nr = self.world * self.cap
+        nr = int(self.rx_cap)
         if self.gpu:
+            if s.cev is not None and self.comm is not None:
+                torch.cuda.current_stream(self.dev).wait_event(s.cev)
+            total = int(self.hcnt[1].sum()) if self.comm is not None else int(s.rcnt.sum())
+            if total > nr:                        # more than the receive buffers hold: grow them
+                self._grow_rx(total)
+                nr = int(self.rx_cap)
             self.nf.gather(p(s.recv), self.world, self.rank, self.cap, p(self.rx_pkts), p(self.rx_inmeta),
                            p(self.rx_n), True, self._stream())
             self.dp.launch(p(self.rx_pkts), p(self.rx_inmeta), nr, p(self.rx_out), p(self.rx_meta),
@@ -120,17 +215,19 @@ class RssShardedDataPlane:
             self.rx_out.numpy()[:m] = r.out
             self.rx_meta.numpy().view(np.uint32)[:m] = r.meta
 
-    def exchange(self, s: _Slot):
-        if not self.host_staged:
-            return dist.all_to_all_single(s.recv, s.send, group=self.group, async_op=True)
-        recv = torch.empty(s.recv.shape, dtype=s.recv.dtype)
-        dist.all_to_all_single(recv, s.send.cpu(), group=self.group)
-        s.recv.copy_(recv)
-        return _Done()
+    def _grow_rx(self, n: int) -> None:
+        n = min(int(n * 1.25) + 4096, self.world * self.cap)
+        u8, i32 = dict(dtype=torch.uint8, device=self.dev), dict(dtype=torch.int32, device=self.dev)
+        self.rx_cap = n
+        self.rx_pkts = torch.zeros((n, 64), **u8)
+        self.rx_inmeta = torch.zeros(n, **i32)
+        self.rx_out = torch.zeros((n, 64), **u8)
+        self.rx_meta = torch.zeros(n, **i32)
+        self.rx_lat = torch.zeros((n + 15) // 16, **i32)
 
     def step(self, pkts: torch.Tensor, inmeta: torch.Tensor) -> None:
         """Process one ingress batch; the packets other GPUs sent for this GPU's flows in the
-        previous step are processed here too (call flush() after the last step)."""
+        previous step are exchanged and processed here too (call flush() after the last step)."""
         n = int(pkts.shape[0])
         if n > self.batch:
             raise ValueError("batch larger than the engine was sized for")
@@ -140,18 +237,17 @@ class RssShardedDataPlane:
         if self.gpu:
             self.nf.launch_stamp(self._p(s.t0), self._stream())
         self.n = n
-        self._remote(s, pkts, inmeta, n)
-        work = self.exchange(s)
-        self.flush()
-        self.pending = (s, work)
+        self._local(s, pkts, inmeta, n)
+        self.flush()                # exchange + receive of the previous step, under this step's kernel
+        self.pending = s
         self.k += 1
+        self.stats["steps"] += 1
 
     def flush(self) -> None:
         if self.pending is not None:
-            s, work = self.pending
+            s = self.pending
             self.pending = None
-            work.wait()
-            self._receive(s)
+            self._receive(self.exchange(s))
 
     # ---------------------------------------------------------------- results
     def out_meta(self) -> np.ndarray:

@@ -384,3 +384,50 @@ def test_graphed_run_matches_oracle_and_recaptures_after_commit():
     assert gr.captures == 2
     assert np.array_equal(r.meta.cpu().numpy().view(np.uint32), rc.meta)
     assert (P.meta_fields(rc.meta)[2] == 4).any()     # the new deny rule fired
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world,frac", [(2, 0.3), (4, 0.75)])
+def test_rss_steer_list_matches_cpu_twin(world, frac):
+    """Flow-owner steering by list (the 1-GPU kernel's LIST instance + steer_kernel) against the
+    CPU twin of REMOTE steering: every meta equal, every locally processed slot equal, and each
+    owner's segment holds the same (slot, ingress meta) multiset - count-first, nothing dropped."""
+    import torch
+
+    from dpu_operator_amd.parallel.rss import RssShardedDataPlane, flow_owner, rss_traffic
+    from dpu_operator_amd.parallel.sharded import shard_filter
+
+    engs = {}
+    for dev in ("cuda", "cpu"):
+        dp = DataPlane(device=dev, flow_buckets=1 << 13, hash_mode="lds")
+        sc = S.build_sfc(dp, n_pods=8, n_flows=20000, n_acl=64, flow_filter=shard_filter(0, world))
+        dp.commit(full=True)
+        owner = flow_owner(sc.keys, world, dp.flows.rss_key)
+        pk, im = rss_traffic(sc, 8192, 0, world, owner, frac, seed=7)
+        eng = RssShardedDataPlane(dp, 0, world, 8192, remote_frac=frac)
+        tpk, tim = torch.from_numpy(pk), torch.from_numpy(im.view(np.int32))
+        if dev == "cuda":
+            tpk, tim = tpk.cuda(), tim.cuda()
+        s = eng.slots[0]
+        eng._local(s, tpk, tim, len(pk))
+        if dev == "cuda":
+            torch.cuda.synchronize()
+        engs[dev] = (eng, s)
+    (g, gs), (c, cs) = engs["cuda"], engs["cpu"]
+    assert g.use_list
+    mg, mc = g.out_meta_t.cpu().numpy().view(np.uint32), c.out_meta_t.numpy().view(np.uint32)
+    assert np.array_equal(mg, mc)
+    loc = P.meta_fields(mc)[2] != 10
+    assert np.array_equal(g.out.cpu().numpy()[loc], c.out.numpy()[loc])
+    assert "overflow" not in g.dp.drop_counters()
+    cg, cc = gs.pcnt.cpu().numpy(), cs.pcnt.numpy()
+    assert np.array_equal(cg, cc) and cg.sum() == (~loc).sum() > 0
+    for j in range(1, world):
+        def seg(eng, sl):
+            buf = sl.send.cpu().numpy()
+            n = int(sl.pcnt.cpu().numpy()[j])
+            b = j * eng.pseg
+            slots = buf[b + 64: b + 64 + 64 * n].reshape(n, 64)
+            metas = buf[b + eng.moff: b + eng.moff + 4 * n].view(np.uint32)
+            return sorted(zip(map(bytes, slots), metas.tolist()))
+        assert seg(g, gs) == seg(c, cs)

@@ -231,3 +231,62 @@ def test_dataplane_spans_recorded():
     finally:
         TRACER.enable(False)
         TRACER.clear()
+
+
+class _SockPort:
+    """A TAP stand-in: one end of an AF_UNIX datagram socketpair (frame boundaries kept)."""
+
+    def __init__(self, sock):
+        import socket as _s
+
+        self.s = sock
+        self.s.setblocking(False)
+        self.fd = sock.fileno()
+        self._err = (BlockingIOError, _s.timeout)
+
+    def read(self):
+        try:
+            return self.s.recv(1 << 16)
+        except self._err:
+            return None
+
+    def write(self, frame):
+        self.s.send(frame)
+        return True
+
+
+def test_livepath_cycle_failure_marks_unhealthy_and_recovers():
+    """A failing LivePath cycle (fault point livepath.poll) marks the path unhealthy and the loop
+    restarts itself; once cycles succeed again it is healthy and forwards."""
+    import socket
+    import time
+
+    from dpu_operator_amd.dataplane import tables as T
+    from dpu_operator_amd.dataplane.netio import LivePath
+
+    dp = DataPlane(device="cpu", flow_buckets=1 << 10, mac_slots=1 << 10)
+    for p in range(2):
+        dp.ports.set(p, flags=T.PORT_VALID, bridge_id=3, default_out=1 - p)
+    dp.commit(full=True)
+    pairs = [socket.socketpair(socket.AF_UNIX, socket.SOCK_DGRAM) for _ in range(2)]
+    live = LivePath(dp, {0: _SockPort(pairs[0][0]), 1: _SockPort(pairs[1][0])})
+    FAULTS.arm("livepath.poll", "error", count=3)
+    try:
+        live.start()
+        end = time.monotonic() + 5
+        while live.restarts < 3 and time.monotonic() < end:
+            time.sleep(0.01)
+        assert live.restarts >= 3 and isinstance(live.error, FaultError)
+        while not live.healthy and time.monotonic() < end:
+            time.sleep(0.01)
+        assert live.healthy
+        fr, ln = P.craft(1, dmac="02:00:00:00:00:02", smac="02:00:00:00:00:01", src_ip=1, dst_ip=2, sport=3, dport=4)
+        pairs[0][1].send(bytes(fr[0, : ln[0]]))
+        pairs[1][1].settimeout(5)
+        assert pairs[1][1].recv(1 << 16) == bytes(fr[0, : ln[0]])
+    finally:
+        FAULTS.disarm("livepath.poll")
+        live.stop()
+        for a, b in pairs:
+            a.close()
+            b.close()

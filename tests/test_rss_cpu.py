@@ -70,6 +70,7 @@ def _worker(rank, world, port, q, steps, frac):
             for a, b, m in zip(rin, rout, rmeta):
                 e = expect.get(a.tobytes())
                 ok &= e is not None and e == (b.tobytes(), int(m))
+        ok &= "overflow" not in dp.drop_counters()          # nothing dropped for lack of room
         q.put((rank, ok, n_remote, n_rx))
     except Exception as ex:  # report instead of hanging the parent
         q.put((rank, False, repr(ex), 0))
@@ -77,7 +78,10 @@ def _worker(rank, world, port, q, steps, frac):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,frac", [(2, 0.2), (3, 0.1), (4, 0.05), (8, 0.05)])
+@pytest.mark.parametrize("world,frac", [(2, 0.2), (3, 0.1), (4, 0.05), (8, 0.05),
+                                        # loss-free at any misdirected fraction (count-first exchange):
+                                        # half the traffic, and a producer that does not steer at all
+                                        (2, 0.5), (3, 2 / 3), (4, 0.75)])
 def test_rss_gloo(world, frac):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

@@ -54,12 +54,14 @@ def probe(world: int, batch: int, flows: int, frac: float, iters: int = 30) -> d
     res = {"world": world, "batch": batch, "fused_ms": round(fused_ms, 4)}
     eng = RssShardedDataPlane(dp, 0, world, batch, remote_frac=frac)
     s = eng.slots[0]
-    steer_ms = _time(lambda: eng._remote(s, pk, im, batch), iters)
+    steer_ms = _time(lambda: eng._local(s, pk, im, batch), iters)
     cnt = s.pcnt.cpu().numpy().copy()
-    s.recv.copy_(s.send)
+    s.recv.copy_(s.send)            # rank 0 "receives" what it sent its peers (timing only)
+    s.recv.view(world, eng.pseg)[:, :4].view(torch.int32)[:, 0].copy_(s.pcnt)
+    eng.hcnt[1].copy_(s.pcnt.cpu())
     rx_ms = _time(lambda: eng._receive(s), iters)
     _, _, rs = P.meta_fields(eng.out_meta_t.cpu().numpy().view(np.uint32)[:batch])
-    res.update(rss_steer_ms=round(steer_ms, 4), rss_rx_ms=round(rx_ms, 4),
+    res.update(rss_local_ms=round(steer_ms, 4), rss_rx_ms=round(rx_ms, 4), list_mode=eng.use_list,
                steered_fraction=round(float(np.mean(rs == 10)), 4), segment_counts=cnt.tolist(),
                per_gpu_vs_1gpu=round(fused_ms / (steer_ms + rx_ms), 3))
     return res
