@@ -631,6 +631,18 @@ PYBIND11_MODULE(_nfdp, m) {
         cfg.hash_mode = hash_mode; cfg.acl_mode = acl_mode; cfg.num_cus = num_cus;
         r.start(f, cfg, deadline_s, ptr<const void>(tables, "flows_alt"));
       })
+      .def("stage_tables", [](RingEngine& r, py::dict tables, py::dict d, int which) {
+        FusedLaunch f{};
+        f.t = tables_from(tables);
+        f.acl_wfrag = ptr<const void>(d, "acl_wfrag"); f.acl_cinit = ptr<const void>(d, "acl_cinit");
+        f.acl_tiles = val<uint32_t>(d, "acl_tiles", 1);
+        f.toep_frag = ptr<const void>(d, "toep_frag"); f.toep_tab = ptr<const uint32_t>(d, "toep_tab");
+        py::gil_scoped_release nogil;
+        r.stage_tables(f, which);
+      })
+      .def("flip_tables", &RingEngine::flip_tables)
+      .def_property_readonly("table_set", &RingEngine::table_set)
+      .def_property_readonly("lds_acl_tiles", &RingEngine::lds_acl_tiles)
       .def("flip", &RingEngine::flip)
       .def("bump_epoch", &RingEngine::bump_epoch)
       .def("grace_over", &RingEngine::grace_over)

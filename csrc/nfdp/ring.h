@@ -61,13 +61,37 @@ constexpr uint64_t kRingEpochMask = (1ull << kRingEpochBits) - 1;
 __host__ __device__ inline uint64_t ring_word(uint64_t count, uint32_t epoch) {
   return (count << kRingEpochBits) | (epoch & kRingEpochMask);
 }
-// Epoch aliasing guard: the host lets at most kRingEpochMask epoch changes happen within
+// Epoch layout (7 bits): bit 0 = flow-table copy, bit 1 = table set (coop rings: every other
+// table, double buffered in device memory and restaged into LDS when it changes), bits 6..2 = a
+// generation bumped by every change (a wave seeing any change drops its cached table lines).
+constexpr uint32_t kEpochFlowBit = 1u, kEpochSetBit = 2u, kEpochGenShift = 2u, kEpochGenMask = 0x1Fu;
+__host__ __device__ inline uint32_t epoch_next_gen(uint32_t e) {
+  return (e & (kEpochFlowBit | kEpochSetBit)) | ((((e >> kEpochGenShift) + 1u) & kEpochGenMask) << kEpochGenShift);
+}
+// Epoch aliasing guard: the host lets at most kEpochGenMask epoch changes happen within
 // kEpochAliasHostUs; a wave whose previous chunk is older than kEpochAliasTicks (half of it, in
 // s_memrealtime ticks) drops its cached table lines whatever epoch value it sees.
 constexpr uint32_t kEpochAliasHostUs = 100;
 constexpr unsigned long long kEpochAliasTicks = kEpochAliasHostUs * 100ull / 2;   // 100 MHz
 __host__ __device__ inline uint64_t ring_count(uint64_t w) { return (w & ~kRingStop) >> kRingEpochBits; }
 __host__ __device__ inline uint32_t ring_epoch(uint64_t w) { return (uint32_t)(w & kRingEpochMask); }
+
+// Everything a coop ring's per-packet stages read besides the flow table: double buffered in
+// device memory (table set = epoch bit 1).  A commit writes the idle set and flips; every
+// workgroup restages its LDS copies (ports, chains, ACL verdicts and rule tiles, Toeplitz tables)
+// from the new set at the first chunk that carries it.  No drain, no relaunch.  `serial` counts
+// the host's uploads: a workgroup idle through two flips sees the same set bit again, the serial
+// tells it the set was rewritten meanwhile.
+struct RingTableSet {
+  TablesView t;
+  const void* acl_wfrag;
+  const void* acl_cinit;
+  const void* toep_frag;
+  const uint32_t* toep_tab;
+  uint32_t acl_tiles;
+  uint32_t serial;
+  uint32_t pad[2];
+};
 
 // Host -> device control block, pinned coherent host memory (one 64-B line).
 struct alignas(64) RingCtl {
@@ -143,9 +167,18 @@ class RingEngine {
   // Grace period of the last flip: every chunk published before it has completed.
   bool grace_over() { return completed() >= flip_prod(); }
   bool wait_grace(double timeout_s);
-  // Epoch + 2 (same flow-table copy): chunks published from now on make their waves drop cached
+  // New generation, same copies: chunks published from now on make their waves drop cached
   // table lines first (after the host changed a table in place, e.g. MAC learning).
   uint32_t bump_epoch();
+  // Coop rings: write table set `which` (the idle one: 1 - table_set()) ...
+  void stage_tables(const FusedLaunch& f, int which);
+  // ... and switch to it (same grace rule as flip()).  Returns the new epoch.
+  uint32_t flip_tables();
+  int table_set() const {
+    std::lock_guard<std::mutex> g(mu_);
+    return (int)((epoch_ & kEpochSetBit) >> 1);
+  }
+  uint32_t lds_acl_tiles() const { return lds_tiles_; }   // ACL tiles the running grid's LDS holds
   uint32_t epoch() const {
     std::lock_guard<std::mutex> g(mu_);
     return epoch_;
@@ -189,6 +222,9 @@ class RingEngine {
   bool running_ = false;
   int device_ = 0;
   FusedLaunch launch_{};
+  RingTableSet* d_sets_ = nullptr;   // [2] device table sets (coop rings)
+  uint32_t lds_tiles_ = 0;
+  uint32_t set_serial_ = 0;
 };
 
 // Launch the persistent kernel (ring.hip).  Exposed for the engine only.
@@ -199,6 +235,9 @@ struct RingLaunch {
   RingCtl* ctl; uint32_t* flags; RingDevState* st; uint32_t* svc;
   unsigned long long deadline_ticks;
   const void* flows_alt;  // second flow-table copy (epoch & 1 == 1); f.t.flows is copy 0
+  const RingTableSet* sets;   // coop: the two table sets
+  uint32_t lds_tiles;         // coop: ACL tiles the LDS layout is sized for (>= any set's tiles)
+  uint32_t epoch0;            // epoch at launch (its set bit names the set to stage first)
 };
 hipError_t launch_ring(const RingLaunch& r, const LaunchCfg& cfg, int wgs_per_cu, bool coop, hipStream_t s);
 

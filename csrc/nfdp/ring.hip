@@ -26,6 +26,9 @@ struct RingArgs {
   const v4i* toep_frag; const uint32_t* toep_tab;
   unsigned long long deadline;
   const void* flows2[2];  // flow-table copies by epoch parity (the same pointer twice if not double buffered)
+  const RingTableSet* sets;  // coop: table sets by epoch bit 1
+  uint32_t lds_tiles;        // coop: ACL tiles the LDS layout holds
+  uint32_t epoch0;
   SideOut side;           // side list (cnt null = off): slots needing replicas / learn events / outer headers
   uint32_t flags_bits;  // bit2: no per-flow counts; bits 5/6: diagnostics (kRingTrace, kRingNoCounters)
 };
@@ -145,27 +148,56 @@ template <int HASH, int ACL, bool COOP>
 __global__ __launch_bounds__(kRingBlock) void ring_kernel(RingArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ unsigned long long coop_tk;                      // ticket
-  __shared__ uint32_t coop_ctl[2];                            // go, epoch
+  __shared__ uint32_t coop_ctl[3];                            // go, epoch, table-set serial
   __shared__ uint32_t coop_best[COOP ? kRingWaves : 1][64];   // per-wave ACL partial minima
-  const RingLds L = ring_lds(HASH, ACL, a.acl_tiles);
+  __shared__ RingTableSet lset;                               // coop: the table set in use (LDS copy)
+  const RingLds L = ring_lds(HASH, ACL, COOP ? a.lds_tiles : a.acl_tiles);
   v4i* lw = reinterpret_cast<v4i*>(smem + L.acl_w);
   v4i* lc = reinterpret_cast<v4i*>(smem + L.acl_c);
   v4i* lt = reinterpret_cast<v4i*>(smem + L.toep_f);
   uint32_t* ltab = reinterpret_cast<uint32_t*>(smem + L.toep_t);
-  if constexpr (ACL == kAclMfma) {
-    const uint32_t lt_ = min(a.acl_tiles, kLdsAclTiles), nw = lt_ * 64, nc = lt_ * 4;
-    for (uint32_t i = threadIdx.x; i < nw; i += kRingBlock) lw[i] = a.acl_wfrag[i];
-    for (uint32_t i = threadIdx.x; i < nc; i += kRingBlock) lc[i] = a.acl_cinit[i];
+  PortEntry* lport = reinterpret_cast<PortEntry*>(smem + L.tports);
+  uint64_t* lchain = reinterpret_cast<uint64_t*>(smem + L.tchain);
+  uint8_t* lperm = smem + L.tperm;
+  // (Re)stage the small tables of a table set into LDS: all threads of the workgroup call it.
+  // Non-coop rings stage the launch tables once (a commit drains and relaunches them).
+  uint32_t cur_set = 0, cur_serial = 0, nport = 0, nchain = 0;
+  bool lds_perm = false;
+  auto stage = [&](const TablesView& t, const v4i* wf, const v4i* ci, uint32_t tiles, const v4i* tf,
+                   const uint32_t* tt) {
+    if constexpr (ACL == kAclMfma) {
+      const uint32_t lt_ = min(tiles, kLdsAclTiles), nw = lt_ * 64, nc = lt_ * 4;
+      for (uint32_t i = threadIdx.x; i < nw; i += kRingBlock) lw[i] = wf[i];
+      for (uint32_t i = threadIdx.x; i < nc; i += kRingBlock) lc[i] = ci[i];
+    }
+    if constexpr (HASH == kHashMfma)
+      for (uint32_t i = threadIdx.x; i < 256; i += kRingBlock) lt[i] = tf[i];
+    if constexpr (HASH == kHashLds)
+      for (uint32_t i = threadIdx.x; i < 4096; i += kRingBlock) ltab[i] = tt[i];
+    // ports / chain words / ACL verdicts in LDS: the per-packet path's only global loads are the
+    // frame and the flow bucket
+    const LdsTables s0 = stage_lds_tables(t, lport, lchain, lperm, true, kRingBlock);
+    nport = s0.nport; nchain = s0.nchain; lds_perm = s0.lds_perm;
+  };
+  auto stage_set = [&](uint32_t which) {
+    __syncthreads();   // no wave still reads the previous copies
+    // the set's buffers are fresh allocations that may reuse addresses this CU / XCD still caches
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(a.sets + which);
+    uint32_t* dst = reinterpret_cast<uint32_t*>(&lset);
+    for (uint32_t i = threadIdx.x; i < sizeof(RingTableSet) / 4; i += kRingBlock) dst[i] = src[i];
+    __syncthreads();
+    stage(lset.t, static_cast<const v4i*>(lset.acl_wfrag), static_cast<const v4i*>(lset.acl_cinit), lset.acl_tiles,
+          static_cast<const v4i*>(lset.toep_frag), lset.toep_tab);
+    cur_set = which;
+    cur_serial = lset.serial;
+    __syncthreads();
+  };
+  if constexpr (COOP) {
+    stage_set((a.epoch0 & kEpochSetBit) >> 1);
+  } else {
+    stage(a.t, a.acl_wfrag, a.acl_cinit, a.acl_tiles, a.toep_frag, a.toep_tab);
   }
-  const AclView av{lw, lc, a.acl_wfrag, a.acl_cinit, a.acl_tiles};
-  if constexpr (HASH == kHashMfma)
-    for (uint32_t i = threadIdx.x; i < 256; i += kRingBlock) lt[i] = a.toep_frag[i];
-  if constexpr (HASH == kHashLds)
-    for (uint32_t i = threadIdx.x; i < 4096; i += kRingBlock) ltab[i] = a.toep_tab[i];
-  // ports / chain words / ACL verdicts in LDS: the per-packet path's only global loads are the
-  // frame and the flow bucket (a session never sees a table change: commit relaunches the grid)
-  const LdsTables ta = stage_lds_tables(a.t, reinterpret_cast<PortEntry*>(smem + L.tports),
-                                        reinterpret_cast<uint64_t*>(smem + L.tchain), smem + L.tperm, true, kRingBlock);
   uint32_t* pc = reinterpret_cast<uint32_t*>(smem + L.pc);
   uint32_t* drops = reinterpret_cast<uint32_t*>(smem + L.drops);
   for (uint32_t i = threadIdx.x; i < kLdsPorts * 4; i += kRingBlock) pc[i] = 0;
@@ -191,6 +223,8 @@ __global__ __launch_bounds__(kRingBlock) void ring_kernel(RingArgs a) {
   const unsigned long long t_begin = __builtin_amdgcn_s_memrealtime();
   uint32_t seen_epoch = 0xFFFFFFFFu;  // epoch of this wave's previous chunk
   unsigned long long seen_t = 0;      // when this wave took its previous chunk
+  uint32_t w0_epoch = 0xFFFFFFFFu;    // coop wave 0: epoch / time of the workgroup's previous chunk
+  unsigned long long w0_t = 0;
 
   for (;;) {
     unsigned long long tk = 0;
@@ -198,7 +232,18 @@ __global__ __launch_bounds__(kRingBlock) void ring_kernel(RingArgs a) {
     if constexpr (COOP) {
       if (wave == 0) {
         const bool go = ring_wait_chunk(a, lane, t_begin, tk, epoch, on_idle);
-        if (lane == 0) { coop_tk = tk; coop_ctl[0] = go ? 1u : 0u; coop_ctl[1] = epoch; }
+        // the serial of the set this epoch names, read only when the epoch moved (or the
+        // workgroup idled long enough for the epoch value to have come round again)
+        uint32_t ser = cur_serial;
+        const unsigned long long tn = __builtin_amdgcn_s_memrealtime();
+        if (go && (epoch != w0_epoch || tn - w0_t > kEpochAliasTicks)) {
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          ser = __hip_atomic_load(&a.sets[(epoch & kEpochSetBit) >> 1].serial, __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT);
+        }
+        w0_epoch = epoch;
+        w0_t = tn;
+        if (lane == 0) { coop_tk = tk; coop_ctl[0] = go ? 1u : 0u; coop_ctl[1] = epoch; coop_ctl[2] = ser; }
       }
       __syncthreads();
       tk = rfl64(coop_tk);
@@ -210,16 +255,27 @@ __global__ __launch_bounds__(kRingBlock) void ring_kernel(RingArgs a) {
     const unsigned long long t_avail = __builtin_amdgcn_s_memrealtime();
     if (epoch != seen_epoch || t_avail - seen_t > kEpochAliasTicks) {
       // A new epoch: the host rewrote a table this kernel reads with ordinary cached loads (the
-      // flow-table copy it now names, or the MAC table after learning).  The lines this wave's
-      // CU L1 and its XCD's L2 still hold may be stale - this grid never sees the cache
-      // invalidate a kernel launch brings - so drop them (agent-scope acquire) before probing.
-      // The epoch is 7 bits: a wave idle through a multiple of 128 changes would see its old
-      // value again.  The host spaces any 128 consecutive changes over >= kEpochAliasHostUs, so a
+      // flow-table copy it now names, the table set, or the MAC table after learning).  The
+      // lines this wave's CU L1 and its XCD's L2 still hold may be stale - this grid never sees
+      // the cache invalidate a kernel launch brings - so drop them (agent-scope acquire) first.
+      // The generation is 5 bits: a wave idle through a multiple of 32 changes would see its old
+      // value again.  The host spaces any 32 consecutive changes over >= kEpochAliasHostUs, so a
       // wave whose previous chunk is older than half of that invalidates regardless.
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       seen_epoch = epoch;
     }
     seen_t = t_avail;
+    if constexpr (COOP) {
+      // a new table set: every wave of the workgroup holds the same epoch (wave 0 broadcast it),
+      // so the branch is uniform and the barriers inside are safe
+      const uint32_t want = (epoch & kEpochSetBit) >> 1;
+      if (want != cur_set || __builtin_amdgcn_readfirstlane(coop_ctl[2]) != cur_serial) stage_set(want);
+    }
+    const TablesView& T = COOP ? lset.t : a.t;
+    const LdsTables ta{T, lport, lchain, lperm, nport, nchain, lds_perm};
+    const AclView av = COOP ? AclView{lw, lc, static_cast<const v4i*>(lset.acl_wfrag),
+                                      static_cast<const v4i*>(lset.acl_cinit), lset.acl_tiles}
+                            : AclView{lw, lc, a.acl_wfrag, a.acl_cinit, a.acl_tiles};
     const bool trace = (a.flags_bits & kRingTrace) != 0 && wave == 0;
     uint32_t tr0 = 0, tr1 = 0, tr2 = 0, tr3 = 0, tr4 = 0, tr5 = 0;
 #define NFDP_RING_MARK(var)                                                 \
@@ -243,20 +299,20 @@ __global__ __launch_bounds__(kRingBlock) void ring_kernel(RingArgs a) {
     NFDP_RING_MARK(tr0)
     Parsed p;
     IngressState st;
-    ingress_stage(a.t, ta, d, im, p, st);
+    ingress_stage(T, ta, d, im, p, st);
     uint32_t hash = 0;
     int acl_rule = -1;
     if constexpr (COOP && ACL == kAclMfma) {
       uint32_t b = 0xFFFFFFFFu;
-      classify_wave<HASH, ACL>(st.key, kx, av, lt, ltab, a.t, hash, acl_rule, wave, kRingWaves, &b);
+      classify_wave<HASH, ACL>(st.key, kx, av, lt, ltab, T, hash, acl_rule, wave, kRingWaves, &b);
       coop_best[wave][lane] = b;
       __syncthreads();
       if (wave != 0) continue;  // helpers go back to wait for the next chunk
       b = min(min(coop_best[0][lane], coop_best[1][lane]), min(coop_best[2][lane], coop_best[3][lane]));
-      acl_rule = acl_rule_of(b, a.t.n_acl);
+      acl_rule = acl_rule_of(b, T.n_acl);
     } else {
       if (COOP && wave != 0) continue;  // nothing to share without the MFMA ACL
-      classify_wave<HASH, ACL>(st.key, kx, av, lt, ltab, a.t, hash, acl_rule);
+      classify_wave<HASH, ACL>(st.key, kx, av, lt, ltab, T, hash, acl_rule);
     }
     NFDP_RING_MARK(tr1)
     bool hit = false;
@@ -264,7 +320,7 @@ __global__ __launch_bounds__(kRingBlock) void ring_kernel(RingArgs a) {
     int64_t slot = -1;
     if (!st.reason && p.ipv4) {
       uint4 v;
-      TablesView tv = a.t;
+      TablesView tv = T;
       tv.flows = static_cast<const FlowSlot*>(a.flows2[epoch & 1u]);
       slot = flow_probe(tv, st.key, hash, v);
       if (slot >= 0) {
@@ -274,7 +330,7 @@ __global__ __launch_bounds__(kRingBlock) void ring_kernel(RingArgs a) {
       }
     }
     NFDP_RING_MARK(tr2)
-    const EgressDecision e = chain_stage(a.t, ta, p, st, hit, act, acl_rule, hash);
+    const EgressDecision e = chain_stage(T, ta, p, st, hit, act, acl_rule, hash);
     const uint32_t olen = egress_len(p, e);
     uint32_t o[kSlotDwords];
     emit(p, e.tci, e.push != 0, o);
@@ -334,7 +390,7 @@ __global__ __launch_bounds__(kRingBlock) void ring_kernel(RingArgs a) {
 
 template <int H, int A, bool C>
 static hipError_t launch_ring_t(const RingArgs& a, int num_cus, int wgs, hipStream_t s) {
-  const size_t lds = ring_lds(H, A, a.acl_tiles).total;
+  const size_t lds = ring_lds(H, A, C ? a.lds_tiles : a.acl_tiles).total;
   if (lds > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&ring_kernel<H, A, C>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -365,6 +421,10 @@ hipError_t launch_ring(const RingLaunch& r, const LaunchCfg& cfg, int wgs_per_cu
   a.flows2[0] = r.f.t.flows;
   a.flows2[1] = r.flows_alt ? r.flows_alt : r.f.t.flows;
   a.flags_bits = r.f.flags;
+  a.sets = r.sets;
+  a.lds_tiles = r.lds_tiles;
+  a.epoch0 = r.epoch0;
+  if (coop && (!a.sets || a.lds_tiles < a.acl_tiles)) return hipErrorInvalidValue;
   if (!a.port_ctr || !a.drop_ctr || !a.ctl || !a.flags || !a.st) return hipErrorInvalidValue;
   if (((r.ring_mask + 1) & r.ring_mask) != 0 || r.ring_mask < 63) return hipErrorInvalidValue;
   if (cfg.acl_mode == kAclMfma && (a.acl_tiles == 0 || a.acl_tiles > kAclMaxRules / 16 || !a.acl_wfrag || !a.acl_cinit))
@@ -429,6 +489,8 @@ RingEngine::RingEngine(uint32_t capacity, int num_cus, int wgs_per_cu, bool coop
   slot_alloc(reinterpret_cast<void**>(&d_out_), (size_t)capacity * 64, "alloc out");
   slot_alloc(reinterpret_cast<void**>(&d_meta_), (size_t)capacity * 4, "alloc meta");
   ck(hipMalloc(reinterpret_cast<void**>(&d_svc_), (size_t)nch_ * 4 * kSvcWords), "dev alloc svc");
+  ck(hipMalloc(reinterpret_cast<void**>(&d_sets_), 2 * sizeof(RingTableSet)), "dev alloc table sets");
+  ck(hipMemset(d_sets_, 0, 2 * sizeof(RingTableSet)), "memset");
   ck(hipMemset(d_svc_, 0, (size_t)nch_ * 4 * kSvcWords), "memset");
   ck(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "stream");
 }
@@ -440,7 +502,7 @@ RingEngine::~RingEngine() {
   }
   (void)hipStreamSynchronize(stream_);
   (void)hipStreamDestroy(stream_);
-  for (void* d : {(void*)st_, (void*)d_svc_}) (void)hipFree(d);
+  for (void* d : {(void*)st_, (void*)d_svc_, (void*)d_sets_}) (void)hipFree(d);
   if (host_slots_) {
     for (void* h : host_ptrs_) (void)hipHostFree(h);
   } else {
@@ -462,8 +524,15 @@ void RingEngine::start(const FusedLaunch& f, const LaunchCfg& cfg, double deadli
   ck(hipMemcpyAsync(st_, &s, sizeof(s), hipMemcpyHostToDevice, stream_), "state upload");
   ck(hipStreamSynchronize(stream_), "state upload");  // `s` lives on this stack frame
   launch_ = f;
+  // coop rings: the session's tables are table set (epoch bit 1); the LDS layout holds up to
+  // kLdsAclTiles rule tiles, so a later set with more tiles than that needs a relaunch
+  lds_tiles_ = coop_ ? std::max<uint32_t>(f.acl_tiles, kLdsAclTiles) : f.acl_tiles;
+  if (coop_) stage_tables(f, (int)((epoch_ & kEpochSetBit) >> 1));
   RingLaunch r;
   r.f = f;
+  r.sets = d_sets_;
+  r.lds_tiles = lds_tiles_;
+  r.epoch0 = epoch_;
   r.pkts = d_in_; r.inmeta = d_im_; r.out = d_out_; r.out_meta = d_meta_;
   r.ring_mask = cap_ - 1;
   void* dctl = nullptr;
@@ -523,10 +592,10 @@ uint64_t RingEngine::publish(uint32_t n, bool check_room) {
 }
 
 void RingEngine::pace_epoch_change() {
-  // (mu_ held) at most kRingEpochMask changes within kEpochAliasHostUs: the value a wave saw
+  // (mu_ held) at most kEpochGenMask changes within kEpochAliasHostUs: the value a wave saw
   // cannot come round again before its idle-time invalidation (ring_kernel) takes over
   const auto now = Clock::now();
-  if (epoch_changes_.size() >= kRingEpochMask) {
+  if (epoch_changes_.size() >= kEpochGenMask) {
     const auto ready = epoch_changes_.front() + std::chrono::microseconds(kEpochAliasHostUs);
     while (Clock::now() < ready) _mm_pause();
     epoch_changes_.pop_front();
@@ -538,7 +607,7 @@ uint32_t RingEngine::flip() {
   if (!grace_over()) throw std::runtime_error("ring: flip before the previous flip's grace period ended");
   std::lock_guard<std::mutex> g(mu_);
   pace_epoch_change();
-  epoch_ = (epoch_ + 1) & (uint32_t)kRingEpochMask;
+  epoch_ = epoch_next_gen(epoch_) ^ kEpochFlowBit;
   flip_prod_ = prod_;
   // same count, new epoch: chunks published from here on carry it (the frontier mirrors a word
   // only when its count grows, so this store alone changes nothing for waiting waves)
@@ -549,7 +618,41 @@ uint32_t RingEngine::flip() {
 uint32_t RingEngine::bump_epoch() {
   std::lock_guard<std::mutex> g(mu_);
   pace_epoch_change();
-  epoch_ = (epoch_ + 2) & (uint32_t)kRingEpochMask;
+  epoch_ = epoch_next_gen(epoch_);
+  if (running_) __atomic_store_n(&ctl_->prod, ring_word(prod_, epoch_), __ATOMIC_RELEASE);
+  return epoch_;
+}
+
+void RingEngine::stage_tables(const FusedLaunch& f, int which) {
+  if (which < 0 || which > 1) throw std::invalid_argument("ring: table set 0 or 1");
+  // (the LDS layout of a coop grid holds kLdsAclTiles rule tiles: any set fits, tiles beyond them
+  // are read from the set's global copy by the kernel as usual)
+  RingTableSet ts{};
+  ts.t = f.t;
+  ts.acl_wfrag = f.acl_wfrag; ts.acl_cinit = f.acl_cinit; ts.acl_tiles = f.acl_tiles;
+  ts.toep_frag = f.toep_frag; ts.toep_tab = f.toep_tab;
+  ts.serial = ++set_serial_;
+  // a copy on the engine's own stream would queue behind the resident kernel: a private
+  // non-blocking stream (the grid never reads the idle set)
+  static thread_local hipStream_t cs = nullptr;
+  if (!cs) ck(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking), "stream");
+  ck(hipMemcpyAsync(d_sets_ + which, &ts, sizeof(ts), hipMemcpyHostToDevice, cs), "table set upload");
+  ck(hipStreamSynchronize(cs), "table set upload");
+  if (running_) {
+    // the side pass (iox / RingPath.side_pass) reads the session's tables from launch()
+    launch_.t = f.t;
+    launch_.acl_wfrag = f.acl_wfrag; launch_.acl_cinit = f.acl_cinit; launch_.acl_tiles = f.acl_tiles;
+    launch_.toep_frag = f.toep_frag; launch_.toep_tab = f.toep_tab;
+  }
+}
+
+uint32_t RingEngine::flip_tables() {
+  if (!coop_) throw std::runtime_error("ring: live table sets need a coop ring");
+  if (!grace_over()) throw std::runtime_error("ring: flip before the previous flip's grace period ended");
+  std::lock_guard<std::mutex> g(mu_);
+  pace_epoch_change();
+  epoch_ = epoch_next_gen(epoch_) ^ kEpochSetBit;
+  flip_prod_ = prod_;
   if (running_) __atomic_store_n(&ctl_->prod, ring_word(prod_, epoch_), __ATOMIC_RELEASE);
   return epoch_;
 }

@@ -167,6 +167,9 @@ class DataPlane:
             if rings and not full and self._only_flows_pending():
                 with TRACER.span("dataplane.commit_live"):
                     return self._commit_flows_live(rings)
+            if rings and not full and all(getattr(r, "coop", False) for r in rings) and "flows_b" in self._dev:
+                with TRACER.span("dataplane.commit_tables_live"):
+                    return self._commit_tables_live(rings)
             for r in rings:
                 r.stop()
             with TRACER.span("dataplane.commit", full=full):
@@ -246,6 +249,37 @@ class DataPlane:
         self.flip_stats["update_s"] += time.perf_counter() - t1
         self.flip_stats["buckets"] += int(len(rows))
         return {"flow_buckets": int(len(dirty)), "flip": self._flow_active}
+
+    def _commit_tables_live(self, rings) -> dict:
+        """Any table change under running coop rings, without draining them: flows go through the
+        flow-table flip; every other changed table is uploaded into NEW device buffers (the
+        running grid still reads the old ones), the idle table set of each ring is pointed at
+        them and the rings flip to it - their workgroups restage the LDS copies at the first
+        chunk that carries the new epoch.  The old buffers live until the flip's grace period is
+        over (the next live commit waits for it, then lets them go)."""
+        t0 = time.perf_counter()
+        sent = {}
+        sent.update(self._commit_flows_live(rings))   # flow buckets by their own flip ({} without any)
+        for r in rings:
+            if not r.eng.wait_grace(10.0):
+                raise TimeoutError("ring: grace period of the previous flip did not end")
+        self._retired = dict(self._dev)             # the running set's buffers stay alive
+        sent.update(self._commit(False))
+        torch = _torch()
+        torch.cuda.current_stream(self.tdev).synchronize()   # uploads complete before any wave can see them
+        tables = self.tables_ptrs()
+        tables["flows"], tables["flows_alt"] = self.flow_copy_ptrs()
+        args = {"acl_wfrag": self._ptr("acl_wfrag"), "acl_cinit": self._ptr("acl_cinit"), "acl_tiles": self._acl_tiles,
+                "toep_frag": self._ptr("toep_frag"), "toep_tab": self._ptr("toep_tab")}
+        for r in rings:
+            with r.lock:
+                r.eng.stage_tables(tables, args, 1 - int(r.eng.table_set))
+                r.eng.flip_tables()
+        self._gen += 1
+        self.flip_stats["table_flips"] = self.flip_stats.get("table_flips", 0) + 1
+        self.flip_stats["table_update_s"] = self.flip_stats.get("table_update_s", 0.0) + time.perf_counter() - t0
+        sent["table_flip"] = True
+        return sent
 
     def _commit(self, full: bool) -> dict:
         sent = {}

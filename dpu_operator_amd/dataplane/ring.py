@@ -66,6 +66,7 @@ class RingPath:
         # a burst (publish -> wait -> read) and a stop / relaunch for a table commit exclude
         # each other: DataPlane.commit() may run on another thread (the VSP's RPCs)
         self.lock = threading.RLock()
+        self.launches = 0            # grid launches (start / resume after a drain)
         rings = getattr(dp, "_rings", None)
         if rings is None:
             dp._rings = rings = []
@@ -123,6 +124,7 @@ class RingPath:
         self.eng.set_epoch(self.dp._flow_active)
         self.eng.start(self._tables(), self._args(), self.dp.hash_mode, self.dp.acl_mode,
                        int(self.dp.num_cus), self.deadline_s)
+        self.launches += 1
 
     def stop(self, timeout_s: float = 30.0) -> None:
         with self.lock:
@@ -135,6 +137,7 @@ class RingPath:
             self.eng.set_epoch(self.dp._flow_active)
             self.eng.start(self._tables(), self._args(), self.dp.hash_mode, self.dp.acl_mode,
                            int(self.dp.num_cus), self.deadline_s)
+            self.launches += 1
 
     def ensure_alive(self) -> bool:
         """Relaunch a ring whose grid left on its own (device deadline); True if it was relaunched."""

@@ -1,6 +1,6 @@
 """Persistent ring kernel (csrc/nfdp/ring.hip): bit-exact with the oracle, drain-on-stop, table
-commits while running (flow updates by epoch flip without stopping the kernel, other tables by
-drain + relaunch), flow churn at >= 100K flows/s under a forwarding ring, device-side deadline,
+commits while running (flow updates by epoch flip, other tables by a table-set flip: the
+kernel is never stopped), flow churn at >= 100K flows/s under a forwarding ring, device-side deadline,
 closed-loop latency probe."""
 import threading
 import time
@@ -74,7 +74,7 @@ def test_ring_bit_exact_and_counters(coop, host_slots, hash_mode, n_acl):
 def test_ring_laps_and_commit_while_running():
     """Several laps of the ring, then a flow update while the kernel is resident: commit()
     writes the idle flow-table copy and flips the epoch (the kernel keeps running), and the next
-    lap sees the new table.  Then a port change: drain + relaunch."""
+    lap sees the new table.  Then a port change: a table-set flip, also without a relaunch."""
     g, sc = _build("cuda")
     c, _ = _build("cpu")
     pk, im = _traffic(sc)
@@ -92,7 +92,7 @@ def test_ring_laps_and_commit_while_running():
             for k in victims:
                 dp.flows.erase(k)
         sent = g.commit()                        # flows only: epoch flip under the running kernel
-        assert sent.get("flip") == 1 and g.flip_stats["flips"] == 1 and ring.eng.epoch == 1
+        assert sent.get("flip") == 1 and g.flip_stats["flips"] == 1 and ring.eng.epoch & 1 == 1
         assert ring.running
         end = ring.publish(CAP)
         ring.wait(end, 10.0)
@@ -103,12 +103,14 @@ def test_ring_laps_and_commit_while_running():
         rc = c.run(pk, im)
         assert np.array_equal(meta, rc.meta)
         assert np.array_equal(out, rc.out)
-        # a port change is staged in LDS by the kernel: drain, update, relaunch
+        # a port change is staged in LDS by the kernel: the coop ring flips to a new table set,
+        # its workgroups restage LDS at the next chunk (no drain, no relaunch)
         ring.start()
+        launches = ring.launches
         for dp in (g, c):
             dp.ports.update(int(sc.pod_port[1]), mtu=20)   # everything to pod 1 is now too big
-        g.commit()
-        assert ring.running
+        sent = g.commit()
+        assert sent.get("table_flip") and ring.running and ring.launches == launches
         end = ring.publish(CAP)
         ring.wait(end, 10.0)
         ring.stop()
@@ -305,3 +307,92 @@ def test_ring_live_flow_churn_no_torn_lookups():
     assert laps >= 10 and hits > 0.9 * laps * CAPL * 0.5
     assert rate >= 100e3, rate
     assert dp.flip_stats["flips"] == stats["commits"]
+
+
+@pytest.mark.gpu
+def test_ring_table_updates_live_without_drain():
+    """Port / ACL / link-state changes at ~1 kHz while a coop ring forwards: every commit flips
+    the ring's table set (its workgroups restage LDS), the grid is never stopped or relaunched,
+    every published chunk completes, and the final lap is bit-exact with the oracle holding the
+    final tables."""
+    g, sc = _build("cuda", n_acl=64)
+    c, _ = _build("cpu", n_acl=64)
+    pk, im = _traffic(sc)
+    ring = RingPath(g, capacity=CAP, deadline_s=60.0, coop=True)
+    stop = threading.Event()
+    done = {"commits": 0, "laps": 0}
+    err = []
+    try:
+        ring.stage(pk, im)
+        ring.start()
+        launches = ring.launches
+
+        def control():
+            k = 0
+            try:
+                while not stop.is_set():
+                    port = int(sc.pod_port[k % 4 + 4])
+                    g.ports.update(port, mtu=1400 + (k % 50))        # CreateBridgePort-style edits
+                    if k % 3 == 0:
+                        g.ports.set_link(port, k % 2 == 0)          # agent link flaps
+                    if k % 7 == 0:
+                        g.acl.add(permit=False, dst=f"192.0.{k % 250}.0/24", dport=9)   # ACL edits
+                    g.commit()
+                    done["commits"] += 1
+                    k += 1
+                    time.sleep(0.001)
+            except Exception as e:  # noqa: BLE001
+                err.append(e)
+
+        th = threading.Thread(target=control)
+        th.start()
+        t_end = time.time() + 3.0
+        while time.time() < t_end:
+            end = ring.publish(CAP)
+            ring.wait(end, 10.0)
+            done["laps"] += 1
+        stop.set()
+        th.join()
+        assert not err, err
+        assert ring.running and ring.eng.alive() and ring.launches == launches
+        assert done["commits"] >= 500 and g.flip_stats["table_flips"] >= done["commits"] - 1
+        assert ring.completed() == ring.eng.published
+        per_commit_ms = 1e3 * g.flip_stats["table_update_s"] / g.flip_stats["table_flips"]
+        print(f"live table commits: {done['commits']} in 3 s, {per_commit_ms:.3f} ms each, ring stall 0, "
+              f"{done['laps']} laps")
+        # the stall a commit costs the packets: closed-loop chunk latency with and without a
+        # table flip every millisecond (a workgroup restages its LDS copy at the first chunk of
+        # a new set; nothing is drained)
+        base, _ = ring.probe(batches=3000, batch=64, inflight=1)
+        stop.clear()
+        th = threading.Thread(target=control)
+        th.start()
+        flips0 = g.flip_stats["table_flips"]
+        churn, el = ring.probe(batches=6000, batch=64, inflight=1)
+        stop.set()
+        th.join()
+        assert not err, err
+        nflip = g.flip_stats["table_flips"] - flips0
+        stall = float(np.max(churn) - np.percentile(base, 50))
+        print(f"probe p50/p99/max us: idle {np.percentile(base, 50):.2f}/{np.percentile(base, 99):.2f}/"
+              f"{np.max(base):.2f}, with {nflip} table flips {np.percentile(churn, 50):.2f}/"
+              f"{np.percentile(churn, 99):.2f}/{np.max(churn):.2f}; worst commit stall {stall:.2f} us")
+        assert nflip >= 100 and ring.launches == launches
+        assert np.percentile(churn, 99) < np.percentile(base, 99) + 50.0
+        # the final tables: mirror them into the oracle and compare one more lap
+        c.ports.a[:] = g.ports.a
+        c.ports.version += 1
+        c.acl.rules = list(g.acl.rules)
+        c.acl.version += 1
+        c.commit()
+        g.commit()
+        end = ring.publish(CAP)
+        ring.wait(end, 10.0)
+        ring.stop()
+        out, meta = ring.results()
+    finally:
+        stop.set()
+        ring.close()
+    rc = c.run(pk, im)
+    assert np.array_equal(meta, rc.meta)
+    assert np.array_equal(out, rc.out)
