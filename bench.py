@@ -139,6 +139,16 @@ def measure_variants(a, dp, sc, dev, torch, S, P) -> dict:
     el, meta = _time_fused(dp, b, a.variant_steps, torch)
     res["acl1024_mpps"] = round(n * a.variant_steps / el / 1e6, 1)
     res["acl1024_forwarded_fraction"] = round(float(np.mean(P.meta_fields(meta.cpu().numpy().view(np.uint32))[2] == 0)), 4)
+    # ClassBench-style ACL: 1024 5-tuple rules, nested prefixes, port ranges, wildcard protocols
+    info = S.install_acl_wild(dp, 1024)
+    dp.commit()
+    el, meta = _time_fused(dp, b, a.variant_steps, torch)
+    res["acl_wild_mpps"] = round(n * a.variant_steps / el / 1e6, 1)
+    res["acl_wild"] = {"rules": info["rules"], "ternary_entries": info["entries"], "rule_tiles": int(dp._acl_tiles),
+                       "forwarded_fraction": round(float(np.mean(P.meta_fields(meta.cpu().numpy().view(np.uint32))[2] == 0)), 4)}
+    dp.acl.rules = info["saved"]
+    dp.acl.version += 1
+    dp.commit()
     del mixed, b
     return res
 
@@ -518,6 +528,7 @@ def main() -> None:
             "forwarded_fraction": round(fwd_local, 6),
             "value_mixed": None if not variants else variants["mixed_mpps"],
             "value_acl1024": None if not variants else variants["acl1024_mpps"],
+            "value_acl_wild": None if not variants else variants["acl_wild_mpps"],
             "value_l3": None if not variants else variants["l3_mpps"],
             "imix": None if not variants else variants["imix"],
             "variants": variants,

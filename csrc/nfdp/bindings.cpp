@@ -339,10 +339,11 @@ PYBIND11_MODULE(_nfdp, m) {
                            uintptr_t lat, uintptr_t acl_wfrag, uintptr_t acl_cinit, uint32_t acl_tiles,
                            uintptr_t toep_frag, uintptr_t toep_tab, int hash_mode, int acl_mode, int num_cus,
                            uintptr_t stream, uint32_t flags, py::object side, uintptr_t n_dev, uintptr_t steer_list,
-                           uintptr_t steer_cnt, uint32_t nranks, uint32_t rank) {
+                           uintptr_t steer_cnt, uint32_t nranks, uint32_t rank, uint32_t steer_cap) {
     FusedLaunch f{};
     f.steer_list = reinterpret_cast<uint32_t*>(steer_list);
     f.steer_cnt = reinterpret_cast<uint32_t*>(steer_cnt);
+    f.steer_cap = steer_cap;
     if (f.steer_list) { f.nranks = nranks; f.rank = rank; }
     f.side = side_from(side);
     f.t = tables_from(tables);
@@ -376,14 +377,16 @@ PYBIND11_MODULE(_nfdp, m) {
      py::arg("acl_wfrag"), py::arg("acl_cinit"), py::arg("acl_tiles"), py::arg("toep_frag"), py::arg("toep_tab"),
      py::arg("hash_mode"), py::arg("acl_mode"), py::arg("num_cus"), py::arg("stream"), py::arg("flags") = 0,
      py::arg("side") = py::none(), py::arg("n_dev") = 0, py::arg("steer_list") = 0, py::arg("steer_cnt") = 0,
-     py::arg("nranks") = 0, py::arg("rank") = 0);
+     py::arg("nranks") = 0, py::arg("rank") = 0, py::arg("steer_cap") = 0);
   m.def("launch_steer", [](uintptr_t out, uintptr_t inmeta, uintptr_t list, uintptr_t list_cnt, uint32_t cap_list,
-                           uintptr_t send, uintptr_t pcnt, uint32_t nranks, uint32_t cap, uintptr_t stream) {
+                           uint32_t cnt_len, uintptr_t send, uintptr_t pcnt, uint32_t nranks, uint32_t cap,
+                           uintptr_t stream) {
     check(launch_steer(reinterpret_cast<const void*>(out), reinterpret_cast<const uint32_t*>(inmeta),
                        reinterpret_cast<const uint32_t*>(list), reinterpret_cast<const uint32_t*>(list_cnt), cap_list,
-                       reinterpret_cast<uint8_t*>(send), reinterpret_cast<uint32_t*>(pcnt), nranks, cap,
+                       cnt_len, reinterpret_cast<uint8_t*>(send), reinterpret_cast<uint32_t*>(pcnt), nranks, cap,
                        reinterpret_cast<hipStream_t>(stream)), "launch_steer");
   });
+  m.def("steer_list_len", &steer_list_len, py::arg("n"), py::arg("num_cus"));
   m.def("gather", [](uintptr_t recv, uint32_t nranks, uint32_t rank, uint32_t cap, uintptr_t pkts, uintptr_t inmeta,
                      uintptr_t n_dev, bool device, uintptr_t stream) -> uint32_t {
     const size_t seg = pkt_seg_bytes(cap), moff = pkt_meta_off(cap);

@@ -111,13 +111,16 @@ struct FusedLaunch {
   const uint32_t* n_dev = nullptr; // device-side count (<= n)
   // steer-by-list (1-GPU instances with nranks > 1): other GPUs' packets listed, not processed
   uint32_t* steer_list = nullptr;
-  uint32_t* steer_cnt = nullptr;
+  uint32_t* steer_cnt = nullptr;   // 2 + 4 * num_cus words: {grid, region size, count per workgroup}
+  uint32_t steer_cap = 0;          // steer_list entries (>= steer_list_len(n, num_cus))
 };
 // Second half of steer-by-list: listed packets -> their owners' exchange segments (count-first,
 // segments sized for the whole batch).
 hipError_t launch_steer(const void* out, const uint32_t* inmeta, const uint32_t* list, const uint32_t* list_cnt,
-                        uint32_t cap_list, uint8_t* send, uint32_t* pcnt, uint32_t nranks, uint32_t cap,
-                        hipStream_t s);
+                        uint32_t cap_list, uint32_t cnt_len, uint8_t* send, uint32_t* pcnt, uint32_t nranks,
+                        uint32_t cap, hipStream_t s);
+// steer_list entries a LIST launch over n packets can need
+uint32_t steer_list_len(uint32_t n, int num_cus);
 hipError_t launch_fused(const FusedLaunch& f, const LaunchCfg& cfg, hipStream_t s);
 // Side pass alone (flood / mirror / ARP replicas, learn events, tunnel headers) over a side list
 // another kernel filled (the persistent ring kernel): slots / meta are that kernel's buffers.

@@ -77,12 +77,14 @@ struct FusedArgs {
   const uint32_t* n_dev;          // optional device-side packet count (<= n): batches whose size only
                                   // the GPU knows (packets gathered from the exchange)
   // Flow-owner steering by list (1-GPU instances, nranks > 1): a packet of another GPU's flow
-  // shard is not probed / chained / counted here; its index | owner << 26 is appended to
-  // steer_list (wave-aggregated, sized for the whole batch) and steer_kernel copies it to the
-  // owner's exchange segment afterwards.  The hot instance keeps its register budget and its
-  // fixed-count store tail; only a wave-uniform owner test is added.
+  // shard is not probed / chained / counted here; its index | owner << 26 is appended to this
+  // workgroup's region of steer_list (steer_cap_blk entries per workgroup: every packet it could
+  // see; the claim is an LDS atomic per wave, no global counter) and steer_kernel copies it to
+  // the owner's exchange segment afterwards.  steer_cnt = {grid, steer_cap_blk, count[grid]}.
+  // The hot instance keeps its register budget and its fixed-count store tail.
   uint32_t* steer_list;
   uint32_t* steer_cnt;
+  uint32_t steer_cap_blk;
 };
 
 __device__ __forceinline__ size_t lds_align16(size_t x) { return (x + 15) & ~(size_t)15; }
@@ -120,6 +122,7 @@ template <int HASH, int ACL, bool REMOTE, bool EARLY, bool LIST = false>
 __global__ __launch_bounds__(kFB, EARLY ? NFDP_EARLY_WAVES_PER_EU : NFDP_FUSED_WAVES_PER_EU) void fused_kernel(FusedArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ uint32_t rcnt[REMOTE ? 2 * kMaxRanks : 1], rbase[REMOTE ? kMaxRanks : 1];  // rcnt double-buffered
+  __shared__ uint32_t lst_n;                                  // LIST: entries of this workgroup's region
   const LdsLayout L = lds_layout(HASH, ACL, a.acl_tiles);
   v4i* lw = reinterpret_cast<v4i*>(smem + L.acl_w);
   v4i* lc = reinterpret_cast<v4i*>(smem + L.acl_c);
@@ -144,6 +147,8 @@ __global__ __launch_bounds__(kFB, EARLY ? NFDP_EARLY_WAVES_PER_EU : NFDP_FUSED_W
   if (threadIdx.x < kNumReasons) drops[threadIdx.x] = 0;
   if constexpr (REMOTE)
     if (threadIdx.x < 2 * kMaxRanks) rcnt[threadIdx.x] = 0;
+  if constexpr (LIST)
+    if (threadIdx.x == 0) lst_n = 0;
   PortEntry* lport = reinterpret_cast<PortEntry*>(smem + L.tports);
   uint64_t* lchain = reinterpret_cast<uint64_t*>(smem + L.tchain);
   uint8_t* lperm = smem + L.tperm;
@@ -222,10 +227,10 @@ __global__ __launch_bounds__(kFB, EARLY ? NFDP_EARLY_WAVES_PER_EU : NFDP_FUSED_W
         const uint32_t lane = threadIdx.x & 63u;
         const int leader = __ffsll((long long)m) - 1;
         uint32_t base = 0;
-        if ((int)lane == leader) base = atomicAdd(a.steer_cnt, (uint32_t)__popcll(m));
+        if ((int)lane == leader) base = atomicAdd(&lst_n, (uint32_t)__popcll(m));
         base = __shfl(base, leader);
         const unsigned long long lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-        if (to_owner) a.steer_list[base + (uint32_t)__popcll(m & lt)] = i | (own << 26);
+        if (to_owner) a.steer_list[blockIdx.x * a.steer_cap_blk + base + (uint32_t)__popcll(m & lt)] = i | (own << 26);
       }
     }
     if constexpr (!REMOTE) {
@@ -361,6 +366,12 @@ __global__ __launch_bounds__(kFB, EARLY ? NFDP_EARLY_WAVES_PER_EU : NFDP_FUSED_W
   }
   if (threadIdx.x < kNumReasons && drops[threadIdx.x])
     atomicAdd(a.drop_ctr + threadIdx.x, (unsigned long long)drops[threadIdx.x]);
+  if constexpr (LIST) {
+    if (threadIdx.x == 0) {
+      a.steer_cnt[2 + blockIdx.x] = lst_n;
+      if (blockIdx.x == 0) { a.steer_cnt[0] = gridDim.x; a.steer_cnt[1] = a.steer_cap_blk; }
+    }
+  }
 }
 
 // Side pass (pipeline.h side_stage) over the packets the per-packet kernel put on the side list:
@@ -418,24 +429,42 @@ __global__ __launch_bounds__(256) void gather_kernel(const uint8_t* recv, uint32
 
 // Steer-list mode, second half: every listed packet (index | owner << 26) goes to its owner's
 // exchange segment - the slot as it came in (re-emitted by the fused kernel into out[i]) and its
-// ingress meta, at a position claimed per owner.  Segments are sized for the whole batch
-// (count-first exchange: nothing can overflow).  Then the segment headers carry the counts.
+// ingress meta.  One workgroup walks one fused workgroup's list region 256 entries at a time;
+// positions are claimed per owner in LDS, then ONE global atomic per owner per 256 entries
+// reserves the run in that owner's segment.  Segments are sized for the whole batch (count-first
+// exchange: nothing can overflow).
 __global__ __launch_bounds__(256) void steer_kernel(const uint4* out, const uint32_t* inmeta, const uint32_t* list,
-                                                    const uint32_t* list_cnt, uint32_t cap_list, uint8_t* send,
-                                                    uint32_t* pcnt, uint32_t nranks, uint32_t cap, uint32_t seg_bytes,
-                                                    uint32_t meta_off) {
-  const uint32_t n = min(*list_cnt, cap_list);
-  for (uint32_t j = blockIdx.x * 256 + threadIdx.x; j < n; j += gridDim.x * 256) {
-    const uint32_t e = list[j];
-    const uint32_t i = e & ((1u << 26) - 1u), o = e >> 26;
-    if (o >= nranks) continue;
-    const uint32_t pos = atomicAdd(&pcnt[o], 1u);
-    if (pos >= cap) continue;   // cannot happen with cap = batch (kept as a guard)
-    uint8_t* seg = send + (size_t)o * seg_bytes;
-    uint4* dst = reinterpret_cast<uint4*>(seg + 64 + (size_t)pos * 64);
+                                                    const uint32_t* list_cnt, uint32_t cap_list, uint32_t max_blk,
+                                                    uint8_t* send, uint32_t* pcnt, uint32_t nranks, uint32_t cap,
+                                                    uint32_t seg_bytes, uint32_t meta_off) {
+  __shared__ uint32_t oc[kMaxRanks], ob[kMaxRanks];
+  const uint32_t G = min(list_cnt[0], max_blk), capb = list_cnt[1];
+  if ((unsigned long long)G * capb > cap_list) return;   // a header this launch did not write
+  for (uint32_t b = blockIdx.x; b < G; b += gridDim.x) {
+    const uint32_t c = min(list_cnt[2 + b], capb);
+    for (uint32_t j0 = 0; j0 < c; j0 += 256) {
+      if (threadIdx.x < kMaxRanks) oc[threadIdx.x] = 0;
+      __syncthreads();
+      const uint32_t j = j0 + threadIdx.x;
+      const uint32_t e = j < c ? list[(size_t)b * capb + j] : 0xFFFFFFFFu;
+      const uint32_t i = e & ((1u << 26) - 1u), o = e >> 26;
+      const bool ok = j < c && o < nranks;
+      const uint32_t local = ok ? atomicAdd(&oc[o], 1u) : 0u;
+      __syncthreads();
+      if (threadIdx.x < nranks && oc[threadIdx.x]) ob[threadIdx.x] = atomicAdd(&pcnt[threadIdx.x], oc[threadIdx.x]);
+      __syncthreads();
+      if (ok) {
+        const uint32_t pos = ob[o] + local;
+        if (pos < cap) {   // cannot fail with cap = batch (kept as a guard)
+          uint8_t* seg = send + (size_t)o * seg_bytes;
+          uint4* dst = reinterpret_cast<uint4*>(seg + 64 + (size_t)pos * 64);
 #pragma unroll
-    for (int k = 0; k < 4; ++k) dst[k] = out[(size_t)i * 4 + k];
-    reinterpret_cast<uint32_t*>(seg + meta_off)[pos] = inmeta[i];
+          for (int k = 0; k < 4; ++k) dst[k] = out[(size_t)i * 4 + k];
+          reinterpret_cast<uint32_t*>(seg + meta_off)[pos] = inmeta[i];
+        }
+      }
+      __syncthreads();   // ob / oc are reused by the next 256 entries
+    }
   }
 }
 
@@ -525,7 +554,8 @@ size_t fused_lds_bytes(int hash_mode, int acl_mode, uint32_t acl_tiles) {
 template <int H, int A, bool R, bool E = false, bool LS = false>
 static hipError_t launch_fused_t(const FusedArgs& a, int num_cus, hipStream_t s) {
   // static LDS (REMOTE reservation counters) + dynamic tables must fit 160 KiB
-  constexpr size_t kStatic = 3 * (R ? kMaxRanks : 1) * sizeof(uint32_t);  // rcnt[2][..] + rbase
+  // rcnt[2][..] + rbase + lst_n, with room for the compiler's alignment of the static block
+  constexpr size_t kStatic = (3 * (R ? kMaxRanks : 1) + 1) * sizeof(uint32_t) + 64;
   constexpr size_t kMaxDyn = 160 * 1024 - kStatic;
   const size_t lds = lds_layout(H, A, a.acl_tiles).total;
   if (lds > kMaxDyn) return hipErrorInvalidValue;
@@ -547,7 +577,15 @@ static hipError_t launch_fused_t(const FusedArgs& a, int num_cus, hipStream_t s)
   uint32_t grid = (uint32_t)(per_cu * num_cus);
   if (need < grid) grid = need;
   if (grid == 0) return hipSuccess;
-  hipLaunchKernelGGL((fused_kernel<H, A, R, E, LS>), dim3(grid), dim3(kFB), lds, s, a);
+  FusedArgs b = a;
+  if constexpr (LS) {
+    // each workgroup's list region holds every packet its grid-stride loop visits
+    const uint64_t stride = (uint64_t)grid * kFB;
+    b.steer_cap_blk = (uint32_t)(((a.n + stride - 1) / stride) * kFB);
+    if ((uint64_t)grid * b.steer_cap_blk > a.steer_cap_blk || grid > (uint32_t)(4 * num_cus))
+      return hipErrorInvalidValue;   // (steer_cap_blk carries the list's capacity in)
+  }
+  hipLaunchKernelGGL((fused_kernel<H, A, R, E, LS>), dim3(grid), dim3(kFB), lds, s, b);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || !a.side.cnt || a.side.cap_list == 0) return e;
   return launch_side(a.t, a.pkts, a.inmeta, a.out, a.out_meta, a.side, a.port_ctr, a.drop_ctr, s);
@@ -588,6 +626,7 @@ hipError_t launch_fused(const FusedLaunch& f, const LaunchCfg& cfg, hipStream_t 
   a.n_dev = f.n_dev;
   a.steer_list = f.steer_list;
   a.steer_cnt = f.steer_cnt;
+  a.steer_cap_blk = f.steer_cap;
   if (f.steer_list && (!f.steer_cnt || f.nranks < 2 || f.nranks > kMaxRanks || f.rank >= f.nranks || f.n >= (1u << 26)))
     return hipErrorInvalidValue;
   if (a.side.cnt && ((a.side.cap_rep && (!a.side.rep_hdr || !a.side.rep_meta || !a.side.rep_src)) ||
@@ -636,16 +675,22 @@ hipError_t launch_gather(const uint8_t* recv, uint32_t nranks, uint32_t rank, ui
 }
 
 hipError_t launch_steer(const void* out, const uint32_t* inmeta, const uint32_t* list, const uint32_t* list_cnt,
-                        uint32_t cap_list, uint8_t* send, uint32_t* pcnt, uint32_t nranks, uint32_t cap,
-                        hipStream_t s) {
-  if (!out || !inmeta || !list || !list_cnt || !send || !pcnt || nranks < 2 || nranks > kMaxRanks)
+                        uint32_t cap_list, uint32_t cnt_len, uint8_t* send, uint32_t* pcnt, uint32_t nranks,
+                        uint32_t cap, hipStream_t s) {
+  if (!out || !inmeta || !list || !list_cnt || !send || !pcnt || nranks < 2 || nranks > kMaxRanks || cnt_len < 3)
     return hipErrorInvalidValue;
   if (pkt_seg_bytes(cap) * nranks >= (1ull << 40)) return hipErrorInvalidValue;
-  uint32_t grid = (cap_list + 255) / 256;
-  grid = grid < 1 ? 1 : (grid > 1024 ? 1024 : grid);
+  const uint32_t max_blk = cnt_len - 2;
+  const uint32_t grid = max_blk < 1024 ? max_blk : 1024;
   hipLaunchKernelGGL(steer_kernel, dim3(grid), dim3(256), 0, s, reinterpret_cast<const uint4*>(out), inmeta, list,
-                     list_cnt, cap_list, send, pcnt, nranks, cap, (uint32_t)pkt_seg_bytes(cap), (uint32_t)pkt_meta_off(cap));
+                     list_cnt, cap_list, max_blk, send, pcnt, nranks, cap, (uint32_t)pkt_seg_bytes(cap),
+                     (uint32_t)pkt_meta_off(cap));
   return hipGetLastError();
+}
+
+uint32_t steer_list_len(uint32_t n, int num_cus) {
+  // what launch_fused_t's LIST regions can need: n rounded up per workgroup, <= 4 workgroups/CU
+  return n + (uint32_t)(4 * num_cus) * (uint32_t)kFB;
 }
 
 hipError_t launch_stamp(unsigned long long* dst, hipStream_t s) {

@@ -269,6 +269,79 @@ def add_acl_rules(dp, total: int, seed: int = 5) -> None:
     dp.acl.version += 1
 
 
+WELL_KNOWN_PORTS = (20, 21, 22, 23, 25, 53, 67, 69, 80, 110, 123, 137, 161, 179, 389, 443, 445, 500, 514, 636,
+                    993, 1433, 1521, 1812, 2049, 3306, 3389, 4500, 5060, 5432, 6379, 8080, 8443, 9090)
+
+
+def acl_wild_rules(n_rules: int = 1024, seed: int = 21, max_entries: int = 4000) -> list[dict]:
+    """A ClassBench-style ACL (the shape of the public "acl1" seed filters): 5-tuple rules with
+    overlapping, nested source / destination prefixes of every length (a third wildcard), TCP /
+    UDP / wildcard protocols, wildcard, exact and range ports (ranges expand into several ternary
+    entries).  Some prefixes sit inside the pod network, so traffic meets partial matches all
+    through the list and no tile prefilter can skip most of it.  Returns `acl.add` keyword dicts,
+    highest priority first; their expansion stays within `max_entries` ternary entries."""
+    rng = np.random.default_rng(seed)
+
+    def seeds(k, inside):
+        out = []
+        for _ in range(k):
+            ln = int(rng.choice([8, 12, 16, 20, 24, 28, 32]))
+            base = (POD_NET | int(rng.integers(0, 1 << 16))) if inside and ln >= 16 else int(rng.integers(1, 224)) << 24 | int(rng.integers(0, 1 << 24))
+            net = ipaddress.IPv4Network((base & ~((1 << (32 - ln)) - 1) & 0xFFFFFFFF, ln))
+            out.append(net)
+        return out
+
+    pool = seeds(48, True) + seeds(144, False)
+    # nesting: narrower children of some pool prefixes (overlap in both directions)
+    for net in list(pool[:64]):
+        if net.prefixlen <= 24:
+            sub = list(net.subnets(new_prefix=min(32, net.prefixlen + int(rng.integers(2, 9)))))
+            pool.append(sub[int(rng.integers(0, len(sub)))])
+
+    def pfx():
+        return None if rng.random() < 0.33 else str(pool[int(rng.integers(0, len(pool)))])
+
+    def port(kind_p):
+        u = rng.random()
+        if u < kind_p[0]:
+            return None
+        if u < kind_p[0] + kind_p[1]:
+            return int(rng.choice(WELL_KNOWN_PORTS)) if rng.random() < 0.7 else int(rng.integers(1024, 65536))
+        if u < kind_p[0] + kind_p[1] + kind_p[2]:
+            return (1024, 65535) if rng.random() < 0.6 else (0, 1023)
+        lo = int(rng.integers(1024, 60000))
+        return (lo, lo + int(rng.integers(3, 200)))
+
+    rules, entries = [], 0
+    while len(rules) < n_rules:
+        r = dict(permit=bool(rng.random() < 0.25), src=pfx(), dst=pfx(),
+                 proto=[6, 17, None][int(rng.choice(3, p=[0.45, 0.35, 0.20]))],
+                 sport=port((0.78, 0.08, 0.12)), dport=port((0.30, 0.42, 0.18)))
+        ns = 1 if not isinstance(r["sport"], tuple) else len(T.range_to_prefixes(*r["sport"]))
+        nd = 1 if not isinstance(r["dport"], tuple) else len(T.range_to_prefixes(*r["dport"]))
+        if entries + ns * nd > max_entries - (n_rules - len(rules) - 1):
+            r["sport"] = None if ns > 1 else r["sport"]
+            r["dport"] = int(rng.choice(WELL_KNOWN_PORTS)) if nd > 1 else r["dport"]
+            ns = nd = 1
+        rules.append(r)
+        entries += ns * nd
+    return rules
+
+
+def install_acl_wild(dp, n_rules: int = 1024, seed: int = 21) -> dict:
+    """Replace the ACL with `acl_wild_rules` + build_sfc's final pod-network permit.  Returns the
+    previous rules (restore with ``dp.acl.rules = info["saved"]; dp.acl.version += 1``) and sizes."""
+    saved = list(dp.acl.rules)
+    final = saved[-1] if saved else None
+    dp.acl.rules = []
+    for r in acl_wild_rules(n_rules, seed):
+        dp.acl.add(**r)
+    if final is not None:
+        dp.acl.rules.append(final)
+    dp.acl.version += 1
+    return {"saved": saved, "rules": n_rules + (final is not None), "entries": len(dp.acl.rules)}
+
+
 ROUTER_MAC = "02:00:00:00:fe:01"
 
 

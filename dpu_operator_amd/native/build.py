@@ -78,13 +78,41 @@ def _newest_header(d: Path) -> float:
     return max(ts) if ts else 0.0
 
 
+# HIP sources whose kernels' register / spill / occupancy figures are recorded at build time
+# (compiler resource remarks -> <module>.resources.json next to the module; the spill guard test
+# tests/test_kernel_resources.py and tools/kernel_resources.py read them)
+RESOURCE_SOURCES = ("kernels.hip", "ring.hip")
+RESOURCE_FIELDS = ("VGPRs", "AGPRs", "ScratchSize [bytes/lane]", "Occupancy [waves/SIMD]", "SGPRs Spill", "VGPRs Spill",
+                   "LDS Size [bytes/block]")
+
+
+def parse_resource_remarks(text: str) -> list[dict]:
+    """Rows {name, VGPRs, ..., VGPRs Spill} from `-Rpass-analysis=kernel-resource-usage` output."""
+    import re
+
+    rows, cur = [], None
+    for line in text.splitlines():
+        m = re.search(r"remark:\s+Function Name: (\S+)", line)
+        if m:
+            cur = {"name": m.group(1)}
+            rows.append(cur)
+            continue
+        m = re.search(r"remark:\s+([A-Za-z \[\]/]+?): (\d+)", line)
+        if m and cur is not None and m.group(1).strip() in RESOURCE_FIELDS:
+            cur[m.group(1).strip()] = int(m.group(2))
+    return rows
+
+
 def _compile(src: Path, obj: Path, hip: bool, verbose: bool) -> None:
     obj.parent.mkdir(parents=True, exist_ok=True)
     common = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function", *_includes(), "-I", str(src.parent)]
+    remarks = hip and src.name in RESOURCE_SOURCES
     if hip:
         extra = os.environ.get("NFDP_HIPCC_FLAGS", "").split()  # build-time experiments (-D...)
         cmd = [HIPCC, "-x", "hip", f"--offload-arch={ARCH}", "-munsafe-fp-atomics", *common, *extra, "-c", str(src),
                "-o", str(obj)]
+        if remarks:
+            cmd.append("-Rpass-analysis=kernel-resource-usage")
     else:
         cxx = shutil.which("g++") or "g++"
         cmd = [cxx, *common, "-pthread", "-c", str(src), "-o", str(obj)]
@@ -93,8 +121,14 @@ def _compile(src: Path, obj: Path, hip: bool, verbose: bool) -> None:
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"compile failed: {src}\n{r.stdout}\n{r.stderr}")
-    if verbose and r.stderr.strip():
-        print(r.stderr, file=sys.stderr)
+    err = r.stderr
+    if remarks:
+        import json
+
+        obj.with_suffix(".resources.json").write_text(json.dumps(parse_resource_remarks(err)))
+        err = "\n".join(ln for ln in err.splitlines() if "kernel-resource-usage" not in ln)
+    if verbose and err.strip():
+        print(err, file=sys.stderr)
 
 
 def _flags_changed(name: str, hip: bool) -> bool:
@@ -140,7 +174,21 @@ def build_module(name: str, force: bool = False, verbose: bool = False) -> Path:
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed: {name}\n{r.stdout}\n{r.stderr}")
+        if spec["hip"]:
+            _write_resources(name, out, [BUILD / name / (s + ".resources.json") for s in spec["sources"]
+                                         if s in RESOURCE_SOURCES])
     return out
+
+
+def _write_resources(name: str, out: Path, parts: list[Path]) -> None:
+    import json
+
+    rows = {}
+    for p in parts:
+        if p.exists():
+            rows[p.name.replace(".resources.json", "")] = json.loads(p.read_text())
+    res = out.parent / f"{name}.resources.json"
+    res.write_text(json.dumps({"flags": os.environ.get("NFDP_HIPCC_FLAGS", "").strip(), "sources": rows}, indent=0))
 
 
 def build_exe(name: str, force: bool = False, verbose: bool = False) -> Path:

@@ -8,18 +8,19 @@ SNAT, L2 steer) with the 1-GPU fused kernel and egresses the frame itself: pod r
 memory, which every GPU can write, so no frame has to reach a "pod's GPU" first.
 
 Packets the I/O layer could not steer (a producer without the hash, a reconfigured key) are
-caught inside the fused kernel right after classification: the REMOTE variant in flow-owner mode
-(steer = 1) writes the packet's INPUT header slot + ingress meta into the owner's exchange
-segment instead of probing; one all-to-all per step delivers the segments (RCCL over xGMI); the
-owner gathers them into a dense batch (device-side count, no host round trip) and runs the fused
-kernel on it.  The exchange of step k overlaps the next step's kernel:
+caught inside the fused kernel right after classification: the LIST instance of the 1-GPU kernel
+puts them on a per-workgroup steer list (no probe, no chain, no counters) and steer_kernel copies
+their INPUT header slot + ingress meta into the owner's exchange segment (sized for the whole
+batch).  The exchange is count-first and loss-free: an all-to-all of the per-peer counts, then a
+grouped send/recv of exactly those bytes (RCCL P2P over xGMI); the owner gathers them into a
+dense batch and runs the fused kernel on it.  The exchange of step k overlaps the next step's
+kernel:
 
-    compute stream:  fused(k) | wait a2a(k-1) | gather(k-1) + fused_rx(k-1) | fused(k+1) | ...
-    RCCL stream:               a2a(k) ...................................... (overlaps)
+    compute stream:  fused(k) + steer(k) | gather(k-1) + fused_rx(k-1) | fused(k+1) | ...
+    comm stream:                counts(k), send/recv(k) ............... (overlaps)
 
 Cross-GPU bytes per packet: 68 B (header slot + meta) for misdirected packets only; the payload
-never moves.  Exchange segments are sized from the expected misdirected count (overflow ->
-reason `overflow`, counted).  The CPU twins (oracle + gather) run the same class on gloo ranks.
+never moves.  The CPU twins (oracle REMOTE steer + gather) run the same class on gloo ranks.
 """
 from __future__ import annotations
 
@@ -41,14 +42,15 @@ def flow_owner(keys: np.ndarray, world: int, rss_key: bytes) -> np.ndarray:
 
 
 class _Slot:
-    def __init__(self, dev, world: int, pseg: int, batch: int, gpu: bool):
+    def __init__(self, dev, world: int, pseg: int, batch: int, gpu: bool, list_len: int = 0, cnt_blocks: int = 1):
         self.send = torch.zeros(world * pseg, dtype=torch.uint8, device=dev)
         self.recv = torch.zeros(world * pseg, dtype=torch.uint8, device=dev)
         self.pcnt = torch.zeros(world, dtype=torch.int32, device=dev)    # packets this rank sends to each peer
         self.rcnt = torch.zeros(world, dtype=torch.int32, device=dev)    # packets each peer sends this rank
         self.t0 = torch.zeros(1, dtype=torch.int64, device=dev)
-        self.list = torch.zeros(max(batch, 1), dtype=torch.int32, device=dev)   # steer list (GPU)
-        self.list_cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+        # steer list (GPU): a region per fused workgroup; {grid, region size, count per workgroup}
+        self.list = torch.zeros(max(list_len, 1), dtype=torch.int32, device=dev)
+        self.list_cnt = torch.zeros(2 + cnt_blocks, dtype=torch.int32, device=dev)
         self.ev = torch.cuda.Event() if gpu else None     # local step (kernel + steer) done
         self.cev = torch.cuda.Event() if gpu else None    # exchange done
 
@@ -79,7 +81,13 @@ class RssShardedDataPlane:
         self.cap = max(int(batch), 64)      # a segment holds the whole batch: loss-free at any fraction
         self.pseg = int(self.nf.pkt_seg_bytes(self.cap))
         self.moff = int(self.nf.pkt_meta_off(self.cap))
-        self.slots = [_Slot(self.dev, world, self.pseg, batch, self.gpu) for _ in range(2)]
+        self.hash_mode = dp.hash_mode if dp.hash_mode != 0 else 1
+        self.acl_mode = dp.acl_mode
+        # LIST instances exist for the LDS / MFMA hash with the MFMA / no ACL; others use REMOTE steer
+        self.use_list = self.gpu and self.hash_mode in (1, 2) and self.acl_mode in (1, 2)
+        nl = int(self.nf.steer_list_len(batch, int(dp.num_cus))) if self.use_list else 0
+        self.slots = [_Slot(self.dev, world, self.pseg, batch, self.gpu, nl, 4 * int(dp.num_cus) if self.use_list else 1)
+                      for _ in range(2)]
         u8, i32 = dict(dtype=torch.uint8, device=self.dev), dict(dtype=torch.int32, device=self.dev)
         self.out = torch.zeros((batch, 64), **u8)
         self.out_meta_t = torch.zeros(batch, **i32)
@@ -95,11 +103,7 @@ class RssShardedDataPlane:
         self.n = 0
         self.k = 0
         self.pending = None
-        self.hash_mode = dp.hash_mode if dp.hash_mode != 0 else 1
-        self.acl_mode = dp.acl_mode
         self.host_staged = self.gpu and dist.is_initialized() and dist.get_backend(group) == "gloo"
-        # LIST instances exist for the LDS / MFMA hash with the MFMA / no ACL; others use REMOTE steer
-        self.use_list = self.gpu and self.hash_mode in (1, 2) and self.acl_mode in (1, 2)
         self.comm = torch.cuda.Stream(self.dev) if self.gpu and not self.host_staged else None
         self.hcnt = torch.zeros((2, world), dtype=torch.int32).pin_memory() if self.gpu else torch.zeros((2, world), dtype=torch.int32)
         self.stats = {"sent": 0, "received": 0, "steps": 0, "max_peer": 0}
@@ -123,9 +127,10 @@ class RssShardedDataPlane:
                                  dp._ptr("flow_ctr"), dp._ptr("port_ctr"), dp._ptr("drop_ctr"), p(s.t0), p(self.lat),
                                  dp._ptr("acl_wfrag"), dp._ptr("acl_cinit"), dp._acl_tiles, dp._ptr("toep_frag"),
                                  dp._ptr("toep_tab"), self.hash_mode, self.acl_mode, dp.num_cus, st,
-                                 0 if dp.count_flows else 4, None, 0, p(s.list), p(s.list_cnt), self.world, self.rank)
-            self.nf.launch_steer(p(self.out), p(inmeta), p(s.list), p(s.list_cnt), n, p(s.send), p(s.pcnt),
-                                 self.world, self.cap, st)
+                                 0 if dp.count_flows else 4, None, 0, p(s.list), p(s.list_cnt), self.world, self.rank,
+                                 s.list.numel())
+            self.nf.launch_steer(p(self.out), p(inmeta), p(s.list), p(s.list_cnt), s.list.numel(), s.list_cnt.numel(),
+                                 p(s.send), p(s.pcnt), self.world, self.cap, st)
         else:
             d = dict(nranks=self.world, rank=self.rank, cap_desc=0, cap_pkt=self.cap, steer=1,
                      pkts=p(pkts), inmeta=p(inmeta), out=p(self.out), out_meta=p(self.out_meta_t), n=n,

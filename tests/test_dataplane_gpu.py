@@ -431,3 +431,27 @@ def test_rss_steer_list_matches_cpu_twin(world, frac):
             metas = buf[b + eng.moff: b + eng.moff + 4 * n].view(np.uint32)
             return sorted(zip(map(bytes, slots), metas.tolist()))
         assert seg(g, gs) == seg(c, cs)
+
+
+@pytest.mark.parametrize("hash_mode,acl_mode", [("lds", "mfma"), ("mfma", "mfma"), ("lds", "scalar")])
+def test_acl_wild_bit_exact(hash_mode, acl_mode):
+    """ClassBench-style 1024-rule ACL (> 3000 ternary entries: tiles beyond the LDS-staged 64,
+    the early-fetch instance) is bit-exact with the oracle, which is itself checked against an
+    independent first-match model (test_dataplane_oracle.py)."""
+    torch = _torch()
+    res = {}
+    for dev in ("cuda", "cpu"):
+        dp, sc = _build(dev, hash_mode if dev == "cuda" else "mfma", acl_mode if dev == "cuda" else "mfma")
+        S.install_acl_wild(dp, 1024)
+        dp.commit()
+        pk, im = _traffic(sc)
+        if dev == "cuda":
+            r = dp.run(torch.from_numpy(pk).cuda(), torch.from_numpy(im.view(np.int32)).cuda())
+            torch.cuda.synchronize()
+            res[dev] = (r.meta.cpu().numpy().view(np.uint32), r.out.cpu().numpy())
+            assert dp._acl_tiles > 64
+        else:
+            r = dp.run(pk, im)
+            res[dev] = (r.meta, r.out)
+    assert np.array_equal(res["cuda"][0], res["cpu"][0])
+    assert np.array_equal(res["cuda"][1], res["cpu"][1])

@@ -293,3 +293,47 @@ def test_other_hops(hops):
         assert np.array_equal(fr[0, 0:6], np.frombuffer(S.pod_mac(int(sc.flow_src_pod[3])), np.uint8))
     if "vlan" in hops:
         assert vid[0] == 100
+
+
+def _first_match_deny(rules, keys, default_permit=True):
+    """Independent TCAM model: first rule with key & mask == value decides (numpy, no nfdp)."""
+    val = np.stack([r.value for r in rules]).astype(np.uint32)
+    msk = np.stack([r.mask for r in rules]).astype(np.uint32)
+    per = np.array([r.permit for r in rules])
+    deny = np.zeros(len(keys), bool)
+    for a in range(0, len(keys), 512):
+        k = keys[a:a + 512]
+        hit = ((k[:, None, :] & msk[None]) == val[None]).all(-1)
+        anyh = hit.any(1)
+        first = hit.argmax(1)
+        deny[a:a + 512] = np.where(anyh, ~per[first], not default_permit)
+    return deny
+
+
+def test_acl_wild_classbench_style_first_match():
+    """The ClassBench-style rule set (bench value_acl_wild): 1024 5-tuple rules with nested
+    prefixes, port ranges and wildcard protocols expand to > 1024 ternary entries, and the oracle's
+    verdict for every packet equals an independent numpy first-match model over them (with 32
+    extra rules cut from real flow keys so both verdicts occur)."""
+    rules = S.acl_wild_rules(1024)
+    assert len(rules) == 1024
+    assert sum(r["src"] is None for r in rules) > 200 and sum(isinstance(r["dport"], tuple) for r in rules) > 100
+    dp = DataPlane(device="cpu", flow_buckets=1 << 13)
+    sc = S.build_sfc(dp, n_pods=16, n_flows=1 << 13, n_acl=256, seed=0)
+    info = S.install_acl_wild(dp, 1024)
+    assert info["rules"] == 1025 and 1024 < info["entries"] <= T.AclTable.MAX_RULES
+    rng = np.random.default_rng(3)
+    final = dp.acl.rules.pop()
+    for _ in range(32):
+        k = sc.keys[rng.integers(0, len(sc.keys))]
+        m = (rng.integers(0, 2**32, 4, dtype=np.uint64) & rng.integers(0, 2**32, 4, dtype=np.uint64)).astype(np.uint32)
+        dp.acl.rules.insert(int(rng.integers(0, len(dp.acl.rules) + 1)), T.AclRule(k & m, m, bool(rng.integers(0, 2))))
+    dp.acl.rules.append(final)
+    dp.acl.version += 1
+    dp.commit()
+    pk, im, f = S.traffic(sc, 1 << 13, seed=4, return_flows=True)
+    r = dp.run(pk, im)
+    reasons = P.meta_fields(r.meta)[2]
+    want = _first_match_deny(dp.acl.rules, sc.keys[f], dp.acl.default_permit)
+    assert 0 < want.sum() < len(want)
+    assert np.array_equal(reasons == 4, want)

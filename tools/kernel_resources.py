@@ -5,7 +5,6 @@ docs/DATAPLANE.md "Register budget").
 python tools/kernel_resources.py [--max-vgpr-spill N]   (exit 1 if a fused / ring instance spills more)
 """
 import argparse
-import re
 import subprocess
 import sys
 from pathlib import Path
@@ -16,21 +15,13 @@ FIELDS = ("VGPRs", "AGPRs", "ScratchSize [bytes/lane]", "Occupancy [waves/SIMD]"
 
 
 def remarks(src: Path) -> list[dict]:
+    sys.path.insert(0, str(REPO))
+    from dpu_operator_amd.native.build import parse_resource_remarks
+
     cmd = [CLANG, "--offload-arch=gfx950", "-x", "hip", "-munsafe-fp-atomics", "-O3", "-std=c++17",
            "-I", str(REPO / "csrc/nfdp"), "--cuda-device-only", "-c", str(src), "-o", "/dev/null",
            "-Rpass-analysis=kernel-resource-usage"]
-    out = subprocess.run(cmd, capture_output=True, text=True).stderr
-    rows, cur = [], None
-    for line in out.splitlines():
-        m = re.search(r"remark:\s+Function Name: (\S+)", line)
-        if m:
-            cur = {"name": m.group(1)}
-            rows.append(cur)
-            continue
-        m = re.search(r"remark:\s+([A-Za-z \[\]/]+?): (\d+)", line)
-        if m and cur is not None and m.group(1).strip() in FIELDS:
-            cur[m.group(1).strip()] = int(m.group(2))
-    return rows
+    return parse_resource_remarks(subprocess.run(cmd, capture_output=True, text=True).stderr)
 
 
 def demangle(n: str) -> str:
