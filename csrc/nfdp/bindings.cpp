@@ -378,10 +378,10 @@ PYBIND11_MODULE(_nfdp, m) {
      py::arg("hash_mode"), py::arg("acl_mode"), py::arg("num_cus"), py::arg("stream"), py::arg("flags") = 0,
      py::arg("side") = py::none(), py::arg("n_dev") = 0, py::arg("steer_list") = 0, py::arg("steer_cnt") = 0,
      py::arg("nranks") = 0, py::arg("rank") = 0, py::arg("steer_cap") = 0);
-  m.def("launch_steer", [](uintptr_t out, uintptr_t inmeta, uintptr_t list, uintptr_t list_cnt, uint32_t cap_list,
+  m.def("launch_steer", [](uintptr_t pkts, uintptr_t inmeta, uintptr_t list, uintptr_t list_cnt, uint32_t cap_list,
                            uint32_t cnt_len, uintptr_t send, uintptr_t pcnt, uint32_t nranks, uint32_t cap,
                            uintptr_t stream) {
-    check(launch_steer(reinterpret_cast<const void*>(out), reinterpret_cast<const uint32_t*>(inmeta),
+    check(launch_steer(reinterpret_cast<const void*>(pkts), reinterpret_cast<const uint32_t*>(inmeta),
                        reinterpret_cast<const uint32_t*>(list), reinterpret_cast<const uint32_t*>(list_cnt), cap_list,
                        cnt_len, reinterpret_cast<uint8_t*>(send), reinterpret_cast<uint32_t*>(pcnt), nranks, cap,
                        reinterpret_cast<hipStream_t>(stream)), "launch_steer");

@@ -116,7 +116,7 @@ struct FusedLaunch {
 };
 // Second half of steer-by-list: listed packets -> their owners' exchange segments (count-first,
 // segments sized for the whole batch).
-hipError_t launch_steer(const void* out, const uint32_t* inmeta, const uint32_t* list, const uint32_t* list_cnt,
+hipError_t launch_steer(const void* pkts, const uint32_t* inmeta, const uint32_t* list, const uint32_t* list_cnt,
                         uint32_t cap_list, uint32_t cnt_len, uint8_t* send, uint32_t* pcnt, uint32_t nranks,
                         uint32_t cap, hipStream_t s);
 // steer_list entries a LIST launch over n packets can need

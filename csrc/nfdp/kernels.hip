@@ -185,6 +185,9 @@ __global__ __launch_bounds__(kFB, EARLY ? NFDP_EARLY_WAVES_PER_EU : NFDP_FUSED_W
   // REMOTE: the per-peer segments (< 2 GiB in all, checked at launch)
   const __amdgpu_buffer_rsrc_t r_send = __builtin_amdgcn_make_buffer_rsrc(
       (void*)a.send_pkt, (short)0, REMOTE ? (int)(a.nranks * pkt_seg_bytes(a.cap_pkt)) : 0, kBufCfg);
+  // LIST: the steer list (entries < 2^26, checked at launch: byte offsets fit 32 bits)
+  const __amdgpu_buffer_rsrc_t r_list = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.steer_list, (short)0, LIST ? (int)(gridDim.x * a.steer_cap_blk * 4u) : 0, kBufCfg);
   uint32_t it = 0;  // loop iteration (REMOTE reservation buffers alternate)
   for (uint32_t base = blockIdx.x * kFB; base < n; base += stride, ++it) {
     const uint32_t i = base + threadIdx.x;
@@ -217,21 +220,10 @@ __global__ __launch_bounds__(kFB, EARLY ? NFDP_EARLY_WAVES_PER_EU : NFDP_FUSED_W
         if (to_owner) st.reason = kRemote;  // no local probe / chain / counters
       }
     } else if constexpr (LIST) {   // separate instances: the 1-GPU hot kernel is untouched
-      // steer list: the append happens here, so the owner id is dead before the probe / chain
-      // (the hot instance's register budget stays what it was)
-      const uint32_t own = owner_of(hash, a.nranks);
-      to_owner = valid && !st.reason && p.ipv4 && own != a.rank;
-      if (to_owner) st.reason = kRemote;
-      const unsigned long long m = __ballot(to_owner);
-      if (__builtin_expect(m != 0ull, 0)) {
-        const uint32_t lane = threadIdx.x & 63u;
-        const int leader = __ffsll((long long)m) - 1;
-        uint32_t base = 0;
-        if ((int)lane == leader) base = atomicAdd(&lst_n, (uint32_t)__popcll(m));
-        base = __shfl(base, leader);
-        const unsigned long long lt = lane ? (~0ull >> (64 - lane)) : 0ull;
-        if (to_owner) a.steer_list[blockIdx.x * a.steer_cap_blk + base + (uint32_t)__popcll(m & lt)] = i | (own << 26);
-      }
+      // the owner test only (the flag lives in st.reason: no probe / chain / counters); the list
+      // append comes after the tail's stores, where the register pressure is lowest (placed
+      // here, the same append cost the instance 15 more spilled VGPRs)
+      if (valid && !st.reason && p.ipv4 && owner_of(hash, a.nranks) != a.rank) st.reason = kRemote;
     }
     if constexpr (!REMOTE) {
       // prefetch the next slot now: it lands under this slot's probe and chain
@@ -288,7 +280,8 @@ __global__ __launch_bounds__(kFB, EARLY ? NFDP_EARLY_WAVES_PER_EU : NFDP_FUSED_W
       }
     }
     if (REMOTE && to_owner && !to_peer) reason = kOverflow;  // the owner's segment was full: dropped here
-    const bool listed = LIST && to_owner;                     // steer list: always delivered to the owner
+    // steer list: always delivered to the owner (kRemote is set only by the steer test here)
+    const bool listed = LIST && e.reason == kRemote;
     const uint32_t olen = reason == e.reason ? egress_len(p, e) : 0u;
     const uint32_t meta = (to_peer || listed)
                               ? make_meta((a.steer || listed) ? kPortNone : e.out_port,
@@ -296,7 +289,7 @@ __global__ __launch_bounds__(kFB, EARLY ? NFDP_EARLY_WAVES_PER_EU : NFDP_FUSED_W
                               : make_meta(reason == kOverflow ? kPortNone : e.out_port, olen, reason,
                                           !reason && e.xhdr, !reason && e.flood);
     // port / drop counters: LDS, global only for ports >= kLdsPorts (issued before the tail)
-    if (valid && !(a.flags & 1u) && !(to_owner && (to_peer || listed))) {  // a steered packet is counted by its owner
+    if (valid && !(a.flags & 1u) && !((to_owner && to_peer) || listed)) {  // a steered packet is counted by its owner
       if (st.in_port < kLdsPorts) {
         atomicAdd(&pc[st.in_port], 1u); atomicAdd(&pc[kLdsPorts + st.in_port], st.wire_len);
       } else if (st.in_port < (uint32_t)kMaxPorts) {
@@ -313,7 +306,8 @@ __global__ __launch_bounds__(kFB, EARLY ? NFDP_EARLY_WAVES_PER_EU : NFDP_FUSED_W
       }
     }
     uint32_t o[kSlotDwords];
-    // a steered packet travels as it came in (p is untouched: the chain never ran on it)
+    // a steered packet travels as it came in (p is untouched: the chain never ran on it); a listed
+    // one is copied from the INPUT slot by steer_kernel (its out[] slot is not read)
 #ifndef NFDP_ABL_NO_EMIT
     emit(p, to_owner ? p.tci : e.tci, to_owner ? p.tagged : e.push != 0, o);
 #else  // cost attribution only (wrong results): the normalized header as is
@@ -344,6 +338,24 @@ __global__ __launch_bounds__(kFB, EARLY ? NFDP_EARLY_WAVES_PER_EU : NFDP_FUSED_W
       wave_frames_store<kStreamAux>(kx, o, r_out, run_of(base));
       __builtin_amdgcn_raw_buffer_store_b32(meta, r_meta, valid ? i * 4u : kNoRun, 0, kStreamAux);
       __builtin_amdgcn_raw_buffer_store_b32(lat_now, r_lat, sample ? (i >> 4) * 4u : kNoRun, 0, 0);
+      if constexpr (LIST) {
+        const unsigned long long m = __ballot(listed);
+        uint32_t off = kNoRun;   // byte offset into the list; out of range = the lane stores nothing
+        if (__builtin_expect(m != 0ull, 0)) {
+          // rank among the wave's listed lanes (mbcnt: no 64-bit lane masks in VGPRs); the lowest
+          // listed lane claims the wave's run with one LDS atomic, readlane broadcasts it (SGPR)
+          const uint32_t pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+          const int leader = __builtin_ctzll(m);
+          uint32_t base = 0;
+          if (listed && pre == 0) base = atomicAdd(&lst_n, (uint32_t)__builtin_popcountll(m));   // LDS: lgkmcnt only
+          base = __builtin_amdgcn_readlane(base, leader);
+          if (listed) off = (blockIdx.x * a.steer_cap_blk + base + pre) * 4u;
+        }
+        // one store per iteration whatever the ballot: the loop's vector-memory count stays fixed,
+        // so the wait for the prefetched frame keeps its vmcnt(N > 0) (a store under a branch
+        // would force vmcnt(0) at the loop head and expose this slot's tail)
+        __builtin_amdgcn_raw_buffer_store_b32(i | (owner_of(hash, a.nranks) << 26), r_list, off, 0, 0);
+      }
     } else {
       if (hit && a.flow_ctr && !(a.flags & 4u)) atomicAdd(a.flow_ctr + slot, ctr_inc(st.wire_len));
       // frames for a peer: per lane into its segment slot; local frames: coalesced into out[]
@@ -428,12 +440,11 @@ __global__ __launch_bounds__(256) void gather_kernel(const uint8_t* recv, uint32
 }
 
 // Steer-list mode, second half: every listed packet (index | owner << 26) goes to its owner's
-// exchange segment - the slot as it came in (re-emitted by the fused kernel into out[i]) and its
-// ingress meta.  One workgroup walks one fused workgroup's list region 256 entries at a time;
+// exchange segment - its input slot and ingress meta, as they came in.  One workgroup walks one fused workgroup's list region 256 entries at a time;
 // positions are claimed per owner in LDS, then ONE global atomic per owner per 256 entries
 // reserves the run in that owner's segment.  Segments are sized for the whole batch (count-first
 // exchange: nothing can overflow).
-__global__ __launch_bounds__(256) void steer_kernel(const uint4* out, const uint32_t* inmeta, const uint32_t* list,
+__global__ __launch_bounds__(256) void steer_kernel(const uint4* pkts, const uint32_t* inmeta, const uint32_t* list,
                                                     const uint32_t* list_cnt, uint32_t cap_list, uint32_t max_blk,
                                                     uint8_t* send, uint32_t* pcnt, uint32_t nranks, uint32_t cap,
                                                     uint32_t seg_bytes, uint32_t meta_off) {
@@ -459,7 +470,7 @@ __global__ __launch_bounds__(256) void steer_kernel(const uint4* out, const uint
           uint8_t* seg = send + (size_t)o * seg_bytes;
           uint4* dst = reinterpret_cast<uint4*>(seg + 64 + (size_t)pos * 64);
 #pragma unroll
-          for (int k = 0; k < 4; ++k) dst[k] = out[(size_t)i * 4 + k];
+          for (int k = 0; k < 4; ++k) dst[k] = pkts[(size_t)i * 4 + k];
           reinterpret_cast<uint32_t*>(seg + meta_off)[pos] = inmeta[i];
         }
       }
@@ -674,15 +685,15 @@ hipError_t launch_gather(const uint8_t* recv, uint32_t nranks, uint32_t rank, ui
   return hipGetLastError();
 }
 
-hipError_t launch_steer(const void* out, const uint32_t* inmeta, const uint32_t* list, const uint32_t* list_cnt,
+hipError_t launch_steer(const void* pkts, const uint32_t* inmeta, const uint32_t* list, const uint32_t* list_cnt,
                         uint32_t cap_list, uint32_t cnt_len, uint8_t* send, uint32_t* pcnt, uint32_t nranks,
                         uint32_t cap, hipStream_t s) {
-  if (!out || !inmeta || !list || !list_cnt || !send || !pcnt || nranks < 2 || nranks > kMaxRanks || cnt_len < 3)
+  if (!pkts || !inmeta || !list || !list_cnt || !send || !pcnt || nranks < 2 || nranks > kMaxRanks || cnt_len < 3)
     return hipErrorInvalidValue;
   if (pkt_seg_bytes(cap) * nranks >= (1ull << 40)) return hipErrorInvalidValue;
   const uint32_t max_blk = cnt_len - 2;
   const uint32_t grid = max_blk < 1024 ? max_blk : 1024;
-  hipLaunchKernelGGL(steer_kernel, dim3(grid), dim3(256), 0, s, reinterpret_cast<const uint4*>(out), inmeta, list,
+  hipLaunchKernelGGL(steer_kernel, dim3(grid), dim3(256), 0, s, reinterpret_cast<const uint4*>(pkts), inmeta, list,
                      list_cnt, cap_list, max_blk, send, pcnt, nranks, cap, (uint32_t)pkt_seg_bytes(cap),
                      (uint32_t)pkt_meta_off(cap));
   return hipGetLastError();

@@ -129,7 +129,7 @@ class RssShardedDataPlane:
                                  dp._ptr("toep_tab"), self.hash_mode, self.acl_mode, dp.num_cus, st,
                                  0 if dp.count_flows else 4, None, 0, p(s.list), p(s.list_cnt), self.world, self.rank,
                                  s.list.numel())
-            self.nf.launch_steer(p(self.out), p(inmeta), p(s.list), p(s.list_cnt), s.list.numel(), s.list_cnt.numel(),
+            self.nf.launch_steer(p(pkts), p(inmeta), p(s.list), p(s.list_cnt), s.list.numel(), s.list_cnt.numel(),
                                  p(s.send), p(s.pcnt), self.world, self.cap, st)
         else:
             d = dict(nranks=self.world, rank=self.rank, cap_desc=0, cap_pkt=self.cap, steer=1,

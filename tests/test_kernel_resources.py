@@ -1,0 +1,67 @@
+"""Register-budget guard for the hot kernels (CPU: reads the compiler's resource remarks).
+
+The 4-wave fused instances run at the 128-VGPR cap; spilling more than the budget below moved
+header dwords through scratch in the past (docs/DATAPLANE.md "Register budget": a 64-spill
+build corrupted ~0.1 % of egress dwords).  The build records `-Rpass-analysis=kernel-resource-
+usage` for kernels.hip / ring.hip in dpu_operator_amd/native/_nfdp.resources.json
+(native/build.py); without a current record the remarks are produced here (slow: ~2 min).
+"""
+import json
+import subprocess
+from pathlib import Path
+
+import pytest
+
+from dpu_operator_amd.native.build import parse_resource_remarks
+
+REPO = Path(__file__).resolve().parent.parent
+SRC = REPO / "csrc" / "nfdp"
+RECORD = REPO / "dpu_operator_amd" / "native" / "_nfdp.resources.json"
+
+# (source, mangled-name prefix, max spilled VGPRs, min waves / SIMD)
+BUDGET = [
+    # headline: lds hash + MFMA ACL, 1 GPU; and the MFMA-hash twin
+    ("kernels.hip", "_ZN4nfdp12fused_kernelILi1ELi1ELb0ELb0ELb0E", 17, 4),
+    ("kernels.hip", "_ZN4nfdp12fused_kernelILi2ELi1ELb0ELb0ELb0E", 24, 4),
+    # early-fetch instances (2 waves / SIMD by design): no spills
+    ("kernels.hip", "_ZN4nfdp12fused_kernelILi1ELi1ELb0ELb1ELb0E", 0, 2),
+    ("kernels.hip", "_ZN4nfdp12fused_kernelILi2ELi1ELb0ELb1ELb0E", 0, 2),
+    # steer-list instance (multi-GPU RSS): within one register of the hot instance
+    ("kernels.hip", "_ZN4nfdp12fused_kernelILi1ELi1ELb0ELb0ELb1E", 18, 4),
+    # persistent ring kernels: no spills at all
+    ("ring.hip", "_ZN4nfdp11ring_kernel", 0, 2),
+]
+
+
+def _rows() -> dict[str, list[dict]]:
+    newest = max(p.stat().st_mtime for p in list(SRC.glob("*.h")) + [SRC / "kernels.hip", SRC / "ring.hip"])
+    if RECORD.exists() and RECORD.stat().st_mtime >= newest:
+        rec = json.loads(RECORD.read_text())
+        if not rec.get("flags") and all(s in rec["sources"] for s in ("kernels.hip", "ring.hip")):
+            return rec["sources"]
+    out = {}
+    for src in ("kernels.hip", "ring.hip"):
+        cmd = ["/opt/rocm/lib/llvm/bin/clang++", "--offload-arch=gfx950", "-x", "hip", "-munsafe-fp-atomics", "-O3",
+               "-std=c++17", "-I", str(SRC), "--cuda-device-only", "-c", str(SRC / src), "-o", "/dev/null",
+               "-Rpass-analysis=kernel-resource-usage"]
+        try:
+            r = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
+        except (OSError, subprocess.TimeoutExpired) as e:
+            pytest.skip(f"no gfx950 compiler here: {e}")
+        out[src] = parse_resource_remarks(r.stderr)
+    return out
+
+
+@pytest.fixture(scope="module")
+def rows():
+    return _rows()
+
+
+@pytest.mark.parametrize("src,prefix,max_spill,min_occ", BUDGET)
+def test_hot_kernel_register_budget(rows, src, prefix, max_spill, min_occ):
+    hits = [r for r in rows[src] if r["name"].startswith(prefix)]
+    assert hits, f"{prefix} not found in {src}"
+    for r in hits:
+        assert r.get("VGPRs Spill", 0) <= max_spill, (r["name"], r)
+        assert r.get("Occupancy [waves/SIMD]", 0) >= min_occ, (r["name"], r)
+        assert r.get("ScratchSize [bytes/lane]", 0) <= 4 * max_spill + 64, (r["name"], r)

@@ -55,6 +55,18 @@ def probe(world: int, batch: int, flows: int, frac: float, iters: int = 30) -> d
     eng = RssShardedDataPlane(dp, 0, world, batch, remote_frac=frac)
     s = eng.slots[0]
     steer_ms = _time(lambda: eng._local(s, pk, im, batch), iters)
+    if eng.use_list:   # the LIST fused kernel alone (steer_kernel skipped), then restore
+        real = eng.nf
+
+        class _NoSteer:
+            def __getattr__(self, k):
+                return (lambda *a, **kw: None) if k == "launch_steer" else getattr(real, k)
+
+        eng.nf = _NoSteer()
+        res["list_kernel_ms"] = round(_time(lambda: eng._local(s, pk, im, batch), iters), 4)
+        eng.nf = real
+        eng._local(s, pk, im, batch)
+        torch.cuda.synchronize()
     cnt = s.pcnt.cpu().numpy().copy()
     s.recv.copy_(s.send)            # rank 0 "receives" what it sent its peers (timing only)
     s.recv.view(world, eng.pseg)[:, :4].view(torch.int32)[:, 0].copy_(s.pcnt)
