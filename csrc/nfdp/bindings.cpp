@@ -73,6 +73,14 @@ TablesView tables_from(const py::dict& d) {
   t.terms = ptr<const TermEntry>(d, "terms");
   t.term_mask = t.terms ? val<uint32_t>(d, "term_mask", 0) : 0u;
   if (t.terms && ((t.term_mask + 1) & t.term_mask)) throw std::invalid_argument("term table size must be a power of two");
+  t.terms6 = ptr<const Term6Entry>(d, "terms6");
+  t.term6_mask = t.terms6 ? val<uint32_t>(d, "term6_mask", 0) : 0u;
+  if (t.terms6 && ((t.term6_mask + 1) & t.term6_mask)) throw std::invalid_argument("term6 table size must be a power of two");
+  if (d.contains("vtep6")) {
+    const auto v = d["vtep6"].cast<std::vector<uint32_t>>();
+    if (v.size() != 4) throw std::invalid_argument("vtep6: 4 raw words");
+    for (int k = 0; k < 4; ++k) t.vtep6[k] = v[k];
+  }
   t.vmmac = ptr<const VmMacEntry>(d, "vmmac");
   t.vmmac_mask = t.vmmac ? val<uint32_t>(d, "vmmac_mask", 0) : 0u;
   if (t.vmmac && ((t.vmmac_mask + 1) & t.vmmac_mask)) throw std::invalid_argument("vmmac table size must be a power of two");
@@ -378,6 +386,19 @@ PYBIND11_MODULE(_nfdp, m) {
      py::arg("hash_mode"), py::arg("acl_mode"), py::arg("num_cus"), py::arg("stream"), py::arg("flags") = 0,
      py::arg("side") = py::none(), py::arg("n_dev") = 0, py::arg("steer_list") = 0, py::arg("steer_cnt") = 0,
      py::arg("nranks") = 0, py::arg("rank") = 0, py::arg("steer_cap") = 0);
+  m.def("launch_pairs", [](py::dict tables, uintptr_t pkts, uintptr_t inmeta, uint32_t n, uintptr_t port_ctr, bool count,
+                           uintptr_t stream) {
+    const TablesView t = tables_from(tables);
+    check(launch_pairs(reinterpret_cast<void*>(pkts), reinterpret_cast<uint32_t*>(inmeta), n, t,
+                       reinterpret_cast<unsigned long long*>(port_ctr), count, reinterpret_cast<hipStream_t>(stream)),
+          "launch_pairs");
+  });
+  m.def("launch_pair_fix", [](uintptr_t inmeta, uintptr_t out_meta, uint32_t n, uintptr_t drop_ctr, bool count,
+                              uintptr_t stream) {
+    check(launch_pair_fix(reinterpret_cast<const uint32_t*>(inmeta), reinterpret_cast<uint32_t*>(out_meta), n,
+                          reinterpret_cast<unsigned long long*>(drop_ctr), count, reinterpret_cast<hipStream_t>(stream)),
+          "launch_pair_fix");
+  });
   m.def("launch_steer", [](uintptr_t pkts, uintptr_t inmeta, uintptr_t list, uintptr_t list_cnt, uint32_t cap_list,
                            uint32_t cnt_len, uintptr_t send, uintptr_t pcnt, uint32_t nranks, uint32_t cap,
                            uintptr_t stream) {
@@ -674,14 +695,16 @@ PYBIND11_MODULE(_nfdp, m) {
       });
 
   m.def("launch_side", [](py::dict tables, uintptr_t pkts, uintptr_t inmeta, uintptr_t out, uintptr_t out_meta,
-                          py::object side, uintptr_t port_ctr, uintptr_t drop_ctr, uintptr_t stream) {
+                          py::object side, uintptr_t port_ctr, uintptr_t drop_ctr, uintptr_t stream, uint32_t n_slots,
+                          bool wrap) {
     const TablesView t = tables_from(tables);
     const SideOut so = side_from(side);
     check(launch_side(t, reinterpret_cast<const void*>(pkts), reinterpret_cast<const uint32_t*>(inmeta),
                       reinterpret_cast<const void*>(out), reinterpret_cast<const uint32_t*>(out_meta), so,
                       reinterpret_cast<unsigned long long*>(port_ctr), reinterpret_cast<unsigned long long*>(drop_ctr),
-                      reinterpret_cast<hipStream_t>(stream)), "launch_side");
-  });
+                      reinterpret_cast<hipStream_t>(stream), n_slots, wrap), "launch_side");
+  }, py::arg("tables"), py::arg("pkts"), py::arg("inmeta"), py::arg("out"), py::arg("out_meta"), py::arg("side"),
+     py::arg("port_ctr"), py::arg("drop_ctr"), py::arg("stream"), py::arg("n_slots") = 0, py::arg("wrap") = false);
   // ---- IPsec ESP engine ----
   m.attr("ESP_SA_BYTES") = (int)sizeof(EspSa);
   m.attr("ESP_CLEAR_OFF") = kClearOff;

@@ -307,11 +307,28 @@ uint32_t mac_learn_cpu(MacEntry* macs, uint32_t mask, const uint32_t* ev, uint32
 void oracle_run(const TablesView& t, const uint32_t* pkts, const uint32_t* inmeta, uint32_t n,
                 uint32_t* out, uint32_t* out_meta, uint64_t* flow_ctr, uint64_t* port_ctr,
                 uint64_t* drop_ctr, uint32_t* hashes, int32_t* acl_rules, const SideOut* side) {
+  uint32_t prev_ci = (uint32_t)kSlotBytes << 8;   // strip | hv << 8 of the previous slot when it heads a pair
   for (uint32_t i = 0; i < n; ++i) {
     const uint32_t* d = pkts + (size_t)i * kSlotDwords;
+    // wide header pairs (pipeline.h decap_pair): a continuation belongs to the slot before it
+    uint32_t im = inmeta[i], ci = (uint32_t)kSlotBytes << 8;
+    uint32_t inner[kSlotDwords];
+    const bool cont = (im & 0xFFFFu) == kPortCont;
+    if (!cont && i + 1 < n && (inmeta[i + 1] & 0xFFFFu) == kPortCont) {
+      uint32_t strip, hv;
+      const int tp = decap_pair(t, DirectTables{t}, d, pkts + (size_t)(i + 1) * kSlotDwords, im, inner, strip, hv);
+      if (tp >= 0) {
+        if (port_ctr) port_ctr[2 * (im & 0xFFFFu)] += ctr_inc(im >> 16);   // the outer frame on its VTEP port
+        d = inner;
+        im = (uint32_t)tp | (((im >> 16) - strip) << 16);
+        ci = strip | (hv << 8);
+      }
+    }
     Parsed p;
     IngressState st;
-    ingress_stage(t, d, inmeta[i], p, st);
+    ingress_stage(t, d, im, p, st);
+    if (cont) { st.reason = kCont; st.in_ext = i ? prev_ci : ((uint32_t)kSlotBytes << 8); }
+    prev_ci = ci;
     const uint32_t h = toeplitz_scalar(st.key, t.rss_key);
     const int acl = acl_first_match(t, st.key);
     if (hashes) hashes[i] = h;
@@ -343,14 +360,20 @@ void oracle_run(const TablesView& t, const uint32_t* pkts, const uint32_t* inmet
     }
     if (drop_ctr && e.reason) drop_ctr[e.reason & (kNumReasons - 1)] += 1;
   }
-  // side pass (GPU: side_kernel after the fused kernel)
+  // side pass (GPU: side_kernel after the fused kernel); a terminated pair head works on its inner frame
   if (side && side->cnt) {
     CpuSideSink sk{*side, port_ctr, drop_ctr};
     const uint32_t nl = std::min(side->cnt[5], side->cap_list);
     for (uint32_t j = 0; j < nl; ++j) {
       const uint32_t i = side->list[j];
-      side_stage(t, DirectTables{t}, pkts + (size_t)i * kSlotDwords, inmeta[i], out + (size_t)i * kSlotDwords,
-                 out_meta[i], i, sk);
+      const uint32_t* d = pkts + (size_t)i * kSlotDwords;
+      uint32_t im = inmeta[i], inner[kSlotDwords];
+      if (i + 1 < n && (im & 0xFFFFu) != kPortCont && (inmeta[i + 1] & 0xFFFFu) == kPortCont) {
+        uint32_t strip, hv;
+        const int tp = decap_pair(t, DirectTables{t}, d, pkts + (size_t)(i + 1) * kSlotDwords, im, inner, strip, hv);
+        if (tp >= 0) { d = inner; im = (uint32_t)tp | (((im >> 16) - strip) << 16); }
+      }
+      side_stage(t, DirectTables{t}, d, im, out + (size_t)i * kSlotDwords, out_meta[i], i, sk);
     }
   }
 }
@@ -359,16 +382,33 @@ void oracle_run_remote(const TablesView& t, const uint32_t* pkts, const uint32_t
                        uint32_t* out, uint32_t* out_meta, uint64_t* flow_ctr, uint64_t* port_ctr,
                        uint64_t* drop_ctr, const RemoteOut& r) {
   const size_t pseg = pkt_seg_bytes(r.cap_pkt);
+  uint32_t prev_ci = (uint32_t)kSlotBytes << 8;   // strip | hv << 8 of the previous slot when it heads a pair
   for (uint32_t i = 0; i < n; ++i) {
     const uint32_t* d = pkts + (size_t)i * kSlotDwords;
+    // wide header pairs (pipeline.h decap_pair): a continuation belongs to the slot before it
+    uint32_t im = inmeta[i], ci = (uint32_t)kSlotBytes << 8;
+    uint32_t inner[kSlotDwords];
+    const bool cont = (im & 0xFFFFu) == kPortCont;
+    if (!cont && i + 1 < n && (inmeta[i + 1] & 0xFFFFu) == kPortCont) {
+      uint32_t strip, hv;
+      const int tp = decap_pair(t, DirectTables{t}, d, pkts + (size_t)(i + 1) * kSlotDwords, im, inner, strip, hv);
+      if (tp >= 0) {
+        if (port_ctr) port_ctr[2 * (im & 0xFFFFu)] += ctr_inc(im >> 16);   // the outer frame on its VTEP port
+        d = inner;
+        im = (uint32_t)tp | (((im >> 16) - strip) << 16);
+        ci = strip | (hv << 8);
+      }
+    }
     Parsed p;
     IngressState st;
-    ingress_stage(t, d, inmeta[i], p, st);
+    ingress_stage(t, d, im, p, st);
+    if (cont) { st.reason = kCont; st.in_ext = i ? prev_ci : ((uint32_t)kSlotBytes << 8); }
+    prev_ci = ci;
     const uint32_t h = toeplitz_scalar(st.key, t.rss_key);
     const int acl = acl_first_match(t, st.key);
     // flow-owner steering: another GPU's flow goes to its owner as it came in
     const uint32_t owner = owner_of(h, r.nranks);
-    const bool to_owner = r.steer && !st.reason && p.ipv4 && owner != r.rank;
+    const bool to_owner = r.steer && !st.reason && p.ipv4 && owner != r.rank && im == inmeta[i];   // (terminated: stays)
     if (to_owner) st.reason = kRemote;
     bool hit = false;
     FlowAction act = {};

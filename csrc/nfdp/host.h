@@ -138,8 +138,16 @@ void esp_run_cpu(const EspBatch& a, bool enc);
 
 hipError_t launch_side(const TablesView& t, const void* pkts, const uint32_t* inmeta, const void* out,
                        const uint32_t* out_meta, const SideOut& side, unsigned long long* port_ctr,
-                       unsigned long long* drop_ctr, hipStream_t s);
+                       unsigned long long* drop_ctr, hipStream_t s,
+                       uint32_t n_slots = 0, bool wrap = false);
 size_t fused_lds_bytes(int hash_mode, int acl_mode, uint32_t acl_tiles);
+// Wide header pairs of a batch resolved in place (kernels.hip pair_kernel; launch_fused runs it
+// under launch flag 1 << 10).
+hipError_t launch_pairs(void* pkts, uint32_t* inmeta, uint32_t n, const TablesView& t, unsigned long long* port_ctr,
+                        bool count, hipStream_t s);
+// ... and afterwards: continuation slots' metas -> kCont with the pair's strip / hv (pair_fix_kernel)
+hipError_t launch_pair_fix(const uint32_t* inmeta, uint32_t* out_meta, uint32_t n, unsigned long long* drop_ctr,
+                           bool count, hipStream_t s);
 hipError_t launch_stamp(unsigned long long* dst, hipStream_t s);
 hipError_t launch_bucket_update(const uint32_t* idx, uint32_t nb, const void* rows, void* flows,
                                 uint32_t bucket_mask, hipStream_t s);

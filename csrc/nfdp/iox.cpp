@@ -285,7 +285,7 @@ void GpuBackend::side_pass(SideBatch& out) {
   if (!side_stream_) thread_init();
   hipStream_t s = side_stream_;
   hck(launch_side(f.t, ring_->dev_in(), ring_->dev_inmeta(), ring_->dev_out(), ring_->dev_meta(), f.side, f.port_ctr,
-                  f.drop_ctr, s), "side kernel");
+                  f.drop_ctr, s, ring_->capacity(), true), "side kernel");
   if (f.side.cap_learn && f.t.macs)
     hck(launch_mac_learn(const_cast<MacEntry*>(f.t.macs), f.t.mac_mask, f.side.learn, f.side.cnt + 1, f.side.cap_learn,
                          stamp++, f.side.cnt + 4, s), "learn kernel");

@@ -40,6 +40,7 @@ namespace nfdp {
 constexpr uint32_t kEarlyAclTiles = NFDP_EARLY_ACL_TILES;
 constexpr uint32_t kFlagNoEarly = 1u << 8;     // launch flag: never the early-fetch instance (A/B)
 constexpr uint32_t kFlagForceEarly = 1u << 9;  // launch flag: the early-fetch instance at any rule count (A/B)
+constexpr uint32_t kFlagPairs = 1u << 10;      // launch flag: the batch may hold wide header pairs (pair_kernel first)
 #ifndef NFDP_FUSED_WAVES_PER_EU
 #define NFDP_FUSED_WAVES_PER_EU 4
 #endif
@@ -196,6 +197,8 @@ __global__ __launch_bounds__(kFB, EARLY ? NFDP_EARLY_WAVES_PER_EU : NFDP_FUSED_W
     Parsed p;
     IngressState st;
     ingress_stage(a.t, ta, dn, imn, p, st);  // copies the frame into p.s: dn is free for the prefetch
+    // (a continuation slot of a wide header pair is bad_port here - in-meta port kPortCont;
+    // pair_fix_kernel turns its meta / counters into kCont afterwards: no pair code in this loop)
 
     if (!valid) st.reason = kMalformed;
 
@@ -386,6 +389,83 @@ __global__ __launch_bounds__(kFB, EARLY ? NFDP_EARLY_WAVES_PER_EU : NFDP_FUSED_W
   }
 }
 
+// Wide header pairs, batch form: one thread per continuation slot runs decap_pair on (head,
+// continuation) and rewrites them in place - a terminated head's slot becomes its inner frame and
+// its in-meta the tunnel port + inner length (its outer rx is counted on the VTEP port here); the
+// continuation's in-meta keeps kPortCont and carries strip | hv << 8 | kPairDone.  The fused
+// kernel then sees only ordinary slots (its register budget is untouched).  Idempotent: a pair
+// already marked done is skipped, so a batch can be run again.
+__global__ __launch_bounds__(256) void pair_kernel(uint4* pkts, uint32_t* inmeta, uint32_t n, TablesView t,
+                                                   unsigned long long* port_ctr, uint32_t count) {
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    const uint32_t cim = inmeta[i];
+    if ((cim & 0xFFFFu) != kPortCont || ((cim >> 16) & kPairDone)) continue;
+    uint32_t ci = (uint32_t)kSlotBytes << 8;
+    const uint32_t him = i ? inmeta[i - 1] : kPortCont;
+    if ((him & 0xFFFFu) != kPortCont) {
+      uint32_t d[kSlotDwords], x[kSlotDwords], inner[kSlotDwords], strip, hv;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint4 v = pkts[(size_t)(i - 1) * 4 + q], w = pkts[(size_t)i * 4 + q];
+        d[4 * q] = v.x; d[4 * q + 1] = v.y; d[4 * q + 2] = v.z; d[4 * q + 3] = v.w;
+        x[4 * q] = w.x; x[4 * q + 1] = w.y; x[4 * q + 2] = w.z; x[4 * q + 3] = w.w;
+      }
+      const int tp = decap_pair(t, DirectTables{t}, d, x, him, inner, strip, hv);
+      if (tp >= 0) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          pkts[(size_t)(i - 1) * 4 + q] = make_uint4(inner[4 * q], inner[4 * q + 1], inner[4 * q + 2], inner[4 * q + 3]);
+        inmeta[i - 1] = (uint32_t)tp | (((him >> 16) - strip) << 16);
+        if (count) atomicAdd(port_ctr + 2 * (him & 0xFFFFu), ctr_inc(him >> 16));   // the outer frame, VTEP port
+        ci = strip | (hv << 8);
+      }
+    }
+    inmeta[i] = kPortCont | ((ci | kPairDone) << 16);
+  }
+}
+
+// After the fused kernel: each continuation slot's meta becomes kCont with its pair's strip / hv,
+// and its bad_port count (in-meta port kPortCont) moves to kCont.
+__global__ __launch_bounds__(256) void pair_fix_kernel(const uint32_t* inmeta, uint32_t* out_meta, uint32_t n,
+                                                       unsigned long long* drop_ctr, uint32_t count) {
+  __shared__ uint32_t c;
+  if (threadIdx.x == 0) c = 0;
+  __syncthreads();
+  uint32_t mine = 0;
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
+    const uint32_t im = inmeta[i];
+    if ((im & 0xFFFFu) != kPortCont) continue;
+    const uint32_t ci = pair_cinfo(im);
+    out_meta[i] = cont_meta(ci & 0xFFu, ci >> 8);
+    ++mine;
+  }
+  if (mine) atomicAdd(&c, mine);
+  __syncthreads();
+  if (threadIdx.x == 0 && c && count) {
+    atomicAdd(drop_ctr + kBadPort, 0ull - (unsigned long long)c);
+    atomicAdd(drop_ctr + kCont, (unsigned long long)c);
+  }
+}
+
+hipError_t launch_pair_fix(const uint32_t* inmeta, uint32_t* out_meta, uint32_t n, unsigned long long* drop_ctr,
+                           bool count, hipStream_t s) {
+  if (!inmeta || !out_meta || !drop_ctr) return hipErrorInvalidValue;
+  if (n == 0) return hipSuccess;
+  const uint32_t g = (n + 255) / 256 < 1024 ? (n + 255) / 256 : 1024;
+  hipLaunchKernelGGL(pair_fix_kernel, dim3(g), dim3(256), 0, s, inmeta, out_meta, n, drop_ctr, count ? 1u : 0u);
+  return hipGetLastError();
+}
+
+hipError_t launch_pairs(void* pkts, uint32_t* inmeta, uint32_t n, const TablesView& t, unsigned long long* port_ctr,
+                        bool count, hipStream_t s) {
+  if (!pkts || !inmeta || !port_ctr) return hipErrorInvalidValue;
+  if (n == 0) return hipSuccess;
+  const uint32_t g = (n + 255) / 256 < 2048 ? (n + 255) / 256 : 2048;
+  hipLaunchKernelGGL(pair_kernel, dim3(g), dim3(256), 0, s, reinterpret_cast<uint4*>(pkts), inmeta, n, t, port_ctr,
+                     count ? 1u : 0u);
+  return hipGetLastError();
+}
+
 // Side pass (pipeline.h side_stage) over the packets the per-packet kernel put on the side list:
 // flood replicas, mirror and ARP copies, learn events.  Reads the list length on the device.
 struct SideArgs {
@@ -393,6 +473,8 @@ struct SideArgs {
   const uint4* pkts; const uint32_t* inmeta; const uint4* out; const uint32_t* out_meta;
   SideOut side;
   unsigned long long* port_ctr; unsigned long long* drop_ctr;
+  uint32_t n_slots;   // slots of the batch / ring (0: no wide pairs); a pair's continuation is the next slot
+  uint32_t wrap;      // 1: ring slots (the next slot wraps modulo n_slots)
 };
 __global__ __launch_bounds__(256) void side_kernel(SideArgs a) {
   const uint32_t n = min(a.side.cnt[5], a.side.cap_list);
@@ -405,8 +487,29 @@ __global__ __launch_bounds__(256) void side_kernel(SideArgs a) {
       d[4 * q] = v.x; d[4 * q + 1] = v.y; d[4 * q + 2] = v.z; d[4 * q + 3] = v.w;
       o[4 * q] = w.x; o[4 * q + 1] = w.y; o[4 * q + 2] = w.z; o[4 * q + 3] = w.w;
     }
+    // a terminated pair head: its side work is on the inner frame (the same decap_pair decision
+    // the pair pass / ring kernel took; a batch's pair pass already rewrote it: then decap_pair
+    // sees an ordinary frame and returns -1)
+    uint32_t im = a.inmeta[i];
+    if (a.n_slots && (im & 0xFFFFu) != kPortCont) {
+      const uint32_t j = a.wrap ? (i + 1) % a.n_slots : i + 1;
+      if (j < a.n_slots && (a.inmeta[j] & 0xFFFFu) == kPortCont) {
+        uint32_t x[kSlotDwords], inner[kSlotDwords], strip, hv;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const uint4 v = a.pkts[(size_t)j * 4 + q];
+          x[4 * q] = v.x; x[4 * q + 1] = v.y; x[4 * q + 2] = v.z; x[4 * q + 3] = v.w;
+        }
+        const int tp = decap_pair(a.t, DirectTables{a.t}, d, x, im, inner, strip, hv);
+        if (tp >= 0) {
+#pragma unroll
+          for (int k = 0; k < kSlotDwords; ++k) d[k] = inner[k];
+          im = (uint32_t)tp | (((im >> 16) - strip) << 16);
+        }
+      }
+    }
     GpuSideSink sk{a.side, a.port_ctr, a.drop_ctr};
-    side_stage(a.t, DirectTables{a.t}, d, a.inmeta[i], o, a.out_meta[i], i, sk);
+    side_stage(a.t, DirectTables{a.t}, d, im, o, a.out_meta[i], i, sk);
   }
 }
 
@@ -599,22 +702,22 @@ static hipError_t launch_fused_t(const FusedArgs& a, int num_cus, hipStream_t s)
   hipLaunchKernelGGL((fused_kernel<H, A, R, E, LS>), dim3(grid), dim3(kFB), lds, s, b);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || !a.side.cnt || a.side.cap_list == 0) return e;
-  return launch_side(a.t, a.pkts, a.inmeta, a.out, a.out_meta, a.side, a.port_ctr, a.drop_ctr, s);
+  return launch_side(a.t, a.pkts, a.inmeta, a.out, a.out_meta, a.side, a.port_ctr, a.drop_ctr, s, a.n, false);
 }
 
 hipError_t launch_side(const TablesView& t, const void* pkts, const uint32_t* inmeta, const void* out,
                        const uint32_t* out_meta, const SideOut& side, unsigned long long* port_ctr,
-                       unsigned long long* drop_ctr, hipStream_t s) {
+                       unsigned long long* drop_ctr, hipStream_t s, uint32_t n_slots, bool wrap) {
   if (!side.cnt || side.cap_list == 0) return hipSuccess;
   if (!pkts || !inmeta || !out || !out_meta || !side.list || !port_ctr || !drop_ctr) return hipErrorInvalidValue;
   SideArgs sa{t, reinterpret_cast<const uint4*>(pkts), inmeta, reinterpret_cast<const uint4*>(out), out_meta, side,
-              port_ctr, drop_ctr};
+              port_ctr, drop_ctr, n_slots, wrap ? 1u : 0u};
   const uint32_t sg = (side.cap_list + 255) / 256 < 512 ? (side.cap_list + 255) / 256 : 512;
   hipLaunchKernelGGL(side_kernel, dim3(sg), dim3(256), 0, s, sa);
   return hipGetLastError();
 }
 
-hipError_t launch_fused(const FusedLaunch& f, const LaunchCfg& cfg, hipStream_t s) {
+static FusedArgs make_fused_args(const FusedLaunch& f) {
   FusedArgs a;
   a.t = f.t;
   a.pkts = reinterpret_cast<const uint4*>(f.pkts);
@@ -638,11 +741,30 @@ hipError_t launch_fused(const FusedLaunch& f, const LaunchCfg& cfg, hipStream_t 
   a.steer_list = f.steer_list;
   a.steer_cnt = f.steer_cnt;
   a.steer_cap_blk = f.steer_cap;
+  return a;
+}
+
+static hipError_t launch_fused_body(const FusedLaunch& f, const LaunchCfg& cfg, hipStream_t s);
+
+hipError_t launch_fused(const FusedLaunch& f, const LaunchCfg& cfg, hipStream_t s) {
   if (f.steer_list && (!f.steer_cnt || f.nranks < 2 || f.nranks > kMaxRanks || f.rank >= f.nranks || f.n >= (1u << 26)))
     return hipErrorInvalidValue;
-  if (a.side.cnt && ((a.side.cap_rep && (!a.side.rep_hdr || !a.side.rep_meta || !a.side.rep_src)) ||
-                     (a.side.cap_learn && !a.side.learn) || (a.side.cap_list && !a.side.list)))
+  if (f.side.cnt && ((f.side.cap_rep && (!f.side.rep_hdr || !f.side.rep_meta || !f.side.rep_src)) ||
+                     (f.side.cap_learn && !f.side.learn) || (f.side.cap_list && !f.side.list)))
     return hipErrorInvalidValue;
+  if (f.flags & kFlagPairs) {   // wide header pairs: resolved in place before the pipeline (pair_kernel)
+    const hipError_t e = launch_pairs(const_cast<void*>(f.pkts), const_cast<uint32_t*>(f.inmeta), f.n, f.t, f.port_ctr,
+                                      !(f.flags & 1u), s);
+    if (e != hipSuccess) return e;
+    const hipError_t e2 = launch_fused_body(f, cfg, s);
+    if (e2 != hipSuccess) return e2;
+    return launch_pair_fix(f.inmeta, f.out_meta, f.n, f.drop_ctr, !(f.flags & 1u), s);
+  }
+  return launch_fused_body(f, cfg, s);
+}
+
+static hipError_t launch_fused_body(const FusedLaunch& f, const LaunchCfg& cfg, hipStream_t s) {
+  FusedArgs a = make_fused_args(f);
   const bool remote = f.nranks > 1 && !f.steer_list;   // steer list: the 1-GPU instances
   if (cfg.acl_mode == kAclMfma && (f.acl_tiles == 0 || f.acl_tiles > kAclMaxRules / 16)) return hipErrorInvalidValue;
   const int h = cfg.hash_mode, ac = cfg.acl_mode, cu = cfg.num_cus;

@@ -42,6 +42,7 @@ constexpr int kBucketSlots = 4;        // flow-table bucket = 4 x {key, action} 
 constexpr uint32_t kSlotUsed = 0x100u; // occupied marker, stored in FlowKey.meta byte 1
 constexpr uint16_t kPortNone = 0xFFFF; // dropped
 constexpr uint16_t kPortPunt = 0xFFFE; // to slow path (control plane upcall)
+constexpr uint32_t kPortCont = 0xFFFDu; // in-meta port of the continuation slot of a wide header pair
 // (kMaxPorts real ports; the 12-bit egress meta port field keeps 0xFFF / 0xFFE for none / punt)
 constexpr int kMaxHops = 7;
 constexpr int kAclKeyBits = 128;       // ACL / hash key = the 16-byte FlowKey
@@ -64,6 +65,9 @@ enum Reason : uint32_t {
   kRecirc = 13,    // tunnel terminated: recirculate frame[len - olen:] with in_port = meta port (decap)
   kRecirc6 = 14,   // IPv6-underlay VXLAN / GENEVE to the local VTEP: the VNI lies past the header slot, so
                    // the I/O layer finishes ipv6_tunnel_term_table on the whole frame (decap, recirculate)
+  kCont = 15,      // continuation slot of a wide (128-B) header pair (pipeline.h decap_pair): not a
+                   // frame; its meta's port field = bytes the head's egress strips from the head's
+                   // input frame (0: not terminated), len field = valid bytes of the head's out slot
   kNumReasons = 16,
 };
 
@@ -223,6 +227,14 @@ struct alignas(16) TermEntry {   // 16 B: (outer src ip, vni) -> tunnel port (ip
   uint32_t pad;
 };
 static_assert(sizeof(TermEntry) == 16, "TermEntry");
+struct alignas(16) Term6Entry {  // 32 B: (outer IPv6 src, vni) -> tunnel port (ipv6_tunnel_term_table)
+  uint32_t src[4];               // raw words (network-order bytes, little-endian loads)
+  uint32_t vni;
+  uint16_t port;
+  uint16_t valid;
+  uint32_t pad[2];
+};
+static_assert(sizeof(Term6Entry) == 32, "Term6Entry");
 // VM IPv4 -> MAC maps (P4 vm_src_ip4_mac_map_table / vm_dst_ip4_mac_map_table): a routed
 // packet from a mapped source gets that source MAC, one to a mapped destination that
 // destination MAC.  Open addressing over (ip, kind); kind 0 = empty slot.
@@ -477,12 +489,24 @@ NFDP_HD uint32_t meta_port(uint32_t m) {
   return p >= 0xFFEu ? (p | 0xF000u) : p;
 }
 NFDP_HD uint32_t meta_len(uint32_t m) { return (m >> 12) & 0x3FFFu; }
+NFDP_HD uint32_t cont_meta(uint32_t strip, uint32_t hv) { return make_meta(strip, hv, kCont); }
+// A continuation slot's in-meta: kPortCont | len << 16 from the producer; once its pair was
+// resolved (kernels.hip pair_kernel / the ring kernel) the len field is strip | hv << 8 | kPairDone.
+constexpr uint32_t kPairDone = 0x8000u;
+NFDP_HD uint32_t pair_cinfo(uint32_t cont_inmeta) {   // strip | hv << 8 (no strip: not resolved / not terminated)
+  const uint32_t f = cont_inmeta >> 16;
+  return (f & kPairDone) ? (f & 0x7FFFu) : ((uint32_t)kSlotBytes << 8);
+}
 NFDP_HD uint32_t meta_reason(uint32_t m) { return (m >> 26) & 0xFu; }
 // Header bytes `hl` of the out slot that are valid and the offset `to` in the input frame where the
 // unchanged tail continues (both from the in/out lengths; the `xlen` outer-header bytes excluded).
-NFDP_HD void out_tail(uint32_t in_len, uint32_t olen, uint32_t xlen, uint32_t& hl, uint32_t& to) {
+// `hv`: valid bytes of the input view the out slot was built from (64; fewer for an IPv6-underlay
+// terminated frame, see decap_pair).  A terminated frame passes in_len = len - strip and reads its
+// tail from in_frame + strip.
+NFDP_HD void out_tail(uint32_t in_len, uint32_t olen, uint32_t xlen, uint32_t& hl, uint32_t& to,
+                      uint32_t hv = kSlotBytes) {
   const int d = (int)olen - (int)xlen - (int)in_len;
-  const int h_in = in_len < (uint32_t)kSlotBytes ? (int)in_len : kSlotBytes;
+  const int h_in = in_len < hv ? (int)in_len : (int)hv;
   int h = h_in + d;
   if (h > kSlotBytes) h = kSlotBytes;
   hl = (uint32_t)h;
@@ -538,6 +562,9 @@ struct TablesView {
   uint32_t vtep6_fold;           // vtep6_fold() of the local IPv6 VTEP address (0: no IPv6 VTEP)
   const TermEntry* terms;        // term_mask + 1 slots, open addressing (nullable)
   uint32_t term_mask;
+  const Term6Entry* terms6;      // term6_mask + 1 slots, open addressing (nullable: no IPv6 terminations)
+  uint32_t term6_mask;
+  uint32_t vtep6[4];             // the local IPv6 VTEP address, raw words (with vtep6_fold != 0)
   const VmMacEntry* vmmac;       // vmmac_mask + 1 slots, open addressing (nullable: no VM MAC maps)
   uint32_t vmmac_mask;
   // IPv6 FIB (P4 ipv6_table): one open-addressing table over (prefix, length) and the distinct
@@ -613,6 +640,21 @@ NFDP_HD int term_lookup(const TablesView& t, uint32_t src_ip, uint32_t vni) {
     const TermEntry& e = t.terms[(h + q) & t.term_mask];
     if (!e.valid) return -1;
     if (e.src_ip == src_ip && e.vni == vni) return e.port;
+  }
+  return -1;
+}
+
+NFDP_HD uint32_t term6_hash(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3, uint32_t vni) {
+  return fmix32(a0 ^ fmix32(a1 ^ fmix32(a2 ^ fmix32(a3 ^ (vni * 0x9E3779B1u)))));
+}
+// (outer src IPv6 raw words, vni) -> tunnel port or -1
+NFDP_HD int term6_lookup(const TablesView& t, uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3, uint32_t vni) {
+  if (!t.terms6) return -1;
+  const uint32_t h = term6_hash(a0, a1, a2, a3, vni);
+  for (uint32_t q = 0; q < 8; ++q) {
+    const Term6Entry& e = t.terms6[(h + q) & t.term6_mask];
+    if (!e.valid) return -1;
+    if (e.src[0] == a0 && e.src[1] == a1 && e.src[2] == a2 && e.src[3] == a3 && e.vni == vni) return e.port;
   }
   return -1;
 }

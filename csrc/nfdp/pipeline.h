@@ -67,6 +67,74 @@ NFDP_HD void ingress_stage(const TablesView& t, const uint32_t* d, uint32_t inme
   ingress_stage(t, DirectTables{t}, d, inmeta, p, st);
 }
 
+// ---- Wide header pairs: single-pass tunnel termination ----
+// A frame on a VTEP (underlay) port may arrive as TWO consecutive slots: its bytes 0..63 (the
+// head) and 64..127 (the continuation, in-meta port kPortCont, same length).  When the head is
+// VXLAN / GENEVE (IPv4 or IPv6 underlay, an outer 802.1Q tag allowed) to the local VTEP, passes
+// its port's ingress checks and (outer source, VNI) has a termination entry, the pipeline runs on
+// the INNER frame in the same pass, as received on the tunnel port (P4 ipv4 / ipv6_tunnel_term_
+// table + rx_*_tunnel_source_port, without the recirculation).  decap_pair returns that port and
+// fills `inner` with the inner frame's first bytes: 64 over an IPv4 underlay, 58 / 54 over IPv6
+// (untagged / tagged outer: the pair ends at byte 128) - `hv`; `strip` = the outer bytes.  -1:
+// not terminated (the head goes through the pipeline as received).  Every rewrite stays in the
+// first 56 bytes, so the egress takes the out slot's first hv (+ tag) bytes and the tail from
+// in_frame + strip (nfdp.h out_tail).
+NFDP_HD uint32_t pair_dw(const uint32_t* d, const uint32_t* x, int j) {   // dword j of head ++ continuation
+  return j < kSlotDwords ? d[j] : (j < 2 * kSlotDwords ? x[j - kSlotDwords] : 0u);
+}
+template <class TA>
+NFDP_HD int decap_pair(const TablesView& t, const TA& ta, const uint32_t* d, const uint32_t* x, uint32_t inmeta,
+                       uint32_t* inner, uint32_t& strip, uint32_t& hv) {
+  strip = 0; hv = kSlotBytes;
+  const uint32_t in_port = inmeta & 0xFFFFu, len = inmeta >> 16;
+  if (in_port >= (uint32_t)kMaxPorts || len > kMaxFrame || len < 18) return -1;
+  const PortEntry pe = ta.port(in_port);
+  if ((pe.flags & (kPortValid | kPortLinkDown | kPortVtep)) != (kPortValid | kPortVtep)) return -1;
+  const bool tg = be16_at(d, 12) == 0x8100u;
+  // the outer frame's ingress checks (ingress_stage): a frame its port drops is not terminated
+  if ((pe.flags & kPortVlanIsolate) && tg && (be16_at(d, 14) & 0xFFFu) != pe.vlan) return -1;
+  if ((pe.flags & kPortSpoofChk) && (smac_lo(d) != pe.mac_lo || smac_hi(d) != pe.mac_hi)) return -1;
+  // untagged view of the pair (dword j; constant j only: a run-time index would go to scratch)
+  auto sn = [&](int j) -> uint32_t { return j < 3 ? d[j] : (tg ? pair_dw(d, x, j + 1) : pair_dw(d, x, j)); };
+  auto a2 = [&](int b) -> uint32_t { return (sn(b >> 2) >> 16) | (sn((b >> 2) + 1) << 16); };   // raw32 at b = 2 mod 4
+  auto sw = [](uint32_t v) -> uint32_t { return ((v & 0xFFu) << 8) | ((v >> 8) & 0xFFu); };    // be16 of a raw half
+  const uint32_t nlen = tg ? len - 4u : len;
+  const uint32_t et = sw(sn(3));
+  bool v6 = false;
+  int tp = -1;
+  if (et == 0x0800u) {
+    const bool ip_ok = ((sn(3) >> 16) & 0xFFu) == 0x45u && (sw(sn(5)) & 0x1FFFu) == 0u && (sn(5) >> 24) == 17u;
+    if (!ip_ok || a2(30) != pe.ext || nlen < kEncapBytes + 14u) return -1;
+    const uint32_t dport = sw(sn(9)), gopt = (sn(10) >> 16) & 0xFFu;
+    if (!(dport == 4789u || (dport == 6081u && (gopt & 0x3Fu) == 0u))) return -1;
+    const uint32_t vni = (((sn(11) >> 16) & 0xFFu) << 16) | ((sn(11) >> 24) << 8) | (sn(12) & 0xFFu);
+    tp = term_lookup(t, a2(26), vni);
+  } else if (et == 0x86DDu && t.vtep6_fold) {
+    v6 = true;
+    if (((sn(3) >> 20) & 0xFu) != 6u || (sn(5) & 0xFFu) != 17u || nlen < kEncap6Bytes + 14u) return -1;
+    if (a2(38) != t.vtep6[0] || a2(42) != t.vtep6[1] || a2(46) != t.vtep6[2] || a2(50) != t.vtep6[3]) return -1;
+    const uint32_t dport = sw(sn(14)), gopt = (sn(15) >> 16) & 0xFFu;
+    if (!(dport == 4789u || (dport == 6081u && (gopt & 0x3Fu) == 0u))) return -1;
+    const uint32_t vni = (((sn(16) >> 16) & 0xFFu) << 16) | ((sn(16) >> 24) << 8) | (sn(17) & 0xFFu);
+    tp = term6_lookup(t, a2(22), a2(26), a2(30), a2(34), vni);
+  } else {
+    return -1;
+  }
+  if (tp < 0 || tp >= kMaxPorts) return -1;
+  strip = (v6 ? kEncap6Bytes : kEncapBytes) + (tg ? 4u : 0u);
+  hv = 2u * kSlotBytes - strip < (uint32_t)kSlotBytes ? 2u * kSlotBytes - strip : (uint32_t)kSlotBytes;
+  // inner dword k = bytes strip + 4k .. of the pair; strip = 2 (mod 4): halves of two dwords
+#pragma unroll
+  for (int k = 0; k < kSlotDwords; ++k) {
+    const uint32_t w12 = (pair_dw(d, x, 12 + k) >> 16) | (pair_dw(d, x, 13 + k) << 16);
+    const uint32_t w13 = (pair_dw(d, x, 13 + k) >> 16) | (pair_dw(d, x, 14 + k) << 16);
+    const uint32_t w17 = (pair_dw(d, x, 17 + k) >> 16) | (pair_dw(d, x, 18 + k) << 16);
+    const uint32_t w18 = (pair_dw(d, x, 18 + k) >> 16) | (pair_dw(d, x, 19 + k) << 16);
+    inner[k] = v6 ? (tg ? w18 : w17) : (tg ? w13 : w12);
+  }
+  return tp;
+}
+
 struct EgressDecision {
   uint32_t out_port;
   uint32_t reason;
@@ -83,7 +151,7 @@ struct EgressDecision {
 // Length of the frame that leaves (the meta word's len): inner frame for a recirculation, tag and
 // outer-header bytes included otherwise, 0 for drops.
 NFDP_HD uint32_t egress_len(const Parsed& p, const EgressDecision& e) {
-  if (e.reason == kRecirc || e.reason == kRecirc6) return e.inner_len;
+  if (e.reason == kRecirc || e.reason == kRecirc6 || e.reason == kCont) return e.inner_len;
   if (e.reason) return 0u;
   return p.len + (e.push ? 4u : 0u) + e.xhdr;
 }
@@ -192,7 +260,11 @@ NFDP_HD EgressDecision chain_stage(const TablesView& t, const TA& ta, Parsed& p,
   EgressDecision e;
   e.out_port = kPortNone; e.reason = st.reason; e.push = 0; e.tci = 0; e.mirror = 0; e.flood = 0;
   e.xhdr = 0; e.inner_len = 0;
-  if (e.reason) return e;
+  if (e.reason) {
+    // continuation slot: the meta carries the head's strip / valid bytes (set in st.in_ext)
+    if (e.reason == kCont) { e.out_port = st.in_ext & 0xFFu; e.inner_len = st.in_ext >> 8; }
+    return e;
+  }
   bool vlan_done = false;
   if (!hit) {
     // tunnel termination on an underlay port (ipv4_tunnel_term_table + rx_ipv4_tunnel_source_port):

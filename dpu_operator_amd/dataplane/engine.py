@@ -187,7 +187,7 @@ class DataPlane:
         return (("ports", self.ports), ("chains", self.chains), ("macs", self.macs), ("lag", self.lag),
                 ("flood", self.flood), ("nexthops", self.nexthops), ("ecmp", self.ecmp),
                 ("tunnels", self.tunnels), ("terms", self.terms), ("vmmac", self.vmmac),
-                ("tunnels6", self.tunnels6),
+                ("tunnels6", self.tunnels6), ("terms6", self.terms6),
                 ("vtep6", self.vtep6))   # vtep6: a kernarg fold, listed for the version tracking
 
     def _only_flows_pending(self) -> bool:
@@ -381,7 +381,14 @@ class DataPlane:
             "n_lpm6_lens": int(getattr(self, "_lpm6", (0, 0))[1]),
             "tunnels6": self._ptr("tunnels6") if self.tunnels6.n else 0, "n_tunnels6": int(self.tunnels6.n),
             "vtep6_fold": int(self.nf.vtep6_fold(*(int(x) for x in self.vtep6.a))) if self.vtep6.active else 0,
+            "vtep6": [int(x) for x in self.vtep6.a],
+            "terms6": self._ptr("terms6") if len(self.terms6) else 0, "term6_mask": int(self.terms6.mask),
         }
+
+    def pairs_possible(self) -> bool:
+        """Wide header pairs (128-B slots of VTEP-port frames: single-pass tunnel termination) can
+        be in a batch: some port is a VTEP."""
+        return bool(np.any(self.ports.a["flags"] & np.uint32(T.PORT_VTEP)))
 
     # ------------------------------------------------------------------ side outputs / learning
     SIDE_FLAGS = T.PORT_LEARN | T.PORT_ARP_TRAP | T.PORT_MIRROR | T.PORT_TUNNEL
@@ -526,6 +533,11 @@ class DataPlane:
                 self.nf.launch_stamp(self._ptr("t0"), s)
             if not self.count_flows:
                 flags |= 4  # the kernel always gets the counter table; bit 2 makes it add 0
+            pairs = self.pairs_possible()
+            if pairs:
+                # wide header pairs resolved in place over the whole batch first (kernels.hip pair_kernel)
+                self.nf.launch_pairs(tp, pkts.data_ptr(), inmeta.data_ptr(), n, self._ptr("port_ctr"),
+                                     not (flags & 1), s)
             side = self._side_buffers(n) if self.side_active() else None
             # one launch covers < 2^25 slots (32-bit buffer views); bigger batches are split
             for lo in range(0, n, self.MAX_LAUNCH):
@@ -540,6 +552,8 @@ class DataPlane:
                     self._ptr("toep_frag"), self._ptr("toep_tab"),
                     self.hash_mode, self.acl_mode, self.num_cus, s, flags, side,
                 )
+            if pairs:   # continuation slots: kCont metas carrying their pair's strip / valid bytes
+                self.nf.launch_pair_fix(inmeta.data_ptr(), meta.data_ptr(), n, self._ptr("drop_ctr"), not (flags & 1), s)
             if side is not None:
                 self._apply_learn(s)
             return BatchResult(out, meta, n, {"lat": lat})

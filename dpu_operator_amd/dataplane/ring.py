@@ -176,7 +176,8 @@ class RingPath:
         dp = self.dp
         s = _torch().cuda.current_stream(dp.tdev).cuda_stream
         dp.nf.launch_side(dp.tables_ptrs(), self.eng.dev_in(), self.eng.dev_inmeta(), self.eng.dev_out(),
-                          self.eng.dev_meta(), self._side, dp._ptr("port_ctr"), dp._ptr("drop_ctr"), s)
+                          self.eng.dev_meta(), self._side, dp._ptr("port_ctr"), dp._ptr("drop_ctr"), s,
+                          self.capacity, True)
         dp._apply_learn(s)
         return dp.side_result()
 

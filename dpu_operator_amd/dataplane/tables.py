@@ -60,7 +60,7 @@ HOP_NAMES = {
 REASONS = {
     0: "ok", 1: "bad_port", 2: "vlan_drop", 3: "spoof", 4: "acl_deny", 5: "no_route",
     6: "too_big", 7: "chain_drop", 8: "ttl_expired", 9: "malformed", 10: "remote", 11: "overflow",
-    12: "arp_trap", 13: "recirc", 14: "recirc6",
+    12: "arp_trap", 13: "recirc", 14: "recirc6", 15: "cont",
 }
 
 PORT_DTYPE = np.dtype(
@@ -82,6 +82,8 @@ TUNNEL_DTYPE = np.dtype([("src_ip", "<u4"), ("dst_ip", "<u4"), ("sport", "<u2"),
                          ("smac_lo", "<u4"), ("smac_hi", "<u2"), ("out_port", "<u2"), ("dmac_lo", "<u4"),
                          ("dmac_hi", "<u2"), ("type", "<u2")])
 TERM_DTYPE = np.dtype([("src_ip", "<u4"), ("vni", "<u4"), ("port", "<u2"), ("valid", "<u2"), ("pad", "<u4")])
+TERM6_DTYPE = np.dtype([("src", "<u4", (4,)), ("vni", "<u4"), ("port", "<u2"), ("valid", "<u2"), ("pad", "<u4", (2,))])
+PORT_CONT = 0xFFFD      # in-meta port of a wide header pair's continuation slot (nfdp.h kPortCont)
 VMMAC_DTYPE = np.dtype([("ip", "<u4"), ("kind", "<u4"), ("mac_lo", "<u4"), ("mac_hi", "<u4")])   # nfdp.h VmMacEntry
 VMMAC_SRC, VMMAC_DST = 1, 2
 TUNNEL6_DTYPE = np.dtype([("src", "<u4", (4,)), ("dst", "<u4", (4,)), ("sport", "<u2"), ("dport", "<u2"), ("vni", "<u4"),
@@ -482,21 +484,47 @@ class Vtep6:
 
 class Term6Table:
     """ipv6_tunnel_term_table + rx_ipv6_tunnel_source_port: (outer IPv6 source, VNI) -> the tunnel
-    port the inner frame re-enters on.  The VNI lies past the 64-B header slot (frame bytes
-    66..68), so the kernel only recognises the tunnel (reason recirc6) and this host table is
-    consulted on the whole frame by the I/O layer (`DataPlane.resolve_recirc6`)."""
+    port the inner frame enters on.  The VNI lies past a 64-B header slot (frame bytes 66..68):
+    a frame that arrives as a wide header pair (128 B, nfdp.h kPortCont) is terminated by the
+    kernels from the device copy `a` (open addressing over term6_hash, 32-B entries) in the same
+    pass; a plain 64-B slot is only recognised (reason recirc6) and finished on the whole frame by
+    the I/O layer with `lookup` (`DataPlane.resolve_recirc6`)."""
+
+    SLOTS = 256
 
     def __init__(self):
         self.entries: dict[tuple[int, int], int] = {}
         self.version = 0
+        self.a = np.zeros(self.SLOTS, TERM6_DTYPE)
+        self.mask = self.SLOTS - 1
+
+    def _rebuild(self) -> None:
+        a = np.zeros(self.SLOTS, TERM6_DTYPE)
+        for (src, vni), port in self.entries.items():
+            w = np.frombuffer(ipaddress.IPv6Address(src).packed, "<u4").astype(np.uint32)
+            with np.errstate(over="ignore"):
+                h = fmix32(w[3] ^ (np.uint32(vni) * np.uint32(0x9E3779B1)))
+                h = fmix32(w[2] ^ h)
+                h = fmix32(w[1] ^ h)
+                h = int(fmix32(w[0] ^ h))
+            for q in range(8):
+                i = (h + q) & self.mask
+                if not a[i]["valid"]:
+                    a[i] = (w, vni, port, 1, (0, 0))
+                    break
+            else:
+                raise RuntimeError("term6 table probe limit reached")
+        self.a = a
 
     def insert(self, src, vni: int, port: int) -> None:
         self.entries[(int(ipaddress.IPv6Address(int(src) if isinstance(src, (int, np.integer)) else src)),
                       vni & 0xFFFFFF)] = int(port)
+        self._rebuild()
         self.version += 1
 
     def clear(self) -> None:
         self.entries.clear()
+        self._rebuild()
         self.version += 1
 
     def lookup(self, frame: bytes) -> tuple[int, int] | None:

@@ -364,22 +364,63 @@ def xhdr_len(rec) -> int:
     return ENCAP6_BYTES if (int(r[12]) << 8 | int(r[13])) == 0x86DD else ENCAP_BYTES
 
 
-def out_tail(in_len, olen, xlen=0):
+def out_tail(in_len, olen, xlen=0, hv=SLOT):
     """nfdp.h out_tail: (hl, to) - valid header bytes of the out slot, tail offset in the input
-    (`xlen`: outer-header bytes of an encapsulated packet, 0 otherwise)."""
+    (`xlen`: outer-header bytes of an encapsulated packet, 0 otherwise; `hv`: valid bytes of the
+    view the out slot was built from - less than 64 for an IPv6-underlay terminated frame)."""
     d = np.asarray(olen, np.int64) - np.asarray(xlen, np.int64) - np.asarray(in_len, np.int64)
-    h = np.minimum(np.minimum(np.asarray(in_len, np.int64), SLOT) + d, SLOT)
+    h = np.minimum(np.minimum(np.asarray(in_len, np.int64), np.asarray(hv, np.int64)) + d, SLOT)
     return h, h - d
 
 
-def assemble(ohdr: np.ndarray, meta: int, in_frame: np.ndarray, in_len: int, xhdr_rec: np.ndarray | None = None) -> bytes:
-    """The frame that leaves for one packet: [outer header] ++ ohdr[:hl] ++ in_frame[to:in_len]."""
+def wide_slots(arena: np.ndarray, lens: np.ndarray, in_ports, wide_ports=()) -> tuple[np.ndarray, np.ndarray, np.ndarray]:
+    """Header slots + in-meta of frames, with a wide header pair (nfdp.h kPortCont) for every frame
+    longer than 64 B that arrives on a port in `wide_ports` (VTEP ports: single-pass tunnel
+    termination).  Returns (slots [m,64], inmeta [m], head position of each frame)."""
+    arena = np.asarray(arena, np.uint8)
+    lens = np.asarray(lens, np.uint32)
+    ports = np.broadcast_to(np.asarray(in_ports, np.uint32), lens.shape)
+    wide = np.isin(ports, np.asarray(list(wide_ports), np.uint32)) & (lens > SLOT)
+    pos = np.zeros(len(lens), np.int64)
+    pos[1:] = np.cumsum(1 + wide.astype(np.int64))[:-1]
+    m = int(len(lens) + wide.sum())
+    slots = np.zeros((m, SLOT), np.uint8)
+    im = np.zeros(m, np.uint32)
+    cols = np.arange(SLOT)
+    slots[pos] = np.where(cols[None, :] < lens[:, None], arena[:, :SLOT], 0)
+    im[pos] = inmeta(ports, lens)
+    w = np.nonzero(wide)[0]
+    if len(w):
+        second = arena[w, SLOT:2 * SLOT] if arena.shape[1] >= 2 * SLOT else np.pad(
+            arena[w, SLOT:], ((0, 0), (0, 2 * SLOT - arena.shape[1])))
+        slots[pos[w] + 1] = np.where(cols[None, :] + SLOT < lens[w, None], second, 0)
+        im[pos[w] + 1] = np.uint32(0xFFFD) | (lens[w] << np.uint32(16))
+    return slots, im, pos
+
+
+def cont_info(meta) -> tuple[int, int]:
+    """(strip, hv) of a continuation slot's egress meta (reason cont): the bytes the head's egress
+    strips from its input frame and the valid bytes of the head's out slot."""
+    port, ln, reason = meta_fields(np.array([meta], np.uint32))
+    if int(reason[0]) != 15:
+        raise ValueError("not a continuation meta")
+    return int(port[0]) & 0xFF, int(ln[0])
+
+
+def assemble(ohdr: np.ndarray, meta: int, in_frame: np.ndarray, in_len: int, xhdr_rec: np.ndarray | None = None,
+             cont_meta: int | None = None) -> bytes:
+    """The frame that leaves for one packet: [outer header] ++ ohdr[:hl] ++ in_frame[to:in_len].
+    `cont_meta`: the egress meta of the packet's continuation slot when it arrived as a wide header
+    pair (a terminated tunnel frame leaves without its outer `strip` bytes)."""
     _, olen, _ = meta_fields(np.array([meta], np.uint32))
     x = bool(meta_xhdr(np.array([meta], np.uint32))[0])
     if x and xhdr_rec is None:
         raise ValueError("meta says encapsulated but no outer-header record given")
+    strip, hv = cont_info(cont_meta) if cont_meta is not None else (0, SLOT)
+    in_frame = np.asarray(in_frame, np.uint8)[strip:]
+    in_len = int(in_len) - strip
     xl = xhdr_len(xhdr_rec) if x else 0
-    hl, to = out_tail(in_len, int(olen[0]), xl)
+    hl, to = out_tail(in_len, int(olen[0]), xl, hv)
     hl, to = int(hl), int(to)
     pre = bytes(np.asarray(xhdr_rec, np.uint8)[:xl]) if x else b""
     out = pre + bytes(np.asarray(ohdr, np.uint8)[:hl]) + bytes(np.asarray(in_frame, np.uint8)[to:in_len])

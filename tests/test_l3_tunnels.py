@@ -427,3 +427,134 @@ def test_ipv6_tunnels_gpu_bit_exact(kind):
     torch.cuda.synchronize()
     assert np.array_equal(r2g.meta.cpu().numpy().view(np.uint32), r2c.meta)
     assert (P.meta_fields(r2c.meta)[2] == 14).all()
+
+
+# ---- single-pass termination: wide header pairs (pipeline.h decap_pair, kernels.hip pair_kernel) ----
+def _tag(frames: list[bytes], vid: int = 0) -> list[bytes]:
+    """The same frames with an outer 802.1Q tag (vid 0: priority tag, passes VLAN isolation)."""
+    return [f[:12] + bytes([0x81, 0x00, vid >> 8, vid & 0xFF]) + f[12:] for f in frames]
+
+
+def _arena(frames: list[bytes]):
+    ln = np.array([len(f) for f in frames], np.uint32)
+    ar = np.zeros((len(frames), max(int(ln.max()), 128)), np.uint8)
+    for i, f in enumerate(frames):
+        ar[i, : len(f)] = np.frombuffer(f, np.uint8)
+    return ar, ln
+
+
+def _two_pass(dp, frame: bytes, enc: int) -> tuple[int, int, bytes]:
+    """The recirculation path for one terminated frame: the inner frame re-entered on the tunnel
+    port as a 64-B slot.  (egress port, reason, assembled frame)."""
+    tp = 20 if enc == 50 else 21
+    inner = frame[enc:]
+    ia, il = _arena([inner])
+    r = dp.run(P.header_slots(ia, il), P.inmeta(np.array([tp]), il))
+    port, _, reason = P.meta_fields(r.meta)
+    out = P.assemble(r.out[0], int(r.meta[0]), ia[0], int(il[0])) if int(reason[0]) == 0 else b""
+    return int(port[0]), int(reason[0]), out
+
+
+def _reverse_v4(outs):
+    back = []
+    for o in outs:
+        b = bytearray(o)
+        b[26:30], b[30:34] = o[30:34], o[26:30]
+        inner = bytearray(b[50:])
+        inner[0:6], inner[6:12] = inner[6:12], inner[0:6]
+        b[50:] = inner
+        back.append(bytes(b))
+    return back
+
+
+def _underlay_frames(dp, v6: bool):
+    slots, im, arena, lens = _encap_trace()
+    r = dp.run(slots, im)
+    side = dp.side_result()
+    outs = [P.assemble(r.out[i], int(r.meta[i]), arena[i], int(lens[i]), side["xhdr"][i]) for i in range(3)]
+    return _reverse6(outs)[0] if v6 else _reverse_v4(outs)
+
+
+@pytest.mark.parametrize("v6", [False, True])
+@pytest.mark.parametrize("tagged", [False, True])
+@pytest.mark.parametrize("kind", [T.TUN_VXLAN, T.TUN_GENEVE])
+def test_single_pass_termination_equals_recirculation(v6, tagged, kind):
+    """A tunnel frame that arrives as a wide header pair is terminated in ONE pass (IPv4 and IPv6
+    underlays, outer tag or not, VXLAN and GENEVE): the head's egress is the inner frame bridged to
+    the pod, byte for byte what the two-pass path (recirculate the inner frame on the tunnel port)
+    delivers; the continuation's meta carries strip / valid bytes; rx is counted on the VTEP port
+    (outer) and the tunnel port (inner); nothing is recirculated."""
+    dp = (_overlay6 if v6 else _overlay)("cpu", kind)
+    frames = _underlay_frames(dp, v6)
+    if tagged:
+        frames = _tag(frames)
+    enc = (70 if v6 else 50) + (4 if tagged else 0)
+    ar, ln = _arena(frames)
+    slots, im, pos = P.wide_slots(ar, ln, 30, wide_ports={30})
+    assert len(slots) == 6                                  # every frame is longer than 64 B: a pair
+    dp.reset_counters()
+    r = dp.run(slots, im)
+    port, olen, reason = P.meta_fields(r.meta)
+    for i, f in enumerate(frames):
+        h = int(pos[i])
+        assert int(reason[h + 1]) == 15 and P.cont_info(int(r.meta[h + 1])) == (enc, min(64, 128 - enc))
+        assert (int(port[h]), int(reason[h]), int(olen[h])) == (1, 0, len(f) - enc)
+        got = P.assemble(r.out[h], int(r.meta[h]), ar[i], int(ln[i]), cont_meta=int(r.meta[h + 1]))
+        ref = _two_pass(_overlay6("cpu", kind) if v6 else _overlay("cpu", kind), f if not tagged else
+                        f[:12] + f[16:], enc - (4 if tagged else 0))
+        assert ref[:2] == (1, 0) and got == ref[2]
+    pc = dp.port_counters()
+    assert int(pc[30, 0]) == 3 and int(pc[20 if not v6 else 21, 0]) == 3 and int(pc[1, 2]) == 3
+    assert int(pc[30, 1]) == sum(len(f) for f in frames)
+    d = dp.drop_counters()
+    assert d.get("cont") == 3 and not d.get("recirc") and not d.get("recirc6") and not d.get("bad_port")
+
+
+def test_single_pass_unknown_vni_falls_back():
+    """A pair whose (source, VNI) has no termination entry goes through the pipeline as received,
+    exactly like a 64-B slot of the same frame (here: IPv4 punted to the slow path, IPv6 recirc6);
+    the continuation then says strip 0 / 64 valid bytes."""
+    for v6 in (False, True):
+        dp = (_overlay6 if v6 else _overlay)("cpu")
+        frames = _underlay_frames(dp, v6)
+        b = bytearray(frames[1])
+        b[68 if v6 else 48] ^= 1
+        ar, ln = _arena([bytes(b)])
+        slots, im, pos = P.wide_slots(ar, ln, 30, wide_ports={30})
+        r = dp.run(slots, im)
+        r1 = dp.run(P.header_slots(ar, ln), P.inmeta(np.array([30]), ln))
+        assert int(r.meta[0]) == int(r1.meta[0]) and np.array_equal(r.out[0], r1.out[0])
+        assert P.cont_info(int(r.meta[1])) == (0, 64)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("v6", [False, True])
+def test_single_pass_termination_gpu_bit_exact(v6):
+    """pair_kernel + fused kernel + pair_fix on the GPU = the oracle, bit for bit (metas, out slots,
+    port / drop counters), on a mix of pairs (tagged / untagged, known / unknown VNI) and plain
+    pod traffic; running the same (rewritten-in-place) batch again gives the same metas / slots."""
+    import torch
+
+    c, g = (_overlay6 if v6 else _overlay)("cpu"), (_overlay6 if v6 else _overlay)("cuda")
+    frames = _underlay_frames(c, v6)
+    frames = frames + _tag(frames)
+    bad = bytearray(frames[0])
+    bad[68 if v6 else 48] ^= 1
+    frames.append(bytes(bad))
+    pod, pl = P.craft(4, dmac=REMOTE_MAC, smac=POD_MAC, src_ip=0x0A000001, dst_ip=0x0A000002, sport=5, dport=6)
+    mix = frames[:3] + [bytes(pod[k, : pl[k]]) for k in range(4)] + frames[3:]
+    ports = [30, 30, 30, 1, 1, 1, 1] + [30] * (len(frames) - 3)
+    ar, ln = _arena(mix)
+    slots, im, pos = P.wide_slots(ar, ln, np.array(ports), wide_ports={30})
+    c.reset_counters()
+    g.reset_counters()
+    rc = c.run(slots, im)
+    ts, ti = torch.from_numpy(slots).cuda(), torch.from_numpy(im.view(np.int32)).cuda()
+    for rnd in range(2):
+        rg = g.run(ts, ti)
+        torch.cuda.synchronize()
+        assert np.array_equal(rg.meta.cpu().numpy().view(np.uint32), rc.meta), rnd
+        assert np.array_equal(rg.out.cpu().numpy(), rc.out), rnd
+        if rnd == 0:   # (a rerun finds the heads already rewritten: the outer rx is not counted again)
+            assert np.array_equal(g.port_counters(), c.port_counters())
+            assert g.drop_counters() == c.drop_counters()
