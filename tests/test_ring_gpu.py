@@ -368,7 +368,7 @@ def test_ring_table_updates_live_without_drain():
         th = threading.Thread(target=control)
         th.start()
         flips0 = g.flip_stats["table_flips"]
-        churn, el = ring.probe(batches=6000, batch=64, inflight=1)
+        churn, el = ring.probe(batches=20000, batch=64, inflight=1)
         stop.set()
         th.join()
         assert not err, err
