@@ -51,9 +51,13 @@ constexpr uint32_t kAclIdxBits = 12;                      // rule index bits: up
 constexpr uint32_t kAclMaxRules = 1u << kAclIdxBits;
 constexpr int kE8M0Idx = 0x8B8B8B8B;                      // block scales 2^12 = 2^kAclIdxBits
 struct AclView {
-  const v4i* lw; const v4i* lc;   // LDS: first min(tiles, kLdsAclTiles) tiles
+  const v4i* lw; const v4i* lc;   // LDS: A fragments of the first ltiles tiles, C init of the first ctiles
   const v4i* gw; const v4i* gc;   // global: all tiles (+ prefilters after gc's tiles * 4 entries)
   uint32_t tiles;
+  // tiles staged in LDS (A fragments: a multiple of kAclGroup or all of them; C init: ctiles >=
+  // ltiles).  The fused kernel's one-block-per-CU instances stage more than kLdsAclTiles.
+  uint32_t ltiles = tiles < kLdsAclTiles ? tiles : kLdsAclTiles;
+  uint32_t ctiles = ltiles;
 };
 NFDP_HD uint32_t acl_groups(uint32_t tiles) { return (tiles + kAclGroup - 1) / kAclGroup; }
 // Raw first-match value (mismatch << 12 | rule) -> rule index or -1.
@@ -74,11 +78,17 @@ NFDP_HD int acl_rule_of(uint32_t b, uint32_t n_acl) {
 // Prefilter: a tile (and a group of 8 tiles) carries the bits ALL its rules care about and agree
 // on; a wave skips it - no LDS reads, no MFMAs - unless one of its packets has those bits.
 // The MFMA Toeplitz hash keeps the i8 form (it needs the parity of integer sums).
+#ifndef NFDP_PIPE_PF
+#define NFDP_PIPE_PF 1   // r3 s15 A/B: tile prefilters cost the ClassBench set 41 % (1.95 vs 1.38 ms)
+#endif
+#ifndef NFDP_PIPE_UNROLL
+#define NFDP_PIPE_UNROLL 1   // r3 s16 A/B: ACL1024 0.3145 vs 0.3211 ms, ClassBench unchanged
+#endif
 struct NoHashHook {
   __device__ void operator()(uint32_t) const {}
 };
 
-template <int HASH, int ACL, class OnHash = NoHashHook>
+template <int HASH, int ACL, class OnHash = NoHashHook, bool PIPE = false>
 __device__ __forceinline__ void classify_wave(const FlowKey& key, uint4* kx, const AclView& av, const v4i* lt,
                                               const uint32_t* ltab, const TablesView& t,
                                               uint32_t& hash, int& acl_rule, uint32_t tile0 = 0,
@@ -183,27 +193,117 @@ __device__ __forceinline__ void classify_wave(const FlowKey& key, uint4* kx, con
                                      min(__float_as_uint(acc[tt][2]), __float_as_uint(acc[tt][3]))));
       }
     };
+    // Straight-line form for batches (PIPE): the MFMAs always issue; `dead` (wave-uniform, all
+    // ones for an empty batch slot) turns the tile's result into "no match".
+    auto run_tile_m = [&](const v4i& a4, const v4i& ci, uint32_t dead) {
+      const v8i_t a = {a4[0], a4[1], a4[2], a4[3], 0, 0, 0, 0};
+      const v4f_t c = {__int_as_float(ci[0]), __int_as_float(ci[1]), __int_as_float(ci[2]), __int_as_float(ci[3])};
+      v4f_t acc[4];
+#pragma unroll
+      for (int tt = 0; tt < 4; ++tt) {
+        const v8i_t b = {bq[tt][0], bq[tt][1], bq[tt][2], bq[tt][3], 0, 0, 0, 0};
+        acc[tt] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 4, 4, 0, kE8M0Idx, 0, kE8M0One);
+      }
+#pragma unroll
+      for (int tt = 0; tt < 4; ++tt) {
+        best[tt] = min(best[tt], dead | min(min(__float_as_uint(acc[tt][0]), __float_as_uint(acc[tt][1])),
+                                            min(__float_as_uint(acc[tt][2]), __float_as_uint(acc[tt][3]))));
+      }
+    };
     // Two phases so that the LDS-resident tiles never share a join point with global loads (the
     // wait there would be vmcnt(0): the frame prefetch in flight).  Groups of 8 tiles never
-    // straddle kLdsAclTiles (a multiple of 8).
+    // straddle ltiles (a multiple of 8 unless it covers every tile).
     const uint32_t ngroups = acl_groups(av.tiles);
-    const uint32_t lds_groups = min(ngroups, kLdsAclTiles / kAclGroup);
-    for (uint32_t gi = 0; gi < lds_groups; ++gi) {
-      if (!pass(gpf + 8 * gi)) continue;
-      const uint32_t t_beg = gi * kAclGroup, t_end = min(av.tiles, t_beg + kAclGroup);
-      // this wave's first tile of the group (tiles == tile0 mod tstep)
-      for (uint32_t nt = t_beg + (tile0 + tstep - t_beg % tstep) % tstep; nt < t_end; nt += tstep) {
-        if (!pass(pf + 8 * nt)) continue;
-        run_tile(av.lw[nt * 64 + lane], av.lc[nt * 4 + g]);
+    const uint32_t lds_groups = min(ngroups, (PIPE ? av.ltiles : kLdsAclTiles) / kAclGroup);
+    // PIPE cursor: this wave's next tile >= t and < lim that passes its group and tile prefilters
+    // (scalar; the group verdict is cached).  NFDP_PIPE_PF: 2 = group + tile prefilters, 1 = group
+    // prefilters only, 0 = none (prefilters only ever skip work: results are the same).
+    uint32_t gcur = 0xFFFFFFFFu;
+    bool gok = false;
+    auto next = [&](uint32_t t, uint32_t lim) -> uint32_t {
+      t += (tile0 + tstep - t % tstep) % tstep;
+      while (t < lim) {
+        const uint32_t gi = t / kAclGroup;
+        if (gi != gcur) { gcur = gi; gok = NFDP_PIPE_PF >= 1 ? pass(gpf + 8 * gi) : true; }
+        if (gok && (NFDP_PIPE_PF < 2 || pass(pf + 8 * t))) return t;
+        if (!gok) {
+          const uint32_t nb = (gi + 1) * kAclGroup;
+          t = nb + (tile0 + tstep - nb % tstep) % tstep;
+        } else {
+          t += tstep;
+        }
+      }
+      return lim;
+    };
+    {
+      // (batches of 4 LDS tiles with their 8 fragment reads in flight together: slower, r3 s15 A/B)
+      for (uint32_t gi = 0; gi < lds_groups; ++gi) {
+        if ((!PIPE || NFDP_PIPE_PF >= 1) && !pass(gpf + 8 * gi)) continue;
+        const uint32_t t_beg = gi * kAclGroup, t_end = min(av.tiles, t_beg + kAclGroup);
+#if NFDP_PIPE_UNROLL
+        if (PIPE && NFDP_PIPE_PF < 2 && tstep == 1 && t_end - t_beg == kAclGroup) {
+          // a whole group with no tile prefilter: straight-line, so the fragment reads of later
+          // tiles issue under the MFMAs of earlier ones
+#pragma unroll
+          for (uint32_t k = 0; k < kAclGroup; ++k) run_tile(av.lw[(t_beg + k) * 64 + lane], av.lc[(t_beg + k) * 4 + g]);
+          continue;
+        }
+#endif
+        // this wave's first tile of the group (tiles == tile0 mod tstep)
+        for (uint32_t nt = t_beg + (tile0 + tstep - t_beg % tstep) % tstep; nt < t_end; nt += tstep) {
+          if ((!PIPE || NFDP_PIPE_PF >= 2) && !pass(pf + 8 * nt)) continue;
+          run_tile(av.lw[nt * 64 + lane], av.lc[nt * 4 + g]);
+        }
       }
     }
-    for (uint32_t gi = lds_groups; gi < ngroups; ++gi) {
-      if (!pass(gpf + 8 * gi)) continue;
-      const uint32_t t_beg = gi * kAclGroup, t_end = min(av.tiles, t_beg + kAclGroup);
-      for (uint32_t nt = t_beg + (tile0 + tstep - t_beg % tstep) % tstep; nt < t_end; nt += tstep) {
-        if (!pass(pf + 8 * nt)) continue;
-        run_tile(__builtin_bit_cast(v4i, __builtin_amdgcn_raw_buffer_load_b128(r_gw, (nt * 64u + lane) * 16u, 0, 0)),
-                 __builtin_bit_cast(v4i, __builtin_amdgcn_raw_buffer_load_b128(r_gc, (nt * 4u + g) * 16u, 0, 0)));
+    if (!PIPE) {
+      // tiles past the LDS copy, one at a time (instances at the 4-wave register budget; their
+      // layouts stage C init for exactly the LDS tiles: ctiles == ltiles)
+      for (uint32_t gi = lds_groups; gi < ngroups; ++gi) {
+        if (!pass(gpf + 8 * gi)) continue;
+        const uint32_t t_beg = gi * kAclGroup, t_end = min(av.tiles, t_beg + kAclGroup);
+        for (uint32_t nt = t_beg + (tile0 + tstep - t_beg % tstep) % tstep; nt < t_end; nt += tstep) {
+          if (!pass(pf + 8 * nt)) continue;
+          run_tile(__builtin_bit_cast(v4i, __builtin_amdgcn_raw_buffer_load_b128(r_gw, (nt * 64u + lane) * 16u, 0, 0)),
+                   __builtin_bit_cast(v4i, __builtin_amdgcn_raw_buffer_load_b128(r_gc, (nt * 4u + g) * 16u, 0, 0)));
+        }
+      }
+    } else if (lds_groups < ngroups) {
+      // (PIPE: the 2-wave instances, which have the registers for 8 tiles in flight)
+      // Tiles past the LDS copy: a scalar cursor yields this wave's next tile that passes its group
+      // and tile prefilters; A fragments come in batches of 4 buffer loads, the next batch issued
+      // before the current one runs (a fixed 4 loads per batch, out-of-range offsets past the last
+      // tile read 0, so every wait is a counted vmcnt: one L2 trip per 4 tiles, overlapped with
+      // the previous 4 tiles' MFMAs, instead of one exposed trip per tile).  C init from LDS when
+      // staged (ctiles), else a buffer load next to its A fragment.
+      auto ld_a = [&](uint32_t t) {
+        return __builtin_bit_cast(v4i, __builtin_amdgcn_raw_buffer_load_b128(r_gw, t < av.tiles ? (t * 64u + lane) * 16u : 0x80000000u, 0, 0));
+      };
+      auto ld_c = [&](uint32_t t) {
+        if (t < av.ctiles) return av.lc[t * 4 + g];
+        return __builtin_bit_cast(v4i, __builtin_amdgcn_raw_buffer_load_b128(r_gc, (t * 4u + g) * 16u, 0, 0));
+      };
+      // two batches with fixed roles (a register copy of a batch still in flight would wait for it)
+      uint32_t c0[4], c1[4], t = next(lds_groups * kAclGroup, av.tiles);
+      v4i a0[4], a1[4];
+      auto fill = [&](uint32_t (&c)[4], v4i (&av4)[4]) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          c[k] = t; av4[k] = ld_a(t);
+          if (t < av.tiles) t = next(t + tstep, av.tiles);
+        }
+      };
+      auto run4 = [&](const uint32_t (&c)[4], const v4i (&av4)[4]) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) run_tile_m(av4[k], ld_c(c[k] < av.tiles ? c[k] : 0u), c[k] < av.tiles ? 0u : 0xFFFFFFFFu);
+      };
+      fill(c0, a0);
+      while (c0[0] < av.tiles) {
+        fill(c1, a1);
+        run4(c0, a0);
+        if (c1[0] >= av.tiles) break;
+        fill(c0, a0);
+        run4(c1, a1);
       }
     }
 #pragma unroll

@@ -92,14 +92,28 @@ __device__ __forceinline__ size_t lds_align16(size_t x) { return (x + 15) & ~(si
 
 struct LdsLayout {
   size_t acl_w, acl_c, toep_f, toep_t, kx, pc, drops, tports, tchain, tperm, total;
+  uint32_t ltiles, ctiles;  // ACL tiles whose A fragments / C init are staged
   bool tabs;  // small tables (ports < kLdsPorts, chain words, ACL verdicts) staged in LDS
 };
-__host__ __device__ inline LdsLayout lds_layout(int hash_mode, int acl_mode, uint32_t acl_tiles) {
+// `one_block`: the instance runs one workgroup per CU (EARLY: 2 waves / SIMD), so the rule tiles
+// may use the LDS the second block would have had: every tile's C init and as many A fragments
+// as fit (ClassBench-sized rule sets: ~100 of 199 tiles instead of 64).
+__host__ __device__ inline LdsLayout lds_layout(int hash_mode, int acl_mode, uint32_t acl_tiles, bool one_block = false) {
   LdsLayout L;
   size_t o = 0;
-  const uint32_t lt = acl_tiles < kLdsAclTiles ? acl_tiles : kLdsAclTiles;
+  uint32_t lt = acl_tiles < kLdsAclTiles ? acl_tiles : kLdsAclTiles, ct = lt;
+  if (one_block && acl_mode == kAclMfma && acl_tiles > kLdsAclTiles) {
+    const size_t rest = (hash_mode == kHashMfma ? 2 * 2 * 64 * 16 : 0) + (hash_mode == kHashLds ? 16 * 256 * 4 : 0) +
+                        kFWaves * 64 * 16 + kLdsPorts * 4 * 4 + kNumReasons * 4 + 16 + kLdsTabBytes;
+    const size_t budget = 160 * 1024 - 2048;   // static LDS + alignment margin
+    ct = acl_tiles;
+    const size_t room = budget > rest + (size_t)ct * 64 ? budget - rest - (size_t)ct * 64 : 0;
+    const uint32_t fit = (uint32_t)(room / 1024) & ~(kAclGroup - 1);
+    lt = fit > lt ? (fit < acl_tiles ? fit : acl_tiles) : lt;
+  }
+  L.ltiles = lt; L.ctiles = ct;
   L.acl_w = o; if (acl_mode == kAclMfma) o += (size_t)lt * 64 * 16;
-  L.acl_c = o; if (acl_mode == kAclMfma) o += (size_t)lt * 4 * 16;
+  L.acl_c = o; if (acl_mode == kAclMfma) o += (size_t)ct * 4 * 16;
   L.toep_f = o; if (hash_mode == kHashMfma) o += 2 * 2 * 64 * 16;
   L.toep_t = o; if (hash_mode == kHashLds) o += 16 * 256 * 4;
   L.kx = o; o += kFWaves * 64 * 16;
@@ -116,6 +130,21 @@ __host__ __device__ inline LdsLayout lds_layout(int hash_mode, int acl_mode, uin
   return L;
 }
 
+// Per-flow packed counter add (no return).  The ablation forms are cost attribution only: without
+// the add the headline kernel runs 0.219 instead of 0.273 ms per 4M packets; the same add at
+// workgroup scope costs the same; issued one iteration later (after the next bucket loads, state
+// in LDS) it is slower, 0.292 ms (r3 s13 A/B, profiles/r3_s13_flowctr_ab.txt): the cost is the
+// random read-modify-write itself, not the wait behind it.
+__device__ __forceinline__ void flow_ctr_add(unsigned long long* p, unsigned long long v) {
+#if defined(NFDP_ABL_NO_FLOWCTR)     // no per-flow counts at all (wrong counters)
+  (void)p; (void)v;
+#elif defined(NFDP_ABL_FLOWCTR_WG)   // workgroup scope (not coherent across XCDs)
+  __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#else
+  atomicAdd(p, v);
+#endif
+}
+
 constexpr int kBufCfg = 0x00020000;  // buffer resource word 3 (gfx9 family raw buffer)
 constexpr int kStreamAux = 2;        // nt: frames are read once / written once (streaming)
 
@@ -124,7 +153,7 @@ __global__ __launch_bounds__(kFB, EARLY ? NFDP_EARLY_WAVES_PER_EU : NFDP_FUSED_W
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ uint32_t rcnt[REMOTE ? 2 * kMaxRanks : 1], rbase[REMOTE ? kMaxRanks : 1];  // rcnt double-buffered
   __shared__ uint32_t lst_n;                                  // LIST: entries of this workgroup's region
-  const LdsLayout L = lds_layout(HASH, ACL, a.acl_tiles);
+  const LdsLayout L = lds_layout(HASH, ACL, a.acl_tiles, EARLY);
   v4i* lw = reinterpret_cast<v4i*>(smem + L.acl_w);
   v4i* lc = reinterpret_cast<v4i*>(smem + L.acl_c);
   v4i* lt = reinterpret_cast<v4i*>(smem + L.toep_f);
@@ -135,11 +164,11 @@ __global__ __launch_bounds__(kFB, EARLY ? NFDP_EARLY_WAVES_PER_EU : NFDP_FUSED_W
 
   // ---- stage classification tables + zero counters ----
   if constexpr (ACL == kAclMfma) {
-    const uint32_t lt_ = min(a.acl_tiles, kLdsAclTiles), nw = lt_ * 64, nc = lt_ * 4;
+    const uint32_t nw = L.ltiles * 64, nc = L.ctiles * 4;
     for (uint32_t i = threadIdx.x; i < nw; i += kFB) lw[i] = a.acl_wfrag[i];
     for (uint32_t i = threadIdx.x; i < nc; i += kFB) lc[i] = a.acl_cinit[i];
   }
-  const AclView av{lw, lc, a.acl_wfrag, a.acl_cinit, a.acl_tiles};
+  const AclView av{lw, lc, a.acl_wfrag, a.acl_cinit, a.acl_tiles, L.ltiles, L.ctiles};
   if constexpr (HASH == kHashMfma)
     for (uint32_t i = threadIdx.x; i < 256; i += kFB) lt[i] = a.toep_frag[i];
   if constexpr (HASH == kHashLds)
@@ -207,8 +236,8 @@ __global__ __launch_bounds__(kFB, EARLY ? NFDP_EARLY_WAVES_PER_EU : NFDP_FUSED_W
     uint4 bv[8];
     if constexpr (EARLY) {
       // the bucket fetch leaves as soon as the hash is known: its latency runs under the ACL
-      classify_wave<HASH, ACL>(st.key, kx, av, lt, ltab, a.t, hash, acl_rule, 0, 1, nullptr,
-                               [&](uint32_t h) { flow_probe_issue(a.t, h, bv); });
+      auto issue = [&](uint32_t h) { flow_probe_issue(a.t, h, bv); };
+      classify_wave<HASH, ACL, decltype(issue), true>(st.key, kx, av, lt, ltab, a.t, hash, acl_rule, 0, 1, nullptr, issue);
     } else {
       classify_wave<HASH, ACL>(st.key, kx, av, lt, ltab, a.t, hash, acl_rule);
     }
@@ -337,7 +366,7 @@ __global__ __launch_bounds__(kFB, EARLY ? NFDP_EARLY_WAVES_PER_EU : NFDP_FUSED_W
       // so the compiler can wait for the prefetched frame with vmcnt(N > 0) at the loop head
       // instead of draining this slot's atomic and stores.
       const uint32_t cslot = hit ? (uint32_t)slot : (i & ctr_mask);
-      atomicAdd(a.flow_ctr + cslot, (hit && !(a.flags & 4u)) ? ctr_inc(st.wire_len) : 0ull);
+      flow_ctr_add(a.flow_ctr + cslot, (hit && !(a.flags & 4u)) ? ctr_inc(st.wire_len) : 0ull);
       wave_frames_store<kStreamAux>(kx, o, r_out, run_of(base));
       __builtin_amdgcn_raw_buffer_store_b32(meta, r_meta, valid ? i * 4u : kNoRun, 0, kStreamAux);
       __builtin_amdgcn_raw_buffer_store_b32(lat_now, r_lat, sample ? (i >> 4) * 4u : kNoRun, 0, 0);
@@ -671,7 +700,7 @@ static hipError_t launch_fused_t(const FusedArgs& a, int num_cus, hipStream_t s)
   // rcnt[2][..] + rbase + lst_n, with room for the compiler's alignment of the static block
   constexpr size_t kStatic = (3 * (R ? kMaxRanks : 1) + 1) * sizeof(uint32_t) + 64;
   constexpr size_t kMaxDyn = 160 * 1024 - kStatic;
-  const size_t lds = lds_layout(H, A, a.acl_tiles).total;
+  const size_t lds = lds_layout(H, A, a.acl_tiles, E).total;
   if (lds > kMaxDyn) return hipErrorInvalidValue;
   if (R && (a.nranks == 0 || a.nranks > kMaxRanks || a.rank >= a.nranks || !a.send_pkt || !a.pcnt ||
             (size_t)a.nranks * pkt_seg_bytes(a.cap_pkt) >= (1ull << 31) || a.n >= (1u << 25)))

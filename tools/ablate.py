@@ -25,9 +25,11 @@ def main():
     for name, hm, am, nacl in (("lds+mfmaACL256", "lds", "mfma", 256), ("mfma+mfmaACL256", "mfma", "mfma", 256),
                                ("lds+aclOff", "lds", "off", 256), ("mfma+mfmaACL1024", "mfma", "mfma", 1024),
                                ("lds+mfmaACL1024", "lds", "mfma", 1024), ("mfma+mfmaACL512", "mfma", "mfma", 512),
-                               ("lds+scalarACL256", "lds", "scalar", 256)):
+                               ("lds+scalarACL256", "lds", "scalar", 256), ("lds+mfmaWild", "lds", "mfma", "wild")):
         g = DataPlane(device=dev, flow_buckets=1 << 19, hash_mode=hm, acl_mode=am)
-        sc = S.build_sfc(g, n_pods=8, n_flows=1 << 20, n_acl=nacl, seed=0)
+        sc = S.build_sfc(g, n_pods=8, n_flows=1 << 20, n_acl=nacl if nacl != "wild" else 256, seed=0)
+        if nacl == "wild":   # ClassBench-style rule set (bench.py value_acl_wild)
+            S.install_acl_wild(g)
         g.commit(full=True)
         variants[name] = (g, 0, True)
         if base is None:

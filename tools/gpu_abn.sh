@@ -10,7 +10,7 @@ for pass in $(seq 1 "${PASSES:-2}"); do
     for v in "$V" ""; do
       echo "variant=${v:-default} pass=$pass" | tee -a gpurun_out/abn_results.txt
       NFDP_EXT_DIR="$v" timeout -k 10 200 python tools/ablate.py --rounds 3 > gpurun_out/abn_run.log 2>&1 || exit 1
-      grep -E "ACL256|aclOff|ACL1024" gpurun_out/abn_run.log | tee -a gpurun_out/abn_results.txt
+      grep -E "ACL256|aclOff|ACL1024|Wild" gpurun_out/abn_run.log | tee -a gpurun_out/abn_results.txt
     done
   done
 done
