@@ -150,6 +150,25 @@ def measure_variants(a, dp, sc, dev, torch, S, P) -> dict:
     dp.acl.version += 1
     dp.commit()
     del mixed, b
+    # dual stack: half the batch IPv6 (64K IPv6 flows of the same pods, 64 IPv6 ACL rules: the
+    # v6_kernel pre-pass + the IPv6-capable fused instance), half the headline's IPv4 traffic.
+    # Last: it turns the data plane's IPv6 features on.
+    info6 = S.install_ipv6(dp, sc, 1 << 16, 64)
+    dp.commit()
+    b = []
+    for r in range(2):
+        pk4, im4 = S.traffic(sc, n - n // 2, seed=9200 + r)
+        pk6, im6 = S.traffic_ipv6(sc, info6, n // 2, seed=9300 + r)
+        perm = np.random.default_rng(r).permutation(n)
+        pk, im = np.concatenate([pk4, pk6])[perm], np.concatenate([im4, im6])[perm]
+        b.append((torch.from_numpy(np.ascontiguousarray(pk)).to(dev),
+                  torch.from_numpy(np.ascontiguousarray(im).view(np.int32)).to(dev)))
+    el, meta = _time_fused(dp, b, a.variant_steps, torch)
+    res["ipv6_mpps"] = round(n * a.variant_steps / el / 1e6, 1)
+    res["ipv6"] = {"ipv6_fraction": 0.5, "ipv6_flows": info6["flows"], "ipv6_acl_rules": info6["rules"],
+                   "forwarded_fraction": round(float(np.mean(P.meta_fields(meta.cpu().numpy().view(np.uint32))[2] == 0)), 4),
+                   "frames": "64-B IPv4 + 66-B tagged IPv6/UDP (the smallest)"}
+    del b
     return res
 
 
@@ -530,6 +549,7 @@ def main() -> None:
             "value_acl1024": None if not variants else variants["acl1024_mpps"],
             "value_acl_wild": None if not variants else variants["acl_wild_mpps"],
             "value_l3": None if not variants else variants["l3_mpps"],
+            "value_ipv6": None if not variants else variants["ipv6_mpps"],
             "imix": None if not variants else variants["imix"],
             "variants": variants,
             # live pod -> pod through the native I/O engine + ring kernel (memif vports, 64-B frames)

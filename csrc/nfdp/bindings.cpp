@@ -33,6 +33,14 @@ T val(const py::dict& d, const char* k, T def) {
   return d[k].cast<T>();
 }
 
+TablesView tables_from(const py::dict& d);
+// IPv6 ACL tiles of a fused launch (tables dict: acl6_wfrag / acl6_cinit / acl6_tiles)
+void acl6_from(FusedLaunch& f, const py::dict& d) {
+  f.acl6_wfrag = ptr<const void>(d, "acl6_wfrag");
+  f.acl6_cinit = ptr<const void>(d, "acl6_cinit");
+  f.acl6_tiles = val<uint32_t>(d, "acl6_tiles", 0);
+}
+
 TablesView tables_from(const py::dict& d) {
   TablesView t{};
   t.ports = ptr<const PortEntry>(d, "ports");
@@ -56,6 +64,12 @@ TablesView tables_from(const py::dict& d) {
   t.lpm6_mask = t.lpm6 ? val<uint32_t>(d, "lpm6_mask", 0) : 0u;
   t.lpm6_lens = ptr<const uint8_t>(d, "lpm6_lens");
   t.n_lpm6_lens = t.lpm6_lens ? val<uint32_t>(d, "n_lpm6_lens", 0) : 0u;
+  t.flow6_on = val<uint32_t>(d, "flow6_on", 0);
+  t.acl6_value = ptr<const uint32_t>(d, "acl6_value");
+  t.acl6_mask = ptr<const uint32_t>(d, "acl6_mask");
+  t.n_acl6 = (t.acl6_value && t.acl6_mask) ? val<uint32_t>(d, "n_acl6", 0) : 0u;
+  if (t.n_acl6 > 4096) throw std::invalid_argument("at most 4096 IPv6 ACL rules");
+  if (t.n_acl6 && !t.acl_permit) throw std::invalid_argument("n_acl6 > 0 but acl_permit missing");
   if (t.lpm6 && ((t.lpm6_mask + 1) & t.lpm6_mask)) throw std::invalid_argument("lpm6 table size must be a power of two");
   if (t.n_lpm6_lens > 129) throw std::invalid_argument("at most 129 IPv6 prefix lengths");
   t.lpm24 = ptr<const uint32_t>(d, "lpm24");
@@ -304,6 +318,15 @@ PYBIND11_MODULE(_nfdp, m) {
     return py::make_tuple(py::array_t<int8_t>(f.wfrag.size(), f.wfrag.data()),
                           py::array_t<int32_t>(f.cinit.size(), f.cinit.data()), f.tiles);
   });
+  m.def("build_acl6_frags", [](U32Arr value, U32Arr mask) {
+    if (value.ndim() != 2 || value.shape(1) != 12 || mask.ndim() != 2 || mask.shape(1) != 12 ||
+        value.shape(0) != mask.shape(0))
+      throw std::invalid_argument("IPv6 ACL value/mask must be [n,12] uint32");
+    AclFrags f = build_acl6_frags(value.data(), mask.data(), (uint32_t)value.shape(0));
+    return py::make_tuple(py::array_t<int8_t>(f.wfrag.size(), f.wfrag.data()),
+                          py::array_t<int32_t>(f.cinit.size(), f.cinit.data()), f.tiles);
+  });
+  m.def("fold6", [](uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3) { return fold6(a0, a1, a2, a3); });
   m.def("build_toeplitz_frags", [](py::bytes rss) {
     std::string s = rss;
     if (s.size() < 20) throw std::invalid_argument("rss key must be >= 20 bytes");
@@ -355,6 +378,7 @@ PYBIND11_MODULE(_nfdp, m) {
     if (f.steer_list) { f.nranks = nranks; f.rank = rank; }
     f.side = side_from(side);
     f.t = tables_from(tables);
+    acl6_from(f, tables);
     f.pkts = reinterpret_cast<const void*>(pkts);
     f.inmeta = reinterpret_cast<const uint32_t*>(inmeta);
     f.out = reinterpret_cast<void*>(out);
@@ -449,6 +473,7 @@ PYBIND11_MODULE(_nfdp, m) {
                                 uintptr_t stream) {
     IngressArgs a{};
     a.t = tables_from(tables);
+    a.t.flow6_on = 0;   // IPv6 flows need the addresses at the probe: not on the sharded path (shard.hip)
     a.pkts = ptr<const uint4>(d, "pkts"); a.inmeta = ptr<const uint32_t>(d, "inmeta");
     a.n = val<uint32_t>(d, "n", 0); a.g = geom(d);
     a.send_desc = ptr<uint8_t>(d, "send_desc"); a.cnt = ptr<uint32_t>(d, "cnt");
@@ -509,6 +534,7 @@ PYBIND11_MODULE(_nfdp, m) {
     ShardGeom g = geom(d);
     FusedLaunch f{};
     f.t = tables_from(tables);
+    acl6_from(f, tables);
     f.pkts = ptr<const void>(d, "pkts"); f.inmeta = ptr<const uint32_t>(d, "inmeta");
     f.out = ptr<void>(d, "out"); f.out_meta = ptr<uint32_t>(d, "out_meta"); f.n = val<uint32_t>(d, "n", 0);
     f.flow_ctr = ptr<unsigned long long>(d, "flow_ctr"); f.port_ctr = ptr<unsigned long long>(d, "port_ctr");
@@ -572,6 +598,7 @@ PYBIND11_MODULE(_nfdp, m) {
                         int num_cus) {
         FusedLaunch f{};
         f.t = tables_from(tables);
+        acl6_from(f, tables);
         f.flow_ctr = ptr<unsigned long long>(d, "flow_ctr"); f.port_ctr = ptr<unsigned long long>(d, "port_ctr");
         f.drop_ctr = ptr<unsigned long long>(d, "drop_ctr"); f.t0 = ptr<const unsigned long long>(d, "t0");
         f.acl_wfrag = ptr<const void>(d, "acl_wfrag"); f.acl_cinit = ptr<const void>(d, "acl_cinit");
@@ -638,6 +665,7 @@ PYBIND11_MODULE(_nfdp, m) {
                        double deadline_s) {
         FusedLaunch f{};
         f.t = tables_from(tables);
+        acl6_from(f, tables);
         f.flow_ctr = ptr<unsigned long long>(d, "flow_ctr"); f.port_ctr = ptr<unsigned long long>(d, "port_ctr");
         f.drop_ctr = ptr<unsigned long long>(d, "drop_ctr");
         f.acl_wfrag = ptr<const void>(d, "acl_wfrag"); f.acl_cinit = ptr<const void>(d, "acl_cinit");
@@ -658,6 +686,7 @@ PYBIND11_MODULE(_nfdp, m) {
       .def("stage_tables", [](RingEngine& r, py::dict tables, py::dict d, int which) {
         FusedLaunch f{};
         f.t = tables_from(tables);
+        acl6_from(f, tables);
         f.acl_wfrag = ptr<const void>(d, "acl_wfrag"); f.acl_cinit = ptr<const void>(d, "acl_cinit");
         f.acl_tiles = val<uint32_t>(d, "acl_tiles", 1);
         f.toep_frag = ptr<const void>(d, "toep_frag"); f.toep_tab = ptr<const uint32_t>(d, "toep_tab");

@@ -369,14 +369,15 @@ struct LdsTables {
 __device__ __forceinline__ LdsTables stage_lds_tables(const TablesView& t, PortEntry* lport, uint64_t* lchain,
                                                       uint8_t* lperm, bool enabled, uint32_t nthreads) {
   const uint32_t nchain = enabled ? min(t.n_chains, kLdsChains) : 0u;
-  const bool lds_perm = enabled && t.n_acl <= 1024;  // verdict bytes staged for the first 1024 rules
+  const uint32_t nperm = t.n_acl + t.n_acl6;           // IPv4 then IPv6 rule verdicts
+  const bool lds_perm = enabled && nperm <= 1024;      // verdict bytes staged for up to 1024 rules
   if (enabled) {
     const uint4* gp = reinterpret_cast<const uint4*>(t.ports);
     uint4* lp = reinterpret_cast<uint4*>(lport);
     for (uint32_t i = threadIdx.x; i < kLdsPorts * 2; i += nthreads) lp[i] = gp[i];
     for (uint32_t i = threadIdx.x; i < nchain; i += nthreads) lchain[i] = *reinterpret_cast<const uint64_t*>(&t.chains[i]);
     if (lds_perm)
-      for (uint32_t i = threadIdx.x; i < t.n_acl; i += nthreads) lperm[i] = t.acl_permit[i];
+      for (uint32_t i = threadIdx.x; i < nperm; i += nthreads) lperm[i] = t.acl_permit[i];
   }
   return LdsTables{t, lport, lchain, lperm, enabled ? (uint32_t)kLdsPorts : 0u, nchain, lds_perm};
 }

@@ -38,7 +38,7 @@ int64_t FlowTableHost::find(const FlowKey& k) const {
 }
 
 int64_t FlowTableHost::insert(const FlowKey& key, const FlowAction& act) {
-  if (key.meta & 0xFF00u) throw std::invalid_argument("FlowKey.meta byte 1 must be zero");
+  if (key.meta & 0xFF00u & ~kKeyV6) throw std::invalid_argument("FlowKey.meta byte 1 must be zero (but kKeyV6)");
   const int64_t existing = find(key);
   if (existing >= 0) {
     slots_[existing].act = act;
@@ -216,6 +216,41 @@ AclFrags build_acl_frags(const uint32_t* value, const uint32_t* mask, uint32_t n
   return f;
 }
 
+AclFrags build_acl6_frags(const uint32_t* value, const uint32_t* mask, uint32_t n) {
+  if (n > 4096) throw std::invalid_argument("IPv6 ACL supports at most 4096 rules (12-bit rule index)");
+  AclFrags f;
+  f.tiles = (n + 15) / 16;
+  if (f.tiles == 0) f.tiles = 1;
+  f.wfrag.assign((size_t)f.tiles * 3 * 64 * 16, 0);
+  f.cinit.assign((size_t)f.tiles * 16, 0);
+  for (uint32_t nt = 0; nt < f.tiles; ++nt)
+    for (int k = 0; k < 3; ++k)
+      for (int l = 0; l < 64; ++l)
+        for (int j = 0; j < 32; ++j) {
+          const uint32_t r = nt * 16 + (l & 15);
+          if (r >= n) continue;
+          const int b = 32 * (l >> 4) + j;   // bit of words 4k .. 4k+3
+          const uint32_t* mw = mask + 12 * (size_t)r + 4 * k;
+          const uint32_t* vw = value + 12 * (size_t)r + 4 * k;
+          if (!key_bit(mw, b)) continue;
+          const uint8_t w = key_bit(vw, b) ? 0xA : 0x2;
+          uint8_t& byte = reinterpret_cast<uint8_t&>(f.wfrag[(((size_t)nt * 3 + k) * 64 + l) * 16 + j / 2]);
+          byte = (uint8_t)(byte | (w << (4 * (j & 1))));
+        }
+  for (uint32_t k = 0; k < f.tiles * 16; ++k) {
+    float c = 4096.0f + 4095.0f;   // padding row: never a match
+    if (k < n) {
+      int32_t bb = 0;
+      for (int b = 0; b < 384; ++b)
+        if (key_bit(mask + 12 * (size_t)k, b) && key_bit(value + 12 * (size_t)k, b)) ++bb;
+      c = (float)bb * 4096.0f + (float)k;
+    }
+    const uint32_t nt = k / 16, row = k % 16;
+    std::memcpy(&f.cinit[((size_t)nt * 4 + row / 4) * 4 + row % 4], &c, 4);
+  }
+  return f;
+}
+
 static inline int rss_bit(const uint8_t* key, int x) { return (key[x >> 3] >> (7 - (x & 7))) & 1; }
 
 std::vector<int8_t> build_toeplitz_frags(const uint8_t* rss_key) {
@@ -330,13 +365,14 @@ void oracle_run(const TablesView& t, const uint32_t* pkts, const uint32_t* inmet
     if (cont) { st.reason = kCont; st.in_ext = i ? prev_ci : ((uint32_t)kSlotBytes << 8); }
     prev_ci = ci;
     const uint32_t h = toeplitz_scalar(st.key, t.rss_key);
-    const int acl = acl_first_match(t, st.key);
+    const int acl = acl_rule_scalar(t, p, st);
     if (hashes) hashes[i] = h;
     if (acl_rules) acl_rules[i] = acl;
     bool hit = false;
     FlowAction act = {};
-    if (!st.reason && p.ipv4) {
-      const int64_t slot = flow_lookup(t, st.key, h);
+    if (!st.reason && flowable(t, p)) {
+      int64_t slot = flow_lookup(t, st.key, h);
+      if (slot >= 0 && p.ipv6 && !flow6_verify(t, p, slot)) slot = -1;
       if (slot >= 0) {
         hit = true;
         act = t.flows[slot].act;
@@ -405,15 +441,16 @@ void oracle_run_remote(const TablesView& t, const uint32_t* pkts, const uint32_t
     if (cont) { st.reason = kCont; st.in_ext = i ? prev_ci : ((uint32_t)kSlotBytes << 8); }
     prev_ci = ci;
     const uint32_t h = toeplitz_scalar(st.key, t.rss_key);
-    const int acl = acl_first_match(t, st.key);
+    const int acl = acl_rule_scalar(t, p, st);
     // flow-owner steering: another GPU's flow goes to its owner as it came in
     const uint32_t owner = owner_of(h, r.nranks);
-    const bool to_owner = r.steer && !st.reason && p.ipv4 && owner != r.rank && im == inmeta[i];   // (terminated: stays)
+    const bool to_owner = r.steer && !st.reason && flowable(t, p) && owner != r.rank && im == inmeta[i];   // (terminated: stays)
     if (to_owner) st.reason = kRemote;
     bool hit = false;
     FlowAction act = {};
-    if (!st.reason && p.ipv4) {
-      const int64_t slot = flow_lookup(t, st.key, h);
+    if (!st.reason && flowable(t, p)) {
+      int64_t slot = flow_lookup(t, st.key, h);
+      if (slot >= 0 && p.ipv6 && !flow6_verify(t, p, slot)) slot = -1;
       if (slot >= 0) {
         hit = true;
         act = t.flows[slot].act;

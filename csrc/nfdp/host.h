@@ -54,6 +54,9 @@ struct AclFrags {
   uint32_t tiles = 0;
 };
 AclFrags build_acl_frags(const uint32_t* value, const uint32_t* mask, uint32_t n);
+// IPv6 ACL tiles: 16 rules x 3 K-blocks of 128 key6 bits ([tiles][3][64] A fragments, [tiles][16]
+// C init); rules keep their order (the rule index rides in the accumulator).
+AclFrags build_acl6_frags(const uint32_t* value, const uint32_t* mask, uint32_t n);
 std::vector<int8_t> build_toeplitz_frags(const uint8_t* rss_key);   // [2][2][64][16]
 std::vector<uint32_t> build_toeplitz_table(const uint8_t* rss_key); // [16][256]
 
@@ -113,6 +116,8 @@ struct FusedLaunch {
   uint32_t* steer_list = nullptr;
   uint32_t* steer_cnt = nullptr;   // 2 + 4 * num_cus words: {grid, region size, count per workgroup}
   uint32_t steer_cap = 0;          // steer_list entries (>= steer_list_len(n, num_cus))
+  // IPv6 ACL (t.n_acl6 > 0): acl6_kernel classifies the batch's IPv6 packets first (into out_meta)
+  const void* acl6_wfrag = nullptr; const void* acl6_cinit = nullptr; uint32_t acl6_tiles = 0;
 };
 // Second half of steer-by-list: listed packets -> their owners' exchange segments (count-first,
 // segments sized for the whole batch).

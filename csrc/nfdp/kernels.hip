@@ -148,8 +148,14 @@ __device__ __forceinline__ void flow_ctr_add(unsigned long long* p, unsigned lon
 constexpr int kBufCfg = 0x00020000;  // buffer resource word 3 (gfx9 family raw buffer)
 constexpr int kStreamAux = 2;        // nt: frames are read once / written once (streaming)
 
-template <int HASH, int ACL, bool REMOTE, bool EARLY, bool LIST = false>
+// V6: the instances for tables with IPv6 flows / rules (1-GPU, not REMOTE / LIST): IPv6 keys,
+// rules and flow checks come from v6_kernel.  Overriding the key costs its rematerialisation
+// (the key words are otherwise recomputed from the header), so these instances load the next
+// frame after the tail instead of prefetching it under this slot's work: the IPv4-only
+// instances keep their register budget untouched.
+template <int HASH, int ACL, bool REMOTE, bool EARLY, bool LIST = false, bool V6 = false>
 __global__ __launch_bounds__(kFB, EARLY ? NFDP_EARLY_WAVES_PER_EU : NFDP_FUSED_WAVES_PER_EU) void fused_kernel(FusedArgs a) {
+  static_assert(!V6 || (!REMOTE && !LIST), "IPv6 instances are 1-GPU instances");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ uint32_t rcnt[REMOTE ? 2 * kMaxRanks : 1], rbase[REMOTE ? kMaxRanks : 1];  // rcnt double-buffered
   __shared__ uint32_t lst_n;                                  // LIST: entries of this workgroup's region
@@ -225,7 +231,18 @@ __global__ __launch_bounds__(kFB, EARLY ? NFDP_EARLY_WAVES_PER_EU : NFDP_FUSED_W
     wave_frames_to_lanes(kx, cn, dn);
     Parsed p;
     IngressState st;
-    ingress_stage(a.t, ta, dn, imn, p, st);  // copies the frame into p.s: dn is free for the prefetch
+    ingress_stage<LdsTables, false>(a.t, ta, dn, imn, p, st);  // copies the frame into p.s: dn is free for the prefetch
+    // IPv6 keys (tables with IPv6 flows / rules): v6_kernel folded them into out[i] (overwritten
+    // by this lane's egress slot in the tail)
+    if constexpr (V6) {
+      if (__builtin_expect(__any(p.ipv6), 0)) {
+        if (p.ipv6 && valid) {
+          const uint4 k6 = a.out[i];
+          st.key.src_ip = k6.x; st.key.dst_ip = k6.y; st.key.ports = k6.z; st.key.meta = k6.w;
+        }
+      }
+    }
+    const bool flowp = V6 ? flowable(a.t, p) : p.ipv4;   // takes part in the flow stage
     // (a continuation slot of a wide header pair is bad_port here - in-meta port kPortCont;
     // pair_fix_kernel turns its meta / counters into kCont afterwards: no pair code in this loop)
 
@@ -241,6 +258,22 @@ __global__ __launch_bounds__(kFB, EARLY ? NFDP_EARLY_WAVES_PER_EU : NFDP_FUSED_W
     } else {
       classify_wave<HASH, ACL>(st.key, kx, av, lt, ltab, a.t, hash, acl_rule);
     }
+    // IPv6: the rule comes from the IPv6 TCAM (v6_kernel ran over this batch), never from the
+    // IPv4 rules over the folded key (wave-uniform skip for all-IPv4 waves)
+    // (instances without V6 run only for tables with no IPv6 flows / rules: an IPv6 packet's key
+    // carries kKeyV6, which no IPv4 rule or flow matches)
+    bool v6ok = false;
+    if constexpr (V6) {
+      if (__builtin_expect(__any(p.ipv6), 0)) {
+        // (v6_kernel parks each IPv6 packet's rule + 1 | verified-hit << 31 in its out_meta word,
+        // which this lane overwrites with the egress meta in the tail)
+        if (p.ipv6) {
+          const uint32_t w6 = valid ? a.out_meta[i] : 0u;
+          acl_rule = (int)(w6 & 0xFFFFu) - 1;
+          v6ok = (w6 >> 31) != 0;
+        }
+      }
+    }
     // flow-owner steering (REMOTE steer = 1, or the 1-GPU instance's steer list): a packet of
     // another GPU's flow shard leaves now, as it came in; its owner runs the whole pipeline on it
     bool to_owner = false;
@@ -248,16 +281,16 @@ __global__ __launch_bounds__(kFB, EARLY ? NFDP_EARLY_WAVES_PER_EU : NFDP_FUSED_W
     if constexpr (REMOTE) {
       if (a.steer) {
         owner = owner_of(hash, a.nranks);
-        to_owner = valid && !st.reason && p.ipv4 && owner != a.rank;
+        to_owner = valid && !st.reason && flowp && owner != a.rank;
         if (to_owner) st.reason = kRemote;  // no local probe / chain / counters
       }
     } else if constexpr (LIST) {   // separate instances: the 1-GPU hot kernel is untouched
       // the owner test only (the flag lives in st.reason: no probe / chain / counters); the list
       // append comes after the tail's stores, where the register pressure is lowest (placed
       // here, the same append cost the instance 15 more spilled VGPRs)
-      if (valid && !st.reason && p.ipv4 && owner_of(hash, a.nranks) != a.rank) st.reason = kRemote;
+      if (valid && !st.reason && flowp && owner_of(hash, a.nranks) != a.rank) st.reason = kRemote;
     }
-    if constexpr (!REMOTE) {
+    if constexpr (!REMOTE && !V6) {
       // prefetch the next slot now: it lands under this slot's probe and chain
       const uint32_t nx = i + stride;
       wave_frames_load<kStreamAux>(r_pk, run_of(base + stride), cn);
@@ -270,13 +303,16 @@ __global__ __launch_bounds__(kFB, EARLY ? NFDP_EARLY_WAVES_PER_EU : NFDP_FUSED_W
 #ifndef NFDP_LANE_PROBE
     {
       uint4 v;
-      if constexpr (EARLY) slot = flow_probe_finish(a.t, st.key, hash, !st.reason && p.ipv4, kx, bv, v);
-      else slot = flow_probe_wave(a.t, st.key, hash, !st.reason && p.ipv4, kx, v);
+      if constexpr (EARLY) slot = flow_probe_finish(a.t, st.key, hash, !st.reason && flowp, kx, bv, v);
+      else slot = flow_probe_wave(a.t, st.key, hash, !st.reason && flowp, kx, v);
 #else
-    if (!st.reason && p.ipv4) {
+    if (!st.reason && flowp) {
       uint4 v;
       slot = flow_probe(a.t, st.key, hash, v);
 #endif
+      // an IPv6 folded-key hit counts only if the slot's side entry holds this packet's addresses:
+      // v6_kernel checked that before this kernel (bit 31 of the word it parked in out_meta[i])
+      if (V6 && p.ipv6 && !v6ok) slot = -1;
       if (slot >= 0) {
         hit = true;
         act.chain_id = v.x & 0xFFFFu; act.out_port = v.x >> 16; act.nat_ip = v.y;
@@ -387,6 +423,11 @@ __global__ __launch_bounds__(kFB, EARLY ? NFDP_EARLY_WAVES_PER_EU : NFDP_FUSED_W
         // so the wait for the prefetched frame keeps its vmcnt(N > 0) (a store under a branch
         // would force vmcnt(0) at the loop head and expose this slot's tail)
         __builtin_amdgcn_raw_buffer_store_b32(i | (owner_of(hash, a.nranks) << 26), r_list, off, 0, 0);
+      }
+      if constexpr (V6) {   // (no prefetch in these instances: the next slot is loaded here)
+        const uint32_t nx = i + stride;
+        wave_frames_load<kStreamAux>(r_pk, run_of(base + stride), cn);
+        imn = __builtin_amdgcn_raw_buffer_load_b32(r_im, nx < n ? nx * 4u : kNoRun, 0, kStreamAux);
       }
     } else {
       if (hit && a.flow_ctr && !(a.flags & 4u)) atomicAdd(a.flow_ctr + slot, ctr_inc(st.wire_len));
@@ -694,7 +735,139 @@ size_t fused_lds_bytes(int hash_mode, int acl_mode, uint32_t acl_tiles) {
   return lds_layout(hash_mode, acl_mode, acl_tiles).total;
 }
 
-template <int H, int A, bool R, bool E = false, bool LS = false>
+// IPv6 pre-pass (v6_kernel), run before the fused kernel when the tables hold IPv6 rules or
+// IPv6 flows, so the hot kernel's register budget carries neither the 384-bit TCAM nor the
+// address check.  Per IPv6 packet it leaves one word in the batch's out_meta[i] (the fused
+// kernel reads it, then writes its egress meta there): rule + 1 in bits 0..15 (0 = no rule),
+// bit 31 = its folded FlowKey hits a flow whose side entry holds the packet's addresses
+// (flow6_verify; the fused kernel's own probe finds the same slot) - and the packet's folded
+// FlowKey in the first 16 B of its out slot (the fused kernel's key for it).
+//  * ACL: the FP4 MFMA tile of classify_wave with K = 3 x 128 over the key6 (pipeline.h
+//    key6_word), the three products chained through one accumulator (C init = bias * 4096 +
+//    rule, A scaled by 2^12: the accumulator is (mismatch << 12) | rule exactly); rule tiles
+//    stream from the global copy (L2-resident).
+//  * flow check: Toeplitz (LDS byte tables) of the folded key, the cuckoo probe, the 32-B side
+//    entry compare.
+// One packet per lane; a wave with no IPv6 packet skips all of it (wave-uniform), so an IPv4
+// batch costs one header read.
+struct V6Args {
+  TablesView t;
+  const uint4* pkts;
+  const uint32_t* inmeta;
+  uint32_t n;
+  const v4i* wfrag;    // [tiles][3][64] A fragments
+  const v4i* cinit;    // [tiles][4] C init
+  uint32_t tiles;      // 0: no IPv6 rules
+  const uint32_t* toep_tab;   // [16][256] byte tables (null: scalar Toeplitz)
+  uint32_t* res;              // the batch's out_meta: rule + 1 | verified << 31
+  uint4* keys;                // the batch's out slots: word 0..3 = the packet's folded FlowKey
+};
+
+__global__ __launch_bounds__(256) void v6_kernel(V6Args a) {
+  __shared__ uint32_t kw[4][64 * 13];   // per wave: 64 key6 rows of 12 words (+1 pad: bank spread)
+  __shared__ uint32_t ltab[16 * 256];
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  const uint32_t g = lane >> 4, col = lane & 15u;
+  uint32_t* row = kw[wv];
+  if (a.toep_tab)
+    for (uint32_t q = threadIdx.x; q < 16 * 256; q += 256) ltab[q] = a.toep_tab[q];
+  __syncthreads();
+  for (uint32_t base = blockIdx.x * 256u; base < a.n; base += gridDim.x * 256u) {   // block-uniform trips
+    const uint32_t i = base + threadIdx.x;
+    const bool valid = i < a.n;
+    uint32_t d[kSlotDwords];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const uint4 v = valid ? a.pkts[(size_t)i * 4 + q] : make_uint4(0u, 0u, 0u, 0u);
+      d[4 * q] = v.x; d[4 * q + 1] = v.y; d[4 * q + 2] = v.z; d[4 * q + 3] = v.w;
+    }
+    Parsed p;
+    IngressState st;
+    ingress_stage(a.t, d, valid ? a.inmeta[i] : 0u, p, st);
+    const bool v6 = valid && p.ipv6;
+    uint32_t word = 0;
+    if (__any(v6)) {   // wave-uniform: EXEC full from here (MFMA, cross-lane reads)
+      int rule = -1;
+      if (a.tiles) {
+#pragma unroll
+        for (int w = 0; w < 12; ++w) row[lane * 13 + w] = key6_word(p, st.bridge, w);
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        v8i_t b[3][4];
+#pragma unroll
+        for (int k = 0; k < 3; ++k)
+#pragma unroll
+          for (int tt = 0; tt < 4; ++tt) {
+            const uint32_t w = row[(16 * tt + col) * 13 + 4 * k + g];
+            b[k][tt] = v8i_t{(int)spread8_fp4(w & 0xFFu), (int)spread8_fp4((w >> 8) & 0xFFu),
+                             (int)spread8_fp4((w >> 16) & 0xFFu), (int)spread8_fp4(w >> 24), 0, 0, 0, 0};
+          }
+        uint32_t best[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+        for (uint32_t t = 0; t < a.tiles; ++t) {
+          const v4i ci = a.cinit[t * 4 + g];
+          const v4f_t c = {__int_as_float(ci[0]), __int_as_float(ci[1]), __int_as_float(ci[2]), __int_as_float(ci[3])};
+          v4f_t acc[4] = {c, c, c, c};
+#pragma unroll
+          for (int k = 0; k < 3; ++k) {
+            const v4i a4 = a.wfrag[((size_t)t * 3 + k) * 64 + lane];
+            const v8i_t av = {a4[0], a4[1], a4[2], a4[3], 0, 0, 0, 0};
+#pragma unroll
+            for (int tt = 0; tt < 4; ++tt)
+              acc[tt] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(av, b[k][tt], acc[tt], 4, 4, 0, kE8M0Idx, 0, kE8M0One);
+          }
+#pragma unroll
+          for (int tt = 0; tt < 4; ++tt)
+            best[tt] = min(best[tt], min(min(__float_as_uint(acc[tt][0]), __float_as_uint(acc[tt][1])),
+                                         min(__float_as_uint(acc[tt][2]), __float_as_uint(acc[tt][3]))));
+        }
+#pragma unroll
+        for (int tt = 0; tt < 4; ++tt) {
+          best[tt] = min(best[tt], (uint32_t)__shfl_xor(best[tt], 16));
+          best[tt] = min(best[tt], (uint32_t)__shfl_xor(best[tt], 32));
+        }
+        const uint32_t bb = pick4(g, best[0], best[1], best[2], best[3]);
+        const uint32_t bv = bb == 0xFFFFFFFFu ? bb : (uint32_t)__uint_as_float(bb);
+        const int r = acl_rule_of(bv, a.t.n_acl6);
+        rule = r >= 0 ? (int)(a.t.n_acl + (uint32_t)r) : -1;
+        __builtin_amdgcn_wave_barrier();
+      }
+      bool ok = false;
+      if (v6 && !st.reason && a.t.flow6_on) {
+        uint32_t h = 0;
+        if (a.toep_tab) {
+          const uint32_t w[4] = {st.key.src_ip, st.key.dst_ip, st.key.ports, st.key.meta};
+#pragma unroll
+          for (int q = 0; q < 16; ++q) h ^= ltab[q * 256 + ((w[q >> 2] >> (8 * (q & 3))) & 0xFFu)];
+        } else {
+          h = toeplitz_scalar(st.key, a.t.rss_key);
+        }
+        const int64_t slot = flow_lookup(a.t, st.key, h);
+        ok = slot >= 0 && flow6_verify(a.t, p, slot);
+      }
+      word = (uint32_t)(rule + 1) | (ok ? 0x80000000u : 0u);
+    }
+    if (valid) a.res[i] = v6 ? word : 0u;
+    if (v6) a.keys[i] = make_uint4(st.key.src_ip, st.key.dst_ip, st.key.ports, st.key.meta);
+  }
+}
+
+static hipError_t launch_v6(const FusedLaunch& f, int num_cus, hipStream_t s) {
+  if (!f.pkts || !f.inmeta || !f.out_meta || !f.out) return hipErrorInvalidValue;
+  if (f.t.n_acl6 && (!f.acl6_wfrag || !f.acl6_cinit || f.acl6_tiles == 0 || f.acl6_tiles > kAclMaxRules / 16 ||
+                     f.t.n_acl6 > f.acl6_tiles * 16))
+    return hipErrorInvalidValue;
+  V6Args a{f.t, reinterpret_cast<const uint4*>(f.pkts), f.inmeta, f.n, reinterpret_cast<const v4i*>(f.acl6_wfrag),
+           reinterpret_cast<const v4i*>(f.acl6_cinit), f.t.n_acl6 ? f.acl6_tiles : 0u, f.toep_tab, f.out_meta,
+           reinterpret_cast<uint4*>(f.out)};
+  uint32_t grid = (f.n + 255) / 256;
+  const uint32_t cap = (uint32_t)num_cus * 8u;
+  if (grid > cap) grid = cap;
+  if (grid == 0) return hipSuccess;
+  hipLaunchKernelGGL(v6_kernel, dim3(grid), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+template <int H, int A, bool R, bool E = false, bool LS = false, bool V6 = false>
 static hipError_t launch_fused_t(const FusedArgs& a, int num_cus, hipStream_t s) {
   // static LDS (REMOTE reservation counters) + dynamic tables must fit 160 KiB
   // rcnt[2][..] + rbase + lst_n, with room for the compiler's alignment of the static block
@@ -709,7 +882,7 @@ static hipError_t launch_fused_t(const FusedArgs& a, int num_cus, hipStream_t s)
   if (!R && (a.n >= (1u << 25) || !a.flow_ctr || !a.out_meta)) return hipErrorInvalidValue;
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&fused_kernel<H, A, R, E, LS>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&fused_kernel<H, A, R, E, LS, V6>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxDyn);
     if (e != hipSuccess) return e;
     attr_set = true;
@@ -728,7 +901,7 @@ static hipError_t launch_fused_t(const FusedArgs& a, int num_cus, hipStream_t s)
     if ((uint64_t)grid * b.steer_cap_blk > a.steer_cap_blk || grid > (uint32_t)(4 * num_cus))
       return hipErrorInvalidValue;   // (steer_cap_blk carries the list's capacity in)
   }
-  hipLaunchKernelGGL((fused_kernel<H, A, R, E, LS>), dim3(grid), dim3(kFB), lds, s, b);
+  hipLaunchKernelGGL((fused_kernel<H, A, R, E, LS, V6>), dim3(grid), dim3(kFB), lds, s, b);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || !a.side.cnt || a.side.cap_list == 0) return e;
   return launch_side(a.t, a.pkts, a.inmeta, a.out, a.out_meta, a.side, a.port_ctr, a.drop_ctr, s, a.n, false);
@@ -781,13 +954,23 @@ hipError_t launch_fused(const FusedLaunch& f, const LaunchCfg& cfg, hipStream_t 
   if (f.side.cnt && ((f.side.cap_rep && (!f.side.rep_hdr || !f.side.rep_meta || !f.side.rep_src)) ||
                      (f.side.cap_learn && !f.side.learn) || (f.side.cap_list && !f.side.list)))
     return hipErrorInvalidValue;
+  if (f.t.n_acl6 && (!f.out_meta || !f.acl6_wfrag || !f.acl6_cinit || f.acl6_tiles == 0)) return hipErrorInvalidValue;
+  const bool v6pass = f.t.n_acl6 || f.t.flow6_on;
   if (f.flags & kFlagPairs) {   // wide header pairs: resolved in place before the pipeline (pair_kernel)
     const hipError_t e = launch_pairs(const_cast<void*>(f.pkts), const_cast<uint32_t*>(f.inmeta), f.n, f.t, f.port_ctr,
                                       !(f.flags & 1u), s);
     if (e != hipSuccess) return e;
+    if (v6pass) {
+      const hipError_t e6 = launch_v6(f, cfg.num_cus, s);
+      if (e6 != hipSuccess) return e6;
+    }
     const hipError_t e2 = launch_fused_body(f, cfg, s);
     if (e2 != hipSuccess) return e2;
     return launch_pair_fix(f.inmeta, f.out_meta, f.n, f.drop_ctr, !(f.flags & 1u), s);
+  }
+  if (v6pass) {
+    const hipError_t e6 = launch_v6(f, cfg.num_cus, s);
+    if (e6 != hipSuccess) return e6;
   }
   return launch_fused_body(f, cfg, s);
 }
@@ -799,6 +982,13 @@ static hipError_t launch_fused_body(const FusedLaunch& f, const LaunchCfg& cfg, 
   const int h = cfg.hash_mode, ac = cfg.acl_mode, cu = cfg.num_cus;
   const bool early = ac == kAclMfma && !(f.flags & kFlagNoEarly) &&
                      (f.acl_tiles >= kEarlyAclTiles || (f.flags & kFlagForceEarly));
+  if (f.t.n_acl6 || f.t.flow6_on) {   // IPv6 flows / rules: the V6 instances (1 GPU, MFMA ACL)
+    if (remote || f.steer_list || ac != kAclMfma || h == kHashScalar) return hipErrorNotSupported;
+    if (h == kHashLds) return early ? launch_fused_t<kHashLds, kAclMfma, false, true, false, true>(a, cu, s)
+                                    : launch_fused_t<kHashLds, kAclMfma, false, false, false, true>(a, cu, s);
+    return early ? launch_fused_t<kHashMfma, kAclMfma, false, true, false, true>(a, cu, s)
+                 : launch_fused_t<kHashMfma, kAclMfma, false, false, false, true>(a, cu, s);
+  }
   if (f.steer_list) {   // flow-owner steering by list: the LIST instances (multi-GPU RSS)
 #define NFDP_LCASE(HH, AA)                                                                 \
     if (h == HH && ac == AA)                                                               \

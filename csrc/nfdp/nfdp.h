@@ -40,6 +40,7 @@ constexpr uint32_t kFloodMaxRows = 0x7000;   // link targets (rows) below this
 constexpr int kMaxPorts = 4094;        // vport table rows (VF / NF / wire / PR ports); 4094/4095 = meta sentinels
 constexpr int kBucketSlots = 4;        // flow-table bucket = 4 x {key, action} = one 128-B line
 constexpr uint32_t kSlotUsed = 0x100u; // occupied marker, stored in FlowKey.meta byte 1
+constexpr uint32_t kKeyV6 = 0x200u;    // FlowKey.meta: an IPv6 key (folded addresses, see make_key)
 constexpr uint16_t kPortNone = 0xFFFF; // dropped
 constexpr uint16_t kPortPunt = 0xFFFE; // to slow path (control plane upcall)
 constexpr uint32_t kPortCont = 0xFFFDu; // in-meta port of the continuation slot of a wide header pair
@@ -131,9 +132,9 @@ static_assert(sizeof(PortEntry) == 32, "PortEntry");
 
 struct alignas(16) FlowKey {     // 16 B; also the ACL / Toeplitz input (128 bits)
   uint32_t src_ip;               // raw network-order bytes (little-endian load of the header)
-  uint32_t dst_ip;
+  uint32_t dst_ip;               // (IPv6: fold6 of the four raw address words)
   uint32_t ports;                // sport (raw) | dport (raw) << 16
-  uint32_t meta;                 // proto | (zone << 16); byte 1 must be 0 in the key
+  uint32_t meta;                 // proto | (zone << 16) [| kKeyV6]; kSlotUsed never set in a packet key
 };
 static_assert(sizeof(FlowKey) == 16, "FlowKey");
 
@@ -266,6 +267,12 @@ NFDP_HD uint32_t fmix32(uint32_t h) {
   return h;
 }
 
+// IPv6 address -> one 32-bit FlowKey word (raw words, a0 = bytes 0..3).  Nested fmix32 so no
+// word enters linearly; lookups stay exact through the flow6 side array (flow6_verify).
+NFDP_HD uint32_t fold6(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3) {
+  return fmix32(a0 ^ fmix32(a1 ^ fmix32(a2 ^ fmix32(a3 ^ 0x6b43a9b5u))));
+}
+
 // Standard (Microsoft RSS) Toeplitz over the 16 key bytes in memory order, MSB-first bits.
 // `rss_key` is >= 20 bytes.  Its first 12 input bytes (src ip, dst ip, sport, dport) give the
 // standard RSS 4-tuple hash contribution; proto/zone extend it.
@@ -374,12 +381,33 @@ NFDP_HD void set_smac(uint32_t* s, uint32_t lo, uint32_t hi) {
   s[2] = (lo >> 16) | (hi << 16);
 }
 
-NFDP_HD FlowKey make_key(const Parsed& p, uint32_t zone) {
+// IPv6 (fixed header at 14..53 of the normalized view): next header at byte 20, addresses at
+// 22 / 38, TCP / UDP ports at 54 when the slot holds them.
+NFDP_HD uint32_t v6_nh(const Parsed& p) { return (p.s[5] >> 0) & 0xFFu; }
+NFDP_HD uint32_t v6_ports(const Parsed& p) {
+  const uint32_t nh = v6_nh(p);
+  return ((nh == 6u || nh == 17u) && p.len >= 58) ? raw32_at2(p.s, 54) : 0u;
+}
+
+// `v6fold`: build IPv6 keys (the tables use IPv6 features: TablesView::v6_keys); otherwise an
+// IPv6 packet keeps the IPv4-offset key (it takes no flow / ACL part then).
+NFDP_HD FlowKey make_key(const Parsed& p, uint32_t zone, bool v6fold = true) {
   FlowKey k;
   k.src_ip = raw32_at2(p.s, 26);
   k.dst_ip = raw32_at2(p.s, 30);
   k.ports = p.l4 ? raw32_at2(p.s, 34) : 0u;
   k.meta = (p.s[5] >> 24) | (zone << 16);
+#if NFDP_IPV6
+  // an IPv6 packet's key always carries kKeyV6: IPv4 rules (AclTable: kKeyV6 clear) and IPv4
+  // flows never match it
+  k.meta |= p.ipv6 ? kKeyV6 : 0u;
+  if (v6fold && p.ipv6) {
+    k.src_ip = fold6(raw32_at2(p.s, 22), raw32_at2(p.s, 26), raw32_at2(p.s, 30), raw32_at2(p.s, 34));
+    k.dst_ip = fold6(raw32_at2(p.s, 38), raw32_at2(p.s, 42), raw32_at2(p.s, 46), raw32_at2(p.s, 50));
+    k.ports = v6_ports(p);
+    k.meta = v6_nh(p) | kKeyV6 | (zone << 16);
+  }
+#endif
   return k;
 }
 
@@ -573,6 +601,17 @@ struct TablesView {
   uint32_t lpm6_mask;
   const uint8_t* lpm6_lens;      // n_lpm6_lens lengths, descending
   uint32_t n_lpm6_lens;
+  // IPv6 flows: the flow-table buffer carries, after its nbuckets * 128 B of buckets, a side
+  // array of the same geometry holding each slot's full IPv6 addresses (2 x 16 B: src, dst raw
+  // words).  An IPv6 packet probes the folded key (make_key) and a hit counts only when the side
+  // entry equals the packet's addresses (flow6_verify), so every flow-table copy (the ring's
+  // double buffer) carries its own side array and a lookup is exact.
+  uint32_t flow6_on;
+  // IPv6 ACL (TCAM over the 384-bit key6: src6, dst6, ports, proto | zone << 16, 0, 0): rules in
+  // priority order, their verdicts at acl_permit[n_acl + j] (one rule index space).
+  const uint32_t* acl6_value;    // n_acl6 * 12
+  const uint32_t* acl6_mask;     // n_acl6 * 12
+  uint32_t n_acl6;
 };
 
 NFDP_HD uint32_t lpm_lookup(const TablesView& t, uint32_t dst /* host order */) {
@@ -715,6 +754,38 @@ NFDP_HD int acl_first_match(const TablesView& t, const FlowKey& k) {
     bool m = true;
     for (int i = 0; i < 4; ++i) m = m && ((w[i] ^ t.acl_value[4 * r + i]) & t.acl_mask[4 * r + i]) == 0;
     if (m) return (int)r;
+  }
+  return -1;
+}
+
+// IPv6 flows (TablesView::flow6_on): the side entry of flow slot `slot`.
+NFDP_HD const uint32_t* flow6_side(const TablesView& t, int64_t slot) {
+  return reinterpret_cast<const uint32_t*>(t.flows + (size_t)(t.bucket_mask + 1u) * kBucketSlots) + (size_t)slot * 8;
+}
+// Exact check of an IPv6 packet's folded-key hit: the slot's side entry holds its addresses.
+NFDP_HD bool flow6_verify(const TablesView& t, const Parsed& p, int64_t slot) {
+  const uint32_t* e = flow6_side(t, slot);
+  bool ok = true;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) ok = ok && e[k] == raw32_at2(p.s, 22 + 4 * k);
+  return ok;
+}
+
+// The 12-word IPv6 ACL key: src6 (4 raw words), dst6 (4), ports, next header | zone << 16, 0, 0.
+NFDP_HD uint32_t key6_word(const Parsed& p, uint32_t zone, int w) {
+  return w < 8 ? raw32_at2(p.s, 22 + 4 * w) : (w == 8 ? v6_ports(p) : (w == 9 ? (v6_nh(p) | (zone << 16)) : 0u));
+}
+// Scalar IPv6 ACL (priority order, first match) -> index in the shared verdict space (n_acl + j)
+// or -1.
+NFDP_HD int acl6_first_match(const TablesView& t, const Parsed& p, uint32_t zone) {
+  uint32_t kw[12];   // constant indices only (unrolled): stays in registers on the GPU
+#pragma unroll
+  for (int i = 0; i < 12; ++i) kw[i] = key6_word(p, zone, i);
+  for (uint32_t r = 0; r < t.n_acl6; ++r) {
+    uint32_t x = 0;
+#pragma unroll
+    for (int i = 0; i < 12; ++i) x |= (kw[i] ^ t.acl6_value[12 * r + i]) & t.acl6_mask[12 * r + i];
+    if (!x) return (int)(t.n_acl + r);
   }
   return -1;
 }

@@ -34,7 +34,12 @@ struct DirectTables {
   NFDP_HD bool permit(int rule) const { return rule >= 0 ? t.acl_permit[rule] != 0 : t.acl_default_permit != 0; }
 };
 
-template <class TA>
+// IPv6 flow / ACL features in use: IPv6 packets get folded 5-tuple keys (make_key).
+NFDP_HD bool v6_keys(const TablesView& t) { return t.flow6_on || t.n_acl6; }
+
+// FOLD6 false: the caller fills IPv6 keys itself (the fused kernel takes them from v6_kernel, so
+// the fold's registers stay out of its budget).
+template <class TA, bool FOLD6 = true>
 NFDP_HD void ingress_stage(const TablesView& t, const TA& ta, const uint32_t* d, uint32_t inmeta, Parsed& p,
                            IngressState& st) {
   st.in_port = inmeta & 0xFFFFu;
@@ -61,10 +66,24 @@ NFDP_HD void ingress_stage(const TablesView& t, const TA& ta, const uint32_t* d,
       st.reason = st.reason ? st.reason : kSpoof;
     st.bridge = ((pe.flags & kPortVlanBridge) && p.tagged) ? vid : pe.bridge_id;
   }
-  st.key = make_key(p, st.bridge);
+  st.key = make_key(p, st.bridge, FOLD6 && v6_keys(t));
 }
 NFDP_HD void ingress_stage(const TablesView& t, const uint32_t* d, uint32_t inmeta, Parsed& p, IngressState& st) {
   ingress_stage(t, DirectTables{t}, d, inmeta, p, st);
+}
+
+// A packet that takes part in the exact-match flow stage: IPv4, or IPv6 when the flow table
+// carries the IPv6 side array (its folded-key hits are verified against it: flow6_verify).
+NFDP_HD bool flowable(const TablesView& t, const Parsed& p) { return p.ipv4 || (NFDP_IPV6 && p.ipv6 && t.flow6_on); }
+// The ACL rule of a packet.  With IPv6 features in the tables (v6_keys), an IPv6 packet's rule
+// comes from the IPv6 rules (acl6), never from the IPv4 TCAM over the folded key; without them
+// its key (kKeyV6 set) goes through the IPv4 TCAM like any other, where AclTable's rules (which
+// require kKeyV6 clear) never match it.
+NFDP_HD int acl_rule_v6(const TablesView& t, const Parsed& p, const IngressState& st) {
+  return t.n_acl6 ? acl6_first_match(t, p, st.bridge) : -1;
+}
+NFDP_HD int acl_rule_scalar(const TablesView& t, const Parsed& p, const IngressState& st) {
+  return (p.ipv6 && v6_keys(t)) ? acl_rule_v6(t, p, st) : acl_first_match(t, st.key);
 }
 
 // ---- Wide header pairs: single-pass tunnel termination ----
@@ -233,7 +252,7 @@ NFDP_HD void vm_mac_map(const TablesView& t, Parsed& p) {
 // IPv6 routing (P4 ipv6_table): LPM on the destination, hop limit - 1 (no header checksum in
 // IPv6), neighbour / router MACs, egress port.  ECMP members are picked by a hash of the IPv6
 // addresses and ports (the packet's Toeplitz hash covers IPv4 fields only).  Returns a drop
-// reason (0 = routed).  Only the routed-interface miss path calls it (IPv6 never hits a flow).
+// reason (0 = routed).  Only the routed-interface miss path calls it (an IPv6 flow hit takes the chain).
 NFDP_HD uint32_t route_ipv6(const TablesView& t, Parsed& p, uint32_t& out_port) {
   const uint32_t d0 = __builtin_bswap32(raw32_at2(p.s, 38)), d1 = __builtin_bswap32(raw32_at2(p.s, 42));
   const uint32_t d2 = __builtin_bswap32(raw32_at2(p.s, 46)), d3 = __builtin_bswap32(raw32_at2(p.s, 50));

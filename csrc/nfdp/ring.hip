@@ -144,7 +144,10 @@ __device__ __forceinline__ bool ring_wait_chunk(const RingArgs& a, uint32_t lane
 // all 4 waves parse the chunk and each scans a quarter of the ACL rule tiles on its own SIMD
 // (the single-wave MFMA chain is the longest stage of a chunk), wave 0 combines the partial
 // first-match minima through LDS and finishes the chunk.
-template <int HASH, int ACL, bool COOP>
+// V6: instances for tables with IPv6 flows / rules (the IPv6 key fold, the IPv6 TCAM and the
+// address check inline); the others keep the IPv4 path's register budget (an IPv6 packet's key
+// carries kKeyV6 there and takes no flow / ACL part).
+template <int HASH, int ACL, bool COOP, bool V6 = false>
 __global__ __launch_bounds__(kRingBlock) void ring_kernel(RingArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ unsigned long long coop_tk;                      // ticket
@@ -299,7 +302,7 @@ __global__ __launch_bounds__(kRingBlock) void ring_kernel(RingArgs a) {
     NFDP_RING_MARK(tr0)
     Parsed p;
     IngressState st;
-    ingress_stage(T, ta, d, im, p, st);
+    ingress_stage<LdsTables, V6>(T, ta, d, im, p, st);
     uint32_t hash = 0;
     int acl_rule = -1;
     if constexpr (COOP && ACL == kAclMfma) {
@@ -314,15 +317,22 @@ __global__ __launch_bounds__(kRingBlock) void ring_kernel(RingArgs a) {
       if (COOP && wave != 0) continue;  // nothing to share without the MFMA ACL
       classify_wave<HASH, ACL>(st.key, kx, av, lt, ltab, T, hash, acl_rule);
     }
+    // IPv6: the IPv6 TCAM (scalar here: the ring keeps its register budget for the IPv4 path)
+    if constexpr (V6) {
+      if (__builtin_expect(__any(p.ipv6 && v6_keys(T)), 0)) {
+        if (p.ipv6 && v6_keys(T)) acl_rule = acl_rule_v6(T, p, st);
+      }
+    }
     NFDP_RING_MARK(tr1)
     bool hit = false;
     FlowAction act = {};
     int64_t slot = -1;
-    if (!st.reason && p.ipv4) {
+    if (!st.reason && (V6 ? flowable(T, p) : p.ipv4)) {
       uint4 v;
       TablesView tv = T;
-      tv.flows = static_cast<const FlowSlot*>(a.flows2[epoch & 1u]);
+      tv.flows = static_cast<const FlowSlot*>(a.flows2[epoch & 1u]);   // (its IPv6 side array follows it)
       slot = flow_probe(tv, st.key, hash, v);
+      if (V6 && slot >= 0 && p.ipv6 && !flow6_verify(tv, p, slot)) slot = -1;
       if (slot >= 0) {
         hit = true;
         act.chain_id = v.x & 0xFFFFu; act.out_port = v.x >> 16; act.nat_ip = v.y;
@@ -388,16 +398,16 @@ __global__ __launch_bounds__(kRingBlock) void ring_kernel(RingArgs a) {
   on_idle();  // exit: whatever this wave counted since its last flush reaches the global table
 }
 
-template <int H, int A, bool C>
+template <int H, int A, bool C, bool V6 = false>
 static hipError_t launch_ring_t(const RingArgs& a, int num_cus, int wgs, hipStream_t s) {
   const size_t lds = ring_lds(H, A, C ? a.lds_tiles : a.acl_tiles).total;
   if (lds > 64 * 1024) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&ring_kernel<H, A, C>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&ring_kernel<H, A, C, V6>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
   if ((lds + 2048) * (size_t)wgs > 160 * 1024) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((ring_kernel<H, A, C>), dim3((uint32_t)(num_cus * wgs)), dim3(kRingBlock), lds, s, a);
+  hipLaunchKernelGGL((ring_kernel<H, A, C, V6>), dim3((uint32_t)(num_cus * wgs)), dim3(kRingBlock), lds, s, a);
   return hipGetLastError();
 }
 
@@ -433,6 +443,13 @@ hipError_t launch_ring(const RingLaunch& r, const LaunchCfg& cfg, int wgs_per_cu
   if (cfg.hash_mode == kHashLds && !a.toep_tab) return hipErrorInvalidValue;
   if (wgs_per_cu < 1 || wgs_per_cu > 8 || cfg.num_cus < 1) return hipErrorInvalidValue;
   const int h = cfg.hash_mode, ac = cfg.acl_mode;
+  if (v6_keys(a.t)) {   // IPv6 flows / rules: the V6 instances (LDS or MFMA hash, MFMA ACL)
+    if (ac != kAclMfma || h == kHashScalar) return hipErrorNotSupported;
+    if (h == kHashLds) return coop ? launch_ring_t<kHashLds, kAclMfma, true, true>(a, cfg.num_cus, wgs_per_cu, s)
+                                   : launch_ring_t<kHashLds, kAclMfma, false, true>(a, cfg.num_cus, wgs_per_cu, s);
+    return coop ? launch_ring_t<kHashMfma, kAclMfma, true, true>(a, cfg.num_cus, wgs_per_cu, s)
+                : launch_ring_t<kHashMfma, kAclMfma, false, true>(a, cfg.num_cus, wgs_per_cu, s);
+  }
 #define NFDP_RCASE(HH, AA)                                                                   \
   if (h == HH && ac == AA)                                                                   \
     return coop ? launch_ring_t<HH, AA, true>(a, cfg.num_cus, wgs_per_cu, s)                 \

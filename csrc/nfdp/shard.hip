@@ -72,6 +72,11 @@ __global__ __launch_bounds__(kBlock) void ingress_kernel(IngressArgs a) {
     uint32_t hash = 0;
     int acl = -1;
     classify_wave<HASH, ACL>(st.key, kx, av, lt, ltab, a.t, hash, acl);
+    if (__builtin_expect(__any(p.ipv6 && v6_keys(a.t)), 0)) {
+      if (p.ipv6) acl = acl_rule_v6(a.t, p, st);
+    }
+    // (IPv6 flows need the packet's addresses at the probe (flow6_verify): the owner here sees
+    // only the 16-B key, so the sharded path keeps IPv6 on L2 / L3 - its launcher clears flow6_on)
     const bool need = valid && !st.reason && p.ipv4;
     const uint32_t owner = owner_of(hash, a.g.nranks);
     const uint32_t pos = reserve_block(a.cnt, owner, need, a.g.nranks, rcnt, rbase);

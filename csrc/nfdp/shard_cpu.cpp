@@ -17,7 +17,7 @@ void ingress_cpu(const IngressArgs& a) {
     IngressState st;
     ingress_stage(a.t, d, a.inmeta[i], p, st);
     const uint32_t h = toeplitz_scalar(st.key, a.t.rss_key);
-    const int acl = acl_first_match(a.t, st.key);
+    const int acl = acl_rule_scalar(a.t, p, st);
     uint32_t ref = kRefNone;
     if (!st.reason && p.ipv4) {
       const uint32_t owner = owner_of(h, a.g.nranks);

@@ -79,6 +79,11 @@ class DataPlane:
         self._ipsec = None               # ESP engine (dataplane/ipsec.py), created on first use
         self.acl = T.AclTable()
         self.flows = T.FlowTable(flow_buckets, rss_key)
+        # IPv6 flows: folded FlowKey -> the 8 raw address words of its side entry (TablesView
+        # flow6_on: the device flow buffer carries the side array after the buckets)
+        self.flows6: dict[tuple, np.ndarray] = {}
+        self._flow6_on = False
+        self._flow6_full = False
         self.rss_key = rss_key
         self.hash_mode = HASH_MODES[hash_mode]
         self.acl_mode = ACL_MODES[acl_mode]
@@ -167,7 +172,8 @@ class DataPlane:
             if rings and not full and self._only_flows_pending():
                 with TRACER.span("dataplane.commit_live"):
                     return self._commit_flows_live(rings)
-            if rings and not full and all(getattr(r, "coop", False) for r in rings) and "flows_b" in self._dev:
+            if (rings and not full and all(getattr(r, "coop", False) for r in rings) and "flows_b" in self._dev
+                    and not self._flow6_full and all(getattr(r, "v6", False) == self._v6_keys() for r in rings)):
                 with TRACER.span("dataplane.commit_tables_live"):
                     return self._commit_tables_live(rings)
             for r in rings:
@@ -194,6 +200,8 @@ class DataPlane:
         """True when the device is current in everything but (possibly) flow buckets."""
         if "flows" not in self._dev or "rss_key" not in self._dev or "acl_value" not in self._dev:
             return False
+        if self._flow6_full:   # the flow buffer grows its IPv6 side array: a full upload
+            return False
         if any(self._versions.get(n) != m.version or n not in self._dev for n, m in self._models()):
             return False
         if len(self.routes) and (self._versions.get("routes") != self.routes.version or "lpm24" not in self._dev):
@@ -201,6 +209,54 @@ class DataPlane:
         if len(self.routes6) and (self._versions.get("routes6") != self.routes6.version or "lpm6" not in self._dev):
             return False
         return self._versions.get("acl") == self.acl.version
+
+    # ------------------------------------------------------------------ IPv6 flows
+    def _v6_keys(self) -> bool:
+        """IPv6 flows / rules in the tables (after the pending commit): IPv6-capable kernels."""
+        return bool(self._flow6_on or self.acl.rules6)
+
+    def add_flow6(self, src, dst, sport: int = 0, dport: int = 0, proto: int = 17, zone: int = 0,
+                  action=None) -> int:
+        """Install an IPv6 5-tuple flow (pushed by the next commit).  The table holds its folded
+        key (tables.flow_key6); the side entry of its slot holds the addresses, which the data
+        plane compares on every hit (nfdp.h flow6_verify), so lookups are exact.  Two 5-tuples
+        with one folded key cannot both be installed (ValueError)."""
+        key, addrs = T.flow_key6(src, dst, sport, dport, proto, zone)
+        k = tuple(int(x) for x in key)
+        old = self.flows6.get(k)
+        if old is not None and not np.array_equal(old, addrs):
+            raise ValueError("IPv6 flow key collision: the folded key belongs to another 5-tuple")
+        slot = self.flows.insert(key, action if action is not None else T.flow_action()[0])
+        self.flows6[k] = addrs
+        if not self._flow6_on:
+            self._flow6_on = True
+            self._flow6_full = True
+        return slot
+
+    def remove_flow6(self, src, dst, sport: int = 0, dport: int = 0, proto: int = 17, zone: int = 0) -> bool:
+        key, _ = T.flow_key6(src, dst, sport, dport, proto, zone)
+        self.flows6.pop(tuple(int(x) for x in key), None)
+        return self.flows.erase(key)
+
+    def _side6_rows(self, buckets: np.ndarray, slots: np.ndarray | None = None) -> np.ndarray:
+        """IPv6 side rows (uint32 [len(buckets), 32]: 4 slots x {src6, dst6}) of these buckets."""
+        sl = (slots if slots is not None else self.flows.t.slots()).reshape(-1, 32)[buckets].reshape(-1, 4, 8)
+        out = np.zeros((len(buckets), 4, 8), np.uint32)
+        meta = sl[:, :, 3]
+        for b, j in zip(*np.nonzero((meta & np.uint32(T.KEY_V6 | T.SLOT_USED)) == np.uint32(T.KEY_V6 | T.SLOT_USED))):
+            k = (int(sl[b, j, 0]), int(sl[b, j, 1]), int(sl[b, j, 2]), int(meta[b, j]) & ~T.SLOT_USED)
+            a = self.flows6.get(k)
+            if a is not None:
+                out[b, j] = a
+        return out.reshape(-1, 32)
+
+    def _flow_image(self) -> np.ndarray:
+        """The device flow buffer: the buckets, then (IPv6 flows on) their side rows."""
+        slots = self.flows.t.slots()
+        if not self._flow6_on:
+            return slots
+        side = self._side6_rows(np.arange(self.flows.nbuckets), slots)
+        return np.concatenate([slots.reshape(-1), side.reshape(-1)])
 
     # ------------------------------------------------------------------ live flow updates
     # Double-buffered flow table: copy 0 = "flows", copy 1 = "flows_b"; tables_ptrs() and the
@@ -320,16 +376,31 @@ class DataPlane:
             self._buf("acl_cinit", c)
             self._acl_tiles = int(tiles)
             self._n_acl = n
+            # IPv6 rules: their verdicts follow the IPv4 ones (one rule index space), MFMA tiles
+            # for v6_kernel, value / mask for the scalar paths
+            v6, m6, p6, n6 = self.acl.arrays6()
+            self._n_acl6 = n6
+            if n6:
+                self._buf("acl_permit", np.concatenate([per[: max(n, 1)] if n else np.zeros(0, np.uint8), p6[:n6]]))
+                self._buf("acl6_value", v6[:n6])
+                self._buf("acl6_mask", m6[:n6])
+                w6, c6, t6 = self.nf.build_acl6_frags(v6[:n6], m6[:n6])
+                self._buf("acl6_wfrag", w6)
+                self._buf("acl6_cinit", c6)
+                self._acl6_tiles = int(t6)
             self._versions["acl"] = self.acl.version
             sent["acl"] = n
         ft = self.flows.t
-        if full or "flows" not in self._dev:
+        if full or "flows" not in self._dev or self._flow6_full:
             self.harvest()
-            self._buf("flows", ft.slots())
+            img = self._flow_image()
+            self._buf("flows", img)
             if "flows_b" in self._dev:   # both copies current: nothing lags
-                self._buf("flows_b", ft.slots())
+                self._buf("flows_b", img)
                 self._flow_lag = np.zeros(0, np.int64)
             ft.clear_dirty()
+            ft.take_moves()
+            self._flow6_full = False
             sent["flows_full"] = len(self.flows)
         else:
             dirty = ft.take_dirty()
@@ -346,17 +417,25 @@ class DataPlane:
 
     def _push_buckets(self, dirty: np.ndarray, dst: str = "flows") -> None:
         ft = self.flows.t
-        rows = ft.slots().reshape(-1, 32)[dirty]   # whole 128-B buckets
+        slots = ft.slots()
+        rows = slots.reshape(-1, 32)[dirty]   # whole 128-B buckets
+        idx, mask = dirty.astype(np.uint32), ft.mask
+        if self._flow6_on:
+            # the side rows of the same buckets follow (rows nbuckets + b of the 2x buffer)
+            nb = self.flows.nbuckets
+            rows = np.concatenate([rows, self._side6_rows(dirty, slots)])
+            idx = np.concatenate([idx, idx + np.uint32(nb)])
+            mask = 2 * nb - 1
         if self.gpu:
             torch = _torch()
             up = {k: torch.from_numpy(np.ascontiguousarray(v).view(np.uint8).reshape(-1).copy()).to(self.tdev)
-                  for k, v in (("idx", dirty.astype(np.uint32)), ("rows", rows))}
+                  for k, v in (("idx", idx), ("rows", rows))}
             s = torch.cuda.current_stream(self.tdev).cuda_stream
-            self.nf.launch_bucket_update(up["idx"].data_ptr(), len(dirty), up["rows"].data_ptr(), self._ptr(dst),
-                                         ft.mask, s)
+            self.nf.launch_bucket_update(up["idx"].data_ptr(), len(idx), up["rows"].data_ptr(), self._ptr(dst),
+                                         mask, s)
             self._keepalive = up
         else:
-            self._dev[dst].view(np.uint32).reshape(-1, 32)[dirty] = rows
+            self._dev[dst].view(np.uint32).reshape(-1, 32)[idx] = rows
 
     def tables_ptrs(self) -> dict:
         return {
@@ -383,6 +462,13 @@ class DataPlane:
             "vtep6_fold": int(self.nf.vtep6_fold(*(int(x) for x in self.vtep6.a))) if self.vtep6.active else 0,
             "vtep6": [int(x) for x in self.vtep6.a],
             "terms6": self._ptr("terms6") if len(self.terms6) else 0, "term6_mask": int(self.terms6.mask),
+            "flow6_on": 1 if self._flow6_on and not self._flow6_full else 0,
+            "n_acl6": int(getattr(self, "_n_acl6", 0)),
+            "acl6_value": self._ptr("acl6_value") if getattr(self, "_n_acl6", 0) else 0,
+            "acl6_mask": self._ptr("acl6_mask") if getattr(self, "_n_acl6", 0) else 0,
+            "acl6_wfrag": self._ptr("acl6_wfrag") if getattr(self, "_n_acl6", 0) else 0,
+            "acl6_cinit": self._ptr("acl6_cinit") if getattr(self, "_n_acl6", 0) else 0,
+            "acl6_tiles": int(getattr(self, "_acl6_tiles", 0)) if getattr(self, "_n_acl6", 0) else 0,
         }
 
     def pairs_possible(self) -> bool:

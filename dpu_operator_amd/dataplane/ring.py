@@ -115,6 +115,8 @@ class RingPath:
     def _tables(self) -> dict:
         t = self.dp.tables_ptrs()
         t["flows"], t["flows_alt"] = self.dp.flow_copy_ptrs()   # copies by epoch parity
+        # the kernel instance depends on it (ring.hip V6): a live table flip keeps it
+        self.v6 = bool(t["flow6_on"] or t["n_acl6"])
         return t
 
     def start(self) -> None:

@@ -375,3 +375,73 @@ def install_l3_routes(dp, sc: Scenario, n_background: int = 100_000, seed: int =
         added += 1
     dp.chains.set(sc.chain_id, ["acl", "nat", "route"])
     return {"pod_routes": sc.n_pods, "ecmp_ways": 8, "background_prefixes": added, "nexthops": nh + 1}
+
+
+# ---- dual stack: IPv6 pod flows next to the IPv4 SFC (bench value_ipv6) ----
+POD6_NET = 0xFD00_0000_0000_0000_0000_0000_0A80_0000   # fd00::10.128.0.0/112-style pod addresses
+
+
+def install_ipv6(dp, sc: Scenario, n_flows: int = 1 << 16, n_rules: int = 64, seed: int = 17) -> dict:
+    """IPv6 flows between the scenario's pods (same chain: the NAT hop leaves IPv6 alone) and an
+    IPv6 ACL of `n_rules` rules: /48 denies of unused fd01:: prefixes and dport denies, then a
+    pod-network permit.  Vectorized: folded keys via tables.fold6's numpy twin, one insert_many.
+    Returns the flows (for traffic_ipv6)."""
+    rng = np.random.default_rng(seed)
+    src = rng.integers(0, sc.n_pods, n_flows)
+    dst = (src + rng.integers(1, max(sc.n_pods, 2), n_flows)) % sc.n_pods
+    sport = rng.integers(1024, 65536, n_flows)
+    dport = rng.integers(1024, 65536, n_flows)
+    # addresses: POD6_NET + pod, unique per pod; words are the raw little-endian loads
+    w_src = np.stack([T.ip6_raw(POD6_NET + int(p)) for p in range(sc.n_pods)])[src]
+    w_dst = np.stack([T.ip6_raw(POD6_NET + int(p)) for p in range(sc.n_pods)])[dst]
+
+    def fold(w):
+        h = T.fmix32(w[:, 3] ^ np.uint32(0x6B43A9B5))
+        for k in (2, 1, 0):
+            h = T.fmix32(w[:, k] ^ h)
+        return h
+
+    keys = np.zeros((n_flows, 4), np.uint32)
+    keys[:, 0], keys[:, 1] = fold(w_src), fold(w_dst)
+    keys[:, 2] = P.port_raw(sport) | (P.port_raw(dport) << np.uint32(16))
+    keys[:, 3] = 17 | T.KEY_V6 | (sc.bridge << 16)
+    _, uniq = np.unique(keys.view(np.dtype((np.void, 16))), return_index=True)
+    keep = np.sort(uniq)
+    keys, src, dst, sport, dport = keys[keep], src[keep], dst[keep], sport[keep], dport[keep]
+    w_src, w_dst = w_src[keep], w_dst[keep]
+    actions = T.flow_action(chain_id=sc.chain_id, out_port=sc.pod_port[dst], flow_id=np.arange(len(keys)))
+    dp.flows.insert_many(keys, actions)
+    addrs = np.concatenate([w_src, w_dst], axis=1).astype(np.uint32)
+    for k, a in zip(map(tuple, keys.tolist()), addrs):
+        dp.flows6[k] = a
+    if not dp._flow6_on:
+        dp._flow6_on = True
+        dp._flow6_full = True
+    for r in range(max(n_rules - 1, 0)):
+        if r % 8 == 7:
+            dp.acl.add(permit=False, dport=int(rng.integers(1, 1024)), proto=17, family=6)
+        else:
+            dp.acl.add(permit=False, dst=f"fd01:{r:x}::/48", dport=int(1000 + r))
+    if n_rules:
+        dp.acl.add(permit=True, src="fd00::/96")
+    return {"src": src, "dst": dst, "sport": sport, "dport": dport, "flows": len(keys), "rules": n_rules}
+
+
+def traffic_ipv6(sc: Scenario, info: dict, n: int, seed: int = 1, frame_len: int = 62) -> tuple[np.ndarray, np.ndarray]:
+    """n tagged IPv6 / UDP frames of random installed IPv6 flows from the source pod's VF
+    (frame_len: untagged, no FCS; 62 = the smallest IPv6 / UDP frame).  (slots, inmeta)."""
+    rng = np.random.default_rng(seed)
+    f = rng.integers(0, len(info["src"]), n)
+    s, d = info["src"][f], info["dst"][f]
+    smac = np.frombuffer(b"".join(pod_mac(int(i)) for i in range(sc.n_pods)), np.uint8).reshape(-1, 6)[s]
+    fr, ln = P.craft6_full(n, dmac=GW_MAC, smac=smac, src6=[POD6_NET + int(x) for x in s],
+                           dst6=[POD6_NET + int(x) for x in d], sport=info["sport"][f], dport=info["dport"][f],
+                           frame_len=frame_len, payload_seed=seed)
+    tagged = np.zeros((n, frame_len + 4), np.uint8)
+    tagged[:, :12] = fr[:, :12]
+    tagged[:, 12], tagged[:, 13] = 0x81, 0x00
+    vid = (s % 4094) + 2
+    tagged[:, 14], tagged[:, 15] = (vid >> 8) & 0xFF, vid & 0xFF
+    tagged[:, 16:] = fr[:, 12:]
+    lens = ln + 4
+    return P.header_slots(tagged, lens), P.inmeta(sc.pod_port[s], lens)

@@ -136,6 +136,33 @@ def flow_key(src_ip, dst_ip, sport=0, dport=0, proto=17, zone=0) -> np.ndarray:
     return k
 
 
+KEY_V6 = 0x200   # FlowKey.meta bit of an IPv6 key (nfdp.h kKeyV6)
+SLOT_USED = 0x100
+
+
+def fold6(words) -> int:
+    """nfdp.h fold6: the four raw words of an IPv6 address -> one FlowKey word."""
+    w = [np.uint32(x) for x in words]
+    with np.errstate(over="ignore"):
+        h = fmix32(w[3] ^ np.uint32(0x6B43A9B5))
+        h = fmix32(w[2] ^ h)
+        h = fmix32(w[1] ^ h)
+        h = fmix32(w[0] ^ h)
+    return int(h)
+
+
+def flow_key6(src, dst, sport=0, dport=0, proto=17, zone=0) -> tuple[np.ndarray, np.ndarray]:
+    """IPv6 5-tuple -> (the folded FlowKey uint32[4] the data plane probes, the 8 raw address
+    words of its side entry).  Ports count for TCP / UDP only (nfdp.h v6_ports)."""
+    s6, d6 = ip6_raw(src), ip6_raw(dst)
+    ports = 0
+    if proto in (6, 17):
+        ports = int(port_raw(np.uint32(sport))) | (int(port_raw(np.uint32(dport))) << 16)
+    meta = (proto & 0xFF) | KEY_V6 | ((zone & 0xFFFF) << 16)
+    key = np.array([fold6(s6), fold6(d6), ports, meta], np.uint32)
+    return key, np.concatenate([s6, d6]).astype(np.uint32)
+
+
 def flow_action(chain_id=0, out_port=0, nat_ip=0, nat_port=0, vlan=0, flow_id=0) -> np.ndarray:
     """Vectorized FlowAction -> uint32[n,4] (nat ip/port host order in)."""
     w0 = (np.asarray(chain_id, np.uint32) & 0xFFFF) | ((np.asarray(out_port, np.uint32) & 0xFFFF) << np.uint32(16))
@@ -897,20 +924,82 @@ class AclTable:
 
     def __init__(self, default_permit: bool = True):
         self.rules: list[AclRule] = []
+        self.rules6: list[AclRule] = []   # IPv6 rules (their own priority order)
         self.default_permit = default_permit
         self.version = 0
 
     def add_raw(self, value, mask, permit: bool) -> int:
+        """An IPv4 rule over the FlowKey words.  The rule also requires kKeyV6 clear, so it never
+        matches an IPv6 packet's key."""
         if len(self.rules) >= self.MAX_RULES:
             raise RuntimeError(f"ACL full ({self.MAX_RULES} rules)")
-        v = np.asarray(value, np.uint32) & np.asarray(mask, np.uint32)
-        self.rules.append(AclRule(v, np.asarray(mask, np.uint32), bool(permit)))
+        m = np.asarray(mask, np.uint32).copy()
+        m[3] |= np.uint32(KEY_V6)
+        v = np.asarray(value, np.uint32) & m
+        self.rules.append(AclRule(v, m, bool(permit)))
         self.version += 1
         return len(self.rules) - 1
 
-    def add(self, *, permit: bool, src=None, dst=None, sport=None, dport=None, proto=None, zone=None) -> list[int]:
+    def add_raw6(self, value, mask, permit: bool) -> int:
+        """An IPv6 rule over the 12 key6 words (nfdp.h key6_word: src6, dst6, ports, next header
+        | zone << 16, 0, 0).  Returns its index among the IPv6 rules."""
+        if len(self.rules6) >= self.MAX_RULES:
+            raise RuntimeError(f"IPv6 ACL full ({self.MAX_RULES} rules)")
+        m = np.asarray(mask, np.uint32)
+        v = np.asarray(value, np.uint32) & m
+        if v.shape != (12,):
+            raise ValueError("IPv6 rule value / mask are 12 words")
+        self.rules6.append(AclRule(v, m.copy(), bool(permit)))
+        self.version += 1
+        return len(self.rules6) - 1
+
+    @staticmethod
+    def _family(cidr):
+        return None if cidr is None else ipaddress.ip_network(cidr, strict=False).version
+
+    def add(self, *, permit: bool, src=None, dst=None, sport=None, dport=None, proto=None, zone=None,
+            family=None) -> list[int]:
         """Add a rule from fields; CIDRs for src/dst, int or (lo, hi) ranges for ports.
-        Port ranges expand to several ternary entries (returned indices)."""
+        Port ranges expand to several ternary entries (returned indices).  IPv6 CIDRs make an
+        IPv6 rule (indices among the IPv6 rules).  A rule with no address is an IPv4 rule, or
+        with `family` 6 an IPv6 one, or with family "any" one of each (the IPv4 indices are
+        returned).  (IPv6 rules switch the data plane to its IPv6-capable kernel instances.)"""
+        fams = {f for f in (self._family(src), self._family(dst)) if f}
+        if len(fams) > 1:
+            raise ValueError("src and dst CIDRs must be the same address family")
+        fam = fams.pop() if fams else {None: 4, 4: 4, 6: 6, "any": None}[family]
+
+        def prefixes(p):
+            if p is None:
+                return [(0, 0)]
+            if isinstance(p, tuple):
+                return range_to_prefixes(p[0], p[1])
+            return [(int(p), 0xFFFF)]
+
+        if fam in (None, 6):
+            v6 = np.zeros(12, np.uint32)
+            m6 = np.zeros(12, np.uint32)
+            for base, cidr in ((0, src), (4, dst)):
+                if cidr is None:
+                    continue
+                net = ipaddress.IPv6Network(cidr, strict=False)
+                v6[base:base + 4] = ip6_raw(int(net.network_address))
+                m6[base:base + 4] = ip6_raw(int(net.netmask))
+            if proto is not None:
+                v6[9] |= np.uint32(proto & 0xFF)
+                m6[9] |= np.uint32(0xFF)
+            if zone is not None:
+                v6[9] |= np.uint32((zone & 0xFFFF) << 16)
+                m6[9] |= np.uint32(0xFFFF0000)
+            idx6 = []
+            for sv, sm in prefixes(sport):
+                for dv, dm in prefixes(dport):
+                    v, m = v6.copy(), m6.copy()
+                    v[8] = port_raw(np.uint32(sv)) | (port_raw(np.uint32(dv)) << np.uint32(16))
+                    m[8] = port_raw(np.uint32(sm)) | (port_raw(np.uint32(dm)) << np.uint32(16))
+                    idx6.append(self.add_raw6(v, m, permit))
+            if fam == 6:
+                return idx6
         base_v = np.zeros(4, np.uint32)
         base_m = np.zeros(4, np.uint32)
         for word, cidr in ((0, src), (1, dst)):
@@ -926,13 +1015,6 @@ class AclTable:
             base_v[3] |= np.uint32((zone & 0xFFFF) << 16)
             base_m[3] |= np.uint32(0xFFFF0000)
 
-        def prefixes(p):
-            if p is None:
-                return [(0, 0)]
-            if isinstance(p, tuple):
-                return range_to_prefixes(p[0], p[1])
-            return [(int(p), 0xFFFF)]
-
         idx = []
         for sv, sm in prefixes(sport):
             for dv, dm in prefixes(dport):
@@ -941,6 +1023,16 @@ class AclTable:
                 m[2] = port_raw(np.uint32(sm)) | (port_raw(np.uint32(dm)) << np.uint32(16))
                 idx.append(self.add_raw(v, m, permit))
         return idx
+
+    def arrays6(self):
+        """IPv6 rules: value / mask [n, 12], verdicts, n."""
+        n = len(self.rules6)
+        val = np.zeros((max(n, 1), 12), np.uint32)
+        msk = np.zeros((max(n, 1), 12), np.uint32)
+        per = np.zeros(max(n, 1), np.uint8)
+        for i, r in enumerate(self.rules6):
+            val[i], msk[i], per[i] = r.value, r.mask, 1 if r.permit else 0
+        return val, msk, per, n
 
     def arrays(self):
         n = len(self.rules)
