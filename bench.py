@@ -165,6 +165,8 @@ def measure_variants(a, dp, sc, dev, torch, S, P) -> dict:
                   torch.from_numpy(np.ascontiguousarray(im).view(np.int32)).to(dev)))
     el, meta = _time_fused(dp, b, a.variant_steps, torch)
     res["ipv6_mpps"] = round(n * a.variant_steps / el / 1e6, 1)
+    rs6 = P.meta_fields(meta.cpu().numpy().view(np.uint32))[2]
+    res["ipv6_dispositions"] = {int(k): int(v) for k, v in zip(*np.unique(rs6, return_counts=True))}
     res["ipv6"] = {"ipv6_fraction": 0.5, "ipv6_flows": info6["flows"], "ipv6_acl_rules": info6["rules"],
                    "forwarded_fraction": round(float(np.mean(P.meta_fields(meta.cpu().numpy().view(np.uint32))[2] == 0)), 4),
                    "frames": "64-B IPv4 + 66-B tagged IPv6/UDP (the smallest)"}

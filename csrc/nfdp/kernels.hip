@@ -765,28 +765,33 @@ struct V6Args {
 
 __global__ __launch_bounds__(256) void v6_kernel(V6Args a) {
   __shared__ uint32_t kw[4][64 * 13];   // per wave: 64 key6 rows of 12 words (+1 pad: bank spread)
+  __shared__ uint4 kxs[4][64];          // per wave: frame transposition / probe key exchange scratch
   __shared__ uint32_t ltab[16 * 256];
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   const uint32_t g = lane >> 4, col = lane & 15u;
   uint32_t* row = kw[wv];
+  uint4* kx = kxs[wv];
   if (a.toep_tab)
     for (uint32_t q = threadIdx.x; q < 16 * 256; q += 256) ltab[q] = a.toep_tab[q];
   __syncthreads();
+  // coalesced frame loads (the wave's 64 slots = one 4-KiB run, device.h wave_frames_load)
+  const __amdgpu_buffer_rsrc_t r_pk = __builtin_amdgcn_make_buffer_rsrc((void*)a.pkts, (short)0, (int)(a.n * 64u), kBufCfg);
+  const uint32_t wave0 = __builtin_amdgcn_readfirstlane(threadIdx.x) & ~63u;
   for (uint32_t base = blockIdx.x * 256u; base < a.n; base += gridDim.x * 256u) {   // block-uniform trips
     const uint32_t i = base + threadIdx.x;
     const bool valid = i < a.n;
     uint32_t d[kSlotDwords];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const uint4 v = valid ? a.pkts[(size_t)i * 4 + q] : make_uint4(0u, 0u, 0u, 0u);
-      d[4 * q] = v.x; d[4 * q + 1] = v.y; d[4 * q + 2] = v.z; d[4 * q + 3] = v.w;
+    {
+      v4u cn[4];
+      wave_frames_load<0>(r_pk, base + wave0 < a.n ? (base + wave0) * 64u : kNoRun, cn);
+      wave_frames_to_lanes(kx, cn, d);
     }
     Parsed p;
     IngressState st;
     ingress_stage(a.t, d, valid ? a.inmeta[i] : 0u, p, st);
     const bool v6 = valid && p.ipv6;
     uint32_t word = 0;
-    if (__any(v6)) {   // wave-uniform: EXEC full from here (MFMA, cross-lane reads)
+    if (__any(v6)) {   // wave-uniform: EXEC full from here (MFMA, cross-lane reads, the wave probe)
       int rule = -1;
       if (a.tiles) {
 #pragma unroll
@@ -832,7 +837,8 @@ __global__ __launch_bounds__(256) void v6_kernel(V6Args a) {
         __builtin_amdgcn_wave_barrier();
       }
       bool ok = false;
-      if (v6 && !st.reason && a.t.flow6_on) {
+      if (a.t.flow6_on) {
+        // the folded key's Toeplitz hash, the wave-cooperative bucket probe, the side entry check
         uint32_t h = 0;
         if (a.toep_tab) {
           const uint32_t w[4] = {st.key.src_ip, st.key.dst_ip, st.key.ports, st.key.meta};
@@ -841,7 +847,8 @@ __global__ __launch_bounds__(256) void v6_kernel(V6Args a) {
         } else {
           h = toeplitz_scalar(st.key, a.t.rss_key);
         }
-        const int64_t slot = flow_lookup(a.t, st.key, h);
+        uint4 act;
+        const int64_t slot = flow_probe_wave(a.t, st.key, h, v6 && !st.reason, kx, act);
         ok = slot >= 0 && flow6_verify(a.t, p, slot);
       }
       word = (uint32_t)(rule + 1) | (ok ? 0x80000000u : 0u);

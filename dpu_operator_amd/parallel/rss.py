@@ -16,8 +16,14 @@ grouped send/recv of exactly those bytes (RCCL P2P over xGMI); the owner gathers
 dense batch and runs the fused kernel on it.  The exchange of step k overlaps the next step's
 kernel:
 
-    compute stream:  fused(k) + steer(k) | gather(k-1) + fused_rx(k-1) | fused(k+1) | ...
-    comm stream:                counts(k), send/recv(k) ............... (overlaps)
+    compute stream:  fused(k) + steer(k) | fused(k+1) + steer(k+1) | ...
+    comm stream:          counts(k), send/recv(k) ....... (overlaps)
+    rx stream:                        gather(k) + fused_rx(k)  (overlaps fused(k+1))
+
+(The rx pass of step k used to run on the compute stream between fused(k) and fused(k+1): its
+launches and its workgroups' table staging cost a fixed ~27-46 us per step, rss_probe r3 s11.
+On its own stream it overlaps the next step's kernel; the slot events order the reuse of the
+two exchange slots and of the receive buffers.)
 
 Cross-GPU bytes per packet: 68 B (header slot + meta) for misdirected packets only; the payload
 never moves.  The CPU twins (oracle REMOTE steer + gather) run the same class on gloo ranks.
@@ -53,6 +59,8 @@ class _Slot:
         self.list_cnt = torch.zeros(2 + cnt_blocks, dtype=torch.int32, device=dev)
         self.ev = torch.cuda.Event() if gpu else None     # local step (kernel + steer) done
         self.cev = torch.cuda.Event() if gpu else None    # exchange done
+        self.rev = torch.cuda.Event() if gpu else None    # rx pass over this slot's receive segments done
+        self.used = False                                 # the events were recorded (slot in use before)
 
 
 class RssShardedDataPlane:
@@ -105,6 +113,7 @@ class RssShardedDataPlane:
         self.pending = None
         self.host_staged = self.gpu and dist.is_initialized() and dist.get_backend(group) == "gloo"
         self.comm = torch.cuda.Stream(self.dev) if self.gpu and not self.host_staged else None
+        self.rx_stream = torch.cuda.Stream(self.dev) if self.comm is not None else None
         self.hcnt = torch.zeros((2, world), dtype=torch.int32).pin_memory() if self.gpu else torch.zeros((2, world), dtype=torch.int32)
         self.stats = {"sent": 0, "received": 0, "steps": 0, "max_peer": 0}
 
@@ -119,6 +128,9 @@ class RssShardedDataPlane:
         """This rank's share: its own flows through the whole pipeline, other GPUs' packets into
         their owners' segments (count in pcnt)."""
         dp, p = self.dp, self._p
+        if self.comm is not None and s.used:
+            # this slot's previous exchange still reads its send segments / counts
+            torch.cuda.current_stream(self.dev).wait_event(s.cev)
         s.pcnt.zero_()
         if self.use_list:
             s.list_cnt.zero_()
@@ -169,6 +181,8 @@ class RssShardedDataPlane:
             cs = self.comm
             with torch.cuda.stream(cs):
                 cs.wait_event(s.ev)
+                if s.used:
+                    cs.wait_event(s.rev)          # the previous rx pass over s.recv is done
                 dist.all_to_all_single(s.rcnt, s.pcnt, group=self.group)
                 self.hcnt[0].copy_(s.pcnt, non_blocking=True)
                 self.hcnt[1].copy_(s.rcnt, non_blocking=True)
@@ -203,16 +217,21 @@ class RssShardedDataPlane:
         p = self._p
         nr = int(self.rx_cap)
         if self.gpu:
-            if s.cev is not None and self.comm is not None:
-                torch.cuda.current_stream(self.dev).wait_event(s.cev)
+            rs = self.rx_stream
+            if rs is not None:
+                rs.wait_event(s.cev)
             total = int(self.hcnt[1].sum()) if self.comm is not None else int(s.rcnt.sum())
             if total > nr:                        # more than the receive buffers hold: grow them
                 self._grow_rx(total)
                 nr = int(self.rx_cap)
+            st = rs.cuda_stream if rs is not None else self._stream()
             self.nf.gather(p(s.recv), self.world, self.rank, self.cap, p(self.rx_pkts), p(self.rx_inmeta),
-                           p(self.rx_n), True, self._stream())
+                           p(self.rx_n), True, st)
             self.dp.launch(p(self.rx_pkts), p(self.rx_inmeta), nr, p(self.rx_out), p(self.rx_meta),
-                           lat=p(self.rx_lat), t0=p(s.t0), stream=self._stream(), n_dev=p(self.rx_n))
+                           lat=p(self.rx_lat), t0=p(s.t0), stream=st, n_dev=p(self.rx_n))
+            if rs is not None:
+                s.rev.record(rs)
+            s.used = True
         else:
             m = self.nf.gather(p(s.recv), self.world, self.rank, self.cap, p(self.rx_pkts), p(self.rx_inmeta),
                                p(self.rx_n), False, 0)
@@ -221,6 +240,8 @@ class RssShardedDataPlane:
             self.rx_meta.numpy().view(np.uint32)[:m] = r.meta
 
     def _grow_rx(self, n: int) -> None:
+        if self.rx_stream is not None:
+            self.rx_stream.synchronize()          # the old buffers may still be in use there
         n = min(int(n * 1.25) + 4096, self.world * self.cap)
         u8, i32 = dict(dtype=torch.uint8, device=self.dev), dict(dtype=torch.int32, device=self.dev)
         self.rx_cap = n
@@ -255,6 +276,14 @@ class RssShardedDataPlane:
             self._receive(self.exchange(s))
 
     # ---------------------------------------------------------------- results
+    def sync(self) -> None:
+        """Wait for every stream of this engine (compute, exchange, rx)."""
+        if self.gpu:
+            torch.cuda.current_stream(self.dev).synchronize()
+            for st in (self.comm, self.rx_stream):
+                if st is not None:
+                    st.synchronize()
+
     def out_meta(self) -> np.ndarray:
         return self.out_meta_t.cpu().numpy().view(np.uint32)[: self.n]
 
@@ -263,11 +292,13 @@ class RssShardedDataPlane:
 
     def received(self) -> tuple[np.ndarray, np.ndarray, np.ndarray]:
         """Last processed receive batch: (input slots, egress slots, egress metas)."""
+        self.sync()
         m = int(self.rx_n.cpu().numpy()[0])
         return (self.rx_pkts.cpu().numpy()[:m], self.rx_out.cpu().numpy()[:m],
                 self.rx_meta.cpu().numpy().view(np.uint32)[:m])
 
     def latency_samples_us(self) -> np.ndarray:
+        self.sync()
         xs = []
         for t in (self.lat, self.rx_lat):
             a = t.cpu().numpy().view(np.uint32)
@@ -276,6 +307,7 @@ class RssShardedDataPlane:
 
     def harvest_flow_counters(self) -> np.ndarray:
         """Per-flow counters live on the owner only: the shard's [slots, 2] (pkts, bytes)."""
+        self.sync()
         self.dp.harvest()
         return self.dp.flow_totals
 

@@ -25,16 +25,17 @@ from dpu_operator_amd.parallel.sharded import shard_filter  # noqa: E402
 
 
 def _time(fn, iters: int) -> float:
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    """ms per call, device-wide (the RSS engine's rx pass runs on its own stream)."""
+    import time
+
     for _ in range(3):
         fn()
     torch.cuda.synchronize()
-    e0.record()
+    t0 = time.perf_counter()
     for _ in range(iters):
         fn()
-    e1.record()
-    e1.synchronize()
-    return e0.elapsed_time(e1) / iters
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) * 1e3 / iters
 
 
 def probe(world: int, batch: int, flows: int, frac: float, iters: int = 30) -> dict:
@@ -73,9 +74,23 @@ def probe(world: int, batch: int, flows: int, frac: float, iters: int = 30) -> d
     eng.hcnt[1].copy_(s.pcnt.cpu())
     rx_ms = _time(lambda: eng._receive(s), iters)
     _, _, rs = P.meta_fields(eng.out_meta_t.cpu().numpy().view(np.uint32)[:batch])
+    # the engine's step sequence (exchange stood in by the prepared receive segments): local pass
+    # of step k on the compute stream, rx pass of step k - 1 on the rx stream
+    s2 = eng.slots[1]
+    s2.recv.copy_(s.recv)
+    kk = [0]
+
+    def pipe():
+        k = kk[0]
+        eng._local(eng.slots[k & 1], pk, im, batch)
+        eng._receive(eng.slots[(k + 1) & 1])
+        kk[0] += 1
+
+    step_ms = _time(pipe, iters)
     res.update(rss_local_ms=round(steer_ms, 4), rss_rx_ms=round(rx_ms, 4), list_mode=eng.use_list,
                steered_fraction=round(float(np.mean(rs == 10)), 4), segment_counts=cnt.tolist(),
-               per_gpu_vs_1gpu=round(fused_ms / (steer_ms + rx_ms), 3))
+               per_gpu_vs_1gpu_serial=round(fused_ms / (steer_ms + rx_ms), 3),
+               rss_step_ms=round(step_ms, 4), per_gpu_vs_1gpu=round(fused_ms / step_ms, 3))
     return res
 
 
