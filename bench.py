@@ -171,6 +171,24 @@ def measure_variants(a, dp, sc, dev, torch, S, P) -> dict:
                    "forwarded_fraction": round(float(np.mean(P.meta_fields(meta.cpu().numpy().view(np.uint32))[2] == 0)), 4),
                    "frames": "64-B IPv4 + 66-B tagged IPv6/UDP (the smallest)"}
     del b
+    # overlay: the headline's traffic VXLAN-encapsulated on an underlay VTEP port (64-B inner frames,
+    # 114-B outer): single-pass termination of wide header pairs (pair_kernel -> fused ->
+    # pair_fix), the SFC on the inner frame.  n / 2 frames = n slots per step.
+    ports = S.install_vxlan(dp, sc)
+    dp.commit()
+    b = []
+    for r in range(2):
+        pk, im, _ = S.traffic_vxlan(sc, ports, n // 2, seed=9400 + r)
+        b.append((torch.from_numpy(pk).to(dev), torch.from_numpy(im.view(np.int32)).to(dev)))
+    el, meta = _time_fused(dp, b, a.variant_steps, torch)
+    rsx = P.meta_fields(meta.cpu().numpy().view(np.uint32))[2]
+    res["vxlan_mpps"] = round((n // 2) * a.variant_steps / el / 1e6, 1)
+    res["vxlan"] = {"frames_per_step": n // 2, "slots_per_step": n, "inner": "64-B frames of the headline's flows",
+                    "forwarded_fraction": round(float(np.mean(rsx[0::2] == 0)), 4),
+                    "note": "Mpps of encapsulated frames; each is a 128-B wide header pair (two slots)"}
+    dp.ports.clear(ports["vtep"])
+    dp.commit()
+    del b
     return res
 
 
@@ -552,6 +570,7 @@ def main() -> None:
             "value_acl_wild": None if not variants else variants["acl_wild_mpps"],
             "value_l3": None if not variants else variants["l3_mpps"],
             "value_ipv6": None if not variants else variants["ipv6_mpps"],
+            "value_vxlan": None if not variants else variants["vxlan_mpps"],
             "imix": None if not variants else variants["imix"],
             "variants": variants,
             # live pod -> pod through the native I/O engine + ring kernel (memif vports, 64-B frames)

@@ -237,7 +237,7 @@ __global__ __launch_bounds__(kFB, EARLY ? NFDP_EARLY_WAVES_PER_EU : NFDP_FUSED_W
     if constexpr (V6) {
       if (__builtin_expect(__any(p.ipv6), 0)) {
         if (p.ipv6 && valid) {
-          const uint4 k6 = a.out[i];
+          const uint4 k6 = a.out[(size_t)i * 4];   // first 16 B of slot i
           st.key.src_ip = k6.x; st.key.dst_ip = k6.y; st.key.ports = k6.z; st.key.meta = k6.w;
         }
       }
@@ -854,7 +854,7 @@ __global__ __launch_bounds__(256) void v6_kernel(V6Args a) {
       word = (uint32_t)(rule + 1) | (ok ? 0x80000000u : 0u);
     }
     if (valid) a.res[i] = v6 ? word : 0u;
-    if (v6) a.keys[i] = make_uint4(st.key.src_ip, st.key.dst_ip, st.key.ports, st.key.meta);
+    if (v6) a.keys[(size_t)i * 4] = make_uint4(st.key.src_ip, st.key.dst_ip, st.key.ports, st.key.meta);   // slot i
   }
 }
 

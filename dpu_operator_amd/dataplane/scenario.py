@@ -445,3 +445,64 @@ def traffic_ipv6(sc: Scenario, info: dict, n: int, seed: int = 1, frame_len: int
     tagged[:, 16:] = fr[:, 12:]
     lens = ln + 4
     return P.header_slots(tagged, lens), P.inmeta(sc.pod_port[s], lens)
+
+
+# ---- overlay: the SFC's traffic arriving VXLAN-encapsulated on a VTEP port (bench value_vxlan) ----
+LOCAL_VTEP, REMOTE_VTEP, VXLAN_VNI = 0xC0000201, 0xC0000202, 5000   # 192.0.2.1 / .2
+VTEP_MAC, UNDERLAY_GW_MAC, REMOTE_POD_MAC = "02:00:00:00:0e:01", "02:00:00:00:0e:02", "02:00:00:00:bb:01"
+
+
+def install_vxlan(dp, sc: Scenario) -> dict:
+    """An underlay VTEP port (local VTEP 192.0.2.1) and a tunnel port on the scenario's bridge whose
+    (remote VTEP 192.0.2.2, VNI 5000) frames are terminated in one pass (wide header pairs) and run
+    through the SFC as received on the tunnel port.  Returns the two ports."""
+    vtep = int(sc.pod_port.max()) + 1
+    tun = vtep + 1
+    dp.ports.set(vtep, flags=T.PORT_VALID | T.PORT_VTEP, mac=VTEP_MAC)
+    dp.ports.a[vtep]["ext"] = int(P.ip_raw(np.uint32(LOCAL_VTEP)))
+    dp.ports.set(tun, flags=T.PORT_VALID | T.PORT_TUNNEL, bridge_id=sc.bridge)
+    dp.ports.a[tun]["lag"] = 0
+    dp.tunnels.set(0, src=str(ipaddress.IPv4Address(LOCAL_VTEP)), dst=str(ipaddress.IPv4Address(REMOTE_VTEP)),
+                   vni=VXLAN_VNI, out_port=vtep, smac=VTEP_MAC, dmac=UNDERLAY_GW_MAC)
+    dp.terms.insert(str(ipaddress.IPv4Address(REMOTE_VTEP)), VXLAN_VNI, tun)
+    dp.ports.version += 1
+    return {"vtep": vtep, "tunnel": tun}
+
+
+def traffic_vxlan(sc: Scenario, ports: dict, n: int, seed: int = 1, inner_len: int = 60):
+    """n VXLAN frames on the VTEP port: each inner frame (inner_len B, untagged, no FCS) is a packet
+    of a random installed flow, from a remote MAC to the gateway.  Every frame is longer than 64 B,
+    so it arrives as a wide header pair: returns (slots [2n, 64], inmeta [2n]) and the inner
+    frames' flow indices."""
+    rng = np.random.default_rng(seed)
+    f = rng.integers(0, len(sc.keys), n)
+    s, d = sc.flow_src_pod[f], sc.flow_dst_pod[f]
+    inner, ilen = P.craft_full(n, dmac=GW_MAC, smac=REMOTE_POD_MAC, src_ip=POD_NET + s, dst_ip=POD_NET + d,
+                               sport=sc.flow_sport[f], dport=sc.flow_dport[f], proto=17, frame_len=inner_len,
+                               payload_seed=seed)
+    L = 50 + inner_len
+    fr = np.zeros((n, max(L, 128)), np.uint8)
+    fr[:, 0:6] = P.mac_bytes(VTEP_MAC)
+    fr[:, 6:12] = P.mac_bytes(UNDERLAY_GW_MAC)
+    fr[:, 12], fr[:, 13] = 0x08, 0x00
+    ip = np.zeros(20, np.uint8)
+    ip[0], ip[8], ip[9] = 0x45, 64, 17
+    ip[2:4] = np.frombuffer((20 + 8 + 8 + inner_len).to_bytes(2, "big"), np.uint8)
+    ip[6] = 0x40
+    ip[12:16] = np.frombuffer(REMOTE_VTEP.to_bytes(4, "big"), np.uint8)
+    ip[16:20] = np.frombuffer(LOCAL_VTEP.to_bytes(4, "big"), np.uint8)
+    c = int(sum(int.from_bytes(bytes(ip[k:k + 2]), "big") for k in range(0, 20, 2)))
+    while c >> 16:
+        c = (c & 0xFFFF) + (c >> 16)
+    ip[10:12] = np.frombuffer((~c & 0xFFFF).to_bytes(2, "big"), np.uint8)
+    fr[:, 14:34] = ip
+    sport = 0xC000 | (rng.integers(0, 0x4000, n))
+    fr[:, 34], fr[:, 35] = (sport >> 8) & 0xFF, sport & 0xFF
+    fr[:, 36], fr[:, 37] = 4789 >> 8, 4789 & 0xFF
+    fr[:, 38], fr[:, 39] = ((8 + 8 + inner_len) >> 8) & 0xFF, (8 + 8 + inner_len) & 0xFF
+    fr[:, 42] = 0x08
+    fr[:, 46:49] = np.frombuffer(VXLAN_VNI.to_bytes(3, "big"), np.uint8)
+    fr[:, 50:50 + inner_len] = inner[:, :inner_len]
+    lens = np.full(n, L, np.uint32)
+    slots, im, _ = P.wide_slots(fr, lens, ports["vtep"], wide_ports={ports["vtep"]})
+    return slots, im, f

@@ -251,3 +251,76 @@ def test_dual_stack_scenario_forwards_everything():
     assert np.array_equal(port[512:], sc.pod_port[info["dst"][f]])
     dp.harvest()
     assert int(dp.flow_totals[:, 0].sum()) == 1024
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_acl", [256, 1024])
+def test_ipv6_flows_big_batch_gpu_bit_exact(n_acl):
+    """More packets than one grid-stride pass of v6_kernel and of the fused kernel (the IPv6 key
+    hand-over through the out slots must address whole slots), on the 4-wave and the early-fetch
+    V6 instances."""
+    import torch
+
+    from dpu_operator_amd.dataplane import scenario as S
+
+    def build(dev):
+        dp = DataPlane(device=dev, flow_buckets=1 << 16, hash_mode="lds", acl_mode="mfma")
+        sc = S.build_sfc(dp, n_pods=8, n_flows=1 << 16, n_acl=n_acl, seed=0)
+        info6 = S.install_ipv6(dp, sc, 1 << 14, 64)
+        dp.commit(full=True)
+        return dp, sc, info6
+
+    (g, sc, info6), (c, _, _) = build("cuda"), build("cpu")
+    pk6, im6 = S.traffic_ipv6(sc, info6, 1 << 19, seed=5)
+    pk4, im4 = S.traffic(sc, 1 << 19, seed=6)
+    perm = np.random.default_rng(1).permutation(1 << 20)
+    pk, im = np.ascontiguousarray(np.concatenate([pk4, pk6])[perm]), np.ascontiguousarray(np.concatenate([im4, im6])[perm])
+    rc = c.run(pk, im)
+    r = g.run(torch.from_numpy(pk).cuda(), torch.from_numpy(im.view(np.int32)).cuda())
+    torch.cuda.synchronize()
+    m = r.meta.cpu().numpy().view(np.uint32)
+    assert np.array_equal(m, rc.meta)
+    assert np.array_equal(r.out.cpu().numpy(), rc.out)
+    assert (P.meta_fields(m)[2] == 0).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("coop", [True, False])
+def test_ipv6_flows_ring_kernel_bit_exact(coop):
+    """The persistent ring kernel's V6 instances (inline fold, scalar IPv6 TCAM, side check) on a
+    dual-stack trace, against the oracle."""
+    from dpu_operator_amd.dataplane import scenario as S
+    from dpu_operator_amd.dataplane.ring import RingPath
+
+    cap = 1 << 14
+
+    def build(dev):
+        dp = DataPlane(device=dev, flow_buckets=1 << 14, hash_mode="lds", acl_mode="mfma")
+        sc = S.build_sfc(dp, n_pods=8, n_flows=1 << 14, n_acl=64, seed=0)
+        info6 = S.install_ipv6(dp, sc, 1 << 12, 16)
+        dp.commit(full=True)
+        return dp, sc, info6
+
+    (g, sc, info6), (c, _, _) = build("cuda"), build("cpu")
+    pk6, im6 = S.traffic_ipv6(sc, info6, cap // 2, seed=5)
+    pk4, im4 = S.traffic(sc, cap // 2, seed=6)
+    perm = np.random.default_rng(2).permutation(cap)
+    pk, im = np.ascontiguousarray(np.concatenate([pk4, pk6])[perm]), np.ascontiguousarray(np.concatenate([im4, im6])[perm])
+    ring = RingPath(g, capacity=cap, deadline_s=30.0, coop=coop)
+    try:
+        ring.stage(pk, im)
+        ring.start()
+        for _ in range(4):
+            end = ring.publish(cap // 4)
+        ring.wait(end, 10.0)
+        ring.stop()
+        out, meta = ring.results()
+    finally:
+        ring.close()
+    rc = c.run(pk, im)
+    assert np.array_equal(meta, rc.meta)
+    assert np.array_equal(out, rc.out)
+    assert (P.meta_fields(meta)[2] == 0).all()
+    g.harvest()
+    c.harvest()
+    assert np.array_equal(g.flow_totals, c.flow_totals)
