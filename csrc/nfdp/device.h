@@ -84,6 +84,26 @@ NFDP_HD int acl_rule_of(uint32_t b, uint32_t n_acl) {
 #ifndef NFDP_PIPE_UNROLL
 #define NFDP_PIPE_UNROLL 1   // r3 s16 A/B: ACL1024 0.3145 vs 0.3211 ms, ClassBench unchanged
 #endif
+// Toeplitz LDS tables (HASH == kHashLds).  Byte tables: 16 x 256 words (16 KiB), one lookup per
+// key byte at a random entry (bank conflicts: ~4-way for 64 random entries over 64 banks).
+// NFDP_HASH_NIBBLE=1: 32 x 16 words (2 KiB), two lookups per byte, each table 16 consecutive
+// words = 16 distinct banks, so a wave's 64 reads are conflict-free (equal addresses broadcast);
+// derived from the byte tables at staging (Toeplitz is XOR-linear: T[v] = T[v & 0xF0] ^ T[v & 0xF]).
+#ifndef NFDP_HASH_NIBBLE
+#define NFDP_HASH_NIBBLE 0
+#endif
+constexpr uint32_t kToepLdsWords = NFDP_HASH_NIBBLE ? 32 * 16 : 16 * 256;
+__device__ __forceinline__ void stage_toep(uint32_t* dst, const uint32_t* bytes, uint32_t tid, uint32_t nthr) {
+  for (uint32_t i = tid; i < kToepLdsWords; i += nthr) {
+    if (NFDP_HASH_NIBBLE) {
+      const uint32_t pos = i >> 4, x = i & 15u, b = pos >> 1;
+      dst[i] = bytes[b * 256 + ((pos & 1u) ? x : (x << 4))];
+    } else {
+      dst[i] = bytes[i];
+    }
+  }
+}
+
 struct NoHashHook {
   __device__ void operator()(uint32_t) const {}
 };
@@ -148,8 +168,16 @@ __device__ __forceinline__ void classify_wave(const FlowKey& key, uint4* kx, con
   } else if constexpr (HASH == kHashLds) {
     const uint32_t w[4] = {key.src_ip, key.dst_ip, key.ports, key.meta};
     uint32_t h = 0;
+#if NFDP_HASH_NIBBLE
+#pragma unroll
+    for (int b = 0; b < 16; ++b) {
+      const uint32_t v = w[b >> 2] >> (8 * (b & 3));
+      h ^= ltab[(2 * b) * 16 + ((v >> 4) & 15u)] ^ ltab[(2 * b + 1) * 16 + (v & 15u)];
+    }
+#else
 #pragma unroll
     for (int b = 0; b < 16; ++b) h ^= ltab[b * 256 + ((w[b >> 2] >> (8 * (b & 3))) & 0xFFu)];
+#endif
     hash = h;
 #ifdef NFDP_ABL_NO_HASH  // cost attribution only (wrong results): a two-instruction stand-in hash
     hash = (key.src_ip ^ key.ports) * 0x9E3779B1u;

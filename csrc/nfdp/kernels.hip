@@ -103,7 +103,7 @@ __host__ __device__ inline LdsLayout lds_layout(int hash_mode, int acl_mode, uin
   size_t o = 0;
   uint32_t lt = acl_tiles < kLdsAclTiles ? acl_tiles : kLdsAclTiles, ct = lt;
   if (one_block && acl_mode == kAclMfma && acl_tiles > kLdsAclTiles) {
-    const size_t rest = (hash_mode == kHashMfma ? 2 * 2 * 64 * 16 : 0) + (hash_mode == kHashLds ? 16 * 256 * 4 : 0) +
+    const size_t rest = (hash_mode == kHashMfma ? 2 * 2 * 64 * 16 : 0) + (hash_mode == kHashLds ? kToepLdsWords * 4 : 0) +
                         kFWaves * 64 * 16 + kLdsPorts * 4 * 4 + kNumReasons * 4 + 16 + kLdsTabBytes;
     const size_t budget = 160 * 1024 - 2048;   // static LDS + alignment margin
     ct = acl_tiles;
@@ -115,7 +115,7 @@ __host__ __device__ inline LdsLayout lds_layout(int hash_mode, int acl_mode, uin
   L.acl_w = o; if (acl_mode == kAclMfma) o += (size_t)lt * 64 * 16;
   L.acl_c = o; if (acl_mode == kAclMfma) o += (size_t)ct * 4 * 16;
   L.toep_f = o; if (hash_mode == kHashMfma) o += 2 * 2 * 64 * 16;
-  L.toep_t = o; if (hash_mode == kHashLds) o += 16 * 256 * 4;
+  L.toep_t = o; if (hash_mode == kHashLds) o += kToepLdsWords * 4;
   L.kx = o; o += kFWaves * 64 * 16;
   L.pc = o; o += kLdsPorts * 4 * 4;
   L.drops = o; o += kNumReasons * 4;
@@ -178,7 +178,7 @@ __global__ __launch_bounds__(kFB, EARLY ? NFDP_EARLY_WAVES_PER_EU : NFDP_FUSED_W
   if constexpr (HASH == kHashMfma)
     for (uint32_t i = threadIdx.x; i < 256; i += kFB) lt[i] = a.toep_frag[i];
   if constexpr (HASH == kHashLds)
-    for (uint32_t i = threadIdx.x; i < 4096; i += kFB) ltab[i] = a.toep_tab[i];
+    stage_toep(ltab, a.toep_tab, threadIdx.x, kFB);
   for (uint32_t i = threadIdx.x; i < kLdsPorts * 4; i += kFB) pc[i] = 0;
   if (threadIdx.x < kNumReasons) drops[threadIdx.x] = 0;
   if constexpr (REMOTE)
@@ -467,30 +467,38 @@ __global__ __launch_bounds__(kFB, EARLY ? NFDP_EARLY_WAVES_PER_EU : NFDP_FUSED_W
 // already marked done is skipped, so a batch can be run again.
 __global__ __launch_bounds__(256) void pair_kernel(uint4* pkts, uint32_t* inmeta, uint32_t n, TablesView t,
                                                    unsigned long long* port_ctr, uint32_t count) {
-  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n; i += gridDim.x * 256) {
-    const uint32_t cim = inmeta[i];
-    if ((cim & 0xFFFFu) != kPortCont || ((cim >> 16) & kPairDone)) continue;
-    uint32_t ci = (uint32_t)kSlotBytes << 8;
-    const uint32_t him = i ? inmeta[i - 1] : kPortCont;
-    if ((him & 0xFFFFu) != kPortCont) {
-      uint32_t d[kSlotDwords], x[kSlotDwords], inner[kSlotDwords], strip, hv;
+  // block-uniform trips: the VTEP rx count is wave-aggregated (one atomic per distinct port per
+  // wave; every pair of a VTEP port adding to the same counter word serialised at the memory
+  // side: 25 ms per 2M pairs, r3 s23 trace)
+  for (uint32_t base = blockIdx.x * 256; base < n; base += gridDim.x * 256) {
+    const uint32_t i = base + threadIdx.x;
+    bool term = false;
+    uint32_t vport = 0, vlen = 0;
+    const uint32_t cim = i < n ? inmeta[i] : 0u;
+    if (i < n && (cim & 0xFFFFu) == kPortCont && !((cim >> 16) & kPairDone)) {
+      uint32_t ci = (uint32_t)kSlotBytes << 8;
+      const uint32_t him = i ? inmeta[i - 1] : kPortCont;
+      if ((him & 0xFFFFu) != kPortCont) {
+        uint32_t d[kSlotDwords], x[kSlotDwords], inner[kSlotDwords], strip, hv;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const uint4 v = pkts[(size_t)(i - 1) * 4 + q], w = pkts[(size_t)i * 4 + q];
-        d[4 * q] = v.x; d[4 * q + 1] = v.y; d[4 * q + 2] = v.z; d[4 * q + 3] = v.w;
-        x[4 * q] = w.x; x[4 * q + 1] = w.y; x[4 * q + 2] = w.z; x[4 * q + 3] = w.w;
-      }
-      const int tp = decap_pair(t, DirectTables{t}, d, x, him, inner, strip, hv);
-      if (tp >= 0) {
+        for (int q = 0; q < 4; ++q) {
+          const uint4 v = pkts[(size_t)(i - 1) * 4 + q], w = pkts[(size_t)i * 4 + q];
+          d[4 * q] = v.x; d[4 * q + 1] = v.y; d[4 * q + 2] = v.z; d[4 * q + 3] = v.w;
+          x[4 * q] = w.x; x[4 * q + 1] = w.y; x[4 * q + 2] = w.z; x[4 * q + 3] = w.w;
+        }
+        const int tp = decap_pair(t, DirectTables{t}, d, x, him, inner, strip, hv);
+        if (tp >= 0) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
-          pkts[(size_t)(i - 1) * 4 + q] = make_uint4(inner[4 * q], inner[4 * q + 1], inner[4 * q + 2], inner[4 * q + 3]);
-        inmeta[i - 1] = (uint32_t)tp | (((him >> 16) - strip) << 16);
-        if (count) atomicAdd(port_ctr + 2 * (him & 0xFFFFu), ctr_inc(him >> 16));   // the outer frame, VTEP port
-        ci = strip | (hv << 8);
+          for (int q = 0; q < 4; ++q)
+            pkts[(size_t)(i - 1) * 4 + q] = make_uint4(inner[4 * q], inner[4 * q + 1], inner[4 * q + 2], inner[4 * q + 3]);
+          inmeta[i - 1] = (uint32_t)tp | (((him >> 16) - strip) << 16);
+          term = true; vport = him & 0xFFFFu; vlen = him >> 16;   // the outer frame, on its VTEP port
+          ci = strip | (hv << 8);
+        }
       }
+      inmeta[i] = kPortCont | ((ci | kPairDone) << 16);
     }
-    inmeta[i] = kPortCont | ((ci | kPairDone) << 16);
+    if (count) wave_counter_add(port_ctr, 2 * vport, vlen, true, term);
   }
 }
 

@@ -72,7 +72,7 @@ __host__ __device__ inline RingLds ring_lds(int hash_mode, int acl_mode, uint32_
   L.acl_w = o; if (acl_mode == kAclMfma) o += (size_t)lt * 64 * 16;
   L.acl_c = o; if (acl_mode == kAclMfma) o += (size_t)lt * 4 * 16;
   L.toep_f = o; if (hash_mode == kHashMfma) o += 2 * 2 * 64 * 16;
-  L.toep_t = o; if (hash_mode == kHashLds) o += 16 * 256 * 4;
+  L.toep_t = o; if (hash_mode == kHashLds) o += kToepLdsWords * 4;
   L.kx = o; o += kRingWaves * 64 * 16;
   L.tports = o; o += kLdsPorts * sizeof(PortEntry);
   L.tchain = o; o += kLdsChains * 8;
@@ -176,7 +176,7 @@ __global__ __launch_bounds__(kRingBlock) void ring_kernel(RingArgs a) {
     if constexpr (HASH == kHashMfma)
       for (uint32_t i = threadIdx.x; i < 256; i += kRingBlock) lt[i] = tf[i];
     if constexpr (HASH == kHashLds)
-      for (uint32_t i = threadIdx.x; i < 4096; i += kRingBlock) ltab[i] = tt[i];
+      stage_toep(ltab, tt, threadIdx.x, kRingBlock);
     // ports / chain words / ACL verdicts in LDS: the per-packet path's only global loads are the
     // frame and the flow bucket
     const LdsTables s0 = stage_lds_tables(t, lport, lchain, lperm, true, kRingBlock);

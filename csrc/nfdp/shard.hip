@@ -14,7 +14,7 @@ __host__ __device__ inline ShardLds shard_lds(int hash_mode, int acl_mode, uint3
   L.acl_w = o; if (acl_mode == kAclMfma) o += (size_t)lt * 64 * 16;
   L.acl_c = o; if (acl_mode == kAclMfma) o += (size_t)lt * 4 * 16;
   L.toep_f = o; if (hash_mode == kHashMfma) o += 2 * 2 * 64 * 16;
-  L.toep_t = o; if (hash_mode == kHashLds) o += 16 * 256 * 4;
+  L.toep_t = o; if (hash_mode == kHashLds) o += kToepLdsWords * 4;
   L.kx = o; o += kWaves * 64 * 16;
   L.pc = o; if (ports) o += kLdsPorts * 4 * 4 + kNumReasons * 4;
   L.total = (o + 15) & ~(size_t)15;
@@ -47,7 +47,7 @@ __global__ __launch_bounds__(kBlock) void ingress_kernel(IngressArgs a) {
     for (uint32_t i = threadIdx.x; i < 256; i += kBlock) lt[i] = gt[i];
   }
   if constexpr (HASH == kHashLds)
-    for (uint32_t i = threadIdx.x; i < 4096; i += kBlock) ltab[i] = a.toep_tab[i];
+    stage_toep(ltab, a.toep_tab, threadIdx.x, kBlock);
   __syncthreads();
   const size_t seg = desc_seg_bytes(a.g.cap_desc);
   for (uint32_t base = blockIdx.x * kBlock; base < a.n; base += gridDim.x * kBlock) {
