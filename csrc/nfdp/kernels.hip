@@ -467,12 +467,30 @@ __global__ __launch_bounds__(kFB, EARLY ? NFDP_EARLY_WAVES_PER_EU : NFDP_FUSED_W
 // already marked done is skipped, so a batch can be run again.
 __global__ __launch_bounds__(256) void pair_kernel(uint4* pkts, uint32_t* inmeta, uint32_t n, TablesView t,
                                                    unsigned long long* port_ctr, uint32_t count) {
-  // block-uniform trips: the VTEP rx count is wave-aggregated (one atomic per distinct port per
-  // wave; every pair of a VTEP port adding to the same counter word serialised at the memory
-  // side: 25 ms per 2M pairs, r3 s23 trace)
+  // A wave owns a run of 64 consecutive slots: one coalesced 4-KiB load into its LDS tile (per-lane
+  // 64-B slots at a 64-B stride ran at a quarter of the bandwidth), the pairs whose continuation
+  // lies in the run are resolved from the tile, and only the head slots it rewrote are stored back
+  // (coalesced, the other chunks masked off).  A head just before the run (the previous run's last
+  // slot) belongs to this wave's lane 0 and is read / written in global memory: its own run never
+  // stores an unmodified slot, so nothing races with that write.  Block-uniform trips; the VTEP rx
+  // count is wave-aggregated (every pair of a VTEP port adding to one counter word serialised at
+  // the memory side: 25 ms per 2M pairs, r3 s23 trace).
+  __shared__ uint4 tile[4][256];
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  uint4* T = tile[wv];
+  const __amdgpu_buffer_rsrc_t r_pk = __builtin_amdgcn_make_buffer_rsrc((void*)pkts, (short)0, (int)(n * 64u), kBufCfg);
   for (uint32_t base = blockIdx.x * 256; base < n; base += gridDim.x * 256) {
-    const uint32_t i = base + threadIdx.x;
-    bool term = false;
+    const uint32_t run0 = base + (wv << 6);
+    const uint32_t soff = run0 < n ? run0 * 64u : kNoRun;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const v4u c = __builtin_amdgcn_raw_buffer_load_b128(r_pk, lane * 16u + q * 1024u, soff, 0);
+      T[q * 64 + lane] = make_uint4(c.x, c.y, c.z, c.w);
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    const uint32_t i = run0 + lane;
+    bool term = false, in_tile = false;
     uint32_t vport = 0, vlen = 0;
     const uint32_t cim = i < n ? inmeta[i] : 0u;
     if (i < n && (cim & 0xFFFFu) == kPortCont && !((cim >> 16) & kPairDone)) {
@@ -480,17 +498,22 @@ __global__ __launch_bounds__(256) void pair_kernel(uint4* pkts, uint32_t* inmeta
       const uint32_t him = i ? inmeta[i - 1] : kPortCont;
       if ((him & 0xFFFFu) != kPortCont) {
         uint32_t d[kSlotDwords], x[kSlotDwords], inner[kSlotDwords], strip, hv;
+        in_tile = lane > 0;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const uint4 v = pkts[(size_t)(i - 1) * 4 + q], w = pkts[(size_t)i * 4 + q];
+          const uint4 v = in_tile ? T[4 * (lane - 1) + q] : pkts[(size_t)(i - 1) * 4 + q];
+          const uint4 w = T[4 * lane + q];
           d[4 * q] = v.x; d[4 * q + 1] = v.y; d[4 * q + 2] = v.z; d[4 * q + 3] = v.w;
           x[4 * q] = w.x; x[4 * q + 1] = w.y; x[4 * q + 2] = w.z; x[4 * q + 3] = w.w;
         }
         const int tp = decap_pair(t, DirectTables{t}, d, x, him, inner, strip, hv);
         if (tp >= 0) {
 #pragma unroll
-          for (int q = 0; q < 4; ++q)
-            pkts[(size_t)(i - 1) * 4 + q] = make_uint4(inner[4 * q], inner[4 * q + 1], inner[4 * q + 2], inner[4 * q + 3]);
+          for (int q = 0; q < 4; ++q) {
+            const uint4 o = make_uint4(inner[4 * q], inner[4 * q + 1], inner[4 * q + 2], inner[4 * q + 3]);
+            if (in_tile) T[4 * (lane - 1) + q] = o;
+            else pkts[(size_t)(i - 1) * 4 + q] = o;
+          }
           inmeta[i - 1] = (uint32_t)tp | (((him >> 16) - strip) << 16);
           term = true; vport = him & 0xFFFFu; vlen = him >> 16;   // the outer frame, on its VTEP port
           ci = strip | (hv << 8);
@@ -498,6 +521,20 @@ __global__ __launch_bounds__(256) void pair_kernel(uint4* pkts, uint32_t* inmeta
       }
       inmeta[i] = kPortCont | ((ci | kPairDone) << 16);
     }
+    // slots of the run this wave rewrote: the head before each terminating lane > 0
+    const unsigned long long mod = __ballot(term && in_tile) >> 1;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    if (mod) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint4 v = T[q * 64 + lane];
+        const v4u w = {v.x, v.y, v.z, v.w};
+        const bool keep = (mod >> (16u * q + (lane >> 2))) & 1ull;   // chunk q*64+lane is part of slot 16q + lane/4
+        __builtin_amdgcn_raw_buffer_store_b128(w, r_pk, keep ? lane * 16u + q * 1024u : kNoRun, soff, 0);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();   // the tile is reloaded next trip
     if (count) wave_counter_add(port_ctr, 2 * vport, vlen, true, term);
   }
 }
@@ -537,6 +574,7 @@ hipError_t launch_pair_fix(const uint32_t* inmeta, uint32_t* out_meta, uint32_t 
 hipError_t launch_pairs(void* pkts, uint32_t* inmeta, uint32_t n, const TablesView& t, unsigned long long* port_ctr,
                         bool count, hipStream_t s) {
   if (!pkts || !inmeta || !port_ctr) return hipErrorInvalidValue;
+  if (n >= (1u << 25)) return hipErrorInvalidValue;   // 32-bit buffer views of the slots
   if (n == 0) return hipSuccess;
   const uint32_t g = (n + 255) / 256 < 2048 ? (n + 255) / 256 : 2048;
   hipLaunchKernelGGL(pair_kernel, dim3(g), dim3(256), 0, s, reinterpret_cast<uint4*>(pkts), inmeta, n, t, port_ctr,
