@@ -473,11 +473,14 @@ __global__ __launch_bounds__(256) void pair_kernel(uint4* pkts, uint32_t* inmeta
   // (coalesced, the other chunks masked off).  A head just before the run (the previous run's last
   // slot) belongs to this wave's lane 0 and is read / written in global memory: its own run never
   // stores an unmodified slot, so nothing races with that write.  Block-uniform trips; the VTEP rx
-  // count is wave-aggregated (every pair of a VTEP port adding to one counter word serialised at
-  // the memory side: 25 ms per 2M pairs, r3 s23 trace).
+  // count is tallied per workgroup (every pair of a VTEP port adding to one counter word
+  // serialised at the memory side: 25 ms per 2M pairs, r3 s23 trace).
   __shared__ uint4 tile[4][256];
+  __shared__ uint32_t vpk[kLdsPorts], vby[kLdsPorts];   // VTEP rx counts of this workgroup (ports < 256)
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   uint4* T = tile[wv];
+  for (uint32_t q = threadIdx.x; q < kLdsPorts; q += 256) { vpk[q] = 0; vby[q] = 0; }
+  __syncthreads();
   const __amdgpu_buffer_rsrc_t r_pk = __builtin_amdgcn_make_buffer_rsrc((void*)pkts, (short)0, (int)(n * 64u), kBufCfg);
   for (uint32_t base = blockIdx.x * 256; base < n; base += gridDim.x * 256) {
     const uint32_t run0 = base + (wv << 6);
@@ -535,7 +538,18 @@ __global__ __launch_bounds__(256) void pair_kernel(uint4* pkts, uint32_t* inmeta
       }
     }
     __builtin_amdgcn_wave_barrier();   // the tile is reloaded next trip
-    if (count) wave_counter_add(port_ctr, 2 * vport, vlen, true, term);
+    if (count) {
+      // per-workgroup LDS tallies, one global atomic per port per workgroup at the end (a
+      // per-wave atomic on the VTEP port's counter word still serialised 64K waves at the memory
+      // side: 0.81 ms per 4M slots, r3 s27 trace)
+      if (term && vport < (uint32_t)kLdsPorts) { atomicAdd(&vpk[vport], 1u); atomicAdd(&vby[vport], vlen); }
+      wave_counter_add(port_ctr, 2 * vport, vlen, true, term && vport >= (uint32_t)kLdsPorts);
+    }
+  }
+  if (count) {
+    __syncthreads();
+    for (uint32_t q = threadIdx.x; q < kLdsPorts; q += 256)
+      if (vpk[q]) atomicAdd(port_ctr + 2 * q, ((unsigned long long)vpk[q] << 40) | vby[q]);
   }
 }
 
@@ -566,7 +580,9 @@ hipError_t launch_pair_fix(const uint32_t* inmeta, uint32_t* out_meta, uint32_t 
                            bool count, hipStream_t s) {
   if (!inmeta || !out_meta || !drop_ctr) return hipErrorInvalidValue;
   if (n == 0) return hipSuccess;
-  const uint32_t g = (n + 255) / 256 < 1024 ? (n + 255) / 256 : 1024;
+  // few workgroups: each ends with two atomics on the same two counter words, which serialise
+  // at the memory side (1024 workgroups: 24 us per 4M slots, r3 s27 trace)
+  const uint32_t g = (n + 255) / 256 < 256 ? (n + 255) / 256 : 256;
   hipLaunchKernelGGL(pair_fix_kernel, dim3(g), dim3(256), 0, s, inmeta, out_meta, n, drop_ctr, count ? 1u : 0u);
   return hipGetLastError();
 }
