@@ -565,6 +565,24 @@ __device__ __forceinline__ void wave_counter_add(unsigned long long* ctr, uint32
 
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 
+// Wave-aggregated append to the side list (flagged lanes): ONE atomic on the list counter per wave
+// instead of one per lane (every lane of a wave adding to one counter word serialises at the
+// memory side; an overlay egress flags every packet for its outer header).  EXEC must be full.
+__device__ __forceinline__ void side_list_append(const SideOut& so, bool sn, uint32_t i) {
+  const unsigned long long m = __ballot(sn);
+  const uint32_t pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+  const int leader = __builtin_ctzll(m);
+  uint32_t base = 0;
+  if (sn && pre == 0) base = atomicAdd(so.cnt + 5, (uint32_t)__builtin_popcountll(m));
+  base = __builtin_amdgcn_readlane(base, leader);
+  if (sn) {
+    const uint32_t q = base + pre;
+    if (q < so.cap_list) so.list[q] = i;
+    else atomicAdd(so.cnt + 6, 1u);
+  }
+}
+
+
 // GPU sink of pipeline.h side_stage: one global atomic per replica / learn event (rare paths:
 // flooding, mirroring, ARP-trap and learning ports only).  Replica tx and ARP-trap counts go
 // straight to the global counters.

@@ -386,13 +386,7 @@ __global__ __launch_bounds__(kFB, EARLY ? NFDP_EARLY_WAVES_PER_EU : NFDP_FUSED_W
       // flood / mirror / ARP-trap / learning packets go on the side list (side_kernel emits their
       // replicas and learn events after this kernel): a wave-uniform skip in the common case
       const bool sn = valid && side_needed(st, p, e);
-      if (__builtin_expect(__any(sn), 0)) {
-        if (sn) {
-          const uint32_t q = atomicAdd(a.side.cnt + 5, 1u);
-          if (q < a.side.cap_list) a.side.list[q] = i;
-          else atomicAdd(a.side.cnt + 6, 1u);
-        }
-      }
+      if (__builtin_expect(__any(sn), 0)) side_list_append(a.side, sn, i);
     }
     const bool sample = a.lat && !(a.flags & 2u) && (i & 15u) == 0 && !to_peer && !listed;
     const uint32_t lat_now = sample ? (uint32_t)(__builtin_amdgcn_s_memrealtime() - t0) : 0u;

@@ -351,13 +351,7 @@ __global__ __launch_bounds__(kRingBlock) void ring_kernel(RingArgs a) {
       // flood / mirror / ARP-trap / learning / tunnel packets go on the side list; the host runs
       // the side pass over them once the chunk's flag is seen (before the flag: vmcnt covers it)
       const bool sn = !pad && side_needed(st, p, e);
-      if (__builtin_expect(__any(sn), 0)) {
-        if (sn) {
-          const uint32_t q = atomicAdd(a.side.cnt + 5, 1u);
-          if (q < a.side.cap_list) a.side.list[q] = i;
-          else atomicAdd(a.side.cnt + 6, 1u);
-        }
-      }
+      if (__builtin_expect(__any(sn), 0)) side_list_append(a.side, sn, i);
     }
     NFDP_RING_MARK(tr3)
 

@@ -506,3 +506,19 @@ def traffic_vxlan(sc: Scenario, ports: dict, n: int, seed: int = 1, inner_len: i
     lens = np.full(n, L, np.uint32)
     slots, im, _ = P.wide_slots(fr, lens, ports["vtep"], wide_ports={ports["vtep"]})
     return slots, im, f
+
+
+def install_vxlan_egress(dp, sc: Scenario) -> dict:
+    """Every pod's VF becomes a VXLAN tunnel port (tunnel 0: local VTEP 192.0.2.1 -> remote
+    192.0.2.2, VNI 5000, out of an underlay VTEP port): the headline's traffic then leaves
+    encapsulated, so each forwarded packet also gets its outer-header record from the side pass.
+    Returns the underlay port."""
+    vtep = int(sc.pod_port.max()) + 1
+    dp.ports.set(vtep, flags=T.PORT_VALID, mac=VTEP_MAC)
+    dp.tunnels.set(0, src=str(ipaddress.IPv4Address(LOCAL_VTEP)), dst=str(ipaddress.IPv4Address(REMOTE_VTEP)),
+                   vni=VXLAN_VNI, out_port=vtep, smac=VTEP_MAC, dmac=UNDERLAY_GW_MAC)
+    for p in sc.pod_port:
+        dp.ports.a[int(p)]["flags"] |= np.uint32(T.PORT_TUNNEL)
+        dp.ports.a[int(p)]["lag"] = 0
+    dp.ports.version += 1
+    return {"underlay": vtep}

@@ -14,9 +14,15 @@ from dpu_operator_amd.dataplane.engine import DataPlane  # noqa: E402
 dev = torch.device("cuda", 0)
 dp = DataPlane(device="cuda:0", flow_buckets=1 << 19, hash_mode="lds", acl_mode="mfma")
 sc = S.build_sfc(dp, n_pods=8, n_flows=1 << 20, n_acl=256, seed=0)
-ports = S.install_vxlan(dp, sc)
-dp.commit(full=True)
-pk, im, _ = S.traffic_vxlan(sc, ports, 1 << 21, seed=1)
+egress = len(sys.argv) > 1 and sys.argv[1] == "egress"
+if egress:   # the headline's traffic leaving encapsulated (every packet on the side list)
+    S.install_vxlan_egress(dp, sc)
+    dp.commit(full=True)
+    pk, im = S.traffic(sc, 1 << 22, seed=1)
+else:
+    ports = S.install_vxlan(dp, sc)
+    dp.commit(full=True)
+    pk, im, _ = S.traffic_vxlan(sc, ports, 1 << 21, seed=1)
 src = (torch.from_numpy(pk).to(dev), torch.from_numpy(im.view(np.int32)).to(dev))
 work = [(src[0].clone(), src[1].clone()) for _ in range(12)]
 out, meta, lat = dp.alloc_batch(1 << 22)
@@ -28,4 +34,6 @@ for k in range(2, 12):
     dp.run(*work[k], out, meta, lat)
 torch.cuda.synchronize()
 el = (time.perf_counter() - t0) / 10
-print({"ms_per_step": round(el * 1e3, 4), "frames": 1 << 21, "mpps": round((1 << 21) / el / 1e6, 1)}, flush=True)
+nf = (1 << 22) if egress else (1 << 21)
+print({"mode": "egress" if egress else "terminate", "ms_per_step": round(el * 1e3, 4), "frames": nf,
+       "mpps": round(nf / el / 1e6, 1), "side": {k: v for k, v in dp.side_result().items() if k.startswith("n_")}}, flush=True)
