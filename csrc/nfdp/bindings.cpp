@@ -117,6 +117,8 @@ SideOut side_from(const py::object& o) {
   so.cnt = ptr<uint32_t>(d, "cnt");
   so.list = ptr<uint32_t>(d, "list"); so.cap_list = val<uint32_t>(d, "cap_list", 0);
   so.xhdr = ptr<uint32_t>(d, "xhdr");
+  so.blk_cnt = ptr<uint32_t>(d, "blk_cnt");              // per-workgroup regions (fused kernel)
+  so.nblk = so.blk_cnt ? val<uint32_t>(d, "blk_max", 0) : 0u;   // blk_cnt entries (the launcher's grid cap)
   if (!so.cnt) throw std::invalid_argument("side outputs need a 'cnt' buffer (4 x u32)");
   if (so.cap_rep && (!so.rep_hdr || !so.rep_meta || !so.rep_src)) throw std::invalid_argument("side: replica buffers missing");
   if (so.cap_learn && !so.learn) throw std::invalid_argument("side: learn buffer missing");
@@ -344,7 +346,8 @@ PYBIND11_MODULE(_nfdp, m) {
                          uintptr_t out_meta, uintptr_t flow_ctr, uintptr_t port_ctr, uintptr_t drop_ctr,
                          uintptr_t hashes, uintptr_t acl, py::object side) {
     TablesView t = tables_from(tables);
-    const SideOut so = side_from(side);
+    SideOut so = side_from(side);
+    so.blk_cnt = nullptr;       // standalone side pass / oracle: one flat list
     py::gil_scoped_release nogil;
     oracle_run(t, reinterpret_cast<const uint32_t*>(pkts), reinterpret_cast<const uint32_t*>(inmeta), n,
                reinterpret_cast<uint32_t*>(out), reinterpret_cast<uint32_t*>(out_meta),
@@ -673,6 +676,7 @@ PYBIND11_MODULE(_nfdp, m) {
         f.toep_frag = ptr<const void>(d, "toep_frag"); f.toep_tab = ptr<const uint32_t>(d, "toep_tab");
         f.flags = val<uint32_t>(d, "flags", 0);
         if (d.contains("side")) f.side = side_from(d["side"]);
+        f.side.blk_cnt = nullptr;   // the ring appends to one flat list
         if (f.side.cnt && (!f.side.list || f.side.cap_list < r.capacity()))
           throw std::invalid_argument("ring side list must hold a whole ring");
         if (!f.port_ctr || !f.drop_ctr) throw std::invalid_argument("ring start: null counters");
@@ -727,7 +731,8 @@ PYBIND11_MODULE(_nfdp, m) {
                           py::object side, uintptr_t port_ctr, uintptr_t drop_ctr, uintptr_t stream, uint32_t n_slots,
                           bool wrap) {
     const TablesView t = tables_from(tables);
-    const SideOut so = side_from(side);
+    SideOut so = side_from(side);
+    so.blk_cnt = nullptr;       // standalone side pass / oracle: one flat list
     check(launch_side(t, reinterpret_cast<const void*>(pkts), reinterpret_cast<const uint32_t*>(inmeta),
                       reinterpret_cast<const void*>(out), reinterpret_cast<const uint32_t*>(out_meta), so,
                       reinterpret_cast<unsigned long long*>(port_ctr), reinterpret_cast<unsigned long long*>(drop_ctr),
@@ -794,7 +799,8 @@ PYBIND11_MODULE(_nfdp, m) {
       .def("configure", [](OracleBackend& b, py::dict tables, uintptr_t flow_ctr, uintptr_t port_ctr, uintptr_t drop_ctr,
                            py::object side) {
         const TablesView t = tables_from(tables);
-        const SideOut so = side_from(side);
+        SideOut so = side_from(side);
+    so.blk_cnt = nullptr;       // standalone side pass / oracle: one flat list
         b.configure(t, reinterpret_cast<uint64_t*>(flow_ctr), reinterpret_cast<uint64_t*>(port_ctr),
                     reinterpret_cast<uint64_t*>(drop_ctr), so, const_cast<MacEntry*>(t.macs), t.mac_mask);
       })

@@ -565,6 +565,19 @@ __device__ __forceinline__ void wave_counter_add(unsigned long long* ctr, uint32
 
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 
+// Per-workgroup-region form (SideOut::blk_cnt): the wave's claim is an LDS atomic on the
+// workgroup's count, so no global atomic at all (a per-wave atomic on one global counter still
+// serialised 64K waves at the memory side when every packet is flagged: an overlay egress).
+__device__ __forceinline__ void side_list_append_blk(const SideOut& so, uint32_t* lds_n, bool sn, uint32_t i) {
+  const unsigned long long m = __ballot(sn);
+  const uint32_t pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+  const int leader = __builtin_ctzll(m);
+  uint32_t base = 0;
+  if (sn && pre == 0) base = atomicAdd(lds_n, (uint32_t)__builtin_popcountll(m));
+  base = __builtin_amdgcn_readlane(base, leader);
+  if (sn && base + pre < so.blk_cap) so.list[blockIdx.x * so.blk_cap + base + pre] = i;
+}
+
 // Wave-aggregated append to the side list (flagged lanes): ONE atomic on the list counter per wave
 // instead of one per lane (every lane of a wave adding to one counter word serialises at the
 // memory side; an overlay egress flags every packet for its outer header).  EXEC must be full.

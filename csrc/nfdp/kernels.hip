@@ -159,6 +159,7 @@ __global__ __launch_bounds__(kFB, EARLY ? NFDP_EARLY_WAVES_PER_EU : NFDP_FUSED_W
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ uint32_t rcnt[REMOTE ? 2 * kMaxRanks : 1], rbase[REMOTE ? kMaxRanks : 1];  // rcnt double-buffered
   __shared__ uint32_t lst_n;                                  // LIST: entries of this workgroup's region
+  __shared__ uint32_t side_n;                                 // side-list entries of this workgroup (regions)
   const LdsLayout L = lds_layout(HASH, ACL, a.acl_tiles, EARLY);
   v4i* lw = reinterpret_cast<v4i*>(smem + L.acl_w);
   v4i* lc = reinterpret_cast<v4i*>(smem + L.acl_c);
@@ -185,6 +186,7 @@ __global__ __launch_bounds__(kFB, EARLY ? NFDP_EARLY_WAVES_PER_EU : NFDP_FUSED_W
     if (threadIdx.x < 2 * kMaxRanks) rcnt[threadIdx.x] = 0;
   if constexpr (LIST)
     if (threadIdx.x == 0) lst_n = 0;
+  if (threadIdx.x == 0) side_n = 0;
   PortEntry* lport = reinterpret_cast<PortEntry*>(smem + L.tports);
   uint64_t* lchain = reinterpret_cast<uint64_t*>(smem + L.tchain);
   uint8_t* lperm = smem + L.tperm;
@@ -386,7 +388,12 @@ __global__ __launch_bounds__(kFB, EARLY ? NFDP_EARLY_WAVES_PER_EU : NFDP_FUSED_W
       // flood / mirror / ARP-trap / learning packets go on the side list (side_kernel emits their
       // replicas and learn events after this kernel): a wave-uniform skip in the common case
       const bool sn = valid && side_needed(st, p, e);
-      if (__builtin_expect(__any(sn), 0)) side_list_append(a.side, sn, i);
+      if (__builtin_expect(__any(sn), 0)) {
+        // (the LIST instances keep the flat list: their register budget has no room for the
+        // region form, and multi-GPU steering is where flagged packets are rare)
+        if constexpr (LIST) side_list_append(a.side, sn, i);
+        else side_list_append_blk(a.side, &side_n, sn, i);
+      }
     }
     const bool sample = a.lat && !(a.flags & 2u) && (i & 15u) == 0 && !to_peer && !listed;
     const uint32_t lat_now = sample ? (uint32_t)(__builtin_amdgcn_s_memrealtime() - t0) : 0u;
@@ -445,6 +452,13 @@ __global__ __launch_bounds__(kFB, EARLY ? NFDP_EARLY_WAVES_PER_EU : NFDP_FUSED_W
   }
   if (threadIdx.x < kNumReasons && drops[threadIdx.x])
     atomicAdd(a.drop_ctr + threadIdx.x, (unsigned long long)drops[threadIdx.x]);
+  if (!LIST && a.side.cnt && threadIdx.x == 0) {
+    // this workgroup's side-list region: its count for side_kernel, the batch total for the host
+    const uint32_t c = side_n;
+    a.side.blk_cnt[blockIdx.x] = c < a.side.blk_cap ? c : a.side.blk_cap;
+    if (c) atomicAdd(a.side.cnt + 5, c);
+    if (c > a.side.blk_cap) atomicAdd(a.side.cnt + 6, c - a.side.blk_cap);
+  }
   if constexpr (LIST) {
     if (threadIdx.x == 0) {
       a.steer_cnt[2 + blockIdx.x] = lst_n;
@@ -603,8 +617,14 @@ struct SideArgs {
   uint32_t wrap;      // 1: ring slots (the next slot wraps modulo n_slots)
 };
 __global__ __launch_bounds__(256) void side_kernel(SideArgs a) {
-  const uint32_t n = min(a.side.cnt[5], a.side.cap_list);
+  // flat list [0, cnt[5]) or the fused kernel's per-workgroup regions (blk_cnt[b] entries each)
+  const bool blk = a.side.blk_cnt != nullptr;
+  const uint32_t n = blk ? a.side.nblk * a.side.blk_cap : min(a.side.cnt[5], a.side.cap_list);
   for (uint32_t j = blockIdx.x * 256 + threadIdx.x; j < n; j += gridDim.x * 256) {
+    if (blk) {
+      const uint32_t r = j / a.side.blk_cap;
+      if (j - r * a.side.blk_cap >= a.side.blk_cnt[r]) continue;
+    }
     const uint32_t i = a.side.list[j];
     uint32_t d[kSlotDwords], o[kSlotDwords];
 #pragma unroll
@@ -957,6 +977,16 @@ static hipError_t launch_fused_t(const FusedArgs& a, int num_cus, hipStream_t s)
   if (need < grid) grid = need;
   if (grid == 0) return hipSuccess;
   FusedArgs b = a;
+  if (b.side.cnt && LS) b.side.blk_cnt = nullptr;   // LIST instances: one flat list
+  if (b.side.cnt && !LS) {
+    // side-list regions: a region holds every packet its workgroup's grid-stride loop visits, or
+    // its share of a smaller list (entries past it are counted as dropped, cnt[6])
+    if (!b.side.blk_cnt || grid > b.side.nblk) return hipErrorInvalidValue;
+    const uint64_t stride = (uint64_t)grid * kFB;
+    const uint64_t need = ((a.n + stride - 1) / stride) * kFB, share = b.side.cap_list / grid;
+    b.side.blk_cap = (uint32_t)(need < share ? need : share);
+    b.side.nblk = grid;
+  }
   if constexpr (LS) {
     // each workgroup's list region holds every packet its grid-stride loop visits
     const uint64_t stride = (uint64_t)grid * kFB;
@@ -967,7 +997,7 @@ static hipError_t launch_fused_t(const FusedArgs& a, int num_cus, hipStream_t s)
   hipLaunchKernelGGL((fused_kernel<H, A, R, E, LS, V6>), dim3(grid), dim3(kFB), lds, s, b);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || !a.side.cnt || a.side.cap_list == 0) return e;
-  return launch_side(a.t, a.pkts, a.inmeta, a.out, a.out_meta, a.side, a.port_ctr, a.drop_ctr, s, a.n, false);
+  return launch_side(a.t, a.pkts, a.inmeta, a.out, a.out_meta, b.side, a.port_ctr, a.drop_ctr, s, a.n, false);
 }
 
 hipError_t launch_side(const TablesView& t, const void* pkts, const uint32_t* inmeta, const void* out,

@@ -713,6 +713,12 @@ struct SideOut {
   uint32_t* list;                // packets flagged by the per-packet kernel for the side pass
   uint32_t cap_list;
   uint32_t* xhdr;                // [batch] x kXhdrBytes outer-header records of tunnel-encapsulated packets
+  // Per-workgroup regions (fused kernel; null blk_cnt: one flat list claimed with a global
+  // counter): workgroup b appends to list[b * blk_cap ...) with LDS claims and leaves its count in
+  // blk_cnt[b]; set by the launcher (blk_cap, nblk) when the list holds every region.
+  uint32_t* blk_cnt;
+  uint32_t blk_cap;
+  uint32_t nblk;
 };
 
 // Flow-table lookup (scalar).  Returns slot index or -1.

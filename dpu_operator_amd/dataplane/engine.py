@@ -501,12 +501,17 @@ class DataPlane:
             self._zeros("side_cnt", 8, np.uint32)
         # with tunnel ports every packet of a batch can need its outer-header record: the side list
         # holds the whole batch then (replicas keep their own cap)
-        if self._tunnels_on() and len(self._dev["side_list"]) < n:
-            self._zeros("side_list", n, np.uint32)
+        if len(self._dev["side_list"]) < n + 4 * self.num_cus * 512:
+            # every packet of a batch can need the side pass (tunnel encap, learning ports); the
+            # fused kernel's per-workgroup regions round each workgroup's share up to a block
+            self._zeros("side_list", n + 4 * self.num_cus * 512, np.uint32)
+        if "side_blk" not in self._dev:
+            self._zeros("side_blk", 4 * self.num_cus, np.uint32)   # region counts (<= 4 workgroups / CU)
         self._dev["side_cnt"][:] = 0
         return {"rep_hdr": self._ptr("side_hdr"), "rep_meta": self._ptr("side_meta"), "rep_src": self._ptr("side_src"),
                 "cap_rep": self.cap_rep, "learn": self._ptr("side_learn"), "cap_learn": self.cap_learn,
                 "cnt": self._ptr("side_cnt"), "list": self._ptr("side_list"), "cap_list": int(len(self._dev["side_list"])),
+                "blk_cnt": self._ptr("side_blk"), "blk_max": 4 * int(self.num_cus),
                 "xhdr": self._ptr("side_xhdr") if self._tunnels_on() else 0}
 
     def _apply_learn(self, stream=None) -> None:
