@@ -144,7 +144,7 @@ void esp_run_cpu(const EspBatch& a, bool enc);
 hipError_t launch_side(const TablesView& t, const void* pkts, const uint32_t* inmeta, const void* out,
                        const uint32_t* out_meta, const SideOut& side, unsigned long long* port_ctr,
                        unsigned long long* drop_ctr, hipStream_t s,
-                       uint32_t n_slots = 0, bool wrap = false);
+                       uint32_t n_slots = 0, bool wrap = false, const uint32_t* toep_tab = nullptr);
 size_t fused_lds_bytes(int hash_mode, int acl_mode, uint32_t acl_tiles);
 // Wide header pairs of a batch resolved in place (kernels.hip pair_kernel; launch_fused runs it
 // under launch flag 1 << 10).

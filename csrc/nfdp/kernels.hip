@@ -615,8 +615,25 @@ struct SideArgs {
   unsigned long long* port_ctr; unsigned long long* drop_ctr;
   uint32_t n_slots;   // slots of the batch / ring (0: no wide pairs); a pair's continuation is the next slot
   uint32_t wrap;      // 1: ring slots (the next slot wraps modulo n_slots)
+  const uint32_t* toep_tab;   // [16][256] Toeplitz byte tables (null: bit-by-bit hash)
+};
+// Toeplitz from byte tables staged in LDS (the side pass's tunnel entropy / flood LAG hash; the
+// bit-by-bit form was most of side_kernel's time with every packet encapsulated)
+struct LdsToeplitz {
+  const uint32_t* tab;
+  __device__ uint32_t operator()(const FlowKey& k) const {
+    const uint32_t w[4] = {k.src_ip, k.dst_ip, k.ports, k.meta};
+    uint32_t h = 0;
+#pragma unroll
+    for (int b = 0; b < 16; ++b) h ^= tab[b * 256 + ((w[b >> 2] >> (8 * (b & 3))) & 0xFFu)];
+    return h;
+  }
 };
 __global__ __launch_bounds__(256) void side_kernel(SideArgs a) {
+  __shared__ uint32_t stab[16 * 256];
+  if (a.toep_tab)
+    for (uint32_t q = threadIdx.x; q < 16 * 256; q += 256) stab[q] = a.toep_tab[q];
+  __syncthreads();
   // flat list [0, cnt[5]) or the fused kernel's per-workgroup regions (blk_cnt[b] entries each)
   const bool blk = a.side.blk_cnt != nullptr;
   const uint32_t n = blk ? a.side.nblk * a.side.blk_cap : min(a.side.cnt[5], a.side.cap_list);
@@ -655,7 +672,8 @@ __global__ __launch_bounds__(256) void side_kernel(SideArgs a) {
       }
     }
     GpuSideSink sk{a.side, a.port_ctr, a.drop_ctr};
-    side_stage(a.t, DirectTables{a.t}, d, im, o, a.out_meta[i], i, sk);
+    if (a.toep_tab) side_stage(a.t, DirectTables{a.t}, d, im, o, a.out_meta[i], i, sk, LdsToeplitz{stab});
+    else side_stage(a.t, DirectTables{a.t}, d, im, o, a.out_meta[i], i, sk);
   }
 }
 
@@ -997,16 +1015,17 @@ static hipError_t launch_fused_t(const FusedArgs& a, int num_cus, hipStream_t s)
   hipLaunchKernelGGL((fused_kernel<H, A, R, E, LS, V6>), dim3(grid), dim3(kFB), lds, s, b);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || !a.side.cnt || a.side.cap_list == 0) return e;
-  return launch_side(a.t, a.pkts, a.inmeta, a.out, a.out_meta, b.side, a.port_ctr, a.drop_ctr, s, a.n, false);
+  return launch_side(a.t, a.pkts, a.inmeta, a.out, a.out_meta, b.side, a.port_ctr, a.drop_ctr, s, a.n, false, a.toep_tab);
 }
 
 hipError_t launch_side(const TablesView& t, const void* pkts, const uint32_t* inmeta, const void* out,
                        const uint32_t* out_meta, const SideOut& side, unsigned long long* port_ctr,
-                       unsigned long long* drop_ctr, hipStream_t s, uint32_t n_slots, bool wrap) {
+                       unsigned long long* drop_ctr, hipStream_t s, uint32_t n_slots, bool wrap,
+                       const uint32_t* toep_tab) {
   if (!side.cnt || side.cap_list == 0) return hipSuccess;
   if (!pkts || !inmeta || !out || !out_meta || !side.list || !port_ctr || !drop_ctr) return hipErrorInvalidValue;
   SideArgs sa{t, reinterpret_cast<const uint4*>(pkts), inmeta, reinterpret_cast<const uint4*>(out), out_meta, side,
-              port_ctr, drop_ctr, n_slots, wrap ? 1u : 0u};
+              port_ctr, drop_ctr, n_slots, wrap ? 1u : 0u, toep_tab};
   const uint32_t sg = (side.cap_list + 255) / 256 < 512 ? (side.cap_list + 255) / 256 : 512;
   hipLaunchKernelGGL(side_kernel, dim3(sg), dim3(256), 0, s, sa);
   return hipGetLastError();

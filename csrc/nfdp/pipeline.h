@@ -7,6 +7,8 @@
 //   chain_stage   : built-in NF hops (ACL verdict, SNAT, TTL, L2 steer, VLAN, hairpin) or the
 //                   (bridge, dst-MAC) L2 table on a flow miss (K5); egress port tagging (K6)
 #pragma once
+#include <type_traits>
+
 #include "nfdp.h"
 
 namespace nfdp {
@@ -493,13 +495,24 @@ NFDP_HD bool side_needed(const IngressState& st, const Parsed& p, const EgressDe
          (!st.reason && ((st.in_flags & kPortLearn) || (p.arp && (st.in_flags & kPortArpTrap))));
 }
 
-template <class TA, class Sink>
+// The packet hash of the side pass (tunnel entropy port, flood LAG members): the Toeplitz hash of
+// the ingress key, bit by bit (the oracle) or from byte tables (side_kernel: LDS copies).
+struct ScalarToeplitz {
+  const uint8_t* rss_key;
+  NFDP_HD uint32_t operator()(const FlowKey& k) const { return toeplitz_scalar(k, rss_key); }
+};
+
+template <class TA, class Sink, class Hash = ScalarToeplitz>
 NFDP_HD void side_stage(const TablesView& t, const TA& ta, const uint32_t* d_in, uint32_t inmeta, const uint32_t* o,
-                        uint32_t ometa, uint32_t src, Sink& sink) {
+                        uint32_t ometa, uint32_t src, Sink& sink, Hash hasher = Hash{nullptr}) {
   Parsed p;
   IngressState st;
   ingress_stage(t, ta, d_in, inmeta, p, st);
   if (st.reason) return;
+  auto khash = [&]() -> uint32_t {
+    if constexpr (std::is_same<Hash, ScalarToeplitz>::value) return toeplitz_scalar(st.key, t.rss_key);
+    else return hasher(st.key);
+  };
   // MAC learning (OvS NORMAL): (bridge, src MAC) -> in_port when the table disagrees
   if (st.in_flags & kPortLearn) {
     const uint32_t lo = smac_lo(p.s), hi = smac_hi(p.s);
@@ -516,12 +529,12 @@ NFDP_HD void side_stage(const TablesView& t, const TA& ta, const uint32_t* d_in,
       uint32_t x[kXhdrBytes / 4];
       if ((pe.flags & kPortTunnel) && (pe.flags & kPortTunnel6)) {
         if (t.tunnels6 && pe.lag < t.n_tunnels6) {
-          make_outer6(t.tunnels6[pe.lag], meta_len(ometa) - kEncap6Bytes, toeplitz_scalar(st.key, t.rss_key), x);
+          make_outer6(t.tunnels6[pe.lag], meta_len(ometa) - kEncap6Bytes, khash(), x);
           sink.xhdr(x, src);
         }
       } else if ((pe.flags & kPortTunnel) && t.tunnels && pe.lag < t.n_tunnels) {
         for (int i = kSlotDwords; i < kXhdrBytes / 4; ++i) x[i] = 0;
-        make_outer(t.tunnels[pe.lag], meta_len(ometa) - kEncapBytes, toeplitz_scalar(st.key, t.rss_key), x);
+        make_outer(t.tunnels[pe.lag], meta_len(ometa) - kEncapBytes, khash(), x);
         sink.xhdr(x, src);
       }
     }
@@ -553,7 +566,7 @@ NFDP_HD void side_stage(const TablesView& t, const TA& ta, const uint32_t* d_in,
       uint32_t push = (st.in_flags & kPortIngressTag) ? 1u : 0u;
       uint32_t tci = push ? (st.in_ext & 0xFFFu) : 0u;
       uint32_t xh = 0;  // tunnel members are not flooded: remote MACs come from l2_to_tunnel entries
-      if (finish_port(t, ta, m, toeplitz_scalar(st.key, t.rss_key), push != 0, push, tci, p.len, &xh) != kOk || xh)
+      if (finish_port(t, ta, m, khash(), push != 0, push, tci, p.len, &xh) != kOk || xh)
         continue;
       uint32_t c[kSlotDwords];
       emit(p, tci, push != 0, c);
