@@ -210,6 +210,24 @@ def measure_variants(a, dp, sc, dev, torch, S, P) -> dict:
     dp.ports.clear(ports["vtep"])
     dp.commit()
     del b
+    # overlay egress: every pod VF a VXLAN tunnel port, so every forwarded packet also gets its
+    # outer-header record from the side pass (the headline's traffic, 4M packets per step)
+    eg = S.install_vxlan_egress(dp, sc)
+    dp.commit()
+    pk, im = S.traffic(sc, n, seed=9500)
+    b = [(torch.from_numpy(pk).to(dev), torch.from_numpy(im.view(np.int32)).to(dev))]
+    el, meta = _time_fused(dp, b, a.variant_steps, torch)
+    m = meta.cpu().numpy().view(np.uint32)
+    res["vxlan_egress_mpps"] = round(n * a.variant_steps / el / 1e6, 1)
+    res["vxlan_egress"] = {"forwarded_fraction": round(float(np.mean(P.meta_fields(m)[2] == 0)), 4),
+                           "encapsulated_fraction": round(float(np.mean(P.meta_xhdr(m))), 4),
+                           "note": "fused kernel + side pass (50-B outer-header record per packet)"}
+    for p_ in sc.pod_port:
+        dp.ports.a[int(p_)]["flags"] &= ~np.uint32(S.T.PORT_TUNNEL)
+    dp.ports.clear(eg["underlay"])
+    dp.ports.version += 1
+    dp.commit()
+    del b
     return res
 
 
@@ -592,6 +610,7 @@ def main() -> None:
             "value_l3": None if not variants else variants["l3_mpps"],
             "value_ipv6": None if not variants else variants["ipv6_mpps"],
             "value_vxlan": None if not variants else variants["vxlan_mpps"],
+            "value_vxlan_egress": None if not variants else variants["vxlan_egress_mpps"],
             "imix": None if not variants else variants["imix"],
             "variants": variants,
             # live pod -> pod through the native I/O engine + ring kernel (memif vports, 64-B frames)
