@@ -1026,7 +1026,9 @@ hipError_t launch_side(const TablesView& t, const void* pkts, const uint32_t* in
   if (!pkts || !inmeta || !out || !out_meta || !side.list || !port_ctr || !drop_ctr) return hipErrorInvalidValue;
   SideArgs sa{t, reinterpret_cast<const uint4*>(pkts), inmeta, reinterpret_cast<const uint4*>(out), out_meta, side,
               port_ctr, drop_ctr, n_slots, wrap ? 1u : 0u, toep_tab};
-  const uint32_t sg = (side.cap_list + 255) / 256 < 512 ? (side.cap_list + 255) / 256 : 512;
+  // grid for what the batch can put on the list (each workgroup stages the Toeplitz tables)
+  const uint32_t lim = n_slots && n_slots < side.cap_list ? n_slots : side.cap_list;
+  const uint32_t sg = (lim + 255) / 256 < 512 ? (lim + 255) / 256 : 512;
   hipLaunchKernelGGL(side_kernel, dim3(sg), dim3(256), 0, s, sa);
   return hipGetLastError();
 }
