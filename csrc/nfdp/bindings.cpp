@@ -812,14 +812,14 @@ PYBIND11_MODULE(_nfdp, m) {
       .def("add_port", &Engine::add_port)
       .def("remove_port", &Engine::remove_port)
       .def("port", &Engine::port)
-      .def("set_steering", [](Engine& e, py::buffer ports, py::bytes rss) {
+      .def("set_steering", [](Engine& e, py::buffer ports, py::bytes rss, bool v6) {
         py::buffer_info bi = ports.request();
         const size_t n = (size_t)bi.size * bi.itemsize / sizeof(PortEntry);
         std::vector<PortEntry> v(n);
         std::memcpy(v.data(), bi.ptr, n * sizeof(PortEntry));
         std::string k = rss;
-        e.set_steering(v, std::vector<uint8_t>(k.begin(), k.end()));
-      })
+        e.set_steering(v, std::vector<uint8_t>(k.begin(), k.end()), v6);
+      }, py::arg("ports"), py::arg("rss"), py::arg("v6") = false)
       .def("set_redirect", &Engine::set_redirect)
       .def("set_side_ports", &Engine::set_side_ports)
       .def("set_side_always", &Engine::set_side_always)
@@ -851,7 +851,7 @@ PYBIND11_MODULE(_nfdp, m) {
         return py::array_t<double>(v.size(), v.data());
       });
   m.def("owner_of_frames", [](py::array_t<uint8_t, py::array::c_style | py::array::forcecast> slots, U32Arr inmeta,
-                              py::buffer ports, py::bytes rss, uint32_t n) {
+                              py::buffer ports, py::bytes rss, uint32_t n, bool v6) {
     if (slots.ndim() != 2 || slots.shape(1) != kSlotBytes || inmeta.ndim() != 1 || inmeta.shape(0) != slots.shape(0))
       throw std::invalid_argument("owner_of_frames: slots [n, 64] u8, inmeta [n] u32");
     py::buffer_info bi = ports.request();
@@ -865,9 +865,9 @@ PYBIND11_MODULE(_nfdp, m) {
     const uint32_t* ip = inmeta.data();
     const auto* pt = static_cast<const PortEntry*>(bi.ptr);
     for (size_t i = 0; i < cnt; ++i)
-      o[i] = frame_owner(sp + i * kSlotBytes, ip[i] >> 16, ip[i] & 0xFFFFu, pt, reinterpret_cast<const uint8_t*>(k.data()), n);
+      o[i] = frame_owner(sp + i * kSlotBytes, ip[i] >> 16, ip[i] & 0xFFFFu, pt, reinterpret_cast<const uint8_t*>(k.data()), n, v6);
     return out;
-  });
+  }, py::arg("slots"), py::arg("inmeta"), py::arg("ports"), py::arg("rss"), py::arg("n"), py::arg("v6") = false);
   // pod side of a memif vport (tests / tools): frames in, frames out
   struct MemifEndpoint {
     std::unique_ptr<memif::Region> reg;

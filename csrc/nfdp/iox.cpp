@@ -435,12 +435,13 @@ std::shared_ptr<Port> Engine::port(uint32_t id) {
   return id < t->size() ? (*t)[id] : nullptr;
 }
 
-void Engine::set_steering(const std::vector<PortEntry>& ports, const std::vector<uint8_t>& rss_key) {
+void Engine::set_steering(const std::vector<PortEntry>& ports, const std::vector<uint8_t>& rss_key, bool v6) {
   if (run_ && !pause_) throw std::runtime_error("iox: set_steering while running (pause first)");
   if (rss_key.size() < 20) throw std::invalid_argument("iox: rss key too short");
   steer_ports_ = ports;
   steer_ports_.resize((size_t)kMaxPorts + 2);
   rss_key_ = rss_key;
+  steer_v6_ = v6;
 }
 
 void Engine::set_redirect(uint32_t port, uint32_t underlay) {
@@ -459,17 +460,18 @@ bool Engine::needs_side(uint32_t in_port) const {
 }
 
 uint32_t frame_owner(const uint8_t* hdr, uint32_t len, uint32_t in_port, const PortEntry* ports, const uint8_t* rss_key,
-                     uint32_t n) {
+                     uint32_t n, bool v6) {
   if (n <= 1) return 0;
   if (!ports || !rss_key) return in_port % n;
   uint32_t d[kSlotDwords] = {};
   std::memcpy(d, hdr, std::min<uint32_t>(len, kSlotBytes));
   TablesView tv{};
   tv.ports = ports;
+  tv.flow6_on = v6 ? 1u : 0u;   // IPv6 keys folded as the owners' tables hold them
   Parsed p;
   IngressState st;
   ingress_stage(tv, DirectTables{tv}, d, (in_port & 0xFFFFu) | (std::min<uint32_t>(len, kMaxFrame) << 16), p, st);
-  if (!st.reason && p.ipv4) return owner_of(toeplitz_scalar(st.key, rss_key), n);
+  if (!st.reason && (p.ipv4 || (v6 && p.ipv6))) return owner_of(toeplitz_scalar(st.key, rss_key), n);
   return in_port % n;
 }
 
@@ -477,7 +479,7 @@ uint32_t Engine::owner_of_frame(const uint8_t* f, uint32_t len, uint32_t in_port
   const uint32_t n = (uint32_t)lanes_.size();
   if (n <= 1) return 0;
   if (steer_ports_.empty() || rss_key_.empty()) return in_port % n;
-  return frame_owner(f, len, in_port, steer_ports_.data(), rss_key_.data(), n);
+  return frame_owner(f, len, in_port, steer_ports_.data(), rss_key_.data(), n, steer_v6_);
 }
 
 void Engine::start() {

@@ -41,8 +41,10 @@ namespace iox {
 // Owner GPU of a frame (RSS): owner_of(toeplitz(FlowKey), n) for IPv4 frames the ingress stage
 // accepts (the key the flow table is sharded by), in_port % n otherwise.  `hdr` holds the first
 // min(len, 64) bytes; `ports` is the port table (kMaxPorts rows).
+// `v6`: the data planes keep IPv6 flows / rules, so an IPv6 frame's owner is its folded 5-tuple's
+// (the key the owner's table holds); otherwise IPv6 steers by ingress port.
 uint32_t frame_owner(const uint8_t* hdr, uint32_t len, uint32_t in_port, const PortEntry* ports, const uint8_t* rss_key,
-                     uint32_t n);
+                     uint32_t n, bool v6 = false);
 
 // ---------------------------------------------------------------------------------- ports
 struct RxRef {
@@ -284,7 +286,7 @@ class Engine {
   std::shared_ptr<Port> remove_port(uint32_t id);
   std::shared_ptr<Port> port(uint32_t id);
   // Host-side steering inputs (N > 1): a copy of the port table and the RSS key.
-  void set_steering(const std::vector<PortEntry>& ports, const std::vector<uint8_t>& rss_key);
+  void set_steering(const std::vector<PortEntry>& ports, const std::vector<uint8_t>& rss_key, bool v6 = false);
   void set_redirect(uint32_t port, uint32_t underlay);   // tunnel port -> its underlay port
   void set_side_ports(const std::vector<uint32_t>& ports); // ingress ports whose packets may need side work
   void set_side_always(bool on) { side_always_.store(on); }
@@ -346,6 +348,7 @@ class Engine {
   std::vector<uint8_t> side_ports_;
   std::atomic<bool> side_always_{false};
   std::vector<PortEntry> steer_ports_;
+  bool steer_v6_ = false;
   std::vector<uint8_t> rss_key_;
   std::atomic<bool> run_{false}, pause_{false}, paused_ack_{false};
   std::thread rx_th_;

@@ -148,7 +148,27 @@ class MultiDataPlane:
         return np.asarray(nfdp().owner_of_frames(np.ascontiguousarray(pkts, np.uint8),
                                                  np.ascontiguousarray(inmeta, np.uint32),
                                                  np.ascontiguousarray(self.ports.a), bytes(self.flows.rss_key),
-                                                 self.n), np.int64)
+                                                 self.n, self._v6_keys()), np.int64)
+
+    def _v6_keys(self) -> bool:
+        return any(p._v6_keys() for p in self.planes)
+
+    # ------------------------------------------------------------------ IPv6 flows
+    def add_flow6(self, src, dst, sport: int = 0, dport: int = 0, proto: int = 17, zone: int = 0, action=None) -> int:
+        """An IPv6 flow on its owner GPU (the Toeplitz owner of its folded key: where owners()
+        and the native engine steer its frames)."""
+        from . import tables as T2
+
+        key, _ = T2.flow_key6(src, dst, sport, dport, proto, zone)
+        g = int(self.flows.owner(key[None, :])[0])
+        return self.planes[g].add_flow6(src, dst, sport, dport, proto, zone, action)
+
+    def remove_flow6(self, src, dst, sport: int = 0, dport: int = 0, proto: int = 17, zone: int = 0) -> bool:
+        from . import tables as T2
+
+        key, _ = T2.flow_key6(src, dst, sport, dport, proto, zone)
+        g = int(self.flows.owner(key[None, :])[0])
+        return self.planes[g].remove_flow6(src, dst, sport, dport, proto, zone)
 
     def run(self, pkts, inmeta, **kw) -> BatchResult:
         """A batch split by owner, each part through its GPU, results back in arrival order

@@ -204,7 +204,8 @@ class NativeLivePath:
             if lag < len(tab.a):
                 eng.set_redirect(int(i), int(tab.a[lag]["out_port"]))
         if len(self.dps) > 1:
-            eng.set_steering(np.ascontiguousarray(a), bytes(dp0.rss_key))
+            v6 = any(d._v6_keys() for d in self.dps)   # IPv6 frames steer by their folded 5-tuple
+            eng.set_steering(np.ascontiguousarray(a), bytes(dp0.rss_key), v6)
 
     # ------------------------------------------------------------------ ports
     def add_port(self, idx: int, spec) -> None:

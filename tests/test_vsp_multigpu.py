@@ -171,3 +171,43 @@ def test_vsp_two_gpus_native_path(shm):
         assert all(int(p.port_counters()[0, 0]) > 0 for p in vsp.dp.planes)
     finally:
         vsp.stop()
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_ipv6_flows_sharded_match_one_plane(n):
+    """IPv6 flows on a multi-GPU plane: each lands on the owner of its folded 5-tuple, frames are
+    steered by the same hash (owners() / the native engine with v6 steering), and the dual-stack
+    result equals one plane holding every flow."""
+    from dpu_operator_amd.dataplane import tables as T
+
+    def v6flows(dp):
+        for i in range(64):
+            dp.add_flow6(f"fd00::{i + 1:x}", f"fd00::{(i * 7) % 50 + 100:x}", 1000 + i, 80, 17, 1,
+                         T.flow_action(chain_id=1, out_port=i % 6, flow_id=i)[0])
+
+    m = MultiDataPlane(["cpu"] * n, flow_buckets=1 << 12)
+    sc = S.build_sfc(m, n_pods=6, n_flows=4000, n_acl=32, seed=0)
+    v6flows(m)
+    m.acl.add(permit=False, dst="fd00::80/124", family=6)
+    m.commit(full=True)
+    ref = DataPlane("cpu", flow_buckets=1 << 13)
+    S.build_sfc(ref, n_pods=6, n_flows=4000, n_acl=32, seed=0)
+    v6flows(ref)
+    ref.acl.add(permit=False, dst="fd00::80/124", family=6)
+    ref.commit(full=True)
+    assert sum(len(p.flows6) for p in m.planes) == 64 and sum(1 for p in m.planes if p.flows6) > 1
+    frames = []
+    for i in range(64):
+        fr, ln = P.craft6_full(1, dmac=S.GW_MAC, smac=S.pod_mac(i % 6), src6=f"fd00::{i + 1:x}",
+                               dst6=f"fd00::{(i * 7) % 50 + 100:x}", sport=1000 + i, dport=80, frame_len=62)
+        t = np.zeros(66, np.uint8)
+        t[:12], t[12:14], t[14:16], t[16:] = fr[0, :12], (0x81, 0), (0, (i % 6) + 2), fr[0, 12:]
+        frames.append(t)
+    s6 = P.header_slots(np.stack(frames), np.full(64, 66, np.uint32))
+    i6 = P.inmeta(sc.pod_port[np.arange(64) % 6], np.full(64, 66, np.uint32))
+    pk4, im4 = S.traffic(sc, 512, seed=3)
+    pk, im = np.concatenate([pk4, s6]), np.concatenate([im4, i6])
+    r, rr = m.run(pk, im), ref.run(pk, im)
+    assert np.array_equal(r.meta, rr.meta) and np.array_equal(r.out, rr.out)
+    _, _, rs = P.meta_fields(r.meta[512:])
+    assert (rs == 0).sum() > 40 and (rs == 4).sum() >= 1      # IPv6 flows hit; the /124 deny applies
