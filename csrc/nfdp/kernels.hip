@@ -322,7 +322,7 @@ __global__ __launch_bounds__(kFB, EARLY ? NFDP_EARLY_WAVES_PER_EU : NFDP_FUSED_W
       }
     }
 #ifndef NFDP_ABL_NO_CHAIN
-    const EgressDecision e = chain_stage(a.t, ta, p, st, hit, act, acl_rule, hash);
+    const EgressDecision e = chain_stage<LdsTables, V6>(a.t, ta, p, st, hit, act, acl_rule, hash);
 #else  // cost attribution only (wrong results): no chain, the flow's port
     EgressDecision e{};
     e.out_port = hit ? act.out_port : kPortNone;

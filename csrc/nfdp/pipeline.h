@@ -275,7 +275,11 @@ NFDP_HD uint32_t route_ipv6(const TablesView& t, Parsed& p, uint32_t& out_port) 
 
 // `hit`: flow entry found; `act`: its action; `acl_rule`: first matching ACL rule or -1;
 // `hash`: the packet's Toeplitz hash (LAG member selection uses hash[2:0], K8).
-template <class TA>
+// V6HOPS: the ttl hop also decrements an IPv6 hop limit.  A hop runs only on a flow hit and an
+// IPv6 packet hits a flow only with IPv6 features in the tables, i.e. in the kernels' V6
+// instances, so the IPv4-only instances compile it out (their register budget) with the same
+// results as the oracle, which always has it.
+template <class TA, bool V6HOPS = true>
 NFDP_HD EgressDecision chain_stage(const TablesView& t, const TA& ta, Parsed& p, const IngressState& st,
                                    bool hit, const FlowAction& act, int acl_rule, uint32_t hash) {
   EgressDecision e;
@@ -398,6 +402,11 @@ NFDP_HD EgressDecision chain_stage(const TablesView& t, const TA& ta, Parsed& p,
         }
       } else if (op == kHopTtl) {
         if (p.ipv4 && !act_ttl(p)) { e.reason = kTtlExpired; e.out_port = kPortNone; return e; }
+        if (V6HOPS && NFDP_IPV6 && p.ipv6) {   // hop limit - 1 (no IPv6 header checksum)
+          const uint32_t hl = byte_at(p.s, 21);
+          if (hl <= 1u) { e.reason = kTtlExpired; e.out_port = kPortNone; return e; }
+          p.s[5] = (p.s[5] & ~(0xFFu << 8)) | ((hl - 1u) << 8);
+        }
       } else if (op == kHopHairpin) {
         e.out_port = st.in_port;
         const uint32_t dl = dmac_lo(p.s), dh = dmac_hi(p.s);

@@ -52,11 +52,11 @@ def _colliding_addr(addr: str) -> str:
     return str(ipaddress.IPv6Address(np.array(w2, "<u4").tobytes()))
 
 
-def _plane(device, nflows=64, seed=0):
+def _plane(device, nflows=64, seed=0, hops=("acl", "l2fwd")):
     dp = DataPlane(device=device, flow_buckets=1 << 10)
     for p in POD_MAC:
         dp.ports.set(p, flags=T.PORT_VALID, bridge_id=BRIDGE, mac=POD_MAC[p], peer_mac=PEER_MAC[p])
-    chain = dp.chains.add(["acl", "l2fwd"])
+    chain = dp.chains.add(list(hops))
     # IPv6 ACL: deny one /32, deny TCP dport 22, permit the rest of fd00::/8 explicitly
     dp.acl.add(permit=False, dst="fd00:bad::/32")
     dp.acl.add(permit=False, proto=6, dport=22, family=6)
@@ -324,3 +324,41 @@ def test_ipv6_flows_ring_kernel_bit_exact(coop):
     g.harvest()
     c.harvest()
     assert np.array_equal(g.flow_totals, c.flow_totals)
+
+
+def _hop_limits(slots, every=5):
+    s = slots.copy()
+    s[::every, 21] = 1          # (UDP checksum does not cover the hop limit)
+    return s
+
+
+def test_ipv6_ttl_hop_decrements_hop_limit():
+    """The chain's ttl hop on an IPv6 flow: hop limit - 1, or ttl_expired at 1."""
+    dp, flows = _plane("cpu", hops=("acl", "ttl", "l2fwd"))
+    slots, im, pk = _trace(flows, n=256)
+    slots = _hop_limits(slots)
+    r = dp.run(slots, im)
+    port, _, reason = P.meta_fields(r.meta)
+    exp = _expect(dp, flows, pk)
+    for j, (er, _) in enumerate(exp):
+        if er != 0:
+            continue
+        if slots[j, 21] == 1:
+            assert int(reason[j]) == 8
+        else:
+            assert int(reason[j]) == 0 and r.out[j, 21] == slots[j, 21] - 1
+
+
+@pytest.mark.gpu
+def test_ipv6_ttl_hop_gpu_bit_exact():
+    import torch
+
+    (c, flows), (g, _) = _plane("cpu", hops=("acl", "ttl", "l2fwd")), _plane("cuda", hops=("acl", "ttl", "l2fwd"))
+    slots, im, _ = _trace(flows, n=4096, seed=6)
+    slots = _hop_limits(slots)
+    rc = c.run(slots, im)
+    r = g.run(torch.from_numpy(slots).cuda(), torch.from_numpy(im.view(np.int32)).cuda())
+    torch.cuda.synchronize()
+    assert np.array_equal(r.meta.cpu().numpy().view(np.uint32), rc.meta)
+    assert np.array_equal(r.out.cpu().numpy(), rc.out)
+    assert (P.meta_fields(rc.meta)[2] == 8).sum() > 100
