@@ -483,10 +483,14 @@ __global__ __launch_bounds__(256) void pair_kernel(uint4* pkts, uint32_t* inmeta
   // stores an unmodified slot, so nothing races with that write.  Block-uniform trips; the VTEP rx
   // count is tallied per workgroup (every pair of a VTEP port adding to one counter word
   // serialised at the memory side: 25 ms per 2M pairs, r3 s23 trace).
+  // The tile's 16-B chunks are XOR-swizzled per group of 4 slots (chunk q of slot s at 4s + (q ^
+  // (s >> 2 & 3))): a lane reading its own 64-B slot otherwise hits the banks of lanes 4, 8, 12 on.
   __shared__ uint4 tile[4][256];
   __shared__ uint32_t vpk[kLdsPorts], vby[kLdsPorts];   // VTEP rx counts of this workgroup (ports < 256)
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   uint4* T = tile[wv];
+  const uint32_t lsw = (lane >> 4) & 3u;   // swizzle of linear chunk q*64 + lane
+  auto at = [](uint32_t s, int q) { return 4u * s + ((uint32_t)q ^ ((s >> 2) & 3u)); };
   for (uint32_t q = threadIdx.x; q < kLdsPorts; q += 256) { vpk[q] = 0; vby[q] = 0; }
   __syncthreads();
   const __amdgpu_buffer_rsrc_t r_pk = __builtin_amdgcn_make_buffer_rsrc((void*)pkts, (short)0, (int)(n * 64u), kBufCfg);
@@ -496,7 +500,7 @@ __global__ __launch_bounds__(256) void pair_kernel(uint4* pkts, uint32_t* inmeta
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const v4u c = __builtin_amdgcn_raw_buffer_load_b128(r_pk, lane * 16u + q * 1024u, soff, 0);
-      T[q * 64 + lane] = make_uint4(c.x, c.y, c.z, c.w);
+      T[(q * 64 + lane) ^ lsw] = make_uint4(c.x, c.y, c.z, c.w);
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
@@ -512,8 +516,8 @@ __global__ __launch_bounds__(256) void pair_kernel(uint4* pkts, uint32_t* inmeta
         in_tile = lane > 0;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const uint4 v = in_tile ? T[4 * (lane - 1) + q] : pkts[(size_t)(i - 1) * 4 + q];
-          const uint4 w = T[4 * lane + q];
+          const uint4 v = in_tile ? T[at(lane - 1, q)] : pkts[(size_t)(i - 1) * 4 + q];
+          const uint4 w = T[at(lane, q)];
           d[4 * q] = v.x; d[4 * q + 1] = v.y; d[4 * q + 2] = v.z; d[4 * q + 3] = v.w;
           x[4 * q] = w.x; x[4 * q + 1] = w.y; x[4 * q + 2] = w.z; x[4 * q + 3] = w.w;
         }
@@ -522,7 +526,7 @@ __global__ __launch_bounds__(256) void pair_kernel(uint4* pkts, uint32_t* inmeta
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             const uint4 o = make_uint4(inner[4 * q], inner[4 * q + 1], inner[4 * q + 2], inner[4 * q + 3]);
-            if (in_tile) T[4 * (lane - 1) + q] = o;
+            if (in_tile) T[at(lane - 1, q)] = o;
             else pkts[(size_t)(i - 1) * 4 + q] = o;
           }
           inmeta[i - 1] = (uint32_t)tp | (((him >> 16) - strip) << 16);
@@ -539,7 +543,7 @@ __global__ __launch_bounds__(256) void pair_kernel(uint4* pkts, uint32_t* inmeta
     if (mod) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        const uint4 v = T[q * 64 + lane];
+        const uint4 v = T[(q * 64 + lane) ^ lsw];
         const v4u w = {v.x, v.y, v.z, v.w};
         const bool keep = (mod >> (16u * q + (lane >> 2))) & 1ull;   // chunk q*64+lane is part of slot 16q + lane/4
         __builtin_amdgcn_raw_buffer_store_b128(w, r_pk, keep ? lane * 16u + q * 1024u : kNoRun, soff, 0);
@@ -549,8 +553,22 @@ __global__ __launch_bounds__(256) void pair_kernel(uint4* pkts, uint32_t* inmeta
     if (count) {
       // per-workgroup LDS tallies, one global atomic per port per workgroup at the end (a
       // per-wave atomic on the VTEP port's counter word still serialised 64K waves at the memory
-      // side: 0.81 ms per 4M slots, r3 s27 trace)
-      if (term && vport < (uint32_t)kLdsPorts) { atomicAdd(&vpk[vport], 1u); atomicAdd(&vby[vport], vlen); }
+      // side: 0.81 ms per 4M slots, r3 s27 trace).  A wave whose pairs all sit on one VTEP port
+      // (the usual case) adds its sums with one LDS atomic each: 64 lanes on one word serialise.
+      const bool tv = term && vport < (uint32_t)kLdsPorts;
+      const unsigned long long tb = __ballot(tv);
+      if (tb) {
+        const int lead = __builtin_ctzll(tb);
+        const uint32_t p0 = __shfl(vport, lead);
+        if (!__ballot(tv && vport != p0)) {
+          uint32_t sum = tv ? vlen : 0u;
+#pragma unroll
+          for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+          if ((int)lane == lead) { atomicAdd(&vpk[p0], (uint32_t)__popcll(tb)); atomicAdd(&vby[p0], sum); }
+        } else if (tv) {
+          atomicAdd(&vpk[vport], 1u); atomicAdd(&vby[vport], vlen);
+        }
+      }
       wave_counter_add(port_ctr, 2 * vport, vlen, true, term && vport >= (uint32_t)kLdsPorts);
     }
   }
