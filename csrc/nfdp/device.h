@@ -645,17 +645,23 @@ __device__ __forceinline__ void wave_frames_load(__amdgpu_buffer_rsrc_t r, uint3
   for (int q = 0; q < 4; ++q) c[q] = __builtin_amdgcn_raw_buffer_load_b128(r, lane * 16u + q * 1024u, run, AUX);
 }
 
+// SW: the 16 slots of a pass sit in kx with their 16-B chunks XOR-swizzled per group of 4 slots
+// (chunk k of slot s at 4s + (k ^ (s >> 2 & 3))): 16 lanes reading their own 64-B slot otherwise
+// hit the banks of lanes 4, 8 and 12 (4-way conflicts).  Off in the fused kernel, whose register
+// allocation the extra addressing pushes from 17 to 35 spilled VGPRs.
+template <bool SW = false>
 __device__ __forceinline__ void wave_frames_to_lanes(uint4* kx, const v4u c[4], uint32_t* d) {
   const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t lw = SW ? lane ^ ((lane >> 4) & 3u) : lane, sw = SW ? (lane >> 2) & 3u : 0u;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    kx[lane] = make_uint4(c[q].x, c[q].y, c[q].z, c[q].w);
+    kx[lw] = make_uint4(c[q].x, c[q].y, c[q].z, c[q].w);
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     if ((lane >> 4) == (uint32_t)q) {
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        const uint4 v = kx[4u * (lane & 15u) + k];
+        const uint4 v = kx[4u * (lane & 15u) + ((uint32_t)k ^ sw)];
         d[4 * k] = v.x; d[4 * k + 1] = v.y; d[4 * k + 2] = v.z; d[4 * k + 3] = v.w;
       }
     }

@@ -896,7 +896,7 @@ __global__ __launch_bounds__(256) void v6_kernel(V6Args a) {
     {
       v4u cn[4];
       wave_frames_load<0>(r_pk, base + wave0 < a.n ? (base + wave0) * 64u : kNoRun, cn);
-      wave_frames_to_lanes(kx, cn, d);
+      wave_frames_to_lanes<true>(kx, cn, d);
     }
     Parsed p;
     IngressState st;
