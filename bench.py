@@ -58,7 +58,9 @@ def parse():
     ap.add_argument("--no-lowlat", action="store_true", help="skip the small-batch latency probe")
     ap.add_argument("--no-variants", action="store_true", help="skip the mixed / ACL1024 / IMIX measurements")
     ap.add_argument("--no-live", action="store_true", help="skip the live pod-to-pod (native I/O engine) block")
-    ap.add_argument("--live-workers", type=int, default=8, help="native I/O engine delivery threads")
+    ap.add_argument("--live-workers", type=int, default=1, help="native I/O engine delivery threads per queue")
+    ap.add_argument("--live-queues", type=int, default=4, help="native I/O engine rx queues (threads)")
+    ap.add_argument("--live-gen-threads", type=int, default=4, help="pod traffic generator threads")
     ap.add_argument("--variant-steps", type=int, default=30)
     ap.add_argument("--chunks", type=int, default=4, help="pipeline chunks per step (N > 1)")
     ap.add_argument("--mode", default="rss", choices=["rss", "replicated", "sharded"],
@@ -562,7 +564,8 @@ def main() -> None:
             lb = importlib.util.module_from_spec(spec)
             spec.loader.exec_module(lb)
             live = lb.run(device=str(dev), n_pods=a.pods_per_gpu, flows=a.flows, n_acl=a.acl, duration=0.5,
-                          threads=6, tx_workers=a.live_workers, hash_mode=a.hash)
+                          threads=a.live_gen_threads, tx_workers=a.live_workers, queues=a.live_queues,
+                          hash_mode=a.hash)
         except Exception as ex:  # the headline number must still be reported
             live = {"error": str(ex)[:200]}
 

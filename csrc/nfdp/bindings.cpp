@@ -646,13 +646,15 @@ PYBIND11_MODULE(_nfdp, m) {
   // Persistent ring kernel (low-latency path): the host publishes 64-packet chunks, resident
   // waves process them as they appear, completion flags come back through pinned host memory.
   py::class_<RingEngine>(m, "RingEngine")
-      .def(py::init<uint32_t, int, int, bool, bool>(), py::arg("capacity"), py::arg("num_cus"),
-           py::arg("wgs_per_cu") = 1, py::arg("coop") = true, py::arg("host_slots") = false)
+      .def(py::init<uint32_t, int, int, bool, bool, uint32_t>(), py::arg("capacity"), py::arg("num_cus"),
+           py::arg("wgs_per_cu") = 1, py::arg("coop") = true, py::arg("host_slots") = false, py::arg("queues") = 1)
+      .def_property_readonly("queues", &RingEngine::queues)
       .def_property_readonly("host_slots", &RingEngine::host_slots)
       .def_property_readonly("capacity", &RingEngine::capacity)
       .def_property_readonly("running", &RingEngine::running)
       .def("alive", &RingEngine::alive)
-      .def_property_readonly("published", &RingEngine::published)
+      .def_property_readonly("published", [](const RingEngine& r) { return r.published(0); })
+      .def("published_q", &RingEngine::published, py::arg("q") = 0)
       .def("dev_in", [](RingEngine& r) { return reinterpret_cast<uintptr_t>(r.dev_in()); })
       .def("dev_inmeta", [](RingEngine& r) { return reinterpret_cast<uintptr_t>(r.dev_inmeta()); })
       .def("dev_out", [](RingEngine& r) { return reinterpret_cast<uintptr_t>(r.dev_out()); })
@@ -701,6 +703,7 @@ PYBIND11_MODULE(_nfdp, m) {
       .def_property_readonly("table_set", &RingEngine::table_set)
       .def_property_readonly("lds_acl_tiles", &RingEngine::lds_acl_tiles)
       .def("flip", &RingEngine::flip)
+      .def("change_epoch", &RingEngine::change_epoch, py::arg("flow"), py::arg("set"))
       .def("bump_epoch", &RingEngine::bump_epoch)
       .def("grace_over", &RingEngine::grace_over)
       .def("wait_grace", [](RingEngine& r, double timeout_s) {
@@ -711,12 +714,12 @@ PYBIND11_MODULE(_nfdp, m) {
       .def("set_epoch", &RingEngine::set_epoch)
       .def("stop", [](RingEngine& r, double timeout_s) { py::gil_scoped_release nogil; r.stop(timeout_s); },
            py::arg("timeout_s") = 30.0)
-      .def("completed", &RingEngine::completed)
-      .def("publish", &RingEngine::publish, py::arg("n"), py::arg("check_room") = true)
-      .def("wait", [](RingEngine& r, uint64_t end, double timeout_s) {
+      .def("completed", &RingEngine::completed, py::arg("q") = 0)
+      .def("publish", &RingEngine::publish, py::arg("n"), py::arg("check_room") = true, py::arg("q") = 0)
+      .def("wait", [](RingEngine& r, uint64_t end, double timeout_s, uint32_t q) {
         py::gil_scoped_release nogil;
-        return r.wait(end, timeout_s);
-      })
+        return r.wait(end, timeout_s, q);
+      }, py::arg("end"), py::arg("timeout_s") = 10.0, py::arg("q") = 0)
       .def("probe", [](RingEngine& r, uint32_t batches, uint32_t batch, uint32_t inflight) {
         double el = 0;
         std::vector<double> v;
@@ -790,28 +793,78 @@ PYBIND11_MODULE(_nfdp, m) {
       .def(py::init<int, uint32_t, uint32_t>(), py::arg("fd"), py::arg("nbufs") = 256, py::arg("buf_size") = 9728);
   py::class_<Backend, std::shared_ptr<Backend>>(m, "IoBackend")
       .def_property_readonly("capacity", &Backend::capacity)
-      .def("published", &Backend::published)
-      .def("completed", &Backend::completed);
+      .def_property_readonly("queues", &Backend::queues)
+      .def("published", &Backend::published, py::arg("q") = 0);
   py::class_<GpuBackend, Backend, std::shared_ptr<GpuBackend>>(m, "GpuBackend")
       .def(py::init<RingEngine*>(), py::arg("ring"), py::keep_alive<1, 2>());
   py::class_<OracleBackend, Backend, std::shared_ptr<OracleBackend>>(m, "OracleBackend")
-      .def(py::init<uint32_t>(), py::arg("capacity"))
-      .def("configure", [](OracleBackend& b, py::dict tables, uintptr_t flow_ctr, uintptr_t port_ctr, uintptr_t drop_ctr,
-                           py::object side) {
+      .def(py::init<uint32_t, uint32_t>(), py::arg("capacity"), py::arg("queues") = 1)
+      .def("configure", [](OracleBackend& b, py::dict tables, uintptr_t flow_ctr, uintptr_t port_ctr, uintptr_t drop_ctr) {
         const TablesView t = tables_from(tables);
-        SideOut so = side_from(side);
-    so.blk_cnt = nullptr;       // standalone side pass / oracle: one flat list
         b.configure(t, reinterpret_cast<uint64_t*>(flow_ctr), reinterpret_cast<uint64_t*>(port_ctr),
-                    reinterpret_cast<uint64_t*>(drop_ctr), so, const_cast<MacEntry*>(t.macs), t.mac_mask);
-      })
-      .def_readwrite("stamp", &OracleBackend::stamp);
+                    reinterpret_cast<uint64_t*>(drop_ctr), const_cast<MacEntry*>(t.macs), t.mac_mask);
+      });
+  // host snapshot of the side pass's tables: host arrays (numpy) copied at construction
+  py::class_<SideTables, std::shared_ptr<SideTables>>(m, "SideTables")
+      .def(py::init([](py::buffer ports, py::buffer macs, uint32_t mac_mask, py::buffer lag, uint32_t n_lag_groups,
+                       py::buffer flood, uint32_t n_flood, py::buffer tunnels, uint32_t n_tunnels, py::buffer tunnels6,
+                       uint32_t n_tunnels6, py::bytes rss, bool v6) {
+        auto req = [](py::buffer& b, size_t elem, size_t need, const char* what) {
+          py::buffer_info bi = b.request();
+          const size_t bytes = (size_t)bi.size * bi.itemsize;
+          if (bytes < need * elem) throw std::invalid_argument(std::string("SideTables: ") + what + " too small");
+          return std::make_pair(bi.ptr, bytes / elem);
+        };
+        SideTables::Src src{};
+        auto pp = req(ports, sizeof(PortEntry), 1, "ports");
+        src.ports = static_cast<const PortEntry*>(pp.first); src.n_ports = pp.second;
+        auto mp = req(macs, sizeof(MacEntry), (size_t)mac_mask + 1, "macs");
+        src.macs = static_cast<const MacEntry*>(mp.first); src.mac_mask = mac_mask;
+        auto lp = req(lag, 2, (size_t)n_lag_groups * kLagWays, "lag");
+        src.lag = static_cast<const uint16_t*>(lp.first); src.n_lag_groups = n_lag_groups;
+        auto fp = req(flood, 2, (size_t)n_flood * kFloodWays, "flood");
+        src.flood = static_cast<const uint16_t*>(fp.first); src.flood_rows = fp.second / kFloodWays; src.n_flood = n_flood;
+        if (src.flood_rows > kFloodMaxRows) throw std::invalid_argument("SideTables: flood rows beyond kFloodMaxRows");
+        auto tp = req(tunnels, sizeof(TunnelEntry), n_tunnels, "tunnels");
+        src.tunnels = static_cast<const TunnelEntry*>(tp.first); src.n_tunnels = n_tunnels;
+        auto t6 = req(tunnels6, sizeof(Tunnel6Entry), n_tunnels6, "tunnels6");
+        src.tunnels6 = static_cast<const Tunnel6Entry*>(t6.first); src.n_tunnels6 = n_tunnels6;
+        std::string k = rss;
+        if (k.size() < 52) k.resize(52, '\0');
+        src.rss_key = reinterpret_cast<const uint8_t*>(k.data());
+        src.v6 = v6;
+        return std::make_shared<SideTables>(src);
+      }), py::arg("ports"), py::arg("macs"), py::arg("mac_mask"), py::arg("lag"), py::arg("n_lag_groups"),
+         py::arg("flood"), py::arg("n_flood"), py::arg("tunnels"), py::arg("n_tunnels"), py::arg("tunnels6"),
+         py::arg("n_tunnels6"), py::arg("rss"), py::arg("v6") = false)
+      .def("mac_lookup", [](SideTables& t, uint32_t bridge, uint32_t lo, uint32_t hi) {
+        std::shared_lock<std::shared_mutex> g(t.mac_mu);
+        return mac_lookup(t.view(), bridge, lo, hi);
+      });
   py::class_<Engine>(m, "IoEngine")
-      .def(py::init<uint32_t, uint32_t, uint32_t>(), py::arg("burst") = 256, py::arg("inflight") = 64,
-           py::arg("tx_workers") = 1)
+      .def(py::init<uint32_t, uint32_t, uint32_t, uint32_t, uint32_t>(), py::arg("burst") = 256,
+           py::arg("inflight") = 64, py::arg("tx_workers") = 1, py::arg("queues") = 1,
+           py::arg("max_inflight_frames") = 0)
+      .def_property_readonly("queues", &Engine::queues)
       .def("add_backend", &Engine::add_backend)
-      .def("add_port", &Engine::add_port)
+      .def("add_port", &Engine::add_port, py::arg("id"), py::arg("port"), py::arg("queue") = -1)
       .def("remove_port", &Engine::remove_port)
       .def("port", &Engine::port)
+      .def("port_queue", &Engine::port_queue)
+      .def("set_side_tables", &Engine::set_side_tables)
+      .def("set_redirects", &Engine::set_redirects)
+      .def("hold", [](Engine& e) { py::gil_scoped_release nogil; e.hold(); })
+      .def("release", &Engine::release)
+      .def("flush_learning", [](Engine& e) { py::gil_scoped_release nogil; e.flush_learning(); })
+      .def_property("learn_stamp", &Engine::learn_stamp, &Engine::set_learn_stamp)
+      .def("side_port_counters", [](const Engine& e) {
+        auto v = e.side_port_counters();
+        return py::array_t<uint64_t>(v.size(), v.data());
+      })
+      .def("side_drop_counters", [](const Engine& e) {
+        auto v = e.side_drop_counters();
+        return py::array_t<uint64_t>(v.size(), v.data());
+      })
       .def("set_steering", [](Engine& e, py::buffer ports, py::bytes rss, bool v6) {
         py::buffer_info bi = ports.request();
         const size_t n = (size_t)bi.size * bi.itemsize / sizeof(PortEntry);

@@ -41,23 +41,25 @@ Port::Port(uint32_t window) {
   mask_ = w - 1;
 }
 
-bool Port::tx(const uint8_t* a, uint32_t na, const uint8_t* b, uint32_t nb, const uint8_t* c, uint32_t nc) {
+uint32_t Port::tx_batch(const TxItem* it, uint32_t n) {
   std::lock_guard<std::mutex> g(tx_mu_);
-  const bool ok = tx_locked(a, na, b, nb, c, nc);
-  if (ok) {
-    tx_dirty_ = true;
-    tx_pkts.fetch_add(1, std::memory_order_relaxed);
-    tx_bytes.fetch_add(na + nb + nc, std::memory_order_relaxed);
-  } else {
-    tx_full.fetch_add(1, std::memory_order_relaxed);
+  uint32_t ok = 0;
+  uint64_t bytes = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    const TxItem& x = it[i];
+    if (!tx_locked(x.a, x.na, x.b, x.nb, x.c, x.nc)) break;   // full: the rest of the batch finds no room either
+    ++ok;
+    bytes += x.na + x.nb + x.nc;
   }
+  if (ok) flush_locked();
+  // counters change under the tx lock only: plain read-modify-store, no atomic RMW
+  auto add = [](std::atomic<uint64_t>& c, uint64_t v) {
+    if (v) c.store(c.load(std::memory_order_relaxed) + v, std::memory_order_relaxed);
+  };
+  add(tx_pkts, ok);
+  add(tx_bytes, bytes);
+  add(tx_full, n - ok);
   return ok;
-}
-
-void Port::flush() {
-  std::lock_guard<std::mutex> g(tx_mu_);
-  if (tx_dirty_) flush_locked();
-  tx_dirty_ = false;
 }
 
 void Port::reclaim() {
@@ -209,7 +211,6 @@ void PacketPort::flush_locked() { (void)::sendto(fd_, nullptr, 0, MSG_DONTWAIT, 
 FdPort::FdPort(int fd, uint32_t nbufs, uint32_t buf_size)
     : Port(nbufs), fd_(fd), nbufs_(pow2_at_least(nbufs)), bsize_(buf_size) {
   bufs_.resize((size_t)nbufs_ * bsize_);
-  lens_.resize(nbufs_);
   txbuf_.resize(bsize_ + 256);
 }
 
@@ -261,203 +262,40 @@ void RecircPort::release_to(uint32_t seq_end) {
   }
 }
 
-// ---------------------------------------------------------------------------------- GpuBackend
-GpuBackend::GpuBackend(RingEngine* ring) : ring_(ring) {
-  if (!ring->host_slots()) throw std::invalid_argument("iox: the ring needs host_slots=True");
-  in_ = static_cast<uint8_t*>(ring->host_ptr(0));
-  im_ = static_cast<uint32_t*>(ring->host_ptr(1));
-  out_ = static_cast<uint8_t*>(ring->host_ptr(2));
-  om_ = static_cast<uint32_t*>(ring->host_ptr(3));
+// ---------------------------------------------------------------------------------- Toeplitz tables
+ToeplitzTab::ToeplitzTab(const uint8_t* rss_key) : tab((size_t)16 * 256) {
+  // XOR-linear in the key bits: the hash of a key is the XOR of the hashes of its bytes alone
+  for (int b = 0; b < 16; ++b)
+    for (uint32_t v = 0; v < 256; ++v) {
+      uint8_t raw[16] = {};
+      raw[b] = (uint8_t)v;
+      FlowKey k;
+      std::memcpy(&k, raw, sizeof(k));
+      tab[(size_t)b * 256 + v] = toeplitz_scalar(k, rss_key);
+    }
 }
 
-GpuBackend::~GpuBackend() {
-  if (side_stream_) (void)hipStreamDestroy(side_stream_);
-}
+namespace {
+struct TabHash {   // side_stage's hasher: by pointer (the tables are 16 KiB)
+  const ToeplitzTab* t;
+  uint32_t operator()(const FlowKey& k) const { return (*t)(k); }
+};
 
-void GpuBackend::thread_init() {
-  hck(hipSetDevice(ring_->device()), "set device");
-  if (!side_stream_) hck(hipStreamCreateWithFlags(&side_stream_, hipStreamNonBlocking), "side stream");
+uint32_t owner_tab(const uint8_t* hdr, uint32_t len, uint32_t in_port, const PortEntry* ports, const ToeplitzTab& h,
+                   uint32_t n, bool v6) {
+  if (n <= 1) return 0;
+  uint32_t d[kSlotDwords] = {};
+  std::memcpy(d, hdr, std::min<uint32_t>(len, kSlotBytes));
+  TablesView tv{};
+  tv.ports = ports;
+  tv.flow6_on = v6 ? 1u : 0u;   // IPv6 keys folded as the owners' tables hold them
+  Parsed p;
+  IngressState st;
+  ingress_stage(tv, DirectTables{tv}, d, (in_port & 0xFFFFu) | (std::min<uint32_t>(len, kMaxFrame) << 16), p, st);
+  if (!st.reason && (p.ipv4 || (v6 && p.ipv6))) return owner_of(h(st.key), n);
+  return in_port % n;
 }
-
-void GpuBackend::side_pass(SideBatch& out) {
-  const FusedLaunch& f = ring_->launch();
-  if (!f.side.cnt) return;
-  if (!side_stream_) thread_init();
-  hipStream_t s = side_stream_;
-  hck(launch_side(f.t, ring_->dev_in(), ring_->dev_inmeta(), ring_->dev_out(), ring_->dev_meta(), f.side, f.port_ctr,
-                  f.drop_ctr, s, ring_->capacity(), true), "side kernel");
-  if (f.side.cap_learn && f.t.macs)
-    hck(launch_mac_learn(const_cast<MacEntry*>(f.t.macs), f.t.mac_mask, f.side.learn, f.side.cnt + 1, f.side.cap_learn,
-                         stamp++, f.side.cnt + 4, s), "learn kernel");
-  h_cnt_.assign(8, 0);
-  hck(hipMemcpyAsync(h_cnt_.data(), f.side.cnt, 32, hipMemcpyDeviceToHost, s), "side counts");
-  hck(hipStreamSynchronize(s), "side sync");
-  const uint32_t n = std::min(h_cnt_[0], f.side.cap_rep);
-  if (n) {
-    h_meta_.resize(n); h_src_.resize(n); h_hdr_.resize((size_t)n * kSlotDwords);
-    hck(hipMemcpyAsync(h_meta_.data(), f.side.rep_meta, n * 4ull, hipMemcpyDeviceToHost, s), "rep meta");
-    hck(hipMemcpyAsync(h_src_.data(), f.side.rep_src, n * 4ull, hipMemcpyDeviceToHost, s), "rep src");
-    hck(hipMemcpyAsync(h_hdr_.data(), f.side.rep_hdr, n * 64ull, hipMemcpyDeviceToHost, s), "rep hdr");
-  }
-  if (f.side.xhdr) {
-    out.xall.resize((size_t)capacity() * kXhdrBytes);
-    hck(hipMemcpyAsync(out.xall.data(), f.side.xhdr, out.xall.size(), hipMemcpyDeviceToHost, s), "xhdr");
-  }
-  hck(hipMemsetAsync(f.side.cnt, 0, 32, s), "side reset");
-  hck(hipStreamSynchronize(s), "side sync");
-  out.reps.resize(n);
-  for (uint32_t k = 0; k < n; ++k) {
-    out.reps[k].src_pos = h_src_[k];
-    out.reps[k].meta = h_meta_[k];
-    std::memcpy(out.reps[k].hdr, &h_hdr_[(size_t)k * kSlotDwords], kSlotBytes);
-  }
-  out.learned = h_cnt_[1];
-  if (out.learned) ring_->bump_epoch();   // learned MACs: the next chunks drop cached table lines
-}
-
-// ---------------------------------------------------------------------------------- OracleBackend
-OracleBackend::OracleBackend(uint32_t capacity) : cap_(capacity) {
-  if (capacity < 64 || (capacity & (capacity - 1))) throw std::invalid_argument("iox: oracle capacity: power of two >= 64");
-  in_.assign((size_t)cap_ * kSlotBytes, 0);
-  out_.assign((size_t)cap_ * kSlotBytes, 0);
-  im_.assign(cap_, 0);
-  om_.assign(cap_, 0);
-}
-
-void OracleBackend::configure(const TablesView& t, uint64_t* flow_ctr, uint64_t* port_ctr, uint64_t* drop_ctr,
-                              const SideOut& side, MacEntry* macs, uint32_t mac_mask) {
-  t_ = t; flow_ctr_ = flow_ctr; port_ctr_ = port_ctr; drop_ctr_ = drop_ctr; side_ = side;
-  macs_ = macs; mac_mask_ = mac_mask;
-  configured_ = true;
-}
-
-void OracleBackend::run_segment(uint32_t pos, uint32_t n) {
-  const uint32_t p = pos & (cap_ - 1);
-  if (side_.cnt) std::memset(side_.cnt, 0, 32);
-  oracle_run(t_, reinterpret_cast<const uint32_t*>(in_.data() + (size_t)p * kSlotBytes), im_.data() + p, n,
-             reinterpret_cast<uint32_t*>(out_.data() + (size_t)p * kSlotBytes), om_.data() + p, flow_ctr_, port_ctr_,
-             drop_ctr_, nullptr, nullptr, side_.cnt ? &side_ : nullptr);
-  if (!side_.cnt) return;
-  const uint32_t nr = std::min(side_.cnt[0], side_.cap_rep);
-  for (uint32_t k = 0; k < nr; ++k) {
-    Replica r;
-    r.src_pos = (p + side_.rep_src[k]) & (cap_ - 1);
-    r.meta = side_.rep_meta[k];
-    std::memcpy(r.hdr, side_.rep_hdr + (size_t)k * kSlotDwords, kSlotBytes);
-    pending_.reps.push_back(r);
-  }
-  if (side_.xhdr) {
-    if (pending_.xall.empty()) pending_.xall.assign((size_t)cap_ * kXhdrBytes, 0);
-    for (uint32_t i = 0; i < n; ++i)
-      if (om_[p + i] & kMetaXhdr)
-        std::memcpy(pending_.xall.data() + (size_t)(p + i) * kXhdrBytes,
-                    reinterpret_cast<const uint8_t*>(side_.xhdr) + (size_t)i * kXhdrBytes, kXhdrBytes);
-  }
-  const uint32_t nl = std::min(side_.cnt[1], side_.cap_learn);
-  if (nl && macs_) {
-    mac_learn_cpu(macs_, mac_mask_, side_.learn, nl, stamp);
-    pending_.learned += nl;
-  }
-}
-
-uint64_t OracleBackend::publish(uint32_t n) {
-  if (!configured_) throw std::runtime_error("iox: oracle backend not configured");
-  if (n == 0 || (n & 63u) || n > cap_) throw std::invalid_argument("iox: publish a multiple of 64 packets");
-  // real packets first, filler slots (kRingPadMeta) at the end of the publish: run the prefix
-  uint32_t real = 0;
-  while (real < n && im_[(prod_ + real) & (cap_ - 1)] != kRingPadMeta) ++real;
-  for (uint32_t i = real; i < n; ++i) om_[(prod_ + i) & (cap_ - 1)] = make_meta(kPortNone, 0, kMalformed);
-  uint32_t done = 0;
-  while (done < real) {
-    const uint32_t p = (uint32_t)((prod_ + done) & (cap_ - 1));
-    const uint32_t k = std::min(real - done, cap_ - p);   // contiguous piece (a wrap splits it)
-    run_segment(p, k);
-    done += k;
-  }
-  ++stamp;
-  prod_ += n;
-  return prod_;
-}
-
-void OracleBackend::side_pass(SideBatch& out) {
-  out.reps.swap(pending_.reps);
-  out.xall.swap(pending_.xall);
-  out.learned = pending_.learned;
-  pending_ = SideBatch{};
-}
-
-// ---------------------------------------------------------------------------------- Engine
-Engine::Engine(uint32_t burst, uint32_t inflight, uint32_t tx_workers)
-    : burst_(burst), inflight_(std::max<uint32_t>(inflight, 1)), workers_(std::max<uint32_t>(tx_workers, 1)) {
-  if (burst_ < 1 || burst_ > (1u << 16)) throw std::invalid_argument("iox: burst in [1, 65536]");
-  if (workers_ > 16) throw std::invalid_argument("iox: at most 16 tx workers per backend");
-  ports_ = std::make_shared<PortTab>((size_t)kMaxPorts + 2);
-  redirect_.assign((size_t)kMaxPorts + 2, 0xFFFFFFFFu);
-  side_ports_.assign((size_t)kMaxPorts + 2, 0);
-  recirc_ = std::make_shared<RecircPort>(4096);
-}
-
-Engine::~Engine() {
-  try {
-    stop();
-  } catch (...) {
-  }
-}
-
-void Engine::add_backend(std::shared_ptr<Backend> b) {
-  if (run_) throw std::runtime_error("iox: add backends before start()");
-  auto L = std::make_unique<Lane>();
-  L->be = std::move(b);
-  L->slots.reset(new Burst[inflight_]);
-  lanes_.push_back(std::move(L));
-}
-
-void Engine::add_port(uint32_t id, std::shared_ptr<Port> p) {
-  if (id >= (uint32_t)kMaxPorts) throw std::invalid_argument("iox: port id out of range");
-  std::lock_guard<std::mutex> g(ports_mu_);
-  auto t = std::make_shared<PortTab>(*ports_);
-  (*t)[id] = std::move(p);
-  std::atomic_store(&ports_, std::shared_ptr<const PortTab>(t));
-}
-
-std::shared_ptr<Port> Engine::remove_port(uint32_t id) {
-  if (id >= (uint32_t)kMaxPorts) return nullptr;
-  std::lock_guard<std::mutex> g(ports_mu_);
-  auto t = std::make_shared<PortTab>(*ports_);
-  auto old = (*t)[id];
-  (*t)[id].reset();
-  std::atomic_store(&ports_, std::shared_ptr<const PortTab>(t));
-  return old;   // frames of it still in flight keep it alive through the snapshot the threads hold
-}
-
-std::shared_ptr<Port> Engine::port(uint32_t id) {
-  auto t = std::atomic_load(&ports_);
-  return id < t->size() ? (*t)[id] : nullptr;
-}
-
-void Engine::set_steering(const std::vector<PortEntry>& ports, const std::vector<uint8_t>& rss_key, bool v6) {
-  if (run_ && !pause_) throw std::runtime_error("iox: set_steering while running (pause first)");
-  if (rss_key.size() < 20) throw std::invalid_argument("iox: rss key too short");
-  steer_ports_ = ports;
-  steer_ports_.resize((size_t)kMaxPorts + 2);
-  rss_key_ = rss_key;
-  steer_v6_ = v6;
-}
-
-void Engine::set_redirect(uint32_t port, uint32_t underlay) {
-  if (port < redirect_.size()) redirect_[port] = underlay;
-}
-
-void Engine::set_side_ports(const std::vector<uint32_t>& ports) {
-  std::vector<uint8_t> s((size_t)kMaxPorts + 2, 0);
-  for (uint32_t p : ports)
-    if (p < s.size()) s[p] = 1;
-  side_ports_.swap(s);   // read by the rx thread; set while paused (or benignly racy: a flag per port)
-}
-
-bool Engine::needs_side(uint32_t in_port) const {
-  return side_always_.load(std::memory_order_relaxed) || (in_port < side_ports_.size() && side_ports_[in_port]);
-}
+}  // namespace
 
 uint32_t frame_owner(const uint8_t* hdr, uint32_t len, uint32_t in_port, const PortEntry* ports, const uint8_t* rss_key,
                      uint32_t n, bool v6) {
@@ -467,7 +305,7 @@ uint32_t frame_owner(const uint8_t* hdr, uint32_t len, uint32_t in_port, const P
   std::memcpy(d, hdr, std::min<uint32_t>(len, kSlotBytes));
   TablesView tv{};
   tv.ports = ports;
-  tv.flow6_on = v6 ? 1u : 0u;   // IPv6 keys folded as the owners' tables hold them
+  tv.flow6_on = v6 ? 1u : 0u;
   Parsed p;
   IngressState st;
   ingress_stage(tv, DirectTables{tv}, d, (in_port & 0xFFFFu) | (std::min<uint32_t>(len, kMaxFrame) << 16), p, st);
@@ -475,46 +313,353 @@ uint32_t frame_owner(const uint8_t* hdr, uint32_t len, uint32_t in_port, const P
   return in_port % n;
 }
 
-uint32_t Engine::owner_of_frame(const uint8_t* f, uint32_t len, uint32_t in_port) const {
-  const uint32_t n = (uint32_t)lanes_.size();
+// ---------------------------------------------------------------------------------- SideTables
+SideTables::SideTables(const Src& s) {
+  ports_.assign((size_t)kMaxPorts + 2, PortEntry{});
+  if (s.ports) std::memcpy(ports_.data(), s.ports, std::min<size_t>(s.n_ports, kMaxPorts) * sizeof(PortEntry));
+  if (s.macs && s.mac_mask != ~0u && ((s.mac_mask + 1) & s.mac_mask) == 0)
+    macs_.assign(s.macs, s.macs + (size_t)s.mac_mask + 1);
+  if (s.lag && s.n_lag_groups) lag_.assign(s.lag, s.lag + (size_t)s.n_lag_groups * kLagWays);
+  if (s.flood && s.n_flood) {
+    // every row a link can name (< kFloodMaxRows) exists in the copy: side_stage follows links
+    // without knowing how many rows the control plane allocated
+    flood_.assign((size_t)std::max<size_t>(s.flood_rows, kFloodMaxRows) * kFloodWays, (uint16_t)kPortNone);
+    std::memcpy(flood_.data(), s.flood, s.flood_rows * kFloodWays * sizeof(uint16_t));
+  }
+  if (s.tunnels && s.n_tunnels) tun_.assign(s.tunnels, s.tunnels + s.n_tunnels);
+  if (s.tunnels6 && s.n_tunnels6) tun6_.assign(s.tunnels6, s.tunnels6 + s.n_tunnels6);
+  rss_.assign(64, 0);
+  if (s.rss_key) std::memcpy(rss_.data(), s.rss_key, 52);
+  hash_ = ToeplitzTab(rss_.data());
+  t_.ports = ports_.data();
+  t_.macs = macs_.empty() ? nullptr : macs_.data();
+  t_.mac_mask = macs_.empty() ? 0 : s.mac_mask;
+  t_.rss_key = rss_.data();
+  t_.lag_members = lag_.empty() ? nullptr : lag_.data();
+  t_.n_lag_groups = lag_.empty() ? 0 : s.n_lag_groups;
+  t_.flood = flood_.empty() ? nullptr : flood_.data();
+  t_.n_flood = flood_.empty() ? 0 : s.n_flood;
+  t_.tunnels = tun_.empty() ? nullptr : tun_.data();
+  t_.n_tunnels = (uint32_t)tun_.size();
+  t_.tunnels6 = tun6_.empty() ? nullptr : tun6_.data();
+  t_.n_tunnels6 = (uint32_t)tun6_.size();
+  t_.flow6_on = s.v6 ? 1u : 0u;   // the key fold only (make_key): the side pass never probes flows
+}
+
+// ---------------------------------------------------------------------------------- GpuBackend
+GpuBackend::GpuBackend(RingEngine* ring) : ring_(ring), cap_(ring->capacity()) {
+  if (!ring->host_slots()) throw std::invalid_argument("iox: the ring needs host_slots=True");
+  in_ = static_cast<uint8_t*>(ring->host_ptr(0));
+  im_ = static_cast<uint32_t*>(ring->host_ptr(1));
+  out_ = static_cast<uint8_t*>(ring->host_ptr(2));
+  om_ = static_cast<uint32_t*>(ring->host_ptr(3));
+}
+
+GpuBackend::~GpuBackend() {
+  if (d_learn_) (void)hipFree(d_learn_);
+  if (learn_stream_) (void)hipStreamDestroy(learn_stream_);
+}
+
+void GpuBackend::thread_init() { hck(hipSetDevice(ring_->device()), "set device"); }
+
+void GpuBackend::apply_learn(const uint32_t* ev, uint32_t n, uint32_t stamp) {
+  if (!n) return;
+  thread_init();
+  if (!learn_stream_) hck(hipStreamCreateWithFlags(&learn_stream_, hipStreamNonBlocking), "learn stream");
+  const auto mt = ring_->mac_table();
+  if (!mt.first) return;
+  if (n > learn_cap_) {
+    if (d_learn_) hck(hipFree(d_learn_), "free");
+    learn_cap_ = pow2_at_least(std::max<uint32_t>(n, 1024));
+    hck(hipMalloc(reinterpret_cast<void**>(&d_learn_), ((size_t)learn_cap_ * 4 + 4) * 4), "learn buffer");
+  }
+  uint32_t* cnt = d_learn_ + (size_t)learn_cap_ * 4;
+  const uint32_t hdr[4] = {n, 0, 0, 0};
+  hck(hipMemcpyAsync(d_learn_, ev, (size_t)n * 16, hipMemcpyHostToDevice, learn_stream_), "learn events");
+  hck(hipMemcpyAsync(cnt, hdr, 16, hipMemcpyHostToDevice, learn_stream_), "learn count");
+  hck(launch_mac_learn(mt.first, mt.second, d_learn_, cnt, n, stamp, cnt + 1, learn_stream_), "learn kernel");
+  hck(hipStreamSynchronize(learn_stream_), "learn sync");
+  ring_->bump_epoch();   // chunks published from now on drop cached MAC-table lines first
+}
+
+// ---------------------------------------------------------------------------------- OracleBackend
+OracleBackend::OracleBackend(uint32_t capacity, uint32_t queues) : cap_(capacity), nq_(queues) {
+  if (capacity < 64 || (capacity & (capacity - 1))) throw std::invalid_argument("iox: oracle capacity: power of two >= 64");
+  if (queues < 1 || queues > 64) throw std::invalid_argument("iox: oracle queues in [1, 64]");
+  in_.assign((size_t)cap_ * nq_ * kSlotBytes, 0);
+  out_.assign((size_t)cap_ * nq_ * kSlotBytes, 0);
+  im_.assign((size_t)cap_ * nq_, 0);
+  om_.assign((size_t)cap_ * nq_, 0);
+  prod_.reset(new std::atomic<uint64_t>[nq_]);
+  for (uint32_t q = 0; q < nq_; ++q) prod_[q].store(0);
+}
+
+void OracleBackend::configure(const TablesView& t, uint64_t* flow_ctr, uint64_t* port_ctr, uint64_t* drop_ctr,
+                              MacEntry* macs, uint32_t mac_mask) {
+  std::lock_guard<std::mutex> g(run_mu_);
+  t_ = t; flow_ctr_ = flow_ctr; port_ctr_ = port_ctr; drop_ctr_ = drop_ctr;
+  macs_ = macs; mac_mask_ = mac_mask;
+  configured_ = true;
+}
+
+void OracleBackend::run_segment(uint32_t q, uint32_t pos, uint32_t n) {
+  const size_t p = (size_t)q * cap_ + (pos & (cap_ - 1));
+  oracle_run(t_, reinterpret_cast<const uint32_t*>(in_.data() + p * kSlotBytes), im_.data() + p, n,
+             reinterpret_cast<uint32_t*>(out_.data() + p * kSlotBytes), om_.data() + p, flow_ctr_, port_ctr_,
+             drop_ctr_, nullptr, nullptr, nullptr);
+}
+
+uint64_t OracleBackend::publish(uint32_t q, uint32_t n) {
+  if (!configured_) throw std::runtime_error("iox: oracle backend not configured");
+  if (q >= nq_) throw std::invalid_argument("iox: no such queue");
+  if (n == 0 || (n & 63u) || n > cap_) throw std::invalid_argument("iox: publish a multiple of 64 packets");
+  const uint64_t prod = prod_[q].load(std::memory_order_relaxed);
+  uint32_t* im = in_meta(q);
+  uint32_t* om = om_.data() + (size_t)q * cap_;
+  // real packets first, filler slots (kRingPadMeta) at the end of the publish: run the prefix
+  uint32_t real = 0;
+  while (real < n && im[(prod + real) & (cap_ - 1)] != kRingPadMeta) ++real;
+  for (uint32_t i = real; i < n; ++i) om[(prod + i) & (cap_ - 1)] = make_meta(kPortNone, 0, kMalformed);
+  {
+    std::lock_guard<std::mutex> g(run_mu_);
+    uint32_t done = 0;
+    while (done < real) {
+      const uint32_t p = (uint32_t)((prod + done) & (cap_ - 1));
+      const uint32_t k = std::min(real - done, cap_ - p);   // contiguous piece (a wrap splits it)
+      run_segment(q, p, k);
+      done += k;
+    }
+  }
+  prod_[q].store(prod + n, std::memory_order_release);
+  return prod + n;
+}
+
+void OracleBackend::apply_learn(const uint32_t* ev, uint32_t n, uint32_t stamp) {
+  std::lock_guard<std::mutex> g(run_mu_);
+  if (macs_ && n) mac_learn_cpu(macs_, mac_mask_, ev, n, stamp);
+}
+
+// ---------------------------------------------------------------------------------- Engine
+Engine::Engine(uint32_t burst, uint32_t inflight, uint32_t tx_workers, uint32_t queues, uint32_t max_inflight_frames)
+    : burst_(burst), inflight_(std::max<uint32_t>(inflight, 1)), workers_(std::max<uint32_t>(tx_workers, 1)),
+      nq_(queues), max_frames_(max_inflight_frames) {
+  if (burst_ < 1 || burst_ > (1u << 16)) throw std::invalid_argument("iox: burst in [1, 65536]");
+  if (workers_ > 16) throw std::invalid_argument("iox: at most 16 tx workers per queue");
+  if (nq_ < 1 || nq_ > 64) throw std::invalid_argument("iox: queues in [1, 64]");
+  if (max_frames_ && max_frames_ < 64) throw std::invalid_argument("iox: max_inflight_frames >= 64 (or 0: ring capacity)");
+  ports_ = std::make_shared<PortTab>((size_t)kMaxPorts + 2);
+  auto c = std::make_shared<Cfg>();
+  c->redirect.assign((size_t)kMaxPorts + 2, 0xFFFFFFFFu);
+  c->side_ports.assign((size_t)kMaxPorts + 2, 0);
+  cfg_ = c;
+  recirc_ = std::make_shared<RecircPort>(4096);
+  for (uint32_t q = 0; q < nq_; ++q) {
+    auto Q = std::make_unique<Queue>();
+    Q->id = q;
+    Q->wst.reset(new QStats[workers_]);
+    Q->side_ctr.reset(new std::atomic<uint64_t>[(size_t)2 * kMaxPorts]);
+    for (size_t i = 0; i < (size_t)2 * kMaxPorts; ++i) Q->side_ctr[i].store(0);
+    Q->side_drop.reset(new std::atomic<uint64_t>[kNumReasons]);
+    for (int i = 0; i < kNumReasons; ++i) Q->side_drop[i].store(0);
+    queues_.push_back(std::move(Q));
+  }
+}
+
+Engine::~Engine() {
+  try {
+    stop();
+  } catch (...) {
+  }
+}
+
+template <class F>
+void Engine::update_cfg(F f) {
+  std::lock_guard<std::mutex> g(cfg_mu_);
+  auto c = std::make_shared<Cfg>(*std::atomic_load(&cfg_));
+  f(*c);
+  std::atomic_store(&cfg_, std::shared_ptr<const Cfg>(c));
+}
+
+void Engine::add_backend(std::shared_ptr<Backend> b) {
+  if (run_) throw std::runtime_error("iox: add backends before start()");
+  if (b->queues() < nq_) throw std::invalid_argument("iox: the backend has fewer ring queues than the engine");
+  const uint32_t g = (uint32_t)backends_.size();
+  backends_.push_back(b);
+  for (uint32_t q = 0; q < nq_; ++q) {
+    auto L = std::make_unique<Lane>();
+    L->be = b;
+    L->q = q;
+    L->g = g;
+    L->slots.reset(new Burst[inflight_]);
+    queues_[q]->lanes.push_back(L.get());
+    lanes_.push_back(std::move(L));
+  }
+  update_cfg([&](Cfg& c) { c.side.resize(backends_.size()); });
+}
+
+void Engine::add_port(uint32_t id, std::shared_ptr<Port> p, int queue) {
+  if (id >= (uint32_t)kMaxPorts) throw std::invalid_argument("iox: port id out of range");
+  std::lock_guard<std::mutex> g(ports_mu_);
+  auto t = std::make_shared<PortTab>(*ports_);
+  if ((*t)[id].p) queues_[(*t)[id].q]->nports.fetch_sub(1);
+  uint32_t q = 0;
+  if (queue >= 0) {
+    q = (uint32_t)queue % nq_;
+  } else {   // least loaded queue
+    for (uint32_t k = 1; k < nq_; ++k)
+      if (queues_[k]->nports.load() < queues_[q]->nports.load()) q = k;
+  }
+  (*t)[id] = PortRef{std::move(p), q};
+  queues_[q]->nports.fetch_add(1);
+  std::atomic_store(&ports_, std::shared_ptr<const PortTab>(t));
+}
+
+std::shared_ptr<Port> Engine::remove_port(uint32_t id) {
+  if (id >= (uint32_t)kMaxPorts) return nullptr;
+  std::lock_guard<std::mutex> g(ports_mu_);
+  auto t = std::make_shared<PortTab>(*ports_);
+  auto old = (*t)[id].p;
+  if (old) queues_[(*t)[id].q]->nports.fetch_sub(1);
+  (*t)[id] = PortRef{};
+  std::atomic_store(&ports_, std::shared_ptr<const PortTab>(t));
+  return old;   // frames of it still in flight keep it alive through the snapshot the threads hold
+}
+
+std::shared_ptr<Port> Engine::port(uint32_t id) {
+  auto t = std::atomic_load(&ports_);
+  return id < t->size() ? (*t)[id].p : nullptr;
+}
+
+int Engine::port_queue(uint32_t id) {
+  auto t = std::atomic_load(&ports_);
+  return id < t->size() && (*t)[id].p ? (int)(*t)[id].q : -1;
+}
+
+void Engine::set_steering(const std::vector<PortEntry>& ports, const std::vector<uint8_t>& rss_key, bool v6) {
+  if (rss_key.size() < 20) throw std::invalid_argument("iox: rss key too short");
+  auto s = std::make_shared<Steer>();
+  s->ports = ports;
+  s->ports.resize((size_t)kMaxPorts + 2);
+  s->rss_key = rss_key;
+  s->rss_key.resize(std::max<size_t>(rss_key.size(), 64), 0);
+  s->v6 = v6;
+  s->hash = ToeplitzTab(s->rss_key.data());
+  update_cfg([&](Cfg& c) { c.steer = s; });
+}
+
+void Engine::set_redirects(const std::vector<std::pair<uint32_t, uint32_t>>& m) {
+  update_cfg([&](Cfg& c) {
+    c.redirect.assign((size_t)kMaxPorts + 2, 0xFFFFFFFFu);
+    for (const auto& e : m)
+      if (e.first < c.redirect.size()) c.redirect[e.first] = e.second;
+  });
+}
+
+void Engine::set_redirect(uint32_t port, uint32_t underlay) {
+  update_cfg([&](Cfg& c) {
+    if (port < c.redirect.size()) c.redirect[port] = underlay;
+  });
+}
+
+void Engine::set_side_ports(const std::vector<uint32_t>& ports) {
+  update_cfg([&](Cfg& c) {
+    c.side_ports.assign((size_t)kMaxPorts + 2, 0);
+    for (uint32_t p : ports)
+      if (p < c.side_ports.size()) c.side_ports[p] = 1;
+  });
+}
+
+void Engine::set_side_always(bool on) {
+  update_cfg([&](Cfg& c) { c.side_always = on; });
+}
+
+void Engine::set_side_tables(uint32_t backend, std::shared_ptr<SideTables> t) {
+  update_cfg([&](Cfg& c) {
+    if (backend >= c.side.size()) c.side.resize(backend + 1);
+    c.side[backend] = std::move(t);
+  });
+}
+
+uint32_t Engine::owner(const Steer* s, uint32_t n, const uint8_t* f, uint32_t len, uint32_t in_port) {
   if (n <= 1) return 0;
-  if (steer_ports_.empty() || rss_key_.empty()) return in_port % n;
-  return frame_owner(f, len, in_port, steer_ports_.data(), rss_key_.data(), n, steer_v6_);
+  if (!s) return in_port % n;
+  return owner_tab(f, len, in_port, s->ports.data(), s->hash, n, s->v6);
+}
+
+uint32_t Engine::owner_of_frame(const uint8_t* f, uint32_t len, uint32_t in_port) const {
+  return owner(cfg()->steer.get(), (uint32_t)backends_.size(), f, len, in_port);
 }
 
 void Engine::start() {
   if (run_) return;
-  if (lanes_.empty()) throw std::runtime_error("iox: no backend");
+  if (backends_.empty()) throw std::runtime_error("iox: no backend");
   {
     std::lock_guard<std::mutex> g(err_mu_);
     err_.clear();
   }
+  abandon_ = false;
   run_ = true;
-  pause_ = false;
-  for (auto& L : lanes_) L->freed_pos.store(L->be->published());
+  learner_run_ = true;
+  for (auto& L : lanes_) {
+    const uint64_t p = L->be->published(L->q);
+    L->freed_pos.store(p);
+  }
+  learner_ = std::thread(&Engine::learner_loop, this);
+  for (auto& Q : queues_) {
+    for (uint32_t w = 0; w < workers_; ++w) Q->tx.emplace_back(&Engine::tx_loop, this, Q.get(), w);
+    Q->rx = std::thread(&Engine::rx_loop, this, Q.get());
+  }
+}
+
+bool Engine::lanes_idle() const {
   for (auto& L : lanes_)
-    for (uint32_t w = 0; w < workers_; ++w) L->th.emplace_back(&Engine::tx_loop, this, L.get(), w);
-  rx_th_ = std::thread(&Engine::rx_loop, this);
+    if (L->done.load(std::memory_order_acquire) != L->head.load(std::memory_order_acquire)) return false;
+  return true;
 }
 
 void Engine::stop() {
-  const bool was = run_.exchange(false);
-  if (rx_th_.joinable()) rx_th_.join();
-  for (auto& L : lanes_) {
-    for (auto& t : L->th)
+  run_ = false;
+  for (auto& Q : queues_)
+    if (Q->rx.joinable()) Q->rx.join();
+  // the tx workers deliver what was published; a pipeline that stopped completing is abandoned
+  const auto t0 = Clock::now();
+  while (!lanes_idle() && !abandon_.load() && Clock::now() - t0 < std::chrono::seconds(10))
+    std::this_thread::sleep_for(std::chrono::microseconds(100));
+  abandon_ = true;
+  for (auto& Q : queues_) {
+    for (auto& t : Q->tx)
       if (t.joinable()) t.join();
-    L->th.clear();
+    Q->tx.clear();
   }
-  (void)was;
+  {
+    std::lock_guard<std::mutex> g(learn_mu_);
+    learner_run_ = false;
+  }
+  learn_cv_.notify_all();
+  if (learner_.joinable()) learner_.join();
+  // frames of abandoned bursts go back to their ports (a rebuilt engine reuses the ports)
+  for (auto& L : lanes_) {
+    for (uint32_t k = 0; k < inflight_; ++k) {
+      Burst& b = L->slots[k];
+      if (b.state.load() != 0) {
+        for (const Pkt& q : b.pkts) q.holder->complete(q.seq);
+        b.pkts.clear();
+        b.reps.clear();
+        b.state.store(0);
+      }
+    }
+    L->done.store(L->head.load());
+  }
 }
 
 void Engine::pause() {
-  pause_ = true;
+  pause_n_.fetch_add(1);
   if (!run_) return;
   const auto t0 = Clock::now();
   for (;;) {
-    bool idle = paused_ack_.load();
-    for (auto& L : lanes_) idle = idle && L->done.load() == L->head;
+    bool idle = true;
+    for (auto& Q : queues_) idle = idle && Q->held_epoch.load(std::memory_order_acquire) == ctl_epoch_.load();
+    idle = idle && lanes_idle();
     if (idle || !run_) return;
     if (Clock::now() - t0 > std::chrono::seconds(10)) throw std::runtime_error("iox: pause timed out");
     std::this_thread::sleep_for(std::chrono::microseconds(20));
@@ -522,8 +667,26 @@ void Engine::pause() {
 }
 
 void Engine::resume() {
-  paused_ack_ = false;
-  pause_ = false;
+  if (pause_n_.load() > 0) pause_n_.fetch_sub(1);
+}
+
+void Engine::hold() {
+  ctl_epoch_.fetch_add(1);
+  hold_n_.fetch_add(1);
+  if (!run_) return;
+  const uint64_t want = ctl_epoch_.load();
+  const auto t0 = Clock::now();
+  for (;;) {
+    bool held = true;
+    for (auto& Q : queues_) held = held && Q->held_epoch.load(std::memory_order_acquire) >= want;
+    if (held || !run_) return;
+    if (Clock::now() - t0 > std::chrono::seconds(10)) throw std::runtime_error("iox: hold timed out");
+    _mm_pause();
+  }
+}
+
+void Engine::release() {
+  if (hold_n_.load() > 0) hold_n_.fetch_sub(1);
 }
 
 std::string Engine::error() const {
@@ -537,6 +700,7 @@ void Engine::fail(const std::string& what) {
     if (err_.empty()) err_ = what;
   }
   run_ = false;
+  abandon_ = true;
 }
 
 std::vector<Punt> Engine::take_punts(size_t max) {
@@ -557,17 +721,46 @@ std::vector<double> Engine::take_latency_us() {
 }
 
 std::unordered_map<std::string, uint64_t> Engine::stats() const {
-  return {{"rx", st_rx_.load()},         {"tx", st_tx_.load()},         {"drop", st_drop_.load()},
-          {"punt", st_punt_.load()},     {"recirc", st_recirc_.load()}, {"replicas", st_reps_.load()},
-          {"bursts", st_bursts_.load()}, {"side_passes", st_side_.load()}, {"no_netdev", st_no_port_.load()},
-          {"punt_dropped", st_punt_drop_.load()}, {"tx_full", st_tx_full_.load()},
-          {"publish_ns", st_pub_ns_.load()}, {"deliver_ns", st_deliver_ns_.load()},
-          {"rx_idle_polls", st_idle_.load()}, {"rx_wait_tx", st_wait_tx_.load()}};
+  std::unordered_map<std::string, uint64_t> m;
+  auto fold = [&](const QStats& s) {
+    m["rx"] += s.rx.load(); m["tx"] += s.tx.load(); m["drop"] += s.drop.load(); m["punt"] += s.punt.load();
+    m["recirc"] += s.recirc.load(); m["replicas"] += s.reps.load(); m["bursts"] += s.bursts.load();
+    m["side_passes"] += s.side.load(); m["no_netdev"] += s.no_port.load(); m["tx_full"] += s.tx_full.load();
+    m["publish_ns"] += s.pub_ns.load(); m["deliver_ns"] += s.deliver_ns.load(); m["rx_idle_polls"] += s.idle.load();
+    m["rx_wait_tx"] += s.wait_tx.load(); m["learn_events"] += s.learn.load(); m["rx_held"] += s.held.load();
+  };
+  for (auto& Q : queues_) {
+    fold(Q->st);
+    for (uint32_t w = 0; w < workers_; ++w) fold(Q->wst[w]);
+  }
+  m["punt_dropped"] = punt_drop_.load();
+  m["queues"] = nq_;
+  {
+    std::lock_guard<std::mutex> g(learn_mu_);
+    m["learn_applied"] = learn_applied_n_;
+    m["learn_dropped"] = learn_dropped_;
+  }
+  return m;
 }
 
-void Engine::punt(uint32_t in_port, uint32_t reason, const uint8_t* a, uint32_t na, const uint8_t* b, uint32_t nb) {
+std::vector<uint64_t> Engine::side_port_counters() const {
+  std::vector<uint64_t> v((size_t)2 * kMaxPorts, 0);
+  for (auto& Q : queues_)
+    for (size_t i = 0; i < v.size(); ++i) v[i] += Q->side_ctr[i].load(std::memory_order_relaxed);
+  return v;
+}
+
+std::vector<uint64_t> Engine::side_drop_counters() const {
+  std::vector<uint64_t> v(kNumReasons, 0);
+  for (auto& Q : queues_)
+    for (int i = 0; i < kNumReasons; ++i) v[i] += Q->side_drop[i].load(std::memory_order_relaxed);
+  return v;
+}
+
+void Engine::punt(QStats& st, uint32_t in_port, uint32_t reason, const uint8_t* a, uint32_t na, const uint8_t* b,
+                  uint32_t nb) {
   std::lock_guard<std::mutex> g(punt_mu_);
-  if (punts_.size() >= 4096) { st_punt_drop_.fetch_add(1); return; }
+  if (punts_.size() >= 4096) { punt_drop_.fetch_add(1); return; }
   Punt p;
   p.in_port = (uint16_t)in_port;
   p.reason = (uint8_t)reason;
@@ -575,243 +768,361 @@ void Engine::punt(uint32_t in_port, uint32_t reason, const uint8_t* a, uint32_t 
   p.frame.insert(p.frame.end(), a, a + na);
   if (nb) p.frame.insert(p.frame.end(), b, b + nb);
   punts_.push_back(std::move(p));
-  st_punt_.fetch_add(1, std::memory_order_relaxed);
+  st.add(st.punt, 1);
 }
 
-void Engine::send(const PortTab& tab, uint32_t port, const uint8_t* x, uint32_t nx, const uint8_t* h, uint32_t nh,
-                  const uint8_t* t, uint32_t nt, std::vector<Port*>& touched, TxTally& tally) {
-  if (port < redirect_.size() && redirect_[port] != 0xFFFFFFFFu) port = redirect_[port];   // tunnel -> underlay
-  Port* p = port < tab.size() ? tab[port].get() : nullptr;
-  if (!p) { ++tally.no_port; return; }
-  if (p->tx(x, nx, h, nh, t, nt)) {
-    ++tally.tx;
-    if (touched.empty() || touched.back() != p)
-      if (std::find(touched.begin(), touched.end(), p) == touched.end()) touched.push_back(p);
-  } else {
-    ++tally.full;
+void Engine::flush_learning() {
+  std::unique_lock<std::mutex> lk(learn_mu_);
+  const uint64_t want = learn_seq_;
+  learn_cv_.wait_for(lk, std::chrono::seconds(10), [&] { return learn_applied_ >= want || !learner_run_; });
+}
+
+void Engine::learner_loop() {
+  std::vector<uint32_t> ev;
+  try {
+    for (;;) {
+      uint64_t seq;
+      {
+        std::unique_lock<std::mutex> lk(learn_mu_);
+        learn_cv_.wait(lk, [&] { return !learn_q_.empty() || !learner_run_; });
+        if (learn_q_.empty()) return;   // stopping with nothing left
+        ev.swap(learn_q_);
+        learn_q_.clear();
+        seq = learn_seq_;
+      }
+      const uint32_t n = (uint32_t)(ev.size() / 4);
+      const uint32_t stamp = ++learn_stamp_;
+      // every GPU learns what any of them saw (one MAC table model for the node); then the side
+      // passes' snapshots, so they stop reporting the MAC
+      for (auto& b : backends_) b->apply_learn(ev.data(), n, stamp);
+      auto c = cfg();
+      for (auto& st : c->side)
+        if (st && st->has_macs()) {
+          std::unique_lock<std::shared_mutex> g(st->mac_mu);
+          mac_learn_cpu(st->macs(), st->mac_mask(), ev.data(), n, stamp);
+        }
+      {
+        std::lock_guard<std::mutex> lk(learn_mu_);
+        learn_applied_ = seq;
+        learn_applied_n_ += n;
+      }
+      learn_cv_.notify_all();
+      ev.clear();
+    }
+  } catch (const std::exception& e) {
+    {
+      std::lock_guard<std::mutex> lk(learn_mu_);
+      learner_run_ = false;
+    }
+    learn_cv_.notify_all();
+    fail(std::string("learner: ") + e.what());
   }
 }
 
-void Engine::rx_loop() {
+void Engine::rx_loop(Queue* Q) {
   std::vector<RxRef> buf(burst_);
   uint32_t rr = 0;
   std::shared_ptr<const PortTab> cached;
-  std::vector<std::pair<uint32_t, Port*>> active;   // configured ports of the snapshot, in id order
+  std::vector<std::pair<uint32_t, Port*>> active;   // this queue's ports of the snapshot, in id order
+  const uint32_t nb = (uint32_t)backends_.size();
+  const uint32_t q = Q->id;
+  QStats& st = Q->st;
   try {
     while (run_) {
-      if (pause_) {
-        paused_ack_ = true;
-        std::this_thread::sleep_for(std::chrono::microseconds(20));
+      if (pause_n_.load(std::memory_order_acquire) || hold_n_.load(std::memory_order_acquire)) {
+        // nothing is being published by this thread from here until it sees the flags clear
+        Q->held_epoch.store(ctl_epoch_.load(std::memory_order_acquire), std::memory_order_release);
+        st.add(st.held, 1);
+        for (int k = 0; k < 64 && (pause_n_.load() || hold_n_.load()); ++k) _mm_pause();
+        if (pause_n_.load()) std::this_thread::sleep_for(std::chrono::microseconds(10));
         continue;
       }
-      paused_ack_ = false;
       auto tab = std::atomic_load(&ports_);
       if (tab != cached) {
         cached = tab;
         active.clear();
         for (uint32_t i = 0; i < (uint32_t)tab->size(); ++i)
-          if ((*tab)[i]) active.emplace_back(i, (*tab)[i].get());
+          if ((*tab)[i].p && (*tab)[i].q == q) active.emplace_back(i, (*tab)[i].p.get());
       }
       for (auto& a : active) a.second->reclaim();
-      recirc_->reclaim();
-      // room: a burst of k frames takes ceil(k / 64) chunks on its backend; bound the take by
-      // the fullest lane (frames are steered after they are read)
+      if (q == 0) recirc_->reclaim();
+      const auto c = cfg();
+      const Steer* steer = c->steer.get();
+      // room: a burst of k frames takes ceil(k / 64) chunks on its lane; bound the take by the
+      // fullest lane (frames are steered after they are read)
       uint32_t take = burst_;
-      for (auto& L : lanes_) {
-        if (!L->be->ready() || L->head - L->done.load(std::memory_order_acquire) >= inflight_) {
+      for (Lane* L : Q->lanes) {
+        if (!L->be->ready() ||
+            L->head.load(std::memory_order_relaxed) - L->done.load(std::memory_order_acquire) >= inflight_) {
           take = 0;
-          st_wait_tx_.fetch_add(1, std::memory_order_relaxed);
           break;
         }
         // slots are reusable once DELIVERED (their out slot / meta read), not merely completed
-        const uint64_t used = L->be->published() - L->freed_pos.load(std::memory_order_acquire);
-        const uint64_t room = L->be->capacity() > used ? L->be->capacity() - used : 0;
+        const uint64_t used = L->be->published(q) - L->freed_pos.load(std::memory_order_acquire);
+        uint64_t room = L->be->capacity() > used ? L->be->capacity() - used : 0;
+        if (max_frames_) room = std::min<uint64_t>(room, max_frames_ > used ? max_frames_ - used : 0);
         take = (uint32_t)std::min<uint64_t>(take, room & ~63ull);
       }
-      if (take == 0) { _mm_pause(); continue; }
+      if (take == 0) {
+        st.add(st.wait_tx, 1);
+        _mm_pause();
+        continue;
+      }
       const uint64_t t_rx = now_ns();
       uint32_t got = 0;
-      auto stage = [&](uint32_t pid, Port* p, const RxRef& r) {
-        if (r.seq + 1 - p->seen_ <= 0x7FFFFFFFu) p->seen_ = r.seq + 1;
-        if (r.len < 14 || r.len > kMaxFrame) { p->complete(r.seq); return; }   // runt / oversize / own tx
-        const uint32_t in_port = r.in_port != ~0u ? r.in_port : pid;
-        p->rx_pkts.fetch_add(1, std::memory_order_relaxed);
-        p->rx_bytes.fetch_add(r.len, std::memory_order_relaxed);
-        const uint32_t o = owner_of_frame(r.data, r.len, in_port);
-        lanes_[o]->stage.push_back(Pkt{in_port, r.seq, r.data, r.len, p});
-        ++got;
+      auto read_port = [&](uint32_t pid, Port* p, uint32_t max) {
+        const uint32_t n = p->rx(buf.data(), max);
+        uint64_t pk = 0, by = 0;
+        for (uint32_t i = 0; i < n; ++i) {
+          const RxRef& r = buf[i];
+          if (r.seq + 1 - p->seen_ <= 0x7FFFFFFFu) p->seen_ = r.seq + 1;
+          if (r.len < 14 || r.len > kMaxFrame) { p->complete(r.seq); continue; }   // runt / oversize / own tx
+          const uint32_t in_port = r.in_port != ~0u ? r.in_port : pid;
+          const uint32_t o = nb > 1 ? owner(steer, nb, r.data, r.len, in_port) : 0u;
+          Q->lanes[o]->stage.push_back(Pkt{in_port, r.seq, r.data, r.len, p});
+          ++pk;
+          by += r.len;
+        }
+        p->count_rx(pk, by);
+        got += (uint32_t)pk;
+        return n;
       };
-      {
-        const uint32_t n = recirc_->rx(buf.data(), take);
-        for (uint32_t i = 0; i < n; ++i) stage(0, recirc_.get(), buf[i]);
-      }
+      if (q == 0) (void)read_port(0, recirc_.get(), take);
       // every port gets an equal share of the burst first (round-robin start), then leftovers
       const uint32_t np = (uint32_t)active.size();
       if (np) {
         const uint32_t share = std::max<uint32_t>(1, take / np);
-        for (int pass = 0; pass < 2 && got < take; ++pass) {
-          for (uint32_t k = 0; k < np && got < take; ++k) {
+        uint32_t taken = got;
+        for (int pass = 0; pass < 2 && taken < take; ++pass) {
+          for (uint32_t k = 0; k < np && taken < take; ++k) {
             const auto& a = active[(rr + k) % np];
-            const uint32_t n = a.second->rx(buf.data(), std::min(take - got, pass ? take : share));
-            for (uint32_t i = 0; i < n; ++i) stage(a.first, a.second, buf[i]);
+            taken += read_port(a.first, a.second, std::min(take - taken, pass ? take : share));
           }
         }
         rr = (rr + 1) % np;
       }
       if (got == 0) {
-        st_idle_.fetch_add(1, std::memory_order_relaxed);
+        st.add(st.idle, 1);
         _mm_pause();
         continue;
       }
-      for (auto& Lp : lanes_) {
-        Lane* L = Lp.get();
+      const std::vector<uint8_t>& side_ports = c->side_ports;
+      const bool side_always = c->side_always;
+      for (Lane* L : Q->lanes) {
         if (L->stage.empty()) continue;
-        std::lock_guard<std::mutex> pg(L->pub_mu);
         Backend& be = *L->be;
         const uint32_t k = (uint32_t)L->stage.size();
         const uint32_t npad = (k + 63u) & ~63u;
-        const uint64_t start = be.published();
-        uint32_t* im = be.in_meta();
+        const uint64_t start = be.published(q);
+        uint32_t* im = be.in_meta(q);
         const uint32_t cmask = be.capacity() - 1;
-        Burst& b = L->slots[L->head % inflight_];   // free: head - done < inflight
+        const uint64_t head = L->head.load(std::memory_order_relaxed);
+        Burst& b = L->slots[head % inflight_];   // free: head - done < inflight
         b.start = start;
         b.end = start + npad;
         b.t_rx_ns = t_rx;
-        b.side = false;
-        b.reps.clear();
-        b.xhdr.clear();
+        bool side = side_always;
         for (uint32_t i = 0; i < k; ++i) {
-          const Pkt& q = L->stage[i];
-          uint8_t* slot = be.in_slot((uint32_t)(start + i));
-          const uint32_t h = std::min<uint32_t>(q.len, kSlotBytes);
-          std::memcpy(slot, q.data, h);
+          const Pkt& pk = L->stage[i];
+          uint8_t* slot = be.in_slot(q, (uint32_t)(start + i));
+          const uint32_t h = std::min<uint32_t>(pk.len, kSlotBytes);
+          std::memcpy(slot, pk.data, h);
           if (h < kSlotBytes) std::memset(slot + h, 0, kSlotBytes - h);
-          im[(start + i) & cmask] = (q.port & 0xFFFFu) | (q.len << 16);
-          b.side = b.side || needs_side(q.port);
+          im[(start + i) & cmask] = (pk.port & 0xFFFFu) | (pk.len << 16);
+          side = side || (pk.port < side_ports.size() && side_ports[pk.port]);
         }
         for (uint32_t i = k; i < npad; ++i) im[(start + i) & cmask] = kRingPadMeta;
+        b.side = side;
         b.pkts.swap(L->stage);
         L->stage.clear();
-        b.id = L->head;
+        b.id = head;
         b.left.store(workers_, std::memory_order_relaxed);
         b.state.store(1, std::memory_order_release);
-        ++L->head;
+        L->head.store(head + 1, std::memory_order_release);
         const uint64_t tp0 = now_ns();
-        be.publish(npad);
-        st_pub_ns_.fetch_add(now_ns() - tp0, std::memory_order_relaxed);
-        st_bursts_.fetch_add(1, std::memory_order_relaxed);
+        be.publish(q, npad);
+        st.add(st.pub_ns, now_ns() - tp0);
+        st.add(st.bursts, 1);
       }
-      st_rx_.fetch_add(got, std::memory_order_relaxed);
+      st.add(st.rx, got);
     }
   } catch (const std::exception& e) {
     fail(std::string("rx: ") + e.what());
   }
 }
 
-void Engine::side_pass(Lane* L, uint64_t from_id) {
-  std::lock_guard<std::mutex> pg(L->pub_mu);   // no publish on this lane during the pass
+namespace {
+// side_stage's sink for one burst: replicas and outer headers stay with the burst, learn events
+// go to the learner (consecutive duplicates of one burst folded)
+struct BurstSink {
+  std::vector<Replica>& reps;
+  std::vector<uint8_t>& xbuf;
+  std::vector<uint8_t>& has_x;
+  std::vector<uint32_t>& learn_ev;
+  uint32_t i = 0;   // packet index in the burst
+  void rep(const uint32_t* hdr, uint32_t meta, uint32_t) {
+    reps.emplace_back();
+    Replica& r = reps.back();
+    r.src = i;
+    r.meta = meta;
+    std::memcpy(r.hdr, hdr, kSlotBytes);
+  }
+  void xhdr_rec(const uint32_t* x) {
+    std::memcpy(xbuf.data() + (size_t)i * kXhdrBytes, x, kXhdrBytes);
+    has_x[i] = 1;
+  }
+  void xhdr(const uint32_t* x, uint32_t) { xhdr_rec(x); }
+  void learn(uint32_t bridge, uint32_t lo, uint32_t hi, uint32_t port) {
+    const uint32_t e1 = (hi & 0xFFFFu) | (bridge << 16);
+    const size_t n = learn_ev.size();
+    if (n >= 4 && learn_ev[n - 4] == lo && learn_ev[n - 3] == e1 && learn_ev[n - 2] == port) return;
+    learn_ev.insert(learn_ev.end(), {lo, e1, port, 0u});
+  }
+};
+}  // namespace
+
+void Engine::side_work(Queue* Q, Lane* L, Burst& b, const Cfg& c, TxScratch& sc, uint32_t w) {
   Backend& be = *L->be;
-  const auto t0 = Clock::now();
-  while (be.completed() < be.published()) {     // nothing in flight: the side list is final
-    _mm_pause();
-    if (Clock::now() - t0 > std::chrono::seconds(5)) throw std::runtime_error("side pass: ring did not drain");
-  }
-  SideBatch sb;
-  be.side_pass(sb);
-  st_side_.fetch_add(1, std::memory_order_relaxed);
-  // Every listed packet belongs to a burst not delivered yet (earlier bursts were covered by
-  // earlier passes): hand each replica / outer header to its burst, from_id .. head - 1.
-  const uint32_t cap = be.capacity();
-  auto burst_of = [&](uint32_t pos) -> Burst* {
-    for (uint64_t id = from_id; id < L->head; ++id) {
-      Burst& b = L->slots[id % inflight_];
-      if (((pos - (uint32_t)b.start) & (cap - 1)) < (uint32_t)b.pkts.size()) return &b;
+  const uint32_t q = Q->id, cmask = be.capacity() - 1;
+  const uint32_t* om = be.out_meta(q);
+  const uint32_t* im = be.in_meta(q);
+  const uint32_t np = (uint32_t)b.pkts.size();
+  SideTables* stab = L->g < c.side.size() ? c.side[L->g].get() : nullptr;
+  if (!stab) return;   // no snapshot (no side features configured): flagged packets fall to deliver()'s checks
+  const TablesView& t = stab->view();
+  const TabHash hasher{&stab->hash()};
+  const std::vector<uint8_t>& sp = c.side_ports;
+  sc.learn.clear();
+  BurstSink sink{b.reps, b.xhdr, b.has_x, sc.learn};
+  std::shared_lock<std::shared_mutex> g(stab->mac_mu);   // the learner updates the snapshot's MAC table
+  for (uint32_t i = 0; i < np; ++i) {
+    const uint32_t pos = (uint32_t)((b.start + i) & cmask);
+    const uint32_t m = om[pos];
+    const uint32_t port = b.pkts[i].port;
+    if (!(m & (kMetaFlood | kMetaXhdr)) && !c.side_always && !(port < sp.size() && sp[port])) continue;
+    if ((m & kMetaXhdr) && b.xhdr.empty()) {
+      b.xhdr.assign((size_t)np * kXhdrBytes, 0);
+      b.has_x.assign(np, 0);
     }
-    return nullptr;
-  };
-  for (auto& r : sb.reps) {
-    Burst* b = burst_of(r.src_pos & (cap - 1));
-    if (b) b->reps.push_back(r);
+    sink.i = i;
+    side_stage(t, DirectTables{t}, reinterpret_cast<const uint32_t*>(be.in_slot(q, pos)), im[pos],
+               reinterpret_cast<const uint32_t*>(be.out_slot(q, pos)), m, i, sink, hasher);
   }
-  if (!sb.xall.empty()) {
-    for (uint64_t id = from_id; id < L->head; ++id) {
-      Burst& b = L->slots[id % inflight_];
-      for (uint32_t i = 0; i < (uint32_t)b.pkts.size(); ++i) {
-        const uint32_t pos = (uint32_t)((b.start + i) & (cap - 1));
-        if (be.out_meta()[pos] & kMetaXhdr)
-          b.xhdr.emplace_back(pos, std::vector<uint8_t>(sb.xall.begin() + (size_t)pos * kXhdrBytes,
-                                                        sb.xall.begin() + (size_t)(pos + 1) * kXhdrBytes));
+  g.unlock();
+  // replicas count where the batch path's side pass counts them (port tx / drop by reason)
+  for (const Replica& r : b.reps) {
+    const uint32_t rr = meta_reason(r.meta), p = meta_port(r.meta);
+    if (rr) {
+      auto& d = Q->side_drop[rr & (kNumReasons - 1)];
+      d.store(d.load(std::memory_order_relaxed) + 1, std::memory_order_relaxed);
+    } else if (p < (uint32_t)kMaxPorts) {
+      auto& cp = Q->side_ctr[2 * (size_t)p];
+      auto& cb = Q->side_ctr[2 * (size_t)p + 1];
+      cp.store(cp.load(std::memory_order_relaxed) + 1, std::memory_order_relaxed);
+      cb.store(cb.load(std::memory_order_relaxed) + meta_len(r.meta), std::memory_order_relaxed);
+    }
+  }
+  QStats& st = Q->wst[w];
+  st.add(st.side, 1);
+  if (!sc.learn.empty()) {
+    st.add(st.learn, sc.learn.size() / 4);
+    {
+      std::lock_guard<std::mutex> lk(learn_mu_);
+      if (learn_q_.size() < (1u << 20)) {
+        learn_q_.insert(learn_q_.end(), sc.learn.begin(), sc.learn.end());
+        ++learn_seq_;
+      } else {
+        learn_dropped_ += sc.learn.size() / 4;
       }
     }
+    learn_cv_.notify_one();
   }
-  L->side_upto = be.published();
 }
 
-void Engine::deliver(Lane* L, Burst& b, uint32_t w, std::vector<Port*>& touched) {
+void Engine::deliver(Queue* Q, Lane* L, Burst& b, uint32_t w, const Cfg& c, TxScratch& sc) {
   Backend& be = *L->be;
-  const uint32_t cmask = be.capacity() - 1;
-  const uint32_t* om = be.out_meta();
+  const uint32_t q = Q->id, cmask = be.capacity() - 1;
+  const uint32_t* om = be.out_meta(q);
   auto tab = std::atomic_load(&ports_);
-  auto mine = [&](uint32_t port) {
-    if (port < redirect_.size() && redirect_[port] != 0xFFFFFFFFu) port = redirect_[port];
-    return port % workers_ == w;
+  const std::vector<uint32_t>& red = c.redirect;
+  auto route = [&](uint32_t port) {   // tunnel port -> its underlay port
+    return port < red.size() && red[port] != 0xFFFFFFFFu ? red[port] : port;
   };
   TxTally tally;
+  auto add = [&](uint32_t port, const TxItem& it) {
+    if (port >= tab->size() || !(*tab)[port].p) { ++tally.no_port; return; }
+    auto& v = sc.by_port[port];
+    if (v.empty()) sc.touched.push_back(port);
+    v.push_back(it);
+  };
   const uint32_t np = (uint32_t)b.pkts.size();
-  constexpr uint32_t kAhead = 8;   // out slots / payloads of later packets are fetched ahead
+  constexpr uint32_t kAhead = 8;   // out slots of later packets are fetched ahead
   for (uint32_t i = 0; i < np; ++i) {
     if (i + kAhead < np) {
       const uint32_t pa = (uint32_t)((b.start + i + kAhead) & cmask);
-      if (meta_port(om[pa]) % workers_ == w) __builtin_prefetch(be.out_slot(pa), 0, 0);
+      if (route(meta_port(om[pa])) % workers_ == w) __builtin_prefetch(be.out_slot(q, pa), 0, 0);
     }
-    const Pkt& q = b.pkts[i];
+    const Pkt& pk = b.pkts[i];
     const uint32_t pos = (uint32_t)((b.start + i) & cmask);
     const uint32_t meta = om[pos];
     const uint32_t reason = meta_reason(meta), oport = meta_port(meta), olen = meta_len(meta);
     if (reason == 0) {
-      if (!mine(oport)) continue;
+      const uint32_t dst = route(oport);
+      if (dst % workers_ != w) continue;
       const uint8_t* x = nullptr;
       uint32_t xl = 0;
       if (meta & kMetaXhdr) {
-        for (const auto& e : b.xhdr)
-          if (e.first == pos) { x = e.second.data(); xl = xhdr_len(x); break; }
-        if (!x) { ++tally.drop; continue; }   // never sent bare
+        if (b.has_x.empty() || !b.has_x[i]) { ++tally.drop; continue; }   // never sent bare
+        x = b.xhdr.data() + (size_t)i * kXhdrBytes;
+        xl = xhdr_len(x);
       }
       uint32_t hl = 0, to = 0;
-      out_tail(q.len, olen, xl, hl, to);
-      if (to > q.len) to = q.len;
-      send(*tab, oport, x, xl, be.out_slot(pos), hl, q.data + to, q.len - to, touched, tally);
+      out_tail(pk.len, olen, xl, hl, to);
+      if (to > pk.len) to = pk.len;
+      add(dst, TxItem{x, xl, be.out_slot(q, pos), hl, pk.data + to, pk.len - to});
     } else if (w != 0) {
       continue;
-    } else if (reason == kRecirc && olen <= q.len) {
-      recirc_->push(oport, q.data + (q.len - olen), olen);   // terminated tunnel: the inner frame re-enters
-      st_recirc_.fetch_add(1, std::memory_order_relaxed);
+    } else if (reason == kRecirc && olen <= pk.len) {
+      recirc_->push(oport, pk.data + (pk.len - olen), olen);   // terminated tunnel: the inner frame re-enters
+      QStats& st = Q->wst[w];
+      st.add(st.recirc, 1);
     } else if (reason == kRecirc6) {
-      punt(q.port, reason, q.data, q.len, nullptr, 0);       // the VNI lookup needs the whole frame
+      punt(Q->wst[w], pk.port, reason, pk.data, pk.len, nullptr, 0);   // the VNI lookup needs the whole frame
     } else {
       ++tally.drop;
     }
   }
   for (const Replica& r : b.reps) {
-    const uint32_t i = (uint32_t)((r.src_pos - (uint32_t)b.start) & cmask);
-    const Pkt& q = b.pkts[i];
+    const Pkt& pk = b.pkts[r.src];
     uint32_t hl = 0, to = 0;
     const uint32_t rlen = meta_len(r.meta), rr = meta_reason(r.meta);
-    out_tail(q.len, rlen, 0, hl, to);
-    if (to > q.len) to = q.len;
+    out_tail(pk.len, rlen, 0, hl, to);
+    if (to > pk.len) to = pk.len;
     if (rr) {
-      if (w == 0) punt(q.port, rr, r.hdr, hl, q.data + to, q.len - to);   // ARP trap: the slow path's copy
-    } else if (mine(meta_port(r.meta))) {
-      send(*tab, meta_port(r.meta), nullptr, 0, r.hdr, hl, q.data + to, q.len - to, touched, tally);
-      ++tally.reps;
+      if (w == 0) punt(Q->wst[w], pk.port, rr, r.hdr, hl, pk.data + to, pk.len - to);   // ARP trap: the slow path's copy
+    } else {
+      const uint32_t dst = route(meta_port(r.meta));
+      if (dst % workers_ == w) {
+        add(dst, TxItem{nullptr, 0, r.hdr, hl, pk.data + to, pk.len - to});
+        ++tally.reps;
+      }
     }
   }
-  // one atomic per counter per burst (per-packet atomics on shared lines cost more than the copy)
-  if (tally.tx) st_tx_.fetch_add(tally.tx, std::memory_order_relaxed);
-  if (tally.full) st_tx_full_.fetch_add(tally.full, std::memory_order_relaxed);
-  if (tally.no_port) st_no_port_.fetch_add(tally.no_port, std::memory_order_relaxed);
-  if (tally.drop) st_drop_.fetch_add(tally.drop, std::memory_order_relaxed);
-  if (tally.reps) st_reps_.fetch_add(tally.reps, std::memory_order_relaxed);
+  // one locked batch per egress port
+  for (uint32_t port : sc.touched) {
+    auto& v = sc.by_port[port];
+    const uint32_t ok = (*tab)[port].p->tx_batch(v.data(), (uint32_t)v.size());
+    tally.tx += ok;
+    tally.full += v.size() - ok;
+    v.clear();
+  }
+  sc.touched.clear();
+  QStats& st = Q->wst[w];
+  st.add(st.tx, tally.tx);
+  st.add(st.tx_full, tally.full);
+  st.add(st.no_port, tally.no_port);
+  st.add(st.drop, tally.drop);
+  st.add(st.reps, tally.reps);
 }
 
 void Engine::finish(Lane* L, Burst& b) {
@@ -824,52 +1135,79 @@ void Engine::finish(Lane* L, Burst& b) {
   b.pkts.clear();
   b.reps.clear();
   b.xhdr.clear();
+  b.has_x.clear();
   L->freed_pos.store(b.end, std::memory_order_release);
   b.state.store(0, std::memory_order_release);
   L->done.fetch_add(1, std::memory_order_release);
 }
 
-void Engine::tx_loop(Lane* L, uint32_t w) {
+void Engine::tx_loop(Queue* Q, uint32_t w) {
   try {
-    L->be->thread_init();
-    const uint32_t cmask = L->be->capacity() - 1;
-    std::vector<Port*> touched;
-    for (uint64_t cur = 0;;) {
-      Burst& b = L->slots[cur % inflight_];
-      const uint32_t want = w == 0 ? 1u : 2u;
-      uint32_t spin = 0;
-      while (!(b.state.load(std::memory_order_acquire) >= want && b.id == cur)) {
-        if (!run_ && L->done.load() == L->head) return;
-        _mm_pause();
-        if ((++spin & 0xFFFFu) == 0) std::this_thread::yield();
-      }
-      if (w == 0) {
-        // leader: completion, side pass, then the burst is ready for every worker
-        const auto t0 = Clock::now();
-        spin = 0;
-        while (!L->be->range_done(b.start, b.end)) {
-          _mm_pause();
-          if ((++spin & 0xFFFu) == 0) {
-            const auto waited = Clock::now() - t0;
-            if (waited > std::chrono::milliseconds(200) && !L->be->alive())
-              throw std::runtime_error("tx: the ring kernel is gone (device deadline or fault)");
-            if (waited > std::chrono::seconds(5)) throw std::runtime_error("tx: burst not completed within 5 s");
+    TxScratch sc;
+    sc.by_port.resize((size_t)kMaxPorts + 2);
+    const uint32_t nl = (uint32_t)Q->lanes.size();
+    std::vector<uint64_t> cur(nl, 0);
+    std::vector<Clock::time_point> wait_since(nl);
+    std::vector<uint8_t> waiting(nl, 0);
+    const uint32_t want = w == 0 ? 1u : 2u;
+    uint32_t idle = 0;
+    QStats& st = Q->wst[w];
+    for (;;) {
+      bool any = false;
+      for (uint32_t li = 0; li < nl; ++li) {
+        Lane* L = Q->lanes[li];
+        Burst& b = L->slots[cur[li] % inflight_];
+        if (!(b.state.load(std::memory_order_acquire) >= want && b.id == cur[li])) continue;
+        if (w == 0) {
+          // leader: completion, side work, then the burst is ready for every worker
+          if (!L->be->range_done(Q->id, b.start, b.end)) {
+            if (!waiting[li]) { waiting[li] = 1; wait_since[li] = Clock::now(); }
+            else if ((++idle & 0xFFFu) == 0) {
+              const auto waited = Clock::now() - wait_since[li];
+              if (waited > std::chrono::milliseconds(200) && !L->be->alive())
+                throw std::runtime_error("tx: the ring kernel is gone (device deadline or fault)");
+              if (waited > std::chrono::seconds(5)) throw std::runtime_error("tx: burst not completed within 5 s");
+            }
+            continue;
           }
+          waiting[li] = 0;
+          const auto c = cfg();
+          bool side = b.side;
+          if (!side) {
+            const uint32_t* om = L->be->out_meta(Q->id);
+            const uint32_t cm = L->be->capacity() - 1;
+            for (uint64_t p = b.start; p < b.start + b.pkts.size() && !side; ++p)
+              side = (om[p & cm] & (kMetaFlood | kMetaXhdr)) != 0;
+          }
+          if (side) side_work(Q, L, b, *c, sc, w);
+          b.state.store(2, std::memory_order_release);
+          const uint64_t td0 = now_ns();
+          deliver(Q, L, b, w, *c, sc);
+          st.add(st.deliver_ns, now_ns() - td0);
+        } else {
+          const auto c = cfg();
+          const uint64_t td0 = now_ns();
+          deliver(Q, L, b, w, *c, sc);
+          st.add(st.deliver_ns, now_ns() - td0);
         }
-        bool side = b.side;
-        const uint32_t* om = L->be->out_meta();
-        for (uint64_t p = b.start; p < b.start + b.pkts.size() && !side; ++p)
-          side = (om[p & cmask] & (kMetaFlood | kMetaXhdr)) != 0;
-        if (side && b.end > L->side_upto) side_pass(L, cur);
-        b.state.store(2, std::memory_order_release);
+        if (b.left.fetch_sub(1, std::memory_order_acq_rel) == 1) finish(L, b);
+        ++cur[li];
+        any = true;
       }
-      const uint64_t td0 = now_ns();
-      touched.clear();
-      deliver(L, b, w, touched);
-      for (Port* p : touched) p->flush();
-      st_deliver_ns_.fetch_add(now_ns() - td0, std::memory_order_relaxed);
-      if (b.left.fetch_sub(1, std::memory_order_acq_rel) == 1) finish(L, b);
-      ++cur;
+      if (any) {
+        idle = 0;
+        continue;
+      }
+      if (abandon_.load(std::memory_order_relaxed)) return;
+      if (!run_.load(std::memory_order_relaxed)) {
+        bool drained = true;
+        for (uint32_t li = 0; li < nl; ++li)
+          drained = drained && Q->lanes[li]->done.load() == Q->lanes[li]->head.load() &&
+                    cur[li] == Q->lanes[li]->head.load();
+        if (drained) return;
+      }
+      _mm_pause();
+      if ((++idle & 0xFFFFu) == 0) std::this_thread::yield();
     }
   } catch (const std::exception& e) {
     fail(std::string("tx: ") + e.what());

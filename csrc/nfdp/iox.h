@@ -3,22 +3,32 @@
 // The reference's data ports never touch a per-frame interpreter loop: OvS-DPDK polls NIC / vhost
 // queues from PMD threads (ovs-dp/ovsdp.go:39-55 binds them `type=dpdk`), the IPU's FXP is
 // silicon.  This engine is the MI355X data plane's equivalent, in C++ with Python only
-// configuring it:
+// configuring it.  It is organised like a multi-queue NIC driver:
 //
-//   ports (memif shared-memory vports, AF_PACKET TPACKET_V2 rings on veth/netdevs, TAP fds)
-//     --rx thread--> owner GPU = owner_of(toeplitz(FlowKey), N) (the RSS a NIC would do; 1 GPU: 0)
-//       -> 64-B header slot + ingress meta written straight into that GPU's ring slots (pinned host
-//          memory the resident ring kernel reads over PCIe), bursts padded to whole 64-packet
-//          chunks, published at once (no batching delay: a lone packet is its own chunk)
-//     --tx thread per GPU--> completion flag -> egress meta -> frame = [outer hdr] ++ out slot[:hl]
-//          ++ in_frame[to:len] written to the egress port (the payload never left the rx buffer);
-//          side work (flood replicas, mirror / ARP copies, MAC learning, tunnel outer headers)
-//          through the side kernel; recirculation (tunnel termination) re-enters on the rx
-//          thread; slow-path frames (ARP trap, IPv6 termination) queue up for the control plane
+//   queue q (one rx thread + its tx workers) owns a group of ports
+//     --rx thread q--> owner GPU g = owner_of(toeplitz(FlowKey), N) (the RSS a NIC would do; 1 GPU: 0)
+//       -> 64-B header slot + ingress meta written straight into ring queue q of GPU g (pinned host
+//          memory the resident ring kernel reads over PCIe; one kernel per GPU serves every queue,
+//          ring.h), bursts padded to whole 64-packet chunks, published at once
+//     --tx workers of queue q--> completion flags of each lane (q, g) in order -> egress frames
+//          = [outer hdr] ++ out slot[:hl] ++ in_frame[to:len], written to the egress ports in one
+//          locked batch per port and burst (the payload never left the rx buffer)
+//     -> side work (flood replicas, mirror / ARP copies, MAC learning, tunnel outer headers) is done
+//          per burst by the tx leader on the CPU (pipeline.h side_stage over the burst's flagged
+//          packets, against a host snapshot of the tables): nothing waits for the ring to drain;
+//          learn events go to a learner thread that updates every GPU's MAC table
 //     -> rx buffers are handed back to their port in rx order once every frame below is sent.
 //
-// Backends: `GpuBackend` (RingEngine with host slots: the persistent HIP kernel) or
-// `OracleBackend` (the bit-exact C++ pipeline, synchronous: CPU tests / no-GPU nodes).
+// Queues share nothing on the packet path: no lock, no shared counter line (statistics are per
+// queue, port rx counters are per-burst stores of the single rx thread that owns the port).
+// Configuration the threads read (steering, redirects, side ports, side tables) is published
+// copy-on-write (RCU style): a commit swaps it in without stopping traffic; `hold()` briefly
+// stops publication (no drain) so an epoch flip on every GPU plus a configuration swap take
+// effect between two bursts of every queue.
+//
+// Backends: `GpuBackend` (RingEngine with host slots and one ring queue per engine queue: the
+// persistent HIP kernel) or `OracleBackend` (the bit-exact C++ pipeline, synchronous: CPU tests /
+// no-GPU nodes).
 #pragma once
 #include <atomic>
 #include <condition_variable>
@@ -26,6 +36,7 @@
 #include <deque>
 #include <memory>
 #include <mutex>
+#include <shared_mutex>
 #include <string>
 #include <thread>
 #include <unordered_map>
@@ -46,6 +57,20 @@ namespace iox {
 uint32_t frame_owner(const uint8_t* hdr, uint32_t len, uint32_t in_port, const PortEntry* ports, const uint8_t* rss_key,
                      uint32_t n, bool v6 = false);
 
+// Toeplitz hash from byte tables (16 key bytes x 256 values, XOR-linear in the key): the CPU
+// twin of the kernels' LDS byte tables, ~20x the bit-serial toeplitz_scalar.  Bit-exact with it.
+struct ToeplitzTab {
+  std::vector<uint32_t> tab;   // [16][256]
+  ToeplitzTab() = default;
+  explicit ToeplitzTab(const uint8_t* rss_key);
+  uint32_t operator()(const FlowKey& k) const {
+    const uint32_t w[4] = {k.src_ip, k.dst_ip, k.ports, k.meta};
+    uint32_t h = 0;
+    for (int b = 0; b < 16; ++b) h ^= tab[(size_t)b * 256 + ((w[b >> 2] >> (8 * (b & 3))) & 0xFFu)];
+    return h;
+  }
+};
+
 // ---------------------------------------------------------------------------------- ports
 struct RxRef {
   const uint8_t* data;
@@ -54,22 +79,38 @@ struct RxRef {
   uint32_t in_port;   // ingress port for the pipeline (~0u: the port's own id)
 };
 
+// One frame of a tx batch, assembled from up to three pieces (outer header, rewritten header,
+// payload tail).
+struct TxItem {
+  const uint8_t* a; uint32_t na;
+  const uint8_t* b; uint32_t nb;
+  const uint8_t* c; uint32_t nc;
+};
+
 class Port {
  public:
   explicit Port(uint32_t window);
   virtual ~Port() = default;
   // Up to `max` received frames; each stays valid until its sequence number is released.
   virtual uint32_t rx(RxRef* out, uint32_t max) = 0;
-  // Frame assembled from up to three pieces (outer header, rewritten header, payload tail);
-  // false when the port has no room (dropped, as on a full NIC queue).  Thread safe.
-  bool tx(const uint8_t* a, uint32_t na, const uint8_t* b, uint32_t nb, const uint8_t* c, uint32_t nc);
-  void flush();
-  // A frame is done (sent or dropped): any thread.  reclaim(): rx thread only.
+  // A batch of frames under one lock acquisition and one ring commit; returns how many were
+  // written (the rest found no room and are dropped, as on a full NIC queue).  Thread safe.
+  uint32_t tx_batch(const TxItem* items, uint32_t n);
+  bool tx(const uint8_t* a, uint32_t na, const uint8_t* b, uint32_t nb, const uint8_t* c, uint32_t nc) {
+    const TxItem it{a, na, b, nb, c, nc};
+    return tx_batch(&it, 1) == 1;
+  }
+  // A frame is done (sent or dropped): any thread.  reclaim(): the owning rx thread only.
   void complete(uint32_t seq) { done_[seq & mask_].store(1, std::memory_order_release); }
   void reclaim();
   virtual std::string kind() const = 0;
-  // rx counters (rx thread) and tx counters (one delivery worker per port) on separate lines
+  // rx counters: single writer (the rx thread owning the port) adds a burst at a time
+  void count_rx(uint64_t pkts, uint64_t bytes) {
+    rx_pkts.store(rx_pkts.load(std::memory_order_relaxed) + pkts, std::memory_order_relaxed);
+    rx_bytes.store(rx_bytes.load(std::memory_order_relaxed) + bytes, std::memory_order_relaxed);
+  }
   alignas(64) std::atomic<uint64_t> rx_pkts{0}, rx_bytes{0};
+  // tx counters: updated under the tx lock, once per batch
   alignas(64) std::atomic<uint64_t> tx_pkts{0}, tx_full{0}, tx_bytes{0};
 
  protected:
@@ -79,7 +120,6 @@ class Port {
   void set_first_seq(uint32_t s) { rel_ = s; seen_ = s; }
   uint32_t window() const { return mask_ + 1; }
   std::mutex tx_mu_;
-  bool tx_dirty_ = false;
 
  private:
   std::unique_ptr<std::atomic<uint8_t>[]> done_;
@@ -148,7 +188,6 @@ class FdPort : public Port {
   int fd_;
   uint32_t nbufs_, bsize_;
   std::vector<uint8_t> bufs_;
-  std::vector<uint32_t> lens_;
   uint32_t next_ = 0;
   std::atomic<uint32_t> freed_{0};
   std::vector<uint8_t> txbuf_;
@@ -173,35 +212,60 @@ class RecircPort : public Port {
   uint32_t next_ = 0, base_ = 0;
 };
 
-// ---------------------------------------------------------------------------------- backends
-struct Replica {
-  uint32_t src_pos;     // ring position of the source packet
-  uint32_t meta;
-  uint8_t hdr[kSlotBytes];
-};
-struct SideBatch {
-  std::vector<Replica> reps;
-  std::vector<uint8_t> xall;   // capacity x kXhdrBytes outer-header records by ring slot (tunnels only)
-  uint32_t learned = 0;
+// ---------------------------------------------------------------------------------- side tables
+// Host copies of the tables the side pass reads (ports, MAC table, LAG, flood groups, tunnels,
+// RSS key), taken at commit time: the control plane may change its own models at any moment,
+// the tx leaders read this immutable-but-for-learning snapshot.
+class SideTables {
+ public:
+  struct Src {   // host arrays (copied)
+    const PortEntry* ports; size_t n_ports;
+    const MacEntry* macs; uint32_t mac_mask;
+    const uint16_t* lag; uint32_t n_lag_groups;
+    const uint16_t* flood; size_t flood_rows; uint32_t n_flood;
+    const TunnelEntry* tunnels; uint32_t n_tunnels;
+    const Tunnel6Entry* tunnels6; uint32_t n_tunnels6;
+    const uint8_t* rss_key;
+    bool v6;   // IPv6 flows / rules in the data plane: IPv6 keys are folded (make_key)
+  };
+  explicit SideTables(const Src& s);
+  const TablesView& view() const { return t_; }
+  const ToeplitzTab& hash() const { return hash_; }
+  // learning (learner thread) vs the side pass's learn check (tx leaders)
+  std::shared_mutex mac_mu;
+  MacEntry* macs() { return macs_.data(); }
+  uint32_t mac_mask() const { return t_.mac_mask; }
+  bool has_macs() const { return !macs_.empty(); }
+
+ private:
+  TablesView t_{};
+  std::vector<PortEntry> ports_;
+  std::vector<MacEntry> macs_;
+  std::vector<uint16_t> lag_, flood_;
+  std::vector<TunnelEntry> tun_;
+  std::vector<Tunnel6Entry> tun6_;
+  std::vector<uint8_t> rss_;
+  ToeplitzTab hash_;
 };
 
+// ---------------------------------------------------------------------------------- backends
 class Backend {
  public:
   virtual ~Backend() = default;
-  virtual uint32_t capacity() const = 0;
-  virtual uint8_t* in_slot(uint32_t pos) = 0;      // pos: ring position (mod capacity)
-  virtual uint32_t* in_meta() = 0;
-  virtual const uint8_t* out_slot(uint32_t pos) = 0;
-  virtual const uint32_t* out_meta() = 0;
-  virtual uint64_t published() = 0;
-  virtual uint64_t publish(uint32_t n) = 0;        // multiple of 64
-  virtual uint64_t completed() = 0;
-  virtual bool range_done(uint64_t start, uint64_t end) = 0;   // positions [start, end) processed
-  virtual bool ready() = 0;                         // can take a publish now (ring running)
-  virtual bool alive() { return true; }             // the pipeline still makes progress (slow check)
-  // Side pass over every completed slot the pipeline listed since the last pass (call only when
-  // completed() == published(): nothing is in flight).
-  virtual void side_pass(SideBatch& out) = 0;
+  virtual uint32_t queues() const = 0;
+  virtual uint32_t capacity() const = 0;                         // slots per queue
+  virtual uint8_t* in_slot(uint32_t q, uint32_t pos) = 0;        // pos: ring position (mod capacity)
+  virtual uint32_t* in_meta(uint32_t q) = 0;
+  virtual const uint8_t* out_slot(uint32_t q, uint32_t pos) = 0;
+  virtual const uint32_t* out_meta(uint32_t q) = 0;
+  virtual uint64_t published(uint32_t q) = 0;
+  virtual uint64_t publish(uint32_t q, uint32_t n) = 0;           // multiple of 64
+  virtual bool range_done(uint32_t q, uint64_t start, uint64_t end) = 0;   // positions [start, end) processed
+  virtual bool ready() = 0;                                       // can take a publish now (ring running)
+  virtual bool alive() { return true; }                           // the pipeline still makes progress (slow check)
+  // MAC-learn events ({mac_lo, mac_hi | bridge << 16, port, 0} each) into the MAC table the
+  // pipeline reads; learner thread only.
+  virtual void apply_learn(const uint32_t* ev, uint32_t n, uint32_t stamp) = 0;
   virtual void thread_init() {}
 };
 
@@ -209,61 +273,59 @@ class GpuBackend : public Backend {
  public:
   explicit GpuBackend(RingEngine* ring);
   ~GpuBackend() override;
+  uint32_t queues() const override { return ring_->queues(); }
   uint32_t capacity() const override { return ring_->capacity(); }
-  uint8_t* in_slot(uint32_t pos) override { return in_ + (size_t)(pos & (capacity() - 1)) * kSlotBytes; }
-  uint32_t* in_meta() override { return im_; }
-  const uint8_t* out_slot(uint32_t pos) override { return out_ + (size_t)(pos & (capacity() - 1)) * kSlotBytes; }
-  const uint32_t* out_meta() override { return om_; }
-  uint64_t published() override { return ring_->published(); }
-  uint64_t publish(uint32_t n) override { return ring_->publish(n, false); }
-  uint64_t completed() override { return ring_->completed(); }
-  bool range_done(uint64_t start, uint64_t end) override { return ring_->range_done(start, end); }
+  uint8_t* in_slot(uint32_t q, uint32_t pos) override { return in_ + ((size_t)q * cap_ + (pos & (cap_ - 1))) * kSlotBytes; }
+  uint32_t* in_meta(uint32_t q) override { return im_ + (size_t)q * cap_; }
+  const uint8_t* out_slot(uint32_t q, uint32_t pos) override { return out_ + ((size_t)q * cap_ + (pos & (cap_ - 1))) * kSlotBytes; }
+  const uint32_t* out_meta(uint32_t q) override { return om_ + (size_t)q * cap_; }
+  uint64_t published(uint32_t q) override { return ring_->published(q); }
+  uint64_t publish(uint32_t q, uint32_t n) override { return ring_->publish(n, false, q); }
+  bool range_done(uint32_t q, uint64_t start, uint64_t end) override { return ring_->range_done(start, end, q); }
   bool ready() override { return ring_->running(); }
   bool alive() override { return ring_->alive(); }
-  void side_pass(SideBatch& out) override;
+  void apply_learn(const uint32_t* ev, uint32_t n, uint32_t stamp) override;
   void thread_init() override;
-  uint32_t stamp = 1;
 
  private:
   RingEngine* ring_;
+  uint32_t cap_;
   uint8_t* in_; uint32_t* im_; uint8_t* out_; uint32_t* om_;
-  hipStream_t side_stream_{};
-  std::vector<uint32_t> h_cnt_, h_meta_, h_src_, h_hdr_;
+  hipStream_t learn_stream_{};
+  uint32_t* d_learn_ = nullptr;   // device: [cap] events, then count + dropped words
+  uint32_t learn_cap_ = 0;
 };
 
 class OracleBackend : public Backend {
  public:
-  explicit OracleBackend(uint32_t capacity);
+  explicit OracleBackend(uint32_t capacity, uint32_t queues = 1);
+  uint32_t queues() const override { return nq_; }
   uint32_t capacity() const override { return cap_; }
-  uint8_t* in_slot(uint32_t pos) override { return in_.data() + (size_t)(pos & (cap_ - 1)) * kSlotBytes; }
-  uint32_t* in_meta() override { return im_.data(); }
-  const uint8_t* out_slot(uint32_t pos) override { return out_.data() + (size_t)(pos & (cap_ - 1)) * kSlotBytes; }
-  const uint32_t* out_meta() override { return om_.data(); }
-  uint64_t published() override { return prod_; }
-  uint64_t publish(uint32_t n) override;
-  uint64_t completed() override { return prod_; }
-  bool range_done(uint64_t, uint64_t end) override { return end <= prod_; }
-  bool ready() override { return configured_; }
-  void side_pass(SideBatch& out) override;
-  // tables / counters / side buffers of the CPU DataPlane (replaced after every commit, while
-  // the engine is paused)
-  void configure(const TablesView& t, uint64_t* flow_ctr, uint64_t* port_ctr, uint64_t* drop_ctr, const SideOut& side,
-                 MacEntry* macs, uint32_t mac_mask);
-  uint32_t stamp = 1;
+  uint8_t* in_slot(uint32_t q, uint32_t pos) override { return in_.data() + ((size_t)q * cap_ + (pos & (cap_ - 1))) * kSlotBytes; }
+  uint32_t* in_meta(uint32_t q) override { return im_.data() + (size_t)q * cap_; }
+  const uint8_t* out_slot(uint32_t q, uint32_t pos) override { return out_.data() + ((size_t)q * cap_ + (pos & (cap_ - 1))) * kSlotBytes; }
+  const uint32_t* out_meta(uint32_t q) override { return om_.data() + (size_t)q * cap_; }
+  uint64_t published(uint32_t q) override { return prod_[q].load(std::memory_order_acquire); }
+  uint64_t publish(uint32_t q, uint32_t n) override;
+  bool range_done(uint32_t q, uint64_t, uint64_t end) override { return end <= published(q); }
+  bool ready() override { return configured_.load(); }
+  void apply_learn(const uint32_t* ev, uint32_t n, uint32_t stamp) override;
+  // tables / counters of the CPU DataPlane (replaced after every commit, while the engine is paused)
+  void configure(const TablesView& t, uint64_t* flow_ctr, uint64_t* port_ctr, uint64_t* drop_ctr, MacEntry* macs,
+                 uint32_t mac_mask);
 
  private:
-  void run_segment(uint32_t pos, uint32_t n);
-  uint32_t cap_;
+  void run_segment(uint32_t q, uint32_t pos, uint32_t n);
+  uint32_t cap_, nq_;
   std::vector<uint8_t> in_, out_;
   std::vector<uint32_t> im_, om_;
-  uint64_t prod_ = 0;
-  bool configured_ = false;
+  std::unique_ptr<std::atomic<uint64_t>[]> prod_;
+  std::atomic<bool> configured_{false};
+  std::mutex run_mu_;   // the pipeline's counters / MAC table are shared by every queue
   TablesView t_{};
   uint64_t *flow_ctr_ = nullptr, *port_ctr_ = nullptr, *drop_ctr_ = nullptr;
-  SideOut side_{};
   MacEntry* macs_ = nullptr;
   uint32_t mac_mask_ = 0;
-  SideBatch pending_;
 };
 
 // ---------------------------------------------------------------------------------- engine
@@ -273,34 +335,64 @@ struct Punt {
   std::vector<uint8_t> frame;
 };
 
+struct Replica {
+  uint32_t src;         // index of the source packet in its burst
+  uint32_t meta;
+  uint8_t hdr[kSlotBytes];
+};
+
 class Engine {
  public:
-  // burst: frames per publish (at most); inflight: bursts in flight per backend; tx_workers:
-  // delivery threads per backend (each owns the egress ports with port % tx_workers == its index,
-  // so frames of one port leave in order)
-  Engine(uint32_t burst, uint32_t inflight_bursts, uint32_t tx_workers = 1);
+  // burst: frames per publish (at most); inflight: bursts in flight per lane; tx_workers:
+  // delivery threads per queue (each owns the egress ports with port % tx_workers == its index,
+  // so frames of one port from one queue leave in order); queues: rx threads (each with its
+  // ring queue on every backend); max_inflight_frames: frames in flight per lane (bounds the
+  // engine's own queueing delay: frames beyond it wait in the ports' rings).
+  Engine(uint32_t burst, uint32_t inflight_bursts, uint32_t tx_workers = 1, uint32_t queues = 1,
+         uint32_t max_inflight_frames = 0);
   ~Engine();
   void add_backend(std::shared_ptr<Backend> b);       // index = GPU (shard) number
-  void add_port(uint32_t id, std::shared_ptr<Port> p);
+  // queue: the rx thread serving the port (-1: the least loaded queue)
+  void add_port(uint32_t id, std::shared_ptr<Port> p, int queue = -1);
   void inject(uint32_t in_port, const uint8_t* f, uint32_t n) { recirc_->push(in_port, f, n); }
   std::shared_ptr<Port> remove_port(uint32_t id);
   std::shared_ptr<Port> port(uint32_t id);
-  // Host-side steering inputs (N > 1): a copy of the port table and the RSS key.
+  int port_queue(uint32_t id);
+  // Configuration (copy-on-write: safe while traffic flows).
   void set_steering(const std::vector<PortEntry>& ports, const std::vector<uint8_t>& rss_key, bool v6 = false);
-  void set_redirect(uint32_t port, uint32_t underlay);   // tunnel port -> its underlay port
-  void set_side_ports(const std::vector<uint32_t>& ports); // ingress ports whose packets may need side work
-  void set_side_always(bool on) { side_always_.store(on); }
+  void set_redirects(const std::vector<std::pair<uint32_t, uint32_t>>& tunnel_to_underlay);   // replaces all
+  void set_redirect(uint32_t port, uint32_t underlay);   // one entry (0xFFFFFFFF clears it)
+  void set_side_ports(const std::vector<uint32_t>& ports); // ingress ports whose packets need side work
+  void set_side_always(bool on);
+  void set_side_tables(uint32_t backend, std::shared_ptr<SideTables> t);
   void start();
   void stop();
   void pause();    // no publish until resume(); returns once nothing is in flight
   void resume();
+  // hold(): no publish until release(), without waiting for the bursts in flight (a commit's
+  // epoch flips land between two bursts of every queue); returns once every rx thread holds.
+  void hold();
+  void release();
   bool running() const { return run_.load(); }
+  uint32_t queues() const { return nq_; }
   std::string error() const;
   std::vector<Punt> take_punts(size_t max);
   std::vector<double> take_latency_us();              // rx -> tx time per burst (engine side)
   std::unordered_map<std::string, uint64_t> stats() const;
+  // [kMaxPorts][2] replica tx pkts / bytes (side pass output, not in the pipeline's counters)
+  std::vector<uint64_t> side_port_counters() const;
+  std::vector<uint64_t> side_drop_counters() const;   // [kNumReasons]
   uint32_t owner_of_frame(const uint8_t* f, uint32_t len, uint32_t in_port) const;
   void inject_failure(const std::string& what) { fail(what); }   // fault injection (tests)
+  // wait until every learn event found so far is applied (tests / commit ordering)
+  void flush_learning();
+  // last-seen stamp of learned MAC entries (the control plane's aging clock): never goes back
+  uint32_t learn_stamp() const { return learn_stamp_.load(); }
+  void set_learn_stamp(uint32_t s) {
+    uint32_t c = learn_stamp_.load();
+    while (s > c && !learn_stamp_.compare_exchange_weak(c, s)) {
+    }
+  }
 
  private:
   struct Pkt { uint32_t port; uint32_t seq; const uint8_t* data; uint32_t len; Port* holder; };
@@ -308,59 +400,104 @@ class Engine {
     uint64_t id = ~0ull;   // burst number on its lane (slot = id % inflight)
     uint64_t start = 0, end = 0;   // ring positions [start, end)
     std::vector<Pkt> pkts;
-    bool side = false;
+    bool side = false;     // some ingress port needs side work
     uint64_t t_rx_ns = 0;
-    std::vector<Replica> reps;                                    // side-pass output for this burst
-    std::vector<std::pair<uint32_t, std::vector<uint8_t>>> xhdr;  // (position, outer-header record)
+    std::vector<Replica> reps;          // side-pass output for this burst
+    std::vector<uint8_t> xhdr;          // per packet kXhdrBytes outer-header record (tunnels)
+    std::vector<uint8_t> has_x;         // per packet: xhdr record present
     std::atomic<uint32_t> state{0};   // 0 free, 1 published, 2 ready to deliver (completed + side done)
     std::atomic<uint32_t> left{0};    // delivery workers still working on it
   };
-  struct Lane {                 // one backend + its delivery workers
+  struct Lane {                 // (queue, backend): one ring queue and its bursts
     std::shared_ptr<Backend> be;
-    std::mutex pub_mu;          // rx thread's staging + publish vs the leader's side pass
+    uint32_t q = 0, g = 0;
     std::unique_ptr<Burst[]> slots;
-    uint64_t head = 0;          // rx thread: next burst id
-    std::atomic<uint64_t> done{0};   // bursts fully delivered (in order)
+    std::atomic<uint64_t> head{0};        // rx thread: next burst id
+    std::atomic<uint64_t> done{0};        // bursts fully delivered (in order)
     std::atomic<uint64_t> freed_pos{0};   // ring position below which every slot is delivered (reusable)
-    std::vector<std::thread> th;
     std::vector<Pkt> stage;     // rx thread: frames bound for this backend
-    uint64_t side_upto = 0;     // published count covered by the last side pass (leader only)
   };
-  using PortTab = std::vector<std::shared_ptr<Port>>;
-  void rx_loop();
-  void tx_loop(Lane* L, uint32_t w);
-  void deliver(Lane* L, Burst& b, uint32_t w, std::vector<Port*>& touched);
-  void finish(Lane* L, Burst& b);
-  void side_pass(Lane* L, uint64_t from_id);
-  bool needs_side(uint32_t in_port) const;
+  struct alignas(64) QStats {
+    std::atomic<uint64_t> rx{0}, tx{0}, drop{0}, punt{0}, recirc{0}, reps{0}, bursts{0}, side{0}, no_port{0},
+        tx_full{0}, pub_ns{0}, deliver_ns{0}, idle{0}, wait_tx{0}, learn{0}, held{0};
+    void add(std::atomic<uint64_t>& c, uint64_t v) { if (v) c.store(c.load(std::memory_order_relaxed) + v, std::memory_order_relaxed); }
+  };
+  struct Queue {                // one rx thread + its tx workers
+    uint32_t id = 0;
+    std::vector<Lane*> lanes;   // one per backend
+    std::thread rx;
+    std::vector<std::thread> tx;
+    std::atomic<uint64_t> held_epoch{0};   // last control epoch (pause / hold) the rx thread acknowledged
+    QStats st;                  // rx-thread counters
+    std::unique_ptr<QStats[]> wst;   // per tx worker
+    std::unique_ptr<std::atomic<uint64_t>[]> side_ctr;   // per worker x kMaxPorts x 2 (replica tx pkts / bytes)
+    std::unique_ptr<std::atomic<uint64_t>[]> side_drop;  // per worker x kNumReasons
+    std::atomic<uint32_t> nports{0};
+  };
+  struct PortRef { std::shared_ptr<Port> p; uint32_t q = 0; };
+  using PortTab = std::vector<PortRef>;
+  struct Steer {
+    std::vector<PortEntry> ports;
+    std::vector<uint8_t> rss_key;
+    bool v6 = false;
+    ToeplitzTab hash;
+  };
+  struct Cfg {                   // everything the packet threads read from the control plane
+    std::vector<uint32_t> redirect;      // tunnel port -> underlay port (0xFFFFFFFF: none)
+    std::vector<uint8_t> side_ports;     // ingress ports with side work
+    bool side_always = false;
+    std::shared_ptr<const Steer> steer;
+    std::vector<std::shared_ptr<SideTables>> side;   // per backend
+  };
   struct TxTally { uint64_t tx = 0, full = 0, no_port = 0, drop = 0, reps = 0; };
-  void send(const PortTab& tab, uint32_t port, const uint8_t* x, uint32_t nx, const uint8_t* h, uint32_t nh,
-            const uint8_t* t, uint32_t nt, std::vector<Port*>& touched, TxTally& tally);
-  void punt(uint32_t in_port, uint32_t reason, const uint8_t* a, uint32_t na, const uint8_t* b, uint32_t nb);
-  void fail(const std::string& what);
+  struct TxScratch {            // per tx worker
+    std::vector<std::vector<TxItem>> by_port;
+    std::vector<uint32_t> touched;
+    std::vector<uint32_t> learn;   // learn events of the current burst
+  };
 
-  uint32_t burst_, inflight_, workers_;
-  std::vector<std::unique_ptr<Lane>> lanes_;
+  void rx_loop(Queue* Q);
+  void tx_loop(Queue* Q, uint32_t w);
+  void learner_loop();
+  void deliver(Queue* Q, Lane* L, Burst& b, uint32_t w, const Cfg& cfg, TxScratch& sc);
+  void side_work(Queue* Q, Lane* L, Burst& b, const Cfg& cfg, TxScratch& sc, uint32_t w);
+  void finish(Lane* L, Burst& b);
+  bool lanes_idle() const;
+  void punt(QStats& st, uint32_t in_port, uint32_t reason, const uint8_t* a, uint32_t na, const uint8_t* b, uint32_t nb);
+  void fail(const std::string& what);
+  std::shared_ptr<const Cfg> cfg() const { return std::atomic_load(&cfg_); }
+  template <class F> void update_cfg(F f);
+  static uint32_t owner(const Steer* s, uint32_t n, const uint8_t* f, uint32_t len, uint32_t in_port);
+
+  uint32_t burst_, inflight_, workers_, nq_, max_frames_;
+  std::vector<std::unique_ptr<Lane>> lanes_;     // q * nbackends + g
+  std::vector<std::shared_ptr<Backend>> backends_;
+  std::vector<std::unique_ptr<Queue>> queues_;
   mutable std::mutex ports_mu_;
   std::shared_ptr<const PortTab> ports_;              // copy-on-write snapshot, by port id
   std::shared_ptr<RecircPort> recirc_;
-  std::vector<uint32_t> redirect_;
-  std::vector<uint8_t> side_ports_;
-  std::atomic<bool> side_always_{false};
-  std::vector<PortEntry> steer_ports_;
-  bool steer_v6_ = false;
-  std::vector<uint8_t> rss_key_;
-  std::atomic<bool> run_{false}, pause_{false}, paused_ack_{false};
-  std::thread rx_th_;
+  mutable std::mutex cfg_mu_;                         // writers of cfg_
+  std::shared_ptr<const Cfg> cfg_;
+  std::atomic<bool> run_{false}, abandon_{false};
+  // pause / hold requests (counters: nested commits of several data planes are fine); an rx
+  // thread that sees one acknowledges the current control epoch before idling
+  std::atomic<uint32_t> pause_n_{0}, hold_n_{0};
+  std::atomic<uint64_t> ctl_epoch_{0};
   mutable std::mutex err_mu_;
   std::string err_;
   std::mutex punt_mu_;
   std::deque<Punt> punts_;
+  std::atomic<uint64_t> punt_drop_{0};
   std::mutex lat_mu_;
   std::vector<double> lat_us_;
-  std::atomic<uint64_t> st_rx_{0}, st_tx_{0}, st_drop_{0}, st_punt_{0}, st_recirc_{0}, st_reps_{0}, st_bursts_{0},
-      st_side_{0}, st_no_port_{0}, st_punt_drop_{0}, st_tx_full_{0}, st_pub_ns_{0}, st_deliver_ns_{0},
-      st_idle_{0}, st_wait_tx_{0};
+  // learning: tx leaders -> learner thread -> every backend's MAC table + every side snapshot
+  mutable std::mutex learn_mu_;
+  std::condition_variable learn_cv_;
+  std::vector<uint32_t> learn_q_;
+  uint64_t learn_seq_ = 0, learn_applied_ = 0, learn_applied_n_ = 0, learn_dropped_ = 0;
+  bool learner_run_ = false;
+  std::atomic<uint32_t> learn_stamp_{1};
+  std::thread learner_;
 };
 
 }  // namespace iox

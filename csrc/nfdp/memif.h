@@ -101,11 +101,25 @@ class Region {
       hdr()->buf_size = buf_size;
       std::atomic_thread_fence(std::memory_order_release);
       hdr()->magic = kMagic;
-    } else if (hdr()->magic != kMagic || hdr()->version != kVersion ||
-               bytes_ < region_bytes(hdr()->ring_size, hdr()->buf_size)) {
-      close();
-      throw std::runtime_error("memif: " + path + " is not a memif region");
+    } else {
+      // the peer can rewrite the shared header at any time: read the geometry ONCE, validate it
+      // against the mapping, and never look at the shared copy again
+      ring_size = hdr()->ring_size;
+      buf_size = hdr()->buf_size;
+      std::atomic_thread_fence(std::memory_order_acquire);
+      if (hdr()->magic != kMagic || hdr()->version != kVersion || ring_size < 2 || (ring_size & (ring_size - 1)) ||
+          ring_size > (1u << 20) || buf_size < 64 || buf_size > (1u << 16) || bytes_ < region_bytes(ring_size, buf_size)) {
+        close();
+        throw std::runtime_error("memif: " + path + " is not a memif region");
+      }
     }
+    // private geometry: every index below is masked with these, so a peer that corrupts the
+    // shared header or descriptors can at worst garble its own frames, never reach outside the map
+    ring_size_ = ring_size;
+    mask_ = ring_size - 1;
+    buf_size_ = buf_size;
+    desc_base_ = base_ + sizeof(Hdr) + 2 * sizeof(Ctl);
+    buf_base_ = desc_base_ + 2 * (size_t)ring_size * sizeof(Desc);
     path_ = path;
   }
   void close() {
@@ -117,22 +131,25 @@ class Region {
   bool is_open() const { return base_ != nullptr; }
   const std::string& path() const { return path_; }
   Hdr* hdr() const { return reinterpret_cast<Hdr*>(base_); }
-  uint32_t ring_size() const { return hdr()->ring_size; }
-  uint32_t mask() const { return hdr()->ring_size - 1; }
-  uint32_t buf_size() const { return hdr()->buf_size; }
-  Ctl* ctl(int r) const { return reinterpret_cast<Ctl*>(base_ + sizeof(Hdr)) + r; }
-  Desc* desc(int r) const {
-    return reinterpret_cast<Desc*>(base_ + sizeof(Hdr) + 2 * sizeof(Ctl)) + (size_t)r * ring_size();
-  }
+  size_t bytes() const { return bytes_; }
+  uint8_t* base() const { return base_; }
+  // geometry: private snapshots taken at open (never re-read from the shared header)
+  uint32_t ring_size() const { return ring_size_; }
+  uint32_t mask() const { return mask_; }
+  uint32_t buf_size() const { return buf_size_; }
+  Ctl* ctl(int r) const { return reinterpret_cast<Ctl*>(base_ + sizeof(Hdr)) + (r & 1); }
+  Desc* desc(int r) const { return reinterpret_cast<Desc*>(desc_base_) + (size_t)(r & 1) * ring_size_; }
   uint8_t* buf(int r, uint32_t slot) const {
-    uint8_t* b0 = base_ + sizeof(Hdr) + 2 * sizeof(Ctl) + 2 * (size_t)ring_size() * sizeof(Desc);
-    return b0 + ((size_t)r * ring_size() + (slot & mask())) * buf_size();
+    return buf_base_ + ((size_t)(r & 1) * ring_size_ + (slot & mask_)) * buf_size_;
   }
 
  private:
   int fd_ = -1;
   uint8_t* base_ = nullptr;
   size_t bytes_ = 0;
+  uint32_t ring_size_ = 0, mask_ = 0, buf_size_ = 0;
+  uint8_t* desc_base_ = nullptr;
+  uint8_t* buf_base_ = nullptr;
   std::string path_;
 };
 
@@ -176,14 +193,18 @@ struct Consumer {
   int ring = 0;
   uint32_t next = 0;         // next slot to read
   uint32_t head_cache = 0;
+  uint32_t released = 0;     // slots below this went back to the producer
   void init(const Region* reg, int rg) {
     r = reg; ring = rg;
-    next = r->ctl(rg)->tail.load(std::memory_order_relaxed);
+    next = released = r->ctl(rg)->tail.load(std::memory_order_relaxed);
     head_cache = r->ctl(rg)->head.load(std::memory_order_acquire);
   }
+  // Frames ready to read.  Bounded by the ring: a producer that publishes a bogus head never
+  // makes the consumer hold more than ring_size slots at once.
   uint32_t available() {
     if (head_cache == next) head_cache = r->ctl(ring)->head.load(std::memory_order_acquire);
-    return head_cache - next;
+    const uint32_t a = head_cache - next, room = r->ring_size() - (next - released);
+    return a < room ? a : room;
   }
   // Frame at the read cursor (valid until released); advances the cursor.
   const uint8_t* get(uint32_t& len) {
@@ -194,7 +215,10 @@ struct Consumer {
     return p;
   }
   // Return every slot below `upto` to the producer.
-  void release_to(uint32_t upto) { r->ctl(ring)->tail.store(upto, std::memory_order_release); }
+  void release_to(uint32_t upto) {
+    released = upto;
+    r->ctl(ring)->tail.store(upto, std::memory_order_release);
+  }
 };
 
 }  // namespace memif

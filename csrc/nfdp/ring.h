@@ -18,6 +18,12 @@
 //                                            chain, emit (same stages as the fused kernel)
 //   poll flags[t % (R/64)] == t+1   <----  release fence (system scope), flags[t] = t + 1
 //
+// Queues: one grid serves Q independent rings ("queues", like a NIC's RSS queues).  Workgroup b
+// serves queue b % Q: its own control word, ticket counter, prod mirror, completion flags and
+// slot range, so Q host producers (the I/O engine's rx threads) publish without sharing anything
+// but the tables.  One resident kernel per GPU whatever Q is: a second persistent grid on the same
+// device could wait forever behind the first on a shared hardware queue.
+//
 // Drain semantics: `stop` makes a wave exit only while it WAITS for an unpublished chunk, and
 // tickets are claimed in order, so every chunk published before the stop is processed.  Every
 // wave also exits on a device-side deadline (s_memrealtime), so the grid always drains even if
@@ -38,10 +44,13 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <chrono>
 #include <cstdint>
+#include <memory>
 #include <deque>
 #include <mutex>
+#include <utility>
 #include <vector>
 
 #include "host.h"
@@ -112,29 +121,38 @@ static_assert(sizeof(RingDevState) == 256, "RingDevState");
 
 class RingEngine {
  public:
-  // capacity: ring slots (power of two, >= 64).  wgs_per_cu: resident 256-thread workgroups per CU.
-  // coop: the 4 waves of a workgroup share each chunk (ACL tiles split 4 ways: lowest latency);
-  // otherwise every wave takes its own chunks (highest throughput).
+  // capacity: ring slots per queue (power of two, >= 64).  wgs_per_cu: resident 256-thread
+  // workgroups per CU.  coop: the 4 waves of a workgroup share each chunk (ACL tiles split 4 ways:
+  // lowest latency); otherwise every wave takes its own chunks (highest throughput).
   // host_slots: ring slots in pinned coherent host memory instead of HBM (zero-copy host I/O).
-  RingEngine(uint32_t capacity, int num_cus, int wgs_per_cu = 1, bool coop = true, bool host_slots = false);
+  // queues: independent rings served by one grid (workgroup b serves queue b % queues).
+  RingEngine(uint32_t capacity, int num_cus, int wgs_per_cu = 1, bool coop = true, bool host_slots = false,
+             uint32_t queues = 1);
   ~RingEngine();
   RingEngine(const RingEngine&) = delete;
   RingEngine& operator=(const RingEngine&) = delete;
 
-  uint32_t capacity() const { return cap_; }
+  uint32_t capacity() const { return cap_; }   // per queue
+  uint32_t queues() const { return nq_; }
   int device() const { return device_; }                 // HIP device the ring lives on
   const FusedLaunch& launch() const { return launch_; }  // tables / counters / side buffers of the session
+  // The MAC table the running grid reads (a live table flip may replace it): learners write here.
+  std::pair<MacEntry*, uint32_t> mac_table() const {
+    std::lock_guard<std::mutex> g(mu_);
+    return {const_cast<MacEntry*>(launch_.t.macs), launch_.t.mac_mask};
+  }
   bool running() const { return running_; }
   // The grid is still resident (false once every wave left: stop, or the device deadline passed).
   bool alive() const { return running_ && hipStreamQuery(stream_) == hipErrorNotReady; }
   bool host_slots() const { return host_slots_; }
-  // device ring buffers (the producer stages frames here before publishing them)
+  // device ring buffers (the producer stages frames here before publishing them); queue q's
+  // slots follow queue q-1's (q * capacity slots in)
   void* dev_in() const { return d_in_; }
   uint32_t* dev_inmeta() const { return d_im_; }
   void* dev_out() const { return d_out_; }
   uint32_t* dev_meta() const { return d_meta_; }
   uint32_t* dev_svc() const { return d_svc_; }  // per-chunk device service time (ticks, 100 MHz)
-  // host_slots rings: host addresses of the pinned in / inmeta / out / meta buffers
+  // host_slots rings: host addresses of the pinned in / inmeta / out / meta buffers (all queues)
   void* host_ptr(int i) const { return host_slots_ && i >= 0 && i < (int)host_ptrs_.size() ? host_ptrs_[i] : nullptr; }
 
   // Launch the persistent kernel over the tables/counters in `f` (pkts/out/n are ignored).
@@ -143,29 +161,33 @@ class RingEngine {
   // Drain published chunks, stop every wave, wait for the grid to exit (throws on timeout).
   void stop(double timeout_s = 30.0);
 
-  uint64_t published() const {
-    std::lock_guard<std::mutex> g(mu_);
-    return prod_;
+  uint64_t published(uint32_t q = 0) const {
+    std::lock_guard<std::mutex> g(qs_[q].mu);
+    return qs_[q].prod;
   }
-  uint64_t completed();  // packets whose chunks all completed (in order)
-  // Publish n packets (multiple of 64) starting at ring position published() % capacity.
-  // Throws if the ring lacks room (producer must wait for completions).
-  uint64_t publish(uint32_t n, bool check_room = true);
-  // Every chunk of ring positions [start, end) completed (lock-free flag reads; chunks complete
-  // out of order across waves, so this looks at each of them).
-  bool range_done(uint64_t start, uint64_t end) const {
+  uint64_t completed(uint32_t q = 0);  // packets of queue q whose chunks all completed (in order)
+  // Publish n packets (multiple of 64) on queue q starting at position published(q) % capacity.
+  // Throws if the ring lacks room (producer must wait for completions).  Queues publish
+  // independently (one lock each): one producer thread per queue never waits for another.
+  uint64_t publish(uint32_t n, bool check_room = true, uint32_t q = 0);
+  // Every chunk of queue q's positions [start, end) completed (lock-free flag reads; chunks
+  // complete out of order across waves, so this looks at each of them).
+  bool range_done(uint64_t start, uint64_t end, uint32_t q = 0) const {
     for (uint64_t c = start / 64; c < (end + 63) / 64; ++c)
-      if (!chunk_done(c)) return false;
+      if (!chunk_done(c, q)) return false;
     return true;
   }
-  // Spin until every chunk below `end` completed; false on timeout.
-  bool wait(uint64_t end, double timeout_s);
+  // Spin until every chunk of queue q below `end` completed; false on timeout.
+  bool wait(uint64_t end, double timeout_s, uint32_t q = 0);
 
   // Epoch flip (see the header comment): the waves switch to flow-table copy `epoch & 1` for
   // every chunk published from now on.  Throws unless the previous flip's grace period is over.
-  uint32_t flip();
-  // Grace period of the last flip: every chunk published before it has completed.
-  bool grace_over() { return completed() >= flip_prod(); }
+  uint32_t flip() { return change_epoch(true, false); }
+  // One epoch change switching the flow-table copy and / or the table set together (a commit
+  // that touched both takes effect for every chunk at once).
+  uint32_t change_epoch(bool flow, bool set);
+  // Grace period of the last flip: on every queue, every chunk published before it has completed.
+  bool grace_over();
   bool wait_grace(double timeout_s);
   // New generation, same copies: chunks published from now on make their waves drop cached
   // table lines first (after the host changed a table in place, e.g. MAC learning).
@@ -173,52 +195,49 @@ class RingEngine {
   // Coop rings: write table set `which` (the idle one: 1 - table_set()) ...
   void stage_tables(const FusedLaunch& f, int which);
   // ... and switch to it (same grace rule as flip()).  Returns the new epoch.
-  uint32_t flip_tables();
-  int table_set() const {
-    std::lock_guard<std::mutex> g(mu_);
-    return (int)((epoch_ & kEpochSetBit) >> 1);
-  }
+  uint32_t flip_tables() { return change_epoch(false, true); }
+  int table_set() const { return (int)((epoch() & kEpochSetBit) >> 1); }
   uint32_t lds_acl_tiles() const { return lds_tiles_; }   // ACL tiles the running grid's LDS holds
-  uint32_t epoch() const {
-    std::lock_guard<std::mutex> g(mu_);
-    return epoch_;
-  }
+  uint32_t epoch() const { return epoch_.load(std::memory_order_acquire); }
   void set_epoch(uint32_t e);   // only while stopped
 
-  // Closed-loop probe run entirely in C++ (no Python in the timed loop): `batches` batches of
-  // `batch` packets, at most `inflight` outstanding.  Returns per-batch publish->completion
-  // latencies (µs, host steady clock) and sets *elapsed_s to the wall time of the whole run.
+  // Closed-loop probe run entirely in C++ (no Python in the timed loop) on queue 0: `batches`
+  // batches of `batch` packets, at most `inflight` outstanding.  Returns per-batch
+  // publish->completion latencies (µs, host steady clock) and sets *elapsed_s to the wall time.
   std::vector<double> probe(uint32_t batches, uint32_t batch, uint32_t inflight, double* elapsed_s);
 
  private:
-  bool chunk_done(uint64_t chunk) const;
+  bool chunk_done(uint64_t chunk, uint32_t q) const;
   void pace_epoch_change();
+  // (mu_ held) a new epoch for every queue: each queue's flip point is its published count now
+  void set_epoch_all(uint32_t e);
   std::deque<std::chrono::steady_clock::time_point> epoch_changes_;   // last kRingEpochMask changes
-  uint64_t flip_prod() const {
-    std::lock_guard<std::mutex> g(mu_);
-    return flip_prod_;
-  }
-  // publish / flip / completion scans may come from different host threads (a producer thread
-  // and the control plane's commit): the host-side ring state is guarded
-  mutable std::mutex mu_;
-  uint32_t cap_, nch_;
+  // Host-side state of one queue.  Its producer thread and completion scans take `mu`; an epoch
+  // change takes the engine lock, then every queue's in turn (publish reads epoch_ under its
+  // queue lock, so a queue's word never goes back to an older epoch).
+  struct alignas(64) Queue {
+    mutable std::mutex mu;
+    uint64_t prod = 0;        // host copy of ctl[q].prod's count
+    uint64_t floor = 0;       // chunks < floor are complete
+    uint64_t flip_prod = 0;   // packets published before the last epoch change
+  };
+  mutable std::mutex mu_;     // epoch changes / table sets (engine-wide)
+  uint32_t cap_, nch_, nq_;
   int num_cus_, wgs_;
   bool coop_;
   bool host_slots_;
   std::vector<void*> host_ptrs_;  // host_slots: pinned allocations to free
-  RingCtl* ctl_ = nullptr;        // pinned, coherent
-  uint32_t* flags_ = nullptr;     // pinned, coherent: [nch] completion sequence numbers
-  RingDevState* st_ = nullptr;    // device
+  RingCtl* ctl_ = nullptr;        // pinned, coherent: [nq]
+  uint32_t* flags_ = nullptr;     // pinned, coherent: [nq][nch] completion sequence numbers
+  RingDevState* st_ = nullptr;    // device: [nq]
   uint8_t* d_in_ = nullptr;
   uint32_t* d_im_ = nullptr;
   uint8_t* d_out_ = nullptr;
   uint32_t* d_meta_ = nullptr;
   uint32_t* d_svc_ = nullptr;
   hipStream_t stream_{};
-  uint64_t prod_ = 0;             // host copy of ctl->prod
-  uint64_t floor_ = 0;            // chunks < floor_ are complete
-  uint32_t epoch_ = 0;            // current flow-table epoch (copy epoch_ & 1)
-  uint64_t flip_prod_ = 0;        // packets published before the last flip
+  std::unique_ptr<Queue[]> qs_;
+  std::atomic<uint32_t> epoch_{0};   // current flow-table epoch (copy epoch_ & 1)
   bool running_ = false;
   int device_ = 0;
   FusedLaunch launch_{};
@@ -232,6 +251,7 @@ struct RingLaunch {
   FusedLaunch f;
   const void* pkts; const uint32_t* inmeta; void* out; uint32_t* out_meta;
   uint32_t ring_mask;
+  uint32_t queues;            // independent rings (per-queue buffers follow each other)
   RingCtl* ctl; uint32_t* flags; RingDevState* st; uint32_t* svc;
   unsigned long long deadline_ticks;
   const void* flows_alt;  // second flow-table copy (epoch & 1 == 1); f.t.flows is copy 0

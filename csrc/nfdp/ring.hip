@@ -31,6 +31,7 @@ struct RingArgs {
   uint32_t epoch0;
   SideOut side;           // side list (cnt null = off): slots needing replicas / learn events / outer headers
   uint32_t flags_bits;  // bit2: no per-flow counts; bits 5/6: diagnostics (kRingTrace, kRingNoCounters)
+  uint32_t nq;          // queues: workgroup b serves queue b % nq (ctl / st / flags / svc / slots per queue)
 };
 // Frames are read and written with system-coherent buffer ops (sc0 sc1): the loads never hit a
 // stale L2 line of a slot a producer (host / NIC DMA) rewrote, and the stores write through to
@@ -98,10 +99,11 @@ __device__ __forceinline__ unsigned long long rfl64(unsigned long long v) {
 // (s_sleep grows with the distance in chunks), so ~1K waiting waves do not turn the prod mirror
 // into a hot spot that slows the waves doing work.
 template <class OnIdle>
-__device__ __forceinline__ bool ring_wait_chunk(const RingArgs& a, uint32_t lane, unsigned long long t_begin,
-                                                unsigned long long& tk_out, uint32_t& epoch_out, OnIdle on_idle) {
+__device__ __forceinline__ bool ring_wait_chunk(const RingArgs& a, RingCtl* ctl, RingDevState* st, uint32_t lane,
+                                                unsigned long long t_begin, unsigned long long& tk_out,
+                                                uint32_t& epoch_out, OnIdle on_idle) {
   unsigned long long tk = 0;
-  if (lane == 0) tk = atomicAdd(&a.st->claim, 1ull);
+  if (lane == 0) tk = atomicAdd(&st->claim, 1ull);
   tk = rfl64(tk);
   tk_out = tk;
   const unsigned long long first = tk * 64ull;
@@ -109,12 +111,12 @@ __device__ __forceinline__ bool ring_wait_chunk(const RingArgs& a, uint32_t lane
   for (;;) {
     unsigned long long v = 0;
     if (lane == 0) {
-      v = __hip_atomic_load(&a.st->dprod, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      v = __hip_atomic_load(&st->dprod, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (ring_count(v) < need && ring_count(v) == first && !(v & kRingStop)) {
         // frontier wave (its chunk is the first unpublished one): the only PCIe poller
-        const unsigned long long hv = __hip_atomic_load(&a.ctl->prod, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        const unsigned long long hv = __hip_atomic_load(&ctl->prod, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         if (hv > v) {
-          __hip_atomic_fetch_max(&a.st->dprod, hv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_fetch_max(&st->dprod, hv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           v = hv;
         }
       }
@@ -207,12 +209,20 @@ __global__ __launch_bounds__(kRingBlock) void ring_kernel(RingArgs a) {
   if (threadIdx.x < kNumReasons) drops[threadIdx.x] = 0;
   __syncthreads();
 
-  // raw buffer views over the ring (capacity <= 2^24 slots: byte offsets fit 32 bits)
+  // this workgroup's queue (wave-uniform): its control word, ticket state, flags and slot range
+  const uint32_t nch_q = (a.ring_mask >> 6) + 1u;   // chunks per queue
+  const uint32_t qi = a.nq > 1 ? blockIdx.x % a.nq : 0u;
+  RingCtl* const qctl = a.ctl + qi;
+  RingDevState* const qst = a.st + qi;
+  uint32_t* const qflags = a.flags + (size_t)qi * nch_q;
+  uint32_t* const qsvc = a.svc ? a.svc + (size_t)qi * nch_q * kSvcWords : nullptr;
+  // raw buffer views over the queue's ring (capacity <= 2^24 slots: byte offsets fit 32 bits)
   const uint32_t rbytes = (a.ring_mask + 1u) * 64u;
-  const __amdgpu_buffer_rsrc_t r_pk = __builtin_amdgcn_make_buffer_rsrc((void*)a.pkts, (short)0, (int)rbytes, kBufRaw);
-  const __amdgpu_buffer_rsrc_t r_im = __builtin_amdgcn_make_buffer_rsrc((void*)a.inmeta, (short)0, (int)(rbytes / 16), kBufRaw);
-  const __amdgpu_buffer_rsrc_t r_out = __builtin_amdgcn_make_buffer_rsrc((void*)a.out, (short)0, (int)rbytes, kBufRaw);
-  const __amdgpu_buffer_rsrc_t r_meta = __builtin_amdgcn_make_buffer_rsrc((void*)a.out_meta, (short)0, (int)(rbytes / 16), kBufRaw);
+  const size_t qslot0 = (size_t)qi * (a.ring_mask + 1u);
+  const __amdgpu_buffer_rsrc_t r_pk = __builtin_amdgcn_make_buffer_rsrc((void*)(a.pkts + qslot0 * 4), (short)0, (int)rbytes, kBufRaw);
+  const __amdgpu_buffer_rsrc_t r_im = __builtin_amdgcn_make_buffer_rsrc((void*)(a.inmeta + qslot0), (short)0, (int)(rbytes / 16), kBufRaw);
+  const __amdgpu_buffer_rsrc_t r_out = __builtin_amdgcn_make_buffer_rsrc((void*)(a.out + qslot0 * 4), (short)0, (int)rbytes, kBufRaw);
+  const __amdgpu_buffer_rsrc_t r_meta = __builtin_amdgcn_make_buffer_rsrc((void*)(a.out_meta + qslot0), (short)0, (int)(rbytes / 16), kBufRaw);
   const bool counters = !(a.flags_bits & kRingNoCounters);
   uint32_t since_flush = 0;  // chunks this wave added to the LDS counters since its last flush
   auto on_idle = [&]() {
@@ -234,7 +244,7 @@ __global__ __launch_bounds__(kRingBlock) void ring_kernel(RingArgs a) {
     uint32_t epoch = 0;
     if constexpr (COOP) {
       if (wave == 0) {
-        const bool go = ring_wait_chunk(a, lane, t_begin, tk, epoch, on_idle);
+        const bool go = ring_wait_chunk(a, qctl, qst, lane, t_begin, tk, epoch, on_idle);
         // the serial of the set this epoch names, read only when the epoch moved (or the
         // workgroup idled long enough for the epoch value to have come round again)
         uint32_t ser = cur_serial;
@@ -253,7 +263,7 @@ __global__ __launch_bounds__(kRingBlock) void ring_kernel(RingArgs a) {
       epoch = __builtin_amdgcn_readfirstlane(coop_ctl[1]);
       if (!__builtin_amdgcn_readfirstlane(coop_ctl[0])) break;
     } else {
-      if (!ring_wait_chunk(a, lane, t_begin, tk, epoch, on_idle)) break;
+      if (!ring_wait_chunk(a, qctl, qst, lane, t_begin, tk, epoch, on_idle)) break;
     }
     const unsigned long long t_avail = __builtin_amdgcn_s_memrealtime();
     if (epoch != seen_epoch || t_avail - seen_t > kEpochAliasTicks) {
@@ -359,8 +369,8 @@ __global__ __launch_bounds__(kRingBlock) void ring_kernel(RingArgs a) {
     __builtin_amdgcn_s_waitcnt(0);
     NFDP_RING_MARK(tr4)
     if (lane == 0) {
-      if (a.svc) a.svc[(size_t)(tk32 & nch_mask) * kSvcWords + 7] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_avail);
-      __hip_atomic_store(&a.flags[tk32 & nch_mask], tk32 + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (qsvc) qsvc[(size_t)(tk32 & nch_mask) * kSvcWords + 7] = (uint32_t)(__builtin_amdgcn_s_memrealtime() - t_avail);
+      __hip_atomic_store(&qflags[tk32 & nch_mask], tk32 + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 
     // ---- counters, off the latency path (after the flag): port / drop counters into the
@@ -384,8 +394,8 @@ __global__ __launch_bounds__(kRingBlock) void ring_kernel(RingArgs a) {
     }
     NFDP_RING_MARK(tr5)
 #undef NFDP_RING_MARK
-    if (trace && lane == 0 && a.svc) {
-      uint32_t* sv = a.svc + (size_t)(tk32 & nch_mask) * kSvcWords;
+    if (trace && lane == 0 && qsvc) {
+      uint32_t* sv = qsvc + (size_t)(tk32 & nch_mask) * kSvcWords;
       sv[0] = tr0; sv[1] = tr1; sv[2] = tr2; sv[3] = tr3; sv[4] = tr4; sv[5] = tr5; sv[6] = 0;
     }
   }
@@ -428,6 +438,9 @@ hipError_t launch_ring(const RingLaunch& r, const LaunchCfg& cfg, int wgs_per_cu
   a.sets = r.sets;
   a.lds_tiles = r.lds_tiles;
   a.epoch0 = r.epoch0;
+  a.nq = r.queues ? r.queues : 1u;
+  // every queue needs a workgroup; the side list indexes slots of one ring only
+  if ((uint64_t)cfg.num_cus * (uint64_t)wgs_per_cu < a.nq || (a.nq > 1 && a.side.cnt)) return hipErrorInvalidValue;
   if (coop && (!a.sets || a.lds_tiles < a.acl_tiles)) return hipErrorInvalidValue;
   if (!a.port_ctr || !a.drop_ctr || !a.ctl || !a.flags || !a.st) return hipErrorInvalidValue;
   if (((r.ring_mask + 1) & r.ring_mask) != 0 || r.ring_mask < 63) return hipErrorInvalidValue;
@@ -466,20 +479,25 @@ using Clock = std::chrono::steady_clock;
 inline double secs(Clock::time_point a, Clock::time_point b) { return std::chrono::duration<double>(b - a).count(); }
 }  // namespace
 
-RingEngine::RingEngine(uint32_t capacity, int num_cus, int wgs_per_cu, bool coop, bool host_slots)
-    : cap_(capacity), nch_(capacity / 64), num_cus_(num_cus), wgs_(wgs_per_cu), coop_(coop), host_slots_(host_slots) {
+RingEngine::RingEngine(uint32_t capacity, int num_cus, int wgs_per_cu, bool coop, bool host_slots, uint32_t queues)
+    : cap_(capacity), nch_(capacity / 64), nq_(queues), num_cus_(num_cus), wgs_(wgs_per_cu), coop_(coop),
+      host_slots_(host_slots) {
   if (capacity < 64 || (capacity & (capacity - 1)) || capacity > (1u << 24))
     throw std::invalid_argument("ring: capacity must be a power of two in [64, 2^24]");
   if (num_cus < 1 || wgs_per_cu < 1 || wgs_per_cu > 8) throw std::invalid_argument("ring: bad grid");
+  if (queues < 1 || queues > 64 || (uint64_t)queues > (uint64_t)num_cus * wgs_per_cu)
+    throw std::invalid_argument("ring: queues in [1, 64] and at most one per workgroup");
+  if ((uint64_t)capacity * queues > (1u << 26)) throw std::invalid_argument("ring: capacity x queues too large");
+  qs_.reset(new Queue[nq_]);
   ck(hipGetDevice(&device_), "get device");
-  // control line + completion flags: pinned, coherent (the GPU polls / writes them over PCIe)
-  ck(hipHostMalloc(reinterpret_cast<void**>(&ctl_), sizeof(RingCtl), hipHostMallocCoherent | hipHostMallocMapped),
+  // control lines + completion flags: pinned, coherent (the GPU polls / writes them over PCIe)
+  ck(hipHostMalloc(reinterpret_cast<void**>(&ctl_), sizeof(RingCtl) * nq_, hipHostMallocCoherent | hipHostMallocMapped),
      "host alloc ctl");
-  ck(hipHostMalloc(reinterpret_cast<void**>(&flags_), (size_t)nch_ * 4, hipHostMallocCoherent | hipHostMallocMapped),
+  ck(hipHostMalloc(reinterpret_cast<void**>(&flags_), (size_t)nq_ * nch_ * 4, hipHostMallocCoherent | hipHostMallocMapped),
      "host alloc flags");
-  std::memset(ctl_, 0, sizeof(RingCtl));
-  std::memset(flags_, 0, (size_t)nch_ * 4);
-  ck(hipMalloc(reinterpret_cast<void**>(&st_), sizeof(RingDevState)), "dev alloc state");
+  std::memset(ctl_, 0, sizeof(RingCtl) * nq_);
+  std::memset(flags_, 0, (size_t)nq_ * nch_ * 4);
+  ck(hipMalloc(reinterpret_cast<void**>(&st_), sizeof(RingDevState) * nq_), "dev alloc state");
   // Slots: HBM (the wire side is the GPU: NIC DMA into device memory), or pinned coherent host
   // memory (host-resident rings — pod vhost / AF_XDP style): the kernel's system-coherent buffer
   // ops then read and write the frames over PCIe directly, with no separate copy step.
@@ -495,14 +513,15 @@ RingEngine::RingEngine(uint32_t capacity, int num_cus, int wgs_per_cu, bool coop
       ck(hipMemset(*p, 0, bytes), what);
     }
   };
-  slot_alloc(reinterpret_cast<void**>(&d_in_), (size_t)capacity * 64, "alloc in");
-  slot_alloc(reinterpret_cast<void**>(&d_im_), (size_t)capacity * 4, "alloc inmeta");
-  slot_alloc(reinterpret_cast<void**>(&d_out_), (size_t)capacity * 64, "alloc out");
-  slot_alloc(reinterpret_cast<void**>(&d_meta_), (size_t)capacity * 4, "alloc meta");
-  ck(hipMalloc(reinterpret_cast<void**>(&d_svc_), (size_t)nch_ * 4 * kSvcWords), "dev alloc svc");
+  const size_t slots = (size_t)capacity * nq_;
+  slot_alloc(reinterpret_cast<void**>(&d_in_), slots * 64, "alloc in");
+  slot_alloc(reinterpret_cast<void**>(&d_im_), slots * 4, "alloc inmeta");
+  slot_alloc(reinterpret_cast<void**>(&d_out_), slots * 64, "alloc out");
+  slot_alloc(reinterpret_cast<void**>(&d_meta_), slots * 4, "alloc meta");
+  ck(hipMalloc(reinterpret_cast<void**>(&d_svc_), (size_t)nq_ * nch_ * 4 * kSvcWords), "dev alloc svc");
   ck(hipMalloc(reinterpret_cast<void**>(&d_sets_), 2 * sizeof(RingTableSet)), "dev alloc table sets");
   ck(hipMemset(d_sets_, 0, 2 * sizeof(RingTableSet)), "memset");
-  ck(hipMemset(d_svc_, 0, (size_t)nch_ * 4 * kSvcWords), "memset");
+  ck(hipMemset(d_svc_, 0, (size_t)nq_ * nch_ * 4 * kSvcWords), "memset");
   ck(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "stream");
 }
 
@@ -526,26 +545,33 @@ RingEngine::~RingEngine() {
 void RingEngine::start(const FusedLaunch& f, const LaunchCfg& cfg, double deadline_s, const void* flows_alt) {
   if (running_) throw std::runtime_error("ring: already running");
   if (!(deadline_s > 0.0) || deadline_s > 3600.0) throw std::invalid_argument("ring: deadline in (0, 3600] s");
-  if (completed() != prod_) throw std::runtime_error("ring: previous session left chunks unprocessed");
-  // resume at the published position: tickets restart at prod/64, nothing outstanding
-  RingDevState s{};
-  s.claim = prod_ / 64;
-  s.dprod = ring_word(prod_, epoch_);
-  __atomic_store_n(&ctl_->prod, ring_word(prod_, epoch_), __ATOMIC_RELEASE);
-  ck(hipMemcpyAsync(st_, &s, sizeof(s), hipMemcpyHostToDevice, stream_), "state upload");
+  if ((uint64_t)cfg.num_cus * (uint64_t)wgs_ < nq_) throw std::invalid_argument("ring: fewer workgroups than queues");
+  const uint32_t ep = epoch();
+  // resume at the published positions: tickets restart at prod/64, nothing outstanding
+  std::vector<RingDevState> s(nq_);
+  for (uint32_t q = 0; q < nq_; ++q) {
+    if (completed(q) != published(q)) throw std::runtime_error("ring: previous session left chunks unprocessed");
+    const uint64_t p = published(q);
+    std::memset(&s[q], 0, sizeof(RingDevState));
+    s[q].claim = p / 64;
+    s[q].dprod = ring_word(p, ep);
+    __atomic_store_n(&ctl_[q].prod, ring_word(p, ep), __ATOMIC_RELEASE);
+  }
+  ck(hipMemcpyAsync(st_, s.data(), sizeof(RingDevState) * nq_, hipMemcpyHostToDevice, stream_), "state upload");
   ck(hipStreamSynchronize(stream_), "state upload");  // `s` lives on this stack frame
   launch_ = f;
   // coop rings: the session's tables are table set (epoch bit 1); the LDS layout holds up to
   // kLdsAclTiles rule tiles, so a later set with more tiles than that needs a relaunch
   lds_tiles_ = coop_ ? std::max<uint32_t>(f.acl_tiles, kLdsAclTiles) : f.acl_tiles;
-  if (coop_) stage_tables(f, (int)((epoch_ & kEpochSetBit) >> 1));
+  if (coop_) stage_tables(f, (int)((ep & kEpochSetBit) >> 1));
   RingLaunch r;
   r.f = f;
   r.sets = d_sets_;
   r.lds_tiles = lds_tiles_;
-  r.epoch0 = epoch_;
+  r.epoch0 = ep;
   r.pkts = d_in_; r.inmeta = d_im_; r.out = d_out_; r.out_meta = d_meta_;
   r.ring_mask = cap_ - 1;
+  r.queues = nq_;
   void* dctl = nullptr;
   void* dflags = nullptr;
   ck(hipHostGetDevicePointer(&dctl, ctl_, 0), "device ptr ctl");
@@ -564,7 +590,11 @@ void RingEngine::stop(double timeout_s) {
   if (!running_) return;
   {
     std::lock_guard<std::mutex> g(mu_);
-    __atomic_store_n(&ctl_->prod, ring_word(prod_, epoch_) | kRingStop, __ATOMIC_RELEASE);
+    const uint32_t ep = epoch();
+    for (uint32_t q = 0; q < nq_; ++q) {
+      std::lock_guard<std::mutex> gq(qs_[q].mu);
+      __atomic_store_n(&ctl_[q].prod, ring_word(qs_[q].prod, ep) | kRingStop, __ATOMIC_RELEASE);
+    }
   }
   const auto t0 = Clock::now();
   for (;;) {
@@ -575,31 +605,47 @@ void RingEngine::stop(double timeout_s) {
     std::this_thread::sleep_for(std::chrono::microseconds(50));
   }
   running_ = false;
-  if (completed() != published()) throw std::runtime_error("ring: stopped with published chunks unprocessed");
+  for (uint32_t q = 0; q < nq_; ++q)
+    if (completed(q) != published(q)) throw std::runtime_error("ring: stopped with published chunks unprocessed");
 }
 
-bool RingEngine::chunk_done(uint64_t chunk) const {
-  return __atomic_load_n(&flags_[chunk & (nch_ - 1)], __ATOMIC_ACQUIRE) == (uint32_t)(chunk + 1);
+bool RingEngine::chunk_done(uint64_t chunk, uint32_t q) const {
+  return __atomic_load_n(&flags_[(size_t)q * nch_ + (chunk & (nch_ - 1))], __ATOMIC_ACQUIRE) == (uint32_t)(chunk + 1);
 }
 
-uint64_t RingEngine::completed() {
-  std::lock_guard<std::mutex> g(mu_);
-  const uint64_t end = prod_ / 64;
-  while (floor_ < end && chunk_done(floor_)) ++floor_;
-  return floor_ * 64;
+uint64_t RingEngine::completed(uint32_t q) {
+  Queue& Q = qs_[q];
+  std::lock_guard<std::mutex> g(Q.mu);
+  const uint64_t end = Q.prod / 64;
+  while (Q.floor < end && chunk_done(Q.floor, q)) ++Q.floor;
+  return Q.floor * 64;
 }
 
-uint64_t RingEngine::publish(uint32_t n, bool check_room) {
+uint64_t RingEngine::publish(uint32_t n, bool check_room, uint32_t q) {
   if (!running_) throw std::runtime_error("ring: not running");
   if (n == 0 || (n & 63u)) throw std::invalid_argument("ring: publish a positive multiple of 64 packets");
+  if (q >= nq_) throw std::invalid_argument("ring: no such queue");
   // check_room = false: the producer tracks slot reuse itself (the native I/O engine frees slots
   // only after it has read their results, a stricter bound than completion)
-  const uint64_t done = completed();   // also keeps the in-order floor current (amortised scan)
-  std::lock_guard<std::mutex> g(mu_);
-  if (check_room && prod_ + n - done > cap_) throw std::runtime_error("ring: no room (wait for completions)");
-  prod_ += n;
-  __atomic_store_n(&ctl_->prod, ring_word(prod_, epoch_), __ATOMIC_RELEASE);
-  return prod_;
+  const uint64_t done = check_room ? completed(q) : 0;   // (also keeps the in-order floor current)
+  Queue& Q = qs_[q];
+  std::lock_guard<std::mutex> g(Q.mu);
+  if (check_room && Q.prod + n - done > cap_) throw std::runtime_error("ring: no room (wait for completions)");
+  Q.prod += n;
+  __atomic_store_n(&ctl_[q].prod, ring_word(Q.prod, epoch()), __ATOMIC_RELEASE);
+  return Q.prod;
+}
+
+bool RingEngine::grace_over() {
+  for (uint32_t q = 0; q < nq_; ++q) {
+    uint64_t fp;
+    {
+      std::lock_guard<std::mutex> g(qs_[q].mu);
+      fp = qs_[q].flip_prod;
+    }
+    if (completed(q) < fp) return false;
+  }
+  return true;
 }
 
 void RingEngine::pace_epoch_change() {
@@ -614,24 +660,41 @@ void RingEngine::pace_epoch_change() {
   epoch_changes_.push_back(now > Clock::now() ? now : Clock::now());
 }
 
-uint32_t RingEngine::flip() {
+void RingEngine::set_epoch_all(uint32_t e) {
+  epoch_.store(e, std::memory_order_release);
+  for (uint32_t q = 0; q < nq_; ++q) {
+    Queue& Q = qs_[q];
+    std::lock_guard<std::mutex> g(Q.mu);
+    Q.flip_prod = Q.prod;
+    // same count, new epoch: chunks published from here on carry it (the frontier mirrors a word
+    // only when its count grows, so this store alone changes nothing for waiting waves)
+    if (running_) __atomic_store_n(&ctl_[q].prod, ring_word(Q.prod, e), __ATOMIC_RELEASE);
+  }
+}
+
+uint32_t RingEngine::change_epoch(bool flow, bool set) {
+  if (set && !coop_) throw std::runtime_error("ring: live table sets need a coop ring");
   if (!grace_over()) throw std::runtime_error("ring: flip before the previous flip's grace period ended");
   std::lock_guard<std::mutex> g(mu_);
   pace_epoch_change();
-  epoch_ = epoch_next_gen(epoch_) ^ kEpochFlowBit;
-  flip_prod_ = prod_;
-  // same count, new epoch: chunks published from here on carry it (the frontier mirrors a word
-  // only when its count grows, so this store alone changes nothing for waiting waves)
-  if (running_) __atomic_store_n(&ctl_->prod, ring_word(prod_, epoch_), __ATOMIC_RELEASE);
-  return epoch_;
+  uint32_t e = epoch_next_gen(epoch());
+  if (flow) e ^= kEpochFlowBit;
+  if (set) e ^= kEpochSetBit;
+  set_epoch_all(e);
+  return e;
 }
 
 uint32_t RingEngine::bump_epoch() {
   std::lock_guard<std::mutex> g(mu_);
   pace_epoch_change();
-  epoch_ = epoch_next_gen(epoch_);
-  if (running_) __atomic_store_n(&ctl_->prod, ring_word(prod_, epoch_), __ATOMIC_RELEASE);
-  return epoch_;
+  // same copies: only the generation moves, so the flip points (grace periods) stay as they are
+  const uint32_t e = epoch_next_gen(epoch());
+  epoch_.store(e, std::memory_order_release);
+  for (uint32_t q = 0; q < nq_; ++q) {
+    std::lock_guard<std::mutex> gq(qs_[q].mu);
+    if (running_) __atomic_store_n(&ctl_[q].prod, ring_word(qs_[q].prod, e), __ATOMIC_RELEASE);
+  }
+  return e;
 }
 
 void RingEngine::stage_tables(const FusedLaunch& f, int which) {
@@ -642,6 +705,7 @@ void RingEngine::stage_tables(const FusedLaunch& f, int which) {
   ts.t = f.t;
   ts.acl_wfrag = f.acl_wfrag; ts.acl_cinit = f.acl_cinit; ts.acl_tiles = f.acl_tiles;
   ts.toep_frag = f.toep_frag; ts.toep_tab = f.toep_tab;
+  std::lock_guard<std::mutex> g(mu_);
   ts.serial = ++set_serial_;
   // a copy on the engine's own stream would queue behind the resident kernel: a private
   // non-blocking stream (the grid never reads the idle set)
@@ -650,22 +714,11 @@ void RingEngine::stage_tables(const FusedLaunch& f, int which) {
   ck(hipMemcpyAsync(d_sets_ + which, &ts, sizeof(ts), hipMemcpyHostToDevice, cs), "table set upload");
   ck(hipStreamSynchronize(cs), "table set upload");
   if (running_) {
-    // the side pass (iox / RingPath.side_pass) reads the session's tables from launch()
+    // the side pass (RingPath.side_pass) reads the session's tables from launch()
     launch_.t = f.t;
     launch_.acl_wfrag = f.acl_wfrag; launch_.acl_cinit = f.acl_cinit; launch_.acl_tiles = f.acl_tiles;
     launch_.toep_frag = f.toep_frag; launch_.toep_tab = f.toep_tab;
   }
-}
-
-uint32_t RingEngine::flip_tables() {
-  if (!coop_) throw std::runtime_error("ring: live table sets need a coop ring");
-  if (!grace_over()) throw std::runtime_error("ring: flip before the previous flip's grace period ended");
-  std::lock_guard<std::mutex> g(mu_);
-  pace_epoch_change();
-  epoch_ = epoch_next_gen(epoch_) ^ kEpochSetBit;
-  flip_prod_ = prod_;
-  if (running_) __atomic_store_n(&ctl_->prod, ring_word(prod_, epoch_), __ATOMIC_RELEASE);
-  return epoch_;
 }
 
 bool RingEngine::wait_grace(double timeout_s) {
@@ -681,15 +734,14 @@ bool RingEngine::wait_grace(double timeout_s) {
 void RingEngine::set_epoch(uint32_t e) {
   if (running_) throw std::runtime_error("ring: set_epoch while running");
   std::lock_guard<std::mutex> g(mu_);
-  epoch_ = e & (uint32_t)kRingEpochMask;
-  flip_prod_ = prod_;
+  set_epoch_all(e & (uint32_t)kRingEpochMask);
 }
 
-bool RingEngine::wait(uint64_t end, double timeout_s) {
-  if (end > published()) throw std::invalid_argument("ring: waiting for unpublished packets");
+bool RingEngine::wait(uint64_t end, double timeout_s, uint32_t q) {
+  if (end > published(q)) throw std::invalid_argument("ring: waiting for unpublished packets");
   const auto t0 = Clock::now();
   uint32_t spin = 0;
-  while (completed() < end) {
+  while (completed(q) < end) {
     _mm_pause();
     if ((++spin & 1023u) == 0 && secs(t0, Clock::now()) > timeout_s) return false;
   }

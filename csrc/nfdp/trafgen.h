@@ -30,6 +30,7 @@ struct Pod {
   std::vector<uint8_t> frames;      // templates, each `stride` bytes
   std::vector<uint32_t> lens;       // template lengths
   uint32_t stride = 0;
+  std::vector<uint32_t> ts_off;     // timestamp offset of each template (filled by run())
 };
 
 struct Config {
@@ -66,8 +67,12 @@ inline uint32_t ts_offset(const uint8_t* f, uint32_t len) {
   return l4 + 8 <= len ? l4 : 0;
 }
 
-inline Result run(const std::vector<Pod>& pods, const Config& cfg) {
+inline Result run(std::vector<Pod> pods, const Config& cfg) {
   const size_t np = pods.size();
+  for (auto& p : pods) {
+    p.ts_off.resize(p.lens.size());
+    for (size_t c = 0; c < p.lens.size(); ++c) p.ts_off[c] = ts_offset(p.frames.data() + c * p.stride, p.lens[c]);
+  }
   std::vector<std::unique_ptr<memif::Region>> regs;
   for (const auto& p : pods) regs.emplace_back(new memif::Region(p.path, false));
   const uint32_t nth = std::max<uint32_t>(1, std::min<uint32_t>(cfg.threads, (uint32_t)np));
@@ -129,6 +134,7 @@ inline Result run(const std::vector<Pod>& pods, const Config& cfg) {
             n = (uint32_t)std::min<int64_t>(n, std::max<int64_t>(0, (int64_t)cfg.inflight - o));
           }
           uint32_t put = 0;
+          const uint64_t ts = now_ns();   // one send time per burst: the burst leaves together
           for (uint32_t i = 0; i < n; ++i) {
             const uint32_t c = cursor[k];
             const uint8_t* f = pd.frames.data() + (size_t)c * pd.stride;
@@ -136,8 +142,7 @@ inline Result run(const std::vector<Pod>& pods, const Config& cfg) {
             if (prod[k].room() == 0) { ++me.full; break; }
             uint8_t* dst = prod[k].r->buf(0, prod[k].head);
             std::memcpy(dst, f, len);
-            const uint32_t off = ts_offset(f, len);
-            const uint64_t ts = now_ns();
+            const uint32_t off = pd.ts_off[c];
             if (off) std::memcpy(dst + off, &ts, 8);
             memif::Desc& d = prod[k].r->desc(0)[prod[k].head & prod[k].r->mask()];
             d.len = len;
@@ -149,7 +154,7 @@ inline Result run(const std::vector<Pod>& pods, const Config& cfg) {
           if (put) {
             prod[k].commit();
             if (now >= t_meas) { me.sent += put; me.tx_pod[mine[k]] += put; }
-            outstanding.fetch_add(put, std::memory_order_acq_rel);
+            if (cfg.inflight) outstanding.fetch_add(put, std::memory_order_acq_rel);
             if (per_thread_rate > 0) credit -= put;
           }
         }
@@ -175,8 +180,10 @@ inline Result run(const std::vector<Pod>& pods, const Config& cfg) {
             }
           }
           cons[k].release_to(cons[k].next);
-          outstanding.fetch_sub(mine_rx, std::memory_order_acq_rel);
-          last_rx.store(trx, std::memory_order_relaxed);
+          if (cfg.inflight) {
+            outstanding.fetch_sub(mine_rx, std::memory_order_acq_rel);
+            last_rx.store(trx, std::memory_order_relaxed);
+          }
         }
       }
     });

@@ -154,28 +154,38 @@ class DataPlane:
         self._zeros("t0", 1)
 
     # ------------------------------------------------------------------ commit
-    def commit(self, full: bool = False) -> dict:
+    def commit(self, full: bool = False, _hooks: bool = True) -> dict:
         """Push host table changes to the device.  Returns what was sent.
 
-        With resident ring kernels (dataplane/ring.py) running: a commit that changes only flows
-        is applied under the running rings by an epoch flip of the double-buffered flow table
-        (`_commit_flows_live`, no stall); any other change drains and stops the rings, updates the
-        tables and relaunches them (their small tables are staged in LDS at launch)."""
+        With resident ring kernels (dataplane/ring.py) running, a commit is applied under them
+        without a stall whenever it can be: flow changes go to the idle copy of the
+        double-buffered flow table, any other table to new buffers staged as each coop ring's idle
+        table set; then ONE epoch change switches both (`_live_prepare` / `_live_flip`).  The
+        native I/O engines feeding this plane only hold publication across that switch (no
+        drain), so every burst sees either the old or the new tables.  Anything else (non-coop
+        rings, a first IPv6 upload, `full`) pauses the engines, drains and stops the rings,
+        updates the tables and relaunches them (their small tables are staged in LDS at launch).
+        `_hooks=False`: the caller (MultiDataPlane) runs the engine hooks once for all planes."""
         FAULTS.check("dataplane.commit")
+        hooks = list(getattr(self, "_io_hooks", ())) if _hooks else []
+        rings = self._running_rings()
+        plan = self._live_plan(rings, full)
+        if plan is not None:
+            with TRACER.span("dataplane.commit_live", plan=plan):
+                prep = self._live_prepare(rings, plan)
+                for h in hooks:
+                    h.hold(self)
+                try:
+                    self._live_flip(rings, prep)
+                finally:
+                    for h in hooks:
+                        h.release(self)
+            return prep["sent"]
         # native I/O engines (dataplane/native_io.py) feeding this data plane: nothing in flight
         # while tables move, then they re-read the new tables
-        hooks = list(getattr(self, "_io_hooks", ()))
         for h in hooks:
             h.pre_commit(self)
         try:
-            rings = [r for r in getattr(self, "_rings", []) if r.running]
-            if rings and not full and self._only_flows_pending():
-                with TRACER.span("dataplane.commit_live"):
-                    return self._commit_flows_live(rings)
-            if (rings and not full and all(getattr(r, "coop", False) for r in rings) and "flows_b" in self._dev
-                    and not self._flow6_full and all(getattr(r, "v6", False) == self._v6_keys() for r in rings)):
-                with TRACER.span("dataplane.commit_tables_live"):
-                    return self._commit_tables_live(rings)
             for r in rings:
                 r.stop()
             with TRACER.span("dataplane.commit", full=full):
@@ -188,6 +198,21 @@ class DataPlane:
         finally:
             for h in hooks:
                 h.post_commit(self)
+
+    def _running_rings(self) -> list:
+        return [r for r in getattr(self, "_rings", []) if r.running]
+
+    def _live_plan(self, rings, full: bool) -> str | None:
+        """How a commit can be applied under running rings: "flows" (flow buckets only), "tables"
+        (any table: coop rings with the double-buffered flow table), or None (drain + relaunch)."""
+        if not rings or full:
+            return None
+        if self._only_flows_pending():
+            return "flows"
+        if (all(getattr(r, "coop", False) for r in rings) and "flows_b" in self._dev and not self._flow6_full
+                and all(getattr(r, "v6", False) == self._v6_keys() for r in rings)):
+            return "tables"
+        return None
 
     def _models(self):
         return (("ports", self.ports), ("chains", self.chains), ("macs", self.macs), ("lag", self.lag),
@@ -276,66 +301,65 @@ class DataPlane:
     def flow_copy_ptrs(self) -> tuple[int, int]:
         return self._ptr("flows"), self._ptr("flows_b") or self._ptr("flows")
 
-    def _commit_flows_live(self, rings) -> dict:
-        ft = self.flows.t
-        dirty = ft.take_dirty()
-        moves = ft.take_moves()
-        if not len(dirty):
-            return {}
-        if moves:
-            self.harvest()  # counters of moved slots are attributed before the move
-        if "flows_b" not in self._dev:
-            raise RuntimeError("live flow updates need enable_flow_flip() before the rings start")
+    def _live_prepare(self, rings, plan: str) -> dict:
+        """Everything of a live commit but the switch: the previous flip's grace period waited
+        out, the idle flow-table copy brought up to date, and ("tables") every other changed
+        table uploaded into NEW device buffers (the running grid still reads the old ones) and
+        staged as each ring's idle table set.  The old buffers live until the next grace period
+        is over (the next live commit waits for it, then lets them go)."""
         t0 = time.perf_counter()
-        for r in rings:
-            if not r.eng.wait_grace(10.0):
-                raise TimeoutError("ring: grace period of the previous flow-table flip did not end")
-        t1 = time.perf_counter()
-        rows = np.union1d(dirty, self._flow_lag)
-        inactive = self._flow_active ^ 1
-        self._push_buckets(rows, self._flows_key(inactive))
-        _torch().cuda.current_stream(self.tdev).synchronize()   # the copy is complete before any wave can pick it
-        self._flow_active = inactive
-        self._gen += 1
-        for r in rings:
-            r.eng.flip()
-        self._flow_lag = dirty
-        self.flip_stats["flips"] += 1
-        self.flip_stats["grace_s"] += t1 - t0
-        self.flip_stats["update_s"] += time.perf_counter() - t1
-        self.flip_stats["buckets"] += int(len(rows))
-        return {"flow_buckets": int(len(dirty)), "flip": self._flow_active}
-
-    def _commit_tables_live(self, rings) -> dict:
-        """Any table change under running coop rings, without draining them: flows go through the
-        flow-table flip; every other changed table is uploaded into NEW device buffers (the
-        running grid still reads the old ones), the idle table set of each ring is pointed at
-        them and the rings flip to it - their workgroups restage the LDS copies at the first
-        chunk that carries the new epoch.  The old buffers live until the flip's grace period is
-        over (the next live commit waits for it, then lets them go)."""
-        t0 = time.perf_counter()
-        sent = {}
-        sent.update(self._commit_flows_live(rings))   # flow buckets by their own flip ({} without any)
         for r in rings:
             if not r.eng.wait_grace(10.0):
                 raise TimeoutError("ring: grace period of the previous flip did not end")
-        self._retired = dict(self._dev)             # the running set's buffers stay alive
-        sent.update(self._commit(False))
-        torch = _torch()
-        torch.cuda.current_stream(self.tdev).synchronize()   # uploads complete before any wave can see them
-        tables = self.tables_ptrs()
-        tables["flows"], tables["flows_alt"] = self.flow_copy_ptrs()
-        args = {"acl_wfrag": self._ptr("acl_wfrag"), "acl_cinit": self._ptr("acl_cinit"), "acl_tiles": self._acl_tiles,
-                "toep_frag": self._ptr("toep_frag"), "toep_tab": self._ptr("toep_tab")}
+        t1 = time.perf_counter()
+        sent: dict = {}
+        ft = self.flows.t
+        dirty = ft.take_dirty()
+        moves = ft.take_moves()
+        flow = bool(len(dirty))
+        if flow:
+            if "flows_b" not in self._dev:
+                raise RuntimeError("live flow updates need enable_flow_flip() before the rings start")
+            if moves:
+                self.harvest()  # counters of moved slots are attributed before the move
+            rows = np.union1d(dirty, self._flow_lag)
+            self._push_buckets(rows, self._flows_key(self._flow_active ^ 1))
+            sent["flow_buckets"] = int(len(dirty))
+            self.flip_stats["buckets"] += int(len(rows))
+        tset = plan == "tables"
+        if tset:
+            self._retired = dict(self._dev)             # the running set's buffers stay alive
+            sent.update(self._commit(False))
+        _torch().cuda.current_stream(self.tdev).synchronize()   # uploads complete before any wave can see them
+        if tset:
+            tables = self.tables_ptrs()
+            tables["flows"], tables["flows_alt"] = self.flow_copy_ptrs()
+            args = {"acl_wfrag": self._ptr("acl_wfrag"), "acl_cinit": self._ptr("acl_cinit"),
+                    "acl_tiles": self._acl_tiles, "toep_frag": self._ptr("toep_frag"), "toep_tab": self._ptr("toep_tab")}
+            for r in rings:
+                with r.lock:
+                    r.eng.stage_tables(tables, args, 1 - int(r.eng.table_set))
+            sent["table_flip"] = True
+        self.flip_stats["grace_s"] += t1 - t0
+        return {"sent": sent, "flow": flow, "set": tset, "dirty": dirty, "t0": t0, "t1": t1}
+
+    def _live_flip(self, rings, prep: dict) -> None:
+        """The switch: one epoch change per ring (flow copy and / or table set together)."""
+        if not (prep["flow"] or prep["set"]):
+            return
+        if prep["flow"]:
+            self._flow_active ^= 1
+            self._flow_lag = prep["dirty"]          # rows the now idle copy missed
+            self.flip_stats["flips"] += 1
+            prep["sent"]["flip"] = self._flow_active
         for r in rings:
-            with r.lock:
-                r.eng.stage_tables(tables, args, 1 - int(r.eng.table_set))
-                r.eng.flip_tables()
+            r.eng.change_epoch(prep["flow"], prep["set"])
         self._gen += 1
-        self.flip_stats["table_flips"] = self.flip_stats.get("table_flips", 0) + 1
-        self.flip_stats["table_update_s"] = self.flip_stats.get("table_update_s", 0.0) + time.perf_counter() - t0
-        sent["table_flip"] = True
-        return sent
+        now = time.perf_counter()
+        if prep["set"]:
+            self.flip_stats["table_flips"] = self.flip_stats.get("table_flips", 0) + 1
+            self.flip_stats["table_update_s"] = self.flip_stats.get("table_update_s", 0.0) + now - prep["t0"]
+        self.flip_stats["update_s"] += now - prep["t1"]
 
     def _commit(self, full: bool) -> dict:
         sent = {}
@@ -718,12 +742,30 @@ class DataPlane:
         raw = raw.cpu().numpy().view(np.uint64) if self.gpu else raw
         rx_p, rx_b = unpack_ctr(raw[0::2])
         tx_p, tx_b = unpack_ctr(raw[1::2])
-        return np.stack([rx_p, rx_b, tx_p, tx_b], axis=1)
+        out = np.stack([rx_p, rx_b, tx_p, tx_b], axis=1)
+        # side-pass output of native I/O engines (replicas they emitted on the host)
+        for h in getattr(self, "_ctr_hooks", ()):
+            sp = np.asarray(h.side_port_counters(), np.uint64).reshape(-1, 2)
+            n = min(len(sp), len(out))
+            out[:n, 2] += sp[:n, 0]
+            out[:n, 3] += sp[:n, 1]
+        return out
 
     def drop_counters(self) -> dict:
         raw = self._dev["drop_ctr"]
-        raw = raw.cpu().numpy().view(np.uint64) if self.gpu else raw
+        raw = (raw.cpu().numpy().view(np.uint64) if self.gpu else raw).copy()
+        for h in getattr(self, "_ctr_hooks", ()):
+            d = np.asarray(h.side_drop_counters(), np.uint64)
+            raw[: len(d)] += d[: len(raw)]
         return {T.REASONS.get(i, str(i)): int(v) for i, v in enumerate(raw) if v}
+
+    def side_tables_host(self) -> dict:
+        """Host copies of the tables the native engine's CPU side pass reads (iox SideTables):
+        ports, MAC table, LAG groups, flood rows, tunnels, RSS key."""
+        return {"ports": self.ports.a, "macs": self.macs.a, "mac_mask": int(self.macs.mask),
+                "lag": self.lag.a, "n_lag_groups": int(self.lag.n), "flood": self.flood.a, "n_flood": int(self.flood.n),
+                "tunnels": self.tunnels.a, "n_tunnels": int(self.tunnels.n), "tunnels6": self.tunnels6.a,
+                "n_tunnels6": int(self.tunnels6.n), "rss": bytes(self.rss_key), "v6": bool(self._v6_keys())}
 
     TICK_S = 1e-8  # s_memrealtime: 100 MHz
 

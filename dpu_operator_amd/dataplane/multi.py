@@ -103,15 +103,49 @@ class MultiDataPlane:
 
     # ------------------------------------------------------------------ commit / learning
     def commit(self, full: bool = False) -> dict:
+        """Every plane's commit as one update for the engines that feed them.
+
+        Live (every GPU's rings can take it without a relaunch): all planes prepare first (idle
+        flow copies written, new table sets staged), then the engines hold publication once, every
+        GPU switches epoch, and they release - so no burst sees GPU g on new tables and GPU h on
+        old ones.  Otherwise the engines pause once around all planes' commits (not once per
+        plane), and resume when every plane has its new tables."""
         # learned MACs of every GPU reach the shared model before it is re-uploaded anywhere
         if any(getattr(p, "_learned_on_device", False) for p in self.planes):
             mv = self.planes[0].macs.version
             if any(p._versions.get("macs") != mv for p in self.planes) or full:
                 self.pull_learned()
+        hooks = []
+        for p in self.planes:
+            for h in getattr(p, "_io_hooks", ()):
+                if h not in hooks:
+                    hooks.append(h)
+        rings = [p._running_rings() for p in self.planes]
+        plans = [p._live_plan(r, full) for p, r in zip(self.planes, rings)]
         sent = {}
-        for g, p in enumerate(self.planes):
-            for k, v in p.commit(full).items():
-                sent[f"{k}@{g}"] = v
+        if all(pl is not None for pl in plans):
+            preps = [p._live_prepare(r, pl) for p, r, pl in zip(self.planes, rings, plans)]
+            for h in hooks:
+                h.hold(self)
+            try:
+                for p, r, pr in zip(self.planes, rings, preps):
+                    p._live_flip(r, pr)
+            finally:
+                for h in hooks:
+                    h.release(self)
+            for g, pr in enumerate(preps):
+                for k, v in pr["sent"].items():
+                    sent[f"{k}@{g}"] = v
+            return sent
+        for h in hooks:
+            h.pre_commit(self)
+        try:
+            for g, p in enumerate(self.planes):
+                for k, v in p.commit(full, _hooks=False).items():
+                    sent[f"{k}@{g}"] = v
+        finally:
+            for h in hooks:
+                h.post_commit(self)
         return sent
 
     def pull_learned(self) -> int:

@@ -2,24 +2,30 @@
 plane, with Python only configuring it.
 
 ``netio.LivePath`` moves every frame through a Python loop (os.read / os.write per frame, header
-slots copied in Python).  ``NativeLivePath`` hands the same job to the native engine:
+slots copied in Python).  ``NativeLivePath`` hands the same job to the native engine, organised
+like a multi-queue NIC driver:
 
-    vports (memif shared-memory rings, AF_PACKET rings on veth ends, TAP fds)
-      -> engine rx thread: 64-B header slots + ingress meta straight into the pinned host slots of
-         the owner GPU's persistent ring kernel (RSS owner = owner_of(toeplitz(FlowKey), N))
-      -> engine tx thread per GPU: completion -> egress frames assembled from the rewritten header
-         and the payload still in the rx buffer; replicas / learn events / outer headers through
-         the side kernel; recirculation re-enters natively; slow-path frames come back here
-         (`on_punt`).
+    vports (memif shared-memory rings, AF_PACKET rings on veth ends, TAP fds), split over
+    `queues` rx threads
+      -> rx thread q: 64-B header slots + ingress meta straight into ring queue q of the owner
+         GPU's persistent ring kernel (pinned host slots; RSS owner = owner_of(toeplitz(FlowKey), N))
+      -> tx workers of queue q: completion -> egress frames assembled from the rewritten header
+         and the payload still in the rx buffer; replicas / learn events / outer headers from a
+         per-burst CPU side pass (no ring drain); recirculation re-enters natively; slow-path
+         frames come back here (`on_punt`).
 
 One engine drives every data plane it is given: ``NativeLivePath([dp_gpu0, dp_gpu1, ...], ports)``
 steers each flow to its owner GPU (the flow table of a multi-GPU data plane is sharded the same
 way, dataplane/multi.py).  Without a GPU the backends are the bit-exact C++ oracle, so the whole
 native path is tested on CPU (tests/test_native_io.py).
 
-Table commits: the engine is paused around every commit of any of its data planes (no frame is
-in flight while tables move; ring kernels are drained / relaunched by the commit itself), then the
-oracle backends are re-pointed at the new tables and the side / tunnel / steering inputs refreshed.
+Table commits (DataPlane.commit hooks):
+  * GPU planes with running coop rings: the commit is applied under traffic; the engine only
+    holds publication for the epoch switch (`hold` / `release`: microseconds, nothing drained)
+    and swaps its own configuration (steering, tunnel redirects, side ports, side-pass table
+    snapshot) copy-on-write at the same moment;
+  * otherwise (CPU oracle planes, ring relaunches): the engine is paused around the commit
+    (`pre_commit` / `post_commit`: nothing in flight while tables move).
 
 Health: a failed engine (a ring that stopped completing, an I/O error) sets ``error`` and
 ``healthy = False``; with ``auto_restart`` the supervisor thread rebuilds the engine in place.
@@ -71,11 +77,16 @@ def _make_port(nf, spec):
 
 class NativeLivePath:
     def __init__(self, dps, ports: dict, burst: int = 256, ring_capacity: int = 4096, inflight: int = 64,
-                 on_punt=None, auto_restart: bool = True, tx_workers: int = 2):
+                 on_punt=None, auto_restart: bool = True, tx_workers: int = 1, queues: int = 1,
+                 max_inflight_frames: int = 0, port_queues: dict | None = None):
+        """dps: one data plane or a list (one per GPU, or a MultiDataPlane's planes); ports:
+        {port id: vport spec}; queues: rx threads (each with a ring queue on every GPU);
+        port_queues: {port id: queue} (default: least loaded); max_inflight_frames: per lane
+        bound of the engine's own queueing (0: the ring capacity)."""
         from ..native import nfdp
 
         self.nf = nfdp()
-        self.dps = list(dps) if isinstance(dps, (list, tuple)) else [dps]
+        self.dps = list(dps) if isinstance(dps, (list, tuple)) else list(getattr(dps, "planes", [dps]))
         if not self.dps:
             raise ValueError("at least one data plane")
         self.gpu = self.dps[0].gpu
@@ -84,8 +95,10 @@ class NativeLivePath:
         if ring_capacity < 64 or ring_capacity & (ring_capacity - 1):
             raise ValueError("ring_capacity must be a power of two >= 64")
         self.burst, self.capacity, self.inflight = int(burst), int(ring_capacity), int(inflight)
-        self.tx_workers = int(tx_workers)
+        self.tx_workers, self.queues = int(tx_workers), int(queues)
+        self.max_inflight_frames = int(max_inflight_frames)
         self.specs = dict(ports)
+        self.port_queues = dict(port_queues or {})
         self.on_punt = on_punt
         self.auto_restart = auto_restart
         self.error: str | None = None
@@ -99,6 +112,7 @@ class NativeLivePath:
         self._sup: threading.Thread | None = None
         self._stop = threading.Event()
         self._totals: dict[str, int] = {}
+        self._side_base = None          # side counters of engines that were torn down
         self.punts = 0
 
     # ------------------------------------------------------------------ lifecycle
@@ -112,7 +126,7 @@ class NativeLivePath:
 
     def _build(self) -> None:
         nf = self.nf
-        eng = nf.IoEngine(self.burst, self.inflight, self.tx_workers)
+        eng = nf.IoEngine(self.burst, self.inflight, self.tx_workers, self.queues, self.max_inflight_frames)
         self._rings, self._backends = [], []
         for dp in self.dps:
             if self.gpu:
@@ -121,23 +135,28 @@ class NativeLivePath:
                 from .ring import RingPath
 
                 with torch.cuda.device(dp.tdev):
-                    ring = RingPath(dp, capacity=self.capacity, host_slots=True, coop=True, side=True,
-                                    deadline_s=3600.0)
+                    ring = RingPath(dp, capacity=self.capacity, host_slots=True, coop=True, side=False,
+                                    deadline_s=3600.0, queues=self.queues)
                     ring.start()
                 self._rings.append(ring)
                 be = nf.GpuBackend(ring.eng)
             else:
-                be = nf.OracleBackend(self.capacity)
+                be = nf.OracleBackend(self.capacity, self.queues)
             self._backends.append(be)
             eng.add_backend(be)
             if self not in getattr(dp, "_io_hooks", []):
                 dp._io_hooks = getattr(dp, "_io_hooks", []) + [self]
             dp._learned_on_device = True     # the engine learns into the device MAC table: commits pull first
+        # replica counters appear in the first plane's counters (a MultiDataPlane sums its planes)
+        hooks = getattr(self.dps[0], "_ctr_hooks", [])
+        if self not in hooks:
+            self.dps[0]._ctr_hooks = hooks + [self]
         for idx, spec in self.specs.items():
             p = self._ports.get(idx)
             if p is None:
                 p = self._ports[idx] = _make_port(nf, spec)
-            eng.add_port(int(idx), p)
+            eng.add_port(int(idx), p, int(self.port_queues.get(idx, -1)))
+        eng.learn_stamp = max(int(getattr(d, "stamp", 0)) for d in self.dps) + 1
         self._eng = eng
         self._refresh()
         eng.start()
@@ -153,12 +172,17 @@ class NativeLivePath:
             hooks = getattr(dp, "_io_hooks", [])
             if self in hooks:
                 hooks.remove(self)
+            ch = getattr(dp, "_ctr_hooks", [])
+            if self in ch:
+                ch.remove(self)
 
     def _teardown(self) -> None:
         if self._eng is not None:
             self._accumulate()
             self._eng.stop()
             self._sync_stamps()
+            sp, sd = np.asarray(self._eng.side_port_counters()), np.asarray(self._eng.side_drop_counters())
+            self._side_base = (sp, sd) if self._side_base is None else (self._side_base[0] + sp, self._side_base[1] + sd)
         errs = []
         for r in self._rings:
             try:
@@ -171,14 +195,15 @@ class NativeLivePath:
             raise errs[0]
 
     def _sync_stamps(self) -> None:
-        for dp, be in zip(self.dps, self._backends):
-            st = getattr(be, "stamp", None)
-            if st is not None:
-                dp.stamp = max(dp.stamp, int(st))
+        st = int(self._eng.learn_stamp)
+        for dp in self.dps:
+            dp.stamp = max(dp.stamp, st)
 
     # ------------------------------------------------------------------ table commits (DataPlane hooks)
     def pre_commit(self, dp) -> None:
+        """Tables move with nothing in flight (oracle planes, ring relaunches)."""
         if self._eng is not None and self._eng.running:
+            self._eng.flush_learning()
             self._eng.pause()
 
     def post_commit(self, dp) -> None:
@@ -187,43 +212,81 @@ class NativeLivePath:
         self._refresh()
         self._eng.resume()
 
+    def hold(self, dp) -> None:
+        """A live commit's epoch switch: publication stops between two bursts (no drain)."""
+        if self._eng is not None and self._eng.running:
+            self._eng.hold()
+
+    def release(self, dp) -> None:
+        if self._eng is None:
+            return
+        self._refresh()
+        self._eng.release()
+
     def _refresh(self) -> None:
-        """Point the oracle backends at the current tables; side ports, tunnel redirects, steering."""
+        """Point the oracle backends at the current tables; the side-pass table snapshots, side
+        ports, tunnel redirects and steering (copy-on-write in the engine)."""
         eng = self._eng
-        for dp, be in zip(self.dps, self._backends):
+        for g, (dp, be) in enumerate(zip(self.dps, self._backends)):
             if not self.gpu:
-                side = dp._side_buffers(self.capacity) if dp.side_active() else None
-                be.configure(dp.tables_ptrs(), dp._ptr("flow_ctr"), dp._ptr("port_ctr"), dp._ptr("drop_ctr"), side)
+                be.configure(dp.tables_ptrs(), dp._ptr("flow_ctr"), dp._ptr("port_ctr"), dp._ptr("drop_ctr"))
+            eng.set_side_tables(g, self.nf.SideTables(**dp.side_tables_host()))
         dp0 = self.dps[0]
         a = dp0.ports.a
         flags = a["flags"].astype(np.uint32)
         eng.set_side_ports([int(i) for i in np.nonzero(flags & np.uint32(SIDE_PORT_FLAGS))[0]])
+        red = []
         for i in np.nonzero(flags & np.uint32(T.PORT_TUNNEL))[0]:
             tab = dp0.tunnels6 if flags[i] & T.PORT_TUNNEL6 else dp0.tunnels
             lag = int(a[i]["lag"])
             if lag < len(tab.a):
-                eng.set_redirect(int(i), int(tab.a[lag]["out_port"]))
+                red.append((int(i), int(tab.a[lag]["out_port"])))
+        eng.set_redirects(red)   # the whole map: a port that stopped being a tunnel loses its entry
         if len(self.dps) > 1:
             v6 = any(d._v6_keys() for d in self.dps)   # IPv6 frames steer by their folded 5-tuple
             eng.set_steering(np.ascontiguousarray(a), bytes(dp0.rss_key), v6)
 
+    # ------------------------------------------------------------------ counters (DataPlane._ctr_hooks)
+    def side_port_counters(self) -> np.ndarray:
+        v = np.asarray(self._eng.side_port_counters()) if self._eng is not None else np.zeros(0, np.uint64)
+        if self._side_base is not None:
+            v = self._side_base[0] + v if len(v) else self._side_base[0]
+        return v
+
+    def side_drop_counters(self) -> np.ndarray:
+        v = np.asarray(self._eng.side_drop_counters()) if self._eng is not None else np.zeros(0, np.uint64)
+        if self._side_base is not None:
+            v = self._side_base[1] + v if len(v) else self._side_base[1]
+        return v
+
+    def flush_learning(self) -> None:
+        """Block until every MAC the engine has seen so far is in every plane's table."""
+        if self._eng is not None:
+            self._eng.flush_learning()
+
     # ------------------------------------------------------------------ ports
-    def add_port(self, idx: int, spec) -> None:
+    def add_port(self, idx: int, spec, queue: int = -1) -> None:
         with self._lock:
             self.specs[idx] = spec
+            if queue >= 0:
+                self.port_queues[idx] = queue
             p = self._ports[idx] = _make_port(self.nf, spec)
             if self._eng is not None:
-                self._eng.add_port(int(idx), p)
+                self._eng.add_port(int(idx), p, int(self.port_queues.get(idx, -1)))
 
     def remove_port(self, idx: int):
         with self._lock:
             self.specs.pop(idx, None)
+            self.port_queues.pop(idx, None)
             self._ports.pop(idx, None)
             if self._eng is not None:
                 return self._eng.remove_port(int(idx))
 
     def port(self, idx: int):
         return self._ports.get(idx)
+
+    def port_queue(self, idx: int) -> int:
+        return int(self._eng.port_queue(int(idx))) if self._eng is not None else -1
 
     # ------------------------------------------------------------------ slow path + supervision
     def poll_punts(self) -> int:
@@ -277,14 +340,15 @@ class NativeLivePath:
         if self._eng is None:
             return
         for k, v in self._eng.stats().items():
-            self._totals[k] = self._totals.get(k, 0) + int(v)
+            if k != "queues":
+                self._totals[k] = self._totals.get(k, 0) + int(v)
 
     @property
     def stats(self) -> dict:
         s = dict(self._totals)
         if self._eng is not None:
             for k, v in self._eng.stats().items():
-                s[k] = s.get(k, 0) + int(v)
+                s[k] = (s.get(k, 0) if k != "queues" else 0) + int(v)
         s["punt_handled"] = self.punts
         s["restarts"] = self.restarts
         return s

@@ -40,13 +40,15 @@ from .engine import DataPlane
 
 class RingPath:
     def __init__(self, dp: DataPlane, capacity: int = 1 << 16, wgs_per_cu: int = 1, deadline_s: float = 120.0,
-                 knobs: int = 0, coop: bool = True, host_slots: bool = False, side: bool = False):
+                 knobs: int = 0, coop: bool = True, host_slots: bool = False, side: bool = False, queues: int = 1):
         """coop=True: a workgroup's 4 waves share each chunk (ACL rule tiles split 4 ways) —
         lowest latency.  coop=False: every wave takes its own chunks — highest throughput.
         host_slots=True: the ring slots live in pinned host memory and the resident kernel reads /
         writes the frames over PCIe itself (zero-copy host rings, e.g. pod vhost / AF_XDP).
         side=True: the kernel puts packets that need replicas / learn events / outer headers on
-        the data plane's side list; `side_pass()` runs the side kernel over them (live path)."""
+        the data plane's side list; `side_pass()` runs the side kernel over them.
+        queues: independent rings served by the one resident grid (workgroup b serves queue
+        b % queues): one per producer thread of the native I/O engine (ring.h)."""
         if not dp.gpu:
             raise RuntimeError("RingPath needs a GPU data plane")
         if capacity < 64 or capacity & (capacity - 1):
@@ -57,7 +59,11 @@ class RingPath:
         self.knobs = int(knobs) & 0x60  # diagnostic knobs (ring.hip kRingTrace / kRingNoCounters), attribution only
         self.coop = bool(coop)
         self.host_slots = bool(host_slots)
-        self.eng = dp.nf.RingEngine(self.capacity, int(dp.num_cus), int(wgs_per_cu), self.coop, self.host_slots)
+        if queues > 1 and side:
+            raise ValueError("the side list indexes one queue's slots: side=True needs queues=1")
+        self.queues = int(queues)
+        self.eng = dp.nf.RingEngine(self.capacity, int(dp.num_cus), int(wgs_per_cu), self.coop, self.host_slots,
+                                    self.queues)
         self._staged = 0
         self.side = bool(side)
         if self.side and self.capacity > dp.cap_rep:

@@ -11,7 +11,7 @@ Measured, per device:
                       vport accepts (64-B frames, 8 pods, random pod -> pod flows);
   * `p50/p99_us`    : one-way latency of that saturated run (queueing included);
   * `idle_p50/p99`  : closed loop, one frame in flight (the unloaded pod -> pod latency);
-  * `half_p50/p99`  : offered load at half the measured maximum.
+  * `load90_*`, `half_*` : offered load at 90 % / 50 % of the measured maximum.
 
     python tools/live_bench.py [--device cuda|cpu] [--duration 1.0] [--flows 1048576]
 """
@@ -57,8 +57,9 @@ def drain(nf, pods, live, quiet_s: float = 0.05, limit_s: float = 10.0) -> int:
 
 
 def run(device: str = "cuda", n_pods: int = 8, flows: int = 1 << 20, n_acl: int = 256, duration: float = 1.0,
-        threads: int = 4, burst: int = 512, inflight: int = 192, ring_capacity: int = 16384,
-        hash_mode: str = "lds", tx_workers: int = 2) -> dict:
+        threads: int = 4, burst: int = 512, inflight: int = 64, ring_capacity: int = 16384,
+        hash_mode: str = "lds", tx_workers: int = 1, queues: int = 4, max_inflight_frames: int = 4096,
+        pod_ring: int = 1024) -> dict:
     nf = nfdp()
     t0 = time.perf_counter()
     dp = DataPlane(device=device, flow_buckets=max(1 << 12, 1 << int(np.ceil(np.log2(max(flows, 1) / 2)))),
@@ -66,16 +67,18 @@ def run(device: str = "cuda", n_pods: int = 8, flows: int = 1 << 20, n_acl: int 
     sc = S.build_sfc(dp, n_pods=n_pods, n_flows=flows, n_acl=n_acl, seed=0)
     dp.commit(full=True)
     d = tempfile.mkdtemp(prefix="dpu-live-", dir=memif_dir())
-    ports = {int(sc.pod_port[i]): MemifVport(os.path.join(d, f"pod{i}"), ring_size=4096) for i in range(n_pods)}
+    ports = {int(sc.pod_port[i]): MemifVport(os.path.join(d, f"pod{i}"), ring_size=pod_ring) for i in range(n_pods)}
     live = NativeLivePath(dp, ports, burst=burst, ring_capacity=ring_capacity, inflight=inflight,
-                          tx_workers=tx_workers).start()
+                          tx_workers=tx_workers, queues=queues, max_inflight_frames=max_inflight_frames).start()
     setup_s = time.perf_counter() - t0
     try:
         pods = []
         for i in range(n_pods):
             slots, im = S.traffic(sc, 4096, seed=100 + i, src_pods=np.array([i]))
             pods.append((ports[int(sc.pod_port[i])].path, slots, (im >> 16).astype(np.uint32)))
-        out = {"device": device, "tx_workers": tx_workers, "inflight_bursts": inflight, "pods": n_pods, "flows": int(len(sc.keys)), "acl_rules": n_acl, "frame_bytes": 64,
+        out = {"device": device, "queues": queues, "tx_workers": tx_workers, "inflight_bursts": inflight,
+               "max_inflight_frames": max_inflight_frames, "pod_ring": pod_ring, "gen_threads": threads,
+               "pods": n_pods, "flows": int(len(sc.keys)), "acl_rules": n_acl, "frame_bytes": 64,
                "setup_s": round(setup_s, 1)}
         # saturated: every pod as fast as its vport takes frames
         r = nf.trafgen_run(pods, duration_s=duration, warmup_s=0.2, threads=threads, burst=32)
@@ -88,15 +91,21 @@ def run(device: str = "cuda", n_pods: int = 8, flows: int = 1 << 20, n_acl: int 
         out.update(idle_p50_us=_pct(r1["lat_us"], 50), idle_p99_us=_pct(r1["lat_us"], 99),
                    idle_frames=int(r1["received"]))
         drain(nf, pods, live)
-        # half load
+        # offered loads below saturation: 90 % and 50 % of the measured maximum
         if mpps > 0:
-            r2 = nf.trafgen_run(pods, duration_s=min(duration, 0.5), warmup_s=0.1, threads=threads, burst=8,
-                                rate_pps=0.5 * mpps * 1e6)
-            out.update(half_load_mpps=round(r2["received"] / min(duration, 0.5) / 1e6, 3),
-                       half_p50_us=_pct(r2["lat_us"], 50), half_p99_us=_pct(r2["lat_us"], 99))
+            for tag, frac in (("load90", 0.9), ("half", 0.5)):
+                r2 = nf.trafgen_run(pods, duration_s=min(duration, 0.5), warmup_s=0.1, threads=threads, burst=8,
+                                    rate_pps=frac * mpps * 1e6)
+                out.update({f"{tag}_mpps": round(r2["received"] / min(duration, 0.5) / 1e6, 3),
+                            f"{tag}_p50_us": _pct(r2["lat_us"], 50), f"{tag}_p99_us": _pct(r2["lat_us"], 99)})
+                drain(nf, pods, live)
+            out["half_load_mpps"] = out.pop("half_mpps")
         st = live.stats
         out["engine"] = {k: int(v) for k, v in st.items() if k in ("rx", "tx", "drop", "bursts", "tx_full",
-                                                                    "side_passes", "punt", "rx_wait_tx")}
+                                                                    "side_passes", "punt", "rx_wait_tx",
+                                                                    "rx_idle_polls", "publish_ns", "deliver_ns")}
+        if st.get("bursts"):
+            out["engine"]["frames_per_burst"] = round(st["rx"] / st["bursts"], 1)
         lat = live.latency_us()
         out["engine_burst_p50_us"] = _pct(lat, 50)
         out["error"] = live.error
@@ -120,11 +129,15 @@ def main() -> None:
     ap.add_argument("--pods", type=int, default=8)
     ap.add_argument("--threads", type=int, default=4)
     ap.add_argument("--burst", type=int, default=512)
-    ap.add_argument("--inflight", type=int, default=192)
-    ap.add_argument("--tx-workers", type=int, default=2)
+    ap.add_argument("--inflight", type=int, default=64)
+    ap.add_argument("--tx-workers", type=int, default=1)
+    ap.add_argument("--queues", type=int, default=4)
+    ap.add_argument("--max-inflight-frames", type=int, default=4096)
+    ap.add_argument("--pod-ring", type=int, default=1024)
     a = ap.parse_args()
     print(json.dumps(run(a.device, a.pods, a.flows, duration=a.duration, threads=a.threads, burst=a.burst,
-                         inflight=a.inflight, tx_workers=a.tx_workers)), flush=True)
+                         inflight=a.inflight, tx_workers=a.tx_workers, queues=a.queues,
+                         max_inflight_frames=a.max_inflight_frames, pod_ring=a.pod_ring)), flush=True)
 
 
 if __name__ == "__main__":
