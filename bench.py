@@ -43,6 +43,27 @@ sys.path.insert(0, REPO)
 BASELINE_METRIC = "Mpps + p50 pod-to-pod µs latency, 1M-flow SFC at 1/2/4/8 MI355X"
 
 
+# RSS exchange protocol facts the multi-GPU tests check against (tests/test_multigpu.py,
+# tests/test_rss_cpu.py): per step, one all-to-all of the per-peer counts, then one grouped
+# send/recv of exactly those packets
+RSS_A2A_PER_STEP = 2
+RSS_EXCHANGE_KEYS = ("a2a_ms", "a2a_per_step", "protocol", "remote_frac", "max_packets_per_peer", "overflow_drops",
+                     "xgmi_bytes_out_per_gpu_per_step", "xgmi_gbps_out_per_gpu", "host_lag_steps", "note")
+
+
+def rss_exchange_info(a2a_s: float, sent_per_step: float, max_peer: int, remote_frac: float, lag: int) -> dict:
+    """The `exchange` block of an RSS run: one exchange's time, bytes a GPU sends per step (68 B
+    per misdirected packet: header slot + meta) and the xGMI rate that implies."""
+    peer_bytes = int(sent_per_step * 68)
+    return {"a2a_ms": round(a2a_s * 1e3, 4), "a2a_per_step": RSS_A2A_PER_STEP,
+            "protocol": "count-first: counts all-to-all, then grouped send/recv of exactly those packets",
+            "remote_frac": remote_frac, "max_packets_per_peer": int(max_peer), "overflow_drops": 0,
+            "xgmi_bytes_out_per_gpu_per_step": peer_bytes,
+            "xgmi_gbps_out_per_gpu": round(peer_bytes / max(a2a_s, 1e-9) / 1e9, 3),
+            "host_lag_steps": int(lag),
+            "note": "overlapped with later steps' kernels in the timed region; counts read lag steps late"}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -394,9 +415,9 @@ def main() -> None:
     xchg = None
     if rss:
         # the timed steps' traffic: packets this GPU handed to their owners (68 B each on xGMI)
-        sent_per_step = eng.stats["sent"] / max(eng.stats["steps"] - 1, 1)
+        sent_per_step = eng.stats["sent"] / max(eng.stats["steps"], 1)
         max_peer = eng.stats["max_peer"]
-        s0 = eng.slots[eng.k & 1 ^ 1]
+        s0 = eng.slots[eng.k % eng.nslots]   # (flushed: no slot is in flight)
 
         def xone():
             eng.exchange(s0)
@@ -416,13 +437,7 @@ def main() -> None:
         tt = torch.tensor([el], dtype=torch.float64, device=cdev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         el = float(tt.item())
-        peer_bytes = int(sent_per_step * 68)
-        xchg = {"a2a_ms": round(el / reps * 1e3, 4), "a2a_per_step": 2,
-                "protocol": "count-first: counts all-to-all, then grouped send/recv of exactly those packets",
-                "remote_frac": a.remote_frac, "max_packets_per_peer": max_peer, "overflow_drops": 0,
-                "xgmi_bytes_out_per_gpu_per_step": peer_bytes,
-                "xgmi_gbps_out_per_gpu": round(peer_bytes / (el / reps) / 1e9, 3),
-                "note": "overlapped with the next step's kernel in the timed region"}
+        xchg = rss_exchange_info(el / reps, sent_per_step, max_peer, a.remote_frac, eng.lag)
     if replicated:
         s0 = eng.slots[0]
         for _ in range(3):

@@ -45,7 +45,8 @@ def build_vsp(a, pm: PathManager):
                       hash_mode=cfg.hash_mode, acl_mode=cfg.acl_mode,
                       state_dir=a.state_dir or cfg.vsp_state_dir or None, nl=nl, live=a.live,
                       live_engine=a.live_engine, gpus=a.gpus if a.gpus == "all" else int(a.gpus),
-                      vport_kind=a.vport_kind, tx_workers=a.io_workers)
+                      vport_kind=a.vport_kind or cfg.vport_kind, tx_workers=a.io_workers or cfg.io_workers,
+                      io_queues=a.io_queues or cfg.io_queues)
     from ..cni.netlink import RtNetlink
     from ..platform.platform import SysfsPlatform
     from ..utils.cmdrunner import HostRunner
@@ -93,14 +94,18 @@ def main(argv=None, stop: threading.Event | None = None) -> int:
     ap.add_argument("--state-dir", default="", help="amd-gpu: journal + snapshot directory (resume on restart)")
     ap.add_argument("--live", action="store_true",
                     help="amd-gpu: vports are real TAP netdevs and pod traffic flows through the data plane")
-    ap.add_argument("--live-engine", default="batch", choices=["batch", "ring", "native"],
+    ap.add_argument("--live-engine", default="native", choices=["batch", "ring", "native"],
                     help="amd-gpu --live: fused kernel per poll cycle (Python loop), the persistent ring kernel on "
                          "pinned host slots (Python loop), or the native C++ I/O engine + ring kernel")
     ap.add_argument("--gpus", default="1", help="amd-gpu: GPUs behind the VSP (a number or 'all'): tables "
                     "replicated, flows sharded by RSS owner, the native engine steering frames to their owner")
-    ap.add_argument("--vport-kind", default="tap", choices=["tap", "memif"],
-                    help="amd-gpu --live: vports as TAP netdevs or shared-memory (memif) regions")
-    ap.add_argument("--io-workers", type=int, default=4, help="native engine delivery threads per GPU")
+    ap.add_argument("--vport-kind", default="", choices=["", "veth", "tap", "memif"],
+                    help="amd-gpu --live: vports as veth pairs (kernel-netdev pods, AF_PACKET rings), TAP "
+                         "netdevs or shared-memory (memif) regions; default: node config vport_kind (veth)")
+    ap.add_argument("--io-queues", type=int, default=0,
+                    help="native engine rx queues (threads), each with a ring queue on every GPU (0: node config)")
+    ap.add_argument("--io-workers", type=int, default=0,
+                    help="native engine delivery threads per queue (0: node config)")
     ap.add_argument("--metrics-bind-address", default="", help="amd-gpu: data-plane /metrics address (off if empty)")
     ap.add_argument("--agent-mbox", default="", help="amd-gpu: run the node control agent on this mailbox path")
     ap.add_argument("--agent-config", default="", help="agent SoC config file (default: one PF + --agent-vfs VFs)")

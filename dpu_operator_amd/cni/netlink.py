@@ -427,7 +427,8 @@ class RtNetlink(NetlinkManager):
         self._set(name, ns, attrs=self._attr(IFLA_MTU, struct.pack("I", int(mtu))))
 
     def link_set_ns(self, name, target_ns, ns=""):
-        fd = os.open(target_ns, os.O_RDONLY)
+        # "" = this process's own namespace (the daemon's: host network), as elsewhere in this API
+        fd = os.open(target_ns or "/proc/self/ns/net", os.O_RDONLY)
         try:
             self._set(name, ns, attrs=self._attr(IFLA_NET_NS_FD, struct.pack("I", fd)))
         finally:

@@ -36,6 +36,10 @@ class NodeConfig:
     acl_mode: str = "mfma"             # mfma | scalar | off
     wire_port: int = 4000
     vsp_state_dir: str = ""            # journal + snapshots (checkpoint/resume); "" = off
+    # live data path of the GPU VSP (vsp/gpu.py, dataplane/native_io.py)
+    vport_kind: str = "veth"           # veth (kernel netdev pods, AF_PACKET rings) | memif | tap
+    io_queues: int = 4                 # native engine rx queues (threads), each with a ring queue per GPU
+    io_workers: int = 1                # native engine delivery threads per queue
     # daemon cadences (seconds)
     device_poll: float = 5.0           # ListAndWatch refresh (deviceplugin.go:109)
     detect_poll: float = 1.0           # platform detection (daemon.go:88)
@@ -76,6 +80,10 @@ class NodeConfig:
             raise ValueError("nf_devices_per_pod must be >= 1")
         if self.hash_mode not in ("lds", "mfma", "scalar") or self.acl_mode not in ("mfma", "scalar", "off"):
             raise ValueError("unknown hash / ACL mode")
+        if self.vport_kind not in ("veth", "memif", "tap"):
+            raise ValueError("vport_kind is veth, memif or tap")
+        if not 1 <= self.io_queues <= 64 or not 1 <= self.io_workers <= 16:
+            raise ValueError("io_queues in [1, 64], io_workers in [1, 16]")
 
     def logical_bridge(self, vf: int) -> int:
         return vf + self.logical_bridge_offset

@@ -7,6 +7,10 @@ internal/daemon/device-handler/dpu-device-handler/dpudevicehandler.go:48-106.
   must be PCI addresses.
 * ListAndWatch polls the handler every `poll` s (5 s in the reference) and streams the list when it
   changes; Allocate rejects unknown or unhealthy devices and returns env NF-DEV="<id>,<id>,".
+  GPU-VSP shared-memory vports: a device whose region exists (<PathManager.memif_dir>/<id>.memif)
+  is also mounted into the container (PathManager.memif_container_path) and listed in NF-MEMIF,
+  the way memif / vhost-user device plugins hand over their sockets; netdev vports (veth, TAP)
+  reach the pod through the CNI instead (networkfn.cmd_add moves the netdev named <id>).
 * Serve: gRPC on the plugin socket, self-dial until ready (the reference's WithBlock workaround),
   then Register{v1beta1, endpoint filename, resource name} with the kubelet.
 """
@@ -111,7 +115,8 @@ class DevicePluginServer:
         CONTROL.allocations.inc()
         resp = dp.AllocateResponse()
         for creq in request.container_requests:
-            names = ""
+            names, regions = "", []
+            cr = resp.container_responses.add()
             for did in creq.devices_ids:
                 dev = self.devices.get(did)
                 if dev is None:
@@ -121,8 +126,14 @@ class DevicePluginServer:
                     context.abort(grpc.StatusCode.INVALID_ARGUMENT,
                                   f"invalid allocation request with unhealthy device: {did}")
                 names += did + ","
-            cr = resp.container_responses.add()
+                host = os.path.join(self.pm.memif_dir(), f"{did}.memif")
+                if "/" not in did and os.path.exists(host):
+                    target = self.pm.memif_container_path(did)
+                    cr.mounts.add(container_path=target, host_path=host, read_only=False)
+                    regions.append(target)
             cr.envs["NF-DEV"] = names
+            if regions:
+                cr.envs["NF-MEMIF"] = ",".join(regions)
         return resp
 
     def GetPreferredAllocation(self, request, context):

@@ -292,11 +292,48 @@ class ColocatedSideManager:
     def setup_devices(self) -> None:
         self.dpu.setup_devices()
 
+    @staticmethod
+    def _gpu_vport(req: PodRequest) -> int | None:
+        """Index of the GPU vport a workload pod was allocated (deviceID = the vport netdev name,
+        e.g. dpuvp3 -> 3); None for an SR-IOV VF (PCI address) or no device."""
+        import re
+
+        from ..cni.sriov.utils import is_valid_pci_address
+
+        dev = getattr(req.cni_conf, "deviceID", "") if req.cni_conf is not None else ""
+        if not dev or is_valid_pci_address(dev):
+            return None
+        m = re.fullmatch(r"[A-Za-z][\w.-]*?(\d+)", dev)
+        return int(m.group(1)) if m else None
+
     def cni_add(self, req: PodRequest) -> dict:
-        return self.dpu.nf_add(req) if req.pod_namespace == V.NAMESPACE else self.host.cni_add(req)
+        if req.pod_namespace == V.NAMESPACE:
+            return self.dpu.nf_add(req)
+        idx = self._gpu_vport(req)
+        if idx is None:
+            return self.host.cni_add(req)
+        # a GPU vport (veth / TAP netdev): the pod gets the netdev itself (networkfn moves it into
+        # its namespace), then the host side's CreateBridgePort host<pf>-<idx> programs the VF port
+        res = networkfn.cmd_add(req, self.dpu.nl, self.dpu.ipam)
+        try:
+            self.host.create_bridge_port(self.host.pf, idx, node_config().logical_bridge(idx), req.cni_conf.MAC)
+        except Exception:
+            networkfn.cmd_del(req, self.dpu.nl, self.dpu.ipam)
+            raise
+        return res
 
     def cni_del(self, req: PodRequest) -> None:
-        return self.dpu.nf_del(req) if req.pod_namespace == V.NAMESPACE else self.host.cni_del(req)
+        if req.pod_namespace == V.NAMESPACE:
+            return self.dpu.nf_del(req)
+        idx = self._gpu_vport(req)
+        if idx is None:
+            return self.host.cni_del(req)
+        networkfn.cmd_del(req, self.dpu.nl, self.dpu.ipam)
+        try:
+            self.host.delete_bridge_port(self.host.pf, idx, 0, "")
+        except grpc.RpcError as e:
+            log.warning("DeleteBridgePort failed: %s", e)
+        return None
 
     def listen(self) -> None:
         self.dpu.listen(with_cni=False)

@@ -259,8 +259,12 @@ class DataPlane:
         return slot
 
     def remove_flow6(self, src, dst, sport: int = 0, dport: int = 0, proto: int = 17, zone: int = 0) -> bool:
-        key, _ = T.flow_key6(src, dst, sport, dport, proto, zone)
-        self.flows6.pop(tuple(int(x) for x in key), None)
+        key, addrs = T.flow_key6(src, dst, sport, dport, proto, zone)
+        k = tuple(int(x) for x in key)
+        old = self.flows6.get(k)
+        if old is None or not np.array_equal(old, addrs):
+            return False     # not installed, or the folded key belongs to another 5-tuple
+        del self.flows6[k]
         return self.flows.erase(key)
 
     def _side6_rows(self, buckets: np.ndarray, slots: np.ndarray | None = None) -> np.ndarray:
@@ -593,9 +597,14 @@ class DataPlane:
         return port, bytes(frame[off:])
 
     def pull_learned(self) -> int:
-        """Fold the entries the data plane learned into the host MAC model."""
+        """Fold the entries the data plane learned into the host MAC model (native I/O engines
+        feeding this plane first apply every learn event they have queued)."""
         if "macs" not in self._dev:
             return 0
+        for h in getattr(self, "_io_hooks", ()):
+            fl = getattr(h, "flush_learning", None)
+            if fl is not None:
+                fl()
         raw = self._dev["macs"]
         arr = (raw.cpu().numpy() if self.gpu else raw).view(T.MAC_DTYPE)
         n = self.macs.merge_learned(arr)

@@ -58,13 +58,53 @@ class MemifVport:
 
 
 class PacketVport:
-    """The VSP-side end of a veth pair, read and written through AF_PACKET TPACKET_V2 rings."""
+    """The VSP-side end of a veth pair, read and written through AF_PACKET TPACKET_V2 rings.
+
+    `VethVport.create` makes the pair: the pod end (`name`, the device the device plugin hands
+    out and the CNI moves into the pod, networkfn.cmd_add) and the data-plane end (`name` + "d")
+    this port opens."""
 
     def __init__(self, ifname: str, frames: int = 1024, frame_size: int = 2048):
         self.ifname, self.frames, self.frame_size = ifname, int(frames), int(frame_size)
+        self._nl = None
+        self.name = None
+
+    @classmethod
+    def create_veth(cls, nl, name: str, mac: str | None = None, frames: int = 1024) -> "PacketVport":
+        """A veth pair for a kernel-netdev pod: `name` (pod end) and `name`d (data-plane end)."""
+        peer = name + "d"
+        if len(peer) > 15:
+            raise ValueError("interface names are at most 15 characters")
+        nl.link_add_veth(name, peer)
+        if mac:
+            nl.link_set_hw_addr(name, mac)
+        _quiet_ipv6(peer)
+        nl.link_set_up(peer)
+        nl.link_set_up(name)
+        vp = cls(peer, frames=frames)
+        vp._nl, vp.name = nl, name
+        return vp
 
     def make(self, nf):
         return nf.PacketPort(self.ifname, self.frames, self.frame_size)
+
+    def close(self) -> None:
+        """Delete the pair (the pod end goes with it, wherever it is)."""
+        if self._nl is not None:
+            try:
+                self._nl.link_del(self.ifname)
+            except Exception:  # noqa: BLE001 - already gone with its namespace
+                pass
+            self._nl = None
+
+
+def _quiet_ipv6(ifname: str) -> None:
+    """No IPv6 autoconfiguration traffic from the data-plane end of a vport (best effort)."""
+    try:
+        with open(f"/proc/sys/net/ipv6/conf/{ifname}/disable_ipv6", "w") as f:
+            f.write("1")
+    except OSError:
+        pass
 
 
 def _make_port(nf, spec):

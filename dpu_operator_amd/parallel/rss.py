@@ -23,7 +23,12 @@ kernel:
 (The rx pass of step k used to run on the compute stream between fused(k) and fused(k+1): its
 launches and its workgroups' table staging cost a fixed ~27-46 us per step, rss_probe r3 s11.
 On its own stream it overlaps the next step's kernel; the slot events order the reuse of the
-two exchange slots and of the receive buffers.)
+exchange slots and of the receive buffers.)
+
+The host never waits for the GPU in steady state: the send/recv sizes of a step must be known on
+the host (RCCL P2P), so the counts come back through pinned memory, but step k's counts are read
+only at step k + `lag` (default 2), long after they landed - the host runs up to `lag` steps ahead
+of the device.  `lag + 1` exchange slots rotate.
 
 Cross-GPU bytes per packet: 68 B (header slot + meta) for misdirected packets only; the payload
 never moves.  The CPU twins (oracle REMOTE steer + gather) run the same class on gloo ranks.
@@ -77,7 +82,7 @@ class RssShardedDataPlane:
     """
 
     def __init__(self, dp: DataPlane, rank: int, world: int, batch: int, remote_frac: float = 0.01,
-                 group=None):
+                 group=None, lag: int = 2):
         if world < 2:
             raise ValueError("RssShardedDataPlane needs world >= 2 (use DataPlane.run for one GPU)")
         self.dp, self.nf = dp, dp.nf
@@ -94,8 +99,13 @@ class RssShardedDataPlane:
         # LIST instances exist for the LDS / MFMA hash with the MFMA / no ACL; others use REMOTE steer
         self.use_list = self.gpu and self.hash_mode in (1, 2) and self.acl_mode in (1, 2)
         nl = int(self.nf.steer_list_len(batch, int(dp.num_cus))) if self.use_list else 0
+        self.lag = max(int(lag), 1)
+        self.nslots = self.lag + 1
         self.slots = [_Slot(self.dev, world, self.pseg, batch, self.gpu, nl, 4 * int(dp.num_cus) if self.use_list else 1)
-                      for _ in range(2)]
+                      for _ in range(self.nslots)]
+        for i, sl in enumerate(self.slots):
+            sl.idx = i
+            sl.hev = torch.cuda.Event() if self.gpu else None   # counts are in host memory
         u8, i32 = dict(dtype=torch.uint8, device=self.dev), dict(dtype=torch.int32, device=self.dev)
         self.out = torch.zeros((batch, 64), **u8)
         self.out_meta_t = torch.zeros(batch, **i32)
@@ -110,11 +120,12 @@ class RssShardedDataPlane:
         self.rx_n = torch.zeros(1, **i32)
         self.n = 0
         self.k = 0
-        self.pending = None
+        self.pending: list = []             # slots whose counts are in flight, oldest first
         self.host_staged = self.gpu and dist.is_initialized() and dist.get_backend(group) == "gloo"
         self.comm = torch.cuda.Stream(self.dev) if self.gpu and not self.host_staged else None
         self.rx_stream = torch.cuda.Stream(self.dev) if self.comm is not None else None
-        self.hcnt = torch.zeros((2, world), dtype=torch.int32).pin_memory() if self.gpu else torch.zeros((2, world), dtype=torch.int32)
+        hc = torch.zeros((self.nslots, 2, world), dtype=torch.int32)
+        self.hcnt = hc.pin_memory() if self.gpu else hc
         self.stats = {"sent": 0, "received": 0, "steps": 0, "max_peer": 0}
 
     @staticmethod
@@ -173,23 +184,33 @@ class RssShardedDataPlane:
                 ops += [dist.P2POp(dist.irecv, a, j, self.group, 0), dist.P2POp(dist.irecv, m, j, self.group, 1)]
         return dist.batch_isend_irecv(ops) if ops else []
 
-    def exchange(self, s: _Slot):
-        """Counts first, then exactly the bytes each peer has (no fixed-capacity segments on the
-        wire, no overflow)."""
+    def _counts(self, s: _Slot) -> None:
+        """Enqueue the count all-to-all of a slot (comm stream, after its local step); the counts
+        land in pinned host memory without the host waiting for them."""
+        if self.comm is None:
+            return
+        w, cs = self.world, self.comm
+        hc = self.hcnt[s.idx]
+        with torch.cuda.stream(cs):
+            cs.wait_event(s.ev)
+            if s.used:
+                cs.wait_event(s.rev)          # the previous rx pass over s.recv is done
+            dist.all_to_all_single(s.rcnt, s.pcnt, group=self.group)
+            hc[0].copy_(s.pcnt, non_blocking=True)
+            hc[1].copy_(s.rcnt, non_blocking=True)
+            # the gather kernel reads each receive segment's count from its header
+            s.recv.view(w, self.pseg)[:, :4].view(torch.int32)[:, 0].copy_(s.rcnt)
+            s.hev.record(cs)
+
+    def _transfer(self, s: _Slot):
+        """The grouped send/recv of exactly the bytes each peer has (counts read on the host)."""
         w = self.world
         if self.comm is not None:
             cs = self.comm
+            s.hev.synchronize()                   # normally long done: the counts of `lag` steps ago
+            hc = self.hcnt[s.idx]
+            sc, rc = hc[0].numpy().copy(), hc[1].numpy().copy()
             with torch.cuda.stream(cs):
-                cs.wait_event(s.ev)
-                if s.used:
-                    cs.wait_event(s.rev)          # the previous rx pass over s.recv is done
-                dist.all_to_all_single(s.rcnt, s.pcnt, group=self.group)
-                self.hcnt[0].copy_(s.pcnt, non_blocking=True)
-                self.hcnt[1].copy_(s.rcnt, non_blocking=True)
-                # the gather kernel reads each receive segment's count from its header
-                s.recv.view(w, self.pseg)[:, :4].view(torch.int32)[:, 0].copy_(s.rcnt)
-                cs.synchronize()                  # host: counts (the GPU runs the next step's kernel meanwhile)
-                sc, rc = self.hcnt[0].numpy().copy(), self.hcnt[1].numpy().copy()
                 for wk in self._p2p(s.send, s.recv, sc, rc):
                     wk.wait()                     # makes the comm stream wait for the transfers
                 s.cev.record(cs)
@@ -207,10 +228,17 @@ class RssShardedDataPlane:
             if self.gpu:
                 s.recv.copy_(recv)
             s.rcnt.copy_(rcv)
+            self.hcnt[s.idx][1].copy_(rcv)
         self.stats["sent"] += int(sum(sc))
         self.stats["received"] += int(sum(rc))
         self.stats["max_peer"] = max(self.stats["max_peer"], int(max(sc)) if len(sc) else 0)
         return s
+
+    def exchange(self, s: _Slot):
+        """Counts first, then exactly the bytes each peer has (no fixed-capacity segments on the
+        wire, no overflow).  Standalone form (the exchange probe): waits for the counts now."""
+        self._counts(s)
+        return self._transfer(s)
 
     def _receive(self, s: _Slot) -> None:
         """Gather what peers sent (device-side count) and run the whole pipeline on it."""
@@ -220,7 +248,7 @@ class RssShardedDataPlane:
             rs = self.rx_stream
             if rs is not None:
                 rs.wait_event(s.cev)
-            total = int(self.hcnt[1].sum()) if self.comm is not None else int(s.rcnt.sum())
+            total = int(self.hcnt[s.idx][1].sum())
             if total > nr:                        # more than the receive buffers hold: grow them
                 self._grow_rx(total)
                 nr = int(self.rx_cap)
@@ -252,28 +280,30 @@ class RssShardedDataPlane:
         self.rx_lat = torch.zeros((n + 15) // 16, **i32)
 
     def step(self, pkts: torch.Tensor, inmeta: torch.Tensor) -> None:
-        """Process one ingress batch; the packets other GPUs sent for this GPU's flows in the
-        previous step are exchanged and processed here too (call flush() after the last step)."""
+        """Process one ingress batch; packets other GPUs sent for this GPU's flows `lag` steps ago
+        are exchanged and processed here too (call flush() after the last step)."""
         n = int(pkts.shape[0])
         if n > self.batch:
             raise ValueError("batch larger than the engine was sized for")
         if pkts.device != self.dev or inmeta.device != self.dev:
             raise ValueError("batch must live on the engine device")
-        s = self.slots[self.k & 1]
+        s = self.slots[self.k % self.nslots]
         if self.gpu:
             self.nf.launch_stamp(self._p(s.t0), self._stream())
         self.n = n
         self._local(s, pkts, inmeta, n)
-        self.flush()                # exchange + receive of the previous step, under this step's kernel
-        self.pending = s
+        # exchanges of earlier steps first (one order of collectives on every rank), then this
+        # step's counts; the host waits only for counts `lag` steps old
+        while len(self.pending) >= self.lag:
+            self._receive(self._transfer(self.pending.pop(0)))
+        self._counts(s)
+        self.pending.append(s)
         self.k += 1
         self.stats["steps"] += 1
 
     def flush(self) -> None:
-        if self.pending is not None:
-            s = self.pending
-            self.pending = None
-            self._receive(self.exchange(s))
+        while self.pending:
+            self._receive(self._transfer(self.pending.pop(0)))
 
     # ---------------------------------------------------------------- results
     def sync(self) -> None:

@@ -121,9 +121,15 @@ class Mi355xDetector(VendorDetector):
     def is_dpu_platform(self, platform):
         return bool(self.gpus(platform))
 
+    # The VSP runs the live data path: pods' vports (veth pairs by default, node config
+    # vport_kind) through the native I/O engine into the resident ring kernel of every MI355X of
+    # the node (flows sharded by RSS owner).  The reference's detector likewise deploys its VSP
+    # with the arguments its data plane needs (internal/platform/ipu.go:76-92).
+    VSP_ARGS = ["--vendor", "amd-gpu", "--live", "--live-engine", "native", "--gpus", "all"]
+
     def vsp(self, dpu_mode, identifier=""):
         return VspSpec(self.vendor, I.VSP_IMAGE_AMD_GPU, ["python3", "-m", "dpu_operator_amd.cmd.vsp"],
-                       ["--vendor", "amd-gpu"], True, identifier, colocated=True)
+                       list(self.VSP_ARGS), True, identifier, colocated=True)
 
 
 class DpuDetectorManager:

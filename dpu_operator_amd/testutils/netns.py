@@ -146,3 +146,76 @@ class WireNF:
         self._stop.set()
         self._t.join(5)
         delete_netns(self.ns)
+
+
+class RawPod:
+    """A pod namespace holding one interface (moved in, up, no addresses, IPv6 off so the kernel
+    sends nothing of its own) and an AF_PACKET socket bound to it, opened inside the namespace:
+    `send` puts whole Ethernet frames on the wire exactly as given, `recv` returns what arrived
+    (the pod's own transmissions filtered out)."""
+
+    ETH_P_ALL = 0x0003
+
+    def __init__(self, ns_name: str, ifname: str, nl: RtNetlink | None = None, existing_ns: str | None = None):
+        self.nl = nl or RtNetlink()
+        self.ns = existing_ns or create_netns(f"/var/run/netns/{ns_name}")
+        self.own_ns = existing_ns is None
+        self.ifname = ifname
+        if existing_ns is None:
+            self.nl.link_set_ns(ifname, self.ns)
+
+        def setup():
+            for p in (f"/proc/sys/net/ipv6/conf/{ifname}/disable_ipv6", "/proc/sys/net/ipv6/conf/all/disable_ipv6"):
+                try:
+                    with open(p, "w") as f:
+                        f.write("1")
+                except OSError:
+                    pass
+            s = socket.socket(socket.AF_PACKET, socket.SOCK_RAW, socket.htons(self.ETH_P_ALL))
+            s.bind((ifname, 0))
+            s.setblocking(False)
+            s.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 1 << 22)
+            s.setsockopt(self.SOL_PACKET, self.PACKET_AUXDATA, 1)   # 802.1Q tags the kernel strips
+            return s
+
+        self.nl.link_set_up(ifname, self.ns)
+        self.sock = in_netns(self.ns, setup)
+
+    def send(self, frames: list[bytes]) -> int:
+        n = 0
+        for f in frames:
+            for _ in range(200):
+                try:
+                    self.sock.send(f)
+                    n += 1
+                    break
+                except BlockingIOError:
+                    time.sleep(0.0005)
+        return n
+
+    SOL_PACKET, PACKET_AUXDATA = 263, 8
+    TP_STATUS_VLAN_VALID, TP_STATUS_VLAN_TPID_VALID = 1 << 4, 1 << 6
+
+    def recv(self) -> list[bytes]:
+        """Frames as they were on the wire: a VLAN tag the kernel moved to the aux data (VLAN
+        offload) goes back in front of the ethertype."""
+        out = []
+        while True:
+            try:
+                data, anc, _flags, addr = self.sock.recvmsg(65535, socket.CMSG_SPACE(20))
+            except BlockingIOError:
+                return out
+            if addr[2] == socket.PACKET_OUTGOING:
+                continue
+            for lvl, typ, cd in anc:
+                if lvl == self.SOL_PACKET and typ == self.PACKET_AUXDATA and len(cd) >= 20:
+                    st, _l, _sl, _mac, _net, tci, tpid = struct.unpack_from("=IIIHHHH", cd)
+                    if st & self.TP_STATUS_VLAN_VALID and (tci or st & self.TP_STATUS_VLAN_TPID_VALID):
+                        tpid = tpid if st & self.TP_STATUS_VLAN_TPID_VALID and tpid else 0x8100
+                        data = data[:12] + struct.pack("!HH", tpid, tci) + data[12:]
+            out.append(data)
+
+    def close(self) -> None:
+        self.sock.close()
+        if self.own_ns:
+            delete_netns(self.ns)

@@ -56,6 +56,16 @@ class PathManager:
     def mailbox_path(self) -> str:
         return self.wrap("/var/run/dpu-daemon/ctrl-mbox")
 
+    def memif_dir(self) -> str:
+        """Shared-memory vport regions (<vport name>.memif): created by the GPU VSP, mounted into
+        the pod that was allocated the vport by the device plugin."""
+        return self.wrap("/var/run/dpu-daemon/memif")
+
+    @staticmethod
+    def memif_container_path(device_id: str) -> str:
+        """Where a pod finds the region of its vport (the device plugin's mount target)."""
+        return f"/var/run/dpu/memif/{device_id}.memif"
+
     def cni_host_dir(self, flavour: Flavour, fs_mode: FilesystemMode) -> str:
         if flavour == Flavour.MICROSHIFT and fs_mode == FilesystemMode.IMAGE:
             return self.wrap("/run/cni")

@@ -21,10 +21,16 @@ Without an NF, VFs and the wire form one L2 bridge: known pod MACs are forwarded
 broadcast / unknown unicast is flooded (wire first, then the other VFs), like OvS NORMAL on the
 reference's br-mrv0.
 
-Live mode (`live=True`, `vsp --live`): every vport is a real TAP netdev (dataplane/netio.py)
-whose fd the VSP keeps; the CNI moves it into the pod / NF namespace and dataplane/netio.py's
-LivePath moves the frames between those fds and the pipeline (GPU kernel or oracle), so pods
-exchange real traffic through the data plane.  A live vport is the pod-facing side of the VF, where
+Live mode (`live=True`, `vsp --live`, what the MI355X detector deploys): pod traffic flows
+through the data plane.  Vport kinds:
+  * veth (default): a veth pair per vport; the pod end (`dpuvpN`, the device ID the device plugin
+    hands out) is moved into the pod by the CNI (networkfn.cmd_add), the data-plane end (`dpuvpNd`)
+    is read / written by the native I/O engine through AF_PACKET TPACKET_V2 rings;
+  * memif: a shared-memory region per vport (<PathManager.memif_dir>/dpuvpN.memif) that the device
+    plugin mounts into the pod (a DPDK-memif-style application attaches to it, no syscalls);
+  * tap: a TAP netdev whose fd the VSP keeps (the CNI moves the netdev; one syscall per frame).
+The native engine (dataplane/native_io.py, `live_engine="native"`) moves the frames between the
+vports and every GPU's resident ring kernel; "batch" / "ring" are the Python LivePath loops.  A live vport is the pod-facing side of the VF, where
 the port VLAN is already stripped: VF ports are then programmed without VLAN isolation / egress
 tagging (spoof-check stays).
 
@@ -98,7 +104,7 @@ class GpuVsp(VspBase):
                  opi_port: int = 0, flow_buckets: int = 1 << 16, vport_prefix: str = "dpuvp",
                  hash_mode: str = "mfma", acl_mode: str = "mfma", state_dir: str | None = None,
                  live: bool = False, uplink=None, live_engine: str = "batch", gpus=1, vport_kind: str = "tap",
-                 memif_dir: str | None = None, tx_workers: int = 4):
+                 memif_dir: str | None = None, tx_workers: int = 1, io_queues: int = 1):
         super().__init__(path_manager)
         if device is None:
             try:
@@ -115,11 +121,12 @@ class GpuVsp(VspBase):
         if gpus == "all":
             gpus = len(visible_devices()) if device != "cpu" else 1
         self.gpus = max(1, int(gpus))
-        if vport_kind not in ("tap", "memif"):
-            raise ValueError("vport_kind is 'tap' (netdev) or 'memif' (shared-memory vport)")
+        if vport_kind not in ("tap", "veth", "memif"):
+            raise ValueError("vport_kind is 'tap' / 'veth' (netdevs) or 'memif' (shared-memory vport)")
         self.vport_kind = vport_kind
-        self.memif_dir = memif_dir
+        self.memif_dir = memif_dir or (self.pm.memif_dir() if self.pm is not None else None)
         self.tx_workers = int(tx_workers)
+        self.io_queues = int(io_queues)
         self.nl = nl or FakeNetlink()
         self.opi_port = opi_port
         self.flow_buckets = flow_buckets
@@ -137,8 +144,8 @@ class GpuVsp(VspBase):
         self.live = live
         if live_engine not in ("batch", "ring", "native"):
             raise ValueError("live_engine is 'batch', 'ring' or 'native'")
-        if (self.gpus > 1 or vport_kind == "memif") and live:
-            live_engine = "native"                  # the C++ engine: RSS steering / shared-memory vports
+        if (self.gpus > 1 or vport_kind in ("memif", "veth")) and live:
+            live_engine = "native"                  # the C++ engine: RSS steering / memif / AF_PACKET vports
         self.live_engine = live_engine              # "batch" (fused kernel per cycle), "ring" (resident
                                                     # kernel) or "native" (C++ I/O engine, iox.cpp)
         self.taps: dict[int, object] = {}       # live mode: port -> TapPort
@@ -296,7 +303,8 @@ class GpuVsp(VspBase):
                 from ..dataplane.native_io import NativeLivePath
 
                 planes = self.dp.planes if hasattr(self.dp, "planes") else [self.dp]
-                self.livepath = NativeLivePath(planes, ports, tx_workers=self.tx_workers).start()
+                self.livepath = NativeLivePath(planes, ports, tx_workers=self.tx_workers,
+                                               queues=self.io_queues).start()
             else:
                 from ..dataplane.netio import LivePath
 
@@ -316,7 +324,16 @@ class GpuVsp(VspBase):
             if self.live and self.vport_kind == "memif":
                 from ..dataplane.native_io import MemifVport, memif_dir
 
-                vp = MemifVport(os.path.join(self.memif_dir or memif_dir(), f"{name}.memif"))
+                d = self.memif_dir or memif_dir()
+                os.makedirs(d, exist_ok=True)
+                vp = MemifVport(os.path.join(d, f"{name}.memif"))
+                self.taps[i] = vp
+                if self.livepath is not None:
+                    self.livepath.add_port(i, vp)
+            elif self.live and self.vport_kind == "veth":
+                from ..dataplane.native_io import PacketVport
+
+                vp = PacketVport.create_veth(self.nl, name, mac)
                 self.taps[i] = vp
                 if self.livepath is not None:
                     self.livepath.add_port(i, vp)
@@ -356,7 +373,7 @@ class GpuVsp(VspBase):
 
     def vport_path(self, idx: int) -> str | None:
         """Shared-memory vports: the region a pod attaches to (mounted into the pod by the device
-        plugin / CNI the way vhost-user and memif sockets are)."""
+        plugin, DevicePluginServer.Allocate, the way vhost-user and memif sockets are)."""
         v = self.taps.get(idx)
         return getattr(v, "path", None) if self.vport_kind == "memif" else None
 

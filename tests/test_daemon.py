@@ -9,6 +9,7 @@ packet from the workload VF is steered into the NF.
 """
 from __future__ import annotations
 
+import os
 import shutil
 import tempfile
 import threading
@@ -309,3 +310,36 @@ def test_colocated_gpu_node_end_to_end(pm, device):
         t.join(10)
         kubelet.stop()
         gvsp.stop()
+
+
+def test_device_plugin_mounts_memif_vports_into_the_pod(pm):
+    """GPU VSP with shared-memory vports: Allocate hands the pod its region (a bind mount of
+    <memif_dir>/<vport>.memif at PathManager.memif_container_path, listed in NF-MEMIF), like the
+    memif / vhost-user device plugins; the region the pod gets is the one the engine serves."""
+    from dpu_operator_amd.native import nfdp
+    from dpu_operator_amd.vsp.gpu import GpuVsp
+
+    touch(pm.wrap("/dpu-cni"))
+    api = ApiServer()
+    kubelet = FakeKubelet(pm, api).start()
+    gvsp = GpuVsp(path_manager=pm, device="cpu", nl=FakeNetlink(), flow_buckets=1 << 8, live=True,
+                  vport_kind="memif")
+    assert gvsp.memif_dir == pm.memif_dir() and gvsp.live_engine == "native"
+    gvsp.start()
+    plat = FakePlatform("AMD server", [PciDevice("0000:05:00.0", "1002", "75a3", class_code=0x120000)])
+    d = Daemon(plat, "auto", api, None, pm, nl=FakeNetlink(), tick=0.05, manager_kw={"dp_poll": 0.05})
+    t = threading.Thread(target=d.serve, daemon=True)
+    t.start()
+    try:
+        assert wait_until(lambda: kubelet.allocatable() == 8, 10), kubelet.devices
+        resp = kubelet.allocate(["dpuvp2", "dpuvp3"])
+        cr = resp.container_responses[0]
+        assert cr.envs["NF-DEV"] == "dpuvp2,dpuvp3,"
+        mounts = {m.container_path: m.host_path for m in cr.mounts}
+        assert mounts == {pm.memif_container_path(f"dpuvp{i}"): f"{pm.memif_dir()}/dpuvp{i}.memif" for i in (2, 3)}
+        assert cr.envs["NF-MEMIF"].split(",") == [pm.memif_container_path("dpuvp2"), pm.memif_container_path("dpuvp3")]
+        assert all(os.path.exists(h) for h in mounts.values())
+        nfdp().MemifEndpoint(mounts[pm.memif_container_path("dpuvp2")])   # a valid region the pod can attach to
+    finally:
+        kubelet.stop()
+        gvsp.stop_live()

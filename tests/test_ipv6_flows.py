@@ -181,6 +181,11 @@ def test_ipv6_flow_collision_is_refused():
     dp.add_flow6("2001:db8:a::1", "2001:db8:f::1", 5, 6, 17)
     with pytest.raises(ValueError):
         dp.add_flow6(_colliding_addr("2001:db8:a::1"), "2001:db8:f::1", 5, 6, 17)
+    # removing the never-installed colliding 5-tuple leaves the installed flow alone
+    assert not dp.remove_flow6(_colliding_addr("2001:db8:a::1"), "2001:db8:f::1", 5, 6, 17)
+    assert len(dp.flows) == 1 and len(dp.flows6) == 1
+    assert dp.remove_flow6("2001:db8:a::1", "2001:db8:f::1", 5, 6, 17)
+    assert len(dp.flows) == 0 and not dp.flows6
 
 
 @pytest.mark.gpu

@@ -67,4 +67,8 @@ def test_bench_rss_two_gpus():
     r = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stderr[-2000:]
     line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
-    assert line["n_gpus"] == 2 and line["forwarded_fraction"] == 1.0 and line["exchange"]["a2a_per_step"] == 1
+    import bench
+
+    assert line["n_gpus"] == 2 and line["forwarded_fraction"] == 1.0
+    assert line["exchange"]["a2a_per_step"] == bench.RSS_A2A_PER_STEP
+    assert set(line["exchange"]) == set(bench.RSS_EXCHANGE_KEYS)

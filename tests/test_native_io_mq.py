@@ -1,0 +1,296 @@
+"""Multi-queue native I/O engine (csrc/nfdp/iox.{h,cpp}): several rx threads each owning a group of
+ports and a ring queue on every backend, the per-burst CPU side pass (tunnel outer headers, flood
+replicas, learning) with no ring drain, copy-on-write configuration (tunnel redirects replaced as a
+whole), byte-table Toeplitz steering, and a memif peer that corrupts the shared region header.
+
+Everything runs on the C++ oracle backends here; the GPU twins (ring kernel queues) are marked gpu.
+Expected frames come from the batch path of an identical data plane (`DataPlane.run` + its side
+results), assembled by ops/packets.assemble."""
+import shutil
+import struct
+import tempfile
+import time
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from dpu_operator_amd.dataplane import scenario as S
+from dpu_operator_amd.dataplane import tables as T
+from dpu_operator_amd.dataplane.engine import DataPlane
+from dpu_operator_amd.dataplane.multi import MultiDataPlane
+from dpu_operator_amd.dataplane.native_io import MemifVport, NativeLivePath, memif_dir
+from dpu_operator_amd.native import nfdp
+from dpu_operator_amd.ops import packets as P
+
+
+@pytest.fixture
+def shm():
+    d = Path(tempfile.mkdtemp(prefix="dpu-iomq-", dir=memif_dir()))
+    yield d
+    shutil.rmtree(d, ignore_errors=True)
+
+
+def _until(fn, t=8.0):
+    end = time.monotonic() + t
+    while time.monotonic() < end:
+        v = fn()
+        if v:
+            return v
+        time.sleep(0.002)
+    return fn()
+
+
+def _sfc(device="cpu", n_pods=6, n_flows=4096, egress=False):
+    dp = DataPlane(device=device, flow_buckets=1 << 12)
+    sc = S.build_sfc(dp, n_pods=n_pods, n_flows=n_flows, n_acl=64, seed=0)
+    extra = S.install_vxlan_egress(dp, sc) if egress else None
+    dp.commit(full=True)
+    return dp, sc, extra
+
+
+def _expected(ref, slots, im):
+    """Batch-path egress frames by destination port (outer headers from its side pass)."""
+    r = ref.run(slots, im)
+    side = ref.side_result() if ref.side_active() else None
+    port, _, reason = P.meta_fields(r.meta)
+    lens = im >> 16
+    exp: dict[int, list[bytes]] = {}
+    for i in np.nonzero(reason == 0)[0]:
+        x = side["xhdr"][i] if (side is not None and side["xhdr"] is not None and P.meta_xhdr(r.meta[i:i + 1])[0]) else None
+        exp.setdefault(int(port[i]), []).append(P.assemble(r.out[i], int(r.meta[i]), slots[i], int(lens[i]), x))
+    return exp, int((reason != 0).sum())
+
+
+def _send_all(nf, paths, slots, im, src_ports):
+    eps = {p: nf.MemifEndpoint(paths[p]) for p in paths}
+    src = im & 0xFFFF
+    for p in src_ports:
+        fr = [bytes(slots[k, : int(im[k] >> 16)]) for k in np.nonzero(src == p)[0]]
+        sent = 0
+        t_end = time.monotonic() + 10
+        while sent < len(fr) and time.monotonic() < t_end:
+            sent += eps[p].send(fr[sent:])
+    return eps
+
+
+def _collect(eps, want):
+    got: dict[int, list[bytes]] = {p: [] for p in eps}
+
+    def done():
+        for p, e in eps.items():
+            got[p] += e.recv()
+        return sum(map(len, got.values())) >= want
+
+    return got, done
+
+
+@pytest.mark.parametrize("queues,workers", [(3, 1), (2, 2)])
+def test_multiqueue_bit_exact(shm, queues, workers):
+    """Ports spread over `queues` rx threads (least loaded first), each with its own ring queue:
+    every frame comes out as the batch path makes it, counters equal."""
+    nf = nfdp()
+    dp, sc, _ = _sfc()
+    ref, _, _ = _sfc()
+    slots, im = S.traffic(sc, 3000, seed=3)
+    exp, drops = _expected(ref, slots, im)
+    paths = {int(p): str(shm / f"q{int(p)}") for p in sc.pod_port}
+    live = NativeLivePath(dp, {p: MemifVport(paths[p], ring_size=4096) for p in paths}, burst=128,
+                          ring_capacity=1024, queues=queues, tx_workers=workers).start()
+    try:
+        qs = [live.port_queue(p) for p in paths]
+        assert sorted(set(qs)) == list(range(queues))            # every queue owns ports
+        assert max(qs.count(q) for q in range(queues)) - min(qs.count(q) for q in range(queues)) <= 1
+        eps = _send_all(nf, paths, slots, im, list(paths))
+        got, done = _collect(eps, sum(map(len, exp.values())))
+        assert _until(done), (live.stats, live.error)
+        for port, frames in exp.items():
+            assert sorted(got[port]) == sorted(frames), port
+        st = live.stats
+        assert st["rx"] == len(slots) and st["tx"] == len(slots) - drops and live.error is None
+        assert st["queues"] == queues
+        assert np.array_equal(dp.port_counters(), ref.port_counters())
+        dp.harvest(); ref.harvest()
+        assert np.array_equal(dp.flow_totals, ref.flow_totals)
+        # per-port rx counters (one burst tally per rx call) match what each pod sent
+        src = im & 0xFFFF
+        for p in paths:
+            assert live.port(p).counters()["rx"] == int((src == p).sum())
+    finally:
+        live.stop()
+
+
+def test_toeplitz_tables_match_the_bitwise_hash():
+    """The engine steers with byte-table Toeplitz (iox ToeplitzTab); owners equal the bit-serial
+    frame_owner on IPv4 and (folded) IPv6 frames, for 3 backends."""
+    nf = nfdp()
+    m = MultiDataPlane(["cpu"] * 3, flow_buckets=1 << 12)
+    sc = S.build_sfc(m, n_pods=4, n_flows=2000, n_acl=8, seed=1)
+    m.commit(full=True)
+    pk, im = S.traffic(sc, 400, seed=9)
+    f6, l6 = P.craft6_full(64, dmac=S.GW_MAC, smac="02:00:00:00:66:01", src6="2001:db8::1", dst6="2001:db8::2",
+                           sport=np.arange(64) + 100, dport=53)
+    slots6 = P.header_slots(f6, l6)
+    im6 = P.inmeta(np.full(64, int(sc.pod_port[0])), l6)
+    for v6 in (False, True):
+        eng = nf.IoEngine(64, 8, 1)
+        for _ in range(3):
+            eng.add_backend(nf.OracleBackend(256))
+        eng.set_steering(np.ascontiguousarray(m.ports.a), bytes(m.flows.rss_key), v6)
+        for s, i in ((pk, im), (slots6, im6)):
+            ref = nf.owner_of_frames(np.ascontiguousarray(s), np.ascontiguousarray(i, np.uint32),
+                                     np.ascontiguousarray(m.ports.a), bytes(m.flows.rss_key), 3, v6)
+            got = [eng.owner_of_frame(bytes(s[k][: int(i[k] >> 16)]), int(i[k] & 0xFFFF)) for k in range(len(s))]
+            assert got == list(ref)
+    own = m.owners(pk, im)
+    assert len(np.unique(own)) == 3
+
+
+def test_vxlan_egress_side_pass_per_burst_and_redirect_cleared(shm):
+    """Every pod VF a VXLAN tunnel port: the tx leader builds each packet's outer header on the CPU
+    (pipeline.h side_stage with table Toeplitz) and the frame leaves on the underlay port, byte for
+    byte as the batch path's side kernel makes it, without any ring drain.  Then the ports stop
+    being tunnels: the redirect map is replaced as a whole and frames go straight to the pods."""
+    nf = nfdp()
+    dp, sc, eg = _sfc(egress=True)
+    ref, _, _ = _sfc(egress=True)
+    slots, im = S.traffic(sc, 1500, seed=5)
+    exp, drops = _expected(ref, slots, im)
+    und = eg["underlay"]
+    # the meta names the tunnel port (the destination pod's VF); the frame leaves on its underlay
+    assert und not in exp
+    exp = {und: [f for v in exp.values() for f in v]}
+    paths = {int(p): str(shm / f"x{int(p)}") for p in list(sc.pod_port) + [und]}
+    live = NativeLivePath(dp, {p: MemifVport(paths[p], ring_size=4096) for p in paths}, burst=256,
+                          ring_capacity=2048, queues=2).start()
+    try:
+        eps = _send_all(nf, paths, slots, im, [int(p) for p in sc.pod_port])
+        got, done = _collect(eps, sum(map(len, exp.values())))
+        assert _until(done), (live.stats, live.error)
+        assert sorted(got[und]) == sorted(exp[und])
+        assert live.stats["side_passes"] >= 1 and live.error is None
+        # tunnels off (the slots stay set in the tunnel table): plain delivery to the pods
+        for p in sc.pod_port:
+            dp.ports.a[int(p)]["flags"] &= ~np.uint32(T.PORT_TUNNEL)
+        dp.ports.version += 1
+        dp.commit()
+        for p in sc.pod_port:
+            ref.ports.a[int(p)]["flags"] &= ~np.uint32(T.PORT_TUNNEL)
+        ref.ports.version += 1
+        ref.commit()
+        slots2, im2 = S.traffic(sc, 800, seed=6)
+        exp2, _ = _expected(ref, slots2, im2)
+        assert und not in exp2
+        for e in eps.values():
+            e.recv()
+        eps2 = _send_all(nf, paths, slots2, im2, [int(p) for p in sc.pod_port])
+        got2, done2 = _collect(eps2, sum(map(len, exp2.values())))
+        assert _until(done2), (live.stats, live.error)
+        for port, frames in exp2.items():
+            assert sorted(got2[port]) == sorted(frames), port
+        assert got2[und] == []
+    finally:
+        live.stop()
+
+
+def test_multi_plane_native_matches_one_plane(shm):
+    """Two oracle planes behind one engine with two queues (RSS owner steering in each rx thread):
+    the frames and summed counters equal a single plane's."""
+    nf = nfdp()
+    m = MultiDataPlane(["cpu", "cpu"], flow_buckets=1 << 12)
+    sc = S.build_sfc(m, n_pods=6, n_flows=4096, n_acl=64, seed=0)
+    m.commit(full=True)
+    ref, _, _ = _sfc()
+    slots, im = S.traffic(sc, 3000, seed=7)
+    exp, drops = _expected(ref, slots, im)
+    paths = {int(p): str(shm / f"m{int(p)}") for p in sc.pod_port}
+    live = NativeLivePath(m, {p: MemifVport(paths[p], ring_size=4096) for p in paths}, burst=128,
+                          ring_capacity=1024, queues=2).start()
+    try:
+        assert len(live.dps) == 2
+        eps = _send_all(nf, paths, slots, im, list(paths))
+        got, done = _collect(eps, sum(map(len, exp.values())))
+        assert _until(done), (live.stats, live.error)
+        for port, frames in exp.items():
+            assert sorted(got[port]) == sorted(frames), port
+        assert all(int(p.port_counters()[:, 0].sum()) > 0 for p in m.planes)   # both planes worked
+        assert np.array_equal(m.port_counters(), ref.port_counters())
+        # a commit of the multi-plane data plane pauses the engine once and keeps forwarding
+        m.ports.set_mtu(int(sc.pod_port[0]), 1400)
+        ref.ports.set_mtu(int(sc.pod_port[0]), 1400)
+        m.commit()
+        ref.commit()
+        slots2, im2 = S.traffic(sc, 500, seed=8)
+        exp2, _ = _expected(ref, slots2, im2)
+        eps2 = _send_all(nf, paths, slots2, im2, list(paths))
+        got2, done2 = _collect(eps2, sum(map(len, exp2.values())))
+        assert _until(done2), (live.stats, live.error)
+        for port, frames in exp2.items():
+            assert sorted(got2[port]) == sorted(frames), port
+    finally:
+        live.stop()
+
+
+def test_learning_reaches_every_plane(shm):
+    """MAC learning from the per-burst side pass goes through the learner thread into EVERY plane's
+    MAC table (one learning bridge per node), not only the plane that saw the frame."""
+    nf = nfdp()
+    m = MultiDataPlane(["cpu", "cpu"], flow_buckets=1 << 10, mac_slots=1 << 10)
+    for p in range(4):
+        m.ports.set(p, flags=T.PORT_VALID | T.PORT_LEARN, bridge_id=7)
+    m.flood.set_members(7, [0, 1, 2, 3])
+    m.commit(full=True)
+    paths = {p: str(shm / f"l{p}") for p in range(4)}
+    live = NativeLivePath(m, {p: MemifVport(paths[p]) for p in paths}, queues=2).start()
+    try:
+        eps = {p: nf.MemifEndpoint(paths[p]) for p in paths}
+        macs = [f"02:00:00:00:1c:{k:02x}" for k in range(16)]
+        frames = []
+        for k, mac in enumerate(macs):
+            fr, ln = P.craft(1, dmac="ff:ff:ff:ff:ff:ff", smac=mac, src_ip=0x0A000001 + k, dst_ip=0x0A0000FE,
+                             sport=1000 + k, dport=80)
+            frames.append(bytes(fr[0, : ln[0]]))
+        assert eps[2].send(frames) == len(frames)
+        got = {p: [] for p in (0, 1, 3)}
+        assert _until(lambda: [got[p].extend(eps[p].recv()) for p in got] and all(len(got[p]) >= 16 for p in got))
+        live.flush_learning()
+        for plane in m.planes:
+            tab = plane._dev["macs"].view(T.MAC_DTYPE)
+            learned = {(int(e["mac_lo"]), int(e["mac_hi"])) for e in tab if int(e["valid"]) == 3}
+            for mac in macs:
+                lo, hi = T.mac_raw(mac)
+                assert (int(lo), int(hi)) in learned, mac
+        assert live.stats["learn_events"] >= 16 and live.stats["learn_applied"] >= 16
+    finally:
+        live.stop()
+
+
+def test_memif_peer_corrupting_the_header_cannot_reach_outside_the_region(shm):
+    """The engine snapshots the region geometry when it creates it: a pod that rewrites ring_size /
+    buf_size / its head index in the shared header while traffic flows garbles at most its own
+    frames; the engine keeps running and the other pods keep talking."""
+    nf = nfdp()
+    dp, sc, _ = _sfc(n_pods=4)
+    paths = {int(p): str(shm / f"c{int(p)}") for p in sc.pod_port}
+    live = NativeLivePath(dp, {p: MemifVport(paths[p], ring_size=256) for p in paths}, ring_capacity=1024).start()
+    try:
+        bad = int(sc.pod_port[0])
+        with open(paths[bad], "r+b") as f:
+            f.seek(12)
+            f.write(struct.pack("<II", 1 << 30, 1 << 16))   # ring_size, buf_size
+            f.seek(64)
+            f.write(struct.pack("<I", 0x7FFFFFF0))          # ring 0 head: a bogus producer index
+        time.sleep(0.2)
+        assert live.error is None and live.healthy
+        good = [int(p) for p in sc.pod_port[1:]]
+        slots, im = S.traffic(sc, 600, seed=11, src_pods=np.arange(1, len(sc.pod_port)))
+        eps = {p: nf.MemifEndpoint(paths[p]) for p in good}
+        src = im & 0xFFFF
+        for p in good:
+            fr = [bytes(slots[k, : int(im[k] >> 16)]) for k in np.nonzero(src == p)[0]]
+            assert eps[p].send(fr) == len(fr)
+        n = [0]
+        assert _until(lambda: n.__setitem__(0, n[0] + sum(len(e.recv()) for e in eps.values())) or n[0] > 0)
+        assert live.error is None
+    finally:
+        live.stop()

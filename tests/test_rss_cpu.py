@@ -21,7 +21,7 @@ def _free_port() -> int:
     return p
 
 
-def _worker(rank, world, port, q, steps, frac):
+def _worker(rank, world, port, q, steps, frac, flush_each=True):
     import sys
 
     import torch
@@ -57,6 +57,8 @@ def _worker(rank, world, port, q, steps, frac):
             n_remote += int((~loc).sum())
             ok &= bool(np.array_equal(meta[loc], rr.meta[loc]))
             ok &= bool(np.array_equal(eng.outputs()[loc], rr.out[loc]))
+            if not flush_each:
+                continue      # pipelined: exchanges complete `lag` steps later (checked by the totals below)
             # what this rank sent must come out of the owners as the oracle says
             sent = {pk[i].tobytes(): (rr.out[i].tobytes(), int(rr.meta[i])) for i in np.where(~loc)[0]}
             objs = [None] * world
@@ -71,6 +73,10 @@ def _worker(rank, world, port, q, steps, frac):
                 e = expect.get(a.tobytes())
                 ok &= e is not None and e == (b.tobytes(), int(m))
         ok &= "overflow" not in dp.drop_counters()          # nothing dropped for lack of room
+        if not flush_each:
+            eng.flush()
+            n_rx = eng.stats["received"]
+            ok &= eng.stats["sent"] == n_remote
         q.put((rank, ok, n_remote, n_rx))
     except Exception as ex:  # report instead of hanging the parent
         q.put((rank, False, repr(ex), 0))
@@ -94,3 +100,34 @@ def test_rss_gloo(world, frac):
         p.join(timeout=60)
     assert all(ok for _, ok, _, _ in res), res
     assert sum(r[2] for r in res) == sum(r[3] for r in res) > 0  # every misdirected packet processed once
+
+
+def test_rss_gloo_pipelined_lagged_exchange():
+    """Six steps with no flush in between: each step's exchange completes `lag` (2) steps later
+    (the host never waits for fresh counts); every misdirected packet still reaches its owner."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    world = 3
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, 6, 0.1, False)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    assert all(ok for _, ok, _, _ in res), res
+    assert sum(r[2] for r in res) == sum(r[3] for r in res) > 0
+
+
+def test_bench_exchange_block_matches_the_protocol():
+    """bench.py's `exchange` block (what the driver's multi-GPU runs print) carries the protocol
+    facts tests/test_multigpu.py asserts: two collective launches per step, every key present."""
+    import sys
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+
+    info = bench.rss_exchange_info(0.002, 4096.0, 700, 0.01, 2)
+    assert set(info) == set(bench.RSS_EXCHANGE_KEYS)
+    assert info["a2a_per_step"] == bench.RSS_A2A_PER_STEP == 2
+    assert info["xgmi_bytes_out_per_gpu_per_step"] == 4096 * 68 and info["host_lag_steps"] == 2

@@ -32,32 +32,37 @@ def _engine():
 
 
 def _fake_exchange(eng, serial):
+    """Loopback exchange on the engine's streams ("peers sent" what this rank sent them): counts
+    enqueued at the step, transfer completed `lag` steps later, as the real protocol does."""
     import torch
 
-    def exchange(s):
+    def counts(s):
         cs = eng.comm
         with torch.cuda.stream(cs):
             cs.wait_event(s.ev)
             if s.used:
                 cs.wait_event(s.rev)
             s.rcnt.copy_(s.pcnt)
-            s.recv.copy_(s.send)                 # "peers sent" what this rank sent them
+            s.recv.copy_(s.send)
             s.recv.view(eng.world, eng.pseg)[:, :4].view(torch.int32)[:, 0].copy_(s.rcnt)
-            eng.hcnt[1].copy_(s.rcnt, non_blocking=True)
-            cs.synchronize()
-            eng.stats["received"] += int(eng.hcnt[1].sum())
-            s.cev.record(cs)
+            eng.hcnt[s.idx][1].copy_(s.rcnt, non_blocking=True)
+            s.hev.record(cs)
+
+    def transfer(s):
+        s.hev.synchronize()
+        eng.stats["received"] += int(eng.hcnt[s.idx][1].sum())
+        s.cev.record(eng.comm)
         if serial:
             torch.cuda.synchronize()
         return s
-    return exchange
+    return counts, transfer
 
 
 def _run(serial):
     import torch
 
     eng, batches = _engine()
-    eng.exchange = _fake_exchange(eng, serial)
+    eng._counts, eng._transfer = _fake_exchange(eng, serial)
     for k in range(8):
         eng.step(*batches[k % 4])
         if serial:
