@@ -1,4 +1,6 @@
-// iox.cpp — native packet I/O engine (see iox.h).
+// iox.cpp — native packet I/O engine (see iox.h).  Host code only: the GPU backend (the one part
+// that calls HIP) is iox_gpu.cpp, so the engine, its ports and the oracle backend also build as
+// plain C++ under ThreadSanitizer / AddressSanitizer (iox_stress.cpp, native/build.py).
 #include "iox.h"
 
 #include <arpa/inet.h>
@@ -25,9 +27,6 @@ inline uint32_t pow2_at_least(uint32_t x) {
   uint32_t p = 1;
   while (p < x) p <<= 1;
   return p;
-}
-void hck(hipError_t e, const char* what) {
-  if (e != hipSuccess) throw std::runtime_error(std::string("iox: ") + what + ": " + hipGetErrorString(e));
 }
 // outer-header bytes of a side-pass record (IPv6 underlay: 70, IPv4: 50; ethertype at 12..13)
 inline uint32_t xhdr_len(const uint8_t* rec) { return (rec[12] == 0x86 && rec[13] == 0xDD) ? kEncap6Bytes : kEncapBytes; }
@@ -346,42 +345,6 @@ SideTables::SideTables(const Src& s) {
   t_.flow6_on = s.v6 ? 1u : 0u;   // the key fold only (make_key): the side pass never probes flows
 }
 
-// ---------------------------------------------------------------------------------- GpuBackend
-GpuBackend::GpuBackend(RingEngine* ring) : ring_(ring), cap_(ring->capacity()) {
-  if (!ring->host_slots()) throw std::invalid_argument("iox: the ring needs host_slots=True");
-  in_ = static_cast<uint8_t*>(ring->host_ptr(0));
-  im_ = static_cast<uint32_t*>(ring->host_ptr(1));
-  out_ = static_cast<uint8_t*>(ring->host_ptr(2));
-  om_ = static_cast<uint32_t*>(ring->host_ptr(3));
-}
-
-GpuBackend::~GpuBackend() {
-  if (d_learn_) (void)hipFree(d_learn_);
-  if (learn_stream_) (void)hipStreamDestroy(learn_stream_);
-}
-
-void GpuBackend::thread_init() { hck(hipSetDevice(ring_->device()), "set device"); }
-
-void GpuBackend::apply_learn(const uint32_t* ev, uint32_t n, uint32_t stamp) {
-  if (!n) return;
-  thread_init();
-  if (!learn_stream_) hck(hipStreamCreateWithFlags(&learn_stream_, hipStreamNonBlocking), "learn stream");
-  const auto mt = ring_->mac_table();
-  if (!mt.first) return;
-  if (n > learn_cap_) {
-    if (d_learn_) hck(hipFree(d_learn_), "free");
-    learn_cap_ = pow2_at_least(std::max<uint32_t>(n, 1024));
-    hck(hipMalloc(reinterpret_cast<void**>(&d_learn_), ((size_t)learn_cap_ * 4 + 4) * 4), "learn buffer");
-  }
-  uint32_t* cnt = d_learn_ + (size_t)learn_cap_ * 4;
-  const uint32_t hdr[4] = {n, 0, 0, 0};
-  hck(hipMemcpyAsync(d_learn_, ev, (size_t)n * 16, hipMemcpyHostToDevice, learn_stream_), "learn events");
-  hck(hipMemcpyAsync(cnt, hdr, 16, hipMemcpyHostToDevice, learn_stream_), "learn count");
-  hck(launch_mac_learn(mt.first, mt.second, d_learn_, cnt, n, stamp, cnt + 1, learn_stream_), "learn kernel");
-  hck(hipStreamSynchronize(learn_stream_), "learn sync");
-  ring_->bump_epoch();   // chunks published from now on drop cached MAC-table lines first
-}
-
 // ---------------------------------------------------------------------------------- OracleBackend
 OracleBackend::OracleBackend(uint32_t capacity, uint32_t queues) : cap_(capacity), nq_(queues) {
   if (capacity < 64 || (capacity & (capacity - 1))) throw std::invalid_argument("iox: oracle capacity: power of two >= 64");
@@ -653,12 +616,14 @@ void Engine::stop() {
 }
 
 void Engine::pause() {
+  ctl_epoch_.fetch_add(1);
   pause_n_.fetch_add(1);
   if (!run_) return;
+  const uint64_t want = ctl_epoch_.load();
   const auto t0 = Clock::now();
   for (;;) {
     bool idle = true;
-    for (auto& Q : queues_) idle = idle && Q->held_epoch.load(std::memory_order_acquire) == ctl_epoch_.load();
+    for (auto& Q : queues_) idle = idle && Q->held_epoch.load(std::memory_order_acquire) >= want;
     idle = idle && lanes_idle();
     if (idle || !run_) return;
     if (Clock::now() - t0 > std::chrono::seconds(10)) throw std::runtime_error("iox: pause timed out");
@@ -823,10 +788,15 @@ void Engine::rx_loop(Queue* Q) {
   std::vector<RxRef> buf(burst_);
   uint32_t rr = 0;
   std::shared_ptr<const PortTab> cached;
-  std::vector<std::pair<uint32_t, Port*>> active;   // this queue's ports of the snapshot, in id order
+  std::vector<std::pair<uint32_t, Port*>> active;    // ports of this queue this thread owns and polls
+  std::vector<std::pair<uint32_t, Port*>> pending;   // ports of this queue another rx thread still holds
   const uint32_t nb = (uint32_t)backends_.size();
   const uint32_t q = Q->id;
   QStats& st = Q->st;
+  auto release_all = [&]() {
+    for (auto& a : active) a.second->rx_owner_.store(-1, std::memory_order_release);
+    active.clear();
+  };
   try {
     while (run_) {
       if (pause_n_.load(std::memory_order_acquire) || hold_n_.load(std::memory_order_acquire)) {
@@ -839,10 +809,32 @@ void Engine::rx_loop(Queue* Q) {
       }
       auto tab = std::atomic_load(&ports_);
       if (tab != cached) {
-        cached = tab;
-        active.clear();
+        std::vector<std::pair<uint32_t, Port*>> want;
         for (uint32_t i = 0; i < (uint32_t)tab->size(); ++i)
-          if ((*tab)[i].p && (*tab)[i].q == q) active.emplace_back(i, (*tab)[i].p.get());
+          if ((*tab)[i].p && (*tab)[i].q == q) want.emplace_back(i, (*tab)[i].p.get());
+        std::vector<std::pair<uint32_t, Port*>> keep;
+        for (auto& a : active) {
+          const bool still = std::any_of(want.begin(), want.end(), [&](const auto& w) { return w.second == a.second; });
+          if (still) keep.push_back(a);
+          else a.second->rx_owner_.store(-1, std::memory_order_release);   // moved away or removed: let go
+        }
+        active.swap(keep);
+        pending.clear();
+        for (auto& w : want)
+          if (std::none_of(active.begin(), active.end(), [&](const auto& a) { return a.second == w.second; }))
+            pending.push_back(w);
+        cached = tab;   // (after letting go: the old snapshot may hold the last reference to a removed port)
+      }
+      // take over ports whose previous rx thread has let go (acquire: its reads of the port happened before)
+      for (size_t k = 0; k < pending.size();) {
+        int exp = -1;
+        if (pending[k].second->rx_owner_.compare_exchange_strong(exp, (int)q, std::memory_order_acquire)) {
+          active.push_back(pending[k]);
+          pending[k] = pending.back();
+          pending.pop_back();
+        } else {
+          ++k;
+        }
       }
       for (auto& a : active) a.second->reclaim();
       if (q == 0) recirc_->reclaim();
@@ -946,7 +938,9 @@ void Engine::rx_loop(Queue* Q) {
       }
       st.add(st.rx, got);
     }
+    release_all();
   } catch (const std::exception& e) {
+    release_all();
     fail(std::string("rx: ") + e.what());
   }
 }

@@ -126,6 +126,9 @@ class Port {
   uint32_t mask_;
   uint32_t rel_ = 0;   // next sequence number to release
   uint32_t seen_ = 0;  // rx sequence numbers handed out so far (upper bound of reclaim)
+  // The rx queue polling this port (-1: none).  The rx side is single-consumer: a port moved to
+  // another queue is polled there only once its previous rx thread has let go of it.
+  std::atomic<int> rx_owner_{-1};
   friend class Engine;
 };
 

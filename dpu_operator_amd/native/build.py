@@ -46,7 +46,7 @@ MODULES = {
     "_nfdp": {
         "dir": CSRC / "nfdp",
         "sources": ["kernels.hip", "shard.hip", "pktio.hip", "ring.hip", "ipsec.hip", "host.cpp", "shard_cpu.cpp",
-                    "ipsec_cpu.cpp", "iox.cpp", "bindings.cpp"],
+                    "ipsec_cpu.cpp", "iox.cpp", "iox_gpu.cpp", "bindings.cpp"],
         "hip": True,
     },
     "_agent": {
@@ -221,18 +221,29 @@ AGENT_CORE = ["mbox.cpp", "ctrl_net.cpp", "config.cpp", "agent.cpp", "plugin_ser
 SANITIZERS = {"tsan": ["-fsanitize=thread"], "asan": ["-fsanitize=address,undefined", "-fno-omit-frame-pointer"]}
 
 
-def build_sanitized(kind: str, verbose: bool = False) -> Path:
-    """Host-only sanitizer build of the agent stress driver (csrc/agent/stress_main.cpp).
-    GPU sanitizers are unavailable on the MI355X pool; the native runtime is pure host code."""
-    d = CSRC / "agent"
-    out = BUILD / "sanitize" / f"agent-stress-{kind}"
+# host-only sanitizer targets: sources and extra flags.  The I/O engine and its oracle backend are
+# plain C++ (the GPU backend lives in iox_gpu.cpp), compiled against the HIP headers only.
+SANITIZE_TARGETS = {
+    "agent": {"dir": CSRC / "agent", "sources": AGENT_CORE + ["stress_main.cpp"], "flags": []},
+    "iox": {"dir": CSRC / "nfdp", "sources": ["iox_stress.cpp", "iox.cpp", "host.cpp"],
+            "flags": ["-D__HIP_PLATFORM_AMD__", "-I", str(ROCM / "include")]},
+}
+
+
+def build_sanitized(kind: str, verbose: bool = False, target: str = "agent") -> Path:
+    """Host-only sanitizer build of a stress driver: the agent (csrc/agent/stress_main.cpp) or the
+    native I/O engine (csrc/nfdp/iox_stress.cpp).  GPU sanitizers are unavailable on the MI355X
+    pool; both are pure host code."""
+    spec = SANITIZE_TARGETS[target]
+    d = spec["dir"]
+    out = BUILD / "sanitize" / f"{target}-stress-{kind}"
     out.parent.mkdir(parents=True, exist_ok=True)
-    srcs = [d / s for s in AGENT_CORE + ["stress_main.cpp"]]
+    srcs = [d / s for s in spec["sources"]]
     newest = max(max(s.stat().st_mtime for s in srcs), _newest_header(d))
     if out.exists() and out.stat().st_mtime >= newest:
         return out
-    cmd = [shutil.which("g++") or "g++", "-std=c++17", "-O1", "-g", "-pthread", *SANITIZERS[kind],
-           *map(str, srcs), "-o", str(out)]
+    cmd = [shutil.which("g++") or "g++", "-std=c++17", "-O1", "-g", "-pthread", *SANITIZERS[kind], *spec["flags"],
+           "-I", str(d), *map(str, srcs), "-o", str(out)]
     if verbose:
         print(" ".join(cmd), flush=True)
     r = subprocess.run(cmd, capture_output=True, text=True)

@@ -212,3 +212,24 @@ def test_native_path_gpu_ring_bit_exact(tmp_path):
             assert sorted(got[port]) == sorted(frames), port
     finally:
         live.stop()
+
+
+@pytest.mark.parametrize("kind", ["tsan", "asan"])
+def test_native_sanitizer_stress(kind, tmp_path):
+    """Race / memory-error detection on the native I/O engine (csrc/nfdp/iox_stress.cpp, host-only
+    TSan or ASan+UBSan build): two queues x two oracle backends x two tx workers under memif
+    traffic, while commits pause / hold the engine and swap its configuration, a port is removed
+    and re-added, statistics are read, and an injected failure rebuilds the engine."""
+    import subprocess
+
+    from dpu_operator_amd.native.build import build_sanitized
+
+    try:
+        exe = build_sanitized(kind, target="iox")
+    except RuntimeError as e:  # toolchain without the sanitizer runtime
+        pytest.skip(str(e)[:200])
+    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1", ASAN_OPTIONS="detect_leaks=1:abort_on_error=1",
+               UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
+    r = subprocess.run([str(exe), str(tmp_path), "1.5"], capture_output=True, text=True, timeout=180, env=env)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-4000:]
+    assert r.stdout.strip().endswith("ok")
