@@ -100,6 +100,14 @@ NFDP_HD int acl_rule_scalar(const TablesView& t, const Parsed& p, const IngressS
 // not terminated (the head goes through the pipeline as received).  Every rewrite stays in the
 // first 56 bytes, so the egress takes the out slot's first hv (+ tag) bytes and the tail from
 // in_frame + strip (nfdp.h out_tail).
+// The tunnel header after the outer UDP header: VXLAN (4789) with its I flag (RFC 7348: the VNI is
+// valid), or GENEVE (6081) version 0 with no options, not an OAM frame, carrying Ethernet (RFC
+// 8926 protocol 0x6558).  b01: tunnel-header bytes 0 | 1 << 8 (raw), ptype: bytes 2..3 (raw).
+NFDP_HD bool tunnel_hdr_ok(uint32_t dport, uint32_t b01, uint32_t ptype_raw) {
+  if (dport == 4789u) return (b01 & 0x08u) != 0u;
+  return dport == 6081u && (b01 & 0xFFu) == 0u && (b01 & 0x8000u) == 0u && ptype_raw == 0x5865u;
+}
+
 NFDP_HD uint32_t pair_dw(const uint32_t* d, const uint32_t* x, int j) {   // dword j of head ++ continuation
   return j < kSlotDwords ? d[j] : (j < 2 * kSlotDwords ? x[j - kSlotDwords] : 0u);
 }
@@ -124,18 +132,19 @@ NFDP_HD int decap_pair(const TablesView& t, const TA& ta, const uint32_t* d, con
   bool v6 = false;
   int tp = -1;
   if (et == 0x0800u) {
-    const bool ip_ok = ((sn(3) >> 16) & 0xFFu) == 0x45u && (sw(sn(5)) & 0x1FFFu) == 0u && (sn(5) >> 24) == 17u;
+    // a whole datagram (neither MF nor a fragment offset), no options, UDP
+    const bool ip_ok = ((sn(3) >> 16) & 0xFFu) == 0x45u && (sw(sn(5)) & 0x3FFFu) == 0u && (sn(5) >> 24) == 17u;
     if (!ip_ok || a2(30) != pe.ext || nlen < kEncapBytes + 14u) return -1;
-    const uint32_t dport = sw(sn(9)), gopt = (sn(10) >> 16) & 0xFFu;
-    if (!(dport == 4789u || (dport == 6081u && (gopt & 0x3Fu) == 0u))) return -1;
+    const uint32_t dport = sw(sn(9));
+    if (!tunnel_hdr_ok(dport, sn(10) >> 16, sn(11) & 0xFFFFu)) return -1;
     const uint32_t vni = (((sn(11) >> 16) & 0xFFu) << 16) | ((sn(11) >> 24) << 8) | (sn(12) & 0xFFu);
     tp = term_lookup(t, a2(26), vni);
   } else if (et == 0x86DDu && t.vtep6_fold) {
     v6 = true;
     if (((sn(3) >> 20) & 0xFu) != 6u || (sn(5) & 0xFFu) != 17u || nlen < kEncap6Bytes + 14u) return -1;
     if (a2(38) != t.vtep6[0] || a2(42) != t.vtep6[1] || a2(46) != t.vtep6[2] || a2(50) != t.vtep6[3]) return -1;
-    const uint32_t dport = sw(sn(14)), gopt = (sn(15) >> 16) & 0xFFu;
-    if (!(dport == 4789u || (dport == 6081u && (gopt & 0x3Fu) == 0u))) return -1;
+    const uint32_t dport = sw(sn(14));
+    if (!tunnel_hdr_ok(dport, sn(15) >> 16, sn(16) & 0xFFFFu)) return -1;
     const uint32_t vni = (((sn(16) >> 16) & 0xFFu) << 16) | ((sn(16) >> 24) << 8) | (sn(17) & 0xFFu);
     tp = term6_lookup(t, a2(22), a2(26), a2(30), a2(34), vni);
   } else {
@@ -306,12 +315,17 @@ NFDP_HD EgressDecision chain_stage(const TablesView& t, const TA& ta, Parsed& p,
                                          raw32_at2(p.s, 50)) == t.vtep6_fold
                             : raw32_at2(p.s, 30) == st.in_ext;
       const uint32_t proto = v6 ? byte_at(p.s, 20) : (p.s[5] >> 24);
-      if (to_me && proto == 17u && p.len >= enc + 14u) {
+      // (IPv4: parse() took offset 0 only; a first fragment, MF set, is not a whole datagram either)
+      const bool whole = v6 || (be16_at(p.s, 20) & 0x2000u) == 0u;
+      if (to_me && whole && proto == 17u && p.len >= enc + 14u) {
         // constant offsets only (a run-time index into p.s would move the header to scratch)
         const uint32_t dport = v6 ? be16_at(p.s, 56) : be16_at(p.s, 36);
-        const uint32_t gopt = v6 ? byte_at(p.s, 62) : byte_at(p.s, 42);
-        const bool vx = dport == 4789u, gn = dport == 6081u && (gopt & 0x3Fu) == 0u;
-        if (vx || gn) {
+        // IPv4: the tunnel header is in the slot; IPv6: it may lie past it (a tagged outer frame), so
+        // the I/O layer checks it with the VNI on the whole frame (resolve_recirc6)
+        const bool hdr_ok = v6 ? (dport == 4789u || dport == 6081u)
+                               : tunnel_hdr_ok(dport, byte_at(p.s, 42) | (byte_at(p.s, 43) << 8),
+                                               byte_at(p.s, 44) | (byte_at(p.s, 45) << 8));
+        if (hdr_ok) {
           if (v6) {
             e.reason = kRecirc6; e.out_port = kPortNone; e.inner_len = p.len - kEncap6Bytes;
             return e;

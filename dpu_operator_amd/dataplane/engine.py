@@ -588,7 +588,8 @@ class DataPlane:
         whole frame (its VNI lies past the header slot), or None when no tunnel matches (the frame
         then goes to the slow path)."""
         fr = bytes(frame)
-        if not self.vtep6.active or fr[38:54] != self.vtep6.a.tobytes():   # the kernel compared a fold
+        off = 4 if fr[12:14] == b"\x81\x00" else 0
+        if not self.vtep6.active or fr[38 + off:54 + off] != self.vtep6.a.tobytes():   # the kernel compared a fold
             return None
         r = self.terms6.lookup(fr)
         if r is None:

@@ -555,13 +555,27 @@ class Term6Table:
         self.version += 1
 
     def lookup(self, frame: bytes) -> tuple[int, int] | None:
-        """(tunnel port, inner offset) of an IPv6 VXLAN / GENEVE frame, or None."""
-        if len(frame) < 84:
+        """(tunnel port, inner offset) of an IPv6 VXLAN / GENEVE frame (an outer 802.1Q tag
+        allowed), or None: VXLAN needs its I flag, GENEVE version 0, no options, not OAM, an
+        Ethernet payload (the checks the kernel leaves to the whole frame: pipeline.h
+        tunnel_hdr_ok)."""
+        off = 4 if frame[12:14] == b"\x81\x00" else 0
+        if len(frame) < 84 + off or frame[12 + off:14 + off] != b"\x86\xdd" or frame[20 + off] != 17:
             return None
-        src = int.from_bytes(frame[22:38], "big")
-        vni = int.from_bytes(frame[66:69], "big")
+        t = 62 + off
+        dport = int.from_bytes(frame[56 + off:58 + off], "big")
+        if dport == 4789:
+            if not frame[t] & 0x08:
+                return None
+        elif dport == 6081:
+            if frame[t] != 0 or frame[t + 1] & 0x80 or frame[t + 2:t + 4] != b"\x65\x58":
+                return None
+        else:
+            return None
+        src = int.from_bytes(frame[22 + off:38 + off], "big")
+        vni = int.from_bytes(frame[t + 4:t + 7], "big")
         p = self.entries.get((src, vni))
-        return None if p is None else (p, 70)
+        return None if p is None else (p, t + 8)
 
     def __len__(self) -> int:
         return len(self.entries)
