@@ -14,6 +14,7 @@
 #include "ring.h"
 #include "shard.h"
 #include "trafgen.h"
+#include "trafgen_pkt.h"
 
 namespace py = pybind11;
 using namespace nfdp;
@@ -783,8 +784,9 @@ PYBIND11_MODULE(_nfdp, m) {
                         py::arg("tx_bytes") = p.tx_bytes.load());
       });
   py::class_<MemifPort, Port, std::shared_ptr<MemifPort>>(m, "MemifPort")
-      .def(py::init<const std::string&, uint32_t, uint32_t>(), py::arg("path"), py::arg("ring_size") = 1024,
-           py::arg("buf_size") = 2048)
+      .def(py::init<const std::string&, uint32_t, uint32_t, uint32_t>(), py::arg("path"), py::arg("ring_size") = 1024,
+           py::arg("buf_size") = 2048, py::arg("tx_rings") = 1)
+      .def_property_readonly("tx_rings", &MemifPort::tx_queues)
       .def_property_readonly("path", &MemifPort::path);
   py::class_<PacketPort, Port, std::shared_ptr<PacketPort>>(m, "PacketPort")
       .def(py::init<const std::string&, uint32_t, uint32_t>(), py::arg("ifname"), py::arg("frames") = 1024,
@@ -804,6 +806,9 @@ PYBIND11_MODULE(_nfdp, m) {
         b.configure(t, reinterpret_cast<uint64_t*>(flow_ctr), reinterpret_cast<uint64_t*>(port_ctr),
                     reinterpret_cast<uint64_t*>(drop_ctr), const_cast<MacEntry*>(t.macs), t.mac_mask);
       });
+  py::class_<WireBackend, OracleBackend, std::shared_ptr<WireBackend>>(m, "WireBackend")
+      .def(py::init<uint32_t, uint32_t, const std::vector<std::pair<uint64_t, uint32_t>>&>(), py::arg("capacity"),
+           py::arg("queues"), py::arg("mac_to_port"));
   // host snapshot of the side pass's tables: host arrays (numpy) copied at construction
   py::class_<SideTables, std::shared_ptr<SideTables>>(m, "SideTables")
       .def(py::init([](py::buffer ports, py::buffer macs, uint32_t mac_mask, py::buffer lag, uint32_t n_lag_groups,
@@ -853,6 +858,7 @@ PYBIND11_MODULE(_nfdp, m) {
       .def("port_queue", &Engine::port_queue)
       .def("set_side_tables", &Engine::set_side_tables)
       .def("set_redirects", &Engine::set_redirects)
+      .def("set_coalesce", &Engine::set_coalesce, py::arg("frames") = 64, py::arg("window_us") = 0.0)
       .def("hold", [](Engine& e) { py::gil_scoped_release nogil; e.hold(); })
       .def("release", &Engine::release)
       .def("flush_learning", [](Engine& e) { py::gil_scoped_release nogil; e.flush_learning(); })
@@ -925,14 +931,15 @@ PYBIND11_MODULE(_nfdp, m) {
   struct MemifEndpoint {
     std::unique_ptr<memif::Region> reg;
     memif::Producer prod;
-    memif::Consumer cons;
+    std::vector<memif::Consumer> cons;   // one per data plane -> pod ring
   };
   py::class_<MemifEndpoint>(m, "MemifEndpoint")
       .def(py::init([](const std::string& path) {
         auto* e = new MemifEndpoint;
         e->reg.reset(new memif::Region(path, false));
         e->prod.init(e->reg.get(), 0);
-        e->cons.init(e->reg.get(), 1);
+        e->cons.resize(e->reg->rx_rings());
+        for (uint32_t r = 0; r < (uint32_t)e->cons.size(); ++r) e->cons[r].init(e->reg.get(), 1 + r);
         e->reg->hdr()->peer_up.store(1);
         return e;
       }))
@@ -948,13 +955,17 @@ PYBIND11_MODULE(_nfdp, m) {
       })
       .def("recv", [](MemifEndpoint& e, uint32_t max) {
         py::list out;
-        uint32_t n = std::min(e.cons.available(), max);
-        for (uint32_t i = 0; i < n; ++i) {
-          uint32_t len = 0;
-          const uint8_t* p = e.cons.get(len);
-          out.append(py::bytes(reinterpret_cast<const char*>(p), len));
+        uint32_t left = max;
+        for (memif::Consumer& c : e.cons) {
+          const uint32_t n = std::min(c.available(), left);
+          for (uint32_t i = 0; i < n; ++i) {
+            uint32_t len = 0;
+            const uint8_t* p = c.get(len);
+            out.append(py::bytes(reinterpret_cast<const char*>(p), len));
+          }
+          c.release_to(c.next);
+          left -= n;
         }
-        e.cons.release_to(e.cons.next);
         return out;
       }, py::arg("max") = 4096);
   // pod-side generator / sink (trafgen.h); pods: list of (path, frames [k, stride] u8, lens [k] u32)
@@ -990,4 +1001,38 @@ PYBIND11_MODULE(_nfdp, m) {
     return d;
   }, py::arg("pods"), py::arg("duration_s") = 1.0, py::arg("warmup_s") = 0.1, py::arg("rate_pps") = 0.0,
      py::arg("threads") = 1, py::arg("burst") = 32, py::arg("inflight") = 0);
+  // the same generator / sink for kernel-netdev pods (trafgen_pkt.h): pods are
+  // (netns path, ifname, frames [k, stride] u8, lens [k] u32)
+  m.def("trafgen_run_netns", [](py::list pods, double duration_s, double warmup_s, double rate_pps, uint32_t threads,
+                                uint32_t burst) {
+    std::vector<trafgen::NetPod> v;
+    for (auto o : pods) {
+      py::tuple t = o.cast<py::tuple>();
+      trafgen::NetPod p;
+      p.netns = t[0].cast<std::string>();
+      p.ifname = t[1].cast<std::string>();
+      auto fr = t[2].cast<py::array_t<uint8_t, py::array::c_style | py::array::forcecast>>();
+      auto ln = t[3].cast<U32Arr>();
+      if (fr.ndim() != 2 || ln.ndim() != 1 || fr.shape(0) != ln.shape(0)) throw std::invalid_argument("trafgen: frames [k, stride], lens [k]");
+      p.stride = (uint32_t)fr.shape(1);
+      p.frames.assign(fr.data(), fr.data() + fr.size());
+      p.lens.assign(ln.data(), ln.data() + ln.size());
+      for (uint32_t x : p.lens) if (x > p.stride) throw std::invalid_argument("trafgen: len > stride");
+      v.push_back(std::move(p));
+    }
+    trafgen::Config c;
+    c.duration_s = duration_s; c.warmup_s = warmup_s; c.rate_pps = rate_pps; c.threads = threads; c.burst = burst;
+    trafgen::Result r;
+    {
+      py::gil_scoped_release nogil;
+      r = trafgen::run_netns(v, c);
+    }
+    py::dict d;
+    d["sent"] = r.sent; d["received"] = r.received; d["tx_full"] = r.tx_full; d["bad"] = r.bad;
+    d["elapsed_s"] = r.elapsed_s;
+    d["lat_us"] = py::array_t<double>(r.lat_us.size(), r.lat_us.data());
+    d["rx_per_pod"] = r.rx_per_pod; d["tx_per_pod"] = r.tx_per_pod;
+    return d;
+  }, py::arg("pods"), py::arg("duration_s") = 1.0, py::arg("warmup_s") = 0.1, py::arg("rate_pps") = 0.0,
+     py::arg("threads") = 1, py::arg("burst") = 32);
 }

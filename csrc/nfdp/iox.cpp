@@ -40,20 +40,24 @@ Port::Port(uint32_t window) {
   mask_ = w - 1;
 }
 
-uint32_t Port::tx_batch(const TxItem* it, uint32_t n) {
-  std::lock_guard<std::mutex> g(tx_mu_);
+uint32_t Port::tx_batch(const TxItem* it, uint32_t n, uint32_t txq) {
+  const uint32_t nq = std::min<uint32_t>(std::max<uint32_t>(tx_queues(), 1), kMaxTxQueues);
+  const uint32_t q = txq % nq;
   uint32_t ok = 0;
   uint64_t bytes = 0;
-  for (uint32_t i = 0; i < n; ++i) {
-    const TxItem& x = it[i];
-    if (!tx_locked(x.a, x.na, x.b, x.nb, x.c, x.nc)) break;   // full: the rest of the batch finds no room either
-    ++ok;
-    bytes += x.na + x.nb + x.nc;
+  {
+    std::lock_guard<std::mutex> g(tx_mu_[q].mu);
+    for (uint32_t i = 0; i < n; ++i) {
+      const TxItem& x = it[i];
+      if (!tx_locked(q, x.a, x.na, x.b, x.nb, x.c, x.nc)) break;   // full: the rest of the batch finds no room either
+      ++ok;
+      bytes += x.na + x.nb + x.nc;
+    }
+    if (ok) flush_locked(q);
   }
-  if (ok) flush_locked();
-  // counters change under the tx lock only: plain read-modify-store, no atomic RMW
+  // one add per batch (several tx queues may count at once)
   auto add = [](std::atomic<uint64_t>& c, uint64_t v) {
-    if (v) c.store(c.load(std::memory_order_relaxed) + v, std::memory_order_relaxed);
+    if (v) c.fetch_add(v, std::memory_order_relaxed);
   };
   add(tx_pkts, ok);
   add(tx_bytes, bytes);
@@ -74,10 +78,13 @@ void Port::reclaim() {
 }
 
 // ---------------------------------------------------------------------------------- MemifPort
-MemifPort::MemifPort(const std::string& path, uint32_t ring_size, uint32_t buf_size)
-    : Port(ring_size), reg_(path, true, ring_size, buf_size), unlink_(true) {
+MemifPort::MemifPort(const std::string& path, uint32_t ring_size, uint32_t buf_size, uint32_t tx_rings)
+    : Port(ring_size), reg_(path, true, ring_size, buf_size, std::min<uint32_t>(std::max<uint32_t>(tx_rings, 1), kMaxTxQueues)),
+      unlink_(true) {
+  nprod_ = reg_.rx_rings();
+  prod_.reset(new Prod[nprod_]);
   cons_.init(&reg_, 0);
-  prod_.init(&reg_, 1);
+  for (uint32_t q = 0; q < nprod_; ++q) prod_[q].init(&reg_, 1 + q);
   set_first_seq(cons_.next);
 }
 
@@ -94,10 +101,6 @@ uint32_t MemifPort::rx(RxRef* out, uint32_t max) {
     out[i] = RxRef{p, len, seq, ~0u};
   }
   return n;
-}
-
-bool MemifPort::tx_locked(const uint8_t* a, uint32_t na, const uint8_t* b, uint32_t nb, const uint8_t* c, uint32_t nc) {
-  return prod_.put(a, na, b, nb, c, nc);
 }
 
 // ---------------------------------------------------------------------------------- PacketPort
@@ -187,7 +190,7 @@ void PacketPort::release_to(uint32_t seq_end) {
   rel_done_ = seq_end;
 }
 
-bool PacketPort::tx_locked(const uint8_t* a, uint32_t na, const uint8_t* b, uint32_t nb, const uint8_t* c, uint32_t nc) {
+bool PacketPort::tx_locked(uint32_t, const uint8_t* a, uint32_t na, const uint8_t* b, uint32_t nb, const uint8_t* c, uint32_t nc) {
   auto* h = reinterpret_cast<tpacket2_hdr*>(frame(1, tx_next_));
   uint32_t st = __atomic_load_n(&h->tp_status, __ATOMIC_ACQUIRE);
   if (st == TP_STATUS_WRONG_FORMAT) st = TP_STATUS_AVAILABLE;
@@ -204,7 +207,7 @@ bool PacketPort::tx_locked(const uint8_t* a, uint32_t na, const uint8_t* b, uint
   return true;
 }
 
-void PacketPort::flush_locked() { (void)::sendto(fd_, nullptr, 0, MSG_DONTWAIT, nullptr, 0); }
+void PacketPort::flush_locked(uint32_t) { (void)::sendto(fd_, nullptr, 0, MSG_DONTWAIT, nullptr, 0); }
 
 // ---------------------------------------------------------------------------------- FdPort
 FdPort::FdPort(int fd, uint32_t nbufs, uint32_t buf_size)
@@ -225,7 +228,7 @@ uint32_t FdPort::rx(RxRef* out, uint32_t max) {
   return n;
 }
 
-bool FdPort::tx_locked(const uint8_t* a, uint32_t na, const uint8_t* b, uint32_t nb, const uint8_t* c, uint32_t nc) {
+bool FdPort::tx_locked(uint32_t, const uint8_t* a, uint32_t na, const uint8_t* b, uint32_t nb, const uint8_t* c, uint32_t nc) {
   const uint32_t n = na + nb + nc;
   if (n > txbuf_.size()) return false;
   uint8_t* d = txbuf_.data();
@@ -384,7 +387,8 @@ uint64_t OracleBackend::publish(uint32_t q, uint32_t n) {
   while (real < n && im[(prod + real) & (cap_ - 1)] != kRingPadMeta) ++real;
   for (uint32_t i = real; i < n; ++i) om[(prod + i) & (cap_ - 1)] = make_meta(kPortNone, 0, kMalformed);
   {
-    std::lock_guard<std::mutex> g(run_mu_);
+    std::unique_lock<std::mutex> g(run_mu_, std::defer_lock);
+    if (serial_) g.lock();
     uint32_t done = 0;
     while (done < real) {
       const uint32_t p = (uint32_t)((prod + done) & (cap_ - 1));
@@ -400,6 +404,43 @@ uint64_t OracleBackend::publish(uint32_t q, uint32_t n) {
 void OracleBackend::apply_learn(const uint32_t* ev, uint32_t n, uint32_t stamp) {
   std::lock_guard<std::mutex> g(run_mu_);
   if (macs_ && n) mac_learn_cpu(macs_, mac_mask_, ev, n, stamp);
+}
+
+// ---------------------------------------------------------------------------------- WireBackend
+namespace {
+inline uint32_t mac_slot(uint64_t k, uint32_t mask) { return (uint32_t)((k * 0x9E3779B97F4A7C15ull) >> 40) & mask; }
+}  // namespace
+
+WireBackend::WireBackend(uint32_t capacity, uint32_t queues, const std::vector<std::pair<uint64_t, uint32_t>>& m)
+    : OracleBackend(capacity, queues) {
+  tmask_ = pow2_at_least(std::max<uint32_t>(16, (uint32_t)m.size() * 4)) - 1;
+  tab_.assign((size_t)tmask_ + 1, {0, 0});
+  for (const auto& e : m) {
+    const uint64_t k = (e.first & 0xFFFFFFFFFFFFull) + 1;
+    uint32_t i = mac_slot(k, tmask_);
+    while (tab_[i].first && tab_[i].first != k) i = (i + 1) & tmask_;
+    tab_[i] = {k, e.second};
+  }
+  serial_ = false;   // no shared state: queues run in parallel
+  configure(TablesView{}, nullptr, nullptr, nullptr, nullptr, 0);
+}
+
+void WireBackend::run_segment(uint32_t q, uint32_t pos, uint32_t n) {
+  const size_t p = (size_t)q * cap_ + (pos & (cap_ - 1));
+  std::memcpy(out_.data() + p * kSlotBytes, in_.data() + p * kSlotBytes, (size_t)n * kSlotBytes);
+  for (uint32_t i = 0; i < n; ++i) {
+    const uint8_t* f = in_.data() + (p + i) * kSlotBytes;
+    uint64_t k = 0;
+    std::memcpy(&k, f, 6);
+    k += 1;
+    const uint32_t len = im_[p + i] >> 16;
+    uint32_t j = mac_slot(k, tmask_), port = kPortNone;
+    while (tab_[j].first) {
+      if (tab_[j].first == k) { port = tab_[j].second; break; }
+      j = (j + 1) & tmask_;
+    }
+    om_[p + i] = port == kPortNone ? make_meta(kPortNone, 0, kMalformed) : make_meta(port, len, kOk);
+  }
 }
 
 // ---------------------------------------------------------------------------------- Engine
@@ -441,6 +482,7 @@ void Engine::update_cfg(F f) {
   auto c = std::make_shared<Cfg>(*std::atomic_load(&cfg_));
   f(*c);
   std::atomic_store(&cfg_, std::shared_ptr<const Cfg>(c));
+  cfg_ver_.fetch_add(1, std::memory_order_release);
 }
 
 void Engine::add_backend(std::shared_ptr<Backend> b) {
@@ -475,6 +517,7 @@ void Engine::add_port(uint32_t id, std::shared_ptr<Port> p, int queue) {
   (*t)[id] = PortRef{std::move(p), q};
   queues_[q]->nports.fetch_add(1);
   std::atomic_store(&ports_, std::shared_ptr<const PortTab>(t));
+  ports_ver_.fetch_add(1, std::memory_order_release);
 }
 
 std::shared_ptr<Port> Engine::remove_port(uint32_t id) {
@@ -485,6 +528,7 @@ std::shared_ptr<Port> Engine::remove_port(uint32_t id) {
   if (old) queues_[(*t)[id].q]->nports.fetch_sub(1);
   (*t)[id] = PortRef{};
   std::atomic_store(&ports_, std::shared_ptr<const PortTab>(t));
+  ports_ver_.fetch_add(1, std::memory_order_release);
   return old;   // frames of it still in flight keep it alive through the snapshot the threads hold
 }
 
@@ -612,6 +656,8 @@ void Engine::stop() {
       }
     }
     L->done.store(L->head.load());
+    for (const Pkt& q : L->stage) q.holder->complete(q.seq);   // read but never published
+    L->stage.clear();
   }
 }
 
@@ -679,9 +725,12 @@ std::vector<Punt> Engine::take_punts(size_t max) {
 }
 
 std::vector<double> Engine::take_latency_us() {
-  std::lock_guard<std::mutex> g(lat_mu_);
   std::vector<double> v;
-  v.swap(lat_us_);
+  for (auto& Q : queues_) {
+    std::lock_guard<std::mutex> g(Q->lat_mu);
+    v.insert(v.end(), Q->lat_us.begin(), Q->lat_us.end());
+    Q->lat_us.clear();
+  }
   return v;
 }
 
@@ -788,6 +837,8 @@ void Engine::rx_loop(Queue* Q) {
   std::vector<RxRef> buf(burst_);
   uint32_t rr = 0;
   std::shared_ptr<const PortTab> cached;
+  uint64_t cached_ver = ~0ull;
+  Snap<Cfg> csnap;
   std::vector<std::pair<uint32_t, Port*>> active;    // ports of this queue this thread owns and polls
   std::vector<std::pair<uint32_t, Port*>> pending;   // ports of this queue another rx thread still holds
   const uint32_t nb = (uint32_t)backends_.size();
@@ -807,8 +858,10 @@ void Engine::rx_loop(Queue* Q) {
         if (pause_n_.load()) std::this_thread::sleep_for(std::chrono::microseconds(10));
         continue;
       }
-      auto tab = std::atomic_load(&ports_);
-      if (tab != cached) {
+      const uint64_t pv = ports_ver_.load(std::memory_order_acquire);
+      if (pv != cached_ver) {
+        auto tab = std::atomic_load(&ports_);
+        cached_ver = pv;
         std::vector<std::pair<uint32_t, Port*>> want;
         for (uint32_t i = 0; i < (uint32_t)tab->size(); ++i)
           if ((*tab)[i].p && (*tab)[i].q == q) want.emplace_back(i, (*tab)[i].p.get());
@@ -838,10 +891,10 @@ void Engine::rx_loop(Queue* Q) {
       }
       for (auto& a : active) a.second->reclaim();
       if (q == 0) recirc_->reclaim();
-      const auto c = cfg();
+      const Cfg* c = &cfg_of(csnap);
       const Steer* steer = c->steer.get();
       // room: a burst of k frames takes ceil(k / 64) chunks on its lane; bound the take by the
-      // fullest lane (frames are steered after they are read)
+      // fullest lane (frames are steered after they are read), counting what is staged already
       uint32_t take = burst_;
       for (Lane* L : Q->lanes) {
         if (!L->be->ready() ||
@@ -853,66 +906,76 @@ void Engine::rx_loop(Queue* Q) {
         const uint64_t used = L->be->published(q) - L->freed_pos.load(std::memory_order_acquire);
         uint64_t room = L->be->capacity() > used ? L->be->capacity() - used : 0;
         if (max_frames_) room = std::min<uint64_t>(room, max_frames_ > used ? max_frames_ - used : 0);
-        take = (uint32_t)std::min<uint64_t>(take, room & ~63ull);
-      }
-      if (take == 0) {
-        st.add(st.wait_tx, 1);
-        _mm_pause();
-        continue;
+        room &= ~63ull;
+        const uint64_t staged = L->stage.size();
+        L->room = room;
+        take = (uint32_t)std::min<uint64_t>(take, room > staged ? room - staged : 0);
+        take = (uint32_t)std::min<uint64_t>(take, burst_ > staged ? burst_ - staged : 0);
       }
       const uint64_t t_rx = now_ns();
       uint32_t got = 0;
-      auto read_port = [&](uint32_t pid, Port* p, uint32_t max) {
-        const uint32_t n = p->rx(buf.data(), max);
-        uint64_t pk = 0, by = 0;
-        for (uint32_t i = 0; i < n; ++i) {
-          const RxRef& r = buf[i];
-          if (r.seq + 1 - p->seen_ <= 0x7FFFFFFFu) p->seen_ = r.seq + 1;
-          if (r.len < 14 || r.len > kMaxFrame) { p->complete(r.seq); continue; }   // runt / oversize / own tx
-          const uint32_t in_port = r.in_port != ~0u ? r.in_port : pid;
-          const uint32_t o = nb > 1 ? owner(steer, nb, r.data, r.len, in_port) : 0u;
-          Q->lanes[o]->stage.push_back(Pkt{in_port, r.seq, r.data, r.len, p});
-          ++pk;
-          by += r.len;
-        }
-        p->count_rx(pk, by);
-        got += (uint32_t)pk;
-        return n;
-      };
-      if (q == 0) (void)read_port(0, recirc_.get(), take);
-      // every port gets an equal share of the burst first (round-robin start), then leftovers
-      const uint32_t np = (uint32_t)active.size();
-      if (np) {
-        const uint32_t share = std::max<uint32_t>(1, take / np);
-        uint32_t taken = got;
-        for (int pass = 0; pass < 2 && taken < take; ++pass) {
-          for (uint32_t k = 0; k < np && taken < take; ++k) {
-            const auto& a = active[(rr + k) % np];
-            taken += read_port(a.first, a.second, std::min(take - taken, pass ? take : share));
+      if (take) {
+        auto read_port = [&](uint32_t pid, Port* p, uint32_t max) {
+          const uint32_t n = p->rx(buf.data(), max);
+          uint64_t pk = 0, by = 0;
+          for (uint32_t i = 0; i < n; ++i) {
+            const RxRef& r = buf[i];
+            p->handed_out(r.seq);
+            if (r.len < 14 || r.len > kMaxFrame) { p->complete(r.seq); continue; }   // runt / oversize / own tx
+            const uint32_t in_port = r.in_port != ~0u ? r.in_port : pid;
+            const uint32_t o = nb > 1 ? owner(steer, nb, r.data, r.len, in_port) : 0u;
+            Lane* L = Q->lanes[o];
+            if (L->stage.empty()) L->stage_t0 = t_rx;
+            L->stage.push_back(Pkt{in_port, r.seq, r.data, r.len, p});
+            ++pk;
+            by += r.len;
           }
+          p->count_rx(pk, by);
+          got += (uint32_t)pk;
+          return n;
+        };
+        if (q == 0) (void)read_port(0, recirc_.get(), take);
+        // every port gets an equal share of the burst first (round-robin start), then leftovers
+        const uint32_t np = (uint32_t)active.size();
+        if (np) {
+          const uint32_t share = std::max<uint32_t>(1, take / np);
+          uint32_t taken = got;
+          for (int pass = 0; pass < 2 && taken < take; ++pass) {
+            for (uint32_t k = 0; k < np && taken < take; ++k) {
+              const auto& a = active[(rr + k) % np];
+              taken += read_port(a.first, a.second, std::min(take - taken, pass ? take : share));
+            }
+          }
+          rr = (rr + 1) % np;
         }
-        rr = (rr + 1) % np;
+        st.add(st.rx, got);
       }
-      if (got == 0) {
-        st.add(st.idle, 1);
-        _mm_pause();
-        continue;
-      }
+      // publication: a lane's staged frames go out at once when nothing of the lane is in
+      // flight (the unloaded case: no added latency); under load they gather into whole 64-slot
+      // chunks (no padding, fewer bursts for the GPU and the tx threads), bounded in time by
+      // the coalescing window and in size by the burst / the lane's room
       const std::vector<uint8_t>& side_ports = c->side_ports;
       const bool side_always = c->side_always;
+      const uint64_t win = coalesce_ns_.load(std::memory_order_relaxed);
+      const uint32_t cmin = coalesce_frames_.load(std::memory_order_relaxed);
+      uint32_t pubs = 0;
       for (Lane* L : Q->lanes) {
         if (L->stage.empty()) continue;
-        Backend& be = *L->be;
+        const uint64_t head = L->head.load(std::memory_order_relaxed);
+        const uint64_t inflight = head - L->done.load(std::memory_order_acquire);
+        if (inflight >= inflight_ || !L->be->ready()) continue;
         const uint32_t k = (uint32_t)L->stage.size();
+        const bool go = inflight == 0 || k >= cmin || k >= burst_ || k + 64 > L->room || t_rx - L->stage_t0 >= win;
+        if (!go) continue;
+        Backend& be = *L->be;
         const uint32_t npad = (k + 63u) & ~63u;
         const uint64_t start = be.published(q);
         uint32_t* im = be.in_meta(q);
         const uint32_t cmask = be.capacity() - 1;
-        const uint64_t head = L->head.load(std::memory_order_relaxed);
         Burst& b = L->slots[head % inflight_];   // free: head - done < inflight
         b.start = start;
         b.end = start + npad;
-        b.t_rx_ns = t_rx;
+        b.t_rx_ns = L->stage_t0;
         bool side = side_always;
         for (uint32_t i = 0; i < k; ++i) {
           const Pkt& pk = L->stage[i];
@@ -935,8 +998,12 @@ void Engine::rx_loop(Queue* Q) {
         be.publish(q, npad);
         st.add(st.pub_ns, now_ns() - tp0);
         st.add(st.bursts, 1);
+        ++pubs;
       }
-      st.add(st.rx, got);
+      if (got == 0 && pubs == 0) {
+        st.add(take ? st.idle : st.wait_tx, 1);
+        _mm_pause();
+      }
     }
     release_all();
   } catch (const std::exception& e) {
@@ -1033,18 +1100,17 @@ void Engine::side_work(Queue* Q, Lane* L, Burst& b, const Cfg& c, TxScratch& sc,
   }
 }
 
-void Engine::deliver(Queue* Q, Lane* L, Burst& b, uint32_t w, const Cfg& c, TxScratch& sc) {
+void Engine::deliver(Queue* Q, Lane* L, Burst& b, uint32_t w, const Cfg& c, const PortTab& tab, TxScratch& sc) {
   Backend& be = *L->be;
   const uint32_t q = Q->id, cmask = be.capacity() - 1;
   const uint32_t* om = be.out_meta(q);
-  auto tab = std::atomic_load(&ports_);
   const std::vector<uint32_t>& red = c.redirect;
   auto route = [&](uint32_t port) {   // tunnel port -> its underlay port
     return port < red.size() && red[port] != 0xFFFFFFFFu ? red[port] : port;
   };
   TxTally tally;
   auto add = [&](uint32_t port, const TxItem& it) {
-    if (port >= tab->size() || !(*tab)[port].p) { ++tally.no_port; return; }
+    if (port >= tab.size() || !tab[port].p) { ++tally.no_port; return; }
     auto& v = sc.by_port[port];
     if (v.empty()) sc.touched.push_back(port);
     v.push_back(it);
@@ -1105,7 +1171,7 @@ void Engine::deliver(Queue* Q, Lane* L, Burst& b, uint32_t w, const Cfg& c, TxSc
   // one locked batch per egress port
   for (uint32_t port : sc.touched) {
     auto& v = sc.by_port[port];
-    const uint32_t ok = (*tab)[port].p->tx_batch(v.data(), (uint32_t)v.size());
+    const uint32_t ok = tab[port].p->tx_batch(v.data(), (uint32_t)v.size(), q);   // this queue's tx ring
     tally.tx += ok;
     tally.full += v.size() - ok;
     v.clear();
@@ -1119,12 +1185,12 @@ void Engine::deliver(Queue* Q, Lane* L, Burst& b, uint32_t w, const Cfg& c, TxSc
   st.add(st.reps, tally.reps);
 }
 
-void Engine::finish(Lane* L, Burst& b) {
+void Engine::finish(Queue* Q, Lane* L, Burst& b) {
   for (const Pkt& q : b.pkts) q.holder->complete(q.seq);
   const double us = (double)(now_ns() - b.t_rx_ns) * 1e-3;
   {
-    std::lock_guard<std::mutex> g(lat_mu_);
-    if (lat_us_.size() < (1u << 20)) lat_us_.push_back(us);
+    std::lock_guard<std::mutex> g(Q->lat_mu);
+    if (Q->lat_us.size() < (1u << 18)) Q->lat_us.push_back(us);
   }
   b.pkts.clear();
   b.reps.clear();
@@ -1146,6 +1212,8 @@ void Engine::tx_loop(Queue* Q, uint32_t w) {
     const uint32_t want = w == 0 ? 1u : 2u;
     uint32_t idle = 0;
     QStats& st = Q->wst[w];
+    Snap<Cfg> csnap;
+    Snap<PortTab> psnap;
     for (;;) {
       bool any = false;
       for (uint32_t li = 0; li < nl; ++li) {
@@ -1165,7 +1233,7 @@ void Engine::tx_loop(Queue* Q, uint32_t w) {
             continue;
           }
           waiting[li] = 0;
-          const auto c = cfg();
+          const Cfg* c = &cfg_of(csnap);
           bool side = b.side;
           if (!side) {
             const uint32_t* om = L->be->out_meta(Q->id);
@@ -1176,15 +1244,15 @@ void Engine::tx_loop(Queue* Q, uint32_t w) {
           if (side) side_work(Q, L, b, *c, sc, w);
           b.state.store(2, std::memory_order_release);
           const uint64_t td0 = now_ns();
-          deliver(Q, L, b, w, *c, sc);
+          deliver(Q, L, b, w, *c, ports_of(psnap), sc);
           st.add(st.deliver_ns, now_ns() - td0);
         } else {
-          const auto c = cfg();
+          const Cfg& c = cfg_of(csnap);
           const uint64_t td0 = now_ns();
-          deliver(Q, L, b, w, *c, sc);
+          deliver(Q, L, b, w, c, ports_of(psnap), sc);
           st.add(st.deliver_ns, now_ns() - td0);
         }
-        if (b.left.fetch_sub(1, std::memory_order_acq_rel) == 1) finish(L, b);
+        if (b.left.fetch_sub(1, std::memory_order_acq_rel) == 1) finish(Q, L, b);
         ++cur[li];
         any = true;
       }
@@ -1201,7 +1269,8 @@ void Engine::tx_loop(Queue* Q, uint32_t w) {
         if (drained) return;
       }
       _mm_pause();
-      if ((++idle & 0xFFFFu) == 0) std::this_thread::yield();
+      if ((++idle & 0x3FFu) == 0) (void)ports_of(psnap);   // idle: let go of a replaced port table too
+      if ((idle & 0xFFFFu) == 0) std::this_thread::yield();
     }
   } catch (const std::exception& e) {
     fail(std::string("tx: ") + e.what());

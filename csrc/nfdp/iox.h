@@ -93,15 +93,21 @@ class Port {
   virtual ~Port() = default;
   // Up to `max` received frames; each stays valid until its sequence number is released.
   virtual uint32_t rx(RxRef* out, uint32_t max) = 0;
-  // A batch of frames under one lock acquisition and one ring commit; returns how many were
-  // written (the rest found no room and are dropped, as on a full NIC queue).  Thread safe.
-  uint32_t tx_batch(const TxItem* items, uint32_t n);
+  // A batch of frames into tx queue `txq` (mod tx_queues()) under one lock acquisition and one
+  // ring commit; returns how many were written (the rest found no room and are dropped, as on a
+  // full NIC queue).  Thread safe; writers of different tx queues never share a lock.
+  uint32_t tx_batch(const TxItem* items, uint32_t n, uint32_t txq = 0);
   bool tx(const uint8_t* a, uint32_t na, const uint8_t* b, uint32_t nb, const uint8_t* c, uint32_t nc) {
     const TxItem it{a, na, b, nb, c, nc};
     return tx_batch(&it, 1) == 1;
   }
-  // A frame is done (sent or dropped): any thread.  reclaim(): the owning rx thread only.
+  virtual uint32_t tx_queues() const { return 1; }
+  // A frame is done (sent or dropped): any thread.  reclaim(): the owning rx thread only, after
+  // marking what rx() handed out (handed_out: sequence numbers up to seq are in use).
   void complete(uint32_t seq) { done_[seq & mask_].store(1, std::memory_order_release); }
+  void handed_out(uint32_t seq) {
+    if (seq + 1 - seen_ <= 0x7FFFFFFFu) seen_ = seq + 1;
+  }
   void reclaim();
   virtual std::string kind() const = 0;
   // rx counters: single writer (the rx thread owning the port) adds a burst at a time
@@ -110,16 +116,20 @@ class Port {
     rx_bytes.store(rx_bytes.load(std::memory_order_relaxed) + bytes, std::memory_order_relaxed);
   }
   alignas(64) std::atomic<uint64_t> rx_pkts{0}, rx_bytes{0};
-  // tx counters: updated under the tx lock, once per batch
+  // tx counters: added once per batch
   alignas(64) std::atomic<uint64_t> tx_pkts{0}, tx_full{0}, tx_bytes{0};
+  static constexpr uint32_t kMaxTxQueues = 16;
 
  protected:
-  virtual bool tx_locked(const uint8_t* a, uint32_t na, const uint8_t* b, uint32_t nb, const uint8_t* c, uint32_t nc) = 0;
-  virtual void flush_locked() {}
+  // under tx queue q's lock (q < tx_queues())
+  virtual bool tx_locked(uint32_t q, const uint8_t* a, uint32_t na, const uint8_t* b, uint32_t nb, const uint8_t* c,
+                         uint32_t nc) = 0;
+  virtual void flush_locked(uint32_t) {}
   virtual void release_to(uint32_t seq_end) = 0;   // every frame below seq_end is done
   void set_first_seq(uint32_t s) { rel_ = s; seen_ = s; }
   uint32_t window() const { return mask_ + 1; }
-  std::mutex tx_mu_;
+  struct alignas(64) TxLock { std::mutex mu; };
+  TxLock tx_mu_[kMaxTxQueues];
 
  private:
   std::unique_ptr<std::atomic<uint8_t>[]> done_;
@@ -132,24 +142,31 @@ class Port {
   friend class Engine;
 };
 
-// Shared-memory vport (memif.h): the pod produces ring 0, the engine ring 1.
+// Shared-memory vport (memif.h): the pod produces ring 0, the engine rings 1..tx_rings (tx
+// queue q writes ring 1 + q).
 class MemifPort : public Port {
  public:
-  MemifPort(const std::string& path, uint32_t ring_size, uint32_t buf_size);
+  MemifPort(const std::string& path, uint32_t ring_size, uint32_t buf_size, uint32_t tx_rings = 1);
   ~MemifPort() override;
   uint32_t rx(RxRef* out, uint32_t max) override;
   std::string kind() const override { return "memif"; }
   const std::string& path() const { return reg_.path(); }
+  uint32_t tx_queues() const override { return nprod_; }
 
  protected:
-  bool tx_locked(const uint8_t* a, uint32_t na, const uint8_t* b, uint32_t nb, const uint8_t* c, uint32_t nc) override;
-  void flush_locked() override { prod_.commit(); }
+  bool tx_locked(uint32_t q, const uint8_t* a, uint32_t na, const uint8_t* b, uint32_t nb, const uint8_t* c,
+                 uint32_t nc) override {
+    return prod_[q].put(a, na, b, nb, c, nc);
+  }
+  void flush_locked(uint32_t q) override { prod_[q].commit(); }
   void release_to(uint32_t seq_end) override { cons_.release_to(seq_end); }
 
  private:
   memif::Region reg_;
   memif::Consumer cons_;
-  memif::Producer prod_;
+  struct alignas(64) Prod : memif::Producer {};
+  std::unique_ptr<Prod[]> prod_;
+  uint32_t nprod_;
   bool unlink_;
 };
 
@@ -162,8 +179,9 @@ class PacketPort : public Port {
   std::string kind() const override { return "af_packet"; }
 
  protected:
-  bool tx_locked(const uint8_t* a, uint32_t na, const uint8_t* b, uint32_t nb, const uint8_t* c, uint32_t nc) override;
-  void flush_locked() override;
+  bool tx_locked(uint32_t q, const uint8_t* a, uint32_t na, const uint8_t* b, uint32_t nb, const uint8_t* c,
+                 uint32_t nc) override;
+  void flush_locked(uint32_t q) override;
   void release_to(uint32_t seq_end) override;
 
  private:
@@ -184,7 +202,8 @@ class FdPort : public Port {
   std::string kind() const override { return "fd"; }
 
  protected:
-  bool tx_locked(const uint8_t* a, uint32_t na, const uint8_t* b, uint32_t nb, const uint8_t* c, uint32_t nc) override;
+  bool tx_locked(uint32_t q, const uint8_t* a, uint32_t na, const uint8_t* b, uint32_t nb, const uint8_t* c,
+                 uint32_t nc) override;
   void release_to(uint32_t seq_end) override { freed_.store(seq_end, std::memory_order_release); }
 
  private:
@@ -205,7 +224,9 @@ class RecircPort : public Port {
   std::string kind() const override { return "recirc"; }
 
  protected:
-  bool tx_locked(const uint8_t*, uint32_t, const uint8_t*, uint32_t, const uint8_t*, uint32_t) override { return false; }
+  bool tx_locked(uint32_t, const uint8_t*, uint32_t, const uint8_t*, uint32_t, const uint8_t*, uint32_t) override {
+    return false;
+  }
   void release_to(uint32_t seq_end) override;
 
  private:
@@ -317,18 +338,35 @@ class OracleBackend : public Backend {
   void configure(const TablesView& t, uint64_t* flow_ctr, uint64_t* port_ctr, uint64_t* drop_ctr, MacEntry* macs,
                  uint32_t mac_mask);
 
- private:
-  void run_segment(uint32_t q, uint32_t pos, uint32_t n);
+ protected:
+  virtual void run_segment(uint32_t q, uint32_t pos, uint32_t n);
   uint32_t cap_, nq_;
   std::vector<uint8_t> in_, out_;
   std::vector<uint32_t> im_, om_;
   std::unique_ptr<std::atomic<uint64_t>[]> prod_;
   std::atomic<bool> configured_{false};
   std::mutex run_mu_;   // the pipeline's counters / MAC table are shared by every queue
+  bool serial_ = true;  // queues run one at a time (run_mu_)
   TablesView t_{};
   uint64_t *flow_ctr_ = nullptr, *port_ctr_ = nullptr, *drop_ctr_ = nullptr;
   MacEntry* macs_ = nullptr;
   uint32_t mac_mask_ = 0;
+};
+
+// A pipeline that costs nothing: every frame leaves unchanged through the port its destination
+// MAC is bound to (unknown MACs drop).  It measures the I/O engine alone — ports, steering,
+// publication, delivery — the ceiling any pipeline behind it is held to (tools/live_bench.py
+// --backend wire).
+class WireBackend : public OracleBackend {
+ public:
+  WireBackend(uint32_t capacity, uint32_t queues, const std::vector<std::pair<uint64_t, uint32_t>>& mac_to_port);
+
+ protected:
+  void run_segment(uint32_t q, uint32_t pos, uint32_t n) override;
+
+ private:
+  std::vector<std::pair<uint64_t, uint32_t>> tab_;   // open addressing, 48-bit MAC + 1 (0: empty)
+  uint32_t tmask_ = 0;
 };
 
 // ---------------------------------------------------------------------------------- engine
@@ -367,6 +405,13 @@ class Engine {
   void set_redirect(uint32_t port, uint32_t underlay);   // one entry (0xFFFFFFFF clears it)
   void set_side_ports(const std::vector<uint32_t>& ports); // ingress ports whose packets need side work
   void set_side_always(bool on);
+  // Publication coalescing: with bursts of a lane in flight, frames gather until `frames` are
+  // staged or the oldest waited `window_us` (an idle lane publishes at once).  (64, 0): every
+  // read publishes.
+  void set_coalesce(uint32_t frames, double window_us) {
+    coalesce_frames_.store(std::max<uint32_t>(frames, 1));
+    coalesce_ns_.store((uint64_t)(std::max(window_us, 0.0) * 1e3));
+  }
   void set_side_tables(uint32_t backend, std::shared_ptr<SideTables> t);
   void start();
   void stop();
@@ -418,7 +463,9 @@ class Engine {
     std::atomic<uint64_t> head{0};        // rx thread: next burst id
     std::atomic<uint64_t> done{0};        // bursts fully delivered (in order)
     std::atomic<uint64_t> freed_pos{0};   // ring position below which every slot is delivered (reusable)
-    std::vector<Pkt> stage;     // rx thread: frames bound for this backend
+    std::vector<Pkt> stage;     // rx thread: frames bound for this backend, not published yet
+    uint64_t stage_t0 = 0;      // rx time of the first staged frame
+    uint64_t room = 0;          // rx thread: free ring slots at the last look (multiple of 64)
   };
   struct alignas(64) QStats {
     std::atomic<uint64_t> rx{0}, tx{0}, drop{0}, punt{0}, recirc{0}, reps{0}, bursts{0}, side{0}, no_port{0},
@@ -436,6 +483,8 @@ class Engine {
     std::unique_ptr<std::atomic<uint64_t>[]> side_ctr;   // per worker x kMaxPorts x 2 (replica tx pkts / bytes)
     std::unique_ptr<std::atomic<uint64_t>[]> side_drop;  // per worker x kNumReasons
     std::atomic<uint32_t> nports{0};
+    std::mutex lat_mu;           // rx -> tx time per burst, this queue's samples
+    std::vector<double> lat_us;
   };
   struct PortRef { std::shared_ptr<Port> p; uint32_t q = 0; };
   using PortTab = std::vector<PortRef>;
@@ -462,14 +511,31 @@ class Engine {
   void rx_loop(Queue* Q);
   void tx_loop(Queue* Q, uint32_t w);
   void learner_loop();
-  void deliver(Queue* Q, Lane* L, Burst& b, uint32_t w, const Cfg& cfg, TxScratch& sc);
+  void deliver(Queue* Q, Lane* L, Burst& b, uint32_t w, const Cfg& cfg, const PortTab& tab, TxScratch& sc);
   void side_work(Queue* Q, Lane* L, Burst& b, const Cfg& cfg, TxScratch& sc, uint32_t w);
-  void finish(Lane* L, Burst& b);
+  void finish(Queue* Q, Lane* L, Burst& b);
   bool lanes_idle() const;
   void punt(QStats& st, uint32_t in_port, uint32_t reason, const uint8_t* a, uint32_t na, const uint8_t* b, uint32_t nb);
   void fail(const std::string& what);
   std::shared_ptr<const Cfg> cfg() const { return std::atomic_load(&cfg_); }
   template <class F> void update_cfg(F f);
+  // A packet thread's private reference to a copy-on-write snapshot, re-read only when the
+  // snapshot's version moved: the hot loops touch one read-mostly version word, never the
+  // shared_ptr's control block (whose atomic load is a global lock in libstdc++) or its refcount.
+  template <class T> struct Snap {
+    uint64_t ver = ~0ull;
+    std::shared_ptr<const T> p;
+  };
+  const Cfg& cfg_of(Snap<Cfg>& s) const {
+    const uint64_t v = cfg_ver_.load(std::memory_order_acquire);
+    if (v != s.ver) { s.p = std::atomic_load(&cfg_); s.ver = v; }
+    return *s.p;
+  }
+  const PortTab& ports_of(Snap<PortTab>& s) const {
+    const uint64_t v = ports_ver_.load(std::memory_order_acquire);
+    if (v != s.ver) { s.p = std::atomic_load(&ports_); s.ver = v; }
+    return *s.p;
+  }
   static uint32_t owner(const Steer* s, uint32_t n, const uint8_t* f, uint32_t len, uint32_t in_port);
 
   uint32_t burst_, inflight_, workers_, nq_, max_frames_;
@@ -478,6 +544,8 @@ class Engine {
   std::vector<std::unique_ptr<Queue>> queues_;
   mutable std::mutex ports_mu_;
   std::shared_ptr<const PortTab> ports_;              // copy-on-write snapshot, by port id
+  alignas(64) std::atomic<uint64_t> ports_ver_{0};    // bumped after every ports_ / cfg_ store
+  std::atomic<uint64_t> cfg_ver_{0};
   std::shared_ptr<RecircPort> recirc_;
   mutable std::mutex cfg_mu_;                         // writers of cfg_
   std::shared_ptr<const Cfg> cfg_;
@@ -486,13 +554,13 @@ class Engine {
   // thread that sees one acknowledges the current control epoch before idling
   std::atomic<uint32_t> pause_n_{0}, hold_n_{0};
   std::atomic<uint64_t> ctl_epoch_{0};
+  std::atomic<uint32_t> coalesce_frames_{64};
+  std::atomic<uint64_t> coalesce_ns_{0};
   mutable std::mutex err_mu_;
   std::string err_;
   std::mutex punt_mu_;
   std::deque<Punt> punts_;
   std::atomic<uint64_t> punt_drop_{0};
-  std::mutex lat_mu_;
-  std::vector<double> lat_us_;
   // learning: tx leaders -> learner thread -> every backend's MAC table + every side snapshot
   mutable std::mutex learn_mu_;
   std::condition_variable learn_cv_;

@@ -1112,6 +1112,10 @@ static hipError_t launch_fused_body(const FusedLaunch& f, const LaunchCfg& cfg, 
   const bool remote = f.nranks > 1 && !f.steer_list;   // steer list: the 1-GPU instances
   if (cfg.acl_mode == kAclMfma && (f.acl_tiles == 0 || f.acl_tiles > kAclMaxRules / 16)) return hipErrorInvalidValue;
   const int h = cfg.hash_mode, ac = cfg.acl_mode, cu = cfg.num_cus;
+#ifdef NFDP_HEADLINE_ONLY   // register-budget experiments: compile the headline instance alone
+  (void)h; (void)remote;
+  return launch_fused_t<kHashLds, kAclMfma, false, false>(a, cu, s);
+#else
   const bool early = ac == kAclMfma && !(f.flags & kFlagNoEarly) &&
                      (f.acl_tiles >= kEarlyAclTiles || (f.flags & kFlagForceEarly));
   if (f.t.n_acl6 || f.t.flow6_on) {   // IPv6 flows / rules: the V6 instances (1 GPU, MFMA ACL)
@@ -1144,6 +1148,7 @@ static hipError_t launch_fused_body(const FusedLaunch& f, const LaunchCfg& cfg, 
   NFDP_CASE(2, 0) NFDP_CASE(2, 1) NFDP_CASE(2, 2)
 #undef NFDP_CASE
   return hipErrorInvalidValue;
+#endif
 }
 
 hipError_t launch_gather(const uint8_t* recv, uint32_t nranks, uint32_t rank, uint32_t cap, uint32_t seg_bytes,

@@ -10,9 +10,11 @@
 // copies its 64-B header slot into the GPU ring and later bumps `tail` once the egress copy no
 // longer needs the payload (the frame stays in place while the GPU works on its header).
 //
-//   region  = [Hdr 64 B][Ctl ring 0 | Ctl ring 1, 128 B each][Desc ring 0][Desc ring 1]
-//             [buffers ring 0][buffers ring 1]
-//   ring 0  = pod -> data plane (the pod produces),  ring 1 = data plane -> pod (the engine produces)
+//   region  = [Hdr 64 B][Ctl ring 0 .. R, 128 B each][Desc ring 0 .. R][buffers ring 0 .. R]
+//   ring 0     = pod -> data plane (the pod produces)
+//   ring 1..R  = data plane -> pod (the engine produces; one ring per engine queue, as a NIC
+//                gives every queue its own tx ring: the queues' tx threads never share a ring,
+//                a lock or a cache line; the pod drains all R)
 //   slot i of a ring always uses buffer i (the consumer returns slots in order).
 //
 // Header-only, no HIP: the I/O engine, the pod-side endpoint and the standalone traffic tool
@@ -33,7 +35,8 @@ namespace nfdp {
 namespace memif {
 
 constexpr uint64_t kMagic = 0x4d49463335355846ull;   // "FX553FIM"
-constexpr uint32_t kVersion = 1;
+constexpr uint32_t kVersion = 2;
+constexpr uint32_t kMaxRxRings = 64;   // data plane -> pod rings (R)
 
 struct alignas(64) Hdr {
   uint64_t magic;
@@ -43,7 +46,8 @@ struct alignas(64) Hdr {
   uint32_t flags;
   uint8_t mac[8];          // the vport's MAC (informational, set by the data plane)
   std::atomic<uint32_t> peer_up;   // pod side attached (informational)
-  uint32_t pad[5];
+  uint32_t rx_rings;       // R: data plane -> pod rings
+  uint32_t pad[4];
 };
 static_assert(sizeof(Hdr) == 64, "memif Hdr");
 
@@ -60,28 +64,32 @@ struct Desc {
   uint32_t flags;
 };
 
-inline size_t region_bytes(uint32_t ring_size, uint32_t buf_size) {
-  return sizeof(Hdr) + 2 * sizeof(Ctl) + 2 * (size_t)ring_size * sizeof(Desc) + 2 * (size_t)ring_size * buf_size;
+inline size_t region_bytes(uint32_t ring_size, uint32_t buf_size, uint32_t rx_rings = 1) {
+  const size_t n = 1 + (size_t)rx_rings;
+  return sizeof(Hdr) + n * sizeof(Ctl) + n * (size_t)ring_size * sizeof(Desc) + n * (size_t)ring_size * buf_size;
 }
 
 // A mapped region (either side).  `create` sizes and initialises it; otherwise it attaches.
 class Region {
  public:
   Region() = default;
-  Region(const std::string& path, bool create, uint32_t ring_size = 1024, uint32_t buf_size = 2048) { open(path, create, ring_size, buf_size); }
+  Region(const std::string& path, bool create, uint32_t ring_size = 1024, uint32_t buf_size = 2048, uint32_t rx_rings = 1) {
+    open(path, create, ring_size, buf_size, rx_rings);
+  }
   ~Region() { close(); }
   Region(const Region&) = delete;
   Region& operator=(const Region&) = delete;
 
-  void open(const std::string& path, bool create, uint32_t ring_size, uint32_t buf_size) {
+  void open(const std::string& path, bool create, uint32_t ring_size, uint32_t buf_size, uint32_t rx_rings = 1) {
     if (create) {
+      if (rx_rings < 1 || rx_rings > kMaxRxRings) throw std::invalid_argument("memif: rx_rings must be in [1, 64]");
       if (ring_size < 2 || (ring_size & (ring_size - 1)) || ring_size > (1u << 20))
         throw std::invalid_argument("memif: ring_size must be a power of two in [2, 2^20]");
       if (buf_size < 64 || buf_size > (1u << 16) || (buf_size & 63))
         throw std::invalid_argument("memif: buf_size must be a multiple of 64 in [64, 65536]");
       fd_ = ::open(path.c_str(), O_RDWR | O_CREAT | O_TRUNC, 0600);
       if (fd_ < 0) throw std::runtime_error("memif: cannot create " + path);
-      bytes_ = region_bytes(ring_size, buf_size);
+      bytes_ = region_bytes(ring_size, buf_size, rx_rings);
       if (ftruncate(fd_, (off_t)bytes_) != 0) { close(); throw std::runtime_error("memif: ftruncate " + path); }
     } else {
       fd_ = ::open(path.c_str(), O_RDWR);
@@ -99,6 +107,7 @@ class Region {
       hdr()->version = kVersion;
       hdr()->ring_size = ring_size;
       hdr()->buf_size = buf_size;
+      hdr()->rx_rings = rx_rings;
       std::atomic_thread_fence(std::memory_order_release);
       hdr()->magic = kMagic;
     } else {
@@ -106,9 +115,11 @@ class Region {
       // against the mapping, and never look at the shared copy again
       ring_size = hdr()->ring_size;
       buf_size = hdr()->buf_size;
+      rx_rings = hdr()->rx_rings;
       std::atomic_thread_fence(std::memory_order_acquire);
       if (hdr()->magic != kMagic || hdr()->version != kVersion || ring_size < 2 || (ring_size & (ring_size - 1)) ||
-          ring_size > (1u << 20) || buf_size < 64 || buf_size > (1u << 16) || bytes_ < region_bytes(ring_size, buf_size)) {
+          ring_size > (1u << 20) || buf_size < 64 || buf_size > (1u << 16) || rx_rings < 1 || rx_rings > kMaxRxRings ||
+          bytes_ < region_bytes(ring_size, buf_size, rx_rings)) {
         close();
         throw std::runtime_error("memif: " + path + " is not a memif region");
       }
@@ -118,8 +129,9 @@ class Region {
     ring_size_ = ring_size;
     mask_ = ring_size - 1;
     buf_size_ = buf_size;
-    desc_base_ = base_ + sizeof(Hdr) + 2 * sizeof(Ctl);
-    buf_base_ = desc_base_ + 2 * (size_t)ring_size * sizeof(Desc);
+    nrings_ = 1 + rx_rings;
+    desc_base_ = base_ + sizeof(Hdr) + (size_t)nrings_ * sizeof(Ctl);
+    buf_base_ = desc_base_ + (size_t)nrings_ * ring_size * sizeof(Desc);
     path_ = path;
   }
   void close() {
@@ -137,17 +149,19 @@ class Region {
   uint32_t ring_size() const { return ring_size_; }
   uint32_t mask() const { return mask_; }
   uint32_t buf_size() const { return buf_size_; }
-  Ctl* ctl(int r) const { return reinterpret_cast<Ctl*>(base_ + sizeof(Hdr)) + (r & 1); }
-  Desc* desc(int r) const { return reinterpret_cast<Desc*>(desc_base_) + (size_t)(r & 1) * ring_size_; }
-  uint8_t* buf(int r, uint32_t slot) const {
-    return buf_base_ + ((size_t)(r & 1) * ring_size_ + (slot & mask_)) * buf_size_;
+  uint32_t rx_rings() const { return nrings_ - 1; }   // R
+  // ring r (0: pod -> data plane, 1..R: data plane -> pod); out-of-range indices wrap
+  Ctl* ctl(uint32_t r) const { return reinterpret_cast<Ctl*>(base_ + sizeof(Hdr)) + r % nrings_; }
+  Desc* desc(uint32_t r) const { return reinterpret_cast<Desc*>(desc_base_) + (size_t)(r % nrings_) * ring_size_; }
+  uint8_t* buf(uint32_t r, uint32_t slot) const {
+    return buf_base_ + ((size_t)(r % nrings_) * ring_size_ + (slot & mask_)) * buf_size_;
   }
 
  private:
   int fd_ = -1;
   uint8_t* base_ = nullptr;
   size_t bytes_ = 0;
-  uint32_t ring_size_ = 0, mask_ = 0, buf_size_ = 0;
+  uint32_t ring_size_ = 0, mask_ = 0, buf_size_ = 0, nrings_ = 2;
   uint8_t* desc_base_ = nullptr;
   uint8_t* buf_base_ = nullptr;
   std::string path_;
@@ -156,10 +170,10 @@ class Region {
 // Producer side of one ring: reserve -> fill buffer -> commit (batched head publication).
 struct Producer {
   const Region* r = nullptr;
-  int ring = 0;
+  uint32_t ring = 0;
   uint32_t head = 0;         // private copy (published with commit())
   uint32_t tail_cache = 0;   // last tail seen
-  void init(const Region* reg, int rg) {
+  void init(const Region* reg, uint32_t rg) {
     r = reg; ring = rg;
     head = r->ctl(rg)->head.load(std::memory_order_relaxed);
     tail_cache = r->ctl(rg)->tail.load(std::memory_order_acquire);
@@ -175,6 +189,7 @@ struct Producer {
     const uint32_t n = na + nb + nc;
     if (n > r->buf_size() || room() == 0) return false;
     uint8_t* dst = r->buf(ring, head);
+    __builtin_prefetch(r->buf(ring, head + 8), 1, 3);   // the buffers of later puts: ownership requested early
     if (na) std::memcpy(dst, a, na);
     if (nb) std::memcpy(dst + na, b, nb);
     if (nc) std::memcpy(dst + na + nb, c, nc);
@@ -190,11 +205,11 @@ struct Producer {
 // Consumer side of one ring.  `next` walks received frames; `release` hands slots back in order.
 struct Consumer {
   const Region* r = nullptr;
-  int ring = 0;
+  uint32_t ring = 0;
   uint32_t next = 0;         // next slot to read
   uint32_t head_cache = 0;
   uint32_t released = 0;     // slots below this went back to the producer
-  void init(const Region* reg, int rg) {
+  void init(const Region* reg, uint32_t rg) {
     r = reg; ring = rg;
     next = released = r->ctl(rg)->tail.load(std::memory_order_relaxed);
     head_cache = r->ctl(rg)->head.load(std::memory_order_acquire);
@@ -211,6 +226,7 @@ struct Consumer {
     const Desc& d = r->desc(ring)[next & r->mask()];
     len = d.len < r->buf_size() ? d.len : r->buf_size();
     const uint8_t* p = r->buf(ring, next);
+    __builtin_prefetch(r->buf(ring, next + 8), 0, 3);   // later frames' first line, fetched ahead
     ++next;
     return p;
   }

@@ -99,11 +99,12 @@ inline Result run(std::vector<Pod> pods, const Config& cfg) {
       std::vector<size_t> mine;
       for (size_t i = t; i < np; i += nth) mine.push_back(i);
       std::vector<memif::Producer> prod(mine.size());
-      std::vector<memif::Consumer> cons(mine.size());
+      std::vector<std::vector<memif::Consumer>> cons(mine.size());   // every data plane -> pod ring
       std::vector<uint32_t> cursor(mine.size(), 0);
       for (size_t k = 0; k < mine.size(); ++k) {
         prod[k].init(regs[mine[k]].get(), 0);
-        cons[k].init(regs[mine[k]].get(), 1);
+        cons[k].resize(regs[mine[k]]->rx_rings());
+        for (uint32_t r = 0; r < (uint32_t)cons[k].size(); ++r) cons[k][r].init(regs[mine[k]].get(), 1 + r);
         regs[mine[k]]->hdr()->peer_up.store(1);
       }
       ready.fetch_add(1);
@@ -141,6 +142,7 @@ inline Result run(std::vector<Pod> pods, const Config& cfg) {
             const uint32_t len = pd.lens[c];
             if (prod[k].room() == 0) { ++me.full; break; }
             uint8_t* dst = prod[k].r->buf(0, prod[k].head);
+            __builtin_prefetch(prod[k].r->buf(0, prod[k].head + 8), 1, 3);
             std::memcpy(dst, f, len);
             const uint32_t off = pd.ts_off[c];
             if (off) std::memcpy(dst + off, &ts, 8);
@@ -159,14 +161,14 @@ inline Result run(std::vector<Pod> pods, const Config& cfg) {
           }
         }
         // ---- rx: everything that arrived on this thread's pods
-        for (size_t k = 0; k < mine.size(); ++k) {
-          uint32_t avail = cons[k].available();
+        for (size_t k = 0; k < mine.size(); ++k) for (memif::Consumer& cn : cons[k]) {
+          uint32_t avail = cn.available();
           if (!avail) continue;
           const uint64_t trx = now_ns();
           uint32_t mine_rx = 0;   // frames of this run (a previous run's leftovers do not give credit back)
           for (uint32_t i = 0; i < avail; ++i) {
             uint32_t len = 0;
-            const uint8_t* f = cons[k].get(len);
+            const uint8_t* f = cn.get(len);
             const uint32_t off = ts_offset(f, len);
             uint64_t ts = 0;
             if (off) std::memcpy(&ts, f + off, 8);
@@ -179,7 +181,7 @@ inline Result run(std::vector<Pod> pods, const Config& cfg) {
               if (me.lat.size() < cfg.max_samples / nth + 1) me.lat.push_back((double)(trx - ts) * 1e-3);
             }
           }
-          cons[k].release_to(cons[k].next);
+          cn.release_to(cn.next);
           if (cfg.inflight) {
             outstanding.fetch_sub(mine_rx, std::memory_order_acq_rel);
             last_rx.store(trx, std::memory_order_relaxed);

@@ -208,6 +208,7 @@ NLM_F_REQUEST, NLM_F_ACK, NLM_F_EXCL, NLM_F_CREATE, NLM_F_DUMP = 1, 4, 0x200, 0x
 NLA_F_NESTED = 0x8000
 IFLA_ADDRESS, IFLA_IFNAME, IFLA_MTU, IFLA_LINKINFO, IFLA_IFALIAS = 1, 3, 4, 18, 20
 IFLA_VFINFO_LIST, IFLA_NET_NS_FD = 22, 28
+IFLA_MASTER = 10
 IFLA_INFO_KIND, IFLA_INFO_DATA, VETH_INFO_PEER = 1, 2, 1
 IFLA_VF_INFO = 1
 IFLA_VF_MAC, IFLA_VF_VLAN, IFLA_VF_SPOOFCHK, IFLA_VF_LINK_STATE, IFLA_VF_RATE, IFLA_VF_TRUST = 1, 2, 4, 5, 6, 9
@@ -445,6 +446,21 @@ class RtNetlink(NetlinkManager):
         def op():
             idx = self.link_by_name(name).index
             self._link_msg(RTM_DELLINK, NLM_F_ACK, idx)
+
+        in_netns(ns, op)
+
+    def link_add_bridge(self, name, ns=""):
+        """A Linux bridge netdev (`ip link add NAME type bridge`)."""
+        info = self._nest(IFLA_LINKINFO, self._attr(IFLA_INFO_KIND, b"bridge\0"))
+        attrs = self._attr(IFLA_IFNAME, name.encode() + b"\0") + info
+        in_netns(ns, lambda: self._link_msg(RTM_NEWLINK, NLM_F_ACK | NLM_F_CREATE | NLM_F_EXCL, attrs=attrs))
+
+    def link_set_master(self, name, master, ns=""):
+        """Enslave `name` to the bridge `master` (`ip link set NAME master MASTER`)."""
+        def op():
+            m = self.link_by_name(master).index
+            idx = self.link_by_name(name).index
+            self._link_msg(RTM_NEWLINK, NLM_F_ACK, idx, 0, 0, self._attr(IFLA_MASTER, struct.pack("I", m)))
 
         in_netns(ns, op)
 

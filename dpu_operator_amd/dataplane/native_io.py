@@ -48,13 +48,16 @@ SIDE_PORT_FLAGS = T.PORT_LEARN | T.PORT_ARP_TRAP | T.PORT_MIRROR
 
 class MemifVport:
     """A shared-memory vport (csrc/nfdp/memif.h): the data plane owns the region file; the pod
-    (or NF) side attaches to `path` (nf.MemifEndpoint, the trafgen tool, a DPDK memif-style app)."""
+    (or NF) side attaches to `path` (nf.MemifEndpoint, the trafgen tool, a DPDK memif-style app).
+    The region has one data-plane -> pod ring per engine queue (`tx_rings`, 0: the engine's
+    queue count), so the queues' tx threads never contend for a pod."""
 
-    def __init__(self, path: str, ring_size: int = 1024, buf_size: int = 2048):
+    def __init__(self, path: str, ring_size: int = 1024, buf_size: int = 2048, tx_rings: int = 0):
         self.path, self.ring_size, self.buf_size = path, int(ring_size), int(buf_size)
+        self.tx_rings = int(tx_rings)
 
-    def make(self, nf):
-        return nf.MemifPort(self.path, self.ring_size, self.buf_size)
+    def make(self, nf, queues: int = 1):
+        return nf.MemifPort(self.path, self.ring_size, self.buf_size, self.tx_rings or max(1, int(queues)))
 
 
 class PacketVport:
@@ -85,7 +88,7 @@ class PacketVport:
         vp._nl, vp.name = nl, name
         return vp
 
-    def make(self, nf):
+    def make(self, nf, queues: int = 1):
         return nf.PacketPort(self.ifname, self.frames, self.frame_size)
 
     def close(self) -> None:
@@ -107,9 +110,9 @@ def _quiet_ipv6(ifname: str) -> None:
         pass
 
 
-def _make_port(nf, spec):
+def _make_port(nf, spec, queues: int = 1):
     if hasattr(spec, "make"):
-        return spec.make(nf)
+        return spec.make(nf, queues)
     if hasattr(spec, "fd"):            # netio.TapPort and anything else with a packet fd
         return nf.FdPort(int(spec.fd))
     raise TypeError(f"unsupported vport {spec!r}")
@@ -118,11 +121,14 @@ def _make_port(nf, spec):
 class NativeLivePath:
     def __init__(self, dps, ports: dict, burst: int = 256, ring_capacity: int = 4096, inflight: int = 64,
                  on_punt=None, auto_restart: bool = True, tx_workers: int = 1, queues: int = 1,
-                 max_inflight_frames: int = 0, port_queues: dict | None = None):
+                 max_inflight_frames: int = 0, port_queues: dict | None = None, coalesce_us: float = 8.0,
+                 coalesce_frames: int = 64):
         """dps: one data plane or a list (one per GPU, or a MultiDataPlane's planes); ports:
         {port id: vport spec}; queues: rx threads (each with a ring queue on every GPU);
         port_queues: {port id: queue} (default: least loaded); max_inflight_frames: per lane
-        bound of the engine's own queueing (0: the ring capacity)."""
+        bound of the engine's own queueing (0: the ring capacity); coalesce_us / coalesce_frames:
+        with bursts of a lane in flight, frames gather into one publish until that many are read
+        or the oldest waited that long (an idle lane publishes at once)."""
         from ..native import nfdp
 
         self.nf = nfdp()
@@ -137,6 +143,7 @@ class NativeLivePath:
         self.burst, self.capacity, self.inflight = int(burst), int(ring_capacity), int(inflight)
         self.tx_workers, self.queues = int(tx_workers), int(queues)
         self.max_inflight_frames = int(max_inflight_frames)
+        self.coalesce_us, self.coalesce_frames = float(coalesce_us), int(coalesce_frames)
         self.specs = dict(ports)
         self.port_queues = dict(port_queues or {})
         self.on_punt = on_punt
@@ -167,6 +174,7 @@ class NativeLivePath:
     def _build(self) -> None:
         nf = self.nf
         eng = nf.IoEngine(self.burst, self.inflight, self.tx_workers, self.queues, self.max_inflight_frames)
+        eng.set_coalesce(self.coalesce_frames, self.coalesce_us)
         self._rings, self._backends = [], []
         for dp in self.dps:
             if self.gpu:
@@ -194,7 +202,7 @@ class NativeLivePath:
         for idx, spec in self.specs.items():
             p = self._ports.get(idx)
             if p is None:
-                p = self._ports[idx] = _make_port(nf, spec)
+                p = self._ports[idx] = _make_port(nf, spec, self.queues)
             eng.add_port(int(idx), p, int(self.port_queues.get(idx, -1)))
         eng.learn_stamp = max(int(getattr(d, "stamp", 0)) for d in self.dps) + 1
         self._eng = eng
@@ -310,7 +318,7 @@ class NativeLivePath:
             self.specs[idx] = spec
             if queue >= 0:
                 self.port_queues[idx] = queue
-            p = self._ports[idx] = _make_port(self.nf, spec)
+            p = self._ports[idx] = _make_port(self.nf, spec, self.queues)
             if self._eng is not None:
                 self._eng.add_port(int(idx), p, int(self.port_queues.get(idx, -1)))
 

@@ -78,6 +78,28 @@ def _newest_header(d: Path) -> float:
     return max(ts) if ts else 0.0
 
 
+def _newest_dep(src: Path) -> float:
+    """mtime of the newest local header `src` includes (transitively, `#include "x.h"` lines):
+    a header edit rebuilds only the sources that see it."""
+    import re
+
+    seen, todo, newest = set(), [src], 0.0
+    while todo:
+        f = todo.pop()
+        try:
+            text = f.read_text(errors="replace")
+        except OSError:
+            continue
+        for m in re.finditer(r'^\s*#\s*include\s+"([^"]+)"', text, re.M):
+            h = (f.parent / m.group(1)).resolve()
+            if h in seen or not h.exists():
+                continue
+            seen.add(h)
+            newest = max(newest, h.stat().st_mtime)
+            todo.append(h)
+    return newest
+
+
 # HIP sources whose kernels' register / spill / occupancy figures are recorded at build time
 # (compiler resource remarks -> <module>.resources.json next to the module; the spill guard test
 # tests/test_kernel_resources.py and tools/kernel_resources.py read them)
@@ -150,14 +172,13 @@ def build_module(name: str, force: bool = False, verbose: bool = False) -> Path:
     out = (Path(VARIANT_OUT) if VARIANT_OUT else HERE) / f"{name}{EXT}"
     out.parent.mkdir(parents=True, exist_ok=True)
     force = _flags_changed(name, spec["hip"]) or force
-    hdr = _newest_header(d)
     objs = []
     jobs = []
     for s in spec["sources"]:
         src = d / s
         obj = BUILD / name / (s + ".o")
         objs.append(obj)
-        stale = force or not obj.exists() or obj.stat().st_mtime < max(src.stat().st_mtime, hdr)
+        stale = force or not obj.exists() or obj.stat().st_mtime < max(src.stat().st_mtime, _newest_dep(src))
         if stale:
             jobs.append((src, obj))
     if jobs:

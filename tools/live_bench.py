@@ -4,7 +4,9 @@ Pods are shared-memory vports (csrc/nfdp/memif.h) driven by the C++ generator / 
 (csrc/nfdp/trafgen.h: every frame carries its send time, so one-way pod -> pod latency is read on
 one clock).  Between them: the native I/O engine and the headline pipeline (1M flows, 256-rule
 ACL -> SNAT -> L2 steer) on the persistent ring kernel of the GPU, or the C++ oracle on the CPU
-(`--device cpu`, the comparator: same I/O engine, CPU pipeline).
+(`--device cpu`, the comparator: same I/O engine, CPU pipeline), or nothing at all (`--backend wire`:
+a zero-cost pipeline that forwards every frame by destination MAC — the ceiling of the I/O engine
+and the pods themselves, what any pipeline behind the engine is held to).
 
 Measured, per device:
   * `mpps`          : aggregate frames delivered per second with every pod sending as fast as its
@@ -39,14 +41,14 @@ def _pct(x, q):
     return round(float(np.percentile(x, q)), 2) if len(x) else None
 
 
-def drain(nf, pods, live, quiet_s: float = 0.05, limit_s: float = 10.0) -> int:
+def drain(nf, pods, stats, quiet_s: float = 0.05, limit_s: float = 10.0) -> int:
     """Let the engine deliver what the previous phase left queued; empty the pods' rx rings."""
     eps = [nf.MemifEndpoint(p[0]) for p in pods]
     n, last, t_end = 0, time.perf_counter(), time.perf_counter() + limit_s
-    prev = live.stats.get("tx", 0)
+    prev = stats().get("tx", 0)
     while time.perf_counter() < t_end:
         k = sum(len(e.recv()) for e in eps)
-        cur = live.stats.get("tx", 0)
+        cur = stats().get("tx", 0)
         n += k
         if k or cur != prev:
             last, prev = time.perf_counter(), cur
@@ -56,41 +58,102 @@ def drain(nf, pods, live, quiet_s: float = 0.05, limit_s: float = 10.0) -> int:
     return n
 
 
+class _WireLive:
+    """The I/O engine over a zero-cost pipeline (nf.WireBackend): pods are port i, MAC 02:00:00:00:00:i+1."""
+
+    def __init__(self, nf, d: str, n_pods: int, burst: int, inflight: int, tx_workers: int, queues: int,
+                 max_inflight_frames: int, ring_capacity: int, pod_ring: int, coalesce_us: float):
+        self.eng = nf.IoEngine(burst, inflight, tx_workers, queues, max_inflight_frames)
+        self.eng.set_coalesce(64, coalesce_us)
+        macs = [(int.from_bytes(self.mac(i), "little"), i) for i in range(n_pods)]
+        self.eng.add_backend(nf.WireBackend(ring_capacity, queues, macs))
+        self.paths = [os.path.join(d, f"pod{i}") for i in range(n_pods)]
+        for i, p in enumerate(self.paths):
+            self.eng.add_port(i, nf.MemifPort(p, pod_ring, int(os.environ.get("WIRE_BUF", 2048)), queues))
+        self.eng.start()
+
+    @staticmethod
+    def mac(i: int) -> bytes:
+        return bytes([2, 0, 0, 0, 0, i + 1])
+
+    def frames(self, i: int, n_pods: int, k: int = 4096, seed: int = 0):
+        """k 60-B IPv4 / UDP frames from pod i to random other pods (distinct 5-tuples)."""
+        rng = np.random.default_rng(seed)
+        f = np.zeros((k, 64), np.uint8)
+        dst = (i + 1 + rng.integers(0, n_pods - 1, k)) % n_pods
+        for j in range(k):
+            d = int(dst[j])
+            f[j, 0:6] = np.frombuffer(self.mac(d), np.uint8)
+            f[j, 6:12] = np.frombuffer(self.mac(i), np.uint8)
+            f[j, 12:14] = (8, 0)
+            f[j, 14:24] = (0x45, 0, 0, 46, 0, 0, 0, 0, 64, 17)
+            f[j, 26:30] = (10, 0, 0, i + 1)
+            f[j, 30:34] = (10, 0, 0, d + 1)
+            f[j, 34:38] = (0x10, (j >> 8) & 0xFF, 0x00, 0x50 + (j & 0x0F))
+            f[j, 38:40] = (0, 26)
+        return f, np.full(k, 60, np.uint32)
+
+    @property
+    def stats(self) -> dict:
+        return dict(self.eng.stats())
+
+    def latency_us(self):
+        return np.asarray(self.eng.take_latency_us())
+
+    @property
+    def error(self):
+        return self.eng.error() or None
+
+    def stop(self):
+        self.eng.stop()
+
+
 def run(device: str = "cuda", n_pods: int = 8, flows: int = 1 << 20, n_acl: int = 256, duration: float = 1.0,
         threads: int = 4, burst: int = 512, inflight: int = 64, ring_capacity: int = 16384,
         hash_mode: str = "lds", tx_workers: int = 1, queues: int = 4, max_inflight_frames: int = 4096,
-        pod_ring: int = 1024) -> dict:
+        pod_ring: int = 1024, backend: str = "pipeline", coalesce_us: float = 8.0) -> dict:
     nf = nfdp()
     t0 = time.perf_counter()
-    dp = DataPlane(device=device, flow_buckets=max(1 << 12, 1 << int(np.ceil(np.log2(max(flows, 1) / 2)))),
-                   hash_mode=hash_mode if device != "cpu" else "mfma")
-    sc = S.build_sfc(dp, n_pods=n_pods, n_flows=flows, n_acl=n_acl, seed=0)
-    dp.commit(full=True)
     d = tempfile.mkdtemp(prefix="dpu-live-", dir=memif_dir())
-    ports = {int(sc.pod_port[i]): MemifVport(os.path.join(d, f"pod{i}"), ring_size=pod_ring) for i in range(n_pods)}
-    live = NativeLivePath(dp, ports, burst=burst, ring_capacity=ring_capacity, inflight=inflight,
-                          tx_workers=tx_workers, queues=queues, max_inflight_frames=max_inflight_frames).start()
-    setup_s = time.perf_counter() - t0
-    try:
-        pods = []
+    pods = []
+    if backend == "wire":
+        live = _WireLive(nf, d, n_pods, burst, inflight, tx_workers, queues, max_inflight_frames, ring_capacity,
+                         pod_ring, coalesce_us)
+        for i in range(n_pods):
+            fr, ln = live.frames(i, n_pods, seed=100 + i)
+            pods.append((live.paths[i], fr, ln))
+        device, flows, n_acl = "none", n_pods * 4096, 0
+    else:
+        dp = DataPlane(device=device, flow_buckets=max(1 << 12, 1 << int(np.ceil(np.log2(max(flows, 1) / 2)))),
+                       hash_mode=hash_mode if device != "cpu" else "mfma")
+        sc = S.build_sfc(dp, n_pods=n_pods, n_flows=flows, n_acl=n_acl, seed=0)
+        dp.commit(full=True)
+        ports = {int(sc.pod_port[i]): MemifVport(os.path.join(d, f"pod{i}"), ring_size=pod_ring) for i in range(n_pods)}
+        live = NativeLivePath(dp, ports, burst=burst, ring_capacity=ring_capacity, inflight=inflight,
+                              tx_workers=tx_workers, queues=queues, max_inflight_frames=max_inflight_frames,
+                              coalesce_us=coalesce_us).start()
         for i in range(n_pods):
             slots, im = S.traffic(sc, 4096, seed=100 + i, src_pods=np.array([i]))
             pods.append((ports[int(sc.pod_port[i])].path, slots, (im >> 16).astype(np.uint32)))
-        out = {"device": device, "queues": queues, "tx_workers": tx_workers, "inflight_bursts": inflight,
+        flows = int(len(sc.keys))
+    setup_s = time.perf_counter() - t0
+    stats = lambda: live.stats  # noqa: E731
+    try:
+        out = {"backend": backend, "device": device, "queues": queues, "coalesce_us": coalesce_us, "tx_workers": tx_workers, "inflight_bursts": inflight,
                "max_inflight_frames": max_inflight_frames, "pod_ring": pod_ring, "gen_threads": threads,
-               "pods": n_pods, "flows": int(len(sc.keys)), "acl_rules": n_acl, "frame_bytes": 64,
+               "pods": n_pods, "flows": flows, "acl_rules": n_acl, "frame_bytes": 64,
                "setup_s": round(setup_s, 1)}
         # saturated: every pod as fast as its vport takes frames
         r = nf.trafgen_run(pods, duration_s=duration, warmup_s=0.2, threads=threads, burst=32)
         mpps = r["received"] / duration / 1e6
         out.update(mpps=round(mpps, 3), offered_mpps=round(r["sent"] / duration / 1e6, 3),
                    p50_us=_pct(r["lat_us"], 50), p99_us=_pct(r["lat_us"], 99))
-        drain(nf, pods, live)
+        drain(nf, pods, stats)
         # unloaded: closed loop, one frame in flight
         r1 = nf.trafgen_run(pods, duration_s=min(duration, 0.5), warmup_s=0.05, threads=1, burst=1, inflight=1)
         out.update(idle_p50_us=_pct(r1["lat_us"], 50), idle_p99_us=_pct(r1["lat_us"], 99),
                    idle_frames=int(r1["received"]))
-        drain(nf, pods, live)
+        drain(nf, pods, stats)
         # offered loads below saturation: 90 % and 50 % of the measured maximum
         if mpps > 0:
             for tag, frac in (("load90", 0.9), ("half", 0.5)):
@@ -98,7 +161,7 @@ def run(device: str = "cuda", n_pods: int = 8, flows: int = 1 << 20, n_acl: int 
                                     rate_pps=frac * mpps * 1e6)
                 out.update({f"{tag}_mpps": round(r2["received"] / min(duration, 0.5) / 1e6, 3),
                             f"{tag}_p50_us": _pct(r2["lat_us"], 50), f"{tag}_p99_us": _pct(r2["lat_us"], 99)})
-                drain(nf, pods, live)
+                drain(nf, pods, stats)
             out["half_load_mpps"] = out.pop("half_mpps")
         st = live.stats
         out["engine"] = {k: int(v) for k, v in st.items() if k in ("rx", "tx", "drop", "bursts", "tx_full",
@@ -134,10 +197,13 @@ def main() -> None:
     ap.add_argument("--queues", type=int, default=4)
     ap.add_argument("--max-inflight-frames", type=int, default=4096)
     ap.add_argument("--pod-ring", type=int, default=1024)
+    ap.add_argument("--backend", choices=("pipeline", "wire"), default="pipeline")
+    ap.add_argument("--coalesce-us", type=float, default=8.0)
     a = ap.parse_args()
     print(json.dumps(run(a.device, a.pods, a.flows, duration=a.duration, threads=a.threads, burst=a.burst,
                          inflight=a.inflight, tx_workers=a.tx_workers, queues=a.queues,
-                         max_inflight_frames=a.max_inflight_frames, pod_ring=a.pod_ring)), flush=True)
+                         max_inflight_frames=a.max_inflight_frames, pod_ring=a.pod_ring,
+                         backend=a.backend, coalesce_us=a.coalesce_us)), flush=True)
 
 
 if __name__ == "__main__":
