@@ -329,3 +329,28 @@ def test_memif_tx_rings_per_queue(shm):
             assert seq == list(range(20))
     finally:
         eng.stop()
+
+
+def test_coalescing_never_delays_an_idle_lane(shm):
+    """Publication coalescing (Engine::set_coalesce) gathers frames only while bursts of the lane
+    are in flight: with a one-second window, single frames on an idle engine still come out at
+    once, every one of them."""
+    nf = nfdp()
+    eng = nf.IoEngine(64, 8, 1, 1, 0)
+    eng.set_coalesce(64, 1e6)
+    eng.add_backend(nf.WireBackend(256, 1, [(int.from_bytes(bytes([2, 0, 0, 0, 0, 1]), "little"), 0)]))
+    dst = nf.MemifPort(str(shm / "d"), 64, 2048, 1)
+    src = nf.MemifPort(str(shm / "s"), 64, 2048, 1)
+    eng.add_port(0, dst)
+    eng.add_port(1, src)
+    eng.start()
+    try:
+        a, b = nf.MemifEndpoint(str(shm / "s")), nf.MemifEndpoint(str(shm / "d"))
+        for i in range(20):
+            t0 = time.perf_counter()
+            assert a.send([bytes([2, 0, 0, 0, 0, 1, 2, 0, 0, 0, 0, 9, 0x88, 0xB5, i]) + bytes(45)]) == 1
+            got = _until(lambda: b.recv(), t=0.5)
+            assert got and got[0][14] == i
+            assert time.perf_counter() - t0 < 0.25      # far below the 1 s window
+    finally:
+        eng.stop()

@@ -201,3 +201,22 @@ def test_daemon_allocates_veth_vports_and_pods_ping_through_the_native_path(pm):
         gvsp.stop_live()
         for ns in pods:
             NS.delete_netns(ns)
+
+
+@pytest.mark.parametrize("mode", ["linux-bridge", "engine"])
+def test_veth_comparator_same_generator(mode):
+    """tools/live_bench.py --veth: netns pods on veth pairs driven by the C++ generator / sink
+    (trafgen_pkt.h, AF_PACKET rings opened inside each namespace), switched by a Linux bridge
+    (the comparator) or by the native engine; every measured frame carries a valid send time and
+    the report has loaded / half-load / idle latency."""
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location(
+        "live_bench", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "live_bench.py"))
+    lb = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(lb)
+    r = lb.run_veth(mode, n_pods=3, duration=0.2, threads=1, queues=1)
+    assert r["switch"] == mode and r["mpps"] > 0 and r["p50_us"] is not None
+    assert r["half_p99_us"] is not None and r["idle_p50_us"] is not None
+    if mode == "engine":
+        assert r["error"] is None and r["engine"]["rx"] > 0

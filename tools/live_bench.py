@@ -91,6 +91,11 @@ class _WireLive:
             f[j, 30:34] = (10, 0, 0, d + 1)
             f[j, 34:38] = (0x10, (j >> 8) & 0xFF, 0x00, 0x50 + (j & 0x0F))
             f[j, 38:40] = (0, 26)
+            w = f[j, 14:34].astype(np.uint32)
+            c = int(np.sum((w[0::2] << 8) | w[1::2]))
+            c = (c & 0xFFFF) + (c >> 16)
+            c = ~((c & 0xFFFF) + (c >> 16)) & 0xFFFF
+            f[j, 24:26] = (c >> 8, c & 0xFF)       # a valid IPv4 header (a kernel bridge checks it)
         return f, np.full(k, 60, np.uint32)
 
     @property
@@ -184,6 +189,93 @@ def run(device: str = "cuda", n_pods: int = 8, flows: int = 1 << 20, n_acl: int 
         shutil.rmtree(d, ignore_errors=True)
 
 
+def run_veth(mode: str = "linux-bridge", n_pods: int = 4, duration: float = 1.0, threads: int = 2,
+             queues: int = 2, tx_workers: int = 1, burst: int = 256, inflight: int = 64, ring_capacity: int = 16384,
+             max_inflight_frames: int = 4096, coalesce_us: float = 8.0) -> dict:
+    """Kernel-netdev pods: every pod a network namespace holding one end of a veth pair, driven by
+    the same C++ generator / sink through AF_PACKET rings opened inside the namespace
+    (csrc/nfdp/trafgen_pkt.h).  The host ends go either to a Linux bridge (`linux-bridge`: the
+    kernel's own L2 switch, the comparator) or to the native I/O engine as PacketPorts over the
+    zero-cost wire pipeline (`engine`), so both switch identical pods with identical frames."""
+    from dpu_operator_amd.cni.netlink import RtNetlink, create_netns, delete_netns
+
+    nf = nfdp()
+    nl = RtNetlink()
+    tag = f"{os.getpid() % 10000}"
+    br = f"lbbr{tag}"
+    nss, hosts, eng = [], [], None   # (IPv6 autoconfiguration frames of the pods count as `bad`)
+    wire = _WireLive.__new__(_WireLive)
+    try:
+        if mode == "linux-bridge":
+            nl.link_add_bridge(br)
+            nl.link_set_up(br)
+        for i in range(n_pods):
+            pod, host = f"lb{tag}p{i}", f"lb{tag}p{i}d"
+            nl.link_add_veth(pod, host)
+            hosts.append(host)
+            ns = create_netns(f"/var/run/netns/lb{tag}-{i}")
+            nss.append(ns)
+            nl.link_set_hw_addr(pod, ":".join(f"{b:02x}" for b in _WireLive.mac(i)))
+            nl.link_set_ns(pod, ns)
+            nl.link_set_up(pod, ns)
+            if mode == "linux-bridge":
+                nl.link_set_master(host, br)
+            nl.link_set_up(host)
+        if mode == "engine":
+            eng = nf.IoEngine(burst, inflight, tx_workers, queues, max_inflight_frames)
+            eng.set_coalesce(64, coalesce_us)
+            macs = [(int.from_bytes(_WireLive.mac(i), "little"), i) for i in range(n_pods)]
+            eng.add_backend(nf.WireBackend(ring_capacity, queues, macs))
+            for i, h in enumerate(hosts):
+                eng.add_port(i, nf.PacketPort(h, 2048, 2048))
+            eng.start()
+        pods = []
+        for i in range(n_pods):
+            fr, ln = wire.frames(i, n_pods, k=1024, seed=100 + i)
+            pods.append((nss[i], f"lb{tag}p{i}", fr, ln))
+        out = {"vports": "veth", "switch": mode, "pods": n_pods, "gen_threads": threads, "frame_bytes": 64}
+        if mode == "engine":
+            out.update(queues=queues, coalesce_us=coalesce_us)
+        # warm-up (the bridge learns every MAC), then saturated
+        nf.trafgen_run_netns(pods, duration_s=0.2, warmup_s=0.0, threads=threads, burst=32)
+        time.sleep(0.1)
+        r = nf.trafgen_run_netns(pods, duration_s=duration, warmup_s=0.2, threads=threads, burst=32)
+        mpps = r["received"] / duration / 1e6
+        out.update(mpps=round(mpps, 3), offered_mpps=round(r["sent"] / duration / 1e6, 3),
+                   p50_us=_pct(r["lat_us"], 50), p99_us=_pct(r["lat_us"], 99), bad=int(r["bad"]))
+        time.sleep(0.1)
+        for tag_, frac in (("load90", 0.9), ("half", 0.5)):
+            r2 = nf.trafgen_run_netns(pods, duration_s=min(duration, 0.5), warmup_s=0.1, threads=threads, burst=8,
+                                      rate_pps=frac * mpps * 1e6)
+            out.update({f"{tag_}_mpps": round(r2["received"] / min(duration, 0.5) / 1e6, 3),
+                        f"{tag_}_p50_us": _pct(r2["lat_us"], 50), f"{tag_}_p99_us": _pct(r2["lat_us"], 99)})
+            time.sleep(0.1)
+        # unloaded: a slow trickle (1 kpps): no queueing anywhere
+        r3 = nf.trafgen_run_netns(pods, duration_s=min(duration, 0.5), warmup_s=0.05, threads=1, burst=1,
+                                  rate_pps=1000.0)
+        out.update(idle_p50_us=_pct(r3["lat_us"], 50), idle_p99_us=_pct(r3["lat_us"], 99))
+        if eng is not None:
+            st = dict(eng.stats())
+            out["engine"] = {k: int(st.get(k, 0)) for k in ("rx", "tx", "drop", "bursts", "tx_full")}
+            out["error"] = eng.error() or None
+        return out
+    finally:
+        if eng is not None:
+            eng.stop()
+        for ns in nss:
+            delete_netns(ns)
+        for h in hosts:
+            try:
+                nl.link_del(h)
+            except Exception:  # noqa: BLE001 - went with its namespace peer
+                pass
+        if mode == "linux-bridge":
+            try:
+                nl.link_del(br)
+            except Exception:  # noqa: BLE001
+                pass
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--device", default="cuda")
@@ -199,7 +291,13 @@ def main() -> None:
     ap.add_argument("--pod-ring", type=int, default=1024)
     ap.add_argument("--backend", choices=("pipeline", "wire"), default="pipeline")
     ap.add_argument("--coalesce-us", type=float, default=8.0)
+    ap.add_argument("--veth", choices=("linux-bridge", "engine"), default=None,
+                    help="netns pods on veth pairs, switched by a Linux bridge or by the native engine")
     a = ap.parse_args()
+    if a.veth:
+        print(json.dumps(run_veth(a.veth, n_pods=min(a.pods, 8), duration=a.duration, threads=min(a.threads, a.pods),
+                                  queues=a.queues, tx_workers=a.tx_workers, coalesce_us=a.coalesce_us)), flush=True)
+        return
     print(json.dumps(run(a.device, a.pods, a.flows, duration=a.duration, threads=a.threads, burst=a.burst,
                          inflight=a.inflight, tx_workers=a.tx_workers, queues=a.queues,
                          max_inflight_frames=a.max_inflight_frames, pod_ring=a.pod_ring,
