@@ -753,9 +753,20 @@ NFDP_HD int mac_lookup(const TablesView& t, uint32_t bridge, uint32_t lo, uint32
   return -1;
 }
 
+// The ACL key is the flow key with two port-class bits added to its meta word: "source port >=
+// 1024" and "destination port >= 1024".  The range [1024, 65535] (the unprivileged / ephemeral
+// ports, the most common range of real ACLs) is then ONE ternary entry instead of the six
+// prefixes of a TCAM range expansion (AclTable.add).  Ports are raw (network order): a port's
+// high byte is the low byte of its half, and port >= 1024 <=> high byte >= 4.  Never part of a
+// flow key (bits 10 / 11 of meta are zero in every flow key and packet key).
+constexpr uint32_t kAclSportHi = 0x400u, kAclDportHi = 0x800u;
+NFDP_HD uint32_t acl_key_meta(uint32_t ports, uint32_t meta) {
+  return meta | ((ports & 0xFCu) ? kAclSportHi : 0u) | ((ports & 0xFC0000u) ? kAclDportHi : 0u);
+}
+
 // Scalar ACL (priority order, first match).  Returns rule index or -1.
 NFDP_HD int acl_first_match(const TablesView& t, const FlowKey& k) {
-  const uint32_t w[4] = {k.src_ip, k.dst_ip, k.ports, k.meta};
+  const uint32_t w[4] = {k.src_ip, k.dst_ip, k.ports, acl_key_meta(k.ports, k.meta)};
   for (uint32_t r = 0; r < t.n_acl; ++r) {
     bool m = true;
     for (int i = 0; i < 4; ++i) m = m && ((w[i] ^ t.acl_value[4 * r + i]) & t.acl_mask[4 * r + i]) == 0;

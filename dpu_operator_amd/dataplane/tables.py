@@ -137,6 +137,17 @@ def flow_key(src_ip, dst_ip, sport=0, dport=0, proto=17, zone=0) -> np.ndarray:
 
 
 KEY_V6 = 0x200   # FlowKey.meta bit of an IPv6 key (nfdp.h kKeyV6)
+# ACL key port-class bits (nfdp.h acl_key_meta): meta of the ACL key only, never of a flow key
+ACL_SPORT_HI, ACL_DPORT_HI = 0x400, 0x800
+
+
+def acl_key(keys: np.ndarray) -> np.ndarray:
+    """Flow keys uint32[n, 4] -> the ACL keys the TCAM matches (port-class bits added to meta)."""
+    k = np.array(keys, np.uint32, copy=True).reshape(-1, 4)
+    ports = k[:, 2]
+    k[:, 3] |= np.where(ports & np.uint32(0xFC), np.uint32(ACL_SPORT_HI), np.uint32(0))
+    k[:, 3] |= np.where(ports & np.uint32(0xFC0000), np.uint32(ACL_DPORT_HI), np.uint32(0))
+    return k
 SLOT_USED = 0x100
 
 
@@ -1029,12 +1040,20 @@ class AclTable:
             base_v[3] |= np.uint32((zone & 0xFFFF) << 16)
             base_m[3] |= np.uint32(0xFFFF0000)
 
+        def ports4(p, hi_bit):
+            # [1024, 65535]: one entry on the ACL key's port-class bit (nfdp.h acl_key_meta)
+            if isinstance(p, tuple) and (int(p[0]), int(p[1])) == (1024, 0xFFFF):
+                return [(0, 0, hi_bit)]
+            return [(v, m, 0) for v, m in prefixes(p)]
+
         idx = []
-        for sv, sm in prefixes(sport):
-            for dv, dm in prefixes(dport):
+        for sv, sm, sf in ports4(sport, ACL_SPORT_HI):
+            for dv, dm, df in ports4(dport, ACL_DPORT_HI):
                 v, m = base_v.copy(), base_m.copy()
                 v[2] = port_raw(np.uint32(sv)) | (port_raw(np.uint32(dv)) << np.uint32(16))
                 m[2] = port_raw(np.uint32(sm)) | (port_raw(np.uint32(dm)) << np.uint32(16))
+                v[3] |= np.uint32(sf | df)
+                m[3] |= np.uint32(sf | df)
                 idx.append(self.add_raw(v, m, permit))
         return idx
 

@@ -296,7 +296,13 @@ def test_other_hops(hops):
 
 
 def _first_match_deny(rules, keys, default_permit=True):
-    """Independent TCAM model: first rule with key & mask == value decides (numpy, no nfdp)."""
+    """Independent TCAM model: first rule with key & mask == value decides (numpy, no nfdp).  The
+    TCAM key is the flow key plus the port-class bits (meta bit 10: source port >= 1024, bit 11:
+    destination port >= 1024), derived here from the host-order ports."""
+    keys = np.array(keys, np.uint32, copy=True)
+    sport = ((keys[:, 2] & 0xFF) << 8) | ((keys[:, 2] >> 8) & 0xFF)
+    dport = (((keys[:, 2] >> 16) & 0xFF) << 8) | (keys[:, 2] >> 24)
+    keys[:, 3] |= np.where(sport >= 1024, 0x400, 0).astype(np.uint32) | np.where(dport >= 1024, 0x800, 0).astype(np.uint32)
     val = np.stack([r.value for r in rules]).astype(np.uint32)
     msk = np.stack([r.mask for r in rules]).astype(np.uint32)
     per = np.array([r.permit for r in rules])

@@ -49,9 +49,11 @@ def _model(frame: bytes, in_port: int, ln: int, sc, flows: dict, acl, default_pe
     act = flows.get((src, dst, sport, dport))
     if act is None:
         return NOROUTE, T.PORT_PUNT, None      # no flow, GW MAC unknown on the bridge: slow path
-    # ACL over the 128-bit key: the frame's address / port bytes as little-endian words + proto | zone
+    # ACL over the 128-bit key: the frame's address / port bytes as little-endian words + proto |
+    # zone, with the port-class bits (meta bit 10: sport >= 1024, bit 11: dport >= 1024)
+    pcls = (0x400 if sport >= 1024 else 0) | (0x800 if dport >= 1024 else 0)
     words = np.array([int.from_bytes(src, "little"), int.from_bytes(dst, "little"),
-                      int.from_bytes(bytes(u[34:38]), "little"), u[23] | (sc.bridge << 16)], np.uint64)
+                      int.from_bytes(bytes(u[34:38]), "little"), u[23] | (sc.bridge << 16) | pcls], np.uint64)
     permit = default_permit
     for value, mask, rule_permit in acl:
         if ((words & mask) == value).all():

@@ -193,11 +193,13 @@ def test_vxlan_egress_side_pass_per_burst_and_redirect_cleared(shm):
         live.stop()
 
 
-def test_multi_plane_native_matches_one_plane(shm):
-    """Two oracle planes behind one engine with two queues (RSS owner steering in each rx thread):
-    the frames and summed counters equal a single plane's."""
+@pytest.mark.parametrize("devices", [["cpu", "cpu"], pytest.param(["cuda:0", "cuda:0"], marks=pytest.mark.gpu)])
+def test_multi_plane_native_matches_one_plane(shm, devices):
+    """Two planes behind one engine with two queues (RSS owner steering in each rx thread): the
+    frames and summed counters equal a single plane's.  On a GPU box both planes are ring kernels
+    of the same MI355X (two lanes per queue on one device: the multi-GPU code path on one card)."""
     nf = nfdp()
-    m = MultiDataPlane(["cpu", "cpu"], flow_buckets=1 << 12)
+    m = MultiDataPlane(devices, flow_buckets=1 << 12)
     sc = S.build_sfc(m, n_pods=6, n_flows=4096, n_acl=64, seed=0)
     m.commit(full=True)
     ref, _, _ = _sfc()
