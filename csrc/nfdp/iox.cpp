@@ -1116,11 +1116,13 @@ void Engine::deliver(Queue* Q, Lane* L, Burst& b, uint32_t w, const Cfg& c, cons
     v.push_back(it);
   };
   const uint32_t np = (uint32_t)b.pkts.size();
+  const uint32_t nw = workers_;
+  auto mine = [&](uint32_t port) { return nw == 1 || port % nw == w; };   // no division with one worker
   constexpr uint32_t kAhead = 8;   // out slots of later packets are fetched ahead
   for (uint32_t i = 0; i < np; ++i) {
     if (i + kAhead < np) {
       const uint32_t pa = (uint32_t)((b.start + i + kAhead) & cmask);
-      if (route(meta_port(om[pa])) % workers_ == w) __builtin_prefetch(be.out_slot(q, pa), 0, 0);
+      if (mine(route(meta_port(om[pa])))) __builtin_prefetch(be.out_slot(q, pa), 0, 0);
     }
     const Pkt& pk = b.pkts[i];
     const uint32_t pos = (uint32_t)((b.start + i) & cmask);
@@ -1128,7 +1130,7 @@ void Engine::deliver(Queue* Q, Lane* L, Burst& b, uint32_t w, const Cfg& c, cons
     const uint32_t reason = meta_reason(meta), oport = meta_port(meta), olen = meta_len(meta);
     if (reason == 0) {
       const uint32_t dst = route(oport);
-      if (dst % workers_ != w) continue;
+      if (!mine(dst)) continue;
       const uint8_t* x = nullptr;
       uint32_t xl = 0;
       if (meta & kMetaXhdr) {
@@ -1162,7 +1164,7 @@ void Engine::deliver(Queue* Q, Lane* L, Burst& b, uint32_t w, const Cfg& c, cons
       if (w == 0) punt(Q->wst[w], pk.port, rr, r.hdr, hl, pk.data + to, pk.len - to);   // ARP trap: the slow path's copy
     } else {
       const uint32_t dst = route(meta_port(r.meta));
-      if (dst % workers_ == w) {
+      if (mine(dst)) {
         add(dst, TxItem{nullptr, 0, r.hdr, hl, pk.data + to, pk.len - to});
         ++tally.reps;
       }

@@ -11,7 +11,9 @@ and the pods themselves, what any pipeline behind the engine is held to).
 Measured, per device:
   * `mpps`          : aggregate frames delivered per second with every pod sending as fast as its
                       vport accepts (64-B frames, 8 pods, random pod -> pod flows);
-  * `p50/p99_us`    : one-way latency of that saturated run (queueing included);
+  * `p50/p99_us`    : one-way latency of that saturated run (queueing in the pod rings included);
+  * `loaded_*`      : closed loop with `loaded_window` frames in flight: saturated throughput with
+                      the queueing bounded (the loaded latency);
   * `idle_p50/p99`  : closed loop, one frame in flight (the unloaded pod -> pod latency);
   * `load90_*`, `half_*` : offered load at 90 % / 50 % of the measured maximum.
 
@@ -116,7 +118,7 @@ class _WireLive:
 def run(device: str = "cuda", n_pods: int = 8, flows: int = 1 << 20, n_acl: int = 256, duration: float = 1.0,
         threads: int = 4, burst: int = 512, inflight: int = 64, ring_capacity: int = 16384,
         hash_mode: str = "lds", tx_workers: int = 1, queues: int = 4, max_inflight_frames: int = 4096,
-        pod_ring: int = 1024, backend: str = "pipeline", coalesce_us: float = 8.0) -> dict:
+        pod_ring: int = 1024, backend: str = "pipeline", coalesce_us: float = 8.0, loaded_window: int = 2048) -> dict:
     nf = nfdp()
     t0 = time.perf_counter()
     d = tempfile.mkdtemp(prefix="dpu-live-", dir=memif_dir())
@@ -153,6 +155,13 @@ def run(device: str = "cuda", n_pods: int = 8, flows: int = 1 << 20, n_acl: int 
         mpps = r["received"] / duration / 1e6
         out.update(mpps=round(mpps, 3), offered_mpps=round(r["sent"] / duration / 1e6, 3),
                    p50_us=_pct(r["lat_us"], 50), p99_us=_pct(r["lat_us"], 99))
+        drain(nf, pods, stats)
+        # loaded, closed loop: `loaded_window` frames in flight over all pods (the generator
+        # refills as frames arrive): the throughput of a saturated path with its queueing bounded
+        # by the window, not by the pod rings (one-way latency = window / rate, Little's law)
+        rl = nf.trafgen_run(pods, duration_s=duration, warmup_s=0.2, threads=threads, burst=32, inflight=loaded_window)
+        out.update(loaded_window=loaded_window, loaded_mpps=round(rl["received"] / duration / 1e6, 3),
+                   loaded_p50_us=_pct(rl["lat_us"], 50), loaded_p99_us=_pct(rl["lat_us"], 99))
         drain(nf, pods, stats)
         # unloaded: closed loop, one frame in flight
         r1 = nf.trafgen_run(pods, duration_s=min(duration, 0.5), warmup_s=0.05, threads=1, burst=1, inflight=1)
@@ -291,6 +300,7 @@ def main() -> None:
     ap.add_argument("--pod-ring", type=int, default=1024)
     ap.add_argument("--backend", choices=("pipeline", "wire"), default="pipeline")
     ap.add_argument("--coalesce-us", type=float, default=8.0)
+    ap.add_argument("--loaded-window", type=int, default=2048, help="frames in flight of the closed-loop loaded run")
     ap.add_argument("--veth", choices=("linux-bridge", "engine"), default=None,
                     help="netns pods on veth pairs, switched by a Linux bridge or by the native engine")
     a = ap.parse_args()
@@ -301,7 +311,7 @@ def main() -> None:
     print(json.dumps(run(a.device, a.pods, a.flows, duration=a.duration, threads=a.threads, burst=a.burst,
                          inflight=a.inflight, tx_workers=a.tx_workers, queues=a.queues,
                          max_inflight_frames=a.max_inflight_frames, pod_ring=a.pod_ring,
-                         backend=a.backend, coalesce_us=a.coalesce_us)), flush=True)
+                         backend=a.backend, coalesce_us=a.coalesce_us, loaded_window=a.loaded_window)), flush=True)
 
 
 if __name__ == "__main__":
