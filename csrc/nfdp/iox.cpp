@@ -980,6 +980,10 @@ void Engine::rx_loop(Queue* Q) {
         for (uint32_t i = 0; i < k; ++i) {
           const Pkt& pk = L->stage[i];
           uint8_t* slot = be.in_slot(q, (uint32_t)(start + i));
+          if (i + 4 < k) {   // later slots' lines (last written by the GPU) and frames, requested early
+            __builtin_prefetch(be.in_slot(q, (uint32_t)(start + i + 4)), 1, 3);
+            __builtin_prefetch(L->stage[i + 4].data, 0, 3);
+          }
           const uint32_t h = std::min<uint32_t>(pk.len, kSlotBytes);
           std::memcpy(slot, pk.data, h);
           if (h < kSlotBytes) std::memset(slot + h, 0, kSlotBytes - h);
