@@ -57,13 +57,20 @@ inline uint64_t now_ns() {
 }
 
 // Byte offset of the timestamp: right after the L4 header (UDP 8 B, TCP 20 B) of an IPv4 frame,
-// after a 802.1Q tag if present; 0 when the frame is too short / not IPv4.
-inline uint32_t ts_offset(const uint8_t* f, uint32_t len) {
+// after a 802.1Q tag if present; 0 when the frame is too short / not IPv4.  A VXLAN frame (outer
+// IPv4 / UDP to 4789) carries it in its inner frame: a pod behind a VTEP receives the encapsulated
+// copy of what another pod sent.
+inline uint32_t ts_offset(const uint8_t* f, uint32_t len, int depth = 0) {
   uint32_t l3 = 14;
   if (len >= 18 && f[12] == 0x81 && f[13] == 0x00) l3 = 18;
   if (len < l3 + 20 || f[l3 - 2] != 0x08 || f[l3 - 1] != 0x00) return 0;
   const uint32_t ihl = (f[l3] & 0xFu) * 4u;
   const uint32_t l4 = l3 + ihl + (f[l3 + 9] == 6 ? 20u : 8u);
+  if (depth == 0 && f[l3 + 9] == 17 && l4 + 8 + 14 <= len && f[l3 + ihl + 2] == 0x12 && f[l3 + ihl + 3] == 0xB5) {
+    const uint32_t in = l4 + 8;   // past the 8-B VXLAN header
+    const uint32_t o = ts_offset(f + in, len - in, 1);
+    return o ? in + o : 0;
+  }
   return l4 + 8 <= len ? l4 : 0;
 }
 

@@ -78,14 +78,15 @@ class _WireLive:
     def mac(i: int) -> bytes:
         return bytes([2, 0, 0, 0, 0, i + 1])
 
-    def frames(self, i: int, n_pods: int, k: int = 4096, seed: int = 0):
-        """k 60-B IPv4 / UDP frames from pod i to random other pods (distinct 5-tuples)."""
+    def frames(self, i: int, n_pods: int, k: int = 4096, seed: int = 0, broadcast: bool = False):
+        """k 60-B IPv4 / UDP frames from pod i to random other pods (distinct 5-tuples); with
+        `broadcast` to ff:ff:ff:ff:ff:ff."""
         rng = np.random.default_rng(seed)
         f = np.zeros((k, 64), np.uint8)
         dst = (i + 1 + rng.integers(0, n_pods - 1, k)) % n_pods
         for j in range(k):
             d = int(dst[j])
-            f[j, 0:6] = np.frombuffer(self.mac(d), np.uint8)
+            f[j, 0:6] = 0xFF if broadcast else np.frombuffer(self.mac(d), np.uint8)
             f[j, 6:12] = np.frombuffer(self.mac(i), np.uint8)
             f[j, 12:14] = (8, 0)
             f[j, 14:24] = (0x45, 0, 0, 46, 0, 0, 0, 0, 64, 17)
@@ -118,7 +119,13 @@ class _WireLive:
 def run(device: str = "cuda", n_pods: int = 8, flows: int = 1 << 20, n_acl: int = 256, duration: float = 1.0,
         threads: int = 4, burst: int = 512, inflight: int = 64, ring_capacity: int = 16384,
         hash_mode: str = "lds", tx_workers: int = 1, queues: int = 4, max_inflight_frames: int = 4096,
-        pod_ring: int = 1024, backend: str = "pipeline", coalesce_us: float = 8.0, loaded_window: int = 2048) -> dict:
+        pod_ring: int = 1024, backend: str = "pipeline", coalesce_us: float = 8.0, loaded_window: int = 2048,
+        traffic: str = "plain") -> dict:
+    """traffic: "plain" (the headline SFC), "vxlan-egress" (every pod's VF a VXLAN tunnel port:
+    all frames leave encapsulated through one underlay vport, outer headers from the per-burst
+    side pass) or "broadcast" (pods on one learning bridge sending to ff:ff:ff:ff:ff:ff: every
+    frame floods to the other pods, one copy from the GPU and the rest from the side pass;
+    `mpps` counts delivered copies)."""
     nf = nfdp()
     t0 = time.perf_counter()
     d = tempfile.mkdtemp(prefix="dpu-live-", dir=memif_dir())
@@ -130,23 +137,46 @@ def run(device: str = "cuda", n_pods: int = 8, flows: int = 1 << 20, n_acl: int 
             fr, ln = live.frames(i, n_pods, seed=100 + i)
             pods.append((live.paths[i], fr, ln))
         device, flows, n_acl = "none", n_pods * 4096, 0
+    elif traffic == "broadcast":
+        from dpu_operator_amd.dataplane import tables as T
+
+        dp = DataPlane(device=device, flow_buckets=1 << 12, mac_slots=1 << 12,
+                       hash_mode=hash_mode if device != "cpu" else "mfma")
+        for p in range(n_pods):
+            dp.ports.set(p, flags=T.PORT_VALID | T.PORT_LEARN, bridge_id=5)
+        dp.flood.set_members(5, list(range(n_pods)))
+        dp.commit(full=True)
+        ports = {p: MemifVport(os.path.join(d, f"pod{p}"), ring_size=pod_ring) for p in range(n_pods)}
+        live = NativeLivePath(dp, ports, burst=burst, ring_capacity=ring_capacity, inflight=inflight,
+                              tx_workers=tx_workers, queues=queues, max_inflight_frames=max_inflight_frames,
+                              coalesce_us=coalesce_us).start()
+        gen = _WireLive.__new__(_WireLive)
+        for i in range(n_pods):
+            fr, ln = gen.frames(i, n_pods, k=1024, seed=100 + i, broadcast=True)
+            pods.append((ports[i].path, fr, ln))
+        flows, n_acl = 0, 0
     else:
         dp = DataPlane(device=device, flow_buckets=max(1 << 12, 1 << int(np.ceil(np.log2(max(flows, 1) / 2)))),
                        hash_mode=hash_mode if device != "cpu" else "mfma")
         sc = S.build_sfc(dp, n_pods=n_pods, n_flows=flows, n_acl=n_acl, seed=0)
+        underlay = S.install_vxlan_egress(dp, sc)["underlay"] if traffic == "vxlan-egress" else None
         dp.commit(full=True)
         ports = {int(sc.pod_port[i]): MemifVport(os.path.join(d, f"pod{i}"), ring_size=pod_ring) for i in range(n_pods)}
+        if underlay is not None:
+            ports[underlay] = MemifVport(os.path.join(d, "underlay"), ring_size=4 * pod_ring)
         live = NativeLivePath(dp, ports, burst=burst, ring_capacity=ring_capacity, inflight=inflight,
                               tx_workers=tx_workers, queues=queues, max_inflight_frames=max_inflight_frames,
                               coalesce_us=coalesce_us).start()
         for i in range(n_pods):
             slots, im = S.traffic(sc, 4096, seed=100 + i, src_pods=np.array([i]))
             pods.append((ports[int(sc.pod_port[i])].path, slots, (im >> 16).astype(np.uint32)))
+        if underlay is not None:   # the VTEP's pod only receives
+            pods.append((ports[underlay].path, np.zeros((0, 64), np.uint8), np.zeros(0, np.uint32)))
         flows = int(len(sc.keys))
     setup_s = time.perf_counter() - t0
     stats = lambda: live.stats  # noqa: E731
     try:
-        out = {"backend": backend, "device": device, "queues": queues, "coalesce_us": coalesce_us, "tx_workers": tx_workers, "inflight_bursts": inflight,
+        out = {"backend": backend, "traffic": traffic, "device": device, "queues": queues, "coalesce_us": coalesce_us, "tx_workers": tx_workers, "inflight_bursts": inflight,
                "max_inflight_frames": max_inflight_frames, "pod_ring": pod_ring, "gen_threads": threads,
                "pods": n_pods, "flows": flows, "acl_rules": n_acl, "frame_bytes": 64,
                "setup_s": round(setup_s, 1)}
@@ -299,6 +329,7 @@ def main() -> None:
     ap.add_argument("--max-inflight-frames", type=int, default=4096)
     ap.add_argument("--pod-ring", type=int, default=1024)
     ap.add_argument("--backend", choices=("pipeline", "wire"), default="pipeline")
+    ap.add_argument("--traffic", choices=("plain", "vxlan-egress", "broadcast"), default="plain")
     ap.add_argument("--coalesce-us", type=float, default=8.0)
     ap.add_argument("--loaded-window", type=int, default=2048, help="frames in flight of the closed-loop loaded run")
     ap.add_argument("--veth", choices=("linux-bridge", "engine"), default=None,
@@ -311,7 +342,8 @@ def main() -> None:
     print(json.dumps(run(a.device, a.pods, a.flows, duration=a.duration, threads=a.threads, burst=a.burst,
                          inflight=a.inflight, tx_workers=a.tx_workers, queues=a.queues,
                          max_inflight_frames=a.max_inflight_frames, pod_ring=a.pod_ring,
-                         backend=a.backend, coalesce_us=a.coalesce_us, loaded_window=a.loaded_window)), flush=True)
+                         backend=a.backend, coalesce_us=a.coalesce_us, loaded_window=a.loaded_window,
+                         traffic=a.traffic)), flush=True)
 
 
 if __name__ == "__main__":
