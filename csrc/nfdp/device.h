@@ -122,7 +122,10 @@ __device__ __forceinline__ void classify_wave(const FlowKey& key, uint4* kx, con
   v4i bf[4][2];   // i8 B operands (MFMA hash)
   v4i bq[4];      // FP4 B operands (MFMA ACL)
   if constexpr (HASH == kHashMfma || ACL == kAclMfma) {
-    kx[lane] = make_uint4(key.src_ip, key.dst_ip, key.ports, key.meta);
+    // the ACL key's meta word (nfdp.h acl_key_meta) goes to the exchange directly unless the MFMA
+    // hash reads the flow key from it too
+    kx[lane] = make_uint4(key.src_ip, key.dst_ip, key.ports,
+                          (ACL == kAclMfma && HASH != kHashMfma) ? acl_key_meta(key.ports, key.meta) : key.meta);
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
 #pragma unroll
@@ -136,7 +139,8 @@ __device__ __forceinline__ void classify_wave(const FlowKey& key, uint4* kx, con
       }
       if constexpr (ACL == kAclMfma) {
         uint32_t w = src[g];
-        if (g == 3) w = acl_key_meta(src[2], w);   // the ACL key's meta word (nfdp.h)
+        if constexpr (HASH == kHashMfma)
+          if (g == 3) w = acl_key_meta(src[2], w);   // (the exchange holds the flow key's meta)
         bq[tt][0] = (int)spread8_fp4(w & 0xFFu);
         bq[tt][1] = (int)spread8_fp4((w >> 8) & 0xFFu);
         bq[tt][2] = (int)spread8_fp4((w >> 16) & 0xFFu);
@@ -195,10 +199,9 @@ __device__ __forceinline__ void classify_wave(const FlowKey& key, uint4* kx, con
     typedef const __attribute__((address_space(4))) uint32_t* cu32;
     const cu32 pf = (cu32)(reinterpret_cast<const uint32_t*>(av.gc) + (size_t)av.tiles * 16);  // [tiles][8]
     const cu32 gpf = pf + (size_t)av.tiles * 8;                                                // [groups][8]
-    const uint32_t ameta = acl_key_meta(key.ports, key.meta);
     auto pass = [&](cu32 f) {
       const uint32_t x = ((key.src_ip & f[0]) ^ f[4]) | ((key.dst_ip & f[1]) ^ f[5]) |
-                         ((key.ports & f[2]) ^ f[6]) | ((ameta & f[3]) ^ f[7]);
+                         ((key.ports & f[2]) ^ f[6]) | ((key.meta & f[3]) ^ f[7]);   // (no port-class bits: host.cpp)
       return __any(x == 0u);
     };
     // tiles past the LDS copy: buffer loads (a distinct path the compiler cannot merge with the

@@ -149,6 +149,7 @@ void prefilter(const uint32_t* value, const uint32_t* mask, const uint32_t* rule
       diff |= (value[4 * r + w] & mask[4 * r + w]) ^ v0;
     }
     cm &= ~diff;
+    if (w == 3) cm &= ~(kAclSportHi | kAclDportHi);   // prefilters test the flow key: no port-class bits
     out[w] = cm;
     out[4 + w] = v0 & cm;
   }

@@ -617,7 +617,17 @@ uint64_t RingEngine::completed(uint32_t q) {
   Queue& Q = qs_[q];
   std::lock_guard<std::mutex> g(Q.mu);
   const uint64_t end = Q.prod / 64;
-  while (Q.floor < end && chunk_done(Q.floor, q)) ++Q.floor;
+  // A producer reuses a chunk's slots (and its flag word) only once that chunk is done, so every
+  // chunk more than a ring behind the newest published one is done, and a flag word holding a
+  // LATER chunk's number means its earlier chunk completed.  Producers that track room
+  // themselves (the native I/O engine: publish(.., check_room = false)) never advance the floor;
+  // without these two rules it would stall more than a ring behind and never catch up.
+  if (Q.floor + nch_ < end) Q.floor = end - nch_;
+  while (Q.floor < end) {
+    const uint32_t v = __atomic_load_n(&flags_[(size_t)q * nch_ + (Q.floor & (nch_ - 1))], __ATOMIC_ACQUIRE);
+    if ((int32_t)(v - (uint32_t)(Q.floor + 1)) < 0) break;
+    ++Q.floor;
+  }
   return Q.floor * 64;
 }
 
