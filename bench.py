@@ -79,7 +79,7 @@ def parse():
     ap.add_argument("--no-lowlat", action="store_true", help="skip the small-batch latency probe")
     ap.add_argument("--no-variants", action="store_true", help="skip the mixed / ACL1024 / IMIX measurements")
     ap.add_argument("--no-live", action="store_true", help="skip the live pod-to-pod (native I/O engine) block")
-    ap.add_argument("--live-workers", type=int, default=1, help="native I/O engine delivery threads per queue")
+    ap.add_argument("--live-workers", type=int, default=2, help="native I/O engine delivery threads per queue")
     ap.add_argument("--live-queues", type=int, default=4, help="native I/O engine rx queues (threads)")
     ap.add_argument("--live-gen-threads", type=int, default=4, help="pod traffic generator threads")
     ap.add_argument("--variant-steps", type=int, default=30)

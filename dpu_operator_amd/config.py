@@ -39,7 +39,7 @@ class NodeConfig:
     # live data path of the GPU VSP (vsp/gpu.py, dataplane/native_io.py)
     vport_kind: str = "veth"           # veth (kernel netdev pods, AF_PACKET rings) | memif | tap
     io_queues: int = 4                 # native engine rx queues (threads), each with a ring queue per GPU
-    io_workers: int = 1                # native engine delivery threads per queue
+    io_workers: int = 2                # native engine delivery threads per queue (4 x 2: 57.9 Mpps, r4 s4)
     # daemon cadences (seconds)
     device_poll: float = 5.0           # ListAndWatch refresh (deviceplugin.go:109)
     detect_poll: float = 1.0           # platform detection (daemon.go:88)

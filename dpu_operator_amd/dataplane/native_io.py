@@ -206,6 +206,7 @@ class NativeLivePath:
             eng.add_port(int(idx), p, int(self.port_queues.get(idx, -1)))
         eng.learn_stamp = max(int(getattr(d, "stamp", 0)) for d in self.dps) + 1
         self._eng = eng
+        self._applied = {}   # a new engine holds no configuration yet
         self._refresh()
         eng.start()
 
@@ -261,38 +262,59 @@ class NativeLivePath:
         self._eng.resume()
 
     def hold(self, dp) -> None:
-        """A live commit's epoch switch: publication stops between two bursts (no drain)."""
+        """A live commit's epoch switch: publication stops between two bursts (no drain).  The
+        engine's new configuration (side-table snapshots, side ports, redirects, steering) is
+        built BEFORE publication stops; only pointer swaps happen inside the hold."""
         if self._eng is not None and self._eng.running:
+            self._staged = self._collect()
             self._eng.hold()
 
     def release(self, dp) -> None:
         if self._eng is None:
             return
-        self._refresh()
+        staged, self._staged = getattr(self, "_staged", None), None
+        self._apply(staged if staged is not None else self._collect())
         self._eng.release()
 
     def _refresh(self) -> None:
         """Point the oracle backends at the current tables; the side-pass table snapshots, side
         ports, tunnel redirects and steering (copy-on-write in the engine)."""
-        eng = self._eng
-        for g, (dp, be) in enumerate(zip(self.dps, self._backends)):
-            if not self.gpu:
-                be.configure(dp.tables_ptrs(), dp._ptr("flow_ctr"), dp._ptr("port_ctr"), dp._ptr("drop_ctr"))
-            eng.set_side_tables(g, self.nf.SideTables(**dp.side_tables_host()))
+        self._apply(self._collect())
+
+    def _collect(self) -> dict:
+        side = [self.nf.SideTables(**dp.side_tables_host()) for dp in self.dps]
         dp0 = self.dps[0]
         a = dp0.ports.a
         flags = a["flags"].astype(np.uint32)
-        eng.set_side_ports([int(i) for i in np.nonzero(flags & np.uint32(SIDE_PORT_FLAGS))[0]])
+        side_ports = [int(i) for i in np.nonzero(flags & np.uint32(SIDE_PORT_FLAGS))[0]]
         red = []
         for i in np.nonzero(flags & np.uint32(T.PORT_TUNNEL))[0]:
             tab = dp0.tunnels6 if flags[i] & T.PORT_TUNNEL6 else dp0.tunnels
             lag = int(a[i]["lag"])
             if lag < len(tab.a):
                 red.append((int(i), int(tab.a[lag]["out_port"])))
-        eng.set_redirects(red)   # the whole map: a port that stopped being a tunnel loses its entry
+        steer = None
         if len(self.dps) > 1:
             v6 = any(d._v6_keys() for d in self.dps)   # IPv6 frames steer by their folded 5-tuple
-            eng.set_steering(np.ascontiguousarray(a), bytes(dp0.rss_key), v6)
+            steer = (np.ascontiguousarray(a).copy(), bytes(dp0.rss_key), v6)
+        return {"side": side, "side_ports": side_ports, "redirects": red, "steer": steer}
+
+    def _apply(self, c: dict) -> None:
+        eng = self._eng
+        for g, (dp, be) in enumerate(zip(self.dps, self._backends)):
+            if not self.gpu:
+                be.configure(dp.tables_ptrs(), dp._ptr("flow_ctr"), dp._ptr("port_ctr"), dp._ptr("drop_ctr"))
+            eng.set_side_tables(g, c["side"][g])
+        last = getattr(self, "_applied", {})
+        if last.get("side_ports") != c["side_ports"]:
+            eng.set_side_ports(c["side_ports"])
+        if last.get("redirects") != c["redirects"]:
+            eng.set_redirects(c["redirects"])   # the whole map: a port that stopped being a tunnel loses its entry
+        st = c["steer"]
+        old = last.get("steer")
+        if st is not None and (old is None or old[1:] != st[1:] or not np.array_equal(old[0], st[0])):
+            eng.set_steering(*st)
+        self._applied = {"side_ports": c["side_ports"], "redirects": c["redirects"], "steer": st}
 
     # ------------------------------------------------------------------ counters (DataPlane._ctr_hooks)
     def side_port_counters(self) -> np.ndarray:

@@ -118,7 +118,7 @@ class _WireLive:
 
 def run(device: str = "cuda", n_pods: int = 8, flows: int = 1 << 20, n_acl: int = 256, duration: float = 1.0,
         threads: int = 4, burst: int = 512, inflight: int = 64, ring_capacity: int = 16384,
-        hash_mode: str = "lds", tx_workers: int = 1, queues: int = 4, max_inflight_frames: int = 4096,
+        hash_mode: str = "lds", tx_workers: int = 2, queues: int = 4, max_inflight_frames: int = 4096,
         pod_ring: int = 1024, backend: str = "pipeline", coalesce_us: float = 8.0, loaded_window: int = 2048,
         traffic: str = "plain") -> dict:
     """traffic: "plain" (the headline SFC), "vxlan-egress" (every pod's VF a VXLAN tunnel port:
@@ -324,7 +324,7 @@ def main() -> None:
     ap.add_argument("--threads", type=int, default=4)
     ap.add_argument("--burst", type=int, default=512)
     ap.add_argument("--inflight", type=int, default=64)
-    ap.add_argument("--tx-workers", type=int, default=1)
+    ap.add_argument("--tx-workers", type=int, default=2)
     ap.add_argument("--queues", type=int, default=4)
     ap.add_argument("--max-inflight-frames", type=int, default=4096)
     ap.add_argument("--pod-ring", type=int, default=1024)
