@@ -881,6 +881,44 @@ PYBIND11_MODULE(_nfdp, m) {
       }, py::arg("ports"), py::arg("rss"), py::arg("v6") = false)
       .def("set_redirect", &Engine::set_redirect)
       .def("set_side_ports", &Engine::set_side_ports)
+      // A live commit's switch in one native call, without the GIL: hold publication (every rx
+      // thread between two bursts), change every ring's epoch (flow copy and / or table set), swap
+      // in the side-table snapshots and lists built beforehand, release.  The hold lasts only as
+      // long as these pointer swaps; nothing of it waits for Python.
+      .def("switch_tables", [](Engine& e, py::list rings, py::list flow, py::list set, py::list side,
+                               py::object side_ports, py::object redirects) {
+        std::vector<RingEngine*> rs;
+        std::vector<std::pair<bool, bool>> fs;
+        for (size_t i = 0; i < rings.size(); ++i) {
+          rs.push_back(rings[i].cast<RingEngine*>());
+          fs.emplace_back(flow[i].cast<bool>(), set[i].cast<bool>());
+        }
+        std::vector<std::shared_ptr<SideTables>> st;
+        for (auto o : side) st.push_back(o.is_none() ? nullptr : o.cast<std::shared_ptr<SideTables>>());
+        const bool sp = !side_ports.is_none(), rd = !redirects.is_none();
+        std::vector<uint32_t> spv;
+        std::vector<std::pair<uint32_t, uint32_t>> rdv;
+        if (sp) spv = side_ports.cast<std::vector<uint32_t>>();
+        if (rd) rdv = redirects.cast<std::vector<std::pair<uint32_t, uint32_t>>>();
+        std::vector<uint32_t> epochs;
+        {
+          py::gil_scoped_release nogil;
+          e.hold();
+          try {
+            for (size_t i = 0; i < rs.size(); ++i) epochs.push_back(rs[i]->change_epoch(fs[i].first, fs[i].second));
+            for (size_t g = 0; g < st.size(); ++g)
+              if (st[g]) e.set_side_tables((uint32_t)g, st[g]);
+            if (sp) e.set_side_ports(spv);
+            if (rd) e.set_redirects(rdv);
+          } catch (...) {
+            e.release();
+            throw;
+          }
+          e.release();
+        }
+        return epochs;
+      }, py::arg("rings"), py::arg("flow"), py::arg("set"), py::arg("side"), py::arg("side_ports") = py::none(),
+         py::arg("redirects") = py::none())
       .def("set_side_always", &Engine::set_side_always)
       .def("inject", [](Engine& e, uint32_t port, py::bytes f) {
         std::string s = f;

@@ -173,13 +173,7 @@ class DataPlane:
         if plan is not None:
             with TRACER.span("dataplane.commit_live", plan=plan):
                 prep = self._live_prepare(rings, plan)
-                for h in hooks:
-                    h.hold(self)
-                try:
-                    self._live_flip(rings, prep)
-                finally:
-                    for h in hooks:
-                        h.release(self)
+                live_switch(self, [(self, rings, prep)], hooks)
             return prep["sent"]
         # native I/O engines (dataplane/native_io.py) feeding this data plane: nothing in flight
         # while tables move, then they re-read the new tables
@@ -351,13 +345,19 @@ class DataPlane:
         """The switch: one epoch change per ring (flow copy and / or table set together)."""
         if not (prep["flow"] or prep["set"]):
             return
+        for r in rings:
+            r.eng.change_epoch(prep["flow"], prep["set"])
+        self._after_flip(prep)
+
+    def _after_flip(self, prep: dict) -> None:
+        """Host bookkeeping of a switch that happened (the rings' epochs changed)."""
+        if not (prep["flow"] or prep["set"]):
+            return
         if prep["flow"]:
             self._flow_active ^= 1
             self._flow_lag = prep["dirty"]          # rows the now idle copy missed
             self.flip_stats["flips"] += 1
             prep["sent"]["flip"] = self._flow_active
-        for r in rings:
-            r.eng.change_epoch(prep["flow"], prep["set"])
         self._gen += 1
         now = time.perf_counter()
         if prep["set"]:
@@ -845,3 +845,26 @@ class GraphedRun:
                               non_blocking=True)
         self.graph.replay()
         return BatchResult(self.out, self.meta, self.n, {"lat": self.lat})
+
+
+def live_switch(dp, items, hooks) -> None:
+    """The switch of a live commit over one or several planes: items = [(plane, running rings,
+    its _live_prepare result)].  Behind a single native I/O engine the whole switch is one native
+    call (hold, every ring's epoch change, the engine's new side tables / lists, release: the
+    hold lasts microseconds and never waits for Python); otherwise the hooks hold, the epochs
+    change, the hooks release."""
+    flips = [(r, pr) for _p, rs, pr in items if (pr["flow"] or pr["set"]) for r in rs]
+    if len(hooks) == 1 and hasattr(hooks[0], "switch"):
+        hooks[0].switch(dp, [r.eng for r, _ in flips], [bool(pr["flow"]) for _, pr in flips],
+                        [bool(pr["set"]) for _, pr in flips])
+    else:
+        for h in hooks:
+            h.hold(dp)
+        try:
+            for r, pr in flips:
+                r.eng.change_epoch(pr["flow"], pr["set"])
+        finally:
+            for h in hooks:
+                h.release(dp)
+    for p, _rs, pr in items:
+        p._after_flip(pr)

@@ -23,7 +23,7 @@ from __future__ import annotations
 
 import numpy as np
 
-from .engine import BatchResult, DataPlane
+from .engine import BatchResult, DataPlane, live_switch
 
 # table models shared by all planes (one host object, replicated to every device)
 SHARED_MODELS = ("ports", "chains", "macs", "lag", "flood", "routes", "routes6", "nexthops", "ecmp", "tunnels",
@@ -125,14 +125,7 @@ class MultiDataPlane:
         sent = {}
         if all(pl is not None for pl in plans):
             preps = [p._live_prepare(r, pl) for p, r, pl in zip(self.planes, rings, plans)]
-            for h in hooks:
-                h.hold(self)
-            try:
-                for p, r, pr in zip(self.planes, rings, preps):
-                    p._live_flip(r, pr)
-            finally:
-                for h in hooks:
-                    h.release(self)
+            live_switch(self, list(zip(self.planes, rings, preps)), hooks)
             for g, pr in enumerate(preps):
                 for k, v in pr["sent"].items():
                     sent[f"{k}@{g}"] = v

@@ -276,6 +276,27 @@ class NativeLivePath:
         self._apply(staged if staged is not None else self._collect())
         self._eng.release()
 
+    def switch(self, dp, engs, flows, sets) -> None:
+        """A live commit's switch (engine.live_switch): the new configuration is built first, then
+        ONE native call holds publication, changes every ring's epoch, swaps the configuration
+        in and releases."""
+        if self._eng is None or not self._eng.running:
+            for e, f, st in zip(engs, flows, sets):
+                e.change_epoch(f, st)
+            if self._eng is not None:
+                self._refresh()
+            return
+        c = self._collect()
+        last = getattr(self, "_applied", {})
+        st = c["steer"]
+        old = last.get("steer")
+        if st is not None and (old is None or old[1:] != st[1:] or not np.array_equal(old[0], st[0])):
+            self._eng.set_steering(*st)   # (steering only picks the GPU: any burst may take either)
+        sp = c["side_ports"] if last.get("side_ports") != c["side_ports"] else None
+        rd = c["redirects"] if last.get("redirects") != c["redirects"] else None
+        self._eng.switch_tables(list(engs), list(flows), list(sets), c["side"], sp, rd)
+        self._applied = {"side_ports": c["side_ports"], "redirects": c["redirects"], "steer": st}
+
     def _refresh(self) -> None:
         """Point the oracle backends at the current tables; the side-pass table snapshots, side
         ports, tunnel redirects and steering (copy-on-write in the engine)."""
