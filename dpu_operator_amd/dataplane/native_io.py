@@ -176,15 +176,22 @@ class NativeLivePath:
         eng = nf.IoEngine(self.burst, self.inflight, self.tx_workers, self.queues, self.max_inflight_frames)
         eng.set_coalesce(self.coalesce_frames, self.coalesce_us)
         self._rings, self._backends = [], []
+        # planes sharing a GPU split its CUs between their resident grids (a resident grid never
+        # yields: a second full-size grid on the same device would never be scheduled)
+        per_dev: dict = {}
+        for dp in self.dps:
+            per_dev[str(getattr(dp, "tdev", ""))] = per_dev.get(str(getattr(dp, "tdev", "")), 0) + 1
         for dp in self.dps:
             if self.gpu:
                 import torch
 
                 from .ring import RingPath
 
+                share = per_dev[str(dp.tdev)]
                 with torch.cuda.device(dp.tdev):
                     ring = RingPath(dp, capacity=self.capacity, host_slots=True, coop=True, side=False,
-                                    deadline_s=3600.0, queues=self.queues)
+                                    deadline_s=3600.0, queues=self.queues,
+                                    cus=max(1, int(dp.num_cus) // share))
                     ring.start()
                 self._rings.append(ring)
                 be = nf.GpuBackend(ring.eng)

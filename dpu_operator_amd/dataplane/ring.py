@@ -40,7 +40,8 @@ from .engine import DataPlane
 
 class RingPath:
     def __init__(self, dp: DataPlane, capacity: int = 1 << 16, wgs_per_cu: int = 1, deadline_s: float = 120.0,
-                 knobs: int = 0, coop: bool = True, host_slots: bool = False, side: bool = False, queues: int = 1):
+                 knobs: int = 0, coop: bool = True, host_slots: bool = False, side: bool = False, queues: int = 1,
+                 cus: int = 0):
         """coop=True: a workgroup's 4 waves share each chunk (ACL rule tiles split 4 ways) —
         lowest latency.  coop=False: every wave takes its own chunks — highest throughput.
         host_slots=True: the ring slots live in pinned host memory and the resident kernel reads /
@@ -48,7 +49,9 @@ class RingPath:
         side=True: the kernel puts packets that need replicas / learn events / outer headers on
         the data plane's side list; `side_pass()` runs the side kernel over them.
         queues: independent rings served by the one resident grid (workgroup b serves queue
-        b % queues): one per producer thread of the native I/O engine (ring.h)."""
+        b % queues): one per producer thread of the native I/O engine (ring.h).
+        cus: CUs the resident grid takes (0: all).  Resident grids never yield their CUs, so rings
+        sharing one GPU (two planes on one device) must split them, or the later grid never runs."""
         if not dp.gpu:
             raise RuntimeError("RingPath needs a GPU data plane")
         if capacity < 64 or capacity & (capacity - 1):
@@ -62,7 +65,10 @@ class RingPath:
         if queues > 1 and side:
             raise ValueError("the side list indexes one queue's slots: side=True needs queues=1")
         self.queues = int(queues)
-        self.eng = dp.nf.RingEngine(self.capacity, int(dp.num_cus), int(wgs_per_cu), self.coop, self.host_slots,
+        self.cus = int(cus) if cus else int(dp.num_cus)
+        if not 1 <= self.cus <= int(dp.num_cus):
+            raise ValueError(f"cus must be in [1, {int(dp.num_cus)}]")
+        self.eng = dp.nf.RingEngine(self.capacity, self.cus, int(wgs_per_cu), self.coop, self.host_slots,
                                     self.queues)
         self._staged = 0
         self.side = bool(side)
@@ -131,7 +137,7 @@ class RingPath:
         _torch().cuda.current_stream(self.dp.tdev).synchronize()  # tables are in HBM before launch
         self.eng.set_epoch(self.dp._flow_active)
         self.eng.start(self._tables(), self._args(), self.dp.hash_mode, self.dp.acl_mode,
-                       int(self.dp.num_cus), self.deadline_s)
+                       self.cus, self.deadline_s)
         self.launches += 1
 
     def stop(self, timeout_s: float = 30.0) -> None:
@@ -144,7 +150,7 @@ class RingPath:
             _torch().cuda.current_stream(self.dp.tdev).synchronize()
             self.eng.set_epoch(self.dp._flow_active)
             self.eng.start(self._tables(), self._args(), self.dp.hash_mode, self.dp.acl_mode,
-                           int(self.dp.num_cus), self.deadline_s)
+                           self.cus, self.deadline_s)
             self.launches += 1
 
     def ensure_alive(self) -> bool:
