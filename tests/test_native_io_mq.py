@@ -216,7 +216,8 @@ def test_multi_plane_native_matches_one_plane(shm, devices):
         for port, frames in exp.items():
             assert sorted(got[port]) == sorted(frames), port
         assert all(int(p.port_counters()[:, 0].sum()) > 0 for p in m.planes)   # both planes worked
-        assert np.array_equal(m.port_counters(), ref.port_counters())
+        # (ring kernels flush their LDS counter tallies when their waves next go idle)
+        assert _until(lambda: np.array_equal(m.port_counters(), ref.port_counters()), 2.0)
         # a commit of the multi-plane data plane pauses the engine once and keeps forwarding
         m.ports.set_mtu(int(sc.pod_port[0]), 1400)
         ref.ports.set_mtu(int(sc.pod_port[0]), 1400)
