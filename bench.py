@@ -37,6 +37,9 @@ import time
 
 import numpy as np
 
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import dpu_operator_amd  # noqa: E402,F401  (HIP queue settings before torch starts HIP)
+
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 

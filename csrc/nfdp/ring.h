@@ -223,6 +223,7 @@ class RingEngine {
   };
   mutable std::mutex mu_;     // epoch changes / table sets (engine-wide)
   uint32_t cap_, nch_, nq_;
+  hipStream_t stage_stream_ = nullptr;   // table-set uploads (created on first use, mu_ held)
   int num_cus_, wgs_;
   bool coop_;
   bool host_slots_;

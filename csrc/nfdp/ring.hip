@@ -532,6 +532,7 @@ RingEngine::~RingEngine() {
   }
   (void)hipStreamSynchronize(stream_);
   (void)hipStreamDestroy(stream_);
+  if (stage_stream_) (void)hipStreamDestroy(stage_stream_);
   for (void* d : {(void*)st_, (void*)d_svc_, (void*)d_sets_}) (void)hipFree(d);
   if (host_slots_) {
     for (void* h : host_ptrs_) (void)hipHostFree(h);
@@ -717,12 +718,11 @@ void RingEngine::stage_tables(const FusedLaunch& f, int which) {
   ts.toep_frag = f.toep_frag; ts.toep_tab = f.toep_tab;
   std::lock_guard<std::mutex> g(mu_);
   ts.serial = ++set_serial_;
-  // a copy on the engine's own stream would queue behind the resident kernel: a private
-  // non-blocking stream (the grid never reads the idle set)
-  static thread_local hipStream_t cs = nullptr;
-  if (!cs) ck(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking), "stream");
-  ck(hipMemcpyAsync(d_sets_ + which, &ts, sizeof(ts), hipMemcpyHostToDevice, cs), "table set upload");
-  ck(hipStreamSynchronize(cs), "table set upload");
+  // a copy on the engine's own stream would queue behind the resident kernel: the engine's
+  // staging stream (one per engine, whatever thread commits; the grid never reads the idle set)
+  if (!stage_stream_) ck(hipStreamCreateWithFlags(&stage_stream_, hipStreamNonBlocking), "stream");
+  ck(hipMemcpyAsync(d_sets_ + which, &ts, sizeof(ts), hipMemcpyHostToDevice, stage_stream_), "table set upload");
+  ck(hipStreamSynchronize(stage_stream_), "table set upload");
   if (running_) {
     // the side pass (RingPath.side_pass) reads the session's tables from launch()
     launch_.t = f.t;
