@@ -376,7 +376,7 @@ __global__ __launch_bounds__(kRingBlock) void ring_kernel(RingArgs a) {
     // ---- counters, off the latency path (after the flag): port / drop counters into the
     // workgroup's LDS (flushed when idle, every kFlushChunks chunks and at exit), per-flow words
     // (nearly distinct per packet) straight to the global table.
-    if (counters && !pad) {
+    if (counters && !pad) {   // (per lane: filler lanes count nothing)
       if (st.in_port < (uint32_t)kLdsPorts) {
         atomicAdd(&pc[st.in_port], 1u); atomicAdd(&pc[kLdsPorts + st.in_port], st.wire_len);
       } else if (st.in_port < (uint32_t)kMaxPorts) {
@@ -390,8 +390,12 @@ __global__ __launch_bounds__(kRingBlock) void ring_kernel(RingArgs a) {
         atomicAdd(a.port_ctr + 2 * e.out_port + 1, ctr_inc(olen));
       }
       if (hit && a.flow_ctr && !(a.flags_bits & 4u)) atomicAdd(a.flow_ctr + slot, ctr_inc(st.wire_len));
-      if (++since_flush >= kFlushChunks) on_idle();
     }
+    // Wave-uniform: the flush moves every port's tally with the lane that owns that port index
+    // (flush_lds_counters), whatever lane counted the packet, so it must run with EXEC full.  (A
+    // per-lane count inside the branch above left a port's tallies behind for good whenever its
+    // lane had been a filler lane of every chunk since its last flush.)
+    if (counters && ++since_flush >= kFlushChunks) on_idle();
     NFDP_RING_MARK(tr5)
 #undef NFDP_RING_MARK
     if (trace && lane == 0 && qsvc) {

@@ -122,7 +122,7 @@ class NativeLivePath:
     def __init__(self, dps, ports: dict, burst: int = 256, ring_capacity: int = 4096, inflight: int = 64,
                  on_punt=None, auto_restart: bool = True, tx_workers: int = 1, queues: int = 1,
                  max_inflight_frames: int = 0, port_queues: dict | None = None, coalesce_us: float = 8.0,
-                 coalesce_frames: int = 64):
+                 coalesce_frames: int = 64, ring_cus: int = 0):
         """dps: one data plane or a list (one per GPU, or a MultiDataPlane's planes); ports:
         {port id: vport spec}; queues: rx threads (each with a ring queue on every GPU);
         port_queues: {port id: queue} (default: least loaded); max_inflight_frames: per lane
@@ -144,6 +144,7 @@ class NativeLivePath:
         self.tx_workers, self.queues = int(tx_workers), int(queues)
         self.max_inflight_frames = int(max_inflight_frames)
         self.coalesce_us, self.coalesce_frames = float(coalesce_us), int(coalesce_frames)
+        self.ring_cus = int(ring_cus)   # CUs of each ring grid (0: the GPU's, split between planes sharing it)
         self.specs = dict(ports)
         self.port_queues = dict(port_queues or {})
         self.on_punt = on_punt
@@ -191,7 +192,7 @@ class NativeLivePath:
                 with torch.cuda.device(dp.tdev):
                     ring = RingPath(dp, capacity=self.capacity, host_slots=True, coop=True, side=False,
                                     deadline_s=3600.0, queues=self.queues,
-                                    cus=max(1, int(dp.num_cus) // share))
+                                    cus=self.ring_cus or max(1, int(dp.num_cus) // share))
                     ring.start()
                 self._rings.append(ring)
                 be = nf.GpuBackend(ring.eng)

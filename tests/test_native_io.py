@@ -184,14 +184,17 @@ def test_commit_under_traffic_and_failure_restart(tmp_path):
 
 
 @pytest.mark.gpu
-def test_native_path_gpu_ring_bit_exact(tmp_path):
-    """The GPU backend: header slots into the persistent ring kernel's pinned host slots."""
+@pytest.mark.parametrize("queues", [1, 2])
+def test_native_path_gpu_ring_bit_exact(tmp_path, queues):
+    """The GPU backend: header slots into the persistent ring kernel's pinned host slots (one
+    ring queue per engine queue); frames bit-exact and counters exact."""
     nf = nfdp()
     dp, sc = _sfc("cuda")
     ref, _ = _sfc("cpu")
     slots, im = S.traffic(sc, 3000, seed=5)
     exp, drops = _expected(ref, slots, im)
-    live = NativeLivePath(dp, _vports(tmp_path, sc.n_pods, "g"), burst=256, ring_capacity=4096).start()
+    live = NativeLivePath(dp, _vports(tmp_path, sc.n_pods, "g"), burst=256, ring_capacity=4096,
+                          queues=queues).start()
     try:
         eps = {i: nf.MemifEndpoint(str(tmp_path / f"g{i}")) for i in range(sc.n_pods)}
         src = im & 0xFFFF
@@ -210,6 +213,11 @@ def test_native_path_gpu_ring_bit_exact(tmp_path):
         assert _until(drained, 10), (live.stats, live.error)
         for port, frames in exp.items():
             assert sorted(got[port]) == sorted(frames), port
+        # counters: the ring kernel's LDS tallies reach the device counters when its waves idle
+        if not _until(lambda: np.array_equal(dp.port_counters(), ref.port_counters()), 2.0):
+            g, w = dp.port_counters(), ref.port_counters()
+            bad = np.nonzero((g != w).any(1))[0]
+            raise AssertionError(f"ports {bad.tolist()}: got {g[bad].tolist()} want {w[bad].tolist()} {live.stats}")
     finally:
         live.stop()
 

@@ -217,7 +217,17 @@ def test_multi_plane_native_matches_one_plane(shm, devices):
             assert sorted(got[port]) == sorted(frames), port
         assert all(int(p.port_counters()[:, 0].sum()) > 0 for p in m.planes)   # both planes worked
         # (ring kernels flush their LDS counter tallies when their waves next go idle)
-        assert _until(lambda: np.array_equal(m.port_counters(), ref.port_counters()), 2.0)
+        ok = _until(lambda: np.array_equal(m.port_counters(), ref.port_counters()), 2.0)
+        if not ok:
+            got_c, want_c = m.port_counters(), ref.port_counters()
+            bad = np.nonzero((got_c != want_c).any(1))[0]
+            per = [p.port_counters()[bad] for p in m.planes]
+            st = dict(live.stats)
+            live.stop()
+            after = m.port_counters()
+            raise AssertionError(f"ports {bad.tolist()}: got {got_c[bad].tolist()} want {want_c[bad].tolist()} "
+                                 f"per plane {[x.tolist() for x in per]} after stop {after[bad].tolist()} "
+                                 f"equal after stop {np.array_equal(after, want_c)} stats {st}")
         # a commit of the multi-plane data plane pauses the engine once and keeps forwarding
         m.ports.set_mtu(int(sc.pod_port[0]), 1400)
         ref.ports.set_mtu(int(sc.pod_port[0]), 1400)
