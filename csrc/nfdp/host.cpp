@@ -163,8 +163,10 @@ AclFrags build_acl_frags(const uint32_t* value, const uint32_t* mask, uint32_t n
   if (f.tiles == 0) f.tiles = 1;
   const uint32_t npad = f.tiles * 16;
   const uint32_t groups = (f.tiles + 7) / 8;
-  // placement: sort by (dst, ports, src, meta) masks then values, in network byte order, so a tile
-  // holds rules of one shape over neighbouring values (e.g. consecutive /24s, low dports)
+  // placement: sort by the protocol byte (mask, value) first, then by (dst, ports, src, meta)
+  // masks and values in network byte order, so a tile holds rules of one protocol and one shape
+  // over neighbouring values (e.g. consecutive /24s, low dports): a group of TCP-only rules then
+  // agrees on the protocol byte and its prefilter lets no UDP wave in (and vice versa)
   std::vector<uint32_t> order(n);
   for (uint32_t r = 0; r < n; ++r) order[r] = r;
   auto sig = [&](uint32_t r) {
@@ -172,8 +174,8 @@ AclFrags build_acl_frags(const uint32_t* value, const uint32_t* mask, uint32_t n
     const uint32_t* m = mask + 4 * r;
     auto p16 = [](uint32_t raw) { return ((raw & 0xFFu) << 8) | ((raw >> 8) & 0xFFu); };
     const uint32_t mp = (p16(m[2] >> 16) << 16) | p16(m[2] & 0xFFFFu), vp = (p16(v[2] >> 16) << 16) | p16(v[2] & 0xFFFFu);
-    return std::make_tuple(bswap32(m[1]), mp, bswap32(m[0]), m[3], bswap32(v[1] & m[1]), vp & mp, bswap32(v[0] & m[0]),
-                           v[3] & m[3], r);
+    return std::make_tuple(m[3] & 0xFFu, v[3] & m[3] & 0xFFu, bswap32(m[1]), mp, bswap32(m[0]), m[3],
+                           bswap32(v[1] & m[1]), vp & mp, bswap32(v[0] & m[0]), v[3] & m[3], r);
   };
   std::sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return sig(x) < sig(y); });
   f.wfrag.assign((size_t)f.tiles * 64 * 16, 0);
