@@ -705,6 +705,22 @@ PYBIND11_MODULE(_nfdp, m) {
       .def_property_readonly("lds_acl_tiles", &RingEngine::lds_acl_tiles)
       .def("flip", &RingEngine::flip)
       .def("change_epoch", &RingEngine::change_epoch, py::arg("flow"), py::arg("set"))
+      // control mailbox: dwords to a device address, applied by the running grid
+      .def("post_write", [](RingEngine& r, uint64_t dst, py::bytes data, double timeout_s) {
+        std::string s = data;
+        if (s.size() % 4) throw std::invalid_argument("ring: control data is whole dwords");
+        std::vector<uint32_t> w(s.size() / 4);
+        std::memcpy(w.data(), s.data(), s.size());
+        py::gil_scoped_release nogil;
+        return r.post_write(dst, w.data(), (uint32_t)w.size(), timeout_s);
+      }, py::arg("dst"), py::arg("data"), py::arg("timeout_s") = 1.0)
+      .def_property_readonly("ctrl_done", &RingEngine::ctrl_done)
+      .def_property_readonly("ctrl_posted", &RingEngine::ctrl_posted)
+      .def("wait_ctrl", [](RingEngine& r, uint64_t seq, double timeout_s) {
+        py::gil_scoped_release nogil;
+        return r.wait_ctrl(seq, timeout_s);
+      }, py::arg("seq"), py::arg("timeout_s") = 1.0)
+      .def("set_ctrl_regions", &RingEngine::set_ctrl_regions)
       .def("bump_epoch", &RingEngine::bump_epoch)
       .def("grace_over", &RingEngine::grace_over)
       .def("wait_grace", [](RingEngine& r, double timeout_s) {

@@ -115,7 +115,33 @@ struct alignas(128) RingDevState {
   uint64_t claim;  // next chunk ticket (64-bit: tickets never wrap)
   uint32_t pad0[30];
   uint64_t dprod;  // device mirror of ctl.prod (advanced by the frontier wave), bit 63 = stop
-  uint32_t pad1[30];
+  uint32_t ctl_gen;   // (queue 0's state only) control-mailbox writes applied so far: a workgroup
+                      // seeing it move restages its LDS copies of the small tables
+  uint32_t pad1[29];
+};
+
+// Control mailbox: the control plane's small table writes (a port entry on a link / MTU / RX-state
+// change, a chain word, a MAC entry), applied by the resident grid itself.  Pinned coherent host
+// memory; the host fills an entry, then publishes it (seq, then head, release order); the grid's
+// poller wave (workgroup 0, wave 0: when idle, rate-limited, and every 16 chunks when busy) copies
+// the words to their device addresses, releases them at agent scope, bumps ctl_gen and reports
+// `done`.  No copy engine, no epoch change, no hold: the analogue of the Octeon control agent's
+// mailbox that the SoC polls (octep_ctrl_mbox.c / loop.c), with the GPU as the SoC.
+constexpr uint32_t kCtrlSlots = 64;
+constexpr uint32_t kCtrlWords = 12;
+struct alignas(64) RingCtrlEntry {
+  uint64_t dst;               // device address of the first dword (4-B aligned)
+  uint32_t nwords;            // 1..kCtrlWords
+  uint32_t seq;               // entry number + 1 (written after the rest of the entry)
+  uint32_t data[kCtrlWords];
+};
+static_assert(sizeof(RingCtrlEntry) == 64, "RingCtrlEntry");
+struct alignas(64) RingCtrlRing {
+  uint64_t head;              // host: entries posted
+  uint32_t pad0[14];
+  uint64_t done;              // device: entries applied (released to every workgroup)
+  uint32_t pad1[14];
+  RingCtrlEntry e[kCtrlSlots];
 };
 static_assert(sizeof(RingDevState) == 256, "RingDevState");
 
@@ -201,6 +227,18 @@ class RingEngine {
   uint32_t epoch() const { return epoch_.load(std::memory_order_acquire); }
   void set_epoch(uint32_t e);   // only while stopped
 
+  // Control mailbox (see RingCtrlRing): `n` dwords to device address `dst`, applied by the running
+  // grid; coop rings then restage their LDS copies of ports / chain words / ACL verdicts.  Returns
+  // the entry's number (ctrl_done() >= it once applied).  Throws if the grid is not running or the
+  // mailbox stays full for `timeout_s`.
+  uint64_t post_write(uint64_t dst, const uint32_t* data, uint32_t n, double timeout_s = 1.0);
+  uint64_t ctrl_posted() const { return ctrl_head_; }
+  // Device buffers control writes may target ([base, bytes) each: the running table set's small
+  // tables); anything else is refused on the host, so a bad address never reaches the GPU.
+  void set_ctrl_regions(const std::vector<std::pair<uint64_t, uint64_t>>& regions);
+  uint64_t ctrl_done() const;
+  bool wait_ctrl(uint64_t seq, double timeout_s);
+
   // Closed-loop probe run entirely in C++ (no Python in the timed loop) on queue 0: `batches`
   // batches of `batch` packets, at most `inflight` outstanding.  Returns per-batch
   // publish->completion latencies (µs, host steady clock) and sets *elapsed_s to the wall time.
@@ -243,6 +281,10 @@ class RingEngine {
   int device_ = 0;
   FusedLaunch launch_{};
   RingTableSet* d_sets_ = nullptr;   // [2] device table sets (coop rings)
+  RingCtrlRing* ctrl_ = nullptr;     // pinned, coherent: the control mailbox
+  uint64_t ctrl_head_ = 0;           // (ctrl_mu_) entries posted
+  std::mutex ctrl_mu_;
+  std::vector<std::pair<uint64_t, uint64_t>> ctrl_regions_;   // (mu_) writable device ranges
   uint32_t lds_tiles_ = 0;
   uint32_t set_serial_ = 0;
 };
@@ -259,6 +301,7 @@ struct RingLaunch {
   const RingTableSet* sets;   // coop: the two table sets
   uint32_t lds_tiles;         // coop: ACL tiles the LDS layout is sized for (>= any set's tiles)
   uint32_t epoch0;            // epoch at launch (its set bit names the set to stage first)
+  RingCtrlRing* ctrl;         // device view of the control mailbox
 };
 hipError_t launch_ring(const RingLaunch& r, const LaunchCfg& cfg, int wgs_per_cu, bool coop, hipStream_t s);
 

@@ -32,6 +32,7 @@ struct RingArgs {
   SideOut side;           // side list (cnt null = off): slots needing replicas / learn events / outer headers
   uint32_t flags_bits;  // bit2: no per-flow counts; bits 5/6: diagnostics (kRingTrace, kRingNoCounters)
   uint32_t nq;          // queues: workgroup b serves queue b % nq (ctl / st / flags / svc / slots per queue)
+  RingCtrlRing* ctrl;   // control mailbox (pinned host memory, device view)
 };
 // Frames are read and written with system-coherent buffer ops (sc0 sc1): the loads never hit a
 // stale L2 line of a slot a producer (host / NIC DMA) rewrote, and the stores write through to
@@ -101,7 +102,7 @@ __device__ __forceinline__ unsigned long long rfl64(unsigned long long v) {
 template <class OnIdle>
 __device__ __forceinline__ bool ring_wait_chunk(const RingArgs& a, RingCtl* ctl, RingDevState* st, uint32_t lane,
                                                 unsigned long long t_begin, unsigned long long& tk_out,
-                                                uint32_t& epoch_out, OnIdle on_idle) {
+                                                uint32_t& epoch_out, uint32_t& gen_out, OnIdle on_idle) {
   unsigned long long tk = 0;
   if (lane == 0) tk = atomicAdd(&st->claim, 1ull);
   tk = rfl64(tk);
@@ -110,7 +111,10 @@ __device__ __forceinline__ bool ring_wait_chunk(const RingArgs& a, RingCtl* ctl,
   const unsigned long long need = first + 64ull;
   for (;;) {
     unsigned long long v = 0;
+    uint32_t g = 0;
     if (lane == 0) {
+      // the control-mailbox generation rides along with the poll (two loads in flight together)
+      g = __hip_atomic_load(&a.st->ctl_gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       v = __hip_atomic_load(&st->dprod, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (ring_count(v) < need && ring_count(v) == first && !(v & kRingStop)) {
         // frontier wave (its chunk is the first unpublished one): the only PCIe poller
@@ -128,6 +132,7 @@ __device__ __forceinline__ bool ring_wait_chunk(const RingArgs& a, RingCtl* ctl,
       // older than the last flip has count <= the flip point, so only chunks below it (the
       // grace period's) can still use the previous copy
       epoch_out = ring_epoch(v);
+      gen_out = __builtin_amdgcn_readfirstlane(g);
       return true;
     }
     on_idle();                        // no published work for this wave: settle its bookkeeping
@@ -153,7 +158,7 @@ template <int HASH, int ACL, bool COOP, bool V6 = false>
 __global__ __launch_bounds__(kRingBlock) void ring_kernel(RingArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ unsigned long long coop_tk;                      // ticket
-  __shared__ uint32_t coop_ctl[3];                            // go, epoch, table-set serial
+  __shared__ uint32_t coop_ctl[4];                            // go, epoch, table-set serial, ctl gen
   __shared__ uint32_t coop_best[COOP ? kRingWaves : 1][64];   // per-wave ACL partial minima
   __shared__ RingTableSet lset;                               // coop: the table set in use (LDS copy)
   const RingLds L = ring_lds(HASH, ACL, COOP ? a.lds_tiles : a.acl_tiles);
@@ -167,6 +172,8 @@ __global__ __launch_bounds__(kRingBlock) void ring_kernel(RingArgs a) {
   // (Re)stage the small tables of a table set into LDS: all threads of the workgroup call it.
   // Non-coop rings stage the launch tables once (a commit drains and relaunches them).
   uint32_t cur_set = 0, cur_serial = 0, nport = 0, nchain = 0;
+  // control-mailbox generation the LDS copies reflect (read before the first staging)
+  uint32_t cur_gen = __hip_atomic_load(&a.st->ctl_gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   bool lds_perm = false;
   auto stage = [&](const TablesView& t, const v4i* wf, const v4i* ci, uint32_t tiles, const v4i* tf,
                    const uint32_t* tt) {
@@ -225,13 +232,58 @@ __global__ __launch_bounds__(kRingBlock) void ring_kernel(RingArgs a) {
   const __amdgpu_buffer_rsrc_t r_meta = __builtin_amdgcn_make_buffer_rsrc((void*)(a.out_meta + qslot0), (short)0, (int)(rbytes / 16), kBufRaw);
   const bool counters = !(a.flags_bits & kRingNoCounters);
   uint32_t since_flush = 0;  // chunks this wave added to the LDS counters since its last flush
-  auto on_idle = [&]() {
-    if (since_flush) { flush_lds_counters(pc, drops, a.port_ctr, a.drop_ctr); since_flush = 0; }
-  };
-
   const uint32_t wave = threadIdx.x >> 6;
   uint4* kx = reinterpret_cast<uint4*>(smem + L.kx) + wave * 64;
   const uint32_t lane = threadIdx.x & 63u;
+
+  // ---- control mailbox (ring.h RingCtrlRing): workgroup 0's wave 0 applies posted writes ----
+  const bool poller = blockIdx.x == 0 && wave == 0 && a.ctrl != nullptr;
+  unsigned long long ctrl_n = 0, ctrl_t = 0;
+  uint32_t ctrl_tick = 0;
+  if (poller) {
+    unsigned long long d0 = 0;
+    if (lane == 0) d0 = __hip_atomic_load(&a.ctrl->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    ctrl_n = rfl64(d0);
+  }
+  auto poll_ctrl = [&]() {   // EXEC full
+    unsigned long long h = 0;
+    if (lane == 0) h = __hip_atomic_load(&a.ctrl->head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    h = rfl64(h);
+    const unsigned long long n0 = ctrl_n;
+    while (ctrl_n < h && ctrl_n - n0 < kCtrlSlots) {
+      RingCtrlEntry* e = a.ctrl->e + (ctrl_n % kCtrlSlots);
+      uint32_t sq = 0, lo = 0, hi = 0, nw = 0;
+      if (lane == 0) {
+        sq = __hip_atomic_load(&e->seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+        lo = __hip_atomic_load(reinterpret_cast<uint32_t*>(&e->dst), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        hi = __hip_atomic_load(reinterpret_cast<uint32_t*>(&e->dst) + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        nw = __hip_atomic_load(&e->nwords, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      if (__builtin_amdgcn_readfirstlane(sq) != (uint32_t)(ctrl_n + 1)) break;   // not visible yet: next poll
+      uint32_t* dst = reinterpret_cast<uint32_t*>(((unsigned long long)__builtin_amdgcn_readfirstlane(hi) << 32) |
+                                                  __builtin_amdgcn_readfirstlane(lo));
+      const uint32_t n = min(__builtin_amdgcn_readfirstlane(nw), kCtrlWords);
+      if (lane < n) {
+        const uint32_t v = __hip_atomic_load(&e->data[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(dst + lane, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      ++ctrl_n;
+    }
+    if (ctrl_n == n0) return;
+    // the writes reach every XCD before the generation moves; then the host hears it
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    if (lane == 0) {
+      __hip_atomic_fetch_add(&a.st->ctl_gen, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&a.ctrl->done, ctrl_n, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  };
+  auto on_idle = [&]() {
+    if (since_flush) { flush_lds_counters(pc, drops, a.port_ctr, a.drop_ctr); since_flush = 0; }
+    if (poller) {   // idle: look at the mailbox at most every microsecond (one PCIe read)
+      const unsigned long long tn = __builtin_amdgcn_s_memrealtime();
+      if (tn - ctrl_t >= 100) { ctrl_t = tn; poll_ctrl(); }
+    }
+  };
   const uint32_t nch_mask = a.ring_mask >> 6;  // R/64 - 1
   const unsigned long long t_begin = __builtin_amdgcn_s_memrealtime();
   uint32_t seen_epoch = 0xFFFFFFFFu;  // epoch of this wave's previous chunk
@@ -244,7 +296,8 @@ __global__ __launch_bounds__(kRingBlock) void ring_kernel(RingArgs a) {
     uint32_t epoch = 0;
     if constexpr (COOP) {
       if (wave == 0) {
-        const bool go = ring_wait_chunk(a, qctl, qst, lane, t_begin, tk, epoch, on_idle);
+        uint32_t gen = cur_gen;
+        const bool go = ring_wait_chunk(a, qctl, qst, lane, t_begin, tk, epoch, gen, on_idle);
         // the serial of the set this epoch names, read only when the epoch moved (or the
         // workgroup idled long enough for the epoch value to have come round again)
         uint32_t ser = cur_serial;
@@ -256,14 +309,15 @@ __global__ __launch_bounds__(kRingBlock) void ring_kernel(RingArgs a) {
         }
         w0_epoch = epoch;
         w0_t = tn;
-        if (lane == 0) { coop_tk = tk; coop_ctl[0] = go ? 1u : 0u; coop_ctl[1] = epoch; coop_ctl[2] = ser; }
+        if (lane == 0) { coop_tk = tk; coop_ctl[0] = go ? 1u : 0u; coop_ctl[1] = epoch; coop_ctl[2] = ser; coop_ctl[3] = gen; }
       }
       __syncthreads();
       tk = rfl64(coop_tk);
       epoch = __builtin_amdgcn_readfirstlane(coop_ctl[1]);
       if (!__builtin_amdgcn_readfirstlane(coop_ctl[0])) break;
     } else {
-      if (!ring_wait_chunk(a, qctl, qst, lane, t_begin, tk, epoch, on_idle)) break;
+      uint32_t gen = 0;   // (non-coop rings stage their LDS copies at launch only)
+      if (!ring_wait_chunk(a, qctl, qst, lane, t_begin, tk, epoch, gen, on_idle)) break;
     }
     const unsigned long long t_avail = __builtin_amdgcn_s_memrealtime();
     if (epoch != seen_epoch || t_avail - seen_t > kEpochAliasTicks) {
@@ -283,6 +337,17 @@ __global__ __launch_bounds__(kRingBlock) void ring_kernel(RingArgs a) {
       // so the branch is uniform and the barriers inside are safe
       const uint32_t want = (epoch & kEpochSetBit) >> 1;
       if (want != cur_set || __builtin_amdgcn_readfirstlane(coop_ctl[2]) != cur_serial) stage_set(want);
+      // control-mailbox writes applied since this workgroup staged its copies: restage the small
+      // tables (ports, chain words, ACL verdicts) from the set's device buffers, which hold them
+      const uint32_t gen = __builtin_amdgcn_readfirstlane(coop_ctl[3]);
+      if (gen != cur_gen) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        __syncthreads();   // no wave still reads the LDS copies
+        const LdsTables s1 = stage_lds_tables(lset.t, lport, lchain, lperm, true, kRingBlock);
+        nport = s1.nport; nchain = s1.nchain; lds_perm = s1.lds_perm;
+        __syncthreads();
+        cur_gen = gen;
+      }
     }
     const TablesView& T = COOP ? lset.t : a.t;
     const LdsTables ta{T, lport, lchain, lperm, nport, nchain, lds_perm};
@@ -396,6 +461,7 @@ __global__ __launch_bounds__(kRingBlock) void ring_kernel(RingArgs a) {
     // per-lane count inside the branch above left a port's tallies behind for good whenever its
     // lane had been a filler lane of every chunk since its last flush.)
     if (counters && ++since_flush >= kFlushChunks) on_idle();
+    if (poller && (++ctrl_tick & 15u) == 0) poll_ctrl();   // busy: the mailbox every 16 chunks
     NFDP_RING_MARK(tr5)
 #undef NFDP_RING_MARK
     if (trace && lane == 0 && qsvc) {
@@ -442,6 +508,7 @@ hipError_t launch_ring(const RingLaunch& r, const LaunchCfg& cfg, int wgs_per_cu
   a.sets = r.sets;
   a.lds_tiles = r.lds_tiles;
   a.epoch0 = r.epoch0;
+  a.ctrl = r.ctrl;
   a.nq = r.queues ? r.queues : 1u;
   // every queue needs a workgroup; the side list indexes slots of one ring only
   if ((uint64_t)cfg.num_cus * (uint64_t)wgs_per_cu < a.nq || (a.nq > 1 && a.side.cnt)) return hipErrorInvalidValue;
@@ -501,6 +568,9 @@ RingEngine::RingEngine(uint32_t capacity, int num_cus, int wgs_per_cu, bool coop
      "host alloc flags");
   std::memset(ctl_, 0, sizeof(RingCtl) * nq_);
   std::memset(flags_, 0, (size_t)nq_ * nch_ * 4);
+  ck(hipHostMalloc(reinterpret_cast<void**>(&ctrl_), sizeof(RingCtrlRing), hipHostMallocCoherent | hipHostMallocMapped),
+     "host alloc ctrl");
+  std::memset(ctrl_, 0, sizeof(RingCtrlRing));
   ck(hipMalloc(reinterpret_cast<void**>(&st_), sizeof(RingDevState) * nq_), "dev alloc state");
   // Slots: HBM (the wire side is the GPU: NIC DMA into device memory), or pinned coherent host
   // memory (host-resident rings — pod vhost / AF_XDP style): the kernel's system-coherent buffer
@@ -545,6 +615,7 @@ RingEngine::~RingEngine() {
   }
   (void)hipHostFree(ctl_);
   (void)hipHostFree(flags_);
+  (void)hipHostFree(ctrl_);
 }
 
 void RingEngine::start(const FusedLaunch& f, const LaunchCfg& cfg, double deadline_s, const void* flows_alt) {
@@ -574,6 +645,15 @@ void RingEngine::start(const FusedLaunch& f, const LaunchCfg& cfg, double deadli
   r.sets = d_sets_;
   r.lds_tiles = lds_tiles_;
   r.epoch0 = ep;
+  {
+    // entries posted but not applied by a previous session are dropped: the relaunch stages the
+    // host's tables, which hold them already
+    std::lock_guard<std::mutex> gc(ctrl_mu_);
+    __atomic_store_n(&ctrl_->done, ctrl_head_, __ATOMIC_RELEASE);
+    void* dc = nullptr;
+    ck(hipHostGetDevicePointer(&dc, ctrl_, 0), "device ptr ctrl");
+    r.ctrl = reinterpret_cast<RingCtrlRing*>(dc);
+  }
   r.pkts = d_in_; r.inmeta = d_im_; r.out = d_out_; r.out_meta = d_meta_;
   r.ring_mask = cap_ - 1;
   r.queues = nq_;
@@ -749,6 +829,50 @@ void RingEngine::set_epoch(uint32_t e) {
   if (running_) throw std::runtime_error("ring: set_epoch while running");
   std::lock_guard<std::mutex> g(mu_);
   set_epoch_all(e & (uint32_t)kRingEpochMask);
+}
+
+uint64_t RingEngine::post_write(uint64_t dst, const uint32_t* data, uint32_t n, double timeout_s) {
+  if (n == 0 || n > kCtrlWords) throw std::invalid_argument("ring: a control write is 1..12 dwords");
+  if (dst == 0 || (dst & 3u)) throw std::invalid_argument("ring: control write to a null / unaligned address");
+  bool ok = false;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    for (const auto& r : ctrl_regions_)
+      ok = ok || (dst >= r.first && dst + 4ull * n <= r.first + r.second);
+  }
+  if (!ok) throw std::invalid_argument("ring: control write outside the registered table buffers");
+  if (!running_) throw std::runtime_error("ring: control write with no grid running");
+  std::lock_guard<std::mutex> g(ctrl_mu_);
+  const auto t0 = Clock::now();
+  while (ctrl_head_ - __atomic_load_n(&ctrl_->done, __ATOMIC_ACQUIRE) >= kCtrlSlots) {   // mailbox full
+    if (secs(t0, Clock::now()) > timeout_s || !alive()) throw std::runtime_error("ring: control mailbox not drained");
+    _mm_pause();
+  }
+  RingCtrlEntry& e = ctrl_->e[ctrl_head_ % kCtrlSlots];
+  e.dst = dst;
+  e.nwords = n;
+  std::memcpy(e.data, data, 4ull * n);
+  __atomic_store_n(&e.seq, (uint32_t)(ctrl_head_ + 1), __ATOMIC_RELEASE);
+  ++ctrl_head_;
+  __atomic_store_n(&ctrl_->head, ctrl_head_, __ATOMIC_RELEASE);
+  return ctrl_head_;
+}
+
+uint64_t RingEngine::ctrl_done() const { return __atomic_load_n(&ctrl_->done, __ATOMIC_ACQUIRE); }
+
+bool RingEngine::wait_ctrl(uint64_t seq, double timeout_s) {
+  const auto t0 = Clock::now();
+  uint32_t spin = 0;
+  while (ctrl_done() < seq) {
+    _mm_pause();
+    if ((++spin & 1023u) == 0 && (secs(t0, Clock::now()) > timeout_s || !alive())) return ctrl_done() >= seq;
+  }
+  return true;
+}
+
+void RingEngine::set_ctrl_regions(const std::vector<std::pair<uint64_t, uint64_t>>& regions) {
+  std::lock_guard<std::mutex> g(mu_);
+  ctrl_regions_ = regions;
 }
 
 bool RingEngine::wait(uint64_t end, double timeout_s, uint32_t q) {

@@ -114,7 +114,9 @@ class DataPlanePorts:
         p.set_link(port, link)
         p.set_rx(port, rx)
         p.set_mtu(port, mtu)
-        self.dp.commit()
+        ctrl = getattr(self.dp, "ctrl_ports", None)   # running rings: their control mailbox
+        if ctrl is None or not ctrl([port]):
+            self.dp.commit()
 
 
 class PortStateSync:

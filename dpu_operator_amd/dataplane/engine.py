@@ -334,12 +334,52 @@ class DataPlane:
             tables["flows"], tables["flows_alt"] = self.flow_copy_ptrs()
             args = {"acl_wfrag": self._ptr("acl_wfrag"), "acl_cinit": self._ptr("acl_cinit"),
                     "acl_tiles": self._acl_tiles, "toep_frag": self._ptr("toep_frag"), "toep_tab": self._ptr("toep_tab")}
+            regions = self.ctrl_regions()
             for r in rings:
                 with r.lock:
                     r.eng.stage_tables(tables, args, 1 - int(r.eng.table_set))
+                    r.eng.set_ctrl_regions(regions)
             sent["table_flip"] = True
         self.flip_stats["grace_s"] += t1 - t0
         return {"sent": sent, "flow": flow, "set": tset, "dirty": dirty, "t0": t0, "t1": t1}
+
+    # ------------------------------------------------------------------ device control mailbox
+    CTRL_TABLES = ("ports", "chains", "acl_permit", "macs")
+
+    def ctrl_regions(self) -> list[tuple[int, int]]:
+        """Device buffers a running ring's control mailbox may write: the small tables of the
+        current table set (flow tables are excluded: they change only through the epoch flip)."""
+        out = []
+        for name in self.CTRL_TABLES:
+            b = self._dev.get(name)
+            if b is not None and self.gpu:
+                out.append((int(b.data_ptr()), int(b.numel() * b.element_size())))
+        return out
+
+    def ctrl_ports(self, ports, timeout_s: float = 1.0) -> bool:
+        """Push the host's entries of `ports` to the running coop rings through their control
+        mailbox (ring.h RingCtrlRing): the resident grid writes them into its port table and every
+        workgroup restages its LDS port copies.  A ctrl-net link / RX-state / MTU change this way
+        costs no commit, no epoch change and no hold (a few microseconds of the poller wave).  The
+        host model keeps the change; the next commit uploads it with everything else.  Returns
+        False, having done nothing, when no coop ring runs (then commit() is the way)."""
+        rings = [r for r in self._running_rings() if getattr(r, "coop", False)]
+        if not rings or not self.gpu or "ports" not in self._dev:
+            return False
+        base = int(self._dev["ports"].data_ptr())
+        size = self.ports.a.dtype.itemsize
+        writes = [(base + int(p) * size, self.ports.a[int(p)].tobytes()) for p in ports]
+        for r in rings:
+            seq = 0
+            for dst, data in writes:
+                seq = r.eng.post_write(dst, data, timeout_s)
+            if not r.eng.wait_ctrl(seq, timeout_s):
+                raise TimeoutError("ring: control mailbox write not applied")
+        for h in getattr(self, "_io_hooks", ()):
+            if hasattr(h, "refresh"):
+                h.refresh(self)   # the native engine's side-pass snapshot follows
+        self.flip_stats["ctrl_writes"] = self.flip_stats.get("ctrl_writes", 0) + len(writes)
+        return True
 
     def _live_flip(self, rings, prep: dict) -> None:
         """The switch: one epoch change per ring (flow copy and / or table set together)."""

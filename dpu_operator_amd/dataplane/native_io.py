@@ -305,6 +305,12 @@ class NativeLivePath:
         self._eng.switch_tables(list(engs), list(flows), list(sets), c["side"], sp, rd)
         self._applied = {"side_ports": c["side_ports"], "redirects": c["redirects"], "steer": st}
 
+    def refresh(self, dp) -> None:
+        """Rebuild and swap the engine's configuration now (copy-on-write, no hold): after table
+        writes that went through the rings' control mailbox (DataPlane.ctrl_ports)."""
+        if self._eng is not None:
+            self._apply(self._collect())
+
     def _refresh(self) -> None:
         """Point the oracle backends at the current tables; the side-pass table snapshots, side
         ports, tunnel redirects and steering (copy-on-write in the engine)."""

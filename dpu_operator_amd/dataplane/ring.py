@@ -138,6 +138,7 @@ class RingPath:
         self.eng.set_epoch(self.dp._flow_active)
         self.eng.start(self._tables(), self._args(), self.dp.hash_mode, self.dp.acl_mode,
                        self.cus, self.deadline_s)
+        self.eng.set_ctrl_regions(self.dp.ctrl_regions())
         self.launches += 1
 
     def stop(self, timeout_s: float = 30.0) -> None:
@@ -151,6 +152,7 @@ class RingPath:
             self.eng.set_epoch(self.dp._flow_active)
             self.eng.start(self._tables(), self._args(), self.dp.hash_mode, self.dp.acl_mode,
                            self.cus, self.deadline_s)
+            self.eng.set_ctrl_regions(self.dp.ctrl_regions())
             self.launches += 1
 
     def ensure_alive(self) -> bool:

@@ -236,7 +236,10 @@ class GpuVsp(VspBase):
             self.port_state[port] = (bool(link), bool(rx), int(mtu))
             if self.dp is not None and (port in self.vports or port == WIRE_PORT):
                 self._apply_port_state(port)
-                self._commit()
+                # running rings take it through their control mailbox (no commit); else commit
+                ctrl = getattr(self.dp, "ctrl_ports", None)
+                if ctrl is None or not ctrl([port]):
+                    self._commit()
 
     def attach_agent(self, agent, state_period_s: float = 0.05, stats_period_s: float = 1.0):
         """Close the loops with the node agent: interface state -> GPU port flags, port

@@ -299,3 +299,66 @@ def test_live_commits_at_1khz_under_traffic(tmp_path):
         assert c99 < b99 + 50.0
     finally:
         live.stop()
+
+
+@pytest.mark.gpu
+def test_ctrl_mailbox_link_state_without_commit(tmp_path):
+    """ctrl-net link state through the rings' control mailbox (ring.h RingCtrlRing): the resident
+    grid writes the port entry itself and every workgroup restages its LDS port copy.  No commit,
+    no epoch change; frames to the downed port are dropped exactly as the oracle drops them, and
+    flow again once the link comes back - bit-exact with the batch path both ways."""
+    nf = nfdp()
+    dp, sc = _sfc("cuda")
+    ref, _ = _sfc("cpu")
+    live = NativeLivePath(dp, _vports(tmp_path, sc.n_pods, "x"), burst=256, ring_capacity=4096, queues=2).start()
+    try:
+        eps = {i: nf.MemifEndpoint(str(tmp_path / f"x{i}")) for i in range(sc.n_pods)}
+        victim = int(sc.pod_port[2])
+
+        def run(seed):
+            slots, im = S.traffic(sc, 2000, seed=seed)
+            exp, drops = _expected(ref, slots, im)
+            src = im & 0xFFFF
+            for i in range(sc.n_pods):
+                fr = [bytes(slots[k, : int(im[k] >> 16)]) for k in np.nonzero(src == i)[0]]
+                sent = 0
+                while sent < len(fr):
+                    sent += eps[i].send(fr[sent:])
+            got = {i: [] for i in range(sc.n_pods)}
+            want = sum(map(len, exp.values()))
+
+            def drained():
+                for i in range(sc.n_pods):
+                    got[i] += eps[i].recv()
+                return sum(map(len, got.values())) >= want
+
+            assert _until(drained, 10), (live.stats, live.error)
+            time.sleep(0.05)
+            for i in range(sc.n_pods):
+                got[i] += eps[i].recv()
+            for port in range(sc.n_pods):
+                assert sorted(got[port]) == sorted(exp.get(port, [])), port
+            return drops
+
+        run(41)
+        ring = live._rings[0]
+        epoch0, flips0 = ring.eng.epoch, dp.flip_stats.get("table_flips", 0)
+        for up in (False, True):
+            dp.ports.set_link(victim, up)
+            ref.ports.set_link(victim, up)
+            ref.commit()
+            t0 = time.perf_counter()
+            assert dp.ctrl_ports([victim])
+            dt = time.perf_counter() - t0
+            drops = run(42 if not up else 43)
+            print(f"link {'up' if up else 'down'} via the control mailbox in {dt * 1e6:.0f} us; "
+                  f"{drops} frames dropped by the oracle")
+            if not up:
+                assert drops > 0
+        assert ring.eng.epoch == epoch0 and dp.flip_stats.get("table_flips", 0) == flips0   # no commit
+        assert ring.eng.ctrl_done == ring.eng.ctrl_posted >= 2
+        # the engine refuses writes outside the registered table buffers
+        with pytest.raises(Exception):
+            ring.eng.post_write(8, b"\0" * 4)
+    finally:
+        live.stop()
