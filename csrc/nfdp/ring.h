@@ -169,7 +169,7 @@ class RingEngine {
   }
   bool running() const { return running_; }
   // The grid is still resident (false once every wave left: stop, or the device deadline passed).
-  bool alive() const { return running_ && hipStreamQuery(stream_) == hipErrorNotReady; }
+  bool alive() const { return running_ && stream_ && hipStreamQuery(stream_) == hipErrorNotReady; }
   bool host_slots() const { return host_slots_; }
   // device ring buffers (the producer stages frames here before publishing them); queue q's
   // slots follow queue q-1's (q * capacity slots in)
@@ -246,6 +246,7 @@ class RingEngine {
 
  private:
   bool chunk_done(uint64_t chunk, uint32_t q) const;
+  void release_streams();   // after the grid exited: the launch and staging streams go
   void pace_epoch_change();
   // (mu_ held) a new epoch for every queue: each queue's flip point is its published count now
   void set_epoch_all(uint32_t e);

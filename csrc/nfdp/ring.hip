@@ -596,7 +596,8 @@ RingEngine::RingEngine(uint32_t capacity, int num_cus, int wgs_per_cu, bool coop
   ck(hipMalloc(reinterpret_cast<void**>(&d_sets_), 2 * sizeof(RingTableSet)), "dev alloc table sets");
   ck(hipMemset(d_sets_, 0, 2 * sizeof(RingTableSet)), "memset");
   ck(hipMemset(d_svc_, 0, (size_t)nq_ * nch_ * 4 * kSvcWords), "memset");
-  ck(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "stream");
+  // (the launch stream is created by start() and destroyed by stop(): a resident grid holds its
+  // stream's hardware queue, and a stopped ring should not keep one that other streams then share)
 }
 
 RingEngine::~RingEngine() {
@@ -604,9 +605,7 @@ RingEngine::~RingEngine() {
     if (running_) stop(60.0);
   } catch (...) {
   }
-  (void)hipStreamSynchronize(stream_);
-  (void)hipStreamDestroy(stream_);
-  if (stage_stream_) (void)hipStreamDestroy(stage_stream_);
+  release_streams();
   for (void* d : {(void*)st_, (void*)d_svc_, (void*)d_sets_}) (void)hipFree(d);
   if (host_slots_) {
     for (void* h : host_ptrs_) (void)hipHostFree(h);
@@ -633,6 +632,7 @@ void RingEngine::start(const FusedLaunch& f, const LaunchCfg& cfg, double deadli
     s[q].dprod = ring_word(p, ep);
     __atomic_store_n(&ctl_[q].prod, ring_word(p, ep), __ATOMIC_RELEASE);
   }
+  if (!stream_) ck(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "stream");
   ck(hipMemcpyAsync(st_, s.data(), sizeof(RingDevState) * nq_, hipMemcpyHostToDevice, stream_), "state upload");
   ck(hipStreamSynchronize(stream_), "state upload");  // `s` lives on this stack frame
   launch_ = f;
@@ -690,8 +690,22 @@ void RingEngine::stop(double timeout_s) {
     std::this_thread::sleep_for(std::chrono::microseconds(50));
   }
   running_ = false;
+  release_streams();
   for (uint32_t q = 0; q < nq_; ++q)
     if (completed(q) != published(q)) throw std::runtime_error("ring: stopped with published chunks unprocessed");
+}
+
+void RingEngine::release_streams() {
+  if (stream_) {
+    (void)hipStreamSynchronize(stream_);
+    (void)hipStreamDestroy(stream_);
+    stream_ = nullptr;
+  }
+  std::lock_guard<std::mutex> g(mu_);
+  if (stage_stream_) {
+    (void)hipStreamDestroy(stage_stream_);
+    stage_stream_ = nullptr;
+  }
 }
 
 bool RingEngine::chunk_done(uint64_t chunk, uint32_t q) const {
