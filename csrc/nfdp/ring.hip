@@ -245,31 +245,28 @@ __global__ __launch_bounds__(kRingBlock) void ring_kernel(RingArgs a) {
     if (lane == 0) d0 = __hip_atomic_load(&a.ctrl->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     ctrl_n = rfl64(d0);
   }
-  auto poll_ctrl = [&]() {   // EXEC full
-    unsigned long long h = 0;
-    if (lane == 0) h = __hip_atomic_load(&a.ctrl->head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    h = rfl64(h);
+  auto poll_ctrl = [&]() {   // EXEC full; every lane reads the same words (one request per wave)
+    const unsigned long long h = __hip_atomic_load(&a.ctrl->head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     const unsigned long long n0 = ctrl_n;
-    while (ctrl_n < h && ctrl_n - n0 < kCtrlSlots) {
-      RingCtrlEntry* e = a.ctrl->e + (ctrl_n % kCtrlSlots);
-      uint32_t sq = 0, lo = 0, hi = 0, nw = 0;
-      if (lane == 0) {
-        sq = __hip_atomic_load(&e->seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
-        lo = __hip_atomic_load(reinterpret_cast<uint32_t*>(&e->dst), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        hi = __hip_atomic_load(reinterpret_cast<uint32_t*>(&e->dst) + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        nw = __hip_atomic_load(&e->nwords, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      }
+    bool moved = false;
+    while (__builtin_amdgcn_readfirstlane((uint32_t)(ctrl_n < h && ctrl_n - n0 < kCtrlSlots))) {
+      RingCtrlEntry* ent = a.ctrl->e + (ctrl_n % kCtrlSlots);
+      const uint32_t sq = __hip_atomic_load(&ent->seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
       if (__builtin_amdgcn_readfirstlane(sq) != (uint32_t)(ctrl_n + 1)) break;   // not visible yet: next poll
-      uint32_t* dst = reinterpret_cast<uint32_t*>(((unsigned long long)__builtin_amdgcn_readfirstlane(hi) << 32) |
-                                                  __builtin_amdgcn_readfirstlane(lo));
-      const uint32_t n = min(__builtin_amdgcn_readfirstlane(nw), kCtrlWords);
+      const unsigned long long dst64 = __hip_atomic_load(&ent->dst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      const uint32_t nw = __hip_atomic_load(&ent->nwords, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      const uint32_t n = min(nw, kCtrlWords);
       if (lane < n) {
-        const uint32_t v = __hip_atomic_load(&e->data[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(dst + lane, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t v = __hip_atomic_load(&ent->data[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(reinterpret_cast<uint32_t*>(dst64) + lane, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
+#ifdef NFDP_CTRL_DEBUG
+      if (lane == 0) printf("ctrl poll: h %llu n0 %llu entry %llu seq %u dst %llx words %u\n", h, n0, ctrl_n, sq, dst64, n);
+#endif
       ++ctrl_n;
+      moved = true;
     }
-    if (ctrl_n == n0) return;
+    if (!moved) return;
     // the writes reach every XCD before the generation moves; then the host hears it
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     if (lane == 0) {
@@ -341,6 +338,9 @@ __global__ __launch_bounds__(kRingBlock) void ring_kernel(RingArgs a) {
       // tables (ports, chain words, ACL verdicts) from the set's device buffers, which hold them
       const uint32_t gen = __builtin_amdgcn_readfirstlane(coop_ctl[3]);
       if (gen != cur_gen) {
+#ifdef NFDP_CTRL_DEBUG
+        if (threadIdx.x == 0) printf("restage: block %u gen %u -> %u ports %p\n", blockIdx.x, cur_gen, gen, (const void*)lset.t.ports);
+#endif
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         __syncthreads();   // no wave still reads the LDS copies
         const LdsTables s1 = stage_lds_tables(lset.t, lport, lchain, lperm, true, kRingBlock);
