@@ -369,12 +369,15 @@ class DataPlane:
         base = int(self._dev["ports"].data_ptr())
         size = self.ports.a.dtype.itemsize
         writes = [(base + int(p) * size, self.ports.a[int(p)].tobytes()) for p in ports]
+        t0 = time.perf_counter()
         for r in rings:
             seq = 0
             for dst, data in writes:
                 seq = r.eng.post_write(dst, data, timeout_s)
             if not r.eng.wait_ctrl(seq, timeout_s):
-                raise TimeoutError("ring: control mailbox write not applied")
+                raise TimeoutError(f"ring: control mailbox write not applied (posted {r.eng.ctrl_posted}, "
+                                   f"done {r.eng.ctrl_done}, alive {r.eng.alive()})")
+        self.flip_stats["ctrl_last_s"] = time.perf_counter() - t0   # post -> applied by every grid
         for h in getattr(self, "_io_hooks", ()):
             if hasattr(h, "refresh"):
                 h.refresh(self)   # the native engine's side-pass snapshot follows

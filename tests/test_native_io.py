@@ -351,7 +351,8 @@ def test_ctrl_mailbox_link_state_without_commit(tmp_path):
             assert dp.ctrl_ports([victim])
             dt = time.perf_counter() - t0
             drops = run(42 if not up else 43)
-            print(f"link {'up' if up else 'down'} via the control mailbox in {dt * 1e6:.0f} us; "
+            print(f"link {'up' if up else 'down'} via the control mailbox in {dt * 1e6:.0f} us "
+                  f"({dp.flip_stats['ctrl_last_s'] * 1e6:.1f} us of it from post to applied on the GPU); "
                   f"{drops} frames dropped by the oracle")
             if not up:
                 assert drops > 0
