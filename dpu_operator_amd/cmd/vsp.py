@@ -54,16 +54,35 @@ def build_vsp(a, pm: PathManager):
     plat, nl, runner = SysfsPlatform(a.sys_root), RtNetlink(), HostRunner()
 
     def dataplane():
+        """One GPU, or with --gpus N|all every one behind a MultiDataPlane (tables replicated,
+        flows sharded by RSS owner, the OvS flow tables compiled once for all of them)."""
         from ..dataplane.engine import DataPlane
+        from ..dataplane.multi import MultiDataPlane, visible_devices
 
-        dp = DataPlane(device=a.device or "cuda", flow_buckets=a.flow_buckets or node_config().flow_buckets)
+        buckets = a.flow_buckets or node_config().flow_buckets
+        n = len(visible_devices()) if a.gpus == "all" else int(a.gpus)
+        if n > 1:
+            dp = MultiDataPlane(visible_devices()[:n], flow_buckets=buckets)
+        else:
+            dp = DataPlane(device=a.device or "cuda", flow_buckets=buckets)
         dp.commit(full=True)
         return dp
+
+    def live_path(dp):
+        """--live: the bridge's netdev ports (uplink, VF representors, NF ports) run on the native
+        I/O engine as AF_PACKET ports, ring kernels behind it (started with no port; OvS add-port
+        adds them)."""
+        from ..dataplane.native_io import NativeLivePath
+
+        cfg = node_config()
+        return NativeLivePath(dp, {}, tx_workers=a.io_workers or cfg.io_workers,
+                              queues=a.io_queues or cfg.io_queues).start()
 
     if a.vendor == "marvell":
         from ..vsp import marvell as M
 
-        ddp = M.DebugDataPlane() if a.debug_dp else M.GpuOvsDataPlane(dataplane(), uplink_name=a.uplink)
+        ddp = M.DebugDataPlane() if a.debug_dp else M.GpuOvsDataPlane(
+            dataplane(), uplink_name=a.uplink, live_factory=live_path if a.live else None)
         return M.MarvellVsp(plat, nl, runner, ddp, pm, a.sys_root)
     if a.vendor == "netsec":
         from ..vsp.netsec import NetsecVsp
@@ -93,11 +112,12 @@ def main(argv=None, stop: threading.Event | None = None) -> int:
     ap.add_argument("--mode", default="ipu")
     ap.add_argument("--state-dir", default="", help="amd-gpu: journal + snapshot directory (resume on restart)")
     ap.add_argument("--live", action="store_true",
-                    help="amd-gpu: vports are real TAP netdevs and pod traffic flows through the data plane")
+                    help="amd-gpu: vports are real netdevs and pod traffic flows through the data plane; "
+                         "marvell: the OvS bridge's netdev ports run on the native I/O engine")
     ap.add_argument("--live-engine", default="native", choices=["batch", "ring", "native"],
                     help="amd-gpu --live: fused kernel per poll cycle (Python loop), the persistent ring kernel on "
                          "pinned host slots (Python loop), or the native C++ I/O engine + ring kernel")
-    ap.add_argument("--gpus", default="1", help="amd-gpu: GPUs behind the VSP (a number or 'all'): tables "
+    ap.add_argument("--gpus", default="1", help="amd-gpu / marvell / netsec: GPUs behind the VSP (a number or 'all'): tables "
                     "replicated, flows sharded by RSS owner, the native engine steering frames to their owner")
     ap.add_argument("--vport-kind", default="", choices=["", "veth", "tap", "memif"],
                     help="amd-gpu --live: vports as veth pairs (kernel-netdev pods, AF_PACKET rings), TAP "

@@ -20,6 +20,7 @@ errors are reported instead of silently returning success (main.go:452-459).
 from __future__ import annotations
 
 import logging
+import os
 import re
 import threading
 from dataclasses import dataclass, field
@@ -202,11 +203,16 @@ class GpuOvsDataPlane(MarvellDataPlane):
     """OvS-compatible bridge semantics compiled onto the MI355X DataPlane (dataplane/ovs.py)."""
 
     def __init__(self, dataplane, uplink_name: str | None = None, uplink_port: int = 4000, first_port: int = 0,
-                 mac_of=None):
+                 mac_of=None, live_factory=None):
+        """live_factory(dataplane) -> a started NativeLivePath: the bridge's netdev ports then
+        carry live traffic (each OvS port an AF_PACKET port of the native I/O engine), the way
+        the reference's OvS-DPDK bridge forwards between its DPDK ports (ovsdp.go:39-55)."""
         from ..dataplane.ovs import OvsSwitch
 
         self.dp = dataplane
         self.sw = OvsSwitch(dataplane)
+        self.live_factory = live_factory
+        self.live = None
         self.uplink_name = uplink_name
         self.uplink_port = uplink_port
         self._next = first_port
@@ -226,14 +232,34 @@ class GpuOvsDataPlane(MarvellDataPlane):
         if self.uplink_name:
             br.add_port(self.uplink_name, self.uplink_port)
         self.dp.commit()
+        if self.live_factory is not None and self.live is None:
+            self.live = self.live_factory(self.dp)
+        if self.uplink_name:
+            self._live_add(self.uplink_name, self.uplink_port)
+
+    def _live_add(self, port: str, idx: int) -> None:
+        """A netdev bridge port joins the native engine (ports that are not netdevs here, e.g.
+        DPDK PCI devices bound elsewhere, stay table-only)."""
+        if self.live is not None and os.path.exists(f"/sys/class/net/{port}"):
+            from ..dataplane.native_io import PacketVport
+
+            self.live.add_port(idx, PacketVport(port))
 
     def add_port(self, bridge, port, pci="", dpdk=False):
         self.sw.br(bridge).add_port(port, self._idx(port), mac=self.mac_of(port), pci=pci or None, dpdk=dpdk)
         self.dp.commit()
+        self._live_add(port, self._idx(port))
 
     def delete_port(self, bridge, port):
         self.sw.br(bridge).del_port(port)
+        if self.live is not None and port in self._index:
+            self.live.remove_port(self._index[port])
         self.dp.commit()
+
+    def close(self) -> None:
+        if self.live is not None:
+            self.live.stop()
+            self.live = None
 
     def add_flow_rule(self, bridge, in_port, out_port, dst_mac=""):
         br = self.sw.br(bridge)

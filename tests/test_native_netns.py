@@ -220,3 +220,52 @@ def test_veth_comparator_same_generator(mode):
     assert r["half_p99_us"] is not None and r["idle_p50_us"] is not None
     if mode == "engine":
         assert r["error"] is None and r["engine"]["rx"] > 0
+
+
+@pytest.mark.parametrize("planes", [1, 2])
+def test_marvell_ovs_bridge_live_on_the_native_engine(planes):
+    """The Marvell VSP's OvS bridge on the GPU data plane with live I/O (`vsp --vendor marvell
+    --live [--gpus N]`): every OvS port that is a netdev joins the native engine as an AF_PACKET
+    port, OpenFlow rules program the tables, frames from one netns pod reach the other only where a
+    rule sends them; with two planes (MultiDataPlane) the flows and rules span both."""
+    from dpu_operator_amd.cni.netlink import RtNetlink
+    from dpu_operator_amd.dataplane.engine import DataPlane
+    from dpu_operator_amd.dataplane.multi import MultiDataPlane
+    from dpu_operator_amd.dataplane.native_io import NativeLivePath, PacketVport
+    from dpu_operator_amd.vsp.marvell import GpuOvsDataPlane
+
+    nl = RtNetlink()
+    dp = MultiDataPlane(["cpu"] * planes, flow_buckets=1 << 10) if planes > 1 else DataPlane(device="cpu", flow_buckets=1 << 10)
+    dp.commit(full=True)
+    tag = f"mv{planes}{os.getpid() % 1000}"
+    vps, pods = [], []
+    ovs = GpuOvsDataPlane(dp, live_factory=lambda d: NativeLivePath(d, {}, burst=64, ring_capacity=1024, queues=2).start())
+    try:
+        names = [f"{tag}a", f"{tag}b"]
+        for n in names:
+            vp = PacketVport.create_veth(nl, n)       # pod end n, bridge end n + "d"
+            vps.append(vp)
+            pods.append(NS.RawPod(f"{n}-ns", n, nl))
+        ovs.init_data_plane("br-test")
+        for n in names:
+            ovs.add_port("br-test", n + "d")
+        a, b = ovs.port_index(names[0] + "d"), ovs.port_index(names[1] + "d")
+        assert ovs.live is not None and ovs.live.port(a) is not None and ovs.live.port(b) is not None
+        ovs.add_flow_rule("br-test", names[0] + "d", names[1] + "d")      # a -> b only
+        frame = bytes.fromhex("02000000000b" "02000000000a" "0800") + bytes(46)
+        frames = [frame[:-1] + bytes([i]) for i in range(20)]
+        assert pods[0].send(frames) == 20
+        got = []
+        assert _until(lambda: got.extend(pods[1].recv()) or len(got) >= 20, 5.0), (len(got), ovs.live.stats)
+        assert sorted(got) == sorted(frames)
+        assert pods[1].send(frames[:5]) == 5          # b -> a: no rule, nothing arrives
+        time.sleep(0.3)
+        assert pods[0].recv() == []
+        ovs.delete_port("br-test", names[1] + "d")
+        assert ovs.live.port(b) is None
+    finally:
+        ovs.close()
+        for p in pods:
+            p.close()
+        for v in vps:
+            v.close()
