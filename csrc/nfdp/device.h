@@ -46,7 +46,7 @@ constexpr int kE8M0One = 0x7F7F7F7F;  // block scales 2^0 (every byte)
 // per-tile prefilters [tiles][8] and the per-group (8 tiles) prefilters [groups][8] (host.cpp
 // build_acl_frags).
 constexpr uint32_t kLdsAclTiles = 64;
-constexpr uint32_t kAclGroup = 8;
+constexpr uint32_t kAclGroup = kAclGroupTiles;   // (host.h NFDP_ACL_GROUP)
 constexpr uint32_t kAclIdxBits = 12;                      // rule index bits: up to 4096 rules
 constexpr uint32_t kAclMaxRules = 1u << kAclIdxBits;
 constexpr int kE8M0Idx = 0x8B8B8B8B;                      // block scales 2^12 = 2^kAclIdxBits

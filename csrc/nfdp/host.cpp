@@ -162,7 +162,7 @@ AclFrags build_acl_frags(const uint32_t* value, const uint32_t* mask, uint32_t n
   f.tiles = (n + 15) / 16;
   if (f.tiles == 0) f.tiles = 1;
   const uint32_t npad = f.tiles * 16;
-  const uint32_t groups = (f.tiles + 7) / 8;
+  const uint32_t groups = (f.tiles + kAclGroupTiles - 1) / kAclGroupTiles;
   // placement: sort by the protocol byte (mask, value) first, then by (dst, ports, src, meta)
   // masks and values in network byte order, so a tile holds rules of one protocol and one shape
   // over neighbouring values (e.g. consecutive /24s, low dports): a group of TCP-only rules then
@@ -174,8 +174,10 @@ AclFrags build_acl_frags(const uint32_t* value, const uint32_t* mask, uint32_t n
     const uint32_t* m = mask + 4 * r;
     auto p16 = [](uint32_t raw) { return ((raw & 0xFFu) << 8) | ((raw >> 8) & 0xFFu); };
     const uint32_t mp = (p16(m[2] >> 16) << 16) | p16(m[2] & 0xFFFFu), vp = (p16(v[2] >> 16) << 16) | p16(v[2] & 0xFFFFu);
-    return std::make_tuple(m[3] & 0xFFu, v[3] & m[3] & 0xFFu, bswap32(m[1]), mp, bswap32(m[0]), m[3],
-                           bswap32(v[1] & m[1]), vp & mp, bswap32(v[0] & m[0]), v[3] & m[3], r);
+    // (then destination: specific prefixes before wildcards, by value, so a group's rules share
+    // the destination's leading bits whenever the rule set allows)
+    return std::make_tuple(m[3] & 0xFFu, v[3] & m[3] & 0xFFu, m[1] == 0u, bswap32(v[1] & m[1]), bswap32(m[1]), mp,
+                           bswap32(m[0]), m[3], vp & mp, bswap32(v[0] & m[0]), v[3] & m[3], r);
   };
   std::sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return sig(x) < sig(y); });
   f.wfrag.assign((size_t)f.tiles * 64 * 16, 0);
@@ -213,7 +215,7 @@ AclFrags build_acl_frags(const uint32_t* value, const uint32_t* mask, uint32_t n
     prefilter(value, mask, order.data() + b, e > b ? e - b : 0, pf + 8 * nt);
   }
   for (uint32_t g = 0; g < groups; ++g) {
-    const uint32_t b = g * 128, e = std::min(n, b + 128);
+    const uint32_t b = g * 16 * kAclGroupTiles, e = std::min(n, b + 16 * kAclGroupTiles);
     prefilter(value, mask, order.data() + b, e > b ? e - b : 0, gpf + 8 * g);
   }
   return f;

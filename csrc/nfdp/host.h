@@ -11,6 +11,12 @@
 
 namespace nfdp {
 
+// ACL rule tiles per prefilter group (device.h kAclGroup; host.cpp build_acl_frags).
+#ifndef NFDP_ACL_GROUP
+#define NFDP_ACL_GROUP 8
+#endif
+constexpr uint32_t kAclGroupTiles = NFDP_ACL_GROUP;
+
 // Authoritative host copy of the exact-match flow table.  Bucketized (8 slots) 2-choice cuckoo
 // with eviction; every mutation records the touched bucket so the device copy is kept in sync by
 // re-sending whole buckets (bucket_update_kernel), ordered on the data-plane stream between
