@@ -21,7 +21,7 @@ RECORD = REPO / "dpu_operator_amd" / "native" / "_nfdp.resources.json"
 # (source, mangled-name prefix, max spilled VGPRs, min waves / SIMD)
 BUDGET = [
     # headline: lds hash + MFMA ACL, 1 GPU; and the MFMA-hash twin
-    ("kernels.hip", "_ZN4nfdp12fused_kernelILi1ELi1ELb0ELb0ELb0E", 16, 4),
+    ("kernels.hip", "_ZN4nfdp12fused_kernelILi1ELi1ELb0ELb0ELb0ELb0E", 16, 4),
     ("kernels.hip", "_ZN4nfdp12fused_kernelILi2ELi1ELb0ELb0ELb0E", 24, 4),
     # early-fetch instances (2 waves / SIMD by design): no spills
     ("kernels.hip", "_ZN4nfdp12fused_kernelILi1ELi1ELb0ELb1ELb0E", 0, 2),
