@@ -729,6 +729,8 @@ PYBIND11_MODULE(_nfdp, m) {
       }, py::arg("timeout_s") = 10.0)
       .def_property_readonly("epoch", &RingEngine::epoch)
       .def("set_epoch", &RingEngine::set_epoch)
+      .def("set_frame_addrs", &RingEngine::set_frame_addrs, py::arg("on"))
+      .def_property_readonly("frame_addrs_on", &RingEngine::frame_addrs_on)
       .def("stop", [](RingEngine& r, double timeout_s) { py::gil_scoped_release nogil; r.stop(timeout_s); },
            py::arg("timeout_s") = 30.0)
       .def("completed", &RingEngine::completed, py::arg("q") = 0)
@@ -821,7 +823,8 @@ PYBIND11_MODULE(_nfdp, m) {
         const TablesView t = tables_from(tables);
         b.configure(t, reinterpret_cast<uint64_t*>(flow_ctr), reinterpret_cast<uint64_t*>(port_ctr),
                     reinterpret_cast<uint64_t*>(drop_ctr), const_cast<MacEntry*>(t.macs), t.mac_mask);
-      });
+      })
+      .def("set_frame_addrs", &OracleBackend::set_frame_addrs, py::arg("on"));
   py::class_<WireBackend, OracleBackend, std::shared_ptr<WireBackend>>(m, "WireBackend")
       .def(py::init<uint32_t, uint32_t, const std::vector<std::pair<uint64_t, uint32_t>>&>(), py::arg("capacity"),
            py::arg("queues"), py::arg("mac_to_port"));
@@ -875,6 +878,8 @@ PYBIND11_MODULE(_nfdp, m) {
       .def("set_side_tables", &Engine::set_side_tables)
       .def("set_redirects", &Engine::set_redirects)
       .def("set_coalesce", &Engine::set_coalesce, py::arg("frames") = 64, py::arg("window_us") = 0.0)
+      .def("set_zero_copy", &Engine::set_zero_copy, py::arg("on"))
+      .def_property_readonly("zero_copy", &Engine::zero_copy)
       .def("hold", [](Engine& e) { py::gil_scoped_release nogil; e.hold(); })
       .def("release", &Engine::release)
       .def("flush_learning", [](Engine& e) { py::gil_scoped_release nogil; e.flush_learning(); })

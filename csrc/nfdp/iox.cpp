@@ -89,6 +89,7 @@ MemifPort::MemifPort(const std::string& path, uint32_t ring_size, uint32_t buf_s
 }
 
 MemifPort::~MemifPort() {
+  unmap_rx();   // before the region's mapping goes (the Region member's destructor)
   if (unlink_) ::unlink(reg_.path().c_str());
 }
 
@@ -375,6 +376,12 @@ void OracleBackend::run_segment(uint32_t q, uint32_t pos, uint32_t n) {
              drop_ctr_, nullptr, nullptr, nullptr);
 }
 
+void OracleBackend::set_frame_addrs(bool on) {
+  if (!on) { fa_.clear(); return; }
+  fa_.resize((size_t)cap_ * nq_);
+  for (size_t i = 0; i < fa_.size(); ++i) fa_[i] = reinterpret_cast<uint64_t>(in_.data() + i * kSlotBytes);
+}
+
 uint64_t OracleBackend::publish(uint32_t q, uint32_t n) {
   if (!configured_) throw std::runtime_error("iox: oracle backend not configured");
   if (q >= nq_) throw std::invalid_argument("iox: no such queue");
@@ -386,6 +393,19 @@ uint64_t OracleBackend::publish(uint32_t q, uint32_t n) {
   uint32_t real = 0;
   while (real < n && im[(prod + real) & (cap_ - 1)] != kRingPadMeta) ++real;
   for (uint32_t i = real; i < n; ++i) om[(prod + i) & (cap_ - 1)] = make_meta(kPortNone, 0, kMalformed);
+  if (!fa_.empty()) {
+    // what the GPU ring does in frame-address mode: each frame from where its address points,
+    // the bytes past its length zero
+    for (uint32_t i = 0; i < n; ++i) {
+      const size_t pos = (size_t)q * cap_ + ((prod + i) & (cap_ - 1));
+      uint8_t* slot = in_.data() + pos * kSlotBytes;
+      const uint8_t* src = reinterpret_cast<const uint8_t*>(fa_[pos]);
+      if (src == slot) continue;
+      const uint32_t len = i < real ? std::min<uint32_t>(im_[pos] >> 16, kSlotBytes) : 0u;
+      std::memcpy(slot, src, len);
+      std::memset(slot + len, 0, kSlotBytes - len);
+    }
+  }
   {
     std::unique_lock<std::mutex> g(run_mu_, std::defer_lock);
     if (serial_) g.lock();
@@ -514,6 +534,8 @@ void Engine::add_port(uint32_t id, std::shared_ptr<Port> p, int queue) {
     for (uint32_t k = 1; k < nq_; ++k)
       if (queues_[k]->nports.load() < queues_[q]->nports.load()) q = k;
   }
+  if (zero_copy_.load()) map_port(*p);   // before any packet thread can see the port
+  reap_retired(false);
   (*t)[id] = PortRef{std::move(p), q};
   queues_[q]->nports.fetch_add(1);
   std::atomic_store(&ports_, std::shared_ptr<const PortTab>(t));
@@ -529,7 +551,52 @@ std::shared_ptr<Port> Engine::remove_port(uint32_t id) {
   (*t)[id] = PortRef{};
   std::atomic_store(&ports_, std::shared_ptr<const PortTab>(t));
   ports_ver_.fetch_add(1, std::memory_order_release);
-  return old;   // frames of it still in flight keep it alive through the snapshot the threads hold
+  reap_retired(false);
+  // Frames of it may still be in a pipeline (a packet thread's snapshot can hold it a little
+  // longer, its bursts complete within milliseconds): the engine keeps the port alive — its
+  // memory mapped for the GPU — for kRetireNs after the removal, or until stop().
+  if (old) retired_.emplace_back(now_ns(), old);
+  return old;
+}
+
+namespace {
+constexpr uint64_t kRetireNs = 5'000'000'000ull;
+}
+
+void Engine::reap_retired(bool all) {
+  const uint64_t t = now_ns();
+  while (!retired_.empty() && (all || t - retired_.front().first > kRetireNs)) retired_.pop_front();
+}
+
+void Engine::map_port(Port& p) {
+  const auto mem = p.rx_memory();
+  if (!mem.first || !mem.second || p.zc_.lo) return;
+  Port::Mapped m;
+  m.off.assign(backends_.size(), 0);
+  for (size_t g = 0; g < backends_.size(); ++g) {
+    std::function<void()> rel;
+    const uint64_t a = backends_[g]->map_host(mem.first, mem.second, &rel);
+    if (rel) m.release = std::move(rel);   // (at most one backend registers: the first)
+    if (!a) {   // a backend cannot read it: the port's frames are copied, as without the mode
+      if (m.release) m.release();
+      return;
+    }
+    m.off[g] = (int64_t)(a - reinterpret_cast<uint64_t>(mem.first));
+  }
+  m.lo = mem.first;
+  m.hi = mem.first + mem.second;
+  p.zc_ = std::move(m);
+}
+
+void Engine::set_zero_copy(bool on) {
+  if (run_) throw std::runtime_error("iox: set_zero_copy while running");
+  std::lock_guard<std::mutex> g(ports_mu_);
+  zero_copy_ = on;
+  for (const PortRef& r : *ports_) {
+    if (!r.p) continue;
+    if (on) map_port(*r.p);
+    else r.p->unmap_rx();
+  }
 }
 
 std::shared_ptr<Port> Engine::port(uint32_t id) {
@@ -659,6 +726,8 @@ void Engine::stop() {
     for (const Pkt& q : L->stage) q.holder->complete(q.seq);   // read but never published
     L->stage.clear();
   }
+  std::lock_guard<std::mutex> g(ports_mu_);
+  reap_retired(true);
 }
 
 void Engine::pause() {
@@ -742,6 +811,7 @@ std::unordered_map<std::string, uint64_t> Engine::stats() const {
     m["side_passes"] += s.side.load(); m["no_netdev"] += s.no_port.load(); m["tx_full"] += s.tx_full.load();
     m["publish_ns"] += s.pub_ns.load(); m["deliver_ns"] += s.deliver_ns.load(); m["rx_idle_polls"] += s.idle.load();
     m["rx_wait_tx"] += s.wait_tx.load(); m["learn_events"] += s.learn.load(); m["rx_held"] += s.held.load();
+    m["zero_copy_frames"] += s.zc.load();
   };
   for (auto& Q : queues_) {
     fold(Q->st);
@@ -977,18 +1047,45 @@ void Engine::rx_loop(Queue* Q) {
         b.end = start + npad;
         b.t_rx_ns = L->stage_t0;
         bool side = side_always;
-        for (uint32_t i = 0; i < k; ++i) {
-          const Pkt& pk = L->stage[i];
-          uint8_t* slot = be.in_slot(q, (uint32_t)(start + i));
-          if (i + 4 < k) {   // later slots' lines (last written by the GPU) and frames, requested early
-            __builtin_prefetch(be.in_slot(q, (uint32_t)(start + i + 4)), 1, 3);
-            __builtin_prefetch(L->stage[i + 4].data, 0, 3);
+        uint64_t* fa = be.frame_addrs(q);
+        if (fa) {
+          // zero-copy: the pipeline reads a mapped port's frame in place (16-B aligned, its first
+          // 64 bytes inside the mapping); any other frame is copied and read from its in slot
+          uint32_t zc = 0;
+          for (uint32_t i = 0; i < k; ++i) {
+            const Pkt& pk = L->stage[i];
+            const uint32_t pos = (uint32_t)((start + i) & cmask);
+            const Port::Mapped& m = pk.holder->zc_;
+            if (pk.data >= m.lo && pk.data + kSlotBytes <= m.hi && L->g < m.off.size() &&
+                !(reinterpret_cast<uintptr_t>(pk.data) & 15u)) {
+              fa[pos] = (uint64_t)((int64_t)reinterpret_cast<uint64_t>(pk.data) + m.off[L->g]);
+              ++zc;
+            } else {
+              uint8_t* slot = be.in_slot(q, pos);
+              const uint32_t h = std::min<uint32_t>(pk.len, kSlotBytes);
+              std::memcpy(slot, pk.data, h);
+              if (h < kSlotBytes) std::memset(slot + h, 0, kSlotBytes - h);
+              fa[pos] = be.in_slot_addr(q, pos);
+            }
+            im[pos] = (pk.port & 0xFFFFu) | (pk.len << 16);
+            side = side || (pk.port < side_ports.size() && side_ports[pk.port]);
           }
-          const uint32_t h = std::min<uint32_t>(pk.len, kSlotBytes);
-          std::memcpy(slot, pk.data, h);
-          if (h < kSlotBytes) std::memset(slot + h, 0, kSlotBytes - h);
-          im[(start + i) & cmask] = (pk.port & 0xFFFFu) | (pk.len << 16);
-          side = side || (pk.port < side_ports.size() && side_ports[pk.port]);
+          for (uint32_t i = k; i < npad; ++i) fa[(start + i) & cmask] = be.in_slot_addr(q, (uint32_t)(start + i));
+          st.add(st.zc, zc);
+        } else {
+          for (uint32_t i = 0; i < k; ++i) {
+            const Pkt& pk = L->stage[i];
+            uint8_t* slot = be.in_slot(q, (uint32_t)(start + i));
+            if (i + 4 < k) {   // later slots' lines (last written by the GPU) and frames, requested early
+              __builtin_prefetch(be.in_slot(q, (uint32_t)(start + i + 4)), 1, 3);
+              __builtin_prefetch(L->stage[i + 4].data, 0, 3);
+            }
+            const uint32_t h = std::min<uint32_t>(pk.len, kSlotBytes);
+            std::memcpy(slot, pk.data, h);
+            if (h < kSlotBytes) std::memset(slot + h, 0, kSlotBytes - h);
+            im[(start + i) & cmask] = (pk.port & 0xFFFFu) | (pk.len << 16);
+            side = side || (pk.port < side_ports.size() && side_ports[pk.port]);
+          }
         }
         for (uint32_t i = k; i < npad; ++i) im[(start + i) & cmask] = kRingPadMeta;
         b.side = side;
@@ -1057,6 +1154,7 @@ void Engine::side_work(Queue* Q, Lane* L, Burst& b, const Cfg& c, TxScratch& sc,
   const TablesView& t = stab->view();
   const TabHash hasher{&stab->hash()};
   const std::vector<uint8_t>& sp = c.side_ports;
+  const bool zc = be.frame_addrs(q) != nullptr;
   sc.learn.clear();
   BurstSink sink{b.reps, b.xhdr, b.has_x, sc.learn};
   std::shared_lock<std::shared_mutex> g(stab->mac_mu);   // the learner updates the snapshot's MAC table
@@ -1070,7 +1168,15 @@ void Engine::side_work(Queue* Q, Lane* L, Burst& b, const Cfg& c, TxScratch& sc,
       b.has_x.assign(np, 0);
     }
     sink.i = i;
-    side_stage(t, DirectTables{t}, reinterpret_cast<const uint32_t*>(be.in_slot(q, pos)), im[pos],
+    const uint32_t* fin = reinterpret_cast<const uint32_t*>(be.in_slot(q, pos));
+    alignas(16) uint32_t zf[kSlotBytes / 4];
+    if (zc) {   // (a zero-copy frame may not be in its in slot: the frame itself, zero-padded)
+      const uint32_t h = std::min<uint32_t>(b.pkts[i].len, kSlotBytes);
+      std::memset(zf, 0, sizeof(zf));
+      std::memcpy(zf, b.pkts[i].data, h);
+      fin = zf;
+    }
+    side_stage(t, DirectTables{t}, fin, im[pos],
                reinterpret_cast<const uint32_t*>(be.out_slot(q, pos)), m, i, sink, hasher);
   }
   g.unlock();

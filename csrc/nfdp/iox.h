@@ -34,6 +34,7 @@
 #include <condition_variable>
 #include <cstdint>
 #include <deque>
+#include <functional>
 #include <memory>
 #include <mutex>
 #include <shared_mutex>
@@ -102,6 +103,8 @@ class Port {
     return tx_batch(&it, 1) == 1;
   }
   virtual uint32_t tx_queues() const { return 1; }
+  // Memory every frame rx() hands out lies in (zero-copy rx maps it for the pipeline), or null.
+  virtual std::pair<const uint8_t*, size_t> rx_memory() const { return {nullptr, 0}; }
   // A frame is done (sent or dropped): any thread.  reclaim(): the owning rx thread only, after
   // marking what rx() handed out (handed_out: sequence numbers up to seq are in use).
   void complete(uint32_t seq) { done_[seq & mask_].store(1, std::memory_order_release); }
@@ -127,6 +130,15 @@ class Port {
   virtual void flush_locked(uint32_t) {}
   virtual void release_to(uint32_t seq_end) = 0;   // every frame below seq_end is done
   void set_first_seq(uint32_t s) { rel_ = s; seen_ = s; }
+  // Drop the pipeline's mapping of rx_memory() (a port that unmaps it calls this first).
+  void unmap_rx() {
+    if (zc_.release) {
+      auto f = std::move(zc_.release);
+      zc_.release = nullptr;
+      f();
+    }
+    zc_.lo = zc_.hi = nullptr;
+  }
   uint32_t window() const { return mask_ + 1; }
   struct alignas(64) TxLock { std::mutex mu; };
   TxLock tx_mu_[kMaxTxQueues];
@@ -139,6 +151,16 @@ class Port {
   // The rx queue polling this port (-1: none).  The rx side is single-consumer: a port moved to
   // another queue is polled there only once its previous rx thread has let go of it.
   std::atomic<int> rx_owner_{-1};
+  // Zero-copy rx (Engine::set_zero_copy): rx_memory() as the pipelines see it.  Frames in
+  // [lo, hi) are read at data + off[g] by backend g; written by the engine before the port is
+  // published to the packet threads, read-only afterwards.
+  struct Mapped {
+    const uint8_t* lo = nullptr;
+    const uint8_t* hi = nullptr;
+    std::vector<int64_t> off;
+    std::function<void()> release;   // unregisters the memory (the registering backend's)
+  };
+  Mapped zc_;
   friend class Engine;
 };
 
@@ -152,6 +174,7 @@ class MemifPort : public Port {
   std::string kind() const override { return "memif"; }
   const std::string& path() const { return reg_.path(); }
   uint32_t tx_queues() const override { return nprod_; }
+  std::pair<const uint8_t*, size_t> rx_memory() const override { return {reg_.base(), reg_.bytes()}; }
 
  protected:
   bool tx_locked(uint32_t q, const uint8_t* a, uint32_t na, const uint8_t* b, uint32_t nb, const uint8_t* c,
@@ -291,6 +314,14 @@ class Backend {
   // pipeline reads; learner thread only.
   virtual void apply_learn(const uint32_t* ev, uint32_t n, uint32_t stamp) = 0;
   virtual void thread_init() {}
+  // Zero-copy rx.  frame_addrs(q) non-null: the pipeline reads slot i's frame at the address
+  // frame_addrs(q)[i] names (the engine writes one for every slot it publishes: a mapped port's
+  // frame, or in_slot_addr() for a copied frame or a filler slot).
+  virtual uint64_t* frame_addrs(uint32_t) { return nullptr; }
+  virtual uint64_t in_slot_addr(uint32_t q, uint32_t pos) { return reinterpret_cast<uint64_t>(in_slot(q, pos)); }
+  // Make host memory [p, p + n) readable by the pipeline: its address there (0: cannot).  Sets
+  // *release when this call registered it (run it once nothing of the memory is in flight).
+  virtual uint64_t map_host(const void*, size_t, std::function<void()>*) { return 0; }
 };
 
 class GpuBackend : public Backend {
@@ -310,6 +341,11 @@ class GpuBackend : public Backend {
   bool alive() override { return ring_->alive(); }
   void apply_learn(const uint32_t* ev, uint32_t n, uint32_t stamp) override;
   void thread_init() override;
+  uint64_t* frame_addrs(uint32_t q) override {
+    return ring_->frame_addrs_on() ? ring_->frame_addrs() + (size_t)q * cap_ : nullptr;
+  }
+  uint64_t in_slot_addr(uint32_t q, uint32_t pos) override { return ring_->in_slot_addr(q, pos); }
+  uint64_t map_host(const void* p, size_t n, std::function<void()>* release) override;
 
  private:
   RingEngine* ring_;
@@ -337,12 +373,18 @@ class OracleBackend : public Backend {
   // tables / counters of the CPU DataPlane (replaced after every commit, while the engine is paused)
   void configure(const TablesView& t, uint64_t* flow_ctr, uint64_t* port_ctr, uint64_t* drop_ctr, MacEntry* macs,
                  uint32_t mac_mask);
+  // Zero-copy rx on the CPU: frames are gathered from their addresses (host pointers) into the
+  // in slots at publish, as the GPU ring reads them (the engine's side of the mode, testable here)
+  void set_frame_addrs(bool on);
+  uint64_t* frame_addrs(uint32_t q) override { return fa_.empty() ? nullptr : fa_.data() + (size_t)q * cap_; }
+  uint64_t map_host(const void* p, size_t, std::function<void()>*) override { return reinterpret_cast<uint64_t>(p); }
 
  protected:
   virtual void run_segment(uint32_t q, uint32_t pos, uint32_t n);
   uint32_t cap_, nq_;
   std::vector<uint8_t> in_, out_;
   std::vector<uint32_t> im_, om_;
+  std::vector<uint64_t> fa_;   // zero-copy: per-slot frame addresses (empty: off)
   std::unique_ptr<std::atomic<uint64_t>[]> prod_;
   std::atomic<bool> configured_{false};
   std::mutex run_mu_;   // the pipeline's counters / MAC table are shared by every queue
@@ -413,6 +455,12 @@ class Engine {
     coalesce_ns_.store((uint64_t)(std::max(window_us, 0.0) * 1e3));
   }
   void set_side_tables(uint32_t backend, std::shared_ptr<SideTables> t);
+  // Zero-copy rx: map every port's rx memory (rx_memory()) for the backends; a backend reading
+  // frames by address (frame_addrs()) then reads mapped frames in place — the engine writes an
+  // address per slot instead of copying the frame's first 64 bytes.  Ports added later are
+  // mapped as they come.
+  void set_zero_copy(bool on);
+  bool zero_copy() const { return zero_copy_.load(); }
   void start();
   void stop();
   void pause();    // no publish until resume(); returns once nothing is in flight
@@ -469,7 +517,7 @@ class Engine {
   };
   struct alignas(64) QStats {
     std::atomic<uint64_t> rx{0}, tx{0}, drop{0}, punt{0}, recirc{0}, reps{0}, bursts{0}, side{0}, no_port{0},
-        tx_full{0}, pub_ns{0}, deliver_ns{0}, idle{0}, wait_tx{0}, learn{0}, held{0};
+        tx_full{0}, pub_ns{0}, deliver_ns{0}, idle{0}, wait_tx{0}, learn{0}, held{0}, zc{0};
     void add(std::atomic<uint64_t>& c, uint64_t v) { if (v) c.store(c.load(std::memory_order_relaxed) + v, std::memory_order_relaxed); }
   };
   struct Queue {                // one rx thread + its tx workers
@@ -543,6 +591,12 @@ class Engine {
   std::vector<std::shared_ptr<Backend>> backends_;
   std::vector<std::unique_ptr<Queue>> queues_;
   mutable std::mutex ports_mu_;
+  std::atomic<bool> zero_copy_{false};
+  // removed ports stay referenced a while (frames of theirs may still be in a pipeline: the GPU
+  // reads a zero-copy frame where its port holds it)
+  std::deque<std::pair<uint64_t, std::shared_ptr<Port>>> retired_;   // (ports_mu_) removal time (ns)
+  void map_port(Port& p);            // (ports_mu_)
+  void reap_retired(bool all);       // (ports_mu_)
   std::shared_ptr<const PortTab> ports_;              // copy-on-write snapshot, by port id
   alignas(64) std::atomic<uint64_t> ports_ver_{0};    // bumped after every ports_ / cfg_ store
   std::atomic<uint64_t> cfg_ver_{0};

@@ -36,6 +36,27 @@ GpuBackend::~GpuBackend() {
 
 void GpuBackend::thread_init() { hck(hipSetDevice(ring_->device()), "set device"); }
 
+// Host memory pinned and mapped for every device (portable): a second backend finds it
+// registered already and only looks up its address.
+uint64_t GpuBackend::map_host(const void* p, size_t n, std::function<void()>* release) {
+  thread_init();
+  void* h = const_cast<void*>(p);
+  const hipError_t e = hipHostRegister(h, n, hipHostRegisterMapped | hipHostRegisterPortable);
+  if (e == hipSuccess) {
+    *release = [h]() { (void)hipHostUnregister(h); };
+  } else {
+    (void)hipGetLastError();
+    if (e != hipErrorHostMemoryAlreadyRegistered) return 0;
+  }
+  void* d = nullptr;
+  if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess || !d) {
+    (void)hipGetLastError();
+    if (*release) { (*release)(); *release = nullptr; }
+    return 0;
+  }
+  return reinterpret_cast<uint64_t>(d);
+}
+
 void GpuBackend::apply_learn(const uint32_t* ev, uint32_t n, uint32_t stamp) {
   if (!n) return;
   thread_init();

@@ -180,6 +180,17 @@ class RingEngine {
   uint32_t* dev_svc() const { return d_svc_; }  // per-chunk device service time (ticks, 100 MHz)
   // host_slots rings: host addresses of the pinned in / inmeta / out / meta buffers (all queues)
   void* host_ptr(int i) const { return host_slots_ && i >= 0 && i < (int)host_ptrs_.size() ? host_ptrs_[i] : nullptr; }
+  // Frame addresses (host_slots rings): with the mode on, the grid reads slot i's frame from the
+  // device address in frame_addrs()[q * capacity + i] (pinned, written by the producer before it
+  // publishes) instead of from the in slot — frames are read where the producer's ports hold
+  // them (zero-copy rx).  Every published slot needs an address: an in slot's own (in_slot_addr)
+  // for frames the producer copied, and for filler slots.  Set while stopped; takes effect at start().
+  void set_frame_addrs(bool on);
+  bool frame_addrs_on() const { return faddr_on_; }
+  uint64_t* frame_addrs() const { return h_faddr_; }
+  uint64_t in_slot_addr(uint32_t q, uint32_t pos) const {
+    return reinterpret_cast<uint64_t>(d_in_) + ((uint64_t)q * cap_ + (pos & (cap_ - 1))) * 64u;
+  }
 
   // Launch the persistent kernel over the tables/counters in `f` (pkts/out/n are ignored).
   // flows_alt: the second flow-table copy (epoch & 1 == 1); null = single copy (no live flips).
@@ -275,6 +286,9 @@ class RingEngine {
   uint8_t* d_out_ = nullptr;
   uint32_t* d_meta_ = nullptr;
   uint32_t* d_svc_ = nullptr;
+  uint64_t* h_faddr_ = nullptr;    // host_slots: [nq][cap] frame addresses (pinned)
+  uint64_t* d_faddr_ = nullptr;    // (its device view)
+  bool faddr_on_ = false;
   hipStream_t stream_{};
   std::unique_ptr<Queue[]> qs_;
   std::atomic<uint32_t> epoch_{0};   // current flow-table epoch (copy epoch_ & 1)
@@ -303,6 +317,7 @@ struct RingLaunch {
   uint32_t lds_tiles;         // coop: ACL tiles the LDS layout is sized for (>= any set's tiles)
   uint32_t epoch0;            // epoch at launch (its set bit names the set to stage first)
   RingCtrlRing* ctrl;         // device view of the control mailbox
+  const uint64_t* faddr;      // frame addresses per slot (null: frames are in the in slots)
 };
 hipError_t launch_ring(const RingLaunch& r, const LaunchCfg& cfg, int wgs_per_cu, bool coop, hipStream_t s);
 

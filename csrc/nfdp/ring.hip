@@ -33,6 +33,7 @@ struct RingArgs {
   uint32_t flags_bits;  // bit2: no per-flow counts; bits 5/6: diagnostics (kRingTrace, kRingNoCounters)
   uint32_t nq;          // queues: workgroup b serves queue b % nq (ctl / st / flags / svc / slots per queue)
   RingCtrlRing* ctrl;   // control mailbox (pinned host memory, device view)
+  const unsigned long long* faddr;   // zero-copy rx: per-slot frame addresses (null: in slots)
 };
 // Frames are read and written with system-coherent buffer ops (sc0 sc1): the loads never hit a
 // stale L2 line of a slot a producer (host / NIC DMA) rewrote, and the stores write through to
@@ -89,6 +90,41 @@ __device__ __forceinline__ unsigned long long rfl64(unsigned long long v) {
   const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
   const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
   return ((unsigned long long)hi << 32) | lo;
+}
+
+// Zero-copy rx: the chunk's 64 frames lie wherever the producer's ports hold them (one address
+// per slot in fa[], pinned host memory).  Lane L loads 16-B piece L % 4 of frame q * 16 + L / 4
+// in pass q — the same register layout as a contiguous run's loads (wave_frames_load), so the
+// LDS transpose is shared, and the 4 lanes of a frame read one 64-B line together (one request
+// per line, as for the run).  System-coherent (sc0 sc1): the producer rewrites the buffers.
+__device__ __forceinline__ void ring_frames_gather(const unsigned long long* fa, uint32_t i, v4u c[4]) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const unsigned long long mine = __hip_atomic_load(fa + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  const int lo = (int)(uint32_t)mine, hi = (int)(uint32_t)(mine >> 32);
+  unsigned long long p[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int src = q * 16 + (int)(lane >> 2);
+    p[q] = (((unsigned long long)(uint32_t)__shfl(hi, src) << 32) | (uint32_t)__shfl(lo, src)) + (lane & 3u) * 16u;
+  }
+  asm volatile(
+      "global_load_dwordx4 %0, %4, off sc0 sc1\n\t"
+      "global_load_dwordx4 %1, %5, off sc0 sc1\n\t"
+      "global_load_dwordx4 %2, %6, off sc0 sc1\n\t"
+      "global_load_dwordx4 %3, %7, off sc0 sc1\n\t"
+      "s_waitcnt vmcnt(0)"
+      : "=&v"(c[0]), "=&v"(c[1]), "=&v"(c[2]), "=&v"(c[3])
+      : "v"(p[0]), "v"(p[1]), "v"(p[2]), "v"(p[3])
+      : "memory");
+}
+
+// Bytes at and past `len` read as zero (what a copied frame's in slot holds there).
+__device__ __forceinline__ void frame_clip(uint32_t* d, uint32_t len) {
+#pragma unroll
+  for (int k = 0; k < kSlotDwords; ++k) {
+    const int rem = (int)len - 4 * k;
+    d[k] = rem >= 4 ? d[k] : rem <= 0 ? 0u : d[k] & ((1u << (8 * rem)) - 1u);
+  }
 }
 
 // Claim the next chunk ticket and wait until it is published.  Returns false when the wave must
@@ -368,12 +404,17 @@ __global__ __launch_bounds__(kRingBlock) void ring_kernel(RingArgs a) {
     // the chunk's 64 slots are one 4-KiB run: lane-contiguous loads, transposed through LDS
     const uint32_t run = __builtin_amdgcn_readfirstlane(((tk32 * 64u) & a.ring_mask) * 64u);
     uint32_t d[kSlotDwords];
+    const uint32_t im = __builtin_amdgcn_raw_buffer_load_b32(r_im, i * 4u, 0, kSysAux);
     {
       v4u c[4];
-      wave_frames_load<kSysAux>(r_pk, run, c);
+      if (a.faddr) {
+        ring_frames_gather(a.faddr + qslot0, i, c);
+      } else {
+        wave_frames_load<kSysAux>(r_pk, run, c);
+      }
       wave_frames_to_lanes(kx, c, d);
     }
-    const uint32_t im = __builtin_amdgcn_raw_buffer_load_b32(r_im, i * 4u, 0, kSysAux);
+    if (a.faddr) frame_clip(d, im >> 16);   // the bytes past the frame are not the producer's zeros
     NFDP_RING_MARK(tr0)
     Parsed p;
     IngressState st;
@@ -509,6 +550,7 @@ hipError_t launch_ring(const RingLaunch& r, const LaunchCfg& cfg, int wgs_per_cu
   a.lds_tiles = r.lds_tiles;
   a.epoch0 = r.epoch0;
   a.ctrl = r.ctrl;
+  a.faddr = reinterpret_cast<const unsigned long long*>(r.faddr);
   a.nq = r.queues ? r.queues : 1u;
   // every queue needs a workgroup; the side list indexes slots of one ring only
   if ((uint64_t)cfg.num_cus * (uint64_t)wgs_per_cu < a.nq || (a.nq > 1 && a.side.cnt)) return hipErrorInvalidValue;
@@ -592,6 +634,11 @@ RingEngine::RingEngine(uint32_t capacity, int num_cus, int wgs_per_cu, bool coop
   slot_alloc(reinterpret_cast<void**>(&d_im_), slots * 4, "alloc inmeta");
   slot_alloc(reinterpret_cast<void**>(&d_out_), slots * 64, "alloc out");
   slot_alloc(reinterpret_cast<void**>(&d_meta_), slots * 4, "alloc meta");
+  if (host_slots_) {   // frame addresses (zero-copy rx; set_frame_addrs)
+    slot_alloc(reinterpret_cast<void**>(&d_faddr_), slots * 8, "alloc frame addresses");
+    h_faddr_ = static_cast<uint64_t*>(host_ptrs_.back());
+    for (size_t i = 0; i < slots; ++i) h_faddr_[i] = reinterpret_cast<uint64_t>(d_in_) + i * 64u;
+  }
   ck(hipMalloc(reinterpret_cast<void**>(&d_svc_), (size_t)nq_ * nch_ * 4 * kSvcWords), "dev alloc svc");
   ck(hipMalloc(reinterpret_cast<void**>(&d_sets_), 2 * sizeof(RingTableSet)), "dev alloc table sets");
   ck(hipMemset(d_sets_, 0, 2 * sizeof(RingTableSet)), "memset");
@@ -655,6 +702,7 @@ void RingEngine::start(const FusedLaunch& f, const LaunchCfg& cfg, double deadli
     r.ctrl = reinterpret_cast<RingCtrlRing*>(dc);
   }
   r.pkts = d_in_; r.inmeta = d_im_; r.out = d_out_; r.out_meta = d_meta_;
+  r.faddr = faddr_on_ ? d_faddr_ : nullptr;
   r.ring_mask = cap_ - 1;
   r.queues = nq_;
   void* dctl = nullptr;
@@ -843,6 +891,16 @@ void RingEngine::set_epoch(uint32_t e) {
   if (running_) throw std::runtime_error("ring: set_epoch while running");
   std::lock_guard<std::mutex> g(mu_);
   set_epoch_all(e & (uint32_t)kRingEpochMask);
+}
+
+void RingEngine::set_frame_addrs(bool on) {
+  if (running_) throw std::runtime_error("ring: set_frame_addrs while running");
+  if (on && !host_slots_) throw std::invalid_argument("ring: frame addresses need host_slots=True");
+  if (on && !faddr_on_) {   // every slot starts out naming its own in slot
+    const size_t slots = (size_t)cap_ * nq_;
+    for (size_t i = 0; i < slots; ++i) h_faddr_[i] = reinterpret_cast<uint64_t>(d_in_) + i * 64u;
+  }
+  faddr_on_ = on;
 }
 
 uint64_t RingEngine::post_write(uint64_t dst, const uint32_t* data, uint32_t n, double timeout_s) {

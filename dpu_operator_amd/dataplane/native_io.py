@@ -122,13 +122,15 @@ class NativeLivePath:
     def __init__(self, dps, ports: dict, burst: int = 256, ring_capacity: int = 4096, inflight: int = 64,
                  on_punt=None, auto_restart: bool = True, tx_workers: int = 1, queues: int = 1,
                  max_inflight_frames: int = 0, port_queues: dict | None = None, coalesce_us: float = 8.0,
-                 coalesce_frames: int = 64, ring_cus: int = 0):
+                 coalesce_frames: int = 64, ring_cus: int = 0, zero_copy: bool = False):
         """dps: one data plane or a list (one per GPU, or a MultiDataPlane's planes); ports:
         {port id: vport spec}; queues: rx threads (each with a ring queue on every GPU);
         port_queues: {port id: queue} (default: least loaded); max_inflight_frames: per lane
         bound of the engine's own queueing (0: the ring capacity); coalesce_us / coalesce_frames:
         with bursts of a lane in flight, frames gather into one publish until that many are read
-        or the oldest waited that long (an idle lane publishes at once)."""
+        or the oldest waited that long (an idle lane publishes at once); zero_copy: the pipelines
+        read memif frames where the pods wrote them (the regions pinned and mapped for the GPUs)
+        instead of from copies of their headers in the ring slots."""
         from ..native import nfdp
 
         self.nf = nfdp()
@@ -145,6 +147,7 @@ class NativeLivePath:
         self.max_inflight_frames = int(max_inflight_frames)
         self.coalesce_us, self.coalesce_frames = float(coalesce_us), int(coalesce_frames)
         self.ring_cus = int(ring_cus)   # CUs of each ring grid (0: the GPU's, split between planes sharing it)
+        self.zero_copy = bool(zero_copy)
         self.specs = dict(ports)
         self.port_queues = dict(port_queues or {})
         self.on_punt = on_punt
@@ -193,17 +196,20 @@ class NativeLivePath:
                     ring = RingPath(dp, capacity=self.capacity, host_slots=True, coop=True, side=False,
                                     deadline_s=3600.0, queues=self.queues,
                                     cus=self.ring_cus or max(1, int(dp.num_cus) // share))
+                    ring.eng.set_frame_addrs(self.zero_copy)
                     ring.start()
                 self._rings.append(ring)
                 be = nf.GpuBackend(ring.eng)
             else:
                 be = nf.OracleBackend(self.capacity, self.queues)
+                be.set_frame_addrs(self.zero_copy)
             self._backends.append(be)
             eng.add_backend(be)
             if self not in getattr(dp, "_io_hooks", []):
                 dp._io_hooks = getattr(dp, "_io_hooks", []) + [self]
             dp._learned_on_device = True     # the engine learns into the device MAC table: commits pull first
         # replica counters appear in the first plane's counters (a MultiDataPlane sums its planes)
+        eng.set_zero_copy(self.zero_copy)
         hooks = getattr(self.dps[0], "_ctr_hooks", [])
         if self not in hooks:
             self.dps[0]._ctr_hooks = hooks + [self]

@@ -193,6 +193,41 @@ def test_vxlan_egress_side_pass_per_burst_and_redirect_cleared(shm):
         live.stop()
 
 
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda:0", marks=pytest.mark.gpu)])
+@pytest.mark.parametrize("egress", [False, True])
+def test_zero_copy_rx_bit_exact(shm, device, egress):
+    """Zero-copy rx (iox Engine::set_zero_copy): the pipeline reads every memif frame where the pod
+    wrote it — on the GPU through the pinned, mapped region (ring.hip ring_frames_gather), on the
+    CPU oracle through the same per-slot addresses — and the frames, the side pass's outer headers
+    and the counters come out as the batch path makes them."""
+    nf = nfdp()
+    dp, sc, eg = _sfc(device=device, egress=egress)
+    ref, _, _ = _sfc(egress=egress)
+    slots, im = S.traffic(sc, 3000, seed=11)
+    exp, drops = _expected(ref, slots, im)
+    ports = [int(p) for p in sc.pod_port]
+    if egress:
+        exp = {eg["underlay"]: [f for v in exp.values() for f in v]}
+        ports_all = ports + [eg["underlay"]]
+    else:
+        ports_all = ports
+    paths = {p: str(shm / f"z{p}") for p in ports_all}
+    live = NativeLivePath(dp, {p: MemifVport(paths[p], ring_size=4096) for p in paths}, burst=128,
+                          ring_capacity=1024, queues=2, zero_copy=True).start()
+    try:
+        eps = _send_all(nf, paths, slots, im, ports)
+        got, done = _collect(eps, sum(map(len, exp.values())))
+        assert _until(done, 20.0), (live.stats, live.error)
+        for port, frames in exp.items():
+            assert sorted(got[port]) == sorted(frames), port
+        st = live.stats
+        assert st["rx"] == len(slots) and live.error is None
+        assert st["zero_copy_frames"] == len(slots)          # not one frame copied into a slot
+        assert np.array_equal(dp.port_counters(), ref.port_counters())
+    finally:
+        live.stop()
+
+
 @pytest.mark.parametrize("devices", [["cpu", "cpu"], pytest.param(["cuda:0", "cuda:0"], marks=pytest.mark.gpu)])
 def test_multi_plane_native_matches_one_plane(shm, devices):
     """Two planes behind one engine with two queues (RSS owner steering in each rx thread): the

@@ -120,12 +120,13 @@ def run(device: str = "cuda", n_pods: int = 8, flows: int = 1 << 20, n_acl: int 
         threads: int = 4, burst: int = 512, inflight: int = 64, ring_capacity: int = 16384,
         hash_mode: str = "lds", tx_workers: int = 2, queues: int = 4, max_inflight_frames: int = 4096,
         pod_ring: int = 1024, backend: str = "pipeline", coalesce_us: float = 8.0, loaded_window: int = 2048,
-        traffic: str = "plain") -> dict:
+        traffic: str = "plain", zero_copy: bool = False) -> dict:
     """traffic: "plain" (the headline SFC), "vxlan-egress" (every pod's VF a VXLAN tunnel port:
     all frames leave encapsulated through one underlay vport, outer headers from the per-burst
     side pass) or "broadcast" (pods on one learning bridge sending to ff:ff:ff:ff:ff:ff: every
     frame floods to the other pods, one copy from the GPU and the rest from the side pass;
-    `mpps` counts delivered copies)."""
+    `mpps` counts delivered copies).  zero_copy: the ring reads the pods' frames in their memif
+    regions (NativeLivePath zero_copy) instead of header copies in its slots."""
     nf = nfdp()
     t0 = time.perf_counter()
     d = tempfile.mkdtemp(prefix="dpu-live-", dir=memif_dir())
@@ -149,7 +150,7 @@ def run(device: str = "cuda", n_pods: int = 8, flows: int = 1 << 20, n_acl: int 
         ports = {p: MemifVport(os.path.join(d, f"pod{p}"), ring_size=pod_ring) for p in range(n_pods)}
         live = NativeLivePath(dp, ports, burst=burst, ring_capacity=ring_capacity, inflight=inflight,
                               tx_workers=tx_workers, queues=queues, max_inflight_frames=max_inflight_frames,
-                              coalesce_us=coalesce_us).start()
+                              coalesce_us=coalesce_us, zero_copy=zero_copy).start()
         gen = _WireLive.__new__(_WireLive)
         for i in range(n_pods):
             fr, ln = gen.frames(i, n_pods, k=1024, seed=100 + i, broadcast=True)
@@ -166,7 +167,7 @@ def run(device: str = "cuda", n_pods: int = 8, flows: int = 1 << 20, n_acl: int 
             ports[underlay] = MemifVport(os.path.join(d, "underlay"), ring_size=4 * pod_ring)
         live = NativeLivePath(dp, ports, burst=burst, ring_capacity=ring_capacity, inflight=inflight,
                               tx_workers=tx_workers, queues=queues, max_inflight_frames=max_inflight_frames,
-                              coalesce_us=coalesce_us).start()
+                              coalesce_us=coalesce_us, zero_copy=zero_copy).start()
         for i in range(n_pods):
             slots, im = S.traffic(sc, 4096, seed=100 + i, src_pods=np.array([i]))
             pods.append((ports[int(sc.pod_port[i])].path, slots, (im >> 16).astype(np.uint32)))
@@ -176,7 +177,7 @@ def run(device: str = "cuda", n_pods: int = 8, flows: int = 1 << 20, n_acl: int 
     setup_s = time.perf_counter() - t0
     stats = lambda: live.stats  # noqa: E731
     try:
-        out = {"backend": backend, "traffic": traffic, "device": device, "queues": queues, "coalesce_us": coalesce_us, "tx_workers": tx_workers, "inflight_bursts": inflight,
+        out = {"backend": backend, "traffic": traffic, "zero_copy": zero_copy, "device": device, "queues": queues, "coalesce_us": coalesce_us, "tx_workers": tx_workers, "inflight_bursts": inflight,
                "max_inflight_frames": max_inflight_frames, "pod_ring": pod_ring, "gen_threads": threads,
                "pods": n_pods, "flows": flows, "acl_rules": n_acl, "frame_bytes": 64,
                "setup_s": round(setup_s, 1)}
@@ -210,7 +211,8 @@ def run(device: str = "cuda", n_pods: int = 8, flows: int = 1 << 20, n_acl: int 
         st = live.stats
         out["engine"] = {k: int(v) for k, v in st.items() if k in ("rx", "tx", "drop", "bursts", "tx_full",
                                                                     "side_passes", "punt", "rx_wait_tx",
-                                                                    "rx_idle_polls", "publish_ns", "deliver_ns")}
+                                                                    "rx_idle_polls", "publish_ns", "deliver_ns",
+                                                                    "zero_copy_frames")}
         if st.get("bursts"):
             out["engine"]["frames_per_burst"] = round(st["rx"] / st["bursts"], 1)
         lat = live.latency_us()
@@ -332,6 +334,7 @@ def main() -> None:
     ap.add_argument("--traffic", choices=("plain", "vxlan-egress", "broadcast"), default="plain")
     ap.add_argument("--coalesce-us", type=float, default=8.0)
     ap.add_argument("--loaded-window", type=int, default=2048, help="frames in flight of the closed-loop loaded run")
+    ap.add_argument("--zero-copy", action="store_true", help="the ring reads frames in the pods' memif regions")
     ap.add_argument("--veth", choices=("linux-bridge", "engine"), default=None,
                     help="netns pods on veth pairs, switched by a Linux bridge or by the native engine")
     a = ap.parse_args()
@@ -343,7 +346,7 @@ def main() -> None:
                          inflight=a.inflight, tx_workers=a.tx_workers, queues=a.queues,
                          max_inflight_frames=a.max_inflight_frames, pod_ring=a.pod_ring,
                          backend=a.backend, coalesce_us=a.coalesce_us, loaded_window=a.loaded_window,
-                         traffic=a.traffic)), flush=True)
+                         traffic=a.traffic, zero_copy=a.zero_copy)), flush=True)
 
 
 if __name__ == "__main__":
