@@ -148,6 +148,7 @@ std::unique_ptr<Engine> make_engine(Bridge& br, std::vector<std::shared_ptr<Orac
   auto e = std::make_unique<Engine>(128, 16, 2, 2, 1024);
   br.configure(bes);
   for (auto& b : bes) e->add_backend(b);
+  e->set_zero_copy(true);   // backend 1 reads frames by address (in the pods' regions): zero-copy rx
   for (uint32_t p = 0; p < kPods; ++p) e->add_port(p, ports[p]);
   e->set_steering(br.ports, br.rss, false);
   std::vector<uint32_t> side;
@@ -165,6 +166,7 @@ int main(int argc, char** argv) {
   Bridge br;
   std::vector<std::shared_ptr<OracleBackend>> bes = {std::make_shared<OracleBackend>(1024, 2),
                                                      std::make_shared<OracleBackend>(1024, 2)};
+  bes[1]->set_frame_addrs(true);
   std::vector<std::shared_ptr<Port>> ports;
   std::vector<trafgen::Pod> pods;
   for (uint32_t p = 0; p < kPods; ++p) {
@@ -247,6 +249,7 @@ int main(int argc, char** argv) {
   CHECK(res.bad == 0);
   CHECK(restarts == 1);
   CHECK(st["replicas"] > 0);   // floods to the never-learned pod went through the side pass
+  CHECK(st["zero_copy_frames"] > 0);
   std::printf("ops %u restarts %u sent %llu received %llu engine rx %llu tx %llu replicas %llu learn %llu\n", ops,
               restarts, (unsigned long long)res.sent, (unsigned long long)res.received,
               (unsigned long long)st["rx"], (unsigned long long)st["tx"], (unsigned long long)st["replicas"],

@@ -227,7 +227,8 @@ def test_native_sanitizer_stress(kind, tmp_path):
     """Race / memory-error detection on the native I/O engine (csrc/nfdp/iox_stress.cpp, host-only
     TSan or ASan+UBSan build): two queues x two oracle backends x two tx workers under memif
     traffic, while commits pause / hold the engine and swap its configuration, a port is removed
-    and re-added, statistics are read, and an injected failure rebuilds the engine."""
+    and re-added, statistics are read, and an injected failure rebuilds the engine; one backend
+    reads its frames by address in the pods' regions (zero-copy rx)."""
     import subprocess
 
     from dpu_operator_amd.native.build import build_sanitized
