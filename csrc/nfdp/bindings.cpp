@@ -892,14 +892,14 @@ PYBIND11_MODULE(_nfdp, m) {
         auto v = e.side_drop_counters();
         return py::array_t<uint64_t>(v.size(), v.data());
       })
-      .def("set_steering", [](Engine& e, py::buffer ports, py::bytes rss, bool v6) {
+      .def("set_steering", [](Engine& e, py::buffer ports, py::bytes rss, bool v6, std::vector<uint32_t> port_owner) {
         py::buffer_info bi = ports.request();
         const size_t n = (size_t)bi.size * bi.itemsize / sizeof(PortEntry);
         std::vector<PortEntry> v(n);
         std::memcpy(v.data(), bi.ptr, n * sizeof(PortEntry));
         std::string k = rss;
-        e.set_steering(v, std::vector<uint8_t>(k.begin(), k.end()), v6);
-      }, py::arg("ports"), py::arg("rss"), py::arg("v6") = false)
+        e.set_steering(v, std::vector<uint8_t>(k.begin(), k.end()), v6, port_owner);
+      }, py::arg("ports"), py::arg("rss"), py::arg("v6") = false, py::arg("port_owner") = std::vector<uint32_t>{})
       .def("set_redirect", &Engine::set_redirect)
       .def("set_side_ports", &Engine::set_side_ports)
       // A live commit's switch in one native call, without the GIL: hold publication (every rx

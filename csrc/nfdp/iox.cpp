@@ -609,9 +609,11 @@ int Engine::port_queue(uint32_t id) {
   return id < t->size() && (*t)[id].p ? (int)(*t)[id].q : -1;
 }
 
-void Engine::set_steering(const std::vector<PortEntry>& ports, const std::vector<uint8_t>& rss_key, bool v6) {
+void Engine::set_steering(const std::vector<PortEntry>& ports, const std::vector<uint8_t>& rss_key, bool v6,
+                          const std::vector<uint32_t>& port_owner) {
   if (rss_key.size() < 20) throw std::invalid_argument("iox: rss key too short");
   auto s = std::make_shared<Steer>();
+  s->port_owner = port_owner;
   s->ports = ports;
   s->ports.resize((size_t)kMaxPorts + 2);
   s->rss_key = rss_key;
@@ -657,6 +659,8 @@ void Engine::set_side_tables(uint32_t backend, std::shared_ptr<SideTables> t) {
 uint32_t Engine::owner(const Steer* s, uint32_t n, const uint8_t* f, uint32_t len, uint32_t in_port) {
   if (n <= 1) return 0;
   if (!s) return in_port % n;
+  if (!s->port_owner.empty())   // port placement: the ingress port's GPU (hop-affine chains)
+    return in_port < s->port_owner.size() ? s->port_owner[in_port] % n : in_port % n;
   return owner_tab(f, len, in_port, s->ports.data(), s->hash, n, s->v6);
 }
 

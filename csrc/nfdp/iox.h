@@ -442,7 +442,10 @@ class Engine {
   std::shared_ptr<Port> port(uint32_t id);
   int port_queue(uint32_t id);
   // Configuration (copy-on-write: safe while traffic flows).
-  void set_steering(const std::vector<PortEntry>& ports, const std::vector<uint8_t>& rss_key, bool v6 = false);
+  // port_owner non-empty: port placement — every frame goes to the GPU its ingress port is placed
+  // on (port_owner[in_port]), not to its flow's owner (MultiDataPlane placement="port").
+  void set_steering(const std::vector<PortEntry>& ports, const std::vector<uint8_t>& rss_key, bool v6 = false,
+                    const std::vector<uint32_t>& port_owner = {});
   void set_redirects(const std::vector<std::pair<uint32_t, uint32_t>>& tunnel_to_underlay);   // replaces all
   void set_redirect(uint32_t port, uint32_t underlay);   // one entry (0xFFFFFFFF clears it)
   void set_side_ports(const std::vector<uint32_t>& ports); // ingress ports whose packets need side work
@@ -541,6 +544,7 @@ class Engine {
     std::vector<uint8_t> rss_key;
     bool v6 = false;
     ToeplitzTab hash;
+    std::vector<uint32_t> port_owner;   // port placement (empty: flow owners)
   };
   struct Cfg {                   // everything the packet threads read from the control plane
     std::vector<uint32_t> redirect;      // tunnel port -> underlay port (0xFFFFFFFF: none)

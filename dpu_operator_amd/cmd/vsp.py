@@ -46,7 +46,7 @@ def build_vsp(a, pm: PathManager):
                       state_dir=a.state_dir or cfg.vsp_state_dir or None, nl=nl, live=a.live,
                       live_engine=a.live_engine, gpus=a.gpus if a.gpus == "all" else int(a.gpus),
                       vport_kind=a.vport_kind or cfg.vport_kind, tx_workers=a.io_workers or cfg.io_workers,
-                      io_queues=a.io_queues or cfg.io_queues)
+                      io_queues=a.io_queues or cfg.io_queues, placement=a.placement)
     from ..cni.netlink import RtNetlink
     from ..platform.platform import SysfsPlatform
     from ..utils.cmdrunner import HostRunner
@@ -62,7 +62,7 @@ def build_vsp(a, pm: PathManager):
         buckets = a.flow_buckets or node_config().flow_buckets
         n = len(visible_devices()) if a.gpus == "all" else int(a.gpus)
         if n > 1:
-            dp = MultiDataPlane(visible_devices()[:n], flow_buckets=buckets)
+            dp = MultiDataPlane(visible_devices()[:n], placement=a.placement, flow_buckets=buckets)
         else:
             dp = DataPlane(device=a.device or "cuda", flow_buckets=buckets)
         dp.commit(full=True)
@@ -119,6 +119,9 @@ def main(argv=None, stop: threading.Event | None = None) -> int:
                          "pinned host slots (Python loop), or the native C++ I/O engine + ring kernel")
     ap.add_argument("--gpus", default="1", help="amd-gpu / marvell / netsec: GPUs behind the VSP (a number or 'all'): tables "
                     "replicated, flows sharded by RSS owner, the native engine steering frames to their owner")
+    ap.add_argument("--placement", default="flow", choices=["flow", "port"],
+                    help="--gpus > 1: frames run on their flow's GPU (flows sharded by RSS owner) or on their "
+                         "ingress port's GPU (flows replicated: the SFC hop pipeline across GPUs)")
     ap.add_argument("--vport-kind", default="", choices=["", "veth", "tap", "memif"],
                     help="amd-gpu --live: vports as veth pairs (kernel-netdev pods, AF_PACKET rings), TAP "
                          "netdevs or shared-memory (memif) regions; default: node config vport_kind (veth)")

@@ -18,6 +18,15 @@ the VSP the same table API as a single ``DataPlane`` while spreading the work:
 The planes are ordinary ``DataPlane`` objects on ``cuda:0 .. cuda:N-1`` (or CPU oracle planes in
 tests).  One process drives them: the live path needs no GPU-to-GPU traffic because the host
 steers every frame to its owner's ring (pod rings are host memory every GPU can reach).
+
+``placement="port"`` is the other split — the SFC hop pipeline across GPUs.  Every port (a pod's
+VF, so one hop of a service function chain) is placed on one GPU (``place_port``; default
+port % N) and every frame runs on its ingress port's GPU: a chain A -> B -> C whose hops sit on
+GPUs 0, 1, 2 is processed hop by hop on 0, then 1, then 2, as the frames pass through the NF pods.
+The flow table is then replicated (each hop's GPU meets every flow; 288 GB per GPU holds it many
+times over), and a flow's counters are the sum of its counts on every GPU that carried it.  It
+trades the flow split's memory and insert cost for port affinity: one GPU serves a pod's ingress
+whatever its flows, so per-port order and per-port tables stay on one device.
 """
 from __future__ import annotations
 
@@ -79,23 +88,81 @@ class ShardedFlows:
         return self.planes[g].flows.find(key)
 
 
+class ReplicatedFlows:
+    """The flow-table API over planes that all hold every flow (port placement): inserts and
+    erases go to every plane (identical tables: the same slot everywhere), lookups to plane 0."""
+
+    def __init__(self, planes: list[DataPlane]):
+        self.planes = planes
+        self.rss_key = planes[0].flows.rss_key
+
+    def __len__(self) -> int:
+        return len(self.planes[0].flows)
+
+    @property
+    def nbuckets(self) -> int:
+        return self.planes[0].flows.nbuckets
+
+    def insert_many(self, keys: np.ndarray, actions: np.ndarray) -> np.ndarray:
+        slots = [p.flows.insert_many(keys, actions) for p in self.planes]
+        if any(not np.array_equal(slots[0], s) for s in slots[1:]):
+            raise RuntimeError("replicated flow tables diverged")
+        return slots[0]
+
+    def insert(self, key, action) -> int:
+        return int(self.insert_many(np.asarray([key], np.uint32), np.asarray([action], np.uint32))[0])
+
+    def erase_many(self, keys: np.ndarray) -> int:
+        return [p.flows.erase_many(keys) for p in self.planes][0]
+
+    def erase(self, key) -> bool:
+        return self.erase_many(np.asarray([key], np.uint32)) == 1
+
+    def find(self, key) -> int:
+        return self.planes[0].flows.find(key)
+
+
 class MultiDataPlane:
-    def __init__(self, devices: list[str], **kw):
+    def __init__(self, devices: list[str], placement: str = "flow", **kw):
+        """placement: "flow" (flows sharded by RSS owner, each frame on its flow's GPU) or "port"
+        (each frame on its ingress port's GPU, flows replicated: the SFC hop pipeline)."""
         if not devices:
             raise ValueError("at least one device")
+        if placement not in ("flow", "port"):
+            raise ValueError("placement: 'flow' or 'port'")
         self.planes = [DataPlane(device=d, **kw) for d in devices]
         p0 = self.planes[0]
         for dp in self.planes[1:]:
             for name in SHARED_MODELS:
                 setattr(dp, name, getattr(p0, name))
-        self.flows = ShardedFlows(self.planes)
         self.n = len(self.planes)
+        self.placement = placement
+        self.port_owner = None
+        if placement == "port":
+            from ..native import nfdp
+
+            self.flows = ReplicatedFlows(self.planes)
+            self.port_owner = np.arange(int(nfdp().MAX_PORTS) + 2, dtype=np.int64) % self.n
+            for dp in self.planes:
+                dp._port_owner = self.port_owner   # (the native engine steers by it: NativeLivePath)
+        else:
+            self.flows = ShardedFlows(self.planes)
 
     # table models, modes, device facts: plane 0's (shared objects)
     def __getattr__(self, name):
-        if name in ("planes", "flows", "n"):
+        if name in ("planes", "flows", "n", "placement", "port_owner"):
             raise AttributeError(name)
         return getattr(self.planes[0], name)
+
+    def place_port(self, port: int, gpu: int) -> None:
+        """Port placement: frames entering on `port` run on GPU `gpu` (takes effect for a
+        running native engine at the next commit)."""
+        if self.port_owner is None:
+            raise RuntimeError("place_port needs placement='port'")
+        if not 0 <= gpu < self.n:
+            raise ValueError(f"gpu in [0, {self.n})")
+        self.port_owner[int(port)] = int(gpu)
+        self.ports.version += 1   # the next commit re-applies the engine's steering
 
     @property
     def gpu(self) -> bool:
@@ -167,8 +234,19 @@ class MultiDataPlane:
         return out
 
     def flow_counters(self, key) -> tuple[int, int]:
+        if self.placement == "port":   # every GPU a hop of the flow ran on counted its share
+            c = [p.flow_counters(key) for p in self.planes]
+            return sum(x[0] for x in c), sum(x[1] for x in c)
         g = int(self.flows.owner(np.asarray([key], np.uint32))[0])
         return self.planes[g].flow_counters(key)
+
+    @property
+    def flow_totals(self) -> np.ndarray:
+        """Per-slot [packets, bytes] (harvested).  Port placement: summed over the planes
+        (replicated flows have the same slot on every plane); flow placement: plane 0's."""
+        if self.placement == "port":
+            return sum(p.flow_totals for p in self.planes)
+        return self.planes[0].flow_totals
 
     def reset_counters(self) -> None:
         for p in self.planes:
@@ -178,6 +256,9 @@ class MultiDataPlane:
     def owners(self, pkts: np.ndarray, inmeta: np.ndarray) -> np.ndarray:
         """Owner GPU of each packet, exactly as the native I/O engine steers it on ingress."""
         from ..native import nfdp
+
+        if self.placement == "port":
+            return self.port_owner[np.asarray(inmeta, np.uint32) & 0xFFFF] % self.n
 
         return np.asarray(nfdp().owner_of_frames(np.ascontiguousarray(pkts, np.uint8),
                                                  np.ascontiguousarray(inmeta, np.uint32),
@@ -193,6 +274,9 @@ class MultiDataPlane:
         and the native engine steer its frames)."""
         from . import tables as T2
 
+        if self.placement == "port":
+            slots = [p.add_flow6(src, dst, sport, dport, proto, zone, action) for p in self.planes]
+            return slots[0]
         key, _ = T2.flow_key6(src, dst, sport, dport, proto, zone)
         g = int(self.flows.owner(key[None, :])[0])
         return self.planes[g].add_flow6(src, dst, sport, dport, proto, zone, action)
@@ -200,6 +284,8 @@ class MultiDataPlane:
     def remove_flow6(self, src, dst, sport: int = 0, dport: int = 0, proto: int = 17, zone: int = 0) -> bool:
         from . import tables as T2
 
+        if self.placement == "port":
+            return [p.remove_flow6(src, dst, sport, dport, proto, zone) for p in self.planes][0]
         key, _ = T2.flow_key6(src, dst, sport, dport, proto, zone)
         g = int(self.flows.owner(key[None, :])[0])
         return self.planes[g].remove_flow6(src, dst, sport, dport, proto, zone)

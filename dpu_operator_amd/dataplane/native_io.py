@@ -337,7 +337,9 @@ class NativeLivePath:
         steer = None
         if len(self.dps) > 1:
             v6 = any(d._v6_keys() for d in self.dps)   # IPv6 frames steer by their folded 5-tuple
-            steer = (np.ascontiguousarray(a).copy(), bytes(dp0.rss_key), v6)
+            po = getattr(dp0, "_port_owner", None)   # MultiDataPlane placement="port"
+            steer = (np.ascontiguousarray(a).copy(), bytes(dp0.rss_key), v6,
+                     [int(x) for x in po] if po is not None else [])
         return {"side": side, "side_ports": side_ports, "redirects": red, "steer": steer}
 
     def _apply(self, c: dict) -> None:

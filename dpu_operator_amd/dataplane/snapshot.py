@@ -18,6 +18,9 @@ _USED = 0x100  # kSlotUsed marker in key.meta byte 1 (nfdp.h)
 
 
 def _flows(dp) -> tuple[np.ndarray, np.ndarray, np.ndarray]:
+    if getattr(dp, "placement", "flow") == "port":   # replicated flows: one copy, counts summed
+        parts = [_flows(p) for p in dp.planes]
+        return parts[0][0], parts[0][1], sum(x[2] for x in parts)
     if hasattr(dp, "planes"):       # MultiDataPlane: every GPU's shard
         parts = [_flows(p) for p in dp.planes]
         return tuple(np.concatenate([x[i] for x in parts]) for i in range(3))
@@ -68,7 +71,9 @@ def load(dp, path: str) -> dict:
             slots = np.asarray(dp.flows.insert_many(keys, acts), np.int64)
             if np.any(slots < 0):
                 raise RuntimeError("flow table too small for the snapshot")
-            if hasattr(dp, "planes"):   # counters follow their flow to its owner GPU
+            if getattr(dp, "placement", "flow") == "port":   # a flow's count: on the first plane
+                dp.planes[0].flow_totals[slots] = totals
+            elif hasattr(dp, "planes"):   # counters follow their flow to its owner GPU
                 own = dp.flows.owner(keys)
                 for g, p in enumerate(dp.planes):
                     p.flow_totals[slots[own == g]] = totals[own == g]

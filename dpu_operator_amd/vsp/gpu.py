@@ -104,7 +104,7 @@ class GpuVsp(VspBase):
                  opi_port: int = 0, flow_buckets: int = 1 << 16, vport_prefix: str = "dpuvp",
                  hash_mode: str = "mfma", acl_mode: str = "mfma", state_dir: str | None = None,
                  live: bool = False, uplink=None, live_engine: str = "batch", gpus=1, vport_kind: str = "tap",
-                 memif_dir: str | None = None, tx_workers: int = 1, io_queues: int = 1):
+                 memif_dir: str | None = None, tx_workers: int = 1, io_queues: int = 1, placement: str = "flow"):
         super().__init__(path_manager)
         if device is None:
             try:
@@ -121,6 +121,9 @@ class GpuVsp(VspBase):
         if gpus == "all":
             gpus = len(visible_devices()) if device != "cpu" else 1
         self.gpus = max(1, int(gpus))
+        if placement not in ("flow", "port"):
+            raise ValueError("placement is 'flow' (flows sharded) or 'port' (each vport on one GPU: hop pipeline)")
+        self.placement = placement
         if vport_kind not in ("tap", "veth", "memif"):
             raise ValueError("vport_kind is 'tap' / 'veth' (netdevs) or 'memif' (shared-memory vport)")
         self.vport_kind = vport_kind
@@ -169,7 +172,7 @@ class GpuVsp(VspBase):
                 devs = visible_devices() if self.device != "cpu" else ["cpu"] * self.gpus
                 if self.device != "cpu" and len(devs) < self.gpus:
                     raise RuntimeError(f"{self.gpus} GPUs requested, {len(devs)} visible")
-                self.dp = MultiDataPlane(devs[: self.gpus], **kw)
+                self.dp = MultiDataPlane(devs[: self.gpus], placement=self.placement, **kw)
             else:
                 self.dp = DataPlane(device=self.device, **kw)
             self.dp.ports.set(WIRE_PORT, flags=T.PORT_VALID, bridge_id=VF_BRIDGE, mac="02:00:00:00:0f:a0")

@@ -279,6 +279,74 @@ def test_multi_plane_native_matches_one_plane(shm, devices):
         live.stop()
 
 
+@pytest.mark.parametrize("devices", [["cpu", "cpu", "cpu"], pytest.param(["cuda:0", "cuda:0"], marks=pytest.mark.gpu)])
+def test_port_placement_hop_pipeline(shm, devices):
+    """MultiDataPlane(placement="port"), the SFC hop pipeline across GPUs: every frame runs on the
+    GPU its ingress port (one NF hop) is placed on — batch and live (the engine steers by the
+    port table, iox Steer::port_owner) — with flows replicated: frames equal one plane's, each
+    plane's rx counters hold only its own ports, and the flow counters summed over the planes
+    equal one plane's.  A port moved to another GPU (place_port + commit) is served there."""
+    nf = nfdp()
+    m = MultiDataPlane(devices, placement="port", flow_buckets=1 << 12)
+    sc = S.build_sfc(m, n_pods=6, n_flows=4096, n_acl=64, seed=0)
+    m.commit(full=True)
+    ref, _, _ = _sfc()
+    n = len(devices)
+    pods = [int(p) for p in sc.pod_port]
+    assert len(m.flows) == len(ref.flows) and all(len(p.flows) == len(ref.flows) for p in m.planes)
+    # batch: split by ingress port
+    slots, im = S.traffic(sc, 3000, seed=9)
+    r = m.run(slots, im)
+    r0 = ref.run(slots, im)
+    assert np.array_equal(r.meta, r0.meta) and np.array_equal(r.out, r0.out)
+    assert np.array_equal(r.extra["owner"], (im & 0xFFFF).astype(np.int64) % n)
+    m.reset_counters(); ref.reset_counters()
+    m.harvest(); ref.harvest()
+    # live: the engine steers by ingress port
+    exp, drops = _expected(ref, slots, im)
+    paths = {p: str(shm / f"h{p}") for p in pods}
+    live = NativeLivePath(m, {p: MemifVport(paths[p], ring_size=4096) for p in paths}, burst=128,
+                          ring_capacity=1024, queues=2).start()
+    try:
+        eps = _send_all(nf, paths, slots, im, pods)
+        got, done = _collect(eps, sum(map(len, exp.values())))
+        assert _until(done), (live.stats, live.error)
+        for port, frames in exp.items():
+            assert sorted(got[port]) == sorted(frames), port
+        src = (im & 0xFFFF).astype(np.int64)
+
+        def per_plane_rx_ok():
+            for g, p in enumerate(m.planes):
+                rx = p.port_counters()[:, 0]
+                for q in pods:
+                    want = int((src == q).sum()) if q % n == g else 0
+                    if int(rx[q]) != want:
+                        return False
+            return True
+
+        assert _until(per_plane_rx_ok, 2.0), [p.port_counters()[pods, 0].tolist() for p in m.planes]
+        assert _until(lambda: np.array_equal(m.port_counters(), ref.port_counters()), 2.0)
+        m.harvest(); ref.harvest()
+        assert np.array_equal(m.flow_totals, ref.flow_totals)
+        k = sc.keys[0]
+        assert m.flow_counters(k) == ref.flow_counters(k)
+        # move the first pod's port to another GPU: its next frames are processed there
+        q0 = pods[0]
+        g_new = (q0 + 1) % n
+        before = [int(p.port_counters()[q0, 0]) for p in m.planes]
+        m.place_port(q0, g_new)
+        m.commit()
+        sel = np.nonzero(src == q0)[0][:200]
+        for e in eps.values():
+            e.recv()
+        eps[q0].send([bytes(slots[k, : int(im[k] >> 16)]) for k in sel])
+        assert _until(lambda: int(m.planes[g_new].port_counters()[q0, 0]) - before[g_new] == len(sel), 4.0), \
+            ([int(p.port_counters()[q0, 0]) for p in m.planes], before)
+        assert int(m.planes[q0 % n].port_counters()[q0, 0]) == before[q0 % n]
+    finally:
+        live.stop()
+
+
 def test_learning_reaches_every_plane(shm):
     """MAC learning from the per-burst side pass goes through the learner thread into EVERY plane's
     MAC table (one learning bridge per node), not only the plane that saw the frame."""

@@ -127,6 +127,41 @@ def test_vsp_multi_gpu_bridge_ports_and_network_function(shm, n):
         vsp.stop()
 
 
+def test_vsp_port_placement_runs_each_hop_on_its_gpu(shm):
+    """--placement port on 3 planes (GpuVsp placement="port"): vport i is served by plane i % 3,
+    so with a network function inserted the VF's frames are classified on the VF's plane and the
+    NF's output on the NF-out port's plane — the chain's hops pipeline across the GPUs."""
+    nf = nfdp()
+    vsp = GpuVsp(device="cpu", gpus=3, live=True, vport_kind="memif", memif_dir=str(shm), flow_buckets=1 << 12,
+                 tx_workers=2, placement="port")
+    vsp.init(True, "gpu")
+    vsp.set_num_vfs(6)
+    try:
+        assert vsp.dp.placement == "port"
+        macs = ["02:00:00:00:dd:01", "02:00:00:00:dd:02"]
+        vsp.create_bridge_port("host0-0", bytes.fromhex(macs[0].replace(":", "")), 0, ["2"])
+        vsp.create_bridge_port("host0-1", bytes.fromhex(macs[1].replace(":", "")), 0, ["3"])
+        ep = {i: nf.MemifEndpoint(vsp.vport_path(i)) for i in range(6)}
+        frames = [f for s in range(64) for f in _pod_frame(macs[0], macs[1], 1000 + s)]
+        assert ep[0].send(frames) == len(frames)
+        got = []
+        assert _until(lambda: got.extend(ep[1].recv()) or len(got) >= len(frames)), vsp.livepath.stats
+        assert sorted(got) == sorted(frames)
+        rx0 = [int(p.port_counters()[0, 0]) for p in vsp.dp.planes]
+        assert rx0 == [len(frames), 0, 0]                     # every flow of vport 0 on plane 0
+        vsp.create_network_function(vsp.vports[4]["mac"], vsp.vports[5]["mac"])
+        fr2 = [f for s in range(32) for f in _pod_frame(macs[0], macs[1], 2000 + s)]
+        ep[0].send(fr2)
+        got_nf = []
+        assert _until(lambda: got_nf.extend(ep[4].recv()) or len(got_nf) >= len(fr2)), vsp.livepath.stats
+        assert sorted(got_nf) == sorted(fr2)
+        ep[5].send(got_nf)                                    # the NF passes them on: the next hop
+        assert _until(lambda: int(vsp.dp.planes[2].port_counters()[5, 0]) == len(fr2))
+        assert [int(p.port_counters()[5, 0]) for p in vsp.dp.planes[:2]] == [0, 0]
+    finally:
+        vsp.stop()
+
+
 def test_vsp_unhealthy_while_the_engine_restarts(shm):
     """A failed native engine makes every vport Unhealthy (device plugin), the supervisor
     rebuilds it, and the vports come back Healthy and forwarding."""
