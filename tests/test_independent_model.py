@@ -162,3 +162,107 @@ def test_imix_frames_match_independent_model(device):
         assert got == want, (i, ln)
         big += ln > 64
     assert big > 200
+
+
+def _flow_dict(sc, nat_ip, nat_port, deny, live_mask=None):
+    flows = {}
+    for k in range(len(sc.keys)):
+        if live_mask is not None and not live_mask[k]:
+            continue
+        s, d = S.POD_NET + int(sc.flow_src_pod[k]), S.POD_NET + int(sc.flow_dst_pod[k])
+        flows[(s.to_bytes(4, "big"), d.to_bytes(4, "big"), int(sc.flow_sport[k]), int(sc.flow_dport[k]))] = (
+            int(sc.pod_port[sc.flow_dst_pod[k]]), int(nat_ip[k]), int(nat_port[k]))
+    for j in range(len(deny["src"])):
+        flows[((S.POD_NET + int(deny["src"][j])).to_bytes(4, "big"), int(deny["dst_ip"][j]).to_bytes(4, "big"),
+               int(deny["sport"][j]), int(deny["dport"][j]))] = (0, 0, 0)
+    return flows
+
+
+@pytest.mark.parametrize("device", ["cpu", pytest.param("cuda", marks=pytest.mark.gpu)])
+def test_live_table_flip_matches_independent_model(device):
+    """The live path (native engine; on the GPU the persistent ring kernel) before and after a
+    commit that puts a deny rule first, erases an eighth of the flows and re-points the NAT of
+    another eighth: each phase's delivered frames equal the model's over that phase's tables.
+    On the GPU the commit is a table-set flip under the running ring (no relaunch), so this holds
+    the flip's results — not only the oracle's — to code that shares nothing with pipeline.h."""
+    import ipaddress
+    import shutil
+    import tempfile
+    import time
+    from pathlib import Path
+
+    from dpu_operator_amd.dataplane.native_io import MemifVport, NativeLivePath, memif_dir
+    from dpu_operator_amd.native import nfdp
+
+    nf = nfdp()
+    dp = DataPlane(device=device, flow_buckets=1 << 14, hash_mode="mfma", acl_mode="mfma")
+    sc = S.build_sfc(dp, n_pods=8, n_flows=6000, n_acl=256, seed=0)
+    deny = S.install_deny_flows(dp, sc, k=256)
+    dp.commit(full=True)
+    d = Path(tempfile.mkdtemp(prefix="dpu-flipm-", dir=memif_dir()))
+    pods = [int(p) for p in sc.pod_port]
+    live = NativeLivePath(dp, {p: MemifVport(str(d / f"p{p}"), ring_size=4096) for p in pods}, burst=128,
+                          ring_capacity=1024, queues=2).start()
+    eps = {p: nf.MemifEndpoint(str(d / f"p{p}")) for p in pods}
+
+    def phase(seed, flows):
+        pk, im = S.traffic_mixed(sc, deny, 3000, seed=seed)
+        acl = [(r_.value.astype(np.uint64), r_.mask.astype(np.uint64), r_.permit) for r_ in dp.acl.rules]
+        want: dict[int, list[bytes]] = {}
+        sent = {p: [] for p in pods}
+        seen = {}
+        for i in range(len(pk)):
+            ln = min(int(im[i]) >> 16, 64)
+            fr = bytes(pk[i][:ln])
+            sent[int(im[i]) & 0xFFFF].append(fr)
+            reason, port, out = _model(fr, int(im[i]) & 0xFFFF, ln, sc, flows, acl, dp.acl.default_permit)
+            seen[reason] = seen.get(reason, 0) + 1
+            if reason == OK:
+                want.setdefault(port, []).append(out)
+        for p, frs in sent.items():
+            k, t_end = 0, time.monotonic() + 10
+            while k < len(frs) and time.monotonic() < t_end:
+                k += eps[p].send(frs[k:])
+        got = {p: [] for p in pods}
+        n_want = sum(map(len, want.values()))
+        t_end = time.monotonic() + 15
+        while sum(map(len, got.values())) < n_want and time.monotonic() < t_end:
+            for p in pods:
+                got[p] += eps[p].recv()
+            time.sleep(0.002)
+        time.sleep(0.05)
+        for p in pods:
+            got[p] += eps[p].recv()
+        for p in pods:
+            assert sorted(got[p]) == sorted(want.get(p, [])), (p, len(got[p]), len(want.get(p, [])), live.stats)
+        return seen
+
+    try:
+        kk = np.arange(len(sc.keys))
+        nat_ip, nat_port = S.NAT_NET + (kk % 250) + 1, 1024 + (kk % 60000)   # (build_sfc's, host order)
+        seen_a = phase(31, _flow_dict(sc, nat_ip, nat_port, deny))
+        assert seen_a.get(OK, 0) > 2000 and seen_a.get(DENY, 0) > 20
+        # the commit: a deny rule first (everything to pod 1), flows k % 8 == 3 erased, the NAT of
+        # flows k % 8 == 5 re-pointed
+        dp.acl.add(permit=False, dst=f"{ipaddress.IPv4Address(S.POD_NET + 1)}/32")
+        dp.acl.rules.insert(0, dp.acl.rules.pop())
+        dp.acl.version += 1
+        gone = kk % 8 == 3
+        dp.flows.erase_many(sc.keys[gone])
+        moved = kk % 8 == 5
+        nat_ip, nat_port = nat_ip.copy(), nat_port.copy()
+        nat_ip[moved] = S.NAT_NET + 251 + (kk[moved] % 3)
+        nat_port[moved] = 40000 + (kk[moved] % 1000)
+        acts = sc.actions[moved].copy()
+        acts[:, 1:3] = T.flow_action(nat_ip=nat_ip[moved], nat_port=nat_port[moved])[:, 1:3]
+        dp.flows.erase_many(sc.keys[moved])
+        assert (np.asarray(dp.flows.insert_many(sc.keys[moved], acts)) >= 0).all()
+        dp.commit()
+        seen_b = phase(32, _flow_dict(sc, nat_ip, nat_port, deny, ~gone))
+        assert seen_b.get(DENY, 0) > seen_a.get(DENY, 0) + 200      # the new first rule denies pod 1's traffic
+        assert seen_b.get(NOROUTE, 0) > seen_a.get(NOROUTE, 0) + 200
+        if device == "cuda":
+            assert dp.flip_stats.get("table_flips", 0) >= 1 and live.restarts == 0, dp.flip_stats
+    finally:
+        live.stop()
+        shutil.rmtree(d, ignore_errors=True)
