@@ -295,7 +295,8 @@ class RingEngine {
   bool running_ = false;
   int device_ = 0;
   FusedLaunch launch_{};
-  RingTableSet* d_sets_ = nullptr;   // [2] device table sets (coop rings)
+  RingTableSet* h_sets_ = nullptr;   // [2] table sets (coop rings): pinned coherent host memory
+  RingTableSet* d_sets_ = nullptr;   // (its device view)
   RingCtrlRing* ctrl_ = nullptr;     // pinned, coherent: the control mailbox
   uint64_t ctrl_head_ = 0;           // (ctrl_mu_) entries posted
   std::mutex ctrl_mu_;

@@ -640,8 +640,13 @@ RingEngine::RingEngine(uint32_t capacity, int num_cus, int wgs_per_cu, bool coop
     for (size_t i = 0; i < slots; ++i) h_faddr_[i] = reinterpret_cast<uint64_t>(d_in_) + i * 64u;
   }
   ck(hipMalloc(reinterpret_cast<void**>(&d_svc_), (size_t)nq_ * nch_ * 4 * kSvcWords), "dev alloc svc");
-  ck(hipMalloc(reinterpret_cast<void**>(&d_sets_), 2 * sizeof(RingTableSet)), "dev alloc table sets");
-  ck(hipMemset(d_sets_, 0, 2 * sizeof(RingTableSet)), "memset");
+  // Table sets: pinned, coherent host memory the grid reads (a few hundred bytes, once per set
+  // change).  Staging one is a host store, never a copy on a stream: with resident grids on the
+  // device a stream may share a hardware queue with one of them and would never be served.
+  ck(hipHostMalloc(reinterpret_cast<void**>(&h_sets_), 2 * sizeof(RingTableSet), hipHostMallocCoherent | hipHostMallocMapped),
+     "host alloc table sets");
+  std::memset(static_cast<void*>(h_sets_), 0, 2 * sizeof(RingTableSet));
+  ck(hipHostGetDevicePointer(reinterpret_cast<void**>(&d_sets_), h_sets_, 0), "device ptr table sets");
   ck(hipMemset(d_svc_, 0, (size_t)nq_ * nch_ * 4 * kSvcWords), "memset");
   // (the launch stream is created by start() and destroyed by stop(): a resident grid holds its
   // stream's hardware queue, and a stopped ring should not keep one that other streams then share)
@@ -653,7 +658,8 @@ RingEngine::~RingEngine() {
   } catch (...) {
   }
   release_streams();
-  for (void* d : {(void*)st_, (void*)d_svc_, (void*)d_sets_}) (void)hipFree(d);
+  for (void* d : {(void*)st_, (void*)d_svc_}) (void)hipFree(d);
+  (void)hipHostFree(h_sets_);
   if (host_slots_) {
     for (void* h : host_ptrs_) (void)hipHostFree(h);
   } else {
@@ -864,11 +870,10 @@ void RingEngine::stage_tables(const FusedLaunch& f, int which) {
   ts.toep_frag = f.toep_frag; ts.toep_tab = f.toep_tab;
   std::lock_guard<std::mutex> g(mu_);
   ts.serial = ++set_serial_;
-  // a copy on the engine's own stream would queue behind the resident kernel: the engine's
-  // staging stream (one per engine, whatever thread commits; the grid never reads the idle set)
-  if (!stage_stream_) ck(hipStreamCreateWithFlags(&stage_stream_, hipStreamNonBlocking), "stream");
-  ck(hipMemcpyAsync(d_sets_ + which, &ts, sizeof(ts), hipMemcpyHostToDevice, stage_stream_), "table set upload");
-  ck(hipStreamSynchronize(stage_stream_), "table set upload");
+  // the idle set (the grid never reads it until an epoch names it; the epoch word's release store
+  // orders this store before it)
+  std::memcpy(static_cast<void*>(h_sets_ + which), &ts, sizeof(ts));
+  std::atomic_thread_fence(std::memory_order_release);
   if (running_) {
     // the side pass (RingPath.side_pass) reads the session's tables from launch()
     launch_.t = f.t;
