@@ -177,6 +177,7 @@ def measure_variants(a, dp, sc, dev, torch, S, P) -> dict:
     dp.commit()
     del b
     # ACL1024 on the headline traffic
+    acl_headline = list(dp.acl.rules)
     S.add_acl_rules(dp, 1024)
     dp.commit()
     pk, im = S.traffic(sc, n, seed=9001)
@@ -191,7 +192,9 @@ def measure_variants(a, dp, sc, dev, torch, S, P) -> dict:
     res["acl_wild_mpps"] = round(n * a.variant_steps / el / 1e6, 1)
     res["acl_wild"] = {"rules": info["rules"], "ternary_entries": info["entries"], "rule_tiles": int(dp._acl_tiles),
                        "forwarded_fraction": round(float(np.mean(P.meta_fields(meta.cpu().numpy().view(np.uint32))[2] == 0)), 4)}
-    dp.acl.rules = info["saved"]
+    # back to the headline's 256 rules: the dual-stack variant is the headline plus IPv6 (through
+    # r4 s13 it ran with the 1024-rule variant's 1280 IPv4 rules left in place)
+    dp.acl.rules = acl_headline
     dp.acl.version += 1
     dp.commit()
     del mixed, b
@@ -213,6 +216,7 @@ def measure_variants(a, dp, sc, dev, torch, S, P) -> dict:
     rs6 = P.meta_fields(meta.cpu().numpy().view(np.uint32))[2]
     res["ipv6_dispositions"] = {int(k): int(v) for k, v in zip(*np.unique(rs6, return_counts=True))}
     res["ipv6"] = {"ipv6_fraction": 0.5, "ipv6_flows": info6["flows"], "ipv6_acl_rules": info6["rules"],
+                   "ipv4_acl_rules": len(dp.acl.rules),
                    "forwarded_fraction": round(float(np.mean(P.meta_fields(meta.cpu().numpy().view(np.uint32))[2] == 0)), 4),
                    "frames": "64-B IPv4 + 66-B tagged IPv6/UDP (the smallest)"}
     del b
