@@ -90,7 +90,7 @@ MemifPort::MemifPort(const std::string& path, uint32_t ring_size, uint32_t buf_s
 
 MemifPort::~MemifPort() {
   unmap_rx();   // before the region's mapping goes (the Region member's destructor)
-  if (unlink_) ::unlink(reg_.path().c_str());
+  if (unlink_ && reg_.path_is_mine()) ::unlink(reg_.path().c_str());   // (not a successor's file)
 }
 
 uint32_t MemifPort::rx(RxRef* out, uint32_t max) {

@@ -87,7 +87,10 @@ class Region {
         throw std::invalid_argument("memif: ring_size must be a power of two in [2, 2^20]");
       if (buf_size < 64 || buf_size > (1u << 16) || (buf_size & 63))
         throw std::invalid_argument("memif: buf_size must be a multiple of 64 in [64, 65536]");
-      fd_ = ::open(path.c_str(), O_RDWR | O_CREAT | O_TRUNC, 0600);
+      // a fresh file, never the old one truncated: a previous region at this path may still be
+      // mapped (a removed port the engine keeps for its frames in flight, a pod not yet detached)
+      ::unlink(path.c_str());
+      fd_ = ::open(path.c_str(), O_RDWR | O_CREAT | O_EXCL, 0600);
       if (fd_ < 0) throw std::runtime_error("memif: cannot create " + path);
       bytes_ = region_bytes(ring_size, buf_size, rx_rings);
       if (ftruncate(fd_, (off_t)bytes_) != 0) { close(); throw std::runtime_error("memif: ftruncate " + path); }
@@ -102,6 +105,10 @@ class Region {
     // costs ~1-2 us in a VM, i.e. more than the whole per-frame budget)
     base_ = static_cast<uint8_t*>(mmap(nullptr, bytes_, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_POPULATE, fd_, 0));
     if (base_ == MAP_FAILED) { base_ = nullptr; close(); throw std::runtime_error("memif: mmap " + path); }
+    {
+      struct stat st {};
+      if (fstat(fd_, &st) == 0) { dev_ = (uint64_t)st.st_dev; ino_ = (uint64_t)st.st_ino; }
+    }
     if (create) {
       std::memset(base_, 0, bytes_);   // allocates every page of the region up front
       hdr()->version = kVersion;
@@ -142,6 +149,11 @@ class Region {
   }
   bool is_open() const { return base_ != nullptr; }
   const std::string& path() const { return path_; }
+  // The path still names this region's file (not a newer region created at the same path).
+  bool path_is_mine() const {
+    struct stat st {};
+    return !path_.empty() && ::stat(path_.c_str(), &st) == 0 && (uint64_t)st.st_dev == dev_ && (uint64_t)st.st_ino == ino_;
+  }
   Hdr* hdr() const { return reinterpret_cast<Hdr*>(base_); }
   size_t bytes() const { return bytes_; }
   uint8_t* base() const { return base_; }
@@ -165,6 +177,7 @@ class Region {
   uint8_t* desc_base_ = nullptr;
   uint8_t* buf_base_ = nullptr;
   std::string path_;
+  uint64_t dev_ = 0, ino_ = 0;   // the mapped file's identity
 };
 
 // Producer side of one ring: reserve -> fill buffer -> commit (batched head publication).

@@ -470,3 +470,26 @@ def test_coalescing_never_delays_an_idle_lane(shm):
             assert time.perf_counter() - t0 < 0.25      # far below the 1 s window
     finally:
         eng.stop()
+
+
+def test_memif_region_recreated_at_the_same_path(shm):
+    """A port re-created at the path of one still alive (a removed port the engine keeps while its
+    frames drain) gets a fresh file: the old mapping is never truncated under it, and the old
+    port going away later does not unlink its successor's file."""
+    import gc
+    import os
+
+    nf = nfdp()
+    path = str(shm / "again")
+    old = nf.MemifPort(path, 256, 2048)
+    ep_old = nf.MemifEndpoint(path)
+    new = nf.MemifPort(path, 256, 2048)
+    assert ep_old.send([bytes(64)]) == 1          # the old region is intact (not truncated)
+    del old, ep_old
+    gc.collect()
+    assert os.path.exists(path)                     # still the new port's file
+    ep = nf.MemifEndpoint(path)
+    assert ep.send([bytes(64)]) == 1
+    del ep, new
+    gc.collect()
+    assert not os.path.exists(path)
