@@ -102,7 +102,9 @@ def test_netns_pods_through_the_native_engine_bit_exact(kind):
                 rest.remove(f)
             assert not rest, (p, len(rest))
         assert live.error is None
-        assert live.stats["rx"] == len(slots)
+        # (>=: a netdev's kernel may emit a few frames of its own - IPv6 DAD / MLD before the
+        # pod's IPv6 is off - which the engine reads too and the pipeline drops or punts)
+        assert live.stats["rx"] >= len(slots)
     finally:
         if live is not None:
             live.stop()
