@@ -493,3 +493,115 @@ def test_memif_region_recreated_at_the_same_path(shm):
     del ep, new
     gc.collect()
     assert not os.path.exists(path)
+
+
+@pytest.mark.parametrize("devices", [["cpu", "cpu"], pytest.param(["cuda:0", "cuda:0"], marks=pytest.mark.gpu)])
+def test_live_soak_under_churn(shm, devices):
+    """~10 s of pod traffic through two planes (on a GPU box: two ring kernels on one MI355X; port
+    placement, zero-copy rx)
+    while the control plane churns: ACL rules added and removed (live table-set flips), ports moved
+    between the planes, link flaps through the device control mailbox, a spare vport removed and
+    re-added.  Traffic never stops, the engine never fails or restarts, and once the churn is undone
+    a final batch is bit-exact with a CPU plane holding the same tables."""
+    import ipaddress
+    import threading
+
+    from dpu_operator_amd.dataplane import tables as T2
+
+    nf = nfdp()
+    m = MultiDataPlane(devices, placement="port", flow_buckets=1 << 14)
+    sc = S.build_sfc(m, n_pods=6, n_flows=8192, n_acl=64, seed=0)
+    m.commit(full=True)
+    ref, _, _ = _sfc(n_flows=8192)
+    pods = [int(p) for p in sc.pod_port]
+    spare = max(pods) + 4
+    paths = {p: str(shm / f"s{p}") for p in pods + [spare]}
+    live = NativeLivePath(m, {p: MemifVport(paths[p], ring_size=4096) for p in paths}, burst=128,
+                          ring_capacity=2048, queues=2, zero_copy=True).start()
+    eps = {p: nf.MemifEndpoint(paths[p]) for p in pods}
+    slots, im = S.traffic(sc, 6000, seed=12)
+    src = im & 0xFFFF
+    by_pod = {p: [bytes(slots[k, : int(im[k] >> 16)]) for k in np.nonzero(src == p)[0]] for p in pods}
+    stop = threading.Event()
+    windows: list[int] = []
+    lock = threading.Lock()
+
+    def sender():
+        got = 0
+        t_win = time.monotonic()
+        while not stop.is_set():
+            for p in pods:
+                eps[p].send(by_pod[p][:64])
+            for p in pods:
+                got += len(eps[p].recv())
+            if time.monotonic() - t_win >= 1.0:
+                with lock:
+                    windows.append(got)
+                got, t_win = 0, time.monotonic()
+            time.sleep(0.0005)
+
+    th = threading.Thread(target=sender, daemon=True)
+    th.start()
+    rng = np.random.default_rng(5)
+    ops = {"acl": 0, "move": 0, "flap": 0, "spare": 0}
+    try:
+        t_end = time.monotonic() + 10.0
+        while time.monotonic() < t_end:
+            k = int(rng.integers(0, 4))
+            if k == 0:      # a deny rule in, then out (two live table-set flips)
+                pod = int(rng.integers(0, 6))
+                m.acl.add(permit=False, dst=f"{ipaddress.IPv4Address(S.POD_NET + pod)}/32")
+                m.acl.rules.insert(0, m.acl.rules.pop())
+                m.acl.version += 1
+                m.commit()
+                m.acl.rules.pop(0)
+                m.acl.version += 1
+                m.commit()
+                ops["acl"] += 1
+            elif k == 1:    # a pod's port moves to the other plane
+                p = pods[int(rng.integers(0, len(pods)))]
+                m.place_port(p, 1 - int(m.port_owner[p]))
+                m.commit()
+                ops["move"] += 1
+            elif k == 2:    # link flap through the control mailbox (no commit)
+                p = pods[int(rng.integers(0, len(pods)))]
+                for on in (False, True):
+                    if on:
+                        m.ports.a[p]["flags"] |= np.uint32(T2.PORT_VALID)
+                    else:
+                        m.ports.a[p]["flags"] &= ~np.uint32(T2.PORT_VALID)
+                    if m.gpu:
+                        assert m.ctrl_ports([p])
+                    else:           # (no ring kernel on CPU planes: a commit)
+                        m.ports.version += 1
+                        m.commit()
+                ops["flap"] += 1
+            else:           # the spare vport goes away and comes back
+                live.remove_port(spare)
+                time.sleep(0.005)
+                live.add_port(spare, MemifVport(paths[spare], ring_size=4096))
+                ops["spare"] += 1
+            time.sleep(0.02)
+        stop.set()
+        th.join(timeout=10)
+        assert live.error is None and live.restarts == 0, (live.error, live.restarts)
+        assert min(ops.values()) >= 3, ops
+        with lock:
+            assert len(windows) >= 8 and min(windows) > 0, windows     # traffic never stopped
+        # undo: every pod on its default plane, tables as the reference's; then a final exact batch
+        for p in pods:
+            m.place_port(p, p % 2)
+        m.commit()
+        time.sleep(0.2)
+        for p in pods:
+            eps[p].recv()
+        slots2, im2 = S.traffic(sc, 2000, seed=13)
+        exp, _ = _expected(ref, slots2, im2)
+        eps2 = _send_all(nf, {p: paths[p] for p in pods}, slots2, im2, pods)
+        got, done = _collect(eps2, sum(map(len, exp.values())))
+        assert _until(done, 15.0), (live.stats, live.error)
+        for port, frames in exp.items():
+            assert sorted(got[port]) == sorted(frames), port
+    finally:
+        stop.set()
+        live.stop()
