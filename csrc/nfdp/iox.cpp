@@ -89,8 +89,13 @@ MemifPort::MemifPort(const std::string& path, uint32_t ring_size, uint32_t buf_s
 }
 
 MemifPort::~MemifPort() {
-  unmap_rx();   // before the region's mapping goes (the Region member's destructor)
   if (unlink_ && reg_.path_is_mine()) ::unlink(reg_.path().c_str());   // (not a successor's file)
+  if (rx_mapped()) {
+    // mapped for the GPUs: the region's memory stays until that mapping is gone (deferred while
+    // rings run), so it goes with the unmapping, not with this object
+    auto mem = std::make_shared<memif::Region::Detached>(reg_.detach());
+    unmap_rx([mem] { mem->free(); });
+  }
 }
 
 uint32_t MemifPort::rx(RxRef* out, uint32_t max) {
@@ -571,14 +576,19 @@ void Engine::reap_retired(bool all) {
 void Engine::map_port(Port& p) {
   const auto mem = p.rx_memory();
   if (!mem.first || !mem.second || p.zc_.lo) return;
+  if (p.zc_.release && p.zc_.off.size() == backends_.size()) {   // still mapped from before
+    p.zc_.lo = mem.first;
+    p.zc_.hi = mem.first + mem.second;
+    return;
+  }
   Port::Mapped m;
   m.off.assign(backends_.size(), 0);
   for (size_t g = 0; g < backends_.size(); ++g) {
-    std::function<void()> rel;
+    std::function<void(std::function<void()>)> rel;
     const uint64_t a = backends_[g]->map_host(mem.first, mem.second, &rel);
     if (rel) m.release = std::move(rel);   // (at most one backend registers: the first)
     if (!a) {   // a backend cannot read it: the port's frames are copied, as without the mode
-      if (m.release) m.release();
+      if (m.release) m.release(nullptr);
       return;
     }
     m.off[g] = (int64_t)(a - reinterpret_cast<uint64_t>(mem.first));
@@ -595,7 +605,7 @@ void Engine::set_zero_copy(bool on) {
   for (const PortRef& r : *ports_) {
     if (!r.p) continue;
     if (on) map_port(*r.p);
-    else r.p->unmap_rx();
+    else r.p->zc_.lo = r.p->zc_.hi = nullptr;   // copied from now on (the mapping stays with the port)
   }
 }
 

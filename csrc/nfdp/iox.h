@@ -130,14 +130,17 @@ class Port {
   virtual void flush_locked(uint32_t) {}
   virtual void release_to(uint32_t seq_end) = 0;   // every frame below seq_end is done
   void set_first_seq(uint32_t s) { rel_ = s; seen_ = s; }
-  // Drop the pipeline's mapping of rx_memory() (a port that unmaps it calls this first).
-  void unmap_rx() {
-    if (zc_.release) {
-      auto f = std::move(zc_.release);
-      zc_.release = nullptr;
-      f();
-    }
+  // Drop the pipeline's mapping of rx_memory(); `after` runs once it is gone (it may be deferred
+  // while GPU rings run: a port that frees the memory does so in `after`).  False: nothing was
+  // mapped by this port (`after` not called).
+  bool rx_mapped() const { return (bool)zc_.release; }
+  bool unmap_rx(std::function<void()> after = nullptr) {
     zc_.lo = zc_.hi = nullptr;
+    if (!zc_.release) return false;
+    auto f = std::move(zc_.release);
+    zc_.release = nullptr;
+    f(std::move(after));
+    return true;
   }
   uint32_t window() const { return mask_ + 1; }
   struct alignas(64) TxLock { std::mutex mu; };
@@ -158,7 +161,8 @@ class Port {
     const uint8_t* lo = nullptr;
     const uint8_t* hi = nullptr;
     std::vector<int64_t> off;
-    std::function<void()> release;   // unregisters the memory (the registering backend's)
+    // unregisters the memory (the registering backend's), then runs its argument
+    std::function<void(std::function<void()>)> release;
   };
   Mapped zc_;
   friend class Engine;
@@ -321,7 +325,7 @@ class Backend {
   virtual uint64_t in_slot_addr(uint32_t q, uint32_t pos) { return reinterpret_cast<uint64_t>(in_slot(q, pos)); }
   // Make host memory [p, p + n) readable by the pipeline: its address there (0: cannot).  Sets
   // *release when this call registered it (run it once nothing of the memory is in flight).
-  virtual uint64_t map_host(const void*, size_t, std::function<void()>*) { return 0; }
+  virtual uint64_t map_host(const void*, size_t, std::function<void(std::function<void()>)>*) { return 0; }
 };
 
 class GpuBackend : public Backend {
@@ -345,7 +349,7 @@ class GpuBackend : public Backend {
     return ring_->frame_addrs_on() ? ring_->frame_addrs() + (size_t)q * cap_ : nullptr;
   }
   uint64_t in_slot_addr(uint32_t q, uint32_t pos) override { return ring_->in_slot_addr(q, pos); }
-  uint64_t map_host(const void* p, size_t n, std::function<void()>* release) override;
+  uint64_t map_host(const void* p, size_t n, std::function<void(std::function<void()>)>* release) override;
 
  private:
   RingEngine* ring_;
@@ -377,7 +381,9 @@ class OracleBackend : public Backend {
   // in slots at publish, as the GPU ring reads them (the engine's side of the mode, testable here)
   void set_frame_addrs(bool on);
   uint64_t* frame_addrs(uint32_t q) override { return fa_.empty() ? nullptr : fa_.data() + (size_t)q * cap_; }
-  uint64_t map_host(const void* p, size_t, std::function<void()>*) override { return reinterpret_cast<uint64_t>(p); }
+  uint64_t map_host(const void* p, size_t, std::function<void(std::function<void()>)>*) override {
+    return reinterpret_cast<uint64_t>(p);
+  }
 
  protected:
   virtual void run_segment(uint32_t q, uint32_t pos, uint32_t n);

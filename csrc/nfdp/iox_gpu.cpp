@@ -38,12 +38,13 @@ void GpuBackend::thread_init() { hck(hipSetDevice(ring_->device()), "set device"
 
 // Host memory pinned and mapped for every device (portable): a second backend finds it
 // registered already and only looks up its address.
-uint64_t GpuBackend::map_host(const void* p, size_t n, std::function<void()>* release) {
+uint64_t GpuBackend::map_host(const void* p, size_t n, std::function<void(std::function<void()>)>* release) {
   thread_init();
   void* h = const_cast<void*>(p);
   const hipError_t e = hipHostRegister(h, n, hipHostRegisterMapped | hipHostRegisterPortable);
   if (e == hipSuccess) {
-    *release = [h]() { (void)hipHostUnregister(h); };
+    // (unregistering waits for the device: deferred while any ring grid is resident)
+    *release = [h](std::function<void()> after) { host_unregister_when_idle(h, std::move(after)); };
   } else {
     (void)hipGetLastError();
     if (e != hipErrorHostMemoryAlreadyRegistered) return 0;
@@ -51,7 +52,7 @@ uint64_t GpuBackend::map_host(const void* p, size_t n, std::function<void()>* re
   void* d = nullptr;
   if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess || !d) {
     (void)hipGetLastError();
-    if (*release) { (*release)(); *release = nullptr; }
+    if (*release) { (*release)(nullptr); *release = nullptr; }
     return 0;
   }
   return reinterpret_cast<uint64_t>(d);

@@ -141,6 +141,25 @@ class Region {
     buf_base_ = desc_base_ + (size_t)nrings_ * ring_size * sizeof(Desc);
     path_ = path;
   }
+  // The mapping and descriptor, handed over: this object no longer owns them (a region whose
+  // memory must outlive it - still mapped for a GPU - is freed later through free()).
+  struct Detached {
+    uint8_t* base = nullptr;
+    size_t bytes = 0;
+    int fd = -1;
+    void free() {
+      if (base) munmap(base, bytes);
+      base = nullptr;
+      if (fd >= 0) ::close(fd);
+      fd = -1;
+    }
+  };
+  Detached detach() {
+    Detached d{base_, bytes_, fd_};
+    base_ = nullptr;
+    fd_ = -1;
+    return d;
+  }
   void close() {
     if (base_) munmap(base_, bytes_);
     base_ = nullptr;

@@ -45,6 +45,7 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <functional>
 #include <chrono>
 #include <cstdint>
 #include <memory>
@@ -257,7 +258,8 @@ class RingEngine {
 
  private:
   bool chunk_done(uint64_t chunk, uint32_t q) const;
-  void release_streams();   // after the grid exited: the launch and staging streams go
+  void release_streams();   // after the grid exited: the launch stream goes
+  void set_running(bool on);   // running_, and the process-wide count of running grids
   void pace_epoch_change();
   // (mu_ held) a new epoch for every queue: each queue's flip point is its published count now
   void set_epoch_all(uint32_t e);
@@ -273,7 +275,6 @@ class RingEngine {
   };
   mutable std::mutex mu_;     // epoch changes / table sets (engine-wide)
   uint32_t cap_, nch_, nq_;
-  hipStream_t stage_stream_ = nullptr;   // table-set uploads (created on first use, mu_ held)
   int num_cus_, wgs_;
   bool coop_;
   bool host_slots_;
@@ -304,6 +305,10 @@ class RingEngine {
   uint32_t lds_tiles_ = 0;
   uint32_t set_serial_ = 0;
 };
+
+// hipHostUnregister(p), then after(), once no ring of this process is running (at once if none
+// is): the unregistration waits for the device, which a resident grid never leaves idle.
+void host_unregister_when_idle(void* p, std::function<void()> after);
 
 // Launch the persistent kernel (ring.hip).  Exposed for the engine only.
 struct RingLaunch {

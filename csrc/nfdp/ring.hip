@@ -722,7 +722,47 @@ void RingEngine::start(const FusedLaunch& f, const LaunchCfg& cfg, double deadli
   r.deadline_ticks = (unsigned long long)(deadline_s * 1e8);  // s_memrealtime: 100 MHz
   r.flows_alt = flows_alt;
   ck(launch_ring(r, cfg, wgs_, coop_, stream_), "launch");
-  running_ = true;
+  set_running(true);
+}
+
+// ---- host memory mapped for the grids (zero-copy rx) --------------------------------------------
+// hipHostUnregister waits for the device, which a resident grid never lets go idle: an unmap that
+// comes while any ring of this process runs waits here (memory still mapped and pinned) until the
+// last ring stops.
+namespace {
+std::mutex g_grid_mu;
+int g_grids = 0;   // (g_grid_mu) rings running in this process
+std::vector<std::pair<void*, std::function<void()>>> g_unmaps;   // (g_grid_mu) deferred
+void drain_unmaps(std::vector<std::pair<void*, std::function<void()>>>& v) {
+  for (auto& u : v) {
+    (void)hipHostUnregister(u.first);
+    (void)hipGetLastError();
+    if (u.second) u.second();
+  }
+  v.clear();
+}
+}  // namespace
+
+void host_unregister_when_idle(void* p, std::function<void()> after) {
+  std::vector<std::pair<void*, std::function<void()>>> now;
+  {
+    std::lock_guard<std::mutex> g(g_grid_mu);
+    g_unmaps.emplace_back(p, std::move(after));
+    if (g_grids == 0) now.swap(g_unmaps);
+  }
+  drain_unmaps(now);
+}
+
+void RingEngine::set_running(bool on) {
+  if (on == running_) return;
+  running_ = on;
+  std::vector<std::pair<void*, std::function<void()>>> now;
+  {
+    std::lock_guard<std::mutex> g(g_grid_mu);
+    g_grids += on ? 1 : -1;
+    if (g_grids == 0) now.swap(g_unmaps);
+  }
+  drain_unmaps(now);
 }
 
 void RingEngine::stop(double timeout_s) {
@@ -739,12 +779,12 @@ void RingEngine::stop(double timeout_s) {
   for (;;) {
     const hipError_t q = hipStreamQuery(stream_);
     if (q == hipSuccess) break;
-    if (q != hipErrorNotReady) { running_ = false; ck(q, "kernel"); }
+    if (q != hipErrorNotReady) { set_running(false); ck(q, "kernel"); }
     if (secs(t0, Clock::now()) > timeout_s) throw std::runtime_error("ring: kernel did not drain before the timeout");
     std::this_thread::sleep_for(std::chrono::microseconds(50));
   }
-  running_ = false;
   release_streams();
+  set_running(false);   // (after the stream is gone: a deferred unmap may run now)
   for (uint32_t q = 0; q < nq_; ++q)
     if (completed(q) != published(q)) throw std::runtime_error("ring: stopped with published chunks unprocessed");
 }
@@ -754,11 +794,6 @@ void RingEngine::release_streams() {
     (void)hipStreamSynchronize(stream_);
     (void)hipStreamDestroy(stream_);
     stream_ = nullptr;
-  }
-  std::lock_guard<std::mutex> g(mu_);
-  if (stage_stream_) {
-    (void)hipStreamDestroy(stage_stream_);
-    stage_stream_ = nullptr;
   }
 }
 
