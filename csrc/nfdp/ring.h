@@ -118,7 +118,10 @@ struct alignas(128) RingDevState {
   uint64_t dprod;  // device mirror of ctl.prod (advanced by the frontier wave), bit 63 = stop
   uint32_t ctl_gen;   // (queue 0's state only) control-mailbox writes applied so far: a workgroup
                       // seeing it move restages its LDS copies of the small tables
-  uint32_t pad1[29];
+  uint32_t set_serial[2];   // (queue 0's) device mirror of the table sets' serials: written before
+                            // the flip that names the set (start(), or the control mailbox), so the
+                            // serial check never waits on a host-memory read
+  uint32_t pad1[27];
 };
 
 // Control mailbox: the control plane's small table writes (a port entry on a link / MTU / RX-state
@@ -244,6 +247,9 @@ class RingEngine {
   // the entry's number (ctrl_done() >= it once applied).  Throws if the grid is not running or the
   // mailbox stays full for `timeout_s`.
   uint64_t post_write(uint64_t dst, const uint32_t* data, uint32_t n, double timeout_s = 1.0);
+ private:
+  uint64_t post_ctrl(uint64_t dst, const uint32_t* data, uint32_t n, double timeout_s);   // (no region check)
+ public:
   uint64_t ctrl_posted() const { return ctrl_head_; }
   // Device buffers control writes may target ([base, bytes) each: the running table set's small
   // tables); anything else is refused on the host, so a bad address never reaches the GPU.

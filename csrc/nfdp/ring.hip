@@ -273,7 +273,11 @@ __global__ __launch_bounds__(kRingBlock) void ring_kernel(RingArgs a) {
   const uint32_t lane = threadIdx.x & 63u;
 
   // ---- control mailbox (ring.h RingCtrlRing): workgroup 0's wave 0 applies posted writes ----
+#ifndef NFDP_NO_CTRL_POLL
   const bool poller = blockIdx.x == 0 && wave == 0 && a.ctrl != nullptr;
+#else   // latency attribution only (control writes are never applied)
+  const bool poller = false;
+#endif
   unsigned long long ctrl_n = 0, ctrl_t = 0;
   uint32_t ctrl_tick = 0;
   if (poller) {
@@ -335,10 +339,14 @@ __global__ __launch_bounds__(kRingBlock) void ring_kernel(RingArgs a) {
         // workgroup idled long enough for the epoch value to have come round again)
         uint32_t ser = cur_serial;
         const unsigned long long tn = __builtin_amdgcn_s_memrealtime();
+#ifndef NFDP_NO_SERIAL_ALIAS
         if (go && (epoch != w0_epoch || tn - w0_t > kEpochAliasTicks)) {
+#else   // latency attribution only (misses a set rewritten twice while idle)
+        if (go && epoch != w0_epoch) {
+#endif
           __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-          ser = __hip_atomic_load(&a.sets[(epoch & kEpochSetBit) >> 1].serial, __ATOMIC_RELAXED,
-                                  __HIP_MEMORY_SCOPE_AGENT);
+          ser = __hip_atomic_load(&a.st->set_serial[(epoch & kEpochSetBit) >> 1], __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT);   // (device mirror: no PCIe round trip)
         }
         w0_epoch = epoch;
         w0_t = tn;
@@ -353,7 +361,11 @@ __global__ __launch_bounds__(kRingBlock) void ring_kernel(RingArgs a) {
       if (!ring_wait_chunk(a, qctl, qst, lane, t_begin, tk, epoch, gen, on_idle)) break;
     }
     const unsigned long long t_avail = __builtin_amdgcn_s_memrealtime();
+#ifndef NFDP_NO_ALIAS_FENCE
     if (epoch != seen_epoch || t_avail - seen_t > kEpochAliasTicks) {
+#else   // latency attribution only (stale table lines after 32 idle epoch changes)
+    if (epoch != seen_epoch) {
+#endif
       // A new epoch: the host rewrote a table this kernel reads with ordinary cached loads (the
       // flow-table copy it now names, the table set, or the MAC table after learning).  The
       // lines this wave's CU L1 and its XCD's L2 still hold may be stale - this grid never sees
@@ -675,6 +687,11 @@ void RingEngine::start(const FusedLaunch& f, const LaunchCfg& cfg, double deadli
   if (!(deadline_s > 0.0) || deadline_s > 3600.0) throw std::invalid_argument("ring: deadline in (0, 3600] s");
   if ((uint64_t)cfg.num_cus * (uint64_t)wgs_ < nq_) throw std::invalid_argument("ring: fewer workgroups than queues");
   const uint32_t ep = epoch();
+  launch_ = f;
+  // coop rings: the session's tables are table set (epoch bit 1); the LDS layout holds up to
+  // kLdsAclTiles rule tiles, so a later set with more tiles than that needs a relaunch
+  lds_tiles_ = coop_ ? std::max<uint32_t>(f.acl_tiles, kLdsAclTiles) : f.acl_tiles;
+  if (coop_) stage_tables(f, (int)((ep & kEpochSetBit) >> 1));   // (before the state upload: its serial)
   // resume at the published positions: tickets restart at prod/64, nothing outstanding
   std::vector<RingDevState> s(nq_);
   for (uint32_t q = 0; q < nq_; ++q) {
@@ -685,14 +702,11 @@ void RingEngine::start(const FusedLaunch& f, const LaunchCfg& cfg, double deadli
     s[q].dprod = ring_word(p, ep);
     __atomic_store_n(&ctl_[q].prod, ring_word(p, ep), __ATOMIC_RELEASE);
   }
+  s[0].set_serial[0] = h_sets_[0].serial;
+  s[0].set_serial[1] = h_sets_[1].serial;
   if (!stream_) ck(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "stream");
   ck(hipMemcpyAsync(st_, s.data(), sizeof(RingDevState) * nq_, hipMemcpyHostToDevice, stream_), "state upload");
   ck(hipStreamSynchronize(stream_), "state upload");  // `s` lives on this stack frame
-  launch_ = f;
-  // coop rings: the session's tables are table set (epoch bit 1); the LDS layout holds up to
-  // kLdsAclTiles rule tiles, so a later set with more tiles than that needs a relaunch
-  lds_tiles_ = coop_ ? std::max<uint32_t>(f.acl_tiles, kLdsAclTiles) : f.acl_tiles;
-  if (coop_) stage_tables(f, (int)((ep & kEpochSetBit) >> 1));
   RingLaunch r;
   r.f = f;
   r.sets = d_sets_;
@@ -910,6 +924,11 @@ void RingEngine::stage_tables(const FusedLaunch& f, int which) {
   std::memcpy(static_cast<void*>(h_sets_ + which), &ts, sizeof(ts));
   std::atomic_thread_fence(std::memory_order_release);
   if (running_) {
+    // the serial's device mirror, through the running grid, before any flip can name this set
+    const uint64_t seq = post_ctrl(reinterpret_cast<uint64_t>(&st_[0].set_serial[which]), &ts.serial, 1, 1.0);
+    if (!wait_ctrl(seq, 1.0)) throw std::runtime_error("ring: table-set serial not applied by the grid");
+  }
+  if (running_) {
     // the side pass (RingPath.side_pass) reads the session's tables from launch()
     launch_.t = f.t;
     launch_.acl_wfrag = f.acl_wfrag; launch_.acl_cinit = f.acl_cinit; launch_.acl_tiles = f.acl_tiles;
@@ -953,6 +972,10 @@ uint64_t RingEngine::post_write(uint64_t dst, const uint32_t* data, uint32_t n, 
       ok = ok || (dst >= r.first && dst + 4ull * n <= r.first + r.second);
   }
   if (!ok) throw std::invalid_argument("ring: control write outside the registered table buffers");
+  return post_ctrl(dst, data, n, timeout_s);
+}
+
+uint64_t RingEngine::post_ctrl(uint64_t dst, const uint32_t* data, uint32_t n, double timeout_s) {
   if (!running_) throw std::runtime_error("ring: control write with no grid running");
   std::lock_guard<std::mutex> g(ctrl_mu_);
   const auto t0 = Clock::now();
