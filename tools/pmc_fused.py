@@ -17,6 +17,8 @@ dp = DataPlane(device="cuda", flow_buckets=1 << 19, hash_mode="lds", acl_mode="m
 sc = S.build_sfc(dp, n_pods=8, n_flows=1 << 20, n_acl=min(ACL, 256), seed=0)
 if ACL > 256:
     S.add_acl_rules(dp, ACL)
+if os.environ.get("PMC_WILD"):   # the bench's ClassBench-style set instead (acl_wild variant)
+    S.install_acl_wild(dp, 1024)
 dp.commit(full=True)
 pk, im = S.traffic(sc, 1 << 22, seed=1)
 pk, im = torch.from_numpy(pk).cuda(), torch.from_numpy(im.view(np.int32)).cuda()
