@@ -81,6 +81,9 @@ NFDP_HD int acl_rule_of(uint32_t b, uint32_t n_acl) {
 #ifndef NFDP_PIPE_PF
 #define NFDP_PIPE_PF 1   // r3 s15 A/B: tile prefilters cost the ClassBench set 41 % (1.95 vs 1.38 ms)
 #endif
+#ifndef NFDP_ACL_LOOKAHEAD
+#define NFDP_ACL_LOOKAHEAD 1   // r4 s25 A/B: ClassBench-style set +5.5 % (7.17 -> 7.56 Gpps) over no lookahead
+#endif
 #ifndef NFDP_PIPE_UNROLL
 #define NFDP_PIPE_UNROLL 1   // r3 s16 A/B: ACL1024 0.3145 vs 0.3211 ms, ClassBench unchanged
 #endif
@@ -222,8 +225,13 @@ __device__ __forceinline__ void classify_wave(const FlowKey& key, uint4* kx, con
       }
 #pragma unroll
       for (int tt = 0; tt < 4; ++tt) {
-        best[tt] = min(best[tt], min(min(__float_as_uint(acc[tt][0]), __float_as_uint(acc[tt][1])),
-                                     min(__float_as_uint(acc[tt][2]), __float_as_uint(acc[tt][3]))));
+        if constexpr (PIPE) {   // (2-wave instances) two 3-input minima, the running minimum first
+          const uint32_t m = min(min(best[tt], __float_as_uint(acc[tt][0])), __float_as_uint(acc[tt][1]));
+          best[tt] = min(min(m, __float_as_uint(acc[tt][2])), __float_as_uint(acc[tt][3]));
+        } else {   // (4-wave instances at the register cap: the form their allocation was tuned with)
+          best[tt] = min(best[tt], min(min(__float_as_uint(acc[tt][0]), __float_as_uint(acc[tt][1])),
+                                       min(__float_as_uint(acc[tt][2]), __float_as_uint(acc[tt][3]))));
+        }
       }
     };
     // Straight-line form for batches (PIPE): the MFMAs always issue; `dead` (wave-uniform, all
@@ -277,8 +285,23 @@ __device__ __forceinline__ void classify_wave(const FlowKey& key, uint4* kx, con
         if (PIPE && NFDP_PIPE_PF < 2 && tstep == 1 && t_end - t_beg == kAclGroup) {
           // a whole group with no tile prefilter: straight-line, so the fragment reads of later
           // tiles issue under the MFMAs of earlier ones
+          // (NFDP_ACL_LOOKAHEAD tiles' fragments are read ahead of the tile whose MFMAs issue, so
+          // the LDS latency runs under them instead of in front of every tile)
+          constexpr uint32_t LA = NFDP_ACL_LOOKAHEAD;
+          v4i ab[LA + 1], cb[LA + 1];
 #pragma unroll
-          for (uint32_t k = 0; k < kAclGroup; ++k) run_tile(av.lw[(t_beg + k) * 64 + lane], av.lc[(t_beg + k) * 4 + g]);
+          for (uint32_t k = 0; k < LA; ++k) {
+            ab[k] = av.lw[(t_beg + k) * 64 + lane];
+            cb[k] = av.lc[(t_beg + k) * 4 + g];
+          }
+#pragma unroll
+          for (uint32_t k = 0; k < kAclGroup; ++k) {
+            if (k + LA < kAclGroup) {
+              ab[(k + LA) % (LA + 1)] = av.lw[(t_beg + k + LA) * 64 + lane];
+              cb[(k + LA) % (LA + 1)] = av.lc[(t_beg + k + LA) * 4 + g];
+            }
+            run_tile(ab[k % (LA + 1)], cb[k % (LA + 1)]);
+          }
           continue;
         }
 #endif
