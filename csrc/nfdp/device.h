@@ -84,9 +84,6 @@ NFDP_HD int acl_rule_of(uint32_t b, uint32_t n_acl) {
 #ifndef NFDP_ACL_LOOKAHEAD
 #define NFDP_ACL_LOOKAHEAD 1   // r4 s25 A/B: ClassBench-style set +5.5 % (7.17 -> 7.56 Gpps) over no lookahead
 #endif
-#ifndef NFDP_ACL_DEFER_MIN
-#define NFDP_ACL_DEFER_MIN 0
-#endif
 #ifndef NFDP_PIPE_UNROLL
 #define NFDP_PIPE_UNROLL 1   // r3 s16 A/B: ACL1024 0.3145 vs 0.3211 ms, ClassBench unchanged
 #endif
@@ -237,24 +234,6 @@ __device__ __forceinline__ void classify_wave(const FlowKey& key, uint4* kx, con
         }
       }
     };
-    // The same split in two (PIPE unrolled groups): a tile's MFMAs, and later its minima, so the
-    // next tile's MFMAs issue while this tile's results drain (NFDP_ACL_DEFER_MIN)
-    auto mfma_tile = [&](const v4i& a4, const v4i& ci, v4f_t (&acc)[4]) {
-      const v8i_t a = {a4[0], a4[1], a4[2], a4[3], 0, 0, 0, 0};
-      const v4f_t c = {__int_as_float(ci[0]), __int_as_float(ci[1]), __int_as_float(ci[2]), __int_as_float(ci[3])};
-#pragma unroll
-      for (int tt = 0; tt < 4; ++tt) {
-        const v8i_t b = {bq[tt][0], bq[tt][1], bq[tt][2], bq[tt][3], 0, 0, 0, 0};
-        acc[tt] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 4, 4, 0, kE8M0Idx, 0, kE8M0One);
-      }
-    };
-    auto min_tile = [&](const v4f_t (&acc)[4]) {
-#pragma unroll
-      for (int tt = 0; tt < 4; ++tt) {
-        const uint32_t m = min(min(best[tt], __float_as_uint(acc[tt][0])), __float_as_uint(acc[tt][1]));
-        best[tt] = min(min(m, __float_as_uint(acc[tt][2])), __float_as_uint(acc[tt][3]));
-      }
-    };
     // Straight-line form for batches (PIPE): the MFMAs always issue; `dead` (wave-uniform, all
     // ones for an empty batch slot) turns the tile's result into "no match".
     auto run_tile_m = [&](const v4i& a4, const v4i& ci, uint32_t dead) {
@@ -315,25 +294,14 @@ __device__ __forceinline__ void classify_wave(const FlowKey& key, uint4* kx, con
             ab[k] = av.lw[(t_beg + k) * 64 + lane];
             cb[k] = av.lc[(t_beg + k) * 4 + g];
           }
-#if NFDP_ACL_DEFER_MIN
-          v4f_t acc2[2][4];
-#endif
 #pragma unroll
           for (uint32_t k = 0; k < kAclGroup; ++k) {
             if (k + LA < kAclGroup) {
               ab[(k + LA) % (LA + 1)] = av.lw[(t_beg + k + LA) * 64 + lane];
               cb[(k + LA) % (LA + 1)] = av.lc[(t_beg + k + LA) * 4 + g];
             }
-#if NFDP_ACL_DEFER_MIN
-            mfma_tile(ab[k % (LA + 1)], cb[k % (LA + 1)], acc2[k & 1]);
-            if (k > 0) min_tile(acc2[(k - 1) & 1]);
-#else
             run_tile(ab[k % (LA + 1)], cb[k % (LA + 1)]);
-#endif
           }
-#if NFDP_ACL_DEFER_MIN
-          min_tile(acc2[(kAclGroup - 1) & 1]);
-#endif
           continue;
         }
 #endif
