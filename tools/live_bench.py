@@ -199,11 +199,14 @@ def run(device: str = "cuda", n_pods: int = 8, flows: int = 1 << 20, n_acl: int 
         out.update(idle_p50_us=_pct(r1["lat_us"], 50), idle_p99_us=_pct(r1["lat_us"], 99),
                    idle_frames=int(r1["received"]))
         drain(nf, pods, stats)
-        # offered loads below saturation: 90 % and 50 % of the measured maximum
+        # offered loads below saturation: 90 % and 50 % of the measured maximum (of frames IN: with
+        # broadcast every frame sent comes out as several delivered copies)
+        fan = (r["received"] / r["sent"]) if (traffic == "broadcast" and r["sent"]) else 1.0
+        out["copies_per_frame"] = round(fan, 2)
         if mpps > 0:
             for tag, frac in (("load90", 0.9), ("half", 0.5)):
                 r2 = nf.trafgen_run(pods, duration_s=min(duration, 0.5), warmup_s=0.1, threads=threads, burst=8,
-                                    rate_pps=frac * mpps * 1e6)
+                                    rate_pps=frac * mpps / max(fan, 1.0) * 1e6)
                 out.update({f"{tag}_mpps": round(r2["received"] / min(duration, 0.5) / 1e6, 3),
                             f"{tag}_p50_us": _pct(r2["lat_us"], 50), f"{tag}_p99_us": _pct(r2["lat_us"], 99)})
                 drain(nf, pods, stats)
