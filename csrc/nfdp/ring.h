@@ -133,6 +133,7 @@ struct alignas(128) RingDevState {
 // mailbox that the SoC polls (octep_ctrl_mbox.c / loop.c), with the GPU as the SoC.
 constexpr uint32_t kCtrlSlots = 64;
 constexpr uint32_t kCtrlWords = 12;
+constexpr uint32_t kCtrlNoRestage = 1u << 31;   // RingCtrlEntry.nwords flag: the target is not in any LDS copy
 struct alignas(64) RingCtrlEntry {
   uint64_t dst;               // device address of the first dword (4-B aligned)
   uint32_t nwords;            // 1..kCtrlWords
@@ -248,7 +249,8 @@ class RingEngine {
   // mailbox stays full for `timeout_s`.
   uint64_t post_write(uint64_t dst, const uint32_t* data, uint32_t n, double timeout_s = 1.0);
  private:
-  uint64_t post_ctrl(uint64_t dst, const uint32_t* data, uint32_t n, double timeout_s);   // (no region check)
+  // (no region check; restage = false: the grid's LDS copies do not hold the target)
+  uint64_t post_ctrl(uint64_t dst, const uint32_t* data, uint32_t n, double timeout_s, bool restage = true);
  public:
   uint64_t ctrl_posted() const { return ctrl_head_; }
   // Device buffers control writes may target ([base, bytes) each: the running table set's small

@@ -288,14 +288,15 @@ __global__ __launch_bounds__(kRingBlock) void ring_kernel(RingArgs a) {
   auto poll_ctrl = [&]() {   // EXEC full; every lane reads the same words (one request per wave)
     const unsigned long long h = __hip_atomic_load(&a.ctrl->head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     const unsigned long long n0 = ctrl_n;
-    bool moved = false;
+    bool moved = false, restage = false;
     while (__builtin_amdgcn_readfirstlane((uint32_t)(ctrl_n < h && ctrl_n - n0 < kCtrlSlots))) {
       RingCtrlEntry* ent = a.ctrl->e + (ctrl_n % kCtrlSlots);
       const uint32_t sq = __hip_atomic_load(&ent->seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
       if (__builtin_amdgcn_readfirstlane(sq) != (uint32_t)(ctrl_n + 1)) break;   // not visible yet: next poll
       const unsigned long long dst64 = __hip_atomic_load(&ent->dst, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       const uint32_t nw = __hip_atomic_load(&ent->nwords, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      const uint32_t n = min(nw, kCtrlWords);
+      const uint32_t n = min(nw & ~kCtrlNoRestage, kCtrlWords);
+      restage = restage || !(nw & kCtrlNoRestage);
       if (lane < n) {
         const uint32_t v = __hip_atomic_load(&ent->data[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         __hip_atomic_store(reinterpret_cast<uint32_t*>(dst64) + lane, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -310,7 +311,8 @@ __global__ __launch_bounds__(kRingBlock) void ring_kernel(RingArgs a) {
     // the writes reach every XCD before the generation moves; then the host hears it
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     if (lane == 0) {
-      __hip_atomic_fetch_add(&a.st->ctl_gen, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      // (writes that no LDS copy holds - the table-set serial mirror - leave the copies alone)
+      if (restage) __hip_atomic_fetch_add(&a.st->ctl_gen, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(&a.ctrl->done, ctrl_n, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   };
@@ -925,7 +927,7 @@ void RingEngine::stage_tables(const FusedLaunch& f, int which) {
   std::atomic_thread_fence(std::memory_order_release);
   if (running_) {
     // the serial's device mirror, through the running grid, before any flip can name this set
-    const uint64_t seq = post_ctrl(reinterpret_cast<uint64_t>(&st_[0].set_serial[which]), &ts.serial, 1, 1.0);
+    const uint64_t seq = post_ctrl(reinterpret_cast<uint64_t>(&st_[0].set_serial[which]), &ts.serial, 1, 1.0, false);
     if (!wait_ctrl(seq, 1.0)) throw std::runtime_error("ring: table-set serial not applied by the grid");
   }
   if (running_) {
@@ -975,7 +977,7 @@ uint64_t RingEngine::post_write(uint64_t dst, const uint32_t* data, uint32_t n, 
   return post_ctrl(dst, data, n, timeout_s);
 }
 
-uint64_t RingEngine::post_ctrl(uint64_t dst, const uint32_t* data, uint32_t n, double timeout_s) {
+uint64_t RingEngine::post_ctrl(uint64_t dst, const uint32_t* data, uint32_t n, double timeout_s, bool restage) {
   if (!running_) throw std::runtime_error("ring: control write with no grid running");
   std::lock_guard<std::mutex> g(ctrl_mu_);
   const auto t0 = Clock::now();
@@ -985,7 +987,7 @@ uint64_t RingEngine::post_ctrl(uint64_t dst, const uint32_t* data, uint32_t n, d
   }
   RingCtrlEntry& e = ctrl_->e[ctrl_head_ % kCtrlSlots];
   e.dst = dst;
-  e.nwords = n;
+  e.nwords = n | (restage ? 0u : kCtrlNoRestage);
   std::memcpy(e.data, data, 4ull * n);
   __atomic_store_n(&e.seq, (uint32_t)(ctrl_head_ + 1), __ATOMIC_RELEASE);
   ++ctrl_head_;
