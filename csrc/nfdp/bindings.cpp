@@ -824,7 +824,8 @@ PYBIND11_MODULE(_nfdp, m) {
         b.configure(t, reinterpret_cast<uint64_t*>(flow_ctr), reinterpret_cast<uint64_t*>(port_ctr),
                     reinterpret_cast<uint64_t*>(drop_ctr), const_cast<MacEntry*>(t.macs), t.mac_mask);
       })
-      .def("set_frame_addrs", &OracleBackend::set_frame_addrs, py::arg("on"));
+      .def("set_frame_addrs", &OracleBackend::set_frame_addrs, py::arg("on"))
+      .def("set_completion_gate", &OracleBackend::set_completion_gate, py::arg("on"));
   py::class_<WireBackend, OracleBackend, std::shared_ptr<WireBackend>>(m, "WireBackend")
       .def(py::init<uint32_t, uint32_t, const std::vector<std::pair<uint64_t, uint32_t>>&>(), py::arg("capacity"),
            py::arg("queues"), py::arg("mac_to_port"));

@@ -1103,6 +1103,7 @@ void Engine::rx_loop(Queue* Q) {
         }
         for (uint32_t i = k; i < npad; ++i) im[(start + i) & cmask] = kRingPadMeta;
         b.side = side;
+        b.cfg = csnap.p;   // (one refcount per burst: the snapshot this burst's tables belong to)
         b.pkts.swap(L->stage);
         L->stage.clear();
         b.id = head;
@@ -1322,6 +1323,7 @@ void Engine::finish(Queue* Q, Lane* L, Burst& b) {
   b.reps.clear();
   b.xhdr.clear();
   b.has_x.clear();
+  b.cfg.reset();
   L->freed_pos.store(b.end, std::memory_order_release);
   b.state.store(0, std::memory_order_release);
   L->done.fetch_add(1, std::memory_order_release);
@@ -1359,7 +1361,7 @@ void Engine::tx_loop(Queue* Q, uint32_t w) {
             continue;
           }
           waiting[li] = 0;
-          const Cfg* c = &cfg_of(csnap);
+          const Cfg* c = b.cfg ? b.cfg.get() : &cfg_of(csnap);
           bool side = b.side;
           if (!side) {
             const uint32_t* om = L->be->out_meta(Q->id);
@@ -1373,7 +1375,7 @@ void Engine::tx_loop(Queue* Q, uint32_t w) {
           deliver(Q, L, b, w, *c, ports_of(psnap), sc);
           st.add(st.deliver_ns, now_ns() - td0);
         } else {
-          const Cfg& c = cfg_of(csnap);
+          const Cfg& c = b.cfg ? *b.cfg : cfg_of(csnap);
           const uint64_t td0 = now_ns();
           deliver(Q, L, b, w, c, ports_of(psnap), sc);
           st.add(st.deliver_ns, now_ns() - td0);

@@ -371,8 +371,13 @@ class OracleBackend : public Backend {
   const uint32_t* out_meta(uint32_t q) override { return om_.data() + (size_t)q * cap_; }
   uint64_t published(uint32_t q) override { return prod_[q].load(std::memory_order_acquire); }
   uint64_t publish(uint32_t q, uint32_t n) override;
-  bool range_done(uint32_t q, uint64_t, uint64_t end) override { return end <= published(q); }
+  bool range_done(uint32_t q, uint64_t, uint64_t end) override {
+    return !gate_.load(std::memory_order_acquire) && end <= published(q);
+  }
   bool ready() override { return configured_.load(); }
+  // Test hook: while set, published bursts are processed but never reported complete (they stay
+  // in flight, as on a busy GPU), so a test can change the configuration under them.
+  void set_completion_gate(bool on) { gate_.store(on, std::memory_order_release); }
   void apply_learn(const uint32_t* ev, uint32_t n, uint32_t stamp) override;
   // tables / counters of the CPU DataPlane (replaced after every commit, while the engine is paused)
   void configure(const TablesView& t, uint64_t* flow_ctr, uint64_t* port_ctr, uint64_t* drop_ctr, MacEntry* macs,
@@ -393,6 +398,7 @@ class OracleBackend : public Backend {
   std::vector<uint64_t> fa_;   // zero-copy: per-slot frame addresses (empty: off)
   std::unique_ptr<std::atomic<uint64_t>[]> prod_;
   std::atomic<bool> configured_{false};
+  std::atomic<bool> gate_{false};
   std::mutex run_mu_;   // the pipeline's counters / MAC table are shared by every queue
   bool serial_ = true;  // queues run one at a time (run_mu_)
   TablesView t_{};
@@ -500,6 +506,22 @@ class Engine {
   }
 
  private:
+  struct PortRef { std::shared_ptr<Port> p; uint32_t q = 0; };
+  using PortTab = std::vector<PortRef>;
+  struct Steer {
+    std::vector<PortEntry> ports;
+    std::vector<uint8_t> rss_key;
+    bool v6 = false;
+    ToeplitzTab hash;
+    std::vector<uint32_t> port_owner;   // port placement (empty: flow owners)
+  };
+  struct Cfg {                   // everything the packet threads read from the control plane
+    std::vector<uint32_t> redirect;      // tunnel port -> underlay port (0xFFFFFFFF: none)
+    std::vector<uint8_t> side_ports;     // ingress ports with side work
+    bool side_always = false;
+    std::shared_ptr<const Steer> steer;
+    std::vector<std::shared_ptr<SideTables>> side;   // per backend
+  };
   struct Pkt { uint32_t port; uint32_t seq; const uint8_t* data; uint32_t len; Port* holder; };
   struct Burst {
     uint64_t id = ~0ull;   // burst number on its lane (slot = id % inflight)
@@ -510,6 +532,10 @@ class Engine {
     std::vector<Replica> reps;          // side-pass output for this burst
     std::vector<uint8_t> xhdr;          // per packet kXhdrBytes outer-header record (tunnels)
     std::vector<uint8_t> has_x;         // per packet: xhdr record present
+    // the configuration (side tables, redirects, side ports) current when the burst was
+    // published: its side pass and delivery use the tables its pipeline epoch used, even when a
+    // commit swaps the engine's configuration while the burst is in flight
+    std::shared_ptr<const Cfg> cfg;
     std::atomic<uint32_t> state{0};   // 0 free, 1 published, 2 ready to deliver (completed + side done)
     std::atomic<uint32_t> left{0};    // delivery workers still working on it
   };
@@ -542,22 +568,6 @@ class Engine {
     std::atomic<uint32_t> nports{0};
     std::mutex lat_mu;           // rx -> tx time per burst, this queue's samples
     std::vector<double> lat_us;
-  };
-  struct PortRef { std::shared_ptr<Port> p; uint32_t q = 0; };
-  using PortTab = std::vector<PortRef>;
-  struct Steer {
-    std::vector<PortEntry> ports;
-    std::vector<uint8_t> rss_key;
-    bool v6 = false;
-    ToeplitzTab hash;
-    std::vector<uint32_t> port_owner;   // port placement (empty: flow owners)
-  };
-  struct Cfg {                   // everything the packet threads read from the control plane
-    std::vector<uint32_t> redirect;      // tunnel port -> underlay port (0xFFFFFFFF: none)
-    std::vector<uint8_t> side_ports;     // ingress ports with side work
-    bool side_always = false;
-    std::shared_ptr<const Steer> steer;
-    std::vector<std::shared_ptr<SideTables>> side;   // per backend
   };
   struct TxTally { uint64_t tx = 0, full = 0, no_port = 0, drop = 0, reps = 0; };
   struct TxScratch {            // per tx worker

@@ -32,6 +32,8 @@ def _load(name: str, autobuild: bool = True):
         import torch  # noqa: F401
     except ImportError:
         pass
+    if not variant:
+        _check_provenance(name, autobuild and not os.environ.get("NFDP_NO_AUTOBUILD"))
     try:
         mod = importlib.import_module(name)
     except ImportError:
@@ -43,6 +45,47 @@ def _load(name: str, autobuild: bool = True):
         mod = importlib.import_module(name)
     _cache[name] = mod
     return mod
+
+
+class StaleExtensionError(ImportError):
+    """The built module's embedded source digest is not the digest of the sources in the tree."""
+
+
+def _check_provenance(name: str, autobuild: bool) -> None:
+    """Refuse (or, when building is allowed, rebuild) a module not built from the sources at hand.
+
+    The digest compiled into the ``.so`` (native/build.py ``source_digest``) must equal the digest
+    of csrc/ as it is now.  Without csrc/ (an installed package) there is nothing to compare."""
+    from . import build
+
+    spec = build.MODULES[name]
+    if not all((spec["dir"] / s).exists() for s in spec["sources"]):
+        return
+    so = _HERE / f"{name}{build.EXT}"
+    if not so.exists():
+        return                       # the import below builds it (or fails loudly)
+    want = build.source_digest(name)
+    have = build.embedded_digest(so)
+    if have == want:
+        return
+    if autobuild:
+        build.build_module(name)
+        if build.embedded_digest(so) == want:
+            return
+    raise StaleExtensionError(
+        f"{so.name} was built from other sources (embedded digest {have or 'none'}, csrc/ digest {want[:16]}...): "
+        f"rebuild with `python -m dpu_operator_amd.native.build`")
+
+
+def provenance() -> dict:
+    """{module: {"built": embedded digest, "sources": digest of csrc/ now}} (bench / reports)."""
+    from . import build
+
+    out = {}
+    for name in build.MODULES:
+        so = _HERE / f"{name}{build.EXT}"
+        out[name] = {"built": build.embedded_digest(so), "sources": build.source_digest(name)}
+    return out
 
 
 def nfdp():

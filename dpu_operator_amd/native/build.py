@@ -7,7 +7,14 @@ the repository snapshot to the GPU box:
   ``--offload-arch=gfx950``).
 * ``_agent`` — C++ host<->device control mailbox and control-plane agent (g++/hipcc host code).
 
-Incremental: an object is rebuilt when its source or any header in its directory is newer.
+Incremental by content: an object is rebuilt when the hash of its source, the local headers it
+includes (transitively) and its compile flags differs from the one recorded next to it.
+
+Provenance: every module carries a digest of the exact sources it was built from (``source_digest``:
+sources + their local headers + experiment flags), compiled into a marker string
+(``DPUSRCDIGEST:<hex>``).  The loader (``native/__init__.py``) reads the marker out of the ``.so``
+before importing it and refuses a binary whose digest is not the one of the sources in the tree,
+so a stale extension cannot pass a GPU test silently.
 Usage: ``python -m dpu_operator_amd.native.build [-v] [--force]``.
 """
 from __future__ import annotations
@@ -78,12 +85,11 @@ def _newest_header(d: Path) -> float:
     return max(ts) if ts else 0.0
 
 
-def _newest_dep(src: Path) -> float:
-    """mtime of the newest local header `src` includes (transitively, `#include "x.h"` lines):
-    a header edit rebuilds only the sources that see it."""
+def _deps(src: Path) -> list[Path]:
+    """Local headers `src` includes (transitively, `#include "x.h"` lines), sorted."""
     import re
 
-    seen, todo, newest = set(), [src], 0.0
+    seen, todo = set(), [src]
     while todo:
         f = todo.pop()
         try:
@@ -95,9 +101,65 @@ def _newest_dep(src: Path) -> float:
             if h in seen or not h.exists():
                 continue
             seen.add(h)
-            newest = max(newest, h.stat().st_mtime)
             todo.append(h)
-    return newest
+    return sorted(seen)
+
+
+def _hash_files(files, extra: str = "") -> str:
+    import hashlib
+
+    h = hashlib.sha256()
+    for f in files:
+        h.update(f.name.encode() + b"\0" + f.read_bytes() + b"\0")
+    h.update(extra.encode())
+    return h.hexdigest()
+
+
+def _hip_flags() -> str:
+    return os.environ.get("NFDP_HIPCC_FLAGS", "").strip()
+
+
+def source_digest(name: str) -> str:
+    """Digest of everything a module is compiled from: its sources, the local headers they
+    include and the experiment flags (hip modules).  Embedded in the module at link time."""
+    spec = MODULES[name]
+    d: Path = spec["dir"]
+    files = set()
+    for s in spec["sources"]:
+        files.add((d / s).resolve())
+        files.update(_deps(d / s))
+    return _hash_files(sorted(files), _hip_flags() if spec["hip"] else "")
+
+
+DIGEST_MARKER = b"DPUSRCDIGEST:"
+
+
+def embedded_digest(so: Path) -> str | None:
+    """The source digest compiled into a built module (None: no marker, a pre-provenance build)."""
+    try:
+        data = Path(so).read_bytes()
+    except OSError:
+        return None
+    i = data.find(DIGEST_MARKER)
+    if i < 0:
+        return None
+    return data[i + len(DIGEST_MARKER): i + len(DIGEST_MARKER) + 64].decode("ascii", "replace")
+
+
+def _digest_object(name: str, digest: str, verbose: bool) -> Path:
+    """A one-symbol object carrying the digest marker, linked into the module."""
+    src = BUILD / name / "src_digest.cpp"
+    obj = BUILD / name / "src_digest.cpp.o"
+    text = (f'extern "C" __attribute__((visibility("default"), used)) const char dpu_{name.strip("_")}_src_digest[] = '
+            f'"{DIGEST_MARKER.decode()}{digest}";\n')
+    src.parent.mkdir(parents=True, exist_ok=True)
+    if not obj.exists() or not src.exists() or src.read_text() != text:
+        src.write_text(text)
+        cmd = [shutil.which("g++") or "g++", "-fPIC", "-c", str(src), "-o", str(obj)]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        subprocess.run(cmd, check=True, capture_output=True)
+    return obj
 
 
 # HIP sources whose kernels' register / spill / occupancy figures are recorded at build time
@@ -153,17 +215,17 @@ def _compile(src: Path, obj: Path, hip: bool, verbose: bool) -> None:
         print(err, file=sys.stderr)
 
 
-def _flags_changed(name: str, hip: bool) -> bool:
-    """True when the experiment flags differ from the ones the objects were built with (the
-    stamp is rewritten), so an NFDP_HIPCC_FLAGS build never survives into a default build."""
-    flags = os.environ.get("NFDP_HIPCC_FLAGS", "").strip() if hip else ""
-    stamp = BUILD / name / "flags.stamp"
-    old = stamp.read_text() if stamp.exists() else None
-    if old == flags:
-        return False
-    stamp.parent.mkdir(parents=True, exist_ok=True)
-    stamp.write_text(flags)
-    return True
+def _obj_hash(src: Path, hip: bool) -> str:
+    return _hash_files([src.resolve(), *_deps(src)], ("hip:" + _hip_flags()) if hip else "cxx")
+
+
+def _stale(src: Path, obj: Path, hip: bool, force: bool) -> str | None:
+    """None when `obj` was built from exactly this content, else the hash to record after building."""
+    h = _obj_hash(src, hip)
+    stamp = obj.with_name(obj.name + ".hash")
+    if force or not obj.exists() or not stamp.exists() or stamp.read_text() != h:
+        return h
+    return None
 
 
 def build_module(name: str, force: bool = False, verbose: bool = False) -> Path:
@@ -171,21 +233,26 @@ def build_module(name: str, force: bool = False, verbose: bool = False) -> Path:
     d: Path = spec["dir"]
     out = (Path(VARIANT_OUT) if VARIANT_OUT else HERE) / f"{name}{EXT}"
     out.parent.mkdir(parents=True, exist_ok=True)
-    force = _flags_changed(name, spec["hip"]) or force
     objs = []
     jobs = []
     for s in spec["sources"]:
         src = d / s
         obj = BUILD / name / (s + ".o")
         objs.append(obj)
-        stale = force or not obj.exists() or obj.stat().st_mtime < max(src.stat().st_mtime, _newest_dep(src))
-        if stale:
-            jobs.append((src, obj))
+        h = _stale(src, obj, spec["hip"], force)
+        if h is not None:
+            jobs.append((src, obj, h))
+
+    def run(j):
+        _compile(j[0], j[1], spec["hip"], verbose)
+        j[1].with_name(j[1].name + ".hash").write_text(j[2])
+
     if jobs:
         with cf.ThreadPoolExecutor(max_workers=min(len(jobs), 4)) as ex:
-            list(ex.map(lambda j: _compile(j[0], j[1], spec["hip"], verbose), jobs))
-    newest_obj = max(o.stat().st_mtime for o in objs)
-    if force or jobs or not out.exists() or out.stat().st_mtime < newest_obj:
+            list(ex.map(run, jobs))
+    digest = source_digest(name)
+    objs.append(_digest_object(name, digest, verbose))
+    if force or jobs or not out.exists() or embedded_digest(out) != digest:
         if spec["hip"]:
             cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", str(out)]
         else:
@@ -216,16 +283,17 @@ def build_exe(name: str, force: bool = False, verbose: bool = False) -> Path:
     """Link a standalone executable into dpu_operator_amd/native/bin/ (objects shared with the module)."""
     spec = EXES[name]
     d: Path = spec["dir"]
-    hdr = _newest_header(d)
     objs, jobs = [], []
     for s in spec["sources"]:
         src = d / s
         obj = BUILD / spec["module"] / (s + ".o")
         objs.append(obj)
-        if force or not obj.exists() or obj.stat().st_mtime < max(src.stat().st_mtime, hdr):
-            jobs.append((src, obj))
-    for src, obj in jobs:
+        h = _stale(src, obj, False, force)
+        if h is not None:
+            jobs.append((src, obj, h))
+    for src, obj, h in jobs:
         _compile(src, obj, False, verbose)
+        obj.with_name(obj.name + ".hash").write_text(h)
     out = HERE / "bin" / name
     out.parent.mkdir(exist_ok=True)
     if force or jobs or not out.exists() or out.stat().st_mtime < max(o.stat().st_mtime for o in objs):

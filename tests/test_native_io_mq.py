@@ -607,3 +607,45 @@ def test_live_soak_under_churn(shm, devices):
     finally:
         stop.set()
         live.stop()
+
+
+def test_bursts_in_flight_keep_their_publish_time_configuration(shm):
+    """A burst is side-passed and delivered with the configuration current when it was published
+    (iox Burst::cfg), not with whatever a commit swapped in while it was in flight: VXLAN-egress
+    bursts held in flight (the oracle's completion gate) while the tunnel redirects are cleared still
+    leave encapsulated on the underlay, byte for byte; bursts published afterwards follow the new map."""
+    nf = nfdp()
+    dp, sc, eg = _sfc(egress=True)
+    ref, _, _ = _sfc(egress=True)
+    slots, im = S.traffic(sc, 600, seed=7)
+    exp, _ = _expected(ref, slots, im)
+    und = eg["underlay"]
+    exp = {und: [f for v in exp.values() for f in v]}
+    paths = {int(p): str(shm / f"g{int(p)}") for p in list(sc.pod_port) + [und]}
+    live = NativeLivePath(dp, {p: MemifVport(paths[p], ring_size=4096) for p in paths}, burst=256,
+                          ring_capacity=2048, queues=1).start()
+    try:
+        be = live._backends[0]
+        be.set_completion_gate(True)
+        eps = _send_all(nf, paths, slots, im, [int(p) for p in sc.pod_port])
+        assert _until(lambda: live.stats["rx"] >= len(slots)), live.stats
+        assert _until(lambda: live.stats["bursts"] >= 1)
+        time.sleep(0.05)
+        assert live.stats["tx"] == 0                     # nothing completed: every burst in flight
+        live._eng.set_redirects([])                      # a commit's configuration swap, mid-flight
+        be.set_completion_gate(False)
+        got, done = _collect(eps, sum(map(len, exp.values())))
+        assert _until(done), (live.stats, live.error)
+        assert sorted(got[und]) == sorted(exp[und])
+        assert all(got[int(p)] == [] for p in sc.pod_port)
+        # published after the swap: no redirect, so the frames are delivered to the tunnel port
+        # itself (the pod), still with their outer header
+        eps[und].recv()
+        slots2, im2 = S.traffic(sc, 64, seed=8)
+        _send_all(nf, paths, slots2, im2, [int(p) for p in sc.pod_port])
+        got2, done2 = _collect(eps, 1)
+        assert _until(done2), (live.stats, live.error)
+        assert got2[und] == []
+        assert live.error is None
+    finally:
+        live.stop()
