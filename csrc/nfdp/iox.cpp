@@ -145,6 +145,13 @@ PacketPort::PacketPort(const std::string& ifname, uint32_t frames, uint32_t fram
   sll.sll_ifindex = (int)if_nametoindex(ifname.c_str());
   if (sll.sll_ifindex == 0) fail("if_nametoindex");
   if (bind(fd_, reinterpret_cast<sockaddr*>(&sll), sizeof(sll)) != 0) fail("bind");
+  // A bridge port sees every frame on its link, not only those for its own MAC: a NIC used as the
+  // uplink filters unicast in hardware otherwise.  Membership-based (reference counted by the
+  // kernel, dropped with the socket), so the netdev's own promiscuity setting is left alone.
+  packet_mreq mr{};
+  mr.mr_ifindex = sll.sll_ifindex;
+  mr.mr_type = PACKET_MR_PROMISC;
+  (void)setsockopt(fd_, SOL_PACKET, PACKET_ADD_MEMBERSHIP, &mr, sizeof(mr));
   vlan_copy_.resize((size_t)nframes_ * (fsize_ + 4));
 }
 

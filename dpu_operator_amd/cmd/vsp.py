@@ -46,7 +46,8 @@ def build_vsp(a, pm: PathManager):
                       state_dir=a.state_dir or cfg.vsp_state_dir or None, nl=nl, live=a.live,
                       live_engine=a.live_engine, gpus=a.gpus if a.gpus == "all" else int(a.gpus),
                       vport_kind=a.vport_kind or cfg.vport_kind, tx_workers=a.io_workers or cfg.io_workers,
-                      io_queues=a.io_queues or cfg.io_queues, placement=a.placement)
+                      io_queues=a.io_queues or cfg.io_queues, placement=a.placement,
+                      uplink=(a.uplink or cfg.uplink) if a.live else None)
     from ..cni.netlink import RtNetlink
     from ..platform.platform import SysfsPlatform
     from ..utils.cmdrunner import HostRunner
@@ -82,7 +83,7 @@ def build_vsp(a, pm: PathManager):
         from ..vsp import marvell as M
 
         ddp = M.DebugDataPlane() if a.debug_dp else M.GpuOvsDataPlane(
-            dataplane(), uplink_name=a.uplink, live_factory=live_path if a.live else None)
+            dataplane(), uplink_name=a.uplink or "rpm0", live_factory=live_path if a.live else None)
         return M.MarvellVsp(plat, nl, runner, ddp, pm, a.sys_root)
     if a.vendor == "netsec":
         from ..vsp.netsec import NetsecVsp
@@ -98,6 +99,26 @@ def build_vsp(a, pm: PathManager):
 
 
 def main(argv=None, stop: threading.Event | None = None) -> int:
+    a = parse_args(argv)
+    if a.node_config:
+        set_node_config(NodeConfig.load(a.node_config))
+    logging.basicConfig(level=logging.INFO)
+    vsp = build_vsp(a, PathManager(a.root)).start()
+    services = _extras(a, vsp)
+    stop = stop or threading.Event()
+    if threading.current_thread() is threading.main_thread():
+        signal.signal(signal.SIGTERM, lambda *_: stop.set())
+        signal.signal(signal.SIGINT, lambda *_: stop.set())
+    stop.wait()
+    if getattr(vsp, "journal", None) is not None:
+        vsp.checkpoint()  # clean shutdown: snapshot so the next start skips the replay
+    vsp.stop()
+    for svc in reversed(services):
+        svc.stop()
+    return 0
+
+
+def parse_args(argv=None):
     ap = argparse.ArgumentParser(prog="vsp")
     ap.add_argument("--vendor", default="amd-gpu", choices=["amd-gpu", "mock", "marvell", "netsec", "intel-ipu"])
     ap.add_argument("--root", default="/")
@@ -106,7 +127,9 @@ def main(argv=None, stop: threading.Event | None = None) -> int:
     ap.add_argument("--flow-buckets", type=int, default=0, help="0 = node config (default 2^18)")
     ap.add_argument("--node-config", default="", help="node policy YAML (config.py); also DPU_NODE_CONFIG")
     ap.add_argument("--debug-dp", action="store_true")
-    ap.add_argument("--uplink", default="rpm0")
+    ap.add_argument("--uplink", default="",
+                    help="wire port: marvell: the RPM netdev (default rpm0); amd-gpu --live: 'veth' (a host-side "
+                         "veth pair), 'none' or an existing netdev (the node's data NIC); default: node config uplink")
     ap.add_argument("--p4rt-addr", default="127.0.0.1:9559")
     ap.add_argument("--acc-macs", default="")
     ap.add_argument("--mode", default="ipu")
@@ -133,23 +156,7 @@ def main(argv=None, stop: threading.Event | None = None) -> int:
     ap.add_argument("--agent-mbox", default="", help="amd-gpu: run the node control agent on this mailbox path")
     ap.add_argument("--agent-config", default="", help="agent SoC config file (default: one PF + --agent-vfs VFs)")
     ap.add_argument("--agent-vfs", type=int, default=8)
-    a = ap.parse_args(argv)
-    if a.node_config:
-        set_node_config(NodeConfig.load(a.node_config))
-    logging.basicConfig(level=logging.INFO)
-    vsp = build_vsp(a, PathManager(a.root)).start()
-    services = _extras(a, vsp)
-    stop = stop or threading.Event()
-    if threading.current_thread() is threading.main_thread():
-        signal.signal(signal.SIGTERM, lambda *_: stop.set())
-        signal.signal(signal.SIGINT, lambda *_: stop.set())
-    stop.wait()
-    if getattr(vsp, "journal", None) is not None:
-        vsp.checkpoint()  # clean shutdown: snapshot so the next start skips the replay
-    vsp.stop()
-    for svc in reversed(services):
-        svc.stop()
-    return 0
+    return ap.parse_args(argv)
 
 
 def _extras(a, vsp) -> list:

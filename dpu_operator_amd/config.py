@@ -40,6 +40,13 @@ class NodeConfig:
     vport_kind: str = "veth"           # veth (kernel netdev pods, AF_PACKET rings) | memif | tap
     io_queues: int = 4                 # native engine rx queues (threads), each with a ring queue per GPU
     io_workers: int = 2                # native engine delivery threads per queue (4 x 2: 57.9 Mpps, r4 s4)
+    # the GPU node's wire port (data-plane port `wire_port`, the reference's RPM / SFP uplink):
+    #   "veth"  a veth pair whose host end (`uplink_host_ifname`) the node's stack or a host bridge
+    #           with the physical NIC reaches pods through (an OvS internal port's role);
+    #   <name>  an existing netdev (the node's data NIC), attached through AF_PACKET rings;
+    #   "none"  no wire port (pods reach only each other and NF pods)
+    uplink: str = "veth"
+    uplink_host_ifname: str = "dpuwire"
     # daemon cadences (seconds)
     device_poll: float = 5.0           # ListAndWatch refresh (deviceplugin.go:109)
     detect_poll: float = 1.0           # platform detection (daemon.go:88)
@@ -84,6 +91,8 @@ class NodeConfig:
             raise ValueError("vport_kind is veth, memif or tap")
         if not 1 <= self.io_queues <= 64 or not 1 <= self.io_workers <= 16:
             raise ValueError("io_queues in [1, 64], io_workers in [1, 16]")
+        if not self.uplink or len(self.uplink) > 15 or not 1 <= len(self.uplink_host_ifname) <= 14:
+            raise ValueError("uplink is 'veth', 'none' or a netdev name; uplink_host_ifname at most 14 characters")
 
     def logical_bridge(self, vf: int) -> int:
         return vf + self.logical_bridge_offset

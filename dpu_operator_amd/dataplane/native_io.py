@@ -81,6 +81,12 @@ class PacketVport:
         nl.link_add_veth(name, peer)
         if mac:
             nl.link_set_hw_addr(name, mac)
+        # The engine re-sends every frame as a plain frame: whatever the pod's stack left for the
+        # hardware (checksum-partial UDP / TCP, TSO / GSO super-frames) would reach the next pod
+        # unfinished.  The pod end computes checksums and segments itself; the engine end takes no
+        # GRO aggregates.  (Features move with the netdev into the pod's namespace.)
+        set_offloads(name, tx_csum=False, sg=False, tso=False, gso=False)
+        set_offloads(peer, gro=False)
         _quiet_ipv6(peer)
         nl.link_set_up(peer)
         nl.link_set_up(name)
@@ -88,17 +94,58 @@ class PacketVport:
         vp._nl, vp.name = nl, name
         return vp
 
+    @classmethod
+    def attach(cls, ifname: str, frames: int = 4096) -> "PacketVport":
+        """An existing netdev as a data-plane port (the node's uplink NIC): opened through the same
+        AF_PACKET rings, promiscuous while the engine holds it (the socket's membership), with
+        receive offloads that would hand the engine super-frames (GRO) turned off."""
+        set_offloads(ifname, gro=False)
+        return cls(ifname, frames=frames)
+
     def make(self, nf, queues: int = 1):
         return nf.PacketPort(self.ifname, self.frames, self.frame_size)
 
     def close(self) -> None:
-        """Delete the pair (the pod end goes with it, wherever it is)."""
+        """Delete the pair (the pod end goes with it, wherever it is); an attached netdev is only
+        let go of (the engine's socket closes with the port)."""
         if self._nl is not None:
             try:
                 self._nl.link_del(self.ifname)
             except Exception:  # noqa: BLE001 - already gone with its namespace
                 pass
             self._nl = None
+
+
+_ETHTOOL = {"tx_csum": 0x17, "sg": 0x19, "tso": 0x1F, "gso": 0x24, "gro": 0x2C}   # ETHTOOL_S* (linux/ethtool.h)
+
+
+def set_offloads(ifname: str, ns: str = "", **features: bool) -> dict:
+    """Legacy ethtool feature switches on `ifname` (SIOCETHTOOL, what `ethtool -K` does), best
+    effort: {feature: applied}.  Features: tx_csum, sg, tso, gso, gro."""
+    import ctypes
+    import fcntl
+    import socket
+    import struct
+
+    from ..cni.netlink import in_netns
+
+    def run():
+        out = {}
+        s = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+        try:
+            for name, on in features.items():
+                val = ctypes.create_string_buffer(struct.pack("II", _ETHTOOL[name], 1 if on else 0))
+                ifr = struct.pack("16sP", ifname.encode()[:15], ctypes.addressof(val)) + bytes(16)
+                try:
+                    fcntl.ioctl(s.fileno(), 0x8946, ifr)          # SIOCETHTOOL
+                    out[name] = True
+                except OSError:
+                    out[name] = False
+        finally:
+            s.close()
+        return out
+
+    return in_netns(ns, run)
 
 
 def _quiet_ipv6(ifname: str) -> None:

@@ -128,8 +128,13 @@ class Mi355xDetector(VendorDetector):
     VSP_ARGS = ["--vendor", "amd-gpu", "--live", "--live-engine", "native", "--gpus", "all"]
 
     def vsp(self, dpu_mode, identifier=""):
+        # the wire port (node config `uplink`: a host-side veth pair by default, or the node's data
+        # NIC), as the reference's VSPs take their RPM / SFP port (marvell/main.go:104-154,
+        # intel-netsec/main.go:183-199)
+        from ..config import node_config
+
         return VspSpec(self.vendor, I.VSP_IMAGE_AMD_GPU, ["python3", "-m", "dpu_operator_amd.cmd.vsp"],
-                       list(self.VSP_ARGS), True, identifier, colocated=True)
+                       list(self.VSP_ARGS) + ["--uplink", node_config().uplink], True, identifier, colocated=True)
 
 
 class DpuDetectorManager:

@@ -14,11 +14,17 @@ import time
 from ..cni.netlink import RtNetlink, create_netns, delete_netns, in_netns
 
 
+def netns_path(name: str) -> str:
+    """Where a named test namespace is bound: `DPU_NETNS_DIR` (a private directory when the tests
+    run in a user namespace of their own) or /var/run/netns, where `ip netns` keeps them."""
+    return os.path.join(os.environ.get("DPU_NETNS_DIR", "/var/run/netns"), name)
+
+
 def privileged() -> bool:
     """True when this process can create network namespaces and TAP devices."""
     if not os.path.exists("/dev/net/tun"):
         return False
-    path = f"/var/run/netns/dpu-probe-{os.getpid()}"
+    path = netns_path(f"dpu-probe-{os.getpid()}")
     try:
         create_netns(path)
     except OSError:
@@ -36,11 +42,15 @@ def _csum(b: bytes) -> int:
     return ~s & 0xFFFF
 
 
-def ping(ns: str, dst: str, timeout: float = 3.0, ident: int = 0x4D49, seq: int = 1, payload: bytes = b"mi355x") -> float | None:
-    """One ICMP echo from inside netns `ns`; the RTT in seconds or None."""
+def ping(ns: str, dst: str, timeout: float = 3.0, ident: int = 0x4D49, seq: int = 1, payload: bytes = b"mi355x",
+         dev: str | None = None) -> float | None:
+    """One ICMP echo from inside netns `ns` (out of interface `dev` if given); the RTT in seconds
+    or None."""
 
     def run():
         s = socket.socket(socket.AF_INET, socket.SOCK_RAW, socket.IPPROTO_ICMP)
+        if dev:
+            s.setsockopt(socket.SOL_SOCKET, socket.SO_BINDTODEVICE, dev.encode())
         s.settimeout(0.2)
         try:
             hdr = struct.pack("!BBHHH", 8, 0, 0, ident, seq)
@@ -68,12 +78,35 @@ def ping(ns: str, dst: str, timeout: float = 3.0, ident: int = 0x4D49, seq: int 
     return in_netns(ns, run)
 
 
+def udp_exchange(src_ns: str, dst_ns: str, dst_ip: str, payload: bytes, port: int = 47000, timeout: float = 3.0,
+                 tries: int = 5) -> bytes | None:
+    """One UDP datagram from a socket in `src_ns` to `dst_ip`:`port`, received by a socket in
+    `dst_ns` through the kernels' own UDP stacks (so checksums are verified on receipt); what
+    arrived, or None."""
+    rx = in_netns(dst_ns, lambda: socket.socket(socket.AF_INET, socket.SOCK_DGRAM))
+    tx = in_netns(src_ns, lambda: socket.socket(socket.AF_INET, socket.SOCK_DGRAM))
+    try:
+        rx.bind(("0.0.0.0", port))
+        rx.settimeout(timeout / tries)
+        for _ in range(tries):      # (the first may wait for ARP)
+            tx.sendto(payload, (dst_ip, port))
+            try:
+                data, _addr = rx.recvfrom(65535)
+                return data
+            except socket.timeout:
+                continue
+        return None
+    finally:
+        rx.close()
+        tx.close()
+
+
 class Endpoint:
     """A namespace with one interface: `ifname` moved in, `cidr` assigned, interface + lo up."""
 
     def __init__(self, ns_name: str, ifname: str, cidr: str, nl: RtNetlink | None = None):
         self.nl = nl or RtNetlink()
-        self.ns = create_netns(f"/var/run/netns/{ns_name}")
+        self.ns = create_netns(netns_path(ns_name))
         self.ifname = ifname
         self.nl.link_set_ns(ifname, self.ns)
         self.nl.link_set_up("lo", self.ns)
@@ -92,13 +125,18 @@ class WireNF:
 
     ETH_P_ALL = 0x0003
 
-    def __init__(self, ns_name: str, if_in: str, if_out: str, nl: RtNetlink | None = None):
+    def __init__(self, ns_name: str, if_in: str, if_out: str, nl: RtNetlink | None = None,
+                 existing_ns: str | None = None):
+        """existing_ns: the interfaces are already in that namespace (an NF pod's, moved in by the
+        CNI); it is not deleted on close."""
         self.nl = nl or RtNetlink()
-        self.ns = create_netns(f"/var/run/netns/{ns_name}")
+        self.own_ns = existing_ns is None
+        self.ns = existing_ns or create_netns(netns_path(ns_name))
         self.ifs = (if_in, if_out)
         self.macs = []
         for i in self.ifs:
-            self.nl.link_set_ns(i, self.ns)
+            if existing_ns is None:
+                self.nl.link_set_ns(i, self.ns)
             self.nl.link_set_up(i, self.ns)
             self.macs.append(self.nl.link_by_name(i, self.ns).mac)
         self.forwarded = 0
@@ -145,7 +183,8 @@ class WireNF:
     def close(self) -> None:
         self._stop.set()
         self._t.join(5)
-        delete_netns(self.ns)
+        if self.own_ns:
+            delete_netns(self.ns)
 
 
 class RawPod:
@@ -158,7 +197,7 @@ class RawPod:
 
     def __init__(self, ns_name: str, ifname: str, nl: RtNetlink | None = None, existing_ns: str | None = None):
         self.nl = nl or RtNetlink()
-        self.ns = existing_ns or create_netns(f"/var/run/netns/{ns_name}")
+        self.ns = existing_ns or create_netns(netns_path(ns_name))
         self.own_ns = existing_ns is None
         self.ifname = ifname
         if existing_ns is None:

@@ -153,7 +153,12 @@ class GpuVsp(VspBase):
                                                     # kernel) or "native" (C++ I/O engine, iox.cpp)
         self.taps: dict[int, object] = {}       # live mode: port -> TapPort
         self.livepath = None
-        self.uplink = uplink                    # live mode: netdev (read/write/fd) of the wire port
+        # live mode: the wire port (WIRE_PORT).  A vport spec (netio.TapPort, native_io.PacketVport /
+        # MemifVport, anything with a packet fd), or a string resolved at Init: "veth" (a veth pair
+        # whose host end, `uplink_host_ifname`, the node reaches pods through), "none", or the
+        # name of an existing netdev (the node's data NIC) attached through AF_PACKET rings
+        self.uplink = uplink
+        self._uplink_vp = None                  # the resolved wire vport (closed with the live path)
         self.port_state: dict[int, tuple[bool, bool, int]] = {}  # port -> (link, rx, mtu) from the agent
         self.agent_bridge = None
         self.journal = Journal(state_dir, "gpu-vsp") if state_dir else None
@@ -276,6 +281,12 @@ class GpuVsp(VspBase):
         dp.macs.clear()
         vfs = self._vf_ports()
         dp.ports.update(WIRE_PORT, default_out=None, bridge_id=VF_BRIDGE)
+        # learning only on the plain bridge: a MAC learned on the steer bridge would let a VF's
+        # frame to that host bypass the NF chain
+        learn = self._wire_learns() and not self.nfs
+        dp.ports.a[WIRE_PORT]["flags"] = (dp.ports.a[WIRE_PORT]["flags"] & ~np.uint32(T.PORT_LEARN)) | \
+            np.uint32(T.PORT_LEARN if learn else 0)
+        dp.ports.version += 1
         dp.flood.set_members(VF_BRIDGE, [])
         if not self.nfs:
             # one L2 bridge: pod MACs forwarded, broadcast / unknown unicast flooded (wire first)
@@ -298,13 +309,43 @@ class GpuVsp(VspBase):
         self._commit()
 
     # ------------------------------------------------------------------ VSP hooks
+    def _wire_vport(self):
+        """The wire port's vport (live mode), resolved once from `uplink`."""
+        if self._uplink_vp is not None or self.uplink is None:
+            return self._uplink_vp
+        up = self.uplink
+        if not isinstance(up, str):
+            self._uplink_vp = up
+        elif up in ("", "none"):
+            return None
+        elif up == "veth":
+            from ..dataplane.native_io import PacketVport
+
+            host = node_config().uplink_host_ifname
+            try:
+                self.nl.link_del(host)          # a previous VSP's pair (its engine is gone)
+            except Exception:  # noqa: BLE001 - none left over
+                pass
+            self._uplink_vp = PacketVport.create_veth(self.nl, host)
+        else:
+            from ..dataplane.native_io import PacketVport
+
+            self._uplink_vp = PacketVport.attach(up)
+        return self._uplink_vp
+
+    def _wire_learns(self) -> bool:
+        """A live wire port learns the external hosts' MACs (OvS NORMAL on the reference's
+        br-mrv0 / br-secondary), so pod -> external unicast is forwarded, not flooded."""
+        return bool(self.live and self.uplink not in (None, "", "none"))
+
     def init(self, dpu_mode: bool, dpu_identifier: str):
         self.dpu_mode = dpu_mode
         self._ensure_dp()
         if self.live and self.livepath is None:
             ports = dict(self.taps)
-            if self.uplink is not None:
-                ports[WIRE_PORT] = self.uplink
+            wire = self._wire_vport()
+            if wire is not None:
+                ports[WIRE_PORT] = wire
             if self.live_engine == "native":
                 from ..dataplane.native_io import NativeLivePath
 
@@ -433,6 +474,9 @@ class GpuVsp(VspBase):
             if hasattr(tap, "close"):
                 tap.close()
         self.taps.clear()
+        if self._uplink_vp is not None and isinstance(self.uplink, str) and hasattr(self._uplink_vp, "close"):
+            self._uplink_vp.close()             # (a spec the caller gave stays the caller's)
+        self._uplink_vp = None
 
     def on_gpu_chain(self, sfc_name: str, kinds: list[str]) -> int:
         with self._lock:

@@ -4,14 +4,9 @@ data-plane end) or a TAP netdev (its fd kept by the engine).  Pods put the SFC's
 interfaces with raw sockets; what comes out on every pod must be, byte for byte, what the batch
 path of an identical data plane makes of the same frames.
 
-Then the deployed product path: a GPU VSP in live veth mode behind the node daemon, the device
-plugin allocating vports, the CNI moving each allocated vport into its pod (networkfn) and
-CreateBridgePort programming it, and the two pods pinging each other through the data plane.
-Skipped without CAP_NET_ADMIN / CAP_SYS_ADMIN (namespaces, veth, TAP)."""
+(The deployed product path, daemon + device plugin + CNI + GPU VSP with a wire port and an NF pod,
+is tests/test_deployed_node.py.)  Skipped without CAP_NET_ADMIN / CAP_SYS_ADMIN (namespaces, veth, TAP)."""
 import os
-import shutil
-import tempfile
-import threading
 import time
 
 import numpy as np
@@ -114,97 +109,6 @@ def test_netns_pods_through_the_native_engine_bit_exact(kind):
             t.close()
         for vp in vps:
             vp.close()
-
-
-@pytest.fixture
-def pm():
-    from dpu_operator_amd.utils.paths import PathManager
-
-    root = tempfile.mkdtemp(prefix="dpn", dir="/tmp")
-    yield PathManager(root)
-    shutil.rmtree(root, ignore_errors=True)
-
-
-def test_daemon_allocates_veth_vports_and_pods_ping_through_the_native_path(pm):
-    """The deployed MI355X node path end to end: Mi355xDetector's VSP arguments (live, native
-    engine, veth vports) -> GPU VSP (oracle data plane here) -> daemon device plugin (Allocate of
-    two vports) -> CNI ADD of two workload pods with those devices (the vport netdev moved into
-    each pod, CreateBridgePort programming its port) -> the pods ping each other through the
-    native I/O engine."""
-    from dpu_operator_amd import vars as V
-    from dpu_operator_amd.cmd import vsp as vspcmd
-    from dpu_operator_amd.cni.netlink import RtNetlink
-    from dpu_operator_amd.daemon.daemon import Daemon
-    from dpu_operator_amd.daemon.deviceplugin import wait_until
-    from dpu_operator_amd.k8s.apiserver import ApiServer
-    from dpu_operator_amd.platform.detectors import Mi355xDetector
-    from dpu_operator_amd.platform.platform import FakePlatform, PciDevice
-    from dpu_operator_amd.testutils.kubelet import FakeKubelet, cni_call
-    from dpu_operator_amd.utils.fileutils import touch
-
-    # the VSP the detector deploys, built from its own argument list
-    args = list(Mi355xDetector().vsp(True).args)
-    assert {"--live", "--live-engine", "native", "--gpus", "all"} <= set(args)
-    ap_args = args + ["--device", "cpu", "--flow-buckets", "1024", "--root", pm.root, "--io-queues", "2"]
-    import argparse
-
-    nl = RtNetlink()
-    parsed = None
-    orig = argparse.ArgumentParser.parse_args
-
-    def grab(self, argv=None, namespace=None):
-        nonlocal parsed
-        parsed = orig(self, argv, namespace)
-        raise SystemExit(0)
-
-    argparse.ArgumentParser.parse_args = grab
-    try:
-        with pytest.raises(SystemExit):
-            vspcmd.main(ap_args)
-    finally:
-        argparse.ArgumentParser.parse_args = orig
-    gvsp = vspcmd.build_vsp(parsed, pm)
-    gvsp.prefix = f"dv{os.getpid() % 1000}p"
-    assert gvsp.live and gvsp.live_engine == "native" and gvsp.vport_kind == "veth" and gvsp.io_queues == 2
-    touch(pm.wrap("/dpu-cni"))
-    api = ApiServer()
-    kubelet = FakeKubelet(pm, api).start()
-    gvsp.start()
-    plat = FakePlatform("AMD server", [PciDevice("0000:05:00.0", "1002", "75a3", class_code=0x120000)])
-    d = Daemon(plat, "auto", api, None, pm, nl=nl, tick=0.05, manager_kw={"dp_poll": 0.05})
-    t = threading.Thread(target=d.serve, daemon=True)
-    t.start()
-    pods = []
-    try:
-        assert wait_until(lambda: kubelet.allocatable() == 8, 15), kubelet.devices
-        devs = [f"{gvsp.prefix}0", f"{gvsp.prefix}1"]
-        resp = kubelet.allocate(devs)
-        assert resp.container_responses[0].envs["NF-DEV"] == ",".join(devs) + ","
-        sock = pm.cni_server_path()
-        for i, dev in enumerate(devs):
-            ns = NS.create_netns(f"/var/run/netns/{dev}-pod")
-            pods.append(ns)
-            conf = {"cniVersion": "0.4.0", "name": "dpucni", "type": "dpucni", "deviceID": dev}
-            cni_call(sock, "ADD", conf, netns=ns, ifname="eth1", pod_ns="default", pod_name=f"pod{i}",
-                     container_id=f"c{i}")
-            nl.addr_add("eth1", f"10.97.0.{i + 1}/24", ns)
-        assert wait_until(lambda: {"host0-0", "host0-1"} <= set(gvsp.bridge_ports), 5), gvsp.bridge_ports
-        assert NS.ping(pods[0], "10.97.0.2", timeout=5) is not None, (gvsp.livepath.stats, gvsp.livepath.error)
-        assert NS.ping(pods[1], "10.97.0.1", timeout=5) is not None
-        st = gvsp.livepath.stats
-        assert st["rx"] >= 4 and st["tx"] >= 4 and gvsp.livepath.error is None
-        assert st["queues"] == 2
-        for i, dev in enumerate(devs):
-            conf = {"cniVersion": "0.4.0", "name": "dpucni", "type": "dpucni", "deviceID": dev}
-            cni_call(sock, "DEL", conf, netns=pods[i], ifname="eth1", pod_ns="default", pod_name=f"pod{i}",
-                     container_id=f"c{i}")
-        assert wait_until(lambda: not gvsp.bridge_ports, 5), gvsp.bridge_ports
-    finally:
-        d.stop() if hasattr(d, "stop") else None
-        kubelet.stop()
-        gvsp.stop_live()
-        for ns in pods:
-            NS.delete_netns(ns)
 
 
 @pytest.mark.parametrize("mode", ["linux-bridge", "engine"])
