@@ -874,6 +874,7 @@ PYBIND11_MODULE(_nfdp, m) {
       .def("add_backend", &Engine::add_backend)
       .def("add_port", &Engine::add_port, py::arg("id"), py::arg("port"), py::arg("queue") = -1)
       .def("remove_port", &Engine::remove_port)
+      .def("retired_ports", &Engine::retired_ports, py::call_guard<py::gil_scoped_release>())
       .def("port", &Engine::port)
       .def("port_queue", &Engine::port_queue)
       .def("set_side_tables", &Engine::set_side_tables)

@@ -563,21 +563,40 @@ std::shared_ptr<Port> Engine::remove_port(uint32_t id) {
   (*t)[id] = PortRef{};
   std::atomic_store(&ports_, std::shared_ptr<const PortTab>(t));
   ports_ver_.fetch_add(1, std::memory_order_release);
+  // Frames of it may still be in a pipeline (an rx thread's snapshot still lists it until its
+  // next loop, bursts in flight point into its rx memory — mapped for the GPU with zero-copy rx):
+  // the engine keeps the port alive until no burst can refer to it (reap_retired), or until stop().
+  if (old) retired_.push_back(Retired{ports_ver_.load(), {}, old});
   reap_retired(false);
-  // Frames of it may still be in a pipeline (a packet thread's snapshot can hold it a little
-  // longer, its bursts complete within milliseconds): the engine keeps the port alive — its
-  // memory mapped for the GPU — for kRetireNs after the removal, or until stop().
-  if (old) retired_.emplace_back(now_ns(), old);
   return old;
 }
 
-namespace {
-constexpr uint64_t kRetireNs = 5'000'000'000ull;
+void Engine::reap_retired(bool all) {
+  if (all || !run_.load()) {   // (stopped: every burst was delivered or handed back)
+    retired_.clear();
+    return;
+  }
+  for (auto& r : retired_) {
+    if (!r.heads.empty()) continue;
+    bool seen = true;
+    for (auto& Q : queues_) seen = seen && Q->ports_seen.load(std::memory_order_acquire) >= r.ver;
+    if (!seen) break;          // (versions only grow: later entries are not seen either)
+    r.heads.resize(lanes_.size());
+    for (size_t k = 0; k < lanes_.size(); ++k) r.heads[k] = lanes_[k]->head.load(std::memory_order_acquire);
+  }
+  while (!retired_.empty() && !retired_.front().heads.empty()) {
+    const auto& h = retired_.front().heads;
+    bool done = true;
+    for (size_t k = 0; k < lanes_.size() && done; ++k) done = lanes_[k]->done.load(std::memory_order_acquire) >= h[k];
+    if (!done) break;
+    retired_.pop_front();
+  }
 }
 
-void Engine::reap_retired(bool all) {
-  const uint64_t t = now_ns();
-  while (!retired_.empty() && (all || t - retired_.front().first > kRetireNs)) retired_.pop_front();
+size_t Engine::retired_ports() {
+  std::lock_guard<std::mutex> g(ports_mu_);
+  reap_retired(false);
+  return retired_.size();
 }
 
 void Engine::map_port(Port& p) {
@@ -740,6 +759,7 @@ void Engine::stop() {
         for (const Pkt& q : b.pkts) q.holder->complete(q.seq);
         b.pkts.clear();
         b.reps.clear();
+        b.cfg.reset();
         b.state.store(0);
       }
     }
@@ -967,6 +987,20 @@ void Engine::rx_loop(Queue* Q) {
         for (auto& w : want)
           if (std::none_of(active.begin(), active.end(), [&](const auto& a) { return a.second == w.second; }))
             pending.push_back(w);
+        // frames staged from a port no longer in the table are dropped (handed back, never
+        // published): from here on no burst of this thread can refer to a removed port
+        for (Lane* L : Q->lanes) {
+          if (L->stage.empty()) continue;
+          size_t k = 0;
+          for (const Pkt& pk : L->stage) {
+            bool live = pk.holder == recirc_.get();
+            for (uint32_t i = 0; i < (uint32_t)tab->size() && !live; ++i) live = (*tab)[i].p.get() == pk.holder;
+            if (live) L->stage[k++] = pk;
+            else pk.holder->complete(pk.seq);
+          }
+          L->stage.resize(k);
+        }
+        Q->ports_seen.store(pv, std::memory_order_release);
         cached = tab;   // (after letting go: the old snapshot may hold the last reference to a removed port)
       }
       // take over ports whose previous rx thread has let go (acquire: its reads of the port happened before)

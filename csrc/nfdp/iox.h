@@ -451,6 +451,8 @@ class Engine {
   void add_port(uint32_t id, std::shared_ptr<Port> p, int queue = -1);
   void inject(uint32_t in_port, const uint8_t* f, uint32_t n) { recirc_->push(in_port, f, n); }
   std::shared_ptr<Port> remove_port(uint32_t id);
+  // removed ports still held because a burst may refer to them (released as lanes deliver)
+  size_t retired_ports();
   std::shared_ptr<Port> port(uint32_t id);
   int port_queue(uint32_t id);
   // Configuration (copy-on-write: safe while traffic flows).
@@ -561,6 +563,7 @@ class Engine {
     std::thread rx;
     std::vector<std::thread> tx;
     std::atomic<uint64_t> held_epoch{0};   // last control epoch (pause / hold) the rx thread acknowledged
+    std::atomic<uint64_t> ports_seen{0};   // port-table version the rx thread works from (retiring ports)
     QStats st;                  // rx-thread counters
     std::unique_ptr<QStats[]> wst;   // per tx worker
     std::unique_ptr<std::atomic<uint64_t>[]> side_ctr;   // per worker x kMaxPorts x 2 (replica tx pkts / bytes)
@@ -614,7 +617,15 @@ class Engine {
   std::atomic<bool> zero_copy_{false};
   // removed ports stay referenced a while (frames of theirs may still be in a pipeline: the GPU
   // reads a zero-copy frame where its port holds it)
-  std::deque<std::pair<uint64_t, std::shared_ptr<Port>>> retired_;   // (ports_mu_) removal time (ns)
+  // A removed port is released once nothing can refer to it: every rx thread has seen a port
+  // table without it (dropping what it had staged from it), and every burst published before
+  // that has been delivered (the lanes' done counters passed their heads at that moment).
+  struct Retired {
+    uint64_t ver;                   // ports_ver_ of the first table without the port
+    std::vector<uint64_t> heads;    // per lane: head once every rx thread saw `ver` (empty: not yet)
+    std::shared_ptr<Port> p;
+  };
+  std::deque<Retired> retired_;     // (ports_mu_)
   void map_port(Port& p);            // (ports_mu_)
   void reap_retired(bool all);       // (ports_mu_)
   std::shared_ptr<const PortTab> ports_;              // copy-on-write snapshot, by port id

@@ -115,16 +115,17 @@ class Region {
       hdr()->ring_size = ring_size;
       hdr()->buf_size = buf_size;
       hdr()->rx_rings = rx_rings;
-      std::atomic_thread_fence(std::memory_order_release);
-      hdr()->magic = kMagic;
+      __atomic_store_n(&hdr()->magic, kMagic, __ATOMIC_RELEASE);   // publishes the geometry above
     } else {
-      // the peer can rewrite the shared header at any time: read the geometry ONCE, validate it
-      // against the mapping, and never look at the shared copy again
+      // the creator publishes the geometry with a release store of the magic: acquire the magic
+      // FIRST, then read the geometry (once: the peer can rewrite the shared header at any time),
+      // validate it against the mapping, and never look at the shared copy again
+      const uint64_t magic = __atomic_load_n(&hdr()->magic, __ATOMIC_ACQUIRE);
+      const uint32_t version = hdr()->version;
       ring_size = hdr()->ring_size;
       buf_size = hdr()->buf_size;
       rx_rings = hdr()->rx_rings;
-      std::atomic_thread_fence(std::memory_order_acquire);
-      if (hdr()->magic != kMagic || hdr()->version != kVersion || ring_size < 2 || (ring_size & (ring_size - 1)) ||
+      if (magic != kMagic || version != kVersion || ring_size < 2 || (ring_size & (ring_size - 1)) ||
           ring_size > (1u << 20) || buf_size < 64 || buf_size > (1u << 16) || rx_rings < 1 || rx_rings > kMaxRxRings ||
           bytes_ < region_bytes(ring_size, buf_size, rx_rings)) {
         close();

@@ -649,3 +649,32 @@ def test_bursts_in_flight_keep_their_publish_time_configuration(shm):
         assert live.error is None
     finally:
         live.stop()
+
+
+def test_removed_port_released_once_its_bursts_are_delivered(shm):
+    """A removed port is held only while a burst may still point into its rx memory (iox
+    Engine::reap_retired): with its frames delivered it is released within moments, not after a
+    fixed grace time, and a port removed while frames of it are in flight is kept until they are."""
+    nf = nfdp()
+    dp, sc, _ = _sfc()
+    slots, im = S.traffic(sc, 400, seed=11)
+    paths = {int(p): str(shm / f"r{int(p)}") for p in sc.pod_port}
+    live = NativeLivePath(dp, {p: MemifVport(paths[p], ring_size=1024) for p in paths}, burst=128,
+                          ring_capacity=1024, queues=2).start()
+    try:
+        eng = live._eng
+        src = int(sc.pod_port[0])
+        be = live._backends[0]
+        be.set_completion_gate(True)                       # frames of `src` stay in flight
+        eps = _send_all(nf, paths, slots, im, [src])
+        n_src = int(((im & 0xFFFF) == src).sum())
+        assert _until(lambda: live.stats["rx"] >= n_src), live.stats
+        live.remove_port(src)
+        time.sleep(0.05)
+        assert eng.retired_ports() == 1                     # its bursts are not delivered yet
+        be.set_completion_gate(False)
+        assert _until(lambda: eng.retired_ports() == 0, 2.0), eng.retired_ports()
+        assert live.error is None
+        eps.clear()
+    finally:
+        live.stop()
