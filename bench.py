@@ -67,6 +67,27 @@ def rss_exchange_info(a2a_s: float, sent_per_step: float, max_peer: int, remote_
             "note": "overlapped with later steps' kernels in the timed region; counts read lag steps late"}
 
 
+# The exchange-bound variant of an N > 1 RSS run (`unsteered` block): the same pipeline with traffic
+# no producer steered - every packet arrives at a random GPU, so (N-1)/N of each batch crosses
+# xGMI to its flow's owner.  The headline steers like a NIC's RSS (1 % misdirected) and so mostly
+# measures N independent GPUs; this block measures the all-to-all exchange.
+RSS_UNSTEERED_KEYS = ("mpps", "mpps_per_gpu", "ms_per_step", "steps", "remote_frac", "sent_per_gpu_per_step",
+                      "xgmi_bytes_out_per_gpu_per_step", "xgmi_gbps_out_per_gpu", "forwarded_fraction", "note")
+
+
+def rss_unsteered_info(elapsed_s: float, steps: int, world: int, batch: int, sent_per_step: float,
+                       fwd: float) -> dict:
+    step_s = elapsed_s / max(steps, 1)
+    peer_bytes = int(sent_per_step * 68)
+    return {"mpps": round(world * batch / step_s / 1e6, 2), "mpps_per_gpu": round(batch / step_s / 1e6, 2),
+            "ms_per_step": round(step_s * 1e3, 4), "steps": int(steps), "remote_frac": round((world - 1) / world, 4),
+            "sent_per_gpu_per_step": int(sent_per_step), "xgmi_bytes_out_per_gpu_per_step": peer_bytes,
+            "xgmi_gbps_out_per_gpu": round(peer_bytes / max(step_s, 1e-9) / 1e9, 2),
+            "forwarded_fraction": round(fwd, 6),
+            "note": "unsteered traffic: (N-1)/N of every batch exchanged with its owner over xGMI each step "
+                    "(count-first all-to-all), timed like the headline (barrier + sync, max over ranks)"}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -82,6 +103,7 @@ def parse():
     ap.add_argument("--no-lowlat", action="store_true", help="skip the small-batch latency probe")
     ap.add_argument("--no-variants", action="store_true", help="skip the mixed / ACL1024 / IMIX measurements")
     ap.add_argument("--no-live", action="store_true", help="skip the live pod-to-pod (native I/O engine) block")
+    ap.add_argument("--no-unsteered", action="store_true", help="N > 1 rss: skip the exchange-bound (unsteered) variant")
     ap.add_argument("--live-workers", type=int, default=2, help="native I/O engine delivery threads per queue")
     ap.add_argument("--live-queues", type=int, default=4, help="native I/O engine rx queues (threads)")
     ap.add_argument("--live-gen-threads", type=int, default=4, help="pod traffic generator threads")
@@ -467,6 +489,42 @@ def main() -> None:
                 "xgmi_bytes_out_per_gpu_per_step": peer_bytes * n_chunks,
                 "xgmi_gbps_out_per_gpu": round(peer_bytes / (el / reps) / 1e9, 1)}
 
+    # exchange-bound variant (outside the timed region, N > 1 RSS): unsteered traffic, (N-1)/N of
+    # every batch crosses xGMI to its owner
+    unsteered = None
+    if rss and not a.no_unsteered:
+        rf = (world - 1) / world
+        ub = []
+        for r in range(min(a.rotate, 2)):
+            pk, im = rss_traffic(sc, a.batch, rank, world, owner, rf, seed=7000 + 1000 * rank + r)
+            ub.append((torch.from_numpy(pk).to(dev), torch.from_numpy(im.view(np.int32)).to(dev)))
+            del pk, im
+        eng_u = RssShardedDataPlane(dp, rank, world, a.batch, remote_frac=rf)
+        nu = max(1, min(a.steps, 10))
+        for k in range(2):
+            eng_u.step(*ub[k % len(ub)])
+        eng_u.flush()
+        torch.cuda.synchronize()
+        dist.barrier()
+        torch.cuda.synchronize()
+        s0 = eng_u.stats["sent"]
+        tu = time.perf_counter()
+        for k in range(nu):
+            eng_u.step(*ub[k % len(ub)])
+        eng_u.flush()
+        torch.cuda.synchronize()
+        dist.barrier()
+        el_u = time.perf_counter() - tu
+        tt = torch.tensor([el_u], dtype=torch.float64, device=cdev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el_u = float(tt.item())
+        _, _, ru = P.meta_fields(eng_u.out_meta())
+        fu = torch.tensor([float(np.mean((ru == 0) | (ru == 10)))], dtype=torch.float64, device=cdev)
+        dist.all_reduce(fu, op=dist.ReduceOp.SUM)
+        unsteered = rss_unsteered_info(el_u, nu, world, a.batch, (eng_u.stats["sent"] - s0) / nu, float(fu.item()) / world)
+        del eng_u, ub
+        torch.cuda.empty_cache()
+
     # small-batch latency probe (outside the timed region): 64K packets per step, fused/sharded alike
     p50_small = None
     if not a.no_lowlat and a.io == "device":
@@ -628,6 +686,7 @@ def main() -> None:
             "p50_latency_us_ring": None if not ring or "p50_us" not in ring else ring["p50_us"],
             "ring": ring,
             "exchange": xchg,
+            "unsteered": unsteered,
             "forwarded_fraction": round(fwd_local, 6),
             "value_mixed": None if not variants else variants["mixed_mpps"],
             "value_acl1024": None if not variants else variants["acl1024_mpps"],

@@ -880,6 +880,7 @@ PYBIND11_MODULE(_nfdp, m) {
       .def("set_side_tables", &Engine::set_side_tables)
       .def("set_redirects", &Engine::set_redirects)
       .def("set_coalesce", &Engine::set_coalesce, py::arg("frames") = 64, py::arg("window_us") = 0.0)
+      .def("set_queue_cpus", &Engine::set_queue_cpus, py::arg("queue"), py::arg("cpus"))
       .def("set_zero_copy", &Engine::set_zero_copy, py::arg("on"))
       .def_property_readonly("zero_copy", &Engine::zero_copy)
       .def("hold", [](Engine& e) { py::gil_scoped_release nogil; e.hold(); })

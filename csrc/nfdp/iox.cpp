@@ -9,6 +9,8 @@
 #include <linux/if_ether.h>
 #include <linux/if_packet.h>
 #include <net/if.h>
+#include <pthread.h>
+#include <sched.h>
 #include <sys/socket.h>
 
 #include <algorithm>
@@ -720,9 +722,28 @@ void Engine::start() {
   }
   learner_ = std::thread(&Engine::learner_loop, this);
   for (auto& Q : queues_) {
-    for (uint32_t w = 0; w < workers_; ++w) Q->tx.emplace_back(&Engine::tx_loop, this, Q.get(), w);
+    for (uint32_t w = 0; w < workers_; ++w) {
+      Q->tx.emplace_back(&Engine::tx_loop, this, Q.get(), w);
+      pin(Q->tx.back(), Q->cpus);
+    }
     Q->rx = std::thread(&Engine::rx_loop, this, Q.get());
+    pin(Q->rx, Q->cpus);
   }
+}
+
+void Engine::pin(std::thread& t, const std::vector<int>& cpus) {
+  if (cpus.empty()) return;
+  cpu_set_t set;
+  CPU_ZERO(&set);
+  for (int c : cpus)
+    if (c >= 0 && c < CPU_SETSIZE) CPU_SET(c, &set);
+  (void)pthread_setaffinity_np(t.native_handle(), sizeof(set), &set);   // best effort (a cpuset may refuse)
+}
+
+void Engine::set_queue_cpus(uint32_t q, const std::vector<int>& cpus) {
+  if (q >= nq_) throw std::invalid_argument("iox: no such queue");
+  if (run_) throw std::runtime_error("iox: queue CPUs are set before start()");
+  queues_[q]->cpus = cpus;
 }
 
 bool Engine::lanes_idle() const {

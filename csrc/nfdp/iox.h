@@ -472,6 +472,9 @@ class Engine {
     coalesce_ns_.store((uint64_t)(std::max(window_us, 0.0) * 1e3));
   }
   void set_side_tables(uint32_t backend, std::shared_ptr<SideTables> t);
+  // The CPUs queue q's rx thread and tx workers run on (a GPU's NUMA-local CPUs: the lane group
+  // serving that GPU); before start().
+  void set_queue_cpus(uint32_t q, const std::vector<int>& cpus);
   // Zero-copy rx: map every port's rx memory (rx_memory()) for the backends; a backend reading
   // frames by address (frame_addrs()) then reads mapped frames in place — the engine writes an
   // address per slot instead of copying the frame's first 64 bytes.  Ports added later are
@@ -564,6 +567,7 @@ class Engine {
     std::vector<std::thread> tx;
     std::atomic<uint64_t> held_epoch{0};   // last control epoch (pause / hold) the rx thread acknowledged
     std::atomic<uint64_t> ports_seen{0};   // port-table version the rx thread works from (retiring ports)
+    std::vector<int> cpus;      // the queue's threads run on these CPUs (empty: anywhere)
     QStats st;                  // rx-thread counters
     std::unique_ptr<QStats[]> wst;   // per tx worker
     std::unique_ptr<std::atomic<uint64_t>[]> side_ctr;   // per worker x kMaxPorts x 2 (replica tx pkts / bytes)
@@ -579,6 +583,7 @@ class Engine {
     std::vector<uint32_t> learn;   // learn events of the current burst
   };
 
+  static void pin(std::thread& t, const std::vector<int>& cpus);
   void rx_loop(Queue* Q);
   void tx_loop(Queue* Q, uint32_t w);
   void learner_loop();

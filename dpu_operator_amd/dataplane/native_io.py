@@ -67,13 +67,18 @@ class PacketVport:
     out and the CNI moves into the pod, networkfn.cmd_add) and the data-plane end (`name` + "d")
     this port opens."""
 
-    def __init__(self, ifname: str, frames: int = 1024, frame_size: int = 2048):
+    # AF_PACKET rx ring per port: what an overloaded port can queue.  A NIC-like depth: deep enough
+    # to absorb bursts, shallow enough that overload drops instead of building milliseconds of
+    # standing queue (at ~100 kpps per veth, 512 frames are ~5 ms)
+    DEFAULT_FRAMES = 512
+
+    def __init__(self, ifname: str, frames: int = DEFAULT_FRAMES, frame_size: int = 2048):
         self.ifname, self.frames, self.frame_size = ifname, int(frames), int(frame_size)
         self._nl = None
         self.name = None
 
     @classmethod
-    def create_veth(cls, nl, name: str, mac: str | None = None, frames: int = 1024) -> "PacketVport":
+    def create_veth(cls, nl, name: str, mac: str | None = None, frames: int = DEFAULT_FRAMES) -> "PacketVport":
         """A veth pair for a kernel-netdev pod: `name` (pod end) and `name`d (data-plane end)."""
         peer = name + "d"
         if len(peer) > 15:
@@ -165,13 +170,49 @@ def _make_port(nf, spec, queues: int = 1):
     raise TypeError(f"unsupported vport {spec!r}")
 
 
+def parse_cpulist(text: str) -> list[int]:
+    """sysfs cpulist ("0-3,8,10-11") -> [0, 1, 2, 3, 8, 10, 11]."""
+    out: list[int] = []
+    for part in text.strip().split(","):
+        if not part:
+            continue
+        a, _, b = part.partition("-")
+        out.extend(range(int(a), int(b or a) + 1))
+    return out
+
+
+def device_local_cpus(dev, sys_root: str = "/") -> list[int]:
+    """CPUs NUMA-local to GPU `dev` (its PCI function's local_cpulist) that this process may run
+    on; [] when unknown or when that is every CPU this process has (nothing to pin)."""
+    try:
+        import torch
+
+        d = torch.device(dev)
+        if d.type != "cuda":
+            return []
+        pr = torch.cuda.get_device_properties(d.index or 0)
+        pci = f"{getattr(pr, 'pci_domain_id', 0):04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}.0"
+        with open(os.path.join(sys_root, "sys/bus/pci/devices", pci, "local_cpulist")) as f:
+            local = set(parse_cpulist(f.read()))
+    except Exception:  # noqa: BLE001 - no such attribute / file: leave the threads unpinned
+        return []
+    allowed = os.sched_getaffinity(0)
+    cpus = sorted(local & allowed)
+    return cpus if cpus and set(cpus) != allowed else []
+
+
 class NativeLivePath:
     def __init__(self, dps, ports: dict, burst: int = 256, ring_capacity: int = 4096, inflight: int = 64,
                  on_punt=None, auto_restart: bool = True, tx_workers: int = 1, queues: int = 1,
                  max_inflight_frames: int = 0, port_queues: dict | None = None, coalesce_us: float = 8.0,
-                 coalesce_frames: int = 64, ring_cus: int = 0, zero_copy: bool = False):
+                 coalesce_frames: int = 64, ring_cus: int = 0, zero_copy: bool = False, lane_groups: bool = False,
+                 pin_cpus: bool = False):
         """dps: one data plane or a list (one per GPU, or a MultiDataPlane's planes); ports:
-        {port id: vport spec}; queues: rx threads (each with a ring queue on every GPU);
+        {port id: vport spec}; queues: rx threads (each with a ring queue on every GPU) — with
+        `lane_groups`, per data plane: every plane brings `queues` rx threads (and their tx
+        workers) of its own, so the engine's I/O capacity grows with the GPU count, and a port
+        placed on a plane (MultiDataPlane placement="port") is served by a queue of that plane's
+        group; pin_cpus: each group's threads run on its GPU's NUMA-local CPUs (or {group: CPUs});
         port_queues: {port id: queue} (default: least loaded); max_inflight_frames: per lane
         bound of the engine's own queueing (0: the ring capacity); coalesce_us / coalesce_frames:
         with bursts of a lane in flight, frames gather into one publish until that many are read
@@ -184,6 +225,12 @@ class NativeLivePath:
         self.dps = list(dps) if isinstance(dps, (list, tuple)) else list(getattr(dps, "planes", [dps]))
         if not self.dps:
             raise ValueError("at least one data plane")
+        self._port_owner = getattr(self.dps[0], "_port_owner", None)   # (MultiDataPlane placement="port")
+        self.lane_groups = bool(lane_groups)
+        self.group_queues = int(queues)
+        if self.lane_groups:
+            queues = int(queues) * len(self.dps)
+        self.pin_cpus = pin_cpus if isinstance(pin_cpus, dict) else bool(pin_cpus)
         self.gpu = self.dps[0].gpu
         if any(d.gpu != self.gpu for d in self.dps):
             raise ValueError("data planes must all be GPU or all CPU")
@@ -260,11 +307,18 @@ class NativeLivePath:
         hooks = getattr(self.dps[0], "_ctr_hooks", [])
         if self not in hooks:
             self.dps[0]._ctr_hooks = hooks + [self]
+        if self.pin_cpus:
+            for q in range(self.queues):
+                g = self.group_of(q)
+                cpus = (self.pin_cpus.get(g, []) if isinstance(self.pin_cpus, dict)
+                        else device_local_cpus(getattr(self.dps[g], "tdev", "cpu")))
+                if cpus:
+                    eng.set_queue_cpus(q, list(cpus))
         for idx, spec in self.specs.items():
             p = self._ports.get(idx)
             if p is None:
                 p = self._ports[idx] = _make_port(nf, spec, self.queues)
-            eng.add_port(int(idx), p, int(self.port_queues.get(idx, -1)))
+            eng.add_port(int(idx), p, self._queue_for(idx))
         eng.learn_stamp = max(int(getattr(d, "stamp", 0)) for d in self.dps) + 1
         self._eng = eng
         self._applied = {}   # a new engine holds no configuration yet
@@ -425,6 +479,28 @@ class NativeLivePath:
             self._eng.flush_learning()
 
     # ------------------------------------------------------------------ ports
+    def group_of(self, q: int) -> int:
+        """The data plane (lane group) whose threads queue q is (0 without lane groups)."""
+        return q // self.group_queues if self.lane_groups else 0
+
+    def _queue_for(self, idx: int) -> int:
+        """The queue serving port idx: an explicit choice, else with lane groups and a port placed
+        on a plane the least loaded queue of that plane's group, else the engine's least loaded."""
+        if idx in self.port_queues:
+            return int(self.port_queues[idx])
+        po = self._port_owner
+        if self.lane_groups and po is not None and 0 <= int(idx) < len(po) and self._eng is not None:
+            g = int(po[int(idx)]) % len(self.dps)
+            group = range(g * self.group_queues, (g + 1) * self.group_queues)
+            load = {q: 0 for q in group}
+            for other in self._ports:
+                if other != idx:
+                    q = self.port_queue(other)
+                    if q in load:
+                        load[q] += 1
+            return min(group, key=lambda q: (load[q], q))
+        return -1
+
     def add_port(self, idx: int, spec, queue: int = -1) -> None:
         with self._lock:
             self.specs[idx] = spec
@@ -432,7 +508,7 @@ class NativeLivePath:
                 self.port_queues[idx] = queue
             p = self._ports[idx] = _make_port(self.nf, spec, self.queues)
             if self._eng is not None:
-                self._eng.add_port(int(idx), p, int(self.port_queues.get(idx, -1)))
+                self._eng.add_port(int(idx), p, self._queue_for(idx))
 
     def remove_port(self, idx: int):
         with self._lock:

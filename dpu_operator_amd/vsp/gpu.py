@@ -350,8 +350,10 @@ class GpuVsp(VspBase):
                 from ..dataplane.native_io import NativeLivePath
 
                 planes = self.dp.planes if hasattr(self.dp, "planes") else [self.dp]
-                self.livepath = NativeLivePath(planes, ports, tx_workers=self.tx_workers,
-                                               queues=self.io_queues).start()
+                # lane groups: every GPU brings io_queues rx threads (+ their tx workers) of its
+                # own, pinned to its NUMA-local CPUs, so I/O capacity grows with the GPU count
+                self.livepath = NativeLivePath(planes, ports, tx_workers=self.tx_workers, queues=self.io_queues,
+                                               lane_groups=True, pin_cpus=True).start()
             else:
                 from ..dataplane.netio import LivePath
 

@@ -72,3 +72,6 @@ def test_bench_rss_two_gpus():
     assert line["n_gpus"] == 2 and line["forwarded_fraction"] == 1.0
     assert line["exchange"]["a2a_per_step"] == bench.RSS_A2A_PER_STEP
     assert set(line["exchange"]) == set(bench.RSS_EXCHANGE_KEYS)
+    # the exchange-bound variant: unsteered traffic, half of every batch over xGMI at N = 2
+    assert set(line["unsteered"]) == set(bench.RSS_UNSTEERED_KEYS)
+    assert line["unsteered"]["remote_frac"] == 0.5 and line["unsteered"]["sent_per_gpu_per_step"] > 0

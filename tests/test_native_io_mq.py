@@ -6,6 +6,7 @@ whole), byte-table Toeplitz steering, and a memif peer that corrupts the shared 
 Everything runs on the C++ oracle backends here; the GPU twins (ring kernel queues) are marked gpu.
 Expected frames come from the batch path of an identical data plane (`DataPlane.run` + its side
 results), assembled by ops/packets.assemble."""
+import os
 import shutil
 import struct
 import tempfile
@@ -676,5 +677,36 @@ def test_removed_port_released_once_its_bursts_are_delivered(shm):
         assert _until(lambda: eng.retired_ports() == 0, 2.0), eng.retired_ports()
         assert live.error is None
         eps.clear()
+    finally:
+        live.stop()
+
+
+def test_cpulist_and_lane_group_pinning(shm):
+    """sysfs cpulists parse; each lane group's threads run on the CPUs given for it (set_queue_cpus
+    before start; refused after) and the engine forwards bit-exact as before."""
+    from dpu_operator_amd.dataplane.native_io import parse_cpulist
+
+    assert parse_cpulist("0-3,8,10-11\n") == [0, 1, 2, 3, 8, 10, 11]
+    assert parse_cpulist("") == []
+    nf = nfdp()
+    eng = nf.IoEngine(128, 16, 1, 2, 0)
+    with pytest.raises(ValueError):
+        eng.set_queue_cpus(5, [0])
+    dp, sc, _ = _sfc()
+    ref, _, _ = _sfc()
+    slots, im = S.traffic(sc, 500, seed=12)
+    exp, _ = _expected(ref, slots, im)
+    paths = {int(p): str(shm / f"c{int(p)}") for p in sc.pod_port}
+    cpus = sorted(os.sched_getaffinity(0))
+    live = NativeLivePath([dp], {p: MemifVport(paths[p], ring_size=2048) for p in paths}, burst=128,
+                          ring_capacity=1024, queues=2, lane_groups=True, pin_cpus={0: cpus[:2]}).start()
+    try:
+        with pytest.raises(RuntimeError):
+            live._eng.set_queue_cpus(0, cpus[:1])           # running: too late
+        eps = _send_all(nf, paths, slots, im, list(paths))
+        got, done = _collect(eps, sum(map(len, exp.values())))
+        assert _until(done), (live.stats, live.error)
+        for port, frames in exp.items():
+            assert sorted(got[port]) == sorted(frames), port
     finally:
         live.stop()

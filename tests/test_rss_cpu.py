@@ -131,3 +131,20 @@ def test_bench_exchange_block_matches_the_protocol():
     assert set(info) == set(bench.RSS_EXCHANGE_KEYS)
     assert info["a2a_per_step"] == bench.RSS_A2A_PER_STEP == 2
     assert info["xgmi_bytes_out_per_gpu_per_step"] == 4096 * 68 and info["host_lag_steps"] == 2
+
+
+def test_bench_unsteered_block_keys():
+    """bench.py's exchange-bound variant at N > 1 (`unsteered`: (N-1)/N of every batch crosses
+    xGMI): the block's keys and arithmetic.  The loss-free exchange at those fractions is
+    test_rss_gloo's (3, 2/3) and (4, 3/4) cases; the GPU run asserts the same keys
+    (tests/test_multigpu.py::test_bench_rss_two_gpus)."""
+    import sys
+
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+
+    u = bench.rss_unsteered_info(0.010, 10, 4, 1 << 20, 786432.0, 1.0)
+    assert set(u) == set(bench.RSS_UNSTEERED_KEYS)
+    assert u["remote_frac"] == 0.75 and u["ms_per_step"] == 1.0
+    assert u["mpps"] == round(4 * (1 << 20) / 1e-3 / 1e6, 2) and u["mpps_per_gpu"] * 4 == pytest.approx(u["mpps"], rel=1e-3)
+    assert u["xgmi_bytes_out_per_gpu_per_step"] == 786432 * 68

@@ -138,6 +138,11 @@ def test_vsp_port_placement_runs_each_hop_on_its_gpu(shm):
     vsp.set_num_vfs(6)
     try:
         assert vsp.dp.placement == "port"
+        # lane groups: every plane brings its own rx queue (io_queues = 1 each), and a vport is
+        # read by a queue of its plane's group
+        lp = vsp.livepath
+        assert lp.queues == 3 and lp.stats["queues"] == 3
+        assert [lp.group_of(lp.port_queue(i)) for i in range(6)] == [i % 3 for i in range(6)]
         macs = ["02:00:00:00:dd:01", "02:00:00:00:dd:02"]
         vsp.create_bridge_port("host0-0", bytes.fromhex(macs[0].replace(":", "")), 0, ["2"])
         vsp.create_bridge_port("host0-1", bytes.fromhex(macs[1].replace(":", "")), 0, ["3"])

@@ -235,15 +235,24 @@ def run(device: str = "cuda", n_pods: int = 8, flows: int = 1 << 20, n_acl: int 
 
 def run_veth(mode: str = "linux-bridge", n_pods: int = 4, duration: float = 1.0, threads: int = 2,
              queues: int = 2, tx_workers: int = 1, burst: int = 256, inflight: int = 64, ring_capacity: int = 16384,
-             max_inflight_frames: int = 4096, coalesce_us: float = 8.0) -> dict:
+             max_inflight_frames: int = 4096, coalesce_us: float = 8.0, device: str = "cuda", rx_frames: int = 0) -> dict:
     """Kernel-netdev pods: every pod a network namespace holding one end of a veth pair, driven by
     the same C++ generator / sink through AF_PACKET rings opened inside the namespace
-    (csrc/nfdp/trafgen_pkt.h).  The host ends go either to a Linux bridge (`linux-bridge`: the
-    kernel's own L2 switch, the comparator) or to the native I/O engine as PacketPorts over the
-    zero-cost wire pipeline (`engine`), so both switch identical pods with identical frames."""
+    (csrc/nfdp/trafgen_pkt.h).  The host ends go to
+      * `linux-bridge`: a Linux bridge (the kernel's own L2 switch, the comparator);
+      * `engine`: the native I/O engine as PacketPorts over the zero-cost wire pipeline (the
+        engine's own ceiling on veth);
+      * `pipeline`: the native I/O engine over the data plane on `device` (the resident ring
+        kernel on a GPU): the deployed GPU node's default, its pods on one L2 bridge with their
+        MACs programmed (what the VSP does without an NF), frames switched by the pipeline;
+    so all three switch identical pods with identical frames.  rx_frames: the engine's AF_PACKET rx
+    ring per port (0: the vports' default, native_io.PacketVport)."""
     from dpu_operator_amd.cni.netlink import RtNetlink, create_netns, delete_netns
+    from dpu_operator_amd.dataplane.native_io import PacketVport
 
     nf = nfdp()
+    rx_frames = rx_frames or PacketVport.DEFAULT_FRAMES
+    live = None
     nl = RtNetlink()
     tag = f"{os.getpid() % 10000}"
     br = f"lbbr{tag}"
@@ -257,7 +266,7 @@ def run_veth(mode: str = "linux-bridge", n_pods: int = 4, duration: float = 1.0,
             pod, host = f"lb{tag}p{i}", f"lb{tag}p{i}d"
             nl.link_add_veth(pod, host)
             hosts.append(host)
-            ns = create_netns(f"/var/run/netns/lb{tag}-{i}")
+            ns = create_netns(os.path.join(os.environ.get("DPU_NETNS_DIR", "/var/run/netns"), f"lb{tag}-{i}"))
             nss.append(ns)
             nl.link_set_hw_addr(pod, ":".join(f"{b:02x}" for b in _WireLive.mac(i)))
             nl.link_set_ns(pod, ns)
@@ -271,15 +280,30 @@ def run_veth(mode: str = "linux-bridge", n_pods: int = 4, duration: float = 1.0,
             macs = [(int.from_bytes(_WireLive.mac(i), "little"), i) for i in range(n_pods)]
             eng.add_backend(nf.WireBackend(ring_capacity, queues, macs))
             for i, h in enumerate(hosts):
-                eng.add_port(i, nf.PacketPort(h, 2048, 2048))
+                eng.add_port(i, nf.PacketPort(h, rx_frames, 2048))
             eng.start()
+        elif mode == "pipeline":
+            from dpu_operator_amd.dataplane import tables as T
+
+            dp = DataPlane(device=device, flow_buckets=1 << 12, hash_mode="lds" if device != "cpu" else "mfma")
+            for i in range(n_pods):
+                mac = ":".join(f"{b:02x}" for b in _WireLive.mac(i))
+                dp.ports.set(i, flags=T.PORT_VALID | T.PORT_SPOOFCHK, bridge_id=1, mac=mac, peer_mac=mac)
+                dp.macs.insert(1, mac, i)
+            dp.flood.set_members(1, list(range(n_pods)))
+            dp.commit(full=True)
+            live = NativeLivePath(dp, {i: PacketVport(h, frames=rx_frames) for i, h in enumerate(hosts)}, burst=burst,
+                                  ring_capacity=ring_capacity, inflight=inflight, tx_workers=tx_workers, queues=queues,
+                                  max_inflight_frames=max_inflight_frames, coalesce_us=coalesce_us).start()
+            eng = live._eng
         pods = []
         for i in range(n_pods):
             fr, ln = wire.frames(i, n_pods, k=1024, seed=100 + i)
             pods.append((nss[i], f"lb{tag}p{i}", fr, ln))
         out = {"vports": "veth", "switch": mode, "pods": n_pods, "gen_threads": threads, "frame_bytes": 64}
-        if mode == "engine":
-            out.update(queues=queues, coalesce_us=coalesce_us)
+        if mode != "linux-bridge":
+            out.update(queues=queues, tx_workers=tx_workers, coalesce_us=coalesce_us, rx_frames=rx_frames,
+                       device=device if mode == "pipeline" else "none")
         # warm-up (the bridge learns every MAC), then saturated
         nf.trafgen_run_netns(pods, duration_s=0.2, warmup_s=0.0, threads=threads, burst=32)
         time.sleep(0.1)
@@ -299,12 +323,14 @@ def run_veth(mode: str = "linux-bridge", n_pods: int = 4, duration: float = 1.0,
                                   rate_pps=1000.0)
         out.update(idle_p50_us=_pct(r3["lat_us"], 50), idle_p99_us=_pct(r3["lat_us"], 99))
         if eng is not None:
-            st = dict(eng.stats())
+            st = dict(live.stats if live is not None else eng.stats())
             out["engine"] = {k: int(st.get(k, 0)) for k in ("rx", "tx", "drop", "bursts", "tx_full")}
-            out["error"] = eng.error() or None
+            out["error"] = (live.error if live is not None else eng.error()) or None
         return out
     finally:
-        if eng is not None:
+        if live is not None:
+            live.stop()
+        elif eng is not None:
             eng.stop()
         for ns in nss:
             delete_netns(ns)
@@ -338,12 +364,17 @@ def main() -> None:
     ap.add_argument("--coalesce-us", type=float, default=8.0)
     ap.add_argument("--loaded-window", type=int, default=2048, help="frames in flight of the closed-loop loaded run")
     ap.add_argument("--zero-copy", action="store_true", help="the ring reads frames in the pods' memif regions")
-    ap.add_argument("--veth", choices=("linux-bridge", "engine"), default=None,
-                    help="netns pods on veth pairs, switched by a Linux bridge or by the native engine")
+    ap.add_argument("--veth", choices=("linux-bridge", "engine", "pipeline"), default=None,
+                    help="netns pods on veth pairs, switched by a Linux bridge, by the native engine alone or by the "
+                         "native engine in front of the data plane on --device (the deployed default)")
+    ap.add_argument("--rx-frames", type=int, default=0, help="--veth: the engine's AF_PACKET rx ring per port")
     a = ap.parse_args()
     if a.veth:
+        if "DPU_NETNS_DIR" in os.environ:   # a namespace of our own (unshare -Urnm): loopback starts down
+            os.makedirs(os.environ["DPU_NETNS_DIR"], exist_ok=True)
         print(json.dumps(run_veth(a.veth, n_pods=min(a.pods, 8), duration=a.duration, threads=min(a.threads, a.pods),
-                                  queues=a.queues, tx_workers=a.tx_workers, coalesce_us=a.coalesce_us)), flush=True)
+                                  queues=a.queues, tx_workers=a.tx_workers, coalesce_us=a.coalesce_us,
+                                  device=a.device, rx_frames=a.rx_frames)), flush=True)
         return
     print(json.dumps(run(a.device, a.pods, a.flows, duration=a.duration, threads=a.threads, burst=a.burst,
                          inflight=a.inflight, tx_workers=a.tx_workers, queues=a.queues,
