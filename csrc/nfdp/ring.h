@@ -306,6 +306,10 @@ class RingEngine {
   FusedLaunch launch_{};
   RingTableSet* h_sets_ = nullptr;   // [2] table sets (coop rings): pinned coherent host memory
   RingTableSet* d_sets_ = nullptr;   // (its device view)
+  // [2] the grid's copies of the table sets, in HBM: a flip's restage reads them there, not over
+  // PCIe.  Filled at start() (a copy before the launch) and, under a running grid, by the grid
+  // itself through its control mailbox (stage_tables posts the idle set's words)
+  RingTableSet* dd_sets_ = nullptr;
   RingCtrlRing* ctrl_ = nullptr;     // pinned, coherent: the control mailbox
   uint64_t ctrl_head_ = 0;           // (ctrl_mu_) entries posted
   std::mutex ctrl_mu_;

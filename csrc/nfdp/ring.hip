@@ -661,6 +661,8 @@ RingEngine::RingEngine(uint32_t capacity, int num_cus, int wgs_per_cu, bool coop
      "host alloc table sets");
   std::memset(static_cast<void*>(h_sets_), 0, 2 * sizeof(RingTableSet));
   ck(hipHostGetDevicePointer(reinterpret_cast<void**>(&d_sets_), h_sets_, 0), "device ptr table sets");
+  ck(hipMalloc(reinterpret_cast<void**>(&dd_sets_), 2 * sizeof(RingTableSet)), "dev alloc table sets");
+  ck(hipMemset(dd_sets_, 0, 2 * sizeof(RingTableSet)), "memset table sets");
   ck(hipMemset(d_svc_, 0, (size_t)nq_ * nch_ * 4 * kSvcWords), "memset");
   // (the launch stream is created by start() and destroyed by stop(): a resident grid holds its
   // stream's hardware queue, and a stopped ring should not keep one that other streams then share)
@@ -672,7 +674,7 @@ RingEngine::~RingEngine() {
   } catch (...) {
   }
   release_streams();
-  for (void* d : {(void*)st_, (void*)d_svc_}) (void)hipFree(d);
+  for (void* d : {(void*)st_, (void*)d_svc_, (void*)dd_sets_}) (void)hipFree(d);
   (void)hipHostFree(h_sets_);
   if (host_slots_) {
     for (void* h : host_ptrs_) (void)hipHostFree(h);
@@ -708,10 +710,12 @@ void RingEngine::start(const FusedLaunch& f, const LaunchCfg& cfg, double deadli
   s[0].set_serial[1] = h_sets_[1].serial;
   if (!stream_) ck(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "stream");
   ck(hipMemcpyAsync(st_, s.data(), sizeof(RingDevState) * nq_, hipMemcpyHostToDevice, stream_), "state upload");
+  // both table sets into the grid's HBM copies (the host's are current: stage_tables wrote them)
+  ck(hipMemcpyAsync(dd_sets_, h_sets_, 2 * sizeof(RingTableSet), hipMemcpyHostToDevice, stream_), "table sets upload");
   ck(hipStreamSynchronize(stream_), "state upload");  // `s` lives on this stack frame
   RingLaunch r;
   r.f = f;
-  r.sets = d_sets_;
+  r.sets = dd_sets_;
   r.lds_tiles = lds_tiles_;
   r.epoch0 = ep;
   {
@@ -926,9 +930,17 @@ void RingEngine::stage_tables(const FusedLaunch& f, int which) {
   std::memcpy(static_cast<void*>(h_sets_ + which), &ts, sizeof(ts));
   std::atomic_thread_fence(std::memory_order_release);
   if (running_) {
-    // the serial's device mirror, through the running grid, before any flip can name this set
+    // the set itself into the grid's HBM copy, then the serial's device mirror, through the
+    // running grid's control mailbox (no stream: a stream may share a resident grid's hardware
+    // queue), before any flip can name this set.  The grid applies the entries in order and
+    // releases them before it reports them done; the flip comes after that.
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(&ts);
+    const uint32_t nw = sizeof(RingTableSet) / 4;
+    const uint64_t dst = reinterpret_cast<uint64_t>(dd_sets_ + which);
+    for (uint32_t o = 0; o < nw; o += kCtrlWords)
+      (void)post_ctrl(dst + 4ull * o, w + o, std::min<uint32_t>(kCtrlWords, nw - o), 1.0, false);
     const uint64_t seq = post_ctrl(reinterpret_cast<uint64_t>(&st_[0].set_serial[which]), &ts.serial, 1, 1.0, false);
-    if (!wait_ctrl(seq, 1.0)) throw std::runtime_error("ring: table-set serial not applied by the grid");
+    if (!wait_ctrl(seq, 1.0)) throw std::runtime_error("ring: table set not applied by the grid");
   }
   if (running_) {
     // the side pass (RingPath.side_pass) reads the session's tables from launch()
