@@ -44,6 +44,7 @@ class NodeConfig:
     #   "veth"  a veth pair whose host end (`uplink_host_ifname`) the node's stack or a host bridge
     #           with the physical NIC reaches pods through (an OvS internal port's role);
     #   <name>  an existing netdev (the node's data NIC), attached through AF_PACKET rings;
+    #   "memif" a shared-memory wire region (<memif dir>/wire.memif) for a user-space NIC proxy;
     #   "none"  no wire port (pods reach only each other and NF pods)
     uplink: str = "veth"
     uplink_host_ifname: str = "dpuwire"

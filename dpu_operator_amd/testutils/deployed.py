@@ -191,6 +191,114 @@ def run(device: str = "cpu", queues: int = 2, log=None) -> dict:
         shutil.rmtree(root, ignore_errors=True)
 
 
+def run_memif(device: str = "cpu", queues: int = 2, log=None) -> dict:
+    """The same node and checks without kernel netdevs (the GPU box runs tests with no
+    CAP_NET_ADMIN and no user namespaces): the detector's VSP arguments with shared-memory vports
+    and a shared-memory wire (`--vport-kind memif --uplink memif`) on `device`, the VSP's RPCs as
+    the daemon's CNI / OPI paths issue them, and memif endpoints as pods, external host and NF
+    (which forwards what arrives on its ingress vport to its egress vport).  Frames are IPv4 / UDP
+    between the pods' MACs; every check asserts exactly which endpoints receive them, unchanged."""
+    import numpy as np
+
+    from ..cmd import vsp as vspcmd
+    from ..native import nfdp
+    from ..ops import packets as P
+    from ..platform.detectors import Mi355xDetector
+    from ..utils.paths import PathManager
+
+    say = log or (lambda *_: None)
+    nf = nfdp()
+    root = tempfile.mkdtemp(prefix="dpdepm", dir="/tmp")
+    pm = PathManager(root)
+    res: dict = {"device": device, "queues": queues, "vports": "memif"}
+    gvsp = None
+    try:
+        args = list(Mi355xDetector().vsp(True).args)
+        a = vspcmd.parse_args(args + ["--device", device, "--flow-buckets", "4096", "--root", root,
+                                      "--io-queues", str(queues), "--vport-kind", "memif", "--uplink", "memif"])
+        res["vsp_args"] = args + ["--vport-kind", "memif", "--uplink", "memif"]
+        gvsp = vspcmd.build_vsp(a, pm)
+        gvsp.init(True, "gpu")
+        gvsp.set_num_vfs(8)
+        lp = gvsp.livepath
+        res["ring_on_gpu"] = bool(lp.gpu)
+        mac = {i: gvsp.vports[i]["mac"] for i in range(8)}
+        # workload pods on vports 0 / 1 (CreateBridgePort with the vport's own MAC), NF on 2 / 3
+        for i in (0, 1):
+            gvsp.create_bridge_port(f"host0-{i}", bytes.fromhex(mac[i].replace(":", "")), 0, [str(i + 2)])
+        ep = {i: nf.MemifEndpoint(gvsp.vport_path(i)) for i in range(4)}
+        wire = nf.MemifEndpoint(gvsp._wire_vport().path)
+        EXT = "02:ee:00:00:00:01"
+
+        def frames(src, dst, n, sport0):
+            fr, ln = P.craft(n, dmac=dst, smac=src, src_ip=0x0A610001, dst_ip=0x0A610002,
+                             sport=np.arange(n) + sport0, dport=4789 + 1)
+            return [bytes(fr[k, : ln[k]]) for k in range(n)]
+
+        def deliver(sender, fr, want: dict, quiet_s: float = 0.15) -> bool:
+            """send `fr` from endpoint `sender`; True when exactly `want` ({endpoint: frames})
+            arrive (every other endpoint gets nothing)."""
+            every = {**{k: v for k, v in ep.items()}, "wire": wire}
+            for e in every.values():
+                e.recv()
+            assert sender.send(fr) == len(fr)
+            got = {k: [] for k in every}
+            end = time.monotonic() + 10
+            while time.monotonic() < end:
+                for k, e in every.items():
+                    got[k] += e.recv()
+                if all(len(got[k]) >= len(v) for k, v in want.items()):
+                    break
+                time.sleep(0.002)
+            time.sleep(quiet_s)
+            for k, e in every.items():
+                got[k] += e.recv()
+            ok = all(sorted(got[k]) == sorted(want.get(k, [])) for k in every)
+            if not ok:
+                say("mismatch", {k: (len(got[k]), len(want.get(k, []))) for k in every})
+            return ok
+
+        f01 = frames(mac[0], mac[1], 64, 1000)
+        res["pod_pod"] = deliver(ep[0], f01, {1: f01}) and deliver(ep[1], frames(mac[1], mac[0], 64, 2000),
+                                                                      {0: frames(mac[1], mac[0], 64, 2000)})
+        # an unknown destination floods (wire first, then the other VFs); the external host's reply
+        # teaches the wire port its MAC, after which pod -> external is forwarded to the wire only
+        fx = frames(mac[0], EXT, 8, 3000)
+        res["pod_ext_flood"] = deliver(ep[0], fx, {"wire": fx, 1: fx})
+        fr = frames(EXT, mac[0], 8, 4000)
+        res["ext_pod"] = deliver(wire, fr, {0: fr})
+        lp.flush_learning()
+        time.sleep(0.05)
+        fx2 = frames(mac[0], EXT, 32, 5000)
+        res["pod_ext_learned"] = deliver(ep[0], fx2, {"wire": fx2})
+        # the SFC's network function on vports 2 (in) / 3 (out)
+        gvsp.create_network_function(mac[2], mac[3])
+        fn = frames(mac[0], EXT, 32, 6000)
+        res["pod_to_nf_in"] = deliver(ep[0], fn, {2: fn})
+        res["nf_out_to_ext"] = deliver(ep[3], fn, {"wire": fn})         # the NF passed them on
+        fb = frames(EXT, mac[1], 16, 7000)
+        res["ext_to_nf_out"] = deliver(wire, fb, {3: fb})
+        res["nf_in_to_pod"] = deliver(ep[2], fb, {1: fb})              # (NF-in bridge, pod MAC) -> VF
+        fp = frames(mac[0], mac[1], 16, 8000)
+        res["nf_pod_pod_via_nf"] = deliver(ep[0], fp, {2: fp})          # pod -> pod enters the NF too
+        res["nf_hairpin"] = deliver(ep[3], fp, {3: fp})                # NF-out, dst pod MAC: hairpin
+        gvsp.delete_network_function(mac[2], mac[3])
+        fz = frames(mac[0], mac[1], 16, 9000)
+        res["after_nf_del"] = deliver(ep[0], fz, {1: fz})
+        st = lp.stats
+        res["engine"] = {k: int(st.get(k, 0)) for k in ("rx", "tx", "drop", "replicas", "learn_events", "queues")}
+        res["error"] = lp.error
+        checks = ["pod_pod", "pod_ext_flood", "ext_pod", "pod_ext_learned", "pod_to_nf_in", "nf_out_to_ext",
+                  "ext_to_nf_out", "nf_in_to_pod", "nf_pod_pod_via_nf", "nf_hairpin", "after_nf_del"]
+        res["checks"] = checks
+        res["ok"] = all(bool(res.get(k)) for k in checks) and lp.error is None
+        return res
+    finally:
+        if gvsp is not None:
+            gvsp.stop_live()
+        shutil.rmtree(root, ignore_errors=True)
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(prog="deployed")
     ap.add_argument("--device", default="cpu")

@@ -156,7 +156,8 @@ class GpuVsp(VspBase):
         # live mode: the wire port (WIRE_PORT).  A vport spec (netio.TapPort, native_io.PacketVport /
         # MemifVport, anything with a packet fd), or a string resolved at Init: "veth" (a veth pair
         # whose host end, `uplink_host_ifname`, the node reaches pods through), "none", or the
-        # name of an existing netdev (the node's data NIC) attached through AF_PACKET rings
+        # name of an existing netdev (the node's data NIC) attached through AF_PACKET rings, or
+        # "memif" (a shared-memory wire region next to the memif vports)
         self.uplink = uplink
         self._uplink_vp = None                  # the resolved wire vport (closed with the live path)
         self.port_state: dict[int, tuple[bool, bool, int]] = {}  # port -> (link, rx, mtu) from the agent
@@ -318,6 +319,14 @@ class GpuVsp(VspBase):
             self._uplink_vp = up
         elif up in ("", "none"):
             return None
+        elif up == "memif":
+            # a shared-memory wire: the external side (a DPDK-memif NIC proxy, a test) attaches to
+            # <memif_dir>/wire.memif
+            from ..dataplane.native_io import MemifVport, memif_dir
+
+            d = self.memif_dir or memif_dir()
+            os.makedirs(d, exist_ok=True)
+            self._uplink_vp = MemifVport(os.path.join(d, "wire.memif"), ring_size=4096)
         elif up == "veth":
             from ..dataplane.native_io import PacketVport
 

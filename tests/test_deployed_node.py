@@ -4,10 +4,13 @@ the node daemon, device plugin and CNI; netns pods and an external host; pod <->
 pod <-> external, an SFC network-function pod (pod -> NF -> external, NF -> external, pod <-> NF)
 — the reference's e2e traffic suite (e2e_test/e2e_test.go:399-512) on one node.
 
-On CPU the data plane is the bit-exact oracle; the `gpu` test runs the same scenario with the
-resident ring kernel on cuda:0.  Namespaces need CAP_NET_ADMIN: the GPU box runs tests as an
-ordinary user, so there the scenario runs in a child process in a user + network + mount
-namespace of its own (`unshare -Urnm`), which has it."""
+On CPU the data plane is the bit-exact oracle; the `gpu` tests run with the resident ring kernel
+on cuda:0.  Namespaces need CAP_NET_ADMIN: where the tests run as an ordinary user the netns
+scenario runs in a child process in a user + network + mount namespace of its own
+(`unshare -Urnm`).  The MI355X box of this pool has neither (uid nobody, no capabilities,
+user.max_user_namespaces = 0: profiles/r5_s1_box_probe.txt), so there the same VSP arguments run
+with shared-memory vports and a shared-memory wire (`run_memif`: the same pod / NF / external
+checks, frames asserted per endpoint) in front of the GPU ring."""
 import json
 import os
 import shutil
@@ -76,4 +79,31 @@ def test_deployed_node_traffic_on_the_gpu_ring():
     else:
         pytest.skip("no CAP_NET_ADMIN and no user namespaces")
     _check(res)
+    assert res["ring_on_gpu"]
+
+
+def _check_memif(res: dict) -> None:
+    assert {"--live", "native", "all", "--uplink"} <= set(res["vsp_args"])
+    failed = [k for k in res["checks"] if not res.get(k)]
+    assert not failed, (failed, res)
+    assert res["error"] is None and res["ok"] and res["engine"]["learn_events"] >= 1
+
+
+def test_deployed_node_memif_cpu_oracle():
+    from dpu_operator_amd.testutils import deployed
+
+    res = deployed.run_memif("cpu")
+    _check_memif(res)
+    assert not res["ring_on_gpu"]
+
+
+@pytest.mark.gpu
+def test_deployed_node_memif_on_the_gpu_ring():
+    """The detector's VSP (memif vports, memif wire) in front of the resident ring on cuda:0:
+    pod <-> pod, flooding then learning on the wire, pod -> NF -> external, external -> NF -> pod,
+    the NF hairpin, and the plain bridge again after the NF is gone."""
+    from dpu_operator_amd.testutils import deployed
+
+    res = deployed.run_memif("cuda:0")
+    _check_memif(res)
     assert res["ring_on_gpu"]
