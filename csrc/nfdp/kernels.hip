@@ -45,6 +45,9 @@ constexpr uint32_t kFlagPairs = 1u << 10;      // launch flag: the batch may hol
 #define NFDP_FUSED_WAVES_PER_EU 4
 #endif
 constexpr int kFB = NFDP_FUSED_BLOCK;
+#ifndef NFDP_KARG_RELOAD
+#define NFDP_KARG_RELOAD 1
+#endif
 constexpr int kFWaves = kFB / 64;
 
 struct FusedArgs {
@@ -227,13 +230,32 @@ __global__ __launch_bounds__(kFB, EARLY ? NFDP_EARLY_WAVES_PER_EU : NFDP_FUSED_W
   const __amdgpu_buffer_rsrc_t r_list = __builtin_amdgcn_make_buffer_rsrc(
       (void*)a.steer_list, (short)0, LIST ? (int)(gridDim.x * a.steer_cap_blk * 4u) : 0, kBufCfg);
   uint32_t it = 0;  // loop iteration (REMOTE reservation buffers alternate)
+#if NFDP_KARG_RELOAD
+  // The tables' bases and sizes are read where a stage uses them, from the kernel's argument
+  // block (constant address space: scalar loads that hit the scalar cache), through a pointer
+  // laundered once per iteration so the loads cannot be hoisted out of the loop.  Hoisted, the
+  // ~75 dwords of TablesView stay live in SGPRs across the whole loop and the allocator spills
+  // ~330 of them into VGPR lanes (v_writelane / v_readlane: VALU work and VGPRs the hot instance
+  // does not have).
+  typedef const __attribute__((address_space(4))) FusedArgs KArgs;
+  KArgs* const kargs0 = (KArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+#endif
   for (uint32_t base = blockIdx.x * kFB; base < n; base += stride, ++it) {
     const uint32_t i = base + threadIdx.x;
     const bool valid = i < n;
+#if NFDP_KARG_RELOAD
+    KArgs* ka = kargs0;
+    asm volatile("" : "+s"(ka));
+    const TablesView& TV = *(const TablesView*)&ka->t;
+    const LdsTables ta_it{TV, ta.lport, ta.lchain, ta.lperm, ta.nport, ta.nchain, ta.lds_perm};
+#else
+    const TablesView& TV = a.t;
+    const LdsTables& ta_it = ta;
+#endif
     wave_frames_to_lanes(kx, cn, dn);
     Parsed p;
     IngressState st;
-    ingress_stage<LdsTables, false>(a.t, ta, dn, imn, p, st);  // copies the frame into p.s: dn is free for the prefetch
+    ingress_stage<LdsTables, false>(TV, ta_it, dn, imn, p, st);  // copies the frame into p.s: dn is free for the prefetch
     // IPv6 keys (tables with IPv6 flows / rules): v6_kernel folded them into out[i] (overwritten
     // by this lane's egress slot in the tail)
     if constexpr (V6) {
@@ -244,7 +266,7 @@ __global__ __launch_bounds__(kFB, EARLY ? NFDP_EARLY_WAVES_PER_EU : NFDP_FUSED_W
         }
       }
     }
-    const bool flowp = V6 ? flowable(a.t, p) : p.ipv4;   // takes part in the flow stage
+    const bool flowp = V6 ? flowable(TV, p) : p.ipv4;   // takes part in the flow stage
     // (a continuation slot of a wide header pair is bad_port here - in-meta port kPortCont;
     // pair_fix_kernel turns its meta / counters into kCont afterwards: no pair code in this loop)
 
@@ -255,10 +277,10 @@ __global__ __launch_bounds__(kFB, EARLY ? NFDP_EARLY_WAVES_PER_EU : NFDP_FUSED_W
     uint4 bv[8];
     if constexpr (EARLY) {
       // the bucket fetch leaves as soon as the hash is known: its latency runs under the ACL
-      auto issue = [&](uint32_t h) { flow_probe_issue(a.t, h, bv); };
-      classify_wave<HASH, ACL, decltype(issue), true>(st.key, kx, av, lt, ltab, a.t, hash, acl_rule, 0, 1, nullptr, issue);
+      auto issue = [&](uint32_t h) { flow_probe_issue(TV, h, bv); };
+      classify_wave<HASH, ACL, decltype(issue), true>(st.key, kx, av, lt, ltab, TV, hash, acl_rule, 0, 1, nullptr, issue);
     } else {
-      classify_wave<HASH, ACL>(st.key, kx, av, lt, ltab, a.t, hash, acl_rule);
+      classify_wave<HASH, ACL>(st.key, kx, av, lt, ltab, TV, hash, acl_rule);
     }
     // IPv6: the rule comes from the IPv6 TCAM (v6_kernel ran over this batch), never from the
     // IPv4 rules over the folded key (wave-uniform skip for all-IPv4 waves)
@@ -305,12 +327,12 @@ __global__ __launch_bounds__(kFB, EARLY ? NFDP_EARLY_WAVES_PER_EU : NFDP_FUSED_W
 #ifndef NFDP_LANE_PROBE
     {
       uint4 v;
-      if constexpr (EARLY) slot = flow_probe_finish(a.t, st.key, hash, !st.reason && flowp, kx, bv, v);
-      else slot = flow_probe_wave(a.t, st.key, hash, !st.reason && flowp, kx, v);
+      if constexpr (EARLY) slot = flow_probe_finish(TV, st.key, hash, !st.reason && flowp, kx, bv, v);
+      else slot = flow_probe_wave(TV, st.key, hash, !st.reason && flowp, kx, v);
 #else
     if (!st.reason && flowp) {
       uint4 v;
-      slot = flow_probe(a.t, st.key, hash, v);
+      slot = flow_probe(TV, st.key, hash, v);
 #endif
       // an IPv6 folded-key hit counts only if the slot's side entry holds this packet's addresses:
       // v6_kernel checked that before this kernel (bit 31 of the word it parked in out_meta[i])
@@ -322,7 +344,7 @@ __global__ __launch_bounds__(kFB, EARLY ? NFDP_EARLY_WAVES_PER_EU : NFDP_FUSED_W
       }
     }
 #ifndef NFDP_ABL_NO_CHAIN
-    const EgressDecision e = chain_stage<LdsTables, V6>(a.t, ta, p, st, hit, act, acl_rule, hash);
+    const EgressDecision e = chain_stage<LdsTables, V6>(TV, ta_it, p, st, hit, act, acl_rule, hash);
 #else  // cost attribution only (wrong results): no chain, the flow's port
     EgressDecision e{};
     e.out_port = hit ? act.out_port : kPortNone;
@@ -334,7 +356,7 @@ __global__ __launch_bounds__(kFB, EARLY ? NFDP_EARLY_WAVES_PER_EU : NFDP_FUSED_W
     if constexpr (REMOTE) {
       // egress GPU of the frame (or the flow owner when steering); block-aggregated slot in that
       // GPU's segment (all threads call)
-      eg = a.steer ? owner : (e.reason ? a.rank : (uint32_t)ta.port(e.out_port).gpu);
+      eg = a.steer ? owner : (e.reason ? a.rank : (uint32_t)ta_it.port(e.out_port).gpu);
       const bool remote = a.steer ? to_owner : (valid && !e.reason && eg != a.rank && eg < a.nranks);
       pos = reserve_block(a.pcnt, eg, remote, a.nranks, rcnt + (it & 1u) * kMaxRanks, rbase,
                           rcnt + (~it & 1u) * kMaxRanks);

@@ -1,0 +1,76 @@
+"""Interleaved A/B of build variants of the headline kernel, one process per measurement.
+
+Two builds of `_nfdp` cannot share a process (one module name), so each measurement is a child
+process that loads one variant (NFDP_EXT_DIR, native/build.py NFDP_BUILD_OUT) and times the
+headline step (1M flows, ACL 256 -> SNAT -> L2, 4M-packet batches) with HIP events; variants
+alternate round by round so box drift hits them equally.
+
+python tools/ab_variants.py base= variants/noreload [--rounds 4] [--iters 50]
+  (an empty directory means the in-tree build)
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+
+CHILD = r'''
+import json, sys, numpy as np, torch
+sys.path.insert(0, ".")
+from dpu_operator_amd.dataplane import scenario as S
+from dpu_operator_amd.dataplane.engine import DataPlane
+iters, batch, acl = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3]
+g = DataPlane(device="cuda", flow_buckets=1 << 19, hash_mode="lds", acl_mode="mfma")
+sc = S.build_sfc(g, n_pods=8, n_flows=1 << 20, n_acl=256, seed=0)
+if acl == "wild":
+    S.install_acl_wild(g)
+g.commit(full=True)
+bs = []
+for r in range(4):
+    pk, im = S.traffic(sc, batch, seed=1 + r)
+    bs.append((torch.from_numpy(pk).cuda(), torch.from_numpy(im.view(np.int32)).cuda()))
+out, meta, lat = g.alloc_batch(batch)
+for k in range(10):
+    g.run(*bs[k % 4], out, meta, lat)
+torch.cuda.synchronize()
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+e0.record()
+for k in range(iters):
+    g.run(*bs[k % 4], out, meta, lat)
+e1.record()
+torch.cuda.synchronize()
+ms = e0.elapsed_time(e1) / iters
+print(json.dumps({"ms": ms, "mpps": batch / ms / 1e3}))
+'''
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("variants", nargs="+", help="name=dir (dir empty: in-tree build)")
+    ap.add_argument("--rounds", type=int, default=4)
+    ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--batch", type=int, default=1 << 22)
+    ap.add_argument("--acl", default="256", choices=["256", "wild"])
+    a = ap.parse_args()
+    vs = [v.split("=", 1) if "=" in v else (os.path.basename(v), v) for v in a.variants]
+    res = {n: [] for n, _ in vs}
+    for r in range(a.rounds):
+        for n, d in vs:
+            env = dict(os.environ)
+            env.pop("NFDP_EXT_DIR", None)
+            if d:
+                env["NFDP_EXT_DIR"] = os.path.abspath(d)
+            p = subprocess.run([sys.executable, "-c", CHILD, str(a.iters), str(a.batch), a.acl], env=env,
+                               capture_output=True, text=True, timeout=300)
+            line = [x for x in p.stdout.splitlines() if x.startswith("{")]
+            if not line:
+                print(json.dumps({"variant": n, "error": p.stderr[-1500:]}), flush=True)
+                sys.exit(1)
+            res[n].append(json.loads(line[-1])["mpps"])
+            print(json.dumps({"round": r, "variant": n, "mpps": round(res[n][-1], 1)}), flush=True)
+    print(json.dumps({"summary": {n: {"median_mpps": round(sorted(v)[len(v) // 2], 1), "all": [round(x, 1) for x in v]}
+                                  for n, v in res.items()}, "acl": a.acl, "batch": a.batch}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
