@@ -38,7 +38,7 @@ import time
 import numpy as np
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-import dpu_operator_amd  # noqa: E402,F401  (HIP queue settings before torch starts HIP)
+import dpu_operator_amd  # noqa: E402,F401
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)

@@ -1,15 +1,6 @@
-import os as _os
+"""dpu-operator on MI355X: control plane (Python) + HIP/CDNA4 data plane (native extensions).
 
-# Persistent ring kernels hold their HIP stream's hardware queue for good.  HIP maps streams
-# round-robin onto GPU_MAX_HW_QUEUES queues per device (4 by default), so a stream sharing a ring's
-# queue (the default stream's copies, a learn or staging stream, a second plane's ring on the same
-# GPU) would wait behind the resident grid forever.  Enough queues for every ring, its side streams
-# and the default stream; effective when set before HIP starts (any entry point importing this
-# package first: bench.py, the VSP, the tests' conftest).  A lower value from the environment
-# (e.g. HIP's default written out as 4) is raised too: fewer queues can deadlock the live path.
-try:
-    _hwq = int(_os.environ.get("GPU_MAX_HW_QUEUES", "0"))
-except ValueError:
-    _hwq = 0
-if _hwq < 16:
-    _os.environ["GPU_MAX_HW_QUEUES"] = "16"
+The package leaves the HIP runtime's settings to its operator (GPU_MAX_HW_QUEUES included): the
+resident ring grids and the streams around them are built to run within HIP's default queue
+count (tests/test_ring_gpu.py runs the live paths with GPU_MAX_HW_QUEUES=4 set explicitly).
+"""

@@ -6,7 +6,7 @@ import pytest
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if REPO not in sys.path:
     sys.path.insert(0, REPO)
-import dpu_operator_amd  # noqa: E402,F401  (HIP queue settings before the first HIP call below)
+import dpu_operator_amd  # noqa: E402,F401
 
 
 def pytest_configure(config):
