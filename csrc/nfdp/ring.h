@@ -266,7 +266,8 @@ class RingEngine {
 
  private:
   bool chunk_done(uint64_t chunk, uint32_t q) const;
-  void release_streams();   // after the grid exited: the launch stream goes
+  void release_streams();
+  void create_stream();   // after the grid exited: the launch stream goes
   void set_running(bool on);   // running_, and the process-wide count of running grids
   void pace_epoch_change();
   // (mu_ held) a new epoch for every queue: each queue's flip point is its published count now

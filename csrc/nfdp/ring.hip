@@ -1,6 +1,9 @@
 // ring.hip — persistent ring kernel + host engine (see ring.h for the protocol).
 #include "ring.h"
 
+#include <cstdlib>
+#include <string>
+
 #include <immintrin.h>
 
 #include <chrono>
@@ -708,7 +711,7 @@ void RingEngine::start(const FusedLaunch& f, const LaunchCfg& cfg, double deadli
   }
   s[0].set_serial[0] = h_sets_[0].serial;
   s[0].set_serial[1] = h_sets_[1].serial;
-  if (!stream_) ck(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "stream");
+  if (!stream_) create_stream();
   ck(hipMemcpyAsync(st_, s.data(), sizeof(RingDevState) * nq_, hipMemcpyHostToDevice, stream_), "state upload");
   // both table sets into the grid's HBM copies (the host's are current: stage_tables wrote them)
   ck(hipMemcpyAsync(dd_sets_, h_sets_, 2 * sizeof(RingTableSet), hipMemcpyHostToDevice, stream_), "table sets upload");
@@ -807,6 +810,29 @@ void RingEngine::stop(double timeout_s) {
   set_running(false);   // (after the stream is gone: a deferred unmap may run now)
   for (uint32_t q = 0; q < nq_; ++q)
     if (completed(q) != published(q)) throw std::runtime_error("ring: stopped with published chunks unprocessed");
+}
+
+// The resident grid's stream.  NFDP_RING_STREAM picks how it is made (A/B of queue placement under
+// GPU_MAX_HW_QUEUES): "plain" (a non-blocking stream: HIP maps it round-robin onto the process's
+// hardware queues), "cumask" (hipExtStreamCreateWithCUMask over every CU: a CU mask is a queue
+// property, so the runtime gives the stream a queue of its own) or "prio" (highest priority).
+void RingEngine::create_stream() {
+  const char* m = std::getenv("NFDP_RING_STREAM");
+  const std::string mode = m ? m : "plain";
+  if (mode == "cumask") {
+    int dev = 0, cus = 0;
+    ck(hipGetDevice(&dev), "device");
+    ck(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev), "CU count");
+    std::vector<uint32_t> mask((size_t)(cus + 31) / 32, 0xFFFFFFFFu);
+    if (cus % 32) mask.back() = (1u << (cus % 32)) - 1u;
+    ck(hipExtStreamCreateWithCUMask(&stream_, (uint32_t)mask.size(), mask.data()), "stream (CU mask)");
+  } else if (mode == "prio") {
+    int lo = 0, hi = 0;
+    ck(hipDeviceGetStreamPriorityRange(&lo, &hi), "stream priorities");
+    ck(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, hi), "stream (priority)");
+  } else {
+    ck(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking), "stream");
+  }
 }
 
 void RingEngine::release_streams() {
