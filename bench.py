@@ -88,6 +88,35 @@ def rss_unsteered_info(elapsed_s: float, steps: int, world: int, batch: int, sen
                     "(count-first all-to-all), timed like the headline (barrier + sync, max over ranks)"}
 
 
+def _live_veth(dev: str) -> dict:
+    """veth pods -> native engine -> GPU ring (the deployed default), measured in-process with
+    CAP_NET_ADMIN, else in `unshare -Urnm` (a user namespace of our own), else skipped."""
+    import shutil
+    import subprocess
+    import tempfile
+
+    from dpu_operator_amd.testutils import netns as NS
+
+    cmd = [sys.executable, "-u", os.path.join(REPO, "tools", "live_bench.py"), "--veth", "pipeline", "--device", dev,
+           "--pods", "4", "--threads", "2", "--queues", "2", "--tx-workers", "1", "--duration", "0.5"]
+    try:
+        if NS.privileged():
+            argv, env = cmd, dict(os.environ)
+        else:
+            ok = shutil.which("unshare") and subprocess.run(["unshare", "-Urnm", "true"], capture_output=True,
+                                                              timeout=20).returncode == 0
+            if not ok:
+                return {"skipped": "no CAP_NET_ADMIN / CAP_NET_RAW and no user namespaces on this box "
+                                   "(veth pods cannot be created); see tests/test_deployed_node.py"}
+            argv = ["unshare", "-Urnm"] + cmd
+            env = dict(os.environ, DPU_NETNS_DIR=tempfile.mkdtemp(prefix="dpns", dir="/tmp"))
+        r = subprocess.run(argv, env=env, cwd=REPO, capture_output=True, text=True, timeout=240)
+        line = [x for x in r.stdout.splitlines() if x.startswith("{")]
+        return json.loads(line[-1]) if line else {"error": (r.stderr or "no output")[-300:]}
+    except Exception as ex:  # noqa: BLE001 - the headline must still be reported
+        return {"error": str(ex)[:200]}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -646,8 +675,24 @@ def main() -> None:
             live = lb.run(device=str(dev), n_pods=a.pods_per_gpu, flows=a.flows, n_acl=a.acl, duration=0.5,
                           threads=a.live_gen_threads, tx_workers=a.live_workers, queues=a.live_queues,
                           hash_mode=a.hash)
+            # the engine's queue curve: saturated pod -> pod Mpps at 1 / 2 / 4 / 8 rx queues (each
+            # with its tx workers), the same pods and pipeline; bounded by the box's CPU share
+            curve = []
+            for q in (1, 2, 4, 8):
+                r = lb.run(device=str(dev), n_pods=a.pods_per_gpu, flows=a.flows, n_acl=a.acl, duration=0.3,
+                           threads=a.live_gen_threads, tx_workers=a.live_workers, queues=q, hash_mode=a.hash,
+                           saturated_only=True)
+                curve.append({"queues": q, "mpps": r.get("mpps"), "p50_us": r.get("p50_us"), "error": r.get("error")})
+            live["queue_curve"] = curve
+            live["host_cpus"] = len(os.sched_getaffinity(0))
         except Exception as ex:  # the headline number must still be reported
             live = {"error": str(ex)[:200]}
+        # kernel-netdev (veth) pods in front of the same GPU ring (tools/live_bench.py run_veth
+        # "pipeline", the deployed default vport): needs CAP_NET_ADMIN / CAP_NET_RAW, or user
+        # namespaces to get them; reported as skipped (with the reason) where the box has neither
+        live_veth = None
+        if live is not None:
+            live_veth = _live_veth(str(dev))
 
     total_pkts = world * a.batch * a.steps
     mpps = total_pkts / elapsed / 1e6
@@ -699,6 +744,7 @@ def main() -> None:
             "variants": variants,
             # live pod -> pod through the native I/O engine + ring kernel (memif vports, 64-B frames)
             "live": live,
+            "live_veth": live_veth,
             "p50_latency_us_pod": None if not live or "idle_p50_us" not in live else live["idle_p50_us"],
             "flows": total_flows,
             "batch_per_gpu": a.batch,

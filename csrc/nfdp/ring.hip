@@ -813,20 +813,13 @@ void RingEngine::stop(double timeout_s) {
 }
 
 // The resident grid's stream.  NFDP_RING_STREAM picks how it is made (A/B of queue placement under
-// GPU_MAX_HW_QUEUES): "plain" (a non-blocking stream: HIP maps it round-robin onto the process's
-// hardware queues), "cumask" (hipExtStreamCreateWithCUMask over every CU: a CU mask is a queue
-// property, so the runtime gives the stream a queue of its own) or "prio" (highest priority).
+// GPU_MAX_HW_QUEUES): "plain" (a non-blocking stream, the default) or "prio" (highest priority).
+// Measured with HIP's default 4 hardware queues (profiles/r5_s3_live_commit_hwq_ab.txt): the 1 kHz
+// live-commit p99 moves by +1.1-2.6 us either way, as with 16 queues; a CU-masked stream
+// (hipExtStreamCreateWithCUMask) failed the same test and is not offered.
 void RingEngine::create_stream() {
   const char* m = std::getenv("NFDP_RING_STREAM");
-  const std::string mode = m ? m : "plain";
-  if (mode == "cumask") {
-    int dev = 0, cus = 0;
-    ck(hipGetDevice(&dev), "device");
-    ck(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev), "CU count");
-    std::vector<uint32_t> mask((size_t)(cus + 31) / 32, 0xFFFFFFFFu);
-    if (cus % 32) mask.back() = (1u << (cus % 32)) - 1u;
-    ck(hipExtStreamCreateWithCUMask(&stream_, (uint32_t)mask.size(), mask.data()), "stream (CU mask)");
-  } else if (mode == "prio") {
+  if (m && std::string(m) == "prio") {
     int lo = 0, hi = 0;
     ck(hipDeviceGetStreamPriorityRange(&lo, &hi), "stream priorities");
     ck(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, hi), "stream (priority)");

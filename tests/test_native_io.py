@@ -249,7 +249,9 @@ def test_live_commits_at_1khz_under_traffic(tmp_path):
     """CreateBridgePort-style port edits, ACL edits and agent link flaps committed at ~1 kHz while
     pods send through the GPU live path: every commit is a live table-set flip under the running
     ring (no pause, no drain), nothing is lost, and the one-way p99 with the churn stays within
-    50 us of the p99 without it."""
+    10 us of the p99 without it (the table sets are in HBM: a flip's restage never crosses PCIe;
+    +1.1 to +2.6 us measured, profiles/r5_s3_live_commit_hwq_ab.txt).  One re-measurement of both
+    runs is allowed: a single host-scheduling stall of the 1-s run is not the commit's cost."""
     import threading
 
     nf = nfdp()
@@ -263,7 +265,6 @@ def test_live_commits_at_1khz_under_traffic(tmp_path):
             slots, im = S.traffic(sc, 512, seed=30 + i, src_pods=np.array([i]))
             pods.append((str(tmp_path / f"k{i}"), slots, (im >> 16).astype(np.uint32)))
         kw = dict(duration_s=1.0, warmup_s=0.1, threads=2, burst=4, rate_pps=4e5)
-        base = nf.trafgen_run(pods, **kw)
         stop, err, n = threading.Event(), [], [0]
         flips0 = dp.flip_stats.get("table_flips", 0)
 
@@ -284,20 +285,31 @@ def test_live_commits_at_1khz_under_traffic(tmp_path):
             except Exception as e:  # noqa: BLE001
                 err.append(e)
 
-        th = threading.Thread(target=control)
-        th.start()
-        churn = nf.trafgen_run(pods, **kw)
-        stop.set()
-        th.join()
-        assert not err, err
-        flips = dp.flip_stats.get("table_flips", 0) - flips0
-        b99, c99 = np.percentile(base["lat_us"], 99), np.percentile(churn["lat_us"], 99)
-        print(f"live commits {n[0]} in 1 s ({flips} table flips); one-way p50/p99 us: without "
-              f"{np.percentile(base['lat_us'], 50):.1f}/{b99:.1f}, with {np.percentile(churn['lat_us'], 50):.1f}/{c99:.1f}")
-        assert n[0] >= 300 and flips >= n[0] - 1          # every commit a live flip: nothing paused
-        assert live.error is None and churn["bad"] == 0
-        assert churn["received"] >= 0.99 * churn["sent"]
-        assert c99 < b99 + 50.0
+        def measure():
+            base = nf.trafgen_run(pods, **kw)
+            stop.clear()
+            n[0] = 0
+            f0 = dp.flip_stats.get("table_flips", 0)
+            th = threading.Thread(target=control)
+            th.start()
+            churn = nf.trafgen_run(pods, **kw)
+            stop.set()
+            th.join()
+            assert not err, err
+            flips = dp.flip_stats.get("table_flips", 0) - f0
+            b99, c99 = np.percentile(base["lat_us"], 99), np.percentile(churn["lat_us"], 99)
+            print(f"live commits {n[0]} in 1 s ({flips} table flips); one-way p50/p99 us: without "
+                  f"{np.percentile(base['lat_us'], 50):.1f}/{b99:.1f}, with {np.percentile(churn['lat_us'], 50):.1f}/{c99:.1f}")
+            assert n[0] >= 300 and flips >= n[0] - 1          # every commit a live flip: nothing paused
+            assert live.error is None and churn["bad"] == 0
+            assert churn["received"] >= 0.99 * churn["sent"]
+            return b99, c99
+
+        b99, c99 = measure()
+        if not c99 < b99 + 10.0:
+            b99, c99 = measure()
+        assert c99 < b99 + 10.0
+        assert dp.flip_stats.get("table_flips", 0) > flips0
     finally:
         live.stop()
 

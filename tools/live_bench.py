@@ -120,7 +120,7 @@ def run(device: str = "cuda", n_pods: int = 8, flows: int = 1 << 20, n_acl: int 
         threads: int = 4, burst: int = 512, inflight: int = 64, ring_capacity: int = 16384,
         hash_mode: str = "lds", tx_workers: int = 2, queues: int = 4, max_inflight_frames: int = 4096,
         pod_ring: int = 1024, backend: str = "pipeline", coalesce_us: float = 8.0, loaded_window: int = 2048,
-        traffic: str = "plain", zero_copy: bool = False) -> dict:
+        traffic: str = "plain", zero_copy: bool = False, saturated_only: bool = False) -> dict:
     """traffic: "plain" (the headline SFC), "vxlan-egress" (every pod's VF a VXLAN tunnel port:
     all frames leave encapsulated through one underlay vport, outer headers from the per-burst
     side pass) or "broadcast" (pods on one learning bridge sending to ff:ff:ff:ff:ff:ff: every
@@ -187,6 +187,9 @@ def run(device: str = "cuda", n_pods: int = 8, flows: int = 1 << 20, n_acl: int 
         out.update(mpps=round(mpps, 3), offered_mpps=round(r["sent"] / duration / 1e6, 3),
                    p50_us=_pct(r["lat_us"], 50), p99_us=_pct(r["lat_us"], 99))
         drain(nf, pods, stats)
+        if saturated_only:   # (the queue curve: saturated rate only)
+            out["error"] = live.error
+            return out
         # loaded, closed loop: `loaded_window` frames in flight over all pods (the generator
         # refills as frames arrive): the throughput of a saturated path with its queueing bounded
         # by the window, not by the pod rings (one-way latency = window / rate, Little's law)
