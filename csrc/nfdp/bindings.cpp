@@ -252,6 +252,8 @@ PYBIND11_MODULE(_nfdp, m) {
       .def("take_moves", &FlowTableHost::take_moves)
       .def("clear_dirty", &FlowTableHost::clear_dirty);
 
+  m.def("deferred_host_unmaps", &deferred_host_unmaps,
+        "zero-copy host regions waiting for every ring grid of the process to stop before they unregister");
   m.def("toeplitz", [](U32Arr keys, py::bytes rss) {
     std::string s = rss;
     if (s.size() < 20) throw std::invalid_argument("rss key must be >= 20 bytes");

@@ -245,7 +245,8 @@ __global__ __launch_bounds__(kFB, EARLY ? NFDP_EARLY_WAVES_PER_EU : NFDP_FUSED_W
     const bool valid = i < n;
 #if NFDP_KARG_RELOAD
     KArgs* ka = kargs0;
-    asm volatile("" : "+s"(ka));
+    // (the LIST instances keep their hoisted bases: laundered, their VGPR spills grew 16 -> 19)
+    if constexpr (!LIST) asm volatile("" : "+s"(ka));
     const TablesView& TV = *(const TablesView*)&ka->t;
     const LdsTables ta_it{TV, ta.lport, ta.lchain, ta.lperm, ta.nport, ta.nchain, ta.lds_perm};
 #else

@@ -322,6 +322,9 @@ class RingEngine {
 // hipHostUnregister(p), then after(), once no ring of this process is running (at once if none
 // is): the unregistration waits for the device, which a resident grid never leaves idle.
 void host_unregister_when_idle(void* p, std::function<void()> after);
+// Host regions whose unregistration waits for every ring grid of the process to stop (zero-copy
+// memif vports removed while rings run): the live path restarts its rings when they pile up.
+size_t deferred_host_unmaps();
 
 // Launch the persistent kernel (ring.hip).  Exposed for the engine only.
 struct RingLaunch {

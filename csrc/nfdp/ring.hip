@@ -766,6 +766,11 @@ void drain_unmaps(std::vector<std::pair<void*, std::function<void()>>>& v) {
 }
 }  // namespace
 
+size_t deferred_host_unmaps() {
+  std::lock_guard<std::mutex> g(g_grid_mu);
+  return g_unmaps.size();
+}
+
 void host_unregister_when_idle(void* p, std::function<void()> after) {
   std::vector<std::pair<void*, std::function<void()>>> now;
   {

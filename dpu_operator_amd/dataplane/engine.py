@@ -11,6 +11,9 @@ and harvested (read + reset) before any update batch that moves entries.
 """
 from __future__ import annotations
 
+import contextlib
+import threading
+
 import os
 import time
 from dataclasses import dataclass, field
@@ -58,6 +61,7 @@ class DataPlane:
         num_cus: int | None = None,
         rss_key: bytes = T.RSS_KEY,
     ):
+        self._commit_lock = threading.RLock()   # commits vs the live path's maintenance restarts
         self.nf = _nfdp_mod()
         self.device = device
         self.gpu = device != "cpu"
@@ -167,6 +171,10 @@ class DataPlane:
         updates the tables and relaunches them (their small tables are staged in LDS at launch).
         `_hooks=False`: the caller (MultiDataPlane) runs the engine hooks once for all planes."""
         FAULTS.check("dataplane.commit")
+        with self._commit_lock:
+            return self._commit_locked(full, _hooks)
+
+    def _commit_locked(self, full: bool, _hooks: bool) -> dict:
         hooks = list(getattr(self, "_io_hooks", ())) if _hooks else []
         rings = self._running_rings()
         plan = self._live_plan(rings, full)
@@ -888,6 +896,20 @@ class GraphedRun:
                               non_blocking=True)
         self.graph.replay()
         return BatchResult(self.out, self.meta, self.n, {"lat": self.lat})
+
+
+@contextlib.contextmanager
+def commit_guard(planes):
+    """Hold every plane's commit lock (a fixed order: no inversion between two holders): no
+    commit runs while a live path rebuilds the rings its commits would flip."""
+    locks = [p._commit_lock for p in sorted({id(p): p for p in planes}.values(), key=id) if hasattr(p, "_commit_lock")]
+    for lk in locks:
+        lk.acquire()
+    try:
+        yield
+    finally:
+        for lk in reversed(locks):
+            lk.release()
 
 
 def live_switch(dp, items, hooks) -> None:

@@ -184,6 +184,12 @@ class MultiDataPlane:
         GPU switches epoch, and they release - so no burst sees GPU g on new tables and GPU h on
         old ones.  Otherwise the engines pause once around all planes' commits (not once per
         plane), and resume when every plane has its new tables."""
+        from .engine import commit_guard
+
+        with commit_guard(self.planes):
+            return self._commit_all(full)
+
+    def _commit_all(self, full: bool) -> dict:
         # learned MACs of every GPU reach the shared model before it is re-uploaded anywhere
         if any(getattr(p, "_learned_on_device", False) for p in self.planes):
             mv = self.planes[0].macs.version

@@ -206,7 +206,7 @@ class NativeLivePath:
                  on_punt=None, auto_restart: bool = True, tx_workers: int = 1, queues: int = 1,
                  max_inflight_frames: int = 0, port_queues: dict | None = None, coalesce_us: float = 8.0,
                  coalesce_frames: int = 64, ring_cus: int = 0, zero_copy: bool = False, lane_groups: bool = False,
-                 pin_cpus: bool = False):
+                 pin_cpus: bool = False, max_deferred_unmaps: int = 16):
         """dps: one data plane or a list (one per GPU, or a MultiDataPlane's planes); ports:
         {port id: vport spec}; queues: rx threads (each with a ring queue on every GPU) — with
         `lane_groups`, per data plane: every plane brings `queues` rx threads (and their tx
@@ -218,7 +218,11 @@ class NativeLivePath:
         with bursts of a lane in flight, frames gather into one publish until that many are read
         or the oldest waited that long (an idle lane publishes at once); zero_copy: the pipelines
         read memif frames where the pods wrote them (the regions pinned and mapped for the GPUs)
-        instead of from copies of their headers in the ring slots."""
+        instead of from copies of their headers in the ring slots.  A removed zero-copy vport's
+        region stays pinned until no ring grid of the process runs (hipHostUnregister waits for
+        the device): when more than `max_deferred_unmaps` pile up, the supervisor restarts the
+        rings (a maintenance restart: traffic pauses for the relaunch) and they are released, so
+        pinned memory stays bounded under vport churn."""
         from ..native import nfdp
 
         self.nf = nfdp()
@@ -231,6 +235,8 @@ class NativeLivePath:
         if self.lane_groups:
             queues = int(queues) * len(self.dps)
         self.pin_cpus = pin_cpus if isinstance(pin_cpus, dict) else bool(pin_cpus)
+        self.max_deferred_unmaps = int(max_deferred_unmaps)
+        self.unmap_restarts = 0
         self.gpu = self.dps[0].gpu
         if any(d.gpu != self.gpu for d in self.dps):
             raise ValueError("data planes must all be GPU or all CPU")
@@ -551,6 +557,16 @@ class NativeLivePath:
             self.poll_punts()
             eng = self._eng
             if eng is None:
+                continue
+            if self.gpu and self.zero_copy and self.nf.deferred_host_unmaps() > self.max_deferred_unmaps:
+                from .engine import commit_guard
+
+                with commit_guard(self.dps), self._lock:   # (no commit flips rings being replaced)
+                    log.warning("native I/O engine: %d removed zero-copy regions still pinned: restarting the rings "
+                                "to release them", self.nf.deferred_host_unmaps())
+                    self._teardown()          # (the last grid's stop unregisters them)
+                    self._build()
+                    self.unmap_restarts += 1
                 continue
             err = eng.error()
             if err:

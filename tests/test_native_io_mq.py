@@ -502,8 +502,9 @@ def test_live_soak_under_churn(shm, devices):
     placement, zero-copy rx)
     while the control plane churns: ACL rules added and removed (live table-set flips), ports moved
     between the planes, link flaps through the device control mailbox, a spare vport removed and
-    re-added.  Traffic never stops, the engine never fails or restarts, and once the churn is undone
-    a final batch is bit-exact with a CPU plane holding the same tables."""
+    re-added.  Traffic never stops, the engine never fails, the removed vports' pinned regions stay
+    bounded (maintenance restarts of the rings release them), and once the churn is undone a final
+    batch is bit-exact with a CPU plane holding the same tables."""
     import ipaddress
     import threading
 
@@ -589,6 +590,11 @@ def test_live_soak_under_churn(shm, devices):
         th.join(timeout=10)
         assert live.error is None and live.restarts == 0, (live.error, live.restarts)
         assert min(ops.values()) >= 3, ops
+        if m.gpu:
+            # removed zero-copy regions stay pinned while rings run: bounded by maintenance restarts
+            assert nf.deferred_host_unmaps() <= live.max_deferred_unmaps + 1, nf.deferred_host_unmaps()
+            if ops["spare"] > live.max_deferred_unmaps + 1:
+                assert live.unmap_restarts >= 1
         with lock:
             assert len(windows) >= 8 and min(windows) > 0, windows     # traffic never stopped
         # undo: every pod on its default plane, tables as the reference's; then a final exact batch
