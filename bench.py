@@ -663,7 +663,7 @@ def main() -> None:
     # live pod -> pod path (1 GPU, after the timed region): shared-memory pod vports, the native C++
     # I/O engine (csrc/nfdp/iox) and the persistent ring kernel; C++ pod generator / sinks measure
     # delivered Mpps and one-way latency on one clock (tools/live_bench.py)
-    live = None
+    live = live_veth = None
     if world == 1 and a.io == "device" and not a.no_live:
         try:
             import importlib.util
@@ -690,7 +690,6 @@ def main() -> None:
         # kernel-netdev (veth) pods in front of the same GPU ring (tools/live_bench.py run_veth
         # "pipeline", the deployed default vport): needs CAP_NET_ADMIN / CAP_NET_RAW, or user
         # namespaces to get them; reported as skipped (with the reason) where the box has neither
-        live_veth = None
         if live is not None:
             live_veth = _live_veth(str(dev))
 

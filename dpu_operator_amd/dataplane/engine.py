@@ -371,6 +371,10 @@ class DataPlane:
         costs no commit, no epoch change and no hold (a few microseconds of the poller wave).  The
         host model keeps the change; the next commit uploads it with everything else.  Returns
         False, having done nothing, when no coop ring runs (then commit() is the way)."""
+        with self._commit_lock:   # (a live path's maintenance restart does not replace the rings meanwhile)
+            return self._ctrl_ports_locked(ports, timeout_s)
+
+    def _ctrl_ports_locked(self, ports, timeout_s: float) -> bool:
         rings = [r for r in self._running_rings() if getattr(r, "coop", False)]
         if not rings or not self.gpu or "ports" not in self._dev:
             return False

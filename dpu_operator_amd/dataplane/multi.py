@@ -172,9 +172,12 @@ class MultiDataPlane:
     def ctrl_ports(self, ports, timeout_s: float = 1.0) -> bool:
         """Every plane's rings take the port entries through their control mailbox
         (DataPlane.ctrl_ports); False, with nothing done, unless every plane can."""
-        if not all(any(getattr(r, "coop", False) for r in p._running_rings()) for p in self.planes):
-            return False
-        return all(p.ctrl_ports(ports, timeout_s) for p in self.planes)
+        from .engine import commit_guard
+
+        with commit_guard(self.planes):   # (rings are not replaced meanwhile)
+            if not all(any(getattr(r, "coop", False) for r in p._running_rings()) for p in self.planes):
+                return False
+            return all(p.ctrl_ports(ports, timeout_s) for p in self.planes)
 
     def commit(self, full: bool = False) -> dict:
         """Every plane's commit as one update for the engines that feed them.

@@ -311,11 +311,17 @@ def test_bench_multirank_rehearsal_on_one_gpu(mode, n):
            "--warmup", "1", "--batch", str(1 << 16), "--flows", str(1 << 16), "--rehearse", "--mode", mode,
            "--remote-frac", "0.05", "--no-variants"]
     r = subprocess.run(cmd, cwd=repo, capture_output=True, text=True, timeout=110)
-    assert r.returncode == 0, r.stderr[-2000:]
+    assert r.returncode == 0, "\n".join(ln for ln in r.stderr.splitlines() if ln.startswith("[rank0]"))[-3000:]
     line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
     assert line["n_gpus"] == n and line["forwarded_fraction"] == 1.0
     assert line["config"]["global_batch"] == n << 16
     assert line["exchange"]["a2a_per_step"] >= 1 and line["exchange"]["xgmi_bytes_out_per_gpu_per_step"] > 0
+    if mode == "rss":   # the exchange-bound variant: (N-1)/N of every batch to its owner, all forwarded
+        import bench
+
+        u = line["unsteered"]
+        assert set(u) == set(bench.RSS_UNSTEERED_KEYS) and u["remote_frac"] == round((n - 1) / n, 4)
+        assert u["sent_per_gpu_per_step"] > 0 and u["forwarded_fraction"] == 1.0
 
 
 @pytest.mark.gpu

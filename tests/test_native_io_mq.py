@@ -574,9 +574,9 @@ def test_live_soak_under_churn(shm, devices):
                         m.ports.a[p]["flags"] |= np.uint32(T2.PORT_VALID)
                     else:
                         m.ports.a[p]["flags"] &= ~np.uint32(T2.PORT_VALID)
-                    if m.gpu:
-                        assert m.ctrl_ports([p])
-                    else:           # (no ring kernel on CPU planes: a commit)
+                    # through the running rings' control mailbox; a commit when none runs (CPU
+                    # planes, or rings in a maintenance restart - what GpuVsp.set_port_state does)
+                    if not (m.gpu and m.ctrl_ports([p])):
                         m.ports.version += 1
                         m.commit()
                 ops["flap"] += 1
