@@ -83,6 +83,8 @@ NFDP_HD int acl_rule_of(uint32_t b, uint32_t n_acl) {
 #endif
 #ifndef NFDP_ACL_LOOKAHEAD
 #define NFDP_ACL_LOOKAHEAD 1   // r4 s25 A/B: ClassBench-style set +5.5 % (7.17 -> 7.56 Gpps) over no lookahead
+// (r5: tile MFMAs ping-ponged between two accumulator sets, tile k's minima under tile k+1's
+// MFMAs: ClassBench set 7.84 vs 7.92 Gpps without, profiles/r5_s6_ab_acl_pingpong.jsonl - not kept)
 #endif
 #ifndef NFDP_PIPE_UNROLL
 #define NFDP_PIPE_UNROLL 1   // r3 s16 A/B: ACL1024 0.3145 vs 0.3211 ms, ClassBench unchanged
