@@ -78,3 +78,19 @@ def test_hot_kernel_register_budget(rows, src, prefix, max_spill, min_occ):
 def test_headline_sgpr_spill_budget(rows):
     r = [x for x in rows["kernels.hip"] if x["name"].startswith("_ZN4nfdp12fused_kernelILi1ELi1ELb0ELb0ELb0ELb0E")]
     assert r and r[0].get("SGPRs Spill", 0) <= HEADLINE_SGPR_SPILLS, r
+
+
+def test_no_direct_to_lds_loads_in_the_data_plane():
+    """No kernel of the data plane uses direct-to-LDS buffer loads (buffer_load ... lds).  ROCm 7.2's
+    waitcnt insertion is unreliable for them: tools/lds_dma_probe.hip reads stale LDS in 41 % of its
+    reads in a plain double-buffered loop whose second LDS read carries no s_waitcnt vmcnt for the
+    DMA that wrote it (profiles/r5_s7_lds_dma_waitcnt_repro.txt) - the root cause of the round-2
+    direct-to-LDS prefetch corruption (docs/DATAPLANE.md)."""
+    import re
+
+    hits = []
+    for f in sorted(SRC.glob("*.h")) + sorted(SRC.glob("*.hip")):
+        for i, line in enumerate(f.read_text().splitlines(), 1):
+            if re.search(r"buffer_load_lds|global_load_lds|load_to_lds", line) and not line.lstrip().startswith("//"):
+                hits.append(f"{f.name}:{i}")
+    assert not hits, hits
