@@ -88,6 +88,42 @@ def rss_unsteered_info(elapsed_s: float, steps: int, world: int, batch: int, sen
                     "(count-first all-to-all), timed like the headline (barrier + sync, max over ranks)"}
 
 
+def _unsteered(a, dp, sc, owner, rank, world, dev, cdev, torch, dist, P, RssShardedDataPlane, rss_traffic) -> dict:
+    """The exchange-bound variant of an N > 1 RSS run (rss_unsteered_info)."""
+    rf = (world - 1) / world
+    ub = []
+    for r in range(min(a.rotate, 2)):
+        pk, im = rss_traffic(sc, a.batch, rank, world, owner, rf, seed=7000 + 1000 * rank + r)
+        ub.append((torch.from_numpy(pk).to(dev), torch.from_numpy(im.view(np.int32)).to(dev)))
+        del pk, im
+    eng_u = RssShardedDataPlane(dp, rank, world, a.batch, remote_frac=rf)
+    nu = max(1, min(a.steps, 10))
+    for k in range(2):
+        eng_u.step(*ub[k % len(ub)])
+    eng_u.flush()
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    s0 = eng_u.stats["sent"]
+    tu = time.perf_counter()
+    for k in range(nu):
+        eng_u.step(*ub[k % len(ub)])
+    eng_u.flush()
+    torch.cuda.synchronize()
+    dist.barrier()
+    el_u = time.perf_counter() - tu
+    tt = torch.tensor([el_u], dtype=torch.float64, device=cdev)
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    el_u = float(tt.item())
+    _, _, ru = P.meta_fields(eng_u.out_meta())
+    fu = torch.tensor([float(np.mean((ru == 0) | (ru == 10)))], dtype=torch.float64, device=cdev)
+    dist.all_reduce(fu, op=dist.ReduceOp.SUM)
+    res = rss_unsteered_info(el_u, nu, world, a.batch, (eng_u.stats["sent"] - s0) / nu, float(fu.item()) / world)
+    del eng_u, ub
+    torch.cuda.empty_cache()
+    return res
+
+
 def _live_veth(dev: str) -> dict:
     """veth pods -> native engine -> GPU ring (the deployed default), measured in-process with
     CAP_NET_ADMIN, else in `unshare -Urnm` (a user namespace of our own), else skipped."""
@@ -522,37 +558,11 @@ def main() -> None:
     # every batch crosses xGMI to its owner
     unsteered = None
     if rss and not a.no_unsteered:
-        rf = (world - 1) / world
-        ub = []
-        for r in range(min(a.rotate, 2)):
-            pk, im = rss_traffic(sc, a.batch, rank, world, owner, rf, seed=7000 + 1000 * rank + r)
-            ub.append((torch.from_numpy(pk).to(dev), torch.from_numpy(im.view(np.int32)).to(dev)))
-            del pk, im
-        eng_u = RssShardedDataPlane(dp, rank, world, a.batch, remote_frac=rf)
-        nu = max(1, min(a.steps, 10))
-        for k in range(2):
-            eng_u.step(*ub[k % len(ub)])
-        eng_u.flush()
-        torch.cuda.synchronize()
-        dist.barrier()
-        torch.cuda.synchronize()
-        s0 = eng_u.stats["sent"]
-        tu = time.perf_counter()
-        for k in range(nu):
-            eng_u.step(*ub[k % len(ub)])
-        eng_u.flush()
-        torch.cuda.synchronize()
-        dist.barrier()
-        el_u = time.perf_counter() - tu
-        tt = torch.tensor([el_u], dtype=torch.float64, device=cdev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        el_u = float(tt.item())
-        _, _, ru = P.meta_fields(eng_u.out_meta())
-        fu = torch.tensor([float(np.mean((ru == 0) | (ru == 10)))], dtype=torch.float64, device=cdev)
-        dist.all_reduce(fu, op=dist.ReduceOp.SUM)
-        unsteered = rss_unsteered_info(el_u, nu, world, a.batch, (eng_u.stats["sent"] - s0) / nu, float(fu.item()) / world)
-        del eng_u, ub
-        torch.cuda.empty_cache()
+        try:
+            unsteered = _unsteered(a, dp, sc, owner, rank, world, dev, cdev, torch, dist, P, RssShardedDataPlane,
+                                   rss_traffic)
+        except Exception as ex:  # noqa: BLE001 - the headline must still be reported (every rank gets here)
+            unsteered = {"error": str(ex)[:200]}
 
     # small-batch latency probe (outside the timed region): 64K packets per step, fused/sharded alike
     p50_small = None
