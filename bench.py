@@ -124,6 +124,66 @@ def _unsteered(a, dp, sc, owner, rank, world, dev, cdev, torch, dist, P, RssShar
     return res
 
 
+def measure_hops(a, sc, dev, torch, S, P) -> dict:
+    """SFC hop pipeline across GPUs (BASELINE config 4), rehearsed on one GPU: the headline chain
+    split after nat - acl + nat on plane 0, l2fwd + egress on plane 1 - over two data planes with
+    their own replicated tables (1M flows each).  The hand-off is the product path
+    (parallel/hops.py): XFER fused instance -> hop_pack_kernel storing slot + 32-B record into
+    plane 1's inbox (peer stores; xGMI when the planes are different GPUs) -> resume_kernel.  Both
+    planes share one GPU here, so the stages run back to back: `mpps` is the pipeline's
+    throughput on ONE GPU (two GPUs overlap consecutive batches); `per_hop_us` splits a 64K
+    batch's latency into the first GPU's kernel, the hand-off and the resuming GPU's kernel."""
+    from dpu_operator_amd.dataplane.multi import MultiDataPlane
+    from dpu_operator_amd.parallel.hops import HopPipeline
+
+    multi = MultiDataPlane([str(dev), str(dev)], placement="port", hash_mode=a.hash, acl_mode=a.acl_mode,
+                           flow_buckets=1 << max(10, int(math.ceil(math.log2(a.flows / 2)))))
+    sc2 = S.build_sfc(multi, n_pods=a.pods_per_gpu, n_flows=a.flows, n_acl=a.acl, hops=("acl", "nat", "l2fwd@1"))
+    multi.commit()
+    n = a.batch
+    bs = []
+    for r in range(2):
+        pk, im = S.traffic(sc2, n, seed=9500 + r)
+        bs.append((torch.from_numpy(pk).to(dev), torch.from_numpy(im.view(np.int32)).to(dev)))
+    hp = HopPipeline(multi.planes, n)
+    for k in range(3):
+        hp.step(*bs[k % 2])
+    torch.cuda.synchronize()
+    steps = max(3, a.variant_steps)
+    t0 = time.perf_counter()
+    for k in range(steps):
+        hp.step(*bs[k % 2])
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    out, meta = hp.results(n)
+    rs = P.meta_fields(meta)[2]
+    res = {"split": "acl,nat | l2fwd (plane 0 | plane 1)", "planes": [str(dev), str(dev)],
+           "mpps": round(n * steps / el / 1e6, 1), "ms_per_batch": round(el / steps * 1e3, 4),
+           "forwarded_fraction": round(float(np.mean(rs == 0)), 4),
+           "handed_off_fraction": round(float(multi.planes[0].drop_counters().get("remote", 0)) /
+                                        max(1, n * (steps + 4)), 4)}
+    # per-hop latency: one 64K batch at a time, GPU clock (events) at each stage boundary
+    nsm = min(1 << 16, n)
+    hs = HopPipeline(multi.planes, nsm)
+    small = (bs[0][0][:nsm].contiguous(), bs[0][1][:nsm].contiguous())
+    f_us, h_us, r_us = [], [], []
+    for k in range(60):
+        tm = {}
+        hs.step(*small, timing=tm)
+        torch.cuda.synchronize()
+        if k >= 10:
+            f_us.append(tm["t0"].elapsed_time(tm["fused"]) * 1e3)
+            h_us.append(tm["fused"].elapsed_time(tm["handoff"]) * 1e3)
+            r_us.append(tm["handoff"].elapsed_time(tm["resume"]) * 1e3)
+    res["per_hop_us"] = {"batch": nsm, "first_gpu_kernel": round(float(np.median(f_us)), 2),
+                         "handoff": round(float(np.median(h_us)), 2),
+                         "resume_gpu_kernel": round(float(np.median(r_us)), 2),
+                         "total": round(float(np.median(np.add(np.add(f_us, h_us), r_us))), 2)}
+    del hp, hs, bs, multi
+    torch.cuda.empty_cache()
+    return res
+
+
 def _live_veth(dev: str) -> dict:
     """veth pods -> native engine -> GPU ring (the deployed default), measured in-process with
     CAP_NET_ADMIN, else in `unshare -Urnm` (a user namespace of our own), else skipped."""
@@ -670,6 +730,15 @@ def main() -> None:
     if world == 1 and a.io == "device" and not a.no_variants:
         variants = measure_variants(a, dp, sc, dev, torch, S, P)
 
+    # SFC hop pipeline across GPUs (1 GPU rehearsal, after the timed region): the headline chain
+    # split over two data planes with the in-HBM hand-off between them
+    hops = None
+    if world == 1 and a.io == "device" and not a.no_variants:
+        try:
+            hops = measure_hops(a, sc, dev, torch, S, P)
+        except Exception as ex:  # noqa: BLE001 - the headline must still be reported
+            hops = {"error": str(ex)[:200]}
+
     # live pod -> pod path (1 GPU, after the timed region): shared-memory pod vports, the native C++
     # I/O engine (csrc/nfdp/iox) and the persistent ring kernel; C++ pod generator / sinks measure
     # delivered Mpps and one-way latency on one clock (tools/live_bench.py)
@@ -751,6 +820,8 @@ def main() -> None:
             "value_vxlan_egress": None if not variants else variants["vxlan_egress_mpps"],
             "imix": None if not variants else variants["imix"],
             "variants": variants,
+            # split chain over two data planes (one GPU): pipeline Mpps and per-hop latency
+            "hop_pipeline": hops,
             # live pod -> pod through the native I/O engine + ring kernel (memif vports, 64-B frames)
             "live": live,
             "live_veth": live_veth,

@@ -347,7 +347,7 @@ PYBIND11_MODULE(_nfdp, m) {
 
   m.def("oracle_run", [](py::dict tables, uintptr_t pkts, uintptr_t inmeta, uint32_t n, uintptr_t out,
                          uintptr_t out_meta, uintptr_t flow_ctr, uintptr_t port_ctr, uintptr_t drop_ctr,
-                         uintptr_t hashes, uintptr_t acl, py::object side) {
+                         uintptr_t hashes, uintptr_t acl, py::object side, uintptr_t hop_state) {
     TablesView t = tables_from(tables);
     SideOut so = side_from(side);
     so.blk_cnt = nullptr;       // standalone side pass / oracle: one flat list
@@ -356,10 +356,57 @@ PYBIND11_MODULE(_nfdp, m) {
                reinterpret_cast<uint32_t*>(out), reinterpret_cast<uint32_t*>(out_meta),
                reinterpret_cast<uint64_t*>(flow_ctr), reinterpret_cast<uint64_t*>(port_ctr),
                reinterpret_cast<uint64_t*>(drop_ctr), reinterpret_cast<uint32_t*>(hashes),
-               reinterpret_cast<int32_t*>(acl), so.cnt ? &so : nullptr);
+               reinterpret_cast<int32_t*>(acl), so.cnt ? &so : nullptr, reinterpret_cast<HopState*>(hop_state));
   }, py::arg("tables"), py::arg("pkts"), py::arg("inmeta"), py::arg("n"), py::arg("out"), py::arg("out_meta"),
      py::arg("flow_ctr"), py::arg("port_ctr"), py::arg("drop_ctr"), py::arg("hashes"), py::arg("acl"),
-     py::arg("side") = py::none());
+     py::arg("side") = py::none(), py::arg("hop_state") = 0);
+  // SFC hop pipeline across GPUs (split chains): the oracle's resume, the GPU hand-off and resume
+  m.def("oracle_resume", [](py::dict tables, uintptr_t hdr, uintptr_t state, uint32_t n, uintptr_t out,
+                            uintptr_t out_meta, uintptr_t out_state, uintptr_t port_ctr, uintptr_t drop_ctr) {
+    const TablesView t = tables_from(tables);
+    py::gil_scoped_release nogil;
+    oracle_resume(t, reinterpret_cast<const uint32_t*>(hdr), reinterpret_cast<const HopState*>(state), n,
+                  reinterpret_cast<uint32_t*>(out), reinterpret_cast<uint32_t*>(out_meta),
+                  reinterpret_cast<HopState*>(out_state), reinterpret_cast<uint64_t*>(port_ctr),
+                  reinterpret_cast<uint64_t*>(drop_ctr));
+  }, py::arg("tables"), py::arg("hdr"), py::arg("state"), py::arg("n"), py::arg("out"), py::arg("out_meta"),
+     py::arg("out_state"), py::arg("port_ctr"), py::arg("drop_ctr"));
+  m.def("launch_hop_pack", [](uintptr_t out, uintptr_t meta, uintptr_t state, uint32_t n, uintptr_t n_dev,
+                              uint32_t plane, uintptr_t fill, uintptr_t count, uintptr_t hdr, uintptr_t dst_state,
+                              uintptr_t idx, uint32_t cap, uintptr_t stream) {
+    HopInbox d{reinterpret_cast<uint32_t*>(count), reinterpret_cast<uint4*>(hdr), reinterpret_cast<HopState*>(dst_state),
+               reinterpret_cast<uint32_t*>(idx), cap};
+    check(launch_hop_pack(reinterpret_cast<const void*>(out), reinterpret_cast<const uint32_t*>(meta),
+                          reinterpret_cast<const HopState*>(state), n, reinterpret_cast<const uint32_t*>(n_dev), plane,
+                          reinterpret_cast<uint32_t*>(fill), d, reinterpret_cast<hipStream_t>(stream)), "launch_hop_pack");
+  });
+  m.def("launch_resume", [](py::dict tables, uintptr_t count, uintptr_t hdr, uintptr_t state, uintptr_t idx,
+                            uint32_t cap, uintptr_t out, uintptr_t out_meta, uintptr_t out_state, uintptr_t port_ctr,
+                            uintptr_t drop_ctr, uint32_t flags, int num_cus, uintptr_t stream) {
+    const TablesView t = tables_from(tables);
+    HopInbox in{reinterpret_cast<uint32_t*>(count), reinterpret_cast<uint4*>(hdr), reinterpret_cast<HopState*>(state),
+                reinterpret_cast<uint32_t*>(idx), cap};
+    check(launch_resume(t, in, reinterpret_cast<void*>(out), reinterpret_cast<uint32_t*>(out_meta),
+                        reinterpret_cast<HopState*>(out_state), reinterpret_cast<unsigned long long*>(port_ctr),
+                        reinterpret_cast<unsigned long long*>(drop_ctr), flags, num_cus,
+                        reinterpret_cast<hipStream_t>(stream)), "launch_resume");
+  });
+  // peer access for the hand-off's stores into another GPU's inbox (xGMI); true when the pair can
+  // (already enabled counts), false when the devices cannot reach each other
+  m.def("enable_peer_access", [](int dev, int peer) -> bool {
+    if (dev == peer) return true;
+    int can = 0;
+    check(hipDeviceCanAccessPeer(&can, dev, peer), "hipDeviceCanAccessPeer");
+    if (!can) return false;
+    int cur = 0;
+    check(hipGetDevice(&cur), "hipGetDevice");
+    check(hipSetDevice(dev), "hipSetDevice");
+    const hipError_t e = hipDeviceEnablePeerAccess(peer, 0);
+    check(hipSetDevice(cur), "hipSetDevice");
+    if (e == hipErrorPeerAccessAlreadyEnabled) (void)hipGetLastError();
+    else check(e, "hipDeviceEnablePeerAccess");
+    return true;
+  });
   m.def("mac_learn_cpu", [](uintptr_t macs, uint32_t mask, uintptr_t events, uint32_t n, uint32_t stamp) {
     return mac_learn_cpu(reinterpret_cast<MacEntry*>(macs), mask, reinterpret_cast<const uint32_t*>(events), n, stamp);
   });
@@ -376,8 +423,10 @@ PYBIND11_MODULE(_nfdp, m) {
                            uintptr_t lat, uintptr_t acl_wfrag, uintptr_t acl_cinit, uint32_t acl_tiles,
                            uintptr_t toep_frag, uintptr_t toep_tab, int hash_mode, int acl_mode, int num_cus,
                            uintptr_t stream, uint32_t flags, py::object side, uintptr_t n_dev, uintptr_t steer_list,
-                           uintptr_t steer_cnt, uint32_t nranks, uint32_t rank, uint32_t steer_cap) {
+                           uintptr_t steer_cnt, uint32_t nranks, uint32_t rank, uint32_t steer_cap,
+                           uintptr_t hop_state) {
     FusedLaunch f{};
+    f.hop_state = reinterpret_cast<HopState*>(hop_state);
     f.steer_list = reinterpret_cast<uint32_t*>(steer_list);
     f.steer_cnt = reinterpret_cast<uint32_t*>(steer_cnt);
     f.steer_cap = steer_cap;
@@ -415,7 +464,7 @@ PYBIND11_MODULE(_nfdp, m) {
      py::arg("acl_wfrag"), py::arg("acl_cinit"), py::arg("acl_tiles"), py::arg("toep_frag"), py::arg("toep_tab"),
      py::arg("hash_mode"), py::arg("acl_mode"), py::arg("num_cus"), py::arg("stream"), py::arg("flags") = 0,
      py::arg("side") = py::none(), py::arg("n_dev") = 0, py::arg("steer_list") = 0, py::arg("steer_cnt") = 0,
-     py::arg("nranks") = 0, py::arg("rank") = 0, py::arg("steer_cap") = 0);
+     py::arg("nranks") = 0, py::arg("rank") = 0, py::arg("steer_cap") = 0, py::arg("hop_state") = 0);
   m.def("launch_pairs", [](py::dict tables, uintptr_t pkts, uintptr_t inmeta, uint32_t n, uintptr_t port_ctr, bool count,
                            uintptr_t stream) {
     const TablesView t = tables_from(tables);

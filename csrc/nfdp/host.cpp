@@ -346,7 +346,8 @@ uint32_t mac_learn_cpu(MacEntry* macs, uint32_t mask, const uint32_t* ev, uint32
 
 void oracle_run(const TablesView& t, const uint32_t* pkts, const uint32_t* inmeta, uint32_t n,
                 uint32_t* out, uint32_t* out_meta, uint64_t* flow_ctr, uint64_t* port_ctr,
-                uint64_t* drop_ctr, uint32_t* hashes, int32_t* acl_rules, const SideOut* side) {
+                uint64_t* drop_ctr, uint32_t* hashes, int32_t* acl_rules, const SideOut* side,
+                HopState* hop_state) {
   uint32_t prev_ci = (uint32_t)kSlotBytes << 8;   // strip | hv << 8 of the previous slot when it heads a pair
   for (uint32_t i = 0; i < n; ++i) {
     const uint32_t* d = pkts + (size_t)i * kSlotDwords;
@@ -387,9 +388,10 @@ void oracle_run(const TablesView& t, const uint32_t* pkts, const uint32_t* inmet
     const EgressDecision e = chain_stage(t, p, st, hit, act, acl, h);
     uint32_t o[kSlotDwords];
     emit(p, e.tci, e.push != 0, o);
-    const uint32_t olen = egress_len(p, e);
+    const uint32_t olen = out_len(p, e);
     std::memcpy(out + (size_t)i * kSlotDwords, o, sizeof(o));
     out_meta[i] = make_meta(e.out_port, olen, e.reason, !e.reason && e.xhdr, !e.reason && e.flood);
+    if (hop_state && e.reason == kRemote && e.inner_len) hop_state[i] = hop_state_of(p, st, e, act, acl, h);
     if (side && side->cnt && side_needed(st, p, e)) {
       const uint32_t q = side->cnt[5]++;
       if (q < side->cap_list) side->list[q] = i;
@@ -416,6 +418,26 @@ void oracle_run(const TablesView& t, const uint32_t* pkts, const uint32_t* inmet
       }
       side_stage(t, DirectTables{t}, d, im, out + (size_t)i * kSlotDwords, out_meta[i], i, sk);
     }
+  }
+}
+
+void oracle_resume(const TablesView& t, const uint32_t* hdr, const HopState* state, uint32_t n, uint32_t* out,
+                   uint32_t* out_meta, HopState* out_state, uint64_t* port_ctr, uint64_t* drop_ctr) {
+  const DirectTables ta{t};
+  for (uint32_t i = 0; i < n; ++i) {
+    const HopState hs = state[i];
+    Parsed p;
+    IngressState st;
+    resume_ingress(ta, hdr + (size_t)i * kSlotDwords, hs.inmeta, p, st);
+    const EgressDecision e = resume_stage(t, ta, p, st, hs.act, hs.acl_rule, hs.hash, hs.hop);
+    uint32_t o[kSlotDwords];
+    emit(p, e.tci, e.push != 0, o);
+    const uint32_t olen = out_len(p, e);
+    std::memcpy(out + (size_t)i * kSlotDwords, o, sizeof(o));
+    out_meta[i] = make_meta(e.out_port, olen, e.reason, !e.reason && e.xhdr, false);
+    if (out_state && e.reason == kRemote && e.inner_len) out_state[i] = hop_state_of(p, st, e, hs.act, hs.acl_rule, hs.hash);
+    if (port_ctr && !e.reason) port_ctr[2 * e.out_port + 1] += ctr_inc(olen);
+    if (drop_ctr && e.reason) drop_ctr[e.reason & (kNumReasons - 1)] += 1;
   }
 }
 

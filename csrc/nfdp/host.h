@@ -73,7 +73,14 @@ struct OracleOut {
 };
 void oracle_run(const TablesView& t, const uint32_t* pkts, const uint32_t* inmeta, uint32_t n,
                 uint32_t* out, uint32_t* out_meta, uint64_t* flow_ctr, uint64_t* port_ctr,
-                uint64_t* drop_ctr, uint32_t* hashes, int32_t* acl_rules, const SideOut* side = nullptr);
+                uint64_t* drop_ctr, uint32_t* hashes, int32_t* acl_rules, const SideOut* side = nullptr,
+                HopState* hop_state = nullptr);
+// The SFC hop pipeline across GPUs: the rest of split chains (kHopXfer) over handed-over frames
+// (`hdr` slots + their HopState records); a frame its chain hands on again gets a record in
+// `out_state` (nullable) and meta reason kRemote.  Counts tx / drops in port_ctr / drop_ctr.
+// GPU twin: launch_resume.
+void oracle_resume(const TablesView& t, const uint32_t* hdr, const HopState* state, uint32_t n, uint32_t* out,
+                   uint32_t* out_meta, HopState* out_state, uint64_t* port_ctr, uint64_t* drop_ctr);
 // MAC learning: apply learn events {mac_lo, mac_hi | bridge << 16, port, 0} to the MAC table
 // (learned entries carry `stamp`; static entries are never overridden).  Returns the number of
 // events that found no slot within the probe limit.  GPU twin: launch_mac_learn.
@@ -124,7 +131,24 @@ struct FusedLaunch {
   uint32_t steer_cap = 0;          // steer_list entries (>= steer_list_len(n, num_cus))
   // IPv6 ACL (t.n_acl6 > 0): acl6_kernel classifies the batch's IPv6 packets first (into out_meta)
   const void* acl6_wfrag = nullptr; const void* acl6_cinit = nullptr; uint32_t acl6_tiles = 0;
+  // split chains (kHopXfer): each handed-off frame's HopState (n records, nullable: the XFER
+  // instances run only when it is given)
+  HopState* hop_state = nullptr;
 };
+// The hand-off itself (kernels.hip): frames of `meta` with reason kRemote and port `plane` (and
+// their HopState records) -> the inbox on the GPU that resumes them, written there by this GPU
+// (peer stores over xGMI; the same code when both planes share a device).  Inbox: count word
+// (written by the publish step, <= cap), hdr [cap][64 B], state [cap], idx [cap] (source index).
+struct HopInbox {
+  uint32_t* count; uint4* hdr; HopState* state; uint32_t* idx; uint32_t cap;
+};
+hipError_t launch_hop_pack(const void* out, const uint32_t* meta, const HopState* state, uint32_t n,
+                           const uint32_t* n_dev, uint32_t plane, uint32_t* fill, const HopInbox& dst,
+                           hipStream_t s);
+// resume_kernel over an inbox (count from the device): results + next hand-offs
+hipError_t launch_resume(const TablesView& t, const HopInbox& in, void* out, uint32_t* out_meta, HopState* out_state,
+                         unsigned long long* port_ctr, unsigned long long* drop_ctr, uint32_t flags, int num_cus,
+                         hipStream_t s);
 // Second half of steer-by-list: listed packets -> their owners' exchange segments (count-first,
 // segments sized for the whole batch).
 hipError_t launch_steer(const void* pkts, const uint32_t* inmeta, const uint32_t* list, const uint32_t* list_cnt,

@@ -89,6 +89,8 @@ struct FusedArgs {
   uint32_t* steer_list;
   uint32_t* steer_cnt;
   uint32_t steer_cap_blk;
+  // XFER instances (split chains, kHopXfer): a handed-off frame's HopState record (n x 32 B)
+  HopState* hop_state;
 };
 
 __device__ __forceinline__ size_t lds_align16(size_t x) { return (x + 15) & ~(size_t)15; }
@@ -156,9 +158,12 @@ constexpr int kStreamAux = 2;        // nt: frames are read once / written once 
 // (the key words are otherwise recomputed from the header), so these instances load the next
 // frame after the tail instead of prefetching it under this slot's work: the IPv4-only
 // instances keep their register budget untouched.
-template <int HASH, int ACL, bool REMOTE, bool EARLY, bool LIST = false, bool V6 = false>
+// XFER: the instances for tables with split chains (kHopXfer hops): a frame handed to another GPU
+// leaves its HopState record in a.hop_state (two fixed-count stores in the tail, like the others).
+template <int HASH, int ACL, bool REMOTE, bool EARLY, bool LIST = false, bool V6 = false, bool XFER = false>
 __global__ __launch_bounds__(kFB, EARLY ? NFDP_EARLY_WAVES_PER_EU : NFDP_FUSED_WAVES_PER_EU) void fused_kernel(FusedArgs a) {
   static_assert(!V6 || (!REMOTE && !LIST), "IPv6 instances are 1-GPU instances");
+  static_assert(!XFER || (!REMOTE && !LIST && !V6), "split-chain instances are 1-GPU IPv4 instances");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ uint32_t rcnt[REMOTE ? 2 * kMaxRanks : 1], rbase[REMOTE ? kMaxRanks : 1];  // rcnt double-buffered
   __shared__ uint32_t lst_n;                                  // LIST: entries of this workgroup's region
@@ -229,6 +234,9 @@ __global__ __launch_bounds__(kFB, EARLY ? NFDP_EARLY_WAVES_PER_EU : NFDP_FUSED_W
   // LIST: the steer list (entries < 2^26, checked at launch: byte offsets fit 32 bits)
   const __amdgpu_buffer_rsrc_t r_list = __builtin_amdgcn_make_buffer_rsrc(
       (void*)a.steer_list, (short)0, LIST ? (int)(gridDim.x * a.steer_cap_blk * 4u) : 0, kBufCfg);
+  // XFER: the hand-off records (n * 32 B < 2 GiB: n < 2^25, checked at launch)
+  const __amdgpu_buffer_rsrc_t r_hop = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.hop_state, (short)0, XFER ? (int)(a.n * 32u) : 0, kBufCfg);
   uint32_t it = 0;  // loop iteration (REMOTE reservation buffers alternate)
 #if NFDP_KARG_RELOAD
   // The tables' bases and sizes are read where a stage uses them, from the kernel's argument
@@ -345,7 +353,7 @@ __global__ __launch_bounds__(kFB, EARLY ? NFDP_EARLY_WAVES_PER_EU : NFDP_FUSED_W
       }
     }
 #ifndef NFDP_ABL_NO_CHAIN
-    const EgressDecision e = chain_stage<LdsTables, V6>(TV, ta_it, p, st, hit, act, acl_rule, hash);
+    const EgressDecision e = chain_stage<LdsTables, V6, XFER>(TV, ta_it, p, st, hit, act, acl_rule, hash);
 #else  // cost attribution only (wrong results): no chain, the flow's port
     EgressDecision e{};
     e.out_port = hit ? act.out_port : kPortNone;
@@ -375,7 +383,7 @@ __global__ __launch_bounds__(kFB, EARLY ? NFDP_EARLY_WAVES_PER_EU : NFDP_FUSED_W
     if (REMOTE && to_owner && !to_peer) reason = kOverflow;  // the owner's segment was full: dropped here
     // steer list: always delivered to the owner (kRemote is set only by the steer test here)
     const bool listed = LIST && e.reason == kRemote;
-    const uint32_t olen = reason == e.reason ? egress_len(p, e) : 0u;
+    const uint32_t olen = reason == e.reason ? (XFER ? out_len(p, e) : egress_len(p, e)) : 0u;
     const uint32_t meta = (to_peer || listed)
                               ? make_meta((a.steer || listed) ? kPortNone : e.out_port,
                                           (a.steer || listed) ? st.wire_len : olen, kRemote)
@@ -447,6 +455,19 @@ __global__ __launch_bounds__(kFB, EARLY ? NFDP_EARLY_WAVES_PER_EU : NFDP_FUSED_W
         // so the wait for the prefetched frame keeps its vmcnt(N > 0) (a store under a branch
         // would force vmcnt(0) at the loop head and expose this slot's tail)
         __builtin_amdgcn_raw_buffer_store_b32(i | (owner_of(hash, a.nranks) << 26), r_list, off, 0, 0);
+      }
+      if constexpr (XFER) {
+        // a frame whose chain continues on another GPU: its record (hop_state_of), stored by every
+        // lane (out-of-range offset: dropped) so the tail's memory-instruction count stays fixed
+        const bool xf = valid && e.reason == kRemote && e.inner_len != 0u;
+        const HopState hs = hop_state_of(p, st, e, act, acl_rule, hash);
+        const uint32_t off = xf ? i * 32u : kNoRun;
+        typedef unsigned int v4u_t __attribute__((ext_vector_type(4)));
+        const v4u_t h0 = {hs.inmeta, hs.hash, (uint32_t)hs.acl_rule, hs.hop};
+        const v4u_t h1 = {(uint32_t)act.chain_id | ((uint32_t)act.out_port << 16), act.nat_ip,
+                          (uint32_t)act.nat_port | ((uint32_t)act.vlan << 16), act.flow_id};
+        __builtin_amdgcn_raw_buffer_store_b128(h0, r_hop, off, 0, kStreamAux);
+        __builtin_amdgcn_raw_buffer_store_b128(h1, r_hop, off, 16, kStreamAux);
       }
       if constexpr (V6) {   // (no prefetch in these instances: the next slot is loaded here)
         const uint32_t nx = i + stride;
@@ -993,6 +1014,134 @@ __global__ __launch_bounds__(256) void v6_kernel(V6Args a) {
   }
 }
 
+// ---- SFC hop pipeline across GPUs (split chains, kHopXfer) ----
+// hop_pack_kernel: this GPU's frames handed to `plane` (meta reason kRemote, port = plane, a
+// HopState record beside them) -> that plane's inbox.  The inbox lives on the GPU that resumes the
+// chain, so these are peer stores over xGMI (plain stores into a peer allocation; the same code
+// when both planes share a device).  Positions: one atomic per wave on this GPU's fill counter,
+// arrival order kept inside a wave; the publish step hands the count over once the batch is packed.
+__global__ __launch_bounds__(256) void hop_pack_kernel(const uint4* out, const uint32_t* meta, const HopState* state,
+                                                       uint32_t n, const uint32_t* n_dev, uint32_t plane,
+                                                       uint32_t* fill, HopInbox dst) {
+  const uint32_t nn = n_dev ? min(n, *n_dev) : n;
+  const uint32_t lane = threadIdx.x & 63u;
+  // block-uniform trip count: every wave reaches each ballot
+  for (uint32_t base = blockIdx.x * 256u; base < nn; base += gridDim.x * 256u) {
+    const uint32_t i = base + threadIdx.x;
+    const uint32_t m = i < nn ? meta[i] : 0u;
+    const bool mine = i < nn && ((m >> 26) & 0xFu) == kRemote && (m & 0xFFFu) == plane;
+    const unsigned long long b = __ballot(mine);
+    if (b == 0ull) continue;
+    const uint32_t pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+    const int leader = __builtin_ctzll(b);
+    uint32_t pos0 = 0;
+    if (lane == (uint32_t)leader) pos0 = atomicAdd(fill, (uint32_t)__builtin_popcountll(b));
+    pos0 = __builtin_amdgcn_readlane(pos0, leader);
+    if (mine) {
+      const uint32_t pos = pos0 + pre;
+      if (pos < dst.cap) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) dst.hdr[(size_t)pos * 4 + k] = out[(size_t)i * 4 + k];
+        dst.state[pos] = state[i];
+        dst.idx[pos] = i;
+      }
+    }
+  }
+}
+
+// publish: the inbox count (<= cap) for the resuming GPU; the fill counter is reset for the next
+// batch (stream order: after the pack kernel)
+__global__ void hop_publish_kernel(uint32_t* fill, uint32_t cap, uint32_t* count) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    const uint32_t f = *fill;
+    *count = f < cap ? f : cap;
+    *fill = 0u;
+  }
+}
+
+hipError_t launch_hop_pack(const void* out, const uint32_t* meta, const HopState* state, uint32_t n,
+                           const uint32_t* n_dev, uint32_t plane, uint32_t* fill, const HopInbox& dst,
+                           hipStream_t s) {
+  if (!out || !meta || !state || !fill || !dst.count || !dst.hdr || !dst.state || !dst.idx || plane > kHopXferPlanes)
+    return hipErrorInvalidValue;
+  uint32_t grid = (n + 255) / 256;
+  if (grid > 2048) grid = 2048;
+  if (grid) hipLaunchKernelGGL(hop_pack_kernel, dim3(grid), dim3(256), 0, s, reinterpret_cast<const uint4*>(out),
+                               meta, state, n, n_dev, plane, fill, dst);
+  hipLaunchKernelGGL(hop_publish_kernel, dim3(1), dim3(64), 0, s, fill, dst.cap, dst.count);
+  return hipGetLastError();
+}
+
+// resume_kernel: the rest of the split chains over an inbox (pipeline.h resume_stage), one frame
+// per lane.  Egress counters per workgroup in LDS (ports < kLdsPorts), like the fused kernel's.
+struct ResumeArgs {
+  TablesView t;
+  HopInbox in;
+  uint4* out;
+  uint32_t* out_meta;
+  HopState* out_state;            // next hand-offs (nullable)
+  unsigned long long* port_ctr;
+  unsigned long long* drop_ctr;
+  uint32_t flags;                 // bit0: no counters
+};
+__global__ __launch_bounds__(256) void resume_kernel(ResumeArgs a) {
+  __shared__ uint32_t pc[2 * kLdsPorts];   // tx packets, tx bytes
+  __shared__ uint32_t drops[kNumReasons];
+  for (uint32_t q = threadIdx.x; q < 2 * kLdsPorts; q += 256) pc[q] = 0;
+  if (threadIdx.x < kNumReasons) drops[threadIdx.x] = 0;
+  __syncthreads();
+  const uint32_t n = min(*a.in.count, a.in.cap);
+  const DirectTables ta{a.t};
+  const bool count = !(a.flags & 1u);
+  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) {
+    uint32_t d[kSlotDwords];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint4 v = a.in.hdr[(size_t)i * 4 + k];
+      d[4 * k] = v.x; d[4 * k + 1] = v.y; d[4 * k + 2] = v.z; d[4 * k + 3] = v.w;
+    }
+    const HopState hs = a.in.state[i];
+    Parsed p;
+    IngressState st;
+    resume_ingress(ta, d, hs.inmeta, p, st);
+    const EgressDecision e = resume_stage(a.t, ta, p, st, hs.act, hs.acl_rule, hs.hash, hs.hop);
+    uint32_t o[kSlotDwords];
+    emit(p, e.tci, e.push != 0, o);
+    const uint32_t olen = out_len(p, e);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) a.out[(size_t)i * 4 + k] = make_uint4(o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]);
+    a.out_meta[i] = make_meta(e.out_port, olen, e.reason, !e.reason && e.xhdr, false);
+    if (a.out_state && e.reason == kRemote && e.inner_len) a.out_state[i] = hop_state_of(p, st, e, hs.act, hs.acl_rule, hs.hash);
+    if (count) {
+      if (e.reason) {
+        atomicAdd(&drops[e.reason & (kNumReasons - 1)], 1u);
+      } else if (e.out_port < kLdsPorts) {
+        atomicAdd(&pc[e.out_port], 1u); atomicAdd(&pc[kLdsPorts + e.out_port], olen);
+      } else {
+        atomicAdd(a.port_ctr + 2 * e.out_port + 1, ctr_inc(olen));
+      }
+    }
+  }
+  __syncthreads();
+  for (uint32_t q = threadIdx.x; q < kLdsPorts; q += 256)
+    if (pc[q]) atomicAdd(a.port_ctr + 2 * q + 1, ((unsigned long long)pc[q] << 40) | pc[kLdsPorts + q]);
+  if (threadIdx.x < kNumReasons && drops[threadIdx.x])
+    atomicAdd(a.drop_ctr + threadIdx.x, (unsigned long long)drops[threadIdx.x]);
+}
+
+hipError_t launch_resume(const TablesView& t, const HopInbox& in, void* out, uint32_t* out_meta, HopState* out_state,
+                         unsigned long long* port_ctr, unsigned long long* drop_ctr, uint32_t flags, int num_cus,
+                         hipStream_t s) {
+  if (!in.count || !in.hdr || !in.state || !out || !out_meta || !port_ctr || !drop_ctr) return hipErrorInvalidValue;
+  uint32_t grid = (in.cap + 255) / 256;
+  const uint32_t lim = (uint32_t)(num_cus > 0 ? num_cus : 256) * 8u;
+  if (grid > lim) grid = lim;
+  if (grid == 0) return hipSuccess;
+  ResumeArgs a{t, in, reinterpret_cast<uint4*>(out), out_meta, out_state, port_ctr, drop_ctr, flags};
+  hipLaunchKernelGGL(resume_kernel, dim3(grid), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
 static hipError_t launch_v6(const FusedLaunch& f, int num_cus, hipStream_t s) {
   if (!f.pkts || !f.inmeta || !f.out_meta || !f.out) return hipErrorInvalidValue;
   if (f.t.n_acl6 && (!f.acl6_wfrag || !f.acl6_cinit || f.acl6_tiles == 0 || f.acl6_tiles > kAclMaxRules / 16 ||
@@ -1009,7 +1158,7 @@ static hipError_t launch_v6(const FusedLaunch& f, int num_cus, hipStream_t s) {
   return hipGetLastError();
 }
 
-template <int H, int A, bool R, bool E = false, bool LS = false, bool V6 = false>
+template <int H, int A, bool R, bool E = false, bool LS = false, bool V6 = false, bool X = false>
 static hipError_t launch_fused_t(const FusedArgs& a, int num_cus, hipStream_t s) {
   // static LDS (REMOTE reservation counters) + dynamic tables must fit 160 KiB
   // rcnt[2][..] + rbase + lst_n, with room for the compiler's alignment of the static block
@@ -1024,7 +1173,7 @@ static hipError_t launch_fused_t(const FusedArgs& a, int num_cus, hipStream_t s)
   if (!R && (a.n >= (1u << 25) || !a.flow_ctr || !a.out_meta)) return hipErrorInvalidValue;
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&fused_kernel<H, A, R, E, LS, V6>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&fused_kernel<H, A, R, E, LS, V6, X>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxDyn);
     if (e != hipSuccess) return e;
     attr_set = true;
@@ -1053,7 +1202,8 @@ static hipError_t launch_fused_t(const FusedArgs& a, int num_cus, hipStream_t s)
     if ((uint64_t)grid * b.steer_cap_blk > a.steer_cap_blk || grid > (uint32_t)(4 * num_cus))
       return hipErrorInvalidValue;   // (steer_cap_blk carries the list's capacity in)
   }
-  hipLaunchKernelGGL((fused_kernel<H, A, R, E, LS, V6>), dim3(grid), dim3(kFB), lds, s, b);
+  if (X && !a.hop_state) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((fused_kernel<H, A, R, E, LS, V6, X>), dim3(grid), dim3(kFB), lds, s, b);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || !a.side.cnt || a.side.cap_list == 0) return e;
   return launch_side(a.t, a.pkts, a.inmeta, a.out, a.out_meta, b.side, a.port_ctr, a.drop_ctr, s, a.n, false, a.toep_tab);
@@ -1098,6 +1248,7 @@ static FusedArgs make_fused_args(const FusedLaunch& f) {
   a.steer_list = f.steer_list;
   a.steer_cnt = f.steer_cnt;
   a.steer_cap_blk = f.steer_cap;
+  a.hop_state = f.hop_state;
   return a;
 }
 
@@ -1141,6 +1292,12 @@ static hipError_t launch_fused_body(const FusedLaunch& f, const LaunchCfg& cfg, 
 #else
   const bool early = ac == kAclMfma && !(f.flags & kFlagNoEarly) &&
                      (f.acl_tiles >= kEarlyAclTiles || (f.flags & kFlagForceEarly));
+  if (f.hop_state) {   // split chains: the XFER instances (1 GPU, IPv4 tables, MFMA ACL)
+    if (remote || f.steer_list || f.t.n_acl6 || f.t.flow6_on || ac != kAclMfma || h == kHashScalar)
+      return hipErrorNotSupported;
+    return h == kHashLds ? launch_fused_t<kHashLds, kAclMfma, false, false, false, false, true>(a, cu, s)
+                         : launch_fused_t<kHashMfma, kAclMfma, false, false, false, false, true>(a, cu, s);
+  }
   if (f.t.n_acl6 || f.t.flow6_on) {   // IPv6 flows / rules: the V6 instances (1 GPU, MFMA ACL)
     if (remote || f.steer_list || ac != kAclMfma || h == kHashScalar) return hipErrorNotSupported;
     if (h == kHashLds) return early ? launch_fused_t<kHashLds, kAclMfma, false, true, false, true>(a, cu, s)

@@ -60,7 +60,8 @@ enum Reason : uint32_t {
   kChainDrop = 7,
   kTtlExpired = 8,
   kMalformed = 9,
-  kRemote = 10,    // not a drop: handed to the egress GPU over xGMI (multi-GPU path)
+  kRemote = 10,    // not a drop: handed to the egress GPU over xGMI (multi-GPU path), or the rest of
+                   // its chain runs on another GPU (kHopXfer: port = that GPU's plane, len = frame length)
   kOverflow = 11,  // exchange segment full (multi-GPU path)
   kArpTrap = 12,   // ARP copy trapped to the slow path (P4 always_trap_arp_table)
   kRecirc = 13,    // tunnel terminated: recirculate frame[len - olen:] with in_port = meta port (decap)
@@ -109,7 +110,9 @@ enum Hop : uint8_t {
   kHopDrop = 7,
   kHopPunt = 8,
   kHopRoute = 9,    // IPv4 LPM (ipv4_table) -> nexthop / ECMP group -> MACs, port; TTL - 1
+  kHopXfer = 0x10,  // | plane (0..15): the rest of the chain runs on that GPU (pipeline.h resume_stage)
 };
+constexpr uint32_t kHopXferPlanes = 0xFu;
 
 // ----------------------------------------------------------------------------------------
 // Tables (all POD, 16-B aligned so the kernels use dwordx4 accesses)
@@ -247,6 +250,17 @@ struct alignas(16) VmMacEntry {  // 16 B
 };
 static_assert(sizeof(VmMacEntry) == 16, "VmMacEntry");
 constexpr int kVmMacProbe = 8;
+
+// Hand-off record of a split chain (kHopXfer, the SFC hop pipeline across GPUs): what the GPU that
+// runs the rest of the chain needs besides the 64-B header slot as the earlier hops left it.
+struct alignas(16) HopState {    // 32 B
+  uint32_t inmeta;               // in_port | frame length << 16 (the frame as handed over)
+  uint32_t hash;                 // the packet's Toeplitz hash (LAG members, ECMP)
+  int32_t acl_rule;              // first matching ACL rule (-1: none), for acl hops after the split
+  uint32_t hop;                  // the hop the chain resumes at
+  FlowAction act;                // the flow's action (chain id, out port, NAT, vlan)
+};
+static_assert(sizeof(HopState) == 32, "HopState");
 
 // Verdict returned by the flow owner to the ingress GPU (multi-GPU path).
 struct alignas(16) Verdict {     // 16 B

@@ -175,7 +175,8 @@ struct EgressDecision {
                       // side_stage emits a replica per further member
   uint32_t xhdr;      // outer-header bytes (50 IPv4 / 70 IPv6 underlay) when out_port is a tunnel port:
                       // the side pass writes them; 0 otherwise
-  uint32_t inner_len; // kRecirc / kRecirc6: length of the decapsulated inner frame
+  uint32_t inner_len; // kRecirc / kRecirc6: length of the decapsulated inner frame; kRemote from a
+                      // kHopXfer: the hop the chain resumes at on the other GPU
 };
 
 // Length of the frame that leaves (the meta word's len): inner frame for a recirculation, tag and
@@ -282,13 +283,67 @@ NFDP_HD uint32_t route_ipv6(const TablesView& t, Parsed& p, uint32_t& out_port) 
   return kOk;
 }
 
-// `hit`: flow entry found; `act`: its action; `acl_rule`: first matching ACL rule or -1;
-// `hash`: the packet's Toeplitz hash (LAG member selection uses hash[2:0], K8).
+// One chain hop (chain_stage and resume_stage).  Returns true when the hop ends the chain: a
+// drop / punt (e.reason, e.out_port set) or a hand-off to another GPU (kHopXfer: e.reason =
+// kRemote, e.out_port = that GPU's plane, e.inner_len = the hop the chain resumes at there).
 // V6HOPS: the ttl hop also decrements an IPv6 hop limit.  A hop runs only on a flow hit and an
 // IPv6 packet hits a flow only with IPv6 features in the tables, i.e. in the kernels' V6
 // instances, so the IPv4-only instances compile it out (their register budget) with the same
 // results as the oracle, which always has it.
-template <class TA, bool V6HOPS = true>
+// XFER: hand-offs are honoured (the oracle, the kernels' XFER instances, resume_stage); the other
+// kernel instances never see split chains from the batch engine (DataPlane picks the XFER instances
+// for tables that have them), and the persistent ring kernel runs a split chain whole on the GPU
+// the frame entered (a kHopXfer hop is a no-op there), so their register budgets do not pay for it.
+template <class TA, bool V6HOPS = true, bool XFER = true>
+NFDP_HD bool apply_hop(const TablesView& t, const TA& ta, uint32_t op, int i, Parsed& p, const IngressState& st,
+                       const FlowAction& act, int acl_rule, uint32_t hash, EgressDecision& e, bool& vlan_done) {
+  if (op == kHopAcl) {
+    if (!ta.permit(acl_rule)) { e.reason = kAclDeny; e.out_port = kPortNone; return true; }
+  } else if (op == kHopNat) {
+    if (p.ipv4) act_snat(p, act.nat_ip, act.nat_port);
+  } else if (op == kHopL2Fwd) {
+    e.out_port = act.out_port;
+    if (e.out_port < (uint32_t)kMaxPorts) {
+      const PortEntry pe = ta.port(e.out_port);
+      set_dmac(p.s, pe.peer_mac_lo, pe.peer_mac_hi);
+      set_smac(p.s, pe.mac_lo, pe.mac_hi);
+    }
+  } else if (op == kHopTtl) {
+    if (p.ipv4 && !act_ttl(p)) { e.reason = kTtlExpired; e.out_port = kPortNone; return true; }
+    if (V6HOPS && NFDP_IPV6 && p.ipv6) {   // hop limit - 1 (no IPv6 header checksum)
+      const uint32_t hl = byte_at(p.s, 21);
+      if (hl <= 1u) { e.reason = kTtlExpired; e.out_port = kPortNone; return true; }
+      p.s[5] = (p.s[5] & ~(0xFFu << 8)) | ((hl - 1u) << 8);
+    }
+  } else if (op == kHopHairpin) {
+    e.out_port = st.in_port;
+    const uint32_t dl = dmac_lo(p.s), dh = dmac_hi(p.s);
+    set_dmac(p.s, smac_lo(p.s), smac_hi(p.s));
+    set_smac(p.s, dl, dh);
+  } else if (op == kHopVlan) {
+    if (act.vlan == 0xFFFFu) { e.push = 0; vlan_done = true; }
+    else if (act.vlan) { e.push = 1; e.tci = act.vlan & 0xFFFu; vlan_done = true; }
+  } else if (op == kHopDrop) {
+    e.reason = kChainDrop; e.out_port = kPortNone; return true;
+  } else if (op == kHopPunt) {
+    e.reason = kNoRoute; e.out_port = kPortPunt; return true;
+  } else if (NFDP_L3_ON && op == kHopRoute) {
+    uint32_t rp = kPortNone;
+    const uint32_t r = route_ipv4(t, p, hash, rp);
+    if (r) { e.reason = r; e.out_port = r == kNoRoute ? kPortPunt : kPortNone; return true; }
+    e.out_port = rp;
+  } else if (XFER && op >= kHopXfer) {
+    // the rest of the chain runs on another GPU (resume_stage there): the frame leaves with the
+    // header as the hops so far left it, untagged (a vlan hop's push is replayed at the end)
+    e.reason = kRemote; e.out_port = op & kHopXferPlanes; e.inner_len = (uint32_t)i + 1u; e.push = 0;
+    return true;
+  }
+  return false;
+}
+
+// `hit`: flow entry found; `act`: its action; `acl_rule`: first matching ACL rule or -1;
+// `hash`: the packet's Toeplitz hash (LAG member selection uses hash[2:0], K8).
+template <class TA, bool V6HOPS = true, bool XFER = true>
 NFDP_HD EgressDecision chain_stage(const TablesView& t, const TA& ta, Parsed& p, const IngressState& st,
                                    bool hit, const FlowAction& act, int acl_rule, uint32_t hash) {
   EgressDecision e;
@@ -402,43 +457,8 @@ NFDP_HD EgressDecision chain_stage(const TablesView& t, const TA& ta, Parsed& p,
 #endif
     for (int i = 0; i < kMaxHops; ++i) {
       if ((uint32_t)i >= nh) break;
-      const uint8_t op = (uint8_t)((hw >> (8 * (i + 1))) & 0xFFu);
-      if (op == kHopAcl) {
-        if (!ta.permit(acl_rule)) { e.reason = kAclDeny; e.out_port = kPortNone; return e; }
-      } else if (op == kHopNat) {
-        if (p.ipv4) act_snat(p, act.nat_ip, act.nat_port);
-      } else if (op == kHopL2Fwd) {
-        e.out_port = act.out_port;
-        if (e.out_port < (uint32_t)kMaxPorts) {
-          const PortEntry pe = ta.port(e.out_port);
-          set_dmac(p.s, pe.peer_mac_lo, pe.peer_mac_hi);
-          set_smac(p.s, pe.mac_lo, pe.mac_hi);
-        }
-      } else if (op == kHopTtl) {
-        if (p.ipv4 && !act_ttl(p)) { e.reason = kTtlExpired; e.out_port = kPortNone; return e; }
-        if (V6HOPS && NFDP_IPV6 && p.ipv6) {   // hop limit - 1 (no IPv6 header checksum)
-          const uint32_t hl = byte_at(p.s, 21);
-          if (hl <= 1u) { e.reason = kTtlExpired; e.out_port = kPortNone; return e; }
-          p.s[5] = (p.s[5] & ~(0xFFu << 8)) | ((hl - 1u) << 8);
-        }
-      } else if (op == kHopHairpin) {
-        e.out_port = st.in_port;
-        const uint32_t dl = dmac_lo(p.s), dh = dmac_hi(p.s);
-        set_dmac(p.s, smac_lo(p.s), smac_hi(p.s));
-        set_smac(p.s, dl, dh);
-      } else if (op == kHopVlan) {
-        if (act.vlan == 0xFFFFu) { e.push = 0; vlan_done = true; }
-        else if (act.vlan) { e.push = 1; e.tci = act.vlan & 0xFFFu; vlan_done = true; }
-      } else if (op == kHopDrop) {
-        e.reason = kChainDrop; e.out_port = kPortNone; return e;
-      } else if (op == kHopPunt) {
-        e.reason = kNoRoute; e.out_port = kPortPunt; return e;
-      } else if (NFDP_L3_ON && op == kHopRoute) {
-        uint32_t rp = kPortNone;
-        const uint32_t r = route_ipv4(t, p, hash, rp);
-        if (r) { e.reason = r; e.out_port = r == kNoRoute ? kPortPunt : kPortNone; return e; }
-        e.out_port = rp;
-      }
+      const uint32_t op = (uint32_t)((hw >> (8 * (i + 1))) & 0xFFu);
+      if (apply_hop<TA, V6HOPS, XFER>(t, ta, op, i, p, st, act, acl_rule, hash, e, vlan_done)) return e;
     }
   }
   const uint32_t r = finish_port(t, ta, e.out_port, hash, vlan_done, e.push, e.tci, p.len, &e.xhdr);
@@ -446,9 +466,87 @@ NFDP_HD EgressDecision chain_stage(const TablesView& t, const TA& ta, Parsed& p,
   e.mirror = (st.in_flags & kPortMirror) ? 1u : 0u;  // mirror_and_send (K9)
   return e;
 }
+
+// The rest of a chain on the GPU a kHopXfer handed the frame to (the SFC hop pipeline across
+// GPUs).  The frame arrives as the earlier hops left it (`p`, parsed from the handed-over slot);
+// `st` carries its ingress port (flags from this GPU's replicated port table) and `act`, `acl_rule`,
+// `hash` travel with it from the first GPU.  Hops before `hop0` already ran: their effects on the
+// header are in the slot, and what they decided about the egress (the l2fwd / hairpin port, a vlan
+// push / pop) is replayed from the chain word, which is the same on every GPU.  A route hop cannot
+// come before a hand-off (ChainTable refuses it: its port depends on the header it rewrote).
+// Frames of split chains are not mirrored (K9 copies the ingress frame, which stayed on the first GPU).
+template <class TA, bool V6HOPS = true>
+NFDP_HD EgressDecision resume_stage(const TablesView& t, const TA& ta, Parsed& p, const IngressState& st,
+                                    const FlowAction& act, int acl_rule, uint32_t hash, uint32_t hop0) {
+  EgressDecision e;
+  e.out_port = act.out_port; e.reason = st.reason; e.push = 0; e.tci = 0; e.mirror = 0; e.flood = 0;
+  e.xhdr = 0; e.inner_len = 0;
+  if (e.reason) { e.out_port = kPortNone; return e; }
+  bool vlan_done = false;
+  const uint64_t hw = ta.chain_word(act.chain_id);
+  const uint32_t nh = (uint32_t)(hw & 0xFFu);
+  if (hop0 == 0u || hop0 > nh) { e.reason = kChainDrop; e.out_port = kPortNone; return e; }
+  for (int i = 0; i < kMaxHops; ++i) {
+    if ((uint32_t)i >= nh) break;
+    const uint32_t op = (uint32_t)((hw >> (8 * (i + 1))) & 0xFFu);
+    if ((uint32_t)i < hop0) {   // replay what the earlier GPU's hops decided about the egress
+      if (op == kHopL2Fwd) e.out_port = act.out_port;
+      else if (op == kHopHairpin) e.out_port = st.in_port;
+      else if (op == kHopVlan) {
+        if (act.vlan == 0xFFFFu) { e.push = 0; vlan_done = true; }
+        else if (act.vlan) { e.push = 1; e.tci = act.vlan & 0xFFFu; vlan_done = true; }
+      } else if (op == kHopRoute) { e.reason = kChainDrop; e.out_port = kPortNone; return e; }
+      continue;
+    }
+    if (apply_hop<TA, V6HOPS>(t, ta, op, i, p, st, act, acl_rule, hash, e, vlan_done)) return e;
+  }
+  const uint32_t r = finish_port(t, ta, e.out_port, hash, vlan_done, e.push, e.tci, p.len, &e.xhdr);
+  if (r) { e.reason = r; e.out_port = kPortNone; e.xhdr = 0; return e; }
+  return e;
+}
 NFDP_HD EgressDecision chain_stage(const TablesView& t, Parsed& p, const IngressState& st, bool hit,
                                    const FlowAction& act, int acl_rule, uint32_t hash = 0) {
   return chain_stage(t, DirectTables{t}, p, st, hit, act, acl_rule, hash);
+}
+
+// A handed-over frame on the GPU that resumes its chain: parse the slot as it stands and take the
+// ingress port's flags from this GPU's (replicated) port table.  The ingress checks (VLAN
+// isolation, spoof check) ran on the first GPU against the frame as received; they are not
+// repeated against the rewritten header.
+template <class TA>
+NFDP_HD void resume_ingress(const TA& ta, const uint32_t* d, uint32_t inmeta, Parsed& p, IngressState& st) {
+  st.in_port = inmeta & 0xFFFFu;
+  uint32_t len = inmeta >> 16;
+  st.wire_len = len;
+  st.reason = kOk;
+  if (len < 14 || len > kMaxFrame) { st.reason = kMalformed; len = len < 14 ? 14 : kMaxFrame; }
+  parse(d, len, p);
+  st.bridge = 0; st.in_flags = 0; st.in_ext = 0;
+  if (st.in_port >= (uint32_t)kMaxPorts) {
+    st.reason = kBadPort;
+  } else {
+    const PortEntry pe = ta.port(st.in_port);
+    st.in_flags = pe.flags;
+    st.in_ext = pe.ext;
+  }
+  st.key = FlowKey{0u, 0u, 0u, 0u};
+}
+
+// The hand-off record of a frame whose chain continues on another GPU (e.reason == kRemote from a
+// kHopXfer): the state resume_stage needs there.
+NFDP_HD HopState hop_state_of(const Parsed& p, const IngressState& st, const EgressDecision& e, const FlowAction& act,
+                              int acl_rule, uint32_t hash) {
+  HopState h;
+  h.inmeta = st.in_port | (p.len << 16);
+  h.hash = hash;
+  h.acl_rule = acl_rule;
+  h.hop = e.inner_len;
+  h.act = act;
+  return h;
+}
+// meta len of a frame: a hand-off carries the frame as it stands (egress_len says 0 for reasons)
+NFDP_HD uint32_t out_len(const Parsed& p, const EgressDecision& e) {
+  return (e.reason == kRemote && e.inner_len) ? p.len : egress_len(p, e);
 }
 
 // Outer headers of a tunnel port for an inner frame of `inner_len` bytes (50 B: Ethernet,

@@ -473,7 +473,7 @@ __global__ __launch_bounds__(kRingBlock) void ring_kernel(RingArgs a) {
       }
     }
     NFDP_RING_MARK(tr2)
-    const EgressDecision e = chain_stage<LdsTables, V6>(T, ta, p, st, hit, act, acl_rule, hash);
+    const EgressDecision e = chain_stage<LdsTables, V6, false>(T, ta, p, st, hit, act, acl_rule, hash);
     const uint32_t olen = egress_len(p, e);
     uint32_t o[kSlotDwords];
     emit(p, e.tci, e.push != 0, o);

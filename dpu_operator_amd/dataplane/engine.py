@@ -723,6 +723,9 @@ class DataPlane:
                 self.nf.launch_pairs(tp, pkts.data_ptr(), inmeta.data_ptr(), n, self._ptr("port_ctr"),
                                      not (flags & 1), s)
             side = self._side_buffers(n) if self.side_active() else None
+            # split chains (a hop placed on another GPU): the XFER instances leave each handed-off
+            # frame's HopState record here (MultiDataPlane / parallel.hops resume them there)
+            hop = torch.empty((n, 8), dtype=torch.int32, device=self.tdev) if self.chains.split() else None
             # one launch covers < 2^25 slots (32-bit buffer views); bigger batches are split
             for lo in range(0, n, self.MAX_LAUNCH):
                 m = min(self.MAX_LAUNCH, n - lo)
@@ -735,23 +738,68 @@ class DataPlane:
                     self._ptr("acl_wfrag"), self._ptr("acl_cinit"), self._acl_tiles,
                     self._ptr("toep_frag"), self._ptr("toep_tab"),
                     self.hash_mode, self.acl_mode, self.num_cus, s, flags, side,
+                    hop_state=hop.data_ptr() + 32 * lo if hop is not None else 0,
                 )
             if pairs:   # continuation slots: kCont metas carrying their pair's strip / valid bytes
                 self.nf.launch_pair_fix(inmeta.data_ptr(), meta.data_ptr(), n, self._ptr("drop_ctr"), not (flags & 1), s)
             if side is not None:
                 self._apply_learn(s)
-            return BatchResult(out, meta, n, {"lat": lat})
+            ex = {"lat": lat}
+            if hop is not None:
+                ex["hop_state"] = hop
+            return BatchResult(out, meta, n, ex)
         pk = np.ascontiguousarray(pkts, np.uint8)
         im = np.ascontiguousarray(inmeta, np.uint32)
         hashes = np.zeros(n, np.uint32)
         acl = np.zeros(n, np.int32)
         side = self._side_buffers(n) if self.side_active() else None
+        hop = np.zeros((n, 8), np.uint32) if self.chains.split() else None
         self.nf.oracle_run(tp, pk.ctypes.data, im.ctypes.data, n, out.ctypes.data, meta.ctypes.data,
                            self._ptr("flow_ctr"), self._ptr("port_ctr"), self._ptr("drop_ctr"),
-                           hashes.ctypes.data, acl.ctypes.data, side)
+                           hashes.ctypes.data, acl.ctypes.data, side, hop_state=hop.ctypes.data if hop is not None else 0)
         if side is not None:
             self._apply_learn()
-        return BatchResult(out, meta, n, {"hash": hashes, "acl": acl})
+        ex = {"hash": hashes, "acl": acl}
+        if hop is not None:
+            ex["hop_state"] = hop
+        return BatchResult(out, meta, n, ex)
+
+    def resume(self, hdr, state, stream=None, flags: int = 0) -> BatchResult:
+        """The rest of split chains on this plane (the SFC hop pipeline across GPUs): `hdr` are
+        handed-over header slots ([n,64] uint8), `state` their HopState records ([n,8] 32-bit), as
+        another plane's run() left them (BatchResult.extra["hop_state"] rows of the frames whose meta
+        says REMOTE with this plane as port).  Tx and drops are counted here; a frame its chain hands
+        on again gets its record in extra["hop_state"].  GPU: tensors on this device (copy them over
+        first: that copy is the xGMI hop); CPU: numpy (the oracle)."""
+        n = int(hdr.shape[0])
+        tp = self.tables_ptrs()
+        if self.gpu:
+            torch = _torch()
+            if hdr.device != self.tdev or state.device != self.tdev:
+                raise ValueError("resume: hand-off must live on the data-plane device")
+            if hdr.dtype != torch.uint8 or tuple(hdr.shape) != (n, 64) or not hdr.is_contiguous():
+                raise ValueError("hdr must be contiguous [n,64] uint8")
+            if tuple(state.shape) != (n, 8) or state.element_size() != 4 or not state.is_contiguous():
+                raise ValueError("state must be contiguous [n,8] 32-bit")
+            out = torch.empty((n, 64), dtype=torch.uint8, device=self.tdev)
+            meta = torch.empty(n, dtype=torch.int32, device=self.tdev)
+            nxt = torch.zeros((n, 8), dtype=torch.int32, device=self.tdev)
+            if n:
+                cnt = torch.tensor([n], dtype=torch.int32, device=self.tdev)
+                s = stream if stream is not None else torch.cuda.current_stream(self.tdev).cuda_stream
+                self.nf.launch_resume(tp, cnt.data_ptr(), hdr.data_ptr(), state.data_ptr(), 0, n, out.data_ptr(),
+                                      meta.data_ptr(), nxt.data_ptr(), self._ptr("port_ctr"), self._ptr("drop_ctr"),
+                                      flags, self.num_cus, s)
+            return BatchResult(out, meta, n, {"hop_state": nxt})
+        hdr = np.ascontiguousarray(hdr, np.uint8).reshape(n, 64)
+        state = np.ascontiguousarray(np.asarray(state).view(np.uint32)).reshape(n, 8)
+        out = np.zeros((n, 64), np.uint8)
+        meta = np.zeros(n, np.uint32)
+        nxt = np.zeros((n, 8), np.uint32)
+        if n:
+            self.nf.oracle_resume(tp, hdr.ctypes.data, state.ctypes.data, n, out.ctypes.data, meta.ctypes.data,
+                                  nxt.ctypes.data, self._ptr("port_ctr"), self._ptr("drop_ctr"))
+        return BatchResult(out, meta, n, {"hop_state": nxt})
 
     def capture(self, n: int) -> "GraphedRun":
         """A batch of n slots as a captured HIP graph (see GraphedRun)."""

@@ -301,7 +301,12 @@ class MultiDataPlane:
 
     def run(self, pkts, inmeta, **kw) -> BatchResult:
         """A batch split by owner, each part through its GPU, results back in arrival order
-        (host arrays in and out; the multi-GPU live path is the native engine's job)."""
+        (host arrays in and out; the multi-GPU live path is the native engine's job).
+
+        Split chains (a hop placed on another GPU, ``"ttl@1"``): a frame whose chain hands it over
+        comes out of its first GPU with meta REMOTE (port = the GPU plane) and a HopState record;
+        its header slot and record go device-to-device to that plane (the xGMI hop), which runs the
+        rest of the chain (DataPlane.resume), as often as the chain hands it on."""
         if self.gpu:
             import torch
 
@@ -313,6 +318,7 @@ class MultiDataPlane:
         own = self.owners(pk, im)
         out = np.zeros((n, 64), np.uint8)
         meta = np.zeros(n, np.uint32)
+        pend = []   # (global indices, header slots, HopState records) handed to another plane
         for g, p in enumerate(self.planes):
             sel = np.nonzero(own == g)[0]
             if not len(sel):
@@ -327,7 +333,61 @@ class MultiDataPlane:
             else:
                 r = p.run(pk[sel], im[sel])
                 out[sel], meta[sel] = r.out, r.meta
-        return BatchResult(out, meta, n, {"owner": own})
+            if "hop_state" in r.extra:
+                pend += self._handoffs(sel, meta[sel], r.out, r.extra["hop_state"])
+        hops = 0
+        while pend:
+            hops += 1
+            if hops > 7:   # (a chain has at most 7 hops: a record cannot come round again)
+                raise RuntimeError("split chain handed over more often than it has hops")
+            nxt = []
+            for gidx, tgt, hdr, st in pend:
+                if tgt >= self.n:   # a hop placed on a GPU this node does not have: dropped
+                    meta[gidx] = _drop_meta(T_BADPORT)
+                    continue
+                q = self.planes[tgt]
+                if q.gpu:
+                    import torch
+
+                    rr = q.resume(hdr.to(q.tdev), st.to(q.tdev))   # device to device: the xGMI hop
+                    torch.cuda.synchronize(q.tdev)
+                    out[gidx] = rr.out.cpu().numpy()
+                    meta[gidx] = rr.meta.cpu().numpy().view(np.uint32)
+                else:
+                    rr = q.resume(hdr, st)
+                    out[gidx], meta[gidx] = rr.out, rr.meta
+                nxt += self._handoffs(gidx, meta[gidx], rr.out, rr.extra["hop_state"])
+            pend = nxt
+        return BatchResult(out, meta, n, {"owner": own, "handoff_rounds": hops})
+
+    @staticmethod
+    def _handoffs(gidx: np.ndarray, meta: np.ndarray, out, hop_state) -> list:
+        """The frames of one plane's results that its chains hand to another plane, grouped by
+        target: [(global indices, target plane, header slots, HopState records)] (slots and records
+        stay where they are: device tensors on a GPU plane)."""
+        reason = (meta >> 26) & 0xF
+        h = np.nonzero(reason == T_REMOTE)[0]
+        if not len(h):
+            return []
+        tgt = meta[h] & 0xFFF
+        res = []
+        for t in np.unique(tgt):
+            li = h[tgt == t]
+            if not isinstance(out, np.ndarray):   # a GPU plane's tensors
+                import torch
+
+                ix = torch.from_numpy(li.astype(np.int64)).to(out.device)
+                res.append((gidx[li], int(t), out.index_select(0, ix).contiguous(), hop_state.index_select(0, ix).contiguous()))
+            else:
+                res.append((gidx[li], int(t), np.ascontiguousarray(out[li]), np.ascontiguousarray(hop_state[li])))
+        return res
+
+
+T_BADPORT, T_REMOTE = 1, 10
+
+
+def _drop_meta(reason: int) -> int:
+    return 0xFFF | (reason << 26)
 
 
 def visible_devices() -> list[str]:

@@ -781,11 +781,59 @@ class LagTable:
         self.version += 1
 
 
+HOP_XFER = 0x10          # | plane: the rest of the chain runs on that GPU (nfdp.h kHopXfer)
+MAX_XFER_PLANE = 15
+
+
+def expand_hops(hops) -> list[int]:
+    """Chain hops -> opcodes.  A hop may name the GPU it runs on, ``"ttl@1"``; the chain then hands
+    the frame over (a kHopXfer op) wherever the GPU changes, and a hop without ``@`` runs where the
+    previous one did (the first on the GPU the frame entered).  ``"@1"`` alone is an explicit
+    hand-off.  A route hop cannot come before a hand-off (resume_stage replays the earlier hops'
+    egress decisions, and a route's depends on the header it rewrote)."""
+    codes: list[int] = []
+    cur = None
+    for h in hops:
+        if isinstance(h, str):
+            name, _, at = h.partition("@")
+            if at:
+                g = int(at)
+                if not 0 <= g <= MAX_XFER_PLANE:
+                    raise ValueError(f"hop {h!r}: GPU plane in [0, {MAX_XFER_PLANE}]")
+                if g != cur:
+                    codes.append(HOP_XFER | g)
+                    cur = g
+            if name:
+                if name not in HOP_NAMES:
+                    raise ValueError(f"unknown hop {name!r}")
+                codes.append(HOP_NAMES[name])
+        else:
+            codes.append(int(h))
+    xf = [i for i, c in enumerate(codes) if c >= HOP_XFER]
+    if xf and any(c == HOP_ROUTE for c in codes[: xf[-1]]):
+        raise ValueError("a route hop cannot come before a hand-off to another GPU")
+    return codes
+
+
 class ChainTable:
     def __init__(self, capacity: int = 4096):
         self.a = np.zeros(capacity, CHAIN_DTYPE)
         self.n = 1  # chain 0 = empty chain (plain forward to flow.out_port)
         self.version = 0
+
+    def xfer_planes(self) -> set[int]:
+        """GPU planes that split chains hand frames to (empty: no chain crosses GPUs)."""
+        a = self.a[: self.n]
+        out: set[int] = set()
+        for row in a[a["nhops"] > 0]:
+            out.update(int(c) & MAX_XFER_PLANE for c in row["hop"][: int(row["nhops"])] if c >= HOP_XFER)
+        return out
+
+    def split(self) -> bool:
+        a = self.a[: self.n]
+        hop = a["hop"]
+        live = np.arange(hop.shape[1])[None, :] < a["nhops"][:, None]
+        return bool(((hop >= HOP_XFER) & live).any())
 
     def add(self, hops, acl_id: int = 0) -> int:
         if self.n >= len(self.a):
@@ -796,9 +844,9 @@ class ChainTable:
         return cid
 
     def set(self, cid: int, hops, acl_id: int = 0) -> None:
-        codes = [HOP_NAMES[h] if isinstance(h, str) else int(h) for h in hops]
+        codes = expand_hops(hops)
         if len(codes) > 7:
-            raise ValueError("at most 7 hops per chain")
+            raise ValueError("at most 7 hops per chain (hand-offs to another GPU included)")
         hop = np.zeros(7, np.uint8)
         hop[: len(codes)] = codes
         self.a[cid]["nhops"] = len(codes)

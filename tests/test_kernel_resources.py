@@ -25,7 +25,7 @@ HEADLINE_SGPR_SPILLS = 250
 # (source, mangled-name prefix, max spilled VGPRs, min waves / SIMD)
 BUDGET = [
     # headline: lds hash + MFMA ACL, 1 GPU; and the MFMA-hash twin
-    ("kernels.hip", "_ZN4nfdp12fused_kernelILi1ELi1ELb0ELb0ELb0ELb0E", 16, 4),
+    ("kernels.hip", "_ZN4nfdp12fused_kernelILi1ELi1ELb0ELb0ELb0ELb0ELb0E", 16, 4),
     ("kernels.hip", "_ZN4nfdp12fused_kernelILi2ELi1ELb0ELb0ELb0E", 24, 4),
     # early-fetch instances (2 waves / SIMD by design): no spills
     ("kernels.hip", "_ZN4nfdp12fused_kernelILi1ELi1ELb0ELb1ELb0E", 0, 2),
@@ -36,6 +36,10 @@ BUDGET = [
     # the headline's budget
     ("kernels.hip", "_ZN4nfdp12fused_kernelILi1ELi1ELb0ELb0ELb0ELb1E", 17, 4),
     ("kernels.hip", "_ZN4nfdp9v6_kernel", 0, 2),
+    # split-chain instances (kHopXfer: the SFC hop pipeline across GPUs) and the resume side
+    ("kernels.hip", "_ZN4nfdp12fused_kernelILi1ELi1ELb0ELb0ELb0ELb0ELb1E", 32, 4),
+    ("kernels.hip", "_ZN4nfdp13resume_kernel", 0, 4),
+    ("kernels.hip", "_ZN4nfdp15hop_pack_kernel", 0, 8),
     # persistent ring kernels: no spills at all
     ("ring.hip", "_ZN4nfdp11ring_kernel", 0, 2),
 ]
@@ -76,7 +80,7 @@ def test_hot_kernel_register_budget(rows, src, prefix, max_spill, min_occ):
 
 
 def test_headline_sgpr_spill_budget(rows):
-    r = [x for x in rows["kernels.hip"] if x["name"].startswith("_ZN4nfdp12fused_kernelILi1ELi1ELb0ELb0ELb0ELb0E")]
+    r = [x for x in rows["kernels.hip"] if x["name"].startswith("_ZN4nfdp12fused_kernelILi1ELi1ELb0ELb0ELb0ELb0ELb0E")]
     assert r and r[0].get("SGPRs Spill", 0) <= HEADLINE_SGPR_SPILLS, r
 
 
