@@ -658,6 +658,19 @@ struct GpuSideSink {
   }
 };
 
+// gfx950 store-data hazard: a dwordx4 buffer store whose soffset is an SGPR reads its data VGPRs
+// after issue, and a VALU that overwrote them in the very next instruction stored the NEW value
+// for some lanes (r5 s8: 4 frames of 64K corrupted, dword 1 of the last chunk pass, the meta
+// offset i*4 in their place; tools/store_hazard_scan.py finds the sequence in the assembly).
+// LLVM inserts the wait state only when the soffset is not a register.  Every 16-B buffer store
+// here goes through store_b128: the asm after it claims to rewrite the stored vector, so its VGPRs
+// stay allocated - nothing else can be written into them - until the s_nop has issued.
+template <int AUX>
+__device__ __forceinline__ void store_b128(v4u w, __amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+  __builtin_amdgcn_raw_buffer_store_b128(w, r, voff, soff, AUX);
+  asm volatile("s_nop 1" : "+v"(w));
+}
+
 // ---- coalesced frame I/O (tools/copy_bench.hip: 6.4 TB/s vs 1.4 TB/s for per-lane slots) ----
 // A wave's 64 slots are one contiguous 4-KiB run.  Each dwordx4 instruction covers 1 KiB of it
 // lane-contiguously (16 full 64-B lines) instead of 16 B of 64 different lines, and the wave's
@@ -718,7 +731,7 @@ __device__ __forceinline__ void wave_frames_store(uint4* kx, const uint32_t* o, 
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     const v4u w = {v.x, v.y, v.z, v.w};
     const bool drop = (skip >> (16u * q + (lane >> 2))) & 1ull;
-    __builtin_amdgcn_raw_buffer_store_b128(w, r, drop ? kNoRun : lane * 16u + q * 1024u, run, AUX);
+    store_b128<AUX>(w, r, drop ? kNoRun : lane * 16u + q * 1024u, run);
   }
 }
 
@@ -755,7 +768,7 @@ __device__ __forceinline__ void wave_segment_store(uint4* kx, const uint32_t* o,
       const uint32_t n4 = min(16u, cnt - sub) * 4u;
       const bool ok = lane < n4 && p0 + sub + (lane >> 2) < cap;
       const v4u w = {v.x, v.y, v.z, v.w};
-      __builtin_amdgcn_raw_buffer_store_b128(w, r, ok ? lane * 16u : kNoRun, d * seg_bytes + 64u + (p0 + sub) * 64u, AUX);
+      store_b128<AUX>(w, r, ok ? lane * 16u : kNoRun, d * seg_bytes + 64u + (p0 + sub) * 64u);
     }
   }
 }

@@ -462,12 +462,11 @@ __global__ __launch_bounds__(kFB, EARLY ? NFDP_EARLY_WAVES_PER_EU : NFDP_FUSED_W
         const bool xf = valid && e.reason == kRemote && e.inner_len != 0u;
         const HopState hs = hop_state_of(p, st, e, act, acl_rule, hash);
         const uint32_t off = xf ? i * 32u : kNoRun;
-        typedef unsigned int v4u_t __attribute__((ext_vector_type(4)));
-        const v4u_t h0 = {hs.inmeta, hs.hash, (uint32_t)hs.acl_rule, hs.hop};
-        const v4u_t h1 = {(uint32_t)act.chain_id | ((uint32_t)act.out_port << 16), act.nat_ip,
-                          (uint32_t)act.nat_port | ((uint32_t)act.vlan << 16), act.flow_id};
-        __builtin_amdgcn_raw_buffer_store_b128(h0, r_hop, off, 0, kStreamAux);
-        __builtin_amdgcn_raw_buffer_store_b128(h1, r_hop, off, 16, kStreamAux);
+        const v4u h0 = {hs.inmeta, hs.hash, (uint32_t)hs.acl_rule, hs.hop};
+        const v4u h1 = {(uint32_t)act.chain_id | ((uint32_t)act.out_port << 16), act.nat_ip,
+                        (uint32_t)act.nat_port | ((uint32_t)act.vlan << 16), act.flow_id};
+        store_b128<kStreamAux>(h0, r_hop, off, 0);
+        store_b128<kStreamAux>(h1, r_hop, off, 16);
       }
       if constexpr (V6) {   // (no prefetch in these instances: the next slot is loaded here)
         const uint32_t nx = i + stride;
@@ -590,7 +589,7 @@ __global__ __launch_bounds__(256) void pair_kernel(uint4* pkts, uint32_t* inmeta
         const uint4 v = T[(q * 64 + lane) ^ lsw];
         const v4u w = {v.x, v.y, v.z, v.w};
         const bool keep = (mod >> (16u * q + (lane >> 2))) & 1ull;   // chunk q*64+lane is part of slot 16q + lane/4
-        __builtin_amdgcn_raw_buffer_store_b128(w, r_pk, keep ? lane * 16u + q * 1024u : kNoRun, soff, 0);
+        store_b128<0>(w, r_pk, keep ? lane * 16u + q * 1024u : kNoRun, soff);
       }
     }
     __builtin_amdgcn_wave_barrier();   // the tile is reloaded next trip

@@ -8,7 +8,9 @@ Differences from the reference (documented quirks fixed): a deleted SFC is NOT r
 
 GPU extension: an NF whose image is `gpu-nf://<kind>[,<kind>...]` (acl, nat, l2fwd, ttl, vlan,
 hairpin) needs no pod — it runs inside the GPU pipeline; the reconciler records it in the SFC
-status and the GPU VSP programs it as a chain hop (see vsp/gpu.py).
+status and the GPU VSP programs it as a chain hop (see vsp/gpu.py).  `<kind>@<gpu>` places the hop
+on one of the node's GPUs: the chain hands its frames over to that GPU mid-chain (the SFC hop
+pipeline across GPUs, parallel/hops.py).
 """
 from __future__ import annotations
 

@@ -490,8 +490,17 @@ class GpuVsp(VspBase):
         self._uplink_vp = None
 
     def on_gpu_chain(self, sfc_name: str, kinds: list[str]) -> int:
+        """A gpu-nf:// chain as a chain-table entry.  A hop may name the GPU it runs on
+        (``gpu-nf://acl,nat`` then ``gpu-nf://ttl@1,l2fwd@1``): the chain then hands its frames to
+        that GPU's data plane mid-chain (the SFC hop pipeline across GPUs, dataplane/tables.py
+        expand_hops, parallel/hops.py); the plane must exist on this node."""
         with self._lock:
             self._ensure_dp()
+            planes = len(getattr(self.dp, "planes", [self.dp]))
+            for k in kinds:
+                at = str(k).partition("@")[2]
+                if at and not 0 <= int(at) < planes:
+                    raise ValueError(f"gpu-nf hop {k!r}: this node's data plane has {planes} GPU(s)")
             if sfc_name in self.gpu_chains:
                 cid = self.gpu_chains[sfc_name]
                 self.dp.chains.set(cid, kinds)

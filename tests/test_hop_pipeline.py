@@ -143,3 +143,17 @@ def test_resume_record_layout():
     np.testing.assert_array_equal(hs[:, 2].view(np.int32), r.extra["acl"])
     assert (hs[:, 3] == 2).all()   # acl, xfer -> resumes at hop 2 (nat)
     assert (hs[:, 4] & 0xFFFF == sc.chain_id).all()
+
+
+def test_vsp_places_gpu_nf_hops_on_gpus(tmp_path):
+    """gpu-nf://ttl@1 through the VSP: a split chain on a 2-GPU node, refused on a GPU it lacks."""
+    from dpu_operator_amd.utils.paths import PathManager
+    from dpu_operator_amd.cni.netlink import FakeNetlink
+    from dpu_operator_amd.vsp.gpu import GpuVsp
+
+    vsp = GpuVsp(PathManager(str(tmp_path)), device="cpu", nl=FakeNetlink(), flow_buckets=1 << 8, gpus=2)
+    cid = vsp.on_gpu_chain("sfc-a", ["acl", "nat", "ttl@1", "l2fwd@1"])
+    assert vsp.dp.chains.split() and vsp.dp.chains.xfer_planes() == {1}
+    assert list(vsp.dp.chains.a[cid]["hop"][:5]) == [1, 2, 0x11, 4, 3]
+    with pytest.raises(ValueError):
+        vsp.on_gpu_chain("sfc-b", ["acl", "ttl@2"])

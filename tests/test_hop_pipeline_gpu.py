@@ -36,7 +36,12 @@ def _compare(m1, o1, m2, o2):
     np.testing.assert_array_equal(m1, m2)
     fwd = ((m1 >> 26) & 0xF) == 0
     assert fwd.mean() > 0.5
-    np.testing.assert_array_equal(np.asarray(o1)[fwd], np.asarray(o2)[fwd])
+    o1, o2 = np.asarray(o1), np.asarray(o2)
+    bad = np.nonzero(fwd & (o1 != o2).any(1))[0]
+    for i in bad[:6]:   # (what differs, if anything: frame, meta, byte columns, values)
+        cols = np.nonzero(o1[i] != o2[i])[0]
+        print("frame", i, hex(int(m1[i])), "cols", cols.tolist(), o1[i][cols].tolist(), o2[i][cols].tolist())
+    assert len(bad) == 0, f"{len(bad)} forwarded frames differ"
 
 
 @pytest.mark.parametrize("hash_mode", ["mfma", "lds"])

@@ -98,3 +98,35 @@ def test_no_direct_to_lds_loads_in_the_data_plane():
             if re.search(r"buffer_load_lds|global_load_lds|load_to_lds", line) and not line.lstrip().startswith("//"):
                 hits.append(f"{f.name}:{i}")
     assert not hits, hits
+
+
+def test_no_store_data_hazard_in_device_code(tmp_path):
+    """No 16-B buffer store whose data VGPRs the next instruction overwrites (gfx950 store-data
+    hazard, device.h store_b128; tools/store_hazard_scan.py): scans the built objects' gfx950 code."""
+    import shutil
+    import sys
+
+    sys.path.insert(0, str(REPO / "tools"))
+    from store_hazard_scan import scan_text
+
+    llvm = Path("/opt/rocm/lib/llvm/bin")
+    tools = [llvm / t for t in ("llvm-objcopy", "clang-offload-bundler", "llvm-objdump")]
+    objs = sorted((REPO / "build" / "native" / "_nfdp").glob("*.hip.o"))
+    if not all(t.exists() for t in tools) or not objs:
+        pytest.skip("no gfx950 toolchain / no built objects")
+    scanned = 0
+    for o in objs:
+        fb, co = tmp_path / (o.stem + ".fatbin"), tmp_path / (o.stem + ".co")
+        r = subprocess.run([str(tools[0]), "--dump-section", f".hip_fatbin={fb}", str(o), str(tmp_path / "x.o")],
+                           capture_output=True, text=True)
+        if r.returncode != 0:   # (an object with no device code)
+            continue
+        subprocess.run([str(tools[1]), "--unbundle", "--type=o", f"--input={fb}",
+                        "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", f"--output={co}"], check=True, capture_output=True)
+        dis = subprocess.run([str(tools[2]), "-d", "--mcpu=gfx950", str(co)], check=True, capture_output=True,
+                             text=True).stdout
+        hits = scan_text(dis)
+        assert not hits, (o.name, hits[:3])
+        scanned += 1
+    assert scanned >= 3   # kernels / ring / shard at least
+    shutil.rmtree(tmp_path, ignore_errors=True)
