@@ -160,8 +160,13 @@ constexpr int kStreamAux = 2;        // nt: frames are read once / written once 
 // instances keep their register budget untouched.
 // XFER: the instances for tables with split chains (kHopXfer hops): a frame handed to another GPU
 // leaves its HopState record in a.hop_state (two fixed-count stores in the tail, like the others).
+#ifndef NFDP_XFER_WAVES_PER_EU
+#define NFDP_XFER_WAVES_PER_EU 4   // the split-chain instances (r5 s9: 346 us / 4M frames with 30 spilled
+                                   // VGPRs at 4 waves, 387 us spill-free at 3)
+#endif
 template <int HASH, int ACL, bool REMOTE, bool EARLY, bool LIST = false, bool V6 = false, bool XFER = false>
-__global__ __launch_bounds__(kFB, EARLY ? NFDP_EARLY_WAVES_PER_EU : NFDP_FUSED_WAVES_PER_EU) void fused_kernel(FusedArgs a) {
+__global__ __launch_bounds__(kFB, EARLY ? NFDP_EARLY_WAVES_PER_EU : (XFER ? NFDP_XFER_WAVES_PER_EU : NFDP_FUSED_WAVES_PER_EU))
+void fused_kernel(FusedArgs a) {
   static_assert(!V6 || (!REMOTE && !LIST), "IPv6 instances are 1-GPU instances");
   static_assert(!XFER || (!REMOTE && !LIST && !V6), "split-chain instances are 1-GPU IPv4 instances");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -1017,34 +1022,54 @@ __global__ __launch_bounds__(256) void v6_kernel(V6Args a) {
 // hop_pack_kernel: this GPU's frames handed to `plane` (meta reason kRemote, port = plane, a
 // HopState record beside them) -> that plane's inbox.  The inbox lives on the GPU that resumes the
 // chain, so these are peer stores over xGMI (plain stores into a peer allocation; the same code
-// when both planes share a device).  Positions: one atomic per wave on this GPU's fill counter,
-// arrival order kept inside a wave; the publish step hands the count over once the batch is packed.
+// when both planes share a device).  A workgroup packs a chunk of kPackChunk frames: it counts its
+// chunk's hand-offs (ballots), claims their inbox run with ONE atomic on this GPU's fill counter
+// (per-wave claims on one word serialised at the memory side: 774 us per 4M frames, r5 s9
+// profile), then each wave writes its quarter of the chunk in arrival order.  The publish step
+// hands the count over once the batch is packed.
+constexpr uint32_t kPackChunk = 4096;   // frames per workgroup pass (4 waves x 1024) at full batches
 __global__ __launch_bounds__(256) void hop_pack_kernel(const uint4* out, const uint32_t* meta, const HopState* state,
                                                        uint32_t n, const uint32_t* n_dev, uint32_t plane,
-                                                       uint32_t* fill, HopInbox dst) {
+                                                       uint32_t* fill, HopInbox dst, uint32_t chunk) {
+  __shared__ uint32_t wcnt[4];
+  __shared__ uint32_t wbase[4];
   const uint32_t nn = n_dev ? min(n, *n_dev) : n;
-  const uint32_t lane = threadIdx.x & 63u;
-  // block-uniform trip count: every wave reaches each ballot
-  for (uint32_t base = blockIdx.x * 256u; base < nn; base += gridDim.x * 256u) {
-    const uint32_t i = base + threadIdx.x;
-    const uint32_t m = i < nn ? meta[i] : 0u;
-    const bool mine = i < nn && ((m >> 26) & 0xFu) == kRemote && (m & 0xFFFu) == plane;
-    const unsigned long long b = __ballot(mine);
-    if (b == 0ull) continue;
-    const uint32_t pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
-    const int leader = __builtin_ctzll(b);
-    uint32_t pos0 = 0;
-    if (lane == (uint32_t)leader) pos0 = atomicAdd(fill, (uint32_t)__builtin_popcountll(b));
-    pos0 = __builtin_amdgcn_readlane(pos0, leader);
-    if (mine) {
-      const uint32_t pos = pos0 + pre;
-      if (pos < dst.cap) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) dst.hdr[(size_t)pos * 4 + k] = out[(size_t)i * 4 + k];
-        dst.state[pos] = state[i];
-        dst.idx[pos] = i;
-      }
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6;
+  auto mine = [&](uint32_t i) -> bool {
+    if (i >= nn) return false;
+    const uint32_t m = meta[i];
+    return ((m >> 26) & 0xFu) == kRemote && (m & 0xFFFu) == plane;
+  };
+  // block-uniform trip count: every wave reaches each ballot and barrier
+  for (uint32_t c0 = blockIdx.x * chunk; c0 < nn; c0 += gridDim.x * chunk) {
+    const uint32_t w0 = c0 + wave * (chunk / 4);   // this wave's quarter, 16 runs of 64
+    uint32_t cnt = 0;
+    for (uint32_t k = 0; k < chunk / 4; k += 64) cnt += (uint32_t)__builtin_popcountll(__ballot(mine(w0 + k + lane)));
+    if (lane == 0) wcnt[wave] = cnt;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const uint32_t tot = wcnt[0] + wcnt[1] + wcnt[2] + wcnt[3];
+      uint32_t b0 = tot ? atomicAdd(fill, tot) : 0u;
+      for (int w = 0; w < 4; ++w) { wbase[w] = b0; b0 += wcnt[w]; }
     }
+    __syncthreads();
+    uint32_t pos0 = wbase[wave];
+    for (uint32_t k = 0; k < chunk / 4 && cnt; k += 64) {
+      const uint32_t i = w0 + k + lane;
+      const bool my = mine(i);
+      const unsigned long long bm = __ballot(my);
+      if (my) {
+        const uint32_t pos = pos0 + __builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
+        if (pos < dst.cap) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) dst.hdr[(size_t)pos * 4 + q] = out[(size_t)i * 4 + q];
+          dst.state[pos] = state[i];
+          dst.idx[pos] = i;
+        }
+      }
+      pos0 += (uint32_t)__builtin_popcountll(bm);
+    }
+    __syncthreads();   // (wcnt / wbase are rewritten next pass)
   }
 }
 
@@ -1063,10 +1088,14 @@ hipError_t launch_hop_pack(const void* out, const uint32_t* meta, const HopState
                            hipStream_t s) {
   if (!out || !meta || !state || !fill || !dst.count || !dst.hdr || !dst.state || !dst.idx || plane > kHopXferPlanes)
     return hipErrorInvalidValue;
-  uint32_t grid = (n + 255) / 256;
+  // chunk: 4096 frames per workgroup at full batches (few claims), down to 256 for small ones
+  // (enough workgroups to spread a 64K batch over the CUs); a multiple of 256 (4 waves x 64)
+  uint32_t chunk = kPackChunk;
+  while (chunk > 256 && (n + chunk - 1) / chunk < 512) chunk >>= 1;
+  uint32_t grid = (n + chunk - 1) / chunk;
   if (grid > 2048) grid = 2048;
   if (grid) hipLaunchKernelGGL(hop_pack_kernel, dim3(grid), dim3(256), 0, s, reinterpret_cast<const uint4*>(out),
-                               meta, state, n, n_dev, plane, fill, dst);
+                               meta, state, n, n_dev, plane, fill, dst, chunk);
   hipLaunchKernelGGL(hop_publish_kernel, dim3(1), dim3(64), 0, s, fill, dst.cap, dst.count);
   return hipGetLastError();
 }
