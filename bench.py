@@ -124,64 +124,27 @@ def _unsteered(a, dp, sc, owner, rank, world, dev, cdev, torch, dist, P, RssShar
     return res
 
 
-def measure_hops(a, sc, dev, torch, S, P) -> dict:
-    """SFC hop pipeline across GPUs (BASELINE config 4), rehearsed on one GPU: the headline chain
-    split after nat - acl + nat on plane 0, l2fwd + egress on plane 1 - over two data planes with
-    their own replicated tables (1M flows each).  The hand-off is the product path
-    (parallel/hops.py): XFER fused instance -> hop_pack_kernel storing slot + 32-B record into
-    plane 1's inbox (peer stores; xGMI when the planes are different GPUs) -> resume_kernel.  Both
-    planes share one GPU here, so the stages run back to back: `mpps` is the pipeline's
-    throughput on ONE GPU (two GPUs overlap consecutive batches); `per_hop_us` splits a 64K
-    batch's latency into the first GPU's kernel, the hand-off and the resuming GPU's kernel."""
-    from dpu_operator_amd.dataplane.multi import MultiDataPlane
-    from dpu_operator_amd.parallel.hops import HopPipeline
+def measure_hops(a, devices: str) -> dict:
+    """SFC hop pipeline across GPUs (BASELINE config 4): the headline chain split after nat - acl +
+    nat on one data plane, l2fwd + egress on another - with the product's in-HBM hand-off
+    (parallel/hops.py: XFER fused instance -> hop_pack_kernel storing slot + 32-B record into the
+    other plane's inbox -> resume_kernel).  1 GPU: both planes on cuda:0 (a rehearsal: the stages run
+    back to back on one GPU).  N > 1: rank 0 puts them on cuda:0 and cuda:1, so the hand-off's
+    peer stores cross xGMI.  Run as a child process (tools/hop_bench.py) so nothing on that path
+    can take the headline with it; `per_hop_us` splits a 64K batch's latency."""
+    import subprocess
 
-    multi = MultiDataPlane([str(dev), str(dev)], placement="port", hash_mode=a.hash, acl_mode=a.acl_mode,
-                           flow_buckets=1 << max(10, int(math.ceil(math.log2(a.flows / 2)))))
-    sc2 = S.build_sfc(multi, n_pods=a.pods_per_gpu, n_flows=a.flows, n_acl=a.acl, hops=("acl", "nat", "l2fwd@1"))
-    multi.commit()
-    n = a.batch
-    bs = []
-    for r in range(2):
-        pk, im = S.traffic(sc2, n, seed=9500 + r)
-        bs.append((torch.from_numpy(pk).to(dev), torch.from_numpy(im.view(np.int32)).to(dev)))
-    hp = HopPipeline(multi.planes, n)
-    for k in range(3):
-        hp.step(*bs[k % 2])
-    torch.cuda.synchronize()
-    steps = max(3, a.variant_steps)
-    t0 = time.perf_counter()
-    for k in range(steps):
-        hp.step(*bs[k % 2])
-    torch.cuda.synchronize()
-    el = time.perf_counter() - t0
-    out, meta = hp.results(n)
-    rs = P.meta_fields(meta)[2]
-    res = {"split": "acl,nat | l2fwd (plane 0 | plane 1)", "planes": [str(dev), str(dev)],
-           "mpps": round(n * steps / el / 1e6, 1), "ms_per_batch": round(el / steps * 1e3, 4),
-           "forwarded_fraction": round(float(np.mean(rs == 0)), 4),
-           "handed_off_fraction": round(float(multi.planes[0].drop_counters().get("remote", 0)) /
-                                        max(1, n * (steps + 4)), 4)}
-    # per-hop latency: one 64K batch at a time, GPU clock (events) at each stage boundary
-    nsm = min(1 << 16, n)
-    hs = HopPipeline(multi.planes, nsm)
-    small = (bs[0][0][:nsm].contiguous(), bs[0][1][:nsm].contiguous())
-    f_us, h_us, r_us = [], [], []
-    for k in range(60):
-        tm = {}
-        hs.step(*small, timing=tm)
-        torch.cuda.synchronize()
-        if k >= 10:
-            f_us.append(tm["t0"].elapsed_time(tm["fused"]) * 1e3)
-            h_us.append(tm["fused"].elapsed_time(tm["handoff"]) * 1e3)
-            r_us.append(tm["handoff"].elapsed_time(tm["resume"]) * 1e3)
-    res["per_hop_us"] = {"batch": nsm, "first_gpu_kernel": round(float(np.median(f_us)), 2),
-                         "handoff": round(float(np.median(h_us)), 2),
-                         "resume_gpu_kernel": round(float(np.median(r_us)), 2),
-                         "total": round(float(np.median(np.add(np.add(f_us, h_us), r_us))), 2)}
-    del hp, hs, bs, multi
-    torch.cuda.empty_cache()
-    return res
+    cmd = [sys.executable, os.path.join(os.path.dirname(os.path.abspath(__file__)), "tools", "hop_bench.py"),
+           "--devices", devices, "--batch", str(a.batch), "--flows", str(a.flows), "--acl", str(a.acl),
+           "--pods", str(a.pods_per_gpu), "--steps", str(max(3, a.variant_steps)), "--hash", a.hash]
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=600)
+    except subprocess.TimeoutExpired:
+        return {"error": "timed out (600 s)"}
+    lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    if r.returncode != 0 or not lines:
+        return {"error": f"exit {r.returncode}: {(r.stderr or r.stdout)[-300:]}"}
+    return json.loads(lines[-1])
 
 
 def _live_veth(dev: str) -> dict:
@@ -227,6 +190,7 @@ def parse():
     ap.add_argument("--rotate", type=int, default=4)
     ap.add_argument("--no-lowlat", action="store_true", help="skip the small-batch latency probe")
     ap.add_argument("--no-variants", action="store_true", help="skip the mixed / ACL1024 / IMIX measurements")
+    ap.add_argument("--no-hops", action="store_true", help="skip the SFC hop pipeline across GPUs (tools/hop_bench.py)")
     ap.add_argument("--no-live", action="store_true", help="skip the live pod-to-pod (native I/O engine) block")
     ap.add_argument("--no-unsteered", action="store_true", help="N > 1 rss: skip the exchange-bound (unsteered) variant")
     ap.add_argument("--live-workers", type=int, default=2, help="native I/O engine delivery threads per queue")
@@ -730,14 +694,18 @@ def main() -> None:
     if world == 1 and a.io == "device" and not a.no_variants:
         variants = measure_variants(a, dp, sc, dev, torch, S, P)
 
-    # SFC hop pipeline across GPUs (1 GPU rehearsal, after the timed region): the headline chain
-    # split over two data planes with the in-HBM hand-off between them
+    # SFC hop pipeline across GPUs (after the timed region): the headline chain split over two
+    # data planes with the in-HBM hand-off between them - both on cuda:0 at N = 1, cuda:0 -> cuda:1
+    # over xGMI at N > 1 (rank 0 measures while the other ranks wait at the barrier)
     hops = None
-    if world == 1 and a.io == "device" and not a.no_variants:
-        try:
-            hops = measure_hops(a, sc, dev, torch, S, P)
-        except Exception as ex:  # noqa: BLE001 - the headline must still be reported
-            hops = {"error": str(ex)[:200]}
+    if a.io == "device" and not a.no_variants and not a.no_hops:
+        if world > 1:
+            dist.barrier()
+        if rank == 0:
+            peer = world > 1 and not a.rehearse and torch.cuda.device_count() > 1
+            hops = measure_hops(a, "cuda:0,cuda:1" if peer else "cuda:0,cuda:0")
+        if world > 1:
+            dist.barrier()
 
     # live pod -> pod path (1 GPU, after the timed region): shared-memory pod vports, the native C++
     # I/O engine (csrc/nfdp/iox) and the persistent ring kernel; C++ pod generator / sinks measure
