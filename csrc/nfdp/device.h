@@ -58,6 +58,10 @@ struct AclView {
   // ltiles).  The fused kernel's one-block-per-CU instances stage more than kLdsAclTiles.
   uint32_t ltiles = tiles < kLdsAclTiles ? tiles : kLdsAclTiles;
   uint32_t ctiles = ltiles;
+  // prefilter tiles in LDS (one-block-per-CU fused instances): tile t's prefilter is row t % 16 of
+  // prefilter tile t / 16 (host.cpp build_acl_frags); ptiles 0: the scalar prefilter cursor
+  const v4i* pw = nullptr; const v4i* pc = nullptr;
+  uint32_t ptiles = 0;
 };
 NFDP_HD uint32_t acl_groups(uint32_t tiles) { return (tiles + kAclGroup - 1) / kAclGroup; }
 // Raw first-match value (mismatch << 12 | rule) -> rule index or -1.
@@ -85,6 +89,13 @@ NFDP_HD int acl_rule_of(uint32_t b, uint32_t n_acl) {
 #define NFDP_ACL_LOOKAHEAD 1   // r4 s25 A/B: ClassBench-style set +5.5 % (7.17 -> 7.56 Gpps) over no lookahead
 // (r5: tile MFMAs ping-ponged between two accumulator sets, tile k's minima under tile k+1's
 // MFMAs: ClassBench set 7.84 vs 7.92 Gpps without, profiles/r5_s6_ab_acl_pingpong.jsonl - not kept)
+#endif
+#ifndef NFDP_ACL_PTILES
+// prefilter tiles: 16 tiles' prefilters tested by one MFMA per 16 packets, only admitted tiles run.
+// r5 s11 A/B on the ClassBench-style set: 7.16 vs 7.71 Gpps without (profiles/r5_s11_ab_ptiles.jsonl):
+// half the tile MFMAs, but the per-tile loop loses the straight-line 8-tile groups' overlap, and
+// the 2-wave instance is bound by latency, not by its MFMA count.  Off.
+#define NFDP_ACL_PTILES 0
 #endif
 #ifndef NFDP_PIPE_UNROLL
 #define NFDP_PIPE_UNROLL 1   // r3 s16 A/B: ACL1024 0.3145 vs 0.3211 ms, ClassBench unchanged
@@ -258,6 +269,68 @@ __device__ __forceinline__ void classify_wave(const FlowKey& key, uint4* kx, con
     // straddle ltiles (a multiple of 8 unless it covers every tile).
     const uint32_t ngroups = acl_groups(av.tiles);
     const uint32_t lds_groups = min(ngroups, (PIPE ? av.ltiles : kLdsAclTiles) / kAclGroup);
+    // Prefilter tiles (PIPE instances, LDS): row j of prefilter tile p is tile 16 p + j's prefilter as
+    // a ternary rule, so 4 MFMAs decide 16 tiles for the wave's 64 packets (accumulator < 4096: no
+    // cared bit differs, the tile can match).  Only the admitted tiles run, straight from their
+    // mask, one fragment ahead.  The scalar cursor below admits whole groups of 8 (per-tile scalar
+    // tests cost more than they saved, r3 s15): on the ClassBench-style set 72 tiles per wave ran
+    // where 37 can match (r5 s10 simulation).
+    bool ptiles_done = false;
+    if constexpr (PIPE && NFDP_ACL_PTILES) {
+      if (av.ptiles && tstep == 1) {
+        ptiles_done = true;
+        auto ld_a = [&](uint32_t t) -> v4i {
+          if (t < av.ltiles) return av.lw[t * 64 + lane];
+          return __builtin_bit_cast(v4i, __builtin_amdgcn_raw_buffer_load_b128(r_gw, (t * 64u + lane) * 16u, 0, 0));
+        };
+        auto ld_c = [&](uint32_t t) -> v4i {
+          if (t < av.ctiles) return av.lc[t * 4 + g];
+          return __builtin_bit_cast(v4i, __builtin_amdgcn_raw_buffer_load_b128(r_gc, (t * 4u + g) * 16u, 0, 0));
+        };
+        for (uint32_t pt = 0; pt < av.ptiles; ++pt) {
+          const v4i pa4 = av.pw[pt * 64 + lane], pci = av.pc[pt * 4 + g];
+          const v8i_t pa = {pa4[0], pa4[1], pa4[2], pa4[3], 0, 0, 0, 0};
+          const v4f_t pc = {__int_as_float(pci[0]), __int_as_float(pci[1]), __int_as_float(pci[2]), __int_as_float(pci[3])};
+          v4f_t pacc[4];
+#pragma unroll
+          for (int tt = 0; tt < 4; ++tt) {
+            const v8i_t b = {bq[tt][0], bq[tt][1], bq[tt][2], bq[tt][3], 0, 0, 0, 0};
+            pacc[tt] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(pa, b, pc, 4, 4, 0, kE8M0Idx, 0, kE8M0One);
+          }
+          // lane l holds rows 4 (l >> 4) + i for packet column l & 15 of each 16-packet group tt
+          uint32_t m16 = 0;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float mn = fminf(fminf(pacc[0][i], pacc[1][i]), fminf(pacc[2][i], pacc[3][i]));
+            const unsigned long long bl = __ballot(mn < 4096.0f);
+#pragma unroll
+            for (int gg = 0; gg < 4; ++gg)
+              m16 |= (((bl >> (16 * gg)) & 0xFFFFull) != 0ull ? 1u : 0u) << (4 * gg + i);
+          }
+          const uint32_t base = pt * 16u;
+          if (base + 16u > av.tiles) m16 &= (1u << (av.tiles - base)) - 1u;
+          m16 = __builtin_amdgcn_readfirstlane(m16);
+          if (!m16) continue;
+          uint32_t t = base + (uint32_t)__builtin_ctz(m16);
+          m16 &= m16 - 1u;
+          v4i a = ld_a(t), ci = ld_c(t);
+          for (;;) {
+            const bool more = m16 != 0u;
+            v4i a2 = a, c2 = ci;
+            if (more) {
+              t = base + (uint32_t)__builtin_ctz(m16);
+              m16 &= m16 - 1u;
+              a2 = ld_a(t);
+              c2 = ld_c(t);
+            }
+            run_tile(a, ci);
+            if (!more) break;
+            a = a2;
+            ci = c2;
+          }
+        }
+      }
+    }
     // PIPE cursor: this wave's next tile >= t and < lim that passes its group and tile prefilters
     // (scalar; the group verdict is cached).  NFDP_PIPE_PF: 2 = group + tile prefilters, 1 = group
     // prefilters only, 0 = none (prefilters only ever skip work: results are the same).
@@ -278,7 +351,7 @@ __device__ __forceinline__ void classify_wave(const FlowKey& key, uint4* kx, con
       }
       return lim;
     };
-    {
+    if (!ptiles_done) {
       // (batches of 4 LDS tiles with their 8 fragment reads in flight together: slower, r3 s15 A/B)
       for (uint32_t gi = 0; gi < lds_groups; ++gi) {
         if ((!PIPE || NFDP_PIPE_PF >= 1) && !pass(gpf + 8 * gi)) continue;
@@ -326,7 +399,7 @@ __device__ __forceinline__ void classify_wave(const FlowKey& key, uint4* kx, con
                    __builtin_bit_cast(v4i, __builtin_amdgcn_raw_buffer_load_b128(r_gc, (nt * 4u + g) * 16u, 0, 0)));
         }
       }
-    } else if (lds_groups < ngroups) {
+    } else if (lds_groups < ngroups && !ptiles_done) {
       // (PIPE: the 2-wave instances, which have the registers for 8 tiles in flight)
       // Tiles past the LDS copy: a scalar cursor yields this wave's next tile that passes its group
       // and tile prefilters; A fragments come in batches of 4 buffer loads, the next batch issued

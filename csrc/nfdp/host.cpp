@@ -218,6 +218,35 @@ AclFrags build_acl_frags(const uint32_t* value, const uint32_t* mask, uint32_t n
     const uint32_t b = g * 16 * kAclGroupTiles, e = std::min(n, b + 16 * kAclGroupTiles);
     prefilter(value, mask, order.data() + b, e > b ? e - b : 0, gpf + 8 * g);
   }
+  // Prefilter tiles: tile t's prefilter (mask, value) as ternary rule row t % 16 of prefilter tile
+  // t / 16, in the same FP4 A-fragment / C-init form, so ONE MFMA per 16 packets tests 16 tiles'
+  // prefilters at once (device.h classify_wave): accumulator < 4096 <=> no cared bit differs.
+  // Appended: wfrag [tiles + ptiles][64][16], cinit ... | [ptiles][4][4] C init.
+  const uint32_t ptiles = (f.tiles + 15) / 16;
+  f.ptiles = ptiles;
+  f.wfrag.resize((size_t)(f.tiles + ptiles) * 64 * 16, 0);
+  f.cinit.resize(f.cinit.size() + (size_t)ptiles * 16, 0);
+  const uint32_t* pfw = reinterpret_cast<const uint32_t*>(f.cinit.data()) + (size_t)f.tiles * 16;   // (re-read: resized)
+  float* pci = reinterpret_cast<float*>(f.cinit.data()) + (size_t)f.tiles * 24 + (size_t)groups * 8;
+  for (uint32_t k = 0; k < ptiles * 16; ++k) {
+    const uint32_t p = k / 16, row = k % 16;
+    float c = 4096.0f + 4095.0f;   // padding row: never passes
+    if (k < f.tiles) {
+      const uint32_t* m = pfw + 8 * k;
+      const uint32_t* v = m + 4;
+      int32_t bb = 0;
+      for (int b = 0; b < 128; ++b) {
+        if (!key_bit(m, b)) continue;
+        const int l = 16 * (b / 32) + (int)row, j = b % 32;   // lane (K block, row), nibble j
+        const uint8_t w = key_bit(v, b) ? 0xA : 0x2;
+        bb += key_bit(v, b);
+        uint8_t& byte = reinterpret_cast<uint8_t&>(f.wfrag[(((size_t)f.tiles + p) * 64 + l) * 16 + j / 2]);
+        byte = (uint8_t)(byte | (w << (4 * (j & 1))));
+      }
+      c = (float)bb * 4096.0f + (float)row;
+    }
+    std::memcpy(&pci[((size_t)p * 4 + row / 4) * 4 + row % 4], &c, 4);
+  }
   return f;
 }
 

@@ -56,8 +56,10 @@ class FlowTableHost {
 struct AclFrags {
   std::vector<int8_t> wfrag;   // [tiles][64][16]: FP4 (e2m1) A fragments, 32 nibbles per lane
   std::vector<int32_t> cinit;  // [tiles][4][4] f32 C init (bias * 4096 + rule) | [tiles][8] tile
-                               // prefilters | [groups of 8 tiles][8] group prefilters
+                               // prefilters | [groups of 8 tiles][8] group prefilters | [ptiles][4][4]
+                               // C init of the prefilter tiles (IPv4 tables; A fragments after the tiles')
   uint32_t tiles = 0;
+  uint32_t ptiles = 0;         // prefilter tiles: tile t's prefilter is row t % 16 of prefilter tile t / 16
 };
 AclFrags build_acl_frags(const uint32_t* value, const uint32_t* mask, uint32_t n);
 // IPv6 ACL tiles: 16 rules x 3 K-blocks of 128 key6 bits ([tiles][3][64] A fragments, [tiles][16]

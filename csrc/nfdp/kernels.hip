@@ -96,8 +96,9 @@ struct FusedArgs {
 __device__ __forceinline__ size_t lds_align16(size_t x) { return (x + 15) & ~(size_t)15; }
 
 struct LdsLayout {
-  size_t acl_w, acl_c, toep_f, toep_t, kx, pc, drops, tports, tchain, tperm, total;
+  size_t acl_w, acl_c, toep_f, toep_t, kx, pc, drops, tports, tchain, tperm, pt_w, pt_c, total;
   uint32_t ltiles, ctiles;  // ACL tiles whose A fragments / C init are staged
+  uint32_t ptiles;          // one_block layouts: the prefilter tiles (device.h classify_wave), staged whole
   bool tabs;  // small tables (ports < kLdsPorts, chain words, ACL verdicts) staged in LDS
 };
 // `one_block`: the instance runs one workgroup per CU (EARLY: 2 waves / SIMD), so the rule tiles
@@ -107,18 +108,22 @@ __host__ __device__ inline LdsLayout lds_layout(int hash_mode, int acl_mode, uin
   LdsLayout L;
   size_t o = 0;
   uint32_t lt = acl_tiles < kLdsAclTiles ? acl_tiles : kLdsAclTiles, ct = lt;
+  const uint32_t pt = (one_block && acl_mode == kAclMfma && NFDP_ACL_PTILES) ? (acl_tiles + 15) / 16 : 0u;
   if (one_block && acl_mode == kAclMfma && acl_tiles > kLdsAclTiles) {
     const size_t rest = (hash_mode == kHashMfma ? 2 * 2 * 64 * 16 : 0) + (hash_mode == kHashLds ? kToepLdsWords * 4 : 0) +
-                        kFWaves * 64 * 16 + kLdsPorts * 4 * 4 + kNumReasons * 4 + 16 + kLdsTabBytes;
+                        kFWaves * 64 * 16 + kLdsPorts * 4 * 4 + kNumReasons * 4 + 16 + kLdsTabBytes +
+                        (size_t)pt * (1024 + 64);
     const size_t budget = 160 * 1024 - 2048;   // static LDS + alignment margin
     ct = acl_tiles;
     const size_t room = budget > rest + (size_t)ct * 64 ? budget - rest - (size_t)ct * 64 : 0;
     const uint32_t fit = (uint32_t)(room / 1024) & ~(kAclGroup - 1);
     lt = fit > lt ? (fit < acl_tiles ? fit : acl_tiles) : lt;
   }
-  L.ltiles = lt; L.ctiles = ct;
+  L.ltiles = lt; L.ctiles = ct; L.ptiles = pt;
   L.acl_w = o; if (acl_mode == kAclMfma) o += (size_t)lt * 64 * 16;
   L.acl_c = o; if (acl_mode == kAclMfma) o += (size_t)ct * 4 * 16;
+  L.pt_w = o; o += (size_t)pt * 64 * 16;
+  L.pt_c = o; o += (size_t)pt * 4 * 16;
   L.toep_f = o; if (hash_mode == kHashMfma) o += 2 * 2 * 64 * 16;
   L.toep_t = o; if (hash_mode == kHashLds) o += kToepLdsWords * 4;
   L.kx = o; o += kFWaves * 64 * 16;
@@ -188,7 +193,16 @@ void fused_kernel(FusedArgs a) {
     for (uint32_t i = threadIdx.x; i < nw; i += kFB) lw[i] = a.acl_wfrag[i];
     for (uint32_t i = threadIdx.x; i < nc; i += kFB) lc[i] = a.acl_cinit[i];
   }
-  const AclView av{lw, lc, a.acl_wfrag, a.acl_cinit, a.acl_tiles, L.ltiles, L.ctiles};
+  // one_block (EARLY) layouts: the prefilter tiles after the rule tiles' fragments / the prefilters
+  const v4i* pw = reinterpret_cast<const v4i*>(smem + L.pt_w);
+  const v4i* pcw = reinterpret_cast<const v4i*>(smem + L.pt_c);
+  if constexpr (ACL == kAclMfma && EARLY) {
+    const v4i* gpw = a.acl_wfrag + (size_t)a.acl_tiles * 64;
+    const v4i* gpc = a.acl_cinit + (size_t)a.acl_tiles * 6 + (size_t)acl_groups(a.acl_tiles) * 2;
+    for (uint32_t i = threadIdx.x; i < L.ptiles * 64; i += kFB) const_cast<v4i*>(pw)[i] = gpw[i];
+    for (uint32_t i = threadIdx.x; i < L.ptiles * 4; i += kFB) const_cast<v4i*>(pcw)[i] = gpc[i];
+  }
+  const AclView av{lw, lc, a.acl_wfrag, a.acl_cinit, a.acl_tiles, L.ltiles, L.ctiles, pw, pcw, L.ptiles};
   if constexpr (HASH == kHashMfma)
     for (uint32_t i = threadIdx.x; i < 256; i += kFB) lt[i] = a.toep_frag[i];
   if constexpr (HASH == kHashLds)

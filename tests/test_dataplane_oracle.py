@@ -57,7 +57,8 @@ def _acl_emulate(nf, val, msk, keys):
     C init = bias * 4096 + rule, first match = min over the tiles/groups the prefilters admit."""
     w, c, tiles = nf.build_acl_frags(val, msk)
     # FP4 (e2m1) A fragments of v_mfma_scale_f32_16x16x128_f8f6f4: lane l, nibble j = K 32(l>>4)+j
-    w = w.view(np.uint8).reshape(tiles, 64, 16)
+    # (the rule tiles; the prefilter tiles follow them: _prefilter_tiles_emulate)
+    w = w.view(np.uint8)[: tiles * 1024].reshape(tiles, 64, 16)
     nib = np.stack([w & 0xF, w >> 4], axis=-1).reshape(tiles, 64, 32)
     e2m1 = {0x0: 0, 0x2: 1, 0xA: -1}
     assert set(np.unique(nib).tolist()) <= set(e2m1)
@@ -108,6 +109,46 @@ def test_acl_fragments_emulated(nf):
     ref = np.where(m.any(axis=1), m.argmax(axis=1), -1)
     assert np.array_equal(got, ref)
     assert (got[:n] >= 0).all()
+
+
+def _fp4_weights(wbytes, ntiles):
+    w = wbytes.reshape(ntiles, 64, 16)
+    nib = np.stack([w & 0xF, w >> 4], axis=-1).reshape(ntiles, 64, 32)
+    e2m1 = {0x0: 0, 0x2: 1, 0xA: -1}
+    assert set(np.unique(nib).tolist()) <= set(e2m1)
+    vo = np.vectorize(e2m1.get)(nib).astype(np.int64)
+    W = np.zeros((128, ntiles * 16), np.int64)
+    for nt in range(ntiles):
+        for l in range(64):
+            W[32 * (l >> 4) + np.arange(32), nt * 16 + (l & 15)] = vo[nt, l]
+    return W
+
+
+def test_acl_prefilter_tiles_emulated(nf):
+    """The prefilter tiles (16 tiles' prefilters as the rows of one MFMA tile): accumulator < 4096
+    exactly when the key passes that tile's prefilter, for every tile and key."""
+    from dpu_operator_amd.dataplane import scenario as S
+    from dpu_operator_amd.dataplane.engine import DataPlane
+
+    dp = DataPlane(device="cpu", flow_buckets=1 << 12)
+    sc = S.build_sfc(dp, n_pods=8, n_flows=4096, n_acl=256, seed=0)
+    S.install_acl_wild(dp, 1024)
+    val, msk, _, n = dp.acl.arrays()
+    w, c, tiles = nf.build_acl_frags(val[:n], msk[:n])
+    groups, ptiles = (tiles + 7) // 8, (tiles + 15) // 16
+    assert len(w) == (tiles + ptiles) * 1024 and len(c) == tiles * 24 + groups * 8 + ptiles * 16
+    W = _fp4_weights(w.view(np.uint8)[tiles * 1024:], ptiles)
+    C = c[tiles * 24 + groups * 8:].view(np.float32).reshape(ptiles, 4, 4).reshape(-1).astype(np.int64)
+    pf = c[tiles * 16: tiles * 24].view(np.uint32).reshape(tiles, 8)
+    rng = np.random.default_rng(4)
+    keys = np.concatenate([sc.keys[:2048], rng.integers(0, 2**32, (512, 4), dtype=np.uint64).astype(np.uint32),
+                           (val[:n] | (rng.integers(0, 2**32, (n, 4), dtype=np.uint64).astype(np.uint32) & ~msk[:n]))])
+    bits = ((keys[:, :, None] >> np.arange(32, dtype=np.uint32)) & 1).reshape(len(keys), 128).astype(np.int64)
+    acc = 4096 * (bits @ W) + C   # [keys, ptiles * 16]
+    direct = np.stack([np.all(((keys & f[:4]) ^ f[4:]) == 0, axis=1) for f in pf], axis=1)
+    assert np.array_equal(acc[:, :tiles] < 4096, direct)
+    assert (acc[:, tiles:] >= 4096).all()   # padding rows never pass
+    assert direct.any(axis=0).sum() > tiles // 4   # (the keys exercise both outcomes)
 
 
 def test_acl_prefilter_skips_bench_rules(nf):

@@ -1,0 +1,32 @@
+"""Saturated live pod -> pod Mpps over engine geometries (queues x tx workers x generator threads,
+header copies vs zero copy) in one process: where the box's CPU share goes.  One JSON line per
+configuration.  Usage: python tools/live_sweep.py [--duration 0.3]"""
+import argparse
+import importlib.util
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+GRID = [(4, 2, 4, False), (4, 1, 4, False), (5, 1, 4, False), (6, 1, 4, False), (3, 2, 4, False), (4, 2, 3, False),
+        (4, 2, 6, False), (6, 1, 6, False), (4, 2, 4, True), (6, 1, 4, True), (2, 3, 4, False), (8, 1, 4, False)]
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--duration", type=float, default=0.3)
+    ap.add_argument("--device", default="cuda")
+    a = ap.parse_args()
+    spec = importlib.util.spec_from_file_location("live_bench", os.path.join(os.path.dirname(__file__), "live_bench.py"))
+    lb = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(lb)
+    for q, w, g, zc in GRID:
+        r = lb.run(device=a.device, duration=a.duration, queues=q, tx_workers=w, threads=g, zero_copy=zc,
+                   saturated_only=True)
+        print(json.dumps({"queues": q, "tx_workers": w, "gen_threads": g, "zero_copy": zc, "mpps": r.get("mpps"),
+                          "p50_us": r.get("p50_us"), "error": r.get("error")}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
