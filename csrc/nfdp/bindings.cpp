@@ -766,6 +766,13 @@ PYBIND11_MODULE(_nfdp, m) {
         return r.post_write(dst, w.data(), (uint32_t)w.size(), timeout_s);
       }, py::arg("dst"), py::arg("data"), py::arg("timeout_s") = 1.0)
       .def_property_readonly("ctrl_done", &RingEngine::ctrl_done)
+      // GPU-direct egress (ring.h GdeRing)
+      .def("gde_enable", &RingEngine::gde_enable, py::arg("on") = true)
+      .def_property_readonly("gde_on", &RingEngine::gde_on)
+      .def("gde_set", &RingEngine::gde_set, py::arg("port"), py::arg("q"), py::arg("ctl"), py::arg("desc"), py::arg("buf"),
+           py::arg("ring_size"), py::arg("buf_size"), py::arg("head") = 0, py::arg("tail") = 0,
+           py::call_guard<py::gil_scoped_release>())
+      .def("gde_clear", &RingEngine::gde_clear, py::arg("port"), py::arg("q"), py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("ctrl_posted", &RingEngine::ctrl_posted)
       .def("wait_ctrl", [](RingEngine& r, uint64_t seq, double timeout_s) {
         py::gil_scoped_release nogil;
@@ -933,6 +940,8 @@ PYBIND11_MODULE(_nfdp, m) {
       .def("set_coalesce", &Engine::set_coalesce, py::arg("frames") = 64, py::arg("window_us") = 0.0)
       .def("set_queue_cpus", &Engine::set_queue_cpus, py::arg("queue"), py::arg("cpus"))
       .def("set_zero_copy", &Engine::set_zero_copy, py::arg("on"))
+      .def("set_gpu_egress", &Engine::set_gpu_egress, py::arg("on"))
+      .def_property_readonly("gpu_egress", &Engine::gpu_egress)
       .def_property_readonly("zero_copy", &Engine::zero_copy)
       .def("hold", [](Engine& e) { py::gil_scoped_release nogil; e.hold(); })
       .def("release", &Engine::release)

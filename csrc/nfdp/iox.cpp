@@ -548,7 +548,9 @@ void Engine::add_port(uint32_t id, std::shared_ptr<Port> p, int queue) {
     for (uint32_t k = 1; k < nq_; ++k)
       if (queues_[k]->nports.load() < queues_[q]->nports.load()) q = k;
   }
+  if (gde_.load()) gde_unregister(id);   // (a port replaced at this id)
   if (zero_copy_.load()) map_port(*p);   // before any packet thread can see the port
+  if (gde_.load()) gde_register(id, *p);
   reap_retired(false);
   (*t)[id] = PortRef{std::move(p), q};
   queues_[q]->nports.fetch_add(1);
@@ -562,6 +564,9 @@ std::shared_ptr<Port> Engine::remove_port(uint32_t id) {
   auto t = std::make_shared<PortTab>(*ports_);
   auto old = (*t)[id].p;
   if (old) queues_[(*t)[id].q]->nports.fetch_sub(1);
+  // GPU-direct egress off for it first, applied by every grid: chunks published from here on
+  // leave its frames to the host path (which finds no port); earlier ones are waited for below
+  if (old && gde_.load()) gde_unregister(id);
   (*t)[id] = PortRef{};
   std::atomic_store(&ports_, std::shared_ptr<const PortTab>(t));
   ports_ver_.fetch_add(1, std::memory_order_release);
@@ -624,6 +629,49 @@ void Engine::map_port(Port& p) {
   m.lo = mem.first;
   m.hi = mem.first + mem.second;
   p.zc_ = std::move(m);
+}
+
+void Engine::gde_register(uint32_t id, Port& p) {
+  auto* mp = dynamic_cast<MemifPort*>(&p);
+  if (!mp) return;
+  const memif::Region& reg = mp->region();
+  // the region mapped for every backend (the zero-copy rx mapping: it covers the whole region);
+  // without zero-copy rx the rx path keeps copying (lo / hi cleared)
+  const bool had = p.zc_.lo != nullptr;
+  map_port(p);
+  if (p.zc_.off.size() != backends_.size()) return;   // some backend cannot reach it
+  if (!zero_copy_.load() && !had) p.zc_.lo = p.zc_.hi = nullptr;
+  for (size_t k = 0; k < lanes_.size(); ++k) {
+    Lane* L = lanes_[k].get();
+    const uint32_t r = 1u + nq_ + (uint32_t)k;
+    if (!L->be->gde_ok() || r > reg.rx_rings()) continue;
+    const int64_t off = p.zc_.off[L->g];
+    auto dev = [&](const void* h) { return (uint64_t)((int64_t)reinterpret_cast<uint64_t>(h) + off); };
+    memif::Ctl* c = reg.ctl(r);
+    L->be->gde_set(id, L->q, dev(c), dev(reg.desc(r)), dev(reg.buf(r, 0)), reg.ring_size(), reg.buf_size(),
+                   c->head.load(std::memory_order_acquire), c->tail.load(std::memory_order_acquire));
+  }
+}
+
+void Engine::gde_unregister(uint32_t id) {
+  for (size_t k = 0; k < lanes_.size(); ++k) {
+    Lane* L = lanes_[k].get();
+    if (!L->be->gde_ok()) continue;
+    const uint64_t seq = L->be->gde_clear(id, L->q);
+    if (seq && !L->be->gde_wait(seq, 2.0)) throw std::runtime_error("iox: a grid did not apply the egress removal");
+  }
+}
+
+void Engine::set_gpu_egress(bool on) {
+  if (run_) throw std::runtime_error("iox: set_gpu_egress while running");
+  std::lock_guard<std::mutex> g(ports_mu_);
+  gde_ = on;
+  for (uint32_t id = 0; id < ports_->size(); ++id) {
+    const PortRef& r = (*ports_)[id];
+    if (!r.p) continue;
+    if (on) gde_register(id, *r.p);
+    else gde_unregister(id);
+  }
 }
 
 void Engine::set_zero_copy(bool on) {
@@ -873,7 +921,7 @@ std::unordered_map<std::string, uint64_t> Engine::stats() const {
     m["side_passes"] += s.side.load(); m["no_netdev"] += s.no_port.load(); m["tx_full"] += s.tx_full.load();
     m["publish_ns"] += s.pub_ns.load(); m["deliver_ns"] += s.deliver_ns.load(); m["rx_idle_polls"] += s.idle.load();
     m["rx_wait_tx"] += s.wait_tx.load(); m["learn_events"] += s.learn.load(); m["rx_held"] += s.held.load();
-    m["zero_copy_frames"] += s.zc.load();
+    m["zero_copy_frames"] += s.zc.load(); m["gpu_tx"] += s.gde.load();
   };
   for (auto& Q : queues_) {
     fold(Q->st);
@@ -1315,6 +1363,10 @@ void Engine::deliver(Queue* Q, Lane* L, Burst& b, uint32_t w, const Cfg& c, cons
     const uint32_t pos = (uint32_t)((b.start + i) & cmask);
     const uint32_t meta = om[pos];
     const uint32_t reason = meta_reason(meta), oport = meta_port(meta), olen = meta_len(meta);
+    if (reason == 0 && (meta & 0xFFFu) == kMetaPortGde) {   // the grid wrote it into the pod's ring itself
+      if (w == 0) ++tally.gde;
+      continue;
+    }
     if (reason == 0) {
       const uint32_t dst = route(oport);
       if (!mine(dst)) continue;
@@ -1372,6 +1424,7 @@ void Engine::deliver(Queue* Q, Lane* L, Burst& b, uint32_t w, const Cfg& c, cons
   st.add(st.no_port, tally.no_port);
   st.add(st.drop, tally.drop);
   st.add(st.reps, tally.reps);
+  st.add(st.gde, tally.gde);
 }
 
 void Engine::finish(Queue* Q, Lane* L, Burst& b) {

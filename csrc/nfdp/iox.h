@@ -179,6 +179,7 @@ class MemifPort : public Port {
   const std::string& path() const { return reg_.path(); }
   uint32_t tx_queues() const override { return nprod_; }
   std::pair<const uint8_t*, size_t> rx_memory() const override { return {reg_.base(), reg_.bytes()}; }
+  const memif::Region& region() const { return reg_; }
 
  protected:
   bool tx_locked(uint32_t q, const uint8_t* a, uint32_t na, const uint8_t* b, uint32_t nb, const uint8_t* c,
@@ -326,6 +327,15 @@ class Backend {
   // Make host memory [p, p + n) readable by the pipeline: its address there (0: cannot).  Sets
   // *release when this call registered it (run it once nothing of the memory is in flight).
   virtual uint64_t map_host(const void*, size_t, std::function<void(std::function<void()>)>*) { return 0; }
+  // GPU-direct egress (ring.h GdeRing): the pipeline's grid can deliver memif frames itself;
+  // set / clear a (port, queue) ring entry (returns the control-mailbox entry to wait for, 0 when
+  // applied at once); wait until the grid applied it.
+  virtual bool gde_ok() { return false; }
+  virtual uint64_t gde_set(uint32_t, uint32_t, uint64_t, uint64_t, uint64_t, uint32_t, uint32_t, uint32_t, uint32_t) {
+    return 0;
+  }
+  virtual uint64_t gde_clear(uint32_t, uint32_t) { return 0; }
+  virtual bool gde_wait(uint64_t, double) { return true; }
 };
 
 class GpuBackend : public Backend {
@@ -350,6 +360,13 @@ class GpuBackend : public Backend {
   }
   uint64_t in_slot_addr(uint32_t q, uint32_t pos) override { return ring_->in_slot_addr(q, pos); }
   uint64_t map_host(const void* p, size_t n, std::function<void(std::function<void()>)>* release) override;
+  bool gde_ok() override { return ring_->gde_on(); }
+  uint64_t gde_set(uint32_t port, uint32_t q, uint64_t ctl, uint64_t desc, uint64_t buf, uint32_t ring_size,
+                   uint32_t buf_size, uint32_t head, uint32_t tail) override {
+    return ring_->gde_set(port, q, ctl, desc, buf, ring_size, buf_size, head, tail);
+  }
+  uint64_t gde_clear(uint32_t port, uint32_t q) override { return ring_->gde_clear(port, q); }
+  bool gde_wait(uint64_t seq, double timeout_s) override { return ring_->wait_ctrl(seq, timeout_s); }
 
  private:
   RingEngine* ring_;
@@ -481,6 +498,12 @@ class Engine {
   // mapped as they come.
   void set_zero_copy(bool on);
   bool zero_copy() const { return zero_copy_.load(); }
+  // GPU-direct egress: memif ports added from now on (and those present) get a ring per GPU lane
+  // (memif ring 1 + queues + lane) that the lane's grid writes itself (ring.h GdeRing); needs the
+  // GPU backends' rings gde_enable()d and regions with enough rings (MemifPort tx_rings >= queues +
+  // lanes), else the port stays on the host path.  Set while stopped.
+  void set_gpu_egress(bool on);
+  bool gpu_egress() const { return gde_.load(); }
   void start();
   void stop();
   void pause();    // no publish until resume(); returns once nothing is in flight
@@ -557,7 +580,7 @@ class Engine {
   };
   struct alignas(64) QStats {
     std::atomic<uint64_t> rx{0}, tx{0}, drop{0}, punt{0}, recirc{0}, reps{0}, bursts{0}, side{0}, no_port{0},
-        tx_full{0}, pub_ns{0}, deliver_ns{0}, idle{0}, wait_tx{0}, learn{0}, held{0}, zc{0};
+        tx_full{0}, pub_ns{0}, deliver_ns{0}, idle{0}, wait_tx{0}, learn{0}, held{0}, zc{0}, gde{0};
     void add(std::atomic<uint64_t>& c, uint64_t v) { if (v) c.store(c.load(std::memory_order_relaxed) + v, std::memory_order_relaxed); }
   };
   struct Queue {                // one rx thread + its tx workers
@@ -576,7 +599,7 @@ class Engine {
     std::mutex lat_mu;           // rx -> tx time per burst, this queue's samples
     std::vector<double> lat_us;
   };
-  struct TxTally { uint64_t tx = 0, full = 0, no_port = 0, drop = 0, reps = 0; };
+  struct TxTally { uint64_t tx = 0, full = 0, no_port = 0, drop = 0, reps = 0, gde = 0; };
   struct TxScratch {            // per tx worker
     std::vector<std::vector<TxItem>> by_port;
     std::vector<uint32_t> touched;
@@ -620,6 +643,7 @@ class Engine {
   std::vector<std::unique_ptr<Queue>> queues_;
   mutable std::mutex ports_mu_;
   std::atomic<bool> zero_copy_{false};
+  std::atomic<bool> gde_{false};
   // removed ports stay referenced a while (frames of theirs may still be in a pipeline: the GPU
   // reads a zero-copy frame where its port holds it)
   // A removed port is released once nothing can refer to it: every rx thread has seen a port
@@ -632,6 +656,8 @@ class Engine {
   };
   std::deque<Retired> retired_;     // (ports_mu_)
   void map_port(Port& p);            // (ports_mu_)
+  void gde_register(uint32_t id, Port& p);   // (ports_mu_) GPU-direct egress rings of a memif port
+  void gde_unregister(uint32_t id);          // (ports_mu_) ... off again, applied by every grid
   void reap_retired(bool all);       // (ports_mu_)
   std::shared_ptr<const PortTab> ports_;              // copy-on-write snapshot, by port id
   alignas(64) std::atomic<uint64_t> ports_ver_{0};    // bumped after every ports_ / cfg_ store

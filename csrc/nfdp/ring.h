@@ -121,7 +121,9 @@ struct alignas(128) RingDevState {
   uint32_t set_serial[2];   // (queue 0's) device mirror of the table sets' serials: written before
                             // the flip that names the set (start(), or the control mailbox), so the
                             // serial check never waits on a host-memory read
-  uint32_t pad1[27];
+  uint32_t gde_pad;
+  uint64_t gde_turn;        // GPU-direct egress: the next chunk ticket whose frames may go out (in order)
+  uint32_t pad1[24];
 };
 
 // Control mailbox: the control plane's small table writes (a port entry on a link / MTU / RX-state
@@ -149,6 +151,30 @@ struct alignas(64) RingCtrlRing {
   RingCtrlEntry e[kCtrlSlots];
 };
 static_assert(sizeof(RingDevState) == 256, "RingDevState");
+
+// GPU-direct egress (GDE): a frame whose egress port is a memif vport goes from the grid straight
+// into that vport's data-plane -> pod ring reserved for this GPU and queue (a ring no host thread
+// writes): the frame's 64 B and its descriptor are stored over PCIe, the ring head is published
+// with a system-scope store, and the host's tx path never touches the frame (its meta says
+// kMetaPortGde).  Chunks of a queue take their turn in ticket order (RingDevState.gde_turn), so a
+// pod sees its frames in arrival order; a full ring (the pod's tail, re-read over PCIe when the
+// cached one says full) leaves the rest of the chunk's frames to the host path.  Eligible: no drop,
+// no side work (flood / tunnel header), the whole frame in the 64-B slot.  One entry per (port,
+// queue): the ring's addresses as the GPU sees the mapped memif region, its geometry and the
+// producer's private head (device state).
+constexpr uint32_t kMetaPortGde = 0xFFDu;   // out-meta port of a frame the grid delivered itself
+struct alignas(64) GdeRing {
+  uint64_t ctl;        // device address of the memif ring's Ctl (head written here, tail read)
+  uint64_t desc;       // device address of its Desc[ring_size]
+  uint64_t buf;        // device address of its buffer 0
+  uint32_t mask;       // ring_size - 1
+  uint32_t buf_size;   // bytes per buffer
+  uint32_t head;       // producer head (device private copy, published to ctl)
+  uint32_t tail_cache; // last pod tail seen
+  uint32_t valid;      // 1: in use
+  uint32_t pad[5];
+};
+static_assert(sizeof(GdeRing) == 64, "GdeRing");
 
 class RingEngine {
  public:
@@ -253,6 +279,16 @@ class RingEngine {
   uint64_t post_ctrl(uint64_t dst, const uint32_t* data, uint32_t n, double timeout_s, bool restage = true);
  public:
   uint64_t ctrl_posted() const { return ctrl_head_; }
+  // GPU-direct egress (see GdeRing).  gde_enable while stopped (allocates the [kMaxPorts][queues]
+  // table the next start() passes to the grid); gde_set / gde_clear an entry, through the control
+  // mailbox while the grid runs (returns the entry's number: once ctrl_done() passes it and every
+  // chunk published before it completed, the grid no longer writes that ring) or directly while
+  // stopped (returns 0).
+  void gde_enable(bool on);
+  bool gde_on() const { return d_gde_ != nullptr; }
+  uint64_t gde_set(uint32_t port, uint32_t q, uint64_t ctl, uint64_t desc, uint64_t buf, uint32_t ring_size,
+                   uint32_t buf_size, uint32_t head, uint32_t tail);
+  uint64_t gde_clear(uint32_t port, uint32_t q);
   // Device buffers control writes may target ([base, bytes) each: the running table set's small
   // tables); anything else is refused on the host, so a bad address never reaches the GPU.
   void set_ctrl_regions(const std::vector<std::pair<uint64_t, uint64_t>>& regions);
@@ -317,6 +353,8 @@ class RingEngine {
   std::vector<std::pair<uint64_t, uint64_t>> ctrl_regions_;   // (mu_) writable device ranges
   uint32_t lds_tiles_ = 0;
   uint32_t set_serial_ = 0;
+  GdeRing* d_gde_ = nullptr;         // [kMaxPorts][nq] (HBM), null: GPU-direct egress off
+  uint64_t gde_write(uint32_t port, uint32_t q, const GdeRing& e);
 };
 
 // hipHostUnregister(p), then after(), once no ring of this process is running (at once if none
@@ -340,6 +378,7 @@ struct RingLaunch {
   uint32_t epoch0;            // epoch at launch (its set bit names the set to stage first)
   RingCtrlRing* ctrl;         // device view of the control mailbox
   const uint64_t* faddr;      // frame addresses per slot (null: frames are in the in slots)
+  GdeRing* gde = nullptr;     // GPU-direct egress table [kMaxPorts][queues] (null: off)
 };
 hipError_t launch_ring(const RingLaunch& r, const LaunchCfg& cfg, int wgs_per_cu, bool coop, hipStream_t s);
 

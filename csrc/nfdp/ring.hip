@@ -37,6 +37,7 @@ struct RingArgs {
   uint32_t nq;          // queues: workgroup b serves queue b % nq (ctl / st / flags / svc / slots per queue)
   RingCtrlRing* ctrl;   // control mailbox (pinned host memory, device view)
   const unsigned long long* faddr;   // zero-copy rx: per-slot frame addresses (null: in slots)
+  GdeRing* gde;         // GPU-direct egress table [kMaxPorts][nq] (null: off; ring.h GdeRing)
 };
 // Frames are read and written with system-coherent buffer ops (sc0 sc1): the loads never hit a
 // stale L2 line of a slot a producer (host / NIC DMA) rewrote, and the stores write through to
@@ -183,6 +184,82 @@ __device__ __forceinline__ bool ring_wait_chunk(const RingArgs& a, RingCtl* ctl,
     else if (dist < 64) __builtin_amdgcn_s_sleep(32);
     else __builtin_amdgcn_s_sleep(127);
   }
+}
+
+// GPU-direct egress of one chunk (ring.h GdeRing).  Every lane calls it (EXEC full).  The chunk
+// waits for its turn (tickets of a queue in order: a pod's frames arrive in order), then per egress
+// port: reserve the lanes' slots in the port's GPU ring (the pod's tail re-read over PCIe only
+// when the cached one says full), store each frame's 64 B and its descriptor length
+// (system-coherent buffer stores: write-through to host memory), wait for the stores, publish the
+// head (system scope), and mark the frames delivered in their meta (kMetaPortGde).  Frames that
+// find no room, or are not eligible, stay with the host path.  The turn moves on at the end; a
+// wave still waiting for it at the device deadline goes ahead (the grid is exiting).
+__device__ __forceinline__ void gde_deliver(const RingArgs& a, RingDevState* qst, uint32_t qi, unsigned long long tk,
+                                            uint32_t lane, unsigned long long t_begin, bool elig0, uint32_t port,
+                                            uint32_t olen, const uint32_t* o, uint32_t& meta) {
+  bool elig = elig0 && port < (uint32_t)kMaxPorts;
+  if (elig) {
+    const GdeRing* g = a.gde + (size_t)port * a.nq + qi;
+    elig = __hip_atomic_load(&g->valid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1u;
+  }
+  if (lane == 0) {
+    while (__hip_atomic_load(&qst->gde_turn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != tk) {
+      if (__builtin_amdgcn_s_memrealtime() - t_begin > a.deadline) break;
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // the previous chunk's head / tail updates
+  unsigned long long rem = __ballot(elig);
+  while (rem) {
+    const int leader = __builtin_ctzll(rem);
+    const uint32_t P = __builtin_amdgcn_readlane(port, leader);
+    const bool mine = elig && port == P;
+    const unsigned long long bm = __ballot(mine);
+    rem &= ~bm;
+    GdeRing* g = a.gde + (size_t)P * a.nq + qi;
+    // (atomic loads: vector memory ops that the acquire above covers, never the scalar cache)
+    auto ld32 = [](const uint32_t* x) { return __hip_atomic_load(x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+    auto ld64 = [](const uint64_t* x) { return __hip_atomic_load(x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+    const uint64_t ctl = rfl64(ld64(&g->ctl)), desc = rfl64(ld64(&g->desc)), buf = rfl64(ld64(&g->buf));
+    const uint32_t mask = __builtin_amdgcn_readfirstlane(ld32(&g->mask));
+    const uint32_t bsz = __builtin_amdgcn_readfirstlane(ld32(&g->buf_size));
+    uint32_t head = __builtin_amdgcn_readfirstlane(ld32(&g->head)), tc = __builtin_amdgcn_readfirstlane(ld32(&g->tail_cache));
+    const uint32_t cnt = (uint32_t)__builtin_popcountll(bm);
+    uint32_t room = mask + 1u - (head - tc);
+    if (room < cnt) {   // full by the cached tail: what the pod has drained since (one PCIe read)
+      uint32_t t = 0;
+      if (lane == 0)
+        t = __hip_atomic_load(reinterpret_cast<uint32_t*>(ctl + 64), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      tc = __builtin_amdgcn_readfirstlane(t);
+      room = mask + 1u - (head - tc);
+      if (room > mask + 1u) room = 0;   // (a bogus tail from the pod: deliver nothing)
+    }
+    const uint32_t n_ok = cnt < room ? cnt : room;
+    if (n_ok == 0) continue;
+    const uint32_t pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
+    const bool go = mine && pre < n_ok;
+    const uint32_t pos = (head + pre) & mask;
+    const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(buf), (short)0,
+                                                                        (int)((mask + 1u) * bsz), kBufRaw);
+    const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(desc), (short)0,
+                                                                        (int)((mask + 1u) * 8u), kBufRaw);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const v4u v = {o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]};
+      store_b128<kSysAux>(v, rb, go ? pos * bsz + 16u * k : kNoRun, 0);
+    }
+    __builtin_amdgcn_raw_buffer_store_b32(olen, rd, go ? pos * 8u : kNoRun, 0, kSysAux);
+    __builtin_amdgcn_s_waitcnt(0);   // (write-through stores done: the frames are in host memory)
+    head += n_ok;
+    if (lane == 0) {
+      __hip_atomic_store(&g->head, head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&g->tail_cache, tc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(reinterpret_cast<uint32_t*>(ctl), head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    if (go) meta = make_meta(kMetaPortGde, olen, kOk);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");   // this chunk's head / tail updates, then its turn ends
+  if (lane == 0) __hip_atomic_store(&qst->gde_turn, tk + 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // COOP = false: the 4 waves of a workgroup claim and process chunks independently (throughput).
@@ -477,9 +554,13 @@ __global__ __launch_bounds__(kRingBlock) void ring_kernel(RingArgs a) {
     const uint32_t olen = egress_len(p, e);
     uint32_t o[kSlotDwords];
     emit(p, e.tci, e.push != 0, o);
-    wave_frames_store<kSysAux>(kx, o, r_out, run);
-    __builtin_amdgcn_raw_buffer_store_b32(make_meta(e.out_port, olen, e.reason, !e.reason && e.xhdr, !e.reason && e.flood), r_meta, i * 4u, 0, kSysAux);
     const bool pad = im == kRingPadMeta;  // filler slot of a partial burst: no counters, no side work
+    uint32_t meta = make_meta(e.out_port, olen, e.reason, !e.reason && e.xhdr, !e.reason && e.flood);
+    if (a.gde)   // GPU-direct egress: frames for memif vports straight into the pods' rings
+      gde_deliver(a, qst, qi, tk, lane, t_begin, !pad && !e.reason && !e.xhdr && !e.flood && olen <= 64u,
+                  e.out_port, olen, o, meta);
+    wave_frames_store<kSysAux>(kx, o, r_out, run);
+    __builtin_amdgcn_raw_buffer_store_b32(meta, r_meta, i * 4u, 0, kSysAux);
     if (a.side.cnt) {
       // flood / mirror / ARP-trap / learning / tunnel packets go on the side list; the host runs
       // the side pass over them once the chunk's flag is seen (before the flag: vmcnt covers it)
@@ -568,6 +649,7 @@ hipError_t launch_ring(const RingLaunch& r, const LaunchCfg& cfg, int wgs_per_cu
   a.epoch0 = r.epoch0;
   a.ctrl = r.ctrl;
   a.faddr = reinterpret_cast<const unsigned long long*>(r.faddr);
+  a.gde = r.gde;
   a.nq = r.queues ? r.queues : 1u;
   // every queue needs a workgroup; the side list indexes slots of one ring only
   if ((uint64_t)cfg.num_cus * (uint64_t)wgs_per_cu < a.nq || (a.nq > 1 && a.side.cnt)) return hipErrorInvalidValue;
@@ -677,7 +759,7 @@ RingEngine::~RingEngine() {
   } catch (...) {
   }
   release_streams();
-  for (void* d : {(void*)st_, (void*)d_svc_, (void*)dd_sets_}) (void)hipFree(d);
+  for (void* d : {(void*)st_, (void*)d_svc_, (void*)dd_sets_, (void*)d_gde_}) (void)hipFree(d);
   (void)hipHostFree(h_sets_);
   if (host_slots_) {
     for (void* h : host_ptrs_) (void)hipHostFree(h);
@@ -711,6 +793,7 @@ void RingEngine::start(const FusedLaunch& f, const LaunchCfg& cfg, double deadli
   }
   s[0].set_serial[0] = h_sets_[0].serial;
   s[0].set_serial[1] = h_sets_[1].serial;
+  for (uint32_t q = 0; q < nq_; ++q) s[q].gde_turn = s[q].claim;   // GPU-direct egress: the first ticket's turn
   if (!stream_) create_stream();
   ck(hipMemcpyAsync(st_, s.data(), sizeof(RingDevState) * nq_, hipMemcpyHostToDevice, stream_), "state upload");
   // both table sets into the grid's HBM copies (the host's are current: stage_tables wrote them)
@@ -744,8 +827,57 @@ void RingEngine::start(const FusedLaunch& f, const LaunchCfg& cfg, double deadli
   r.svc = d_svc_;
   r.deadline_ticks = (unsigned long long)(deadline_s * 1e8);  // s_memrealtime: 100 MHz
   r.flows_alt = flows_alt;
+  r.gde = d_gde_;
   ck(launch_ring(r, cfg, wgs_, coop_, stream_), "launch");
   set_running(true);
+}
+
+// ---- GPU-direct egress table -------------------------------------------------------------------
+void RingEngine::gde_enable(bool on) {
+  if (running_) throw std::runtime_error("ring: gde_enable while running");
+  if (!on) {
+    if (d_gde_) (void)hipFree(d_gde_);
+    d_gde_ = nullptr;
+    return;
+  }
+  if (d_gde_) return;
+  const size_t bytes = sizeof(GdeRing) * (size_t)kMaxPorts * nq_;
+  ck(hipMalloc(reinterpret_cast<void**>(&d_gde_), bytes), "alloc gde table");
+  ck(hipMemset(d_gde_, 0, bytes), "memset gde table");
+  ck(hipDeviceSynchronize(), "gde table");
+}
+
+uint64_t RingEngine::gde_write(uint32_t port, uint32_t q, const GdeRing& e) {
+  if (!d_gde_) throw std::runtime_error("ring: GPU-direct egress is off");
+  if (port >= (uint32_t)kMaxPorts || q >= nq_) throw std::invalid_argument("ring: gde entry out of range");
+  GdeRing* dst = d_gde_ + (size_t)port * nq_ + q;
+  if (!running_) {
+    ck(hipMemcpy(dst, &e, sizeof(GdeRing), hipMemcpyHostToDevice), "gde entry");
+    return 0;
+  }
+  // running: through the control mailbox, the entry's words first and its valid word last (a wave
+  // never sees a valid entry with stale addresses); the grid's LDS copies do not hold it
+  uint32_t w[16];
+  std::memcpy(w, &e, sizeof(w));
+  const uint64_t dev = reinterpret_cast<uint64_t>(dst);
+  uint64_t seq = 0;
+  if (e.valid) seq = post_ctrl(dev, w, 10, 1.0, false);
+  return std::max(seq, post_ctrl(dev + 40, &w[10], 1, 1.0, false));
+}
+
+uint64_t RingEngine::gde_set(uint32_t port, uint32_t q, uint64_t ctl, uint64_t desc, uint64_t buf, uint32_t ring_size,
+                             uint32_t buf_size, uint32_t head, uint32_t tail) {
+  if (ring_size < 2 || (ring_size & (ring_size - 1)) || buf_size < 64 || !ctl || !desc || !buf)
+    throw std::invalid_argument("ring: bad gde ring");
+  GdeRing e{};
+  e.ctl = ctl; e.desc = desc; e.buf = buf;
+  e.mask = ring_size - 1; e.buf_size = buf_size; e.head = head; e.tail_cache = tail; e.valid = 1;
+  return gde_write(port, q, e);
+}
+
+uint64_t RingEngine::gde_clear(uint32_t port, uint32_t q) {
+  GdeRing e{};
+  return gde_write(port, q, e);
 }
 
 // ---- host memory mapped for the grids (zero-copy rx) --------------------------------------------

@@ -56,8 +56,13 @@ class MemifVport:
         self.path, self.ring_size, self.buf_size = path, int(ring_size), int(buf_size)
         self.tx_rings = int(tx_rings)
 
-    def make(self, nf, queues: int = 1):
-        return nf.MemifPort(self.path, self.ring_size, self.buf_size, self.tx_rings or max(1, int(queues)))
+    MAX_RINGS = 16   # data plane -> pod rings a region can have (iox.h Port::kMaxTxQueues)
+
+    def make(self, nf, queues: int = 1, gpu_rings: int = 0):
+        """gpu_rings: extra rings the GPUs' grids write themselves (GPU-direct egress, one per engine
+        lane, after the host queues' rings); as many as fit MAX_RINGS."""
+        host = self.tx_rings or max(1, int(queues))
+        return nf.MemifPort(self.path, self.ring_size, self.buf_size, min(self.MAX_RINGS, host + max(0, int(gpu_rings))))
 
 
 class PacketVport:
@@ -162,7 +167,9 @@ def _quiet_ipv6(ifname: str) -> None:
         pass
 
 
-def _make_port(nf, spec, queues: int = 1):
+def _make_port(nf, spec, queues: int = 1, gpu_rings: int = 0):
+    if isinstance(spec, MemifVport):
+        return spec.make(nf, queues, gpu_rings)
     if hasattr(spec, "make"):
         return spec.make(nf, queues)
     if hasattr(spec, "fd"):            # netio.TapPort and anything else with a packet fd
@@ -206,7 +213,7 @@ class NativeLivePath:
                  on_punt=None, auto_restart: bool = True, tx_workers: int = 1, queues: int = 1,
                  max_inflight_frames: int = 0, port_queues: dict | None = None, coalesce_us: float = 8.0,
                  coalesce_frames: int = 64, ring_cus: int = 0, zero_copy: bool = False, lane_groups: bool = False,
-                 pin_cpus: bool = False, max_deferred_unmaps: int = 16):
+                 pin_cpus: bool = False, max_deferred_unmaps: int = 16, gpu_egress: bool = False):
         """dps: one data plane or a list (one per GPU, or a MultiDataPlane's planes); ports:
         {port id: vport spec}; queues: rx threads (each with a ring queue on every GPU) — with
         `lane_groups`, per data plane: every plane brings `queues` rx threads (and their tx
@@ -222,7 +229,11 @@ class NativeLivePath:
         region stays pinned until no ring grid of the process runs (hipHostUnregister waits for
         the device): when more than `max_deferred_unmaps` pile up, the supervisor restarts the
         rings (a maintenance restart: traffic pauses for the relaunch) and they are released, so
-        pinned memory stays bounded under vport churn."""
+        pinned memory stays bounded under vport churn.  gpu_egress (GPU planes): the ring grids
+        write frames bound for memif vports straight into those pods' rings (ring.h GdeRing, one ring
+        per engine lane in each region after the host queues' rings); the tx threads only see the
+        frames that need the host (drops aside: side work, frames longer than the 64-B slot, a full
+        GPU ring)."""
         from ..native import nfdp
 
         self.nf = nfdp()
@@ -248,6 +259,7 @@ class NativeLivePath:
         self.coalesce_us, self.coalesce_frames = float(coalesce_us), int(coalesce_frames)
         self.ring_cus = int(ring_cus)   # CUs of each ring grid (0: the GPU's, split between planes sharing it)
         self.zero_copy = bool(zero_copy)
+        self.gpu_egress = bool(gpu_egress) and self.gpu
         self.specs = dict(ports)
         self.port_queues = dict(port_queues or {})
         self.on_punt = on_punt
@@ -297,6 +309,7 @@ class NativeLivePath:
                                     deadline_s=3600.0, queues=self.queues,
                                     cus=self.ring_cus or max(1, int(dp.num_cus) // share))
                     ring.eng.set_frame_addrs(self.zero_copy)
+                    ring.eng.gde_enable(self.gpu_egress)
                     ring.start()
                 self._rings.append(ring)
                 be = nf.GpuBackend(ring.eng)
@@ -310,6 +323,7 @@ class NativeLivePath:
             dp._learned_on_device = True     # the engine learns into the device MAC table: commits pull first
         # replica counters appear in the first plane's counters (a MultiDataPlane sums its planes)
         eng.set_zero_copy(self.zero_copy)
+        eng.set_gpu_egress(self.gpu_egress)
         hooks = getattr(self.dps[0], "_ctr_hooks", [])
         if self not in hooks:
             self.dps[0]._ctr_hooks = hooks + [self]
@@ -323,7 +337,7 @@ class NativeLivePath:
         for idx, spec in self.specs.items():
             p = self._ports.get(idx)
             if p is None:
-                p = self._ports[idx] = _make_port(nf, spec, self.queues)
+                p = self._ports[idx] = _make_port(nf, spec, self.queues, self._gpu_rings())
             eng.add_port(int(idx), p, self._queue_for(idx))
         eng.learn_stamp = max(int(getattr(d, "stamp", 0)) for d in self.dps) + 1
         self._eng = eng
@@ -507,12 +521,16 @@ class NativeLivePath:
             return min(group, key=lambda q: (load[q], q))
         return -1
 
+    def _gpu_rings(self) -> int:
+        """GPU-direct egress rings a new memif region gets: one per engine lane (queue x plane)."""
+        return self.queues * len(self.dps) if self.gpu_egress else 0
+
     def add_port(self, idx: int, spec, queue: int = -1) -> None:
         with self._lock:
             self.specs[idx] = spec
             if queue >= 0:
                 self.port_queues[idx] = queue
-            p = self._ports[idx] = _make_port(self.nf, spec, self.queues)
+            p = self._ports[idx] = _make_port(self.nf, spec, self.queues, self._gpu_rings())
             if self._eng is not None:
                 self._eng.add_port(int(idx), p, self._queue_for(idx))
 

@@ -184,17 +184,18 @@ def test_commit_under_traffic_and_failure_restart(tmp_path):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("queues", [1, 2])
-def test_native_path_gpu_ring_bit_exact(tmp_path, queues):
+@pytest.mark.parametrize("queues,gpu_egress", [(1, False), (2, False), (1, True), (2, True)])
+def test_native_path_gpu_ring_bit_exact(tmp_path, queues, gpu_egress):
     """The GPU backend: header slots into the persistent ring kernel's pinned host slots (one
-    ring queue per engine queue); frames bit-exact and counters exact."""
+    ring queue per engine queue); frames bit-exact and counters exact.  gpu_egress: the grid
+    writes the frames into the pods' rings itself (ring.h GdeRing), the same frames arrive."""
     nf = nfdp()
     dp, sc = _sfc("cuda")
     ref, _ = _sfc("cpu")
     slots, im = S.traffic(sc, 3000, seed=5)
     exp, drops = _expected(ref, slots, im)
     live = NativeLivePath(dp, _vports(tmp_path, sc.n_pods, "g"), burst=256, ring_capacity=4096,
-                          queues=queues).start()
+                          queues=queues, gpu_egress=gpu_egress).start()
     try:
         eps = {i: nf.MemifEndpoint(str(tmp_path / f"g{i}")) for i in range(sc.n_pods)}
         src = im & 0xFFFF
@@ -213,6 +214,11 @@ def test_native_path_gpu_ring_bit_exact(tmp_path, queues):
         assert _until(drained, 10), (live.stats, live.error)
         for port, frames in exp.items():
             assert sorted(got[port]) == sorted(frames), port
+        st = live.stats
+        if gpu_egress:   # every forwarded 64-B frame went out from the GPU, none through the tx threads
+            assert st["gpu_tx"] == sum(map(len, exp.values())) and st["tx"] == 0, st
+        else:
+            assert st["gpu_tx"] == 0
         # counters: the ring kernel's LDS tallies reach the device counters when its waves idle
         if not _until(lambda: np.array_equal(dp.port_counters(), ref.port_counters()), 2.0):
             g, w = dp.port_counters(), ref.port_counters()
