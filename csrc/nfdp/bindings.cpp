@@ -773,6 +773,7 @@ PYBIND11_MODULE(_nfdp, m) {
            py::arg("ring_size"), py::arg("buf_size"), py::arg("head") = 0, py::arg("tail") = 0,
            py::call_guard<py::gil_scoped_release>())
       .def("gde_clear", &RingEngine::gde_clear, py::arg("port"), py::arg("q"), py::call_guard<py::gil_scoped_release>())
+      .def("gde_stats", &RingEngine::gde_stats)
       .def_property_readonly("ctrl_posted", &RingEngine::ctrl_posted)
       .def("wait_ctrl", [](RingEngine& r, uint64_t seq, double timeout_s) {
         py::gil_scoped_release nogil;

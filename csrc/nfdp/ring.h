@@ -123,7 +123,11 @@ struct alignas(128) RingDevState {
                             // serial check never waits on a host-memory read
   uint32_t gde_pad;
   uint64_t gde_turn;        // GPU-direct egress: the next chunk ticket whose frames may go out (in order)
-  uint32_t pad1[24];
+  uint64_t gde_wait;        // (diagnostics, s_memrealtime ticks) waiting for the turns / in the two
+  uint64_t gde_sect;        // serialised sections; chunks, frames delivered, frames left to the host
+  uint64_t gde_chunks, gde_frames, gde_full;   // for want of room
+  uint64_t gde_commit;      // GPU-direct egress: the next ticket whose ring heads may be published
+  uint32_t pad1[12];
 };
 
 // Control mailbox: the control plane's small table writes (a port entry on a link / MTU / RX-state
@@ -289,6 +293,8 @@ class RingEngine {
   uint64_t gde_set(uint32_t port, uint32_t q, uint64_t ctl, uint64_t desc, uint64_t buf, uint32_t ring_size,
                    uint32_t buf_size, uint32_t head, uint32_t tail);
   uint64_t gde_clear(uint32_t port, uint32_t q);
+  // (diagnostics, while stopped) per queue: {wait ticks, section ticks, chunks, frames, full}
+  std::vector<uint64_t> gde_stats();
   // Device buffers control writes may target ([base, bytes) each: the running table set's small
   // tables); anything else is refused on the host, so a bad address never reaches the GPU.
   void set_ctrl_regions(const std::vector<std::pair<uint64_t, uint64_t>>& regions);

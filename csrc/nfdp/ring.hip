@@ -186,29 +186,54 @@ __device__ __forceinline__ bool ring_wait_chunk(const RingArgs& a, RingCtl* ctl,
   }
 }
 
-// GPU-direct egress of one chunk (ring.h GdeRing).  Every lane calls it (EXEC full).  The chunk
-// waits for its turn (tickets of a queue in order: a pod's frames arrive in order), then per egress
-// port: reserve the lanes' slots in the port's GPU ring (the pod's tail re-read over PCIe only
-// when the cached one says full), store each frame's 64 B and its descriptor length
-// (system-coherent buffer stores: write-through to host memory), wait for the stores, publish the
-// head (system scope), and mark the frames delivered in their meta (kMetaPortGde).  Frames that
-// find no room, or are not eligible, stay with the host path.  The turn moves on at the end; a
-// wave still waiting for it at the device deadline goes ahead (the grid is exiting).
-__device__ __forceinline__ void gde_deliver(const RingArgs& a, RingDevState* qst, uint32_t qi, unsigned long long tk,
-                                            uint32_t lane, unsigned long long t_begin, bool elig0, uint32_t port,
-                                            uint32_t olen, const uint32_t* o, uint32_t& meta) {
-  bool elig = elig0 && port < (uint32_t)kMaxPorts;
-  if (elig) {
-    const GdeRing* g = a.gde + (size_t)port * a.nq + qi;
-    elig = __hip_atomic_load(&g->valid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1u;
-  }
+// GPU-direct egress of one chunk (ring.h GdeRing).  Every lane calls it (EXEC full).  Two short
+// sections taken in ticket order (a pod sees a queue's frames in arrival order) around the frame
+// writes, which chunks do in parallel:
+//   1. reserve (turn gde_turn): per egress port, the lanes' slots in the port's GPU ring (the pod's
+//      tail re-read over PCIe only when the cached one says full); the rest stays with the host;
+//   2. the frames (one full 64-B line each: 16 per pass through the wave's LDS scratch) and their
+//      descriptors, system-coherent write-through stores, waited for;
+//   3. commit (turn gde_commit): each port's head published (system scope), waited for before the
+//      next chunk may publish a later one, so a head never goes back.
+// Every access to the shared egress state is a relaxed agent-scope atomic (no fences: an acquire /
+// release would invalidate / write back the XCD's L2 - the flow table - per chunk).  A wave still
+// waiting for a turn at the device deadline goes ahead (the grid is exiting).
+__device__ __forceinline__ bool gde_turn(uint64_t* turn, unsigned long long tk, uint32_t lane, const RingArgs& a,
+                                         unsigned long long t_begin) {
   if (lane == 0) {
-    while (__hip_atomic_load(&qst->gde_turn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != tk) {
+    while (__hip_atomic_load(turn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != tk) {
       if (__builtin_amdgcn_s_memrealtime() - t_begin > a.deadline) break;
       __builtin_amdgcn_s_sleep(1);
     }
   }
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // the previous chunk's head / tail updates
+  return true;
+}
+__device__ __forceinline__ void gde_deliver(const RingArgs& a, RingDevState* qst, uint32_t qi, unsigned long long tk,
+                                            uint32_t lane, unsigned long long t_begin, bool elig0, uint32_t port,
+                                            uint32_t olen, const uint32_t* o, uint32_t& meta, uint4* kx) {
+  bool elig = elig0 && port < (uint32_t)kMaxPorts;
+  auto ld32 = [](const uint32_t* x) { return __hip_atomic_load(x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+  auto ld64 = [](const uint64_t* x) { return __hip_atomic_load(x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+  // each lane reads its port's ring geometry before any turn (it changes only while the entry is
+  // not valid): the serialised sections then load nothing but the head / tail
+  uint64_t m_ctl = 0, m_desc = 0, m_buf = 0;
+  uint32_t m_mask = 0, m_bsz = 0;
+  if (elig) {
+    const GdeRing* g = a.gde + (size_t)port * a.nq + qi;
+    elig = ld32(&g->valid) == 1u;
+    m_ctl = ld64(&g->ctl); m_desc = ld64(&g->desc); m_buf = ld64(&g->buf);
+    m_mask = ld32(&g->mask); m_bsz = ld32(&g->buf_size);
+  }
+  auto rl64 = [](uint64_t v, int l) {
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(v >> 32), l) << 32) |
+           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+  };
+  const unsigned long long tw0 = __builtin_amdgcn_s_memrealtime();
+  gde_turn(&qst->gde_turn, tk, lane, a, t_begin);
+  const unsigned long long tw1 = __builtin_amdgcn_s_memrealtime();
+  // ---- 1. reserve ----
+  bool go = false;
+  uint32_t pos = 0, end = 0, n_frames = 0, n_full = 0;
   unsigned long long rem = __ballot(elig);
   while (rem) {
     const int leader = __builtin_ctzll(rem);
@@ -217,16 +242,12 @@ __device__ __forceinline__ void gde_deliver(const RingArgs& a, RingDevState* qst
     const unsigned long long bm = __ballot(mine);
     rem &= ~bm;
     GdeRing* g = a.gde + (size_t)P * a.nq + qi;
-    // (atomic loads: vector memory ops that the acquire above covers, never the scalar cache)
-    auto ld32 = [](const uint32_t* x) { return __hip_atomic_load(x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
-    auto ld64 = [](const uint64_t* x) { return __hip_atomic_load(x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
-    const uint64_t ctl = rfl64(ld64(&g->ctl)), desc = rfl64(ld64(&g->desc)), buf = rfl64(ld64(&g->buf));
-    const uint32_t mask = __builtin_amdgcn_readfirstlane(ld32(&g->mask));
-    const uint32_t bsz = __builtin_amdgcn_readfirstlane(ld32(&g->buf_size));
+    const uint32_t mask = __builtin_amdgcn_readlane(m_mask, leader);
     uint32_t head = __builtin_amdgcn_readfirstlane(ld32(&g->head)), tc = __builtin_amdgcn_readfirstlane(ld32(&g->tail_cache));
     const uint32_t cnt = (uint32_t)__builtin_popcountll(bm);
     uint32_t room = mask + 1u - (head - tc);
     if (room < cnt) {   // full by the cached tail: what the pod has drained since (one PCIe read)
+      const uint64_t ctl = rl64(m_ctl, leader);
       uint32_t t = 0;
       if (lane == 0)
         t = __hip_atomic_load(reinterpret_cast<uint32_t*>(ctl + 64), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -235,31 +256,84 @@ __device__ __forceinline__ void gde_deliver(const RingArgs& a, RingDevState* qst
       if (room > mask + 1u) room = 0;   // (a bogus tail from the pod: deliver nothing)
     }
     const uint32_t n_ok = cnt < room ? cnt : room;
-    if (n_ok == 0) continue;
+    n_frames += n_ok;
+    n_full += cnt - n_ok;
     const uint32_t pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
-    const bool go = mine && pre < n_ok;
-    const uint32_t pos = (head + pre) & mask;
+    if (mine && pre < n_ok) { go = true; pos = (head + pre) & mask; end = head + n_ok; }
+    if (lane == 0) {
+      __hip_atomic_store(&g->head, head + n_ok, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&g->tail_cache, tc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0);   // the reservations are in memory before the next chunk reserves
+  if (lane == 0) __hip_atomic_store(&qst->gde_turn, tk + 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned long long tw2 = __builtin_amdgcn_s_memrealtime();
+  // ---- 2. frames and descriptors (parallel across chunks) ----
+  // Each frame as ONE full 64-B line write: 16 frames per pass through the wave's LDS scratch, the
+  // 4 lanes of a frame storing its 4 pieces in the same instruction (they coalesce).  Per-lane 16-B
+  // stores were partial-line writes to host memory: ~11 us per chunk (r5 s12 diagnostics).
+  unsigned long long rgo = __ballot(go);
+  while (rgo) {
+    const int leader = __builtin_ctzll(rgo);
+    const uint32_t P = __builtin_amdgcn_readlane(port, leader);
+    const bool mine = go && port == P;
+    const unsigned long long bgo = __ballot(mine);
+    rgo &= ~bgo;
+    const uint64_t desc = rl64(m_desc, leader), buf = rl64(m_buf, leader);
+    const uint32_t mask = __builtin_amdgcn_readlane(m_mask, leader);
+    const uint32_t bsz = __builtin_amdgcn_readlane(m_bsz, leader);
     const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(buf), (short)0,
                                                                         (int)((mask + 1u) * bsz), kBufRaw);
     const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(desc), (short)0,
                                                                         (int)((mask + 1u) * 8u), kBufRaw);
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const v4u v = {o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]};
-      store_b128<kSysAux>(v, rb, go ? pos * bsz + 16u * k : kNoRun, 0);
+    for (int q = 0; q < 4; ++q) {
+      if (((bgo >> (16 * q)) & 0xFFFFull) == 0ull) continue;   // (wave-uniform)
+      if ((lane >> 4) == (uint32_t)q) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) kx[4u * (lane & 15u) + k] = make_uint4(o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]);
+      }
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      const uint4 v = kx[lane];
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      const int src = 16 * q + (int)(lane >> 2);
+      const uint32_t spos = (uint32_t)__shfl((int)pos, src);
+      const bool sgo = ((bgo >> src) & 1ull) != 0ull;
+      const v4u w = {v.x, v.y, v.z, v.w};
+      store_b128<kSysAux>(w, rb, sgo ? spos * bsz + 16u * (lane & 3u) : kNoRun, 0);
     }
-    __builtin_amdgcn_raw_buffer_store_b32(olen, rd, go ? pos * 8u : kNoRun, 0, kSysAux);
-    __builtin_amdgcn_s_waitcnt(0);   // (write-through stores done: the frames are in host memory)
-    head += n_ok;
-    if (lane == 0) {
-      __hip_atomic_store(&g->head, head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&g->tail_cache, tc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(reinterpret_cast<uint32_t*>(ctl), head, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-    if (go) meta = make_meta(kMetaPortGde, olen, kOk);
+    // descriptors: consecutive positions are consecutive 8-B entries (full lines when 8 in a row)
+    typedef unsigned int v2u_t __attribute__((ext_vector_type(2)));
+    const v2u_t dv = {olen, 0u};
+    __builtin_amdgcn_raw_buffer_store_b64(dv, rd, mine ? pos * 8u : kNoRun, 0, kSysAux);
   }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");   // this chunk's head / tail updates, then its turn ends
-  if (lane == 0) __hip_atomic_store(&qst->gde_turn, tk + 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __builtin_amdgcn_s_waitcnt(0);   // (write-through stores done: the frames are in host memory)
+  if (go) meta = make_meta(kMetaPortGde, olen, kOk);
+  // ---- 3. commit: heads in ticket order ----
+  const unsigned long long tw3 = __builtin_amdgcn_s_memrealtime();
+  gde_turn(&qst->gde_commit, tk, lane, a, t_begin);
+  const unsigned long long tw4 = __builtin_amdgcn_s_memrealtime();
+  rgo = __ballot(go);
+  while (rgo) {
+    const int leader = __builtin_ctzll(rgo);
+    const uint32_t P = __builtin_amdgcn_readlane(port, leader);
+    const uint32_t E = __builtin_amdgcn_readlane(end, leader);
+    rgo &= ~__ballot(go && port == P);
+    const uint64_t ctl = rl64(m_ctl, leader);
+    if (lane == 0) __hip_atomic_store(reinterpret_cast<uint32_t*>(ctl), E, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  __builtin_amdgcn_s_waitcnt(0);   // this chunk's heads are out before a later chunk's may be
+  if (lane == 0) {
+    __hip_atomic_store(&qst->gde_commit, tk + 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long tw5 = __builtin_amdgcn_s_memrealtime();
+    __hip_atomic_fetch_add(&qst->gde_wait, (uint64_t)((tw1 - tw0) + (tw4 - tw3)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(&qst->gde_sect, (uint64_t)((tw2 - tw1) + (tw5 - tw4)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(&qst->gde_chunks, (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(&qst->gde_frames, (uint64_t)n_frames, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_fetch_add(&qst->gde_full, (uint64_t)n_full, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 // COOP = false: the 4 waves of a workgroup claim and process chunks independently (throughput).
@@ -271,7 +345,7 @@ __device__ __forceinline__ void gde_deliver(const RingArgs& a, RingDevState* qst
 // address check inline); the others keep the IPv4 path's register budget (an IPv6 packet's key
 // carries kKeyV6 there and takes no flow / ACL part).
 template <int HASH, int ACL, bool COOP, bool V6 = false>
-__global__ __launch_bounds__(kRingBlock) void ring_kernel(RingArgs a) {
+__global__ __launch_bounds__(kRingBlock, 2) void ring_kernel(RingArgs a) {   // (2 waves / SIMD: <= 256 registers)
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ unsigned long long coop_tk;                      // ticket
   __shared__ uint32_t coop_ctl[4];                            // go, epoch, table-set serial, ctl gen
@@ -558,7 +632,7 @@ __global__ __launch_bounds__(kRingBlock) void ring_kernel(RingArgs a) {
     uint32_t meta = make_meta(e.out_port, olen, e.reason, !e.reason && e.xhdr, !e.reason && e.flood);
     if (a.gde)   // GPU-direct egress: frames for memif vports straight into the pods' rings
       gde_deliver(a, qst, qi, tk, lane, t_begin, !pad && !e.reason && !e.xhdr && !e.flood && olen <= 64u,
-                  e.out_port, olen, o, meta);
+                  e.out_port, olen, o, meta, kx);
     wave_frames_store<kSysAux>(kx, o, r_out, run);
     __builtin_amdgcn_raw_buffer_store_b32(meta, r_meta, i * 4u, 0, kSysAux);
     if (a.side.cnt) {
@@ -793,7 +867,7 @@ void RingEngine::start(const FusedLaunch& f, const LaunchCfg& cfg, double deadli
   }
   s[0].set_serial[0] = h_sets_[0].serial;
   s[0].set_serial[1] = h_sets_[1].serial;
-  for (uint32_t q = 0; q < nq_; ++q) s[q].gde_turn = s[q].claim;   // GPU-direct egress: the first ticket's turn
+  for (uint32_t q = 0; q < nq_; ++q) s[q].gde_turn = s[q].gde_commit = s[q].claim;   // GPU-direct egress: first ticket's turns
   if (!stream_) create_stream();
   ck(hipMemcpyAsync(st_, s.data(), sizeof(RingDevState) * nq_, hipMemcpyHostToDevice, stream_), "state upload");
   // both table sets into the grid's HBM copies (the host's are current: stage_tables wrote them)
@@ -873,6 +947,18 @@ uint64_t RingEngine::gde_set(uint32_t port, uint32_t q, uint64_t ctl, uint64_t d
   e.ctl = ctl; e.desc = desc; e.buf = buf;
   e.mask = ring_size - 1; e.buf_size = buf_size; e.head = head; e.tail_cache = tail; e.valid = 1;
   return gde_write(port, q, e);
+}
+
+std::vector<uint64_t> RingEngine::gde_stats() {
+  if (running_) throw std::runtime_error("ring: gde_stats while running");
+  std::vector<RingDevState> s(nq_);
+  ck(hipMemcpy(s.data(), st_, sizeof(RingDevState) * nq_, hipMemcpyDeviceToHost), "gde stats");
+  std::vector<uint64_t> v;
+  for (const auto& x : s) {
+    v.push_back(x.gde_wait); v.push_back(x.gde_sect); v.push_back(x.gde_chunks); v.push_back(x.gde_frames);
+    v.push_back(x.gde_full);
+  }
+  return v;
 }
 
 uint64_t RingEngine::gde_clear(uint32_t port, uint32_t q) {

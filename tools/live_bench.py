@@ -120,7 +120,7 @@ def run(device: str = "cuda", n_pods: int = 8, flows: int = 1 << 20, n_acl: int 
         threads: int = 4, burst: int = 512, inflight: int = 64, ring_capacity: int = 16384,
         hash_mode: str = "lds", tx_workers: int = 2, queues: int = 4, max_inflight_frames: int = 4096,
         pod_ring: int = 1024, backend: str = "pipeline", coalesce_us: float = 8.0, loaded_window: int = 2048,
-        traffic: str = "plain", zero_copy: bool = False, saturated_only: bool = False) -> dict:
+        traffic: str = "plain", zero_copy: bool = False, saturated_only: bool = False, gpu_egress: bool = False) -> dict:
     """traffic: "plain" (the headline SFC), "vxlan-egress" (every pod's VF a VXLAN tunnel port:
     all frames leave encapsulated through one underlay vport, outer headers from the per-burst
     side pass) or "broadcast" (pods on one learning bridge sending to ff:ff:ff:ff:ff:ff: every
@@ -150,7 +150,7 @@ def run(device: str = "cuda", n_pods: int = 8, flows: int = 1 << 20, n_acl: int 
         ports = {p: MemifVport(os.path.join(d, f"pod{p}"), ring_size=pod_ring) for p in range(n_pods)}
         live = NativeLivePath(dp, ports, burst=burst, ring_capacity=ring_capacity, inflight=inflight,
                               tx_workers=tx_workers, queues=queues, max_inflight_frames=max_inflight_frames,
-                              coalesce_us=coalesce_us, zero_copy=zero_copy).start()
+                              coalesce_us=coalesce_us, zero_copy=zero_copy, gpu_egress=gpu_egress).start()
         gen = _WireLive.__new__(_WireLive)
         for i in range(n_pods):
             fr, ln = gen.frames(i, n_pods, k=1024, seed=100 + i, broadcast=True)
@@ -167,7 +167,7 @@ def run(device: str = "cuda", n_pods: int = 8, flows: int = 1 << 20, n_acl: int 
             ports[underlay] = MemifVport(os.path.join(d, "underlay"), ring_size=4 * pod_ring)
         live = NativeLivePath(dp, ports, burst=burst, ring_capacity=ring_capacity, inflight=inflight,
                               tx_workers=tx_workers, queues=queues, max_inflight_frames=max_inflight_frames,
-                              coalesce_us=coalesce_us, zero_copy=zero_copy).start()
+                              coalesce_us=coalesce_us, zero_copy=zero_copy, gpu_egress=gpu_egress).start()
         for i in range(n_pods):
             slots, im = S.traffic(sc, 4096, seed=100 + i, src_pods=np.array([i]))
             pods.append((ports[int(sc.pod_port[i])].path, slots, (im >> 16).astype(np.uint32)))
@@ -188,7 +188,13 @@ def run(device: str = "cuda", n_pods: int = 8, flows: int = 1 << 20, n_acl: int 
                    p50_us=_pct(r["lat_us"], 50), p99_us=_pct(r["lat_us"], 99))
         drain(nf, pods, stats)
         if saturated_only:   # (the queue curve: saturated rate only)
+            st = live.stats
+            out["engine"] = {k: int(st.get(k, 0)) for k in ("rx", "tx", "gpu_tx", "tx_full", "drop")}
             out["error"] = live.error
+            if gpu_egress and live._rings:   # GPU-direct egress diagnostics (ring.h RingDevState, after stop)
+                rings = list(live._rings)
+                live.stop()
+                out["gde"] = [list(map(int, r.eng.gde_stats())) for r in rings]
             return out
         # loaded, closed loop: `loaded_window` frames in flight over all pods (the generator
         # refills as frames arrive): the throughput of a saturated path with its queueing bounded
@@ -367,6 +373,7 @@ def main() -> None:
     ap.add_argument("--coalesce-us", type=float, default=8.0)
     ap.add_argument("--loaded-window", type=int, default=2048, help="frames in flight of the closed-loop loaded run")
     ap.add_argument("--zero-copy", action="store_true", help="the ring reads frames in the pods' memif regions")
+    ap.add_argument("--gpu-egress", action="store_true", help="the ring grid writes frames into the pods' rings itself")
     ap.add_argument("--veth", choices=("linux-bridge", "engine", "pipeline"), default=None,
                     help="netns pods on veth pairs, switched by a Linux bridge, by the native engine alone or by the "
                          "native engine in front of the data plane on --device (the deployed default)")
@@ -383,7 +390,7 @@ def main() -> None:
                          inflight=a.inflight, tx_workers=a.tx_workers, queues=a.queues,
                          max_inflight_frames=a.max_inflight_frames, pod_ring=a.pod_ring,
                          backend=a.backend, coalesce_us=a.coalesce_us, loaded_window=a.loaded_window,
-                         traffic=a.traffic, zero_copy=a.zero_copy)), flush=True)
+                         traffic=a.traffic, zero_copy=a.zero_copy, gpu_egress=a.gpu_egress)), flush=True)
 
 
 if __name__ == "__main__":

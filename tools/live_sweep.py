@@ -9,8 +9,9 @@ import sys
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
-GRID = [(4, 2, 4, False), (4, 1, 4, False), (5, 1, 4, False), (6, 1, 4, False), (3, 2, 4, False), (4, 2, 3, False),
-        (4, 2, 6, False), (6, 1, 6, False), (4, 2, 4, True), (6, 1, 4, True), (2, 3, 4, False), (8, 1, 4, False)]
+# (queues, tx workers, generator threads, zero copy, GPU-direct egress)
+GRID = [(4, 2, 4, False, False), (4, 2, 4, False, True), (4, 1, 4, False, True), (6, 1, 4, False, True),
+        (8, 1, 4, False, True), (8, 1, 6, False, True), (6, 1, 6, True, True), (8, 1, 4, True, True)]
 
 
 def main() -> None:
@@ -21,11 +22,12 @@ def main() -> None:
     spec = importlib.util.spec_from_file_location("live_bench", os.path.join(os.path.dirname(__file__), "live_bench.py"))
     lb = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(lb)
-    for q, w, g, zc in GRID:
+    for q, w, g, zc, gde in GRID:
         r = lb.run(device=a.device, duration=a.duration, queues=q, tx_workers=w, threads=g, zero_copy=zc,
-                   saturated_only=True)
-        print(json.dumps({"queues": q, "tx_workers": w, "gen_threads": g, "zero_copy": zc, "mpps": r.get("mpps"),
-                          "p50_us": r.get("p50_us"), "error": r.get("error")}), flush=True)
+                   saturated_only=True, gpu_egress=gde)
+        print(json.dumps({"queues": q, "tx_workers": w, "gen_threads": g, "zero_copy": zc, "gpu_egress": gde,
+                          "mpps": r.get("mpps"), "p50_us": r.get("p50_us"), "engine": r.get("engine"),
+                          "gde": r.get("gde"), "error": r.get("error")}), flush=True)
 
 
 if __name__ == "__main__":
