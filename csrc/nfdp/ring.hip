@@ -344,8 +344,10 @@ __device__ __forceinline__ void gde_deliver(const RingArgs& a, RingDevState* qst
 // V6: instances for tables with IPv6 flows / rules (the IPv6 key fold, the IPv6 TCAM and the
 // address check inline); the others keep the IPv4 path's register budget (an IPv6 packet's key
 // carries kKeyV6 there and takes no flow / ACL part).
-template <int HASH, int ACL, bool COOP, bool V6 = false>
-__global__ __launch_bounds__(kRingBlock, 2) void ring_kernel(RingArgs a) {   // (2 waves / SIMD: <= 256 registers)
+// GDE: the GPU-direct egress instances (gde_deliver in the chunk's tail; 2 waves / SIMD, <= 256
+// registers); the others keep the ring's code and register allocation as they were without it.
+template <int HASH, int ACL, bool COOP, bool V6 = false, bool GDE = false>
+__global__ __launch_bounds__(kRingBlock, GDE ? 2 : 1) void ring_kernel(RingArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ unsigned long long coop_tk;                      // ticket
   __shared__ uint32_t coop_ctl[4];                            // go, epoch, table-set serial, ctl gen
@@ -630,7 +632,7 @@ __global__ __launch_bounds__(kRingBlock, 2) void ring_kernel(RingArgs a) {   // 
     emit(p, e.tci, e.push != 0, o);
     const bool pad = im == kRingPadMeta;  // filler slot of a partial burst: no counters, no side work
     uint32_t meta = make_meta(e.out_port, olen, e.reason, !e.reason && e.xhdr, !e.reason && e.flood);
-    if (a.gde)   // GPU-direct egress: frames for memif vports straight into the pods' rings
+    if constexpr (GDE)   // GPU-direct egress: frames for memif vports straight into the pods' rings
       gde_deliver(a, qst, qi, tk, lane, t_begin, !pad && !e.reason && !e.xhdr && !e.flood && olen <= 64u,
                   e.out_port, olen, o, meta, kx);
     wave_frames_store<kSysAux>(kx, o, r_out, run);
@@ -685,16 +687,16 @@ __global__ __launch_bounds__(kRingBlock, 2) void ring_kernel(RingArgs a) {   // 
   on_idle();  // exit: whatever this wave counted since its last flush reaches the global table
 }
 
-template <int H, int A, bool C, bool V6 = false>
+template <int H, int A, bool C, bool V6 = false, bool G = false>
 static hipError_t launch_ring_t(const RingArgs& a, int num_cus, int wgs, hipStream_t s) {
   const size_t lds = ring_lds(H, A, C ? a.lds_tiles : a.acl_tiles).total;
   if (lds > 64 * 1024) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&ring_kernel<H, A, C, V6>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&ring_kernel<H, A, C, V6, G>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
   if ((lds + 2048) * (size_t)wgs > 160 * 1024) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((ring_kernel<H, A, C, V6>), dim3((uint32_t)(num_cus * wgs)), dim3(kRingBlock), lds, s, a);
+  hipLaunchKernelGGL((ring_kernel<H, A, C, V6, G>), dim3((uint32_t)(num_cus * wgs)), dim3(kRingBlock), lds, s, a);
   return hipGetLastError();
 }
 
@@ -736,6 +738,17 @@ hipError_t launch_ring(const RingLaunch& r, const LaunchCfg& cfg, int wgs_per_cu
   if (cfg.hash_mode == kHashLds && !a.toep_tab) return hipErrorInvalidValue;
   if (wgs_per_cu < 1 || wgs_per_cu > 8 || cfg.num_cus < 1) return hipErrorInvalidValue;
   const int h = cfg.hash_mode, ac = cfg.acl_mode;
+  if (a.gde) {   // GPU-direct egress: its instances (LDS or MFMA hash, MFMA ACL, IPv4 or IPv6 tables)
+    if (ac != kAclMfma || h == kHashScalar) return hipErrorNotSupported;
+    const bool v6 = v6_keys(a.t);
+#define NFDP_GCASE(HH, CC, VV) \
+    if (h == HH && coop == CC && v6 == VV) return launch_ring_t<HH, kAclMfma, CC, VV, true>(a, cfg.num_cus, wgs_per_cu, s);
+    NFDP_GCASE(kHashLds, true, false) NFDP_GCASE(kHashLds, false, false) NFDP_GCASE(kHashLds, true, true)
+    NFDP_GCASE(kHashLds, false, true) NFDP_GCASE(kHashMfma, true, false) NFDP_GCASE(kHashMfma, false, false)
+    NFDP_GCASE(kHashMfma, true, true) NFDP_GCASE(kHashMfma, false, true)
+#undef NFDP_GCASE
+    return hipErrorInvalidValue;
+  }
   if (v6_keys(a.t)) {   // IPv6 flows / rules: the V6 instances (LDS or MFMA hash, MFMA ACL)
     if (ac != kAclMfma || h == kHashScalar) return hipErrorNotSupported;
     if (h == kHashLds) return coop ? launch_ring_t<kHashLds, kAclMfma, true, true>(a, cfg.num_cus, wgs_per_cu, s)
