@@ -193,11 +193,11 @@ def parse():
     ap.add_argument("--no-hops", action="store_true", help="skip the SFC hop pipeline across GPUs (tools/hop_bench.py)")
     ap.add_argument("--no-live", action="store_true", help="skip the live pod-to-pod (native I/O engine) block")
     ap.add_argument("--no-unsteered", action="store_true", help="N > 1 rss: skip the exchange-bound (unsteered) variant")
-    ap.add_argument("--live-workers", type=int, default=1, help="native I/O engine delivery threads per queue")
-    ap.add_argument("--live-queues", type=int, default=5, help="native I/O engine rx queues (threads)")
-    ap.add_argument("--live-gen-threads", type=int, default=8, help="pod traffic generator threads")
-    ap.add_argument("--live-host-egress", action="store_true",
-                    help="live block: the tx threads deliver every frame (no GPU-direct egress)")
+    ap.add_argument("--live-workers", type=int, default=2, help="native I/O engine delivery threads per queue")
+    ap.add_argument("--live-queues", type=int, default=4, help="native I/O engine rx queues (threads)")
+    ap.add_argument("--live-gen-threads", type=int, default=4, help="pod traffic generator threads")
+    ap.add_argument("--live-gpu-egress", action="store_true",
+                    help="live block: the ring grid writes frames into the pods' rings itself (GPU-direct egress)")
     ap.add_argument("--variant-steps", type=int, default=30)
     ap.add_argument("--chunks", type=int, default=4, help="pipeline chunks per step (N > 1)")
     ap.add_argument("--mode", default="rss", choices=["rss", "replicated", "sharded"],
@@ -721,17 +721,18 @@ def main() -> None:
                 "live_bench", os.path.join(os.path.dirname(os.path.abspath(__file__)), "tools", "live_bench.py"))
             lb = importlib.util.module_from_spec(spec)
             spec.loader.exec_module(lb)
-            gde = not a.live_host_egress
+            gde = bool(a.live_gpu_egress)
             live = lb.run(device=str(dev), n_pods=a.pods_per_gpu, flows=a.flows, n_acl=a.acl, duration=0.5,
                           threads=a.live_gen_threads, tx_workers=a.live_workers, queues=a.live_queues,
                           hash_mode=a.hash, gpu_egress=gde)
             live["gpu_egress"] = gde
-            # the previous default for comparison: host egress (2 tx threads per queue, 4 queues,
-            # 4 generator threads), saturated rate only
+            # the other egress mode for comparison (GPU-direct egress: 6 queues, 1 tx thread each, 6
+            # generator threads; or host egress), saturated rate only
+            alt = (dict(threads=4, tx_workers=2, queues=4, gpu_egress=False) if gde else
+                   dict(threads=6, tx_workers=1, queues=6, gpu_egress=True))
             hp = lb.run(device=str(dev), n_pods=a.pods_per_gpu, flows=a.flows, n_acl=a.acl, duration=0.3,
-                        threads=4, tx_workers=2, queues=4, hash_mode=a.hash, saturated_only=True)
-            live["host_egress_4q_mpps"] = hp.get("mpps")
-            live["host_egress_4q_p50_us"] = hp.get("p50_us")
+                        hash_mode=a.hash, saturated_only=True, **alt)
+            live["other_egress"] = {**alt, "mpps": hp.get("mpps"), "p50_us": hp.get("p50_us"), "error": hp.get("error")}
             # the engine's queue curve: saturated pod -> pod Mpps at 1 / 2 / 4 / 8 rx queues (each
             # with its tx workers), the same pods and pipeline; bounded by the box's CPU share
             curve = []

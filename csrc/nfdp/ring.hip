@@ -233,7 +233,7 @@ __device__ __forceinline__ void gde_deliver(const RingArgs& a, RingDevState* qst
   const unsigned long long tw1 = __builtin_amdgcn_s_memrealtime();
   // ---- 1. reserve ----
   bool go = false;
-  uint32_t pos = 0, end = 0, n_frames = 0, n_full = 0;
+  uint32_t pos = 0, end = 0, n_frames = 0, n_full = 0;   // (end: the port's new head)
   unsigned long long rem = __ballot(elig);
   while (rem) {
     const int leader = __builtin_ctzll(rem);
@@ -324,6 +324,8 @@ __device__ __forceinline__ void gde_deliver(const RingArgs& a, RingDevState* qst
     const uint64_t ctl = rl64(m_ctl, leader);
     if (lane == 0) __hip_atomic_store(reinterpret_cast<uint32_t*>(ctl), E, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
+  // (waited for: a later chunk's head landing first and then overwritten would go back.  A PCIe
+  // atomic add of the count instead needs no wait, but measured slower: 28-32 vs 42-57 Mpps, r5 s14)
   __builtin_amdgcn_s_waitcnt(0);   // this chunk's heads are out before a later chunk's may be
   if (lane == 0) {
     __hip_atomic_store(&qst->gde_commit, tk + 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

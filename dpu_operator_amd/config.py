@@ -40,6 +40,10 @@ class NodeConfig:
     vport_kind: str = "veth"           # veth (kernel netdev pods, AF_PACKET rings) | memif | tap
     io_queues: int = 4                 # native engine rx queues (threads), each with a ring queue per GPU
     io_workers: int = 2                # native engine delivery threads per queue (4 x 2: 57.9 Mpps, r4 s4)
+    # GPU-direct egress: the ring grids write frames for memif vports into the pods' rings themselves
+    # (ring.h GdeRing).  Off by default: on the GPU box it measured 42-57 Mpps against 56-58 for the
+    # tx threads (r5 s14 interleaved A/B), so it pays only where host CPUs are scarcer than that.
+    gpu_egress: bool = False
     # the GPU node's wire port (data-plane port `wire_port`, the reference's RPM / SFP uplink):
     #   "veth"  a veth pair whose host end (`uplink_host_ifname`) the node's stack or a host bridge
     #           with the physical NIC reaches pods through (an OvS internal port's role);

@@ -361,9 +361,10 @@ class GpuVsp(VspBase):
                 planes = self.dp.planes if hasattr(self.dp, "planes") else [self.dp]
                 # lane groups: every GPU brings io_queues rx threads (+ their tx workers) of its
                 # own, pinned to its NUMA-local CPUs, so I/O capacity grows with the GPU count;
-                # GPU-direct egress: the grids write frames for memif vports into the pods' rings
+                # gpu_egress (node config): the grids write frames for memif vports into the pods' rings
                 self.livepath = NativeLivePath(planes, ports, tx_workers=self.tx_workers, queues=self.io_queues,
-                                               lane_groups=True, pin_cpus=True, gpu_egress=True).start()
+                                               lane_groups=True, pin_cpus=True,
+                                               gpu_egress=node_config().gpu_egress).start()
             else:
                 from ..dataplane.netio import LivePath
 

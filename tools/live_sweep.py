@@ -10,8 +10,8 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 # (queues, tx workers, generator threads, zero copy, GPU-direct egress)
-GRID = [(4, 2, 4, False, False), (4, 1, 8, False, False), (4, 1, 8, False, True), (3, 1, 8, False, True),
-        (4, 1, 6, False, True), (2, 1, 10, False, True), (4, 1, 8, True, True), (5, 1, 8, False, True)]
+GRID = [(4, 2, 4, False, False), (5, 1, 8, False, True), (4, 1, 6, False, True), (4, 1, 4, False, True),
+        (6, 1, 6, False, True)] * 3
 
 
 def main() -> None:
