@@ -578,6 +578,23 @@ __device__ __forceinline__ void flow_probe_issue(const TablesView& t, uint32_t h
 #endif
 }
 
+// 16-B equality as one OR of XORs (v_bitop3 chains, one compare).  Written as four field compares
+// joined with &&, the compiler packs the v_cmp results into a bit vector (v_cndmask + shifts +
+// s_nop per field: 15 VALU per bucket line compare in the probe, r5 s18 ISA histogram).
+// The XORs pass through empty asm: without it InstCombine turns or(xor...) == 0 back into the
+// <4 x i32> compare.
+#ifndef NFDP_EQ16_ASM
+#define NFDP_EQ16_ASM 1   // 0: the field compares (A/B)
+#endif
+__device__ __forceinline__ bool eq16(const uint4& a, const uint4& b) {
+#if !NFDP_EQ16_ASM
+  return a.x == b.x && a.y == b.y && a.z == b.z && a.w == b.w;
+#endif
+  uint32_t x = a.x ^ b.x, y = a.y ^ b.y, z = a.z ^ b.z, w = a.w ^ b.w;
+  asm("" : "+v"(x), "+v"(y), "+v"(z), "+v"(w));
+  return (x | y | z | w) == 0u;
+}
+
 __device__ __forceinline__ int64_t flow_probe_finish(const TablesView& t, const FlowKey& k, uint32_t h, bool probe,
                                                      uint4* kx, const uint4 (&v)[8], uint4& act) {
   const uint32_t lane = threadIdx.x & 63u;
@@ -595,7 +612,7 @@ __device__ __forceinline__ int64_t flow_probe_finish(const TablesView& t, const 
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const uint4 kk = kx[8 * j + q];
-    const bool hit = !(c & 1u) && v[j].x == kk.x && v[j].y == kk.y && v[j].z == kk.z && v[j].w == kk.w;
+    const bool hit = ((c & 1u) == 0u) & eq16(v[j], kk);
     const unsigned long long m = __ballot(hit);
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
@@ -613,7 +630,8 @@ __device__ __forceinline__ int64_t flow_probe_finish(const TablesView& t, const 
     const TableHash th = table_hash(h, t.bucket_mask);
     const uint4* row = fl + (size_t)th.b2 * (kBucketSlots * 2);
     const uint32_t used = k.meta | kSlotUsed;
-    auto eq = [&](const uint4& e) { return e.x == k.src_ip && e.y == k.dst_ip && e.z == k.ports && e.w == used; };
+    const uint4 key = make_uint4(k.src_ip, k.dst_ip, k.ports, used);
+    auto eq = [&](const uint4& e) { return eq16(e, key); };
     const uint4 k0 = row[0], a0 = row[1], k1 = row[2], a1 = row[3];
     const uint4 k2 = row[4], a2 = row[5], k3 = row[6], a3 = row[7];
     const bool n0 = eq(k0), n1 = eq(k1), n2 = eq(k2), n3 = eq(k3);

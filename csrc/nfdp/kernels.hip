@@ -937,35 +937,89 @@ struct V6Args {
   uint4* keys;                // the batch's out slots: word 0..3 = the packet's folded FlowKey
 };
 
-__global__ __launch_bounds__(256) void v6_kernel(V6Args a) {
+// Latency layout (r5 s16: 307 us per 4M-slot dual-stack batch, as long as the fused kernel itself;
+// one dependent chain per iteration - frame, four rule tiles read from L2, bucket line, side entry):
+//  * the first kV6LdsTiles rule tiles (fragments + C init) are staged in LDS once per workgroup;
+//  * the next run's frames and in-meta words are loaded right after this run's parse;
+//  * the bucket lines leave as soon as the folded key's hash is known (IPv6 packets only: an IPv4
+//    packet's lines are not loaded) and land under the ACL's MFMAs.
+#ifndef NFDP_V6_WAVES_PER_EU
+#define NFDP_V6_WAVES_PER_EU 2
+#endif
+#ifndef NFDP_V6_EARLY_PROBE
+#define NFDP_V6_EARLY_PROBE 1   // 0: the bucket lines leave after the ACL (fewer live VGPRs)
+#endif
+constexpr uint32_t kV6LdsTiles = 4;   // 64 IPv6 rules: 12.25 KiB of LDS
+__global__ __launch_bounds__(256, NFDP_V6_WAVES_PER_EU) void v6_kernel(V6Args a) {
   __shared__ uint32_t kw[4][64 * 13];   // per wave: 64 key6 rows of 12 words (+1 pad: bank spread)
   __shared__ uint4 kxs[4][64];          // per wave: frame transposition / probe key exchange scratch
   __shared__ uint32_t ltab[16 * 256];
+  __shared__ v4i lwf[kV6LdsTiles * 3 * 64];
+  __shared__ v4i lci[kV6LdsTiles * 4];
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   const uint32_t g = lane >> 4, col = lane & 15u;
   uint32_t* row = kw[wv];
   uint4* kx = kxs[wv];
   if (a.toep_tab)
     for (uint32_t q = threadIdx.x; q < 16 * 256; q += 256) ltab[q] = a.toep_tab[q];
+  const uint32_t lt6 = a.tiles < kV6LdsTiles ? a.tiles : kV6LdsTiles;
+  for (uint32_t q = threadIdx.x; q < lt6 * 3 * 64; q += 256) lwf[q] = a.wfrag[q];
+  for (uint32_t q = threadIdx.x; q < lt6 * 4; q += 256) lci[q] = a.cinit[q];
   __syncthreads();
   // coalesced frame loads (the wave's 64 slots = one 4-KiB run, device.h wave_frames_load)
   const __amdgpu_buffer_rsrc_t r_pk = __builtin_amdgcn_make_buffer_rsrc((void*)a.pkts, (short)0, (int)(a.n * 64u), kBufCfg);
+  const __amdgpu_buffer_rsrc_t r_im = __builtin_amdgcn_make_buffer_rsrc((void*)a.inmeta, (short)0, (int)(a.n * 4u), kBufCfg);
   const uint32_t wave0 = __builtin_amdgcn_readfirstlane(threadIdx.x) & ~63u;
-  for (uint32_t base = blockIdx.x * 256u; base < a.n; base += gridDim.x * 256u) {   // block-uniform trips
+  const uint32_t stride = gridDim.x * 256u;
+  auto run_of = [&](uint32_t base) { return base + wave0 < a.n ? (base + wave0) * 64u : kNoRun; };
+  v4u cn[4];
+  uint32_t imn;
+  {
+    const uint32_t i0 = blockIdx.x * 256u + threadIdx.x;
+    wave_frames_load<0>(r_pk, run_of(blockIdx.x * 256u), cn);
+    imn = __builtin_amdgcn_raw_buffer_load_b32(r_im, i0 < a.n ? i0 * 4u : kNoRun, 0, 0);
+  }
+  for (uint32_t base = blockIdx.x * 256u; base < a.n; base += stride) {   // block-uniform trips
     const uint32_t i = base + threadIdx.x;
     const bool valid = i < a.n;
     uint32_t d[kSlotDwords];
-    {
-      v4u cn[4];
-      wave_frames_load<0>(r_pk, base + wave0 < a.n ? (base + wave0) * 64u : kNoRun, cn);
-      wave_frames_to_lanes<true>(kx, cn, d);
-    }
+    wave_frames_to_lanes<true>(kx, cn, d);
     Parsed p;
     IngressState st;
-    ingress_stage(a.t, d, valid ? a.inmeta[i] : 0u, p, st);
+    ingress_stage(a.t, d, valid ? imn : 0u, p, st);
+    {   // the next run: lands under this one's classification
+      const uint32_t nx = i + stride;
+      wave_frames_load<0>(r_pk, run_of(base + stride), cn);
+      imn = __builtin_amdgcn_raw_buffer_load_b32(r_im, nx < a.n ? nx * 4u : kNoRun, 0, 0);
+    }
     const bool v6 = valid && p.ipv6;
     uint32_t word = 0;
     if (__any(v6)) {   // wave-uniform: EXEC full from here (MFMA, cross-lane reads, the wave probe)
+      const bool probe = v6 && !st.reason && a.t.flow6_on;
+      uint32_t h = 0;
+      uint4 bv[8];
+      auto issue = [&]() {
+        if (!a.t.flow6_on) return;
+        // the folded key's Toeplitz hash, then the first-choice bucket lines (flow_probe_issue's
+        // wave-cooperative layout: lane 8j + q... loads line part c of packet 8j + q's bucket)
+        if (a.toep_tab) {
+          const uint32_t w[4] = {st.key.src_ip, st.key.dst_ip, st.key.ports, st.key.meta};
+#pragma unroll
+          for (int q = 0; q < 16; ++q) h ^= ltab[q * 256 + ((w[q >> 2] >> (8 * (q & 3))) & 0xFFu)];
+        } else {
+          h = toeplitz_scalar(st.key, a.t.rss_key);
+        }
+        // (flat loads under the lane mask: a multi-GB table is past a buffer's 32-bit offsets)
+        const uint4* fl = reinterpret_cast<const uint4*>(a.t.flows);
+        const uint32_t b1 = probe ? (h & a.t.bucket_mask) : kNoRun;
+        const uint32_t c = lane & 7u, q = lane >> 3;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const uint32_t bj = (uint32_t)__shfl((int)b1, 8 * j + (int)q);
+          bv[j] = bj != kNoRun ? fl[(size_t)bj * (kBucketSlots * 2) + c] : make_uint4(0u, 0u, 0u, 0u);
+        }
+      };
+      if (NFDP_V6_EARLY_PROBE) issue();
       int rule = -1;
       if (a.tiles) {
 #pragma unroll
@@ -982,13 +1036,13 @@ __global__ __launch_bounds__(256) void v6_kernel(V6Args a) {
                              (int)spread8_fp4((w >> 16) & 0xFFu), (int)spread8_fp4(w >> 24), 0, 0, 0, 0};
           }
         uint32_t best[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
-        for (uint32_t t = 0; t < a.tiles; ++t) {
-          const v4i ci = a.cinit[t * 4 + g];
-          const v4f_t c = {__int_as_float(ci[0]), __int_as_float(ci[1]), __int_as_float(ci[2]), __int_as_float(ci[3])};
-          v4f_t acc[4] = {c, c, c, c};
+        auto tile = [&](const v4i* wf, const v4i* ci4, uint32_t t) {
+          const v4i ci = ci4[t * 4 + g];
+          const v4f_t cc = {__int_as_float(ci[0]), __int_as_float(ci[1]), __int_as_float(ci[2]), __int_as_float(ci[3])};
+          v4f_t acc[4] = {cc, cc, cc, cc};
 #pragma unroll
           for (int k = 0; k < 3; ++k) {
-            const v4i a4 = a.wfrag[((size_t)t * 3 + k) * 64 + lane];
+            const v4i a4 = wf[((size_t)t * 3 + k) * 64 + lane];
             const v8i_t av = {a4[0], a4[1], a4[2], a4[3], 0, 0, 0, 0};
 #pragma unroll
             for (int tt = 0; tt < 4; ++tt)
@@ -998,31 +1052,25 @@ __global__ __launch_bounds__(256) void v6_kernel(V6Args a) {
           for (int tt = 0; tt < 4; ++tt)
             best[tt] = min(best[tt], min(min(__float_as_uint(acc[tt][0]), __float_as_uint(acc[tt][1])),
                                          min(__float_as_uint(acc[tt][2]), __float_as_uint(acc[tt][3]))));
-        }
+        };
+        for (uint32_t t = 0; t < lt6; ++t) tile(lwf, lci, t);          // staged (LDS)
+        for (uint32_t t = lt6; t < a.tiles; ++t) tile(a.wfrag, a.cinit, t);   // the rest (L2)
 #pragma unroll
         for (int tt = 0; tt < 4; ++tt) {
           best[tt] = min(best[tt], (uint32_t)__shfl_xor(best[tt], 16));
           best[tt] = min(best[tt], (uint32_t)__shfl_xor(best[tt], 32));
         }
         const uint32_t bb = pick4(g, best[0], best[1], best[2], best[3]);
-        const uint32_t bv = bb == 0xFFFFFFFFu ? bb : (uint32_t)__uint_as_float(bb);
-        const int r = acl_rule_of(bv, a.t.n_acl6);
+        const uint32_t bvv = bb == 0xFFFFFFFFu ? bb : (uint32_t)__uint_as_float(bb);
+        const int r = acl_rule_of(bvv, a.t.n_acl6);
         rule = r >= 0 ? (int)(a.t.n_acl + (uint32_t)r) : -1;
         __builtin_amdgcn_wave_barrier();
       }
+      if (!NFDP_V6_EARLY_PROBE) issue();
       bool ok = false;
       if (a.t.flow6_on) {
-        // the folded key's Toeplitz hash, the wave-cooperative bucket probe, the side entry check
-        uint32_t h = 0;
-        if (a.toep_tab) {
-          const uint32_t w[4] = {st.key.src_ip, st.key.dst_ip, st.key.ports, st.key.meta};
-#pragma unroll
-          for (int q = 0; q < 16; ++q) h ^= ltab[q * 256 + ((w[q >> 2] >> (8 * (q & 3))) & 0xFFu)];
-        } else {
-          h = toeplitz_scalar(st.key, a.t.rss_key);
-        }
         uint4 act;
-        const int64_t slot = flow_probe_wave(a.t, st.key, h, v6 && !st.reason, kx, act);
+        const int64_t slot = flow_probe_finish(a.t, st.key, h, probe, kx, bv, act);
         ok = slot >= 0 && flow6_verify(a.t, p, slot);
       }
       word = (uint32_t)(rule + 1) | (ok ? 0x80000000u : 0u);
@@ -1192,8 +1240,10 @@ static hipError_t launch_v6(const FusedLaunch& f, int num_cus, hipStream_t s) {
   V6Args a{f.t, reinterpret_cast<const uint4*>(f.pkts), f.inmeta, f.n, reinterpret_cast<const v4i*>(f.acl6_wfrag),
            reinterpret_cast<const v4i*>(f.acl6_cinit), f.t.n_acl6 ? f.acl6_tiles : 0u, f.toep_tab, f.out_meta,
            reinterpret_cast<uint4*>(f.out)};
+  // one workgroup per SIMD-resident slot (NFDP_V6_WAVES_PER_EU 4-wave blocks per CU): every block
+  // runs the same number of grid-stride trips, no second round of blocks behind the first
   uint32_t grid = (f.n + 255) / 256;
-  const uint32_t cap = (uint32_t)num_cus * 8u;
+  const uint32_t cap = (uint32_t)num_cus * NFDP_V6_WAVES_PER_EU;
   if (grid > cap) grid = cap;
   if (grid == 0) return hipSuccess;
   hipLaunchKernelGGL(v6_kernel, dim3(grid), dim3(256), 0, s, a);

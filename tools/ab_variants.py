@@ -5,8 +5,10 @@ process that loads one variant (NFDP_EXT_DIR, native/build.py NFDP_BUILD_OUT) an
 headline step (1M flows, ACL 256 -> SNAT -> L2, 4M-packet batches) with HIP events; variants
 alternate round by round so box drift hits them equally.
 
-python tools/ab_variants.py base= variants/noreload [--rounds 4] [--iters 50]
+python tools/ab_variants.py base= variants/noreload [--rounds 4] [--iters 50] [--acl 256|wild|ipv6]
   (an empty directory means the in-tree build)
+python tools/ab_variants.py --inline [--acl ...]   one in-process measurement of the in-tree build
+  (for rocprofv3: no child process)
 """
 import argparse
 import json
@@ -24,10 +26,18 @@ g = DataPlane(device="cuda", flow_buckets=1 << 19, hash_mode="lds", acl_mode="mf
 sc = S.build_sfc(g, n_pods=8, n_flows=1 << 20, n_acl=256, seed=0)
 if acl == "wild":
     S.install_acl_wild(g)
+info6 = S.install_ipv6(g, sc, 1 << 16, 64) if acl == "ipv6" else None
 g.commit(full=True)
 bs = []
 for r in range(4):
-    pk, im = S.traffic(sc, batch, seed=1 + r)
+    if info6 is None:
+        pk, im = S.traffic(sc, batch, seed=1 + r)
+    else:   # bench.py's dual stack: half IPv6, shuffled
+        pk4, im4 = S.traffic(sc, batch - batch // 2, seed=9200 + r)
+        pk6, im6 = S.traffic_ipv6(sc, info6, batch // 2, seed=9300 + r)
+        perm = np.random.default_rng(r).permutation(batch)
+        pk = np.ascontiguousarray(np.concatenate([pk4, pk6])[perm])
+        im = np.ascontiguousarray(np.concatenate([im4, im6])[perm])
     bs.append((torch.from_numpy(pk).cuda(), torch.from_numpy(im.view(np.int32)).cuda()))
 out, meta, lat = g.alloc_batch(batch)
 for k in range(10):
@@ -46,12 +56,17 @@ print(json.dumps({"ms": ms, "mpps": batch / ms / 1e3}))
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("variants", nargs="+", help="name=dir (dir empty: in-tree build)")
+    ap.add_argument("variants", nargs="*", help="name=dir (dir empty: in-tree build)")
+    ap.add_argument("--inline", action="store_true", help="measure the in-tree build in this process")
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--batch", type=int, default=1 << 22)
-    ap.add_argument("--acl", default="256", choices=["256", "wild"])
+    ap.add_argument("--acl", default="256", choices=["256", "wild", "ipv6"])
     a = ap.parse_args()
+    if a.inline:
+        sys.argv = ["-", str(a.iters), str(a.batch), a.acl]
+        exec(compile(CHILD, "ab_variants_child", "exec"), {"__name__": "__child__"})
+        return
     vs = [v.split("=", 1) if "=" in v else (os.path.basename(v), v) for v in a.variants]
     res = {n: [] for n, _ in vs}
     for r in range(a.rounds):
