@@ -424,9 +424,10 @@ PYBIND11_MODULE(_nfdp, m) {
                            uintptr_t toep_frag, uintptr_t toep_tab, int hash_mode, int acl_mode, int num_cus,
                            uintptr_t stream, uint32_t flags, py::object side, uintptr_t n_dev, uintptr_t steer_list,
                            uintptr_t steer_cnt, uint32_t nranks, uint32_t rank, uint32_t steer_cap,
-                           uintptr_t hop_state) {
+                           uintptr_t hop_state, uintptr_t v6_keys) {
     FusedLaunch f{};
     f.hop_state = reinterpret_cast<HopState*>(hop_state);
+    f.v6_keys = reinterpret_cast<void*>(v6_keys);
     f.steer_list = reinterpret_cast<uint32_t*>(steer_list);
     f.steer_cnt = reinterpret_cast<uint32_t*>(steer_cnt);
     f.steer_cap = steer_cap;
@@ -464,7 +465,8 @@ PYBIND11_MODULE(_nfdp, m) {
      py::arg("acl_wfrag"), py::arg("acl_cinit"), py::arg("acl_tiles"), py::arg("toep_frag"), py::arg("toep_tab"),
      py::arg("hash_mode"), py::arg("acl_mode"), py::arg("num_cus"), py::arg("stream"), py::arg("flags") = 0,
      py::arg("side") = py::none(), py::arg("n_dev") = 0, py::arg("steer_list") = 0, py::arg("steer_cnt") = 0,
-     py::arg("nranks") = 0, py::arg("rank") = 0, py::arg("steer_cap") = 0, py::arg("hop_state") = 0);
+     py::arg("nranks") = 0, py::arg("rank") = 0, py::arg("steer_cap") = 0, py::arg("hop_state") = 0,
+     py::arg("v6_keys") = 0);
   m.def("launch_pairs", [](py::dict tables, uintptr_t pkts, uintptr_t inmeta, uint32_t n, uintptr_t port_ctr, bool count,
                            uintptr_t stream) {
     const TablesView t = tables_from(tables);

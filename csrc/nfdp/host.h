@@ -136,6 +136,9 @@ struct FusedLaunch {
   // split chains (kHopXfer): each handed-off frame's HopState (n records, nullable: the XFER
   // instances run only when it is given)
   HopState* hop_state = nullptr;
+  // IPv6 tables: v6_kernel's folded keys, one 16-B row per slot (coalesced for the fused V6
+  // instances); null: parked in the first 16 B of each out slot (a strided read, 1/4 of its lines)
+  void* v6_keys = nullptr;
 };
 // The hand-off itself (kernels.hip): frames of `meta` with reason kRemote and port `plane` (and
 // their HopState records) -> the inbox on the GPU that resumes them, written there by this GPU

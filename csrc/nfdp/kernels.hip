@@ -91,6 +91,10 @@ struct FusedArgs {
   uint32_t steer_cap_blk;
   // XFER instances (split chains, kHopXfer): a handed-off frame's HopState record (n x 32 B)
   HopState* hop_state;
+  // V6 instances: the folded keys (v6_kernel): row i * v6_key_stride (1: the compact buffer, 4: the
+  // out slots)
+  const uint4* v6_key;
+  uint32_t v6_key_stride;
 };
 
 __device__ __forceinline__ size_t lds_align16(size_t x) { return (x + 15) & ~(size_t)15; }
@@ -165,6 +169,9 @@ constexpr int kStreamAux = 2;        // nt: frames are read once / written once 
 // instances keep their register budget untouched.
 // XFER: the instances for tables with split chains (kHopXfer hops): a frame handed to another GPU
 // leaves its HopState record in a.hop_state (two fixed-count stores in the tail, like the others).
+#ifndef NFDP_V6_PREFETCH
+#define NFDP_V6_PREFETCH 0   // 1: the V6 instances prefetch the next slot like the IPv4 ones (A/B)
+#endif
 #ifndef NFDP_XFER_WAVES_PER_EU
 #define NFDP_XFER_WAVES_PER_EU 4   // the split-chain instances (r5 s9: 346 us / 4M frames with 30 spilled
                                    // VGPRs at 4 waves, 387 us spill-free at 3)
@@ -284,12 +291,12 @@ void fused_kernel(FusedArgs a) {
     Parsed p;
     IngressState st;
     ingress_stage<LdsTables, false>(TV, ta_it, dn, imn, p, st);  // copies the frame into p.s: dn is free for the prefetch
-    // IPv6 keys (tables with IPv6 flows / rules): v6_kernel folded them into out[i] (overwritten
-    // by this lane's egress slot in the tail)
+    // IPv6 keys (tables with IPv6 flows / rules): v6_kernel folded them into a.v6_key (the compact
+    // buffer, or out[i], overwritten by this lane's egress slot in the tail)
     if constexpr (V6) {
       if (__builtin_expect(__any(p.ipv6), 0)) {
         if (p.ipv6 && valid) {
-          const uint4 k6 = a.out[(size_t)i * 4];   // first 16 B of slot i
+          const uint4 k6 = a.v6_key[(size_t)i * a.v6_key_stride];
           st.key.src_ip = k6.x; st.key.dst_ip = k6.y; st.key.ports = k6.z; st.key.meta = k6.w;
         }
       }
@@ -342,7 +349,7 @@ void fused_kernel(FusedArgs a) {
       // here, the same append cost the instance 15 more spilled VGPRs)
       if (valid && !st.reason && flowp && owner_of(hash, a.nranks) != a.rank) st.reason = kRemote;
     }
-    if constexpr (!REMOTE && !V6) {
+    if constexpr (!REMOTE && (!V6 || NFDP_V6_PREFETCH)) {
       // prefetch the next slot now: it lands under this slot's probe and chain
       const uint32_t nx = i + stride;
       wave_frames_load<kStreamAux>(r_pk, run_of(base + stride), cn);
@@ -487,7 +494,7 @@ void fused_kernel(FusedArgs a) {
         store_b128<kStreamAux>(h0, r_hop, off, 0);
         store_b128<kStreamAux>(h1, r_hop, off, 16);
       }
-      if constexpr (V6) {   // (no prefetch in these instances: the next slot is loaded here)
+      if constexpr (V6 && !NFDP_V6_PREFETCH) {   // (no prefetch: the next slot is loaded here)
         const uint32_t nx = i + stride;
         wave_frames_load<kStreamAux>(r_pk, run_of(base + stride), cn);
         imn = __builtin_amdgcn_raw_buffer_load_b32(r_im, nx < n ? nx * 4u : kNoRun, 0, kStreamAux);
@@ -934,7 +941,8 @@ struct V6Args {
   uint32_t tiles;      // 0: no IPv6 rules
   const uint32_t* toep_tab;   // [16][256] byte tables (null: scalar Toeplitz)
   uint32_t* res;              // the batch's out_meta: rule + 1 | verified << 31
-  uint4* keys;                // the batch's out slots: word 0..3 = the packet's folded FlowKey
+  uint4* keys;                // row i * key_stride: the packet's folded FlowKey (FusedLaunch::v6_keys)
+  uint32_t key_stride;
 };
 
 // Latency layout (r5 s16: 307 us per 4M-slot dual-stack batch, as long as the fused kernel itself;
@@ -945,6 +953,9 @@ struct V6Args {
 //    packet's lines are not loaded) and land under the ACL's MFMAs.
 #ifndef NFDP_V6_WAVES_PER_EU
 #define NFDP_V6_WAVES_PER_EU 2
+#endif
+#ifndef NFDP_V6_ABL
+#define NFDP_V6_ABL 0
 #endif
 #ifndef NFDP_V6_EARLY_PROBE
 #define NFDP_V6_EARLY_PROBE 1   // 0: the bucket lines leave after the ACL (fewer live VGPRs)
@@ -979,6 +990,17 @@ __global__ __launch_bounds__(256, NFDP_V6_WAVES_PER_EU) void v6_kernel(V6Args a)
     wave_frames_load<0>(r_pk, run_of(blockIdx.x * 256u), cn);
     imn = __builtin_amdgcn_raw_buffer_load_b32(r_im, i0 < a.n ? i0 * 4u : kNoRun, 0, 0);
   }
+  // The side-entry check of a hit is deferred by one iteration (r5 s20 ablation: the flow check was
+  // 120 of the kernel's 252 us, its second dependent random load exposed): the 32-B entry is loaded
+  // when the probe finishes and compared - with the result word stored - after the NEXT run's ACL.
+  uint32_t pv_i = kNoRun, pv_word = 0, pv_addr[8];
+  bool pv_v6 = false, pv_chk = false;
+  uint4 pv_s0 = make_uint4(0u, 0u, 0u, 0u), pv_s1 = pv_s0;
+  auto finish_prev = [&]() {
+    const bool ok = pv_chk && eq16(pv_s0, make_uint4(pv_addr[0], pv_addr[1], pv_addr[2], pv_addr[3])) &&
+                    eq16(pv_s1, make_uint4(pv_addr[4], pv_addr[5], pv_addr[6], pv_addr[7]));
+    if (pv_i != kNoRun) a.res[pv_i] = pv_v6 ? (pv_word | (ok ? 0x80000000u : 0u)) : 0u;
+  };
   for (uint32_t base = blockIdx.x * 256u; base < a.n; base += stride) {   // block-uniform trips
     const uint32_t i = base + threadIdx.x;
     const bool valid = i < a.n;
@@ -993,13 +1015,14 @@ __global__ __launch_bounds__(256, NFDP_V6_WAVES_PER_EU) void v6_kernel(V6Args a)
       imn = __builtin_amdgcn_raw_buffer_load_b32(r_im, nx < a.n ? nx * 4u : kNoRun, 0, 0);
     }
     const bool v6 = valid && p.ipv6;
-    uint32_t word = 0;
-    if (__any(v6)) {   // wave-uniform: EXEC full from here (MFMA, cross-lane reads, the wave probe)
-      const bool probe = v6 && !st.reason && a.t.flow6_on;
-      uint32_t h = 0;
-      uint4 bv[8];
+    const bool any6 = __any(v6);
+    const bool probe = v6 && !st.reason && a.t.flow6_on;
+    uint32_t h = 0;
+    uint4 bv[8];
+    int rule = -1;
+    if (any6) {   // wave-uniform: EXEC full from here (MFMA, cross-lane reads, the wave probe)
       auto issue = [&]() {
-        if (!a.t.flow6_on) return;
+        if (!a.t.flow6_on || NFDP_V6_ABL == 2) return;
         // the folded key's Toeplitz hash, then the first-choice bucket lines (flow_probe_issue's
         // wave-cooperative layout: lane 8j + q... loads line part c of packet 8j + q's bucket)
         if (a.toep_tab) {
@@ -1020,8 +1043,11 @@ __global__ __launch_bounds__(256, NFDP_V6_WAVES_PER_EU) void v6_kernel(V6Args a)
         }
       };
       if (NFDP_V6_EARLY_PROBE) issue();
-      int rule = -1;
+#if NFDP_V6_ABL == 1   // cost attribution only (wrong results): no ACL
+      if (false) {
+#else
       if (a.tiles) {
+#endif
 #pragma unroll
         for (int w = 0; w < 12; ++w) row[lane * 13 + w] = key6_word(p, st.bridge, w);
         __builtin_amdgcn_wave_barrier();
@@ -1067,17 +1093,26 @@ __global__ __launch_bounds__(256, NFDP_V6_WAVES_PER_EU) void v6_kernel(V6Args a)
         __builtin_amdgcn_wave_barrier();
       }
       if (!NFDP_V6_EARLY_PROBE) issue();
-      bool ok = false;
-      if (a.t.flow6_on) {
-        uint4 act;
-        const int64_t slot = flow_probe_finish(a.t, st.key, h, probe, kx, bv, act);
-        ok = slot >= 0 && flow6_verify(a.t, p, slot);
-      }
-      word = (uint32_t)(rule + 1) | (ok ? 0x80000000u : 0u);
     }
-    if (valid) a.res[i] = v6 ? word : 0u;
-    if (v6) a.keys[(size_t)i * 4] = make_uint4(st.key.src_ip, st.key.dst_ip, st.key.ports, st.key.meta);   // slot i
+    finish_prev();   // the previous run's side entries arrived under this run's ACL
+    int64_t slot = -1;
+    if (any6 && a.t.flow6_on && NFDP_V6_ABL != 2) {   // (2: cost attribution only, no flow check)
+      uint4 act;
+      slot = flow_probe_finish(a.t, st.key, h, probe, kx, bv, act);
+    }
+    // this run's check: the hit slot's side entry (flow6_side) leaves now, compared next iteration
+    pv_chk = v6 && slot >= 0;
+    const uint4* se = reinterpret_cast<const uint4*>(flow6_side(a.t, pv_chk ? slot : 0));
+    pv_s0 = pv_chk ? se[0] : make_uint4(0u, 0u, 0u, 0u);
+    pv_s1 = pv_chk ? se[1] : make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) pv_addr[k] = raw32_at2(p.s, 22 + 4 * k);
+    pv_i = valid ? i : kNoRun;
+    pv_v6 = v6;
+    pv_word = (uint32_t)(rule + 1);
+    if (v6) a.keys[(size_t)i * a.key_stride] = make_uint4(st.key.src_ip, st.key.dst_ip, st.key.ports, st.key.meta);
   }
+  finish_prev();
 }
 
 // ---- SFC hop pipeline across GPUs (split chains, kHopXfer) ----
@@ -1239,7 +1274,7 @@ static hipError_t launch_v6(const FusedLaunch& f, int num_cus, hipStream_t s) {
     return hipErrorInvalidValue;
   V6Args a{f.t, reinterpret_cast<const uint4*>(f.pkts), f.inmeta, f.n, reinterpret_cast<const v4i*>(f.acl6_wfrag),
            reinterpret_cast<const v4i*>(f.acl6_cinit), f.t.n_acl6 ? f.acl6_tiles : 0u, f.toep_tab, f.out_meta,
-           reinterpret_cast<uint4*>(f.out)};
+           reinterpret_cast<uint4*>(f.v6_keys ? f.v6_keys : f.out), f.v6_keys ? 1u : 4u};
   // one workgroup per SIMD-resident slot (NFDP_V6_WAVES_PER_EU 4-wave blocks per CU): every block
   // runs the same number of grid-stride trips, no second round of blocks behind the first
   uint32_t grid = (f.n + 255) / 256;
@@ -1341,6 +1376,8 @@ static FusedArgs make_fused_args(const FusedLaunch& f) {
   a.steer_cnt = f.steer_cnt;
   a.steer_cap_blk = f.steer_cap;
   a.hop_state = f.hop_state;
+  a.v6_key = reinterpret_cast<const uint4*>(f.v6_keys ? f.v6_keys : f.out);
+  a.v6_key_stride = f.v6_keys ? 1u : 4u;
   return a;
 }
 

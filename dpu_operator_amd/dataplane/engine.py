@@ -726,6 +726,9 @@ class DataPlane:
             # split chains (a hop placed on another GPU): the XFER instances leave each handed-off
             # frame's HopState record here (MultiDataPlane / parallel.hops resume them there)
             hop = torch.empty((n, 8), dtype=torch.int32, device=self.tdev) if self.chains.split() else None
+            # IPv6 tables: v6_kernel's folded keys, one 16-B row per slot for the fused V6 instances
+            # (parked in the out slots instead, the V6 instance's key read touches 4x the lines)
+            k6 = torch.empty((n, 4), dtype=torch.int32, device=self.tdev) if (tp.get("n_acl6") or tp.get("flow6_on")) else None
             # one launch covers < 2^25 slots (32-bit buffer views); bigger batches are split
             for lo in range(0, n, self.MAX_LAUNCH):
                 m = min(self.MAX_LAUNCH, n - lo)
@@ -739,6 +742,7 @@ class DataPlane:
                     self._ptr("toep_frag"), self._ptr("toep_tab"),
                     self.hash_mode, self.acl_mode, self.num_cus, s, flags, side,
                     hop_state=hop.data_ptr() + 32 * lo if hop is not None else 0,
+                    v6_keys=k6.data_ptr() + 16 * lo if k6 is not None else 0,
                 )
             if pairs:   # continuation slots: kCont metas carrying their pair's strip / valid bytes
                 self.nf.launch_pair_fix(inmeta.data_ptr(), meta.data_ptr(), n, self._ptr("drop_ctr"), not (flags & 1), s)
