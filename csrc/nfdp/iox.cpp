@@ -1013,8 +1013,14 @@ void Engine::learner_loop() {
   }
 }
 
+#ifndef NFDP_IOX_YIELD_MASK
+#define NFDP_IOX_YIELD_MASK 0xFFFFu
+#endif
+constexpr uint32_t kYieldMask = NFDP_IOX_YIELD_MASK;   // idle polls between yields of a spinning thread
+
 void Engine::rx_loop(Queue* Q) {
   std::vector<RxRef> buf(burst_);
+  uint32_t idle_polls = 0;
   uint32_t rr = 0;
   std::shared_ptr<const PortTab> cached;
   uint64_t cached_ver = ~0ull;
@@ -1229,6 +1235,7 @@ void Engine::rx_loop(Queue* Q) {
       if (got == 0 && pubs == 0) {
         st.add(take ? st.idle : st.wait_tx, 1);
         _mm_pause();
+        if ((++idle_polls & kYieldMask) == 0) std::this_thread::yield();
       }
     }
     release_all();
@@ -1513,7 +1520,7 @@ void Engine::tx_loop(Queue* Q, uint32_t w) {
       }
       _mm_pause();
       if ((++idle & 0x3FFu) == 0) (void)ports_of(psnap);   // idle: let go of a replaced port table too
-      if ((idle & 0xFFFFu) == 0) std::this_thread::yield();
+      if ((idle & kYieldMask) == 0) std::this_thread::yield();
     }
   } catch (const std::exception& e) {
     fail(std::string("tx: ") + e.what());

@@ -322,10 +322,15 @@ def run_veth(mode: str = "linux-bridge", n_pods: int = 4, duration: float = 1.0,
                    p50_us=_pct(r["lat_us"], 50), p99_us=_pct(r["lat_us"], 99), bad=int(r["bad"]))
         time.sleep(0.1)
         for tag_, frac in (("load90", 0.9), ("half", 0.5)):
+            if eng is not None:
+                eng.take_latency_us()
             r2 = nf.trafgen_run_netns(pods, duration_s=min(duration, 0.5), warmup_s=0.1, threads=threads, burst=8,
                                       rate_pps=frac * mpps * 1e6)
             out.update({f"{tag_}_mpps": round(r2["received"] / min(duration, 0.5) / 1e6, 3),
                         f"{tag_}_p50_us": _pct(r2["lat_us"], 50), f"{tag_}_p99_us": _pct(r2["lat_us"], 99)})
+            if eng is not None:   # the engine's own share: rx read -> burst delivered
+                el = np.asarray(eng.take_latency_us())
+                out.update({f"{tag_}_engine_p50_us": _pct(el, 50), f"{tag_}_engine_p99_us": _pct(el, 99)})
             time.sleep(0.1)
         # unloaded: a slow trickle (1 kpps): no queueing anywhere
         r3 = nf.trafgen_run_netns(pods, duration_s=min(duration, 0.5), warmup_s=0.05, threads=1, burst=1,
