@@ -170,7 +170,8 @@ constexpr int kStreamAux = 2;        // nt: frames are read once / written once 
 // XFER: the instances for tables with split chains (kHopXfer hops): a frame handed to another GPU
 // leaves its HopState record in a.hop_state (two fixed-count stores in the tail, like the others).
 #ifndef NFDP_V6_PREFETCH
-#define NFDP_V6_PREFETCH 0   // 1: the V6 instances prefetch the next slot like the IPv4 ones (A/B)
+#define NFDP_V6_PREFETCH 0   // 1: the V6 instances prefetch the next slot like the IPv4 ones, 2: after
+                             // the flow probe (A/B)
 #endif
 #ifndef NFDP_XFER_WAVES_PER_EU
 #define NFDP_XFER_WAVES_PER_EU 4   // the split-chain instances (r5 s9: 346 us / 4M frames with 30 spilled
@@ -349,7 +350,7 @@ void fused_kernel(FusedArgs a) {
       // here, the same append cost the instance 15 more spilled VGPRs)
       if (valid && !st.reason && flowp && owner_of(hash, a.nranks) != a.rank) st.reason = kRemote;
     }
-    if constexpr (!REMOTE && (!V6 || NFDP_V6_PREFETCH)) {
+    if constexpr (!REMOTE && (!V6 || NFDP_V6_PREFETCH == 1)) {
       // prefetch the next slot now: it lands under this slot's probe and chain
       const uint32_t nx = i + stride;
       wave_frames_load<kStreamAux>(r_pk, run_of(base + stride), cn);
@@ -377,6 +378,11 @@ void fused_kernel(FusedArgs a) {
         act.chain_id = v.x & 0xFFFFu; act.out_port = v.x >> 16; act.nat_ip = v.y;
         act.nat_port = v.z & 0xFFFFu; act.vlan = v.z >> 16; act.flow_id = v.w;
       }
+    }
+    if constexpr (V6 && NFDP_V6_PREFETCH == 2) {   // the next slot under this one's chain, emit and tail
+      const uint32_t nx = i + stride;
+      wave_frames_load<kStreamAux>(r_pk, run_of(base + stride), cn);
+      imn = __builtin_amdgcn_raw_buffer_load_b32(r_im, nx < n ? nx * 4u : kNoRun, 0, kStreamAux);
     }
 #ifndef NFDP_ABL_NO_CHAIN
     const EgressDecision e = chain_stage<LdsTables, V6, XFER>(TV, ta_it, p, st, hit, act, acl_rule, hash);
@@ -494,7 +500,7 @@ void fused_kernel(FusedArgs a) {
         store_b128<kStreamAux>(h0, r_hop, off, 0);
         store_b128<kStreamAux>(h1, r_hop, off, 16);
       }
-      if constexpr (V6 && !NFDP_V6_PREFETCH) {   // (no prefetch: the next slot is loaded here)
+      if constexpr (V6 && NFDP_V6_PREFETCH == 0) {   // (no prefetch: the next slot is loaded here)
         const uint32_t nx = i + stride;
         wave_frames_load<kStreamAux>(r_pk, run_of(base + stride), cn);
         imn = __builtin_amdgcn_raw_buffer_load_b32(r_im, nx < n ? nx * 4u : kNoRun, 0, kStreamAux);
