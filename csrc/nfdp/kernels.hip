@@ -1161,7 +1161,20 @@ __global__ __launch_bounds__(256) void hop_pack_kernel(const uint4* out, const u
       const uint32_t i = w0 + k + lane;
       const bool my = mine(i);
       const unsigned long long bm = __ballot(my);
-      if (my) {
+      if (bm == ~0ull && pos0 + 64u <= dst.cap) {
+        // a whole run handed to this plane (a chain split for all its traffic: the common case):
+        // contiguous 4-KiB header / 2-KiB record copies, lane-contiguous 16-B chunks, instead of
+        // one 64-B slot per lane (every load and store instruction striding over 64 slots)
+        const uint4* sh = out + (size_t)(w0 + k) * 4;
+        uint4* dh = dst.hdr + (size_t)pos0 * 4;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) dh[q * 64 + lane] = sh[q * 64 + lane];
+        const uint4* ss = reinterpret_cast<const uint4*>(state + (w0 + k));
+        uint4* ds = reinterpret_cast<uint4*>(dst.state + pos0);
+#pragma unroll
+        for (int q = 0; q < 2; ++q) ds[q * 64 + lane] = ss[q * 64 + lane];
+        dst.idx[pos0 + lane] = i;
+      } else if (my) {
         const uint32_t pos = pos0 + __builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
         if (pos < dst.cap) {
 #pragma unroll
