@@ -1231,29 +1231,37 @@ struct ResumeArgs {
 __global__ __launch_bounds__(256) void resume_kernel(ResumeArgs a) {
   __shared__ uint32_t pc[2 * kLdsPorts];   // tx packets, tx bytes
   __shared__ uint32_t drops[kNumReasons];
+  __shared__ uint4 kxs[4][64];   // per wave: the slot-run transposition (device.h wave_frames_*)
   for (uint32_t q = threadIdx.x; q < 2 * kLdsPorts; q += 256) pc[q] = 0;
   if (threadIdx.x < kNumReasons) drops[threadIdx.x] = 0;
   __syncthreads();
   const uint32_t n = min(*a.in.count, a.in.cap);
   const DirectTables ta{a.t};
   const bool count = !(a.flags & 1u);
-  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) {
+  // header slots in and out as coalesced 4-KiB runs per wave (one slot per lane strides every load
+  // and store instruction over 64 slots); block-uniform trips, EXEC full at the transpositions
+  uint4* kx = kxs[threadIdx.x >> 6];
+  const uint32_t wave0 = __builtin_amdgcn_readfirstlane(threadIdx.x) & ~63u;
+  const __amdgpu_buffer_rsrc_t r_in = __builtin_amdgcn_make_buffer_rsrc((void*)a.in.hdr, (short)0, (int)(n * 64u), kBufCfg);
+  const __amdgpu_buffer_rsrc_t r_out = __builtin_amdgcn_make_buffer_rsrc((void*)a.out, (short)0, (int)(n * 64u), kBufCfg);
+  for (uint32_t base = blockIdx.x * 256u; base < n; base += gridDim.x * 256u) {
+    const uint32_t i = base + threadIdx.x;
+    const uint32_t run = base + wave0 < n ? (base + wave0) * 64u : kNoRun;
     uint32_t d[kSlotDwords];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const uint4 v = a.in.hdr[(size_t)i * 4 + k];
-      d[4 * k] = v.x; d[4 * k + 1] = v.y; d[4 * k + 2] = v.z; d[4 * k + 3] = v.w;
+    {
+      v4u cn[4];
+      wave_frames_load<kStreamAux>(r_in, run, cn);
+      wave_frames_to_lanes(kx, cn, d);
     }
+    uint32_t o[kSlotDwords] = {};
+    if (i < n) {
     const HopState hs = a.in.state[i];
     Parsed p;
     IngressState st;
     resume_ingress(ta, d, hs.inmeta, p, st);
     const EgressDecision e = resume_stage(a.t, ta, p, st, hs.act, hs.acl_rule, hs.hash, hs.hop);
-    uint32_t o[kSlotDwords];
     emit(p, e.tci, e.push != 0, o);
     const uint32_t olen = out_len(p, e);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) a.out[(size_t)i * 4 + k] = make_uint4(o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]);
     a.out_meta[i] = make_meta(e.out_port, olen, e.reason, !e.reason && e.xhdr, false);
     if (a.out_state && e.reason == kRemote && e.inner_len) a.out_state[i] = hop_state_of(p, st, e, hs.act, hs.acl_rule, hs.hash);
     if (count) {
@@ -1265,6 +1273,8 @@ __global__ __launch_bounds__(256) void resume_kernel(ResumeArgs a) {
         atomicAdd(a.port_ctr + 2 * e.out_port + 1, ctr_inc(olen));
       }
     }
+    }
+    wave_frames_store<kStreamAux>(kx, o, r_out, run);   // (lanes past n: dropped by the buffer bounds)
   }
   __syncthreads();
   for (uint32_t q = threadIdx.x; q < kLdsPorts; q += 256)
@@ -1277,6 +1287,7 @@ hipError_t launch_resume(const TablesView& t, const HopInbox& in, void* out, uin
                          unsigned long long* port_ctr, unsigned long long* drop_ctr, uint32_t flags, int num_cus,
                          hipStream_t s) {
   if (!in.count || !in.hdr || !in.state || !out || !out_meta || !port_ctr || !drop_ctr) return hipErrorInvalidValue;
+  if (in.cap >= (1u << 25)) return hipErrorInvalidValue;   // (32-bit buffer views of the slot runs)
   uint32_t grid = (in.cap + 255) / 256;
   const uint32_t lim = (uint32_t)(num_cus > 0 ? num_cus : 256) * 8u;
   if (grid > lim) grid = lim;
