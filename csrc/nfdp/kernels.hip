@@ -776,20 +776,28 @@ __global__ __launch_bounds__(256) void side_kernel(SideArgs a) {
 __global__ __launch_bounds__(256) void gather_kernel(const uint8_t* recv, uint32_t nranks, uint32_t rank, uint32_t cap,
                                                      uint32_t seg_bytes, uint32_t meta_off, uint4* pkts, uint32_t* inmeta,
                                                      uint32_t* n_dev) {
-  const uint32_t total = nranks * cap;
-  for (uint32_t idx = blockIdx.x * 256 + threadIdx.x; idx < total; idx += gridDim.x * 256) {
-    const uint32_t s = idx / cap, j = idx % cap;
-    if (s == rank) continue;
-    const uint32_t* hdr = reinterpret_cast<const uint32_t*>(recv + (size_t)s * seg_bytes);
-    const uint32_t c = min(hdr[0], cap);
-    if (j >= c) continue;
-    uint32_t base = 0;
-    for (uint32_t q = 0; q < s; ++q)
-      if (q != rank) base += min(reinterpret_cast<const uint32_t*>(recv + (size_t)q * seg_bytes)[0], cap);
-    const uint4* src = reinterpret_cast<const uint4*>(recv + (size_t)s * seg_bytes + 64 + (size_t)j * 64);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) pkts[(size_t)(base + j) * 4 + k] = src[k];
-    inmeta[base + j] = reinterpret_cast<const uint32_t*>(recv + (size_t)s * seg_bytes + meta_off)[j];
+  // each segment's slots land as one contiguous run of the batch: copied as a flat array of 16-B
+  // chunks (consecutive lanes, consecutive chunks), not one 64-B slot per lane
+  __shared__ uint32_t sbase[kMaxRanks], scnt[kMaxRanks];
+  if (threadIdx.x == 0) {
+    uint32_t b = 0;
+    for (uint32_t q = 0; q < nranks; ++q) {
+      const uint32_t c = q == rank ? 0u : min(reinterpret_cast<const uint32_t*>(recv + (size_t)q * seg_bytes)[0], cap);
+      sbase[q] = b; scnt[q] = c; b += c;
+    }
+  }
+  __syncthreads();
+  const uint32_t cap4 = cap * 4u, total4 = nranks * cap4;   // (< 2^32: checked at launch)
+  for (uint32_t idx = blockIdx.x * 256 + threadIdx.x; idx < total4; idx += gridDim.x * 256) {
+    const uint32_t s = idx / cap4, u = idx - s * cap4;
+    if ((u >> 2) >= scnt[s]) continue;   // (the own segment has count 0)
+    const uint4* src = reinterpret_cast<const uint4*>(recv + (size_t)s * seg_bytes + 64);
+    pkts[(size_t)sbase[s] * 4 + u] = src[u];
+  }
+  for (uint32_t idx = blockIdx.x * 256 + threadIdx.x; idx < nranks * cap; idx += gridDim.x * 256) {
+    const uint32_t s = idx / cap, j = idx - s * cap;
+    if (j >= scnt[s]) continue;
+    inmeta[sbase[s] + j] = reinterpret_cast<const uint32_t*>(recv + (size_t)s * seg_bytes + meta_off)[j];
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     uint32_t t = 0;
@@ -809,6 +817,8 @@ __global__ __launch_bounds__(256) void steer_kernel(const uint4* pkts, const uin
                                                     uint8_t* send, uint32_t* pcnt, uint32_t nranks, uint32_t cap,
                                                     uint32_t seg_bytes, uint32_t meta_off) {
   __shared__ uint32_t oc[kMaxRanks], ob[kMaxRanks];
+  __shared__ uint32_t ssrc[256];            // the pass's entries: source slot (~0: none) ...
+  __shared__ unsigned long long sdst[256];  // ... and the byte offset of its destination slot
   const uint32_t G = min(list_cnt[0], max_blk), capb = list_cnt[1];
   if ((unsigned long long)G * capb > cap_list) return;   // a header this launch did not write
   for (uint32_t b = blockIdx.x; b < G; b += gridDim.x) {
@@ -824,17 +834,26 @@ __global__ __launch_bounds__(256) void steer_kernel(const uint4* pkts, const uin
       __syncthreads();
       if (threadIdx.x < nranks && oc[threadIdx.x]) ob[threadIdx.x] = atomicAdd(&pcnt[threadIdx.x], oc[threadIdx.x]);
       __syncthreads();
+      ssrc[threadIdx.x] = 0xFFFFFFFFu;
       if (ok) {
         const uint32_t pos = ob[o] + local;
         if (pos < cap) {   // cannot fail with cap = batch (kept as a guard)
           uint8_t* seg = send + (size_t)o * seg_bytes;
-          uint4* dst = reinterpret_cast<uint4*>(seg + 64 + (size_t)pos * 64);
-#pragma unroll
-          for (int k = 0; k < 4; ++k) dst[k] = pkts[(size_t)i * 4 + k];
+          ssrc[threadIdx.x] = i;
+          sdst[threadIdx.x] = (unsigned long long)o * seg_bytes + 64ull + (unsigned long long)pos * 64ull;
           reinterpret_cast<uint32_t*>(seg + meta_off)[pos] = inmeta[i];
         }
       }
-      __syncthreads();   // ob / oc are reused by the next 256 entries
+      __syncthreads();
+      // the slots: four lanes per slot (one 16-B chunk each), so an instruction moves 16 whole
+      // 64-B slots instead of 64 scattered 16-B pieces
+#pragma unroll
+      for (uint32_t r = 0; r < 4; ++r) {
+        const uint32_t q = r * 256u + threadIdx.x, e = q >> 2, k = q & 3u;
+        if (ssrc[e] != 0xFFFFFFFFu)
+          reinterpret_cast<uint4*>(send + sdst[e])[k] = pkts[(size_t)ssrc[e] * 4 + k];
+      }
+      __syncthreads();   // ob / oc / the stash are reused by the next 256 entries
     }
   }
 }
@@ -1493,7 +1512,8 @@ static hipError_t launch_fused_body(const FusedLaunch& f, const LaunchCfg& cfg, 
 hipError_t launch_gather(const uint8_t* recv, uint32_t nranks, uint32_t rank, uint32_t cap, uint32_t seg_bytes,
                          uint32_t meta_off, void* pkts, uint32_t* inmeta, uint32_t* n_dev, hipStream_t s) {
   if (!recv || !pkts || !inmeta || !n_dev || rank >= nranks || nranks > kMaxRanks) return hipErrorInvalidValue;
-  const uint32_t total = nranks * cap;
+  if ((uint64_t)nranks * cap * 4u >= (1ull << 32)) return hipErrorInvalidValue;
+  const uint32_t total = nranks * cap * 4u;
   uint32_t grid = (total + 255) / 256;
   if (grid > 1024) grid = 1024;
   if (grid == 0) grid = 1;
