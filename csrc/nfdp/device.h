@@ -736,11 +736,14 @@ struct GpuSideSink {
     if (r) atomicAdd(drop_ctr + r, 1ull);
     else if (port < (uint32_t)kMaxPorts) atomicAdd(port_ctr + 2 * port + 1, ctr_inc(meta_len(meta)));
   }
-  __device__ __forceinline__ void xhdr(const uint32_t* hdr, uint32_t src) {
+  // `nq`: the 16-B chunks the outer header occupies (consumers take its length from its EtherType,
+  // iox.cpp / packets.py xhdr_len); the rest of the 128-B record is not written
+  __device__ __forceinline__ void xhdr(const uint32_t* hdr, uint32_t src, uint32_t nq) {
     if (!so.xhdr) return;
     uint4* dst = reinterpret_cast<uint4*>(so.xhdr) + (size_t)src * (kXhdrBytes / 16);
 #pragma unroll
-    for (int q = 0; q < kXhdrBytes / 16; ++q) dst[q] = make_uint4(hdr[4 * q], hdr[4 * q + 1], hdr[4 * q + 2], hdr[4 * q + 3]);
+    for (int q = 0; q < kXhdrBytes / 16; ++q)
+      if ((uint32_t)q < nq) dst[q] = make_uint4(hdr[4 * q], hdr[4 * q + 1], hdr[4 * q + 2], hdr[4 * q + 3]);
   }
   __device__ __forceinline__ void learn(uint32_t bridge, uint32_t lo, uint32_t hi, uint32_t port) {
     const uint32_t pos = atomicAdd(so.cnt + 1, 1u);

@@ -338,7 +338,7 @@ struct CpuSideSink {
     if (r) { if (drop_ctr) drop_ctr[r] += 1; }
     else if (port < (uint32_t)kMaxPorts && port_ctr) port_ctr[2 * port + 1] += ctr_inc(meta_len(meta));
   }
-  void xhdr(const uint32_t* hdr, uint32_t src) {
+  void xhdr(const uint32_t* hdr, uint32_t src, uint32_t) {   // (the whole record: zero tail included)
     if (so.xhdr) std::memcpy(so.xhdr + (size_t)src * (kXhdrBytes / 4), hdr, kXhdrBytes);
   }
   void learn(uint32_t bridge, uint32_t lo, uint32_t hi, uint32_t port) {

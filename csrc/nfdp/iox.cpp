@@ -1265,7 +1265,7 @@ struct BurstSink {
     std::memcpy(xbuf.data() + (size_t)i * kXhdrBytes, x, kXhdrBytes);
     has_x[i] = 1;
   }
-  void xhdr(const uint32_t* x, uint32_t) { xhdr_rec(x); }
+  void xhdr(const uint32_t* x, uint32_t, uint32_t) { xhdr_rec(x); }
   void learn(uint32_t bridge, uint32_t lo, uint32_t hi, uint32_t port) {
     const uint32_t e1 = (hi & 0xFFFFu) | (bridge << 16);
     const size_t n = learn_ev.size();

@@ -736,13 +736,15 @@ __global__ __launch_bounds__(256) void side_kernel(SideArgs a) {
       if (j - r * a.side.blk_cap >= a.side.blk_cnt[r]) continue;
     }
     const uint32_t i = a.side.list[j];
-    uint32_t d[kSlotDwords], o[kSlotDwords];
+    uint32_t d[kSlotDwords];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const uint4 v = a.pkts[(size_t)i * 4 + q], w = a.out[(size_t)i * 4 + q];
+      const uint4 v = a.pkts[(size_t)i * 4 + q];
       d[4 * q] = v.x; d[4 * q + 1] = v.y; d[4 * q + 2] = v.z; d[4 * q + 3] = v.w;
-      o[4 * q] = w.x; o[4 * q + 1] = w.y; o[4 * q + 2] = w.z; o[4 * q + 3] = w.w;
     }
+    // the egress slot is read only where a replica copies it (mirroring): in place, not loaded for
+    // every listed packet (an overlay egress lists all of them for their outer headers)
+    const uint32_t* o = reinterpret_cast<const uint32_t*>(a.out + (size_t)i * 4);
     // a terminated pair head: its side work is on the inner frame (the same decap_pair decision
     // the pair pass / ring kernel took; a batch's pair pass already rewrote it: then decap_pair
     // sees an ordinary frame and returns -1)

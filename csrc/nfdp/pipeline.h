@@ -553,27 +553,32 @@ NFDP_HD uint32_t out_len(const Parsed& p, const EgressDecision& e) {
 // IPv4 with DF and its checksum, UDP with the entropy source port and checksum 0, VXLAN flags
 // 0x08 + VNI or GENEVE 0x6558 + VNI), as 16 LE dwords.
 NFDP_HD void make_outer(const TunnelEntry& te, uint32_t inner_len, uint32_t hash, uint32_t* x) {
-  uint8_t b[kSlotBytes];
-  for (int i = 0; i < kSlotBytes; ++i) b[i] = 0;
-  auto put32 = [&](int o, uint32_t raw) { b[o] = raw & 0xFF; b[o + 1] = (raw >> 8) & 0xFF; b[o + 2] = (raw >> 16) & 0xFF; b[o + 3] = raw >> 24; };
-  auto be16 = [&](int o, uint32_t v) { b[o] = (v >> 8) & 0xFF; b[o + 1] = v & 0xFF; };
-  put32(0, te.dmac_lo); b[4] = te.dmac_hi & 0xFF; b[5] = te.dmac_hi >> 8;
-  put32(6, te.smac_lo); b[10] = te.smac_hi & 0xFF; b[11] = te.smac_hi >> 8;
-  be16(12, 0x0800);
-  b[14] = 0x45; be16(16, 20 + 8 + 8 + inner_len); be16(20, 0x4000); b[22] = 64; b[23] = 17;
-  put32(26, te.src_ip); put32(30, te.dst_ip);
-  if (te.sport) { b[34] = te.sport & 0xFF; b[35] = te.sport >> 8; } else { be16(34, 0xC000u | (hash & 0x3FFFu)); }
-  b[36] = te.dport & 0xFF; b[37] = te.dport >> 8;
-  be16(38, 8 + 8 + inner_len);
-  if (te.type == kTunGeneve) { be16(44, 0x6558); } else { b[42] = 0x08; }
-  b[46] = (te.vni >> 16) & 0xFF; b[47] = (te.vni >> 8) & 0xFF; b[48] = te.vni & 0xFF;
-  uint32_t c = 0;
-  for (int o = 14; o < 34; o += 2) c += ((uint32_t)b[o] << 8) | b[o + 1];
+  // built as dwords (a byte array here went to scratch memory on the GPU: ~30 private loads and
+  // stores per packet in the side pass, r5 s32)
+  auto bs16 = [](uint32_t v) { return ((v >> 8) & 0xFFu) | ((v & 0xFFu) << 8); };   // 16-bit byte swap
+  const uint32_t tl = 20u + 8u + 8u + inner_len, ul = 8u + 8u + inner_len;
+  const uint32_t sp = te.sport ? (uint32_t)te.sport : bs16(0xC000u | (hash & 0x3FFFu));   // raw (wire order)
+  // IPv4 header checksum over the 16-bit big-endian words of bytes 14..33 (its own field 0)
+  uint32_t c = 0x4500u + (tl & 0xFFFFu) + 0x4000u + 0x4011u + bs16(te.src_ip & 0xFFFFu) + bs16(te.src_ip >> 16) +
+               bs16(te.dst_ip & 0xFFFFu) + bs16(te.dst_ip >> 16);
   c = (c & 0xFFFFu) + (c >> 16);
   c = (c & 0xFFFFu) + (c >> 16);
-  be16(24, ~c & 0xFFFFu);
-  for (int i = 0; i < kSlotDwords; ++i)
-    x[i] = (uint32_t)b[4 * i] | ((uint32_t)b[4 * i + 1] << 8) | ((uint32_t)b[4 * i + 2] << 16) | ((uint32_t)b[4 * i + 3] << 24);
+  const uint32_t ck = bs16(~c & 0xFFFFu);
+  const bool gen = te.type == kTunGeneve;
+  x[0] = te.dmac_lo;
+  x[1] = (uint32_t)te.dmac_hi | (te.smac_lo << 16);
+  x[2] = (te.smac_lo >> 16) | ((uint32_t)te.smac_hi << 16);
+  x[3] = 0x00450008u;                                   // EtherType 0x0800, version / IHL 0x45, TOS 0
+  x[4] = bs16(tl & 0xFFFFu);                            // total length, id 0
+  x[5] = 0x11400040u;                                   // DF, TTL 64, protocol UDP
+  x[6] = ck | ((te.src_ip & 0xFFFFu) << 16);
+  x[7] = (te.src_ip >> 16) | ((te.dst_ip & 0xFFFFu) << 16);
+  x[8] = (te.dst_ip >> 16) | (sp << 16);
+  x[9] = (uint32_t)te.dport | (bs16(ul & 0xFFFFu) << 16);
+  x[10] = gen ? 0u : 0x00080000u;                       // UDP checksum 0; VXLAN flags 0x08
+  x[11] = (gen ? 0x5865u : 0u) | (((te.vni >> 16) & 0xFFu) << 16) | (((te.vni >> 8) & 0xFFu) << 24);   // GENEVE 0x6558
+  x[12] = te.vni & 0xFFu;
+  for (int i = 13; i < kSlotDwords; ++i) x[i] = 0u;
 }
 
 // IPv6-underlay outer headers (70 B: Ethernet, IPv6 with next header UDP, UDP with the entropy
@@ -581,25 +586,29 @@ NFDP_HD void make_outer(const TunnelEntry& te, uint32_t inner_len, uint32_t hash
 // GENEVE + VNI).  The flow label is the entry's or, if 0, 20 bits of the packet hash (RFC 6438).
 // `x` holds kXhdrBytes / 4 LE dwords.
 NFDP_HD void make_outer6(const Tunnel6Entry& te, uint32_t inner_len, uint32_t hash, uint32_t* x) {
-  uint8_t b[kXhdrBytes];
-  for (int i = 0; i < kXhdrBytes; ++i) b[i] = 0;
-  auto put32 = [&](int o, uint32_t raw) { b[o] = raw & 0xFF; b[o + 1] = (raw >> 8) & 0xFF; b[o + 2] = (raw >> 16) & 0xFF; b[o + 3] = raw >> 24; };
-  auto be16 = [&](int o, uint32_t v) { b[o] = (v >> 8) & 0xFF; b[o + 1] = v & 0xFF; };
-  put32(0, te.dmac_lo); b[4] = te.dmac_hi & 0xFF; b[5] = te.dmac_hi >> 8;
-  put32(6, te.smac_lo); b[10] = te.smac_hi & 0xFF; b[11] = te.smac_hi >> 8;
-  be16(12, 0x86DD);
+  // built as dwords, like make_outer (no byte array: scratch memory on the GPU)
+  auto bs16 = [](uint32_t v) { return ((v >> 8) & 0xFFu) | ((v & 0xFFu) << 8); };
   const uint32_t fl = (te.tc_flow & 0xFFFFFu) ? (te.tc_flow & 0xFFFFFu) : (hash & 0xFFFFFu);
   const uint32_t vtf = (6u << 28) | (((te.tc_flow >> 20) & 0xFFu) << 20) | fl;
-  be16(14, vtf >> 16); be16(16, vtf & 0xFFFFu);
-  be16(18, 8 + 8 + inner_len); b[20] = 17; b[21] = (te.hop_limit & 0xFFu) ? (te.hop_limit & 0xFFu) : 64u;
-  for (int k = 0; k < 4; ++k) { put32(22 + 4 * k, te.src[k]); put32(38 + 4 * k, te.dst[k]); }
-  if (te.sport) { b[54] = te.sport & 0xFF; b[55] = te.sport >> 8; } else { be16(54, 0xC000u | (hash & 0x3FFFu)); }
-  b[56] = te.dport & 0xFF; b[57] = te.dport >> 8;
-  be16(58, 8 + 8 + inner_len);
-  if (te.type == kTunGeneve) { be16(64, 0x6558); } else { b[62] = 0x08; }
-  b[66] = (te.vni >> 16) & 0xFF; b[67] = (te.vni >> 8) & 0xFF; b[68] = te.vni & 0xFF;
-  for (int i = 0; i < kXhdrBytes / 4; ++i)
-    x[i] = (uint32_t)b[4 * i] | ((uint32_t)b[4 * i + 1] << 8) | ((uint32_t)b[4 * i + 2] << 16) | ((uint32_t)b[4 * i + 3] << 24);
+  const uint32_t ul = (8u + 8u + inner_len) & 0xFFFFu;
+  const uint32_t hl = (te.hop_limit & 0xFFu) ? (te.hop_limit & 0xFFu) : 64u;
+  const uint32_t sp = te.sport ? (uint32_t)te.sport : bs16(0xC000u | (hash & 0x3FFFu));
+  const bool gen = te.type == kTunGeneve;
+  x[0] = te.dmac_lo;
+  x[1] = (uint32_t)te.dmac_hi | (te.smac_lo << 16);
+  x[2] = (te.smac_lo >> 16) | ((uint32_t)te.smac_hi << 16);
+  x[3] = 0xDD86u | (bs16(vtf >> 16) << 16);             // EtherType 0x86DD, version / class / label
+  x[4] = bs16(vtf & 0xFFFFu) | (bs16(ul) << 16);        // payload length
+  x[5] = 17u | (hl << 8) | ((te.src[0] & 0xFFFFu) << 16);
+  for (int k = 0; k < 3; ++k) x[6 + k] = (te.src[k] >> 16) | ((te.src[k + 1] & 0xFFFFu) << 16);
+  x[9] = (te.src[3] >> 16) | ((te.dst[0] & 0xFFFFu) << 16);
+  for (int k = 0; k < 3; ++k) x[10 + k] = (te.dst[k] >> 16) | ((te.dst[k + 1] & 0xFFFFu) << 16);
+  x[13] = (te.dst[3] >> 16) | (sp << 16);
+  x[14] = (uint32_t)te.dport | (bs16(ul) << 16);
+  x[15] = gen ? 0u : 0x00080000u;                       // UDP checksum 0 (RFC 6935); VXLAN flags 0x08
+  x[16] = (gen ? 0x5865u : 0u) | (((te.vni >> 16) & 0xFFu) << 16) | (((te.vni >> 8) & 0xFFu) << 24);
+  x[17] = te.vni & 0xFFu;
+  for (int i = 18; i < kXhdrBytes / 4; ++i) x[i] = 0u;
 }
 
 // Side outputs: flood replicas, the K9 mirror copy, the ARP slow-path copy and MAC-learn events.
@@ -651,12 +660,12 @@ NFDP_HD void side_stage(const TablesView& t, const TA& ta, const uint32_t* d_in,
       if ((pe.flags & kPortTunnel) && (pe.flags & kPortTunnel6)) {
         if (t.tunnels6 && pe.lag < t.n_tunnels6) {
           make_outer6(t.tunnels6[pe.lag], meta_len(ometa) - kEncap6Bytes, khash(), x);
-          sink.xhdr(x, src);
+          sink.xhdr(x, src, (kEncap6Bytes + 15) / 16);
         }
       } else if ((pe.flags & kPortTunnel) && t.tunnels && pe.lag < t.n_tunnels) {
         for (int i = kSlotDwords; i < kXhdrBytes / 4; ++i) x[i] = 0;
         make_outer(t.tunnels[pe.lag], meta_len(ometa) - kEncapBytes, khash(), x);
-        sink.xhdr(x, src);
+        sink.xhdr(x, src, (kEncapBytes + 15) / 16);
       }
     }
   }
