@@ -994,6 +994,9 @@ __global__ __launch_bounds__(256, NFDP_V6_WAVES_PER_EU) void v6_kernel(V6Args a)
   __shared__ uint32_t ltab[16 * 256];
   __shared__ v4i lwf[kV6LdsTiles * 3 * 64];
   __shared__ v4i lci[kV6LdsTiles * 4];
+  // the small tables (ports < kLdsPorts, chain words, verdicts) staged like the fused kernel's:
+  // the ingress port lookup is an LDS read, not a dependent global load per run
+  __shared__ __attribute__((aligned(16))) uint8_t ltabs[kLdsTabBytes];
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   const uint32_t g = lane >> 4, col = lane & 15u;
   uint32_t* row = kw[wv];
@@ -1003,6 +1006,9 @@ __global__ __launch_bounds__(256, NFDP_V6_WAVES_PER_EU) void v6_kernel(V6Args a)
   const uint32_t lt6 = a.tiles < kV6LdsTiles ? a.tiles : kV6LdsTiles;
   for (uint32_t q = threadIdx.x; q < lt6 * 3 * 64; q += 256) lwf[q] = a.wfrag[q];
   for (uint32_t q = threadIdx.x; q < lt6 * 4; q += 256) lci[q] = a.cinit[q];
+  const LdsTables ta = stage_lds_tables(a.t, reinterpret_cast<PortEntry*>(ltabs),
+                                        reinterpret_cast<uint64_t*>(ltabs + kLdsPorts * sizeof(PortEntry)),
+                                        ltabs + kLdsPorts * sizeof(PortEntry) + kLdsChains * 8, true, 256);
   __syncthreads();
   // coalesced frame loads (the wave's 64 slots = one 4-KiB run, device.h wave_frames_load)
   const __amdgpu_buffer_rsrc_t r_pk = __builtin_amdgcn_make_buffer_rsrc((void*)a.pkts, (short)0, (int)(a.n * 64u), kBufCfg);
@@ -1035,7 +1041,7 @@ __global__ __launch_bounds__(256, NFDP_V6_WAVES_PER_EU) void v6_kernel(V6Args a)
     wave_frames_to_lanes<true>(kx, cn, d);
     Parsed p;
     IngressState st;
-    ingress_stage(a.t, d, valid ? imn : 0u, p, st);
+    ingress_stage<LdsTables, true>(a.t, ta, d, valid ? imn : 0u, p, st);   // (with the IPv6 key fold)
     {   // the next run: lands under this one's classification
       const uint32_t nx = i + stride;
       wave_frames_load<0>(r_pk, run_of(base + stride), cn);
