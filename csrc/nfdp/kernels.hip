@@ -722,10 +722,17 @@ struct LdsToeplitz {
     return h;
   }
 };
-__global__ __launch_bounds__(256) void side_kernel(SideArgs a) {
+#ifndef NFDP_SIDE_WAVES_PER_EU
+#define NFDP_SIDE_WAVES_PER_EU 1
+#endif
+__global__ __launch_bounds__(256, NFDP_SIDE_WAVES_PER_EU) void side_kernel(SideArgs a) {
   __shared__ uint32_t stab[16 * 256];
+  __shared__ __attribute__((aligned(16))) uint8_t ltabs[kLdsTabBytes];   // ports / chain words / verdicts
   if (a.toep_tab)
     for (uint32_t q = threadIdx.x; q < 16 * 256; q += 256) stab[q] = a.toep_tab[q];
+  const LdsTables ta = stage_lds_tables(a.t, reinterpret_cast<PortEntry*>(ltabs),
+                                        reinterpret_cast<uint64_t*>(ltabs + kLdsPorts * sizeof(PortEntry)),
+                                        ltabs + kLdsPorts * sizeof(PortEntry) + kLdsChains * 8, true, 256);
   __syncthreads();
   // flat list [0, cnt[5]) or the fused kernel's per-workgroup regions (blk_cnt[b] entries each)
   const bool blk = a.side.blk_cnt != nullptr;
@@ -767,8 +774,8 @@ __global__ __launch_bounds__(256) void side_kernel(SideArgs a) {
       }
     }
     GpuSideSink sk{a.side, a.port_ctr, a.drop_ctr};
-    if (a.toep_tab) side_stage(a.t, DirectTables{a.t}, d, im, o, a.out_meta[i], i, sk, LdsToeplitz{stab});
-    else side_stage(a.t, DirectTables{a.t}, d, im, o, a.out_meta[i], i, sk);
+    if (a.toep_tab) side_stage(a.t, ta, d, im, o, a.out_meta[i], i, sk, LdsToeplitz{stab});
+    else side_stage(a.t, ta, d, im, o, a.out_meta[i], i, sk);
   }
 }
 
@@ -1259,11 +1266,14 @@ __global__ __launch_bounds__(256) void resume_kernel(ResumeArgs a) {
   __shared__ uint32_t pc[2 * kLdsPorts];   // tx packets, tx bytes
   __shared__ uint32_t drops[kNumReasons];
   __shared__ uint4 kxs[4][64];   // per wave: the slot-run transposition (device.h wave_frames_*)
+  __shared__ __attribute__((aligned(16))) uint8_t ltabs[kLdsTabBytes];   // ports / chain words / verdicts
   for (uint32_t q = threadIdx.x; q < 2 * kLdsPorts; q += 256) pc[q] = 0;
   if (threadIdx.x < kNumReasons) drops[threadIdx.x] = 0;
+  const LdsTables ta = stage_lds_tables(a.t, reinterpret_cast<PortEntry*>(ltabs),
+                                        reinterpret_cast<uint64_t*>(ltabs + kLdsPorts * sizeof(PortEntry)),
+                                        ltabs + kLdsPorts * sizeof(PortEntry) + kLdsChains * 8, true, 256);
   __syncthreads();
   const uint32_t n = min(*a.in.count, a.in.cap);
-  const DirectTables ta{a.t};
   const bool count = !(a.flags & 1u);
   // header slots in and out as coalesced 4-KiB runs per wave (one slot per lane strides every load
   // and store instruction over 64 slots); block-uniform trips, EXEC full at the transpositions
