@@ -97,6 +97,9 @@ NFDP_HD int acl_rule_of(uint32_t b, uint32_t n_acl) {
 // the 2-wave instance is bound by latency, not by its MFMA count.  Off.
 #define NFDP_ACL_PTILES 0
 #endif
+#ifndef NFDP_TILE_PF
+#define NFDP_TILE_PF 1   // 4-wave instances: per-tile prefilters inside a passing group (0: group only, A/B)
+#endif
 #ifndef NFDP_PIPE_UNROLL
 #define NFDP_PIPE_UNROLL 1   // r3 s16 A/B: ACL1024 0.3145 vs 0.3211 ms, ClassBench unchanged
 #endif
@@ -382,7 +385,7 @@ __device__ __forceinline__ void classify_wave(const FlowKey& key, uint4* kx, con
 #endif
         // this wave's first tile of the group (tiles == tile0 mod tstep)
         for (uint32_t nt = t_beg + (tile0 + tstep - t_beg % tstep) % tstep; nt < t_end; nt += tstep) {
-          if ((!PIPE || NFDP_PIPE_PF >= 2) && !pass(pf + 8 * nt)) continue;
+          if (((!PIPE && NFDP_TILE_PF) || (PIPE && NFDP_PIPE_PF >= 2)) && !pass(pf + 8 * nt)) continue;
           run_tile(av.lw[nt * 64 + lane], av.lc[nt * 4 + g]);
         }
       }
