@@ -1094,6 +1094,16 @@ PYBIND11_MODULE(_nfdp, m) {
         return out;
       }, py::arg("max") = 4096);
   // pod-side generator / sink (trafgen.h); pods: list of (path, frames [k, stride] u8, lens [k] u32)
+  m.def("cpu_share_probe", [](uint32_t threads, double seconds) {
+    if (threads < 1 || threads > 1024 || !(seconds > 0.0) || seconds > 10.0)
+      throw std::invalid_argument("cpu_share_probe: threads in [1, 1024], seconds in (0, 10]");
+    py::gil_scoped_release nogil;
+    const auto t0 = std::chrono::steady_clock::now();
+    const double cpu = trafgen::cpu_share_probe(threads, seconds);
+    const double wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    return std::make_pair(cpu, wall);
+  }, py::arg("threads"), py::arg("seconds") = 0.3,
+        "threads busy-loop together: (CPU seconds granted, wall seconds); their ratio = CPUs available");
   m.def("trafgen_run", [](py::list pods, double duration_s, double warmup_s, double rate_pps, uint32_t threads,
                           uint32_t burst, uint32_t inflight) {
     std::vector<trafgen::Pod> v;

@@ -480,7 +480,7 @@ void WireBackend::run_segment(uint32_t q, uint32_t pos, uint32_t n) {
 // ---------------------------------------------------------------------------------- Engine
 Engine::Engine(uint32_t burst, uint32_t inflight, uint32_t tx_workers, uint32_t queues, uint32_t max_inflight_frames)
     : burst_(burst), inflight_(std::max<uint32_t>(inflight, 1)), workers_(std::max<uint32_t>(tx_workers, 1)),
-      nq_(queues), max_frames_(max_inflight_frames) {
+      nq_(queues), max_frames_(max_inflight_frames), inline_tx_(tx_workers == 0) {
   if (burst_ < 1 || burst_ > (1u << 16)) throw std::invalid_argument("iox: burst in [1, 65536]");
   if (workers_ > 16) throw std::invalid_argument("iox: at most 16 tx workers per queue");
   if (nq_ < 1 || nq_ > 64) throw std::invalid_argument("iox: queues in [1, 64]");
@@ -770,7 +770,7 @@ void Engine::start() {
   }
   learner_ = std::thread(&Engine::learner_loop, this);
   for (auto& Q : queues_) {
-    for (uint32_t w = 0; w < workers_; ++w) {
+    for (uint32_t w = 0; w < (inline_tx_ ? 0u : workers_); ++w) {
       Q->tx.emplace_back(&Engine::tx_loop, this, Q.get(), w);
       pin(Q->tx.back(), Q->cpus);
     }
@@ -1018,8 +1018,23 @@ void Engine::learner_loop() {
 #endif
 constexpr uint32_t kYieldMask = NFDP_IOX_YIELD_MASK;   // idle polls between yields of a spinning thread
 
+struct Engine::TxCtx {
+  TxScratch sc;
+  std::vector<uint64_t> cur;                   // per lane: the next burst id to handle
+  std::vector<Clock::time_point> wait_since;   // per lane: since when its next burst is incomplete
+  std::vector<uint8_t> waiting;
+  uint32_t idle = 0;
+  Snap<Cfg> csnap;
+  Snap<PortTab> psnap;
+  explicit TxCtx(size_t lanes) : cur(lanes, 0), wait_since(lanes), waiting(lanes, 0) {
+    sc.by_port.resize((size_t)kMaxPorts + 2);
+  }
+};
+
 void Engine::rx_loop(Queue* Q) {
   std::vector<RxRef> buf(burst_);
+  std::unique_ptr<TxCtx> tx;   // run to completion: this thread delivers its lanes' bursts too
+  if (inline_tx_) tx.reset(new TxCtx(Q->lanes.size()));
   uint32_t idle_polls = 0;
   uint32_t rr = 0;
   std::shared_ptr<const PortTab> cached;
@@ -1040,6 +1055,7 @@ void Engine::rx_loop(Queue* Q) {
         // nothing is being published by this thread from here until it sees the flags clear
         Q->held_epoch.store(ctl_epoch_.load(std::memory_order_acquire), std::memory_order_release);
         st.add(st.held, 1);
+        if (tx) (void)tx_poll(Q, 0, *tx);   // bursts in flight still complete (pause waits for them)
         for (int k = 0; k < 64 && (pause_n_.load() || hold_n_.load()); ++k) _mm_pause();
         if (pause_n_.load()) std::this_thread::sleep_for(std::chrono::microseconds(10));
         continue;
@@ -1232,11 +1248,17 @@ void Engine::rx_loop(Queue* Q) {
         st.add(st.bursts, 1);
         ++pubs;
       }
-      if (got == 0 && pubs == 0) {
+      const uint32_t dlv = tx ? tx_poll(Q, 0, *tx) : 0u;
+      if (got == 0 && pubs == 0 && dlv == 0) {
         st.add(take ? st.idle : st.wait_tx, 1);
         _mm_pause();
         if ((++idle_polls & kYieldMask) == 0) std::this_thread::yield();
       }
+    }
+    if (tx) {   // stopping: deliver what was published (a pipeline that stopped completing throws)
+      const auto t0 = Clock::now();
+      while (!tx_drained(Q, *tx) && !abandon_.load() && Clock::now() - t0 < std::chrono::seconds(10))
+        if (!tx_poll(Q, 0, *tx)) _mm_pause();
     }
     release_all();
   } catch (const std::exception& e) {
@@ -1370,7 +1392,7 @@ void Engine::deliver(Queue* Q, Lane* L, Burst& b, uint32_t w, const Cfg& c, cons
     const uint32_t pos = (uint32_t)((b.start + i) & cmask);
     const uint32_t meta = om[pos];
     const uint32_t reason = meta_reason(meta), oport = meta_port(meta), olen = meta_len(meta);
-    if (reason == 0 && (meta & 0xFFFu) == kMetaPortGde) {   // the grid wrote it into the pod's ring itself
+    if (meta_is_gde(meta)) {   // the grid wrote it into the pod's ring itself
       if (w == 0) ++tally.gde;
       continue;
     }
@@ -1451,76 +1473,75 @@ void Engine::finish(Queue* Q, Lane* L, Burst& b) {
   L->done.fetch_add(1, std::memory_order_release);
 }
 
+uint32_t Engine::tx_poll(Queue* Q, uint32_t w, TxCtx& x) {
+  const uint32_t nl = (uint32_t)Q->lanes.size();
+  const uint32_t want = w == 0 ? 1u : 2u;
+  QStats& st = Q->wst[w];
+  uint32_t handled = 0;
+  for (uint32_t li = 0; li < nl; ++li) {
+    Lane* L = Q->lanes[li];
+    Burst& b = L->slots[x.cur[li] % inflight_];
+    if (!(b.state.load(std::memory_order_acquire) >= want && b.id == x.cur[li])) continue;
+    if (w == 0) {
+      // leader: completion, side work, then the burst is ready for every worker
+      if (!L->be->range_done(Q->id, b.start, b.end)) {
+        if (!x.waiting[li]) { x.waiting[li] = 1; x.wait_since[li] = Clock::now(); }
+        else if ((++x.idle & 0xFFFu) == 0) {
+          const auto waited = Clock::now() - x.wait_since[li];
+          if (waited > std::chrono::milliseconds(200) && !L->be->alive())
+            throw std::runtime_error("tx: the ring kernel is gone (device deadline or fault)");
+          if (waited > std::chrono::seconds(5)) throw std::runtime_error("tx: burst not completed within 5 s");
+        }
+        continue;
+      }
+      x.waiting[li] = 0;
+      const Cfg* c = b.cfg ? b.cfg.get() : &cfg_of(x.csnap);
+      bool side = b.side;
+      if (!side) {
+        const uint32_t* om = L->be->out_meta(Q->id);
+        const uint32_t cm = L->be->capacity() - 1;
+        for (uint64_t p = b.start; p < b.start + b.pkts.size() && !side; ++p)
+          side = (om[p & cm] & (kMetaFlood | kMetaXhdr)) != 0;
+      }
+      if (side) side_work(Q, L, b, *c, x.sc, w);
+      b.state.store(2, std::memory_order_release);
+      const uint64_t td0 = now_ns();
+      deliver(Q, L, b, w, *c, ports_of(x.psnap), x.sc);
+      st.add(st.deliver_ns, now_ns() - td0);
+    } else {
+      const Cfg& c = b.cfg ? *b.cfg : cfg_of(x.csnap);
+      const uint64_t td0 = now_ns();
+      deliver(Q, L, b, w, c, ports_of(x.psnap), x.sc);
+      st.add(st.deliver_ns, now_ns() - td0);
+    }
+    if (b.left.fetch_sub(1, std::memory_order_acq_rel) == 1) finish(Q, L, b);
+    ++x.cur[li];
+    ++handled;
+  }
+  return handled;
+}
+
+bool Engine::tx_drained(Queue* Q, const TxCtx& x) const {
+  for (uint32_t li = 0; li < (uint32_t)Q->lanes.size(); ++li) {
+    const Lane* L = Q->lanes[li];
+    if (L->done.load() != L->head.load() || x.cur[li] != L->head.load()) return false;
+  }
+  return true;
+}
+
 void Engine::tx_loop(Queue* Q, uint32_t w) {
   try {
-    TxScratch sc;
-    sc.by_port.resize((size_t)kMaxPorts + 2);
-    const uint32_t nl = (uint32_t)Q->lanes.size();
-    std::vector<uint64_t> cur(nl, 0);
-    std::vector<Clock::time_point> wait_since(nl);
-    std::vector<uint8_t> waiting(nl, 0);
-    const uint32_t want = w == 0 ? 1u : 2u;
-    uint32_t idle = 0;
-    QStats& st = Q->wst[w];
-    Snap<Cfg> csnap;
-    Snap<PortTab> psnap;
+    TxCtx x(Q->lanes.size());
     for (;;) {
-      bool any = false;
-      for (uint32_t li = 0; li < nl; ++li) {
-        Lane* L = Q->lanes[li];
-        Burst& b = L->slots[cur[li] % inflight_];
-        if (!(b.state.load(std::memory_order_acquire) >= want && b.id == cur[li])) continue;
-        if (w == 0) {
-          // leader: completion, side work, then the burst is ready for every worker
-          if (!L->be->range_done(Q->id, b.start, b.end)) {
-            if (!waiting[li]) { waiting[li] = 1; wait_since[li] = Clock::now(); }
-            else if ((++idle & 0xFFFu) == 0) {
-              const auto waited = Clock::now() - wait_since[li];
-              if (waited > std::chrono::milliseconds(200) && !L->be->alive())
-                throw std::runtime_error("tx: the ring kernel is gone (device deadline or fault)");
-              if (waited > std::chrono::seconds(5)) throw std::runtime_error("tx: burst not completed within 5 s");
-            }
-            continue;
-          }
-          waiting[li] = 0;
-          const Cfg* c = b.cfg ? b.cfg.get() : &cfg_of(csnap);
-          bool side = b.side;
-          if (!side) {
-            const uint32_t* om = L->be->out_meta(Q->id);
-            const uint32_t cm = L->be->capacity() - 1;
-            for (uint64_t p = b.start; p < b.start + b.pkts.size() && !side; ++p)
-              side = (om[p & cm] & (kMetaFlood | kMetaXhdr)) != 0;
-          }
-          if (side) side_work(Q, L, b, *c, sc, w);
-          b.state.store(2, std::memory_order_release);
-          const uint64_t td0 = now_ns();
-          deliver(Q, L, b, w, *c, ports_of(psnap), sc);
-          st.add(st.deliver_ns, now_ns() - td0);
-        } else {
-          const Cfg& c = b.cfg ? *b.cfg : cfg_of(csnap);
-          const uint64_t td0 = now_ns();
-          deliver(Q, L, b, w, c, ports_of(psnap), sc);
-          st.add(st.deliver_ns, now_ns() - td0);
-        }
-        if (b.left.fetch_sub(1, std::memory_order_acq_rel) == 1) finish(Q, L, b);
-        ++cur[li];
-        any = true;
-      }
-      if (any) {
-        idle = 0;
+      if (tx_poll(Q, w, x)) {
+        x.idle = 0;
         continue;
       }
       if (abandon_.load(std::memory_order_relaxed)) return;
-      if (!run_.load(std::memory_order_relaxed)) {
-        bool drained = true;
-        for (uint32_t li = 0; li < nl; ++li)
-          drained = drained && Q->lanes[li]->done.load() == Q->lanes[li]->head.load() &&
-                    cur[li] == Q->lanes[li]->head.load();
-        if (drained) return;
-      }
+      if (!run_.load(std::memory_order_relaxed) && tx_drained(Q, x)) return;
       _mm_pause();
-      if ((++idle & 0x3FFu) == 0) (void)ports_of(psnap);   // idle: let go of a replaced port table too
-      if ((idle & kYieldMask) == 0) std::this_thread::yield();
+      if ((++x.idle & 0x3FFu) == 0) (void)ports_of(x.psnap);   // idle: let go of a replaced port table too
+      if ((x.idle & kYieldMask) == 0) std::this_thread::yield();
     }
   } catch (const std::exception& e) {
     fail(std::string("tx: ") + e.what());

@@ -459,7 +459,9 @@ class Engine {
   // delivery threads per queue (each owns the egress ports with port % tx_workers == its index,
   // so frames of one port from one queue leave in order); queues: rx threads (each with its
   // ring queue on every backend); max_inflight_frames: frames in flight per lane (bounds the
-  // engine's own queueing delay: frames beyond it wait in the ports' rings).
+  // engine's own queueing delay: frames beyond it wait in the ports' rings).  tx_workers = 0:
+  // run to completion — each queue's rx thread also completes and delivers its own bursts (no
+  // delivery threads: one busy thread per queue, the layout that fits a CPU quota best).
   Engine(uint32_t burst, uint32_t inflight_bursts, uint32_t tx_workers = 1, uint32_t queues = 1,
          uint32_t max_inflight_frames = 0);
   ~Engine();
@@ -605,10 +607,15 @@ class Engine {
     std::vector<uint32_t> touched;
     std::vector<uint32_t> learn;   // learn events of the current burst
   };
+  struct TxCtx;                 // one delivery loop's state (a tx worker, or an inline rx thread)
 
   static void pin(std::thread& t, const std::vector<int>& cpus);
   void rx_loop(Queue* Q);
   void tx_loop(Queue* Q, uint32_t w);
+  // one pass over the queue's lanes: each lane's next burst, if it is this worker's turn and
+  // complete, is side-passed / delivered; returns the bursts handled (never blocks)
+  uint32_t tx_poll(Queue* Q, uint32_t w, TxCtx& x);
+  bool tx_drained(Queue* Q, const TxCtx& x) const;
   void learner_loop();
   void deliver(Queue* Q, Lane* L, Burst& b, uint32_t w, const Cfg& cfg, const PortTab& tab, TxScratch& sc);
   void side_work(Queue* Q, Lane* L, Burst& b, const Cfg& cfg, TxScratch& sc, uint32_t w);
@@ -638,6 +645,7 @@ class Engine {
   static uint32_t owner(const Steer* s, uint32_t n, const uint8_t* f, uint32_t len, uint32_t in_port);
 
   uint32_t burst_, inflight_, workers_, nq_, max_frames_;
+  bool inline_tx_ = false;      // tx_workers == 0: the rx threads deliver (workers_ is then 1)
   std::vector<std::unique_ptr<Lane>> lanes_;     // q * nbackends + g
   std::vector<std::shared_ptr<Backend>> backends_;
   std::vector<std::unique_ptr<Queue>> queues_;

@@ -159,14 +159,19 @@ static_assert(sizeof(RingDevState) == 256, "RingDevState");
 // GPU-direct egress (GDE): a frame whose egress port is a memif vport goes from the grid straight
 // into that vport's data-plane -> pod ring reserved for this GPU and queue (a ring no host thread
 // writes): the frame's 64 B and its descriptor are stored over PCIe, the ring head is published
-// with a system-scope store, and the host's tx path never touches the frame (its meta says
-// kMetaPortGde).  Chunks of a queue take their turn in ticket order (RingDevState.gde_turn), so a
+// with a system-scope store, and the host's tx path never touches the frame (its meta's length
+// field says kMetaLenGde).  Chunks of a queue take their turn in ticket order (RingDevState.gde_turn), so a
 // pod sees its frames in arrival order; a full ring (the pod's tail, re-read over PCIe when the
 // cached one says full) leaves the rest of the chunk's frames to the host path.  Eligible: no drop,
 // no side work (flood / tunnel header), the whole frame in the 64-B slot.  One entry per (port,
 // queue): the ring's addresses as the GPU sees the mapped memif region, its geometry and the
 // producer's private head (device state).
-constexpr uint32_t kMetaPortGde = 0xFFDu;   // out-meta port of a frame the grid delivered itself
+// Out-meta length field of a frame the grid delivered itself (reason kOk, the port field keeps the
+// egress port): longer than any frame (kMaxFrame), so no forwarded frame can carry it, whatever its
+// port (the marker used to be port 0xFFD, which is the valid vport 4093).
+constexpr uint32_t kMetaLenGde = 0x3FFFu;
+static_assert(kMetaLenGde > kMaxFrame, "GDE marker must not be a frame length");
+NFDP_HD bool meta_is_gde(uint32_t m) { return meta_reason(m) == kOk && meta_len(m) == kMetaLenGde; }
 struct alignas(64) GdeRing {
   uint64_t ctl;        // device address of the memif ring's Ctl (head written here, tail read)
   uint64_t desc;       // device address of its Desc[ring_size]

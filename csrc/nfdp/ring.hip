@@ -310,7 +310,7 @@ __device__ __forceinline__ void gde_deliver(const RingArgs& a, RingDevState* qst
     __builtin_amdgcn_raw_buffer_store_b64(dv, rd, mine ? pos * 8u : kNoRun, 0, kSysAux);
   }
   __builtin_amdgcn_s_waitcnt(0);   // (write-through stores done: the frames are in host memory)
-  if (go) meta = make_meta(kMetaPortGde, olen, kOk);
+  if (go) meta = make_meta(port, kMetaLenGde, kOk);
   // ---- 3. commit: heads in ticket order ----
   const unsigned long long tw3 = __builtin_amdgcn_s_memrealtime();
   gde_turn(&qst->gde_commit, tk, lane, a, t_begin);

@@ -9,6 +9,7 @@
 // Header-only, no HIP: linked into the _nfdp module and into the standalone `dpu-trafgen` tool.
 #pragma once
 #include <immintrin.h>
+#include <time.h>
 
 #include <algorithm>
 #include <atomic>
@@ -208,6 +209,29 @@ inline Result run(std::vector<Pod> pods, const Config& cfg) {
   }
   r.elapsed_s = cfg.duration_s;
   return r;
+}
+
+// CPU share probe: `threads` threads busy-loop together for `seconds`; returns the CPU seconds
+// they were granted (summed CLOCK_THREAD_CPUTIME_ID).  Divided by the wall time that is the number
+// of CPUs the process really gets — under a CFS quota, less than `threads` once the quota is
+// reached, whatever `nproc` says.  Threads only (no fork: the caller may hold a GPU context).
+inline double cpu_share_probe(uint32_t threads, double seconds) {
+  std::vector<std::thread> th;
+  std::vector<double> used(threads, 0.0);
+  const uint64_t t_end = now_ns() + (uint64_t)(seconds * 1e9);
+  for (uint32_t t = 0; t < threads; ++t) {
+    th.emplace_back([&, t]() {
+      volatile uint64_t x = 0;
+      while (now_ns() < t_end) x = x + 1;
+      timespec ts{};
+      clock_gettime(CLOCK_THREAD_CPUTIME_ID, &ts);
+      used[t] = (double)ts.tv_sec + (double)ts.tv_nsec * 1e-9;
+    });
+  }
+  for (auto& x : th) x.join();
+  double s = 0.0;
+  for (double u : used) s += u;
+  return s;
 }
 
 }  // namespace trafgen

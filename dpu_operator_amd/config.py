@@ -94,8 +94,8 @@ class NodeConfig:
             raise ValueError("unknown hash / ACL mode")
         if self.vport_kind not in ("veth", "memif", "tap"):
             raise ValueError("vport_kind is veth, memif or tap")
-        if not 1 <= self.io_queues <= 64 or not 1 <= self.io_workers <= 16:
-            raise ValueError("io_queues in [1, 64], io_workers in [1, 16]")
+        if not 1 <= self.io_queues <= 64 or not 0 <= self.io_workers <= 16:
+            raise ValueError("io_queues in [1, 64], io_workers in [0, 16] (0: the rx threads deliver)")
         if not self.uplink or len(self.uplink) > 15 or not 1 <= len(self.uplink_host_ifname) <= 14:
             raise ValueError("uplink is 'veth', 'none' or a netdev name; uplink_host_ifname at most 14 characters")
 

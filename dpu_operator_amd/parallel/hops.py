@@ -47,13 +47,18 @@ class _Inbox:
     out: object         # resume results [cap, 64] / [cap] / [cap, 8]
     meta: object
     nxt: object
+    last: object = None  # event after the latest resume over this inbox (the next pack waits for it)
 
 
 class HopPipeline:
-    def __init__(self, planes, batch: int, entry: int = 0):
+    def __init__(self, planes, batch: int, entry: int = 0, streams=None):
+        """streams: per plane, the torch.cuda.Stream its kernels run on (None: the device's current
+        stream at each step).  Consecutive steps reuse the inboxes: a step's pack into an inbox
+        waits for the previous step's resume over it, whatever streams the planes use."""
         import torch
 
         self.torch = torch
+        self.streams = list(streams) if streams is not None else None
         self.planes = planes
         self.batch = batch
         self.entry = entry
@@ -109,17 +114,25 @@ class HopPipeline:
         ib = self.inboxes[self.stages[si][2]]
         return ib.out, ib.meta, ib.nxt, ib.count.data_ptr()
 
+    def _stream(self, plane: int):
+        if self.streams is not None and self.streams[plane] is not None:
+            return self.streams[plane]
+        return self.torch.cuda.current_stream(self.planes[plane].tdev)
+
     def step(self, pkts, inmeta, timing: dict | None = None) -> None:
         """One batch through the split chains (launches and events only; no host wait).  `timing`:
         a dict that receives CUDA events {fused, handoff, resume} boundaries (for the bench)."""
         torch = self.torch
         p0 = self.planes[self.entry]
-        s0 = torch.cuda.current_stream(p0.tdev)
+        s0 = self._stream(self.entry)
         ev = (lambda: torch.cuda.Event(enable_timing=True)) if timing is not None else None
         if timing is not None:
             timing["t0"] = ev()
             timing["t0"].record(s0)
-        r = p0.run(pkts, inmeta, out=self.out0, meta=self.meta0, lat=self.lat0)
+        # (the entry buffers are rewritten on s0: the previous step's packs read them on s0 too;
+        # s0 current while run() allocates, so its per-batch buffers belong to that stream)
+        with torch.cuda.stream(s0):
+            r = p0.run(pkts, inmeta, out=self.out0, meta=self.meta0, lat=self.lat0)
         self.hop0 = r.extra["hop_state"]
         if timing is not None:
             timing["fused"] = ev()
@@ -128,10 +141,11 @@ class HopPipeline:
         done: dict[int, object] = {0: None}
         for k, ib in enumerate(self.inboxes):
             src_plane = self.stages[ib.src][1]
-            ps = self.planes[src_plane]
-            ss = torch.cuda.current_stream(ps.tdev)
+            ss = self._stream(src_plane)
             if ib.src in done and done[ib.src] is not None:
                 ss.wait_event(done[ib.src])
+            if ib.last is not None:   # the previous step's resume still reads this inbox
+                ss.wait_event(ib.last)
             out, meta, hop, n_dev = self._stage_buffers(ib.src)
             self.nf.launch_hop_pack(out.data_ptr(), meta.data_ptr(), hop.data_ptr(), n if ib.src == 0 else self.batch,
                                     n_dev, ib.plane, ib.fill.data_ptr(), ib.count.data_ptr(), ib.hdr.data_ptr(),
@@ -141,7 +155,7 @@ class HopPipeline:
             if timing is not None and "handoff" not in timing:
                 timing["handoff"] = e
             q = self.planes[ib.plane]
-            sq = torch.cuda.current_stream(q.tdev)
+            sq = self._stream(ib.plane)
             sq.wait_event(e)
             self.nf.launch_resume(q.tables_ptrs(), ib.count.data_ptr(), ib.hdr.data_ptr(), ib.state.data_ptr(),
                                   ib.idx.data_ptr(), self.batch, ib.out.data_ptr(), ib.meta.data_ptr(),
@@ -150,11 +164,13 @@ class HopPipeline:
             e2 = torch.cuda.Event(enable_timing=timing is not None)
             e2.record(sq)
             done[k + 1] = e2
+            ib.last = e2
             if timing is not None:
                 timing["resume"] = e2
 
     def synchronize(self) -> None:
-        for p in self.planes:
+        for i, p in enumerate(self.planes):
+            self._stream(i).synchronize()
             self.torch.cuda.synchronize(p.tdev)
 
     def results(self, n: int) -> tuple[np.ndarray, np.ndarray]:

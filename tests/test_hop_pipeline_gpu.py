@@ -100,3 +100,37 @@ def test_multidataplane_run_resolves_handoffs_on_gpu():
     assert r2.extra["handoff_rounds"] == 1
     _compare(r1.meta.cpu().numpy().view(np.uint32), r1.out.cpu().numpy(), r2.meta, r2.out)
     np.testing.assert_array_equal(one.port_counters(), multi.port_counters())
+
+
+def test_hop_pipeline_back_to_back_steps_on_distinct_streams():
+    """Consecutive steps reuse the inboxes: with each plane on its own stream (as on two GPUs), the
+    next step's pack must wait for the previous step's resume over the same inbox.
+    Four steps of alternating batches are queued without any host wait; the last step's frames and
+    the summed counters must equal the one-plane chain run four times."""
+    import torch
+
+    from dpu_operator_amd.parallel.hops import HopPipeline
+
+    one = DataPlane(device="cuda:0")
+    sc, deny = _program(one, ("acl", "nat", "ttl", "l2fwd"))
+    multi = MultiDataPlane(["cuda:0", "cuda:0"], placement="port")
+    _program(multi, ("acl", "nat", "ttl@1", "l2fwd@1"))
+    n = 1 << 16
+    batches = []
+    for s in range(2):
+        pk, im = S.traffic_mixed(sc, deny, n, seed=20 + s, miss=0.05, deny_frac=0.05)
+        batches.append((torch.from_numpy(pk).cuda(), torch.from_numpy(im.view(np.int32)).cuda()))
+    for k in range(4):
+        r1 = one.run(*batches[k % 2])
+    torch.cuda.synchronize()
+    m1, o1 = r1.meta.cpu().numpy().view(np.uint32), r1.out.cpu().numpy()
+    streams = [torch.cuda.Stream(device="cuda:0"), torch.cuda.Stream(device="cuda:0")]
+    hp = HopPipeline(multi.planes, n, streams=streams)
+    for k in range(4):
+        hp.step(*batches[k % 2])
+    o2, m2 = hp.results(n)
+    _compare(m1, o1, m2, o2)
+    np.testing.assert_array_equal(one.port_counters(), multi.port_counters())
+    d1, d2 = one.drop_counters(), multi.drop_counters()
+    d2.pop("remote", 0)
+    assert d1 == d2

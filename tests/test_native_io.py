@@ -62,7 +62,7 @@ def _expected(dp_ref, slots, im):
     return exp, int((reason != 0).sum())
 
 
-@pytest.mark.parametrize("workers", [1, 3])
+@pytest.mark.parametrize("workers", [0, 1, 3])
 def test_memif_sfc_bit_exact_with_the_batch_path(tmp_path, workers):
     nf = nfdp()
     dp, sc = _sfc("cpu")

@@ -86,7 +86,7 @@ def _collect(eps, want):
     return got, done
 
 
-@pytest.mark.parametrize("queues,workers", [(3, 1), (2, 2)])
+@pytest.mark.parametrize("queues,workers", [(3, 1), (2, 2), (2, 0)])
 def test_multiqueue_bit_exact(shm, queues, workers):
     """Ports spread over `queues` rx threads (least loaded first), each with its own ring queue:
     every frame comes out as the batch path makes it, counters equal."""
