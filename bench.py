@@ -193,9 +193,11 @@ def parse():
     ap.add_argument("--no-hops", action="store_true", help="skip the SFC hop pipeline across GPUs (tools/hop_bench.py)")
     ap.add_argument("--no-live", action="store_true", help="skip the live pod-to-pod (native I/O engine) block")
     ap.add_argument("--no-unsteered", action="store_true", help="N > 1 rss: skip the exchange-bound (unsteered) variant")
-    ap.add_argument("--live-workers", type=int, default=2, help="native I/O engine delivery threads per queue")
-    ap.add_argument("--live-queues", type=int, default=4, help="native I/O engine rx queues (threads)")
-    ap.add_argument("--live-gen-threads", type=int, default=4, help="pod traffic generator threads")
+    ap.add_argument("--live-workers", type=int, default=0,
+                    help="native I/O engine delivery threads per queue (0: run to completion, the rx thread delivers)")
+    ap.add_argument("--live-queues", type=int, default=6, help="native I/O engine rx queues (threads)")
+    ap.add_argument("--live-gen-threads", type=int, default=8, help="pod traffic generator threads (one per pod)")
+    ap.add_argument("--live-trials", type=int, default=3, help="saturated live trials of 1 s (median reported)")
     ap.add_argument("--live-gpu-egress", action="store_true",
                     help="live block: the ring grid writes frames into the pods' rings itself (GPU-direct egress)")
     ap.add_argument("--variant-steps", type=int, default=30)
@@ -721,28 +723,36 @@ def main() -> None:
                 "live_bench", os.path.join(os.path.dirname(os.path.abspath(__file__)), "tools", "live_bench.py"))
             lb = importlib.util.module_from_spec(spec)
             spec.loader.exec_module(lb)
+            from dpu_operator_amd.utils import cpuquota
+
             gde = bool(a.live_gpu_egress)
-            live = lb.run(device=str(dev), n_pods=a.pods_per_gpu, flows=a.flows, n_acl=a.acl, duration=0.5,
+            # the CPU time the box really grants (a CFS quota the process cannot read: 256 CPUs
+            # listed, 16 granted on the GPU box) - the live path is host-CPU work: pods + engine
+            share = cpuquota.cpu_share()
+            live = lb.run(device=str(dev), n_pods=a.pods_per_gpu, flows=a.flows, n_acl=a.acl, duration=1.0,
                           threads=a.live_gen_threads, tx_workers=a.live_workers, queues=a.live_queues,
-                          hash_mode=a.hash, gpu_egress=gde)
+                          hash_mode=a.hash, gpu_egress=gde, trials=a.live_trials)
             live["gpu_egress"] = gde
-            # the other egress mode for comparison (GPU-direct egress: 6 queues, 1 tx thread each, 6
-            # generator threads; or host egress), saturated rate only
-            alt = (dict(threads=4, tx_workers=2, queues=4, gpu_egress=False) if gde else
-                   dict(threads=6, tx_workers=1, queues=6, gpu_egress=True))
-            hp = lb.run(device=str(dev), n_pods=a.pods_per_gpu, flows=a.flows, n_acl=a.acl, duration=0.3,
+            # the other egress mode for comparison (GPU-direct egress or host egress), same threads,
+            # saturated rate only
+            alt = dict(threads=a.live_gen_threads, tx_workers=a.live_workers, queues=a.live_queues, gpu_egress=not gde)
+            hp = lb.run(device=str(dev), n_pods=a.pods_per_gpu, flows=a.flows, n_acl=a.acl, duration=0.5,
                         hash_mode=a.hash, saturated_only=True, **alt)
             live["other_egress"] = {**alt, "mpps": hp.get("mpps"), "p50_us": hp.get("p50_us"), "error": hp.get("error")}
-            # the engine's queue curve: saturated pod -> pod Mpps at 1 / 2 / 4 / 8 rx queues (each
-            # with its tx workers), the same pods and pipeline; bounded by the box's CPU share
+            # the engine's queue curve: saturated pod -> pod Mpps at 1 / 2 / 4 / 6 / 8 rx queues, the
+            # same pods, pipeline and delivery mode, each point with the CPUs it used: pods and
+            # engine share the box's CPU grant, so past the grant more queues cannot help
             curve = []
-            for q in (1, 2, 4, 8):
-                r = lb.run(device=str(dev), n_pods=a.pods_per_gpu, flows=a.flows, n_acl=a.acl, duration=0.3,
+            for q in (1, 2, 4, 6, 8):
+                r = lb.run(device=str(dev), n_pods=a.pods_per_gpu, flows=a.flows, n_acl=a.acl, duration=0.5,
                            threads=a.live_gen_threads, tx_workers=a.live_workers, queues=q, hash_mode=a.hash,
                            saturated_only=True, gpu_egress=gde)
-                curve.append({"queues": q, "mpps": r.get("mpps"), "p50_us": r.get("p50_us"), "error": r.get("error")})
+                curve.append({"queues": q, "mpps": r.get("mpps"), "p50_us": r.get("p50_us"),
+                              "cpus_used": (r.get("cpu") or {}).get("process_cpus_used"), "error": r.get("error")})
             live["queue_curve"] = curve
             live["host_cpus"] = len(os.sched_getaffinity(0))
+            live["cpu_share"] = share
+            live["threads_busy"] = a.live_gen_threads + a.live_queues * (1 + a.live_workers)
         except Exception as ex:  # the headline number must still be reported
             live = {"error": str(ex)[:200]}
         # kernel-netdev (veth) pods in front of the same GPU ring (tools/live_bench.py run_veth

@@ -776,6 +776,31 @@ PYBIND11_MODULE(_nfdp, m) {
            py::call_guard<py::gil_scoped_release>())
       .def("gde_clear", &RingEngine::gde_clear, py::arg("port"), py::arg("q"), py::call_guard<py::gil_scoped_release>())
       .def("gde_stats", &RingEngine::gde_stats)
+      // SFC hops across GPUs in the live path (ring.h XferEntry)
+      .def("xfer_enable", &RingEngine::xfer_enable, py::arg("entries"), py::arg("wgs") = 1)
+      .def_property_readonly("xfer_on", &RingEngine::xfer_on)
+      .def_property_readonly("xfer_active", &RingEngine::xfer_active)
+      .def("xfer_desc", [](const RingEngine& r) {
+        const RingEngine::XferDesc d = r.xfer_desc();
+        py::dict o;
+        o["inbox"] = d.inbox; o["entries"] = d.entries; o["out"] = d.out; o["out_meta"] = d.out_meta;
+        o["xpend"] = d.xpend; o["cap"] = d.cap; o["ring_mask"] = d.ring_mask; o["nq"] = d.nq;
+        return o;
+      })
+      .def("xfer_set_peers", [](RingEngine& r, uint32_t my_plane, py::list planes) {
+        std::vector<RingEngine::XferDesc> v;
+        for (auto o : planes) {
+          py::dict d = o.cast<py::dict>();
+          RingEngine::XferDesc x;
+          x.inbox = d["inbox"].cast<uint64_t>(); x.entries = d["entries"].cast<uint64_t>();
+          x.out = d["out"].cast<uint64_t>(); x.out_meta = d["out_meta"].cast<uint64_t>();
+          x.xpend = d["xpend"].cast<uint64_t>(); x.cap = d["cap"].cast<uint32_t>();
+          x.ring_mask = d["ring_mask"].cast<uint32_t>(); x.nq = d["nq"].cast<uint32_t>();
+          v.push_back(x);
+        }
+        r.xfer_set_peers(my_plane, v);
+      }, py::arg("my_plane"), py::arg("planes"))
+      .def("xfer_stats", &RingEngine::xfer_stats)
       .def_property_readonly("ctrl_posted", &RingEngine::ctrl_posted)
       .def("wait_ctrl", [](RingEngine& r, uint64_t seq, double timeout_s) {
         py::gil_scoped_release nogil;

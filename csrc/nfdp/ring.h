@@ -185,6 +185,56 @@ struct alignas(64) GdeRing {
 };
 static_assert(sizeof(GdeRing) == 64, "GdeRing");
 
+// ---- SFC hops across GPUs in the live path (split chains, kHopXfer) --------------------------------
+// A chain whose hops sit on different GPU planes runs hop by hop across the planes' resident grids,
+// with no host hop and no launch:
+//   1. the entry plane's grid (an XF ring instance) runs the hops up to the hand-off, stores the
+//      frame's slot / meta as usual, records the chunk's hand-off count in `xpend` (pinned host
+//      memory, before any entry is visible), then reserves entries in the next plane's INBOX (its
+//      HBM; one system-scope add on the inbox tail per target plane per chunk) and peer-stores the
+//      header slot, the HopState record and the way back (entry plane, queue, slot position);
+//      each entry's `seq` (idx + 1) is stored after its data;
+//   2. the resuming plane's inbox workgroups (the grid's last `xfer_wgs`) claim inbox chunks of 64
+//      entries by ticket, run pipeline.h resume_stage on every entry as it becomes ready, and
+//      store the final slot and meta straight into the ENTRY ring's out slot (pinned host memory:
+//      every GPU reaches it), then subtract the chunk's finished frames from its `xpend` word
+//      (system-scope atomic after the stores are done), and mark the entries consumed; a frame its
+//      chain hands on again is sent to the next inbox with the same way back;
+//   3. the host sees a chunk complete when its flag is written AND its xpend word is back to 0
+//      (RingEngine::chunk_done), so a burst is delivered with every frame's final header.
+// An entry a ring of the inbox ago must be consumed before a producer overwrites it (its seq says
+// so); the inbox is sized for far more frames than the live path keeps in flight.
+constexpr uint64_t kXferDone = 1ull << 63;
+struct alignas(128) XferEntry {
+  uint32_t slot[kSlotDwords];   // header slot as the hops so far left it
+  HopState hs;                  // 32 B: what resume_stage needs
+  uint32_t origin;              // entry plane | queue << 8
+  uint32_t pos;                 // slot position in that queue's ring
+  uint32_t pad0[2];
+  uint64_t seq;                 // idx + 1 once written; | kXferDone once consumed
+  uint64_t pad1;
+};
+static_assert(sizeof(XferEntry) == 128, "XferEntry");
+struct alignas(128) XferInbox {   // (device memory of the resuming plane)
+  uint64_t tail;                  // entries reserved by the producers (system-scope adds)
+  uint32_t pad0[30];
+  uint64_t claim;                 // inbox chunk tickets claimed by this grid's inbox waves
+  uint32_t pad1[30];
+};
+static_assert(sizeof(XferInbox) == 256, "XferInbox");
+struct XferPeer {                 // one plane, as every grid sees it
+  XferInbox* inbox;
+  XferEntry* entries;
+  uint32_t cap_mask;              // inbox entries - 1
+  uint32_t ring_mask;             // its ring's slots per queue - 1
+  uint4* out;                     // its ring's out slots / metas (device view; pinned host memory)
+  uint32_t* out_meta;
+  uint32_t* xpend;                // its ring's [queues][chunks] hand-offs not back yet (pinned)
+  uint32_t nq;
+  uint32_t pad;
+};
+constexpr uint32_t kMaxXferPlanes = 16;   // kHopXfer | plane, plane < 16
+
 class RingEngine {
  public:
   // capacity: ring slots per queue (power of two, >= 64).  wgs_per_cu: resident 256-thread
@@ -300,6 +350,21 @@ class RingEngine {
   uint64_t gde_clear(uint32_t port, uint32_t q);
   // (diagnostics, while stopped) per queue: {wait ticks, section ticks, chunks, frames, full}
   std::vector<uint64_t> gde_stats();
+  // Cross-GPU hops (see XferEntry).  xfer_enable while stopped: an inbox of `entries` (power of
+  // two; 0 = off) served by the grid's last `wgs` workgroups, and the per-chunk pending words.
+  // Every plane's descriptor (xfer_desc) then goes to every plane (xfer_set_peers, this one's
+  // number among them) before the rings start; rings of one node start and stop together.
+  struct XferDesc {
+    uint64_t inbox = 0, entries = 0, out = 0, out_meta = 0, xpend = 0;
+    uint32_t cap = 0, ring_mask = 0, nq = 0;
+  };
+  void xfer_enable(uint32_t entries, uint32_t wgs);
+  bool xfer_on() const { return d_xin_ != nullptr; }
+  bool xfer_active() const { return xfer_active_; }   // the running grid hands frames on (XF instance)
+  XferDesc xfer_desc() const;
+  void xfer_set_peers(uint32_t my_plane, const std::vector<XferDesc>& planes);
+  // (while stopped) {inbox tail, inbox claim}
+  std::vector<uint64_t> xfer_stats();
   // Device buffers control writes may target ([base, bytes) each: the running table set's small
   // tables); anything else is refused on the host, so a bad address never reaches the GPU.
   void set_ctrl_regions(const std::vector<std::pair<uint64_t, uint64_t>>& regions);
@@ -366,6 +431,14 @@ class RingEngine {
   uint32_t set_serial_ = 0;
   GdeRing* d_gde_ = nullptr;         // [kMaxPorts][nq] (HBM), null: GPU-direct egress off
   uint64_t gde_write(uint32_t port, uint32_t q, const GdeRing& e);
+  XferInbox* d_xin_ = nullptr;       // cross-GPU hops: this plane's inbox header (HBM)
+  XferEntry* d_xent_ = nullptr;      // ... and entries
+  uint32_t xcap_ = 0, xwgs_ = 0;
+  uint32_t* h_xpend_ = nullptr;      // [nq][nch] hand-offs per chunk not back yet (pinned)
+  uint32_t* d_xpend_ = nullptr;      // (its device view)
+  XferPeer* d_xpeers_ = nullptr;     // [nplanes] (HBM), null: peers not set
+  uint32_t xplane_ = 0, nplanes_ = 0;
+  bool xfer_active_ = false;
 };
 
 // hipHostUnregister(p), then after(), once no ring of this process is running (at once if none
@@ -390,6 +463,9 @@ struct RingLaunch {
   RingCtrlRing* ctrl;         // device view of the control mailbox
   const uint64_t* faddr;      // frame addresses per slot (null: frames are in the in slots)
   GdeRing* gde = nullptr;     // GPU-direct egress table [kMaxPorts][queues] (null: off)
+  const XferPeer* xpeers = nullptr;   // cross-GPU hops: every plane (null: off)
+  uint32_t xplane = 0, nplanes = 0, xfer_wgs = 0;
+  uint32_t* xpend = nullptr;          // this ring's pending hand-offs per chunk
 };
 hipError_t launch_ring(const RingLaunch& r, const LaunchCfg& cfg, int wgs_per_cu, bool coop, hipStream_t s);
 

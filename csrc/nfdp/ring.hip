@@ -1,6 +1,7 @@
 // ring.hip — persistent ring kernel + host engine (see ring.h for the protocol).
 #include "ring.h"
 
+#include <cstddef>
 #include <cstdlib>
 #include <string>
 
@@ -38,6 +39,9 @@ struct RingArgs {
   RingCtrlRing* ctrl;   // control mailbox (pinned host memory, device view)
   const unsigned long long* faddr;   // zero-copy rx: per-slot frame addresses (null: in slots)
   GdeRing* gde;         // GPU-direct egress table [kMaxPorts][nq] (null: off; ring.h GdeRing)
+  const XferPeer* xpeers;   // cross-GPU hops (ring.h XferEntry): every plane (null: off)
+  uint32_t xplane, nplanes, xfer_wgs;
+  uint32_t* xpend;          // this ring's [nq][chunks] hand-offs not back yet (pinned host memory)
 };
 // Frames are read and written with system-coherent buffer ops (sc0 sc1): the loads never hit a
 // stale L2 line of a slot a producer (host / NIC DMA) rewrote, and the stores write through to
@@ -338,6 +342,196 @@ __device__ __forceinline__ void gde_deliver(const RingArgs& a, RingDevState* qst
   }
 }
 
+// ---- SFC hops across GPUs in the live path (ring.h XferEntry) ----------------------------------
+__device__ __forceinline__ uint32_t lane_rank(unsigned long long bm) {
+  return __builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
+}
+__device__ __forceinline__ void hs_pack(const HopState& h, uint32_t w[8]) {
+  w[0] = h.inmeta; w[1] = h.hash; w[2] = (uint32_t)h.acl_rule; w[3] = h.hop;
+  w[4] = (uint32_t)h.act.chain_id | ((uint32_t)h.act.out_port << 16); w[5] = h.act.nat_ip;
+  w[6] = (uint32_t)h.act.nat_port | ((uint32_t)h.act.vlan << 16); w[7] = h.act.flow_id;
+}
+__device__ __forceinline__ HopState hs_unpack(const uint32_t w[8]) {
+  HopState h;
+  h.inmeta = w[0]; h.hash = w[1]; h.acl_rule = (int32_t)w[2]; h.hop = w[3];
+  h.act.chain_id = (uint16_t)(w[4] & 0xFFFFu); h.act.out_port = (uint16_t)(w[4] >> 16); h.act.nat_ip = w[5];
+  h.act.nat_port = (uint16_t)(w[6] & 0xFFFFu); h.act.vlan = (uint16_t)(w[6] >> 16); h.act.flow_id = w[7];
+  return h;
+}
+// A hand-off op naming no plane of this node (or no hop to resume at) ends the chain as a drop.
+__device__ __forceinline__ void xfer_check(EgressDecision& e, uint32_t nplanes) {
+  if (e.reason == kRemote && (e.out_port >= nplanes || e.inner_len == 0u)) { e.reason = kChainDrop; e.out_port = kPortNone; }
+}
+
+// The `go` lanes' frames to the inboxes of their planes (`plane`).  EXEC full.  Per target plane:
+// one system-scope add on its inbox tail reserves the run of entries; each lane waits until its
+// entry of a ring ago was consumed, stores slot, record and way back (system-coherent stores into
+// the peer's HBM), and once every store is done the entry's seq.
+__device__ __forceinline__ void xfer_send(const RingArgs& a, bool go, uint32_t plane, const uint32_t* o, const HopState& hs,
+                                       uint32_t origin, uint32_t pos, uint32_t lane, unsigned long long t_begin) {
+  uint32_t hw[8];
+  hs_pack(hs, hw);
+  unsigned long long rem = __ballot(go);
+  while (rem) {
+    const int leader = __builtin_ctzll(rem);
+    const uint32_t P = __builtin_amdgcn_readlane(plane, leader);
+    const bool mine = go && plane == P;
+    const unsigned long long bm = __ballot(mine);
+    rem &= ~bm;
+    XferInbox* ib = a.xpeers[P].inbox;
+    XferEntry* ent = a.xpeers[P].entries;
+    const uint32_t cmask = a.xpeers[P].cap_mask;
+    unsigned long long base = 0;
+    if (lane == 0)
+      base = __hip_atomic_fetch_add(&ib->tail, (unsigned long long)__builtin_popcountll(bm), __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_SYSTEM);
+    base = rfl64(base);
+    const unsigned long long idx = base + lane_rank(bm);
+    XferEntry* en = ent + (idx & cmask);
+    if (mine && idx > cmask) {   // the entry a ring of the inbox ago must have been consumed
+      const unsigned long long want = (idx - cmask) | kXferDone;   // ((idx - cap) + 1) | done
+      while (__hip_atomic_load(&en->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != want) {
+        if (__builtin_amdgcn_s_memrealtime() - t_begin > a.deadline) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    const __amdgpu_buffer_rsrc_t re = __builtin_amdgcn_make_buffer_rsrc((void*)ent, (short)0,
+                                                                        (int)((cmask + 1u) * 128u), kBufRaw);
+    const uint32_t off = mine ? (uint32_t)((idx & cmask) * 128u) : kNoRun;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) store_b128<kSysAux>(v4u{o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]}, re, off + 16u * k, 0);
+    store_b128<kSysAux>(v4u{hw[0], hw[1], hw[2], hw[3]}, re, off + 64u, 0);
+    store_b128<kSysAux>(v4u{hw[4], hw[5], hw[6], hw[7]}, re, off + 80u, 0);
+    store_b128<kSysAux>(v4u{origin, pos, 0u, 0u}, re, off + 96u, 0);
+    __builtin_amdgcn_s_waitcnt(0);   // the entry is in the peer's memory before its seq says so
+    if (mine) __hip_atomic_store(&en->seq, idx + 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+// One pass over the `rdy` lanes' inbox entries (EXEC full): the rest of their chains, then either
+// on to the next plane or back to the entry ring's out slot, its chunk's pending count reduced.
+template <bool COOP>
+__device__ __forceinline__ void xfer_resume(const RingArgs& a, bool rdy, XferEntry* en, unsigned long long idx, uint32_t lane,
+                                         unsigned long long t_begin, uint32_t& seen_ep) {
+  unsigned long long v = 0;
+  if (lane == 0) v = __hip_atomic_load(&a.st->dprod, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t ep = ring_epoch(rfl64(v));
+  if (ep != seen_ep) {   // the host changed a table: drop cached lines first (as the chunk waves do)
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    seen_ep = ep;
+  }
+  const TablesView& T = COOP ? a.sets[(ep & kEpochSetBit) >> 1].t : a.t;
+  const DirectTables ta{T};
+  // the entry (system-coherent loads: a peer wrote it)
+  const __amdgpu_buffer_rsrc_t re = __builtin_amdgcn_make_buffer_rsrc((void*)en, (short)0, 128, kBufRaw);
+  uint32_t d[kSlotDwords], hw[8];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const v4u c = __builtin_amdgcn_raw_buffer_load_b128(re, rdy ? 16u * k : kNoRun, 0, kSysAux);
+    d[4 * k] = c[0]; d[4 * k + 1] = c[1]; d[4 * k + 2] = c[2]; d[4 * k + 3] = c[3];
+  }
+  {
+    const v4u c0 = __builtin_amdgcn_raw_buffer_load_b128(re, rdy ? 64u : kNoRun, 0, kSysAux);
+    const v4u c1 = __builtin_amdgcn_raw_buffer_load_b128(re, rdy ? 80u : kNoRun, 0, kSysAux);
+    hw[0] = c0[0]; hw[1] = c0[1]; hw[2] = c0[2]; hw[3] = c0[3]; hw[4] = c1[0]; hw[5] = c1[1]; hw[6] = c1[2]; hw[7] = c1[3];
+  }
+  const v4u way = __builtin_amdgcn_raw_buffer_load_b128(re, rdy ? 96u : kNoRun, 0, kSysAux);
+  const uint32_t origin = way[0], pos = way[1];
+  const HopState hs = hs_unpack(hw);
+  Parsed p;
+  IngressState st;
+  resume_ingress(ta, d, hs.inmeta, p, st);
+  EgressDecision e = resume_stage<DirectTables, false>(T, ta, p, st, hs.act, hs.acl_rule, hs.hash, hs.hop);
+  xfer_check(e, a.nplanes);
+  uint32_t o[kSlotDwords];
+  emit(p, e.tci, e.push != 0, o);
+  const uint32_t olen = out_len(p, e);
+  const bool again = rdy && e.reason == kRemote;   // handed on: same way back, still pending
+  const bool fin = rdy && !again;
+  const uint32_t meta = make_meta(e.out_port, olen, e.reason, !e.reason && e.xhdr, false);
+  if (__ballot(again)) xfer_send(a, again, e.out_port, o, hop_state_of(p, st, e, hs.act, hs.acl_rule, hs.hash),
+                                 origin, pos, lane, t_begin);
+  // back to the entry ring: final slot and meta into its out slot (pinned host memory)
+  const uint32_t oplane = origin & 0xFFu, oq = origin >> 8;
+  unsigned long long rem = __ballot(fin);
+  while (rem) {
+    const int leader = __builtin_ctzll(rem);
+    const uint32_t O = __builtin_amdgcn_readlane(oplane, leader);
+    const bool mine = fin && oplane == O;
+    rem &= ~__ballot(mine);
+    const uint32_t slots = a.xpeers[O].ring_mask + 1u, nq = a.xpeers[O].nq;
+    const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc((void*)a.xpeers[O].out, (short)0,
+                                                                        (int)(nq * slots * 64u), kBufRaw);
+    const __amdgpu_buffer_rsrc_t rm = __builtin_amdgcn_make_buffer_rsrc((void*)a.xpeers[O].out_meta, (short)0,
+                                                                        (int)(nq * slots * 4u), kBufRaw);
+    const uint32_t at = oq * slots + (pos & (slots - 1u));
+    const bool ok = mine && oq < nq;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      store_b128<kSysAux>(v4u{o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]}, ro, ok ? at * 64u + 16u * k : kNoRun, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(meta, rm, ok ? at * 4u : kNoRun, 0, kSysAux);
+  }
+  __builtin_amdgcn_s_waitcnt(0);   // (the slots are in host memory before their chunk's count moves)
+  // pending counts: one system-scope subtraction per (entry plane, queue, chunk)
+  const uint32_t chunk = pos >> 6;
+  rem = __ballot(fin);
+  while (rem) {
+    const int leader = __builtin_ctzll(rem);
+    const uint32_t K0 = __builtin_amdgcn_readlane(origin, leader), K1 = __builtin_amdgcn_readlane(chunk, leader);
+    const unsigned long long bm = __ballot(fin && origin == K0 && chunk == K1);
+    rem &= ~bm;
+    const uint32_t O = K0 & 0xFFu, Q = K0 >> 8;
+    const uint32_t nch = (a.xpeers[O].ring_mask + 1u) >> 6;
+    if (lane == 0 && Q < a.xpeers[O].nq)
+      __hip_atomic_fetch_sub(a.xpeers[O].xpend + (size_t)Q * nch + (K1 & (nch - 1u)), (uint32_t)__builtin_popcountll(bm),
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  // entries consumed (a producer a ring later may reuse them), counters of this plane
+  if (rdy) __hip_atomic_store(&en->seq, (idx + 1ull) | kXferDone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (rdy && !(a.flags_bits & kRingNoCounters)) {
+    if (e.reason) atomicAdd(a.drop_ctr + (e.reason & (kNumReasons - 1)), 1ull);
+    else if (e.out_port < (uint32_t)kMaxPorts) atomicAdd(a.port_ctr + 2 * e.out_port + 1, ctr_inc(olen));
+  }
+}
+
+// The inbox service of an XF grid (its last xfer_wgs workgroups; every wave on its own): claim an
+// inbox chunk of 64 entries by ticket, resume each entry as soon as its seq says it is written, and
+// take the next ticket once all 64 are done.  Exits on the stop word (queue 0's, mirrored by its
+// frontier wave) or the device deadline.
+template <bool COOP>
+__device__ __forceinline__ void xfer_serve(const RingArgs& a, uint32_t lane, unsigned long long t_begin) {
+  XferInbox* ib = a.xpeers[a.xplane].inbox;
+  XferEntry* ent = a.xpeers[a.xplane].entries;
+  const uint32_t cmask = a.xpeers[a.xplane].cap_mask;
+  uint32_t seen_ep = 0xFFFFFFFFu;
+  for (;;) {
+    unsigned long long tk = 0;
+    if (lane == 0) tk = __hip_atomic_fetch_add(&ib->claim, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    tk = rfl64(tk);
+    const unsigned long long idx = tk * 64ull + lane;
+    XferEntry* en = ent + (idx & cmask);
+    bool done = false;
+    for (;;) {
+      const unsigned long long sq = __hip_atomic_load(&en->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      done = done || sq == ((idx + 1ull) | kXferDone);   // (consumed before a restart of this grid)
+      const bool rdy = !done && sq == idx + 1ull;
+      const unsigned long long rb = __ballot(rdy);
+      if (rb) {
+        xfer_resume<COOP>(a, rdy, en, idx, lane, t_begin, seen_ep);
+        done = done || rdy;
+      }
+      if (__ballot(!done) == 0ull) break;   // the ticket's 64 entries are handled
+      if (!rb) {
+        unsigned long long v = 0;
+        if (lane == 0) v = __hip_atomic_load(&a.st->dprod, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (rfl64(v) & kRingStop) return;
+        if (__builtin_amdgcn_s_memrealtime() - t_begin > a.deadline) return;
+        __builtin_amdgcn_s_sleep(2);
+      }
+    }
+  }
+}
+
 // COOP = false: the 4 waves of a workgroup claim and process chunks independently (throughput).
 // COOP = true (latency): the workgroup processes ONE chunk at a time — wave 0 claims and polls,
 // all 4 waves parse the chunk and each scans a quarter of the ACL rule tiles on its own SIMD
@@ -348,8 +542,16 @@ __device__ __forceinline__ void gde_deliver(const RingArgs& a, RingDevState* qst
 // carries kKeyV6 there and takes no flow / ACL part).
 // GDE: the GPU-direct egress instances (gde_deliver in the chunk's tail; 2 waves / SIMD, <= 256
 // registers); the others keep the ring's code and register allocation as they were without it.
-template <int HASH, int ACL, bool COOP, bool V6 = false, bool GDE = false>
-__global__ __launch_bounds__(kRingBlock, GDE ? 2 : 1) void ring_kernel(RingArgs a) {
+// XF: the instances for split chains across the node's GPU planes (hand-offs sent to the next
+// plane's inbox; the grid's last xfer_wgs workgroups serve this plane's inbox).
+template <int HASH, int ACL, bool COOP, bool V6 = false, bool GDE = false, bool XF = false>
+__global__ __launch_bounds__(kRingBlock, (GDE || XF) ? 2 : 1) void ring_kernel(RingArgs a) {
+  if constexpr (XF) {
+    if (blockIdx.x >= gridDim.x - a.xfer_wgs) {   // (block-uniform: the whole workgroup serves the inbox)
+      xfer_serve<COOP>(a, threadIdx.x & 63u, __builtin_amdgcn_s_memrealtime());
+      return;
+    }
+  }
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ unsigned long long coop_tk;                      // ticket
   __shared__ uint32_t coop_ctl[4];                            // go, epoch, table-set serial, ctl gen
@@ -628,7 +830,8 @@ __global__ __launch_bounds__(kRingBlock, GDE ? 2 : 1) void ring_kernel(RingArgs 
       }
     }
     NFDP_RING_MARK(tr2)
-    const EgressDecision e = chain_stage<LdsTables, V6, false>(T, ta, p, st, hit, act, acl_rule, hash);
+    EgressDecision e = chain_stage<LdsTables, V6, XF>(T, ta, p, st, hit, act, acl_rule, hash);
+    if constexpr (XF) xfer_check(e, a.nplanes);
     const uint32_t olen = egress_len(p, e);
     uint32_t o[kSlotDwords];
     emit(p, e.tci, e.push != 0, o);
@@ -639,6 +842,19 @@ __global__ __launch_bounds__(kRingBlock, GDE ? 2 : 1) void ring_kernel(RingArgs 
                   e.out_port, olen, o, meta, kx);
     wave_frames_store<kSysAux>(kx, o, r_out, run);
     __builtin_amdgcn_raw_buffer_store_b32(meta, r_meta, i * 4u, 0, kSysAux);
+    if constexpr (XF) {   // split chains: frames handed to another plane's grid (ring.h XferEntry)
+      const bool xf = !pad && e.reason == kRemote;
+      const unsigned long long bx = __ballot(xf);
+      if (bx) {
+        __builtin_amdgcn_s_waitcnt(0);   // (the resumer's stores into these slots land after ours)
+        if (lane == 0)
+          __hip_atomic_store(a.xpend + (size_t)qi * nch_q + (tk32 & nch_mask), (uint32_t)__builtin_popcountll(bx),
+                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __builtin_amdgcn_s_waitcnt(0);   // the count is in place before any resumer can lower it
+        xfer_send(a, xf, e.out_port, o, hop_state_of(p, st, e, act, acl_rule, hash), a.xplane | (qi << 8), i, lane,
+                  t_begin);
+      }
+    }
     if (a.side.cnt) {
       // flood / mirror / ARP-trap / learning / tunnel packets go on the side list; the host runs
       // the side pass over them once the chunk's flag is seen (before the flag: vmcnt covers it)
@@ -689,16 +905,16 @@ __global__ __launch_bounds__(kRingBlock, GDE ? 2 : 1) void ring_kernel(RingArgs 
   on_idle();  // exit: whatever this wave counted since its last flush reaches the global table
 }
 
-template <int H, int A, bool C, bool V6 = false, bool G = false>
+template <int H, int A, bool C, bool V6 = false, bool G = false, bool X = false>
 static hipError_t launch_ring_t(const RingArgs& a, int num_cus, int wgs, hipStream_t s) {
   const size_t lds = ring_lds(H, A, C ? a.lds_tiles : a.acl_tiles).total;
   if (lds > 64 * 1024) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&ring_kernel<H, A, C, V6, G>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&ring_kernel<H, A, C, V6, G, X>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
   if ((lds + 2048) * (size_t)wgs > 160 * 1024) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((ring_kernel<H, A, C, V6, G>), dim3((uint32_t)(num_cus * wgs)), dim3(kRingBlock), lds, s, a);
+  hipLaunchKernelGGL((ring_kernel<H, A, C, V6, G, X>), dim3((uint32_t)(num_cus * wgs)), dim3(kRingBlock), lds, s, a);
   return hipGetLastError();
 }
 
@@ -728,6 +944,11 @@ hipError_t launch_ring(const RingLaunch& r, const LaunchCfg& cfg, int wgs_per_cu
   a.ctrl = r.ctrl;
   a.faddr = reinterpret_cast<const unsigned long long*>(r.faddr);
   a.gde = r.gde;
+  a.xpeers = r.xpeers;
+  a.xplane = r.xplane;
+  a.nplanes = r.nplanes;
+  a.xfer_wgs = r.xpeers ? r.xfer_wgs : 0u;
+  a.xpend = r.xpend;
   a.nq = r.queues ? r.queues : 1u;
   // every queue needs a workgroup; the side list indexes slots of one ring only
   if ((uint64_t)cfg.num_cus * (uint64_t)wgs_per_cu < a.nq || (a.nq > 1 && a.side.cnt)) return hipErrorInvalidValue;
@@ -740,6 +961,17 @@ hipError_t launch_ring(const RingLaunch& r, const LaunchCfg& cfg, int wgs_per_cu
   if (cfg.hash_mode == kHashLds && !a.toep_tab) return hipErrorInvalidValue;
   if (wgs_per_cu < 1 || wgs_per_cu > 8 || cfg.num_cus < 1) return hipErrorInvalidValue;
   const int h = cfg.hash_mode, ac = cfg.acl_mode;
+  if (a.xpeers) {   // split chains across planes: the XF instances (IPv4 tables, MFMA ACL, no GDE)
+    if (ac != kAclMfma || h == kHashScalar || a.gde || v6_keys(a.t)) return hipErrorNotSupported;
+    if (!a.xpend || a.xfer_wgs == 0 || a.nplanes == 0 || a.nplanes > kMaxXferPlanes || a.xplane >= a.nplanes ||
+        (uint64_t)cfg.num_cus * (uint64_t)wgs_per_cu < (uint64_t)a.nq + a.xfer_wgs)
+      return hipErrorInvalidValue;
+#define NFDP_XCASE(HH, CC) \
+    if (h == HH && coop == CC) return launch_ring_t<HH, kAclMfma, CC, false, false, true>(a, cfg.num_cus, wgs_per_cu, s);
+    NFDP_XCASE(kHashLds, true) NFDP_XCASE(kHashLds, false) NFDP_XCASE(kHashMfma, true) NFDP_XCASE(kHashMfma, false)
+#undef NFDP_XCASE
+    return hipErrorInvalidValue;
+  }
   if (a.gde) {   // GPU-direct egress: its instances (LDS or MFMA hash, MFMA ACL, IPv4 or IPv6 tables)
     if (ac != kAclMfma || h == kHashScalar) return hipErrorNotSupported;
     const bool v6 = v6_keys(a.t);
@@ -808,7 +1040,7 @@ RingEngine::RingEngine(uint32_t capacity, int num_cus, int wgs_per_cu, bool coop
   auto slot_alloc = [&](void** p, size_t bytes, const char* what) {
     if (host_slots_) {
       void* h = nullptr;
-      ck(hipHostMalloc(&h, bytes, hipHostMallocCoherent | hipHostMallocMapped), what);
+      ck(hipHostMalloc(&h, bytes, hipHostMallocCoherent | hipHostMallocMapped | hipHostMallocPortable), what);
       std::memset(h, 0, bytes);
       ck(hipHostGetDevicePointer(p, h, 0), what);
       host_ptrs_.push_back(h);
@@ -848,7 +1080,10 @@ RingEngine::~RingEngine() {
   } catch (...) {
   }
   release_streams();
-  for (void* d : {(void*)st_, (void*)d_svc_, (void*)dd_sets_, (void*)d_gde_}) (void)hipFree(d);
+  for (void* d : {(void*)st_, (void*)d_svc_, (void*)dd_sets_, (void*)d_gde_, (void*)d_xin_, (void*)d_xent_,
+                  (void*)d_xpeers_})
+    (void)hipFree(d);
+  if (h_xpend_) (void)hipHostFree(h_xpend_);
   (void)hipHostFree(h_sets_);
   if (host_slots_) {
     for (void* h : host_ptrs_) (void)hipHostFree(h);
@@ -917,6 +1152,35 @@ void RingEngine::start(const FusedLaunch& f, const LaunchCfg& cfg, double deadli
   r.deadline_ticks = (unsigned long long)(deadline_s * 1e8);  // s_memrealtime: 100 MHz
   r.flows_alt = flows_alt;
   r.gde = d_gde_;
+  xfer_active_ = false;
+  if (d_xin_ && d_xpeers_ && !v6_keys(f.t)) {   // (IPv6 tables: the V6 instances, hand-offs run in place)
+    // the inbox as the previous session left it: peers may already be sending again, so nothing is
+    // reset - the tickets restart at the first entry not yet consumed (the consumer counts the
+    // consumed ones of that chunk as done by their seq)
+    XferInbox h{};
+    ck(hipMemcpyAsync(&h, d_xin_, sizeof(h), hipMemcpyDeviceToHost, stream_), "xfer inbox");
+    ck(hipStreamSynchronize(stream_), "xfer inbox");
+    uint64_t first = h.tail;
+    if (h.tail) {
+      const uint64_t lo = h.tail > xcap_ ? h.tail - xcap_ : 0;
+      std::vector<XferEntry> ents(xcap_);
+      ck(hipMemcpyAsync(ents.data(), d_xent_, (size_t)xcap_ * sizeof(XferEntry), hipMemcpyDeviceToHost, stream_),
+         "xfer entries");
+      ck(hipStreamSynchronize(stream_), "xfer entries");
+      for (uint64_t i = lo; i < h.tail; ++i)
+        if (ents[i & (xcap_ - 1)].seq != ((i + 1) | kXferDone)) { first = i; break; }
+    }
+    const uint64_t claim = first / 64;
+    ck(hipMemcpyAsync(reinterpret_cast<uint8_t*>(d_xin_) + offsetof(XferInbox, claim), &claim, 8, hipMemcpyHostToDevice,
+                      stream_), "xfer claim");
+    ck(hipStreamSynchronize(stream_), "xfer claim");
+    r.xpeers = d_xpeers_;
+    r.xplane = xplane_;
+    r.nplanes = nplanes_;
+    r.xfer_wgs = xwgs_;
+    r.xpend = d_xpend_;
+    xfer_active_ = true;
+  }
   ck(launch_ring(r, cfg, wgs_, coop_, stream_), "launch");
   set_running(true);
 }
@@ -974,6 +1238,79 @@ std::vector<uint64_t> RingEngine::gde_stats() {
     v.push_back(x.gde_full);
   }
   return v;
+}
+
+// ---- SFC hops across GPUs (ring.h XferEntry) -----------------------------------------------------
+void RingEngine::xfer_enable(uint32_t entries, uint32_t wgs) {
+  if (running_) throw std::runtime_error("ring: xfer_enable while running");
+  for (void* d : {(void*)d_xin_, (void*)d_xent_, (void*)d_xpeers_}) (void)hipFree(d);
+  if (h_xpend_) (void)hipHostFree(h_xpend_);
+  d_xin_ = nullptr; d_xent_ = nullptr; d_xpeers_ = nullptr; h_xpend_ = d_xpend_ = nullptr;
+  xcap_ = xwgs_ = nplanes_ = 0;
+  if (!entries) return;
+  if (entries < 64 || (entries & (entries - 1)) || entries > (1u << 22))
+    throw std::invalid_argument("ring: inbox entries must be a power of two in [64, 2^22]");
+  if (wgs < 1 || (uint64_t)num_cus_ * wgs_ < (uint64_t)nq_ + wgs)
+    throw std::invalid_argument("ring: inbox workgroups leave a queue without a workgroup");
+  ck(hipMalloc(reinterpret_cast<void**>(&d_xin_), sizeof(XferInbox)), "alloc inbox");
+  ck(hipMalloc(reinterpret_cast<void**>(&d_xent_), (size_t)entries * sizeof(XferEntry)), "alloc inbox entries");
+  ck(hipMemset(d_xin_, 0, sizeof(XferInbox)), "memset inbox");
+  ck(hipMemset(d_xent_, 0, (size_t)entries * sizeof(XferEntry)), "memset inbox entries");
+  ck(hipHostMalloc(reinterpret_cast<void**>(&h_xpend_), (size_t)nq_ * nch_ * 4,
+                   hipHostMallocCoherent | hipHostMallocMapped | hipHostMallocPortable), "host alloc xpend");
+  std::memset(h_xpend_, 0, (size_t)nq_ * nch_ * 4);
+  ck(hipHostGetDevicePointer(reinterpret_cast<void**>(&d_xpend_), h_xpend_, 0), "device ptr xpend");
+  xcap_ = entries;
+  xwgs_ = wgs;
+}
+
+RingEngine::XferDesc RingEngine::xfer_desc() const {
+  if (!d_xin_) throw std::runtime_error("ring: cross-GPU hops are off (xfer_enable)");
+  XferDesc d;
+  d.inbox = reinterpret_cast<uint64_t>(d_xin_);
+  d.entries = reinterpret_cast<uint64_t>(d_xent_);
+  // the out slots / metas / pending words as any GPU reaches them (pinned host memory: one address
+  // for every agent; HBM slots: this device's, reached over xGMI with peer access)
+  d.out = reinterpret_cast<uint64_t>(host_slots_ ? host_ptrs_[2] : (void*)d_out_);
+  d.out_meta = reinterpret_cast<uint64_t>(host_slots_ ? host_ptrs_[3] : (void*)d_meta_);
+  d.xpend = reinterpret_cast<uint64_t>(h_xpend_);
+  d.cap = xcap_;
+  d.ring_mask = cap_ - 1;
+  d.nq = nq_;
+  return d;
+}
+
+void RingEngine::xfer_set_peers(uint32_t my_plane, const std::vector<XferDesc>& planes) {
+  if (running_) throw std::runtime_error("ring: xfer_set_peers while running");
+  if (!d_xin_) throw std::runtime_error("ring: cross-GPU hops are off (xfer_enable)");
+  if (planes.empty() || planes.size() > kMaxXferPlanes || my_plane >= planes.size())
+    throw std::invalid_argument("ring: 1..16 planes, this one among them");
+  std::vector<XferPeer> v(planes.size());
+  for (size_t k = 0; k < planes.size(); ++k) {
+    const XferDesc& d = planes[k];
+    if (!d.inbox || !d.entries || !d.out || !d.out_meta || !d.xpend || d.cap < 64 || (d.cap & (d.cap - 1)) ||
+        d.ring_mask < 63 || ((d.ring_mask + 1) & d.ring_mask) || d.nq < 1)
+      throw std::invalid_argument("ring: bad plane descriptor");
+    v[k] = XferPeer{reinterpret_cast<XferInbox*>(d.inbox), reinterpret_cast<XferEntry*>(d.entries), d.cap - 1,
+                    d.ring_mask, reinterpret_cast<uint4*>(d.out), reinterpret_cast<uint32_t*>(d.out_meta),
+                    reinterpret_cast<uint32_t*>(d.xpend), d.nq, 0u};
+  }
+  if (planes[my_plane].inbox != reinterpret_cast<uint64_t>(d_xin_))
+    throw std::invalid_argument("ring: my_plane's descriptor is not this ring's");
+  if (d_xpeers_) (void)hipFree(d_xpeers_);
+  d_xpeers_ = nullptr;
+  ck(hipMalloc(reinterpret_cast<void**>(&d_xpeers_), sizeof(XferPeer) * v.size()), "alloc peers");
+  ck(hipMemcpy(d_xpeers_, v.data(), sizeof(XferPeer) * v.size(), hipMemcpyHostToDevice), "peers");
+  xplane_ = my_plane;
+  nplanes_ = (uint32_t)v.size();
+}
+
+std::vector<uint64_t> RingEngine::xfer_stats() {
+  if (running_) throw std::runtime_error("ring: xfer_stats while running");
+  if (!d_xin_) return {};
+  XferInbox h{};
+  ck(hipMemcpy(&h, d_xin_, sizeof(h), hipMemcpyDeviceToHost), "inbox stats");
+  return {h.tail, h.claim};
 }
 
 uint64_t RingEngine::gde_clear(uint32_t port, uint32_t q) {
@@ -1075,7 +1412,11 @@ void RingEngine::release_streams() {
 }
 
 bool RingEngine::chunk_done(uint64_t chunk, uint32_t q) const {
-  return __atomic_load_n(&flags_[(size_t)q * nch_ + (chunk & (nch_ - 1))], __ATOMIC_ACQUIRE) == (uint32_t)(chunk + 1);
+  const size_t w = (size_t)q * nch_ + (chunk & (nch_ - 1));
+  if (__atomic_load_n(&flags_[w], __ATOMIC_ACQUIRE) != (uint32_t)(chunk + 1)) return false;
+  // split chains across planes: the chunk's handed-off frames are back (the count was stored
+  // before the flag, and each resumer subtracts after its slot stores)
+  return !h_xpend_ || __atomic_load_n(&h_xpend_[w], __ATOMIC_ACQUIRE) == 0u;
 }
 
 uint64_t RingEngine::completed(uint32_t q) {
@@ -1089,8 +1430,10 @@ uint64_t RingEngine::completed(uint32_t q) {
   // without these two rules it would stall more than a ring behind and never catch up.
   if (Q.floor + nch_ < end) Q.floor = end - nch_;
   while (Q.floor < end) {
-    const uint32_t v = __atomic_load_n(&flags_[(size_t)q * nch_ + (Q.floor & (nch_ - 1))], __ATOMIC_ACQUIRE);
+    const size_t w = (size_t)q * nch_ + (Q.floor & (nch_ - 1));
+    const uint32_t v = __atomic_load_n(&flags_[w], __ATOMIC_ACQUIRE);
     if ((int32_t)(v - (uint32_t)(Q.floor + 1)) < 0) break;
+    if (v == (uint32_t)(Q.floor + 1) && h_xpend_ && __atomic_load_n(&h_xpend_[w], __ATOMIC_ACQUIRE) != 0u) break;
     ++Q.floor;
   }
   return Q.floor * 64;

@@ -45,7 +45,7 @@ def build_vsp(a, pm: PathManager):
                       hash_mode=cfg.hash_mode, acl_mode=cfg.acl_mode,
                       state_dir=a.state_dir or cfg.vsp_state_dir or None, nl=nl, live=a.live,
                       live_engine=a.live_engine, gpus=a.gpus if a.gpus == "all" else int(a.gpus),
-                      vport_kind=a.vport_kind or cfg.vport_kind, tx_workers=a.io_workers or cfg.io_workers,
+                      vport_kind=a.vport_kind or cfg.vport_kind, tx_workers=cfg.io_workers if a.io_workers < 0 else a.io_workers,
                       io_queues=a.io_queues or cfg.io_queues, placement=a.placement,
                       uplink=(a.uplink or cfg.uplink) if a.live else None)
     from ..cni.netlink import RtNetlink
@@ -76,7 +76,7 @@ def build_vsp(a, pm: PathManager):
         from ..dataplane.native_io import NativeLivePath
 
         cfg = node_config()
-        return NativeLivePath(dp, {}, tx_workers=a.io_workers or cfg.io_workers,
+        return NativeLivePath(dp, {}, tx_workers=cfg.io_workers if a.io_workers < 0 else a.io_workers,
                               queues=a.io_queues or cfg.io_queues).start()
 
     if a.vendor == "marvell":
@@ -150,8 +150,9 @@ def parse_args(argv=None):
                          "netdevs or shared-memory (memif) regions; default: node config vport_kind (veth)")
     ap.add_argument("--io-queues", type=int, default=0,
                     help="native engine rx queues (threads), each with a ring queue on every GPU (0: node config)")
-    ap.add_argument("--io-workers", type=int, default=0,
-                    help="native engine delivery threads per queue (0: node config)")
+    ap.add_argument("--io-workers", type=int, default=-1,
+                    help="native engine delivery threads per queue (0: run to completion, the rx threads deliver; "
+                         "-1: node config)")
     ap.add_argument("--metrics-bind-address", default="", help="amd-gpu: data-plane /metrics address (off if empty)")
     ap.add_argument("--agent-mbox", default="", help="amd-gpu: run the node control agent on this mailbox path")
     ap.add_argument("--agent-config", default="", help="agent SoC config file (default: one PF + --agent-vfs VFs)")

@@ -38,11 +38,14 @@ class NodeConfig:
     vsp_state_dir: str = ""            # journal + snapshots (checkpoint/resume); "" = off
     # live data path of the GPU VSP (vsp/gpu.py, dataplane/native_io.py)
     vport_kind: str = "veth"           # veth (kernel netdev pods, AF_PACKET rings) | memif | tap
-    io_queues: int = 4                 # native engine rx queues (threads), each with a ring queue per GPU
-    io_workers: int = 2                # native engine delivery threads per queue (4 x 2: 57.9 Mpps, r4 s4)
+    io_queues: int = 6                 # native engine rx queues (threads), each with a ring queue per GPU
+    # native engine delivery threads per queue; 0 = run to completion (each rx thread completes and
+    # delivers its own bursts: one busy thread per queue).  On the GPU box (16 CPUs granted) 6 x 0
+    # with 8 pod threads: 91-98 Mpps, 4 x 2: 45-59 (r6 s3 / s4, profiles/r6_s*_live_*.jsonl)
+    io_workers: int = 0
     # GPU-direct egress: the ring grids write frames for memif vports into the pods' rings themselves
-    # (ring.h GdeRing).  Off by default: on the GPU box it measured 42-57 Mpps against 56-58 for the
-    # tx threads (r5 s14 interleaved A/B), so it pays only where host CPUs are scarcer than that.
+    # (ring.h GdeRing).  Off by default: each queue's chunks commit in ticket order over PCIe (~11
+    # Mpps per queue); with run-to-completion engine threads it measured 73 vs 97 Mpps (r6 s4).
     gpu_egress: bool = False
     # the GPU node's wire port (data-plane port `wire_port`, the reference's RPM / SFP uplink):
     #   "veth"  a veth pair whose host end (`uplink_host_ifname`) the node's stack or a host bridge

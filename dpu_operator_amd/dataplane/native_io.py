@@ -272,6 +272,7 @@ class NativeLivePath:
         self._ports: dict[int, object] = {}
         self._rings = []
         self._backends = []
+        self.xfer = False               # rings wired for cross-GPU hops (_wire_xfer)
         self._sup: threading.Thread | None = None
         self._stop = threading.Event()
         self._totals: dict[str, int] = {}
@@ -310,8 +311,7 @@ class NativeLivePath:
                                     cus=self.ring_cus or max(1, int(dp.num_cus) // share))
                     ring.eng.set_frame_addrs(self.zero_copy)
                     ring.eng.gde_enable(self.gpu_egress)
-                    ring.start()
-                self._rings.append(ring)
+                self._rings.append(ring)   # (started below, after the cross-GPU hop wiring)
                 be = nf.GpuBackend(ring.eng)
             else:
                 be = nf.OracleBackend(self.capacity, self.queues)
@@ -321,6 +321,13 @@ class NativeLivePath:
             if self not in getattr(dp, "_io_hooks", []):
                 dp._io_hooks = getattr(dp, "_io_hooks", []) + [self]
             dp._learned_on_device = True     # the engine learns into the device MAC table: commits pull first
+        if self.gpu:
+            self._wire_xfer()
+            import torch
+
+            for ring in self._rings:
+                with torch.cuda.device(ring.dp.tdev):
+                    ring.start()
         # replica counters appear in the first plane's counters (a MultiDataPlane sums its planes)
         eng.set_zero_copy(self.zero_copy)
         eng.set_gpu_egress(self.gpu_egress)
@@ -344,6 +351,32 @@ class NativeLivePath:
         self._applied = {}   # a new engine holds no configuration yet
         self._refresh()
         eng.start()
+
+    # SFC hops across GPUs (ring.h XferEntry): with two or more GPU planes, every ring gets an inbox
+    # that the other planes' grids hand split-chain frames to, and its grid resumes them there and
+    # stores the final header straight into the entry ring's out slot; the engine delivers a burst
+    # once every frame of it is back (no host hop, no launch).  Not with GPU-direct egress (its
+    # instances do not hand off) nor IPv6 tables (the V6 instances run a split chain where it entered).
+    XFER_ENTRIES = 1 << 15
+
+    def _wire_xfer(self) -> None:
+        self.xfer = len(self._rings) > 1 and not self.gpu_egress
+        if not self.xfer:
+            return
+        devs = sorted({int(r.dp.tdev.index or 0) for r in self._rings})
+        for a in devs:
+            for b in devs:
+                if a != b and not self.nf.enable_peer_access(a, b):
+                    raise RuntimeError(f"cuda:{a} cannot store into cuda:{b}'s memory (no peer access)")
+        for r in self._rings:
+            r.eng.xfer_enable(self.XFER_ENTRIES, 1)
+        descs = [r.eng.xfer_desc() for r in self._rings]
+        for k, r in enumerate(self._rings):
+            r.eng.xfer_set_peers(k, descs)
+
+    def xfer_active(self) -> list[bool]:
+        """Per plane: its running grid hands split-chain frames to the next plane (XF instance)."""
+        return [bool(r.eng.xfer_active) for r in self._rings]
 
     def stop(self) -> None:
         self._stop.set()

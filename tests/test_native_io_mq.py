@@ -716,3 +716,47 @@ def test_cpulist_and_lane_group_pinning(shm):
             assert sorted(got[port]) == sorted(frames), port
     finally:
         live.stop()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("placement,split,whole", [
+    ("port", ("acl", "nat", "l2fwd@1"), ("acl", "nat", "l2fwd")),
+    ("flow", ("acl", "nat@1", "ttl@0", "l2fwd@1"), ("acl", "nat", "ttl", "l2fwd")),
+])
+def test_split_chain_live_crosses_planes(shm, placement, split, whole):
+    """SFC hops across GPUs in the LIVE path (ring.h XferEntry): two ring planes behind one engine,
+    a chain whose hops sit on both.  Each frame's first hops run on the plane it entered, the rest
+    on the other plane's resident grid (its inbox), which stores the final header into the entry
+    ring's out slot; the engine delivers the burst once every frame is back.  Frames equal the
+    whole chain on one plane; summed port counters too (tx counted where the chain ended); the
+    drops equal one plane's besides the hand-offs.  The second case crosses twice (0 -> 1 -> 0 -> 1
+    for frames entering on plane 0)."""
+    nf = nfdp()
+    m = MultiDataPlane(["cuda:0", "cuda:0"], placement=placement, flow_buckets=1 << 12)
+    sc = S.build_sfc(m, n_pods=6, n_flows=4096, n_acl=64, seed=0, hops=split)
+    m.commit(full=True)
+    ref = DataPlane(device="cpu", flow_buckets=1 << 12)
+    S.build_sfc(ref, n_pods=6, n_flows=4096, n_acl=64, seed=0, hops=whole)
+    ref.commit(full=True)
+    slots, im = S.traffic(sc, 3000, seed=11)
+    exp, drops = _expected(ref, slots, im)
+    paths = {int(p): str(shm / f"x{int(p)}") for p in sc.pod_port}
+    live = NativeLivePath(m, {p: MemifVport(paths[p], ring_size=4096) for p in paths}, burst=128,
+                          ring_capacity=1024, queues=2).start()
+    try:
+        assert live.xfer and live.xfer_active() == [True, True]
+        eps = _send_all(nf, paths, slots, im, list(paths))
+        got, done = _collect(eps, sum(map(len, exp.values())))
+        assert _until(done), (live.stats, live.error)
+        for port, frames in exp.items():
+            assert sorted(got[port]) == sorted(frames), port
+        assert live.error is None
+        assert _until(lambda: np.array_equal(m.port_counters(), ref.port_counters()), 2.0), \
+            (m.port_counters()[sc.pod_port].tolist(), ref.port_counters()[sc.pod_port].tolist())
+        d1, d2 = ref.drop_counters(), m.drop_counters()
+        assert d2.pop("remote", 0) >= int(sum(map(len, exp.values())))   # every forwarded frame crossed
+        assert d1 == d2, (d1, d2)
+    finally:
+        live.stop()
+    st = [r.eng.xfer_stats() for r in live._rings] if live._rings else None
+    assert st is None or all(len(x) == 2 for x in st)
