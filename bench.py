@@ -124,6 +124,32 @@ def _unsteered(a, dp, sc, owner, rank, world, dev, cdev, torch, dist, P, RssShar
     return res
 
 
+SCALE_KEYS = ("world_size", "backend", "rccl_version", "device_count", "local_devices", "per_rank_ms_per_step",
+              "step_skew", "peer_access")
+
+
+def scale_info(dist, torch, elapsed_s: float, steps: int, cdev) -> dict:
+    """What the N > 1 run actually ran on (every rank calls it; a collective): the process group's
+    size and backend, the RCCL version torch carries, the GPUs this node shows, every rank's own
+    timed-loop ms per step (the headline takes the max) and the peer-access matrix of the local
+    GPUs (the hop pipeline's peer stores need it).  Works under gloo on the CPU as well."""
+    world = dist.get_world_size()
+    mine = torch.tensor([elapsed_s / max(steps, 1) * 1e3], dtype=torch.float64, device=cdev)
+    allr = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(allr, mine)
+    per = [round(float(x.item()), 4) for x in allr]
+    try:
+        v = torch.cuda.nccl.version() if torch.cuda.is_available() else None
+        rccl = ".".join(str(x) for x in v) if isinstance(v, tuple) else (str(v) if v is not None else None)
+    except Exception:  # noqa: BLE001 - no RCCL in this build
+        rccl = None
+    n = torch.cuda.device_count() if torch.cuda.is_available() else 0
+    peer = [[bool(i == j or torch.cuda.can_device_access_peer(i, j)) for j in range(n)] for i in range(n)]
+    return {"world_size": world, "backend": str(dist.get_backend()), "rccl_version": rccl, "device_count": n,
+            "local_devices": n, "per_rank_ms_per_step": per,
+            "step_skew": round(max(per) / max(min(per), 1e-9), 4), "peer_access": peer}
+
+
 def measure_hops(a, devices: str) -> dict:
     """SFC hop pipeline across GPUs (BASELINE config 4): the headline chain split after nat - acl +
     nat on one data plane, l2fwd + egress on another - with the product's in-HBM hand-off
@@ -373,6 +399,29 @@ def measure_variants(a, dp, sc, dev, torch, S, P) -> dict:
     dp.ports.version += 1
     dp.commit()
     del b
+    # BASELINE config 5: the rule set the Intel IPU VSP programs (8 host VFs: AddHostVfP4Rules x 8,
+    # AddPeerToPeerP4Rules O(n^2), one NF: AddNFP4Rules; Init's phy-port / LAG / primary-network
+    # rules) through the P4Runtime compile onto a fresh data plane, then VF->VF, VF->NF, NF->wire
+    # and VF->OvS traffic of a 1M-5-tuple pool (dataplane/p4_scenario.py)
+    from dpu_operator_amd.dataplane import p4_scenario as Q
+    from dpu_operator_amd.dataplane.engine import DataPlane
+
+    d4 = DataPlane(device=str(dev), flow_buckets=1 << 10, hash_mode=a.hash, acl_mode=a.acl_mode)
+    q = Q.build(d4)
+    pk, im, exp, kind = Q.traffic(q, 1 << 20, seed=9600)
+    reps = max(1, n // (1 << 20))
+    b = [(torch.from_numpy(np.tile(pk, (reps, 1))).to(dev), torch.from_numpy(np.tile(im, reps).view(np.int32)).to(dev))]
+    el, meta = _time_fused(d4, b, a.variant_steps, torch)
+    port, _, rs = P.meta_fields(meta.cpu().numpy().view(np.uint32))
+    exp_t = np.tile(exp, reps)
+    res["p4_ipu_mpps"] = round(int(b[0][0].shape[0]) * a.variant_steps / el / 1e6, 1)
+    res["p4_ipu"] = {"host_vfs": len(q.vf_macs), "nf": 1, "p4_entries": q.n_entries, "tables": q.rules,
+                     "batch": int(b[0][0].shape[0]), "mix": {k: w for k, w in Q.MIX},
+                     "forwarded_fraction": round(float(np.mean(rs == 0)), 4),
+                     "expected_port_fraction": round(float(np.mean(port == exp_t)), 4),
+                     "note": "entries compiled from the Intel VSP's p4rt-ctl strings; 64-B frames, fused kernel"}
+    del b, d4
+    torch.cuda.empty_cache()
     return res
 
 
@@ -515,7 +564,9 @@ def main() -> None:
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    scale = None
     if world > 1:
+        scale = scale_info(dist, torch, elapsed, a.steps, cdev)
         t = torch.tensor([elapsed], dtype=torch.float64, device=cdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -750,6 +801,19 @@ def main() -> None:
                 curve.append({"queues": q, "mpps": r.get("mpps"), "p50_us": r.get("p50_us"),
                               "cpus_used": (r.get("cpu") or {}).get("process_cpus_used"), "error": r.get("error")})
             live["queue_curve"] = curve
+            # SFC hops across GPUs in the live path: the headline chain split after nat (acl, nat on
+            # the plane the frame entered, l2fwd on plane 1; ring.h XferEntry), two ring planes (the
+            # two GPUs when there are two, else both on this one: a rehearsal of the xGMI path)
+            import torch as _t
+
+            two = _t.cuda.device_count() > 1
+            sp = lb.run(device=str(dev), n_pods=a.pods_per_gpu, flows=a.flows, n_acl=a.acl, duration=0.5,
+                        threads=a.live_gen_threads, tx_workers=a.live_workers, queues=a.live_queues, hash_mode=a.hash,
+                        split="acl,nat,l2fwd@1", planes="cuda:0,cuda:1" if two else "")
+            live["split_chain"] = {k: sp.get(k) for k in ("split", "planes", "xfer_active", "mpps", "p50_us", "idle_p50_us",
+                                                          "idle_p99_us", "half_p50_us", "half_p99_us", "error")}
+            if sp.get("idle_p50_us") and live.get("idle_p50_us"):
+                live["split_chain"]["hop_handoff_us"] = round(sp["idle_p50_us"] - live["idle_p50_us"], 2)
             live["host_cpus"] = len(os.sched_getaffinity(0))
             live["cpu_share"] = share
             live["threads_busy"] = a.live_gen_threads + a.live_queues * (1 + a.live_workers)
@@ -807,6 +871,7 @@ def main() -> None:
             "value_ipv6": None if not variants else variants["ipv6_mpps"],
             "value_vxlan": None if not variants else variants["vxlan_mpps"],
             "value_vxlan_egress": None if not variants else variants["vxlan_egress_mpps"],
+            "value_p4_ipu": None if not variants else variants.get("p4_ipu_mpps"),
             "imix": None if not variants else variants["imix"],
             "variants": variants,
             # split chain over two data planes (one GPU): pipeline Mpps and per-hop latency
@@ -822,6 +887,8 @@ def main() -> None:
             "setup_s": round(setup_s, 1),
             "baseline_note": "reference publishes no numbers (BASELINE.md); 200GbE line rate at 64B = 297.6 Mpps",
         }
+        if scale is not None:
+            line["scale"] = scale   # what the N > 1 run ran on (SCALE_KEYS)
         if a.rehearse:
             line["rehearsal"] = "all ranks on cuda:0, gloo host-staged exchange: correctness only, not a measurement"
         print(json.dumps(line), flush=True)

@@ -223,3 +223,41 @@ def test_intel_ipu_vsp(dp):
         vsp.create_bridge_port(f"host0-{i}", bytes([0, 0x30 + i, 0, 0, 0, 1]), 0, ["3"])
     with pytest.raises(RuntimeError, match="not available"):
         vsp.create_bridge_port("host0-3", bytes([0, 0x40, 0, 0, 0, 1]), 0, ["3"])
+
+
+def test_ipu_rule_set_scenario_forwards_every_kind():
+    """BASELINE config 5 (dataplane/p4_scenario.py): the Intel VSP's rule set for 8 host VFs and one
+    NF, compiled by P4Runtime, forwards every kind of traffic it exists for to the right port."""
+    from dpu_operator_amd.dataplane import p4_scenario as Q
+
+    d = DataPlane(device="cpu", flow_buckets=1 << 10)
+    sc = Q.build(d)
+    assert sc.rules["vsi_to_vsi_loopback"] == 2 * 28 + 2 * 8 * 2 + 2 * 8 + 2 * 2   # p2p + NF x VF + host VF + NF PR
+    assert sc.rules["tx_source_port"] >= 8 and sc.n_entries > 150
+    slots, im, exp, kind = Q.traffic(sc, 1 << 14, seed=3)
+    r = d.run(slots, im)
+    port, _, reason = P.meta_fields(r.meta)
+    assert (reason == 0).all()
+    assert (port == exp).all()
+    assert set(np.unique(kind).tolist()) == set(range(len(Q.MIX)))
+
+
+@pytest.mark.gpu
+def test_ipu_rule_set_gpu_bit_exact():
+    """The same compiled rule set on the GPU: every frame's egress slot and meta equal the oracle's."""
+    import torch
+
+    from dpu_operator_amd.dataplane import p4_scenario as Q
+
+    g = DataPlane(device="cuda:0", flow_buckets=1 << 10)
+    c = DataPlane(device="cpu", flow_buckets=1 << 10)
+    sg, sc = Q.build(g), Q.build(c)
+    assert sg.rules == sc.rules
+    slots, im, exp, kind = Q.traffic(sc, 1 << 16, seed=5)
+    rg = g.run(torch.from_numpy(slots).cuda(), torch.from_numpy(im.view(np.int32)).cuda())
+    torch.cuda.synchronize()
+    rc = c.run(slots, im)
+    np.testing.assert_array_equal(rg.meta.cpu().numpy().view(np.uint32), rc.meta)
+    np.testing.assert_array_equal(rg.out.cpu().numpy(), rc.out)
+    port, _, reason = P.meta_fields(rc.meta)
+    assert (reason == 0).all() and (port == exp).all()

@@ -122,7 +122,7 @@ def run(device: str = "cuda", n_pods: int = 8, flows: int = 1 << 20, n_acl: int 
         hash_mode: str = "lds", tx_workers: int = 0, queues: int = 6, max_inflight_frames: int = 4096,
         pod_ring: int = 1024, backend: str = "pipeline", coalesce_us: float = 8.0, loaded_window: int = 2048,
         traffic: str = "plain", zero_copy: bool = False, saturated_only: bool = False, gpu_egress: bool = False,
-        trials: int = 1) -> dict:
+        trials: int = 1, split: str = "", planes: str = "") -> dict:
     """traffic: "plain" (the headline SFC), "vxlan-egress" (every pod's VF a VXLAN tunnel port:
     all frames leave encapsulated through one underlay vport, outer headers from the per-burst
     side pass) or "broadcast" (pods on one learning bridge sending to ff:ff:ff:ff:ff:ff: every
@@ -131,7 +131,10 @@ def run(device: str = "cuda", n_pods: int = 8, flows: int = 1 << 20, n_acl: int 
     regions (NativeLivePath zero_copy) instead of header copies in its slots.  trials: saturated
     runs of `duration` each; `mpps` is their median (`mpps_trials` all of them, each with the CPU
     time it cost), the saturated latencies those of the median trial.  tx_workers = 0: run to
-    completion (each queue's rx thread delivers its own bursts)."""
+    completion (each queue's rx thread delivers its own bursts).  split: the SFC's hops with
+    GPU placements, e.g. "acl,nat,l2fwd@1" (SFC hops across GPUs in the live path: two ring planes,
+    `planes` "cuda:0,cuda:1" or by default the device twice, flows sharded by owner; frames cross
+    to the other plane's grid mid-chain, ring.h XferEntry)."""
     nf = nfdp()
     t0 = time.perf_counter()
     d = tempfile.mkdtemp(prefix="dpu-live-", dir=memif_dir())
@@ -162,9 +165,17 @@ def run(device: str = "cuda", n_pods: int = 8, flows: int = 1 << 20, n_acl: int 
             pods.append((ports[i].path, fr, ln))
         flows, n_acl = 0, 0
     else:
-        dp = DataPlane(device=device, flow_buckets=max(1 << 12, 1 << int(np.ceil(np.log2(max(flows, 1) / 2)))),
-                       hash_mode=hash_mode if device != "cpu" else "mfma")
-        sc = S.build_sfc(dp, n_pods=n_pods, n_flows=flows, n_acl=n_acl, seed=0)
+        buckets = max(1 << 12, 1 << int(np.ceil(np.log2(max(flows, 1) / 2))))
+        if split:
+            from dpu_operator_amd.dataplane.multi import MultiDataPlane
+
+            devs = planes.split(",") if planes else [device, device]
+            dp = MultiDataPlane(devs, placement="flow", flow_buckets=buckets,
+                                hash_mode=hash_mode if device != "cpu" else "mfma")
+            sc = S.build_sfc(dp, n_pods=n_pods, n_flows=flows, n_acl=n_acl, seed=0, hops=tuple(split.split(",")))
+        else:
+            dp = DataPlane(device=device, flow_buckets=buckets, hash_mode=hash_mode if device != "cpu" else "mfma")
+            sc = S.build_sfc(dp, n_pods=n_pods, n_flows=flows, n_acl=n_acl, seed=0)
         underlay = S.install_vxlan_egress(dp, sc)["underlay"] if traffic == "vxlan-egress" else None
         dp.commit(full=True)
         ports = {int(sc.pod_port[i]): MemifVport(os.path.join(d, f"pod{i}"), ring_size=pod_ring) for i in range(n_pods)}
@@ -183,6 +194,8 @@ def run(device: str = "cuda", n_pods: int = 8, flows: int = 1 << 20, n_acl: int 
     stats = lambda: live.stats  # noqa: E731
     try:
         out = {"backend": backend, "traffic": traffic, "zero_copy": zero_copy, "device": device, "queues": queues, "coalesce_us": coalesce_us, "tx_workers": tx_workers, "inflight_bursts": inflight,
+               **({"split": split, "planes": [str(getattr(p, "tdev", "cpu")) for p in dp.planes],
+                   "xfer_active": live.xfer_active() if hasattr(live, "xfer_active") else None} if split else {}),
                "max_inflight_frames": max_inflight_frames, "pod_ring": pod_ring, "gen_threads": threads,
                "pods": n_pods, "flows": flows, "acl_rules": n_acl, "frame_bytes": 64,
                "setup_s": round(setup_s, 1)}
@@ -398,6 +411,8 @@ def main() -> None:
     ap.add_argument("--zero-copy", action="store_true", help="the ring reads frames in the pods' memif regions")
     ap.add_argument("--gpu-egress", action="store_true", help="the ring grid writes frames into the pods' rings itself")
     ap.add_argument("--trials", type=int, default=1, help="saturated runs (median reported)")
+    ap.add_argument("--split", default="", help='SFC hops with GPU placements, e.g. "acl,nat,l2fwd@1" (two planes)')
+    ap.add_argument("--planes", default="", help='--split: the planes\' devices, e.g. "cuda:0,cuda:1"')
     ap.add_argument("--veth", choices=("linux-bridge", "engine", "pipeline"), default=None,
                     help="netns pods on veth pairs, switched by a Linux bridge, by the native engine alone or by the "
                          "native engine in front of the data plane on --device (the deployed default)")
@@ -414,7 +429,8 @@ def main() -> None:
                          inflight=a.inflight, tx_workers=a.tx_workers, queues=a.queues,
                          max_inflight_frames=a.max_inflight_frames, pod_ring=a.pod_ring,
                          backend=a.backend, coalesce_us=a.coalesce_us, loaded_window=a.loaded_window,
-                         traffic=a.traffic, zero_copy=a.zero_copy, gpu_egress=a.gpu_egress, trials=a.trials)),
+                         traffic=a.traffic, zero_copy=a.zero_copy, gpu_egress=a.gpu_egress, trials=a.trials,
+                         split=a.split, planes=a.planes)),
           flush=True)
 
 
