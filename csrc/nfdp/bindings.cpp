@@ -895,6 +895,10 @@ PYBIND11_MODULE(_nfdp, m) {
   py::class_<PacketPort, Port, std::shared_ptr<PacketPort>>(m, "PacketPort")
       .def(py::init<const std::string&, uint32_t, uint32_t>(), py::arg("ifname"), py::arg("frames") = 1024,
            py::arg("frame_size") = 2048);
+  py::class_<XdpPort, Port, std::shared_ptr<XdpPort>>(m, "XdpPort")
+      .def(py::init<const std::string&, uint32_t, uint32_t, uint32_t>(), py::arg("ifname"), py::arg("frames") = 2048,
+           py::arg("frame_size") = 2048, py::arg("queue") = 0)
+      .def_property_readonly("native_mode", &XdpPort::native_mode);
   py::class_<FdPort, Port, std::shared_ptr<FdPort>>(m, "FdPort")
       .def(py::init<int, uint32_t, uint32_t>(), py::arg("fd"), py::arg("nbufs") = 256, py::arg("buf_size") = 9728);
   py::class_<Backend, std::shared_ptr<Backend>>(m, "IoBackend")
@@ -1164,7 +1168,7 @@ PYBIND11_MODULE(_nfdp, m) {
   // the same generator / sink for kernel-netdev pods (trafgen_pkt.h): pods are
   // (netns path, ifname, frames [k, stride] u8, lens [k] u32)
   m.def("trafgen_run_netns", [](py::list pods, double duration_s, double warmup_s, double rate_pps, uint32_t threads,
-                                uint32_t burst) {
+                                uint32_t burst, bool xdp) {
     std::vector<trafgen::NetPod> v;
     for (auto o : pods) {
       py::tuple t = o.cast<py::tuple>();
@@ -1185,7 +1189,7 @@ PYBIND11_MODULE(_nfdp, m) {
     trafgen::Result r;
     {
       py::gil_scoped_release nogil;
-      r = trafgen::run_netns(v, c);
+      r = trafgen::run_netns(v, c, xdp);
     }
     py::dict d;
     d["sent"] = r.sent; d["received"] = r.received; d["tx_full"] = r.tx_full; d["bad"] = r.bad;
@@ -1194,5 +1198,5 @@ PYBIND11_MODULE(_nfdp, m) {
     d["rx_per_pod"] = r.rx_per_pod; d["tx_per_pod"] = r.tx_per_pod;
     return d;
   }, py::arg("pods"), py::arg("duration_s") = 1.0, py::arg("warmup_s") = 0.1, py::arg("rate_pps") = 0.0,
-     py::arg("threads") = 1, py::arg("burst") = 32);
+     py::arg("threads") = 1, py::arg("burst") = 32, py::arg("xdp") = false);
 }

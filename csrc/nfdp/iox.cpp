@@ -548,7 +548,24 @@ void Engine::add_port(uint32_t id, std::shared_ptr<Port> p, int queue) {
     for (uint32_t k = 1; k < nq_; ++k)
       if (queues_[k]->nports.load() < queues_[q]->nports.load()) q = k;
   }
-  if (gde_.load()) gde_unregister(id);   // (a port replaced at this id)
+  if (gde_.load() && (*t)[id].p) {
+    // a port replaced at this id: its GPU egress entry off (applied by every grid), then every
+    // chunk published before the clear must be through - one that read the old entry could still
+    // be reserving in it and would advance the new entry's head over slots it never wrote
+    gde_unregister(id);
+    if (run_.load()) {
+      std::vector<uint64_t> heads(lanes_.size());
+      for (size_t k = 0; k < lanes_.size(); ++k) heads[k] = lanes_[k]->head.load(std::memory_order_acquire);
+      const auto t0 = Clock::now();
+      for (;;) {
+        bool done = true;
+        for (size_t k = 0; k < lanes_.size() && done; ++k) done = lanes_[k]->done.load(std::memory_order_acquire) >= heads[k];
+        if (done || !run_.load()) break;
+        if (Clock::now() - t0 > std::chrono::seconds(5)) throw std::runtime_error("iox: bursts before a port replacement did not finish");
+        std::this_thread::sleep_for(std::chrono::microseconds(50));
+      }
+    }
+  }
   if (zero_copy_.load()) map_port(*p);   // before any packet thread can see the port
   if (gde_.load()) gde_register(id, *p);
   reap_retired(false);

@@ -170,6 +170,52 @@ class Port {
 
 // Shared-memory vport (memif.h): the pod produces ring 0, the engine rings 1..tx_rings (tx
 // queue q writes ring 1 + q).
+// AF_XDP port on a netdev (the engine's end of a veth pair, or a NIC queue): an XSK socket with its
+// UMEM (rx frames handed to the kernel through the fill ring, tx frames from a free pool reclaimed
+// through the completion ring) and a 6-instruction XDP program, attached to the netdev through a
+// BPF link, that redirects every frame of queue 0 to the socket (bpf_redirect_map on an XSKMAP,
+// XDP_PASS when the socket is not there).  Frames reach the engine without an skb or a packet
+// socket, the way kernel-netdev pods that are not memif-aware can still be served in bulk.
+// Copy mode (veth has no zero-copy AF_XDP); native XDP when the driver has it, else generic.
+class XdpPort : public Port {
+ public:
+  XdpPort(const std::string& ifname, uint32_t frames, uint32_t frame_size = 2048, uint32_t queue = 0);
+  ~XdpPort() override;
+  uint32_t rx(RxRef* out, uint32_t max) override;
+  std::string kind() const override { return "af_xdp"; }
+  bool native_mode() const { return native_; }   // XDP in the driver (false: generic / skb mode)
+
+ protected:
+  bool tx_locked(uint32_t q, const uint8_t* a, uint32_t na, const uint8_t* b, uint32_t nb, const uint8_t* c,
+                 uint32_t nc) override;
+  void flush_locked(uint32_t q) override;
+  void release_to(uint32_t seq_end) override;
+
+ private:
+  struct Ring {                       // one mmapped AF_XDP ring (producer / consumer / descriptors)
+    uint32_t* prod = nullptr;
+    uint32_t* cons = nullptr;
+    uint32_t* flags = nullptr;
+    void* desc = nullptr;
+    void* map = nullptr;
+    size_t map_len = 0;
+    uint32_t mask = 0;
+  };
+  void reclaim_tx();                  // completion ring -> free tx frames
+  void kick_tx();                     // publish the tx ring and have the kernel send it all
+  void close_all();
+  int fd_ = -1, map_fd_ = -1, prog_fd_ = -1, link_fd_ = -1;
+  uint8_t* umem_ = nullptr;
+  size_t umem_len_ = 0;
+  uint32_t nframes_, fsize_;
+  Ring rx_, tx_, fill_, comp_;
+  std::vector<uint64_t> rx_addr_;     // by rx sequence number: the UMEM frame it holds
+  uint32_t rx_next_ = 0, rel_done_ = 0;
+  std::vector<uint64_t> tx_free_;     // tx frames the kernel gave back
+  uint32_t tx_prod_ = 0;              // private tx producer (published by flush)
+  bool native_ = false;
+};
+
 class MemifPort : public Port {
  public:
   MemifPort(const std::string& path, uint32_t ring_size, uint32_t buf_size, uint32_t tx_rings = 1);

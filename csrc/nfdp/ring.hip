@@ -201,16 +201,18 @@ __device__ __forceinline__ bool ring_wait_chunk(const RingArgs& a, RingCtl* ctl,
 //      next chunk may publish a later one, so a head never goes back.
 // Every access to the shared egress state is a relaxed agent-scope atomic (no fences: an acquire /
 // release would invalidate / write back the XCD's L2 - the flow table - per chunk).  A wave still
-// waiting for a turn at the device deadline goes ahead (the grid is exiting).
+// waiting for a turn at the device deadline (the grid is exiting) does not take it: the chunk's
+// frames stay with the host path, and no head moves without the turn.
 __device__ __forceinline__ bool gde_turn(uint64_t* turn, unsigned long long tk, uint32_t lane, const RingArgs& a,
                                          unsigned long long t_begin) {
+  uint32_t ok = 1u;
   if (lane == 0) {
     while (__hip_atomic_load(turn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != tk) {
-      if (__builtin_amdgcn_s_memrealtime() - t_begin > a.deadline) break;
+      if (__builtin_amdgcn_s_memrealtime() - t_begin > a.deadline) { ok = 0u; break; }
       __builtin_amdgcn_s_sleep(1);
     }
   }
-  return true;
+  return __builtin_amdgcn_readfirstlane(ok) != 0u;
 }
 __device__ __forceinline__ void gde_deliver(const RingArgs& a, RingDevState* qst, uint32_t qi, unsigned long long tk,
                                             uint32_t lane, unsigned long long t_begin, bool elig0, uint32_t port,
@@ -233,7 +235,8 @@ __device__ __forceinline__ void gde_deliver(const RingArgs& a, RingDevState* qst
            (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
   };
   const unsigned long long tw0 = __builtin_amdgcn_s_memrealtime();
-  gde_turn(&qst->gde_turn, tk, lane, a, t_begin);
+  const bool t_res = gde_turn(&qst->gde_turn, tk, lane, a, t_begin);
+  if (!t_res) elig = false;   // (deadline: nothing reserved, the turn is not ours to pass on)
   const unsigned long long tw1 = __builtin_amdgcn_s_memrealtime();
   // ---- 1. reserve ----
   bool go = false;
@@ -270,7 +273,7 @@ __device__ __forceinline__ void gde_deliver(const RingArgs& a, RingDevState* qst
     }
   }
   __builtin_amdgcn_s_waitcnt(0);   // the reservations are in memory before the next chunk reserves
-  if (lane == 0) __hip_atomic_store(&qst->gde_turn, tk + 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (lane == 0 && t_res) __hip_atomic_store(&qst->gde_turn, tk + 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const unsigned long long tw2 = __builtin_amdgcn_s_memrealtime();
   // ---- 2. frames and descriptors (parallel across chunks) ----
   // Each frame as ONE full 64-B line write: 16 frames per pass through the wave's LDS scratch, the
@@ -314,10 +317,13 @@ __device__ __forceinline__ void gde_deliver(const RingArgs& a, RingDevState* qst
     __builtin_amdgcn_raw_buffer_store_b64(dv, rd, mine ? pos * 8u : kNoRun, 0, kSysAux);
   }
   __builtin_amdgcn_s_waitcnt(0);   // (write-through stores done: the frames are in host memory)
-  if (go) meta = make_meta(port, kMetaLenGde, kOk);
   // ---- 3. commit: heads in ticket order ----
   const unsigned long long tw3 = __builtin_amdgcn_s_memrealtime();
-  gde_turn(&qst->gde_commit, tk, lane, a, t_begin);
+  const bool t_com = gde_turn(&qst->gde_commit, tk, lane, a, t_begin);
+  // (deadline: the slots written stay unpublished - the pod never sees them - and the host path
+  // delivers these frames: their meta is left as it was)
+  if (!t_com) go = false;
+  if (go) meta = make_meta(port, kMetaLenGde, kOk);
   const unsigned long long tw4 = __builtin_amdgcn_s_memrealtime();
   rgo = __ballot(go);
   while (rgo) {
@@ -331,7 +337,7 @@ __device__ __forceinline__ void gde_deliver(const RingArgs& a, RingDevState* qst
   // (waited for: a later chunk's head landing first and then overwritten would go back.  A PCIe
   // atomic add of the count instead needs no wait, but measured slower: 28-32 vs 42-57 Mpps, r5 s14)
   __builtin_amdgcn_s_waitcnt(0);   // this chunk's heads are out before a later chunk's may be
-  if (lane == 0) {
+  if (lane == 0 && t_com) {
     __hip_atomic_store(&qst->gde_commit, tk + 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const unsigned long long tw5 = __builtin_amdgcn_s_memrealtime();
     __hip_atomic_fetch_add(&qst->gde_wait, (uint64_t)((tw1 - tw0) + (tw4 - tw3)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -1,6 +1,8 @@
 // trafgen_pkt.h — the pod-side generator / sink of trafgen.h for kernel-netdev pods: every pod is
 // one interface inside its own network namespace (the pod end of a veth pair, as the CNI leaves
-// it), driven through AF_PACKET TPACKET_V2 rings (iox.h PacketPort) opened inside that namespace.
+// it), driven through AF_PACKET TPACKET_V2 rings (iox.h PacketPort) opened inside that namespace,
+// or (`xdp`) through an AF_XDP socket with its redirect program on the pod's interface (iox.h
+// XdpPort: an AF_XDP-capable pod application, e.g. a DPDK af_xdp PMD, on a plain veth).
 // The same generator feeds the native engine's veth vports and the Linux bridge comparator
 // (tools/live_bench.py --comparator), so both are measured with identical pods.
 //
@@ -30,11 +32,11 @@ struct NetPod {
   uint32_t stride = 0;
 };
 
-// A PacketPort opened inside `netns` (a helper thread enters the namespace: namespaces are per
-// thread, the caller's never changes; the socket stays bound to the pod's interface afterwards).
-inline std::shared_ptr<iox::PacketPort> open_in_netns(const std::string& netns, const std::string& ifname,
-                                                      uint32_t frames) {
-  std::shared_ptr<iox::PacketPort> port;
+// A PacketPort (or XdpPort) opened inside `netns` (a helper thread enters the namespace: namespaces
+// are per thread, the caller's never changes; the socket stays bound to the pod's interface).
+inline std::shared_ptr<iox::Port> open_in_netns(const std::string& netns, const std::string& ifname,
+                                                uint32_t frames, bool xdp = false) {
+  std::shared_ptr<iox::Port> port;
   std::string err;
   std::thread t([&] {
     try {
@@ -45,7 +47,8 @@ inline std::shared_ptr<iox::PacketPort> open_in_netns(const std::string& netns, 
         ::close(fd);
         if (r != 0) throw std::runtime_error("trafgen: setns " + netns);
       }
-      port = std::make_shared<iox::PacketPort>(ifname, frames, 2048);
+      if (xdp) port = std::make_shared<iox::XdpPort>(ifname, frames, 2048);
+      else port = std::make_shared<iox::PacketPort>(ifname, frames, 2048);
     } catch (const std::exception& e) {
       err = e.what();
     }
@@ -55,12 +58,12 @@ inline std::shared_ptr<iox::PacketPort> open_in_netns(const std::string& netns, 
   return port;
 }
 
-inline Result run_netns(const std::vector<NetPod>& pods, const Config& cfg) {
+inline Result run_netns(const std::vector<NetPod>& pods, const Config& cfg, bool xdp = false) {
   const size_t np = pods.size();
-  std::vector<std::shared_ptr<iox::PacketPort>> ports;
+  std::vector<std::shared_ptr<iox::Port>> ports;
   std::vector<std::vector<uint32_t>> ts_off(np);
   for (size_t k = 0; k < np; ++k) {
-    ports.push_back(open_in_netns(pods[k].netns, pods[k].ifname, 4096));
+    ports.push_back(open_in_netns(pods[k].netns, pods[k].ifname, 4096, xdp));
     for (size_t c = 0; c < pods[k].lens.size(); ++c)
       ts_off[k].push_back(ts_offset(pods[k].frames.data() + c * pods[k].stride, pods[k].lens[c]));
   }
@@ -118,7 +121,7 @@ inline Result run_netns(const std::vector<NetPod>& pods, const Config& cfg) {
           if (per_thread_rate > 0) credit -= put;
         }
         for (size_t k = 0; k < mine.size(); ++k) {
-          iox::PacketPort& port = *ports[mine[k]];
+          iox::Port& port = *ports[mine[k]];
           const uint32_t got = port.rx(refs.data(), (uint32_t)refs.size());
           if (!got) continue;
           const uint64_t trx = now_ns();

@@ -145,7 +145,7 @@ def parse_args(argv=None):
     ap.add_argument("--placement", default="flow", choices=["flow", "port"],
                     help="--gpus > 1: frames run on their flow's GPU (flows sharded by RSS owner) or on their "
                          "ingress port's GPU (flows replicated: the SFC hop pipeline across GPUs)")
-    ap.add_argument("--vport-kind", default="", choices=["", "veth", "tap", "memif"],
+    ap.add_argument("--vport-kind", default="", choices=["", "veth", "xdp", "tap", "memif"],
                     help="amd-gpu --live: vports as veth pairs (kernel-netdev pods, AF_PACKET rings), TAP "
                          "netdevs or shared-memory (memif) regions; default: node config vport_kind (veth)")
     ap.add_argument("--io-queues", type=int, default=0,

@@ -37,7 +37,7 @@ class NodeConfig:
     wire_port: int = 4000
     vsp_state_dir: str = ""            # journal + snapshots (checkpoint/resume); "" = off
     # live data path of the GPU VSP (vsp/gpu.py, dataplane/native_io.py)
-    vport_kind: str = "veth"           # veth (kernel netdev pods, AF_PACKET rings) | memif | tap
+    vport_kind: str = "veth"           # veth (kernel netdev pods, AF_PACKET rings) | xdp (veth, AF_XDP) | memif | tap
     io_queues: int = 6                 # native engine rx queues (threads), each with a ring queue per GPU
     # native engine delivery threads per queue; 0 = run to completion (each rx thread completes and
     # delivers its own bursts: one busy thread per queue).  On the GPU box (16 CPUs granted) 6 x 0
@@ -95,8 +95,8 @@ class NodeConfig:
             raise ValueError("nf_devices_per_pod must be >= 1")
         if self.hash_mode not in ("lds", "mfma", "scalar") or self.acl_mode not in ("mfma", "scalar", "off"):
             raise ValueError("unknown hash / ACL mode")
-        if self.vport_kind not in ("veth", "memif", "tap"):
-            raise ValueError("vport_kind is veth, memif or tap")
+        if self.vport_kind not in ("veth", "xdp", "memif", "tap"):
+            raise ValueError("vport_kind is veth, xdp, memif or tap")
         if not 1 <= self.io_queues <= 64 or not 0 <= self.io_workers <= 16:
             raise ValueError("io_queues in [1, 64], io_workers in [0, 16] (0: the rx threads deliver)")
         if not self.uplink or len(self.uplink) > 15 or not 1 <= len(self.uplink_host_ifname) <= 14:

@@ -126,6 +126,24 @@ class PacketVport:
             self._nl = None
 
 
+class XdpVport(PacketVport):
+    """The VSP-side end of a veth pair served through AF_XDP (iox.h XdpPort): an XSK socket and
+    a redirect XDP program on the netdev instead of AF_PACKET rings, so frames reach the engine
+    without an skb or a packet socket.  Same pair creation as PacketVport (vport_kind "xdp")."""
+
+    DEFAULT_FRAMES = 2048
+
+    def __init__(self, ifname: str, frames: int = DEFAULT_FRAMES, frame_size: int = 2048):
+        super().__init__(ifname, frames, frame_size)
+
+    @classmethod
+    def create_veth(cls, nl, name: str, mac: str | None = None, frames: int = DEFAULT_FRAMES) -> "XdpVport":
+        return super().create_veth(nl, name, mac, frames)
+
+    def make(self, nf, queues: int = 1):
+        return nf.XdpPort(self.ifname, self.frames, self.frame_size)
+
+
 _ETHTOOL = {"tx_csum": 0x17, "sg": 0x19, "tso": 0x1F, "gso": 0x24, "gro": 0x2C}   # ETHTOOL_S* (linux/ethtool.h)
 
 

@@ -53,7 +53,7 @@ MODULES = {
     "_nfdp": {
         "dir": CSRC / "nfdp",
         "sources": ["kernels.hip", "shard.hip", "pktio.hip", "ring.hip", "ipsec.hip", "host.cpp", "shard_cpu.cpp",
-                    "ipsec_cpu.cpp", "iox.cpp", "iox_gpu.cpp", "bindings.cpp"],
+                    "ipsec_cpu.cpp", "iox.cpp", "iox_xdp.cpp", "iox_gpu.cpp", "bindings.cpp"],
         "hip": True,
     },
     "_agent": {

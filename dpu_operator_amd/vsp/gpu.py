@@ -124,8 +124,9 @@ class GpuVsp(VspBase):
         if placement not in ("flow", "port"):
             raise ValueError("placement is 'flow' (flows sharded) or 'port' (each vport on one GPU: hop pipeline)")
         self.placement = placement
-        if vport_kind not in ("tap", "veth", "memif"):
-            raise ValueError("vport_kind is 'tap' / 'veth' (netdevs) or 'memif' (shared-memory vport)")
+        if vport_kind not in ("tap", "veth", "xdp", "memif"):
+            raise ValueError("vport_kind is 'tap' / 'veth' / 'xdp' (netdevs; xdp: veth served through AF_XDP) "
+                             "or 'memif' (shared-memory vport)")
         self.vport_kind = vport_kind
         self.memif_dir = memif_dir or (self.pm.memif_dir() if self.pm is not None else None)
         self.tx_workers = int(tx_workers)
@@ -147,7 +148,7 @@ class GpuVsp(VspBase):
         self.live = live
         if live_engine not in ("batch", "ring", "native"):
             raise ValueError("live_engine is 'batch', 'ring' or 'native'")
-        if (self.gpus > 1 or vport_kind in ("memif", "veth")) and live:
+        if (self.gpus > 1 or vport_kind in ("memif", "veth", "xdp")) and live:
             live_engine = "native"                  # the C++ engine: RSS steering / memif / AF_PACKET vports
         self.live_engine = live_engine              # "batch" (fused kernel per cycle), "ring" (resident
                                                     # kernel) or "native" (C++ I/O engine, iox.cpp)
@@ -390,10 +391,10 @@ class GpuVsp(VspBase):
                 self.taps[i] = vp
                 if self.livepath is not None:
                     self.livepath.add_port(i, vp)
-            elif self.live and self.vport_kind == "veth":
-                from ..dataplane.native_io import PacketVport
+            elif self.live and self.vport_kind in ("veth", "xdp"):
+                from ..dataplane.native_io import PacketVport, XdpVport
 
-                vp = PacketVport.create_veth(self.nl, name, mac)
+                vp = (XdpVport if self.vport_kind == "xdp" else PacketVport).create_veth(self.nl, name, mac)
                 self.taps[i] = vp
                 if self.livepath is not None:
                     self.livepath.add_port(i, vp)

@@ -39,16 +39,16 @@ def _expected(ref, slots, im):
     return exp
 
 
-@pytest.mark.parametrize("kind", ["veth", "tap"])
+@pytest.mark.parametrize("kind", ["veth", "tap", "xdp"])
 def test_netns_pods_through_the_native_engine_bit_exact(kind):
     from dpu_operator_amd.cni.netlink import RtNetlink
     from dpu_operator_amd.dataplane import scenario as S
     from dpu_operator_amd.dataplane.engine import DataPlane
-    from dpu_operator_amd.dataplane.native_io import NativeLivePath, PacketVport
+    from dpu_operator_amd.dataplane.native_io import NativeLivePath, PacketVport, XdpVport
     from dpu_operator_amd.dataplane.netio import TapPort
 
     nl = RtNetlink()
-    tag = "v" if kind == "veth" else "t"
+    tag = {"veth": "v", "tap": "t", "xdp": "x"}[kind]
     n_pods = 4
     dp = DataPlane(device="cpu", flow_buckets=1 << 12)
     sc = S.build_sfc(dp, n_pods=n_pods, n_flows=2048, n_acl=32, seed=0)
@@ -61,8 +61,8 @@ def test_netns_pods_through_the_native_engine_bit_exact(kind):
     try:
         for i in range(n_pods):
             name = f"nn{tag}{os.getpid() % 1000}p{i}"
-            if kind == "veth":
-                vp = PacketVport.create_veth(nl, name)
+            if kind in ("veth", "xdp"):   # (xdp: the engine's ends through AF_XDP, iox.h XdpPort)
+                vp = (XdpVport if kind == "xdp" else PacketVport).create_veth(nl, name)
                 vps.append(vp)
                 ports[int(sc.pod_port[i])] = vp
             else:

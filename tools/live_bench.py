@@ -275,7 +275,8 @@ def run(device: str = "cuda", n_pods: int = 8, flows: int = 1 << 20, n_acl: int 
 
 def run_veth(mode: str = "linux-bridge", n_pods: int = 4, duration: float = 1.0, threads: int = 2,
              queues: int = 2, tx_workers: int = 1, burst: int = 256, inflight: int = 64, ring_capacity: int = 16384,
-             max_inflight_frames: int = 4096, coalesce_us: float = 8.0, device: str = "cuda", rx_frames: int = 0) -> dict:
+             max_inflight_frames: int = 4096, coalesce_us: float = 8.0, device: str = "cuda", rx_frames: int = 0,
+             pod_xdp: bool = False) -> dict:
     """Kernel-netdev pods: every pod a network namespace holding one end of a veth pair, driven by
     the same C++ generator / sink through AF_PACKET rings opened inside the namespace
     (csrc/nfdp/trafgen_pkt.h).  The host ends go to
@@ -285,13 +286,18 @@ def run_veth(mode: str = "linux-bridge", n_pods: int = 4, duration: float = 1.0,
       * `pipeline`: the native I/O engine over the data plane on `device` (the resident ring
         kernel on a GPU): the deployed GPU node's default, its pods on one L2 bridge with their
         MACs programmed (what the VSP does without an NF), frames switched by the pipeline;
-    so all three switch identical pods with identical frames.  rx_frames: the engine's AF_PACKET rx
-    ring per port (0: the vports' default, native_io.PacketVport)."""
+    so all three switch identical pods with identical frames.  A "-xdp" mode ("engine-xdp",
+    "pipeline-xdp") serves the engine's ends through AF_XDP (native_io.XdpVport) instead of AF_PACKET
+    rings; pod_xdp: the pods' own application uses AF_XDP on its veth (an af_xdp PMD) instead of
+    AF_PACKET.  rx_frames: the engine's rx ring per port (0: the vport kind's default)."""
     from dpu_operator_amd.cni.netlink import RtNetlink, create_netns, delete_netns
-    from dpu_operator_amd.dataplane.native_io import PacketVport
+    from dpu_operator_amd.dataplane.native_io import PacketVport, XdpVport
 
     nf = nfdp()
-    rx_frames = rx_frames or PacketVport.DEFAULT_FRAMES
+    xdp = mode.endswith("-xdp")          # the engine's ends through AF_XDP instead of AF_PACKET rings
+    mode = mode[:-4] if xdp else mode
+    VP = XdpVport if xdp else PacketVport
+    rx_frames = rx_frames or VP.DEFAULT_FRAMES
     live = None
     nl = RtNetlink()
     tag = f"{os.getpid() % 10000}"
@@ -320,7 +326,7 @@ def run_veth(mode: str = "linux-bridge", n_pods: int = 4, duration: float = 1.0,
             macs = [(int.from_bytes(_WireLive.mac(i), "little"), i) for i in range(n_pods)]
             eng.add_backend(nf.WireBackend(ring_capacity, queues, macs))
             for i, h in enumerate(hosts):
-                eng.add_port(i, nf.PacketPort(h, rx_frames, 2048))
+                eng.add_port(i, VP(h, frames=rx_frames).make(nf))
             eng.start()
         elif mode == "pipeline":
             from dpu_operator_amd.dataplane import tables as T
@@ -332,7 +338,7 @@ def run_veth(mode: str = "linux-bridge", n_pods: int = 4, duration: float = 1.0,
                 dp.macs.insert(1, mac, i)
             dp.flood.set_members(1, list(range(n_pods)))
             dp.commit(full=True)
-            live = NativeLivePath(dp, {i: PacketVport(h, frames=rx_frames) for i, h in enumerate(hosts)}, burst=burst,
+            live = NativeLivePath(dp, {i: VP(h, frames=rx_frames) for i, h in enumerate(hosts)}, burst=burst,
                                   ring_capacity=ring_capacity, inflight=inflight, tx_workers=tx_workers, queues=queues,
                                   max_inflight_frames=max_inflight_frames, coalesce_us=coalesce_us).start()
             eng = live._eng
@@ -340,14 +346,16 @@ def run_veth(mode: str = "linux-bridge", n_pods: int = 4, duration: float = 1.0,
         for i in range(n_pods):
             fr, ln = wire.frames(i, n_pods, k=1024, seed=100 + i)
             pods.append((nss[i], f"lb{tag}p{i}", fr, ln))
-        out = {"vports": "veth", "switch": mode, "pods": n_pods, "gen_threads": threads, "frame_bytes": 64}
+        out = {"vports": "veth", "switch": mode, "engine_io": "af_xdp" if xdp else "af_packet",
+               "pod_io": "af_xdp" if pod_xdp else "af_packet", "pods": n_pods,
+               "gen_threads": threads, "frame_bytes": 64}
         if mode != "linux-bridge":
             out.update(queues=queues, tx_workers=tx_workers, coalesce_us=coalesce_us, rx_frames=rx_frames,
                        device=device if mode == "pipeline" else "none")
         # warm-up (the bridge learns every MAC), then saturated
-        nf.trafgen_run_netns(pods, duration_s=0.2, warmup_s=0.0, threads=threads, burst=32)
+        nf.trafgen_run_netns(pods, duration_s=0.2, warmup_s=0.0, threads=threads, burst=32, xdp=pod_xdp)
         time.sleep(0.1)
-        r = nf.trafgen_run_netns(pods, duration_s=duration, warmup_s=0.2, threads=threads, burst=32)
+        r = nf.trafgen_run_netns(pods, duration_s=duration, warmup_s=0.2, threads=threads, burst=32, xdp=pod_xdp)
         mpps = r["received"] / duration / 1e6
         out.update(mpps=round(mpps, 3), offered_mpps=round(r["sent"] / duration / 1e6, 3),
                    p50_us=_pct(r["lat_us"], 50), p99_us=_pct(r["lat_us"], 99), bad=int(r["bad"]))
@@ -356,7 +364,7 @@ def run_veth(mode: str = "linux-bridge", n_pods: int = 4, duration: float = 1.0,
             if eng is not None:
                 eng.take_latency_us()
             r2 = nf.trafgen_run_netns(pods, duration_s=min(duration, 0.5), warmup_s=0.1, threads=threads, burst=8,
-                                      rate_pps=frac * mpps * 1e6)
+                                      rate_pps=frac * mpps * 1e6, xdp=pod_xdp)
             out.update({f"{tag_}_mpps": round(r2["received"] / min(duration, 0.5) / 1e6, 3),
                         f"{tag_}_p50_us": _pct(r2["lat_us"], 50), f"{tag_}_p99_us": _pct(r2["lat_us"], 99)})
             if eng is not None:   # the engine's own share: rx read -> burst delivered
@@ -365,7 +373,7 @@ def run_veth(mode: str = "linux-bridge", n_pods: int = 4, duration: float = 1.0,
             time.sleep(0.1)
         # unloaded: a slow trickle (1 kpps): no queueing anywhere
         r3 = nf.trafgen_run_netns(pods, duration_s=min(duration, 0.5), warmup_s=0.05, threads=1, burst=1,
-                                  rate_pps=1000.0)
+                                  rate_pps=1000.0, xdp=pod_xdp)
         out.update(idle_p50_us=_pct(r3["lat_us"], 50), idle_p99_us=_pct(r3["lat_us"], 99))
         if eng is not None:
             st = dict(live.stats if live is not None else eng.stats())
@@ -413,17 +421,18 @@ def main() -> None:
     ap.add_argument("--trials", type=int, default=1, help="saturated runs (median reported)")
     ap.add_argument("--split", default="", help='SFC hops with GPU placements, e.g. "acl,nat,l2fwd@1" (two planes)')
     ap.add_argument("--planes", default="", help='--split: the planes\' devices, e.g. "cuda:0,cuda:1"')
-    ap.add_argument("--veth", choices=("linux-bridge", "engine", "pipeline"), default=None,
+    ap.add_argument("--veth", choices=("linux-bridge", "engine", "pipeline", "engine-xdp", "pipeline-xdp"), default=None,
                     help="netns pods on veth pairs, switched by a Linux bridge, by the native engine alone or by the "
                          "native engine in front of the data plane on --device (the deployed default)")
-    ap.add_argument("--rx-frames", type=int, default=0, help="--veth: the engine's AF_PACKET rx ring per port")
+    ap.add_argument("--rx-frames", type=int, default=0, help="--veth: the engine's rx ring per port")
+    ap.add_argument("--pod-xdp", action="store_true", help="--veth: the pods' application uses AF_XDP on its veth")
     a = ap.parse_args()
     if a.veth:
         if "DPU_NETNS_DIR" in os.environ:   # a namespace of our own (unshare -Urnm): loopback starts down
             os.makedirs(os.environ["DPU_NETNS_DIR"], exist_ok=True)
         print(json.dumps(run_veth(a.veth, n_pods=min(a.pods, 8), duration=a.duration, threads=min(a.threads, a.pods),
                                   queues=a.queues, tx_workers=a.tx_workers, coalesce_us=a.coalesce_us,
-                                  device=a.device, rx_frames=a.rx_frames)), flush=True)
+                                  device=a.device, rx_frames=a.rx_frames, pod_xdp=a.pod_xdp)), flush=True)
         return
     print(json.dumps(run(a.device, a.pods, a.flows, duration=a.duration, threads=a.threads, burst=a.burst,
                          inflight=a.inflight, tx_workers=a.tx_workers, queues=a.queues,
