@@ -230,6 +230,8 @@ class MemifPort : public Port {
  protected:
   bool tx_locked(uint32_t q, const uint8_t* a, uint32_t na, const uint8_t* b, uint32_t nb, const uint8_t* c,
                  uint32_t nc) override {
+    // (the engine's header piece `b` is always a 64-B slot: an out slot or a replica's header)
+    if (!na && !nc && nb <= 64 && b) return prod_[q].put_slot(b, nb);
     return prod_[q].put(a, na, b, nb, c, nc);
   }
   void flush_locked(uint32_t q) override { prod_[q].commit(); }

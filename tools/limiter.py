@@ -8,7 +8,9 @@ Variants (all 4M 64-B packets of the headline SFC, 256 ACL rules, LDS Toeplitz, 
   * flows_16m     16M flows: 1-GB table, every fetch from HBM;
   * ctr_zero      flow-counter atomics add 0 (kernel flag 4: the atomic is still issued: the
                   difference to base is the counter lines' dirty write-back only);
-  * no_lat        no latency samples, no port counters (flags 1 | 2).
+  * no_lat        no latency samples, no port counters (flags 1 | 2);
+  * wild / wild_no_early   the ClassBench-style 1025-rule ACL: the early-fetch 2-wave instance (its
+                  default) and the 4-wave instance with per-tile prefilters (flag 256).
 A build without the per-flow atomic at all is tools/ab_variants.py with -DNFDP_ABL_NO_FLOWCTR.
 
 Byte model per packet (what has to cross HBM / MALL at minimum): frame in 64 B, frame out 64 B,
@@ -48,8 +50,16 @@ def main():
             pk, im = S.traffic(sc, a.batch, seed=1 + r)
             bs.append((torch.from_numpy(pk).cuda(), torch.from_numpy(im.view(np.int32)).cuda()))
         planes[name] = (g, bs)
+    # the ClassBench-style rule set (bench value_acl_wild) on the headline's flows: the early-fetch
+    # 2-wave instance (default from 33 rule tiles) against the 4-wave instance with per-tile prefilters
+    g = DataPlane(device="cuda", flow_buckets=1 << 19, hash_mode="lds", acl_mode="mfma")
+    sc = S.build_sfc(g, n_pods=8, n_flows=1 << 20, n_acl=256, seed=0)
+    S.install_acl_wild(g, 1024)
+    g.commit(full=True)
+    pk, im = S.traffic(sc, a.batch, seed=9001)
+    planes["wild"] = (g, [(torch.from_numpy(pk).cuda(), torch.from_numpy(im.view(np.int32)).cuda())] * 2)
     variants = {"base": ("base", 0), "flows_64k": ("flows_64k", 0), "flows_16m": ("flows_16m", 0),
-                "ctr_zero": ("base", 4), "no_lat": ("base", 3)}
+                "ctr_zero": ("base", 4), "no_lat": ("base", 3), "wild": ("wild", 0), "wild_no_early": ("wild", 256)}
     res = {k: [] for k in variants}
     bufs = {k: planes[k][0].alloc_batch(a.batch) for k in planes}
     for _ in range(a.rounds):
