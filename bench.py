@@ -44,6 +44,12 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 BASELINE_METRIC = "Mpps + p50 pod-to-pod µs latency, 1M-flow SFC at 1/2/4/8 MI355X"
+_T0 = time.time()
+
+
+def _log(msg: str) -> None:
+    """Progress on stderr (the JSON line stays the only stdout line): a long bench is never silent."""
+    print(f"[bench {time.time() - _T0:7.1f}s] {msg}", file=sys.stderr, flush=True)
 
 
 # RSS exchange protocol facts the multi-GPU tests check against (tests/test_multigpu.py,
@@ -292,6 +298,7 @@ def measure_variants(a, dp, sc, dev, torch, S, P) -> dict:
                    "mix": "7x64,4x576,1x1500", "forwarded_fraction": round(fwd, 4),
                    "note": "header slots through the kernel; payload stays in place (header-split I/O)"}
     del imix
+    _log("variant: mixed")
     # mixed: 5 % flow miss, 2 % ACL deny, 0.1 % malformed
     deny = S.install_deny_flows(dp, sc, k=4096)
     dp.commit()
@@ -304,6 +311,7 @@ def measure_variants(a, dp, sc, dev, torch, S, P) -> dict:
     res["mixed_mpps"] = round(n * a.variant_steps / el / 1e6, 1)
     res["mixed_dispositions"] = {k: round(float(np.mean(rs == v)), 4) for k, v in
                                  (("ok", 0), ("acl_deny", 4), ("no_route", 5), ("malformed", 9))}
+    _log("variant: L3-routed SFC")
     # L3-routed SFC: acl -> nat -> route (pod /32s through 8-way ECMP, 100K background prefixes
     # in the DIR-24-8 FIB), same flows and traffic as the headline
     info = S.install_l3_routes(dp, sc)
@@ -317,6 +325,7 @@ def measure_variants(a, dp, sc, dev, torch, S, P) -> dict:
     dp.chains.set(sc.chain_id, ["acl", "nat", "l2fwd"])
     dp.commit()
     del b
+    _log("variant: ACL1024 on the headline traffic")
     # ACL1024 on the headline traffic
     acl_headline = list(dp.acl.rules)
     S.add_acl_rules(dp, 1024)
@@ -326,6 +335,7 @@ def measure_variants(a, dp, sc, dev, torch, S, P) -> dict:
     el, meta = _time_fused(dp, b, a.variant_steps, torch)
     res["acl1024_mpps"] = round(n * a.variant_steps / el / 1e6, 1)
     res["acl1024_forwarded_fraction"] = round(float(np.mean(P.meta_fields(meta.cpu().numpy().view(np.uint32))[2] == 0)), 4)
+    _log("variant: ClassBench-style ACL")
     # ClassBench-style ACL: 1024 5-tuple rules, nested prefixes, port ranges, wildcard protocols
     info = S.install_acl_wild(dp, 1024)
     dp.commit()
@@ -339,6 +349,7 @@ def measure_variants(a, dp, sc, dev, torch, S, P) -> dict:
     dp.acl.version += 1
     dp.commit()
     del mixed, b
+    _log("variant: dual stack")
     # dual stack: half the batch IPv6 (64K IPv6 flows of the same pods, 64 IPv6 ACL rules: the
     # v6_kernel pre-pass + the IPv6-capable fused instance), half the headline's IPv4 traffic.
     # Last: it turns the data plane's IPv6 features on.
@@ -361,6 +372,7 @@ def measure_variants(a, dp, sc, dev, torch, S, P) -> dict:
                    "forwarded_fraction": round(float(np.mean(P.meta_fields(meta.cpu().numpy().view(np.uint32))[2] == 0)), 4),
                    "frames": "64-B IPv4 + 66-B tagged IPv6/UDP (the smallest)"}
     del b
+    _log("variant: overlay")
     # overlay: the headline's traffic VXLAN-encapsulated on an underlay VTEP port (64-B inner frames,
     # 114-B outer): single-pass termination of wide header pairs (pair_kernel -> fused ->
     # pair_fix), the SFC on the inner frame.  n / 2 frames = n slots per step.
@@ -381,6 +393,7 @@ def measure_variants(a, dp, sc, dev, torch, S, P) -> dict:
     dp.ports.clear(ports["vtep"])
     dp.commit()
     del b
+    _log("variant: overlay egress")
     # overlay egress: every pod VF a VXLAN tunnel port, so every forwarded packet also gets its
     # outer-header record from the side pass (the headline's traffic, 4M packets per step)
     eg = S.install_vxlan_egress(dp, sc)
@@ -399,6 +412,7 @@ def measure_variants(a, dp, sc, dev, torch, S, P) -> dict:
     dp.ports.version += 1
     dp.commit()
     del b
+    _log("variant: BASELINE config 5")
     # BASELINE config 5: the rule set the Intel IPU VSP programs (8 host VFs: AddHostVfP4Rules x 8,
     # AddPeerToPeerP4Rules O(n^2), one NF: AddNFP4Rules; Init's phy-port / LAG / primary-network
     # rules) through the P4Runtime compile onto a fresh data plane, then VF->VF, VF->NF, NF->wire
@@ -547,6 +561,7 @@ def main() -> None:
             return eng.out_meta(), eng.latency_samples_us()
 
     setup_s = time.time() - t_setup
+    _log(f"setup done ({setup_s:.1f} s), warmup + timed steps")
     for k in range(a.warmup):
         step(k)
     if drain:
@@ -571,6 +586,7 @@ def main() -> None:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    _log(f"timed region: {elapsed * 1e3 / a.steps:.4f} ms / step")
     meta_np, lat_us = results()
     _, _, reasons = P.meta_fields(meta_np)
     fwd_local = float(np.mean((reasons == 0) | (reasons == 10)))  # 10: handed to its owner / egress GPU
@@ -681,6 +697,7 @@ def main() -> None:
 
     # host round trip of a small batch (outside the timed region, 1 GPU): submit -> results ready
     # on the host clock, with per-batch launches vs one replay of the captured HIP graph
+    _log("small-batch probes")
     rtt = None
     if not a.no_lowlat and world == 1 and a.io == "device" and not sharded:
         nb = 256
@@ -706,6 +723,7 @@ def main() -> None:
 
     # low-latency path (outside the timed region): persistent ring kernel, host publishes 64-packet
     # chunks and times publish -> completion flag on its own clock (dataplane/ring.py)
+    _log("ring kernel probes")
     ring = None
     if not a.no_lowlat and world == 1 and a.io == "device":
         from dpu_operator_amd.dataplane.ring import RingPath
@@ -745,6 +763,7 @@ def main() -> None:
     # realistic variants (1 GPU, after the timed region, same kernel and table): the headline is the
     # best case (every packet forwarded), so also report a mix with flow misses / ACL denies /
     # malformed frames, a 1024-rule ACL, and IMIX frame sizes (header path; payload stays in place)
+    _log("variants")
     variants = None
     if world == 1 and a.io == "device" and not a.no_variants:
         variants = measure_variants(a, dp, sc, dev, torch, S, P)
@@ -752,6 +771,7 @@ def main() -> None:
     # SFC hop pipeline across GPUs (after the timed region): the headline chain split over two
     # data planes with the in-HBM hand-off between them - both on cuda:0 at N = 1, cuda:0 -> cuda:1
     # over xGMI at N > 1 (rank 0 measures while the other ranks wait at the barrier)
+    _log("hop pipeline")
     hops = None
     if a.io == "device" and not a.no_variants and not a.no_hops:
         if world > 1:
@@ -765,6 +785,7 @@ def main() -> None:
     # live pod -> pod path (1 GPU, after the timed region): shared-memory pod vports, the native C++
     # I/O engine (csrc/nfdp/iox) and the persistent ring kernel; C++ pod generator / sinks measure
     # delivered Mpps and one-way latency on one clock (tools/live_bench.py)
+    _log("live block")
     live = live_veth = None
     if world == 1 and a.io == "device" and not a.no_live:
         try:
@@ -780,6 +801,7 @@ def main() -> None:
             # the CPU time the box really grants (a CFS quota the process cannot read: 256 CPUs
             # listed, 16 granted on the GPU box) - the live path is host-CPU work: pods + engine
             share = cpuquota.cpu_share()
+            _log(f"live: cpu share {share.get('cpus')}; main run")
             live = lb.run(device=str(dev), n_pods=a.pods_per_gpu, flows=a.flows, n_acl=a.acl, duration=1.0,
                           threads=a.live_gen_threads, tx_workers=a.live_workers, queues=a.live_queues,
                           hash_mode=a.hash, gpu_egress=gde, trials=a.live_trials)
@@ -787,6 +809,7 @@ def main() -> None:
             # the other egress mode for comparison (GPU-direct egress or host egress), same threads,
             # saturated rate only
             alt = dict(threads=a.live_gen_threads, tx_workers=a.live_workers, queues=a.live_queues, gpu_egress=not gde)
+            _log(f"live: {live.get('mpps')} Mpps; other egress")
             hp = lb.run(device=str(dev), n_pods=a.pods_per_gpu, flows=a.flows, n_acl=a.acl, duration=0.5,
                         hash_mode=a.hash, saturated_only=True, **alt)
             live["other_egress"] = {**alt, "mpps": hp.get("mpps"), "p50_us": hp.get("p50_us"), "error": hp.get("error")}
@@ -795,6 +818,7 @@ def main() -> None:
             # engine share the box's CPU grant, so past the grant more queues cannot help
             curve = []
             for q in (1, 2, 4, 6, 8):
+                _log(f"live: queue curve {q}")
                 r = lb.run(device=str(dev), n_pods=a.pods_per_gpu, flows=a.flows, n_acl=a.acl, duration=0.5,
                            threads=a.live_gen_threads, tx_workers=a.live_workers, queues=q, hash_mode=a.hash,
                            saturated_only=True, gpu_egress=gde)
@@ -807,6 +831,7 @@ def main() -> None:
             import torch as _t
 
             two = _t.cuda.device_count() > 1
+            _log("live: split chain")
             sp = lb.run(device=str(dev), n_pods=a.pods_per_gpu, flows=a.flows, n_acl=a.acl, duration=0.5,
                         threads=a.live_gen_threads, tx_workers=a.live_workers, queues=a.live_queues, hash_mode=a.hash,
                         split="acl,nat,l2fwd@1", planes="cuda:0,cuda:1" if two else "")
@@ -823,7 +848,9 @@ def main() -> None:
         # "pipeline", the deployed default vport): needs CAP_NET_ADMIN / CAP_NET_RAW, or user
         # namespaces to get them; reported as skipped (with the reason) where the box has neither
         if live is not None:
+            _log("live: veth")
             live_veth = _live_veth(str(dev))
+    _log("done")
 
     total_pkts = world * a.batch * a.steps
     mpps = total_pkts / elapsed / 1e6

@@ -58,8 +58,15 @@ def main():
     g.commit(full=True)
     pk, im = S.traffic(sc, a.batch, seed=9001)
     planes["wild"] = (g, [(torch.from_numpy(pk).cuda(), torch.from_numpy(im.view(np.int32)).cuda())] * 2)
+    g = DataPlane(device="cuda", flow_buckets=1 << 19, hash_mode="lds", acl_mode="mfma")
+    sc = S.build_sfc(g, n_pods=8, n_flows=1 << 20, n_acl=256, seed=0)
+    S.add_acl_rules(g, 1024)
+    g.commit(full=True)
+    pk, im = S.traffic(sc, a.batch, seed=9001)
+    planes["acl1024"] = (g, [(torch.from_numpy(pk).cuda(), torch.from_numpy(im.view(np.int32)).cuda())] * 2)
     variants = {"base": ("base", 0), "flows_64k": ("flows_64k", 0), "flows_16m": ("flows_16m", 0),
-                "ctr_zero": ("base", 4), "no_lat": ("base", 3), "wild": ("wild", 0), "wild_no_early": ("wild", 256)}
+                "ctr_zero": ("base", 4), "no_lat": ("base", 3), "wild": ("wild", 0), "wild_no_early": ("wild", 256),
+                "acl1024": ("acl1024", 0), "acl1024_no_early": ("acl1024", 256)}
     res = {k: [] for k in variants}
     bufs = {k: planes[k][0].alloc_batch(a.batch) for k in planes}
     for _ in range(a.rounds):
