@@ -179,6 +179,25 @@ def measure_hops(a, devices: str) -> dict:
     return json.loads(lines[-1])
 
 
+def _live_split(a, dev: str, planes: str) -> dict:
+    """The live split-chain run (tools/live_bench.py --split) as a child process under a time limit:
+    a stalled hand-off path must not take the headline with it."""
+    import subprocess
+
+    cmd = [sys.executable, "-u", os.path.join(REPO, "tools", "live_bench.py"), "--device", dev,
+           "--pods", str(a.pods_per_gpu), "--flows", str(a.flows), "--duration", "0.5",
+           "--threads", str(a.live_gen_threads), "--tx-workers", str(a.live_workers), "--queues", str(a.live_queues),
+           "--split", "acl,nat,l2fwd@1"] + (["--planes", planes] if planes else [])
+    try:
+        r = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=120)
+    except subprocess.TimeoutExpired:
+        return {"error": "timed out (120 s)"}
+    line = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    if r.returncode != 0 or not line:
+        return {"error": f"exit {r.returncode}: {(r.stderr or r.stdout)[-300:]}"}
+    return json.loads(line[-1])
+
+
 def _live_veth(dev: str) -> dict:
     """veth pods -> native engine -> GPU ring (the deployed default), measured in-process with
     CAP_NET_ADMIN, else in `unshare -Urnm` (a user namespace of our own), else skipped."""
@@ -832,9 +851,7 @@ def main() -> None:
 
             two = _t.cuda.device_count() > 1
             _log("live: split chain")
-            sp = lb.run(device=str(dev), n_pods=a.pods_per_gpu, flows=a.flows, n_acl=a.acl, duration=0.5,
-                        threads=a.live_gen_threads, tx_workers=a.live_workers, queues=a.live_queues, hash_mode=a.hash,
-                        split="acl,nat,l2fwd@1", planes="cuda:0,cuda:1" if two else "")
+            sp = _live_split(a, str(dev), "cuda:0,cuda:1" if two else "")
             live["split_chain"] = {k: sp.get(k) for k in ("split", "planes", "xfer_active", "mpps", "p50_us", "idle_p50_us",
                                                           "idle_p99_us", "half_p50_us", "half_p99_us", "error")}
             if sp.get("idle_p50_us") and live.get("idle_p50_us"):

@@ -418,7 +418,7 @@ __device__ __forceinline__ void xfer_send(const RingArgs& a, bool go, uint32_t p
 // on to the next plane or back to the entry ring's out slot, its chunk's pending count reduced.
 template <bool COOP>
 __device__ __forceinline__ void xfer_resume(const RingArgs& a, bool rdy, XferEntry* en, unsigned long long idx, uint32_t lane,
-                                         unsigned long long t_begin, uint32_t& seen_ep) {
+                                         unsigned long long t_begin, uint32_t& seen_ep, uint4* kx) {
   unsigned long long v = 0;
   if (lane == 0) v = __hip_atomic_load(&a.st->dprod, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const uint32_t ep = ring_epoch(rfl64(v));
@@ -457,14 +457,18 @@ __device__ __forceinline__ void xfer_resume(const RingArgs& a, bool rdy, XferEnt
   const uint32_t meta = make_meta(e.out_port, olen, e.reason, !e.reason && e.xhdr, false);
   if (__ballot(again)) xfer_send(a, again, e.out_port, o, hop_state_of(p, st, e, hs.act, hs.acl_rule, hs.hash),
                                  origin, pos, lane, t_begin);
-  // back to the entry ring: final slot and meta into its out slot (pinned host memory)
+  // back to the entry ring: final slot and meta into its out slot (pinned host memory).  Each slot
+  // goes out as ONE full 64-B line write: 16 frames per pass through the wave's LDS scratch, the 4
+  // lanes of a frame storing its 4 pieces in one instruction (per-lane 16-B stores are partial-line
+  // PCIe writes, ~11 us per 64 frames: the GPU-direct egress measurements, r5 s12)
   const uint32_t oplane = origin & 0xFFu, oq = origin >> 8;
   unsigned long long rem = __ballot(fin);
   while (rem) {
     const int leader = __builtin_ctzll(rem);
     const uint32_t O = __builtin_amdgcn_readlane(oplane, leader);
     const bool mine = fin && oplane == O;
-    rem &= ~__ballot(mine);
+    const unsigned long long bm = __ballot(mine);
+    rem &= ~bm;
     const uint32_t slots = a.xpeers[O].ring_mask + 1u, nq = a.xpeers[O].nq;
     const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc((void*)a.xpeers[O].out, (short)0,
                                                                         (int)(nq * slots * 64u), kBufRaw);
@@ -473,8 +477,22 @@ __device__ __forceinline__ void xfer_resume(const RingArgs& a, bool rdy, XferEnt
     const uint32_t at = oq * slots + (pos & (slots - 1u));
     const bool ok = mine && oq < nq;
 #pragma unroll
-    for (int k = 0; k < 4; ++k)
-      store_b128<kSysAux>(v4u{o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]}, ro, ok ? at * 64u + 16u * k : kNoRun, 0);
+    for (int q = 0; q < 4; ++q) {
+      if (((bm >> (16 * q)) & 0xFFFFull) == 0ull) continue;   // (wave-uniform)
+      if ((lane >> 4) == (uint32_t)q) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) kx[4u * (lane & 15u) + k] = make_uint4(o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]);
+      }
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      const uint4 v = kx[lane];
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+      const int src = 16 * q + (int)(lane >> 2);
+      const uint32_t sat = (uint32_t)__shfl((int)at, src);
+      const bool sok = __shfl(ok ? 1 : 0, src) != 0;
+      store_b128<kSysAux>(v4u{v.x, v.y, v.z, v.w}, ro, sok ? sat * 64u + 16u * (lane & 3u) : kNoRun, 0);
+    }
     __builtin_amdgcn_raw_buffer_store_b32(meta, rm, ok ? at * 4u : kNoRun, 0, kSysAux);
   }
   __builtin_amdgcn_s_waitcnt(0);   // (the slots are in host memory before their chunk's count moves)
@@ -502,37 +520,55 @@ __device__ __forceinline__ void xfer_resume(const RingArgs& a, bool rdy, XferEnt
 
 // The inbox service of an XF grid (its last xfer_wgs workgroups; every wave on its own): claim an
 // inbox chunk of 64 entries by ticket, resume each entry as soon as its seq says it is written, and
-// take the next ticket once all 64 are done.  Exits on the stop word (queue 0's, mirrored by its
-// frontier wave) or the device deadline.
+// take the next ticket once all 64 are done.  One system-scope load of the inbox tail per poll
+// says which of the ticket's entries are reserved at all (a ticket nobody reserved into sleeps
+// longer; the entries' own seq words are read only when reserved).  On the stop word (queue 0's,
+// mirrored by its frontier wave) a wave still finishes every reserved entry of its ticket, and
+// keeps claiming tickets while reserved entries remain, so a producer never waits forever for room.
 template <bool COOP>
-__device__ __forceinline__ void xfer_serve(const RingArgs& a, uint32_t lane, unsigned long long t_begin) {
+__device__ __forceinline__ void xfer_serve(const RingArgs& a, uint32_t lane, unsigned long long t_begin, uint4* kx) {
   XferInbox* ib = a.xpeers[a.xplane].inbox;
   XferEntry* ent = a.xpeers[a.xplane].entries;
   const uint32_t cmask = a.xpeers[a.xplane].cap_mask;
   uint32_t seen_ep = 0xFFFFFFFFu;
+  auto tail_now = [&]() {
+    unsigned long long tl = 0;
+    if (lane == 0) tl = __hip_atomic_load(&ib->tail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    return rfl64(tl);
+  };
+  auto stopping = [&]() {
+    unsigned long long v = 0;
+    if (lane == 0) v = __hip_atomic_load(&a.st->dprod, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return (rfl64(v) & kRingStop) != 0ull || __builtin_amdgcn_s_memrealtime() - t_begin > a.deadline;
+  };
   for (;;) {
     unsigned long long tk = 0;
     if (lane == 0) tk = __hip_atomic_fetch_add(&ib->claim, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     tk = rfl64(tk);
-    const unsigned long long idx = tk * 64ull + lane;
+    const unsigned long long first = tk * 64ull;
+    const unsigned long long idx = first + lane;
     XferEntry* en = ent + (idx & cmask);
     bool done = false;
     for (;;) {
-      const unsigned long long sq = __hip_atomic_load(&en->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      done = done || sq == ((idx + 1ull) | kXferDone);   // (consumed before a restart of this grid)
-      const bool rdy = !done && sq == idx + 1ull;
+      const unsigned long long tl = tail_now();
+      const bool reserved = idx < tl;
+      bool rdy = false;
+      if (reserved && !done) {
+        const unsigned long long sq = __hip_atomic_load(&en->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        done = sq == ((idx + 1ull) | kXferDone);   // (consumed before a restart of this grid)
+        rdy = !done && sq == idx + 1ull;
+      }
       const unsigned long long rb = __ballot(rdy);
       if (rb) {
-        xfer_resume<COOP>(a, rdy, en, idx, lane, t_begin, seen_ep);
+        xfer_resume<COOP>(a, rdy, en, idx, lane, t_begin, seen_ep, kx);
         done = done || rdy;
       }
       if (__ballot(!done) == 0ull) break;   // the ticket's 64 entries are handled
       if (!rb) {
-        unsigned long long v = 0;
-        if (lane == 0) v = __hip_atomic_load(&a.st->dprod, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (rfl64(v) & kRingStop) return;
-        if (__builtin_amdgcn_s_memrealtime() - t_begin > a.deadline) return;
-        __builtin_amdgcn_s_sleep(2);
+        // stopping: what is reserved of this ticket is handled - the rest will never come
+        if (stopping() && __ballot(reserved && !done) == 0ull) return;
+        if (tl <= first) __builtin_amdgcn_s_sleep(32);
+        else __builtin_amdgcn_s_sleep(2);
       }
     }
   }
@@ -552,13 +588,15 @@ __device__ __forceinline__ void xfer_serve(const RingArgs& a, uint32_t lane, uns
 // plane's inbox; the grid's last xfer_wgs workgroups serve this plane's inbox).
 template <int HASH, int ACL, bool COOP, bool V6 = false, bool GDE = false, bool XF = false>
 __global__ __launch_bounds__(kRingBlock, (GDE || XF) ? 2 : 1) void ring_kernel(RingArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   if constexpr (XF) {
     if (blockIdx.x >= gridDim.x - a.xfer_wgs) {   // (block-uniform: the whole workgroup serves the inbox)
-      xfer_serve<COOP>(a, threadIdx.x & 63u, __builtin_amdgcn_s_memrealtime());
+      const RingLds Lx = ring_lds(HASH, ACL, COOP ? a.lds_tiles : a.acl_tiles);
+      uint4* kxx = reinterpret_cast<uint4*>(smem + Lx.kx) + (threadIdx.x >> 6) * 64;
+      xfer_serve<COOP>(a, threadIdx.x & 63u, __builtin_amdgcn_s_memrealtime(), kxx);
       return;
     }
   }
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   __shared__ unsigned long long coop_tk;                      // ticket
   __shared__ uint32_t coop_ctl[4];                            // go, epoch, table-set serial, ctl gen
   __shared__ uint32_t coop_best[COOP ? kRingWaves : 1][64];   // per-wave ACL partial minima
@@ -846,19 +884,21 @@ __global__ __launch_bounds__(kRingBlock, (GDE || XF) ? 2 : 1) void ring_kernel(R
     if constexpr (GDE)   // GPU-direct egress: frames for memif vports straight into the pods' rings
       gde_deliver(a, qst, qi, tk, lane, t_begin, !pad && !e.reason && !e.xhdr && !e.flood && olen <= 64u,
                   e.out_port, olen, o, meta, kx);
-    wave_frames_store<kSysAux>(kx, o, r_out, run);
-    __builtin_amdgcn_raw_buffer_store_b32(meta, r_meta, i * 4u, 0, kSysAux);
-    if constexpr (XF) {   // split chains: frames handed to another plane's grid (ring.h XferEntry)
-      const bool xf = !pad && e.reason == kRemote;
-      const unsigned long long bx = __ballot(xf);
+    // split chains (XF): frames handed to another plane's grid (ring.h XferEntry) are not stored
+    // here - their resumer writes their out slot and meta, so no ordering between the two is needed
+    const unsigned long long bx = XF ? __ballot(!pad && e.reason == kRemote) : 0ull;
+    wave_frames_store<kSysAux>(kx, o, r_out, run, bx);
+    __builtin_amdgcn_raw_buffer_store_b32(meta, r_meta, ((bx >> lane) & 1ull) ? kNoRun : i * 4u, 0, kSysAux);
+    if constexpr (XF) {
       if (bx) {
-        __builtin_amdgcn_s_waitcnt(0);   // (the resumer's stores into these slots land after ours)
+        // the chunk's pending count goes UP by the hand-offs (an add, not a store: a resumer's
+        // decrement may land first; the word reads 0 only once both have, and the add is done
+        // before the chunk's flag - the waitcnt below - so the host never sees an early 0)
         if (lane == 0)
-          __hip_atomic_store(a.xpend + (size_t)qi * nch_q + (tk32 & nch_mask), (uint32_t)__builtin_popcountll(bx),
-                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __builtin_amdgcn_s_waitcnt(0);   // the count is in place before any resumer can lower it
-        xfer_send(a, xf, e.out_port, o, hop_state_of(p, st, e, act, acl_rule, hash), a.xplane | (qi << 8), i, lane,
-                  t_begin);
+          __hip_atomic_fetch_add(a.xpend + (size_t)qi * nch_q + (tk32 & nch_mask), (uint32_t)__builtin_popcountll(bx),
+                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        xfer_send(a, ((bx >> lane) & 1ull) != 0ull, e.out_port, o, hop_state_of(p, st, e, act, acl_rule, hash),
+                  a.xplane | (qi << 8), i, lane, t_begin);
       }
     }
     if (a.side.cnt) {
@@ -1185,6 +1225,7 @@ void RingEngine::start(const FusedLaunch& f, const LaunchCfg& cfg, double deadli
     r.nplanes = nplanes_;
     r.xfer_wgs = xwgs_;
     r.xpend = d_xpend_;
+    std::memset(h_xpend_, 0, (size_t)nq_ * nch_ * 4);   // (chunk pending counts are added to: a new session starts at 0)
     xfer_active_ = true;
   }
   ck(launch_ring(r, cfg, wgs_, coop_, stream_), "launch");

@@ -375,7 +375,11 @@ class NativeLivePath:
     # stores the final header straight into the entry ring's out slot; the engine delivers a burst
     # once every frame of it is back (no host hop, no launch).  Not with GPU-direct egress (its
     # instances do not hand off) nor IPv6 tables (the V6 instances run a split chain where it entered).
-    XFER_ENTRIES = 1 << 15
+    # The inbox holds 128-B entries (16 MB at 1<<17): room for every frame a saturated entry plane
+    # can have in flight; an eighth of each grid's workgroups serve it (every wave on its own ticket
+    # of 64 entries), so a hand-off is picked up within a poll period however many queues feed it.
+    XFER_ENTRIES = 1 << 17
+    XFER_WG_SHARE = 8
 
     def _wire_xfer(self) -> None:
         self.xfer = len(self._rings) > 1 and not self.gpu_egress
@@ -387,7 +391,8 @@ class NativeLivePath:
                 if a != b and not self.nf.enable_peer_access(a, b):
                     raise RuntimeError(f"cuda:{a} cannot store into cuda:{b}'s memory (no peer access)")
         for r in self._rings:
-            r.eng.xfer_enable(self.XFER_ENTRIES, 1)
+            wgs = max(1, min(int(r.cus) - self.queues, int(r.cus) // self.XFER_WG_SHARE))
+            r.eng.xfer_enable(self.XFER_ENTRIES, wgs)
         descs = [r.eng.xfer_desc() for r in self._rings]
         for k, r in enumerate(self._rings):
             r.eng.xfer_set_peers(k, descs)
