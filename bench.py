@@ -758,13 +758,16 @@ def main() -> None:
             # loaded: throughput ring (every wave takes its own chunks), 32 x 4096 packets in flight.
             # One trial is a few ms of GPU work, so a single host-thread stall (the host both
             # publishes and reaps) can halve it: 5 trials of 10000 batches, the median reported.
-            rq = RingPath(dp, capacity=1 << 17, wgs_per_cu=2, deadline_s=120.0, coop=False)
-            rq.stage(batches[0][0][: 1 << 17], batches[0][1][: 1 << 17])
+            # 64 chunks of 4096 in flight (tools/ring_ab.py, r6: 4,622 Mpps median against 2,869 at 32
+            # in flight - the host thread's publish -> reap loop needs that much depth to cover the
+            # grid's completion latency; the r4/r5 swings were this depth at 32 plus box drift)
+            rq = RingPath(dp, capacity=1 << 18, wgs_per_cu=2, deadline_s=120.0, coop=False)
+            rq.stage(batches[0][0][: 1 << 18], batches[0][1][: 1 << 18])
             rq.start()
-            rq.probe(batches=500, batch=4096, inflight=32)  # warm-up
+            rq.probe(batches=500, batch=4096, inflight=64)  # warm-up
             trials, lat2 = [], []
             for _ in range(5):
-                lt, el2 = rq.probe(batches=10000, batch=4096, inflight=32)
+                lt, el2 = rq.probe(batches=10000, batch=4096, inflight=64)
                 trials.append(10000 * 4096 / el2 / 1e6)
                 lat2.append(lt[200:])
             rq.stop()

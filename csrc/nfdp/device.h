@@ -778,6 +778,22 @@ __device__ __forceinline__ void store_b128(v4u w, __amdgpu_buffer_rsrc_t r, uint
 // instruction's SGPR offset, the lane part is one loop-invariant VGPR plus the immediate.
 constexpr uint32_t kNoRun = 0x80000000u;
 
+// LDS layout of one 16-slot pass of the frame transposes (wave_frames_to_lanes / wave_frames_store,
+// the ring's write-backs): chunk k of slot f at kx[16k + (f ^ 5k)].  Both sides of a transpose are
+// then free of bank conflicts - the 16 lanes that each hold a whole slot and touch chunk k of it,
+// and the 64 lanes that each hold one chunk (lane L: chunk L & 3 of slot L >> 2) - where the plain
+// [slot][chunk] layout costs the 16-lane side 4-way conflicts (SQ_LDS_BANK_CONFLICT, r6 PMC pass:
+// 24M conflict cycles per headline dispatch against 19M active LDS cycles).  Off: the per-chunk
+// addresses raise the headline instance's spills from 15 to 19 VGPRs at its 128-VGPR budget, and
+// that costs more than the conflicts (r6 s10 A/B, profiles/r6_s10_ab_256.jsonl: 13,961 vs 15,428
+// Mpps; ClassBench-style set 7,926 vs 7,972).
+#ifndef NFDP_KX_SWZ
+#define NFDP_KX_SWZ 0
+#endif
+__device__ __forceinline__ uint32_t kx_at(uint32_t f, uint32_t k) {
+  return NFDP_KX_SWZ ? 16u * k + (f ^ ((5u * k) & 15u)) : 4u * f + k;
+}
+
 template <int AUX>
 __device__ __forceinline__ void wave_frames_load(__amdgpu_buffer_rsrc_t r, uint32_t run, v4u c[4]) {
   const uint32_t lane = threadIdx.x & 63u;
@@ -792,7 +808,8 @@ __device__ __forceinline__ void wave_frames_load(__amdgpu_buffer_rsrc_t r, uint3
 template <bool SW = false>
 __device__ __forceinline__ void wave_frames_to_lanes(uint4* kx, const v4u c[4], uint32_t* d) {
   const uint32_t lane = threadIdx.x & 63u;
-  const uint32_t lw = SW ? lane ^ ((lane >> 4) & 3u) : lane, sw = SW ? (lane >> 2) & 3u : 0u;
+  const uint32_t lw = NFDP_KX_SWZ ? kx_at(lane >> 2, lane & 3u) : SW ? lane ^ ((lane >> 4) & 3u) : lane;
+  const uint32_t sw = SW && !NFDP_KX_SWZ ? (lane >> 2) & 3u : 0u;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     kx[lw] = make_uint4(c[q].x, c[q].y, c[q].z, c[q].w);
@@ -801,7 +818,7 @@ __device__ __forceinline__ void wave_frames_to_lanes(uint4* kx, const v4u c[4], 
     if ((lane >> 4) == (uint32_t)q) {
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        const uint4 v = kx[4u * (lane & 15u) + ((uint32_t)k ^ sw)];
+        const uint4 v = kx[NFDP_KX_SWZ ? kx_at(lane & 15u, (uint32_t)k) : 4u * (lane & 15u) + ((uint32_t)k ^ sw)];
         d[4 * k] = v.x; d[4 * k + 1] = v.y; d[4 * k + 2] = v.z; d[4 * k + 3] = v.w;
       }
     }
@@ -819,11 +836,11 @@ __device__ __forceinline__ void wave_frames_store(uint4* kx, const uint32_t* o, 
   for (int q = 0; q < 4; ++q) {
     if ((lane >> 4) == (uint32_t)q) {
 #pragma unroll
-      for (int k = 0; k < 4; ++k) kx[4u * (lane & 15u) + k] = make_uint4(o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]);
+      for (int k = 0; k < 4; ++k) kx[kx_at(lane & 15u, k)] = make_uint4(o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]);
     }
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-    const uint4 v = kx[lane];
+    const uint4 v = kx[kx_at(lane >> 2, lane & 3u)];
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
     const v4u w = {v.x, v.y, v.z, v.w};

@@ -298,11 +298,11 @@ __device__ __forceinline__ void gde_deliver(const RingArgs& a, RingDevState* qst
       if (((bgo >> (16 * q)) & 0xFFFFull) == 0ull) continue;   // (wave-uniform)
       if ((lane >> 4) == (uint32_t)q) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) kx[4u * (lane & 15u) + k] = make_uint4(o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]);
+        for (int k = 0; k < 4; ++k) kx[kx_at(lane & 15u, k)] = make_uint4(o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]);
       }
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-      const uint4 v = kx[lane];
+      const uint4 v = kx[kx_at(lane >> 2, lane & 3u)];
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
       const int src = 16 * q + (int)(lane >> 2);
@@ -481,11 +481,11 @@ __device__ __forceinline__ void xfer_resume(const RingArgs& a, bool rdy, XferEnt
       if (((bm >> (16 * q)) & 0xFFFFull) == 0ull) continue;   // (wave-uniform)
       if ((lane >> 4) == (uint32_t)q) {
 #pragma unroll
-        for (int k = 0; k < 4; ++k) kx[4u * (lane & 15u) + k] = make_uint4(o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]);
+        for (int k = 0; k < 4; ++k) kx[kx_at(lane & 15u, k)] = make_uint4(o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]);
       }
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-      const uint4 v = kx[lane];
+      const uint4 v = kx[kx_at(lane >> 2, lane & 3u)];
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
       const int src = 16 * q + (int)(lane >> 2);
@@ -951,6 +951,13 @@ __global__ __launch_bounds__(kRingBlock, (GDE || XF) ? 2 : 1) void ring_kernel(R
   on_idle();  // exit: whatever this wave counted since its last flush reaches the global table
 }
 
+// why the last launch_ring on this thread refused its arguments (RingEngine::start's message)
+thread_local const char* g_ring_why = "";
+static hipError_t ring_bad(const char* why) {
+  g_ring_why = why;
+  return hipErrorInvalidValue;
+}
+
 template <int H, int A, bool C, bool V6 = false, bool G = false, bool X = false>
 static hipError_t launch_ring_t(const RingArgs& a, int num_cus, int wgs, hipStream_t s) {
   const size_t lds = ring_lds(H, A, C ? a.lds_tiles : a.acl_tiles).total;
@@ -959,7 +966,7 @@ static hipError_t launch_ring_t(const RingArgs& a, int num_cus, int wgs, hipStre
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
-  if ((lds + 2048) * (size_t)wgs > 160 * 1024) return hipErrorInvalidValue;
+  if ((lds + 2048) * (size_t)wgs > 160 * 1024) return ring_bad("LDS per workgroup x workgroups per CU exceeds the CU's 160 KB");
   hipLaunchKernelGGL((ring_kernel<H, A, C, V6, G, X>), dim3((uint32_t)(num_cus * wgs)), dim3(kRingBlock), lds, s, a);
   return hipGetLastError();
 }
@@ -997,26 +1004,26 @@ hipError_t launch_ring(const RingLaunch& r, const LaunchCfg& cfg, int wgs_per_cu
   a.xpend = r.xpend;
   a.nq = r.queues ? r.queues : 1u;
   // every queue needs a workgroup; the side list indexes slots of one ring only
-  if ((uint64_t)cfg.num_cus * (uint64_t)wgs_per_cu < a.nq || (a.nq > 1 && a.side.cnt)) return hipErrorInvalidValue;
-  if (coop && (!a.sets || a.lds_tiles < a.acl_tiles)) return hipErrorInvalidValue;
-  if (!a.port_ctr || !a.drop_ctr || !a.ctl || !a.flags || !a.st) return hipErrorInvalidValue;
-  if (((r.ring_mask + 1) & r.ring_mask) != 0 || r.ring_mask < 63) return hipErrorInvalidValue;
+  if ((uint64_t)cfg.num_cus * (uint64_t)wgs_per_cu < a.nq || (a.nq > 1 && a.side.cnt)) return ring_bad("fewer workgroups than queues, or a side list with several queues");
+  if (coop && (!a.sets || a.lds_tiles < a.acl_tiles)) return ring_bad("coop ring without table sets or with fewer LDS tiles than ACL tiles");
+  if (!a.port_ctr || !a.drop_ctr || !a.ctl || !a.flags || !a.st) return ring_bad("missing counters / control words");
+  if (((r.ring_mask + 1) & r.ring_mask) != 0 || r.ring_mask < 63) return ring_bad("ring size not a power of two >= 64");
   if (cfg.acl_mode == kAclMfma && (a.acl_tiles == 0 || a.acl_tiles > kAclMaxRules / 16 || !a.acl_wfrag || !a.acl_cinit))
-    return hipErrorInvalidValue;
-  if (cfg.hash_mode == kHashMfma && !a.toep_frag) return hipErrorInvalidValue;
-  if (cfg.hash_mode == kHashLds && !a.toep_tab) return hipErrorInvalidValue;
-  if (wgs_per_cu < 1 || wgs_per_cu > 8 || cfg.num_cus < 1) return hipErrorInvalidValue;
+    return ring_bad("ACL tiles out of range or missing fragments");
+  if (cfg.hash_mode == kHashMfma && !a.toep_frag) return ring_bad("MFMA hash without its fragments");
+  if (cfg.hash_mode == kHashLds && !a.toep_tab) return ring_bad("LDS hash without its table");
+  if (wgs_per_cu < 1 || wgs_per_cu > 8 || cfg.num_cus < 1) return ring_bad("workgroups per CU not in [1, 8]");
   const int h = cfg.hash_mode, ac = cfg.acl_mode;
   if (a.xpeers) {   // split chains across planes: the XF instances (IPv4 tables, MFMA ACL, no GDE)
     if (ac != kAclMfma || h == kHashScalar || a.gde || v6_keys(a.t)) return hipErrorNotSupported;
     if (!a.xpend || a.xfer_wgs == 0 || a.nplanes == 0 || a.nplanes > kMaxXferPlanes || a.xplane >= a.nplanes ||
         (uint64_t)cfg.num_cus * (uint64_t)wgs_per_cu < (uint64_t)a.nq + a.xfer_wgs)
-      return hipErrorInvalidValue;
+      return ring_bad("cross-plane hops: bad peers / pending words / too few workgroups for queues + inbox service");
 #define NFDP_XCASE(HH, CC) \
     if (h == HH && coop == CC) return launch_ring_t<HH, kAclMfma, CC, false, false, true>(a, cfg.num_cus, wgs_per_cu, s);
     NFDP_XCASE(kHashLds, true) NFDP_XCASE(kHashLds, false) NFDP_XCASE(kHashMfma, true) NFDP_XCASE(kHashMfma, false)
 #undef NFDP_XCASE
-    return hipErrorInvalidValue;
+    return ring_bad("no ring instance for this configuration");
   }
   if (a.gde) {   // GPU-direct egress: its instances (LDS or MFMA hash, MFMA ACL, IPv4 or IPv6 tables)
     if (ac != kAclMfma || h == kHashScalar) return hipErrorNotSupported;
@@ -1027,7 +1034,7 @@ hipError_t launch_ring(const RingLaunch& r, const LaunchCfg& cfg, int wgs_per_cu
     NFDP_GCASE(kHashLds, false, true) NFDP_GCASE(kHashMfma, true, false) NFDP_GCASE(kHashMfma, false, false)
     NFDP_GCASE(kHashMfma, true, true) NFDP_GCASE(kHashMfma, false, true)
 #undef NFDP_GCASE
-    return hipErrorInvalidValue;
+    return ring_bad("no ring instance for this configuration");
   }
   if (v6_keys(a.t)) {   // IPv6 flows / rules: the V6 instances (LDS or MFMA hash, MFMA ACL)
     if (ac != kAclMfma || h == kHashScalar) return hipErrorNotSupported;
@@ -1044,7 +1051,7 @@ hipError_t launch_ring(const RingLaunch& r, const LaunchCfg& cfg, int wgs_per_cu
   NFDP_RCASE(1, 0) NFDP_RCASE(1, 1) NFDP_RCASE(1, 2)
   NFDP_RCASE(2, 0) NFDP_RCASE(2, 1) NFDP_RCASE(2, 2)
 #undef NFDP_RCASE
-  return hipErrorInvalidValue;
+  return ring_bad("no ring instance for this configuration");
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1228,7 +1235,10 @@ void RingEngine::start(const FusedLaunch& f, const LaunchCfg& cfg, double deadli
     std::memset(h_xpend_, 0, (size_t)nq_ * nch_ * 4);   // (chunk pending counts are added to: a new session starts at 0)
     xfer_active_ = true;
   }
-  ck(launch_ring(r, cfg, wgs_, coop_, stream_), "launch");
+  g_ring_why = "";
+  const hipError_t le = launch_ring(r, cfg, wgs_, coop_, stream_);
+  if (le != hipSuccess) throw std::runtime_error(std::string("ring: launch: ") + hipGetErrorString(le) +
+                                                 (*g_ring_why ? std::string(" (") + g_ring_why + ")" : std::string()));
   set_running(true);
 }
 

@@ -6,7 +6,8 @@ headline step (1M flows, ACL 256 -> SNAT -> L2, 4M-packet batches) with HIP even
 alternate round by round so box drift hits them equally.
 
 python tools/ab_variants.py base= variants/noreload [--rounds 4] [--iters 50] [--acl 256|wild|ipv6]
-  (an empty directory means the in-tree build)
+  (an empty directory means the in-tree build; name=dir:kernel launches a stamp kernel before every
+  batch, the pre-r6 release stamp, instead of the fused kernel's own)
 python tools/ab_variants.py --inline [--acl ...]   one in-process measurement of the in-tree build
   (for rocprofv3: no child process)
 """
@@ -22,6 +23,7 @@ sys.path.insert(0, ".")
 from dpu_operator_amd.dataplane import scenario as S
 from dpu_operator_amd.dataplane.engine import DataPlane
 iters, batch, acl = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3]
+stamp_kernel = len(sys.argv) > 4 and sys.argv[4] == "kernel"
 g = DataPlane(device="cuda", flow_buckets=1 << 19, hash_mode="lds", acl_mode="mfma")
 sc = S.build_sfc(g, n_pods=8, n_flows=1 << 20, n_acl=256, seed=0)
 if acl == "wild":
@@ -40,13 +42,19 @@ for r in range(4):
         im = np.ascontiguousarray(np.concatenate([im4, im6])[perm])
     bs.append((torch.from_numpy(pk).cuda(), torch.from_numpy(im.view(np.int32)).cuda()))
 out, meta, lat = g.alloc_batch(batch)
+def step(k):
+    if stamp_kernel:   # the pre-r6 release stamp: a stamp kernel in front of every batch
+        g.nf.launch_stamp(g._ptr("t0"), torch.cuda.current_stream().cuda_stream)
+        g.run(*bs[k % 4], out, meta, lat, stamp=False)
+    else:
+        g.run(*bs[k % 4], out, meta, lat)
 for k in range(10):
-    g.run(*bs[k % 4], out, meta, lat)
+    step(k)
 torch.cuda.synchronize()
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 e0.record()
 for k in range(iters):
-    g.run(*bs[k % 4], out, meta, lat)
+    step(k)
 e1.record()
 torch.cuda.synchronize()
 ms = e0.elapsed_time(e1) / iters
@@ -71,11 +79,12 @@ def main():
     res = {n: [] for n, _ in vs}
     for r in range(a.rounds):
         for n, d in vs:
+            d, _, mode = d.partition(":")   # dir[:kernel] - "kernel": a stamp kernel before each batch
             env = dict(os.environ)
             env.pop("NFDP_EXT_DIR", None)
             if d:
                 env["NFDP_EXT_DIR"] = os.path.abspath(d)
-            p = subprocess.run([sys.executable, "-c", CHILD, str(a.iters), str(a.batch), a.acl], env=env,
+            p = subprocess.run([sys.executable, "-c", CHILD, str(a.iters), str(a.batch), a.acl, mode or "self"], env=env,
                                capture_output=True, text=True, timeout=300)
             line = [x for x in p.stdout.splitlines() if x.startswith("{")]
             if not line:

@@ -50,6 +50,7 @@ def main():
             pk, im = S.traffic(sc, a.batch, seed=1 + r)
             bs.append((torch.from_numpy(pk).cuda(), torch.from_numpy(im.view(np.int32)).cuda()))
         planes[name] = (g, bs)
+        print(f"plane {name} ready", file=sys.stderr, flush=True)
     # the ClassBench-style rule set (bench value_acl_wild) on the headline's flows: the early-fetch
     # 2-wave instance (default from 33 rule tiles) against the 4-wave instance with per-tile prefilters
     g = DataPlane(device="cuda", flow_buckets=1 << 19, hash_mode="lds", acl_mode="mfma")
@@ -69,7 +70,8 @@ def main():
                 "acl1024": ("acl1024", 0), "acl1024_no_early": ("acl1024", 256)}
     res = {k: [] for k in variants}
     bufs = {k: planes[k][0].alloc_batch(a.batch) for k in planes}
-    for _ in range(a.rounds):
+    for rd in range(a.rounds):
+        print(f"round {rd}", file=sys.stderr, flush=True)
         for v, (pl, flags) in variants.items():
             g, bs = planes[pl]
             out, meta, lat = bufs[pl]

@@ -38,12 +38,19 @@ def main():
             "w2_if16_b8192": (2, 16, 8192, 1 << 17)}
     res = {k: [] for k in cfgs}
     lat64 = []
+    errs = {}
     out, meta, lat = dp.alloc_batch(1 << 16)
     for t in range(a.trials):
+        print(f"trial {t}", file=sys.stderr, flush=True)
         for name, (w, inflight, batch, cap) in cfgs.items():
             rq = RingPath(dp, capacity=cap, wgs_per_cu=w, deadline_s=120.0, coop=False)
             rq.stage(tpk[:cap], tim[:cap])
-            rq.start()
+            try:
+                rq.start()
+            except RuntimeError as ex:   # (a configuration the CU cannot hold: recorded, not fatal)
+                errs[name] = str(ex)
+                rq.close()
+                continue
             rq.probe(batches=500, batch=batch, inflight=inflight)
             _, el = rq.probe(batches=a.batches, batch=batch, inflight=inflight)
             rq.stop()
@@ -55,7 +62,8 @@ def main():
         lat64.append(float(np.median(lat.cpu().numpy().view(np.uint32).astype(np.float64) * 0.01)))
         time.sleep(0.05)
     print(json.dumps({"ring_loaded_mpps": {k: {"median": round(float(np.median(v)), 1), "trials": [round(x, 1) for x in v]}
-                                           for k, v in res.items()},
+                                           for k, v in res.items() if v},
+                      "errors": errs,
                       "p50_latency_us_64k_batch": {"median": round(float(np.median(lat64)), 2),
                                                    "trials": [round(x, 2) for x in lat64]}}), flush=True)
 
