@@ -210,7 +210,8 @@ struct alignas(128) XferEntry {
   HopState hs;                  // 32 B: what resume_stage needs
   uint32_t origin;              // entry plane | queue << 8
   uint32_t pos;                 // slot position in that queue's ring
-  uint32_t pad0[2];
+  uint32_t t_send;              // producer's s_memrealtime (low word) at the send
+  uint32_t pad0;
   uint64_t seq;                 // idx + 1 once written; | kXferDone once consumed
   uint64_t pad1;
 };
@@ -219,7 +220,11 @@ struct alignas(128) XferInbox {   // (device memory of the resuming plane)
   uint64_t tail;                  // entries reserved by the producers (system-scope adds)
   uint32_t pad0[30];
   uint64_t claim;                 // inbox chunk tickets claimed by this grid's inbox waves
-  uint32_t pad1[30];
+  // hand-off timing (s_memrealtime ticks, 100 MHz; one sample per resume pass, its first entry):
+  // send -> picked up by an inbox wave, picked up -> written back (slot, meta, pending count)
+  // (t_work split: entry loaded, chain stages done, write-back complete)
+  uint64_t t_wait, t_work, n_timed, t_load, t_stage, t_wb;
+  uint32_t pad1[18];
 };
 static_assert(sizeof(XferInbox) == 256, "XferInbox");
 struct XferPeer {                 // one plane, as every grid sees it

@@ -408,7 +408,7 @@ __device__ __forceinline__ void xfer_send(const RingArgs& a, bool go, uint32_t p
     for (int k = 0; k < 4; ++k) store_b128<kSysAux>(v4u{o[4 * k], o[4 * k + 1], o[4 * k + 2], o[4 * k + 3]}, re, off + 16u * k, 0);
     store_b128<kSysAux>(v4u{hw[0], hw[1], hw[2], hw[3]}, re, off + 64u, 0);
     store_b128<kSysAux>(v4u{hw[4], hw[5], hw[6], hw[7]}, re, off + 80u, 0);
-    store_b128<kSysAux>(v4u{origin, pos, 0u, 0u}, re, off + 96u, 0);
+    store_b128<kSysAux>(v4u{origin, pos, (uint32_t)__builtin_amdgcn_s_memrealtime(), 0u}, re, off + 96u, 0);
     __builtin_amdgcn_s_waitcnt(0);   // the entry is in the peer's memory before its seq says so
     if (mine) __hip_atomic_store(&en->seq, idx + 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
@@ -419,6 +419,7 @@ __device__ __forceinline__ void xfer_send(const RingArgs& a, bool go, uint32_t p
 template <bool COOP>
 __device__ __forceinline__ void xfer_resume(const RingArgs& a, bool rdy, XferEntry* en, unsigned long long idx, uint32_t lane,
                                          unsigned long long t_begin, uint32_t& seen_ep, uint4* kx) {
+  const uint32_t t_pick = (uint32_t)__builtin_amdgcn_s_memrealtime();
   unsigned long long v = 0;
   if (lane == 0) v = __hip_atomic_load(&a.st->dprod, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const uint32_t ep = ring_epoch(rfl64(v));
@@ -428,27 +429,35 @@ __device__ __forceinline__ void xfer_resume(const RingArgs& a, bool rdy, XferEnt
   }
   const TablesView& T = COOP ? a.sets[(ep & kEpochSetBit) >> 1].t : a.t;
   const DirectTables ta{T};
-  // the entry (system-coherent loads: a peer wrote it)
-  const __amdgpu_buffer_rsrc_t re = __builtin_amdgcn_make_buffer_rsrc((void*)en, (short)0, 128, kBufRaw);
+  // the entry (system-coherent loads: a peer wrote it).  One descriptor over the whole inbox and a
+  // per-lane offset: a descriptor built from each lane's own entry pointer is not wave-uniform and
+  // compiles to a loop over the 64 lanes (r6: 17 us of a 22-us resume pass, unloaded)
+  const uint32_t cmask = a.xpeers[a.xplane].cap_mask;
+  const __amdgpu_buffer_rsrc_t re = __builtin_amdgcn_make_buffer_rsrc((void*)a.xpeers[a.xplane].entries, (short)0,
+                                                                      (int)((cmask + 1u) * 128u), kBufRaw);
+  const uint32_t eo = rdy ? (uint32_t)(idx & cmask) * 128u : kNoRun;
   uint32_t d[kSlotDwords], hw[8];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    const v4u c = __builtin_amdgcn_raw_buffer_load_b128(re, rdy ? 16u * k : kNoRun, 0, kSysAux);
+    const v4u c = __builtin_amdgcn_raw_buffer_load_b128(re, eo, 16 * k, kSysAux);
     d[4 * k] = c[0]; d[4 * k + 1] = c[1]; d[4 * k + 2] = c[2]; d[4 * k + 3] = c[3];
   }
   {
-    const v4u c0 = __builtin_amdgcn_raw_buffer_load_b128(re, rdy ? 64u : kNoRun, 0, kSysAux);
-    const v4u c1 = __builtin_amdgcn_raw_buffer_load_b128(re, rdy ? 80u : kNoRun, 0, kSysAux);
+    const v4u c0 = __builtin_amdgcn_raw_buffer_load_b128(re, eo, 64, kSysAux);
+    const v4u c1 = __builtin_amdgcn_raw_buffer_load_b128(re, eo, 80, kSysAux);
     hw[0] = c0[0]; hw[1] = c0[1]; hw[2] = c0[2]; hw[3] = c0[3]; hw[4] = c1[0]; hw[5] = c1[1]; hw[6] = c1[2]; hw[7] = c1[3];
   }
-  const v4u way = __builtin_amdgcn_raw_buffer_load_b128(re, rdy ? 96u : kNoRun, 0, kSysAux);
+  const v4u way = __builtin_amdgcn_raw_buffer_load_b128(re, eo, 96, kSysAux);
   const uint32_t origin = way[0], pos = way[1];
   const HopState hs = hs_unpack(hw);
   Parsed p;
   IngressState st;
+  __builtin_amdgcn_s_waitcnt(0);   // (timing: the entry is in)
+  const uint32_t t_ld = (uint32_t)__builtin_amdgcn_s_memrealtime();
   resume_ingress(ta, d, hs.inmeta, p, st);
   EgressDecision e = resume_stage<DirectTables, false>(T, ta, p, st, hs.act, hs.acl_rule, hs.hash, hs.hop);
   xfer_check(e, a.nplanes);
+  const uint32_t t_sg = (uint32_t)__builtin_amdgcn_s_memrealtime() + (e.out_port & 0u);
   uint32_t o[kSlotDwords];
   emit(p, e.tci, e.push != 0, o);
   const uint32_t olen = out_len(p, e);
@@ -496,6 +505,7 @@ __device__ __forceinline__ void xfer_resume(const RingArgs& a, bool rdy, XferEnt
     __builtin_amdgcn_raw_buffer_store_b32(meta, rm, ok ? at * 4u : kNoRun, 0, kSysAux);
   }
   __builtin_amdgcn_s_waitcnt(0);   // (the slots are in host memory before their chunk's count moves)
+  const uint32_t t_wb = (uint32_t)__builtin_amdgcn_s_memrealtime();
   // pending counts: one system-scope subtraction per (entry plane, queue, chunk)
   const uint32_t chunk = pos >> 6;
   rem = __ballot(fin);
@@ -512,6 +522,19 @@ __device__ __forceinline__ void xfer_resume(const RingArgs& a, bool rdy, XferEnt
   }
   // entries consumed (a producer a ring later may reuse them), counters of this plane
   if (rdy) __hip_atomic_store(&en->seq, (idx + 1ull) | kXferDone, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  {   // hand-off timing sample: this pass's first entry
+    const unsigned long long rbm = __ballot(rdy);
+    if (rbm && lane == 0) {
+      XferInbox* ib = a.xpeers[a.xplane].inbox;
+      const uint32_t ts = __builtin_amdgcn_readlane(way[2], __builtin_ctzll(rbm));
+      atomicAdd(&ib->t_wait, (unsigned long long)(t_pick - ts));
+      atomicAdd(&ib->t_work, (unsigned long long)((uint32_t)__builtin_amdgcn_s_memrealtime() - t_pick));
+      atomicAdd(&ib->n_timed, 1ull);
+      atomicAdd(&ib->t_load, (unsigned long long)(t_ld - t_pick));
+      atomicAdd(&ib->t_stage, (unsigned long long)(t_sg - t_ld));
+      atomicAdd(&ib->t_wb, (unsigned long long)(t_wb - t_sg));
+    }
+  }
   if (rdy && !(a.flags_bits & kRingNoCounters)) {
     if (e.reason) atomicAdd(a.drop_ctr + (e.reason & (kNumReasons - 1)), 1ull);
     else if (e.out_port < (uint32_t)kMaxPorts) atomicAdd(a.port_ctr + 2 * e.out_port + 1, ctr_inc(olen));
@@ -1367,7 +1390,7 @@ std::vector<uint64_t> RingEngine::xfer_stats() {
   if (!d_xin_) return {};
   XferInbox h{};
   ck(hipMemcpy(&h, d_xin_, sizeof(h), hipMemcpyDeviceToHost), "inbox stats");
-  return {h.tail, h.claim};
+  return {h.tail, h.claim, h.t_wait, h.t_work, h.n_timed, h.t_load, h.t_stage, h.t_wb};
 }
 
 uint64_t RingEngine::gde_clear(uint32_t port, uint32_t q) {

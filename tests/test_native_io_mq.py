@@ -759,4 +759,4 @@ def test_split_chain_live_crosses_planes(shm, placement, split, whole):
     finally:
         live.stop()
     st = [r.eng.xfer_stats() for r in live._rings] if live._rings else None
-    assert st is None or all(len(x) == 2 for x in st)
+    assert st is None or all(len(x) == 8 and x[4] > 0 for x in st if x[0])

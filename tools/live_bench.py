@@ -122,7 +122,7 @@ def run(device: str = "cuda", n_pods: int = 8, flows: int = 1 << 20, n_acl: int 
         hash_mode: str = "lds", tx_workers: int = 0, queues: int = 8, max_inflight_frames: int = 4096,
         pod_ring: int = 1024, backend: str = "pipeline", coalesce_us: float = 8.0, loaded_window: int = 2048,
         traffic: str = "plain", zero_copy: bool = False, saturated_only: bool = False, gpu_egress: bool = False,
-        trials: int = 1, split: str = "", planes: str = "") -> dict:
+        trials: int = 1, split: str = "", planes: str = "", idle_only: bool = False) -> dict:
     """traffic: "plain" (the headline SFC), "vxlan-egress" (every pod's VF a VXLAN tunnel port:
     all frames leave encapsulated through one underlay vport, outer headers from the per-burst
     side pass) or "broadcast" (pods on one learning bridge sending to ff:ff:ff:ff:ff:ff: every
@@ -199,6 +199,26 @@ def run(device: str = "cuda", n_pods: int = 8, flows: int = 1 << 20, n_acl: int 
                "max_inflight_frames": max_inflight_frames, "pod_ring": pod_ring, "gen_threads": threads,
                "pods": n_pods, "flows": flows, "acl_rules": n_acl, "frame_bytes": 64,
                "setup_s": round(setup_s, 1)}
+        if split and idle_only:
+            # the split chain's hand-off, unloaded: one frame in flight, then the inbox's timing
+            # (ring.h XferInbox: send -> picked up, picked up -> written back) per plane
+            r1 = nf.trafgen_run(pods, duration_s=min(duration, 0.5), warmup_s=0.05, threads=1, burst=1, inflight=1)
+            out.update(idle_p50_us=_pct(r1["lat_us"], 50), idle_p99_us=_pct(r1["lat_us"], 99),
+                       idle_frames=int(r1["received"]))
+            rings = list(live._rings)
+            live.stop()
+            xs = []
+            for rg in rings:
+                x = list(map(int, rg.eng.xfer_stats()))
+                n = max(x[4], 1) if len(x) >= 5 else 1
+                xs.append({"entries": x[0], "samples": x[4] if len(x) >= 5 else 0,
+                           "send_to_pickup_us": round(x[2] / n * 0.01, 2) if len(x) >= 5 else None,
+                           "pickup_to_back_us": round(x[3] / n * 0.01, 2) if len(x) >= 5 else None,
+                           **({"entry_load_us": round(x[5] / n * 0.01, 2), "stages_us": round(x[6] / n * 0.01, 2),
+                               "write_back_us": round(x[7] / n * 0.01, 2)} if len(x) >= 8 else {})})
+            out["xfer"] = xs
+            out["error"] = live.error
+            return out
         # saturated: every pod as fast as its vport takes frames (with what each trial cost in CPU
         # time: the rate is host-CPU work, bounded by the box's CPU share)
         runs = []
@@ -421,6 +441,7 @@ def main() -> None:
     ap.add_argument("--trials", type=int, default=1, help="saturated runs (median reported)")
     ap.add_argument("--split", default="", help='SFC hops with GPU placements, e.g. "acl,nat,l2fwd@1" (two planes)')
     ap.add_argument("--planes", default="", help='--split: the planes\' devices, e.g. "cuda:0,cuda:1"')
+    ap.add_argument("--idle-only", action="store_true", help="--split: the unloaded run and the inbox timing only")
     ap.add_argument("--veth", choices=("linux-bridge", "engine", "pipeline", "engine-xdp", "pipeline-xdp"), default=None,
                     help="netns pods on veth pairs, switched by a Linux bridge, by the native engine alone or by the "
                          "native engine in front of the data plane on --device (the deployed default)")
@@ -439,7 +460,7 @@ def main() -> None:
                          max_inflight_frames=a.max_inflight_frames, pod_ring=a.pod_ring,
                          backend=a.backend, coalesce_us=a.coalesce_us, loaded_window=a.loaded_window,
                          traffic=a.traffic, zero_copy=a.zero_copy, gpu_egress=a.gpu_egress, trials=a.trials,
-                         split=a.split, planes=a.planes)),
+                         split=a.split, planes=a.planes, idle_only=a.idle_only)),
           flush=True)
 
 
