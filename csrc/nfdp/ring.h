@@ -442,6 +442,7 @@ class RingEngine {
   uint32_t* h_xpend_ = nullptr;      // [nq][nch] hand-offs per chunk not back yet (pinned)
   uint32_t* d_xpend_ = nullptr;      // (its device view)
   XferPeer* d_xpeers_ = nullptr;     // [nplanes] (HBM), null: peers not set
+  std::vector<XferPeer> h_xpeers_;   // the same, host copy (RingArgs::xpv)
   uint32_t xplane_ = 0, nplanes_ = 0;
   bool xfer_active_ = false;
 };
@@ -469,6 +470,7 @@ struct RingLaunch {
   const uint64_t* faddr;      // frame addresses per slot (null: frames are in the in slots)
   GdeRing* gde = nullptr;     // GPU-direct egress table [kMaxPorts][queues] (null: off)
   const XferPeer* xpeers = nullptr;   // cross-GPU hops: every plane (null: off)
+  const XferPeer* xpeers_h = nullptr; // the same records in host memory (copied into the kernargs)
   uint32_t xplane = 0, nplanes = 0, xfer_wgs = 0;
   uint32_t* xpend = nullptr;          // this ring's pending hand-offs per chunk
 };

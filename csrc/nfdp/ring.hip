@@ -40,6 +40,11 @@ struct RingArgs {
   const unsigned long long* faddr;   // zero-copy rx: per-slot frame addresses (null: in slots)
   GdeRing* gde;         // GPU-direct egress table [kMaxPorts][nq] (null: off; ring.h GdeRing)
   const XferPeer* xpeers;   // cross-GPU hops (ring.h XferEntry): every plane (null: off)
+  // the same records by value: indexed by a wave-uniform plane they are scalar loads from the
+  // kernarg segment, so every descriptor built from them is uniform (a record read from global
+  // memory the kernel writes is a vector load, and each access through a descriptor built from it
+  // a loop over the lanes: 26 such loops in the hand-off path, r6 tools/waterfall_scan.py)
+  XferPeer xpv[kMaxXferPlanes];
   uint32_t xplane, nplanes, xfer_wgs;
   uint32_t* xpend;          // this ring's [nq][chunks] hand-offs not back yet (pinned host memory)
 };
@@ -384,9 +389,9 @@ __device__ __forceinline__ void xfer_send(const RingArgs& a, bool go, uint32_t p
     const bool mine = go && plane == P;
     const unsigned long long bm = __ballot(mine);
     rem &= ~bm;
-    XferInbox* ib = a.xpeers[P].inbox;
-    XferEntry* ent = a.xpeers[P].entries;
-    const uint32_t cmask = a.xpeers[P].cap_mask;
+    XferInbox* ib = a.xpv[P].inbox;
+    XferEntry* ent = a.xpv[P].entries;
+    const uint32_t cmask = a.xpv[P].cap_mask;
     unsigned long long base = 0;
     if (lane == 0)
       base = __hip_atomic_fetch_add(&ib->tail, (unsigned long long)__builtin_popcountll(bm), __ATOMIC_RELAXED,
@@ -432,8 +437,8 @@ __device__ __forceinline__ void xfer_resume(const RingArgs& a, bool rdy, XferEnt
   // the entry (system-coherent loads: a peer wrote it).  One descriptor over the whole inbox and a
   // per-lane offset: a descriptor built from each lane's own entry pointer is not wave-uniform and
   // compiles to a loop over the 64 lanes (r6: 17 us of a 22-us resume pass, unloaded)
-  const uint32_t cmask = a.xpeers[a.xplane].cap_mask;
-  const __amdgpu_buffer_rsrc_t re = __builtin_amdgcn_make_buffer_rsrc((void*)a.xpeers[a.xplane].entries, (short)0,
+  const uint32_t cmask = a.xpv[a.xplane].cap_mask;
+  const __amdgpu_buffer_rsrc_t re = __builtin_amdgcn_make_buffer_rsrc((void*)a.xpv[a.xplane].entries, (short)0,
                                                                       (int)((cmask + 1u) * 128u), kBufRaw);
   const uint32_t eo = rdy ? (uint32_t)(idx & cmask) * 128u : kNoRun;
   uint32_t d[kSlotDwords], hw[8];
@@ -478,10 +483,10 @@ __device__ __forceinline__ void xfer_resume(const RingArgs& a, bool rdy, XferEnt
     const bool mine = fin && oplane == O;
     const unsigned long long bm = __ballot(mine);
     rem &= ~bm;
-    const uint32_t slots = a.xpeers[O].ring_mask + 1u, nq = a.xpeers[O].nq;
-    const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc((void*)a.xpeers[O].out, (short)0,
+    const uint32_t slots = a.xpv[O].ring_mask + 1u, nq = a.xpv[O].nq;
+    const __amdgpu_buffer_rsrc_t ro = __builtin_amdgcn_make_buffer_rsrc((void*)a.xpv[O].out, (short)0,
                                                                         (int)(nq * slots * 64u), kBufRaw);
-    const __amdgpu_buffer_rsrc_t rm = __builtin_amdgcn_make_buffer_rsrc((void*)a.xpeers[O].out_meta, (short)0,
+    const __amdgpu_buffer_rsrc_t rm = __builtin_amdgcn_make_buffer_rsrc((void*)a.xpv[O].out_meta, (short)0,
                                                                         (int)(nq * slots * 4u), kBufRaw);
     const uint32_t at = oq * slots + (pos & (slots - 1u));
     const bool ok = mine && oq < nq;
@@ -515,9 +520,9 @@ __device__ __forceinline__ void xfer_resume(const RingArgs& a, bool rdy, XferEnt
     const unsigned long long bm = __ballot(fin && origin == K0 && chunk == K1);
     rem &= ~bm;
     const uint32_t O = K0 & 0xFFu, Q = K0 >> 8;
-    const uint32_t nch = (a.xpeers[O].ring_mask + 1u) >> 6;
-    if (lane == 0 && Q < a.xpeers[O].nq)
-      __hip_atomic_fetch_sub(a.xpeers[O].xpend + (size_t)Q * nch + (K1 & (nch - 1u)), (uint32_t)__builtin_popcountll(bm),
+    const uint32_t nch = (a.xpv[O].ring_mask + 1u) >> 6;
+    if (lane == 0 && Q < a.xpv[O].nq)
+      __hip_atomic_fetch_sub(a.xpv[O].xpend + (size_t)Q * nch + (K1 & (nch - 1u)), (uint32_t)__builtin_popcountll(bm),
                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
   // entries consumed (a producer a ring later may reuse them), counters of this plane
@@ -525,7 +530,7 @@ __device__ __forceinline__ void xfer_resume(const RingArgs& a, bool rdy, XferEnt
   {   // hand-off timing sample: this pass's first entry
     const unsigned long long rbm = __ballot(rdy);
     if (rbm && lane == 0) {
-      XferInbox* ib = a.xpeers[a.xplane].inbox;
+      XferInbox* ib = a.xpv[a.xplane].inbox;
       const uint32_t ts = __builtin_amdgcn_readlane(way[2], __builtin_ctzll(rbm));
       atomicAdd(&ib->t_wait, (unsigned long long)(t_pick - ts));
       atomicAdd(&ib->t_work, (unsigned long long)((uint32_t)__builtin_amdgcn_s_memrealtime() - t_pick));
@@ -550,9 +555,9 @@ __device__ __forceinline__ void xfer_resume(const RingArgs& a, bool rdy, XferEnt
 // keeps claiming tickets while reserved entries remain, so a producer never waits forever for room.
 template <bool COOP>
 __device__ __forceinline__ void xfer_serve(const RingArgs& a, uint32_t lane, unsigned long long t_begin, uint4* kx) {
-  XferInbox* ib = a.xpeers[a.xplane].inbox;
-  XferEntry* ent = a.xpeers[a.xplane].entries;
-  const uint32_t cmask = a.xpeers[a.xplane].cap_mask;
+  XferInbox* ib = a.xpv[a.xplane].inbox;
+  XferEntry* ent = a.xpv[a.xplane].entries;
+  const uint32_t cmask = a.xpv[a.xplane].cap_mask;
   uint32_t seen_ep = 0xFFFFFFFFu;
   auto tail_now = [&]() {
     unsigned long long tl = 0;
@@ -1021,6 +1026,8 @@ hipError_t launch_ring(const RingLaunch& r, const LaunchCfg& cfg, int wgs_per_cu
   a.faddr = reinterpret_cast<const unsigned long long*>(r.faddr);
   a.gde = r.gde;
   a.xpeers = r.xpeers;
+  if (r.xpeers && r.xpeers_h)
+    for (uint32_t i = 0; i < r.nplanes && i < kMaxXferPlanes; ++i) a.xpv[i] = r.xpeers_h[i];
   a.xplane = r.xplane;
   a.nplanes = r.nplanes;
   a.xfer_wgs = r.xpeers ? r.xfer_wgs : 0u;
@@ -1251,6 +1258,7 @@ void RingEngine::start(const FusedLaunch& f, const LaunchCfg& cfg, double deadli
                       stream_), "xfer claim");
     ck(hipStreamSynchronize(stream_), "xfer claim");
     r.xpeers = d_xpeers_;
+    r.xpeers_h = h_xpeers_.data();
     r.xplane = xplane_;
     r.nplanes = nplanes_;
     r.xfer_wgs = xwgs_;
@@ -1381,6 +1389,7 @@ void RingEngine::xfer_set_peers(uint32_t my_plane, const std::vector<XferDesc>& 
   d_xpeers_ = nullptr;
   ck(hipMalloc(reinterpret_cast<void**>(&d_xpeers_), sizeof(XferPeer) * v.size()), "alloc peers");
   ck(hipMemcpy(d_xpeers_, v.data(), sizeof(XferPeer) * v.size(), hipMemcpyHostToDevice), "peers");
+  h_xpeers_ = v;
   xplane_ = my_plane;
   nplanes_ = (uint32_t)v.size();
 }

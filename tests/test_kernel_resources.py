@@ -147,3 +147,21 @@ def test_no_store_data_hazard_in_device_code(tmp_path):
         scanned += 1
     assert scanned >= 3   # kernels / ring / shard at least
     shutil.rmtree(tmp_path, ignore_errors=True)
+
+
+def test_ring_kernels_have_no_descriptor_waterfall_loops():
+    """Buffer descriptors in the ring kernels are wave-uniform (tools/waterfall_scan.py): a
+    non-uniform one compiles each access into a loop over the lanes.  Known: the coop instances'
+    ACL tiles past the LDS copy (> 64 tiles) build their two descriptors from the LDS copy of the
+    table set - one loop pair on that path.  The split-chain hand-off path had 26 more before its
+    peer records moved into the kernargs (r6)."""
+    import importlib.util
+    import shutil
+
+    if not shutil.which("/opt/rocm/lib/llvm/bin/clang++"):
+        pytest.skip("no ROCm clang")
+    spec = importlib.util.spec_from_file_location("waterfall_scan", REPO / "tools" / "waterfall_scan.py")
+    ws = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(ws)
+    hits = ws.scan_asm(ws.compile_asm(REPO / "csrc" / "nfdp" / "ring.hip"))
+    assert all(v <= 2 for v in hits.values()), hits
