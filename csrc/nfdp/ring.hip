@@ -1476,14 +1476,18 @@ void RingEngine::stop(double timeout_s) {
     if (completed(q) != published(q)) throw std::runtime_error("ring: stopped with published chunks unprocessed");
 }
 
-// The resident grid's stream.  NFDP_RING_STREAM picks how it is made (A/B of queue placement under
-// GPU_MAX_HW_QUEUES): "plain" (a non-blocking stream, the default) or "prio" (highest priority).
-// Measured with HIP's default 4 hardware queues (profiles/r5_s3_live_commit_hwq_ab.txt): the 1 kHz
-// live-commit p99 moves by +1.1-2.6 us either way, as with 16 queues; a CU-masked stream
-// (hipExtStreamCreateWithCUMask) failed the same test and is not offered.
+// The resident grid's stream.  NFDP_RING_STREAM picks how it is made: "prio" (highest priority,
+// the default) or "plain" (an ordinary non-blocking stream).  A resident grid holds the hardware
+// queue its stream maps to, and HIP maps ordinary streams round-robin onto GPU_MAX_HW_QUEUES (4)
+// queues: with enough streams made before it, a ring's stream shares the queue of the default
+// stream, and a harvest or copy issued there waits behind the grid forever (r6: the GPU suite hung
+// in test_port_placement_hop_pipeline's harvest after the earlier tests' streams; with the ring
+// streams at the highest priority - their own queue pool - it passes: profiles/r6_s18).  The
+// 1 kHz live-commit p99 is the same either way (profiles/r5_s3_live_commit_hwq_ab.txt); a
+// CU-masked stream (hipExtStreamCreateWithCUMask) failed that test and is not offered.
 void RingEngine::create_stream() {
   const char* m = std::getenv("NFDP_RING_STREAM");
-  if (m && std::string(m) == "prio") {
+  if (!(m && std::string(m) == "plain")) {
     int lo = 0, hi = 0;
     ck(hipDeviceGetStreamPriorityRange(&lo, &hi), "stream priorities");
     ck(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, hi), "stream (priority)");
