@@ -95,6 +95,10 @@ NFDP_HD int acl_rule_of(uint32_t b, uint32_t n_acl) {
 // r5 s11 A/B on the ClassBench-style set: 7.16 vs 7.71 Gpps without (profiles/r5_s11_ab_ptiles.jsonl):
 // half the tile MFMAs, but the per-tile loop loses the straight-line 8-tile groups' overlap, and
 // the 2-wave instance is bound by latency, not by its MFMA count.  Off.
+// r6 (profiles/r6_s20_acl_ab_wild.jsonl, r6_s21_acl_ab_wild.jsonl): with the rules placed
+// source-first (host.cpp NFDP_ACL_ORDER=1) 29 tiles per wave pass their prefilter instead of 37,
+// and the prefilter tiles reach 8,060 Mpps against 8,002 for this default; 2 = one cursor over every
+// prefilter tile's admitted tiles run in batches of 4 (7,217).  Still off.
 #define NFDP_ACL_PTILES 0
 #endif
 #ifndef NFDP_TILE_PF
@@ -290,6 +294,68 @@ __device__ __forceinline__ void classify_wave(const FlowKey& key, uint4* kx, con
           if (t < av.ctiles) return av.lc[t * 4 + g];
           return __builtin_bit_cast(v4i, __builtin_amdgcn_raw_buffer_load_b128(r_gc, (t * 4u + g) * 16u, 0, 0));
         };
+#if NFDP_ACL_PTILES == 2
+        // one cursor over the admitted tiles of every prefilter tile (tested when the cursor reaches
+        // it), run in batches of 4 with the next batch's fragments loading under the current
+        // batch's MFMAs (two batches with fixed roles, as the global-tile path below)
+        uint32_t pt_next = 0, mcur = 0, mbase = 0;
+        constexpr uint32_t kDeadTile = 0xFFFFFFFFu;
+        auto ptest = [&](uint32_t pt) -> uint32_t {
+          const v4i pa4 = av.pw[pt * 64 + lane], pci = av.pc[pt * 4 + g];
+          const v8i_t pa = {pa4[0], pa4[1], pa4[2], pa4[3], 0, 0, 0, 0};
+          const v4f_t pc = {__int_as_float(pci[0]), __int_as_float(pci[1]), __int_as_float(pci[2]), __int_as_float(pci[3])};
+          v4f_t pacc[4];
+#pragma unroll
+          for (int tt = 0; tt < 4; ++tt) {
+            const v8i_t b = {bq[tt][0], bq[tt][1], bq[tt][2], bq[tt][3], 0, 0, 0, 0};
+            pacc[tt] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(pa, b, pc, 4, 4, 0, kE8M0Idx, 0, kE8M0One);
+          }
+          uint32_t m = 0;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float mn = fminf(fminf(pacc[0][i], pacc[1][i]), fminf(pacc[2][i], pacc[3][i]));
+            const unsigned long long bl = __ballot(mn < 4096.0f);
+#pragma unroll
+            for (int gg = 0; gg < 4; ++gg)
+              m |= (((bl >> (16 * gg)) & 0xFFFFull) != 0ull ? 1u : 0u) << (4 * gg + i);
+          }
+          if (pt * 16u + 16u > av.tiles) m &= (1u << (av.tiles - pt * 16u)) - 1u;
+          return __builtin_amdgcn_readfirstlane(m);
+        };
+        auto next_tile = [&]() -> uint32_t {
+          while (!mcur) {
+            if (pt_next >= av.ptiles) return kDeadTile;
+            mbase = pt_next * 16u;
+            mcur = ptest(pt_next++);
+          }
+          const uint32_t t = mbase + (uint32_t)__builtin_ctz(mcur);
+          mcur &= mcur - 1u;
+          return t;
+        };
+        uint32_t b0[4], b1[4];
+        v4i a0[4], a1[4], k0[4], k1[4];
+        auto fill = [&](uint32_t (&c)[4], v4i (&aa)[4], v4i (&kk)[4]) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            c[k] = next_tile();
+            const uint32_t t = c[k] == kDeadTile ? 0u : c[k];
+            aa[k] = ld_a(t);
+            kk[k] = ld_c(t);
+          }
+        };
+        auto run4 = [&](const uint32_t (&c)[4], const v4i (&aa)[4], const v4i (&kk)[4]) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) run_tile_m(aa[k], kk[k], c[k] == kDeadTile ? 0xFFFFFFFFu : 0u);
+        };
+        fill(b0, a0, k0);
+        while (b0[0] != kDeadTile) {
+          fill(b1, a1, k1);
+          run4(b0, a0, k0);
+          if (b1[0] == kDeadTile) break;
+          fill(b0, a0, k0);
+          run4(b1, a1, k1);
+        }
+#else
         for (uint32_t pt = 0; pt < av.ptiles; ++pt) {
           const v4i pa4 = av.pw[pt * 64 + lane], pci = av.pc[pt * 4 + g];
           const v8i_t pa = {pa4[0], pa4[1], pa4[2], pa4[3], 0, 0, 0, 0};
@@ -332,6 +398,7 @@ __device__ __forceinline__ void classify_wave(const FlowKey& key, uint4* kx, con
             ci = c2;
           }
         }
+#endif
       }
     }
     // PIPE cursor: this wave's next tile >= t and < lim that passes its group and tile prefilters

@@ -156,6 +156,9 @@ void prefilter(const uint32_t* value, const uint32_t* mask, const uint32_t* rule
 }
 }  // namespace
 
+#ifndef NFDP_ACL_ORDER
+#define NFDP_ACL_ORDER 0   // rule placement: 0 protocol, destination, ports, source; 1 source first
+#endif
 AclFrags build_acl_frags(const uint32_t* value, const uint32_t* mask, uint32_t n) {
   if (n > 4096) throw std::invalid_argument("ACL supports at most 4096 rules (12-bit rule index)");
   AclFrags f;
@@ -176,8 +179,15 @@ AclFrags build_acl_frags(const uint32_t* value, const uint32_t* mask, uint32_t n
     const uint32_t mp = (p16(m[2] >> 16) << 16) | p16(m[2] & 0xFFFFu), vp = (p16(v[2] >> 16) << 16) | p16(v[2] & 0xFFFFu);
     // (then destination: specific prefixes before wildcards, by value, so a group's rules share
     // the destination's leading bits whenever the rule set allows)
+#if NFDP_ACL_ORDER == 1
+    // source first (then destination, ports): on the ClassBench-style set the tiles' own prefilters
+    // admit 29 tiles per wave instead of 37 (tools/acl_prefilter_sim.py --order)
+    return std::make_tuple(m[3] & 0xFFu, v[3] & m[3] & 0xFFu, m[0] == 0u, bswap32(v[0] & m[0]), bswap32(m[0]),
+                           m[1] == 0u, bswap32(v[1] & m[1]), bswap32(m[1]), mp, vp & mp, m[3], v[3] & m[3], r);
+#else
     return std::make_tuple(m[3] & 0xFFu, v[3] & m[3] & 0xFFu, m[1] == 0u, bswap32(v[1] & m[1]), bswap32(m[1]), mp,
                            bswap32(m[0]), m[3], vp & mp, bswap32(v[0] & m[0]), v[3] & m[3], r);
+#endif
   };
   std::sort(order.begin(), order.end(), [&](uint32_t x, uint32_t y) { return sig(x) < sig(y); });
   f.wfrag.assign((size_t)f.tiles * 64 * 16, 0);

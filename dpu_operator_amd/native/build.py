@@ -199,7 +199,8 @@ def _compile(src: Path, obj: Path, hip: bool, verbose: bool) -> None:
             cmd.append("-Rpass-analysis=kernel-resource-usage")
     else:
         cxx = shutil.which("g++") or "g++"
-        cmd = [cxx, *common, "-pthread", "-c", str(src), "-o", str(obj)]
+        extra = [f for f in os.environ.get("NFDP_HIPCC_FLAGS", "").split() if f.startswith("-D")]   # (same experiments)
+        cmd = [cxx, *common, *extra, "-pthread", "-c", str(src), "-o", str(obj)]
     if verbose:
         print(" ".join(cmd), flush=True)
     r = subprocess.run(cmd, capture_output=True, text=True)
@@ -216,7 +217,7 @@ def _compile(src: Path, obj: Path, hip: bool, verbose: bool) -> None:
 
 
 def _obj_hash(src: Path, hip: bool) -> str:
-    return _hash_files([src.resolve(), *_deps(src)], ("hip:" + _hip_flags()) if hip else "cxx")
+    return _hash_files([src.resolve(), *_deps(src)], ("hip:" + _hip_flags()) if hip else ("cxx:" + _hip_flags()))
 
 
 def _stale(src: Path, obj: Path, hip: bool, force: bool) -> str | None:

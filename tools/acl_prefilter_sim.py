@@ -4,6 +4,10 @@ over the headline's pod traffic.  CPU only.
 
 r5 s10: 1726 ternary entries, 108 tiles, 14 groups; 9 groups pass every wave (72 tiles run with
 group prefilters), 37 tiles can match.  Running only those (NFDP_ACL_PTILES) measured slower.
+r6: with the rules placed source-first (host.cpp NFDP_ACL_ORDER=1) 29 tiles can match; the group
+prefilters still pass 68.  Measured (profiles/r6_s20_*, r6_s21_*): prefilter tiles 7,386 Mpps,
++ source-first 8,060, + a batched cursor over them 7,217, against 8,002 for the group-prefilter
+default - the 2-wave instance waits on its memory latency, not on its tile count.
 """
 import os
 import sys
