@@ -41,6 +41,7 @@ constexpr uint32_t kEarlyAclTiles = NFDP_EARLY_ACL_TILES;
 constexpr uint32_t kFlagNoEarly = 1u << 8;     // launch flag: never the early-fetch instance (A/B)
 constexpr uint32_t kFlagForceEarly = 1u << 9;  // launch flag: the early-fetch instance at any rule count (A/B)
 constexpr uint32_t kFlagPairs = 1u << 10;      // launch flag: the batch may hold wide header pairs (pair_kernel first)
+
 #ifndef NFDP_FUSED_WAVES_PER_EU
 #define NFDP_FUSED_WAVES_PER_EU 4
 #endif
@@ -228,7 +229,7 @@ void fused_kernel(FusedArgs a) {
   const LdsTables ta = stage_lds_tables(a.t, lport, lchain, lperm, L.tabs, kFB);
   __syncthreads();
 
-  const unsigned long long t0 = a.t0 ? *a.t0 : 0ull;
+  const unsigned long long t0 = a.t0 ? *a.t0 : __builtin_amdgcn_s_memrealtime();
   const uint32_t n = a.n_dev ? min(a.n, *a.n_dev) : a.n;
   const uint32_t stride = gridDim.x * kFB;
   // Software pipeline over the grid-stride loop.  s_waitcnt vmcnt retires loads, stores and

@@ -713,11 +713,18 @@ class DataPlane:
             if inmeta.numel() != n or out.shape[0] < n or meta.numel() < n:
                 raise ValueError("batch buffer size mismatch")
             s = stream if stream is not None else torch.cuda.current_stream(self.tdev).cuda_stream
-            if stamp:
-                self.nf.launch_stamp(self._ptr("t0"), s)
             if not self.count_flows:
                 flags |= 4  # the kernel always gets the counter table; bit 2 makes it add 0
             pairs = self.pairs_possible()
+            # batch-release stamp for the latency samples: by default each workgroup of the fused
+            # kernel counts from its own start (t0 pointer null: a resident grid's workgroups all
+            # begin at the launch), so no stamp kernel runs in front of every batch; a stamp kernel
+            # still marks the release before a pair pass, and in a captured graph
+            t0_ptr = self._ptr("t0")
+            if stamp and (pairs or torch.cuda.is_current_stream_capturing()):
+                self.nf.launch_stamp(t0_ptr, s)
+            elif stamp:
+                t0_ptr = 0
             if pairs:
                 # wide header pairs resolved in place over the whole batch first (kernels.hip pair_kernel)
                 self.nf.launch_pairs(tp, pkts.data_ptr(), inmeta.data_ptr(), n, self._ptr("port_ctr"),
@@ -736,7 +743,7 @@ class DataPlane:
                     tp, pkts.data_ptr() + 64 * lo, inmeta.data_ptr() + 4 * lo, out.data_ptr() + 64 * lo,
                     meta.data_ptr() + 4 * lo, m,
                     self._ptr("flow_ctr"), self._ptr("port_ctr"), self._ptr("drop_ctr"),
-                    self._ptr("t0"),
+                    t0_ptr,
                     lat.data_ptr() + 4 * (lo // 16) if lat is not None else 0,
                     self._ptr("acl_wfrag"), self._ptr("acl_cinit"), self._acl_tiles,
                     self._ptr("toep_frag"), self._ptr("toep_tab"),
