@@ -246,7 +246,7 @@ def parse():
     ap.add_argument("--no-unsteered", action="store_true", help="N > 1 rss: skip the exchange-bound (unsteered) variant")
     ap.add_argument("--live-workers", type=int, default=0,
                     help="native I/O engine delivery threads per queue (0: run to completion, the rx thread delivers)")
-    ap.add_argument("--live-queues", type=int, default=8, help="native I/O engine rx queues (threads)")
+    ap.add_argument("--live-queues", type=int, default=6, help="native I/O engine rx queues (threads)")
     ap.add_argument("--live-gen-threads", type=int, default=8, help="pod traffic generator threads (one per pod)")
     ap.add_argument("--live-trials", type=int, default=3, help="saturated live trials of 1 s (median reported)")
     ap.add_argument("--live-gpu-egress", action="store_true",

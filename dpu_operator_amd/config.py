@@ -38,7 +38,7 @@ class NodeConfig:
     vsp_state_dir: str = ""            # journal + snapshots (checkpoint/resume); "" = off
     # live data path of the GPU VSP (vsp/gpu.py, dataplane/native_io.py)
     vport_kind: str = "veth"           # veth (kernel netdev pods, AF_PACKET rings) | xdp (veth, AF_XDP) | memif | tap
-    io_queues: int = 8                 # native engine rx queues (threads), each with a ring queue per GPU
+    io_queues: int = 6                 # native engine rx queues (threads), each with a ring queue per GPU
     # native engine delivery threads per queue; 0 = run to completion (each rx thread completes and
     # delivers its own bursts: one busy thread per queue).  On the GPU box (16 CPUs granted) 6 x 0
     # with 8 pod threads: 91-98 Mpps, 4 x 2: 45-59 (r6 s3 / s4, profiles/r6_s*_live_*.jsonl)

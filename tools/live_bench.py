@@ -119,7 +119,7 @@ class _WireLive:
 
 def run(device: str = "cuda", n_pods: int = 8, flows: int = 1 << 20, n_acl: int = 256, duration: float = 1.0,
         threads: int = 8, burst: int = 512, inflight: int = 64, ring_capacity: int = 16384,
-        hash_mode: str = "lds", tx_workers: int = 0, queues: int = 8, max_inflight_frames: int = 4096,
+        hash_mode: str = "lds", tx_workers: int = 0, queues: int = 6, max_inflight_frames: int = 4096,
         pod_ring: int = 1024, backend: str = "pipeline", coalesce_us: float = 8.0, loaded_window: int = 2048,
         traffic: str = "plain", zero_copy: bool = False, saturated_only: bool = False, gpu_egress: bool = False,
         trials: int = 1, split: str = "", planes: str = "", idle_only: bool = False) -> dict:
@@ -429,7 +429,7 @@ def main() -> None:
     ap.add_argument("--burst", type=int, default=512)
     ap.add_argument("--inflight", type=int, default=64)
     ap.add_argument("--tx-workers", type=int, default=0, help="0: run to completion (the rx threads deliver)")
-    ap.add_argument("--queues", type=int, default=8)
+    ap.add_argument("--queues", type=int, default=6)
     ap.add_argument("--max-inflight-frames", type=int, default=4096)
     ap.add_argument("--pod-ring", type=int, default=1024)
     ap.add_argument("--backend", choices=("pipeline", "wire"), default="pipeline")
