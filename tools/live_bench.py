@@ -222,6 +222,11 @@ def run(device: str = "cuda", n_pods: int = 8, flows: int = 1 << 20, n_acl: int 
         # saturated: every pod as fast as its vport takes frames (with what each trial cost in CPU
         # time: the rate is host-CPU work, bounded by the box's CPU share)
         runs = []
+        if int(trials) > 1:
+            # one untimed run first: the first trial after setup ran 10-25 % low on several boxes
+            # (page faults in fresh pod rings, cold caches; r6_s24, r6_s25)
+            nf.trafgen_run(pods, duration_s=0.3, warmup_s=0.1, threads=threads, burst=32)
+            drain(nf, pods, stats)
         for _ in range(max(1, int(trials))):
             with cpuquota.Meter() as cm:
                 r = nf.trafgen_run(pods, duration_s=duration, warmup_s=0.2, threads=threads, burst=32)
