@@ -623,7 +623,11 @@ __device__ __forceinline__ int64_t flow_probe(const TablesView& t, const FlowKey
 // its latency overlap the ACL classification (fused kernel, NFDP_PROBE_EARLY): issue = the eight
 // wave-cooperative line loads, finish = key compare, action hand-over and the second choice.
 #ifndef NFDP_PROBE_AUX
-#define NFDP_PROBE_AUX -1   // >= 0: bucket loads as raw buffer loads with these cache-policy bits
+// >= 0: bucket loads as raw buffer loads with these cache-policy bits; -1: flat loads.  r6 A/B
+// (profiles/r6_s26_ab_probe_aux.jsonl, r6_s27_*): buffer loads 15,686 vs 15,437 Mpps and 16,081
+// vs 15,964 on another box (policy 0; sc0 / sc1 within noise of it, nt 15,243), ClassBench set
+// unchanged - the descriptor's range check replaces the flat loads' 64-bit address arithmetic
+#define NFDP_PROBE_AUX 0
 #endif
 __device__ __forceinline__ void flow_probe_issue(const TablesView& t, uint32_t h, uint4 (&v)[8]) {
   const uint32_t lane = threadIdx.x & 63u;
