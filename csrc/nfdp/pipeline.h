@@ -179,6 +179,14 @@ struct EgressDecision {
                       // kHopXfer: the hop the chain resumes at on the other GPU
 };
 
+// The resume word of a hand-off (EgressDecision::inner_len of a kRemote from a kHopXfer, HopState::hop):
+// the hop the chain resumes at in the low byte, and the egress port the hops before the hand-off
+// decided (bit 15 set) in the high half - resume_stage replays it for a route hop.
+constexpr uint32_t kHopResumeHopMask = 0xFFu, kHopResumeHasPort = 0x8000u;
+NFDP_HD uint32_t hop_resume_word(uint32_t hop, uint32_t port) {
+  return port < 0xFFFFu ? (hop | kHopResumeHasPort | (port << 16)) : hop;
+}
+
 // Length of the frame that leaves (the meta word's len): inner frame for a recirculation, tag and
 // outer-header bytes included otherwise, 0 for drops.
 NFDP_HD uint32_t egress_len(const Parsed& p, const EgressDecision& e) {
@@ -334,8 +342,11 @@ NFDP_HD bool apply_hop(const TablesView& t, const TA& ta, uint32_t op, int i, Pa
     e.out_port = rp;
   } else if (XFER && op >= kHopXfer) {
     // the rest of the chain runs on another GPU (resume_stage there): the frame leaves with the
-    // header as the hops so far left it, untagged (a vlan hop's push is replayed at the end)
-    e.reason = kRemote; e.out_port = op & kHopXferPlanes; e.inner_len = (uint32_t)i + 1u; e.push = 0;
+    // header as the hops so far left it, untagged (a vlan hop's push is replayed at the end).  The
+    // egress port the hops so far decided travels in the resume word (hop_resume_word): a route
+    // hop's port depends on the header it rewrote, so the resuming GPU cannot recompute it
+    e.inner_len = hop_resume_word((uint32_t)i + 1u, e.out_port);
+    e.reason = kRemote; e.out_port = op & kHopXferPlanes; e.push = 0;
     return true;
   }
   return false;
@@ -472,12 +483,13 @@ NFDP_HD EgressDecision chain_stage(const TablesView& t, const TA& ta, Parsed& p,
 // `st` carries its ingress port (flags from this GPU's replicated port table) and `act`, `acl_rule`,
 // `hash` travel with it from the first GPU.  Hops before `hop0` already ran: their effects on the
 // header are in the slot, and what they decided about the egress (the l2fwd / hairpin port, a vlan
-// push / pop) is replayed from the chain word, which is the same on every GPU.  A route hop cannot
-// come before a hand-off (ChainTable refuses it: its port depends on the header it rewrote).
+// push / pop) is replayed from the chain word, which is the same on every GPU; a route hop's port
+// (it depends on the header the route rewrote) comes with the frame, in the resume word's high half.
 // Frames of split chains are not mirrored (K9 copies the ingress frame, which stayed on the first GPU).
 template <class TA, bool V6HOPS = true>
 NFDP_HD EgressDecision resume_stage(const TablesView& t, const TA& ta, Parsed& p, const IngressState& st,
-                                    const FlowAction& act, int acl_rule, uint32_t hash, uint32_t hop0) {
+                                    const FlowAction& act, int acl_rule, uint32_t hash, uint32_t resume) {
+  const uint32_t hop0 = resume & kHopResumeHopMask;
   EgressDecision e;
   e.out_port = act.out_port; e.reason = st.reason; e.push = 0; e.tci = 0; e.mirror = 0; e.flood = 0;
   e.xhdr = 0; e.inner_len = 0;
@@ -495,7 +507,10 @@ NFDP_HD EgressDecision resume_stage(const TablesView& t, const TA& ta, Parsed& p
       else if (op == kHopVlan) {
         if (act.vlan == 0xFFFFu) { e.push = 0; vlan_done = true; }
         else if (act.vlan) { e.push = 1; e.tci = act.vlan & 0xFFFu; vlan_done = true; }
-      } else if (op == kHopRoute) { e.reason = kChainDrop; e.out_port = kPortNone; return e; }
+      } else if (op == kHopRoute) {
+        if (!(resume & kHopResumeHasPort)) { e.reason = kChainDrop; e.out_port = kPortNone; return e; }
+        e.out_port = resume >> 16;
+      }
       continue;
     }
     if (apply_hop<TA, V6HOPS>(t, ta, op, i, p, st, act, acl_rule, hash, e, vlan_done)) return e;

@@ -789,8 +789,8 @@ def expand_hops(hops) -> list[int]:
     """Chain hops -> opcodes.  A hop may name the GPU it runs on, ``"ttl@1"``; the chain then hands
     the frame over (a kHopXfer op) wherever the GPU changes, and a hop without ``@`` runs where the
     previous one did (the first on the GPU the frame entered).  ``"@1"`` alone is an explicit
-    hand-off.  A route hop cannot come before a hand-off (resume_stage replays the earlier hops'
-    egress decisions, and a route's depends on the header it rewrote)."""
+    hand-off.  A route hop may come before a hand-off: the egress port it decided travels with the
+    frame (pipeline.h hop_resume_word), since it depends on the header the route rewrote."""
     codes: list[int] = []
     cur = None
     for h in hops:
@@ -809,9 +809,6 @@ def expand_hops(hops) -> list[int]:
                 codes.append(HOP_NAMES[name])
         else:
             codes.append(int(h))
-    xf = [i for i, c in enumerate(codes) if c >= HOP_XFER]
-    if xf and any(c == HOP_ROUTE for c in codes[: xf[-1]]):
-        raise ValueError("a route hop cannot come before a hand-off to another GPU")
     return codes
 
 

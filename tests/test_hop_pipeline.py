@@ -74,8 +74,8 @@ def _check(one, multi, sc, n=6000, seed=3):
 def test_expand_hops():
     assert T.expand_hops(["acl", "nat", "ttl@1", "l2fwd@1"]) == [1, 2, 0x11, 4, 3]
     assert T.expand_hops(["acl", "@1", "nat", "@2", "ttl"]) == [1, 0x11, 2, 0x12, 4]
-    with pytest.raises(ValueError):
-        T.expand_hops(["route", "ttl@1"])
+    # a route hop before a hand-off: its egress port travels with the frame (hop_resume_word)
+    assert T.expand_hops(["route", "ttl@1"]) == [T.HOP_ROUTE, 0x11, 4]
     with pytest.raises(ValueError):
         T.expand_hops(["ttl@16"])
     c = T.ChainTable()
@@ -114,6 +114,19 @@ def test_hairpin_before_the_split():
     _check(one, multi, sc)
 
 
+def test_route_before_the_split():
+    """acl, nat, route on plane 0 -> ttl, then back for nothing: the routed egress port (ECMP over
+    the rewritten header) crosses with the frame instead of being recomputed on plane 1."""
+    one, multi, sc, _ = _pair(("acl", "nat", "route", "ttl@1"), ("acl", "nat", "route", "ttl"))
+    for dp in (one, multi):
+        S.install_l3_routes(dp, sc, n_background=2000)
+    one.chains.set(sc.chain_id, ["acl", "nat", "route", "ttl"])
+    multi.chains.set(sc.chain_id, ["acl", "nat", "route", "ttl@1"])
+    m = _check(one, multi, sc)
+    fwd = ((m >> 26) & 0xF) == 0
+    assert multi.drop_counters()["remote"] >= fwd.sum()
+
+
 def test_four_planes_relay():
     one, multi, sc, _ = _pair(("acl", "nat@1", "ttl@2", "l2fwd@3"), ("acl", "nat", "ttl", "l2fwd"), planes=4)
     _check(one, multi, sc)
@@ -141,7 +154,10 @@ def test_resume_record_layout():
     assert ((hs[:, 0] >> 16) == ((m >> 12) & 0x3FFF)).all()   # the frame length, untagged
     np.testing.assert_array_equal(hs[:, 1], r.extra["hash"])
     np.testing.assert_array_equal(hs[:, 2].view(np.int32), r.extra["acl"])
-    assert (hs[:, 3] == 2).all()   # acl, xfer -> resumes at hop 2 (nat)
+    assert (hs[:, 3] & 0xFF == 2).all()   # acl, xfer -> resumes at hop 2 (nat)
+    # the egress port decided before the hand-off (bit 15: present): here the flow's own port
+    assert (hs[:, 3] & 0x8000 != 0).all()
+    assert ((hs[:, 3] >> 16) == (hs[:, 4] >> 16)).all()
     assert (hs[:, 4] & 0xFFFF == sc.chain_id).all()
 
 

@@ -84,6 +84,39 @@ def test_hop_pipeline_two_planes_on_one_gpu(hash_mode, split, whole):
     _compare(m1, o1, m3, o3)
 
 
+def test_route_before_the_split_on_gpu():
+    """acl, nat, route on plane 0 -> ttl on plane 1 (the XFER instance, pack, resume_kernel): the
+    routed egress port crosses in the resume word; bit-exact with the whole chain and the oracle."""
+    import torch
+
+    from dpu_operator_amd.parallel.hops import HopPipeline
+
+    whole, split = ("acl", "nat", "route", "ttl"), ("acl", "nat", "route", "ttl@1")
+    one = DataPlane(device="cuda:0")
+    sc, deny = _program(one, whole)
+    multi = MultiDataPlane(["cuda:0", "cuda:0"], placement="port")
+    _program(multi, split)
+    orc = DataPlane(device="cpu")
+    _program(orc, whole)
+    for dp, hops in ((one, whole), (multi, split), (orc, whole)):
+        S.install_l3_routes(dp, sc, n_background=2000)
+        dp.chains.set(sc.chain_id, list(hops))
+        dp.commit()
+    n = 1 << 16
+    pk, im = S.traffic_mixed(sc, deny, n, seed=11, miss=0.05, deny_frac=0.05)
+    tpk, tim = torch.from_numpy(pk).cuda(), torch.from_numpy(im.view(np.int32)).cuda()
+    r1 = one.run(tpk, tim)
+    torch.cuda.synchronize()
+    m1, o1 = r1.meta.cpu().numpy().view(np.uint32), r1.out.cpu().numpy()
+    ro = orc.run(pk, im)
+    _compare(ro.meta, ro.out, m1, o1)
+    hp = HopPipeline(multi.planes, n)
+    hp.step(tpk, tim)
+    o2, m2 = hp.results(n)
+    _compare(m1, o1, m2, o2)
+    np.testing.assert_array_equal(one.port_counters(), multi.port_counters())
+
+
 def test_multidataplane_run_resolves_handoffs_on_gpu():
     """The host-array API (MultiDataPlane.run): flow placement, frames enter on their owner plane
     and hand off device to device."""
