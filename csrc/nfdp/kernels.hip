@@ -46,6 +46,9 @@ constexpr uint32_t kFlagPairs = 1u << 10;      // launch flag: the batch may hol
 #define NFDP_FUSED_WAVES_PER_EU 4
 #endif
 constexpr int kFB = NFDP_FUSED_BLOCK;
+#ifndef NFDP_FUSED_MAX_PER_CU
+#define NFDP_FUSED_MAX_PER_CU 4   // grid: workgroups per CU the LDS allows, capped here (A/B)
+#endif
 #ifndef NFDP_KARG_RELOAD
 #define NFDP_KARG_RELOAD 1
 #endif
@@ -1374,7 +1377,7 @@ static hipError_t launch_fused_t(const FusedArgs& a, int num_cus, hipStream_t s)
     attr_set = true;
   }
   int per_cu = (int)((160 * 1024) / (lds ? lds : 1));
-  per_cu = per_cu < 1 ? 1 : (per_cu > 4 ? 4 : per_cu);
+  per_cu = per_cu < 1 ? 1 : (per_cu > NFDP_FUSED_MAX_PER_CU ? NFDP_FUSED_MAX_PER_CU : per_cu);
   const uint32_t need = (a.n + kFB - 1) / kFB;
   uint32_t grid = (uint32_t)(per_cu * num_cus);
   if (need < grid) grid = need;
