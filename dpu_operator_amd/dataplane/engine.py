@@ -718,10 +718,11 @@ class DataPlane:
             pairs = self.pairs_possible()
             # batch-release stamp for the latency samples: by default each workgroup of the fused
             # kernel counts from its own start (t0 pointer null: a resident grid's workgroups all
-            # begin at the launch), so no stamp kernel runs in front of every batch; a stamp kernel
-            # still marks the release before a pair pass, and in a captured graph
+            # begin at the launch), so no stamp kernel runs in front of every batch - nor in a
+            # captured graph, whose every replay stamps anew; a stamp kernel still marks the
+            # release before a pair pass
             t0_ptr = self._ptr("t0")
-            if stamp and (pairs or torch.cuda.is_current_stream_capturing()):
+            if stamp and pairs:
                 self.nf.launch_stamp(t0_ptr, s)
             elif stamp:
                 t0_ptr = 0

@@ -355,7 +355,7 @@ def test_batch_larger_than_one_launch():
 
 @pytest.mark.gpu
 def test_graphed_run_matches_oracle_and_recaptures_after_commit():
-    """DataPlane.capture(n): the stamp + fused (+ side + learn) launches of a batch replayed as one
+    """DataPlane.capture(n): the fused (+ side + learn) launches of a batch replayed as one
     HIP graph.  Replays over new inputs match the oracle; a commit that reallocates a table makes
     the next call re-capture (the graph holds device addresses)."""
     import torch
