@@ -912,9 +912,10 @@ class DataPlane:
 
 class GraphedRun:
     """`DataPlane.run` over fixed device buffers, captured once as a HIP graph
-    (torch.cuda.CUDAGraph is hipGraph on ROCm): a replay is ONE graph launch for the batch-release
-    stamp, the fused kernel and (when side outputs are active) the side and learn kernels, instead
-    of several host launches - what a launch-bound loop of small batches pays for.
+    (torch.cuda.CUDAGraph is hipGraph on ROCm): a replay is ONE graph launch for the fused kernel
+    (whose workgroups stamp their own start for the latency samples) and, when side outputs are
+    active, the side and learn kernels, instead of several host launches - what a launch-bound loop
+    of small batches pays for.
 
         g = dp.capture(64)
         r = g(pkts, inmeta)          # copies into the captured input buffers, replays
